@@ -1,0 +1,163 @@
+"""ctypes front-end of the CPU oracle (oracle/pmp_oracle.c).
+
+TEST INFRASTRUCTURE ONLY -- imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg.  The product package python_motion_planning_amd never imports this.
+Each wrapper names the reference function it restates (see pmp_oracle.c for file:line).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+def build(force: bool = False) -> str:
+    src = os.path.join(_HERE, "pmp_oracle.c")
+    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE, "-B" if force else "liboracle.so"])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.oracle_hypot.restype = ctypes.c_double
+        L.oracle_hypot.argtypes = [ctypes.c_double, ctypes.c_double]
+        L.oracle_hypot_many.restype = None
+        L.oracle_hypot_many.argtypes = [_dp, _dp, _dp, ctypes.c_int64]
+        L.oracle_astar2d.restype = ctypes.c_int
+        L.oracle_astar2d.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     _dp, _i32p, ctypes.c_int, _i32p, _i32p, ctypes.c_int, _i32p, _i64p]
+        L.oracle_astar3d.restype = ctypes.c_int
+        L.oracle_astar3d.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     _i32p, _i32p, _dp, _i32p, ctypes.c_int, _i32p, _i32p, ctypes.c_int,
+                                     _i32p, _i64p]
+        L.oracle_dstar2d.restype = ctypes.c_int
+        L.oracle_dstar2d.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, _dp, _i32p, ctypes.c_int, _i32p,
+                                     _i64p, ctypes.c_int64]
+        L.oracle_astar2d_batch.restype = ctypes.c_int
+        L.oracle_astar2d_batch.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p, _i32p,
+                                           ctypes.c_int, _dp, _i32p, ctypes.c_int, _i32p, _i32p, _i64p,
+                                           _i32p, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def hypot(a, b):
+    a = np.ascontiguousarray(a, dtype=np.float64).ravel()
+    b = np.ascontiguousarray(b, dtype=np.float64).ravel()
+    out = np.empty_like(a)
+    lib().oracle_hypot_many(_p(a, _dp), _p(b, _dp), _p(out, _dp), a.size)
+    return out
+
+
+def astar2d(occ: np.ndarray, start, goal, heuristic: str = "euclidean", with_expand: bool = True,
+            path_cap: int | None = None, expand_cap: int | None = None):
+    """Restatement of AStar.plan (a_star.py:39-83).  occ: uint8 [W, H], occ[x, y] != 0 blocked.
+    Returns dict(status, cost, path (goal->start list of (x,y)), expand (closure order), counters)."""
+    occ = np.ascontiguousarray(occ, dtype=np.uint8)
+    W, H = occ.shape
+    path_cap = path_cap or W * H + 1
+    expand_cap = expand_cap or (W * H if with_expand else 0)
+    path = np.zeros(path_cap, np.int32)
+    expand = np.zeros(max(expand_cap, 1), np.int32)
+    cost = ctypes.c_double(0)
+    plen = ctypes.c_int32(0)
+    nexp = ctypes.c_int32(0)
+    ctr = np.zeros(3, np.int64)
+    st = lib().oracle_astar2d(_p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0,
+                              int(start[0]), int(start[1]), int(goal[0]), int(goal[1]),
+                              ctypes.byref(cost), _p(path, _i32p), path_cap, ctypes.byref(plen),
+                              _p(expand, _i32p) if with_expand else None, expand_cap,
+                              ctypes.byref(nexp), _p(ctr, _i64p))
+    cells = path[: plen.value]
+    out = dict(status=st, cost=cost.value, n_expanded=nexp.value,
+               path=[(int(c) // H, int(c) % H) for c in cells], path_cells=cells.copy(),
+               n_push=int(ctr[0]), n_pop=int(ctr[1]))
+    if with_expand:
+        e = expand[: min(nexp.value, expand_cap)]
+        out["expand_cells"] = e.copy()
+    return out
+
+
+def astar3d(occ: np.ndarray, start, goal, heuristic: str = "euclidean", with_expand: bool = True):
+    """Restatement of AStar3D.plan (a_star3d.py:33-78).  occ: uint8 [X, Y, Z]."""
+    occ = np.ascontiguousarray(occ, dtype=np.uint8)
+    X, Y, Z = occ.shape
+    n = X * Y * Z
+    path = np.zeros(n + 1, np.int32)
+    expand = np.zeros(n, np.int32)
+    s = np.asarray(start, np.int32)
+    g = np.asarray(goal, np.int32)
+    cost = ctypes.c_double(0)
+    plen = ctypes.c_int32(0)
+    nexp = ctypes.c_int32(0)
+    ctr = np.zeros(3, np.int64)
+    st = lib().oracle_astar3d(_p(occ, _u8p), X, Y, Z, 1 if heuristic == "manhattan" else 0,
+                              _p(s, _i32p), _p(g, _i32p), ctypes.byref(cost), _p(path, _i32p), n + 1,
+                              ctypes.byref(plen), _p(expand, _i32p) if with_expand else None, n,
+                              ctypes.byref(nexp), _p(ctr, _i64p))
+
+    def dec(c):
+        c = int(c)
+        return (c // (Y * Z), (c // Z) % Y, c % Z)
+
+    out = dict(status=st, cost=cost.value, n_expanded=nexp.value,
+               path=[dec(c) for c in path[: plen.value]], path_cells=path[: plen.value].copy(),
+               n_push=int(ctr[0]), n_pop=int(ctr[1]), n_iter=int(ctr[2]))
+    if with_expand:
+        out["expand_cells"] = expand[: nexp.value].copy()
+    return out
+
+
+def dstar2d(occ: np.ndarray, start, goal, max_process: int = 0):
+    """Restatement of DStar.plan (d_star.py:75-89).  Returns path start->goal."""
+    occ = np.ascontiguousarray(occ, dtype=np.uint8)
+    W, H = occ.shape
+    path = np.zeros(W * H + 1, np.int32)
+    cost = ctypes.c_double(0)
+    plen = ctypes.c_int32(0)
+    nproc = ctypes.c_int64(0)
+    st = lib().oracle_dstar2d(_p(occ, _u8p), W, H, int(start[0]), int(start[1]), int(goal[0]),
+                              int(goal[1]), ctypes.byref(cost), _p(path, _i32p), W * H + 1,
+                              ctypes.byref(plen), ctypes.byref(nproc), max_process)
+    cells = path[: plen.value]
+    return dict(status=st, cost=cost.value, n_process=nproc.value,
+                path=[(int(c) // H, int(c) % H) for c in cells], path_cells=cells.copy())
+
+
+def astar2d_batch(occ: np.ndarray, starts, goals, heuristic: str = "euclidean", path_cap: int = 4096,
+                  nthreads: int = 0):
+    """OpenMP batch of the AStar.plan restatement (one grid, many queries)."""
+    occ = np.ascontiguousarray(occ, dtype=np.uint8)
+    W, H = occ.shape
+    s = np.ascontiguousarray(starts, np.int32).reshape(-1, 2)
+    g = np.ascontiguousarray(goals, np.int32).reshape(-1, 2)
+    nq = len(s)
+    out = dict(cost=np.zeros(nq), path=np.zeros((nq, path_cap), np.int32), path_len=np.zeros(nq, np.int32),
+               n_expanded=np.zeros(nq, np.int32), counters=np.zeros((nq, 3), np.int64),
+               status=np.zeros(nq, np.int32))
+    lib().oracle_astar2d_batch(_p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0, _p(s, _i32p),
+                               _p(g, _i32p), nq, _p(out["cost"], _dp), _p(out["path"], _i32p), path_cap,
+                               _p(out["path_len"], _i32p), _p(out["n_expanded"], _i32p),
+                               _p(out["counters"], _i64p), _p(out["status"], _i32p), int(nthreads))
+    return out

@@ -1,0 +1,14 @@
+"""python_motion_planning_amd -- MI355X-native batched motion-planning core.
+
+Drop-in for the hot path of python_motion_planning (Slenderman00 fork): the same class names
+and plan() conventions, with the inner loops running as gfx950 HIP kernels (libpmp_hip.so,
+C-ABI in include/pmp.h).  There is no CPU fallback: without the library or a HIP device the
+planners raise.
+"""
+from .env import Env, Env3D, Grid, Grid3D, Map, Map3D, Node, Node3D, pack_bits  # noqa: F401
+from .graph_search import AStar, GraphSearcher  # noqa: F401
+from .planner import Planner, Planner3D  # noqa: F401
+from . import batch, workloads  # noqa: F401
+
+__all__ = ["Env", "Env3D", "Grid", "Grid3D", "Map", "Map3D", "Node", "Node3D", "Planner", "Planner3D",
+           "GraphSearcher", "AStar", "batch", "workloads"]

@@ -1,0 +1,94 @@
+"""ctypes binding of libpmp_hip.so (C-ABI declared in include/pmp.h).
+
+The product path has no CPU fallback: if the HIP library or a HIP device is missing, every
+planning call raises.  PyTorch is used only for device memory and the current HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpmp_hip.so")
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+
+# name -> (restype, argtypes); pointers are passed as raw device addresses (c_void_p)
+SIGNATURES = {
+    "pmp_create": (_vp, [_i]),
+    "pmp_destroy": (None, [_vp]),
+    "pmp_last_error": (ctypes.c_char_p, [_vp]),
+    "pmp_version": (ctypes.c_char_p, []),
+    "pmp_astar2d_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _i,
+                               _vp, _vp]),
+    "pmp_astar2d_reserve": (_i, [_vp, _i, _i, _i, _i]),
+}
+
+STATUS_FOUND, STATUS_NO_PATH, STATUS_PATH_OVERFLOW, STATUS_CAP_OVERFLOW, STATUS_REF_RAISES = range(5)
+
+
+class PMPError(RuntimeError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+_ctx = {}
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libpmp_hip.so and bind every C-ABI symbol.  Works without a GPU (no HIP call)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(path):
+                raise PMPError(f"{path} is missing: build it with `make -C {_HERE}/csrc` "
+                               "(python_motion_planning_amd has no CPU fallback)")
+            L = ctypes.CDLL(path)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def device_check():
+    import torch
+
+    if not torch.cuda.is_available():
+        raise PMPError("python_motion_planning_amd needs a HIP device (MI355X); none is visible")
+    return torch
+
+
+def context(device: int | None = None):
+    """Per-(thread, device) pmp_ctx."""
+    torch = device_check()
+    L = load_library()
+    dev = torch.cuda.current_device() if device is None else int(device)
+    key = (threading.get_ident(), dev)
+    c = _ctx.get(key)
+    if c is None:
+        c = L.pmp_create(dev)
+        if not c:
+            raise PMPError(f"pmp_create({dev}) failed")
+        _ctx[key] = c
+    return c
+
+
+def check(ctx, rc: int, what: str):
+    if rc != 0:
+        msg = load_library().pmp_last_error(ctx)
+        raise PMPError(f"{what} failed (rc={rc}): {msg.decode() if msg else ''}")
+
+
+def stream_ptr():
+    import torch
+
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,55 @@
+// Context, error channel and grow-only scratch arena of libpmp_hip.so.
+#include "pmp_internal.h"
+
+int pmp_set_err(pmp_ctx* ctx, int code, const std::string& msg)
+{
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+void* pmp_scratch(pmp_ctx* ctx, int slot, size_t bytes)
+{
+    if (bytes == 0) bytes = 16;
+    if (ctx->cap[slot] >= bytes) return ctx->buf[slot];
+    if (ctx->buf[slot]) {
+        (void)hipDeviceSynchronize();  // the old buffer may still be in use by queued work
+        (void)hipFree(ctx->buf[slot]);
+        ctx->buf[slot] = nullptr;
+        ctx->cap[slot] = 0;
+    }
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) {
+        pmp_set_err(ctx, PMP_ENOMEM, std::string("hipMalloc(") + std::to_string(bytes) + "): " + hipGetErrorString(e));
+        return nullptr;
+    }
+    ctx->buf[slot] = p;
+    ctx->cap[slot] = bytes;
+    return p;
+}
+
+extern "C" {
+
+pmp_ctx* pmp_create(int device)
+{
+    if (hipSetDevice(device) != hipSuccess) return nullptr;
+    pmp_ctx* c = new pmp_ctx();
+    c->device = device;
+    return c;
+}
+
+void pmp_destroy(pmp_ctx* ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipDeviceSynchronize();
+    for (int i = 0; i < 8; i++)
+        if (ctx->buf[i]) (void)hipFree(ctx->buf[i]);
+    delete ctx;
+}
+
+const char* pmp_last_error(pmp_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+const char* pmp_version(void) { return "pmp-hip 0.1 gfx950"; }
+
+}  // extern "C"

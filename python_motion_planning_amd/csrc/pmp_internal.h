@@ -1,0 +1,43 @@
+// Internal helpers shared by the gfx950 kernels of libpmp_hip.so (not part of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/pmp.h"
+
+struct pmp_ctx {
+    int device = 0;
+    std::string err;
+    // grow-only scratch arena, one buffer per use
+    void* buf[8] = {nullptr};
+    size_t cap[8] = {0};
+};
+
+enum ScratchSlot { SCR_HEAP = 0, SCR_CLOSED = 1, SCR_PDIR = 2, SCR_G = 3, SCR_AUX0 = 4, SCR_AUX1 = 5, SCR_AUX2 = 6, SCR_AUX3 = 7 };
+
+int pmp_set_err(pmp_ctx* ctx, int code, const std::string& msg);
+// Ensure scratch buffer `slot` holds at least `bytes`; returns device pointer or nullptr (error set).
+void* pmp_scratch(pmp_ctx* ctx, int slot, size_t bytes);
+
+#define PMP_HIP_CHECK(ctx, call)                                                                     \
+    do {                                                                                             \
+        hipError_t _e = (call);                                                                      \
+        if (_e != hipSuccess) return pmp_set_err((ctx), PMP_EHIP, std::string(#call) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+// ---------------------------------------------------------------------------------------------
+// wave64 helpers
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+__device__ __forceinline__ uint32_t rl_u32(uint32_t v, int lane) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+__device__ __forceinline__ double rl_f64(double v, int lane) {
+    uint64_t b = __double_as_longlong(v);
+    uint32_t lo = rl_u32((uint32_t)b, lane), hi = rl_u32((uint32_t)(b >> 32), lane);
+    return __longlong_as_double(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }

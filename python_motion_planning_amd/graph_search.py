@@ -1,0 +1,98 @@
+"""Graph-search planners: drop-in AStar (global_planner/graph_search/a_star.py) on the HIP kernels.
+
+plan() keeps the reference's signature and return convention; plan_batch() is the batched form
+(many start/goal pairs on one Grid) that the kernels are built for.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from . import batch
+from .env import Grid, Node
+from .planner import Planner
+
+
+class GraphSearcher(Planner):
+    """global_planner/graph_search/graph_search.py:11-87."""
+
+    def __init__(self, start: tuple, goal: tuple, env: Grid, heuristic_type: str = "euclidean") -> None:
+        super().__init__(start, goal, env)
+        self.heuristic_type = heuristic_type
+        self.motions = self.env.motions
+        self.obstacles = self.env.obstacles
+
+    def h(self, node: Node, goal: Node) -> float:
+        if self.heuristic_type == "manhattan":
+            return abs(goal.x - node.x) + abs(goal.y - node.y)
+        elif self.heuristic_type == "euclidean":
+            return math.hypot(goal.x - node.x, goal.y - node.y)
+
+    def cost(self, node1: Node, node2: Node) -> float:
+        if self.isCollision(node1, node2):
+            return float("inf")
+        return self.dist(node1, node2)
+
+    def isCollision(self, node1: Node, node2: Node) -> bool:
+        obs = self.env.obstacles
+        if node1.current in obs or node2.current in obs:
+            return True
+        x1, y1 = node1.x, node1.y
+        x2, y2 = node2.x, node2.y
+        if x1 != x2 and y1 != y2:
+            return (x1, y2) in obs or (x2, y1) in obs
+        return False
+
+
+class AStar(GraphSearcher):
+    """A* (a_star.py:13-124) -- the OPEN/CLOSED loop runs in the gfx950 kernel astar2d.hip."""
+
+    def __str__(self) -> str:
+        return "A*"
+
+    def plan(self) -> tuple:
+        """Returns (cost, path goal->start, expand list of Node) or ([], [], []) (a_star.py:39-83)."""
+        occ = self.env.occupancy()
+        W, H = occ.shape
+        r = batch.astar2d_batch(occ, np.array([self.start.current]), np.array([self.goal.current]),
+                                self.heuristic_type, path_cap=W * H + 1, expand_cap=W * H)
+        st = int(r["status"][0])
+        if st != 0:
+            if st == 1:
+                return [], [], []
+            raise RuntimeError(f"A* kernel status {st}")
+        plen = int(r["path_len"][0])
+        cells = r["path"][0, :plen].cpu().numpy()
+        nexp = int(r["n_expanded"][0])
+        exp = r["expand"][0, :nexp].cpu().numpy().astype(np.uint32)
+        path = [(int(c) // H, int(c) % H) for c in cells]
+        cost = 0
+        for a, b in zip(path[:-1], path[1:]):
+            cost += math.hypot(b[0] - a[0], b[1] - a[1])
+        return cost, path, self._expand_nodes(exp, H)
+
+    def _expand_nodes(self, exp: np.ndarray, H: int) -> list:
+        """Rebuild the reference's CLOSED Node objects (current, parent, g, h) from the kernel's
+        closure-ordered (cell | parent_dir << 28) records; g is re-accumulated exactly as
+        Node.__add__ does (node.py:39-41)."""
+        motions = self.env.motions
+        nodes, gmap = [], {}
+        for e in exp.tolist():
+            cell, d = e & 0x0FFFFFFF, e >> 28
+            cur = (cell // H, cell % H)
+            if d == 8:
+                node = Node(cur, cur, 0, 0)
+            else:
+                m = motions[d]
+                par = (cur[0] - m.x, cur[1] - m.y)
+                node = Node(cur, par, gmap[par] + m.g, self.h(Node(cur), self.goal))
+            gmap[cur] = node.g
+            nodes.append(node)
+        return nodes
+
+    @staticmethod
+    def plan_batch(occ: np.ndarray, starts, goals, heuristic_type: str = "euclidean", **kw):
+        """Batched plan over one occupancy grid; returns the device-tensor dict of
+        batch.astar2d_batch (cost, path_len, path goal->start, n_expanded, status)."""
+        return batch.astar2d_batch(occ, starts, goals, heuristic_type, **kw)

@@ -1,0 +1,157 @@
+"""HIP 2D A* (libpmp_hip.so, via the C-ABI) vs the reference's golden vectors and the oracle.
+
+Bar: bit-exact -- cost bits, path cells, closure (expand) order, expansion counts."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from golden_io import grid_cases, load_json, load_npz, seg
+
+pytestmark = pytest.mark.gpu
+
+
+def _pmp():
+    import python_motion_planning_amd as pmp
+
+    return pmp
+
+
+def test_readme_dropin_class():
+    pmp = _pmp()
+    fx = load_json("astar_readme.json")
+    env = pmp.Grid(51, 31)
+    obstacles = env.obstacles
+    for x, y in fx["obstacles"]:
+        obstacles.add((x, y))
+    env.update(obstacles)
+    for heur in ("euclidean", "manhattan"):
+        planner = pmp.AStar((5, 5), (45, 25), env, heur)
+        cost, path, expand = planner.plan()
+        exp = fx[heur]
+        assert cost == float.fromhex(exp["cost_hex"])
+        assert [x * 31 + y for (x, y) in path] == exp["path"]
+        assert [n.current[0] * 31 + n.current[1] for n in expand] == exp["expand"]
+    cost, path, expand = pmp.AStar((5, 5), (45, 25), env).plan()
+    assert repr(cost) == "54.04163056034261" and len(path) == 48 and len(expand) == 579
+    # expand nodes carry parent / g / h like the reference's CLOSED values
+    assert expand[0].current == (5, 5) and expand[0].parent == (5, 5) and expand[0].g == 0
+
+
+def test_small_grids_against_reference():
+    from python_motion_planning_amd import batch
+
+    for i, occ, z in grid_cases("astar_small.npz"):
+        W, H = occ.shape
+        heur = "manhattan" if z["manhattan"][i] else "euclidean"
+        r = batch.astar2d_batch(occ, z["start"][i][None], z["goal"][i][None], heur, path_cap=W * H + 1,
+                                expand_cap=W * H)
+        st = int(r["status"][0])
+        if not z["found"][i]:
+            assert st == 1, i
+            continue
+        assert st == 0, i
+        assert float(r["cost"][0]) == z["cost"][i], i
+        plen = int(r["path_len"][0])
+        assert np.array_equal(r["path"][0, :plen].cpu().numpy(), seg(z["path"], z["path_off"], i)), i
+        ne = int(r["n_expanded"][0])
+        assert ne == z["n_expanded"][i]
+        e = (r["expand"][0, :ne].cpu().numpy().astype(np.uint32) & 0x0FFFFFFF).astype(np.int32)
+        assert np.array_equal(e, seg(z["expand"], z["expand_off"], i)), i
+
+
+def test_c2_subset_against_reference():
+    from python_motion_planning_amd import batch, workloads as wl
+
+    z = load_npz("astar_1024.npz")
+    occ, starts, goals = wl.c2_workload(nq=4096)
+    idx = z["query_index"]
+    r = batch.astar2d_batch(occ, starts[idx], goals[idx], path_cap=4096, expand_cap=280000)
+    assert (r["status"].cpu().numpy() == 0).all()
+    assert np.array_equal(r["n_expanded"].cpu().numpy(), z["n_expanded"])
+    assert np.array_equal(r["cost"].cpu().numpy(), z["cost"])
+    pl = r["path_len"].cpu().numpy()
+    P = r["path"].cpu().numpy()
+    E = r["expand"].cpu().numpy().astype(np.uint32)
+    for i in range(len(idx)):
+        assert np.array_equal(P[i, :pl[i]], seg(z["path"], z["path_off"], i)), i
+        e = (E[i, : z["n_expanded"][i]] & 0x0FFFFFFF).astype(np.int32)
+        assert hashlib.sha1(e.tobytes()).hexdigest() == str(z["expand_sha1"][i]), i
+
+
+def test_c2_full_batch_against_oracle_and_properties():
+    """All 4096 C2 queries in one launch: a seeded 256-query sample bit-exact vs the oracle,
+    and size-independent properties on every query."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import batch, workloads as wl
+
+    occ, starts, goals = wl.c2_workload(nq=4096)
+    W, H = occ.shape
+    r = batch.astar2d_batch(occ, starts, goals, path_cap=4096, counters=True)
+    st = r["status"].cpu().numpy()
+    assert (st == 0).all()
+    cost = r["cost"].cpu().numpy()
+    pl = r["path_len"].cpu().numpy()
+    P = r["path"].cpu().numpy()
+    ne = r["n_expanded"].cpu().numpy()
+    ctr = r["counters"].cpu().numpy()
+    sample = np.random.default_rng(5).choice(4096, 256, replace=False)
+    ref = O.astar2d_batch(occ, starts[sample], goals[sample], path_cap=4096)
+    assert np.array_equal(ref["cost"], cost[sample])
+    assert np.array_equal(ref["n_expanded"], ne[sample])
+    assert np.array_equal(ref["counters"][:, :2], ctr[sample, :2])  # pushes and pops
+    for k, q in enumerate(sample):
+        assert np.array_equal(ref["path"][k, : ref["path_len"][k]], P[q, : pl[q]])
+    # properties on every query
+    sq2 = 2.0 ** 0.5
+    for q in range(4096):
+        p = P[q, : pl[q]]
+        xs, ys = p // H, p % H
+        assert xs[0] == goals[q, 0] and ys[0] == goals[q, 1]
+        assert xs[-1] == starts[q, 0] and ys[-1] == starts[q, 1]
+        dx, dy = np.diff(xs), np.diff(ys)
+        assert (np.maximum(np.abs(dx), np.abs(dy)) == 1).all()
+        assert not occ[xs, ys].any()
+        c = 0.0
+        for a, b in zip(np.abs(dx).tolist(), np.abs(dy).tolist()):
+            c += sq2 if (a and b) else 1.0
+        assert c == cost[q]
+    assert (ctr[:, 2] == ne).all() and (ctr[:, 1] <= ctr[:, 0]).all()
+
+
+def test_edge_cases():
+    import torch
+
+    from python_motion_planning_amd import batch, workloads as wl
+
+    occ = wl.readme_grid()
+    starts = np.array([[5, 5], [5, 5], [-3, 4], [5, 5], [20, 5], [5, 5]], np.int32)
+    goals = np.array([[45, 25], [5, 5], [45, 25], [60, 2], [45, 25], [20, 5]], np.int32)
+    r = batch.astar2d_batch(occ, starts, goals, path_cap=2048)
+    st = r["status"].cpu().numpy().tolist()
+    assert st == [0, 0, 1, 1, 1, 1]  # (20,5) is a wall cell: start blocked / goal blocked
+    assert int(r["path_len"][1]) == 1 and float(r["cost"][1]) == 0.0
+    # path_cap overflow is reported, never silently truncated
+    r = batch.astar2d_batch(occ, starts[:1], goals[:1], path_cap=10)
+    assert int(r["status"][0]) == 2 and int(r["path_len"][0]) == 48
+    # tiny heap capacity -> status 3
+    r = batch.astar2d_batch(occ, starts[:1], goals[:1], path_cap=64, reserve_slots=1, heap_cap=4)
+    assert int(r["status"][0]) == 3
+    torch.cuda.synchronize()
+    # restore default scratch sizing for later tests
+    batch.astar2d_batch(occ, starts[:1], goals[:1], path_cap=64, reserve_slots=64, heap_cap=0)
+
+
+def test_unreachable_and_empty_batch():
+    from python_motion_planning_amd import batch
+
+    occ = np.zeros((16, 16), np.uint8)
+    occ[:, 0] = occ[:, 15] = occ[0, :] = occ[15, :] = 1
+    occ[8, :] = 1  # wall splits the grid
+    r = batch.astar2d_batch(occ, np.array([[2, 2]]), np.array([[12, 12]]), path_cap=300)
+    assert int(r["status"][0]) == 1
+    from oracle import oracle as O
+
+    assert int(r["n_expanded"][0]) == O.astar2d(occ, (2, 2), (12, 12))["n_expanded"]
+    r = batch.astar2d_batch(occ, np.zeros((0, 2), np.int32), np.zeros((0, 2), np.int32), path_cap=4)
+    assert r["status"].numel() == 0
