@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--nq", type=int, default=4096)
     ap.add_argument("--cpu-sample", type=int, default=1024, help="queries in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workers", type=int, default=1024, help="persistent A* workers (waves) per GPU")
     args = ap.parse_args()
 
     import torch
@@ -71,7 +72,7 @@ def main():
     nexp = torch.empty(nq, dtype=torch.int32, device="cuda")
     status = torch.empty(nq, dtype=torch.int32, device="cuda")
     ctr = torch.empty((nq, 4), dtype=torch.int64, device="cuda")
-    _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, nq, 0), "reserve")
+    _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, args.workers, 0), "reserve")
 
     def step(counters=None):
         rc = L.pmp_astar2d_batch(ctx, _lib.stream_ptr(), occ_bits.data_ptr(), W, H, 0, s_d.data_ptr(),
@@ -156,7 +157,9 @@ def main():
                        "expansions_per_launch": int(counters[:, 2].sum()),
                        "max_expansions_query": int(counters[:, 2].max()),
                        "pushes_per_launch": int(counters[:, 0].sum()),
-                       "pops_per_launch": int(counters[:, 1].sum())},
+                       "pops_per_launch": int(counters[:, 1].sum()),
+                       "max_heap_entries": int(counters[:, 3].max()),
+                       "workers": args.workers},
         }
         print(json.dumps(out), flush=True)
     if dist:

@@ -83,7 +83,7 @@ def astar2d(occ: np.ndarray, start, goal, heuristic: str = "euclidean", with_exp
     cost = ctypes.c_double(0)
     plen = ctypes.c_int32(0)
     nexp = ctypes.c_int32(0)
-    ctr = np.zeros(3, np.int64)
+    ctr = np.zeros(4, np.int64)
     st = lib().oracle_astar2d(_p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0,
                               int(start[0]), int(start[1]), int(goal[0]), int(goal[1]),
                               ctypes.byref(cost), _p(path, _i32p), path_cap, ctypes.byref(plen),
@@ -92,7 +92,7 @@ def astar2d(occ: np.ndarray, start, goal, heuristic: str = "euclidean", with_exp
     cells = path[: plen.value]
     out = dict(status=st, cost=cost.value, n_expanded=nexp.value,
                path=[(int(c) // H, int(c) % H) for c in cells], path_cells=cells.copy(),
-               n_push=int(ctr[0]), n_pop=int(ctr[1]))
+               n_push=int(ctr[0]), n_pop=int(ctr[1]), max_heap=int(ctr[3]))
     if with_expand:
         e = expand[: min(nexp.value, expand_cap)]
         out["expand_cells"] = e.copy()
@@ -154,7 +154,7 @@ def astar2d_batch(occ: np.ndarray, starts, goals, heuristic: str = "euclidean", 
     g = np.ascontiguousarray(goals, np.int32).reshape(-1, 2)
     nq = len(s)
     out = dict(cost=np.zeros(nq), path=np.zeros((nq, path_cap), np.int32), path_len=np.zeros(nq, np.int32),
-               n_expanded=np.zeros(nq, np.int32), counters=np.zeros((nq, 3), np.int64),
+               n_expanded=np.zeros(nq, np.int32), counters=np.zeros((nq, 4), np.int64),
                status=np.zeros(nq, np.int32))
     lib().oracle_astar2d_batch(_p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0, _p(s, _i32p),
                                _p(g, _i32p), nq, _p(out["cost"], _dp), _p(out["path"], _i32p), path_cap,

@@ -171,7 +171,7 @@ int oracle_astar2d(const uint8_t* occ, int W, int H, int heuristic, int sx, int 
     const int64_t ncell = (int64_t)W * H;
     uint8_t* closed = (uint8_t*)calloc((size_t)ncell, 1);
     int32_t* cparent = (int32_t*)malloc(sizeof(int32_t) * (size_t)ncell);
-    int64_t cap = 1024, n = 0, npush = 0, npop = 0, nexp = 0;
+    int64_t cap = 1024, n = 0, npush = 0, npop = 0, nexp = 0, maxn = 1;
     anode_t* heap = (anode_t*)malloc(sizeof(anode_t) * (size_t)cap);
     const double SQ2 = sqrt(2.0);
     int status = 1;
@@ -239,6 +239,7 @@ int oracle_astar2d(const uint8_t* occ, int W, int H, int heuristic, int sx, int 
             }
             heap[n++] = nb;
             npush++;
+            if (n > maxn) maxn = n;
             a_siftdown(heap, 0, n - 1);
             if (nc == goal) break;
         }
@@ -249,7 +250,7 @@ int oracle_astar2d(const uint8_t* occ, int W, int H, int heuristic, int sx, int 
     }
 done:
     *n_expanded = (int32_t)nexp;
-    if (counters) { counters[0] = npush; counters[1] = npop; counters[2] = nexp; }
+    if (counters) { counters[0] = npush; counters[1] = npop; counters[2] = nexp; counters[3] = maxn; }
     if (status == 1) *path_len = 0;
     if (status == 0 && expand && nexp > expand_cap) status = 3;
     free(closed); free(cparent); free(heap);
@@ -607,7 +608,7 @@ ddone:
 }
 
 /* Batch of 2D A* queries on one grid, OpenMP over queries (the CPU baseline of bench.py).
- * path: [nq][path_cap] goal->start cells; counters [nq][3] (push, pop, expansions).
+ * path: [nq][path_cap] goal->start cells; counters [nq][4] (push, pop, expansions, max heap).
  * nthreads <= 0: OpenMP default.  Returns the number of queries with status 0. */
 int oracle_astar2d_batch(const uint8_t* occ, int W, int H, int heuristic, const int32_t* starts,
                          const int32_t* goals, int nq, double* cost, int32_t* path, int path_cap,
@@ -620,7 +621,7 @@ int oracle_astar2d_batch(const uint8_t* occ, int W, int H, int heuristic, const 
     for (int q = 0; q < nq; q++) {
         status[q] = oracle_astar2d(occ, W, H, heuristic, starts[2 * q], starts[2 * q + 1], goals[2 * q],
                                    goals[2 * q + 1], &cost[q], path + (int64_t)q * path_cap, path_cap,
-                                   &path_len[q], NULL, 0, &n_expanded[q], counters ? counters + 3 * (int64_t)q : NULL);
+                                   &path_len[q], NULL, 0, &n_expanded[q], counters ? counters + 4 * (int64_t)q : NULL);
         found += status[q] == 0;
     }
     return found;

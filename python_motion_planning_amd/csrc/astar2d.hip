@@ -1,360 +1,424 @@
-// Batched 2D A* for gfx950: one wave64 per query, bit-exact with the reference
-// AStar.plan (global_planner/graph_search/a_star.py:39-83) including CPython heapq's tie
-// behaviour (Lib/heapq.py heappush/_siftdown, heappop/_siftup) under Node.__lt__
-// (utils/environment/node.py:51-54).
+// Batched 2D A* for gfx950, bit-exact with the reference AStar.plan
+// (global_planner/graph_search/a_star.py:39-83) including CPython heapq's tie behaviour
+// (Lib/heapq.py heappush/_siftdown, heappop/_siftup) under Node.__lt__ (utils/environment/node.py:51-54).
 //
-// Heap entry (16 B, one dwordx4):  f64 f = g + h | u32 cell = x<<13 | y | u32 meta = hkey<<4 | dir
-//   hkey orders h exactly: euclidean h = hypot(dx,dy) == sqrt(d2) for |d| <= 16384 (verified
-//   against the oracle restatement of CPython's vector_norm), so hkey = d2; manhattan hkey = h.
+// Execution model: persistent workers, one wave64 each, pull query indices from an atomic queue.
+// A worker keeps the query's whole CPython heap array in LDS (positions >= lds_cap spill to a
+// per-worker HBM array) and a 4-bit-per-cell state array in HBM (0 = open, dir+1 = closed with
+// parent motion `dir`), reused across the queries it processes.
+//
+// Heap entry (12 B in LDS as SoA: f64 g[] | u32 cm[]):  cm = (x << 13 | y) << 4 | dir
 //   dir = motion index (env.py:52-55) that reached the cell from its parent, 8 = start.
-// g of a popped node is G[parent] + motion cost (G written when the parent was closed), so the
-// entry does not carry g.  Per-query scratch: heap, closed bits, parent-dir bytes, G (f64).
+//   f = g + h is recomputed per lane when an entry is loaded: euclidean h = hypot(dx, dy) ==
+//   sqrt(d2) exactly for |d| <= 16384 (pinned against CPython's vector_norm), manhattan h = |dx|+|dy|.
+//   Node.__lt__: f < f' or (f == f' and h < h'); h order == hkey order (d2, or |dx|+|dy|).
 //
-// Wave-parallel heap operations (the heap stays the CPython array, element for element):
-//   heappop  -> _siftup walks the smaller-child path to a leaf: lanes prefetch the 5-level
-//               subtree (62 entries) below the current position in ONE round, the walk then runs
-//               in registers (readlane); _siftdown of the old last element back up that path is a
-//               ballot over the path (the path is sorted, the "not less" set is a prefix).
-//   heappush -> _siftdown: all ancestors load in one round, one ballot finds the stop level.
+// heappop (CPython: pop last, put it at the root, _siftup walks the smaller child -- right child
+// when not left < right -- to a leaf, then _siftdown moves it back up).  The final array equals a
+// top-down walk along that same child path that moves each chosen child up while
+// !(last < child) and drops `last` at the first child it is less than (the path is sorted, so the
+// "not less" set is a prefix).  A chunk = 6 levels below the hole: lane l < 63 loads one sibling
+// pair, decides the CPython child choice and the two "may move up" bits; three ballots give the
+// masks; the walk itself is scalar; movers store in parallel.
+// heappush (_siftdown): the ancestors load in one round, one ballot finds how many move down.
 #include "pmp_internal.h"
 
 namespace {
 
 constexpr int kMaxDim = 8192;
-constexpr int kSubLanes = 62;  // 2 + 4 + 8 + 16 + 32 entries: subtree of depth 5
 constexpr double kSqrt2 = 1.4142135623730951;  // math.sqrt(2) == math.hypot(1, 1)
 
 __device__ __constant__ int c_mx[8] = {-1, -1, 0, 1, 1, 1, 0, -1};
 __device__ __constant__ int c_my[8] = {0, 1, 1, 1, 0, -1, -1, -1};
 
-struct Ent {
-    double f;
-    uint32_t cell, meta;
+struct Q {  // per-query uniform constants
+    int gx, gy;
+    int heur;
 };
+
+struct Ent {
+    double g, f;
+    uint32_t cm, hk;
+};
+
+__device__ __forceinline__ void ent_key(const Q& q, Ent& e)
+{
+    const int x = (int)(e.cm >> 17), y = (int)((e.cm >> 4) & 8191u);
+    const int dx = q.gx - x, dy = q.gy - y;
+    double h;
+    if (q.heur == 1) {
+        e.hk = (uint32_t)(abs(dx) + abs(dy));
+        h = (double)e.hk;
+    } else {
+        e.hk = (uint32_t)(dx * dx + dy * dy);
+        h = __dsqrt_rn((double)e.hk);
+    }
+    e.f = e.g + h;
+}
+
+// the start node has h = 0 (planner.py:15), not hypot(start, goal)
+__device__ __forceinline__ void ent_key_any(const Q& q, Ent& e)
+{
+    if ((e.cm & 15u) == 8u) {
+        e.hk = 0;
+        e.f = e.g;
+    } else {
+        ent_key(q, e);
+    }
+}
 
 __device__ __forceinline__ bool ent_lt(const Ent& a, const Ent& b)
 {
-    return a.f < b.f || (a.f == b.f && (a.meta >> 4) < (b.meta >> 4));
+    return a.f < b.f || (a.f == b.f && a.hk < b.hk);
 }
 
-__device__ __forceinline__ Ent ld_ent(const uint4* heap, int idx)
-{
-    uint4 v = heap[idx];
-    Ent e;
-    e.f = __hiloint2double((int)v.y, (int)v.x);
-    e.cell = v.z;
-    e.meta = v.w;
-    return e;
-}
+struct Heap {
+    double* lg;        // LDS g[lds_cap]
+    uint32_t* lcm;     // LDS cm[lds_cap]
+    uint4* spill;      // HBM entries for positions >= lds_cap: {g lo, g hi, cm, 0}
+    int lds_cap;
 
-__device__ __forceinline__ void st_ent(uint4* heap, int idx, const Ent& e)
-{
-    uint64_t b = (uint64_t)__double_as_longlong(e.f);
-    heap[idx] = make_uint4((uint32_t)b, (uint32_t)(b >> 32), e.cell, e.meta);
-}
-
-__device__ __forceinline__ Ent rl_ent(const Ent& e, int lane)
-{
-    Ent r;
-    r.f = rl_f64(e.f, lane);
-    r.cell = rl_u32(e.cell, lane);
-    r.meta = rl_u32(e.meta, lane);
-    return r;
-}
-
-__device__ __forceinline__ bool bit_at(const uint32_t* bits, uint32_t i) { return (bits[i >> 5] >> (i & 31)) & 1u; }
+    __device__ __forceinline__ void load(int p, double& g, uint32_t& cm) const
+    {
+        if (p < lds_cap) {
+            g = lg[p];
+            cm = lcm[p];
+        } else {
+            uint4 v = spill[p - lds_cap];
+            g = __hiloint2double((int)v.y, (int)v.x);
+            cm = v.z;
+        }
+    }
+    __device__ __forceinline__ void store(int p, double g, uint32_t cm) const
+    {
+        if (p < lds_cap) {
+            lg[p] = g;
+            lcm[p] = cm;
+        } else {
+            uint64_t b = (uint64_t)__double_as_longlong(g);
+            spill[p - lds_cap] = make_uint4((uint32_t)b, (uint32_t)(b >> 32), cm, 0u);
+        }
+    }
+};
 
 __device__ __forceinline__ bool occ_at(const uint32_t* occ, int W, int H, int x, int y)
 {
     if ((unsigned)x >= (unsigned)W || (unsigned)y >= (unsigned)H) return true;
-    return bit_at(occ, (uint32_t)x * (uint32_t)H + (uint32_t)y);
+    const uint32_t i = (uint32_t)x * (uint32_t)H + (uint32_t)y;
+    return (occ[i >> 5] >> (i & 31)) & 1u;
 }
 
-__device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+// 4-bit cell state: word i >> 3, nibble i & 7
+__device__ __forceinline__ uint32_t cst_at(const uint32_t* cst, uint32_t i) { return (cst[i >> 3] >> ((i & 7) * 4)) & 15u; }
 
-// lane l < 62 of a subtree prefetch below position `pos`: level j in 1..5, offset o
-__device__ __forceinline__ int sub_index(int pos, int l)
+__device__ __forceinline__ void wave_sync_mem()
 {
-    int j = 31 - __clz(l + 2);
-    int o = l + 2 - (1 << j);
-    return ((pos + 1) << j) - 1 + o;
+    // orders this wave's LDS and HBM accesses across lanes (one wave per workgroup)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 }
 
 __global__ __launch_bounds__(64) void astar2d_kernel(
     const uint32_t* __restrict__ occ, int W, int H, int heuristic, const int32_t* __restrict__ start_xy,
-    const int32_t* __restrict__ goal_xy, int nq, int q0, double* __restrict__ cost_out,
+    const int32_t* __restrict__ goal_xy, const int32_t* __restrict__ order, int nq, double* __restrict__ cost_out,
     int32_t* __restrict__ path_len_out, uint32_t* __restrict__ path_out, int path_cap,
     int32_t* __restrict__ nexp_out, uint32_t* __restrict__ expand_out, int expand_cap,
-    int64_t* __restrict__ counters, int32_t* __restrict__ status_out, uint4* __restrict__ heap_all, int heap_cap,
-    uint32_t* __restrict__ closed_all, size_t closed_words, uint8_t* __restrict__ pdir_all,
-    double* __restrict__ G_all, size_t ncell)
+    int64_t* __restrict__ counters, int32_t* __restrict__ status_out, int* __restrict__ queue,
+    uint4* __restrict__ spill_all, int heap_cap, int lds_cap, uint32_t* __restrict__ cst_all, size_t cst_words)
 {
-    const int slot = blockIdx.x;
-    const int q = q0 + slot;
-    if (q >= nq) return;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
-    uint4* heap = heap_all + (size_t)slot * heap_cap;
-    uint32_t* closed = closed_all + (size_t)slot * closed_words;
-    uint8_t* pdir = pdir_all + (size_t)slot * ncell;
-    double* G = G_all + (size_t)slot * ncell;
+    const int worker = blockIdx.x;
+    Heap hp;
+    hp.lg = reinterpret_cast<double*>(smem);
+    hp.lcm = reinterpret_cast<uint32_t*>(smem + (size_t)8 * lds_cap);
+    hp.spill = spill_all + (size_t)worker * (size_t)(heap_cap > lds_cap ? heap_cap - lds_cap : 0);
+    hp.lds_cap = lds_cap;
+    uint32_t* cst = cst_all + (size_t)worker * cst_words;
 
-    const int sx = start_xy[2 * q], sy = start_xy[2 * q + 1];
-    const int gx = goal_xy[2 * q], gy = goal_xy[2 * q + 1];
-    const bool sin_ = (unsigned)sx < (unsigned)W && (unsigned)sy < (unsigned)H;
-    const bool gin_ = (unsigned)gx < (unsigned)W && (unsigned)gy < (unsigned)H;
-    if (!sin_ || !gin_) {  // outside the grid: blocked -> no neighbours -> no path
-        if (lane == 0) {
-            status_out[q] = PMP_NO_PATH;
-            cost_out[q] = 0.0;
-            path_len_out[q] = 0;
-            nexp_out[q] = sin_ ? 1 : 0;
-            if (counters) { counters[4 * q] = 1; counters[4 * q + 1] = 1; counters[4 * q + 2] = 0; counters[4 * q + 3] = 1; }
+    for (;;) {
+        int qi = 0;
+        if (lane == 0) qi = atomicAdd(queue, 1);
+        qi = __shfl(qi, 0);
+        if (qi >= nq) break;
+        const int q = order ? order[qi] : qi;
+
+        // reset this worker's cell-state array
+        {
+            uint4* c4 = reinterpret_cast<uint4*>(cst);
+            const size_t n4 = cst_words / 4;
+            for (size_t i = lane; i < n4; i += 64) c4[i] = make_uint4(0u, 0u, 0u, 0u);
+            for (size_t i = n4 * 4 + lane; i < cst_words; i += 64) cst[i] = 0u;
         }
-        return;
-    }
-    const uint32_t start_cell = ((uint32_t)sx << 13) | (uint32_t)sy;
-    const uint32_t goal_cell = ((uint32_t)gx << 13) | (uint32_t)gy;
+        wave_sync_mem();
 
-    // root of the heap lives in registers (wave-uniform); heap[0] in memory mirrors it
-    Ent root;
-    root.f = 0.0;           // Node(start, start, 0, 0): g = h = 0 (planner.py:15)
-    root.cell = start_cell;
-    root.meta = 8u;         // hkey 0, dir 8 = start
-    if (lane == 0) st_ent(heap, 0, root);
-    wave_fence();
-
-    int n = 1;
-    int64_t npush = 1, npop = 0;
-    int nexp = 0, maxn = 1;
-    int st = PMP_NO_PATH;
-    double goal_cost = 0.0;
-    int plen = 0;
-
-    while (n > 0) {
-        // ------------------------------------------------------------ heappop: take root
-        const Ent node = root;
-        npop++;
-        n -= 1;
-        const int x = (int)(node.cell >> 13), y = (int)(node.cell & 8191u);
-        const int ndir = (int)(node.meta & 15u);
-        const uint32_t nlin = (uint32_t)x * (uint32_t)H + (uint32_t)y;
-
-        // ---- round A: subtree below root, the last element, neighbour occupancy/closed, G[parent]
-        Ent v;
-        v.f = 0.0; v.cell = 0; v.meta = 0;
-        if (lane < kSubLanes) {
-            int idx = sub_index(0, lane);
-            if (idx < n) v = ld_ent(heap, idx);
-        }
-        Ent lastv = v;
-        if (lane == 62 && n > 0) lastv = ld_ent(heap, n);
-        bool nb_ok = false;
-        uint32_t nbcell = 0;
-        bool self_closed = false;
-        if (lane < 8) {
-            const int nx = x + c_mx[lane], ny = y + c_my[lane];
-            bool coll = occ_at(occ, W, H, x, y) || occ_at(occ, W, H, nx, ny);
-            if ((lane & 1) && !coll) coll = occ_at(occ, W, H, x, ny) || occ_at(occ, W, H, nx, y);
-            if (!coll) nb_ok = !bit_at(closed, (uint32_t)nx * (uint32_t)H + (uint32_t)ny);
-            nbcell = ((uint32_t)nx << 13) | (uint32_t)ny;
-        } else if (lane == 8) {
-            self_closed = bit_at(closed, nlin);
-        }
-        double gpar = 0.0;
-        if (lane == 63 && ndir < 8) {
-            const int px = x - c_mx[ndir], py = y - c_my[ndir];
-            gpar = G[(uint32_t)px * (uint32_t)H + (uint32_t)py];
-        }
-        const bool is_stale = __shfl(self_closed ? 1 : 0, 8) != 0;
-
-        // ---- finish the pop (_siftup to a leaf, _siftdown of `last` back up the path)
-        if (n > 0) {
-            const Ent last = rl_ent(lastv, 62);
-            Ent pv;
-            pv.f = 0.0; pv.cell = 0; pv.meta = 0;
-            int ppos = 0;
-            int k = 0;
-            int cur = 0;
-            for (;;) {
-                int ocur = 0;
-                for (int j = 1; j <= 5; j++) {
-                    const int c = 2 * cur + 1;
-                    if (c >= n) break;
-                    const int ll = (1 << j) - 2 + 2 * ocur;
-                    Ent left = rl_ent(v, ll);
-                    Ent chosen = left;
-                    int ch = c, och = 2 * ocur;
-                    if (c + 1 < n) {
-                        Ent right = rl_ent(v, ll + 1);
-                        if (!ent_lt(left, right)) { chosen = right; ch = c + 1; och += 1; }
-                    }
-                    if (lane == k) { pv = chosen; ppos = ch; }
-                    k++;
-                    cur = ch;
-                    ocur = och;
-                }
-                if (2 * cur + 1 >= n) break;
-                // next round: subtree below cur
-                if (lane < kSubLanes) {
-                    int idx = sub_index(cur, lane);
-                    if (idx < n) v = ld_ent(heap, idx);
+        const int sx = start_xy[2 * q], sy = start_xy[2 * q + 1];
+        Q qc;
+        qc.gx = goal_xy[2 * q];
+        qc.gy = goal_xy[2 * q + 1];
+        qc.heur = heuristic;
+        const bool s_in = (unsigned)sx < (unsigned)W && (unsigned)sy < (unsigned)H;
+        const bool g_in = (unsigned)qc.gx < (unsigned)W && (unsigned)qc.gy < (unsigned)H;
+        if (!s_in || !g_in) {  // outside the grid: blocked -> no neighbours -> no path
+            if (lane == 0) {
+                status_out[q] = PMP_NO_PATH;
+                cost_out[q] = 0.0;
+                path_len_out[q] = 0;
+                nexp_out[q] = s_in ? 1 : 0;
+                if (counters) {
+                    counters[4 * q] = 1; counters[4 * q + 1] = 1; counters[4 * q + 2] = s_in ? 1 : 0; counters[4 * q + 3] = 1;
                 }
             }
-            const bool notless = lane < k && !ent_lt(last, pv);
-            const int m = __popcll(ballot(notless));
-            // e_1..e_m move up one level, `last` lands at p_m
-            if (lane < m) st_ent(heap, (ppos - 1) >> 1, pv);
-            const int pm = (m == 0) ? 0 : (int)rl_u32((uint32_t)ppos, m - 1);
-            if (lane == 0) st_ent(heap, pm, last);
-            root = (m >= 1) ? rl_ent(pv, 0) : last;
-            wave_fence();
+            continue;
         }
-        if (is_stale) continue;  // node.current already in CLOSED (a_star.py:57-58)
+        const uint32_t start_xy13 = ((uint32_t)sx << 13) | (uint32_t)sy;
+        const uint32_t goal_xy13 = ((uint32_t)qc.gx << 13) | (uint32_t)qc.gy;
 
-        const double gnode = (ndir == 8) ? 0.0 : rl_f64(gpar, 63) + ((ndir & 1) ? kSqrt2 : 1.0);
+        Ent root;  // heap[0], kept in registers (wave-uniform)
+        root.g = 0.0;
+        root.cm = (start_xy13 << 4) | 8u;
+        root.hk = 0;
+        root.f = 0.0;
+        if (lane == 0) hp.store(0, root.g, root.cm);
+        wave_sync_mem();
 
-        if (node.cell == goal_cell) {  // goal found (a_star.py:61-64)
+        int n = 1;
+        int64_t npush = 1, npop = 0;
+        int nexp = 0, maxn = 1;
+        int st = PMP_NO_PATH;
+        double goal_cost = 0.0;
+        int plen = 0;
+
+        while (n > 0) {
+            const Ent node = root;
+            npop++;
+            n -= 1;
+            const int x = (int)(node.cm >> 17), y = (int)((node.cm >> 4) & 8191u);
+            const int ndir = (int)(node.cm & 15u);
+            const uint32_t nlin = (uint32_t)x * (uint32_t)H + (uint32_t)y;
+
+            // ---- HBM round, issued first so it overlaps the LDS pop: neighbour collision
+            //      (isCollision, graph_search.py:61-87) and CLOSED membership of node + neighbours
+            bool nb_ok = false, self_closed = false;
+            uint32_t nbxy = 0;
+            if (lane < 8) {
+                const int nx = x + c_mx[lane], ny = y + c_my[lane];
+                bool coll = occ_at(occ, W, H, x, y) || occ_at(occ, W, H, nx, ny);
+                if (lane & 1) coll = coll || occ_at(occ, W, H, x, ny) || occ_at(occ, W, H, nx, y);
+                const uint32_t nbl = (uint32_t)nx * (uint32_t)H + (uint32_t)ny;
+                const uint32_t c = coll ? 1u : cst_at(cst, nbl);
+                nb_ok = !coll && c == 0u;
+                nbxy = ((uint32_t)nx << 13) | (uint32_t)ny;
+            } else if (lane == 8) {
+                self_closed = cst_at(cst, nlin) != 0u;
+            }
+
+            // ---- heappop: `last` = heap[n] goes to the root and sifts down the CPython path
+            if (n > 0) {
+                Ent last;
+                hp.load(n, last.g, last.cm);  // uniform address
+                ent_key_any(qc, last);
+                int hole = 0;
+                bool first = true;
+                for (;;) {
+                    // lane l < 63: sibling pair (level j = 1..6 below the hole, pair offset o)
+                    const int j = 32 - __clz(lane + 1);       // 1..7 (lane 63 -> 7: unused)
+                    const int o = lane + 1 - (1 << (j - 1));
+                    const int li = ((hole + 1) << j) - 1 + 2 * o;  // left child position
+                    Ent L, R;
+                    L.g = R.g = 0.0; L.f = R.f = 0.0; L.cm = R.cm = 0u; L.hk = R.hk = 0u;
+                    const bool vl = lane < 63 && li < n;
+                    const bool vr = lane < 63 && li + 1 < n;
+                    if (vl) { hp.load(li, L.g, L.cm); ent_key_any(qc, L); }
+                    if (vr) { hp.load(li + 1, R.g, R.cm); ent_key_any(qc, R); }
+                    const bool pick_r = vr && !ent_lt(L, R);                   // heapq._siftup
+                    const uint64_t dmask = ballot(pick_r);
+                    const uint64_t mlmask = ballot(vl && !ent_lt(last, L));     // may move up
+                    const uint64_t mrmask = ballot(vr && !ent_lt(last, R));
+                    // scalar walk through the chunk
+                    int cur = hole, oc = 0;
+                    uint64_t mover = 0, movr = 0;
+                    bool done = false;
+                    int first_lane = -1, first_r = 0;
+                    for (int lv = 1; lv <= 6; lv++) {
+                        const int c = 2 * cur + 1;
+                        if (c >= n) { done = true; break; }
+                        const int pl = (1 << (lv - 1)) - 1 + oc;  // pair lane
+                        const int r = (int)((dmask >> pl) & 1ull);
+                        const bool mv = r ? ((mrmask >> pl) & 1ull) : ((mlmask >> pl) & 1ull);
+                        if (!mv) { done = true; break; }
+                        mover |= 1ull << pl;
+                        movr |= (uint64_t)r << pl;
+                        if (first_lane < 0) { first_lane = pl; first_r = r; }
+                        cur = c + r;
+                        oc = 2 * oc + r;
+                    }
+                    if ((mover >> lane) & 1ull) {  // chosen child moves up one level
+                        const bool rr = (movr >> lane) & 1ull;
+                        const int pos = rr ? li + 1 : li;
+                        hp.store((pos - 1) >> 1, rr ? R.g : L.g, rr ? R.cm : L.cm);
+                    }
+                    if (first && first_lane >= 0) {
+                        // the child that moved into the root becomes the new root (wave-uniform)
+                        root.g = first_r ? rl_f64(R.g, first_lane) : rl_f64(L.g, first_lane);
+                        root.f = first_r ? rl_f64(R.f, first_lane) : rl_f64(L.f, first_lane);
+                        root.cm = first_r ? rl_u32(R.cm, first_lane) : rl_u32(L.cm, first_lane);
+                        root.hk = first_r ? rl_u32(R.hk, first_lane) : rl_u32(L.hk, first_lane);
+                    }
+                    first = false;
+                    hole = cur;
+                    if (done) break;
+                    wave_sync_mem();
+                }
+                if (lane == 0) hp.store(hole, last.g, last.cm);
+                if (hole == 0) root = last;
+                wave_sync_mem();
+            }
+            const bool stale = __shfl(self_closed ? 1 : 0, 8) != 0;
+            if (stale) continue;  // node.current in CLOSED (a_star.py:57-58)
+
+            if (node.cm >> 4 == goal_xy13) {  // goal found (a_star.py:61-64)
+                if (lane == 0) {
+                    atomicOr(&cst[nlin >> 3], (uint32_t)(ndir + 1) << ((nlin & 7) * 4));
+                    if (expand_out && nexp < expand_cap) expand_out[(size_t)q * expand_cap + nexp] = nlin | ((uint32_t)ndir << 28);
+                }
+                nexp++;
+                st = PMP_FOUND;
+                wave_sync_mem();
+                if (lane == 0) {  // extractPath (a_star.py:98-117): goal -> start, cost in that order
+                    int cx = x, cy = y;
+                    double cost = 0.0;
+                    int len = 0;
+                    uint32_t* pth = path_out + (size_t)q * path_cap;
+                    for (;;) {
+                        const uint32_t li = (uint32_t)cx * (uint32_t)H + (uint32_t)cy;
+                        if (len < path_cap) pth[len] = li;
+                        len++;
+                        if (cx == sx && cy == sy) break;
+                        const int d = (int)cst_at(cst, li) - 1;
+                        cost += (d & 1) ? kSqrt2 : 1.0;
+                        cx -= c_mx[d];
+                        cy -= c_my[d];
+                    }
+                    goal_cost = cost;
+                    plen = len;
+                }
+                break;
+            }
+
+            // g of the popped node (node.py:39-41 accumulated it when it was pushed)
+            const double gnode = node.g;
+            // ---- neighbours in motion order; push the goal and stop (a_star.py:66-80)
+            uint64_t vm = ballot(nb_ok) & 0xffull;
+            const uint64_t gm = ballot(nb_ok && nbxy == goal_xy13) & 0xffull;
+            if (gm) vm &= (gm << 1) - 1;
+            Ent item;
+            {
+                const int m = lane & 7;
+                item.g = gnode + ((m & 1) ? kSqrt2 : 1.0);
+                item.cm = (nbxy << 4) | (uint32_t)m;
+                item.f = 0.0;
+                item.hk = 0u;
+                if (lane < 8) ent_key(qc, item);
+            }
+            bool overflow = false;
+            while (vm) {
+                const int m = __ffsll((long long)vm) - 1;
+                vm &= vm - 1;
+                if (n >= heap_cap) { overflow = true; break; }
+                Ent it;
+                it.g = rl_f64(item.g, m);
+                it.f = rl_f64(item.f, m);
+                it.cm = rl_u32(item.cm, m);
+                it.hk = rl_u32(item.hk, m);
+                const int np1 = n + 1;
+                const int depth = 31 - __clz(np1);
+                Ent a;
+                a.g = a.f = 0.0; a.cm = a.hk = 0u;
+                const bool valid = lane < depth;
+                if (valid) { hp.load((np1 >> (lane + 1)) - 1, a.g, a.cm); ent_key_any(qc, a); }
+                const bool less = valid && ent_lt(it, a);
+                const int t = __popcll(ballot(less));
+                if (lane < t) hp.store((np1 >> lane) - 1, a.g, a.cm);
+                const int ipos = (np1 >> t) - 1;
+                if (lane == 0) hp.store(ipos, it.g, it.cm);
+                if (ipos == 0) root = it;
+                n += 1;
+                npush++;
+                wave_sync_mem();
+            }
+            if (n > maxn) maxn = n;
+            if (overflow) { st = PMP_CAP_OVERFLOW; break; }
+
+            // ---- CLOSED[node.current] = node (a_star.py:82)
             if (lane == 0) {
-                atomicOr(&closed[nlin >> 5], 1u << (nlin & 31));
-                pdir[nlin] = (uint8_t)ndir;
-                G[nlin] = gnode;
+                atomicOr(&cst[nlin >> 3], (uint32_t)(ndir + 1) << ((nlin & 7) * 4));
                 if (expand_out && nexp < expand_cap) expand_out[(size_t)q * expand_cap + nexp] = nlin | ((uint32_t)ndir << 28);
             }
             nexp++;
-            st = PMP_FOUND;
-            wave_fence();
-            if (lane == 0) {  // extractPath (a_star.py:98-117): goal -> start, cost in that order
-                uint32_t cx = (uint32_t)x, cy = (uint32_t)y;
-                double cost = 0.0;
-                int len = 0;
-                uint32_t* pth = path_out + (size_t)q * path_cap;
-                for (;;) {
-                    if (len < path_cap) pth[len] = cx * (uint32_t)H + cy;
-                    len++;
-                    if (((cx << 13) | cy) == start_cell) break;
-                    const int d = pdir[cx * (uint32_t)H + cy];
-                    cost += (d & 1) ? kSqrt2 : 1.0;
-                    cx = (uint32_t)((int)cx - c_mx[d]);
-                    cy = (uint32_t)((int)cy - c_my[d]);
-                }
-                goal_cost = cost;
-                plen = len;
-            }
-            break;
+            wave_sync_mem();
         }
 
-        // ---- neighbours in motion order; push the goal and stop (a_star.py:66-80)
-        uint64_t vm = ballot(nb_ok) & 0xffull;
-        const uint64_t gm = ballot(nb_ok && nbcell == goal_cell) & 0xffull;
-        if (gm) vm &= (gm << 1) - 1;  // keep motions up to and including the goal motion
-        Ent item;
-        {
-            const int m = lane & 7;
-            const int nx = x + c_mx[m], ny = y + c_my[m];
-            const double gn = gnode + ((m & 1) ? kSqrt2 : 1.0);
-            const int dx = gx - nx, dy = gy - ny;
-            uint32_t hk;
-            double h;
-            if (heuristic == 1) {
-                hk = (uint32_t)(abs(dx) + abs(dy));
-                h = (double)hk;
-            } else {
-                hk = (uint32_t)(dx * dx + dy * dy);
-                h = __dsqrt_rn((double)hk);
-            }
-            item.f = gn + h;
-            item.cell = ((uint32_t)nx << 13) | (uint32_t)ny;
-            item.meta = (hk << 4) | (uint32_t)m;
-        }
-        bool overflow = false;
-        while (vm) {
-            const int m = __ffsll((long long)vm) - 1;
-            vm &= vm - 1;
-            const Ent it = rl_ent(item, m);
-            if (n >= heap_cap) { overflow = true; break; }
-            // heappush -> _siftdown: ancestors of position n, one round
-            const int np1 = n + 1;
-            const int depth = 31 - __clz(np1);
-            Ent a;
-            a.f = 0.0; a.cell = 0; a.meta = 0;
-            const bool valid = lane < depth;
-            if (valid) a = ld_ent(heap, (np1 >> (lane + 1)) - 1);
-            const bool less = valid && ent_lt(it, a);
-            const int t = __popcll(ballot(less));
-            if (lane < t) st_ent(heap, (np1 >> lane) - 1, a);
-            const int ipos = (np1 >> t) - 1;
-            if (lane == 0) st_ent(heap, ipos, it);
-            if (ipos == 0) root = it;
-            n += 1;
-            npush++;
-            wave_fence();
-        }
-        if (n > maxn) maxn = n;
-        if (overflow) { st = PMP_CAP_OVERFLOW; break; }
-
-        // ---- CLOSED[node.current] = node (a_star.py:82)
         if (lane == 0) {
-            atomicOr(&closed[nlin >> 5], 1u << (nlin & 31));
-            pdir[nlin] = (uint8_t)ndir;
-            G[nlin] = gnode;
-            if (expand_out && nexp < expand_cap) expand_out[(size_t)q * expand_cap + nexp] = nlin | ((uint32_t)ndir << 28);
+            int s = st;
+            if (s == PMP_FOUND && plen > path_cap) s = PMP_PATH_OVERFLOW;
+            status_out[q] = s;
+            cost_out[q] = (st == PMP_FOUND) ? goal_cost : 0.0;
+            path_len_out[q] = (st == PMP_FOUND) ? plen : 0;
+            nexp_out[q] = nexp;
+            if (counters) {
+                counters[4 * q + 0] = npush;
+                counters[4 * q + 1] = npop;
+                counters[4 * q + 2] = nexp;
+                counters[4 * q + 3] = maxn;
+            }
         }
-        nexp++;
-        wave_fence();
+        wave_sync_mem();
     }
+}
 
-    if (lane == 0) {
-        int s = st;
-        if (s == PMP_FOUND && plen > path_cap) s = PMP_PATH_OVERFLOW;
-        status_out[q] = s;
-        cost_out[q] = (st == PMP_FOUND) ? goal_cost : 0.0;
-        path_len_out[q] = (st == PMP_FOUND) ? plen : 0;
-        nexp_out[q] = nexp;
-        if (counters) {
-            counters[4 * q + 0] = npush;
-            counters[4 * q + 1] = npop;
-            counters[4 * q + 2] = nexp;
-            counters[4 * q + 3] = maxn;
-        }
-    }
+struct AStarCfg {
+    int W = 0, H = 0;
+    int workers = 0;     // persistent waves
+    int heap_cap = 0;    // CPython heap capacity per query (entries)
+    int lds_cap = 0;     // heap entries held in LDS per worker
+};
+AStarCfg g_cfg;
+
+int default_workers() { return 256 * 4; }
+int default_lds_cap(int workers_per_cu)
+{
+    // 160 KiB LDS per CU shared by the resident workers; 12 B per entry, keep a little slack
+    int bytes = (160 * 1024) / workers_per_cu - 256;
+    return (bytes / 12) & ~15;
+}
+int default_heap_cap(int W, int H)
+{
+    size_t c = 8 * (size_t)W * H + 8;
+    return (int)(c < (size_t)(1 << 20) ? c : (size_t)(1 << 20));
 }
 
 }  // namespace
 
-struct AStarCfg {
-    int W = 0, H = 0, slots = 0, heap_cap = 0;
-};
-static AStarCfg g_astar_reserved;  // per-process default; set by pmp_astar2d_reserve
-
-static size_t astar_slot_bytes(int W, int H, int heap_cap)
-{
-    size_t ncell = (size_t)W * H;
-    return (size_t)heap_cap * 16 + ((ncell + 31) / 32) * 4 + ncell + ncell * 8;
-}
-
-static int astar_default_heap_cap(int W, int H)
-{
-    size_t ncell = (size_t)W * H;
-    size_t cap = 8 * ncell + 8;
-    if (cap > (size_t)(1 << 18)) cap = (size_t)1 << 18;
-    return (int)cap;
-}
-
-extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int max_slots, int heap_cap)
+extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int workers, int heap_cap)
 {
     if (!ctx) return PMP_EINVAL;
-    if (W < 1 || H < 1 || W > kMaxDim || H > kMaxDim || max_slots < 1)
-        return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_reserve: bad dims/slots");
-    if (heap_cap <= 0) heap_cap = astar_default_heap_cap(W, H);
-    size_t ncell = (size_t)W * H;
-    if (!pmp_scratch(ctx, SCR_HEAP, (size_t)max_slots * heap_cap * 16)) return PMP_ENOMEM;
-    if (!pmp_scratch(ctx, SCR_CLOSED, (size_t)max_slots * ((ncell + 31) / 32) * 4)) return PMP_ENOMEM;
-    if (!pmp_scratch(ctx, SCR_PDIR, (size_t)max_slots * ncell)) return PMP_ENOMEM;
-    if (!pmp_scratch(ctx, SCR_G, (size_t)max_slots * ncell * 8)) return PMP_ENOMEM;
-    g_astar_reserved.W = W;
-    g_astar_reserved.H = H;
-    g_astar_reserved.slots = max_slots;
-    g_astar_reserved.heap_cap = heap_cap;
+    if (W < 1 || H < 1 || W > kMaxDim || H > kMaxDim || workers < 1)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_reserve: bad dims/workers");
+    if (heap_cap <= 0) heap_cap = default_heap_cap(W, H);
+    const int per_cu = (workers + 255) / 256;
+    int lds_cap = default_lds_cap(per_cu < 1 ? 1 : per_cu);
+    if (lds_cap > heap_cap) lds_cap = (heap_cap + 15) & ~15;
+    const size_t ncell = (size_t)W * H;
+    const size_t cst_words = ((ncell + 7) / 8 + 3) & ~(size_t)3;
+    const size_t spill = heap_cap > lds_cap ? (size_t)(heap_cap - lds_cap) : 0;
+    if (!pmp_scratch(ctx, SCR_HEAP, (size_t)workers * spill * 16 + 16)) return PMP_ENOMEM;
+    if (!pmp_scratch(ctx, SCR_CLOSED, (size_t)workers * cst_words * 4)) return PMP_ENOMEM;
+    if (!pmp_scratch(ctx, SCR_AUX0, 256)) return PMP_ENOMEM;
+    g_cfg.W = W;
+    g_cfg.H = H;
+    g_cfg.workers = workers;
+    g_cfg.heap_cap = heap_cap;
+    g_cfg.lds_cap = lds_cap;
     return PMP_OK;
 }
 
@@ -370,39 +434,28 @@ extern "C" int pmp_astar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
     if (heuristic != 0 && heuristic != 1) return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_batch: heuristic must be 0 or 1");
     if (nq < 0 || path_cap < 1 || (expand && expand_cap < 1))
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_batch: bad nq/path_cap/expand_cap");
+    if (nq == 0) return PMP_OK;
     if (!occ_bits || !start_xy || !goal_xy || !cost || !path_len || !path || !n_expanded || !status)
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_batch: null pointer argument");
-    if (nq == 0) return PMP_OK;
     PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
-    hipStream_t s = (hipStream_t)stream;
-
-    int heap_cap, slots;
-    if (g_astar_reserved.W == W && g_astar_reserved.H == H) {
-        heap_cap = g_astar_reserved.heap_cap;
-        slots = g_astar_reserved.slots;
-    } else {
-        heap_cap = astar_default_heap_cap(W, H);
-        const size_t budget = (size_t)64 << 30;  // 64 GiB of scratch by default
-        size_t per = astar_slot_bytes(W, H, heap_cap);
-        slots = (int)((budget / per) < (size_t)nq ? (budget / per) : (size_t)nq);
-        if (slots < 1) slots = 1;
+    if (!(g_cfg.W == W && g_cfg.H == H)) {
+        int workers = default_workers();
+        if (workers > nq) workers = nq;
+        int rc = pmp_astar2d_reserve(ctx, W, H, workers, 0);
+        if (rc) return rc;
     }
-    if (slots > nq) slots = nq;
+    const int workers = g_cfg.workers < nq ? g_cfg.workers : nq;
     const size_t ncell = (size_t)W * H;
-    const size_t closed_words = (ncell + 31) / 32;
-    uint4* heap = (uint4*)pmp_scratch(ctx, SCR_HEAP, (size_t)slots * heap_cap * 16);
-    uint32_t* closed = (uint32_t*)pmp_scratch(ctx, SCR_CLOSED, (size_t)slots * closed_words * 4);
-    uint8_t* pdir = (uint8_t*)pmp_scratch(ctx, SCR_PDIR, (size_t)slots * ncell);
-    double* G = (double*)pmp_scratch(ctx, SCR_G, (size_t)slots * ncell * 8);
-    if (!heap || !closed || !pdir || !G) return PMP_ENOMEM;
-
-    for (int q0 = 0; q0 < nq; q0 += slots) {
-        const int nb = (nq - q0) < slots ? (nq - q0) : slots;
-        PMP_HIP_CHECK(ctx, hipMemsetAsync(closed, 0, (size_t)nb * closed_words * 4, s));
-        hipLaunchKernelGGL(astar2d_kernel, dim3(nb), dim3(64), 0, s, occ_bits, W, H, heuristic, start_xy, goal_xy,
-                           nq, q0, cost, path_len, path, path_cap, n_expanded, expand, expand_cap, counters,
-                           status, heap, heap_cap, closed, closed_words, pdir, G, ncell);
-        PMP_HIP_CHECK(ctx, hipGetLastError());
-    }
+    const size_t cst_words = ((ncell + 7) / 8 + 3) & ~(size_t)3;
+    uint4* spill = (uint4*)ctx->buf[SCR_HEAP];
+    uint32_t* cst = (uint32_t*)ctx->buf[SCR_CLOSED];
+    int* queue = (int*)ctx->buf[SCR_AUX0];
+    hipStream_t s = (hipStream_t)stream;
+    const size_t lds = (size_t)g_cfg.lds_cap * 12;
+    PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
+    hipLaunchKernelGGL(astar2d_kernel, dim3(workers), dim3(64), lds, s, occ_bits, W, H, heuristic, start_xy,
+                       goal_xy, (const int32_t*)nullptr, nq, cost, path_len, path, path_cap, n_expanded, expand,
+                       expand_cap, counters, status, queue, spill, g_cfg.heap_cap, g_cfg.lds_cap, cst, cst_words);
+    PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }
