@@ -113,8 +113,10 @@ __device__ __forceinline__ uint32_t cst_at(const uint32_t* cst, uint32_t i) { re
 
 __device__ __forceinline__ void wave_sync_mem()
 {
-    // orders this wave's LDS and HBM accesses across lanes (one wave per workgroup)
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    // Orders this wave's LDS and HBM accesses across its lanes.  A wave's memory operations are
+    // performed in order, so wavefront scope needs no s_waitcnt (LLVM AMDGPU memory model): this
+    // is a compiler barrier only and never stalls on outstanding HBM stores.
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
 __global__ __launch_bounds__(64) void astar2d_kernel(
@@ -196,22 +198,26 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
             const int ndir = (int)(node.cm & 15u);
             const uint32_t nlin = (uint32_t)x * (uint32_t)H + (uint32_t)y;
 
-            // ---- HBM round, issued first so it overlaps the LDS pop: neighbour collision
-            //      (isCollision, graph_search.py:61-87) and CLOSED membership of node + neighbours
-            bool nb_ok = false, self_closed = false;
-            uint32_t nbxy = 0;
-            if (lane < 8) {
-                const int nx = x + c_mx[lane], ny = y + c_my[lane];
-                bool coll = occ_at(occ, W, H, x, y) || occ_at(occ, W, H, nx, ny);
-                if (lane & 1) coll = coll || occ_at(occ, W, H, x, ny) || occ_at(occ, W, H, nx, y);
-                const uint32_t nbl = (uint32_t)nx * (uint32_t)H + (uint32_t)ny;
-                const uint32_t c = coll ? 1u : cst_at(cst, nbl);
-                nb_ok = !coll && c == 0u;
-                nbxy = ((uint32_t)nx << 13) | (uint32_t)ny;
-            } else if (lane == 8) {
-                self_closed = cst_at(cst, nlin) != 0u;
+            // ---- HBM round, issued first so it overlaps the LDS pop: the 3x3 block around the node
+            //      (occupancy bits for isCollision, graph_search.py:61-87, and CLOSED state nibbles),
+            //      all loads independent.  Lane i < 9 -> cell (x + i/3 - 1, y + i%3 - 1) occupancy,
+            //      lane 9 + i -> its state word.
+            uint32_t blk_word = 0;
+            bool blk_occ = false;
+            uint32_t blk_shift = 0;
+            bool blk_in = false;
+            {
+                const int i = lane < 9 ? lane : lane - 9;
+                const int cx = x + i / 3 - 1, cy = y + i % 3 - 1;
+                blk_in = lane < 18 && (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
+                const uint32_t ci = (uint32_t)cx * (uint32_t)H + (uint32_t)cy;
+                if (lane < 9) {
+                    blk_occ = blk_in ? ((occ[ci >> 5] >> (ci & 31)) & 1u) != 0u : true;
+                } else if (blk_in) {
+                    blk_word = cst[ci >> 3];
+                    blk_shift = (ci & 7) * 4;
+                }
             }
-
             // ---- heappop: `last` = heap[n] goes to the root and sifts down the CPython path
             if (n > 0) {
                 Ent last;
@@ -273,15 +279,17 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 if (hole == 0) root = last;
                 wave_sync_mem();
             }
-            const bool stale = __shfl(self_closed ? 1 : 0, 8) != 0;
-            if (stale) continue;  // node.current in CLOSED (a_star.py:57-58)
+            // 3x3 masks: bit k = cell (x + k/3 - 1, y + k%3 - 1); node is k = 4
+            const uint32_t occ9 = (uint32_t)ballot(lane < 9 && blk_occ) & 0x1ffu;
+            const uint32_t cls9 = (uint32_t)(ballot(lane >= 9 && lane < 18 && blk_in && ((blk_word >> blk_shift) & 15u) != 0u) >> 9) & 0x1ffu;
+            if (cls9 & 16u) continue;  // node.current in CLOSED (a_star.py:57-58)
+            // CLOSED[node.current] = node (a_star.py:82): the node's state word was loaded by lane 13
+            // and only this wave writes it, so store it back now (fire-and-forget, off the critical path)
+            if (lane == 13) cst[nlin >> 3] = blk_word | ((uint32_t)(ndir + 1) << blk_shift);
+            if (lane == 0 && expand_out && nexp < expand_cap) expand_out[(size_t)q * expand_cap + nexp] = nlin | ((uint32_t)ndir << 28);
+            nexp++;
 
-            if (node.cm >> 4 == goal_xy13) {  // goal found (a_star.py:61-64)
-                if (lane == 0) {
-                    atomicOr(&cst[nlin >> 3], (uint32_t)(ndir + 1) << ((nlin & 7) * 4));
-                    if (expand_out && nexp < expand_cap) expand_out[(size_t)q * expand_cap + nexp] = nlin | ((uint32_t)ndir << 28);
-                }
-                nexp++;
+            if (node.cm >> 4 == goal_xy13) {  // goal found (a_star.py:61-64); already closed above
                 st = PMP_FOUND;
                 wave_sync_mem();
                 if (lane == 0) {  // extractPath (a_star.py:98-117): goal -> start, cost in that order
@@ -308,6 +316,15 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
             // g of the popped node (node.py:39-41 accumulated it when it was pushed)
             const double gnode = node.g;
             // ---- neighbours in motion order; push the goal and stop (a_star.py:66-80)
+            bool nb_ok = false;
+            uint32_t nbxy = 0;
+            if (lane < 8) {
+                const int ax = c_mx[lane] + 1, ay = c_my[lane] + 1;
+                uint32_t need = 16u | (1u << (ax * 3 + ay));                 // both endpoints
+                if (lane & 1) need |= (1u << (3 + ay)) | (1u << (ax * 3 + 1));  // both corners
+                nb_ok = (occ9 & need) == 0u && ((cls9 >> (ax * 3 + ay)) & 1u) == 0u;
+                nbxy = ((uint32_t)(x + c_mx[lane]) << 13) | (uint32_t)(y + c_my[lane]);
+            }
             uint64_t vm = ballot(nb_ok) & 0xffull;
             const uint64_t gm = ballot(nb_ok && nbxy == goal_xy13) & 0xffull;
             if (gm) vm &= (gm << 1) - 1;
@@ -348,14 +365,6 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
             }
             if (n > maxn) maxn = n;
             if (overflow) { st = PMP_CAP_OVERFLOW; break; }
-
-            // ---- CLOSED[node.current] = node (a_star.py:82)
-            if (lane == 0) {
-                atomicOr(&cst[nlin >> 3], (uint32_t)(ndir + 1) << ((nlin & 7) * 4));
-                if (expand_out && nexp < expand_cap) expand_out[(size_t)q * expand_cap + nexp] = nlin | ((uint32_t)ndir << 28);
-            }
-            nexp++;
-            wave_sync_mem();
         }
 
         if (lane == 0) {
