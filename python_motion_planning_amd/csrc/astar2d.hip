@@ -72,10 +72,17 @@ __device__ __forceinline__ bool ent_lt(const Ent& a, const Ent& b)
     return a.f < b.f || (a.f == b.f && a.hk < b.hk);
 }
 
+typedef __attribute__((address_space(3))) double lds_f64;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// The CPython heap array: positions < lds_cap in LDS (explicit address space 3, so every access is
+// a ds_read/ds_write), positions >= lds_cap in a per-worker HBM spill reached only through buffer
+// instructions (a distinct instruction class, so the compiler can never fold the two paths into
+// one flat access that waits on both counters).
 struct Heap {
-    double* lg;        // LDS g[lds_cap]
-    uint32_t* lcm;     // LDS cm[lds_cap]
-    uint4* spill;      // HBM entries for positions >= lds_cap: {g lo, g hi, cm, 0}
+    lds_f64* lg;       // LDS g[lds_cap]
+    lds_u32* lcm;      // LDS cm[lds_cap]
+    __amdgpu_buffer_rsrc_t spill;  // HBM entries {g lo, g hi, cm, 0} for positions >= lds_cap
     int lds_cap;
 
     __device__ __forceinline__ void load(int p, double& g, uint32_t& cm) const
@@ -84,7 +91,7 @@ struct Heap {
             g = lg[p];
             cm = lcm[p];
         } else {
-            uint4 v = spill[p - lds_cap];
+            const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(spill, (p - lds_cap) * 16, 0, 0));
             g = __hiloint2double((int)v.y, (int)v.x);
             cm = v.z;
         }
@@ -95,18 +102,13 @@ struct Heap {
             lg[p] = g;
             lcm[p] = cm;
         } else {
-            uint64_t b = (uint64_t)__double_as_longlong(g);
-            spill[p - lds_cap] = make_uint4((uint32_t)b, (uint32_t)(b >> 32), cm, 0u);
+            const uint64_t b = (uint64_t)__double_as_longlong(g);
+            const uint4 v = make_uint4((uint32_t)b, (uint32_t)(b >> 32), cm, 0u);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
+                                                   spill, (p - lds_cap) * 16, 0, 0);
         }
     }
 };
-
-__device__ __forceinline__ bool occ_at(const uint32_t* occ, int W, int H, int x, int y)
-{
-    if ((unsigned)x >= (unsigned)W || (unsigned)y >= (unsigned)H) return true;
-    const uint32_t i = (uint32_t)x * (uint32_t)H + (uint32_t)y;
-    return (occ[i >> 5] >> (i & 31)) & 1u;
-}
 
 // 4-bit cell state: word i >> 3, nibble i & 7
 __device__ __forceinline__ uint32_t cst_at(const uint32_t* cst, uint32_t i) { return (cst[i >> 3] >> ((i & 7) * 4)) & 15u; }
@@ -117,6 +119,108 @@ __device__ __forceinline__ void wave_sync_mem()
     // performed in order, so wavefront scope needs no s_waitcnt (LLVM AMDGPU memory model): this
     // is a compiler barrier only and never stalls on outstanding HBM stores.
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+// SPILL = false: every position touched is < lds_cap (pure ds_read/ds_write code, no vmcnt waits).
+template <bool SPILL>
+__device__ __forceinline__ void hload(const Heap& hp, int p, double& g, uint32_t& cm)
+{
+    if constexpr (SPILL) {
+        hp.load(p, g, cm);
+    } else {
+        g = hp.lg[p];
+        cm = hp.lcm[p];
+    }
+}
+template <bool SPILL>
+__device__ __forceinline__ void hstore(const Heap& hp, int p, double g, uint32_t cm)
+{
+    if constexpr (SPILL) {
+        hp.store(p, g, cm);
+    } else {
+        hp.lg[p] = g;
+        hp.lcm[p] = cm;
+    }
+}
+
+// heappop on a heap of n (>0, already decremented) entries whose old last element sits at position
+// n; the old root has been taken by the caller.  Updates `root` (wave-uniform copy of heap[0]).
+template <bool SPILL>
+__device__ __forceinline__ void heap_pop(const Heap& hp, const Q& qc, int n, Ent& root, int lane)
+{
+    Ent last;
+    hload<SPILL>(hp, n, last.g, last.cm);  // uniform address
+    ent_key_any(qc, last);
+    int hole = 0;
+    bool first = true;
+    // lane l < 63: sibling pair at level j = 1..6 below the hole, pair offset o
+    const int j = 32 - __clz(lane + 1);  // 1..7 (lane 63 -> 7: unused)
+    const int o = lane + 1 - (1 << (j - 1));
+    for (;;) {
+        const int li = ((hole + 1) << j) - 1 + 2 * o;  // left child position
+        Ent L, R;
+        L.g = R.g = 0.0; L.f = R.f = 0.0; L.cm = R.cm = 0u; L.hk = R.hk = 0u;
+        const bool vl = lane < 63 && li < n;
+        const bool vr = lane < 63 && li + 1 < n;
+        if (vl) { hload<SPILL>(hp, li, L.g, L.cm); ent_key_any(qc, L); }
+        if (vr) { hload<SPILL>(hp, li + 1, R.g, R.cm); ent_key_any(qc, R); }
+        const bool pick_r = vr && !ent_lt(L, R);  // heapq._siftup: right unless left < right
+        const uint64_t dmask = ballot(pick_r);
+        const uint64_t mlmask = ballot(vl && !ent_lt(last, L));  // may move up past `last`
+        const uint64_t mrmask = ballot(vr && !ent_lt(last, R));
+        int cur = hole, oc = 0;
+        uint64_t mover = 0, movr = 0;
+        bool done = false;
+        for (int lv = 1; lv <= 6; lv++) {  // scalar walk through the chunk
+            const int c = 2 * cur + 1;
+            if (c >= n) { done = true; break; }
+            const int pl = (1 << (lv - 1)) - 1 + oc;  // pair lane
+            const int r = (int)((dmask >> pl) & 1ull);
+            const bool mv = r ? ((mrmask >> pl) & 1ull) : ((mlmask >> pl) & 1ull);
+            if (!mv) { done = true; break; }
+            mover |= 1ull << pl;
+            movr |= (uint64_t)r << pl;
+            cur = c + r;
+            oc = 2 * oc + r;
+        }
+        if ((mover >> lane) & 1ull) {  // chosen child moves up one level
+            const bool rr = (movr >> lane) & 1ull;
+            hstore<SPILL>(hp, ((rr ? li + 1 : li) - 1) >> 1, rr ? R.g : L.g, rr ? R.cm : L.cm);
+        }
+        if (first && (mover & 1ull)) {  // the child that moved into the root is the new root
+            const bool r0 = movr & 1ull;
+            root.g = r0 ? rl_f64(R.g, 0) : rl_f64(L.g, 0);
+            root.f = r0 ? rl_f64(R.f, 0) : rl_f64(L.f, 0);
+            root.cm = r0 ? rl_u32(R.cm, 0) : rl_u32(L.cm, 0);
+            root.hk = r0 ? rl_u32(R.hk, 0) : rl_u32(L.hk, 0);
+        }
+        first = false;
+        hole = cur;
+        if (done) break;
+        wave_sync_mem();
+    }
+    if (lane == 0) hstore<SPILL>(hp, hole, last.g, last.cm);
+    if (hole == 0) root = last;
+    wave_sync_mem();
+}
+
+// heappush of `it` onto a heap of n entries (position n is free).
+template <bool SPILL>
+__device__ __forceinline__ void heap_push(const Heap& hp, const Q& qc, int n, const Ent& it, Ent& root, int lane)
+{
+    const int np1 = n + 1;
+    const int depth = 31 - __clz(np1);  // ancestors of position n
+    Ent a;
+    a.g = a.f = 0.0; a.cm = a.hk = 0u;
+    const bool valid = lane < depth;
+    if (valid) { hload<SPILL>(hp, (np1 >> (lane + 1)) - 1, a.g, a.cm); ent_key_any(qc, a); }
+    const bool less = valid && ent_lt(it, a);
+    const int t = __popcll(ballot(less));  // the "less" set is a prefix from the parent upwards
+    if (lane < t) hstore<SPILL>(hp, (np1 >> lane) - 1, a.g, a.cm);
+    const int ipos = (np1 >> t) - 1;
+    if (lane == 0) hstore<SPILL>(hp, ipos, it.g, it.cm);
+    if (ipos == 0) root = it;
+    wave_sync_mem();
 }
 
 __global__ __launch_bounds__(64) void astar2d_kernel(
@@ -131,11 +235,18 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
     const int lane = lane_id();
     const int worker = blockIdx.x;
     Heap hp;
-    hp.lg = reinterpret_cast<double*>(smem);
-    hp.lcm = reinterpret_cast<uint32_t*>(smem + (size_t)8 * lds_cap);
-    hp.spill = spill_all + (size_t)worker * (size_t)(heap_cap > lds_cap ? heap_cap - lds_cap : 0);
+    hp.lg = (lds_f64*)(smem);
+    hp.lcm = (lds_u32*)(smem + (size_t)8 * lds_cap);
+    {
+        const size_t spill_n = (size_t)(heap_cap > lds_cap ? heap_cap - lds_cap : 0);
+        hp.spill = __builtin_amdgcn_make_buffer_rsrc(spill_all + (size_t)worker * spill_n, 0, (int)(spill_n * 16), 0x00020000);
+    }
     hp.lds_cap = lds_cap;
     uint32_t* cst = cst_all + (size_t)worker * cst_words;
+    // this lane's cell of the 3x3 block: lane i < 9 -> occupancy of (x + i/3 - 1, y + i%3 - 1),
+    // lane 9 + i -> its CLOSED-state nibble
+    const int blk_i = lane < 9 ? lane : (lane < 18 ? lane - 9 : 4);
+    const int blk_dx = blk_i / 3 - 1, blk_dy = blk_i % 3 - 1;
 
     for (;;) {
         int qi = 0;
@@ -172,15 +283,14 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
             }
             continue;
         }
-        const uint32_t start_xy13 = ((uint32_t)sx << 13) | (uint32_t)sy;
         const uint32_t goal_xy13 = ((uint32_t)qc.gx << 13) | (uint32_t)qc.gy;
 
         Ent root;  // heap[0], kept in registers (wave-uniform)
         root.g = 0.0;
-        root.cm = (start_xy13 << 4) | 8u;
+        root.cm = ((((uint32_t)sx << 13) | (uint32_t)sy) << 4) | 8u;  // Node(start, start, 0, 0)
         root.hk = 0;
         root.f = 0.0;
-        if (lane == 0) hp.store(0, root.g, root.cm);
+        if (lane == 0) hstore<true>(hp, 0, root.g, root.cm);
         wave_sync_mem();
 
         int n = 1;
@@ -198,98 +308,39 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
             const int ndir = (int)(node.cm & 15u);
             const uint32_t nlin = (uint32_t)x * (uint32_t)H + (uint32_t)y;
 
-            // ---- HBM round, issued first so it overlaps the LDS pop: the 3x3 block around the node
-            //      (occupancy bits for isCollision, graph_search.py:61-87, and CLOSED state nibbles),
-            //      all loads independent.  Lane i < 9 -> cell (x + i/3 - 1, y + i%3 - 1) occupancy,
-            //      lane 9 + i -> its state word.
-            uint32_t blk_word = 0;
-            bool blk_occ = false;
-            uint32_t blk_shift = 0;
-            bool blk_in = false;
+            // ---- HBM round, issued before the LDS pop so the two overlap: one unconditional load
+            //      per lane (raw word kept until after the pop, so no wait is placed before it)
+            uint32_t blk_word, blk_sh;
+            bool blk_in;
             {
-                const int i = lane < 9 ? lane : lane - 9;
-                const int cx = x + i / 3 - 1, cy = y + i % 3 - 1;
+                const int cx = x + blk_dx, cy = y + blk_dy;
                 blk_in = lane < 18 && (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
-                const uint32_t ci = (uint32_t)cx * (uint32_t)H + (uint32_t)cy;
-                if (lane < 9) {
-                    blk_occ = blk_in ? ((occ[ci >> 5] >> (ci & 31)) & 1u) != 0u : true;
-                } else if (blk_in) {
-                    blk_word = cst[ci >> 3];
-                    blk_shift = (ci & 7) * 4;
-                }
+                const uint32_t ci = blk_in ? (uint32_t)cx * (uint32_t)H + (uint32_t)cy : 0u;
+                const uint32_t* ptr = lane < 9 ? occ + (ci >> 5) : cst + (ci >> 3);
+                blk_sh = lane < 9 ? (ci & 31u) : (ci & 7u) * 4u;
+                blk_word = *ptr;
             }
-            // ---- heappop: `last` = heap[n] goes to the root and sifts down the CPython path
+
+            // ---- heappop (a_star.py:54): `last` = heap[n] sifts down the CPython path
             if (n > 0) {
-                Ent last;
-                hp.load(n, last.g, last.cm);  // uniform address
-                ent_key_any(qc, last);
-                int hole = 0;
-                bool first = true;
-                for (;;) {
-                    // lane l < 63: sibling pair (level j = 1..6 below the hole, pair offset o)
-                    const int j = 32 - __clz(lane + 1);       // 1..7 (lane 63 -> 7: unused)
-                    const int o = lane + 1 - (1 << (j - 1));
-                    const int li = ((hole + 1) << j) - 1 + 2 * o;  // left child position
-                    Ent L, R;
-                    L.g = R.g = 0.0; L.f = R.f = 0.0; L.cm = R.cm = 0u; L.hk = R.hk = 0u;
-                    const bool vl = lane < 63 && li < n;
-                    const bool vr = lane < 63 && li + 1 < n;
-                    if (vl) { hp.load(li, L.g, L.cm); ent_key_any(qc, L); }
-                    if (vr) { hp.load(li + 1, R.g, R.cm); ent_key_any(qc, R); }
-                    const bool pick_r = vr && !ent_lt(L, R);                   // heapq._siftup
-                    const uint64_t dmask = ballot(pick_r);
-                    const uint64_t mlmask = ballot(vl && !ent_lt(last, L));     // may move up
-                    const uint64_t mrmask = ballot(vr && !ent_lt(last, R));
-                    // scalar walk through the chunk
-                    int cur = hole, oc = 0;
-                    uint64_t mover = 0, movr = 0;
-                    bool done = false;
-                    int first_lane = -1, first_r = 0;
-                    for (int lv = 1; lv <= 6; lv++) {
-                        const int c = 2 * cur + 1;
-                        if (c >= n) { done = true; break; }
-                        const int pl = (1 << (lv - 1)) - 1 + oc;  // pair lane
-                        const int r = (int)((dmask >> pl) & 1ull);
-                        const bool mv = r ? ((mrmask >> pl) & 1ull) : ((mlmask >> pl) & 1ull);
-                        if (!mv) { done = true; break; }
-                        mover |= 1ull << pl;
-                        movr |= (uint64_t)r << pl;
-                        if (first_lane < 0) { first_lane = pl; first_r = r; }
-                        cur = c + r;
-                        oc = 2 * oc + r;
-                    }
-                    if ((mover >> lane) & 1ull) {  // chosen child moves up one level
-                        const bool rr = (movr >> lane) & 1ull;
-                        const int pos = rr ? li + 1 : li;
-                        hp.store((pos - 1) >> 1, rr ? R.g : L.g, rr ? R.cm : L.cm);
-                    }
-                    if (first && first_lane >= 0) {
-                        // the child that moved into the root becomes the new root (wave-uniform)
-                        root.g = first_r ? rl_f64(R.g, first_lane) : rl_f64(L.g, first_lane);
-                        root.f = first_r ? rl_f64(R.f, first_lane) : rl_f64(L.f, first_lane);
-                        root.cm = first_r ? rl_u32(R.cm, first_lane) : rl_u32(L.cm, first_lane);
-                        root.hk = first_r ? rl_u32(R.hk, first_lane) : rl_u32(L.hk, first_lane);
-                    }
-                    first = false;
-                    hole = cur;
-                    if (done) break;
-                    wave_sync_mem();
-                }
-                if (lane == 0) hp.store(hole, last.g, last.cm);
-                if (hole == 0) root = last;
-                wave_sync_mem();
+                if (n < lds_cap) heap_pop<false>(hp, qc, n, root, lane);
+                else heap_pop<true>(hp, qc, n, root, lane);
             }
-            // 3x3 masks: bit k = cell (x + k/3 - 1, y + k%3 - 1); node is k = 4
-            const uint32_t occ9 = (uint32_t)ballot(lane < 9 && blk_occ) & 0x1ffu;
-            const uint32_t cls9 = (uint32_t)(ballot(lane >= 9 && lane < 18 && blk_in && ((blk_word >> blk_shift) & 15u) != 0u) >> 9) & 0x1ffu;
+
+            // 3x3 masks: bit k = cell (x + k/3 - 1, y + k%3 - 1); the node is k = 4
+            const uint32_t occ9 = (uint32_t)ballot(lane < 9 && (!blk_in || ((blk_word >> blk_sh) & 1u))) & 0x1ffu;
+            const uint32_t cls9 =
+                (uint32_t)(ballot(lane >= 9 && lane < 18 && blk_in && ((blk_word >> blk_sh) & 15u) != 0u) >> 9) & 0x1ffu;
             if (cls9 & 16u) continue;  // node.current in CLOSED (a_star.py:57-58)
-            // CLOSED[node.current] = node (a_star.py:82): the node's state word was loaded by lane 13
-            // and only this wave writes it, so store it back now (fire-and-forget, off the critical path)
-            if (lane == 13) cst[nlin >> 3] = blk_word | ((uint32_t)(ndir + 1) << blk_shift);
-            if (lane == 0 && expand_out && nexp < expand_cap) expand_out[(size_t)q * expand_cap + nexp] = nlin | ((uint32_t)ndir << 28);
+
+            // CLOSED[node.current] = node (a_star.py:82).  The node's state word was loaded by lane 13
+            // and only this wave writes it: store it back now (fire-and-forget, off the critical path).
+            if (lane == 13) cst[nlin >> 3] = blk_word | ((uint32_t)(ndir + 1) << blk_sh);
+            if (lane == 0 && expand_out && nexp < expand_cap)
+                expand_out[(size_t)q * expand_cap + nexp] = nlin | ((uint32_t)ndir << 28);
             nexp++;
 
-            if (node.cm >> 4 == goal_xy13) {  // goal found (a_star.py:61-64); already closed above
+            if (node.cm >> 4 == goal_xy13) {  // goal found (a_star.py:61-64)
                 st = PMP_FOUND;
                 wave_sync_mem();
                 if (lane == 0) {  // extractPath (a_star.py:98-117): goal -> start, cost in that order
@@ -313,25 +364,23 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 break;
             }
 
-            // g of the popped node (node.py:39-41 accumulated it when it was pushed)
-            const double gnode = node.g;
-            // ---- neighbours in motion order; push the goal and stop (a_star.py:66-80)
+            // ---- getNeighbor + the push loop in motion order; push the goal and stop (a_star.py:66-80)
             bool nb_ok = false;
             uint32_t nbxy = 0;
             if (lane < 8) {
                 const int ax = c_mx[lane] + 1, ay = c_my[lane] + 1;
-                uint32_t need = 16u | (1u << (ax * 3 + ay));                 // both endpoints
-                if (lane & 1) need |= (1u << (3 + ay)) | (1u << (ax * 3 + 1));  // both corners
+                uint32_t need = 16u | (1u << (ax * 3 + ay));                     // both endpoints
+                if (lane & 1) need |= (1u << (3 + ay)) | (1u << (ax * 3 + 1));  // both corner cells
                 nb_ok = (occ9 & need) == 0u && ((cls9 >> (ax * 3 + ay)) & 1u) == 0u;
                 nbxy = ((uint32_t)(x + c_mx[lane]) << 13) | (uint32_t)(y + c_my[lane]);
             }
             uint64_t vm = ballot(nb_ok) & 0xffull;
             const uint64_t gm = ballot(nb_ok && nbxy == goal_xy13) & 0xffull;
             if (gm) vm &= (gm << 1) - 1;
-            Ent item;
+            Ent item;  // node + motion (node.py:39-41), h = GraphSearcher.h (graph_search.py:41-44)
             {
                 const int m = lane & 7;
-                item.g = gnode + ((m & 1) ? kSqrt2 : 1.0);
+                item.g = node.g + ((m & 1) ? kSqrt2 : 1.0);
                 item.cm = (nbxy << 4) | (uint32_t)m;
                 item.f = 0.0;
                 item.hk = 0u;
@@ -347,21 +396,10 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 it.f = rl_f64(item.f, m);
                 it.cm = rl_u32(item.cm, m);
                 it.hk = rl_u32(item.hk, m);
-                const int np1 = n + 1;
-                const int depth = 31 - __clz(np1);
-                Ent a;
-                a.g = a.f = 0.0; a.cm = a.hk = 0u;
-                const bool valid = lane < depth;
-                if (valid) { hp.load((np1 >> (lane + 1)) - 1, a.g, a.cm); ent_key_any(qc, a); }
-                const bool less = valid && ent_lt(it, a);
-                const int t = __popcll(ballot(less));
-                if (lane < t) hp.store((np1 >> lane) - 1, a.g, a.cm);
-                const int ipos = (np1 >> t) - 1;
-                if (lane == 0) hp.store(ipos, it.g, it.cm);
-                if (ipos == 0) root = it;
+                if (n < lds_cap) heap_push<false>(hp, qc, n, it, root, lane);
+                else heap_push<true>(hp, qc, n, it, root, lane);
                 n += 1;
                 npush++;
-                wave_sync_mem();
             }
             if (n > maxn) maxn = n;
             if (overflow) { st = PMP_CAP_OVERFLOW; break; }
