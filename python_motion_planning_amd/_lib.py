@@ -10,7 +10,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpmp_hip.so")
+LIB_PATH = os.environ.get("PMP_HIP_LIB") or os.path.join(_HERE, "libpmp_hip.so")  # override: diagnostics only
 
 _vp = ctypes.c_void_p
 _i = ctypes.c_int

@@ -7,11 +7,14 @@
 // per-worker HBM array) and a 4-bit-per-cell state array in HBM (0 = open, dir+1 = closed with
 // parent motion `dir`), reused across the queries it processes.
 //
-// Heap entry (12 B in LDS as SoA: f64 g[] | u32 cm[]):  cm = (x << 13 | y) << 4 | dir
+// Heap entry (12 B in LDS as SoA: f64 f[] | u32 cm[]):  cm = (x << 13 | y) << 4 | dir
 //   dir = motion index (env.py:52-55) that reached the cell from its parent, 8 = start.
-//   f = g + h is recomputed per lane when an entry is loaded: euclidean h = hypot(dx, dy) ==
-//   sqrt(d2) exactly for |d| <= 16384 (pinned against CPython's vector_norm), manhattan h = |dx|+|dy|.
-//   Node.__lt__: f < f' or (f == f' and h < h'); h order == hkey order (d2, or |dx|+|dy|).
+//   f = g + h as Node.__lt__ computes it (euclidean h = hypot(dx, dy) == sqrt(d2) exactly for
+//   |d| <= 16384, pinned against CPython's vector_norm; manhattan h = |dx| + |dy|).
+//   Node.__lt__: f < f' or (f == f' and h < h'); h order == hkey order (d2, or |dx|+|dy|), and hkey
+//   is rebuilt from the cell with integer ops, so loading an entry costs no transcendental.
+//   g of a popped node = G[parent] + motion cost (node.py:39-41), G written when the parent closed,
+//   loaded in the same HBM round as the node's 3x3 occupancy / CLOSED block.
 //
 // heappop (CPython: pop last, put it at the root, _siftup walks the smaller child -- right child
 // when not left < right -- to a leaf, then _siftdown moves it back up).  The final array equals a
@@ -22,6 +25,14 @@
 // masks; the walk itself is scalar; movers store in parallel.
 // heappush (_siftdown): the ancestors load in one round, one ballot finds how many move down.
 #include "pmp_internal.h"
+
+// Diagnostic build only (make stamps -> libpmp_hip_stamps.so): per-query cycle sums of the
+// expansion segments go to counters[4q+0..3] = {pop, 3x3 wait, push, total} instead of the counts.
+#ifdef PMP_STAMPS
+#define STAMP(v) uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define STAMP(v)
+#endif
 
 namespace {
 
@@ -37,34 +48,30 @@ struct Q {  // per-query uniform constants
 };
 
 struct Ent {
-    double g, f;
+    double f;
     uint32_t cm, hk;
 };
 
-__device__ __forceinline__ void ent_key(const Q& q, Ent& e)
+// h of a pushed node (GraphSearcher.h, graph_search.py:41-44) and its integer order key
+__device__ __forceinline__ double h_and_key(const Q& q, uint32_t cm, uint32_t& hk)
 {
-    const int x = (int)(e.cm >> 17), y = (int)((e.cm >> 4) & 8191u);
+    const int x = (int)(cm >> 17), y = (int)((cm >> 4) & 8191u);
     const int dx = q.gx - x, dy = q.gy - y;
-    double h;
     if (q.heur == 1) {
-        e.hk = (uint32_t)(abs(dx) + abs(dy));
-        h = (double)e.hk;
-    } else {
-        e.hk = (uint32_t)(dx * dx + dy * dy);
-        h = __dsqrt_rn((double)e.hk);
+        hk = (uint32_t)(abs(dx) + abs(dy));
+        return (double)hk;
     }
-    e.f = e.g + h;
+    hk = (uint32_t)(dx * dx + dy * dy);
+    return __dsqrt_rn((double)hk);
 }
 
-// the start node has h = 0 (planner.py:15), not hypot(start, goal)
-__device__ __forceinline__ void ent_key_any(const Q& q, Ent& e)
+// order key of a stored entry; the start node has h = 0 (planner.py:15)
+__device__ __forceinline__ uint32_t key_of(const Q& q, uint32_t cm)
 {
-    if ((e.cm & 15u) == 8u) {
-        e.hk = 0;
-        e.f = e.g;
-    } else {
-        ent_key(q, e);
-    }
+    const int x = (int)(cm >> 17), y = (int)((cm >> 4) & 8191u);
+    const int dx = q.gx - x, dy = q.gy - y;
+    const uint32_t k = q.heur == 1 ? (uint32_t)(abs(dx) + abs(dy)) : (uint32_t)(dx * dx + dy * dy);
+    return (cm & 15u) == 8u ? 0u : k;
 }
 
 __device__ __forceinline__ bool ent_lt(const Ent& a, const Ent& b)
@@ -80,9 +87,9 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 // instructions (a distinct instruction class, so the compiler can never fold the two paths into
 // one flat access that waits on both counters).
 struct Heap {
-    lds_f64* lg;       // LDS g[lds_cap]
+    lds_f64* lg;       // LDS f[lds_cap]
     lds_u32* lcm;      // LDS cm[lds_cap]
-    __amdgpu_buffer_rsrc_t spill;  // HBM entries {g lo, g hi, cm, 0} for positions >= lds_cap
+    __amdgpu_buffer_rsrc_t spill;  // HBM entries {f lo, f hi, cm, 0} for positions >= lds_cap
     int lds_cap;
 
     __device__ __forceinline__ void load(int p, double& g, uint32_t& cm) const
@@ -149,8 +156,8 @@ template <bool SPILL>
 __device__ __forceinline__ void heap_pop(const Heap& hp, const Q& qc, int n, Ent& root, int lane)
 {
     Ent last;
-    hload<SPILL>(hp, n, last.g, last.cm);  // uniform address
-    ent_key_any(qc, last);
+    hload<SPILL>(hp, n, last.f, last.cm);  // uniform address
+    last.hk = key_of(qc, last.cm);
     int hole = 0;
     bool first = true;
     // lane l < 63: sibling pair at level j = 1..6 below the hole, pair offset o
@@ -159,11 +166,13 @@ __device__ __forceinline__ void heap_pop(const Heap& hp, const Q& qc, int n, Ent
     for (;;) {
         const int li = ((hole + 1) << j) - 1 + 2 * o;  // left child position
         Ent L, R;
-        L.g = R.g = 0.0; L.f = R.f = 0.0; L.cm = R.cm = 0u; L.hk = R.hk = 0u;
+        L.f = R.f = 0.0; L.cm = R.cm = 0u;
         const bool vl = lane < 63 && li < n;
         const bool vr = lane < 63 && li + 1 < n;
-        if (vl) { hload<SPILL>(hp, li, L.g, L.cm); ent_key_any(qc, L); }
-        if (vr) { hload<SPILL>(hp, li + 1, R.g, R.cm); ent_key_any(qc, R); }
+        if (vl) hload<SPILL>(hp, li, L.f, L.cm);
+        if (vr) hload<SPILL>(hp, li + 1, R.f, R.cm);
+        L.hk = key_of(qc, L.cm);
+        R.hk = key_of(qc, R.cm);
         const bool pick_r = vr && !ent_lt(L, R);  // heapq._siftup: right unless left < right
         const uint64_t dmask = ballot(pick_r);
         const uint64_t mlmask = ballot(vl && !ent_lt(last, L));  // may move up past `last`
@@ -185,11 +194,10 @@ __device__ __forceinline__ void heap_pop(const Heap& hp, const Q& qc, int n, Ent
         }
         if ((mover >> lane) & 1ull) {  // chosen child moves up one level
             const bool rr = (movr >> lane) & 1ull;
-            hstore<SPILL>(hp, ((rr ? li + 1 : li) - 1) >> 1, rr ? R.g : L.g, rr ? R.cm : L.cm);
+            hstore<SPILL>(hp, ((rr ? li + 1 : li) - 1) >> 1, rr ? R.f : L.f, rr ? R.cm : L.cm);
         }
         if (first && (mover & 1ull)) {  // the child that moved into the root is the new root
             const bool r0 = movr & 1ull;
-            root.g = r0 ? rl_f64(R.g, 0) : rl_f64(L.g, 0);
             root.f = r0 ? rl_f64(R.f, 0) : rl_f64(L.f, 0);
             root.cm = r0 ? rl_u32(R.cm, 0) : rl_u32(L.cm, 0);
             root.hk = r0 ? rl_u32(R.hk, 0) : rl_u32(L.hk, 0);
@@ -199,7 +207,7 @@ __device__ __forceinline__ void heap_pop(const Heap& hp, const Q& qc, int n, Ent
         if (done) break;
         wave_sync_mem();
     }
-    if (lane == 0) hstore<SPILL>(hp, hole, last.g, last.cm);
+    if (lane == 0) hstore<SPILL>(hp, hole, last.f, last.cm);
     if (hole == 0) root = last;
     wave_sync_mem();
 }
@@ -211,14 +219,15 @@ __device__ __forceinline__ void heap_push(const Heap& hp, const Q& qc, int n, co
     const int np1 = n + 1;
     const int depth = 31 - __clz(np1);  // ancestors of position n
     Ent a;
-    a.g = a.f = 0.0; a.cm = a.hk = 0u;
+    a.f = 0.0; a.cm = 0u;
     const bool valid = lane < depth;
-    if (valid) { hload<SPILL>(hp, (np1 >> (lane + 1)) - 1, a.g, a.cm); ent_key_any(qc, a); }
+    if (valid) hload<SPILL>(hp, (np1 >> (lane + 1)) - 1, a.f, a.cm);
+    a.hk = key_of(qc, a.cm);
     const bool less = valid && ent_lt(it, a);
     const int t = __popcll(ballot(less));  // the "less" set is a prefix from the parent upwards
-    if (lane < t) hstore<SPILL>(hp, (np1 >> lane) - 1, a.g, a.cm);
+    if (lane < t) hstore<SPILL>(hp, (np1 >> lane) - 1, a.f, a.cm);
     const int ipos = (np1 >> t) - 1;
-    if (lane == 0) hstore<SPILL>(hp, ipos, it.g, it.cm);
+    if (lane == 0) hstore<SPILL>(hp, ipos, it.f, it.cm);
     if (ipos == 0) root = it;
     wave_sync_mem();
 }
@@ -229,7 +238,8 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
     int32_t* __restrict__ path_len_out, uint32_t* __restrict__ path_out, int path_cap,
     int32_t* __restrict__ nexp_out, uint32_t* __restrict__ expand_out, int expand_cap,
     int64_t* __restrict__ counters, int32_t* __restrict__ status_out, int* __restrict__ queue,
-    uint4* __restrict__ spill_all, int heap_cap, int lds_cap, uint32_t* __restrict__ cst_all, size_t cst_words)
+    uint4* __restrict__ spill_all, int heap_cap, int lds_cap, uint32_t* __restrict__ cst_all, size_t cst_words,
+    double* __restrict__ G_all)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
@@ -243,6 +253,7 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
     }
     hp.lds_cap = lds_cap;
     uint32_t* cst = cst_all + (size_t)worker * cst_words;
+    double* G = G_all + (size_t)worker * ((size_t)W * (size_t)H);
     // this lane's cell of the 3x3 block: lane i < 9 -> occupancy of (x + i/3 - 1, y + i%3 - 1),
     // lane 9 + i -> its CLOSED-state nibble
     const int blk_i = lane < 9 ? lane : (lane < 18 ? lane - 9 : 4);
@@ -286,11 +297,10 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
         const uint32_t goal_xy13 = ((uint32_t)qc.gx << 13) | (uint32_t)qc.gy;
 
         Ent root;  // heap[0], kept in registers (wave-uniform)
-        root.g = 0.0;
         root.cm = ((((uint32_t)sx << 13) | (uint32_t)sy) << 4) | 8u;  // Node(start, start, 0, 0)
         root.hk = 0;
         root.f = 0.0;
-        if (lane == 0) hstore<true>(hp, 0, root.g, root.cm);
+        if (lane == 0) hstore<true>(hp, 0, root.f, root.cm);
         wave_sync_mem();
 
         int n = 1;
@@ -300,7 +310,12 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
         double goal_cost = 0.0;
         int plen = 0;
 
+#ifdef PMP_STAMPS
+        uint64_t cyc_pop = 0, cyc_wait = 0, cyc_push = 0;
+        const uint64_t cyc_q0 = __builtin_amdgcn_s_memtime();
+#endif
         while (n > 0) {
+            STAMP(ts0);
             const Ent node = root;
             npop++;
             n -= 1;
@@ -320,6 +335,8 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 blk_sh = lane < 9 ? (ci & 31u) : (ci & 7u) * 4u;
                 blk_word = *ptr;
             }
+            double gpar = 0.0;  // G[parent] (the parent closed earlier); the start has g = 0
+            if (lane == 18 && ndir < 8) gpar = G[(uint32_t)(x - c_mx[ndir]) * (uint32_t)H + (uint32_t)(y - c_my[ndir])];
 
             // ---- heappop (a_star.py:54): `last` = heap[n] sifts down the CPython path
             if (n > 0) {
@@ -327,15 +344,25 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 else heap_pop<true>(hp, qc, n, root, lane);
             }
 
+            STAMP(ts1);
             // 3x3 masks: bit k = cell (x + k/3 - 1, y + k%3 - 1); the node is k = 4
             const uint32_t occ9 = (uint32_t)ballot(lane < 9 && (!blk_in || ((blk_word >> blk_sh) & 1u))) & 0x1ffu;
             const uint32_t cls9 =
                 (uint32_t)(ballot(lane >= 9 && lane < 18 && blk_in && ((blk_word >> blk_sh) & 15u) != 0u) >> 9) & 0x1ffu;
+#ifdef PMP_STAMPS
+            {
+                STAMP(ts2);
+                cyc_pop += ts1 - ts0;
+                cyc_wait += ts2 - ts1;
+            }
+#endif
             if (cls9 & 16u) continue;  // node.current in CLOSED (a_star.py:57-58)
 
             // CLOSED[node.current] = node (a_star.py:82).  The node's state word was loaded by lane 13
             // and only this wave writes it: store it back now (fire-and-forget, off the critical path).
+            const double gnode = ndir == 8 ? 0.0 : rl_f64(gpar, 18) + ((ndir & 1) ? kSqrt2 : 1.0);
             if (lane == 13) cst[nlin >> 3] = blk_word | ((uint32_t)(ndir + 1) << blk_sh);
+            if (lane == 14) G[nlin] = gnode;
             if (lane == 0 && expand_out && nexp < expand_cap)
                 expand_out[(size_t)q * expand_cap + nexp] = nlin | ((uint32_t)ndir << 28);
             nexp++;
@@ -380,11 +407,10 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
             Ent item;  // node + motion (node.py:39-41), h = GraphSearcher.h (graph_search.py:41-44)
             {
                 const int m = lane & 7;
-                item.g = node.g + ((m & 1) ? kSqrt2 : 1.0);
                 item.cm = (nbxy << 4) | (uint32_t)m;
                 item.f = 0.0;
                 item.hk = 0u;
-                if (lane < 8) ent_key(qc, item);
+                if (lane < 8) item.f = (gnode + ((m & 1) ? kSqrt2 : 1.0)) + h_and_key(qc, item.cm, item.hk);
             }
             bool overflow = false;
             while (vm) {
@@ -392,7 +418,6 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 vm &= vm - 1;
                 if (n >= heap_cap) { overflow = true; break; }
                 Ent it;
-                it.g = rl_f64(item.g, m);
                 it.f = rl_f64(item.f, m);
                 it.cm = rl_u32(item.cm, m);
                 it.hk = rl_u32(item.hk, m);
@@ -402,6 +427,12 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 npush++;
             }
             if (n > maxn) maxn = n;
+#ifdef PMP_STAMPS
+            {
+                STAMP(ts3);
+                cyc_push += ts3 - ts1;
+            }
+#endif
             if (overflow) { st = PMP_CAP_OVERFLOW; break; }
         }
 
@@ -413,10 +444,17 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
             path_len_out[q] = (st == PMP_FOUND) ? plen : 0;
             nexp_out[q] = nexp;
             if (counters) {
+#ifdef PMP_STAMPS
+                counters[4 * q + 0] = (int64_t)cyc_pop;
+                counters[4 * q + 1] = (int64_t)cyc_wait;
+                counters[4 * q + 2] = (int64_t)cyc_push;
+                counters[4 * q + 3] = (int64_t)(__builtin_amdgcn_s_memtime() - cyc_q0);
+#else
                 counters[4 * q + 0] = npush;
                 counters[4 * q + 1] = npop;
                 counters[4 * q + 2] = nexp;
                 counters[4 * q + 3] = maxn;
+#endif
             }
         }
         wave_sync_mem();
@@ -461,6 +499,7 @@ extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int workers, int 
     if (!pmp_scratch(ctx, SCR_HEAP, (size_t)workers * spill * 16 + 16)) return PMP_ENOMEM;
     if (!pmp_scratch(ctx, SCR_CLOSED, (size_t)workers * cst_words * 4)) return PMP_ENOMEM;
     if (!pmp_scratch(ctx, SCR_AUX0, 256)) return PMP_ENOMEM;
+    if (!pmp_scratch(ctx, SCR_G, (size_t)workers * ncell * 8)) return PMP_ENOMEM;
     g_cfg.W = W;
     g_cfg.H = H;
     g_cfg.workers = workers;
@@ -497,12 +536,13 @@ extern "C" int pmp_astar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
     uint4* spill = (uint4*)ctx->buf[SCR_HEAP];
     uint32_t* cst = (uint32_t*)ctx->buf[SCR_CLOSED];
     int* queue = (int*)ctx->buf[SCR_AUX0];
+    double* G = (double*)ctx->buf[SCR_G];
     hipStream_t s = (hipStream_t)stream;
     const size_t lds = (size_t)g_cfg.lds_cap * 12;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
     hipLaunchKernelGGL(astar2d_kernel, dim3(workers), dim3(64), lds, s, occ_bits, W, H, heuristic, start_xy,
                        goal_xy, (const int32_t*)nullptr, nq, cost, path_len, path, path_cap, n_expanded, expand,
-                       expand_cap, counters, status, queue, spill, g_cfg.heap_cap, g_cfg.lds_cap, cst, cst_words);
+                       expand_cap, counters, status, queue, spill, g_cfg.heap_cap, g_cfg.lds_cap, cst, cst_words, G);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }
