@@ -155,8 +155,11 @@ __device__ __forceinline__ void hstore(const Heap& hp, int p, double g, uint32_t
 template <bool SPILL>
 __device__ __forceinline__ void heap_pop(const Heap& hp, const Q& qc, int n, Ent& root, int lane)
 {
+    n = uni(n);  // wave-uniform by construction; say so, so the walk below stays on the SALU
     Ent last;
-    hload<SPILL>(hp, n, last.f, last.cm);  // uniform address
+    hload<SPILL>(hp, n, last.f, last.cm);  // uniform address, but an LDS load is not known-uniform:
+    last.f = rl_f64(last.f, 0);            // readlane makes `last` (and the root / node derived from
+    last.cm = rl_u32(last.cm, 0);          // it) SGPR values, keeping the whole walk scalar
     last.hk = key_of(qc, last.cm);
     int hole = 0;
     bool first = true;
@@ -177,7 +180,7 @@ __device__ __forceinline__ void heap_pop(const Heap& hp, const Q& qc, int n, Ent
         const uint64_t dmask = ballot(pick_r);
         const uint64_t mlmask = ballot(vl && !ent_lt(last, L));  // may move up past `last`
         const uint64_t mrmask = ballot(vr && !ent_lt(last, R));
-        int cur = hole, oc = 0;
+        int cur = uni(hole), oc = 0;
         uint64_t mover = 0, movr = 0;
         bool done = false;
         for (int lv = 1; lv <= 6; lv++) {  // scalar walk through the chunk
@@ -216,6 +219,7 @@ __device__ __forceinline__ void heap_pop(const Heap& hp, const Q& qc, int n, Ent
 template <bool SPILL>
 __device__ __forceinline__ void heap_push(const Heap& hp, const Q& qc, int n, const Ent& it, Ent& root, int lane)
 {
+    n = uni(n);
     const int np1 = n + 1;
     const int depth = 31 - __clz(np1);  // ancestors of position n
     Ent a;
@@ -262,9 +266,12 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
     for (;;) {
         int qi = 0;
         if (lane == 0) qi = atomicAdd(queue, 1);
-        qi = __shfl(qi, 0);
+        // readfirstlane (not __shfl): the compiler must SEE the query index as wave-uniform, or
+        // every value derived from it (coordinates, heap size, walk state) lands in VGPRs and the
+        // scalar heap walk is compiled as a divergent loop.
+        qi = uni(qi);
         if (qi >= nq) break;
-        const int q = order ? order[qi] : qi;
+        const int q = uni(order ? order[qi] : qi);
 
         // reset this worker's cell-state array
         {
