@@ -42,9 +42,8 @@ constexpr double kSqrt2 = 1.4142135623730951;  // math.sqrt(2) == math.hypot(1, 
 __device__ __constant__ int c_mx[8] = {-1, -1, 0, 1, 1, 1, 0, -1};
 __device__ __constant__ int c_my[8] = {0, 1, 1, 1, 0, -1, -1, -1};
 
-struct Q {  // per-query uniform constants
+struct Q {  // per-query wave-uniform constants
     int gx, gy;
-    int heur;
 };
 
 struct Ent {
@@ -52,32 +51,38 @@ struct Ent {
     uint32_t cm, hk;
 };
 
-// h of a pushed node (GraphSearcher.h, graph_search.py:41-44) and its integer order key
-__device__ __forceinline__ double h_and_key(const Q& q, uint32_t cm, uint32_t& hk)
+// HEUR: 0 euclidean, 1 manhattan (GraphSearcher.h, graph_search.py:41-44) -- a template parameter,
+// so key computations carry no runtime branch.
+template <int HEUR>
+__device__ __forceinline__ uint32_t hkey_raw(const Q& q, uint32_t cm)
 {
     const int x = (int)(cm >> 17), y = (int)((cm >> 4) & 8191u);
     const int dx = q.gx - x, dy = q.gy - y;
-    if (q.heur == 1) {
-        hk = (uint32_t)(abs(dx) + abs(dy));
-        return (double)hk;
-    }
-    hk = (uint32_t)(dx * dx + dy * dy);
-    return __dsqrt_rn((double)hk);
+    return HEUR == 1 ? (uint32_t)(abs(dx) + abs(dy)) : (uint32_t)(dx * dx + dy * dy);
+}
+
+// h of a pushed node and its integer order key
+template <int HEUR>
+__device__ __forceinline__ double h_and_key(const Q& q, uint32_t cm, uint32_t& hk)
+{
+    hk = hkey_raw<HEUR>(q, cm);
+    return HEUR == 1 ? (double)hk : __dsqrt_rn((double)hk);
 }
 
 // order key of a stored entry; the start node has h = 0 (planner.py:15)
+template <int HEUR>
 __device__ __forceinline__ uint32_t key_of(const Q& q, uint32_t cm)
 {
-    const int x = (int)(cm >> 17), y = (int)((cm >> 4) & 8191u);
-    const int dx = q.gx - x, dy = q.gy - y;
-    const uint32_t k = q.heur == 1 ? (uint32_t)(abs(dx) + abs(dy)) : (uint32_t)(dx * dx + dy * dy);
+    const uint32_t k = hkey_raw<HEUR>(q, cm);
     return (cm & 15u) == 8u ? 0u : k;
 }
 
-__device__ __forceinline__ bool ent_lt(const Ent& a, const Ent& b)
+// Node.__lt__ (node.py:51-54) -- evaluated without short-circuit branches
+__device__ __forceinline__ bool key_lt(double fa, uint32_t ka, double fb, uint32_t kb)
 {
-    return a.f < b.f || (a.f == b.f && a.hk < b.hk);
+    return (fa < fb) | ((fa == fb) & (ka < kb));
 }
+__device__ __forceinline__ bool ent_lt(const Ent& a, const Ent& b) { return key_lt(a.f, a.hk, b.f, b.hk); }
 
 typedef __attribute__((address_space(3))) double lds_f64;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
@@ -152,62 +157,71 @@ __device__ __forceinline__ void hstore(const Heap& hp, int p, double g, uint32_t
 
 // heappop on a heap of n (>0, already decremented) entries whose old last element sits at position
 // n; the old root has been taken by the caller.  Updates `root` (wave-uniform copy of heap[0]).
-template <bool SPILL>
-__device__ __forceinline__ void heap_pop(const Heap& hp, const Q& qc, int n, Ent& root, int lane)
+// jl / ol: this lane's pair level (1..6) and pair offset inside a chunk (lane 63: idle).
+template <bool SPILL, int HEUR>
+__device__ __forceinline__ void heap_pop(const Heap& hp, const Q& qc, int n, Ent& root, int lane, int jl, int ol)
 {
     n = uni(n);  // wave-uniform by construction; say so, so the walk below stays on the SALU
     Ent last;
     hload<SPILL>(hp, n, last.f, last.cm);  // uniform address, but an LDS load is not known-uniform:
     last.f = rl_f64(last.f, 0);            // readlane makes `last` (and the root / node derived from
     last.cm = rl_u32(last.cm, 0);          // it) SGPR values, keeping the whole walk scalar
-    last.hk = key_of(qc, last.cm);
+    last.hk = key_of<HEUR>(qc, last.cm);
     int hole = 0;
     bool first = true;
-    // lane l < 63: sibling pair at level j = 1..6 below the hole, pair offset o
-    const int j = 32 - __clz(lane + 1);  // 1..7 (lane 63 -> 7: unused)
-    const int o = lane + 1 - (1 << (j - 1));
     for (;;) {
-        const int li = ((hole + 1) << j) - 1 + 2 * o;  // left child position
+        const int li = ((hole + 1) << jl) - 1 + 2 * ol;  // left child position of this lane's pair
+        const bool vl = (lane < 63) & (li < n);
+        const bool vr = (lane < 63) & (li + 1 < n);
         Ent L, R;
-        L.f = R.f = 0.0; L.cm = R.cm = 0u;
-        const bool vl = lane < 63 && li < n;
-        const bool vr = lane < 63 && li + 1 < n;
-        if (vl) hload<SPILL>(hp, li, L.f, L.cm);
-        if (vr) hload<SPILL>(hp, li + 1, R.f, R.cm);
-        L.hk = key_of(qc, L.cm);
-        R.hk = key_of(qc, R.cm);
-        const bool pick_r = vr && !ent_lt(L, R);  // heapq._siftup: right unless left < right
-        const uint64_t dmask = ballot(pick_r);
-        const uint64_t mlmask = ballot(vl && !ent_lt(last, L));  // may move up past `last`
-        const uint64_t mrmask = ballot(vr && !ent_lt(last, R));
+        if constexpr (SPILL) {
+            L.f = R.f = 0.0;
+            L.cm = R.cm = 0u;
+            if (vl) hload<true>(hp, li, L.f, L.cm);
+            if (vr) hload<true>(hp, li + 1, R.f, R.cm);
+        } else {  // unconditional loads from clamped (valid) addresses: no branch
+            const int a = vl ? li : 0, b = vr ? li + 1 : 0;
+            L.f = hp.lg[a];
+            L.cm = hp.lcm[a];
+            R.f = hp.lg[b];
+            R.cm = hp.lcm[b];
+        }
+        L.hk = key_of<HEUR>(qc, L.cm);
+        R.hk = key_of<HEUR>(qc, R.cm);
+        const uint64_t dmask = ballot(vr & !ent_lt(L, R));    // heapq._siftup: right unless left < right
+        const uint64_t mlmask = ballot(vl & !ent_lt(last, L));  // child may move up past `last`
+        const uint64_t mrmask = ballot(vr & !ent_lt(last, R));
+        // scalar walk through the chunk's 6 levels (all SGPR, unrolled)
         int cur = uni(hole), oc = 0;
         uint64_t mover = 0, movr = 0;
-        bool done = false;
-        for (int lv = 1; lv <= 6; lv++) {  // scalar walk through the chunk
+        bool go = true;
+#pragma unroll
+        for (int lv = 1; lv <= 6; lv++) {
             const int c = 2 * cur + 1;
-            if (c >= n) { done = true; break; }
             const int pl = (1 << (lv - 1)) - 1 + oc;  // pair lane
             const int r = (int)((dmask >> pl) & 1ull);
-            const bool mv = r ? ((mrmask >> pl) & 1ull) : ((mlmask >> pl) & 1ull);
-            if (!mv) { done = true; break; }
-            mover |= 1ull << pl;
-            movr |= (uint64_t)r << pl;
-            cur = c + r;
-            oc = 2 * oc + r;
+            const uint64_t mm = r ? mrmask : mlmask;
+            go = go & (c < n) & (((mm >> pl) & 1ull) != 0ull);
+            if (go) {
+                mover |= 1ull << pl;
+                movr |= (uint64_t)r << pl;
+                cur = c + r;
+                oc = 2 * oc + r;
+            }
         }
-        if ((mover >> lane) & 1ull) {  // chosen child moves up one level
+        if ((mover >> lane) & 1ull) {  // the chosen child moves up one level
             const bool rr = (movr >> lane) & 1ull;
             hstore<SPILL>(hp, ((rr ? li + 1 : li) - 1) >> 1, rr ? R.f : L.f, rr ? R.cm : L.cm);
         }
         if (first && (mover & 1ull)) {  // the child that moved into the root is the new root
             const bool r0 = movr & 1ull;
-            root.f = r0 ? rl_f64(R.f, 0) : rl_f64(L.f, 0);
-            root.cm = r0 ? rl_u32(R.cm, 0) : rl_u32(L.cm, 0);
-            root.hk = r0 ? rl_u32(R.hk, 0) : rl_u32(L.hk, 0);
+            root.f = rl_f64(r0 ? R.f : L.f, 0);
+            root.cm = rl_u32(r0 ? R.cm : L.cm, 0);
+            root.hk = rl_u32(r0 ? R.hk : L.hk, 0);
         }
         first = false;
         hole = cur;
-        if (done) break;
+        if (!go) break;
         wave_sync_mem();
     }
     if (lane == 0) hstore<SPILL>(hp, hole, last.f, last.cm);
@@ -216,19 +230,25 @@ __device__ __forceinline__ void heap_pop(const Heap& hp, const Q& qc, int n, Ent
 }
 
 // heappush of `it` onto a heap of n entries (position n is free).
-template <bool SPILL>
+template <bool SPILL, int HEUR>
 __device__ __forceinline__ void heap_push(const Heap& hp, const Q& qc, int n, const Ent& it, Ent& root, int lane)
 {
     n = uni(n);
     const int np1 = n + 1;
     const int depth = 31 - __clz(np1);  // ancestors of position n
-    Ent a;
-    a.f = 0.0; a.cm = 0u;
     const bool valid = lane < depth;
-    if (valid) hload<SPILL>(hp, (np1 >> (lane + 1)) - 1, a.f, a.cm);
-    a.hk = key_of(qc, a.cm);
-    const bool less = valid && ent_lt(it, a);
-    const int t = __popcll(ballot(less));  // the "less" set is a prefix from the parent upwards
+    const int apos = valid ? (np1 >> (lane + 1)) - 1 : 0;
+    Ent a;
+    if constexpr (SPILL) {
+        a.f = 0.0;
+        a.cm = 0u;
+        if (valid) hload<true>(hp, apos, a.f, a.cm);
+    } else {
+        a.f = hp.lg[apos];
+        a.cm = hp.lcm[apos];
+    }
+    a.hk = key_of<HEUR>(qc, a.cm);
+    const int t = __popcll(ballot(valid & ent_lt(it, a)));  // the "less" set is a prefix from the parent up
     if (lane < t) hstore<SPILL>(hp, (np1 >> lane) - 1, a.f, a.cm);
     const int ipos = (np1 >> t) - 1;
     if (lane == 0) hstore<SPILL>(hp, ipos, it.f, it.cm);
@@ -236,8 +256,9 @@ __device__ __forceinline__ void heap_push(const Heap& hp, const Q& qc, int n, co
     wave_sync_mem();
 }
 
+template <int HEUR>
 __global__ __launch_bounds__(64) void astar2d_kernel(
-    const uint32_t* __restrict__ occ, int W, int H, int heuristic, const int32_t* __restrict__ start_xy,
+    const uint32_t* __restrict__ occ, int W, int H, const int32_t* __restrict__ start_xy,
     const int32_t* __restrict__ goal_xy, const int32_t* __restrict__ order, int nq, double* __restrict__ cost_out,
     int32_t* __restrict__ path_len_out, uint32_t* __restrict__ path_out, int path_cap,
     int32_t* __restrict__ nexp_out, uint32_t* __restrict__ expand_out, int expand_cap,
@@ -262,6 +283,9 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
     // lane 9 + i -> its CLOSED-state nibble
     const int blk_i = lane < 9 ? lane : (lane < 18 ? lane - 9 : 4);
     const int blk_dx = blk_i / 3 - 1, blk_dy = blk_i % 3 - 1;
+    // this lane's sibling pair inside a pop chunk: level jl = 1..6 below the hole, offset ol
+    const int pop_jl = 32 - __clz(lane + 1);
+    const int pop_ol = lane + 1 - (1 << (pop_jl - 1));
 
     for (;;) {
         int qi = 0;
@@ -286,7 +310,6 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
         Q qc;
         qc.gx = goal_xy[2 * q];
         qc.gy = goal_xy[2 * q + 1];
-        qc.heur = heuristic;
         const bool s_in = (unsigned)sx < (unsigned)W && (unsigned)sy < (unsigned)H;
         const bool g_in = (unsigned)qc.gx < (unsigned)W && (unsigned)qc.gy < (unsigned)H;
         if (!s_in || !g_in) {  // outside the grid: blocked -> no neighbours -> no path
@@ -347,8 +370,8 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
 
             // ---- heappop (a_star.py:54): `last` = heap[n] sifts down the CPython path
             if (n > 0) {
-                if (n < lds_cap) heap_pop<false>(hp, qc, n, root, lane);
-                else heap_pop<true>(hp, qc, n, root, lane);
+                if (n < lds_cap) heap_pop<false, HEUR>(hp, qc, n, root, lane, pop_jl, pop_ol);
+                else heap_pop<true, HEUR>(hp, qc, n, root, lane, pop_jl, pop_ol);
             }
 
             STAMP(ts1);
@@ -417,7 +440,7 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 item.cm = (nbxy << 4) | (uint32_t)m;
                 item.f = 0.0;
                 item.hk = 0u;
-                if (lane < 8) item.f = (gnode + ((m & 1) ? kSqrt2 : 1.0)) + h_and_key(qc, item.cm, item.hk);
+                if (lane < 8) item.f = (gnode + ((m & 1) ? kSqrt2 : 1.0)) + h_and_key<HEUR>(qc, item.cm, item.hk);
             }
             bool overflow = false;
             while (vm) {
@@ -428,8 +451,8 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 it.f = rl_f64(item.f, m);
                 it.cm = rl_u32(item.cm, m);
                 it.hk = rl_u32(item.hk, m);
-                if (n < lds_cap) heap_push<false>(hp, qc, n, it, root, lane);
-                else heap_push<true>(hp, qc, n, it, root, lane);
+                if (n < lds_cap) heap_push<false, HEUR>(hp, qc, n, it, root, lane);
+                else heap_push<true, HEUR>(hp, qc, n, it, root, lane);
                 n += 1;
                 npush++;
             }
@@ -547,7 +570,8 @@ extern "C" int pmp_astar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
     hipStream_t s = (hipStream_t)stream;
     const size_t lds = (size_t)g_cfg.lds_cap * 12;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
-    hipLaunchKernelGGL(astar2d_kernel, dim3(workers), dim3(64), lds, s, occ_bits, W, H, heuristic, start_xy,
+    auto kern = heuristic == 1 ? astar2d_kernel<1> : astar2d_kernel<0>;
+    hipLaunchKernelGGL(kern, dim3(workers), dim3(64), lds, s, occ_bits, W, H, start_xy,
                        goal_xy, (const int32_t*)nullptr, nq, cost, path_len, path, path_cap, n_expanded, expand,
                        expand_cap, counters, status, queue, spill, g_cfg.heap_cap, g_cfg.lds_cap, cst, cst_words, G);
     PMP_HIP_CHECK(ctx, hipGetLastError());
