@@ -33,12 +33,15 @@ def astar_algorithmic_bytes(counters: np.ndarray) -> float:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--nq", type=int, default=4096)
     ap.add_argument("--cpu-sample", type=int, default=1024, help="queries in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workers", type=int, default=1024, help="persistent A* workers (waves) per GPU")
+    ap.add_argument("--workers", type=int, default=2048, help="persistent A* workers (waves) per launch")
+    ap.add_argument("--streams", type=int, default=3,
+                    help="batches in flight: consecutive steps go to different HIP streams (own scratch "
+                         "context each), so one batch's long-query tail overlaps the next batch")
     args = ap.parse_args()
 
     import torch
@@ -61,46 +64,60 @@ def main():
     occ, starts, goals = wl.c2_workload(nq=nq, pair_seed=1 + rank)
     W, H = occ.shape
     L = _lib.load_library()
-    ctx = _lib.context()
     occ_bits = batch.occ_bits_device(occ, torch)
     s_d = torch.as_tensor(starts, device="cuda")
     g_d = torch.as_tensor(goals, device="cuda")
     path_cap = 4096
-    cost = torch.empty(nq, dtype=torch.float64, device="cuda")
-    plen = torch.empty(nq, dtype=torch.int32, device="cuda")
-    path = torch.empty((nq, path_cap), dtype=torch.int32, device="cuda")
-    nexp = torch.empty(nq, dtype=torch.int32, device="cuda")
-    status = torch.empty(nq, dtype=torch.int32, device="cuda")
+    S = max(1, args.streams)
+    lanes = []
+    for _ in range(S):
+        ctx = L.pmp_create(torch.cuda.current_device())
+        _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, args.workers, 0), "reserve")
+        lanes.append(dict(
+            ctx=ctx, stream=torch.cuda.Stream(),
+            cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
+            plen=torch.empty(nq, dtype=torch.int32, device="cuda"),
+            path=torch.empty((nq, path_cap), dtype=torch.int32, device="cuda"),
+            nexp=torch.empty(nq, dtype=torch.int32, device="cuda"),
+            status=torch.empty(nq, dtype=torch.int32, device="cuda")))
     ctr = torch.empty((nq, 4), dtype=torch.int64, device="cuda")
-    _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, args.workers, 0), "reserve")
+    torch.cuda.synchronize()
 
-    def step(counters=None):
-        rc = L.pmp_astar2d_batch(ctx, _lib.stream_ptr(), occ_bits.data_ptr(), W, H, 0, s_d.data_ptr(),
-                                 g_d.data_ptr(), nq, cost.data_ptr(), plen.data_ptr(), path.data_ptr(), path_cap,
-                                 nexp.data_ptr(), None, 0, counters, status.data_ptr())
+    def step(i, counters=None):
+        b = lanes[i % S]
+        rc = L.pmp_astar2d_batch(b["ctx"], b["stream"].cuda_stream, occ_bits.data_ptr(), W, H, 0, s_d.data_ptr(),
+                                 g_d.data_ptr(), nq, b["cost"].data_ptr(), b["plen"].data_ptr(), b["path"].data_ptr(),
+                                 path_cap, b["nexp"].data_ptr(), None, 0, counters, b["status"].data_ptr())
         if rc:
-            _lib.check(ctx, rc, "pmp_astar2d_batch")
+            _lib.check(b["ctx"], rc, "pmp_astar2d_batch")
+        return b
 
-    # warmup (the first pass also records the deterministic push/pop/expansion counts)
-    step(ctr.data_ptr())
-    for _ in range(max(0, args.warmup - 1)):
-        step()
+    # warmup: every stream once (the first pass also records the deterministic push/pop/expansion counts)
+    step(0, ctr.data_ptr())
+    for i in range(1, max(args.warmup, S)):
+        step(i)
     torch.cuda.synchronize()
     counters = ctr.cpu().numpy()
-    st = status.cpu().numpy()
-    assert (st == 0).all(), f"unexpected statuses {np.unique(st)}"
+    cost = lanes[0]["cost"]
+    for b in lanes:
+        st = b["status"].cpu().numpy()
+        assert (st == 0).all(), f"unexpected statuses {np.unique(st)}"
+        assert torch.equal(b["cost"], cost)
     bytes_per_launch = astar_algorithmic_bytes(counters)
 
     # timed region
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    evs = []
     t0 = time.perf_counter()
     for i in range(args.steps):
-        evs[i][0].record()
-        step()
-        evs[i][1].record()
+        b = lanes[i % S]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(b["stream"])
+        step(i)
+        e1.record(b["stream"])
+        evs.append((e0, e1))
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -159,7 +176,7 @@ def main():
                        "pushes_per_launch": int(counters[:, 0].sum()),
                        "pops_per_launch": int(counters[:, 1].sum()),
                        "max_heap_entries": int(counters[:, 3].max()),
-                       "workers": args.workers},
+                       "workers": args.workers, "streams": S},
         }
         print(json.dumps(out), flush=True)
     if dist:

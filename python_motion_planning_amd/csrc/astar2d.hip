@@ -491,14 +491,6 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
     }
 }
 
-struct AStarCfg {
-    int W = 0, H = 0;
-    int workers = 0;     // persistent waves
-    int heap_cap = 0;    // CPython heap capacity per query (entries)
-    int lds_cap = 0;     // heap entries held in LDS per worker
-};
-AStarCfg g_cfg;
-
 int default_workers() { return 256 * 4; }
 int default_lds_cap(int workers_per_cu)
 {
@@ -530,11 +522,11 @@ extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int workers, int 
     if (!pmp_scratch(ctx, SCR_CLOSED, (size_t)workers * cst_words * 4)) return PMP_ENOMEM;
     if (!pmp_scratch(ctx, SCR_AUX0, 256)) return PMP_ENOMEM;
     if (!pmp_scratch(ctx, SCR_G, (size_t)workers * ncell * 8)) return PMP_ENOMEM;
-    g_cfg.W = W;
-    g_cfg.H = H;
-    g_cfg.workers = workers;
-    g_cfg.heap_cap = heap_cap;
-    g_cfg.lds_cap = lds_cap;
+    ctx->astar_W = W;
+    ctx->astar_H = H;
+    ctx->astar_workers = workers;
+    ctx->astar_heap_cap = heap_cap;
+    ctx->astar_lds_cap = lds_cap;
     return PMP_OK;
 }
 
@@ -554,13 +546,13 @@ extern "C" int pmp_astar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
     if (!occ_bits || !start_xy || !goal_xy || !cost || !path_len || !path || !n_expanded || !status)
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_batch: null pointer argument");
     PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
-    if (!(g_cfg.W == W && g_cfg.H == H)) {
+    if (!(ctx->astar_W == W && ctx->astar_H == H)) {
         int workers = default_workers();
         if (workers > nq) workers = nq;
         int rc = pmp_astar2d_reserve(ctx, W, H, workers, 0);
         if (rc) return rc;
     }
-    const int workers = g_cfg.workers < nq ? g_cfg.workers : nq;
+    const int workers = ctx->astar_workers < nq ? ctx->astar_workers : nq;
     const size_t ncell = (size_t)W * H;
     const size_t cst_words = ((ncell + 7) / 8 + 3) & ~(size_t)3;
     uint4* spill = (uint4*)ctx->buf[SCR_HEAP];
@@ -568,12 +560,12 @@ extern "C" int pmp_astar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
     int* queue = (int*)ctx->buf[SCR_AUX0];
     double* G = (double*)ctx->buf[SCR_G];
     hipStream_t s = (hipStream_t)stream;
-    const size_t lds = (size_t)g_cfg.lds_cap * 12;
+    const size_t lds = (size_t)ctx->astar_lds_cap * 12;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
     auto kern = heuristic == 1 ? astar2d_kernel<1> : astar2d_kernel<0>;
     hipLaunchKernelGGL(kern, dim3(workers), dim3(64), lds, s, occ_bits, W, H, start_xy,
                        goal_xy, (const int32_t*)nullptr, nq, cost, path_len, path, path_cap, n_expanded, expand,
-                       expand_cap, counters, status, queue, spill, g_cfg.heap_cap, g_cfg.lds_cap, cst, cst_words, G);
+                       expand_cap, counters, status, queue, spill, ctx->astar_heap_cap, ctx->astar_lds_cap, cst, cst_words, G);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }

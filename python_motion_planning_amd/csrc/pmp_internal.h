@@ -9,6 +9,8 @@
 struct pmp_ctx {
     int device = 0;
     std::string err;
+    // A* scratch geometry (pmp_astar2d_reserve)
+    int astar_W = 0, astar_H = 0, astar_workers = 0, astar_heap_cap = 0, astar_lds_cap = 0;
     // grow-only scratch arena, one buffer per use
     void* buf[8] = {nullptr};
     size_t cap[8] = {0};
