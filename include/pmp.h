@@ -71,6 +71,53 @@ int pmp_astar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int 
                       int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded,
                       uint32_t* expand, int expand_cap, int64_t* counters, int32_t* status);
 
+/* LocalPlanner.params (local_planner/local_planner.py:39-55), same names and units. */
+typedef struct {
+    double dt;             /* TIME_STEP */
+    double lookahead_time; /* LOOKAHEAD_TIME */
+    double max_lookahead;  /* MAX_LOOKAHEAD_DIST */
+    double min_lookahead;  /* MIN_LOOKAHEAD_DIST */
+    double max_v_inc, min_v_inc, max_v, min_v;
+    double max_w_inc, min_w_inc, max_w, min_w;
+    double goal_dist_tol, rotate_tol;
+} pmp_lp_params;
+
+/* DWA constructor parameters (local_planner/dwa.py:45-56). nv, nw > 0 fix the number of (v, w)
+ * samples instead of int((v1 - v0) / v_resolution) (used for the 64 x 64 = 4096-sample bench). */
+typedef struct {
+    double heading_weight, obstacle_weight, velocity_weight;
+    double predict_time;   /* horizon H = int(predict_time / dt) */
+    double inflation;      /* obstacle_inflation_radius */
+    double v_resolution, w_resolution;
+    int32_t nv, nw;
+} pmp_dwa_params;
+
+/*
+ * Batched DWA control steps.  Replaces `iters` iterations of DWA.plan (local_planner/dwa.py:72-93):
+ * reachGoal, getLookaheadPoint (local_planner.py:103-170), calDynamicWin (dwa.py:111-135),
+ * evaluation (dwa.py:137-190: H-step Robot.lookforward rollout of every (v, w) sample, heading /
+ * obstacle (cdist, capped at the inflation radius) / velocity, numpy pairwise-sum normalisation,
+ * eval_win @ factor, first-index argmax) and Robot.kinematic (utils/agent/agent.py:68-116).
+ * One workgroup per agent; agents never interact.
+ *   occ_bits [ceil(W*H/32)] u32  obstacle cells, cell (ox + i, oy + j) at bit i*H + j
+ *   state    [na][5] f64  in/out  x, y, theta, v, w
+ *   goal     [na][3] f64          goal pose
+ *   path_xy  [*][2] f64, path_off [na+1] i32   global path of each agent (start -> goal)
+ *   u        [na][2] f64          last applied (v, w)
+ *   best     [na] i32             argmax sample index of the last step
+ *   status   [na] i32             0 stepped (not at goal), 1 goal reached, 4 the reference raises
+ *   n_steps  [na] i32             steps taken in this call
+ *   hist_pose [na][iters][3] f64  nullable; robot pose before each step (Robot.history_pose)
+ *   eval     [na][4096][3] f64    nullable; eval_win @ factor of the last step, row c = sample c
+ *                                  (c < N = nv*nw <= 4096; v outer, w inner as itertools.product)
+ *   best_traj [na][iters][H][5] f64 nullable; traj_win[argmax] of every step (history_traj)
+ */
+int pmp_dwa_step_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int ox, int oy, int W, int H,
+                       const pmp_lp_params* lp, const pmp_dwa_params* dp, int na, double* state,
+                       const double* goal, const double* path_xy, const int32_t* path_off, int iters,
+                       double* u, int32_t* best, int32_t* status, int32_t* n_steps, double* hist_pose,
+                       double* eval, double* best_traj);
+
 /* Pre-size the A* scratch (heap of heap_cap entries per concurrent query, up to max_slots
  * concurrent queries) so that later batch calls allocate nothing (hipGraph-capturable). */
 int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int max_slots, int heap_cap);

@@ -161,3 +161,118 @@ def astar2d_batch(occ: np.ndarray, starts, goals, heuristic: str = "euclidean", 
                                _p(out["path_len"], _i32p), _p(out["n_expanded"], _i32p),
                                _p(out["counters"], _i64p), _p(out["status"], _i32p), int(nthreads))
     return out
+
+
+# ------------------------------------------------------------------------------------------------
+# local planners
+class LPParams(ctypes.Structure):
+    """LocalPlanner.params (local_planner.py:39-55)."""
+    _fields_ = [(n, ctypes.c_double) for n in (
+        "dt", "lookahead_time", "max_lookahead", "min_lookahead", "max_v_inc", "min_v_inc", "max_v", "min_v",
+        "max_w_inc", "min_w_inc", "max_w", "min_w", "goal_dist_tol", "rotate_tol")]
+
+    @classmethod
+    def default(cls, **kw):
+        import math
+
+        d = dict(dt=0.1, lookahead_time=1.0, max_lookahead=2.5, min_lookahead=1.0, max_v_inc=1.0, min_v_inc=-1.0,
+                 max_v=0.5, min_v=0.0, max_w_inc=math.pi, min_w_inc=-math.pi, max_w=math.pi / 2, min_w=-math.pi / 2,
+                 goal_dist_tol=0.5, rotate_tol=0.5)
+        d.update(kw)
+        return cls(**d)
+
+
+def _lp_lib():
+    L = lib()
+    if not getattr(L, "_lp_bound", False):
+        P = ctypes.POINTER(LPParams)
+        L.oracle_np_sum.restype = ctypes.c_double
+        L.oracle_np_sum.argtypes = [_dp, ctypes.c_int64, ctypes.c_int64]
+        L.oracle_lookahead.restype = ctypes.c_int
+        L.oracle_lookahead.argtypes = [_dp, ctypes.c_int, _dp, P, _dp, _dp, _dp]
+        L.oracle_dwa_window.restype = None
+        L.oracle_dwa_window.argtypes = [ctypes.c_double, ctypes.c_double, P, _dp]
+        L.oracle_dwa_eval.restype = ctypes.c_int
+        L.oracle_dwa_eval.argtypes = [_dp, ctypes.c_int, _dp, _dp, _dp, ctypes.c_double, ctypes.c_double,
+                                      ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                      ctypes.c_double, ctypes.c_double, ctypes.c_double, _dp, _i32p, _dp]
+        L.oracle_dwa_step.restype = ctypes.c_int
+        L.oracle_dwa_step.argtypes = [_dp, ctypes.c_int, _dp, ctypes.c_int, _dp, _dp, P, ctypes.c_double,
+                                      ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                      ctypes.c_double, ctypes.c_double, ctypes.c_double, _dp]
+        L.oracle_reach_goal.restype = ctypes.c_int
+        L.oracle_reach_goal.argtypes = [_dp, _dp, P]
+        L.oracle_lqr_control.restype = None
+        L.oracle_lqr_control.argtypes = [_dp, _dp, _dp, ctypes.c_double, ctypes.c_double, P, ctypes.c_int,
+                                         ctypes.c_double, _dp]
+        L._lp_bound = True
+    return L
+
+
+def _d(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def np_sum(a, stride=1):
+    a = _d(a)
+    n = (a.size + stride - 1) // stride
+    return _lp_lib().oracle_np_sum(_p(a, _dp), n, stride)
+
+
+def lookahead(path, robot_xyv, params=None):
+    """getLookaheadPoint (local_planner.py:103-170) -> (status, (x, y), theta, kappa)."""
+    path = _d(path).reshape(-1, 2)
+    r = _d(robot_xyv)
+    pt = np.zeros(2)
+    th = ctypes.c_double(0)
+    ka = ctypes.c_double(0)
+    st = _lp_lib().oracle_lookahead(_p(path, _dp), len(path), _p(r, _dp), ctypes.byref(params or LPParams.default()),
+                                    _p(pt, _dp), ctypes.byref(th), ctypes.byref(ka))
+    return st, (float(pt[0]), float(pt[1])), th.value, ka.value
+
+
+def dwa_window(v, w, params=None):
+    out = np.zeros(4)
+    _lp_lib().oracle_dwa_window(v, w, ctypes.byref(params or LPParams.default()), _p(out, _dp))
+    return out
+
+
+def dwa_eval(obstacles, state, goal_xy, vr, v_res=0.05, w_res=0.05, nv=0, nw=0, predict_time=1.5, dt=0.1,
+             weights=(0.2, 0.1, 0.05), inflation=1.0):
+    """DWA.evaluation (dwa.py:137-190): returns (eval3 [N,3] = eval_win @ factor, best, best_traj [H,5])."""
+    obs = _d(obstacles).reshape(-1, 2)
+    st = _d(state)
+    g = _d(goal_xy)
+    vr = _d(vr)
+    nv_ = nv if nv > 0 else int((vr[1] - vr[0]) / v_res)
+    nw_ = nw if nw > 0 else int((vr[3] - vr[2]) / w_res)
+    N = max(nv_ * nw_, 0)
+    H = int(predict_time / dt)
+    e3 = np.zeros((max(N, 1), 3))
+    bt = np.zeros((max(H, 1), 5))
+    best = ctypes.c_int32(0)
+    n = _lp_lib().oracle_dwa_eval(_p(obs, _dp), len(obs), _p(st, _dp), _p(g, _dp), _p(vr, _dp), v_res, w_res, nv, nw,
+                                  predict_time, dt, weights[0], weights[1], weights[2], inflation, _p(e3, _dp),
+                                  ctypes.byref(best), _p(bt, _dp))
+    return e3[:n], best.value, bt[:H]
+
+
+def dwa_step(obstacles, path, goal, state, params=None, v_res=0.05, w_res=0.05, nv=0, nw=0, predict_time=1.5,
+             weights=(0.2, 0.1, 0.05), inflation=1.0):
+    """One DWA.plan iteration (dwa.py:72-93); returns (status, new_state, u)."""
+    obs = _d(obstacles).reshape(-1, 2)
+    path = _d(path).reshape(-1, 2)
+    g = _d(goal)
+    st = _d(state).copy()
+    u = np.zeros(2)
+    rc = _lp_lib().oracle_dwa_step(_p(obs, _dp), len(obs), _p(path, _dp), len(path), _p(g, _dp), _p(st, _dp),
+                                   ctypes.byref(params or LPParams.default()), v_res, w_res, nv, nw, predict_time,
+                                   weights[0], weights[1], weights[2], inflation, _p(u, _dp))
+    return rc, st, u
+
+
+def lqr_control(s, s_d, u_r, robot_v, robot_w, params=None, iters=100, eps=0.1):
+    u = np.zeros(2)
+    _lp_lib().oracle_lqr_control(_p(_d(s), _dp), _p(_d(s_d), _dp), _p(_d(u_r), _dp), robot_v, robot_w,
+                                 ctypes.byref(params or LPParams.default()), iters, eps, _p(u, _dp))
+    return u

@@ -626,3 +626,336 @@ int oracle_astar2d_batch(const uint8_t* occ, int W, int H, int heuristic, const 
     }
     return found;
 }
+
+/* ==================================================================================== */
+/* Local planners (local_planner/ of the reference)                                      */
+/* ==================================================================================== */
+
+/* LocalPlanner.params (local_planner/local_planner.py:39-55), in this order */
+typedef struct {
+    double dt, lookahead_time, max_lookahead, min_lookahead, max_v_inc, min_v_inc, max_v, min_v,
+        max_w_inc, min_w_inc, max_w, min_w, goal_dist_tol, rotate_tol;
+} lp_params_t;
+
+static const double PI_ = 3.141592653589793;
+
+/* numpy pairwise summation (numpy/_core/src/umath/loops_utils.h pairwise_sum) over one buffer */
+static double np_pairwise(const double* a, int64_t n, int64_t stride)
+{
+    if (n < 8) {
+        double res = 0.0;
+        for (int64_t i = 0; i < n; i++) res += a[i * stride];
+        return res;
+    } else if (n <= 128) {
+        double r[8];
+        int64_t i;
+        for (int j = 0; j < 8; j++) r[j] = a[j * stride];
+        for (i = 8; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; j++) r[j] += a[(i + j) * stride];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; i++) res += a[i * stride];
+        return res;
+    } else {
+        int64_t n2 = n / 2;
+        n2 -= n2 % 8;
+        return np_pairwise(a, n2, stride) + np_pairwise(a + n2 * stride, n - n2, stride);
+    }
+}
+
+/* np.sum of a strided 1-D view: pairwise per 8192-element buffer, buffers added in order */
+double oracle_np_sum(const double* a, int64_t n, int64_t stride)
+{
+    double res = 0.0;
+    for (int64_t i = 0; i < n; i += 8192) {
+        int64_t m = n - i < 8192 ? n - i : 8192;
+        res += np_pairwise(a + i * stride, m, stride);
+    }
+    return res;
+}
+
+/* np.linspace(a, b, num) (numpy/_core/function_base.py): i*step + a, last element = b */
+static void np_linspace(double a, double b, int64_t num, double* out)
+{
+    if (num <= 0) return;
+    if (num == 1) { out[0] = a; return; }
+    const double div = (double)(num - 1), delta = b - a, step = delta / div;
+    for (int64_t i = 0; i < num; i++) out[i] = (step == 0.0) ? ((double)i / div) * delta + a : (double)i * step + a;
+    out[num - 1] = b;
+}
+
+static double regularize_angle(double a) { return a - 2.0 * PI_ * floor((a + PI_) / (2.0 * PI_)); }
+
+static double clampd(double v, double lo, double hi)
+{
+    if (v < lo) v = lo;
+    if (v > hi) v = hi;
+    return v;
+}
+
+/* LocalPlanner.reachGoal (local_planner.py:233-246) */
+int oracle_reach_goal(const double cur[3], const double goal[3], const lp_params_t* P)
+{
+    double e_theta = regularize_angle(cur[2] - goal[2]);
+    int move = vnorm2(goal[0] - cur[0], goal[1] - cur[1]) > P->goal_dist_tol;
+    int rot = fabs(e_theta) > P->rotate_tol;
+    return !(move || rot);
+}
+
+/* LocalPlanner.getLookaheadPoint (local_planner.py:103-170) with MathHelper
+ * (utils/helper/math_helper.py:11-65).  path: [P][2] start->goal.  robot: px, py, v.
+ * Returns 0, or 4 where the reference raises (math domain error / index error). */
+int oracle_lookahead(const double* path, int P, const double robot[3], const lp_params_t* Pr, double pt[2],
+                     double* theta, double* kappa)
+{
+    const double rx = robot[0], ry = robot[1];
+    const double L = clampd(fabs(robot[2]) * Pr->lookahead_time, Pr->min_lookahead, Pr->max_lookahead);
+    if (P < 1) return 4;
+    int idx_closest = 0;
+    double best = vnorm2(rx - path[0], ry - path[1]);
+    for (int i = 1; i < P; i++) {
+        double d = vnorm2(rx - path[2 * i], ry - path[2 * i + 1]);
+        if (d < best) { best = d; idx_closest = i; }
+    }
+    int idx_goal = P - 1, idx_prev = idx_goal - 1;
+    for (int i = idx_closest; i < P; i++) {
+        if (vnorm2(rx - path[2 * i], ry - path[2 * i + 1]) >= L) { idx_goal = i; break; }
+    }
+#define PX(i) path[2 * (((i) % P + P) % P)]
+#define PY(i) path[2 * (((i) % P + P) % P) + 1]
+    if (idx_goal == P - 1) {
+        pt[0] = PX(idx_goal);
+        pt[1] = PY(idx_goal);
+    } else {
+        if (idx_goal == 0) idx_goal = idx_goal + 1;
+        idx_prev = idx_goal - 1;
+        const double x1 = PX(idx_prev) - rx, y1 = PY(idx_prev) - ry;
+        const double x2 = PX(idx_goal) - rx, y2 = PY(idx_goal) - ry;
+        /* circleSegmentIntersection(prev_p, goal_p, L) */
+        const double dx = x2 - x1, dy = y2 - y1;
+        const double dr2 = dx * dx + dy * dy;
+        const double D = x1 * y2 - x2 * y1;
+        const double d1 = x1 * x1 + y1 * y1, d2 = x2 * x2 + y2 * y2, dd = d2 - d1;
+        const double delta_2 = L * L * dr2 - D * D;
+        double ix, iy;
+        if (delta_2 < 0) {
+            /* closestPointOnLine(prev_p, goal_p) */
+            const double apx = 0.0 - x1, apy = 0.0 - y1, abx = x2 - x1, aby = y2 - y1;
+            const double af = (apx * abx + apy * aby) / (abx * abx + aby * aby);
+            ix = x1 + af * abx;
+            iy = y1 + af * aby;
+        } else {
+            const double delta = sqrt(delta_2);
+            if (delta == 0) {
+                ix = D * dy / dr2;
+                iy = -D * dx / dr2;
+            } else {
+                const double s = copysign(1.0, dd);
+                ix = (D * dy + s * dx * delta) / dr2;
+                iy = (-D * dx + s * dy * delta) / dr2;
+            }
+        }
+        pt[0] = ix + rx;
+        pt[1] = iy + ry;
+    }
+    if (idx_prev < -P || idx_goal >= P) return 4;
+    *theta = atan2(PY(idx_goal) - PY(idx_prev), PX(idx_goal) - PX(idx_prev));
+    if (idx_goal == 1) idx_goal = idx_goal + 1;
+    if (idx_goal >= P) return 4; /* IndexError */
+    idx_prev = idx_goal - 1;
+    int idx_pprev = idx_prev - 1;
+    const double a = vnorm2(PX(idx_goal) - PX(idx_prev), PY(idx_goal) - PY(idx_prev));
+    const double b = vnorm2(PX(idx_goal) - PX(idx_pprev), PY(idx_goal) - PY(idx_pprev));
+    const double c = vnorm2(PX(idx_prev) - PX(idx_pprev), PY(idx_prev) - PY(idx_pprev));
+    if (a == 0.0 || c == 0.0 || b == 0.0) return 4; /* ZeroDivisionError */
+    const double cosB = (a * a + c * c - b * b) / (2 * a * c);
+    if (cosB > 1.0 || cosB < -1.0) return 4; /* math domain error */
+    const double sinB = sin(acos(cosB));
+    const double cross = (PX(idx_prev) - PX(idx_pprev)) * (PY(idx_goal) - PY(idx_pprev)) -
+                         (PY(idx_prev) - PY(idx_pprev)) * (PX(idx_goal) - PX(idx_pprev));
+    *kappa = copysign(2 * sinB / b, cross);
+#undef PX
+#undef PY
+    return 0;
+}
+
+/* DWA.calDynamicWin (dwa.py:111-135) */
+void oracle_dwa_window(double v, double w, const lp_params_t* P, double vr[4])
+{
+    const double vd0 = v + P->min_v_inc * P->dt, vd1 = v + P->max_v_inc * P->dt;
+    const double vd2 = w + P->min_w_inc * P->dt, vd3 = w + P->max_w_inc * P->dt;
+    vr[0] = fmax(P->min_v, vd0);
+    vr[1] = fmin(P->max_v, vd1);
+    vr[2] = fmax(P->min_w, vd2);
+    vr[3] = fmin(P->max_w, vd3);
+}
+
+/* DWA.evaluation (dwa.py:137-190) + generateTraj (:192-212) + Robot.lookforward (agent.py:91-116).
+ * obs: [nobs][2] (integer obstacle cells as doubles).  nv/nw > 0 override int((v1-v0)/v_res).
+ * out: eval3 [N][3] = eval_win @ factor (v, w, score); best = argmax; best_traj [H][5].
+ * Returns N (0 = the reference would raise on the empty window). */
+int oracle_dwa_eval(const double* obs, int nobs, const double st[5], const double goal[2], const double vr[4],
+                    double v_res, double w_res, int nv, int nw, double predict_time, double dt, double hw,
+                    double ow, double vw, double R, double* eval3, int* best, double* best_traj)
+{
+    if (nv <= 0) nv = (int)((vr[1] - vr[0]) / v_res);
+    if (nw <= 0) nw = (int)((vr[3] - vr[2]) / w_res);
+    const int N = nv * nw, H = (int)(predict_time / dt);
+    if (N <= 0 || nv < 0 || nw < 0) return 0;
+    double* vs = (double*)malloc(sizeof(double) * (size_t)nv);
+    double* ws = (double*)malloc(sizeof(double) * (size_t)nw);
+    double* ew = (double*)malloc(sizeof(double) * (size_t)N * 5);
+    np_linspace(vr[0], vr[1], nv, vs);
+    np_linspace(vr[2], vr[3], nw, ws);
+    for (int c = 0; c < N; c++) {
+        const double v = vs[c / nw], w = ws[c % nw];
+        double x = st[0], y = st[1], th = st[2];
+        double mind = INFINITY;
+        for (int k = 0; k < H; k++) {
+            const double nx = x + (dt * cos(th)) * v, ny = y + (dt * sin(th)) * v, nth = th + dt * w;
+            x = nx; y = ny; th = nth;
+            for (int o = 0; o < nobs; o++) {
+                const double dx = obs[2 * o] - x, dy = obs[2 * o + 1] - y;
+                const double d = sqrt(dx * dx + dy * dy);
+                if (d < mind) mind = d;
+            }
+        }
+        const double theta = atan2(goal[1] - y, goal[0] - x);
+        ew[5 * c + 0] = v;
+        ew[5 * c + 1] = w;
+        ew[5 * c + 2] = PI_ - fabs(theta - th);
+        ew[5 * c + 3] = mind < R ? mind : R; /* min(min_D, R): min_D kept on ties, same value */
+        ew[5 * c + 4] = fabs(v);
+    }
+    for (int col = 2; col < 5; col++) {
+        const double s = oracle_np_sum(ew + col, N, 5);
+        if (s != 0)
+            for (int c = 0; c < N; c++) ew[5 * c + col] = ew[5 * c + col] / s;
+    }
+    int bi = 0;
+    double bs = -INFINITY;
+    for (int c = 0; c < N; c++) {
+        const double* e = ew + 5 * c;
+        /* (eval_win @ factor) on OpenBLAS: a k-ordered fma chain per output element */
+        const double c0 = fma(e[4], 0.0, fma(e[3], 0.0, fma(e[2], 0.0, fma(e[1], 0.0, e[0] * 1.0))));
+        const double c1 = fma(e[4], 0.0, fma(e[3], 0.0, fma(e[2], 0.0, fma(e[1], 1.0, e[0] * 0.0))));
+        const double c2 = fma(e[4], vw, fma(e[3], ow, fma(e[2], hw, fma(e[1], 0.0, e[0] * 0.0))));
+        if (eval3) { eval3[3 * c] = c0; eval3[3 * c + 1] = c1; eval3[3 * c + 2] = c2; }
+        if (c2 > bs || c == 0) { bs = c2; bi = c; }
+    }
+    *best = bi;
+    if (best_traj) {
+        const double v = vs[bi / nw], w = ws[bi % nw];
+        double x = st[0], y = st[1], th = st[2];
+        for (int k = 0; k < H; k++) {
+            const double nx = x + (dt * cos(th)) * v, ny = y + (dt * sin(th)) * v, nth = th + dt * w;
+            x = nx; y = ny; th = nth;
+            best_traj[5 * k] = x; best_traj[5 * k + 1] = y; best_traj[5 * k + 2] = th;
+            best_traj[5 * k + 3] = v; best_traj[5 * k + 4] = w;
+        }
+    }
+    free(vs); free(ws); free(ew);
+    return N;
+}
+
+/* one DWA.plan iteration (dwa.py:72-93).  st[5] updated in place.  Returns 0 stepped, 1 goal
+ * reached (no step), 4 the reference raises (empty window / lookahead error). */
+int oracle_dwa_step(const double* obs, int nobs, const double* path, int P, const double goal[3], double st[5],
+                    const lp_params_t* Pr, double v_res, double w_res, int nv, int nw, double predict_time,
+                    double hw, double ow, double vw, double R, double u[2])
+{
+    const double cur[3] = {st[0], st[1], st[2]};
+    if (oracle_reach_goal(cur, goal, Pr)) return 1;
+    double pt[2], theta, kappa;
+    const double rob[3] = {st[0], st[1], st[3]};
+    if (oracle_lookahead(path, P, rob, Pr, pt, &theta, &kappa)) return 4;
+    double vr[4];
+    oracle_dwa_window(st[3], st[4], Pr, vr);
+    int best;
+    double* e3 = NULL;
+    int n = oracle_dwa_eval(obs, nobs, st, pt, vr, v_res, w_res, nv, nw, predict_time, Pr->dt, hw, ow, vw, R, e3, &best, NULL);
+    if (n <= 0) return 4;
+    /* recompute the chosen (v, w) exactly as evaluation's linspace produced them */
+    if (nv <= 0) nv = (int)((vr[1] - vr[0]) / v_res);
+    if (nw <= 0) nw = (int)((vr[3] - vr[2]) / w_res);
+    double* vs = (double*)malloc(sizeof(double) * (size_t)nv);
+    double* ws = (double*)malloc(sizeof(double) * (size_t)nw);
+    np_linspace(vr[0], vr[1], nv, vs);
+    np_linspace(vr[2], vr[3], nw, ws);
+    u[0] = vs[best / nw];
+    u[1] = ws[best % nw];
+    free(vs); free(ws);
+    /* Robot.kinematic -> lookforward(state, u, dt) */
+    const double dt = Pr->dt;
+    const double nx = st[0] + (dt * cos(st[2])) * u[0], ny = st[1] + (dt * sin(st[2])) * u[0];
+    const double nth = st[2] + dt * u[1];
+    st[0] = nx; st[1] = ny; st[2] = nth; st[3] = u[0]; st[4] = u[1];
+    return 0;
+}
+
+/* LQR.lqrControl (local_planner/lqr.py:103-145): one discrete Riccati update (the signed
+ * `max(P - P_) < eps` test), K = -(R + B'P_B)^-1 B'P_A, u = u_r + K e, then regularisation
+ * (local_planner.py:172-206) against the robot's current (v, w).  Q = I3, R = I2 (lqr.py:35-36). */
+void oracle_lqr_control(const double s[3], const double sd[3], const double ur[2], double rv, double rw,
+                        const lp_params_t* Pr, int iters, double eps, double u[2])
+{
+    const double dt = Pr->dt;
+    double A[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}}, B[3][2] = {{0, 0}, {0, 0}, {0, 0}};
+    A[0][2] = -ur[0] * sin(sd[2]) * dt;
+    A[1][2] = ur[0] * cos(sd[2]) * dt;
+    B[0][0] = cos(sd[2]) * dt;
+    B[1][0] = sin(sd[2]) * dt;
+    B[2][1] = dt;
+    double Pm[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}}, Pn[3][3];
+    for (int it = 0; it < iters; it++) {
+        double PA[3][3], PB[3][2], APA[3][3], APB[3][2], BPB[2][2], BPA[2][3], S[2][2], Si[2][2];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) { PA[i][j] = 0; for (int k = 0; k < 3; k++) PA[i][j] += Pm[i][k] * A[k][j]; }
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 2; j++) { PB[i][j] = 0; for (int k = 0; k < 3; k++) PB[i][j] += Pm[i][k] * B[k][j]; }
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) { APA[i][j] = 0; for (int k = 0; k < 3; k++) APA[i][j] += A[k][i] * PA[k][j]; }
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 2; j++) { APB[i][j] = 0; for (int k = 0; k < 3; k++) APB[i][j] += A[k][i] * PB[k][j]; }
+        for (int i = 0; i < 2; i++)
+            for (int j = 0; j < 2; j++) { BPB[i][j] = 0; for (int k = 0; k < 3; k++) BPB[i][j] += B[k][i] * PB[k][j]; }
+        for (int i = 0; i < 2; i++)
+            for (int j = 0; j < 3; j++) { BPA[i][j] = 0; for (int k = 0; k < 3; k++) BPA[i][j] += B[k][i] * PA[k][j]; }
+        for (int i = 0; i < 2; i++) for (int j = 0; j < 2; j++) S[i][j] = (i == j ? 1.0 : 0.0) + BPB[i][j];
+        const double det = S[0][0] * S[1][1] - S[0][1] * S[1][0];
+        Si[0][0] = S[1][1] / det; Si[0][1] = -S[0][1] / det; Si[1][0] = -S[1][0] / det; Si[1][1] = S[0][0] / det;
+        double mx = -INFINITY;
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) {
+                double corr = 0;
+                for (int a = 0; a < 2; a++)
+                    for (int b = 0; b < 2; b++) corr += APB[i][a] * Si[a][b] * BPA[b][j];
+                Pn[i][j] = (i == j ? 1.0 : 0.0) + APA[i][j] - corr;
+                if (Pm[i][j] - Pn[i][j] > mx) mx = Pm[i][j] - Pn[i][j];
+            }
+        if (mx < eps) break;
+        memcpy(Pm, Pn, sizeof(Pm));
+    }
+    /* K = -(R + B'P_B)^-1 B'P_A with P_ the last update */
+    double PB[3][2], PA[3][3], BPB[2][2], BPA[2][3], Si[2][2];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 2; j++) { PB[i][j] = 0; for (int k = 0; k < 3; k++) PB[i][j] += Pn[i][k] * B[k][j]; }
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) { PA[i][j] = 0; for (int k = 0; k < 3; k++) PA[i][j] += Pn[i][k] * A[k][j]; }
+    for (int i = 0; i < 2; i++)
+        for (int j = 0; j < 2; j++) { BPB[i][j] = (i == j ? 1.0 : 0.0); for (int k = 0; k < 3; k++) BPB[i][j] += B[k][i] * PB[k][j]; }
+    for (int i = 0; i < 2; i++)
+        for (int j = 0; j < 3; j++) { BPA[i][j] = 0; for (int k = 0; k < 3; k++) BPA[i][j] += B[k][i] * PA[k][j]; }
+    const double det = BPB[0][0] * BPB[1][1] - BPB[0][1] * BPB[1][0];
+    Si[0][0] = BPB[1][1] / det; Si[0][1] = -BPB[0][1] / det; Si[1][0] = -BPB[1][0] / det; Si[1][1] = BPB[0][0] / det;
+    double K[2][3];
+    for (int i = 0; i < 2; i++)
+        for (int j = 0; j < 3; j++) { K[i][j] = 0; for (int a = 0; a < 2; a++) K[i][j] -= Si[i][a] * BPA[a][j]; }
+    const double e[3] = {s[0] - sd[0], s[1] - sd[1], regularize_angle(s[2] - sd[2])};
+    double uu[2];
+    for (int i = 0; i < 2; i++) { uu[i] = ur[i]; for (int j = 0; j < 3; j++) uu[i] += K[i][j] * e[j]; }
+    /* linearRegularization / angularRegularization */
+    double vi = clampd(uu[0] - rv, Pr->min_v_inc, Pr->max_v_inc);
+    u[0] = clampd(rv + vi, Pr->min_v, Pr->max_v);
+    double wi = clampd(uu[1] - rw, Pr->min_w_inc, Pr->max_w_inc);
+    u[1] = clampd(rw + wi, Pr->min_w, Pr->max_w);
+}

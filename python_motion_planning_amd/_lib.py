@@ -24,7 +24,30 @@ SIGNATURES = {
     "pmp_astar2d_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _i,
                                _vp, _vp]),
     "pmp_astar2d_reserve": (_i, [_vp, _i, _i, _i, _i]),
+    "pmp_dwa_step_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp,
+                                _vp, _vp, _vp, _vp]),
 }
+
+
+class LPParams(ctypes.Structure):
+    """pmp_lp_params == LocalPlanner.params (local_planner/local_planner.py:39-55)."""
+    _fields_ = [(n, ctypes.c_double) for n in (
+        "dt", "lookahead_time", "max_lookahead", "min_lookahead", "max_v_inc", "min_v_inc", "max_v", "min_v",
+        "max_w_inc", "min_w_inc", "max_w", "min_w", "goal_dist_tol", "rotate_tol")]
+
+    @classmethod
+    def from_params(cls, p: dict):
+        return cls(p["TIME_STEP"], p["LOOKAHEAD_TIME"], p["MAX_LOOKAHEAD_DIST"], p["MIN_LOOKAHEAD_DIST"],
+                   p["MAX_V_INC"], p["MIN_V_INC"], p["MAX_V"], p["MIN_V"], p["MAX_W_INC"], p["MIN_W_INC"],
+                   p["MAX_W"], p["MIN_W"], p["GOAL_DIST_TOL"], p["ROTATE_TOL"])
+
+
+class DWAParams(ctypes.Structure):
+    """pmp_dwa_params == the DWA constructor's parameters (local_planner/dwa.py:45-56)."""
+    _fields_ = [("heading_weight", ctypes.c_double), ("obstacle_weight", ctypes.c_double),
+                ("velocity_weight", ctypes.c_double), ("predict_time", ctypes.c_double),
+                ("inflation", ctypes.c_double), ("v_resolution", ctypes.c_double),
+                ("w_resolution", ctypes.c_double), ("nv", ctypes.c_int32), ("nw", ctypes.c_int32)]
 
 STATUS_FOUND, STATUS_NO_PATH, STATUS_PATH_OVERFLOW, STATUS_CAP_OVERFLOW, STATUS_REF_RAISES = range(5)
 

@@ -5,6 +5,8 @@ each one launches the gfx950 kernels of libpmp_hip.so asynchronously on the curr
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 
 from . import _lib
@@ -65,4 +67,66 @@ def astar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: in
                              _lib.ptr(out["counters"]), out["status"].data_ptr())
     _lib.check(ctx, rc, "pmp_astar2d_batch")
     out["W"], out["H"] = W, H
+    return out
+
+
+def obstacle_grid(obstacles):
+    """Obstacle set of (x, y) integer tuples -> (ox, oy, occ[W, H]) covering its bounding box."""
+    if not obstacles:
+        return 0, 0, np.zeros((1, 1), np.uint8)
+    a = np.fromiter((c for t in obstacles for c in t), np.int64, count=2 * len(obstacles)).reshape(-1, 2)
+    ox, oy = int(a[:, 0].min()), int(a[:, 1].min())
+    W, H = int(a[:, 0].max()) - ox + 1, int(a[:, 1].max()) - oy + 1
+    occ = np.zeros((W, H), np.uint8)
+    occ[a[:, 0] - ox, a[:, 1] - oy] = 1
+    return ox, oy, occ
+
+
+def pack_paths(paths):
+    """list of [P_i, 2] paths -> (path_xy [sum P, 2] f64, path_off [n+1] i32) numpy arrays."""
+    off = np.zeros(len(paths) + 1, np.int32)
+    for i, p in enumerate(paths):
+        off[i + 1] = off[i] + len(p)
+    xy = np.concatenate([np.asarray(p, np.float64).reshape(-1, 2) for p in paths]) if off[-1] else np.zeros((0, 2))
+    return xy, off
+
+
+def dwa_step_batch(grid, lp_params, dwa_params, state, goal, path_xy, path_off, iters: int = 1,
+                   want_eval: bool = False, want_traj: bool = False, want_hist: bool = False, stream=None):
+    """Batched DWA.plan iterations (dwa.py:72-93) on the gfx950 kernel dwa.hip.
+
+    grid: (ox, oy, occ[W, H]) from obstacle_grid() (or with occ already a device bit tensor plus W, H).
+    lp_params: _lib.LPParams; dwa_params: _lib.DWAParams.
+    state [na, 5] f64 device tensor, updated in place; goal [na, 3]; path_xy / path_off from pack_paths().
+    Returns dict of device tensors (u, best, status, n_steps, optional hist_pose, eval, best_traj).
+    """
+    torch = _lib.device_check()
+    L = _lib.load_library()
+    ctx = _lib.context()
+    ox, oy, occ = grid[:3]
+    if isinstance(occ, np.ndarray):
+        W, H = occ.shape
+        occ_bits = occ_bits_device(occ, torch)
+    else:
+        occ_bits, (W, H) = occ, grid[3]
+    na = int(state.shape[0])
+    goal = _dev(torch, goal, torch.float64).reshape(-1, 3)
+    path_xy = _dev(torch, path_xy, torch.float64).reshape(-1, 2)
+    path_off = _dev(torch, path_off, torch.int32)
+    H_steps = int(dwa_params.predict_time / lp_params.dt)
+    out = dict(u=torch.empty((na, 2), dtype=torch.float64, device="cuda"),
+               best=torch.empty(na, dtype=torch.int32, device="cuda"),
+               status=torch.empty(na, dtype=torch.int32, device="cuda"),
+               n_steps=torch.empty(na, dtype=torch.int32, device="cuda"))
+    out["hist_pose"] = torch.zeros((na, iters, 3), dtype=torch.float64, device="cuda") if want_hist else None
+    out["eval"] = torch.zeros((na, 4096, 3), dtype=torch.float64, device="cuda") if want_eval else None
+    out["best_traj"] = (torch.zeros((na, iters, max(H_steps, 1), 5), dtype=torch.float64, device="cuda")
+                        if want_traj else None)
+    rc = L.pmp_dwa_step_batch(ctx, stream if stream is not None else _lib.stream_ptr(), occ_bits.data_ptr(),
+                              ox, oy, W, H, ctypes.byref(lp_params), ctypes.byref(dwa_params), na, state.data_ptr(),
+                              goal.data_ptr(), path_xy.data_ptr(), path_off.data_ptr(), int(iters),
+                              out["u"].data_ptr(), out["best"].data_ptr(), out["status"].data_ptr(),
+                              out["n_steps"].data_ptr(), _lib.ptr(out["hist_pose"]), _lib.ptr(out["eval"]),
+                              _lib.ptr(out["best_traj"]))
+    _lib.check(ctx, rc, "pmp_dwa_step_batch")
     return out

@@ -1,0 +1,318 @@
+// Batched DWA control step for gfx950 (local_planner/dwa.py:72-212): one 512-thread workgroup
+// per agent, one lane per (v, w) sample, H-step rollout, obstacle cost from an occupancy stencil,
+// numpy-exact normalisation and scoring, first-index argmax, Robot.kinematic.
+//
+// Numerics follow the reference operation by operation (-ffp-contract=off):
+//  - Robot.lookforward (agent.py:91-116): x' = x + (dt*cos th)*v, y' = y + (dt*sin th)*v,
+//    th' = th + dt*w (the F@state + B@u products with 0/1 entries are exact).
+//  - obstacle = min(min cdist(obstacles, traj), R): only cells with |dx|,|dy| <= R can be < R away,
+//    so a stencil over the occupancy grid gives the same minimum; d = sqrt(dx*dx + dy*dy) as scipy.
+//  - np.sum of a column = numpy pairwise summation (leaves of <= 128 with 8 accumulators, splits at
+//    n/2 rounded down to a multiple of 8), evaluated as that exact tree.
+//  - (eval_win @ factor)[:, 2] = fma(e4, vw, fma(e3, ow, fma(e2, hw, fma(e1, 0, e0*0)))) (OpenBLAS).
+//  - sin/cos/atan2 are the device libm (<= 1 ulp from glibc): trajectories agree to the last bits and
+//    decisions are checked tie-aware in the tests.
+#include "localplan.h"
+
+namespace {
+
+constexpr int kThreads = 512;
+constexpr int kMaxN = 4096;    // samples per step held in LDS
+constexpr int kMaxLeaves = 128;
+
+struct Linsp {  // np.linspace(a, b, n) (numpy/_core/function_base.py)
+    double a, b, step, div, delta;
+    int n;
+};
+
+__device__ inline Linsp make_linsp(double a, double b, int n)
+{
+    Linsp L;
+    L.a = a;
+    L.b = b;
+    L.n = n;
+    L.div = (double)(n - 1);
+    L.delta = b - a;
+    L.step = n > 1 ? L.delta / L.div : 0.0;
+    return L;
+}
+
+__device__ inline double linsp_at(const Linsp& L, int i)
+{
+    if (L.n == 1) return L.a;
+    if (i == L.n - 1) return L.b;
+    return L.step == 0.0 ? ((double)i / L.div) * L.delta + L.a : (double)i * L.step + L.a;
+}
+
+__device__ inline bool occ_at(const uint32_t* occ, int ox, int oy, int W, int H, int cx, int cy)
+{
+    const int i = cx - ox, j = cy - oy;
+    if ((unsigned)i >= (unsigned)W || (unsigned)j >= (unsigned)H) return false;
+    const uint32_t k = (uint32_t)i * (uint32_t)H + (uint32_t)j;
+    return (occ[k >> 5] >> (k & 31)) & 1u;
+}
+
+// numpy pairwise-sum leaf (n <= 128)
+__device__ inline double pw_leaf(const double* a, int n)
+{
+    if (n < 8) {
+        double res = 0.0;
+        for (int i = 0; i < n; i++) res += a[i];
+        return res;
+    }
+    double r[8];
+    for (int j = 0; j < 8; j++) r[j] = a[j];
+    int i;
+    for (i = 8; i < n - (n % 8); i += 8)
+        for (int j = 0; j < 8; j++) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; i++) res += a[i];
+    return res;
+}
+
+__device__ inline int pw_half(int n)
+{
+    int n2 = n / 2;
+    return n2 - n2 % 8;
+}
+
+struct DwaShared {
+    double col[3][kMaxN];            // heading, obstacle, velocity per sample
+    double leafsum[3][kMaxLeaves];
+    int leaf_lo[kMaxLeaves], leaf_n[kMaxLeaves];
+    double redd[kThreads];
+    int redi[kThreads];
+    double sums[3];
+    double pt[2], theta, kappa;
+    int nleaves;
+};
+
+// pairwise tree over the leaves (in left-to-right order) for a column of n samples
+__device__ inline double pw_combine(const double* leafsum, int n)
+{
+    int ns[16], stage[16];
+    double left[16];
+    int sp = 0, leaf = 0;
+    ns[0] = n;
+    stage[0] = 0;
+    bool have = false;
+    double ret = 0.0;
+    while (sp >= 0) {
+        if (have) {
+            if (stage[sp] == 1) {  // left child done -> descend right
+                left[sp] = ret;
+                stage[sp] = 2;
+                have = false;
+                const int n2 = pw_half(ns[sp]);
+                ns[sp + 1] = ns[sp] - n2;
+                stage[sp + 1] = 0;
+                sp++;
+            } else {  // both done
+                ret = left[sp] + ret;
+                sp--;
+            }
+            continue;
+        }
+        const int nn = ns[sp];
+        if (nn <= 128) {
+            ret = leafsum[leaf++];
+            have = true;
+            sp--;
+            continue;
+        }
+        stage[sp] = 1;
+        ns[sp + 1] = pw_half(nn);
+        stage[sp + 1] = 0;
+        sp++;
+    }
+    return ret;
+}
+
+__global__ __launch_bounds__(kThreads) void dwa_kernel(
+    const uint32_t* __restrict__ occ, int ox, int oy, int W, int H, pmp_lp_params P, pmp_dwa_params D, int na,
+    double* __restrict__ state, const double* __restrict__ goal, const double* __restrict__ path_xy,
+    const int32_t* __restrict__ path_off, int iters, double* __restrict__ u_out, int32_t* __restrict__ best_out,
+    int32_t* __restrict__ status_out, int32_t* __restrict__ nsteps_out, double* __restrict__ hist_pose,
+    double* __restrict__ eval_out, double* __restrict__ best_traj)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    DwaShared& S = *reinterpret_cast<DwaShared*>(smem_raw);
+    const int a = blockIdx.x;
+    const int tid = threadIdx.x;
+    if (a >= na) return;
+    const double* path = path_xy + 2 * (size_t)path_off[a];
+    const int Pn = path_off[a + 1] - path_off[a];
+    const double gl[3] = {goal[3 * a], goal[3 * a + 1], goal[3 * a + 2]};
+    double st[5];
+    for (int k = 0; k < 5; k++) st[k] = state[5 * a + k];
+    const double dt = P.dt;
+    const int Hh = (int)(D.predict_time / dt);
+    const double R = D.inflation;
+    int status = 0, steps = 0, best = 0;
+    double u0 = st[3], u1 = st[4];
+
+    for (int it = 0; it < iters; it++) {
+        // reachGoal (dwa.py:77-78)
+        if (lp::reach_goal(st, gl, P)) { status = PMP_FOUND + 1; break; }
+        // getLookaheadPoint
+        double pt[2] = {0, 0}, theta = 0, kappa = 0;
+        const int ls = lp::lookahead_block(path, Pn, st[0], st[1], st[3], P, pt, &theta, &kappa, S.redd, S.redi);
+        if (tid == 0) { S.pt[0] = pt[0]; S.pt[1] = pt[1]; }
+        __syncthreads();
+        if (ls) { status = PMP_REF_RAISES; break; }
+        const double gx = S.pt[0], gy = S.pt[1];
+        // calDynamicWin (dwa.py:111-135)
+        const double vr0 = fmax(P.min_v, st[3] + P.min_v_inc * dt), vr1 = fmin(P.max_v, st[3] + P.max_v_inc * dt);
+        const double vr2 = fmax(P.min_w, st[4] + P.min_w_inc * dt), vr3 = fmin(P.max_w, st[4] + P.max_w_inc * dt);
+        const int nv = D.nv > 0 ? D.nv : (int)((vr1 - vr0) / D.v_resolution);
+        const int nw = D.nw > 0 ? D.nw : (int)((vr3 - vr2) / D.w_resolution);
+        const int N = nv * nw;
+        if (nv <= 0 || nw <= 0 || N > kMaxN) { status = PMP_REF_RAISES; break; }
+        const Linsp LV = make_linsp(vr0, vr1, nv), LW = make_linsp(vr2, vr3, nw);
+
+        // evaluation: one sample per thread per round (dwa.py:152-174)
+        for (int c = tid; c < N; c += kThreads) {
+            const double v = linsp_at(LV, c / nw), w = linsp_at(LW, c % nw);
+            double x = st[0], y = st[1], th = st[2];
+            double mind = INFINITY;
+            for (int k = 0; k < Hh; k++) {
+                double sn, cs;
+                sincos(th, &sn, &cs);
+                const double nx = x + (dt * cs) * v, ny = y + (dt * sn) * v, nth = th + dt * w;
+                x = nx;
+                y = ny;
+                th = nth;
+                const int x0 = (int)ceil(x - R), x1 = (int)floor(x + R);
+                const int y0 = (int)ceil(y - R), y1 = (int)floor(y + R);
+                for (int cx = x0; cx <= x1 && cx <= x0 + 16; cx++)
+                    for (int cy = y0; cy <= y1 && cy <= y0 + 16; cy++) {
+                        if (!occ_at(occ, ox, oy, W, H, cx, cy)) continue;
+                        const double dx = (double)cx - x, dy = (double)cy - y;
+                        const double d = sqrt(dx * dx + dy * dy);
+                        if (d < mind) mind = d;
+                    }
+            }
+            const double ang = atan2(gy - y, gx - x);
+            S.col[0][c] = lp::kPi - fabs(ang - th);
+            S.col[1][c] = mind < R ? mind : R;
+            S.col[2][c] = fabs(v);
+        }
+        // normalisation sums (dwa.py:176-181): numpy pairwise tree, leaves in parallel
+        if (tid == 0) {
+            int stk_lo[32], stk_n[32], sp = 0, nl = 0;
+            stk_lo[0] = 0;
+            stk_n[0] = N;
+            while (sp >= 0) {
+                const int lo = stk_lo[sp], n = stk_n[sp];
+                sp--;
+                if (n <= 128) {
+                    S.leaf_lo[nl] = lo;
+                    S.leaf_n[nl] = n;
+                    nl++;
+                } else {
+                    const int n2 = pw_half(n);
+                    sp++; stk_lo[sp] = lo + n2; stk_n[sp] = n - n2;  // right pushed first
+                    sp++; stk_lo[sp] = lo; stk_n[sp] = n2;           // left popped first
+                }
+            }
+            S.nleaves = nl;
+        }
+        __syncthreads();
+        const int nl = S.nleaves;
+        if (tid < 3 * nl) {
+            const int cidx = tid / nl, l = tid % nl;
+            S.leafsum[cidx][l] = pw_leaf(&S.col[cidx][S.leaf_lo[l]], S.leaf_n[l]);
+        }
+        __syncthreads();
+        if (tid < 3) S.sums[tid] = 0.0 + pw_combine(S.leafsum[tid], N);
+        __syncthreads();
+        const double s0 = S.sums[0], s1 = S.sums[1], s2 = S.sums[2];
+        // scores and first-index argmax (dwa.py:183-190, :89)
+        double bs = -INFINITY;
+        int bi = 0x7fffffff;
+        for (int c = tid; c < N; c += kThreads) {
+            const double e0 = linsp_at(LV, c / nw), e1 = linsp_at(LW, c % nw);
+            const double e2 = s0 != 0 ? S.col[0][c] / s0 : S.col[0][c];
+            const double e3 = s1 != 0 ? S.col[1][c] / s1 : S.col[1][c];
+            const double e4 = s2 != 0 ? S.col[2][c] / s2 : S.col[2][c];
+            const double sc = fma(e4, D.velocity_weight, fma(e3, D.obstacle_weight, fma(e2, D.heading_weight, fma(e1, 0.0, e0 * 0.0))));
+            if (eval_out && it == iters - 1) {
+                double* e = eval_out + ((size_t)a * kMaxN + c) * 3;
+                e[0] = fma(e4, 0.0, fma(e3, 0.0, fma(e2, 0.0, fma(e1, 0.0, e0 * 1.0))));
+                e[1] = fma(e4, 0.0, fma(e3, 0.0, fma(e2, 0.0, fma(e1, 1.0, e0 * 0.0))));
+                e[2] = sc;
+            }
+            if (sc > bs || bi == 0x7fffffff) { bs = sc; bi = c; }
+        }
+        S.redd[tid] = bs;
+        S.redi[tid] = bi;
+        __syncthreads();
+        for (int s = kThreads / 2; s > 0; s >>= 1) {
+            if (tid < s) {
+                const double od = S.redd[tid + s];
+                const int oi = S.redi[tid + s];
+                if (od > S.redd[tid] || (od == S.redd[tid] && oi < S.redi[tid])) { S.redd[tid] = od; S.redi[tid] = oi; }
+            }
+            __syncthreads();
+        }
+        best = S.redi[0];
+        __syncthreads();
+        u0 = linsp_at(LV, best / nw);
+        u1 = linsp_at(LW, best % nw);
+        if (tid == 0 && hist_pose) {
+            double* hp = hist_pose + ((size_t)a * iters + it) * 3;
+            hp[0] = st[0]; hp[1] = st[1]; hp[2] = st[2];
+        }
+        if (tid == 0 && best_traj) {
+            double x = st[0], y = st[1], th = st[2];
+            for (int k = 0; k < Hh; k++) {
+                double sn, cs;
+                sincos(th, &sn, &cs);
+                const double nx = x + (dt * cs) * u0, ny = y + (dt * sn) * u0, nth = th + dt * u1;
+                x = nx; y = ny; th = nth;
+                double* bt = best_traj + (((size_t)a * iters + it) * Hh + k) * 5;
+                bt[0] = x; bt[1] = y; bt[2] = th; bt[3] = u0; bt[4] = u1;
+            }
+        }
+        // Robot.kinematic(u, dt) (agent.py:68-89)
+        {
+            double sn, cs;
+            sincos(st[2], &sn, &cs);
+            const double nx = st[0] + (dt * cs) * u0, ny = st[1] + (dt * sn) * u0, nth = st[2] + dt * u1;
+            st[0] = nx; st[1] = ny; st[2] = nth; st[3] = u0; st[4] = u1;
+        }
+        steps++;
+    }
+    if (tid == 0) {
+        for (int k = 0; k < 5; k++) state[5 * a + k] = st[k];
+        u_out[2 * a] = u0;
+        u_out[2 * a + 1] = u1;
+        best_out[a] = best;
+        status_out[a] = status;
+        nsteps_out[a] = steps;
+    }
+}
+
+}  // namespace
+
+extern "C" int pmp_dwa_step_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int ox, int oy, int W, int H,
+                                  const pmp_lp_params* lp, const pmp_dwa_params* dp, int na, double* state,
+                                  const double* goal, const double* path_xy, const int32_t* path_off, int iters,
+                                  double* u, int32_t* best, int32_t* status, int32_t* n_steps, double* hist_pose,
+                                  double* eval, double* best_traj)
+{
+    if (!ctx) return PMP_EINVAL;
+    if (!lp || !dp || na < 0 || iters < 1 || W < 0 || H < 0)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_dwa_step_batch: bad params/na/iters/dims");
+    if (na == 0) return PMP_OK;
+    if (!occ_bits || !state || !goal || !path_xy || !path_off || !u || !best || !status || !n_steps)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_dwa_step_batch: null pointer argument");
+    if (dp->nv * dp->nw > kMaxN || !(lp->dt > 0) || !(dp->predict_time >= 0))
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_dwa_step_batch: nv*nw must be <= 4096 and dt > 0");
+    PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(dwa_kernel, dim3(na), dim3(kThreads), sizeof(DwaShared), (hipStream_t)stream, occ_bits, ox, oy, W,
+                       H, *lp, *dp, na, state, goal, path_xy, path_off, iters, u, best, status, n_steps, hist_pose, eval,
+                       best_traj);
+    PMP_HIP_CHECK(ctx, hipGetLastError());
+    return PMP_OK;
+}

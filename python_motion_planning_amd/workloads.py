@@ -229,3 +229,20 @@ def c5_workload(nq: int = 8192, X: int = 26, Y: int = 20, Z: int = 16, scenario:
         starts[q] = s
         goals[q] = g
     return occ, starts, goals
+
+
+def c4_workload(na: int = 256, seed: int = 2):
+    """C4: README grid, `na` agents on free cells drawn with default_rng(seed),
+    theta ~ U(-pi, pi), v ~ U(0, 0.5), w ~ U(-pi/2, pi/2); goal (45, 25, 0).  Returns
+    (occ, states [na, 5], goals [na, 3]); the global path of agent i is A* from its cell to (45, 25)."""
+    occ = readme_grid()
+    free = np.argwhere(occ == 0)
+    rng = np.random.default_rng(seed)
+    cells = free[rng.integers(0, len(free), na)]
+    states = np.zeros((na, 5))
+    states[:, 0:2] = cells
+    states[:, 2] = rng.uniform(-np.pi, np.pi, na)
+    states[:, 3] = rng.uniform(0.0, 0.5, na)
+    states[:, 4] = rng.uniform(-np.pi / 2, np.pi / 2, na)
+    goals = np.tile(np.array([45.0, 25.0, 0.0]), (na, 1))
+    return occ, states, goals

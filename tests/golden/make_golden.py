@@ -284,7 +284,123 @@ def sec_astar3d():
     print("astar3d csv rows", len(rows), "runs", len(res))
 
 
-SECTIONS = dict(astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
+# ----------------------------------------------------------------------------------------------
+def readme_env(pmp):
+    from python_motion_planning_amd import workloads as wl
+
+    env = pmp.Grid(51, 31)
+    env.update({(int(x), int(y)) for x, y in np.argwhere(wl.readme_grid())})
+    return env
+
+
+def dwa_eval_case(args):
+    """One DWA.evaluation (dwa.py:137-190) at a chosen robot state; 64x64 or default resolution."""
+    state, grid64, predict_time = args
+    pmp = import_reference()
+    env = readme_env(pmp)
+    p = pmp.DWA((5, 5, 0), (45, 25, 0), env, predict_time=predict_time)
+    r = p.robot
+    r.px, r.py, r.theta, r.v, r.w = state
+    la, theta_trj, kappa = p.getLookaheadPoint()
+    vr = p.calDynamicWin()
+    if grid64:
+        p.v_resolution = (vr[1] - vr[0]) / 64.5
+        p.w_resolution = (vr[3] - vr[2]) / 64.5
+    ev, tw = p.evaluation(vr, la)
+    best = int(np.argmax(ev[:, -1]))
+    close_figs()
+    return dict(state=list(state), lookahead=[float(la[0]), float(la[1])], theta_trj=float(theta_trj),
+                kappa=float(kappa), vr=[float(v) for v in vr], v_res=float(p.v_resolution),
+                w_res=float(p.w_resolution), eval=np.asarray(ev, np.float64), best=best,
+                best_traj=np.asarray(tw[best], np.float64), path=np.asarray(p.path, np.float64))
+
+
+def sec_dwa():
+    pmp = import_reference()
+    rng = np.random.default_rng(31)
+    from python_motion_planning_amd import workloads as wl
+
+    occ = wl.readme_grid()
+    free = np.argwhere(occ == 0)
+    cases = []
+    for i in range(24):
+        c = free[rng.integers(len(free))]
+        st = (float(c[0] + rng.uniform(-0.4, 0.4)), float(c[1] + rng.uniform(-0.4, 0.4)), float(rng.uniform(-np.pi, np.pi)),
+              float(rng.uniform(0, 0.5)), float(rng.uniform(-np.pi / 2, np.pi / 2)))
+        cases.append((st, i < 12, 3.0 if i % 3 else 1.5))
+    with Pool(8) as pool:
+        res = pool.map(dwa_eval_case, cases)
+    out = {}
+    for k in ("state", "lookahead", "vr"):
+        out[k] = np.array([r[k] for r in res], np.float64)
+    for k in ("theta_trj", "kappa", "v_res", "w_res"):
+        out[k] = np.array([r[k] for r in res], np.float64)
+    out["predict_time"] = np.array([c[2] for c in cases])
+    out["best"] = np.array([r["best"] for r in res], np.int32)
+    ev_flat, ev_off = ragged([r["eval"].ravel() for r in res], np.float64)
+    bt_flat, bt_off = ragged([r["best_traj"].ravel() for r in res], np.float64)
+    out.update(eval=ev_flat, eval_off=ev_off, best_traj=bt_flat, best_traj_off=bt_off, path=res[0]["path"])
+    np.savez_compressed(os.path.join(HERE, "dwa_eval.npz"), **out)
+    print("dwa eval", [r["eval"].shape[0] for r in res])
+
+
+def run_local_plan(args):
+    kind, start, goal, kw = args
+    pmp = import_reference()
+    env = readme_env(pmp)
+    cls = {"dwa": pmp.DWA, "lqr": pmp.LQR}[kind]
+    p = cls(start, goal, env, **kw)
+    if kind == "dwa":
+        ok, hist_traj, hist_pose = p.plan()
+        u = np.array([t[0, 3:5] for t in hist_traj]) if ok else np.zeros((0, 2))
+    else:
+        ok, hist_pose = p.plan()
+        u = np.zeros((0, 2))
+    close_figs()
+    return dict(ok=bool(ok), poses=np.asarray(hist_pose if ok else [], np.float64).reshape(-1, 3), u=u,
+                path=np.asarray(p.path, np.float64))
+
+
+def sec_local_plans():
+    cases = [("dwa", (5, 5, 0), (45, 25, 0), {}), ("dwa", (8, 24, -1.0), (45, 25, 0), {"predict_time": 3.0}),
+             ("lqr", (5, 5, 0), (45, 25, 0), {}), ("lqr", (8, 24, -1.0), (45, 25, 0.5), {})]
+    with Pool(4) as pool:
+        res = pool.map(run_local_plan, cases)
+    out = {}
+    for i, (c, r) in enumerate(zip(cases, res)):
+        out[f"c{i}_kind"] = np.array(c[0])
+        out[f"c{i}_start"] = np.array(c[1], np.float64)
+        out[f"c{i}_goal"] = np.array(c[2], np.float64)
+        out[f"c{i}_predict_time"] = np.array(c[3].get("predict_time", 1.5))
+        out[f"c{i}_ok"] = np.array(r["ok"])
+        out[f"c{i}_poses"] = r["poses"]
+        out[f"c{i}_u"] = r["u"]
+        out[f"c{i}_path"] = r["path"]
+    np.savez_compressed(os.path.join(HERE, "local_plans.npz"), **out)
+    print("local plans", [(c[0], r["ok"], len(r["poses"])) for c, r in zip(cases, res)])
+
+
+def sec_lqr():
+    pmp = import_reference()
+    env = readme_env(pmp)
+    p = pmp.LQR((5, 5, 0), (45, 25, 0), env)
+    rng = np.random.default_rng(77)
+    n = 1000
+    S = np.column_stack([rng.uniform(0, 50, n), rng.uniform(0, 30, n), rng.uniform(-np.pi, np.pi, n)])
+    SD = S + np.column_stack([rng.normal(0, 1, n), rng.normal(0, 1, n), rng.normal(0, 0.5, n)])
+    UR = np.column_stack([rng.uniform(0, 0.5, n), rng.uniform(-1, 1, n)])
+    V = rng.uniform(0, 0.5, n)
+    Wv = rng.uniform(-1.5, 1.5, n)
+    U = np.zeros((n, 2))
+    for i in range(n):
+        p.robot.v, p.robot.w = float(V[i]), float(Wv[i])
+        U[i] = p.lqrControl(tuple(S[i]), tuple(SD[i]), tuple(UR[i])).ravel()
+    close_figs()
+    np.savez_compressed(os.path.join(HERE, "lqr_control.npz"), s=S, s_d=SD, u_r=UR, v=V, w=Wv, u=U)
+    print("lqr", U[:3])
+
+
+SECTIONS = dict(dwa=sec_dwa, local_plans=sec_local_plans, lqr=sec_lqr, astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
                 dstar=sec_dstar, astar3d=sec_astar3d)
 
 if __name__ == "__main__":
