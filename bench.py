@@ -10,6 +10,7 @@ the same grid; no collective on the data path.  Rank 0 prints one JSON line.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -30,6 +31,102 @@ def astar_algorithmic_bytes(counters: np.ndarray) -> float:
     return float(np.sum(19.0 * E + 16.0 * (P + Q)))
 
 
+def control_leg(args, torch, dist, world, rank):
+    """BASELINE.json's second metric: MPC-style sampled control steps/s at H=30 x 4096 samples (C4):
+    256 agents per GPU on the README grid, each step = one DWA.plan iteration (dwa.py:72-93) with a
+    64 x 64 (v, w) window, predict_time 3.0 (H = 30).  One timed step = one launch over all agents."""
+    from python_motion_planning_amd import _lib, batch, local_planner, workloads as wl
+
+    na = args.agents
+    occ, states, goals = wl.c4_workload(na, seed=2 + rank)
+    r = batch.astar2d_batch(occ, states[:, :2].astype(np.int32), np.tile([45, 25], (na, 1)).astype(np.int32),
+                            path_cap=2048)
+    pl = r["path_len"].cpu().numpy()
+    P = r["path"].cpu().numpy()
+    Hg = occ.shape[1]
+    paths = []
+    for i in range(na):
+        cells = P[i, : pl[i]][::-1]
+        paths.append(np.column_stack([cells // Hg, cells % Hg]).astype(np.float64))
+    xy, off = batch.pack_paths(paths)
+    lp = _lib.LPParams.from_params(local_planner.LocalPlanner.DEFAULTS)
+    dp = _lib.DWAParams(0.2, 0.1, 0.05, 3.0, 1.0, 0.05, 0.05, 64, 64)
+    grid = batch.obstacle_grid({(int(a), int(b)) for a, b in np.argwhere(occ)})
+    st0 = torch.tensor(states, dtype=torch.float64, device="cuda")
+    st = st0.clone()
+    ox, oy, gocc = grid
+    occ_bits = batch.occ_bits_device(gocc, torch)
+    gd = torch.tensor(goals, dtype=torch.float64, device="cuda")
+    xyd = torch.tensor(xy, dtype=torch.float64, device="cuda")
+    offd = torch.tensor(off, dtype=torch.int32, device="cuda")
+    L = _lib.load_library()
+    ctx = _lib.context()
+    u = torch.empty((na, 2), dtype=torch.float64, device="cuda")
+    best = torch.empty(na, dtype=torch.int32, device="cuda")
+    status = torch.empty(na, dtype=torch.int32, device="cuda")
+    nst = torch.empty(na, dtype=torch.int32, device="cuda")
+
+    def step():
+        rc = L.pmp_dwa_step_batch(ctx, _lib.stream_ptr(), occ_bits.data_ptr(), ox, oy, gocc.shape[0], gocc.shape[1],
+                                  ctypes.byref(lp), ctypes.byref(dp), na, st.data_ptr(), gd.data_ptr(), xyd.data_ptr(),
+                                  offd.data_ptr(), 1, u.data_ptr(), best.data_ptr(), status.data_ptr(),
+                                  nst.data_ptr(), None, None, None)
+        if rc:
+            _lib.check(ctx, rc, "pmp_dwa_step_batch")
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    st.copy_(st0)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = []
+    K = args.control_steps
+    t0 = time.perf_counter()
+    for i in range(K):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        step()
+        e1.record()
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    if dist:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    steps_done = na * K * world
+    # SURVEY.md §8(d) C4: ~8.2 MFLOP per agent-step in the stencil formulation
+    flops_per_step = 4096 * 30 * (12 + 2 * 20) + 4096 * 30 * 9 * 6 + 4096 * 20
+    achieved_tf = flops_per_step * na / (kern_ms * 1e-3) / 1e12
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+
+        threads = min(16, os.cpu_count() or 1)
+        ns = min(32, na)
+        obs = np.argwhere(occ).astype(np.float64)
+        xs, offs = batch.pack_paths(paths[:ns])
+        t = time.perf_counter()
+        O.dwa_step_batch(obs, xs, offs, goals[:ns], states[:ns], nthreads=threads)
+        dt = time.perf_counter() - t
+        cpu = {"value": ns / dt, "unit": "agent-steps/s", "cores": threads, "kind": "port",
+               "sample": f"first {ns} C4 agents, one step each, C restatement of DWA.evaluation (brute-force "
+                         f"cdist like the reference) with OpenMP over agents, {dt:.1f} s wall"}
+    return {"metric": "MPC steps/sec (H=30, 4096 samples): sampled-rollout control step (DWA form)",
+            "value": steps_done / elapsed, "unit": "agent-steps/s", "agents_per_gpu": na, "steps": K,
+            "ms_per_step": elapsed / K * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
+            "config": {"workload": "C4: README 51x31 grid, 64x64 (v,w) samples, H=30, weights 0.2/0.1/0.05"},
+            "roofline": {"bound": "fp64-valu", "achieved": achieved_tf, "peak": 78.6, "unit": "TFLOP/s",
+                         "frac": achieved_tf / 78.6, "traffic": None,
+                         "flops_per_agent_step": flops_per_step},
+            "cpu_baseline": cpu}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -38,6 +135,8 @@ def main():
     ap.add_argument("--nq", type=int, default=4096)
     ap.add_argument("--cpu-sample", type=int, default=1024, help="queries in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--agents", type=int, default=256, help="C4 agents per GPU (control-step leg)")
+    ap.add_argument("--control-steps", type=int, default=20, help="timed control steps")
     ap.add_argument("--workers", type=int, default=2048, help="persistent A* workers (waves) per launch")
     ap.add_argument("--streams", type=int, default=3,
                     help="batches in flight: consecutive steps go to different HIP streams (own scratch "
@@ -150,6 +249,8 @@ def main():
                "sample": f"first {ns} of the 4096 C2 pairs, C restatement (oracle/pmp_oracle.c) with OpenMP over "
                          f"queries, {dt:.1f} s wall"}
 
+    control = control_leg(args, torch, dist, world, rank)
+
     if rank == 0:
         out = {
             "metric": "A* plans/sec on 1024^2 grid (4096 random start/goal pairs per GPU)",
@@ -169,6 +270,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None},
             "cpu_baseline": cpu,
+            "secondary": control,
             "detail": {"kernel_ms_per_launch": kern_ms,
                        "algorithmic_bytes_per_launch": bytes_per_launch,
                        "expansions_per_launch": int(counters[:, 2].sum()),

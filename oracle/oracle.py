@@ -276,3 +276,28 @@ def lqr_control(s, s_d, u_r, robot_v, robot_w, params=None, iters=100, eps=0.1):
     _lp_lib().oracle_lqr_control(_p(_d(s), _dp), _p(_d(s_d), _dp), _p(_d(u_r), _dp), robot_v, robot_w,
                                  ctypes.byref(params or LPParams.default()), iters, eps, _p(u, _dp))
     return u
+
+
+def dwa_step_batch(obstacles, path_xy, path_off, goals, states, params=None, nv=64, nw=64, predict_time=3.0,
+                   v_res=0.05, w_res=0.05, weights=(0.2, 0.1, 0.05), inflation=1.0, nthreads=0):
+    L = _lp_lib()
+    if not getattr(L, "_dwab", False):
+        L.oracle_dwa_step_batch.restype = ctypes.c_int
+        L.oracle_dwa_step_batch.argtypes = [_dp, ctypes.c_int, _dp, _i32p, _dp, _dp, ctypes.c_int,
+                                            ctypes.POINTER(LPParams), ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                            ctypes.c_double, ctypes.c_double, _dp, _i32p, ctypes.c_int]
+        L._dwab = True
+    obs = _d(obstacles).reshape(-1, 2)
+    xy = _d(path_xy).reshape(-1, 2)
+    off = np.ascontiguousarray(path_off, np.int32)
+    g = _d(goals).reshape(-1, 3)
+    st = _d(states).reshape(-1, 5).copy()
+    na = len(st)
+    u = np.zeros((na, 2))
+    status = np.zeros(na, np.int32)
+    L.oracle_dwa_step_batch(_p(obs, _dp), len(obs), _p(xy, _dp), _p(off, _i32p), _p(g, _dp), _p(st, _dp), na,
+                            ctypes.byref(params or LPParams.default()), v_res, w_res, nv, nw, predict_time,
+                            weights[0], weights[1], weights[2], inflation, _p(u, _dp), _p(status, _i32p),
+                            int(nthreads))
+    return st, u, status

@@ -959,3 +959,22 @@ void oracle_lqr_control(const double s[3], const double sd[3], const double ur[2
     double wi = clampd(uu[1] - rw, Pr->min_w_inc, Pr->max_w_inc);
     u[1] = clampd(rw + wi, Pr->min_w, Pr->max_w);
 }
+
+/* OpenMP over agents: one DWA.plan iteration for each (CPU baseline of bench.py's control leg).
+ * paths: path_xy [*][2] + path_off [na+1]; st [na][5] updated; u [na][2]; returns # stepped. */
+int oracle_dwa_step_batch(const double* obs, int nobs, const double* path_xy, const int32_t* path_off,
+                          const double* goals, double* st, int na, const lp_params_t* Pr, double v_res,
+                          double w_res, int nv, int nw, double predict_time, double hw, double ow, double vw,
+                          double R, double* u, int32_t* status, int nthreads)
+{
+    int stepped = 0;
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) reduction(+ : stepped)
+    for (int a = 0; a < na; a++) {
+        status[a] = oracle_dwa_step(obs, nobs, path_xy + 2 * (int64_t)path_off[a], path_off[a + 1] - path_off[a],
+                                    goals + 3 * a, st + 5 * a, Pr, v_res, w_res, nv, nw, predict_time, hw, ow, vw,
+                                    R, u + 2 * a);
+        stepped += status[a] == 0;
+    }
+    return stepped;
+}
