@@ -71,6 +71,22 @@ int pmp_astar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int 
                       int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded,
                       uint32_t* expand, int expand_cap, int64_t* counters, int32_t* status);
 
+/*
+ * Batched 3D A*.  Replaces AStar3D.plan (global_planner/graph_search/a_star3d.py:33-106) with
+ * GraphSearcher3D.h / isCollision (graph_search_3d.py:30-107) over Grid3D's 26 motions
+ * (utils/environment/env3d.py:56-70) and the (f, h, counter) tuple heap.
+ *   occ_bits  per_query ? [nq][ceil(X*Y*Z/32)] : [ceil(X*Y*Z/32)] u32, cell (x*Y + y)*Z + z
+ *   start_xyz, goal_xyz [nq][3] i32;  X, Y, Z <= 256
+ *   cost      [nq] f64   inf when unreachable (a_star3d.py:77-78)
+ *   path      [nq][path_cap] u32 cells start -> goal;  n_expanded = len(CLOSED) (distinct cells)
+ *   expand    nullable [nq][expand_cap] u32 cells in first-insertion order of CLOSED
+ *   counters  nullable [nq][4] i64 pushes, pops, expansions (incl. re-expansions), max heap size
+ */
+int pmp_astar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int per_query, int X, int Y, int Z,
+                      int heuristic, const int32_t* start_xyz, const int32_t* goal_xyz, int nq, double* cost,
+                      int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded, uint32_t* expand,
+                      int expand_cap, int64_t* counters, int32_t* status);
+
 /* LocalPlanner.params (local_planner/local_planner.py:39-55), same names and units. */
 typedef struct {
     double dt;             /* TIME_STEP */

@@ -111,7 +111,7 @@ def astar3d(occ: np.ndarray, start, goal, heuristic: str = "euclidean", with_exp
     cost = ctypes.c_double(0)
     plen = ctypes.c_int32(0)
     nexp = ctypes.c_int32(0)
-    ctr = np.zeros(3, np.int64)
+    ctr = np.zeros(4, np.int64)
     st = lib().oracle_astar3d(_p(occ, _u8p), X, Y, Z, 1 if heuristic == "manhattan" else 0,
                               _p(s, _i32p), _p(g, _i32p), ctypes.byref(cost), _p(path, _i32p), n + 1,
                               ctypes.byref(plen), _p(expand, _i32p) if with_expand else None, n,
@@ -123,7 +123,7 @@ def astar3d(occ: np.ndarray, start, goal, heuristic: str = "euclidean", with_exp
 
     out = dict(status=st, cost=cost.value, n_expanded=nexp.value,
                path=[dec(c) for c in path[: plen.value]], path_cells=path[: plen.value].copy(),
-               n_push=int(ctr[0]), n_pop=int(ctr[1]), n_iter=int(ctr[2]))
+               n_push=int(ctr[0]), n_pop=int(ctr[1]), n_iter=int(ctr[2]), max_heap=int(ctr[3]))
     if with_expand:
         out["expand_cells"] = expand[: nexp.value].copy()
     return out

@@ -349,7 +349,7 @@ int oracle_astar3d(const uint8_t* occ, int X, int Y, int Z, int heuristic, const
     double* cg = (double*)malloc(sizeof(double) * (size_t)ncell);
     int32_t* cparent = (int32_t*)malloc(sizeof(int32_t) * (size_t)ncell);
     uint8_t* closed = (uint8_t*)calloc((size_t)ncell, 1);
-    int64_t cap = 1024, n = 0, npush = 0, npop = 0, nexp = 0, seq = 0, nclose = 0;
+    int64_t cap = 1024, n = 0, npush = 0, npop = 0, nexp = 0, seq = 0, nclose = 0, maxn = 1;
     a3node_t* heap = (a3node_t*)malloc(sizeof(a3node_t) * (size_t)cap);
     int status = 1;
     *path_len = 0;
@@ -426,13 +426,14 @@ int oracle_astar3d(const uint8_t* occ, int X, int Y, int Z, int heuristic, const
             }
             heap[n++] = (a3node_t){tg + hn, hn, tg, seq++, nc, node.cell};
             npush++;
+            if (n > maxn) maxn = n;
             a3_siftdown(heap, 0, n - 1);
         }
     }
 #undef H3
 done3:
     *n_expanded = (int32_t)nclose;
-    if (counters) { counters[0] = npush; counters[1] = npop; counters[2] = nexp; }
+    if (counters) { counters[0] = npush; counters[1] = npop; counters[2] = nexp; counters[3] = maxn; }
     if (status == 1) { *path_len = 0; *cost_out = INFINITY; }
     if (status == 0 && expand && nclose > expand_cap) status = 3;
     free(cg); free(cparent); free(closed); free(heap);

@@ -6,12 +6,12 @@ C-ABI in include/pmp.h).  There is no CPU fallback: without the library or a HIP
 planners raise.
 """
 from .env import Env, Env3D, Grid, Grid3D, Map, Map3D, Node, Node3D, pack_bits  # noqa: F401
-from .graph_search import AStar, GraphSearcher  # noqa: F401
+from .graph_search import AStar, AStar3D, GraphSearcher, GraphSearcher3D  # noqa: F401
 from .factory import ControlFactory, SearchFactory  # noqa: F401
 from .local_planner import DWA, LocalPlanner, Robot  # noqa: F401
 from .planner import Planner, Planner3D  # noqa: F401
 from . import batch, workloads  # noqa: F401
 
 __all__ = ["Env", "Env3D", "Grid", "Grid3D", "Map", "Map3D", "Node", "Node3D", "Planner", "Planner3D",
-           "GraphSearcher", "AStar", "SearchFactory", "ControlFactory", "LocalPlanner", "Robot", "DWA",
+           "GraphSearcher", "AStar", "GraphSearcher3D", "AStar3D", "SearchFactory", "ControlFactory", "LocalPlanner", "Robot", "DWA",
            "batch", "workloads"]

@@ -24,6 +24,8 @@ SIGNATURES = {
     "pmp_astar2d_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _i,
                                _vp, _vp]),
     "pmp_astar2d_reserve": (_i, [_vp, _i, _i, _i, _i]),
+    "pmp_astar3d_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _i,
+                               _vp, _vp]),
     "pmp_dwa_step_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp,
                                 _vp, _vp, _vp, _vp]),
 }

@@ -130,3 +130,44 @@ def dwa_step_batch(grid, lp_params, dwa_params, state, goal, path_xy, path_off, 
                               _lib.ptr(out["best_traj"]))
     _lib.check(ctx, rc, "pmp_dwa_step_batch")
     return out
+
+
+def astar3d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: int | None = None,
+                  expand_cap: int = 0, counters: bool = False):
+    """Batched AStar3D.plan (a_star3d.py:33-106).
+
+    occ: uint8 [X, Y, Z] shared grid or [nq, X, Y, Z] per-query grids (numpy).
+    Returns dict of device tensors: cost (inf if unreachable), path_len, path [nq, path_cap]
+    (cells (x*Y+y)*Z+z, start -> goal), n_expanded (len(CLOSED)), status, optional expand / counters.
+    """
+    torch = _lib.device_check()
+    L = _lib.load_library()
+    ctx = _lib.context()
+    occ = np.asarray(occ)
+    per_query = occ.ndim == 4
+    X, Y, Z = occ.shape[-3:]
+    if per_query:
+        words = np.stack([pack_bits(o) for o in occ])
+    else:
+        words = pack_bits(occ)
+    occ_bits = torch.as_tensor(np.ascontiguousarray(words).view(np.int32), device="cuda")
+    s = _dev(torch, starts, torch.int32).reshape(-1, 3)
+    g = _dev(torch, goals, torch.int32).reshape(-1, 3)
+    nq = int(s.shape[0])
+    if path_cap is None:
+        path_cap = min(X * Y * Z + 1, 1 << 16)
+    out = dict(cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
+               path_len=torch.empty(nq, dtype=torch.int32, device="cuda"),
+               path=torch.empty((nq, path_cap), dtype=torch.int32, device="cuda"),
+               n_expanded=torch.empty(nq, dtype=torch.int32, device="cuda"),
+               status=torch.empty(nq, dtype=torch.int32, device="cuda"))
+    out["expand"] = torch.empty((nq, expand_cap), dtype=torch.int32, device="cuda") if expand_cap else None
+    out["counters"] = torch.empty((nq, 4), dtype=torch.int64, device="cuda") if counters else None
+    rc = L.pmp_astar3d_batch(ctx, _lib.stream_ptr(), occ_bits.data_ptr(), 1 if per_query else 0, X, Y, Z,
+                             1 if heuristic == "manhattan" else 0, s.data_ptr(), g.data_ptr(), nq,
+                             out["cost"].data_ptr(), out["path_len"].data_ptr(), out["path"].data_ptr(), path_cap,
+                             out["n_expanded"].data_ptr(), _lib.ptr(out["expand"]), int(expand_cap),
+                             _lib.ptr(out["counters"]), out["status"].data_ptr())
+    _lib.check(ctx, rc, "pmp_astar3d_batch")
+    out["dims"] = (X, Y, Z)
+    return out

@@ -1,0 +1,450 @@
+// Batched 3D A* for gfx950, exact with the reference AStar3D.plan
+// (global_planner/graph_search/a_star3d.py:33-106) over Grid3D (utils/environment/env3d.py:43-103)
+// with GraphSearcher3D.isCollision (graph_search_3d.py:66-107).
+//
+// The reference heap holds tuples (f, h, counter, node) -> a TOTAL order, so the pop sequence is
+// the sorted order of (f, h, counter) whatever the heap shape; the kernel keeps a binary heap in
+// LDS (spilling deep positions to HBM) with the same key:
+//   entry = {f64 g, u32 seq (push counter), u32 cm = (x<<16 | y<<8 | z) << 5 | dir}   (16 B)
+//   f = g + h recomputed on load with h = math.sqrt(dx**2+dy**2+dz**2) of integers (exactly the
+//   reference's tentative_g + node_n.h), hkey = d2 (sqrt of integers is monotone and exact).
+// Reopening semantics are the reference's: a pop is skipped if CLOSED holds the cell with g <= node.g
+// (:48-50), a neighbour is skipped if CLOSED holds it with g <= tentative_g (:68-70), CLOSED is
+// (over)written before the goal test (:52-63).  Path is reversed to start -> goal (:105).
+// One wave64 per query (persistent workers pulling an atomic queue); per-worker HBM state:
+// u8 closed-dir per cell (0 = open, dir+1 = closed) + f64 closed g per cell, reset per query.
+#include "pmp_internal.h"
+
+namespace {
+
+constexpr int kMaxDim3 = 256;
+
+__device__ __constant__ int8_t c_m3[26][3] = {
+    {-1, 0, 0}, {-1, 1, 0}, {0, 1, 0}, {1, 1, 0}, {1, 0, 0}, {1, -1, 0}, {0, -1, 0}, {-1, -1, 0},
+    {0, 0, 1}, {0, 0, -1},
+    {-1, 0, 1}, {-1, 1, 1}, {0, 1, 1}, {1, 1, 1}, {1, 0, 1}, {1, -1, 1}, {0, -1, 1}, {-1, -1, 1},
+    {-1, 0, -1}, {-1, 1, -1}, {0, 1, -1}, {1, 1, -1}, {1, 0, -1}, {1, -1, -1}, {0, -1, -1}, {-1, -1, -1}};
+
+typedef __attribute__((address_space(3))) double lds_f64;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+struct Q3 {
+    int gx, gy, gz;
+    int heur;  // 0 euclidean, 1 manhattan
+};
+
+struct E3 {
+    double g, f;
+    uint32_t seq, cm, hk;
+};
+
+__device__ __forceinline__ void key3(const Q3& q, E3& e)
+{
+    const int x = (int)(e.cm >> 21), y = (int)((e.cm >> 13) & 255u), z = (int)((e.cm >> 5) & 255u);
+    const int dx = abs(q.gx - x), dy = abs(q.gy - y), dz = abs(q.gz - z);
+    if (q.heur == 1) {
+        e.hk = (uint32_t)(dx + dy + dz);
+        e.f = e.g + (double)e.hk;
+    } else {
+        e.hk = (uint32_t)(dx * dx + dy * dy + dz * dz);
+        e.f = e.g + __dsqrt_rn((double)e.hk);
+    }
+}
+
+// (f, h, counter) tuple order (a_star3d.py:40,75)
+__device__ __forceinline__ bool lt3(const E3& a, const E3& b)
+{
+    return (a.f < b.f) | ((a.f == b.f) & ((a.hk < b.hk) | ((a.hk == b.hk) & (a.seq < b.seq))));
+}
+
+struct Heap3 {
+    lds_f64* lg;
+    lds_u32* lseq;
+    lds_u32* lcm;
+    __amdgpu_buffer_rsrc_t spill;  // {g lo, g hi, seq, cm} for positions >= lds_cap
+    int lds_cap;
+};
+
+template <bool SPILL>
+__device__ __forceinline__ void h3load(const Heap3& hp, int p, E3& e)
+{
+    if (!SPILL || p < hp.lds_cap) {
+        e.g = hp.lg[p];
+        e.seq = hp.lseq[p];
+        e.cm = hp.lcm[p];
+    } else {
+        const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(hp.spill, (p - hp.lds_cap) * 16, 0, 0));
+        e.g = __hiloint2double((int)v.y, (int)v.x);
+        e.seq = v.z;
+        e.cm = v.w;
+    }
+}
+
+template <bool SPILL>
+__device__ __forceinline__ void h3store(const Heap3& hp, int p, const E3& e)
+{
+    if (!SPILL || p < hp.lds_cap) {
+        hp.lg[p] = e.g;
+        hp.lseq[p] = e.seq;
+        hp.lcm[p] = e.cm;
+    } else {
+        const uint64_t b = (uint64_t)__double_as_longlong(e.g);
+        const uint4 v = make_uint4((uint32_t)b, (uint32_t)(b >> 32), e.seq, e.cm);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
+                                               hp.spill, (p - hp.lds_cap) * 16, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void wsync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+__device__ __forceinline__ E3 rl_e3(const E3& e, int lane)
+{
+    E3 r;
+    r.g = rl_f64(e.g, lane);
+    r.f = rl_f64(e.f, lane);
+    r.seq = rl_u32(e.seq, lane);
+    r.cm = rl_u32(e.cm, lane);
+    r.hk = rl_u32(e.hk, lane);
+    return r;
+}
+
+// extract-min on a heap of n (>0, already decremented) entries, old last element at position n
+template <bool SPILL>
+__device__ __forceinline__ void pop3(const Heap3& hp, const Q3& q, int n, E3& root, int lane, int jl, int ol)
+{
+    n = uni(n);
+    E3 last;
+    if (SPILL) {
+        h3load<SPILL>(hp, n, last);
+    } else {
+        h3load<false>(hp, n, last);
+    }
+    last.g = rl_f64(last.g, 0);
+    last.seq = rl_u32(last.seq, 0);
+    last.cm = rl_u32(last.cm, 0);
+    key3(q, last);
+    int hole = 0;
+    bool first = true;
+    for (;;) {
+        const int li = ((hole + 1) << jl) - 1 + 2 * ol;
+        const bool vl = (lane < 63) & (li < n);
+        const bool vr = (lane < 63) & (li + 1 < n);
+        E3 L, R;
+        L.g = R.g = 0.0;
+        L.seq = R.seq = 0u;
+        L.cm = R.cm = 0u;
+        if constexpr (SPILL) {
+            if (vl) h3load<true>(hp, li, L);
+            if (vr) h3load<true>(hp, li + 1, R);
+        } else {
+            h3load<false>(hp, vl ? li : 0, L);
+            h3load<false>(hp, vr ? li + 1 : 0, R);
+        }
+        key3(q, L);
+        key3(q, R);
+        const uint64_t dmask = ballot(vr & lt3(R, L));        // total order: the smaller child
+        const uint64_t mlmask = ballot(vl & lt3(L, last));   // moves up while child < last
+        const uint64_t mrmask = ballot(vr & lt3(R, last));
+        int cur = uni(hole), oc = 0;
+        uint64_t mover = 0, movr = 0;
+        bool go = true;
+#pragma unroll
+        for (int lv = 1; lv <= 6; lv++) {
+            const int c = 2 * cur + 1;
+            const int pl = (1 << (lv - 1)) - 1 + oc;
+            const int r = (int)((dmask >> pl) & 1ull);
+            const uint64_t mm = r ? mrmask : mlmask;
+            go = go & (c < n) & (((mm >> pl) & 1ull) != 0ull);
+            if (go) {
+                mover |= 1ull << pl;
+                movr |= (uint64_t)r << pl;
+                cur = c + r;
+                oc = 2 * oc + r;
+            }
+        }
+        if ((mover >> lane) & 1ull) {
+            const bool rr = (movr >> lane) & 1ull;
+            h3store<SPILL>(hp, ((rr ? li + 1 : li) - 1) >> 1, rr ? R : L);
+        }
+        if (first && (mover & 1ull)) root = rl_e3((movr & 1ull) ? R : L, 0);
+        first = false;
+        hole = cur;
+        if (!go) break;
+        wsync();
+    }
+    if (lane == 0) h3store<SPILL>(hp, hole, last);
+    if (hole == 0) root = last;
+    wsync();
+}
+
+template <bool SPILL>
+__device__ __forceinline__ void push3(const Heap3& hp, const Q3& q, int n, const E3& it, E3& root, int lane)
+{
+    n = uni(n);
+    const int np1 = n + 1;
+    const int depth = 31 - __clz(np1);
+    const bool valid = lane < depth;
+    const int apos = valid ? (np1 >> (lane + 1)) - 1 : 0;
+    E3 a;
+    a.g = 0.0;
+    a.seq = a.cm = 0u;
+    if constexpr (SPILL) {
+        if (valid) h3load<true>(hp, apos, a);
+    } else {
+        h3load<false>(hp, apos, a);
+    }
+    key3(q, a);
+    const int t = __popcll(ballot(valid & lt3(it, a)));
+    if (lane < t) h3store<SPILL>(hp, (np1 >> lane) - 1, a);
+    const int ipos = (np1 >> t) - 1;
+    if (lane == 0) h3store<SPILL>(hp, ipos, it);
+    if (ipos == 0) root = it;
+    wsync();
+}
+
+__device__ __forceinline__ bool occ3(const uint32_t* occ, int X, int Y, int Z, int x, int y, int z)
+{
+    if ((unsigned)x >= (unsigned)X || (unsigned)y >= (unsigned)Y || (unsigned)z >= (unsigned)Z) return true;
+    const uint32_t c = ((uint32_t)x * (uint32_t)Y + (uint32_t)y) * (uint32_t)Z + (uint32_t)z;
+    return (occ[c >> 5] >> (c & 31)) & 1u;
+}
+
+__global__ __launch_bounds__(64) void astar3d_kernel(
+    const uint32_t* __restrict__ occ_all, int per_query, int X, int Y, int Z, int heuristic,
+    const int32_t* __restrict__ start_xyz, const int32_t* __restrict__ goal_xyz, int nq, double* __restrict__ cost_out,
+    int32_t* __restrict__ path_len_out, uint32_t* __restrict__ path_out, int path_cap, int32_t* __restrict__ nexp_out,
+    uint32_t* __restrict__ expand_out, int expand_cap, int64_t* __restrict__ counters, int32_t* __restrict__ status_out,
+    int* __restrict__ queue, uint4* __restrict__ spill_all, int heap_cap, int lds_cap, uint8_t* __restrict__ cdir_all,
+    double* __restrict__ cg_all)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = lane_id();
+    const int worker = blockIdx.x;
+    const size_t ncell = (size_t)X * Y * Z;
+    const size_t words = (ncell + 31) / 32;
+    Heap3 hp;
+    hp.lg = (lds_f64*)smem;
+    hp.lseq = (lds_u32*)(smem + (size_t)8 * lds_cap);
+    hp.lcm = (lds_u32*)(smem + (size_t)12 * lds_cap);
+    hp.lds_cap = lds_cap;
+    {
+        const size_t spill_n = (size_t)(heap_cap > lds_cap ? heap_cap - lds_cap : 0);
+        hp.spill = __builtin_amdgcn_make_buffer_rsrc(spill_all + (size_t)worker * spill_n, 0, (int)(spill_n * 16), 0x00020000);
+    }
+    uint8_t* cdir = cdir_all + (size_t)worker * ncell;
+    double* cg = cg_all + (size_t)worker * ncell;
+    const int pop_jl = 32 - __clz(lane + 1);
+    const int pop_ol = lane + 1 - (1 << (pop_jl - 1));
+    // neighbour lane m < 26: motion m (env3d.py:56-70)
+    const int mdx = lane < 26 ? c_m3[lane][0] : 0, mdy = lane < 26 ? c_m3[lane][1] : 0, mdz = lane < 26 ? c_m3[lane][2] : 0;
+    const int mchg = (mdx != 0) + (mdy != 0) + (mdz != 0);
+    const double mcost = __dsqrt_rn((double)mchg);  // Planner3D.dist: math.sqrt(1|2|3)
+
+    for (;;) {
+        int qi = 0;
+        if (lane == 0) qi = atomicAdd(queue, 1);
+        qi = uni(qi);
+        if (qi >= nq) break;
+        const int q = qi;
+        const uint32_t* occ = occ_all + (per_query ? (size_t)q * words : 0);
+        for (size_t i = lane; i < ncell; i += 64) cdir[i] = 0;
+        wsync();
+        const int sx = start_xyz[3 * q], sy = start_xyz[3 * q + 1], sz = start_xyz[3 * q + 2];
+        Q3 qc;
+        qc.gx = goal_xyz[3 * q];
+        qc.gy = goal_xyz[3 * q + 1];
+        qc.gz = goal_xyz[3 * q + 2];
+        qc.heur = heuristic;
+        const bool s_in = (unsigned)sx < (unsigned)X && (unsigned)sy < (unsigned)Y && (unsigned)sz < (unsigned)Z;
+        const bool g_in = (unsigned)qc.gx < (unsigned)X && (unsigned)qc.gy < (unsigned)Y && (unsigned)qc.gz < (unsigned)Z;
+        if (!s_in || !g_in) {
+            if (lane == 0) {
+                status_out[q] = PMP_NO_PATH;
+                cost_out[q] = __builtin_inf();
+                path_len_out[q] = 0;
+                nexp_out[q] = s_in ? 1 : 0;
+                if (counters) { counters[4 * q] = 1; counters[4 * q + 1] = 1; counters[4 * q + 2] = s_in; counters[4 * q + 3] = 1; }
+            }
+            continue;
+        }
+        const uint32_t scm = (((uint32_t)sx << 16) | ((uint32_t)sy << 8) | (uint32_t)sz) << 5 | 26u;
+        const uint32_t goal_xyz24 = ((uint32_t)qc.gx << 16) | ((uint32_t)qc.gy << 8) | (uint32_t)qc.gz;
+        E3 root;  // start: g = 0, h = heuristic(start), counter 0 (a_star3d.py:38-41)
+        root.g = 0.0;
+        root.seq = 0u;
+        root.cm = scm;
+        key3(qc, root);
+        if (lane == 0) h3store<true>(hp, 0, root);
+        wsync();
+        int n = 1;
+        uint32_t seq = 1;
+        int64_t npush = 1, npop = 0, niter = 0;
+        int nexp = 0, maxn = 1, st = PMP_NO_PATH, plen = 0;
+        double goal_cost = __builtin_inf();
+
+        while (n > 0) {
+            const E3 node = root;
+            npop++;
+            n -= 1;
+            const int x = (int)(node.cm >> 21), y = (int)((node.cm >> 13) & 255u), z = (int)((node.cm >> 5) & 255u);
+            const int ndir = (int)(node.cm & 31u);
+            const uint32_t lin = ((uint32_t)x * (uint32_t)Y + (uint32_t)y) * (uint32_t)Z + (uint32_t)z;
+            // ---- HBM round (issued before the pop): neighbour collision + CLOSED state, node's CLOSED state
+            const int nx = x + mdx, ny = y + mdy, nz = z + mdz;
+            bool coll = true;
+            uint32_t ncd = 0;
+            double ncg = 0.0;
+            uint32_t nlin = 0;
+            if (lane < 26) {
+                coll = occ3(occ, X, Y, Z, x, y, z) || occ3(occ, X, Y, Z, nx, ny, nz);
+                if (mchg == 2) {
+                    if (mdx != 0 && mdy != 0) coll = coll || occ3(occ, X, Y, Z, x + mdx, y, z) || occ3(occ, X, Y, Z, x, y + mdy, z);
+                    else if (mdx != 0 && mdz != 0) coll = coll || occ3(occ, X, Y, Z, x + mdx, y, z) || occ3(occ, X, Y, Z, x, y, z + mdz);
+                    else coll = coll || occ3(occ, X, Y, Z, x, y + mdy, z) || occ3(occ, X, Y, Z, x, y, z + mdz);
+                } else if (mchg == 3) {
+                    coll = coll || occ3(occ, X, Y, Z, x + mdx, y, z) || occ3(occ, X, Y, Z, x, y + mdy, z) ||
+                           occ3(occ, X, Y, Z, x, y, z + mdz);
+                }
+                if (!coll) {
+                    nlin = ((uint32_t)nx * (uint32_t)Y + (uint32_t)ny) * (uint32_t)Z + (uint32_t)nz;
+                    ncd = cdir[nlin];
+                    ncg = cg[nlin];
+                }
+            } else if (lane == 26) {
+                ncd = cdir[lin];
+                ncg = cg[lin];
+            }
+            // ---- pop
+            if (n > 0) {
+                if (n < lds_cap) pop3<false>(hp, qc, n, root, lane, pop_jl, pop_ol);
+                else pop3<true>(hp, qc, n, root, lane, pop_jl, pop_ol);
+            }
+            // best_closed check (a_star3d.py:48-50)
+            const bool sclosed = rl_u32(ncd, 26) != 0u;
+            const double scg = rl_f64(ncg, 26);
+            if (sclosed && node.g >= scg) continue;
+            niter++;
+            if (lane == 0) {
+                if (!sclosed) {
+                    if (expand_out && nexp < expand_cap) expand_out[(size_t)q * expand_cap + nexp] = lin;
+                }
+                cdir[lin] = (uint8_t)(ndir + 1);
+                cg[lin] = node.g;
+            }
+            if (!sclosed) nexp++;
+            if ((node.cm >> 5) == goal_xyz24) {  // goal check (:59-63), path via CLOSED parents
+                st = PMP_FOUND;
+                wsync();
+                if (lane == 0) {
+                    int cx = x, cy = y, cz = z, len = 1;
+                    double cost = 0.0;
+                    while (!(cx == sx && cy == sy && cz == sz)) {  // goal -> start: cost and length
+                        const uint32_t li = ((uint32_t)cx * (uint32_t)Y + (uint32_t)cy) * (uint32_t)Z + (uint32_t)cz;
+                        const int d = (int)cdir[li] - 1;
+                        const int chg = (c_m3[d][0] != 0) + (c_m3[d][1] != 0) + (c_m3[d][2] != 0);
+                        cost += __dsqrt_rn((double)chg);
+                        cx -= c_m3[d][0];
+                        cy -= c_m3[d][1];
+                        cz -= c_m3[d][2];
+                        len++;
+                    }
+                    goal_cost = cost;
+                    plen = len;
+                    if (len <= path_cap) {  // write start -> goal (path.reverse(), :105)
+                        uint32_t* pth = path_out + (size_t)q * path_cap;
+                        cx = x; cy = y; cz = z;
+                        for (int i = len - 1; i >= 0; i--) {
+                            const uint32_t li = ((uint32_t)cx * (uint32_t)Y + (uint32_t)cy) * (uint32_t)Z + (uint32_t)cz;
+                            pth[i] = li;
+                            if (i == 0) break;
+                            const int d = (int)cdir[li] - 1;
+                            cx -= c_m3[d][0];
+                            cy -= c_m3[d][1];
+                            cz -= c_m3[d][2];
+                        }
+                    }
+                }
+                break;
+            }
+            // ---- neighbours (:66-75): skip if CLOSED with g <= tentative_g, else push with counter
+            const double tg = node.g + mcost;
+            const bool ok = lane < 26 && !coll && !(ncd != 0u && tg >= ncg);
+            uint64_t vm = ballot(ok);
+            E3 item;
+            item.g = tg;
+            item.seq = 0u;
+            item.cm = ((((uint32_t)nx & 255u) << 16) | (((uint32_t)ny & 255u) << 8) | ((uint32_t)nz & 255u)) << 5 | (uint32_t)(lane < 26 ? lane : 0);
+            key3(qc, item);
+            bool overflow = false;
+            while (vm) {
+                const int m = __ffsll((long long)vm) - 1;
+                vm &= vm - 1;
+                if (n >= heap_cap) { overflow = true; break; }
+                E3 it = rl_e3(item, m);
+                it.seq = seq++;
+                if (n < lds_cap) push3<false>(hp, qc, n, it, root, lane);
+                else push3<true>(hp, qc, n, it, root, lane);
+                n += 1;
+                npush++;
+            }
+            if (n > maxn) maxn = n;
+            if (overflow) { st = PMP_CAP_OVERFLOW; break; }
+        }
+        if (lane == 0) {
+            int s = st;
+            if (s == PMP_FOUND && plen > path_cap) s = PMP_PATH_OVERFLOW;
+            status_out[q] = s;
+            cost_out[q] = st == PMP_FOUND ? goal_cost : __builtin_inf();
+            path_len_out[q] = st == PMP_FOUND ? plen : 0;
+            nexp_out[q] = nexp;
+            if (counters) {
+                counters[4 * q + 0] = npush;
+                counters[4 * q + 1] = npop;
+                counters[4 * q + 2] = niter;
+                counters[4 * q + 3] = maxn;
+            }
+        }
+        wsync();
+    }
+}
+
+}  // namespace
+
+extern "C" int pmp_astar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int per_query, int X, int Y,
+                                 int Z, int heuristic, const int32_t* start_xyz, const int32_t* goal_xyz, int nq,
+                                 double* cost, int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded,
+                                 uint32_t* expand, int expand_cap, int64_t* counters, int32_t* status)
+{
+    if (!ctx) return PMP_EINVAL;
+    if (X < 1 || Y < 1 || Z < 1 || X > kMaxDim3 || Y > kMaxDim3 || Z > kMaxDim3)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar3d_batch: X, Y, Z must be in [1, 256]");
+    if (heuristic != 0 && heuristic != 1) return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar3d_batch: heuristic must be 0 or 1");
+    if (nq < 0 || path_cap < 1 || (expand && expand_cap < 1))
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar3d_batch: bad nq/path_cap/expand_cap");
+    if (nq == 0) return PMP_OK;
+    if (!occ_bits || !start_xyz || !goal_xyz || !cost || !path_len || !path || !n_expanded || !status)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar3d_batch: null pointer argument");
+    PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    const size_t ncell = (size_t)X * Y * Z;
+    int workers = 256 * 4;
+    if (workers > nq) workers = nq;
+    const int per_cu = 4;
+    int lds_cap = (((160 * 1024) / per_cu - 256) / 16) & ~15;
+    size_t hc = 26 * ncell + 8;
+    if (hc > (size_t)(1 << 22)) hc = (size_t)1 << 22;
+    const int heap_cap = (int)hc;
+    if (lds_cap > heap_cap) lds_cap = (heap_cap + 15) & ~15;
+    const size_t spill_n = heap_cap > lds_cap ? (size_t)(heap_cap - lds_cap) : 0;
+    uint4* spill = (uint4*)pmp_scratch(ctx, SCR_AUX1, (size_t)workers * spill_n * 16 + 16);
+    uint8_t* cdir = (uint8_t*)pmp_scratch(ctx, SCR_AUX2, (size_t)workers * ncell + 16);
+    double* cg = (double*)pmp_scratch(ctx, SCR_AUX3, (size_t)workers * ncell * 8 + 16);
+    int* queue = (int*)pmp_scratch(ctx, SCR_AUX0, 256);
+    if (!spill || !cdir || !cg || !queue) return PMP_ENOMEM;
+    hipStream_t s = (hipStream_t)stream;
+    PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
+    hipLaunchKernelGGL(astar3d_kernel, dim3(workers), dim3(64), (size_t)lds_cap * 16, s, occ_bits, per_query, X, Y, Z,
+                       heuristic, start_xyz, goal_xyz, nq, cost, path_len, path, path_cap, n_expanded, expand, expand_cap,
+                       counters, status, queue, spill, heap_cap, lds_cap, cdir, cg);
+    PMP_HIP_CHECK(ctx, hipGetLastError());
+    return PMP_OK;
+}

@@ -96,3 +96,62 @@ class AStar(GraphSearcher):
         """Batched plan over one occupancy grid; returns the device-tensor dict of
         batch.astar2d_batch (cost, path_len, path goal->start, n_expanded, status)."""
         return batch.astar2d_batch(occ, starts, goals, heuristic_type, **kw)
+
+
+class GraphSearcher3D:
+    """global_planner/graph_search/graph_search_3d.py:11-107 (Planner3D base)."""
+
+    def __init__(self, start: tuple, goal: tuple, env, heuristic_type: str = "euclidean") -> None:
+        from .env import Node3D
+
+        self.start = Node3D(start, start, 0, 0)
+        self.goal = Node3D(goal, goal, 0, 0)
+        self.env = env
+        self.plot = None
+        self.heuristic_type = heuristic_type
+        self.motions = self.env.motions
+        self.obstacles = self.env.obstacles
+
+    def h(self, node, goal) -> float:
+        dx, dy, dz = abs(goal.x - node.x), abs(goal.y - node.y), abs(goal.z - node.z)
+        if self.heuristic_type == "manhattan":
+            return dx + dy + dz
+        return math.sqrt(dx ** 2 + dy ** 2 + dz ** 2)
+
+    def dist(self, node1, node2) -> float:
+        return math.sqrt((node2.x - node1.x) ** 2 + (node2.y - node1.y) ** 2 + (node2.z - node1.z) ** 2)
+
+    def run(self):
+        return self.plan()
+
+
+class AStar3D(GraphSearcher3D):
+    """A* for 3D grids (a_star3d.py:18-111) -- the search runs in the gfx950 kernel astar3d.hip."""
+
+    def __str__(self) -> str:
+        return "A*"
+
+    def plan(self) -> tuple:
+        """(cost, path start->goal, expand) -- (inf, [], expand) when unreachable (a_star3d.py:33-78).
+        expand: one Node3D per CLOSED cell in first-insertion order (its `current`; parent/g/h None)."""
+        from .env import Node3D
+
+        occ = self.env.occupancy()
+        X, Y, Z = occ.shape
+        r = batch.astar3d_batch(occ, np.array([self.start.current]), np.array([self.goal.current]),
+                                self.heuristic_type, path_cap=X * Y * Z + 1, expand_cap=X * Y * Z)
+        st = int(r["status"][0])
+        ne = int(r["n_expanded"][0])
+        ex = r["expand"][0, :ne].cpu().numpy()
+        expand = [Node3D((int(c) // (Y * Z), (int(c) // Z) % Y, int(c) % Z), None, None, None) for c in ex]
+        if st == 1:
+            return float("inf"), [], expand
+        if st != 0:
+            raise RuntimeError(f"AStar3D kernel status {st}")
+        cells = r["path"][0, : int(r["path_len"][0])].cpu().numpy()
+        path = [(int(c) // (Y * Z), (int(c) // Z) % Y, int(c) % Z) for c in cells]
+        return float(r["cost"][0]), path, expand
+
+    @staticmethod
+    def plan_batch(occ, starts, goals, heuristic_type: str = "euclidean", **kw):
+        return batch.astar3d_batch(occ, starts, goals, heuristic_type, **kw)
