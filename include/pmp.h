@@ -134,6 +134,62 @@ int pmp_dwa_step_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int
                        double* u, int32_t* best, int32_t* status, int32_t* n_steps, double* hist_pose,
                        double* eval, double* best_traj);
 
+/* LQR settings (local_planner/lqr.py:35-38): diag Q, diag R, Riccati iteration cap and the
+ * signed exit threshold of lqr.py:134.  Reference defaults: q = 1,1,1  r = 1,1  iters 100  eps 0.1. */
+typedef struct {
+    double q[3], r[2];
+    int32_t iters;
+    double eps;
+} pmp_lqr_params;
+
+/* MPC settings: horizons and weights of mpc.py:37-40 (p = prediction horizon, m = control horizon
+ * <= 8, Q = diag q, R = diag r), then the ADMM settings of the QP solve that replaces OSQP
+ * (mpc.py:196-203): rho, sigma, relaxation alpha, eps_abs / eps_rel on the inf-norm residuals,
+ * max_iter, termination checked every check_every iterations, rho adapted every adaptive_every
+ * iterations (0 = never) when the residual-ratio estimate leaves [rho/adaptive_tol, rho*adaptive_tol]. */
+typedef struct {
+    int32_t p, m;
+    double q[3], r[2];
+    double rho, sigma, alpha, eps_abs, eps_rel, adaptive_tol;
+    int32_t max_iter, check_every, adaptive_every, reserved;
+} pmp_mpc_params;
+
+/*
+ * Batched LQR.lqrControl (local_planner/lqr.py:103-145), one thread per call:
+ *   s, s_d [n][3]   current and desired (x, y, theta)      u_r [n][2]  reference (v, w)
+ *   robot_vw [n][2] the robot's current (v, w) for linear/angularRegularization (local_planner.py:172-206)
+ *   u [n][2]        regularised control
+ */
+int pmp_lqr_control_batch(pmp_ctx* ctx, void* stream, const pmp_lp_params* lp, const pmp_lqr_params* lq, int n,
+                          const double* s, const double* s_d, const double* u_r, const double* robot_vw, double* u);
+
+/*
+ * Batched MPC.mpcControl (local_planner/mpc.py:111-214), one wave64 per call: QP assembly
+ * (S_u'QS_u on the f64 MFMA 16x16x4), ADMM solve, u = du0 + u_p + u_r, regularisation.
+ *   u_p [n][2] in/out  carried control error (returned as u - u_r, before regularisation)
+ *   qp_H [n][2m][2m], qp_g [n][2m], qp_lu [n][2][4m], du [n][2m]   nullable: the assembled QP and its solution
+ *   admm_iters, admm_status [n] i32  nullable: iterations, 0 converged / 1 iteration limit
+ */
+int pmp_mpc_control_batch(pmp_ctx* ctx, void* stream, const pmp_lp_params* lp, const pmp_mpc_params* mp, int n,
+                          const double* s, const double* s_d, const double* u_r, double* u_p, const double* robot_vw,
+                          double* u, double* qp_H, double* qp_g, double* qp_lu, double* du, int32_t* admm_iters,
+                          int32_t* admm_status);
+
+#define PMP_TRACK_LQR 0
+#define PMP_TRACK_MPC 1
+/*
+ * Batched tracking-controller plan iterations: `iters` iterations of LQR.plan (lqr.py:58-86,
+ * kind PMP_TRACK_LQR) or MPC.plan (mpc.py:66-94, kind PMP_TRACK_MPC) per agent, one wave64 per
+ * agent: reachGoal, getLookaheadPoint, the rotate/move branch, lqrControl / mpcControl,
+ * Robot.kinematic.  Arrays as pmp_dwa_step_batch, plus
+ *   u_p [na][2] f64 in/out   MPC's carried u_p (start a plan with zeros); unused for LQR
+ *   admm_iters [na] i32      nullable; ADMM iterations summed over this call's steps
+ */
+int pmp_track_step_batch(pmp_ctx* ctx, void* stream, int kind, const pmp_lp_params* lp, const pmp_lqr_params* lq,
+                         const pmp_mpc_params* mp, int na, double* state, double* u_p, const double* goal,
+                         const double* path_xy, const int32_t* path_off, int iters, double* u, int32_t* status,
+                         int32_t* n_steps, double* hist_pose, int32_t* admm_iters);
+
 /* Pre-size the A* scratch (heap of heap_cap entries per concurrent query, up to max_slots
  * concurrent queries) so that later batch calls allocate nothing (hipGraph-capturable). */
 int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int max_slots, int heap_cap);

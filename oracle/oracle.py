@@ -182,6 +182,36 @@ class LPParams(ctypes.Structure):
         return cls(**d)
 
 
+class LQRParams(ctypes.Structure):
+    """LQR settings (lqr.py:35-38); mirrors pmp_lqr_params."""
+    _fields_ = [("q", ctypes.c_double * 3), ("r", ctypes.c_double * 2), ("iters", ctypes.c_int32),
+                ("eps", ctypes.c_double)]
+
+    @classmethod
+    def default(cls, **kw):
+        d = dict(q=(1.0, 1.0, 1.0), r=(1.0, 1.0), iters=100, eps=0.1)
+        d.update(kw)
+        return cls((ctypes.c_double * 3)(*d["q"]), (ctypes.c_double * 2)(*d["r"]), d["iters"], d["eps"])
+
+
+class MPCParams(ctypes.Structure):
+    """MPC horizons/weights (mpc.py:37-40) + ADMM settings (OSQP defaults); mirrors pmp_mpc_params."""
+    _fields_ = [("p", ctypes.c_int32), ("m", ctypes.c_int32), ("q", ctypes.c_double * 3), ("r", ctypes.c_double * 2),
+                ("rho", ctypes.c_double), ("sigma", ctypes.c_double), ("alpha", ctypes.c_double),
+                ("eps_abs", ctypes.c_double), ("eps_rel", ctypes.c_double), ("adaptive_tol", ctypes.c_double),
+                ("max_iter", ctypes.c_int32), ("check_every", ctypes.c_int32), ("adaptive_every", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+    @classmethod
+    def default(cls, **kw):
+        d = dict(p=12, m=8, q=(0.8, 0.8, 0.5), r=(2.0, 2.0), rho=0.1, sigma=1e-6, alpha=1.6, eps_abs=1e-3,
+                 eps_rel=1e-3, adaptive_tol=5.0, max_iter=4000, check_every=25, adaptive_every=25)
+        d.update(kw)
+        return cls(d["p"], d["m"], (ctypes.c_double * 3)(*d["q"]), (ctypes.c_double * 2)(*d["r"]), d["rho"],
+                   d["sigma"], d["alpha"], d["eps_abs"], d["eps_rel"], d["adaptive_tol"], d["max_iter"],
+                   d["check_every"], d["adaptive_every"], 0)
+
+
 def _lp_lib():
     L = lib()
     if not getattr(L, "_lp_bound", False):
@@ -203,8 +233,21 @@ def _lp_lib():
         L.oracle_reach_goal.restype = ctypes.c_int
         L.oracle_reach_goal.argtypes = [_dp, _dp, P]
         L.oracle_lqr_control.restype = None
-        L.oracle_lqr_control.argtypes = [_dp, _dp, _dp, ctypes.c_double, ctypes.c_double, P, ctypes.c_int,
-                                         ctypes.c_double, _dp]
+        L.oracle_lqr_control.argtypes = [_dp, _dp, _dp, ctypes.c_double, ctypes.c_double, P,
+                                         ctypes.POINTER(LQRParams), _dp]
+        MP = ctypes.POINTER(MPCParams)
+        L.oracle_mpc_assemble.restype = None
+        L.oracle_mpc_assemble.argtypes = [_dp, _dp, _dp, _dp, P, MP, _dp, _dp, _dp, _dp]
+        L.oracle_qp_admm.restype = ctypes.c_int
+        L.oracle_qp_admm.argtypes = [ctypes.c_int, _dp, _dp, _dp, _dp, MP, _dp, _i32p, _dp]
+        L.oracle_mpc_control.restype = ctypes.c_int
+        L.oracle_mpc_control.argtypes = [_dp, _dp, _dp, _dp, ctypes.c_double, ctypes.c_double, P, MP, _dp, _i32p]
+        L.oracle_track_step.restype = ctypes.c_int
+        L.oracle_track_step.argtypes = [ctypes.c_int, _dp, ctypes.c_int, _dp, _dp, _dp, P, ctypes.POINTER(LQRParams),
+                                        MP, _dp, _i32p]
+        L.oracle_track_batch.restype = ctypes.c_int64
+        L.oracle_track_batch.argtypes = [ctypes.c_int, _dp, _i32p, _dp, _dp, _dp, ctypes.c_int, ctypes.c_int, P,
+                                         ctypes.POINTER(LQRParams), MP, _dp, _i32p, _i32p, ctypes.c_int]
         L._lp_bound = True
     return L
 
@@ -271,11 +314,79 @@ def dwa_step(obstacles, path, goal, state, params=None, v_res=0.05, w_res=0.05, 
     return rc, st, u
 
 
-def lqr_control(s, s_d, u_r, robot_v, robot_w, params=None, iters=100, eps=0.1):
+def lqr_control(s, s_d, u_r, robot_v, robot_w, params=None, lqr=None):
+    """LQR.lqrControl (lqr.py:103-145) with the robot's current (v, w)."""
     u = np.zeros(2)
     _lp_lib().oracle_lqr_control(_p(_d(s), _dp), _p(_d(s_d), _dp), _p(_d(u_r), _dp), robot_v, robot_w,
-                                 ctypes.byref(params or LPParams.default()), iters, eps, _p(u, _dp))
+                                 ctypes.byref(params or LPParams.default()), ctypes.byref(lqr or LQRParams.default()),
+                                 _p(u, _dp))
     return u
+
+
+def mpc_assemble(s, s_d, u_r, u_p, params=None, mpc=None):
+    """MPC.mpcControl QP assembly (mpc.py:124-200) -> (H [2m,2m], g [2m], l [4m], u [4m])."""
+    mpc = mpc or MPCParams.default()
+    n = 2 * mpc.m
+    H, g, lo, hi = np.zeros((n, n)), np.zeros(n), np.zeros(2 * n), np.zeros(2 * n)
+    _lp_lib().oracle_mpc_assemble(_p(_d(s), _dp), _p(_d(s_d), _dp), _p(_d(u_r), _dp), _p(_d(u_p), _dp),
+                                  ctypes.byref(params or LPParams.default()), ctypes.byref(mpc), _p(H, _dp), _p(g, _dp),
+                                  _p(lo, _dp), _p(hi, _dp))
+    return H, g, lo, hi
+
+
+def qp_admm(H, g, lo, hi, mpc=None):
+    """ADMM solve of min 1/2 x'Hx + g'x, lo <= [kron(tril(1),I2); I] x <= hi -> (x, status, iters, rho)."""
+    mpc = mpc or MPCParams.default()
+    x = np.zeros(2 * mpc.m)
+    it = ctypes.c_int32(0)
+    rho = ctypes.c_double(0)
+    st = _lp_lib().oracle_qp_admm(mpc.m, _p(_d(H), _dp), _p(_d(g), _dp), _p(_d(lo), _dp), _p(_d(hi), _dp),
+                                  ctypes.byref(mpc), _p(x, _dp), ctypes.byref(it), ctypes.byref(rho))
+    return x, st, it.value, rho.value
+
+
+def mpc_control(s, s_d, u_r, u_p, robot_v, robot_w, params=None, mpc=None):
+    """MPC.mpcControl (mpc.py:111-214) -> (u [2], new u_p [2], admm status, iters)."""
+    up = _d(u_p).copy()
+    u = np.zeros(2)
+    it = ctypes.c_int32(0)
+    st = _lp_lib().oracle_mpc_control(_p(_d(s), _dp), _p(_d(s_d), _dp), _p(_d(u_r), _dp), _p(up, _dp), robot_v,
+                                      robot_w, ctypes.byref(params or LPParams.default()),
+                                      ctypes.byref(mpc or MPCParams.default()), _p(u, _dp), ctypes.byref(it))
+    return u, up, st, it.value
+
+
+def track_step(kind, path, goal, state, u_p=(0.0, 0.0), params=None, lqr=None, mpc=None):
+    """One LQR.plan (kind "lqr") / MPC.plan ("mpc") iteration -> (status, new_state, new_u_p, u, admm_iters)."""
+    path = _d(path).reshape(-1, 2)
+    st = _d(state).copy()
+    up = _d(u_p).copy()
+    u = np.zeros(2)
+    it = ctypes.c_int32(0)
+    rc = _lp_lib().oracle_track_step(0 if kind == "lqr" else 1, _p(path, _dp), len(path), _p(_d(goal), _dp),
+                                     _p(st, _dp), _p(up, _dp), ctypes.byref(params or LPParams.default()),
+                                     ctypes.byref(lqr or LQRParams.default()), ctypes.byref(mpc or MPCParams.default()),
+                                     _p(u, _dp), ctypes.byref(it))
+    return rc, st, up, u, it.value
+
+
+def track_batch(kind, path_xy, path_off, goals, states, u_p=None, iters=1, params=None, lqr=None, mpc=None,
+                nthreads=0):
+    """`iters` LQR/MPC plan iterations for each agent (OpenMP) -> (states, u_p, u, status, n_steps, total)."""
+    xy = _d(path_xy).reshape(-1, 2)
+    off = np.ascontiguousarray(path_off, np.int32)
+    g = _d(goals).reshape(-1, 3)
+    st = _d(states).reshape(-1, 5).copy()
+    na = len(st)
+    up = np.zeros((na, 2)) if u_p is None else _d(u_p).reshape(-1, 2).copy()
+    u = np.zeros((na, 2))
+    status = np.zeros(na, np.int32)
+    nst = np.zeros(na, np.int32)
+    tot = _lp_lib().oracle_track_batch(0 if kind == "lqr" else 1, _p(xy, _dp), _p(off, _i32p), _p(g, _dp), _p(st, _dp),
+                                       _p(up, _dp), na, iters, ctypes.byref(params or LPParams.default()),
+                                       ctypes.byref(lqr or LQRParams.default()), ctypes.byref(mpc or MPCParams.default()),
+                                       _p(u, _dp), _p(status, _i32p), _p(nst, _i32p), nthreads)
+    return st, up, u, status, nst, tot
 
 
 def dwa_step_batch(obstacles, path_xy, path_off, goals, states, params=None, nv=64, nw=64, predict_time=3.0,

@@ -893,11 +893,19 @@ int oracle_dwa_step(const double* obs, int nobs, const double* path, int P, cons
     return 0;
 }
 
-/* LQR.lqrControl (local_planner/lqr.py:103-145): one discrete Riccati update (the signed
- * `max(P - P_) < eps` test), K = -(R + B'P_B)^-1 B'P_A, u = u_r + K e, then regularisation
- * (local_planner.py:172-206) against the robot's current (v, w).  Q = I3, R = I2 (lqr.py:35-36). */
+/* LQR parameters (lqr.py:35-38): diag Q, diag R, Riccati iteration cap, signed exit threshold.
+ * Layout mirrors pmp_lqr_params in include/pmp.h. */
+typedef struct {
+    double q[3], r[2];
+    int32_t iters;
+    double eps;
+} lqr_params_t;
+
+/* LQR.lqrControl (local_planner/lqr.py:103-145): discrete Riccati iteration with the signed
+ * `max(P - P_) < eps` exit (:132-136), K = -(R + B'P_B)^-1 B'P_A (:139), u = u_r + K e (:140-141),
+ * then linear/angular regularisation (local_planner.py:172-206) against the robot's current (v, w). */
 void oracle_lqr_control(const double s[3], const double sd[3], const double ur[2], double rv, double rw,
-                        const lp_params_t* Pr, int iters, double eps, double u[2])
+                        const lp_params_t* Pr, const lqr_params_t* L, double u[2])
 {
     const double dt = Pr->dt;
     double A[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}}, B[3][2] = {{0, 0}, {0, 0}, {0, 0}};
@@ -906,8 +914,9 @@ void oracle_lqr_control(const double s[3], const double sd[3], const double ur[2
     B[0][0] = cos(sd[2]) * dt;
     B[1][0] = sin(sd[2]) * dt;
     B[2][1] = dt;
-    double Pm[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}}, Pn[3][3];
-    for (int it = 0; it < iters; it++) {
+    double Pm[3][3] = {{L->q[0], 0, 0}, {0, L->q[1], 0}, {0, 0, L->q[2]}}, Pn[3][3];
+    memset(Pn, 0, sizeof(Pn));  /* P_ = zeros when the loop body never runs (lqr.py:128) */
+    for (int it = 0; it < L->iters; it++) {
         double PA[3][3], PB[3][2], APA[3][3], APB[3][2], BPB[2][2], BPA[2][3], S[2][2], Si[2][2];
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) { PA[i][j] = 0; for (int k = 0; k < 3; k++) PA[i][j] += Pm[i][k] * A[k][j]; }
@@ -921,7 +930,7 @@ void oracle_lqr_control(const double s[3], const double sd[3], const double ur[2
             for (int j = 0; j < 2; j++) { BPB[i][j] = 0; for (int k = 0; k < 3; k++) BPB[i][j] += B[k][i] * PB[k][j]; }
         for (int i = 0; i < 2; i++)
             for (int j = 0; j < 3; j++) { BPA[i][j] = 0; for (int k = 0; k < 3; k++) BPA[i][j] += B[k][i] * PA[k][j]; }
-        for (int i = 0; i < 2; i++) for (int j = 0; j < 2; j++) S[i][j] = (i == j ? 1.0 : 0.0) + BPB[i][j];
+        for (int i = 0; i < 2; i++) for (int j = 0; j < 2; j++) S[i][j] = (i == j ? L->r[i] : 0.0) + BPB[i][j];
         const double det = S[0][0] * S[1][1] - S[0][1] * S[1][0];
         Si[0][0] = S[1][1] / det; Si[0][1] = -S[0][1] / det; Si[1][0] = -S[1][0] / det; Si[1][1] = S[0][0] / det;
         double mx = -INFINITY;
@@ -930,10 +939,10 @@ void oracle_lqr_control(const double s[3], const double sd[3], const double ur[2
                 double corr = 0;
                 for (int a = 0; a < 2; a++)
                     for (int b = 0; b < 2; b++) corr += APB[i][a] * Si[a][b] * BPA[b][j];
-                Pn[i][j] = (i == j ? 1.0 : 0.0) + APA[i][j] - corr;
+                Pn[i][j] = (i == j ? L->q[i] : 0.0) + APA[i][j] - corr;
                 if (Pm[i][j] - Pn[i][j] > mx) mx = Pm[i][j] - Pn[i][j];
             }
-        if (mx < eps) break;
+        if (mx < L->eps) break;
         memcpy(Pm, Pn, sizeof(Pm));
     }
     /* K = -(R + B'P_B)^-1 B'P_A with P_ the last update */
@@ -943,7 +952,7 @@ void oracle_lqr_control(const double s[3], const double sd[3], const double ur[2
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) { PA[i][j] = 0; for (int k = 0; k < 3; k++) PA[i][j] += Pn[i][k] * A[k][j]; }
     for (int i = 0; i < 2; i++)
-        for (int j = 0; j < 2; j++) { BPB[i][j] = (i == j ? 1.0 : 0.0); for (int k = 0; k < 3; k++) BPB[i][j] += B[k][i] * PB[k][j]; }
+        for (int j = 0; j < 2; j++) { BPB[i][j] = (i == j ? L->r[i] : 0.0); for (int k = 0; k < 3; k++) BPB[i][j] += B[k][i] * PB[k][j]; }
     for (int i = 0; i < 2; i++)
         for (int j = 0; j < 3; j++) { BPA[i][j] = 0; for (int k = 0; k < 3; k++) BPA[i][j] += B[k][i] * PA[k][j]; }
     const double det = BPB[0][0] * BPB[1][1] - BPB[0][1] * BPB[1][0];
@@ -959,6 +968,302 @@ void oracle_lqr_control(const double s[3], const double sd[3], const double ur[2
     u[0] = clampd(rv + vi, Pr->min_v, Pr->max_v);
     double wi = clampd(uu[1] - rw, Pr->min_w_inc, Pr->max_w_inc);
     u[1] = clampd(rw + wi, Pr->min_w, Pr->max_w);
+}
+
+/* MPC parameters: horizons and weights of mpc.py:37-40, then the ADMM settings of the QP solve
+ * (OSQP's defaults: rho 0.1, sigma 1e-6, alpha 1.6, eps 1e-3/1e-3, 4000 iterations, termination
+ * checked every 25, rho adapted every 25 with tolerance 5).  Mirrors pmp_mpc_params. */
+typedef struct {
+    int32_t p, m;
+    double q[3], r[2];
+    double rho, sigma, alpha, eps_abs, eps_rel, adaptive_tol;
+    int32_t max_iter, check_every, adaptive_every, reserved;
+} mpc_params_t;
+
+/* MPC.mpcControl QP assembly (mpc.py:124-200), written literally: A5/B5/C, S_x and S_u from
+ * repeated products of A5 (np.linalg.matrix_power), H = S_u'QS_u + R, g = S_u'Q(S_x x - 0),
+ * l/u of [kron(tril(1_m), I2); I_2m].  H [2m][2m], g [2m], l/u [4m]. */
+void oracle_mpc_assemble(const double s[3], const double sd[3], const double ur[2], const double up[2],
+                         const lp_params_t* Pr, const mpc_params_t* M, double* H, double* g, double* lo, double* hi)
+{
+    const int p = M->p, m = M->m, n = 2 * m;
+    const double dt = Pr->dt;
+    double A[5][5], B[5][2];
+    memset(A, 0, sizeof(A));
+    memset(B, 0, sizeof(B));
+    for (int i = 0; i < 5; i++) A[i][i] = 1.0;
+    A[0][2] = -ur[0] * sin(sd[2]) * dt;
+    A[1][2] = ur[0] * cos(sd[2]) * dt;
+    B[0][0] = cos(sd[2]) * dt;
+    B[1][0] = sin(sd[2]) * dt;
+    B[2][1] = dt;
+    A[0][3] = B[0][0]; A[1][3] = B[1][0]; A[2][4] = B[2][1];  /* [[A, B], [0, I]] */
+    B[3][0] = 1.0; B[4][1] = 1.0;                            /* [B; I] */
+    const double x[5] = {s[0] - sd[0], s[1] - sd[1], s[2] - sd[2], up[0], up[1]};
+    /* powers A^0 .. A^p (first three rows are all C A^k needs) */
+    double (*Ap)[5][5] = (double (*)[5][5])malloc(sizeof(double) * 25 * (size_t)(p + 1));
+    memset(Ap[0], 0, sizeof(Ap[0]));
+    for (int i = 0; i < 5; i++) Ap[0][i][i] = 1.0;
+    for (int k = 1; k <= p; k++)
+        for (int i = 0; i < 5; i++)
+            for (int j = 0; j < 5; j++) {
+                double acc = 0;
+                for (int t = 0; t < 5; t++) acc += Ap[k - 1][i][t] * A[t][j];
+                Ap[k][i][j] = acc;
+            }
+    const int R3 = 3 * p;
+    double* Su = (double*)calloc((size_t)R3 * n, sizeof(double));
+    double* y = (double*)calloc((size_t)R3, sizeof(double));
+    for (int i = 0; i < p; i++) {
+        for (int d = 0; d < 3; d++) {
+            double acc = 0;
+            for (int t = 0; t < 5; t++) acc += Ap[i + 1][d][t] * x[t];
+            y[3 * i + d] = acc;  /* (S_x x)_r ; Yr = 0 */
+        }
+        for (int j = 0; j < m && j <= i; j++)
+            for (int d = 0; d < 3; d++)
+                for (int c = 0; c < 2; c++) {
+                    double acc = 0;
+                    for (int t = 0; t < 5; t++) acc += Ap[i - j][d][t] * B[t][c];
+                    Su[(size_t)(3 * i + d) * n + 2 * j + c] = acc;
+                }
+    }
+    for (int a = 0; a < n; a++) {
+        for (int b = 0; b < n; b++) {
+            double acc = 0;
+            for (int r = 0; r < R3; r++) acc += Su[(size_t)r * n + a] * M->q[r % 3] * Su[(size_t)r * n + b];
+            H[a * n + b] = acc + (a == b ? M->r[a % 2] : 0.0);
+        }
+        double acc = 0;
+        for (int r = 0; r < R3; r++) acc += Su[(size_t)r * n + a] * M->q[r % 3] * y[r];
+        g[a] = acc;
+    }
+    for (int k = 0; k < m; k++) {
+        lo[2 * k] = Pr->min_v - up[0];        hi[2 * k] = Pr->max_v - up[0];
+        lo[2 * k + 1] = Pr->min_w - up[1];    hi[2 * k + 1] = Pr->max_w - up[1];
+        lo[n + 2 * k] = Pr->min_v_inc;        hi[n + 2 * k] = Pr->max_v_inc;
+        lo[n + 2 * k + 1] = Pr->min_w_inc;    hi[n + 2 * k + 1] = Pr->max_w_inc;
+    }
+    free(Ap); free(Su); free(y);
+}
+
+/* y = A x and x = A' y for A = [kron(tril(1_m), I2); I_2m] (mpc.py:185,197) */
+static void mpc_Ax(int m, const double* x, double* Ax)
+{
+    const int n = 2 * m;
+    double c0 = 0, c1 = 0;
+    for (int k = 0; k < m; k++) {
+        c0 += x[2 * k]; c1 += x[2 * k + 1];
+        Ax[2 * k] = c0; Ax[2 * k + 1] = c1;
+        Ax[n + 2 * k] = x[2 * k]; Ax[n + 2 * k + 1] = x[2 * k + 1];
+    }
+}
+
+static void mpc_ATy(int m, const double* y, double* ATy)
+{
+    const int n = 2 * m;
+    double c0 = 0, c1 = 0;
+    for (int k = m - 1; k >= 0; k--) {
+        c0 += y[2 * k]; c1 += y[2 * k + 1];
+        ATy[2 * k] = c0 + y[n + 2 * k];
+        ATy[2 * k + 1] = c1 + y[n + 2 * k + 1];
+    }
+}
+
+/* Cholesky of K = H + sigma I + rho A'A (A'A[2k+c][2k'+c] = m - max(k, k'), plus I) */
+static void mpc_factor(int m, const double* H, double sigma, double rho, double* Lc)
+{
+    const int n = 2 * m;
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            const int ki = i / 2, kj = j / 2;
+            double t = (i % 2 == j % 2) ? (double)(m - (ki > kj ? ki : kj)) : 0.0;
+            Lc[i * n + j] = H[i * n + j] + rho * (t + (i == j ? 1.0 : 0.0)) + (i == j ? sigma : 0.0);
+        }
+    for (int j = 0; j < n; j++) {
+        double d = Lc[j * n + j];
+        for (int k = 0; k < j; k++) d -= Lc[j * n + k] * Lc[j * n + k];
+        d = sqrt(d);
+        Lc[j * n + j] = d;
+        for (int i = j + 1; i < n; i++) {
+            double v = Lc[i * n + j];
+            for (int k = 0; k < j; k++) v -= Lc[i * n + k] * Lc[j * n + k];
+            Lc[i * n + j] = v / d;
+        }
+    }
+}
+
+static void mpc_solve(int n, const double* Lc, double* b)
+{
+    for (int i = 0; i < n; i++) {
+        double v = b[i];
+        for (int k = 0; k < i; k++) v -= Lc[i * n + k] * b[k];
+        b[i] = v / Lc[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; i--) {
+        double v = b[i];
+        for (int k = i + 1; k < n; k++) v -= Lc[k * n + i] * b[k];
+        b[i] = v / Lc[i * n + i];
+    }
+}
+
+static double inf_norm(const double* v, int n)
+{
+    double r = 0;
+    for (int i = 0; i < n; i++) r = fabs(v[i]) > r ? fabs(v[i]) : r;
+    return r;
+}
+
+/* The QP solve of mpc.py:196-203: min 1/2 x'Hx + g'x s.t. lo <= A x <= hi, by OSQP's ADMM
+ * (x~ from the reduced KKT system, relaxation alpha, projection onto [lo, hi], dual update,
+ * termination on the unscaled inf-norm residuals, rho adaptation by the residual ratio).  OSQP
+ * itself is not installed here: this restates its published algorithm without Ruiz scaling or
+ * polishing (parity with OSQP's bits is unpinned; the optimum is pinned by KKT checks).
+ * Returns 0 converged, 1 iteration limit.  *iters = iterations run, *rho_out = final rho. */
+int oracle_qp_admm(int m, const double* H, const double* g, const double* lo, const double* hi,
+                   const mpc_params_t* M, double* x, int* iters, double* rho_out)
+{
+    const int n = 2 * m, nc = 4 * m;
+    double Lc[256], z[32], y[32], rhs[16], w[32], xt[16], zt[32], Ax[32], ATy[16], Hx[16], r[32];
+    double rho = M->rho;
+    const double sigma = M->sigma, alpha = M->alpha;
+    for (int i = 0; i < n; i++) x[i] = 0;
+    for (int i = 0; i < nc; i++) z[i] = y[i] = 0;
+    mpc_factor(m, H, sigma, rho, Lc);
+    int status = 1, it;
+    for (it = 1; it <= M->max_iter; it++) {
+        const double rinv = 1.0 / rho;
+        for (int i = 0; i < nc; i++) w[i] = rho * z[i] - y[i];
+        mpc_ATy(m, w, rhs);
+        for (int i = 0; i < n; i++) rhs[i] = sigma * x[i] - g[i] + rhs[i];
+        mpc_solve(n, Lc, rhs);
+        for (int i = 0; i < n; i++) xt[i] = rhs[i];
+        mpc_Ax(m, xt, zt);
+        for (int i = 0; i < n; i++) x[i] = alpha * xt[i] + (1.0 - alpha) * x[i];
+        for (int i = 0; i < nc; i++) {
+            const double zr = alpha * zt[i] + (1.0 - alpha) * z[i];
+            const double zn = clampd(zr + rinv * y[i], lo[i], hi[i]);
+            y[i] = y[i] + rho * (zr - zn);
+            z[i] = zn;
+        }
+        const int check = (M->check_every > 0 && it % M->check_every == 0) || it == M->max_iter;
+        const int adapt = M->adaptive_every > 0 && it % M->adaptive_every == 0;
+        if (!check && !adapt) continue;
+        mpc_Ax(m, x, Ax);
+        mpc_ATy(m, y, ATy);
+        for (int i = 0; i < n; i++) {
+            double acc = 0;
+            for (int j = 0; j < n; j++) acc += H[i * n + j] * x[j];
+            Hx[i] = acc;
+        }
+        for (int i = 0; i < nc; i++) r[i] = Ax[i] - z[i];
+        const double prim = inf_norm(r, nc);
+        for (int i = 0; i < n; i++) rhs[i] = Hx[i] + g[i] + ATy[i];
+        const double dual = inf_norm(rhs, n);
+        const double nAx = inf_norm(Ax, nc), nz = inf_norm(z, nc);
+        const double nHx = inf_norm(Hx, n), nATy = inf_norm(ATy, n), ng = inf_norm(g, n);
+        const double pscale = nAx > nz ? nAx : nz;
+        double dscale = nHx > nATy ? nHx : nATy;
+        dscale = dscale > ng ? dscale : ng;
+        if (check && prim <= M->eps_abs + M->eps_rel * pscale && dual <= M->eps_abs + M->eps_rel * dscale) {
+            status = 0;
+            break;
+        }
+        if (adapt) {
+            const double pn = prim / (pscale + 1e-30), dn = dual / (dscale + 1e-30);
+            double rn = rho * sqrt(pn / (dn + 1e-30));
+            rn = clampd(rn, 1e-6, 1e6);
+            if (rn > rho * M->adaptive_tol || rn < rho / M->adaptive_tol) {
+                rho = rn;
+                mpc_factor(m, H, sigma, rho, Lc);
+            }
+        }
+    }
+    if (iters) *iters = it > M->max_iter ? M->max_iter : it;
+    if (rho_out) *rho_out = rho;
+    return status;
+}
+
+/* MPC.mpcControl (mpc.py:111-214): assemble, solve, u = du0 + u_p + u_r, regularise; returns the
+ * new u_p = u - u_r (before regularisation).  Returns the ADMM status; *iters as above. */
+int oracle_mpc_control(const double s[3], const double sd[3], const double ur[2], double up[2], double rv, double rw,
+                       const lp_params_t* Pr, const mpc_params_t* M, double u[2], int* iters)
+{
+    double H[256], g[16], lo[32], hi[32], x[16];
+    oracle_mpc_assemble(s, sd, ur, up, Pr, M, H, g, lo, hi);
+    const int st = oracle_qp_admm(M->m, H, g, lo, hi, M, x, iters, NULL);
+    const double uu0 = (x[0] + up[0]) + ur[0], uu1 = (x[1] + up[1]) + ur[1];
+    up[0] = uu0 - ur[0];
+    up[1] = uu1 - ur[1];
+    const double vi = clampd(uu0 - rv, Pr->min_v_inc, Pr->max_v_inc);
+    u[0] = clampd(rv + vi, Pr->min_v, Pr->max_v);
+    const double wi = clampd(uu1 - rw, Pr->min_w_inc, Pr->max_w_inc);
+    u[1] = clampd(rw + wi, Pr->min_w, Pr->max_w);
+    return st;
+}
+
+/* One LQR.plan (lqr.py:58-86) or MPC.plan (mpc.py:66-94) iteration: kind 0 = LQR, 1 = MPC.
+ * st[5] = (x, y, theta, v, w) updated in place; up[2] is MPC's carried u_p.  Returns 0 stepped,
+ * 1 goal reached (no step), 4 the reference raises (getLookaheadPoint). */
+int oracle_track_step(int kind, const double* path, int P, const double goal[3], double st[5], double up[2],
+                      const lp_params_t* Pr, const lqr_params_t* L, const mpc_params_t* M, double u[2], int* admm_iters)
+{
+    const double cur[3] = {st[0], st[1], st[2]};
+    if (admm_iters) *admm_iters = 0;
+    if (oracle_reach_goal(cur, goal, Pr)) return 1;
+    double pt[2], theta, kappa;
+    const double rob[3] = {st[0], st[1], st[3]};
+    if (oracle_lookahead(path, P, rob, Pr, pt, &theta, &kappa)) return 4;
+    const double dt = Pr->dt;
+    double e_theta = regularize_angle(st[2] - goal[2]);
+    /* angularRegularization(w_d) against the current w */
+#define ANGREG(wd) clampd(st[4] + clampd((wd) - st[4], Pr->min_w_inc, Pr->max_w_inc), Pr->min_w, Pr->max_w)
+    if (!(vnorm2(goal[0] - st[0], goal[1] - st[1]) > Pr->goal_dist_tol)) {
+        u[0] = 0.0;
+        u[1] = (fabs(e_theta) > Pr->rotate_tol) ? ANGREG(e_theta / dt) : 0.0;
+    } else {
+        e_theta = regularize_angle(atan2(pt[1] - st[1], pt[0] - st[0]) - st[2]);
+        if (fabs(e_theta) > Pr->rotate_tol) {
+            u[0] = 0.0;
+            u[1] = ANGREG(e_theta / dt);
+        } else {
+            const double s[3] = {st[0], st[1], st[2]}, sd[3] = {pt[0], pt[1], theta};
+            const double ur[2] = {st[3], st[3] * kappa};
+            if (kind == 0)
+                oracle_lqr_control(s, sd, ur, st[3], st[4], Pr, L, u);
+            else
+                oracle_mpc_control(s, sd, ur, up, st[3], st[4], Pr, M, u, admm_iters);
+        }
+    }
+#undef ANGREG
+    /* Robot.kinematic -> lookforward (agent.py:68-116) */
+    const double nx = st[0] + (dt * cos(st[2])) * u[0], ny = st[1] + (dt * sin(st[2])) * u[0];
+    const double nth = st[2] + dt * u[1];
+    st[0] = nx; st[1] = ny; st[2] = nth; st[3] = u[0]; st[4] = u[1];
+    return 0;
+}
+
+/* OpenMP over agents: `iters` plan iterations each (stops at the first non-zero status).
+ * Returns the number of agent-steps taken. */
+int64_t oracle_track_batch(int kind, const double* path_xy, const int32_t* path_off, const double* goals, double* st,
+                           double* up, int na, int iters, const lp_params_t* Pr, const lqr_params_t* L,
+                           const mpc_params_t* M, double* u, int32_t* status, int32_t* n_steps, int nthreads)
+{
+    int64_t total = 0;
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) reduction(+ : total)
+    for (int a = 0; a < na; a++) {
+        int rc = 0, k;
+        for (k = 0; k < iters; k++) {
+            rc = oracle_track_step(kind, path_xy + 2 * (int64_t)path_off[a], path_off[a + 1] - path_off[a], goals + 3 * a,
+                                   st + 5 * a, up + 2 * a, Pr, L, M, u + 2 * a, NULL);
+            if (rc) break;
+        }
+        status[a] = rc;
+        n_steps[a] = k;
+        total += k;
+    }
+    return total;
 }
 
 /* OpenMP over agents: one DWA.plan iteration for each (CPU baseline of bench.py's control leg).

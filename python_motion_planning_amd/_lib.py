@@ -28,6 +28,11 @@ SIGNATURES = {
                                _vp, _vp]),
     "pmp_dwa_step_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp,
                                 _vp, _vp, _vp, _vp]),
+    "pmp_lqr_control_batch": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
+    "pmp_mpc_control_batch": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   _vp]),
+    "pmp_track_step_batch": (_i, [_vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp,
+                                  _vp]),
 }
 
 
@@ -50,6 +55,44 @@ class DWAParams(ctypes.Structure):
                 ("velocity_weight", ctypes.c_double), ("predict_time", ctypes.c_double),
                 ("inflation", ctypes.c_double), ("v_resolution", ctypes.c_double),
                 ("w_resolution", ctypes.c_double), ("nv", ctypes.c_int32), ("nw", ctypes.c_int32)]
+
+class LQRParams(ctypes.Structure):
+    """pmp_lqr_params == LQR's Q, R, lqr_iteration, eps_iter (local_planner/lqr.py:35-38)."""
+    _fields_ = [("q", ctypes.c_double * 3), ("r", ctypes.c_double * 2), ("iters", ctypes.c_int32),
+                ("eps", ctypes.c_double)]
+
+    @classmethod
+    def make(cls, q=(1.0, 1.0, 1.0), r=(1.0, 1.0), iters: int = 100, eps: float = 0.1):
+        return cls((ctypes.c_double * 3)(*[float(v) for v in q]), (ctypes.c_double * 2)(*[float(v) for v in r]),
+                   int(iters), float(eps))
+
+
+# ADMM settings of the MPC QP solve.  OSQP's defaults (OSQP is what mpc.py:196-203 calls) stop at
+# eps 1e-3; the drop-in solves to 1e-9 by default so results do not depend on solver internals.
+OSQP_DEFAULTS = dict(rho=0.1, sigma=1e-6, alpha=1.6, eps_abs=1e-3, eps_rel=1e-3, adaptive_tol=5.0, max_iter=4000,
+                     check_every=25, adaptive_every=25)
+ADMM_DEFAULTS = dict(OSQP_DEFAULTS, eps_abs=1e-9, eps_rel=1e-9)
+
+
+class MPCParams(ctypes.Structure):
+    """pmp_mpc_params == MPC's p, m, Q, R (local_planner/mpc.py:37-40) + the ADMM settings."""
+    _fields_ = [("p", ctypes.c_int32), ("m", ctypes.c_int32), ("q", ctypes.c_double * 3), ("r", ctypes.c_double * 2),
+                ("rho", ctypes.c_double), ("sigma", ctypes.c_double), ("alpha", ctypes.c_double),
+                ("eps_abs", ctypes.c_double), ("eps_rel", ctypes.c_double), ("adaptive_tol", ctypes.c_double),
+                ("max_iter", ctypes.c_int32), ("check_every", ctypes.c_int32), ("adaptive_every", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+    @classmethod
+    def make(cls, p: int = 12, m: int = 8, q=(0.8, 0.8, 0.5), r=(2.0, 2.0), **admm):
+        a = dict(ADMM_DEFAULTS)
+        a.update(admm)
+        return cls(int(p), int(m), (ctypes.c_double * 3)(*[float(v) for v in q]),
+                   (ctypes.c_double * 2)(*[float(v) for v in r]), a["rho"], a["sigma"], a["alpha"], a["eps_abs"],
+                   a["eps_rel"], a["adaptive_tol"], int(a["max_iter"]), int(a["check_every"]),
+                   int(a["adaptive_every"]), 0)
+
+
+TRACK_LQR, TRACK_MPC = 0, 1
 
 STATUS_FOUND, STATUS_NO_PATH, STATUS_PATH_OVERFLOW, STATUS_CAP_OVERFLOW, STATUS_REF_RAISES = range(5)
 

@@ -132,6 +132,82 @@ def dwa_step_batch(grid, lp_params, dwa_params, state, goal, path_xy, path_off, 
     return out
 
 
+def lqr_control_batch(lp_params, lqr_params, s, s_d, u_r, robot_vw, stream=None):
+    """Batched LQR.lqrControl (lqr.py:103-145).  s, s_d [n,3], u_r [n,2], robot_vw [n,2] (the
+    robot's current v, w).  Returns u [n,2] (device tensor)."""
+    torch = _lib.device_check()
+    L = _lib.load_library()
+    ctx = _lib.context()
+    s = _dev(torch, s, torch.float64).reshape(-1, 3)
+    n = int(s.shape[0])
+    s_d = _dev(torch, s_d, torch.float64).reshape(-1, 3)
+    u_r = _dev(torch, u_r, torch.float64).reshape(-1, 2)
+    vw = _dev(torch, robot_vw, torch.float64).reshape(-1, 2)
+    u = torch.empty((n, 2), dtype=torch.float64, device="cuda")
+    rc = L.pmp_lqr_control_batch(ctx, stream if stream is not None else _lib.stream_ptr(), ctypes.byref(lp_params),
+                                 ctypes.byref(lqr_params), n, s.data_ptr(), s_d.data_ptr(), u_r.data_ptr(),
+                                 vw.data_ptr(), u.data_ptr())
+    _lib.check(ctx, rc, "pmp_lqr_control_batch")
+    return u
+
+
+def mpc_control_batch(lp_params, mpc_params, s, s_d, u_r, u_p, robot_vw, want_qp: bool = False, stream=None):
+    """Batched MPC.mpcControl (mpc.py:111-214).  u_p [n,2] device tensor updated in place (the new
+    u_p the reference returns).  Returns dict: u [n,2], iters, status, and with want_qp the assembled
+    QP (H [n,2m,2m], g [n,2m], lu [n,2,4m]) and its solution du [n,2m]."""
+    torch = _lib.device_check()
+    L = _lib.load_library()
+    ctx = _lib.context()
+    s = _dev(torch, s, torch.float64).reshape(-1, 3)
+    n = int(s.shape[0])
+    nv = 2 * int(mpc_params.m)
+    s_d = _dev(torch, s_d, torch.float64).reshape(-1, 3)
+    u_r = _dev(torch, u_r, torch.float64).reshape(-1, 2)
+    vw = _dev(torch, robot_vw, torch.float64).reshape(-1, 2)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    out = dict(u=torch.empty((n, 2), **f64), iters=torch.empty(n, dtype=torch.int32, device="cuda"),
+               status=torch.empty(n, dtype=torch.int32, device="cuda"))
+    out.update(H=torch.zeros((n, nv, nv), **f64), g=torch.zeros((n, nv), **f64), lu=torch.zeros((n, 2, 2 * nv), **f64),
+               du=torch.zeros((n, nv), **f64)) if want_qp else out.update(H=None, g=None, lu=None, du=None)
+    rc = L.pmp_mpc_control_batch(ctx, stream if stream is not None else _lib.stream_ptr(), ctypes.byref(lp_params),
+                                 ctypes.byref(mpc_params), n, s.data_ptr(), s_d.data_ptr(), u_r.data_ptr(),
+                                 u_p.data_ptr(), vw.data_ptr(), out["u"].data_ptr(), _lib.ptr(out["H"]),
+                                 _lib.ptr(out["g"]), _lib.ptr(out["lu"]), _lib.ptr(out["du"]), out["iters"].data_ptr(),
+                                 out["status"].data_ptr())
+    _lib.check(ctx, rc, "pmp_mpc_control_batch")
+    return out
+
+
+def track_step_batch(kind: str, lp_params, state, goal, path_xy, path_off, iters: int = 1, lqr_params=None,
+                     mpc_params=None, u_p=None, want_hist: bool = False, stream=None):
+    """Batched LQR.plan / MPC.plan iterations (lqr.py:58-86, mpc.py:66-94), kind "lqr" or "mpc".
+    state [na,5] f64 device tensor (updated in place); u_p [na,2] device tensor (MPC, in place).
+    Returns dict of device tensors (u, status, n_steps, admm_iters, optional hist_pose)."""
+    torch = _lib.device_check()
+    L = _lib.load_library()
+    ctx = _lib.context()
+    k = {"lqr": _lib.TRACK_LQR, "mpc": _lib.TRACK_MPC}[kind]
+    na = int(state.shape[0])
+    goal = _dev(torch, goal, torch.float64).reshape(-1, 3)
+    path_xy = _dev(torch, path_xy, torch.float64).reshape(-1, 2)
+    path_off = _dev(torch, path_off, torch.int32)
+    if k == _lib.TRACK_MPC and u_p is None:
+        raise ValueError("MPC needs the carried u_p tensor [na, 2]")
+    out = dict(u=torch.empty((na, 2), dtype=torch.float64, device="cuda"),
+               status=torch.empty(na, dtype=torch.int32, device="cuda"),
+               n_steps=torch.empty(na, dtype=torch.int32, device="cuda"),
+               admm_iters=torch.empty(na, dtype=torch.int32, device="cuda"))
+    out["hist_pose"] = torch.zeros((na, iters, 3), dtype=torch.float64, device="cuda") if want_hist else None
+    rc = L.pmp_track_step_batch(ctx, stream if stream is not None else _lib.stream_ptr(), k, ctypes.byref(lp_params),
+                                ctypes.byref(lqr_params) if lqr_params is not None else None,
+                                ctypes.byref(mpc_params) if mpc_params is not None else None, na, state.data_ptr(),
+                                _lib.ptr(u_p), goal.data_ptr(), path_xy.data_ptr(), path_off.data_ptr(), int(iters),
+                                out["u"].data_ptr(), out["status"].data_ptr(), out["n_steps"].data_ptr(),
+                                _lib.ptr(out["hist_pose"]), out["admm_iters"].data_ptr())
+    _lib.check(ctx, rc, "pmp_track_step_batch")
+    return out
+
+
 def astar3d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: int | None = None,
                   expand_cap: int = 0, counters: bool = False):
     """Batched AStar3D.plan (a_star3d.py:33-106).

@@ -170,3 +170,120 @@ class DWA(LocalPlanner):
 
     def run(self):
         return self.plan()
+
+
+class _Tracker(LocalPlanner):
+    """Shared plan loop of LQR / MPC (lqr.py:58-86, mpc.py:66-94) on the gfx950 kernel track.hip."""
+
+    KIND = "lqr"
+
+    def __init__(self, start: tuple, goal: tuple, env: Env, heuristic_type: str = "euclidean", **params) -> None:
+        super().__init__(start, goal, env, heuristic_type, **params)
+        self.g_planner = {"planner_name": "a_star", "start": (start[0], start[1]), "goal": (goal[0], goal[1]),
+                          "env": env}
+        self.path = self.g_path[::-1]
+        self._u_p = (0.0, 0.0)
+
+    def _kernel_params(self):
+        return {}
+
+    def _run(self, iters: int):
+        torch = _lib.device_check()
+        r = self.robot
+        state = torch.tensor([[r.px, r.py, r.theta, r.v, r.w]], dtype=torch.float64, device="cuda")
+        u_p = torch.tensor([self._u_p], dtype=torch.float64, device="cuda")
+        xy, off = batch.pack_paths([np.asarray(self.path, np.float64)])
+        out = batch.track_step_batch(self.KIND, self._lp_params(), state, np.array([self.goal], np.float64), xy, off,
+                                     iters=iters, u_p=u_p, want_hist=True, **self._kernel_params())
+        n = int(out["n_steps"][0])
+        st = int(out["status"][0])
+        for p in out["hist_pose"][0, :n].cpu().numpy():
+            r.history_pose.append((float(p[0]), float(p[1]), float(p[2])))
+        r.px, r.py, r.theta, r.v, r.w = (float(v) for v in state[0].cpu().numpy())
+        self._u_p = tuple(float(v) for v in u_p[0].cpu().numpy())
+        return st
+
+    def step(self):
+        """One iteration of the plan loop.  Returns 'reached' or 'stepped'; raises where the reference does."""
+        st = self._run(1)
+        if st == _lib.STATUS_REF_RAISES:
+            raise IndexError("getLookaheadPoint failed (reference raises)")
+        return "reached" if st == 1 else "stepped"
+
+    def plan(self):
+        """(True, history_pose) or (False, None)."""
+        self._u_p = (0.0, 0.0)  # mpc.py:64 starts every plan() from u_p = (0, 0)
+        st = self._run(int(self.params["MAX_ITERATION"]))
+        if st == 1:
+            return True, self.robot.history_pose
+        if st == _lib.STATUS_REF_RAISES:
+            raise IndexError("getLookaheadPoint failed (reference raises)")
+        return False, None
+
+    def run(self):
+        return self.plan()
+
+
+class LQR(_Tracker):
+    """Linear Quadratic Regulator (local_planner/lqr.py:12-145)."""
+
+    KIND = "lqr"
+
+    def __init__(self, start: tuple, goal: tuple, env: Env, heuristic_type: str = "euclidean", **params) -> None:
+        self.Q = np.diag([1, 1, 1])
+        self.R = np.diag([1, 1])
+        self.lqr_iteration = 100
+        self.eps_iter = 1e-1
+        super().__init__(start, goal, env, heuristic_type, **params)
+
+    def __str__(self) -> str:
+        return "Linear Quadratic Regulator (LQR)"
+
+    def _lqr_params(self):
+        return _lib.LQRParams.make(np.diag(self.Q), np.diag(self.R), self.lqr_iteration, self.eps_iter)
+
+    def _kernel_params(self):
+        return dict(lqr_params=self._lqr_params())
+
+    def lqrControl(self, s: tuple, s_d: tuple, u_r: tuple) -> np.ndarray:
+        """lqr.py:103-145 on the device; returns [[v], [w]]."""
+        u = batch.lqr_control_batch(self._lp_params(), self._lqr_params(), [s], [s_d], [u_r],
+                                    [(self.robot.v, self.robot.w)])
+        return u.cpu().numpy().reshape(2, 1)
+
+
+class MPC(_Tracker):
+    """Model Predictive Control (local_planner/mpc.py:14-214).  The OSQP solve of mpc.py:196-203 is
+    the device ADMM of track.hip (settings in self.admm; OSQP itself is not available)."""
+
+    KIND = "mpc"
+
+    def __init__(self, start: tuple, goal: tuple, env: Env, heuristic_type: str = "euclidean", **params) -> None:
+        self.p = 12
+        self.m = 8
+        self.Q = np.diag([0.8, 0.8, 0.5])
+        self.R = np.diag([2, 2])
+        self.admm = dict(_lib.ADMM_DEFAULTS)
+        super().__init__(start, goal, env, heuristic_type, **params)
+        self.u_min = np.array([[self.params["MIN_V"]], [self.params["MIN_W"]]])
+        self.u_max = np.array([[self.params["MAX_V"]], [self.params["MAX_W"]]])
+        self.du_min = np.array([[self.params["MIN_V_INC"]], [self.params["MIN_W_INC"]]])
+        self.du_max = np.array([[self.params["MAX_V_INC"]], [self.params["MAX_W_INC"]]])
+
+    def __str__(self) -> str:
+        return "Model Predicted Control (MPC)"
+
+    def _mpc_params(self):
+        return _lib.MPCParams.make(self.p, self.m, np.diag(self.Q), np.diag(self.R), **self.admm)
+
+    def _kernel_params(self):
+        return dict(mpc_params=self._mpc_params())
+
+    def mpcControl(self, s: tuple, s_d: tuple, u_r: tuple, u_p: tuple):
+        """mpc.py:111-214 on the device: returns ([[v], [w]], new u_p)."""
+        torch = _lib.device_check()
+        up = torch.tensor([u_p], dtype=torch.float64, device="cuda")
+        out = batch.mpc_control_batch(self._lp_params(), self._mpc_params(), [s], [s_d], [u_r], up,
+                                      [(self.robot.v, self.robot.w)])
+        u = out["u"].cpu().numpy().reshape(2, 1)
+        return u, tuple(float(v) for v in up[0].cpu().numpy())

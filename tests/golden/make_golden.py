@@ -400,7 +400,61 @@ def sec_lqr():
     print("lqr", U[:3])
 
 
-SECTIONS = dict(dwa=sec_dwa, local_plans=sec_local_plans, lqr=sec_lqr, astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
+class _RecordingOSQP:
+    """Stand-in for the absent `osqp` module: records the QP that MPC.mpcControl (mpc.py:196-203)
+    hands to OSQP and returns a zero step.  Only the QP ASSEMBLY is pinned by these vectors; the
+    OSQP solve itself is parity-unpinned (OSQP is not installed in this image)."""
+    last = None
+
+    def setup(self, P, q, A, l, u, **kw):
+        _RecordingOSQP.last = dict(P=P.toarray(), q=np.asarray(q, np.float64).ravel(), A=A.toarray(),
+                                   l=np.asarray(l, np.float64).ravel(), u=np.asarray(u, np.float64).ravel())
+
+    def solve(self):
+        class R:
+            pass
+        r = R()
+        r.x = np.zeros(_RecordingOSQP.last["P"].shape[0])
+        return r
+
+
+def sec_mpc():
+    pmp = import_reference()
+    import python_motion_planning.local_planner.mpc as mpcmod
+
+    mpcmod.osqp = types.SimpleNamespace(OSQP=_RecordingOSQP)
+    env = readme_env(pmp)
+    p = pmp.MPC((5, 5, 0), (45, 25, 0), env)
+    rng = np.random.default_rng(99)
+    out = {}
+    for horizon in (12, 30):
+        p.p = horizon
+        n = 100
+        S = np.column_stack([rng.uniform(0, 50, n), rng.uniform(0, 30, n), rng.uniform(-np.pi, np.pi, n)])
+        SD = S + np.column_stack([rng.normal(0, 1, n), rng.normal(0, 1, n), rng.normal(0, 0.5, n)])
+        UR = np.column_stack([rng.uniform(0, 0.5, n), rng.uniform(-1, 1, n)])
+        UP = np.column_stack([rng.uniform(-0.2, 0.2, n), rng.uniform(-0.5, 0.5, n)])
+        Ps, qs, As, ls, us = [], [], [], [], []
+        for i in range(n):
+            p.robot.v, p.robot.w = 0.2, 0.1
+            p.mpcControl(tuple(S[i]), tuple(SD[i]), tuple(UR[i]), tuple(UP[i]))
+            rec = _RecordingOSQP.last
+            Ps.append(rec["P"]); qs.append(rec["q"]); As.append(rec["A"]); ls.append(rec["l"]); us.append(rec["u"])
+        out[f"p{horizon}_s"] = S
+        out[f"p{horizon}_s_d"] = SD
+        out[f"p{horizon}_u_r"] = UR
+        out[f"p{horizon}_u_p"] = UP
+        out[f"p{horizon}_P"] = np.array(Ps)
+        out[f"p{horizon}_q"] = np.array(qs)
+        out[f"p{horizon}_A"] = np.array(As[0])
+        out[f"p{horizon}_l"] = np.array(ls)
+        out[f"p{horizon}_u"] = np.array(us)
+    close_figs()
+    np.savez_compressed(os.path.join(HERE, "mpc_qp.npz"), **out)
+    print("mpc qp", out["p12_P"].shape, out["p30_P"].shape)
+
+
+SECTIONS = dict(mpc=sec_mpc, dwa=sec_dwa, local_plans=sec_local_plans, lqr=sec_lqr, astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
                 dstar=sec_dstar, astar3d=sec_astar3d)
 
 if __name__ == "__main__":

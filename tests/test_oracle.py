@@ -6,7 +6,7 @@ import math
 import numpy as np
 import pytest
 
-from golden_io import grid_cases, load_json, load_npz, seg
+from golden_io import grid_cases, kkt_certificate, load_json, load_npz, seg
 from oracle import oracle as O
 
 
@@ -193,3 +193,66 @@ def test_lqr_control_against_reference():
     for i in range(len(z["s"])):
         u = O.lqr_control(z["s"][i], z["s_d"][i], z["u_r"][i], z["v"][i], z["w"][i])
         np.testing.assert_allclose(u, z["u"][i], rtol=1e-9, atol=1e-12)
+
+
+def test_lqr_plans_against_reference():
+    """Full LQR.plan runs on the README grid (lqr.py:58-86): the oracle's plan iteration
+    reproduces the reference's whole history of poses."""
+    z = load_npz("local_plans.npz")
+    ran = 0
+    for c in range(4):
+        if str(z[f"c{c}_kind"]) != "lqr" or not bool(z[f"c{c}_ok"]):
+            continue
+        st = np.zeros(5)
+        st[:3] = z[f"c{c}_start"]
+        poses = []
+        for it in range(1500):
+            rc, nst, _, u, _ = O.track_step("lqr", z[f"c{c}_path"], z[f"c{c}_goal"], st)
+            if rc == 1:
+                break
+            assert rc == 0
+            poses.append(st[:3].copy())
+            st = nst
+        ref = z[f"c{c}_poses"]
+        assert len(poses) == len(ref)
+        np.testing.assert_allclose(np.array(poses), ref, rtol=1e-9, atol=1e-9)
+        ran += 1
+    assert ran == 2
+
+
+def test_mpc_qp_assembly_against_reference():
+    """MPC.mpcControl's QP (mpc.py:124-200) as handed to OSQP, captured from the reference with a
+    recording stand-in for the absent osqp module: H, g, A, l, u for p = 12 (reference) and 30."""
+    z = load_npz("mpc_qp.npz")
+    for P in (12, 30):
+        mp = O.MPCParams.default(p=P)
+        A = z[f"p{P}_A"]
+        # the constraint matrix is [kron(tril(1_m), I2); I_2m]
+        assert np.array_equal(A, np.vstack([np.kron(np.tril(np.ones((8, 8))), np.eye(2)), np.eye(16)]))
+        for i in range(len(z[f"p{P}_s"])):
+            H, g, lo, hi = O.mpc_assemble(z[f"p{P}_s"][i], z[f"p{P}_s_d"][i], z[f"p{P}_u_r"][i], z[f"p{P}_u_p"][i],
+                                          mpc=mp)
+            Hr = z[f"p{P}_P"][i]
+            np.testing.assert_allclose(H, Hr, rtol=0, atol=1e-13 * np.abs(Hr).max())
+            gr = z[f"p{P}_q"][i]
+            np.testing.assert_allclose(g, gr, rtol=0, atol=1e-13 * max(np.abs(gr).max(), 1e-300))
+            assert np.array_equal(lo, z[f"p{P}_l"][i]) and np.array_equal(hi, z[f"p{P}_u"][i])
+
+
+def test_mpc_admm_reaches_certified_optimum():
+    """The ADMM restatement of the OSQP solve (parity with OSQP's bits is unpinned: OSQP is not
+    installed) converges on every captured reference QP to the KKT-certified optimum."""
+    z = load_npz("mpc_qp.npz")
+    for P in (12, 30):
+        A = z[f"p{P}_A"]
+        for i in range(len(z[f"p{P}_s"])):
+            H, g, lo, hi = z[f"p{P}_P"][i], z[f"p{P}_q"][i], z[f"p{P}_l"][i], z[f"p{P}_u"][i]
+            x, st, it, _ = O.qp_admm(H, g, lo, hi, O.MPCParams.default(p=P, eps_abs=1e-12, eps_rel=1e-12,
+                                                                       max_iter=100000))
+            assert st == 0
+            xs = kkt_certificate(H, g, A, lo, hi, x)
+            assert xs is not None
+            np.testing.assert_allclose(x, xs, rtol=0, atol=1e-9)
+            # OSQP's default tolerance (1e-3) lands near the same optimum
+            xd, std, _, _ = O.qp_admm(H, g, lo, hi, O.MPCParams.default(p=P))
+            assert std == 0 and np.abs(xd - xs).max() < 2e-2
