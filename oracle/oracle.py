@@ -412,3 +412,74 @@ def dwa_step_batch(obstacles, path_xy, path_off, goals, states, params=None, nv=
                             weights[0], weights[1], weights[2], inflation, _p(u, _dp), _p(status, _i32p),
                             int(nthreads))
     return st, u, status
+
+
+# ------------------------------------------------------------------------------------------------
+# sample search (RRT / RRT*)
+def _rrt_bind():
+    L = lib()
+    if not getattr(L, "_rrt_bound", False):
+        L.oracle_rrt.restype = ctypes.c_int
+        L.oracle_rrt.argtypes = [ctypes.c_int, _dp, ctypes.c_int, _dp, ctypes.c_int, _dp, ctypes.c_int,
+                                 ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                 ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                 ctypes.c_double, _dp, ctypes.c_int64, _dp, ctypes.c_int, _i32p, _i64p]
+        L.oracle_rrt_batch.restype = ctypes.c_int
+        L.oracle_rrt_batch.argtypes = [ctypes.c_int, _dp, ctypes.c_int, _dp, ctypes.c_int, _dp, ctypes.c_int,
+                                       ctypes.c_double, ctypes.c_double, ctypes.c_double, _dp, _dp, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double, _dp,
+                                       ctypes.c_int64, _dp, ctypes.c_int, _i32p, _i32p, ctypes.c_int]
+        L.oracle_map_collision.restype = ctypes.c_int
+        L.oracle_map_collision.argtypes = [_dp, ctypes.c_int, _dp, ctypes.c_int, _dp, ctypes.c_int, ctypes.c_double,
+                                           ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double]
+        L._rrt_bound = True
+    return L
+
+
+def _map_arrays(rects, circs, X, Y, boundary=None):
+    if boundary is None:
+        boundary = [[0, 0, 1, Y], [0, Y, X, 1], [1, 0, X, 1], [X, 1, 1, Y]]
+    r = _d(np.asarray(rects, np.float64).reshape(-1, 4))
+    c = _d(np.asarray(circs, np.float64).reshape(-1, 3))
+    b = _d(np.asarray(boundary, np.float64).reshape(-1, 4))
+    return r, c, b
+
+
+def map_collision(rects, circs, X, Y, p1, p2, delta=0.5):
+    r, c, b = _map_arrays(rects, circs, X, Y)
+    return bool(_rrt_bind().oracle_map_collision(_p(r, _dp), len(r), _p(c, _dp), len(c), _p(b, _dp), len(b), delta,
+                                                 p1[0], p1[1], p2[0], p2[1]))
+
+
+def rrt(star, rects, circs, X, Y, start, goal, rnd, sample_num=10000, max_dist=0.5, radius=10.0, goal_rate=0.05,
+        delta=0.5, cap=None):
+    """RRT / RRT* plan (rrt.py:49-83, rrt_star.py:43-76) on a Map, consuming the double stream
+    `rnd` -> dict(status, tree [n,4] (x, y, g, parent), draws)."""
+    r, c, b = _map_arrays(rects, circs, X, Y)
+    rnd = _d(rnd)
+    cap = cap or sample_num + 2
+    tree = np.zeros((cap, 4))
+    nn = ctypes.c_int32(0)
+    dr = ctypes.c_int64(0)
+    st = _rrt_bind().oracle_rrt(int(bool(star)), _p(r, _dp), len(r), _p(c, _dp), len(c), _p(b, _dp), len(b), delta,
+                                X, Y, start[0], start[1], goal[0], goal[1], sample_num, max_dist, radius, goal_rate,
+                                _p(rnd, _dp), len(rnd), _p(tree, _dp), cap, ctypes.byref(nn), ctypes.byref(dr))
+    return dict(status=st, tree=tree[: nn.value].copy(), draws=dr.value)
+
+
+def rrt_batch(star, rects, circs, X, Y, starts, goals, rnd, sample_num, max_dist=0.5, radius=10.0, goal_rate=0.05,
+              delta=0.5, cap=None, nthreads=0):
+    """Independent RRT(*) queries with OpenMP; rnd [nq, stride] streams."""
+    r, c, b = _map_arrays(rects, circs, X, Y)
+    rnd = _d(rnd)
+    nq, stride = rnd.shape
+    cap = cap or sample_num + 2
+    tree = np.zeros((nq, cap, 4))
+    nn = np.zeros(nq, np.int32)
+    st = np.zeros(nq, np.int32)
+    s = _d(np.asarray(starts, np.float64).reshape(-1, 2))
+    g = _d(np.asarray(goals, np.float64).reshape(-1, 2))
+    _rrt_bind().oracle_rrt_batch(int(bool(star)), _p(r, _dp), len(r), _p(c, _dp), len(c), _p(b, _dp), len(b), delta,
+                                 X, Y, _p(s, _dp), _p(g, _dp), nq, sample_num, max_dist, radius, goal_rate,
+                                 _p(rnd, _dp), stride, _p(tree, _dp), cap, _p(nn, _i32p), _p(st, _i32p), nthreads)
+    return dict(status=st, n_nodes=nn, tree=tree)

@@ -1284,3 +1284,201 @@ int oracle_dwa_step_batch(const double* obs, int nobs, const double* path_xy, co
     }
     return stepped;
 }
+
+/* ==================================================================================== */
+/* Sample search: RRT / RRT* over a Map (global_planner/sample_search/)                  */
+/* ==================================================================================== */
+
+/* Map obstacles: rects [nr][4] (ox, oy, w, h), circles [nc][3] (ox, oy, r), boundary [nb][4]
+ * (utils/environment/env.py:83-117), inflation delta (sample_search.py:22-25). */
+typedef struct {
+    const double *rect, *circ, *bnd;
+    int nr, nc, nb;
+    double delta;
+} map_t;
+
+/* SampleSearcher.isInsideObs (sample_search.py:51-77) */
+static int map_inside(const map_t* M, double x, double y)
+{
+    const double d = M->delta;
+    for (int i = 0; i < M->nc; i++) {
+        const double* c = M->circ + 3 * i;
+        if (vnorm2(x - c[0], y - c[1]) <= c[2] + d) return 1;
+    }
+    for (int i = 0; i < M->nr; i++) {
+        const double* r = M->rect + 4 * i;
+        const double px = x - (r[0] - d), py = y - (r[1] - d);
+        if (0 <= px && px <= r[2] + 2 * d && 0 <= py && py <= r[3] + 2 * d) return 1;
+    }
+    for (int i = 0; i < M->nb; i++) {
+        const double* r = M->bnd + 4 * i;
+        const double px = x - (r[0] - d), py = y - (r[1] - d);
+        if (0 <= px && px <= r[2] + 2 * d && 0 <= py && py <= r[3] + 2 * d) return 1;
+    }
+    return 0;
+}
+
+static double cross3(double p1x, double p1y, double p2x, double p2y, double p3x, double p3y)
+{
+    const double x1 = p2x - p1x, y1 = p2y - p1y, x2 = p3x - p1x, y2 = p3y - p1y;
+    return x1 * y2 - x2 * y1;
+}
+
+/* SampleSearcher.isInterRect (sample_search.py:79-109): all 6 vertex pairs of the inflated rect
+ * (itertools.combinations order), bbox "rapid repulsion" then the straddle test. */
+static int map_inter_rect(const double* r, double d, double x1, double y1, double x2, double y2)
+{
+    const double vx[4] = {r[0] - d, r[0] + r[2] + d, r[0] + r[2] + d, r[0] - d};
+    const double vy[4] = {r[1] - d, r[1] - d, r[1] + r[3] + d, r[1] + r[3] + d};
+    for (int a = 0; a < 4; a++)
+        for (int b = a + 1; b < 4; b++) {
+            if (fmax(x1, x2) >= fmin(vx[a], vx[b]) && fmin(x1, x2) <= fmax(vx[a], vx[b]) &&
+                fmax(y1, y2) >= fmin(vy[a], vy[b]) && fmin(y1, y2) <= fmax(vy[a], vy[b])) {
+                if (cross3(vx[a], vy[a], vx[b], vy[b], x1, y1) * cross3(vx[a], vy[a], vx[b], vy[b], x2, y2) <= 0 &&
+                    cross3(x1, y1, x2, y2, vx[a], vy[a]) * cross3(x1, y1, x2, y2, vx[b], vy[b]) <= 0)
+                    return 1;
+            }
+        }
+    return 0;
+}
+
+/* SampleSearcher.isInterCircle (sample_search.py:111-135).  np.dot of two 2-vectors is OpenBLAS
+ * ddot, whose scalar tail accumulates with FMA: dot = fma(a1, b1, a0 * b0). */
+static int map_inter_circle(const double* c, double d, double x, double y, double x2, double y2)
+{
+    const double dx = x2 - x, dy = y2 - y;
+    const double d2 = fma(dy, dy, dx * dx);
+    if (d2 == 0) return 0;
+    const double t = fma(c[1] - y, dy, (c[0] - x) * dx) / d2;
+    if (0 <= t && t <= 1) {
+        const double sx = x + t * dx, sy = y + t * dy;
+        if (vnorm2(c[0] - sx, c[1] - sy) <= c[2] + d) return 1;
+    }
+    return 0;
+}
+
+/* SampleSearcher.isCollision(node1, node2) (sample_search.py:27-49); argument order matters */
+static int map_collision(const map_t* M, double x1, double y1, double x2, double y2)
+{
+    if (map_inside(M, x1, y1) || map_inside(M, x2, y2)) return 1;
+    for (int i = 0; i < M->nr; i++)
+        if (map_inter_rect(M->rect + 4 * i, M->delta, x1, y1, x2, y2)) return 1;
+    for (int i = 0; i < M->nc; i++)
+        if (map_inter_circle(M->circ + 3 * i, M->delta, x1, y1, x2, y2)) return 1;
+    return 0;
+}
+
+int oracle_map_collision(const double* rect, int nr, const double* circ, int nc, const double* bnd, int nb,
+                         double delta, double x1, double y1, double x2, double y2)
+{
+    const map_t M = {rect, circ, bnd, nr, nc, nb, delta};
+    return map_collision(&M, x1, y1, x2, y2);
+}
+
+/* RRT.plan (rrt.py:49-83) with RRT.getNearest (rrt.py:105-130) or RRTStar.getNearest
+ * (rrt_star.py:43-76).  rnd: the np.random double stream (RandomState.random_sample order) that
+ * generateRandomNode (rrt.py:91-103) consumes: one draw, then two uniforms when it exceeds
+ * goal_rate.  The sample_list dict is the tree array in insertion order; a node whose
+ * coordinates already exist replaces that entry in place (dict semantics).
+ * tree [cap][4] = x, y, g, parent index (the start is its own parent, node.py:33).  Returns 0 found, 1 not found,
+ * 3 capacity / random-stream overflow.  *n_nodes includes the goal when found; *draws = doubles
+ * consumed. */
+int oracle_rrt(int star, const double* rect, int nr, const double* circ, int nc, const double* bnd, int nb,
+               double delta, double X, double Y, double sx, double sy, double gx, double gy, int sample_num,
+               double max_dist, double radius, double goal_rate, const double* rnd, int64_t nrnd, double* tree,
+               int cap, int* n_nodes, int64_t* draws)
+{
+    const map_t M = {rect, circ, bnd, nr, nc, nb, delta};
+    const double lox = delta, rgx = (X - delta) - delta, loy = delta, rgy = (Y - delta) - delta;
+    int n = 1, status = 1;
+    int64_t cur = 0;
+    tree[0] = sx; tree[1] = sy; tree[2] = 0.0; tree[3] = 0;  /* start.parent = start.current */
+    for (int it = 0; it < sample_num; it++) {
+        if (cur + 3 > nrnd) { status = 3; break; }
+        double rx = gx, ry = gy;
+        if (rnd[cur++] > goal_rate) {
+            rx = lox + rgx * rnd[cur++];
+            ry = loy + rgy * rnd[cur++];
+        }
+        int dup = 0, bi = 0;
+        double best = INFINITY;
+        for (int j = 0; j < n; j++) {
+            const double* t = tree + 4 * j;
+            if (t[0] == rx && t[1] == ry) dup = 1;
+            const double d = vnorm2(rx - t[0], ry - t[1]);
+            if (d < best) { best = d; bi = j; }
+        }
+        if (dup) continue;
+        const double* near = tree + 4 * bi;
+        double dist = vnorm2(rx - near[0], ry - near[1]);
+        const double theta = atan2(ry - near[1], rx - near[0]);
+        if (max_dist < dist) dist = max_dist;  /* min(self.max_dist, dist) */
+        const double nx = near[0] + dist * cos(theta), ny = near[1] + dist * sin(theta);
+        double g = near[2] + dist;
+        int parent = bi;
+        if (map_collision(&M, nx, ny, near[0], near[1])) continue;
+        /* where does node_new land in the dict? */
+        int slot = n;
+        if (star) {
+            for (int j = 0; j < n; j++)
+                if (tree[4 * j] == nx && tree[4 * j + 1] == ny) { slot = j; break; }
+            for (int j = 0; j < n; j++) {
+                double* t = tree + 4 * j;
+                const double d = vnorm2(nx - t[0], ny - t[1]);
+                if (!(d < radius)) continue;
+                const double c = t[2] + d;
+                if (g > c && !map_collision(&M, t[0], t[1], nx, ny)) {
+                    parent = j;
+                    g = c;
+                } else {
+                    const double c2 = g + d;
+                    if (t[2] > c2 && !map_collision(&M, t[0], t[1], nx, ny)) {
+                        t[3] = slot;
+                        t[2] = c2;
+                    }
+                }
+            }
+        } else {
+            for (int j = 0; j < n; j++)
+                if (tree[4 * j] == nx && tree[4 * j + 1] == ny) { slot = j; break; }
+        }
+        if (slot == n) {
+            if (n >= cap) { status = 3; break; }
+            n++;
+        }
+        double* t = tree + 4 * slot;
+        t[0] = nx; t[1] = ny; t[2] = g; t[3] = parent;
+        const double dg = vnorm2(gx - nx, gy - ny);
+        if (dg <= max_dist && !map_collision(&M, nx, ny, gx, gy)) {
+            if (n >= cap) { status = 3; break; }
+            double* gt = tree + 4 * n;
+            gt[0] = gx; gt[1] = gy; gt[2] = g + vnorm2(nx - gx, ny - gy); gt[3] = slot;
+            n++;
+            status = 0;
+            break;
+        }
+    }
+    *n_nodes = n;
+    if (draws) *draws = cur;
+    return status;
+}
+
+/* OpenMP over independent queries (bench cpu_baseline): query q uses rnd + q * stride. */
+int oracle_rrt_batch(int star, const double* rect, int nr, const double* circ, int nc, const double* bnd, int nb,
+                     double delta, double X, double Y, const double* starts, const double* goals, int nq,
+                     int sample_num, double max_dist, double radius, double goal_rate, const double* rnd,
+                     int64_t stride, double* tree, int cap, int32_t* n_nodes, int32_t* status, int nthreads)
+{
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+    int found = 0;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) reduction(+ : found)
+    for (int q = 0; q < nq; q++) {
+        int nn = 0;
+        status[q] = oracle_rrt(star, rect, nr, circ, nc, bnd, nb, delta, X, Y, starts[2 * q], starts[2 * q + 1],
+                               goals[2 * q], goals[2 * q + 1], sample_num, max_dist, radius, goal_rate,
+                               rnd + q * stride, stride, tree + (size_t)q * cap * 4, cap, &nn, NULL);
+        n_nodes[q] = nn;
+        found += status[q] == 0;
+    }
+    return found;
+}

@@ -246,3 +246,32 @@ def c4_workload(na: int = 256, seed: int = 2):
     states[:, 4] = rng.uniform(-np.pi / 2, np.pi / 2, na)
     goals = np.tile(np.array([45.0, 25.0, 0.0]), (na, 1))
     return occ, states, goals
+
+
+# --------------------------------------------------------------------------------------------
+# Continuous maps (utils/environment/env.py:83-117 Map) for the sample-search planners
+# --------------------------------------------------------------------------------------------
+README_MAP_RECT = [[14, 12, 8, 2], [18, 22, 8, 3], [26, 7, 2, 12], [32, 14, 10, 2]]
+README_MAP_CIRC = [[7, 12, 3], [46, 20, 2], [15, 5, 2], [37, 7, 3], [37, 23, 3]]
+
+
+def map_boundary(X: int, Y: int):
+    """Map.init (env.py:99-110): the four boundary rectangles."""
+    return [[0, 0, 1, Y], [0, Y, X, 1], [1, 0, X, 1], [X, 1, 1, Y]]
+
+
+def c3_map(X: int = 512, Y: int = 512, n_rect: int = 40, n_circ: int = 40, seed: int = 7):
+    """C3: Map(512, 512); default_rng(7) draws 40 rectangles then 40 circles as
+    floats from 7 vectorised integer draws: x, y in [10, 480), w, h in [5, 40), then cx, cy in
+    [10, 500), r in [3, 20).  Returns (obs_rect, obs_circ) as lists of float lists."""
+    rng = np.random.default_rng(seed)
+    rx = rng.integers(10, 480, n_rect)
+    ry = rng.integers(10, 480, n_rect)
+    rw = rng.integers(5, 40, n_rect)
+    rh = rng.integers(5, 40, n_rect)
+    cx = rng.integers(10, 500, n_circ)
+    cy = rng.integers(10, 500, n_circ)
+    cr = rng.integers(3, 20, n_circ)
+    rects = [[float(a), float(b), float(c), float(d)] for a, b, c, d in zip(rx, ry, rw, rh)]
+    circs = [[float(a), float(b), float(c)] for a, b, c in zip(cx, cy, cr)]
+    return rects, circs

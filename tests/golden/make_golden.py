@@ -454,7 +454,58 @@ def sec_mpc():
     print("mpc qp", out["p12_P"].shape, out["p30_P"].shape)
 
 
-SECTIONS = dict(mpc=sec_mpc, dwa=sec_dwa, local_plans=sec_local_plans, lqr=sec_lqr, astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
+def run_rrt(args):
+    """One RRT / RRT* plan with np.random.seed(seed): result, the whole tree (insertion order,
+    parent as an index) and the next global draw (pins how many draws plan() consumed)."""
+    kind, mapname, seed, sample_num, start, goal = args
+    pmp = import_reference()
+    from python_motion_planning_amd import workloads as wl
+
+    if mapname == "readme":
+        env = pmp.Map(51, 31)
+        env.update(obs_rect=[list(r) for r in wl.README_MAP_RECT], obs_circ=[list(c) for c in wl.README_MAP_CIRC])
+    else:
+        env = pmp.Map(512, 512)
+        rects, circs = wl.c3_map()
+        env.update(obs_rect=rects, obs_circ=circs)
+    cls = pmp.RRTStar if kind == "rrt_star" else pmp.RRT
+    planner = cls(start, goal, env, sample_num=sample_num)
+    np.random.seed(seed)
+    cost, path, expand = planner.plan()
+    nxt = np.random.random()
+    index = {n.current: i for i, n in enumerate(expand)}
+    tree = np.array([[n.x, n.y, n.g, index[n.parent] if n.parent in index else -1] for n in expand], np.float64)
+    close_figs()
+    return dict(cost=float(cost), found=path is not None, path=np.array(path if path else [], np.float64).reshape(-1, 2),
+                tree=tree, next=nxt)
+
+
+def sec_rrt():
+    cases = []
+    for kind in ("rrt", "rrt_star"):
+        for s in range(10):
+            cases.append((kind, "readme", s, 10000, (18, 8), (37, 18)))
+    for s in range(4):
+        cases.append(("rrt_star", "c3", s, 2000, (5, 5), (505, 505)))
+    cases.append(("rrt_star", "c3", 11, 5000, (5, 5), (505, 505)))
+    with Pool(8) as pool:
+        res = pool.map(run_rrt, cases)
+    out = {}
+    for i, (c, r) in enumerate(zip(cases, res)):
+        out[f"c{i}_kind"] = np.array(c[0])
+        out[f"c{i}_map"] = np.array(c[1])
+        out[f"c{i}_seed"] = np.array(c[2])
+        out[f"c{i}_sample_num"] = np.array(c[3])
+        out[f"c{i}_start"] = np.array(c[4], np.float64)
+        out[f"c{i}_goal"] = np.array(c[5], np.float64)
+        for k, v in r.items():
+            out[f"c{i}_{k}"] = np.asarray(v)
+    out["n_cases"] = np.array(len(cases))
+    np.savez_compressed(os.path.join(HERE, "rrt.npz"), **out)
+    print("rrt", [(c[0], c[1], c[2], r["found"], len(r["tree"]), round(r["cost"], 6)) for c, r in zip(cases, res)])
+
+
+SECTIONS = dict(rrt=sec_rrt, mpc=sec_mpc, dwa=sec_dwa, local_plans=sec_local_plans, lqr=sec_lqr, astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
                 dstar=sec_dstar, astar3d=sec_astar3d)
 
 if __name__ == "__main__":

@@ -256,3 +256,30 @@ def test_mpc_admm_reaches_certified_optimum():
             # OSQP's default tolerance (1e-3) lands near the same optimum
             xd, std, _, _ = O.qp_admm(H, g, lo, hi, O.MPCParams.default(p=P))
             assert std == 0 and np.abs(xd - xs).max() < 2e-2
+
+
+def _rrt_map(z, i):
+    from python_motion_planning_amd import workloads as wl
+
+    if str(z[f"c{i}_map"]) == "readme":
+        return wl.README_MAP_RECT, wl.README_MAP_CIRC, 51, 31
+    rects, circs = wl.c3_map()
+    return rects, circs, 512, 512
+
+
+def test_rrt_against_reference():
+    """RRT and RRT* (rrt.py:49-151, rrt_star.py:43-76): README map seeds 0..9 and the C3 512^2 map
+    (2000 and 5000 samples): the whole tree (x, y, g, parent of every node, insertion order) is
+    bit-exact, and the number of np.random draws consumed matches (next draw equal)."""
+    z = load_npz("rrt.npz")
+    for i in range(int(z["n_cases"])):
+        R, C, X, Y = _rrt_map(z, i)
+        sn = int(z[f"c{i}_sample_num"])
+        rnd = np.random.RandomState(int(z[f"c{i}_seed"])).random_sample(3 * sn + 1)
+        o = O.rrt(str(z[f"c{i}_kind"]) == "rrt_star", R, C, X, Y, z[f"c{i}_start"], z[f"c{i}_goal"], rnd,
+                  sample_num=sn)
+        assert np.array_equal(o["tree"], z[f"c{i}_tree"]), i
+        assert (o["status"] == 0) == bool(z[f"c{i}_found"])
+        assert rnd[o["draws"]] == z[f"c{i}_next"]
+        if o["status"] == 0:
+            assert o["tree"][-1, 2] == z[f"c{i}_cost"]
