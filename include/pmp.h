@@ -190,6 +190,41 @@ int pmp_track_step_batch(pmp_ctx* ctx, void* stream, int kind, const pmp_lp_para
                          const double* path_xy, const int32_t* path_off, int iters, double* u, int32_t* status,
                          int32_t* n_steps, double* hist_pose, int32_t* admm_iters);
 
+/* RRT / RRT* settings: Map size (utils/environment/env.py:92), inflation delta (sample_search.py:22),
+ * max_dist, sample_num, goal_sample_rate (rrt.py:36-44), radius r (rrt_star.py:34-38). */
+typedef struct {
+    double x_range, y_range, delta;
+    double max_dist, radius, goal_sample_rate;
+    int32_t sample_num;
+    int32_t star;          /* 1 = RRTStar.getNearest (choose parent + rewire), 0 = RRT */
+} pmp_rrt_params;
+
+/*
+ * Batched RRT / RRT*.  Replaces RRT.plan (global_planner/sample_search/rrt.py:49-151) with
+ * SampleSearcher.isCollision (sample_search.py:27-135) and RRTStar.getNearest (rrt_star.py:43-76).
+ * One workgroup per query; queries never interact.  All arrays are device pointers.
+ *   rect [nr][4] (x, y, w, h), circ [nc][3] (x, y, r), bnd [nb][4]   the Map's obs_rect, obs_circ, boundary
+ *   start_xy, goal_xy [nq][2]
+ *   rnd [nq][rnd_stride]  each query's np.random double stream, in RandomState.random_sample order
+ *                         (generateRandomNode draws one double, then two uniforms if it exceeds
+ *                         goal_sample_rate); 3*sample_num+1 doubles always suffice
+ *   tree_xy [nq][tree_cap][2], tree_g [nq][tree_cap], tree_parent [nq][tree_cap]   out: sample_list in
+ *                         insertion order (the start is node 0 and its own parent; the goal is last when found)
+ *   n_nodes [nq]          out: len(sample_list)
+ *   cost [nq]             out: goal.g, 0 when not found
+ *   path_len [nq], path_xy [nq][path_cap][2]   out: extractPath goal -> start
+ *   draws [nq] i64        out: doubles consumed from rnd (advance the caller's RNG by this many)
+ *   status [nq]           0 found, 1 not found (returns (0, None, nodes)), 2 path_cap overflow,
+ *                         3 tree_cap / stream / candidate-list overflow, 4 parent cycle (reference hangs)
+ * A new RRT* node that lands exactly on an existing one replaces it (dict semantics); plain RRT does
+ * not check for that (a measure-zero event).
+ */
+int pmp_rrt_batch(pmp_ctx* ctx, void* stream, const pmp_rrt_params* p, const double* rect, int nr,
+                  const double* circ, int nc, const double* bnd, int nb, const double* start_xy,
+                  const double* goal_xy, int nq, const double* rnd, int64_t rnd_stride, int tree_cap,
+                  double* tree_xy, double* tree_g, int32_t* tree_parent, int32_t* n_nodes, double* cost,
+                  int32_t* path_len, double* path_xy, int path_cap, int64_t* draws, int32_t* status);
+
 /* Pre-size the A* scratch (heap of heap_cap entries per concurrent query, up to max_slots
  * concurrent queries) so that later batch calls allocate nothing (hipGraph-capturable). */
 int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int max_slots, int heap_cap);

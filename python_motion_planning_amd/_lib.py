@@ -31,6 +31,8 @@ SIGNATURES = {
     "pmp_lqr_control_batch": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
     "pmp_mpc_control_batch": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _vp]),
+    "pmp_rrt_batch": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _i, _vp, _i, _vp, _vp, _i, _vp, ctypes.c_int64, _i, _vp, _vp,
+                           _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp]),
     "pmp_track_step_batch": (_i, [_vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp,
                                   _vp]),
 }
@@ -90,6 +92,13 @@ class MPCParams(ctypes.Structure):
                    (ctypes.c_double * 2)(*[float(v) for v in r]), a["rho"], a["sigma"], a["alpha"], a["eps_abs"],
                    a["eps_rel"], a["adaptive_tol"], int(a["max_iter"]), int(a["check_every"]),
                    int(a["adaptive_every"]), 0)
+
+
+class RRTParams(ctypes.Structure):
+    """pmp_rrt_params == Map size, delta (sample_search.py:22), RRT kwargs (rrt.py:36-44), RRT* r."""
+    _fields_ = [("x_range", ctypes.c_double), ("y_range", ctypes.c_double), ("delta", ctypes.c_double),
+                ("max_dist", ctypes.c_double), ("radius", ctypes.c_double), ("goal_sample_rate", ctypes.c_double),
+                ("sample_num", ctypes.c_int32), ("star", ctypes.c_int32)]
 
 
 TRACK_LQR, TRACK_MPC = 0, 1

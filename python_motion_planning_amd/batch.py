@@ -208,6 +208,53 @@ def track_step_batch(kind: str, lp_params, state, goal, path_xy, path_off, iters
     return out
 
 
+def map_arrays(env, torch=None):
+    """Map obstacle lists (env.py:83-117) -> device f64 tensors rect [nr,4], circ [nc,3], bnd [nb,4]."""
+    torch = torch or _lib.device_check()
+
+    def t(lst, k):
+        a = np.asarray(lst if lst else np.zeros((0, k)), np.float64).reshape(-1, k)
+        return torch.as_tensor(np.ascontiguousarray(a), device="cuda")
+
+    return t(env.obs_rect, 4), t(env.obs_circ, 3), t(env.boundary, 4)
+
+
+def rrt_batch(env, starts, goals, rnd, sample_num: int, star: bool = True, max_dist: float = 0.5,
+              radius: float = 10.0, goal_sample_rate: float = 0.05, delta: float = 0.5, path_cap: int | None = None,
+              stream=None):
+    """Batched RRT / RRT* plans (rrt.py:49-151, rrt_star.py:43-76) on one Map.
+    rnd: [nq, stride] f64 random streams (RandomState.random_sample order; 3*sample_num+1 per query).
+    Returns dict of device tensors: tree_xy [nq,cap,2], tree_g, tree_parent, n_nodes, cost, path_len,
+    path [nq,path_cap,2] (goal -> start), draws, status."""
+    torch = _lib.device_check()
+    L = _lib.load_library()
+    ctx = _lib.context()
+    rect, circ, bnd = map_arrays(env, torch)
+    s = _dev(torch, starts, torch.float64).reshape(-1, 2)
+    g = _dev(torch, goals, torch.float64).reshape(-1, 2)
+    nq = int(s.shape[0])
+    rnd = _dev(torch, rnd, torch.float64).reshape(nq, -1)
+    cap = int(sample_num) + 2
+    path_cap = cap if path_cap is None else int(path_cap)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    i32 = dict(dtype=torch.int32, device="cuda")
+    out = dict(tree_xy=torch.empty((nq, cap, 2), **f64), tree_g=torch.empty((nq, cap), **f64),
+               tree_parent=torch.empty((nq, cap), **i32), n_nodes=torch.empty(nq, **i32),
+               cost=torch.empty(nq, **f64), path_len=torch.empty(nq, **i32),
+               path=torch.empty((nq, max(path_cap, 1), 2), **f64), draws=torch.empty(nq, dtype=torch.int64, device="cuda"),
+               status=torch.empty(nq, **i32))
+    P = _lib.RRTParams(float(env.x_range), float(env.y_range), float(delta), float(max_dist), float(radius),
+                       float(goal_sample_rate), int(sample_num), int(bool(star)))
+    rc = L.pmp_rrt_batch(ctx, stream if stream is not None else _lib.stream_ptr(), ctypes.byref(P), rect.data_ptr(),
+                         int(rect.shape[0]), circ.data_ptr(), int(circ.shape[0]), bnd.data_ptr(), int(bnd.shape[0]),
+                         s.data_ptr(), g.data_ptr(), nq, rnd.data_ptr(), int(rnd.shape[1]), cap,
+                         out["tree_xy"].data_ptr(), out["tree_g"].data_ptr(), out["tree_parent"].data_ptr(),
+                         out["n_nodes"].data_ptr(), out["cost"].data_ptr(), out["path_len"].data_ptr(),
+                         out["path"].data_ptr(), path_cap, out["draws"].data_ptr(), out["status"].data_ptr())
+    _lib.check(ctx, rc, "pmp_rrt_batch")
+    return out
+
+
 def astar3d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: int | None = None,
                   expand_cap: int = 0, counters: bool = False):
     """Batched AStar3D.plan (a_star3d.py:33-106).

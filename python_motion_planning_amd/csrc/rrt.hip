@@ -1,0 +1,410 @@
+// Batched RRT / RRT* for gfx950 (global_planner/sample_search/rrt.py:49-151, rrt_star.py:43-76,
+// sample_search.py:27-135): one 512-thread workgroup per query grows that query's tree.
+//
+// Per iteration (all decisions wave-uniform, results identical to the reference's sequential loop):
+//  1. sample from the query's np.random stream (generateRandomNode, rrt.py:91-103);
+//  2. nearest node = first argmin of the exact CPython hypot (rrt.py:117-118).  A coarse pass over an
+//     f32 copy of the coordinates (8 B/node) finds the minimum; only nodes within a rigorous f32
+//     error band of it are re-evaluated exactly in f64; ties resolve to the lowest index.  A zero
+//     distance means the sample is already in sample_list (rrt.py:67-68);
+//  3. steer (hypot, atan2, cos, sin) and isCollision(new, near), the obstacle tests spread over the
+//     workgroup;
+//  4. RRT*: the sequential choose-parent/rewire scan (rrt_star.py:57-73) in parallel form.  With
+//     G0 = the steered g and c_i = g_i + d_i for in-radius nodes i, node_new.g before node i is
+//     G_{i-1} = min(G0, c_j : j < i, c_j < G0, collision-free) (a strict `>` keeps the earliest
+//     minimum, so the final parent is the lowest index attaining it).  Only the few nodes with
+//     c_i < G0 need a collision test to build that set; then every in-radius node decides its
+//     rewire (g_i > G_{i-1} + d_i and collision-free) independently;
+//  5. insert (a node landing exactly on an existing one replaces it, like the dict), goal test.
+#include "localplan.h"
+
+namespace {
+
+constexpr int kNT = 512;
+constexpr int kWaves = kNT / 64;
+constexpr int kMaxObs = 256;   // per obstacle kind
+constexpr int kMaxBnd = 8;
+constexpr int kMaxA = 2048;    // collision-free improving candidates per iteration
+
+constexpr int KF_A = 1;        // c_i < G0
+constexpr int KF_VALID = 2;    // ... and collision-free
+
+struct KEntry {
+    int j, flags;
+    double d;
+};
+
+struct RrtArgs {
+    pmp_rrt_params P;
+    const double *rect, *circ, *bnd;
+    int nr, nc, nb;
+    const double *start, *goal;
+    int nq;
+    const double* rnd;
+    int64_t stride;
+    int cap;
+    double *txy, *tg;
+    int32_t* tpar;
+    int32_t* n_nodes;
+    double* cost;
+    int32_t* path_len;
+    double* path;
+    int path_cap;
+    int64_t* draws;
+    int32_t* status;
+    float2* xyf;      // scratch [nq][cap]
+    KEntry* klist;    // scratch [nq][cap]
+};
+
+struct RrtShared {
+    double rect[kMaxObs * 4];
+    double circ[kMaxObs * 3];
+    double bnd[kMaxBnd * 4];
+    float redf[kWaves];
+    double redd[kWaves];
+    int redi[kWaves];
+    int aj[kMaxA];
+    double ac[kMaxA];
+    int nK, nA, slot;
+};
+
+// ---- obstacle tests (sample_search.py), same operation order as the oracle ----
+__device__ inline bool in_box(const double* r, double d, double x, double y)
+{
+    const double px = x - (r[0] - d), py = y - (r[1] - d);
+    return 0 <= px && px <= r[2] + 2 * d && 0 <= py && py <= r[3] + 2 * d;
+}
+
+__device__ inline double cross3(double p1x, double p1y, double p2x, double p2y, double p3x, double p3y)
+{
+    const double x1 = p2x - p1x, y1 = p2y - p1y, x2 = p3x - p1x, y2 = p3y - p1y;
+    return x1 * y2 - x2 * y1;
+}
+
+__device__ bool inter_rect(const double* r, double d, double x1, double y1, double x2, double y2)
+{
+    const double vx[4] = {r[0] - d, r[0] + r[2] + d, r[0] + r[2] + d, r[0] - d};
+    const double vy[4] = {r[1] - d, r[1] - d, r[1] + r[3] + d, r[1] + r[3] + d};
+    for (int a = 0; a < 4; a++)
+        for (int b = a + 1; b < 4; b++) {
+            if (fmax(x1, x2) >= fmin(vx[a], vx[b]) && fmin(x1, x2) <= fmax(vx[a], vx[b]) &&
+                fmax(y1, y2) >= fmin(vy[a], vy[b]) && fmin(y1, y2) <= fmax(vy[a], vy[b])) {
+                if (cross3(vx[a], vy[a], vx[b], vy[b], x1, y1) * cross3(vx[a], vy[a], vx[b], vy[b], x2, y2) <= 0 &&
+                    cross3(x1, y1, x2, y2, vx[a], vy[a]) * cross3(x1, y1, x2, y2, vx[b], vy[b]) <= 0)
+                    return true;
+            }
+        }
+    return false;
+}
+
+// np.dot of 2-vectors = OpenBLAS ddot: fma(a1, b1, a0 * b0)
+__device__ bool inter_circle(const double* c, double d, double x, double y, double x2, double y2)
+{
+    const double dx = x2 - x, dy = y2 - y;
+    const double d2 = fma(dy, dy, dx * dx);
+    if (d2 == 0) return false;
+    const double t = fma(c[1] - y, dy, (c[0] - x) * dx) / d2;
+    if (0 <= t && t <= 1) {
+        const double sx = x + t * dx, sy = y + t * dy;
+        if (lp::py_hypot(c[0] - sx, c[1] - sy) <= c[2] + d) return true;
+    }
+    return false;
+}
+
+// collision test item `it` of isCollision(p1, p2): inside(p1) circles/rects/boundary, inside(p2)
+// ..., rect crossings, circle crossings (sample_search.py:27-49)
+__device__ inline bool coll_item(const RrtShared& S, int nr, int nc, int nb, double d, int it, double x1, double y1,
+                                 double x2, double y2)
+{
+    const int per = nc + nr + nb;
+    double x = x1, y = y1;
+    if (it >= per && it < 2 * per) { it -= per; x = x2; y = y2; }
+    if (it < per) {
+        if (it < nc) return lp::py_hypot(x - S.circ[3 * it], y - S.circ[3 * it + 1]) <= S.circ[3 * it + 2] + d;
+        it -= nc;
+        if (it < nr) return in_box(&S.rect[4 * it], d, x, y);
+        return in_box(&S.bnd[4 * (it - nr)], d, x, y);
+    }
+    it -= 2 * per;
+    if (it < nr) return inter_rect(&S.rect[4 * it], d, x1, y1, x2, y2);
+    it -= nr;
+    return inter_circle(&S.circ[3 * it], d, x1, y1, x2, y2);
+}
+
+__device__ bool collision_serial(const RrtShared& S, int nr, int nc, int nb, double d, double x1, double y1, double x2,
+                                 double y2)
+{
+    const int items = 2 * (nc + nr + nb) + nr + nc;
+    for (int it = 0; it < items; it++)
+        if (coll_item(S, nr, nc, nb, d, it, x1, y1, x2, y2)) return true;
+    return false;
+}
+
+// workgroup-parallel isCollision(p1, p2); every thread gets the result
+__device__ bool collision_block(const RrtShared& S, int nr, int nc, int nb, double d, double x1, double y1, double x2,
+                                double y2)
+{
+    const int items = 2 * (nc + nr + nb) + nr + nc;
+    int hit = 0;
+    for (int it = threadIdx.x; it < items; it += kNT) hit |= coll_item(S, nr, nc, nb, d, it, x1, y1, x2, y2);
+    return __syncthreads_or(hit) != 0;
+}
+
+// ---- workgroup reductions ----
+__device__ float block_min_f(float v, RrtShared& S)
+{
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+    if ((threadIdx.x & 63) == 0) S.redf[threadIdx.x >> 6] = v;
+    __syncthreads();
+    float r = S.redf[0];
+    for (int w = 1; w < kWaves; w++) r = fminf(r, S.redf[w]);
+    __syncthreads();
+    return r;
+}
+
+// lexicographic min of (v, i)
+__device__ void block_min_di(double& v, int& i, RrtShared& S)
+{
+    for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(v, o);
+        const int oi = __shfl_xor(i, o);
+        if (ov < v || (ov == v && oi < i)) { v = ov; i = oi; }
+    }
+    if ((threadIdx.x & 63) == 0) { S.redd[threadIdx.x >> 6] = v; S.redi[threadIdx.x >> 6] = i; }
+    __syncthreads();
+    v = S.redd[0];
+    i = S.redi[0];
+    for (int w = 1; w < kWaves; w++)
+        if (S.redd[w] < v || (S.redd[w] == v && S.redi[w] < i)) { v = S.redd[w]; i = S.redi[w]; }
+    __syncthreads();
+}
+
+template <bool STAR>
+__global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
+{
+    __shared__ RrtShared S;
+    const int q = blockIdx.x;
+    const int tid = threadIdx.x;
+    if (q >= A.nq) return;
+    const int nr = A.nr, nc = A.nc, nb = A.nb;
+    for (int i = tid; i < 4 * nr; i += kNT) S.rect[i] = A.rect[i];
+    for (int i = tid; i < 3 * nc; i += kNT) S.circ[i] = A.circ[i];
+    for (int i = tid; i < 4 * nb; i += kNT) S.bnd[i] = A.bnd[i];
+    const pmp_rrt_params P = A.P;
+    const double delta = P.delta;
+    const int cap = A.cap;
+    double* tx = A.txy + (size_t)q * cap * 2;
+    double* tg = A.tg + (size_t)q * cap;
+    int32_t* tpar = A.tpar + (size_t)q * cap;
+    float2* xyf = A.xyf + (size_t)q * cap;
+    KEntry* kl = A.klist + (size_t)q * cap;
+    const double* rnd = A.rnd + (size_t)q * A.stride;
+    const double sx0 = A.start[2 * q], sy0 = A.start[2 * q + 1];
+    const double gx = A.goal[2 * q], gy = A.goal[2 * q + 1];
+    if (tid == 0) {
+        tx[0] = sx0; tx[1] = sy0; tg[0] = 0.0; tpar[0] = 0;
+        xyf[0] = make_float2((float)sx0, (float)sy0);
+    }
+    __syncthreads();
+    const double lox = delta, rgx = (P.x_range - delta) - delta;
+    const double loy = delta, rgy = (P.y_range - delta) - delta;
+    // f32 error band: coordinates of magnitude <= cmax carry <= cmax * 2^-24 rounding each
+    const double cmax = fmax(fmax(P.x_range, P.y_range), fmax(fmax(fabs(gx), fabs(gy)), fmax(fabs(sx0), fabs(sy0)))) + 1.0;
+    const double eps = 4e-6 * cmax + 1e-5;
+    int n = 1, status = 1;
+    int64_t cur = 0;
+
+    for (int it = 0; it < P.sample_num; it++) {
+        if (cur + 3 > A.stride) { status = PMP_CAP_OVERFLOW; break; }
+        double sx = gx, sy = gy;
+        if (rnd[cur++] > P.goal_sample_rate) {
+            sx = lox + rgx * rnd[cur++];
+            sy = loy + rgy * rnd[cur++];
+        }
+        // ---- 2. nearest ----
+        const float sxf = (float)sx, syf = (float)sy;
+        float best = INFINITY;
+        for (int j = tid; j < n; j += kNT) {
+            const float2 p = xyf[j];
+            const float dx = p.x - sxf, dy = p.y - syf;
+            best = fminf(best, dx * dx + dy * dy);
+        }
+        const float m = block_min_f(best, S);
+        const double band = sqrt((double)m) + 2.0 * eps;
+        const float T = (float)(band * band) * 1.0001f;
+        double h = INFINITY;
+        int hi = 0x7fffffff;
+        if (best <= T) {
+            for (int j = tid; j < n; j += kNT) {
+                const float2 p = xyf[j];
+                const float dx = p.x - sxf, dy = p.y - syf;
+                if (dx * dx + dy * dy <= T) {
+                    const double e = lp::py_hypot(tx[2 * j] - sx, tx[2 * j + 1] - sy);
+                    if (e < h) { h = e; hi = j; }  // increasing j per thread: keeps the first
+                }
+            }
+        }
+        block_min_di(h, hi, S);
+        if (h == 0.0) continue;  // node_rand.current already in sample_list
+        const int near = hi;
+        const double nx0 = tx[2 * near], ny0 = tx[2 * near + 1], gnear = tg[near];
+        // ---- 3. steer + collision (rrt.py:121-129) ----
+        double dist = lp::py_hypot(sx - nx0, sy - ny0);
+        const double theta = atan2(sy - ny0, sx - nx0);
+        if (P.max_dist < dist) dist = P.max_dist;
+        const double nx = nx0 + dist * cos(theta), ny = ny0 + dist * sin(theta);
+        const double G0 = gnear + dist;
+        if (collision_block(S, nr, nc, nb, delta, nx, ny, nx0, ny0)) continue;
+        double G = G0;
+        int parent = near;
+        int slot = n;
+        if (tid == 0) { S.nK = 0; S.nA = 0; S.slot = n; }
+        __syncthreads();
+        if (STAR) {
+            // ---- 4a. in-radius candidates ----
+            const float nxf = (float)nx, nyf = (float)ny;
+            const double rb = P.radius + 2.0 * eps;
+            const float Tr = (float)(rb * rb) * 1.0001f;
+            for (int j = tid; j < n; j += kNT) {
+                const float2 p = xyf[j];
+                const float dx = p.x - nxf, dy = p.y - nyf;
+                if (dx * dx + dy * dy > Tr) continue;
+                const double xj = tx[2 * j], yj = tx[2 * j + 1];
+                if (xj == nx && yj == ny) atomicMin(&S.slot, j);
+                const double d = lp::py_hypot(nx - xj, ny - yj);
+                if (!(d < P.radius)) continue;
+                const int k = atomicAdd(&S.nK, 1);
+                KEntry e;
+                e.j = j;
+                e.d = d;
+                e.flags = (tg[j] + d < G0) ? KF_A : 0;
+                kl[k] = e;
+            }
+            __syncthreads();
+            const int nK = S.nK;
+            slot = S.slot;
+            // ---- 4b. collision-free improving candidates ----
+            for (int k = tid; k < nK; k += kNT) {
+                KEntry e = kl[k];
+                if (!(e.flags & KF_A)) continue;
+                const double xj = tx[2 * e.j], yj = tx[2 * e.j + 1];
+                if (collision_serial(S, nr, nc, nb, delta, xj, yj, nx, ny)) continue;
+                const int a = atomicAdd(&S.nA, 1);
+                if (a < kMaxA) { S.aj[a] = e.j; S.ac[a] = tg[e.j] + e.d; }
+                kl[k].flags = KF_A | KF_VALID;
+            }
+            __syncthreads();
+            const int nA = S.nA;
+            if (nA > kMaxA) { status = PMP_CAP_OVERFLOW; break; }
+            double cb = INFINITY;
+            int jb = 0x7fffffff;
+            for (int a = tid; a < nA; a += kNT)
+                if (S.ac[a] < cb || (S.ac[a] == cb && S.aj[a] < jb)) { cb = S.ac[a]; jb = S.aj[a]; }
+            block_min_di(cb, jb, S);
+            if (cb < G0) { G = cb; parent = jb; }
+            // ---- 4c. rewire ----
+            for (int k = tid; k < nK; k += kNT) {
+                const KEntry e = kl[k];
+                double Gp = G0;
+                for (int a = 0; a < nA; a++)
+                    if (S.aj[a] < e.j) Gp = fmin(Gp, S.ac[a]);
+                const double gj = tg[e.j];
+                if ((e.flags & KF_VALID) && Gp > gj + e.d) continue;  // node_new re-parents here
+                const double c2 = Gp + e.d;
+                if (!(gj > c2)) continue;
+                if (e.flags & KF_A) {
+                    if (!(e.flags & KF_VALID)) continue;
+                } else if (collision_serial(S, nr, nc, nb, delta, tx[2 * e.j], tx[2 * e.j + 1], nx, ny)) {
+                    continue;
+                }
+                tg[e.j] = c2;
+                tpar[e.j] = slot;
+            }
+            __syncthreads();  // rewires land before the insert below may overwrite a duplicate slot
+        }
+        // ---- 5. insert + goal test (rrt.py:70-81) ----
+        if (tid == 0) {
+            tx[2 * slot] = nx; tx[2 * slot + 1] = ny; tg[slot] = G; tpar[slot] = parent;
+            xyf[slot] = make_float2((float)nx, (float)ny);
+        }
+        if (slot == n) {
+            if (n >= cap) { status = PMP_CAP_OVERFLOW; break; }
+            n++;
+        }
+        __syncthreads();
+        const double dg = lp::py_hypot(gx - nx, gy - ny);
+        if (dg <= P.max_dist && !collision_block(S, nr, nc, nb, delta, nx, ny, gx, gy)) {
+            if (n >= cap) { status = PMP_CAP_OVERFLOW; break; }
+            if (tid == 0) {
+                tx[2 * n] = gx; tx[2 * n + 1] = gy; tg[n] = G + lp::py_hypot(nx - gx, ny - gy); tpar[n] = slot;
+                xyf[n] = make_float2((float)gx, (float)gy);
+            }
+            n++;
+            status = PMP_FOUND;
+            break;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        A.n_nodes[q] = n;
+        A.draws[q] = cur;
+        int plen = 0;
+        double c = 0.0;
+        if (status == PMP_FOUND) {
+            c = tg[n - 1];
+            // extractPath (rrt.py:133-151): goal -> start through parents
+            int v = n - 1;
+            bool reached = false;
+            double* out = A.path + (size_t)q * A.path_cap * 2;
+            for (int s = 0; s <= n; s++) {
+                if (plen < A.path_cap) { out[2 * plen] = tx[2 * v]; out[2 * plen + 1] = tx[2 * v + 1]; }
+                plen++;
+                if (v == 0) { reached = true; break; }
+                v = tpar[v];
+            }
+            if (!reached) status = PMP_REF_RAISES;  // parent cycle: the reference never terminates
+            else if (plen > A.path_cap) status = PMP_PATH_OVERFLOW;
+        }
+        A.path_len[q] = plen;
+        A.cost[q] = c;
+        A.status[q] = status;
+    }
+}
+
+}  // namespace
+
+extern "C" int pmp_rrt_batch(pmp_ctx* ctx, void* stream, const pmp_rrt_params* p, const double* rect, int nr,
+                             const double* circ, int nc, const double* bnd, int nb, const double* start_xy,
+                             const double* goal_xy, int nq, const double* rnd, int64_t rnd_stride, int tree_cap,
+                             double* tree_xy, double* tree_g, int32_t* tree_parent, int32_t* n_nodes, double* cost,
+                             int32_t* path_len, double* path_xy, int path_cap, int64_t* draws, int32_t* status)
+{
+    if (!ctx) return PMP_EINVAL;
+    if (!p || nq < 0 || nr < 0 || nc < 0 || nb < 0 || nr > kMaxObs || nc > kMaxObs || nb > kMaxBnd)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_rrt_batch: bad params or obstacle counts (<= 256 rects, 256 circles, 8 boundary)");
+    if (p->sample_num < 0 || tree_cap < 2 || rnd_stride < 1 || path_cap < 0 || !(p->delta >= 0) || !(p->max_dist >= 0))
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_rrt_batch: bad sample_num / tree_cap / rnd_stride / path_cap");
+    if (nq == 0) return PMP_OK;
+    if ((nr && !rect) || (nc && !circ) || (nb && !bnd) || !start_xy || !goal_xy || !rnd || !tree_xy || !tree_g ||
+        !tree_parent || !n_nodes || !cost || !path_len || (path_cap && !path_xy) || !draws || !status)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_rrt_batch: null pointer argument");
+    PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    float2* xyf = (float2*)pmp_scratch(ctx, SCR_AUX0, sizeof(float2) * (size_t)nq * tree_cap);
+    KEntry* kl = (KEntry*)pmp_scratch(ctx, SCR_AUX1, sizeof(KEntry) * (size_t)nq * tree_cap);
+    if (!xyf || !kl) return PMP_ENOMEM;
+    RrtArgs A;
+    A.P = *p;
+    A.rect = rect; A.circ = circ; A.bnd = bnd;
+    A.nr = nr; A.nc = nc; A.nb = nb;
+    A.start = start_xy; A.goal = goal_xy; A.nq = nq;
+    A.rnd = rnd; A.stride = rnd_stride; A.cap = tree_cap;
+    A.txy = tree_xy; A.tg = tree_g; A.tpar = tree_parent; A.n_nodes = n_nodes;
+    A.cost = cost; A.path_len = path_len; A.path = path_xy; A.path_cap = path_cap;
+    A.draws = draws; A.status = status; A.xyf = xyf; A.klist = kl;
+    if (p->star)
+        hipLaunchKernelGGL(rrt_kernel<true>, dim3(nq), dim3(kNT), 0, (hipStream_t)stream, A);
+    else
+        hipLaunchKernelGGL(rrt_kernel<false>, dim3(nq), dim3(kNT), 0, (hipStream_t)stream, A);
+    PMP_HIP_CHECK(ctx, hipGetLastError());
+    return PMP_OK;
+}
