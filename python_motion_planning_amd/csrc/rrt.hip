@@ -25,6 +25,7 @@ constexpr int kWaves = kNT / 64;
 constexpr int kMaxObs = 256;   // per obstacle kind
 constexpr int kMaxBnd = 8;
 constexpr int kMaxA = 2048;    // collision-free improving candidates per iteration
+constexpr int kMaxT = 4096;    // candidates awaiting a collision test per phase
 
 constexpr int KF_A = 1;        // c_i < G0
 constexpr int KF_VALID = 2;    // ... and collision-free
@@ -65,7 +66,9 @@ struct RrtShared {
     int redi[kWaves];
     int aj[kMaxA];
     double ac[kMaxA];
-    int nK, nA, slot;
+    int tk[kMaxT];      // K entries awaiting a collision test
+    double tG[kMaxT];   // ... and their G_{i-1}
+    int nK, nA, nT, slot;
 };
 
 // ---- obstacle tests (sample_search.py), same operation order as the oracle ----
@@ -112,7 +115,9 @@ __device__ bool inter_circle(const double* c, double d, double x, double y, doub
 }
 
 // collision test item `it` of isCollision(p1, p2): inside(p1) circles/rects/boundary, inside(p2)
-// ..., rect crossings, circle crossings (sample_search.py:27-49)
+// ..., rect crossings, circle crossings (sample_search.py:27-49).  Exact bounding-box rejections
+// come first: |dx| > r + d already implies hypot > r + d (hypot >= |dx| exactly), and a segment
+// whose bbox misses the inflated rect fails every "rapid repulsion" pair test.
 __device__ inline bool coll_item(const RrtShared& S, int nr, int nc, int nb, double d, int it, double x1, double y1,
                                  double x2, double y2)
 {
@@ -120,31 +125,49 @@ __device__ inline bool coll_item(const RrtShared& S, int nr, int nc, int nb, dou
     double x = x1, y = y1;
     if (it >= per && it < 2 * per) { it -= per; x = x2; y = y2; }
     if (it < per) {
-        if (it < nc) return lp::py_hypot(x - S.circ[3 * it], y - S.circ[3 * it + 1]) <= S.circ[3 * it + 2] + d;
+        if (it < nc) {
+            const double* c = &S.circ[3 * it];
+            const double rr = c[2] + d;
+            if (fabs(x - c[0]) > rr || fabs(y - c[1]) > rr) return false;
+            return lp::py_hypot(x - c[0], y - c[1]) <= rr;
+        }
         it -= nc;
         if (it < nr) return in_box(&S.rect[4 * it], d, x, y);
         return in_box(&S.bnd[4 * (it - nr)], d, x, y);
     }
     it -= 2 * per;
-    if (it < nr) return inter_rect(&S.rect[4 * it], d, x1, y1, x2, y2);
+    const double bx0 = fmin(x1, x2), bx1 = fmax(x1, x2), by0 = fmin(y1, y2), by1 = fmax(y1, y2);
+    if (it < nr) {
+        const double* r = &S.rect[4 * it];
+        if (bx1 < r[0] - d || bx0 > r[0] + r[2] + d || by1 < r[1] - d || by0 > r[1] + r[3] + d) return false;
+        return inter_rect(r, d, x1, y1, x2, y2);
+    }
     it -= nr;
-    return inter_circle(&S.circ[3 * it], d, x1, y1, x2, y2);
+    const double* c = &S.circ[3 * it];
+    // the projected point lies within the segment's bbox (up to rounding): a gap of more than
+    // r + d (with slack for the rounding) rules the circle out
+    const double rr = (c[2] + d) * (1.0 + 1e-12) + 1e-12;
+    if (bx1 < c[0] - rr || bx0 > c[0] + rr || by1 < c[1] - rr || by0 > c[1] + rr) return false;
+    return inter_circle(c, d, x1, y1, x2, y2);
 }
 
-__device__ bool collision_serial(const RrtShared& S, int nr, int nc, int nb, double d, double x1, double y1, double x2,
-                                 double y2)
+__device__ inline int coll_items(int nr, int nc, int nb) { return 2 * (nc + nr + nb) + nr + nc; }
+
+// one wave cooperates on one isCollision(p1, p2); wave-uniform result
+__device__ bool collision_wave(const RrtShared& S, int nr, int nc, int nb, double d, double x1, double y1, double x2,
+                               double y2)
 {
-    const int items = 2 * (nc + nr + nb) + nr + nc;
-    for (int it = 0; it < items; it++)
-        if (coll_item(S, nr, nc, nb, d, it, x1, y1, x2, y2)) return true;
-    return false;
+    const int items = coll_items(nr, nc, nb);
+    bool hit = false;
+    for (int it = lane_id(); it < items; it += 64) hit |= coll_item(S, nr, nc, nb, d, it, x1, y1, x2, y2);
+    return ballot(hit) != 0;
 }
 
 // workgroup-parallel isCollision(p1, p2); every thread gets the result
 __device__ bool collision_block(const RrtShared& S, int nr, int nc, int nb, double d, double x1, double y1, double x2,
                                 double y2)
 {
-    const int items = 2 * (nc + nr + nb) + nr + nc;
+    const int items = coll_items(nr, nc, nb);
     int hit = 0;
     for (int it = threadIdx.x; it < items; it += kNT) hit |= coll_item(S, nr, nc, nb, d, it, x1, y1, x2, y2);
     return __syncthreads_or(hit) != 0;
@@ -258,10 +281,11 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         double G = G0;
         int parent = near;
         int slot = n;
-        if (tid == 0) { S.nK = 0; S.nA = 0; S.slot = n; }
+        if (tid == 0) { S.nK = 0; S.nA = 0; S.nT = 0; S.slot = n; }
         __syncthreads();
         if (STAR) {
-            // ---- 4a. in-radius candidates ----
+            const int wave = tid >> 6, lane = tid & 63;
+            // ---- 4a. in-radius candidates; those with c_i < G0 queue for a collision test ----
             const float nxf = (float)nx, nyf = (float)ny;
             const double rb = P.radius + 2.0 * eps;
             const float Tr = (float)(rb * rb) * 1.0001f;
@@ -279,19 +303,26 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                 e.d = d;
                 e.flags = (tg[j] + d < G0) ? KF_A : 0;
                 kl[k] = e;
+                if (e.flags & KF_A) {
+                    const int t = atomicAdd(&S.nT, 1);
+                    if (t < kMaxT) S.tk[t] = k;
+                }
             }
             __syncthreads();
             const int nK = S.nK;
+            const int nT = S.nT;
             slot = S.slot;
-            // ---- 4b. collision-free improving candidates ----
-            for (int k = tid; k < nK; k += kNT) {
-                KEntry e = kl[k];
-                if (!(e.flags & KF_A)) continue;
-                const double xj = tx[2 * e.j], yj = tx[2 * e.j + 1];
-                if (collision_serial(S, nr, nc, nb, delta, xj, yj, nx, ny)) continue;
-                const int a = atomicAdd(&S.nA, 1);
-                if (a < kMaxA) { S.aj[a] = e.j; S.ac[a] = tg[e.j] + e.d; }
-                kl[k].flags = KF_A | KF_VALID;
+            if (nT > kMaxT) { status = PMP_CAP_OVERFLOW; break; }
+            // ---- 4b. one wave per test: the collision-free improving set ----
+            for (int t = wave; t < nT; t += kWaves) {
+                const int k = S.tk[t];
+                const KEntry e = kl[k];
+                if (collision_wave(S, nr, nc, nb, delta, tx[2 * e.j], tx[2 * e.j + 1], nx, ny)) continue;
+                if (lane == 0) {
+                    const int a = atomicAdd(&S.nA, 1);
+                    if (a < kMaxA) { S.aj[a] = e.j; S.ac[a] = tg[e.j] + e.d; }
+                    kl[k].flags = KF_A | KF_VALID;
+                }
             }
             __syncthreads();
             const int nA = S.nA;
@@ -300,9 +331,10 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             int jb = 0x7fffffff;
             for (int a = tid; a < nA; a += kNT)
                 if (S.ac[a] < cb || (S.ac[a] == cb && S.aj[a] < jb)) { cb = S.ac[a]; jb = S.aj[a]; }
-            block_min_di(cb, jb, S);
+            if (tid == 0) S.nT = 0;
+            block_min_di(cb, jb, S);  // (its barriers also publish nT = 0)
             if (cb < G0) { G = cb; parent = jb; }
-            // ---- 4c. rewire ----
+            // ---- 4c. rewire decisions; untested candidates queue for a collision test ----
             for (int k = tid; k < nK; k += kNT) {
                 const KEntry e = kl[k];
                 double Gp = G0;
@@ -313,12 +345,19 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                 const double c2 = Gp + e.d;
                 if (!(gj > c2)) continue;
                 if (e.flags & KF_A) {
-                    if (!(e.flags & KF_VALID)) continue;
-                } else if (collision_serial(S, nr, nc, nb, delta, tx[2 * e.j], tx[2 * e.j + 1], nx, ny)) {
+                    if (e.flags & KF_VALID) { tg[e.j] = c2; tpar[e.j] = slot; }
                     continue;
                 }
-                tg[e.j] = c2;
-                tpar[e.j] = slot;
+                const int t = atomicAdd(&S.nT, 1);
+                if (t < kMaxT) { S.tk[t] = k; S.tG[t] = Gp; }
+            }
+            __syncthreads();
+            const int nT2 = S.nT;
+            if (nT2 > kMaxT) { status = PMP_CAP_OVERFLOW; break; }
+            for (int t = wave; t < nT2; t += kWaves) {
+                const KEntry e = kl[S.tk[t]];
+                if (collision_wave(S, nr, nc, nb, delta, tx[2 * e.j], tx[2 * e.j + 1], nx, ny)) continue;
+                if (lane == 0) { tg[e.j] = S.tG[t] + e.d; tpar[e.j] = slot; }
             }
             __syncthreads();  // rewires land before the insert below may overwrite a duplicate slot
         }

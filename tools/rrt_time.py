@@ -1,0 +1,31 @@
+"""Dev probe: RRT* kernel time on the C3 map for a few batch sizes (HIP events around the launch)."""
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+import python_motion_planning_amd as pmp  # noqa: E402
+from python_motion_planning_amd import batch, workloads as wl  # noqa: E402
+
+env = pmp.Map(512, 512)
+rects, circs = wl.c3_map()
+env.update(obs_rect=rects, obs_circ=circs)
+for nq, sn in [(int(a), int(b)) for a, b in (x.split("x") for x in sys.argv[1:])] or [(4, 8192), (4, 65536)]:
+    rnd = np.stack([np.random.RandomState(q).random_sample(3 * sn + 1) for q in range(nq)])
+    rnd_d = torch.as_tensor(rnd, device="cuda")
+    s = np.tile([5.0, 5.0], (nq, 1))
+    g = np.tile([505.0, 505.0], (nq, 1))
+    batch.rrt_batch(env, s[:1], g[:1], rnd_d[:1, : 3 * 64 + 1], 64, star=True)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.time()
+    e0.record()
+    out = batch.rrt_batch(env, s, g, rnd_d, sn, star=True)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1)
+    nn = out["n_nodes"].cpu().numpy()
+    print(f"nq={nq} samples={sn}: {ms:.1f} ms ({ms * 1e3 / sn:.2f} us/iteration), nodes mean {nn.mean():.0f} "
+          f"max {nn.max()}, found {(out['status'].cpu().numpy() == 0).sum()}", flush=True)
