@@ -134,6 +134,25 @@ int pmp_dwa_step_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int
                        double* u, int32_t* best, int32_t* status, int32_t* n_steps, double* hist_pose,
                        double* eval, double* best_traj);
 
+/*
+ * Batched D* static plans.  Replaces DStar.plan (global_planner/graph_search/d_star.py:75-291):
+ * __init__ (every cell NEW, insert(goal, 0)), processState until start is CLOSED, extractPath.
+ * OPEN keeps the reference's list semantics exactly (append-always insert, first-minimal-k
+ * min_state, first-occurrence remove).  One wave64 per query; queries never interact.
+ *   occ_bits as pmp_astar2d_batch; start_xy, goal_xy [nq][2] i32
+ *   cost [nq] f64        extractPath cost (sum of GraphSearcher.cost along the path)
+ *   path [nq][path_cap]  cells x*H + y, start -> goal; path_len [nq]
+ *   n_process [nq] i64   processState calls (len(DStar.EXPAND))
+ *   status [nq]          0 found, 2 path_cap overflow, 3 capacity / max_process exceeded,
+ *                        4 the reference raises (OPEN empties: AttributeError at d_star.py:234)
+ *   max_process          0 = unbounded, else stop with status 3 after that many processState calls
+ * Neighbours outside the grid count as blocked (the reference raises KeyError there; grids built
+ * by Grid.init have obstacle borders, so it never happens for them).
+ */
+int pmp_dstar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H, const int32_t* start_xy,
+                      const int32_t* goal_xy, int nq, double* cost, int32_t* path_len, int32_t* path, int path_cap,
+                      int64_t* n_process, int32_t* status, int64_t max_process);
+
 /* LQR settings (local_planner/lqr.py:35-38): diag Q, diag R, Riccati iteration cap and the
  * signed exit threshold of lqr.py:134.  Reference defaults: q = 1,1,1  r = 1,1  iters 100  eps 0.1. */
 typedef struct {

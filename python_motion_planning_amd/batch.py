@@ -208,6 +208,33 @@ def track_step_batch(kind: str, lp_params, state, goal, path_xy, path_off, iters
     return out
 
 
+def dstar2d_batch(occ, starts, goals, path_cap: int | None = None, max_process: int = 0, stream=None):
+    """Batched DStar.plan (d_star.py:75-156) on one Grid.  occ uint8 [W, H] (x-major).
+    Returns dict of device tensors: cost, path_len, path [nq, path_cap] (cells x*H+y, start -> goal),
+    n_process (processState calls), status (4 = the reference raises: start unreachable)."""
+    torch = _lib.device_check()
+    L = _lib.load_library()
+    ctx = _lib.context()
+    occ = np.asarray(occ)
+    W, H = occ.shape
+    occ_bits = occ_bits_device(occ, torch)
+    s = _dev(torch, starts, torch.int32).reshape(-1, 2)
+    g = _dev(torch, goals, torch.int32).reshape(-1, 2)
+    nq = int(s.shape[0])
+    path_cap = W * H + 1 if path_cap is None else int(path_cap)
+    out = dict(cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
+               path_len=torch.empty(nq, dtype=torch.int32, device="cuda"),
+               path=torch.empty((nq, path_cap), dtype=torch.int32, device="cuda"),
+               n_process=torch.empty(nq, dtype=torch.int64, device="cuda"),
+               status=torch.empty(nq, dtype=torch.int32, device="cuda"))
+    rc = L.pmp_dstar2d_batch(ctx, stream if stream is not None else _lib.stream_ptr(), occ_bits.data_ptr(), W, H,
+                             s.data_ptr(), g.data_ptr(), nq, out["cost"].data_ptr(), out["path_len"].data_ptr(),
+                             out["path"].data_ptr(), path_cap, out["n_process"].data_ptr(), out["status"].data_ptr(),
+                             int(max_process))
+    _lib.check(ctx, rc, "pmp_dstar2d_batch")
+    return out
+
+
 def map_arrays(env, torch=None):
     """Map obstacle lists (env.py:83-117) -> device f64 tensors rect [nr,4], circ [nc,3], bnd [nb,4]."""
     torch = torch or _lib.device_check()

@@ -11,9 +11,10 @@
 // Reopening semantics are the reference's: a pop is skipped if CLOSED holds the cell with g <= node.g
 // (:48-50), a neighbour is skipped if CLOSED holds it with g <= tentative_g (:68-70), CLOSED is
 // (over)written before the goal test (:52-63).  Path is reversed to start -> goal (:105).
+// The heap engine is heap16.h (LDS + HBM spill, wave-parallel pop/push).
 // One wave64 per query (persistent workers pulling an atomic queue); per-worker HBM state:
 // u8 closed-dir per cell (0 = open, dir+1 = closed) + f64 closed g per cell, reset per query.
-#include "pmp_internal.h"
+#include "heap16.h"
 
 namespace {
 
@@ -25,182 +26,31 @@ __device__ __constant__ int8_t c_m3[26][3] = {
     {-1, 0, 1}, {-1, 1, 1}, {0, 1, 1}, {1, 1, 1}, {1, 0, 1}, {1, -1, 1}, {0, -1, 1}, {-1, -1, 1},
     {-1, 0, -1}, {-1, 1, -1}, {0, 1, -1}, {1, 1, -1}, {1, 0, -1}, {1, -1, -1}, {0, -1, -1}, {-1, -1, -1}};
 
-typedef __attribute__((address_space(3))) double lds_f64;
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
+using heap16::Ent;  // g = path cost, a = push counter, b = cm; derived f = g + h, hk = h order key
 
-struct Q3 {
+// (f, h, counter) tuple order of a_star3d.py:40,75, with f and h rebuilt from the cell
+struct Key3 {
     int gx, gy, gz;
     int heur;  // 0 euclidean, 1 manhattan
-};
 
-struct E3 {
-    double g, f;
-    uint32_t seq, cm, hk;
-};
-
-__device__ __forceinline__ void key3(const Q3& q, E3& e)
-{
-    const int x = (int)(e.cm >> 21), y = (int)((e.cm >> 13) & 255u), z = (int)((e.cm >> 5) & 255u);
-    const int dx = abs(q.gx - x), dy = abs(q.gy - y), dz = abs(q.gz - z);
-    if (q.heur == 1) {
-        e.hk = (uint32_t)(dx + dy + dz);
-        e.f = e.g + (double)e.hk;
-    } else {
-        e.hk = (uint32_t)(dx * dx + dy * dy + dz * dz);
-        e.f = e.g + __dsqrt_rn((double)e.hk);
-    }
-}
-
-// (f, h, counter) tuple order (a_star3d.py:40,75)
-__device__ __forceinline__ bool lt3(const E3& a, const E3& b)
-{
-    return (a.f < b.f) | ((a.f == b.f) & ((a.hk < b.hk) | ((a.hk == b.hk) & (a.seq < b.seq))));
-}
-
-struct Heap3 {
-    lds_f64* lg;
-    lds_u32* lseq;
-    lds_u32* lcm;
-    __amdgpu_buffer_rsrc_t spill;  // {g lo, g hi, seq, cm} for positions >= lds_cap
-    int lds_cap;
-};
-
-template <bool SPILL>
-__device__ __forceinline__ void h3load(const Heap3& hp, int p, E3& e)
-{
-    if (!SPILL || p < hp.lds_cap) {
-        e.g = hp.lg[p];
-        e.seq = hp.lseq[p];
-        e.cm = hp.lcm[p];
-    } else {
-        const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(hp.spill, (p - hp.lds_cap) * 16, 0, 0));
-        e.g = __hiloint2double((int)v.y, (int)v.x);
-        e.seq = v.z;
-        e.cm = v.w;
-    }
-}
-
-template <bool SPILL>
-__device__ __forceinline__ void h3store(const Heap3& hp, int p, const E3& e)
-{
-    if (!SPILL || p < hp.lds_cap) {
-        hp.lg[p] = e.g;
-        hp.lseq[p] = e.seq;
-        hp.lcm[p] = e.cm;
-    } else {
-        const uint64_t b = (uint64_t)__double_as_longlong(e.g);
-        const uint4 v = make_uint4((uint32_t)b, (uint32_t)(b >> 32), e.seq, e.cm);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
-                                               hp.spill, (p - hp.lds_cap) * 16, 0, 0);
-    }
-}
-
-__device__ __forceinline__ void wsync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
-
-__device__ __forceinline__ E3 rl_e3(const E3& e, int lane)
-{
-    E3 r;
-    r.g = rl_f64(e.g, lane);
-    r.f = rl_f64(e.f, lane);
-    r.seq = rl_u32(e.seq, lane);
-    r.cm = rl_u32(e.cm, lane);
-    r.hk = rl_u32(e.hk, lane);
-    return r;
-}
-
-// extract-min on a heap of n (>0, already decremented) entries, old last element at position n
-template <bool SPILL>
-__device__ __forceinline__ void pop3(const Heap3& hp, const Q3& q, int n, E3& root, int lane, int jl, int ol)
-{
-    n = uni(n);
-    E3 last;
-    if (SPILL) {
-        h3load<SPILL>(hp, n, last);
-    } else {
-        h3load<false>(hp, n, last);
-    }
-    last.g = rl_f64(last.g, 0);
-    last.seq = rl_u32(last.seq, 0);
-    last.cm = rl_u32(last.cm, 0);
-    key3(q, last);
-    int hole = 0;
-    bool first = true;
-    for (;;) {
-        const int li = ((hole + 1) << jl) - 1 + 2 * ol;
-        const bool vl = (lane < 63) & (li < n);
-        const bool vr = (lane < 63) & (li + 1 < n);
-        E3 L, R;
-        L.g = R.g = 0.0;
-        L.seq = R.seq = 0u;
-        L.cm = R.cm = 0u;
-        if constexpr (SPILL) {
-            if (vl) h3load<true>(hp, li, L);
-            if (vr) h3load<true>(hp, li + 1, R);
+    __device__ __forceinline__ void derive(Ent& e) const
+    {
+        const int x = (int)(e.b >> 21), y = (int)((e.b >> 13) & 255u), z = (int)((e.b >> 5) & 255u);
+        const int dx = abs(gx - x), dy = abs(gy - y), dz = abs(gz - z);
+        if (heur == 1) {
+            e.hk = (uint32_t)(dx + dy + dz);
+            e.f = e.g + (double)e.hk;
         } else {
-            h3load<false>(hp, vl ? li : 0, L);
-            h3load<false>(hp, vr ? li + 1 : 0, R);
+            e.hk = (uint32_t)(dx * dx + dy * dy + dz * dz);
+            e.f = e.g + __dsqrt_rn((double)e.hk);
         }
-        key3(q, L);
-        key3(q, R);
-        const uint64_t dmask = ballot(vr & lt3(R, L));        // total order: the smaller child
-        const uint64_t mlmask = ballot(vl & lt3(L, last));   // moves up while child < last
-        const uint64_t mrmask = ballot(vr & lt3(R, last));
-        int cur = uni(hole), oc = 0;
-        uint64_t mover = 0, movr = 0;
-        bool go = true;
-#pragma unroll
-        for (int lv = 1; lv <= 6; lv++) {
-            const int c = 2 * cur + 1;
-            const int pl = (1 << (lv - 1)) - 1 + oc;
-            const int r = (int)((dmask >> pl) & 1ull);
-            const uint64_t mm = r ? mrmask : mlmask;
-            go = go & (c < n) & (((mm >> pl) & 1ull) != 0ull);
-            if (go) {
-                mover |= 1ull << pl;
-                movr |= (uint64_t)r << pl;
-                cur = c + r;
-                oc = 2 * oc + r;
-            }
-        }
-        if ((mover >> lane) & 1ull) {
-            const bool rr = (movr >> lane) & 1ull;
-            h3store<SPILL>(hp, ((rr ? li + 1 : li) - 1) >> 1, rr ? R : L);
-        }
-        if (first && (mover & 1ull)) root = rl_e3((movr & 1ull) ? R : L, 0);
-        first = false;
-        hole = cur;
-        if (!go) break;
-        wsync();
     }
-    if (lane == 0) h3store<SPILL>(hp, hole, last);
-    if (hole == 0) root = last;
-    wsync();
-}
 
-template <bool SPILL>
-__device__ __forceinline__ void push3(const Heap3& hp, const Q3& q, int n, const E3& it, E3& root, int lane)
-{
-    n = uni(n);
-    const int np1 = n + 1;
-    const int depth = 31 - __clz(np1);
-    const bool valid = lane < depth;
-    const int apos = valid ? (np1 >> (lane + 1)) - 1 : 0;
-    E3 a;
-    a.g = 0.0;
-    a.seq = a.cm = 0u;
-    if constexpr (SPILL) {
-        if (valid) h3load<true>(hp, apos, a);
-    } else {
-        h3load<false>(hp, apos, a);
+    static __device__ __forceinline__ bool lt(const Ent& a, const Ent& b)
+    {
+        return (a.f < b.f) | ((a.f == b.f) & ((a.hk < b.hk) | ((a.hk == b.hk) & (a.a < b.a))));
     }
-    key3(q, a);
-    const int t = __popcll(ballot(valid & lt3(it, a)));
-    if (lane < t) h3store<SPILL>(hp, (np1 >> lane) - 1, a);
-    const int ipos = (np1 >> t) - 1;
-    if (lane == 0) h3store<SPILL>(hp, ipos, it);
-    if (ipos == 0) root = it;
-    wsync();
-}
+};
 
 __device__ __forceinline__ bool occ3(const uint32_t* occ, int X, int Y, int Z, int x, int y, int z)
 {
@@ -222,19 +72,12 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
     const int worker = blockIdx.x;
     const size_t ncell = (size_t)X * Y * Z;
     const size_t words = (ncell + 31) / 32;
-    Heap3 hp;
-    hp.lg = (lds_f64*)smem;
-    hp.lseq = (lds_u32*)(smem + (size_t)8 * lds_cap);
-    hp.lcm = (lds_u32*)(smem + (size_t)12 * lds_cap);
-    hp.lds_cap = lds_cap;
-    {
-        const size_t spill_n = (size_t)(heap_cap > lds_cap ? heap_cap - lds_cap : 0);
-        hp.spill = __builtin_amdgcn_make_buffer_rsrc(spill_all + (size_t)worker * spill_n, 0, (int)(spill_n * 16), 0x00020000);
-    }
+    const size_t spill_n = (size_t)(heap_cap > lds_cap ? heap_cap - lds_cap : 0);
+    const heap16::Heap hp = heap16::make_heap(smem, lds_cap, spill_all + (size_t)worker * spill_n, spill_n);
     uint8_t* cdir = cdir_all + (size_t)worker * ncell;
     double* cg = cg_all + (size_t)worker * ncell;
-    const int pop_jl = 32 - __clz(lane + 1);
-    const int pop_ol = lane + 1 - (1 << (pop_jl - 1));
+    int pop_jl, pop_ol;
+    heap16::pop_lane_consts(lane, pop_jl, pop_ol);
     // neighbour lane m < 26: motion m (env3d.py:56-70)
     const int mdx = lane < 26 ? c_m3[lane][0] : 0, mdy = lane < 26 ? c_m3[lane][1] : 0, mdz = lane < 26 ? c_m3[lane][2] : 0;
     const int mchg = (mdx != 0) + (mdy != 0) + (mdz != 0);
@@ -248,9 +91,9 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
         const int q = qi;
         const uint32_t* occ = occ_all + (per_query ? (size_t)q * words : 0);
         for (size_t i = lane; i < ncell; i += 64) cdir[i] = 0;
-        wsync();
+        heap16::wsync();
         const int sx = start_xyz[3 * q], sy = start_xyz[3 * q + 1], sz = start_xyz[3 * q + 2];
-        Q3 qc;
+        Key3 qc;
         qc.gx = goal_xyz[3 * q];
         qc.gy = goal_xyz[3 * q + 1];
         qc.gz = goal_xyz[3 * q + 2];
@@ -269,13 +112,13 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
         }
         const uint32_t scm = (((uint32_t)sx << 16) | ((uint32_t)sy << 8) | (uint32_t)sz) << 5 | 26u;
         const uint32_t goal_xyz24 = ((uint32_t)qc.gx << 16) | ((uint32_t)qc.gy << 8) | (uint32_t)qc.gz;
-        E3 root;  // start: g = 0, h = heuristic(start), counter 0 (a_star3d.py:38-41)
+        Ent root;  // start: g = 0, h = heuristic(start), counter 0 (a_star3d.py:38-41)
         root.g = 0.0;
-        root.seq = 0u;
-        root.cm = scm;
-        key3(qc, root);
-        if (lane == 0) h3store<true>(hp, 0, root);
-        wsync();
+        root.a = 0u;
+        root.b = scm;
+        qc.derive(root);
+        if (lane == 0) heap16::store<true>(hp, 0, root);
+        heap16::wsync();
         int n = 1;
         uint32_t seq = 1;
         int64_t npush = 1, npop = 0, niter = 0;
@@ -283,11 +126,11 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
         double goal_cost = __builtin_inf();
 
         while (n > 0) {
-            const E3 node = root;
+            const Ent node = root;
             npop++;
             n -= 1;
-            const int x = (int)(node.cm >> 21), y = (int)((node.cm >> 13) & 255u), z = (int)((node.cm >> 5) & 255u);
-            const int ndir = (int)(node.cm & 31u);
+            const int x = (int)(node.b >> 21), y = (int)((node.b >> 13) & 255u), z = (int)((node.b >> 5) & 255u);
+            const int ndir = (int)(node.b & 31u);
             const uint32_t lin = ((uint32_t)x * (uint32_t)Y + (uint32_t)y) * (uint32_t)Z + (uint32_t)z;
             // ---- HBM round (issued before the pop): neighbour collision + CLOSED state, node's CLOSED state
             const int nx = x + mdx, ny = y + mdy, nz = z + mdz;
@@ -316,8 +159,8 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
             }
             // ---- pop
             if (n > 0) {
-                if (n < lds_cap) pop3<false>(hp, qc, n, root, lane, pop_jl, pop_ol);
-                else pop3<true>(hp, qc, n, root, lane, pop_jl, pop_ol);
+                if (n < lds_cap) heap16::pop<Key3, false>(hp, qc, n, root, lane, pop_jl, pop_ol);
+                else heap16::pop<Key3, true>(hp, qc, n, root, lane, pop_jl, pop_ol);
             }
             // best_closed check (a_star3d.py:48-50)
             const bool sclosed = rl_u32(ncd, 26) != 0u;
@@ -332,9 +175,9 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
                 cg[lin] = node.g;
             }
             if (!sclosed) nexp++;
-            if ((node.cm >> 5) == goal_xyz24) {  // goal check (:59-63), path via CLOSED parents
+            if ((node.b >> 5) == goal_xyz24) {  // goal check (:59-63), path via CLOSED parents
                 st = PMP_FOUND;
-                wsync();
+                heap16::wsync();
                 if (lane == 0) {
                     int cx = x, cy = y, cz = z, len = 1;
                     double cost = 0.0;
@@ -370,20 +213,20 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
             const double tg = node.g + mcost;
             const bool ok = lane < 26 && !coll && !(ncd != 0u && tg >= ncg);
             uint64_t vm = ballot(ok);
-            E3 item;
+            Ent item;
             item.g = tg;
-            item.seq = 0u;
-            item.cm = ((((uint32_t)nx & 255u) << 16) | (((uint32_t)ny & 255u) << 8) | ((uint32_t)nz & 255u)) << 5 | (uint32_t)(lane < 26 ? lane : 0);
-            key3(qc, item);
+            item.a = 0u;
+            item.b = ((((uint32_t)nx & 255u) << 16) | (((uint32_t)ny & 255u) << 8) | ((uint32_t)nz & 255u)) << 5 | (uint32_t)(lane < 26 ? lane : 0);
+            qc.derive(item);
             bool overflow = false;
             while (vm) {
                 const int m = __ffsll((long long)vm) - 1;
                 vm &= vm - 1;
                 if (n >= heap_cap) { overflow = true; break; }
-                E3 it = rl_e3(item, m);
-                it.seq = seq++;
-                if (n < lds_cap) push3<false>(hp, qc, n, it, root, lane);
-                else push3<true>(hp, qc, n, it, root, lane);
+                Ent it = heap16::rl_ent(item, m);
+                it.a = seq++;
+                if (n < lds_cap) heap16::push<Key3, false>(hp, qc, n, it, root, lane);
+                else heap16::push<Key3, true>(hp, qc, n, it, root, lane);
                 n += 1;
                 npush++;
             }
@@ -404,7 +247,7 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
                 counters[4 * q + 3] = maxn;
             }
         }
-        wsync();
+        heap16::wsync();
     }
 }
 

@@ -1,0 +1,190 @@
+// Wave64 binary min-heap of 16-byte entries for strictly (totally) ordered keys, shared by the
+// 3D A* (astar3d.hip) and D* (dstar.hip) kernels.  Positions < lds_cap live in LDS as three SoA
+// arrays (f64 g, u32 a, u32 b); deeper positions spill to HBM through buffer instructions (one
+// 16 B record each).  With a total order any correct heap pops the same sequence, so the shape is
+// free; the operations are organised for one wave:
+//   pop:  the hole walks down 6 levels per LDS round -- 63 lanes each load one sibling pair of the
+//         next 6 levels, three ballots give "right child is smaller" and "child < last" per pair,
+//         the walk over those masks is scalar, and the movers store in parallel;
+//   push: the ancestors load in one round; the "less than the new item" set is a prefix of the
+//         root path, so a ballot popcount gives the sift-up distance.
+// The key is supplied by a policy type K: K::derive(e) fills e.f / e.hk from the stored fields and
+// K::lt(x, y) is the strict order.
+#pragma once
+#include "pmp_internal.h"
+
+namespace heap16 {
+
+typedef __attribute__((address_space(3))) double lds_f64;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+struct Ent {
+    double g;       // stored
+    uint32_t a, b;  // stored
+    double f;       // derived (K::derive)
+    uint32_t hk;    // derived
+};
+
+struct Heap {
+    lds_f64* lg;
+    lds_u32* la;
+    lds_u32* lb;
+    __amdgpu_buffer_rsrc_t spill;  // {g lo, g hi, a, b} for positions >= lds_cap
+    int lds_cap;
+};
+
+__device__ __forceinline__ Heap make_heap(unsigned char* smem, int lds_cap, uint4* spill_base, size_t spill_n)
+{
+    Heap hp;
+    hp.lg = (lds_f64*)smem;
+    hp.la = (lds_u32*)(smem + (size_t)8 * lds_cap);
+    hp.lb = (lds_u32*)(smem + (size_t)12 * lds_cap);
+    hp.lds_cap = lds_cap;
+    hp.spill = __builtin_amdgcn_make_buffer_rsrc(spill_base, 0, (int)(spill_n * 16), 0x00020000);
+    return hp;
+}
+
+template <bool SPILL>
+__device__ __forceinline__ void load(const Heap& hp, int p, Ent& e)
+{
+    if (!SPILL || p < hp.lds_cap) {
+        e.g = hp.lg[p];
+        e.a = hp.la[p];
+        e.b = hp.lb[p];
+    } else {
+        const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(hp.spill, (p - hp.lds_cap) * 16, 0, 0));
+        e.g = __hiloint2double((int)v.y, (int)v.x);
+        e.a = v.z;
+        e.b = v.w;
+    }
+}
+
+template <bool SPILL>
+__device__ __forceinline__ void store(const Heap& hp, int p, const Ent& e)
+{
+    if (!SPILL || p < hp.lds_cap) {
+        hp.lg[p] = e.g;
+        hp.la[p] = e.a;
+        hp.lb[p] = e.b;
+    } else {
+        const uint64_t bits = (uint64_t)__double_as_longlong(e.g);
+        const uint4 v = make_uint4((uint32_t)bits, (uint32_t)(bits >> 32), e.a, e.b);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
+                                               hp.spill, (p - hp.lds_cap) * 16, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void wsync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+__device__ __forceinline__ Ent rl_ent(const Ent& e, int lane)
+{
+    Ent r;
+    r.g = rl_f64(e.g, lane);
+    r.f = rl_f64(e.f, lane);
+    r.a = rl_u32(e.a, lane);
+    r.b = rl_u32(e.b, lane);
+    r.hk = rl_u32(e.hk, lane);
+    return r;
+}
+
+// Per-lane constants of the 6-level pop chunk: lane l < 63 owns the sibling pair at level jl,
+// offset ol of the chunk below the hole.
+__device__ __forceinline__ void pop_lane_consts(int lane, int& jl, int& ol)
+{
+    jl = 32 - __clz(lane + 1);
+    ol = lane + 1 - (1 << (jl - 1));
+}
+
+// Extract-min on a heap whose size was already decremented to n (> 0); the old last element sits
+// at position n.  `root` receives the new minimum (wave-uniform).
+template <class K, bool SPILL>
+__device__ __forceinline__ void pop(const Heap& hp, const K& key, int n, Ent& root, int lane, int jl, int ol)
+{
+    n = uni(n);
+    Ent last;
+    load<SPILL>(hp, n, last);
+    last.g = rl_f64(last.g, 0);
+    last.a = rl_u32(last.a, 0);
+    last.b = rl_u32(last.b, 0);
+    key.derive(last);
+    int hole = 0;
+    bool first = true;
+    for (;;) {
+        const int li = ((hole + 1) << jl) - 1 + 2 * ol;
+        const bool vl = (lane < 63) & (li < n);
+        const bool vr = (lane < 63) & (li + 1 < n);
+        Ent L, R;
+        L.g = R.g = 0.0;
+        L.a = R.a = 0u;
+        L.b = R.b = 0u;
+        if constexpr (SPILL) {
+            if (vl) load<true>(hp, li, L);
+            if (vr) load<true>(hp, li + 1, R);
+        } else {
+            load<false>(hp, vl ? li : 0, L);
+            load<false>(hp, vr ? li + 1 : 0, R);
+        }
+        key.derive(L);
+        key.derive(R);
+        const uint64_t dmask = ballot(vr & K::lt(R, L));       // the smaller child
+        const uint64_t mlmask = ballot(vl & K::lt(L, last));  // moves up while child < last
+        const uint64_t mrmask = ballot(vr & K::lt(R, last));
+        int cur = uni(hole), oc = 0;
+        uint64_t mover = 0, movr = 0;
+        bool go = true;
+#pragma unroll
+        for (int lv = 1; lv <= 6; lv++) {
+            const int c = 2 * cur + 1;
+            const int pl = (1 << (lv - 1)) - 1 + oc;
+            const int r = (int)((dmask >> pl) & 1ull);
+            const uint64_t mm = r ? mrmask : mlmask;
+            go = go & (c < n) & (((mm >> pl) & 1ull) != 0ull);
+            if (go) {
+                mover |= 1ull << pl;
+                movr |= (uint64_t)r << pl;
+                cur = c + r;
+                oc = 2 * oc + r;
+            }
+        }
+        if ((mover >> lane) & 1ull) {
+            const bool rr = (movr >> lane) & 1ull;
+            store<SPILL>(hp, ((rr ? li + 1 : li) - 1) >> 1, rr ? R : L);
+        }
+        if (first && (mover & 1ull)) root = rl_ent((movr & 1ull) ? R : L, 0);
+        first = false;
+        hole = cur;
+        if (!go) break;
+        wsync();
+    }
+    if (lane == 0) store<SPILL>(hp, hole, last);
+    if (hole == 0) root = last;
+    wsync();
+}
+
+// Insert `it` (wave-uniform, derived) into a heap of n entries; `root` is updated if it becomes the minimum.
+template <class K, bool SPILL>
+__device__ __forceinline__ void push(const Heap& hp, const K& key, int n, const Ent& it, Ent& root, int lane)
+{
+    n = uni(n);
+    const int np1 = n + 1;
+    const int depth = 31 - __clz(np1);
+    const bool valid = lane < depth;
+    const int apos = valid ? (np1 >> (lane + 1)) - 1 : 0;
+    Ent a;
+    a.g = 0.0;
+    a.a = a.b = 0u;
+    if constexpr (SPILL) {
+        if (valid) load<true>(hp, apos, a);
+    } else {
+        load<false>(hp, apos, a);
+    }
+    key.derive(a);
+    const int t = __popcll(ballot(valid & K::lt(it, a)));
+    if (lane < t) store<SPILL>(hp, (np1 >> lane) - 1, a);
+    const int ipos = (np1 >> t) - 1;
+    if (lane == 0) store<SPILL>(hp, ipos, it);
+    if (ipos == 0) root = it;
+    wsync();
+}
+
+}  // namespace heap16

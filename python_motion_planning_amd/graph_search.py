@@ -98,6 +98,40 @@ class AStar(GraphSearcher):
         return batch.astar2d_batch(occ, starts, goals, heuristic_type, **kw)
 
 
+class DStar(GraphSearcher):
+    """Dynamic A* (d_star.py:37-291) -- the static plan (processState until the start is CLOSED)
+    runs in the gfx950 kernel dstar.hip with the reference's list-semantics OPEN."""
+
+    def __init__(self, start: tuple, goal: tuple, env: Grid) -> None:
+        super().__init__(start, goal, env, None)
+        self.EXPAND = []
+
+    def __str__(self) -> str:
+        return "Dynamic A*(D*)"
+
+    def plan(self) -> tuple:
+        """(cost, path start->goal, None) (d_star.py:75-89); raises AttributeError when the start is
+        unreachable, like the reference (min_k of an empty OPEN, :234)."""
+        occ = self.env.occupancy()
+        W, H = occ.shape
+        r = batch.dstar2d_batch(occ, np.array([self.start.current]), np.array([self.goal.current]))
+        st = int(r["status"][0])
+        self.n_process = int(r["n_process"][0])
+        if st == 4:
+            raise AttributeError("'NoneType' object has no attribute 'k'")
+        if st != 0:
+            raise RuntimeError(f"D* kernel status {st}")
+        cells = r["path"][0, : int(r["path_len"][0])].cpu().numpy()
+        return float(r["cost"][0]), [(int(c) // H, int(c) % H) for c in cells], None
+
+    def run(self):
+        return self.plan()
+
+    @staticmethod
+    def plan_batch(occ: np.ndarray, starts, goals, **kw):
+        return batch.dstar2d_batch(occ, starts, goals, **kw)
+
+
 class GraphSearcher3D:
     """global_planner/graph_search/graph_search_3d.py:11-107 (Planner3D base)."""
 
