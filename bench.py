@@ -1,11 +1,14 @@
-"""Benchmark of the hot path (BASELINE.json): batched A* plans/s on a 1024^2 Grid (config 2).
+"""Benchmark of the hot path (BASELINE.json): batched A* plans/s on a 1024^2 Grid (config 2) as the
+headline, and the other configs as secondary legs in the same JSON line.
 
 python bench.py --gpus N --steps K --warmup W      (N>1: launched by torch.distributed.run)
 
-One step = one pass of the hot path over one batch: 4096 start/goal pairs on the C2 grid
+Headline step = one pass of the hot path over one batch: 4096 start/goal pairs on the C2 grid
 (SURVEY.md §8(d) generator), inputs resident in HBM, outputs (cost, path, n_expanded, status)
-written to HBM.  Multi-GPU: weak scaling, rank r plans its own 4096 pairs (pair seed 1 + r) on
-the same grid; no collective on the data path.  Rank 0 prints one JSON line.
+written to HBM.  Secondary legs (--legs): the H=30 x 4096-sample control step (C4, DWA form), RRT*
+on the C3 512^2 map (65,536 samples), 3D A* on C5 (8192 queries), and the LQR / MPC tracking steps
+on the C4 agents.  Multi-GPU: weak scaling, every rank runs its own shard (rank-offset seeds) of
+every leg; no collective on the data path.  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -127,6 +130,218 @@ def control_leg(args, torch, dist, world, rank):
             "cpu_baseline": cpu}
 
 
+def timed(torch, dist, fn, steps, stream=None):
+    """Barrier + sync, run `steps` launches with HIP events around each (on `stream`), barrier +
+    sync; returns (wall seconds, max over ranks; mean event ms per launch)."""
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = []
+    t0 = time.perf_counter()
+    for i in range(steps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if stream is None:
+            e0.record()
+        else:
+            e0.record(stream)
+        fn(i)
+        if stream is None:
+            e1.record()
+        else:
+            e1.record(stream)
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    if dist:
+        t = torch.tensor([elapsed, kern_ms], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0].item()), float(t[1].item())
+    return elapsed, kern_ms
+
+
+def cpu_threads():
+    return min(16, os.cpu_count() or 1)
+
+
+def rrt_leg(args, torch, dist, world, rank):
+    """C3: RRT* on the 512^2 Map (40 rects + 40 circles, default_rng(7)), start (5,5), goal (505,505),
+    65,536 samples, max_dist 0.5, r 10, goal rate 0.05; query q draws from np.random.seed(q) (rank
+    offset).  One timed step = one launch over all queries of the rank."""
+    import python_motion_planning_amd as pmp
+    from python_motion_planning_amd import batch, workloads as wl
+
+    nq, sn = args.rrt_queries, args.rrt_samples
+    env = pmp.Map(512, 512)
+    rects, circs = wl.c3_map()
+    env.update(obs_rect=rects, obs_circ=circs)
+    seeds = np.arange(nq) + rank * nq
+    rnd = np.stack([np.random.RandomState(int(q)).random_sample(3 * sn + 1) for q in seeds])
+    rnd_d = torch.as_tensor(rnd, device="cuda")
+    starts, goals = np.tile([5.0, 5.0], (nq, 1)), np.tile([505.0, 505.0], (nq, 1))
+    out = batch.rrt_batch(env, starts, goals, rnd_d, sn, star=True, counters=True)  # warmup + counters
+    torch.cuda.synchronize()
+    ctr = out["counters"].cpu().numpy()
+    status = out["status"].cpu().numpy()
+    assert np.isin(status, (0, 1)).all(), f"unexpected RRT* statuses {np.unique(status)}"
+    elapsed, kern_ms = timed(torch, dist, lambda i: batch.rrt_batch(env, starts, goals, rnd_d, sn, star=True),
+                             args.rrt_steps)
+    # SURVEY.md §8(d) C3: per plan sum_i 16 n_i (node coordinates scanned) + 8 k_i (g of in-radius nodes)
+    alg_bytes = float(16.0 * ctr[:, 1].sum() + 8.0 * ctr[:, 2].sum())
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+
+        th = cpu_threads()
+        ns = min(args.rrt_cpu_sample, nq)
+        t = time.perf_counter()
+        ref = O.rrt_batch(True, rects, circs, 512, 512, starts[:ns], goals[:ns], rnd[:ns], sn, nthreads=th)
+        dt = time.perf_counter() - t
+        assert np.array_equal(ref["status"], status[:ns]) and np.array_equal(ref["n_nodes"], out["n_nodes"][:ns].cpu().numpy())
+        cpu = {"value": ns / dt, "unit": "plans/s", "cores": th, "kind": "port",
+               "sample": f"first {ns} C3 queries at the full 65,536 samples, C restatement of RRT* "
+                         f"(oracle/pmp_oracle.c, same O(N^2) loops as the reference) with OpenMP over queries, "
+                         f"{dt:.1f} s wall"}
+    return {"metric": "RRT* plans/sec on 512x512 Map, 65536 samples", "value": nq * args.rrt_steps * world / elapsed,
+            "unit": "plans/s", "queries_per_gpu": nq, "steps": args.rrt_steps,
+            "ms_per_step": elapsed / args.rrt_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
+            "config": {"workload": "C3: Map(512,512), 40 rects + 40 circles (default_rng(7)), (5,5)->(505,505), "
+                                   "65536 samples, max_dist 0.5, r 10, goal rate 0.05"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "algorithmic_bytes_per_launch": alg_bytes},
+            "detail": {"found": int((status == 0).sum()), "mean_nodes": float(out["n_nodes"].float().mean().item()),
+                       "iterations_per_launch": int(ctr[:, 0].sum()), "nodes_scanned_per_launch": int(ctr[:, 1].sum()),
+                       "collision_tests_per_launch": int(ctr[:, 3].sum())},
+            "cpu_baseline": cpu}
+
+
+def astar3d_leg(args, torch, dist, world, rank):
+    """C5: AStar3D on Grid3D(26,20,16) door scenario, 8192 queries per GPU (random.seed(i) pairs,
+    safety bubbles carved per query, so each query has its own occupancy)."""
+    from python_motion_planning_amd import _lib, batch, workloads as wl
+
+    nq = args.a3_queries
+    occ, s, g = wl.c5_workload(nq, first_seed=rank * nq)
+    X, Y, Z = occ.shape[1:]
+    words = np.stack([batch.pack_bits(o) for o in occ])
+    occ_d = torch.as_tensor(np.ascontiguousarray(words).view(np.int32), device="cuda")
+    s_d = torch.as_tensor(s, device="cuda")
+    g_d = torch.as_tensor(g, device="cuda")
+    L = _lib.load_library()
+    ctx = _lib.context()
+    cap = X * Y * Z + 1
+    cost = torch.empty(nq, dtype=torch.float64, device="cuda")
+    plen = torch.empty(nq, dtype=torch.int32, device="cuda")
+    path = torch.empty((nq, cap), dtype=torch.int32, device="cuda")
+    nexp = torch.empty(nq, dtype=torch.int32, device="cuda")
+    st = torch.empty(nq, dtype=torch.int32, device="cuda")
+    ctr = torch.empty((nq, 4), dtype=torch.int64, device="cuda")
+
+    def run(i, counters=None):
+        rc = L.pmp_astar3d_batch(ctx, _lib.stream_ptr(), occ_d.data_ptr(), 1, X, Y, Z, 0, s_d.data_ptr(), g_d.data_ptr(),
+                                 nq, cost.data_ptr(), plen.data_ptr(), path.data_ptr(), cap, nexp.data_ptr(), None, 0,
+                                 counters, st.data_ptr())
+        if rc:
+            _lib.check(ctx, rc, "pmp_astar3d_batch")
+
+    run(0, ctr.data_ptr())
+    torch.cuda.synchronize()
+    c = ctr.cpu().numpy()
+    elapsed, kern_ms = timed(torch, dist, run, args.a3_steps)
+    # SURVEY.md §8(d) C5: per plan 55*E3 + 16*(P3 + Q3)
+    alg_bytes = float(np.sum(55.0 * c[:, 2] + 16.0 * (c[:, 0] + c[:, 1])))
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+
+        th = cpu_threads()
+        t = time.perf_counter()
+        rc_, rs_ = O.astar3d_batch(occ, s, g, nthreads=th)
+        dt = time.perf_counter() - t
+        assert np.array_equal(rc_, cost.cpu().numpy()), "GPU/oracle 3D cost mismatch"
+        cpu = {"value": nq / dt, "unit": "plans/s", "cores": th, "kind": "port",
+               "sample": f"all {nq} C5 queries, C restatement of AStar3D (oracle/pmp_oracle.c) with OpenMP over "
+                         f"queries, {dt:.1f} s wall"}
+    return {"metric": "3D A* plans/sec, Grid3D(26,20,16) door scenario, 8192 queries", "value": nq * args.a3_steps * world / elapsed,
+            "unit": "plans/s", "queries_per_gpu": nq, "steps": args.a3_steps,
+            "ms_per_step": elapsed / args.a3_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
+            "config": {"workload": "C5: Grid3D(26,20,16) door, random.seed(i) pairs, safety bubbles r=1, euclidean"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": alg_bytes},
+            "detail": {"expansions_per_launch": int(c[:, 2].sum()), "pushes_per_launch": int(c[:, 0].sum()),
+                       "max_heap_entries": int(c[:, 3].max())},
+            "cpu_baseline": cpu}
+
+
+def track_leg(args, torch, dist, world, rank, kind):
+    """LQR / MPC tracking (lqr.py:58-86 / mpc.py:66-94) for the C4 agents: one timed step = one launch
+    running `iters` plan iterations of every agent (MPC at p = 30, m = 8, ADMM to 1e-9)."""
+    from python_motion_planning_amd import _lib, batch, local_planner, workloads as wl
+
+    na, iters = args.agents, args.track_iters
+    occ, states, goals = wl.c4_workload(na, seed=2 + rank)
+    r = batch.astar2d_batch(occ, states[:, :2].astype(np.int32), np.tile([45, 25], (na, 1)).astype(np.int32),
+                            path_cap=2048)
+    pl, P = r["path_len"].cpu().numpy(), r["path"].cpu().numpy()
+    Hg = occ.shape[1]
+    paths = [np.column_stack([P[i, : pl[i]][::-1] // Hg, P[i, : pl[i]][::-1] % Hg]).astype(np.float64)
+             for i in range(na)]
+    xy, off = batch.pack_paths(paths)
+    lp = _lib.LPParams.from_params(local_planner.LocalPlanner.DEFAULTS)
+    kw = dict(lqr_params=_lib.LQRParams.make()) if kind == "lqr" else dict(mpc_params=_lib.MPCParams.make(p=30))
+    st0 = torch.tensor(states, dtype=torch.float64, device="cuda")
+    st = st0.clone()
+    up = torch.zeros((na, 2), dtype=torch.float64, device="cuda")
+    gd = torch.tensor(goals, dtype=torch.float64, device="cuda")
+    xyd = torch.tensor(xy, dtype=torch.float64, device="cuda")
+    offd = torch.tensor(off, dtype=torch.int32, device="cuda")
+    o = batch.track_step_batch(kind, lp, st, gd, xyd, offd, iters=iters, u_p=up, **kw)
+    torch.cuda.synchronize()
+    stepped = int(o["n_steps"].sum().item())
+    admm = int(o["admm_iters"].sum().item())
+
+    def run(i):
+        st.copy_(st0)
+        up.zero_()
+        batch.track_step_batch(kind, lp, st, gd, xyd, offd, iters=iters, u_p=up, **kw)
+
+    elapsed, kern_ms = timed(torch, dist, run, args.track_steps)
+    if kind == "mpc":
+        # per ADMM iteration ~ 16x16 inverse matvec (512) + scans/projections (~150); assembly 2*16*16*3p (MFMA)
+        flops = admm * 662.0 + stepped * 2 * 16 * 16 * 90
+    else:
+        flops = stepped * 1200.0  # 3x3 Riccati update, 2x2 inverse, K e (lqr.py:116-141)
+    achieved_tf = flops / (kern_ms * 1e-3) / 1e12
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+
+        th = cpu_threads()
+        t = time.perf_counter()
+        ost, oup, ou, ostat, onst, tot = O.track_batch(
+            kind, xy, off, goals, states, iters=iters, nthreads=th,
+            mpc=O.MPCParams.default(p=30, eps_abs=1e-9, eps_rel=1e-9))
+        dt = time.perf_counter() - t
+        assert int(tot) == stepped, "GPU/oracle step-count mismatch"
+        cpu = {"value": tot / dt, "unit": "agent-steps/s", "cores": th, "kind": "port",
+               "sample": f"all {na} C4 agents x {iters} plan iterations, C restatement (oracle/pmp_oracle.c) with "
+                         f"OpenMP over agents, {dt:.2f} s wall"}
+    name = "LQR" if kind == "lqr" else "MPC (p=30, m=8, ADMM QP)"
+    return {"metric": f"{name} tracking agent-steps/sec", "value": stepped * args.track_steps * world / elapsed,
+            "unit": "agent-steps/s", "agents_per_gpu": na, "iterations_per_launch": iters, "steps": args.track_steps,
+            "ms_per_step": elapsed / args.track_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
+            "config": {"workload": f"C4 agents on the README grid, {iters} LQR/MPC plan iterations per launch"},
+            "roofline": {"bound": "fp64-valu", "achieved": achieved_tf, "peak": 78.6, "unit": "TFLOP/s",
+                         "frac": achieved_tf / 78.6, "traffic": None},
+            "detail": {"agent_steps_per_launch": stepped, "admm_iterations_per_launch": admm},
+            "cpu_baseline": cpu}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -138,6 +353,16 @@ def main():
     ap.add_argument("--agents", type=int, default=256, help="C4 agents per GPU (control-step leg)")
     ap.add_argument("--control-steps", type=int, default=20, help="timed control steps")
     ap.add_argument("--workers", type=int, default=2048, help="persistent A* workers (waves) per launch")
+    ap.add_argument("--legs", default="dwa,rrt,astar3d,lqr,mpc",
+                    help="secondary legs to run (comma list of dwa, rrt, astar3d, lqr, mpc; 'none' for none)")
+    ap.add_argument("--rrt-queries", type=int, default=256)
+    ap.add_argument("--rrt-samples", type=int, default=65536)
+    ap.add_argument("--rrt-steps", type=int, default=2)
+    ap.add_argument("--rrt-cpu-sample", type=int, default=16)
+    ap.add_argument("--a3-queries", type=int, default=8192)
+    ap.add_argument("--a3-steps", type=int, default=3)
+    ap.add_argument("--track-iters", type=int, default=20)
+    ap.add_argument("--track-steps", type=int, default=5)
     ap.add_argument("--streams", type=int, default=3,
                     help="batches in flight: consecutive steps go to different HIP streams (own scratch "
                          "context each), so one batch's long-query tail overlaps the next batch")
@@ -249,7 +474,18 @@ def main():
                "sample": f"first {ns} of the 4096 C2 pairs, C restatement (oracle/pmp_oracle.c) with OpenMP over "
                          f"queries, {dt:.1f} s wall"}
 
-    control = control_leg(args, torch, dist, world, rank)
+    legs = [x for x in args.legs.split(",") if x and x != "none"]
+    secondary = {}
+    if "dwa" in legs:
+        secondary["mpc_sampled_dwa"] = control_leg(args, torch, dist, world, rank)
+    if "rrt" in legs:
+        secondary["rrt_star"] = rrt_leg(args, torch, dist, world, rank)
+    if "astar3d" in legs:
+        secondary["astar3d"] = astar3d_leg(args, torch, dist, world, rank)
+    if "lqr" in legs:
+        secondary["lqr"] = track_leg(args, torch, dist, world, rank, "lqr")
+    if "mpc" in legs:
+        secondary["mpc_qp"] = track_leg(args, torch, dist, world, rank, "mpc")
 
     if rank == 0:
         out = {
@@ -270,7 +506,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None},
             "cpu_baseline": cpu,
-            "secondary": control,
+            "secondary": secondary,
             "detail": {"kernel_ms_per_launch": kern_ms,
                        "algorithmic_bytes_per_launch": bytes_per_launch,
                        "expansions_per_launch": int(counters[:, 2].sum()),

@@ -235,6 +235,8 @@ typedef struct {
  *   draws [nq] i64        out: doubles consumed from rnd (advance the caller's RNG by this many)
  *   status [nq]           0 found, 1 not found (returns (0, None, nodes)), 2 path_cap overflow,
  *                         3 tree_cap / stream / candidate-list overflow, 4 parent cycle (reference hangs)
+ *   counters [nq][4] i64  nullable: iterations, nodes scanned (nearest + radius passes), in-radius
+ *                         candidates, segment collision tests
  * A new RRT* node that lands exactly on an existing one replaces it (dict semantics); plain RRT does
  * not check for that (a measure-zero event).
  */
@@ -242,7 +244,8 @@ int pmp_rrt_batch(pmp_ctx* ctx, void* stream, const pmp_rrt_params* p, const dou
                   const double* circ, int nc, const double* bnd, int nb, const double* start_xy,
                   const double* goal_xy, int nq, const double* rnd, int64_t rnd_stride, int tree_cap,
                   double* tree_xy, double* tree_g, int32_t* tree_parent, int32_t* n_nodes, double* cost,
-                  int32_t* path_len, double* path_xy, int path_cap, int64_t* draws, int32_t* status);
+                  int32_t* path_len, double* path_xy, int path_cap, int64_t* draws, int32_t* status,
+                  int64_t* counters);
 
 /* Pre-size the A* scratch (heap of heap_cap entries per concurrent query, up to max_slots
  * concurrent queries) so that later batch calls allocate nothing (hipGraph-capturable). */

@@ -483,3 +483,22 @@ def rrt_batch(star, rects, circs, X, Y, starts, goals, rnd, sample_num, max_dist
                                  X, Y, _p(s, _dp), _p(g, _dp), nq, sample_num, max_dist, radius, goal_rate,
                                  _p(rnd, _dp), stride, _p(tree, _dp), cap, _p(nn, _i32p), _p(st, _i32p), nthreads)
     return dict(status=st, n_nodes=nn, tree=tree)
+
+
+def astar3d_batch(occ, starts, goals, heuristic: str = "euclidean", nthreads: int = 0):
+    """AStar3D over per-query grids occ [nq, X, Y, Z] with OpenMP -> (cost [nq], status [nq])."""
+    L = lib()
+    if not getattr(L, "_a3b", False):
+        L.oracle_astar3d_batch.restype = ctypes.c_int
+        L.oracle_astar3d_batch.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p, _i32p,
+                                           ctypes.c_int, _dp, _i32p, ctypes.c_int]
+        L._a3b = True
+    occ = np.ascontiguousarray(occ, dtype=np.uint8)
+    nq, X, Y, Z = occ.shape
+    s = np.ascontiguousarray(starts, np.int32).reshape(-1, 3)
+    g = np.ascontiguousarray(goals, np.int32).reshape(-1, 3)
+    cost = np.zeros(nq)
+    st = np.zeros(nq, np.int32)
+    L.oracle_astar3d_batch(_p(occ, _u8p), X, Y, Z, 1 if heuristic == "manhattan" else 0, _p(s, _i32p), _p(g, _i32p),
+                           nq, _p(cost, _dp), _p(st, _i32p), nthreads)
+    return cost, st

@@ -1482,3 +1482,27 @@ int oracle_rrt_batch(int star, const double* rect, int nr, const double* circ, i
     }
     return found;
 }
+
+/* OpenMP over independent AStar3D queries with per-query occupancy occ [nq][X*Y*Z] (bench
+ * cpu_baseline of config C5).  cost [nq]; status [nq]. */
+int oracle_astar3d_batch(const uint8_t* occ, int X, int Y, int Z, int heuristic, const int32_t* s,
+                         const int32_t* g, int nq, double* cost, int32_t* status, int nthreads)
+{
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+    const int64_t ncell = (int64_t)X * Y * Z;
+    int found = 0;
+#pragma omp parallel num_threads(nthreads) reduction(+ : found)
+    {
+        int32_t* path = (int32_t*)malloc(sizeof(int32_t) * (size_t)(ncell + 1));
+        int32_t plen, nexp;
+        int64_t ctr[4];
+#pragma omp for schedule(dynamic, 4)
+        for (int q = 0; q < nq; q++) {
+            status[q] = oracle_astar3d(occ + (size_t)q * ncell, X, Y, Z, heuristic, s + 3 * q, g + 3 * q, cost + q, path,
+                                       (int)(ncell + 1), &plen, NULL, 0, &nexp, ctr);
+            found += status[q] == 0;
+        }
+        free(path);
+    }
+    return found;
+}

@@ -248,7 +248,7 @@ def map_arrays(env, torch=None):
 
 def rrt_batch(env, starts, goals, rnd, sample_num: int, star: bool = True, max_dist: float = 0.5,
               radius: float = 10.0, goal_sample_rate: float = 0.05, delta: float = 0.5, path_cap: int | None = None,
-              stream=None):
+              counters: bool = False, stream=None):
     """Batched RRT / RRT* plans (rrt.py:49-151, rrt_star.py:43-76) on one Map.
     rnd: [nq, stride] f64 random streams (RandomState.random_sample order; 3*sample_num+1 per query).
     Returns dict of device tensors: tree_xy [nq,cap,2], tree_g, tree_parent, n_nodes, cost, path_len,
@@ -269,7 +269,8 @@ def rrt_batch(env, starts, goals, rnd, sample_num: int, star: bool = True, max_d
                tree_parent=torch.empty((nq, cap), **i32), n_nodes=torch.empty(nq, **i32),
                cost=torch.empty(nq, **f64), path_len=torch.empty(nq, **i32),
                path=torch.empty((nq, max(path_cap, 1), 2), **f64), draws=torch.empty(nq, dtype=torch.int64, device="cuda"),
-               status=torch.empty(nq, **i32))
+               status=torch.empty(nq, **i32),
+               counters=torch.zeros((nq, 4), dtype=torch.int64, device="cuda") if counters else None)
     P = _lib.RRTParams(float(env.x_range), float(env.y_range), float(delta), float(max_dist), float(radius),
                        float(goal_sample_rate), int(sample_num), int(bool(star)))
     rc = L.pmp_rrt_batch(ctx, stream if stream is not None else _lib.stream_ptr(), ctypes.byref(P), rect.data_ptr(),
@@ -277,7 +278,8 @@ def rrt_batch(env, starts, goals, rnd, sample_num: int, star: bool = True, max_d
                          s.data_ptr(), g.data_ptr(), nq, rnd.data_ptr(), int(rnd.shape[1]), cap,
                          out["tree_xy"].data_ptr(), out["tree_g"].data_ptr(), out["tree_parent"].data_ptr(),
                          out["n_nodes"].data_ptr(), out["cost"].data_ptr(), out["path_len"].data_ptr(),
-                         out["path"].data_ptr(), path_cap, out["draws"].data_ptr(), out["status"].data_ptr())
+                         out["path"].data_ptr(), path_cap, out["draws"].data_ptr(), out["status"].data_ptr(),
+                         _lib.ptr(out["counters"]))
     _lib.check(ctx, rc, "pmp_rrt_batch")
     return out
 

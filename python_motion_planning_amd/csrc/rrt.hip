@@ -53,6 +53,7 @@ struct RrtArgs {
     int path_cap;
     int64_t* draws;
     int32_t* status;
+    int64_t* counters;  // nullable [nq][4]
     float2* xyf;      // scratch [nq][cap]
     KEntry* klist;    // scratch [nq][cap]
 };
@@ -236,6 +237,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
     const double eps = 4e-6 * cmax + 1e-5;
     int n = 1, status = 1;
     int64_t cur = 0;
+    int64_t c_iter = 0, c_scan = 0, c_cand = 0, c_tests = 0;  // iterations, nodes scanned, in-radius, collision tests
 
     for (int it = 0; it < P.sample_num; it++) {
         if (cur + 3 > A.stride) { status = PMP_CAP_OVERFLOW; break; }
@@ -244,6 +246,8 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             sx = lox + rgx * rnd[cur++];
             sy = loy + rgy * rnd[cur++];
         }
+        c_iter++;
+        c_scan += n;
         // ---- 2. nearest ----
         const float sxf = (float)sx, syf = (float)sy;
         float best = INFINITY;
@@ -277,6 +281,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         if (P.max_dist < dist) dist = P.max_dist;
         const double nx = nx0 + dist * cos(theta), ny = ny0 + dist * sin(theta);
         const double G0 = gnear + dist;
+        c_tests++;
         if (collision_block(S, nr, nc, nb, delta, nx, ny, nx0, ny0)) continue;
         double G = G0;
         int parent = near;
@@ -313,6 +318,9 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             const int nT = S.nT;
             slot = S.slot;
             if (nT > kMaxT) { status = PMP_CAP_OVERFLOW; break; }
+            c_cand += nK;
+            c_scan += n;
+            c_tests += nT;
             // ---- 4b. one wave per test: the collision-free improving set ----
             for (int t = wave; t < nT; t += kWaves) {
                 const int k = S.tk[t];
@@ -354,6 +362,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             __syncthreads();
             const int nT2 = S.nT;
             if (nT2 > kMaxT) { status = PMP_CAP_OVERFLOW; break; }
+            c_tests += nT2;
             for (int t = wave; t < nT2; t += kWaves) {
                 const KEntry e = kl[S.tk[t]];
                 if (collision_wave(S, nr, nc, nb, delta, tx[2 * e.j], tx[2 * e.j + 1], nx, ny)) continue;
@@ -372,6 +381,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         }
         __syncthreads();
         const double dg = lp::py_hypot(gx - nx, gy - ny);
+        c_tests += dg <= P.max_dist;
         if (dg <= P.max_dist && !collision_block(S, nr, nc, nb, delta, nx, ny, gx, gy)) {
             if (n >= cap) { status = PMP_CAP_OVERFLOW; break; }
             if (tid == 0) {
@@ -387,6 +397,12 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
     if (tid == 0) {
         A.n_nodes[q] = n;
         A.draws[q] = cur;
+        if (A.counters) {
+            A.counters[4 * q] = c_iter;
+            A.counters[4 * q + 1] = c_scan;
+            A.counters[4 * q + 2] = c_cand;
+            A.counters[4 * q + 3] = c_tests;
+        }
         int plen = 0;
         double c = 0.0;
         if (status == PMP_FOUND) {
@@ -416,7 +432,8 @@ extern "C" int pmp_rrt_batch(pmp_ctx* ctx, void* stream, const pmp_rrt_params* p
                              const double* circ, int nc, const double* bnd, int nb, const double* start_xy,
                              const double* goal_xy, int nq, const double* rnd, int64_t rnd_stride, int tree_cap,
                              double* tree_xy, double* tree_g, int32_t* tree_parent, int32_t* n_nodes, double* cost,
-                             int32_t* path_len, double* path_xy, int path_cap, int64_t* draws, int32_t* status)
+                             int32_t* path_len, double* path_xy, int path_cap, int64_t* draws, int32_t* status,
+                             int64_t* counters)
 {
     if (!ctx) return PMP_EINVAL;
     if (!p || nq < 0 || nr < 0 || nc < 0 || nb < 0 || nr > kMaxObs || nc > kMaxObs || nb > kMaxBnd)
@@ -439,7 +456,7 @@ extern "C" int pmp_rrt_batch(pmp_ctx* ctx, void* stream, const pmp_rrt_params* p
     A.rnd = rnd; A.stride = rnd_stride; A.cap = tree_cap;
     A.txy = tree_xy; A.tg = tree_g; A.tpar = tree_parent; A.n_nodes = n_nodes;
     A.cost = cost; A.path_len = path_len; A.path = path_xy; A.path_cap = path_cap;
-    A.draws = draws; A.status = status; A.xyf = xyf; A.klist = kl;
+    A.draws = draws; A.status = status; A.counters = counters; A.xyf = xyf; A.klist = kl;
     if (p->star)
         hipLaunchKernelGGL(rrt_kernel<true>, dim3(nq), dim3(kNT), 0, (hipStream_t)stream, A);
     else

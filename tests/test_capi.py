@@ -38,3 +38,36 @@ def test_kernels_are_gfx950_code_objects():
     data = open(_lib.LIB_PATH, "rb").read()
     assert b"__CLANG_OFFLOAD_BUNDLE__" in data  # .hip_fatbin offload bundle
     assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def declared_prototypes():
+    """name -> list of parameter type strings, from include/pmp.h."""
+    src = open(os.path.join(REPO, "include", "pmp.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    protos = {}
+    for m in re.finditer(r"\b(pmp_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", src, flags=re.S):
+        params = [p.strip() for p in m.group(2).replace("\n", " ").split(",")]
+        protos[m.group(1)] = [] if params == ["void"] or params == [""] else params
+    return protos
+
+
+def test_bindings_match_prototypes():
+    """Every ctypes binding has exactly the declared arity, and pointer / 64-bit integer parameters
+    are bound as c_void_p / c_int64 (an under-length argtypes list silently truncates the extra
+    pointer arguments to C int)."""
+    import ctypes
+
+    from python_motion_planning_amd import _lib
+
+    protos = declared_prototypes()
+    assert protos
+    for name, params in protos.items():
+        res, args = _lib.SIGNATURES[name]
+        assert len(args) == len(params), f"{name}: {len(args)} bound vs {len(params)} declared"
+        for a, p in zip(args, params):
+            if "*" in p:
+                assert a in (ctypes.c_void_p, ctypes.c_char_p), f"{name}: {p!r} bound as {a}"
+            elif p.startswith("int64_t"):
+                assert a is ctypes.c_int64, f"{name}: {p!r} bound as {a}"
+            elif p.startswith("int") or p.startswith("int32_t"):
+                assert a is ctypes.c_int, f"{name}: {p!r} bound as {a}"
