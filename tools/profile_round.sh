@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round profile on the GPU box: the default bench command under rocprofv3 kernel tracing, then two
+# separate PMC passes (FETCH_SIZE, WRITE_SIZE cannot share a pass on gfx950) of a shorter bench.
+# Outputs under gpurun_out/; copy the summaries to profiles/<round>/ afterwards.
+set -e
+R=${GRAFT_REPO_ROOT:-/root/repo}
+OUT=$R/gpurun_out
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 700 rocprofv3 --kernel-trace --stats -d $OUT/prof_kt -o run -- python3 $R/bench.py \
+    > $OUT/bench_prof.json 2> $OUT/bench_prof.err
+timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE -d $OUT/prof_fetch -o run -- python3 $R/bench.py --no-cpu-baseline \
+    --steps 3 --warmup 1 --rrt-steps 1 --a3-steps 1 --track-steps 1 --control-steps 2 > $OUT/bench_fetch.json 2> $OUT/bench_fetch.err
+timeout -k 10 500 rocprofv3 --pmc WRITE_SIZE -d $OUT/prof_write -o run -- python3 $R/bench.py --no-cpu-baseline \
+    --steps 3 --warmup 1 --rrt-steps 1 --a3-steps 1 --track-steps 1 --control-steps 2 > $OUT/bench_write.json 2> $OUT/bench_write.err
+echo profile-done
