@@ -81,27 +81,8 @@ def control_leg(args, torch, dist, world, rank):
         step()
     torch.cuda.synchronize()
     st.copy_(st0)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    evs = []
     K = args.control_steps
-    t0 = time.perf_counter()
-    for i in range(K):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        step()
-        e1.record()
-        evs.append((e0, e1))
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    if dist:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, kern_ms = timed(torch, dist, lambda i: step(), K)
     steps_done = na * K * world
     # ~8.2 MFLOP per agent-step in the stencil formulation
     flops_per_step = 4096 * 30 * (12 + 2 * 20) + 4096 * 30 * 9 * 6 + 4096 * 20
@@ -124,17 +105,42 @@ def control_leg(args, torch, dist, world, rank):
             "value": steps_done / elapsed, "unit": "agent-steps/s", "agents_per_gpu": na, "steps": K,
             "ms_per_step": elapsed / K * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
             "config": {"workload": "C4: README 51x31 grid, 64x64 (v,w) samples, H=30, weights 0.2/0.1/0.05"},
-            "roofline": {"bound": "fp64-valu", "achieved": achieved_tf, "peak": 78.6, "unit": "TFLOP/s",
-                         "frac": achieved_tf / 78.6, "traffic": None,
-                         "flops_per_agent_step": flops_per_step},
+            "roofline": with_traffic({"bound": "fp64-valu", "achieved": achieved_tf, "peak": 78.6, "unit": "TFLOP/s",
+                                      "frac": achieved_tf / 78.6, "traffic": None,
+                                      "flops_per_agent_step": flops_per_step}, "dwa_kernel"),
             "cpu_baseline": cpu}
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per dispatch of `kernel` from the newest committed profiles/r*/pmc_traffic.json: the
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench (tools/profile_round.sh,
+    summarised by tools/prof_summary.py with the guide's gfx950 correction).  (bytes, source) or
+    (None, None) when no summary is committed."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f).get(kernel) or {}
+    b = d.get("hbm_bytes_per_dispatch")
+    return (float(b) if b is not None else None), os.path.relpath(files[-1], REPO)
+
+
+def with_traffic(roof: dict, kernel: str) -> dict:
+    t, src = pmc_traffic(kernel)
+    roof["traffic"] = t
+    if src:
+        roof["traffic_source"] = f"{src} [{kernel}]"
+    return roof
 
 
 def timed(torch, dist, fn, steps, stream=None):
     """Barrier + sync, run `steps` launches with HIP events around each (on `stream`), barrier +
     sync; returns (wall seconds, max over ranks; mean event ms per launch)."""
-    if dist:
-        dist.barrier()
+    from python_motion_planning_amd import shard
+
+    shard.barrier(dist)
     torch.cuda.synchronize()
     evs = []
     t0 = time.perf_counter()
@@ -151,14 +157,10 @@ def timed(torch, dist, fn, steps, stream=None):
             e1.record(stream)
         evs.append((e0, e1))
     torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
+    shard.barrier(dist)
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    if dist:
-        t = torch.tensor([elapsed, kern_ms], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0].item()), float(t[1].item())
+    elapsed, kern_ms = shard.max_over_ranks(dist, [elapsed, kern_ms], "cuda")
     return elapsed, kern_ms
 
 
@@ -210,9 +212,9 @@ def rrt_leg(args, torch, dist, world, rank):
             "ms_per_step": elapsed / args.rrt_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
             "config": {"workload": "C3: Map(512,512), 40 rects + 40 circles (default_rng(7)), (5,5)->(505,505), "
                                    "65536 samples, max_dist 0.5, r 10, goal rate 0.05"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "algorithmic_bytes_per_launch": alg_bytes},
+            "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                                      "algorithmic_bytes_per_launch": alg_bytes}, "rrt_kernel"),
             "detail": {"found": int((status == 0).sum()), "mean_nodes": float(out["n_nodes"].float().mean().item()),
                        "iterations_per_launch": int(ctr[:, 0].sum()), "nodes_scanned_per_launch": int(ctr[:, 1].sum()),
                        "collision_tests_per_launch": int(ctr[:, 3].sum())},
@@ -277,8 +279,9 @@ def astar3d_leg(args, torch, dist, world, rank):
             "unit": "plans/s", "queries_per_gpu": nq, "steps": args.a3_steps,
             "ms_per_step": elapsed / args.a3_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
             "config": {"workload": "C5: Grid3D(26,20,16) door, random.seed(i) pairs, safety bubbles r=1, euclidean"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": alg_bytes},
+            "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                                      "algorithmic_bytes_per_launch": alg_bytes}, "astar3d_kernel"),
             "detail": {"expansions_per_launch": int(c[:, 2].sum()), "pushes_per_launch": int(c[:, 0].sum()),
                        "max_heap_entries": int(c[:, 3].max())},
             "cpu_baseline": cpu}
@@ -349,8 +352,9 @@ def track_leg(args, torch, dist, world, rank, kind):
             "unit": "agent-steps/s", "agents_per_gpu": na, "iterations_per_launch": iters, "steps": args.track_steps,
             "ms_per_step": elapsed / args.track_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
             "config": {"workload": f"C4 agents on the README grid, {iters} LQR/MPC plan iterations per launch"},
-            "roofline": {"bound": "fp64-valu", "achieved": achieved_tf, "peak": 78.6, "unit": "TFLOP/s",
-                         "frac": achieved_tf / 78.6, "traffic": None},
+            "roofline": with_traffic({"bound": "fp64-valu", "achieved": achieved_tf, "peak": 78.6, "unit": "TFLOP/s",
+                                      "frac": achieved_tf / 78.6, "traffic": None},
+                                     "track_kernel_lqr" if kind == "lqr" else "track_kernel_mpc"),
             "detail": {"agent_steps_per_launch": stepped, "admm_iterations_per_launch": admm},
             "cpu_baseline": cpu}
 
@@ -377,6 +381,8 @@ def main():
     ap.add_argument("--a3-steps", type=int, default=3)
     ap.add_argument("--track-iters", type=int, default=20)
     ap.add_argument("--track-steps", type=int, default=5)
+    ap.add_argument("--schedule", choices=["lpt", "input"], default="lpt",
+                    help="A* query order across workers: longest start-goal distance first, or input order")
     ap.add_argument("--streams", type=int, default=3,
                     help="batches in flight: consecutive steps go to different HIP streams (own scratch "
                          "context each), so one batch's long-query tail overlaps the next batch")
@@ -384,16 +390,11 @@ def main():
 
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
+    from python_motion_planning_amd import shard
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
+    rank, world, local = shard.env_rank()
+    dist = shard.init("nccl")  # RCCL over xGMI; None for a single process
+    if dist is None:
         torch.cuda.set_device(0)
 
     from python_motion_planning_amd import _lib, batch, workloads as wl
@@ -411,6 +412,7 @@ def main():
     for _ in range(S):
         ctx = L.pmp_create(torch.cuda.current_device())
         _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, args.workers, 0), "reserve")
+        _lib.check(ctx, L.pmp_astar2d_set_schedule(ctx, 1 if args.schedule == "lpt" else 0), "schedule")
         lanes.append(dict(
             ctx=ctx, stream=torch.cuda.Stream(),
             cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
@@ -443,31 +445,35 @@ def main():
         assert torch.equal(b["cost"], cost)
     bytes_per_launch = astar_algorithmic_bytes(counters)
 
-    # timed region
-    if dist:
-        dist.barrier()
+    # timed region.  Each launch also records its device-side span (first worker start, last worker
+    # end; pmp_set_timing): with several batches in flight a HIP event pair on the launch's stream
+    # also counts the time the launch waits for CUs held by the other streams' persistent workers.
+    spans = torch.empty((args.steps, 2), dtype=torch.int64, device="cuda")
+    spans[:, 0] = -1  # UINT64_MAX
+    spans[:, 1] = 0
+    khz = ctypes.c_int(0)
+    _lib.check(lanes[0]["ctx"], L.pmp_wall_clock_khz(lanes[0]["ctx"], ctypes.byref(khz)), "wall clock")
+    shard.barrier(dist)
     torch.cuda.synchronize()
     evs = []
     t0 = time.perf_counter()
     for i in range(args.steps):
         b = lanes[i % S]
+        L.pmp_set_timing(b["ctx"], spans[i].data_ptr())
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(b["stream"])
         step(i)
         e1.record(b["stream"])
         evs.append((e0, e1))
     torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
+    shard.barrier(dist)
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    if dist:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        k = torch.tensor([kern_ms], device="cuda", dtype=torch.float64)
-        dist.all_reduce(k, op=dist.ReduceOp.MAX)
-        kern_ms = float(k.item())
+    for b in lanes:
+        L.pmp_set_timing(b["ctx"], None)
+    event_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    sp = spans.cpu().numpy().view(np.uint64)
+    kern_ms = float(np.mean((sp[:, 1] - sp[:, 0]).astype(np.float64)) / khz.value)
+    elapsed, kern_ms = shard.max_over_ranks(dist, [elapsed, kern_ms], "cuda")
 
     plans = nq * args.steps * world
     value = plans / elapsed
@@ -517,11 +523,15 @@ def main():
             "data": "synthetic (SURVEY.md §8(d) C2 generator: default_rng(0) 20% obstacles, default_rng(1+rank) pairs)",
             "config": {"workload": "C2 batched A* 1024x1024 Grid, 4096 start/goal pairs per GPU, euclidean",
                        "grid": [W, H], "queries_per_gpu": nq, "parallelism": f"query-sharded x{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None},
+            "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                                      "algorithmic_bytes_per_launch": bytes_per_launch}, "astar2d_kernel"),
             "cpu_baseline": cpu,
             "secondary": secondary,
             "detail": {"kernel_ms_per_launch": kern_ms,
+                       "kernel_ms_source": "device span per launch (first worker start .. last worker end, "
+                                           "pmp_set_timing), the quantity rocprofv3 reports as the dispatch duration",
+                       "event_ms_per_launch": event_ms, "schedule": args.schedule,
                        "algorithmic_bytes_per_launch": bytes_per_launch,
                        "expansions_per_launch": int(counters[:, 2].sum()),
                        "max_expansions_query": int(counters[:, 2].max()),

@@ -247,6 +247,17 @@ int pmp_rrt_batch(pmp_ctx* ctx, void* stream, const pmp_rrt_params* p, const dou
                   int32_t* path_len, double* path_xy, int path_cap, int64_t* draws, int32_t* status,
                   int64_t* counters);
 
+/* Launch-span recording for profiling: while set, every A* 2D launch of this context folds its
+ * workers' first start and last end wall-clock ticks into span[0] (atomic min) and span[1] (atomic
+ * max); the caller initialises span to {UINT64_MAX, 0}.  NULL switches it off. */
+int pmp_set_timing(pmp_ctx* ctx, uint64_t* span);
+/* Rate of the wall-clock ticks above, in kHz. */
+int pmp_wall_clock_khz(pmp_ctx* ctx, int* khz);
+/* A* 2D query scheduling across the persistent workers: 1 (default) = longest start-goal distance
+ * first (the expansion count grows with it, so long queries stop forming a tail), 0 = input order.
+ * Results are identical either way; only which worker runs which query changes. */
+int pmp_astar2d_set_schedule(pmp_ctx* ctx, int longest_first);
+
 /* Pre-size the A* scratch (heap of heap_cap entries per concurrent query, up to max_slots
  * concurrent queries) so that later batch calls allocate nothing (hipGraph-capturable). */
 int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int max_slots, int heap_cap);

@@ -24,6 +24,9 @@ SIGNATURES = {
     "pmp_astar2d_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _i,
                                _vp, _vp]),
     "pmp_astar2d_reserve": (_i, [_vp, _i, _i, _i, _i]),
+    "pmp_set_timing": (_i, [_vp, _vp]),
+    "pmp_wall_clock_khz": (_i, [_vp, _vp]),
+    "pmp_astar2d_set_schedule": (_i, [_vp, _i]),
     "pmp_astar3d_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _i,
                                _vp, _vp]),
     "pmp_dwa_step_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp,

@@ -264,11 +264,12 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
     int32_t* __restrict__ nexp_out, uint32_t* __restrict__ expand_out, int expand_cap,
     int64_t* __restrict__ counters, int32_t* __restrict__ status_out, int* __restrict__ queue,
     uint4* __restrict__ spill_all, int heap_cap, int lds_cap, uint32_t* __restrict__ cst_all, size_t cst_words,
-    double* __restrict__ G_all)
+    double* __restrict__ G_all, unsigned long long* __restrict__ span)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
     const int worker = blockIdx.x;
+    span_begin(span);
     Heap hp;
     hp.lg = (lds_f64*)(smem);
     hp.lcm = (lds_u32*)(smem + (size_t)8 * lds_cap);
@@ -489,6 +490,38 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
         }
         wave_sync_mem();
     }
+    span_end(span);
+}
+
+// ---- longest-first schedule: counting sort of the queries by descending start-goal distance ----
+__device__ __forceinline__ int lpt_key(const int32_t* s, const int32_t* g, int q)
+{
+    const int dx = s[2 * q] - g[2 * q], dy = s[2 * q + 1] - g[2 * q + 1];
+    return (int)__dsqrt_rn((double)dx * dx + (double)dy * dy);  // expansions grow ~ with distance^2
+}
+
+__global__ void lpt_hist(const int32_t* s, const int32_t* g, int nq, int nb, int* hist)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nq) atomicAdd(&hist[min(lpt_key(s, g, q), nb - 1)], 1);
+}
+
+// offsets[k] = number of queries with a larger key (descending order); one thread, nb <= 16384
+__global__ void lpt_scan(int nb, int* hist)
+{
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    int run = 0;
+    for (int k = nb - 1; k >= 0; k--) {
+        const int c = hist[k];
+        hist[k] = run;
+        run += c;
+    }
+}
+
+__global__ void lpt_scatter(const int32_t* s, const int32_t* g, int nq, int nb, int* offs, int32_t* order)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nq) order[atomicAdd(&offs[min(lpt_key(s, g, q), nb - 1)], 1)] = q;
 }
 
 int default_workers() { return 256 * 4; }
@@ -562,10 +595,22 @@ extern "C" int pmp_astar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
     hipStream_t s = (hipStream_t)stream;
     const size_t lds = (size_t)ctx->astar_lds_cap * 12;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
+    int32_t* order = nullptr;
+    if (ctx->astar_lpt && nq > workers) {
+        const int nb = (int)ceil(sqrt((double)W * W + (double)H * H)) + 1;
+        int* hist = (int*)pmp_scratch(ctx, SCR_PDIR, sizeof(int) * ((size_t)nb + (size_t)nq));
+        if (!hist) return PMP_ENOMEM;
+        order = hist + nb;
+        PMP_HIP_CHECK(ctx, hipMemsetAsync(hist, 0, sizeof(int) * (size_t)nb, s));
+        hipLaunchKernelGGL(lpt_hist, dim3((nq + 255) / 256), dim3(256), 0, s, start_xy, goal_xy, nq, nb, hist);
+        hipLaunchKernelGGL(lpt_scan, dim3(1), dim3(64), 0, s, nb, hist);
+        hipLaunchKernelGGL(lpt_scatter, dim3((nq + 255) / 256), dim3(256), 0, s, start_xy, goal_xy, nq, nb, hist, order);
+    }
     auto kern = heuristic == 1 ? astar2d_kernel<1> : astar2d_kernel<0>;
     hipLaunchKernelGGL(kern, dim3(workers), dim3(64), lds, s, occ_bits, W, H, start_xy,
-                       goal_xy, (const int32_t*)nullptr, nq, cost, path_len, path, path_cap, n_expanded, expand,
-                       expand_cap, counters, status, queue, spill, ctx->astar_heap_cap, ctx->astar_lds_cap, cst, cst_words, G);
+                       goal_xy, (const int32_t*)order, nq, cost, path_len, path, path_cap, n_expanded, expand,
+                       expand_cap, counters, status, queue, spill, ctx->astar_heap_cap, ctx->astar_lds_cap, cst, cst_words, G,
+                       ctx->span);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }

@@ -52,4 +52,25 @@ const char* pmp_last_error(pmp_ctx* ctx) { return ctx ? ctx->err.c_str() : "null
 
 const char* pmp_version(void) { return "pmp-hip 0.1 gfx950"; }
 
+int pmp_set_timing(pmp_ctx* ctx, uint64_t* span)
+{
+    if (!ctx) return PMP_EINVAL;
+    ctx->span = reinterpret_cast<unsigned long long*>(span);
+    return PMP_OK;
+}
+
+int pmp_wall_clock_khz(pmp_ctx* ctx, int* khz)
+{
+    if (!ctx || !khz) return PMP_EINVAL;
+    PMP_HIP_CHECK(ctx, hipDeviceGetAttribute(khz, hipDeviceAttributeWallClockRate, ctx->device));
+    return PMP_OK;
+}
+
+int pmp_astar2d_set_schedule(pmp_ctx* ctx, int longest_first)
+{
+    if (!ctx) return PMP_EINVAL;
+    ctx->astar_lpt = longest_first ? 1 : 0;
+    return PMP_OK;
+}
+
 }  // extern "C"

@@ -11,6 +11,10 @@ struct pmp_ctx {
     std::string err;
     // A* scratch geometry (pmp_astar2d_reserve)
     int astar_W = 0, astar_H = 0, astar_workers = 0, astar_heap_cap = 0, astar_lds_cap = 0;
+    // optional launch-span recording (pmp_set_timing): device u64[2] = {min start, max end}
+    unsigned long long* span = nullptr;
+    // A* 2D query scheduling: 1 = longest (start-goal distance) first, 0 = input order
+    int astar_lpt = 1;
     // grow-only scratch arena, one buffer per use
     void* buf[8] = {nullptr};
     size_t cap[8] = {0};
@@ -43,3 +47,13 @@ __device__ __forceinline__ double rl_f64(double v, int lane) {
 }
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+// launch-span stamps (pmp_set_timing): each worker's lane 0 folds its start / end wall-clock tick
+__device__ __forceinline__ void span_begin(unsigned long long* span)
+{
+    if (span && lane_id() == 0) atomicMin(&span[0], (unsigned long long)wall_clock64());
+}
+__device__ __forceinline__ void span_end(unsigned long long* span)
+{
+    if (span && lane_id() == 0) atomicMax(&span[1], (unsigned long long)wall_clock64());
+}

@@ -1,0 +1,76 @@
+"""Summarise a round's rocprofv3 databases (tools/profile_round.sh) into profiles/<round>/:
+  kernel_stats.csv   -- rocprofv3 --kernel-trace --stats of the default bench command
+  pmc_traffic.json   -- per-kernel FETCH_SIZE / WRITE_SIZE per dispatch from the two --pmc passes,
+                        with the gfx950 correction of MI355X_MICROARCH.md (FETCH_SIZE counts half the
+                        bytes of wide streaming reads: doubled; WRITE_SIZE as is; both in KiB)
+usage: python tools/prof_summary.py gpurun_out profiles/r1
+"""
+import csv
+import json
+import os
+import re
+import sqlite3
+import sys
+
+KERNELS = {  # short name -> regex on the demangled kernel name
+    "astar2d_kernel": r"astar2d_kernel<",
+    "dwa_kernel": r"dwa_kernel\(",
+    "rrt_kernel": r"rrt_kernel<",
+    "astar3d_kernel": r"astar3d_kernel\(",
+    "dstar_kernel": r"dstar_kernel\(",
+    "track_kernel_lqr": r"track_kernel<0>",
+    "track_kernel_mpc": r"track_kernel<1>",
+}
+
+
+def short(name):
+    for k, rx in KERNELS.items():
+        if re.search(rx, name):
+            return k
+    return name.split("(")[0][:60]
+
+
+def main(src, dst):
+    os.makedirs(dst, exist_ok=True)
+    db = sqlite3.connect(os.path.join(src, "prof_kt", "run_results.db"))
+    rows = list(db.execute("select name, count(*), sum(duration), avg(duration), 0.0 from kernels group by name "
+                           "order by sum(duration) desc"))
+    tot = sum(r[2] for r in rows) or 1.0
+    rows = [(n, c, t, a, 100.0 * t / tot) for n, c, t, a, _ in rows]  # durations in ns
+    with open(os.path.join(dst, "kernel_stats.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["kernel", "calls", "total_ns", "avg_ns", "percent"])
+        for n, c, t, a, p in rows:
+            w.writerow([short(n), c, f"{t:.0f}", f"{a:.0f}", f"{p:.3f}"])
+    traffic = {}
+    for counter, sub in (("FETCH_SIZE", "prof_fetch"), ("WRITE_SIZE", "prof_write")):
+        path = os.path.join(src, sub, "run_results.db")
+        if not os.path.exists(path):
+            continue
+        d = sqlite3.connect(path)
+        for name, n, mean_kb in d.execute(
+                "select kernel_name, count(*), avg(value) from counters_collection where counter_name = ? "
+                "group by kernel_name", (counter,)):
+            k = short(name)
+            e = traffic.setdefault(k, {})
+            e[f"{counter}_kib_per_dispatch"] = mean_kb
+            e["dispatches"] = n
+    for k, e in traffic.items():
+        fb = e.get("FETCH_SIZE_kib_per_dispatch")
+        wb = e.get("WRITE_SIZE_kib_per_dispatch")
+        e["read_bytes_per_dispatch"] = None if fb is None else 2.0 * fb * 1024.0
+        e["write_bytes_per_dispatch"] = None if wb is None else wb * 1024.0
+        e["hbm_bytes_per_dispatch"] = (None if fb is None or wb is None
+                                       else e["read_bytes_per_dispatch"] + e["write_bytes_per_dispatch"])
+    traffic["_note"] = ("FETCH_SIZE doubled per MI355X_MICROARCH.md (calibrated for 16 B/lane streaming reads; "
+                        "the planners' reads are scattered 4-16 B accesses, for which the guide gives no "
+                        "calibration) and WRITE_SIZE as is; Infinity-Cache hits are counted by these counters")
+    with open(os.path.join(dst, "pmc_traffic.json"), "w") as f:
+        json.dump(traffic, f, indent=1, sort_keys=True)
+    for n, c, t, a, p in rows[:8]:
+        print(f"{short(n):24s} calls {c:5d} avg {a / 1e6:12.3f} ms  {p:6.2f} %")
+    print(json.dumps({k: v.get("hbm_bytes_per_dispatch") for k, v in traffic.items() if not k.startswith("_")}))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
