@@ -13,6 +13,7 @@ import sqlite3
 import sys
 
 KERNELS = {  # short name -> regex on the demangled kernel name
+    "lpt_hist": r"lpt_hist\(", "lpt_scan": r"lpt_scan\(", "lpt_scatter": r"lpt_scatter\(",
     "astar2d_kernel": r"astar2d_kernel<",
     "dwa_kernel": r"dwa_kernel\(",
     "rrt_kernel": r"rrt_kernel<",
@@ -27,30 +28,41 @@ def short(name):
     for k, rx in KERNELS.items():
         if re.search(rx, name):
             return k
-    return name.split("(")[0][:60]
+    return name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:60]
 
 
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
     db = sqlite3.connect(os.path.join(src, "prof_kt", "run_results.db"))
-    rows = list(db.execute("select name, count(*), sum(duration), avg(duration), 0.0 from kernels group by name "
-                           "order by sum(duration) desc"))
-    tot = sum(r[2] for r in rows) or 1.0
-    rows = [(n, c, t, a, 100.0 * t / tot) for n, c, t, a, _ in rows]  # durations in ns
+    # one row per (kernel, grid size): a planner launched with different batch sizes (e.g. the small
+    # A* batches that build the control legs' global paths) gets separate statistics
+    rows = list(db.execute("select name, grid_x, count(*), sum(duration), avg(duration), min(duration), max(duration) "
+                           "from kernels group by name, grid_x order by sum(duration) desc"))
+    tot = sum(r[3] for r in rows) or 1.0
     with open(os.path.join(dst, "kernel_stats.csv"), "w", newline="") as f:
         w = csv.writer(f)
-        w.writerow(["kernel", "calls", "total_ns", "avg_ns", "percent"])
-        for n, c, t, a, p in rows:
-            w.writerow([short(n), c, f"{t:.0f}", f"{a:.0f}", f"{p:.3f}"])
+        w.writerow(["kernel", "grid_threads", "calls", "total_ns", "avg_ns", "min_ns", "max_ns", "percent"])
+        for n, g, c, t, a, mn, mx in rows:
+            w.writerow([short(n), g, c, f"{t:.0f}", f"{a:.0f}", f"{mn:.0f}", f"{mx:.0f}", f"{100.0 * t / tot:.3f}"])
+    # per-dispatch durations of the headline kernel, in launch order (warmups first)
+    with open(os.path.join(dst, "astar2d_dispatches.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["dispatch", "grid_threads", "duration_ns"])
+        for i, (g, d) in enumerate(db.execute("select grid_x, duration from kernels where name like '%astar2d_kernel%' "
+                                             "order by start")):
+            w.writerow([i, g, d])
+    rows = [(n, c, t, a, 100.0 * t / tot) for n, g, c, t, a, mn, mx in rows]
     traffic = {}
     for counter, sub in (("FETCH_SIZE", "prof_fetch"), ("WRITE_SIZE", "prof_write")):
         path = os.path.join(src, sub, "run_results.db")
         if not os.path.exists(path):
             continue
         d = sqlite3.connect(path)
+        # the largest launch configuration of each kernel (the bench leg's own batch)
         for name, n, mean_kb in d.execute(
-                "select kernel_name, count(*), avg(value) from counters_collection where counter_name = ? "
-                "group by kernel_name", (counter,)):
+                "select kernel_name, count(*), avg(value) from counters_collection c where counter_name = ? "
+                "and grid_size = (select max(grid_size) from counters_collection c2 where c2.kernel_name = "
+                "c.kernel_name and c2.counter_name = c.counter_name) group by kernel_name", (counter,)):
             k = short(name)
             e = traffic.setdefault(k, {})
             e[f"{counter}_kib_per_dispatch"] = mean_kb
