@@ -75,7 +75,8 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
     const size_t spill_n = (size_t)(heap_cap > lds_cap ? heap_cap - lds_cap : 0);
     const heap16::Heap hp = heap16::make_heap(smem, lds_cap, spill_all + (size_t)worker * spill_n, spill_n);
     uint8_t* cdir = cdir_all + (size_t)worker * ncell;
-    double* cg = cg_all + (size_t)worker * ncell;
+    double* cg = cg_all + (size_t)worker * 2 * ncell;  // closed g
+    double* og = cg + ncell;                            // best pending (pushed) g
     int pop_jl, pop_ol;
     heap16::pop_lane_consts(lane, pop_jl, pop_ol);
     // neighbour lane m < 26: motion m (env3d.py:56-70)
@@ -90,7 +91,10 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
         if (qi >= nq) break;
         const int q = qi;
         const uint32_t* occ = occ_all + (per_query ? (size_t)q * words : 0);
-        for (size_t i = lane; i < ncell; i += 64) cdir[i] = 0;
+        for (size_t i = lane; i < ncell; i += 64) {
+            cdir[i] = 0;
+            og[i] = __builtin_inf();
+        }
         heap16::wsync();
         const int sx = start_xyz[3 * q], sy = start_xyz[3 * q + 1], sz = start_xyz[3 * q + 2];
         Key3 qc;
@@ -136,7 +140,7 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
             const int nx = x + mdx, ny = y + mdy, nz = z + mdz;
             bool coll = true;
             uint32_t ncd = 0;
-            double ncg = 0.0;
+            double ncg = 0.0, nog = 0.0;
             uint32_t nlin = 0;
             if (lane < 26) {
                 coll = occ3(occ, X, Y, Z, x, y, z) || occ3(occ, X, Y, Z, nx, ny, nz);
@@ -152,6 +156,7 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
                     nlin = ((uint32_t)nx * (uint32_t)Y + (uint32_t)ny) * (uint32_t)Z + (uint32_t)nz;
                     ncd = cdir[nlin];
                     ncg = cg[nlin];
+                    nog = og[nlin];
                 }
             } else if (lane == 26) {
                 ncd = cdir[lin];
@@ -212,24 +217,34 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
             // ---- neighbours (:66-75): skip if CLOSED with g <= tentative_g, else push with counter
             const double tg = node.g + mcost;
             const bool ok = lane < 26 && !coll && !(ncd != 0u && tg >= ncg);
-            uint64_t vm = ballot(ok);
+            npush += __popcll(ballot(ok));  // the reference's pushes (:66-75)
+            // The key (f, h, counter) is a total order, so only the heap's contents matter.  An entry
+            // whose cell already has a pending entry with g <= tg pops after it (f = g + h, equal
+            // g -> earlier counter) and is then skipped by the CLOSED check (:48-50): it is dead on
+            // arrival and is not inserted.  A strictly better entry is inserted and makes the old
+            // one dead instead (skipped the same way when it pops).
+            const bool live = ok && tg < nog;
+            if (live) og[nlin] = tg;
+            uint64_t vm = ballot(live);
             Ent item;
             item.g = tg;
             item.a = 0u;
             item.b = ((((uint32_t)nx & 255u) << 16) | (((uint32_t)ny & 255u) << 8) | ((uint32_t)nz & 255u)) << 5 | (uint32_t)(lane < 26 ? lane : 0);
             qc.derive(item);
             bool overflow = false;
+            uint32_t okm = (uint32_t)ballot(ok);
             while (vm) {
                 const int m = __ffsll((long long)vm) - 1;
                 vm &= vm - 1;
                 if (n >= heap_cap) { overflow = true; break; }
                 Ent it = heap16::rl_ent(item, m);
-                it.a = seq++;
+                // counter = the reference's push index of this neighbour
+                it.a = seq + (uint32_t)__popc(okm & ((1u << m) - 1u));
                 if (n < lds_cap) heap16::push<Key3, false>(hp, qc, n, it, root, lane);
                 else heap16::push<Key3, true>(hp, qc, n, it, root, lane);
                 n += 1;
-                npush++;
             }
+            seq += (uint32_t)__popc(okm);
             if (n > maxn) maxn = n;
             if (overflow) { st = PMP_CAP_OVERFLOW; break; }
         }
@@ -280,7 +295,7 @@ extern "C" int pmp_astar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
     const size_t spill_n = heap_cap > lds_cap ? (size_t)(heap_cap - lds_cap) : 0;
     uint4* spill = (uint4*)pmp_scratch(ctx, SCR_AUX1, (size_t)workers * spill_n * 16 + 16);
     uint8_t* cdir = (uint8_t*)pmp_scratch(ctx, SCR_AUX2, (size_t)workers * ncell + 16);
-    double* cg = (double*)pmp_scratch(ctx, SCR_AUX3, (size_t)workers * ncell * 8 + 16);
+    double* cg = (double*)pmp_scratch(ctx, SCR_AUX3, (size_t)workers * ncell * 16 + 16);  // closed g + pending g
     int* queue = (int*)pmp_scratch(ctx, SCR_AUX0, 256);
     if (!spill || !cdir || !cg || !queue) return PMP_ENOMEM;
     hipStream_t s = (hipStream_t)stream;

