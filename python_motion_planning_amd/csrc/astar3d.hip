@@ -59,6 +59,19 @@ __device__ __forceinline__ bool occ3(const uint32_t* occ, int X, int Y, int Z, i
     return (occ[c >> 5] >> (c & 31)) & 1u;
 }
 
+typedef __attribute__((address_space(3))) uint32_t lds_w32;
+
+// occupancy bit, blocked outside the grid, from the per-query bitmap staged in LDS
+__device__ __forceinline__ uint32_t occ3l(const lds_w32* occ, int X, int Y, int Z, int x, int y, int z)
+{
+    if ((unsigned)x >= (unsigned)X || (unsigned)y >= (unsigned)Y || (unsigned)z >= (unsigned)Z) return 1u;
+    const uint32_t c = ((uint32_t)x * (uint32_t)Y + (uint32_t)y) * (uint32_t)Z + (uint32_t)z;
+    return (occ[c >> 5] >> (c & 31)) & 1u;
+}
+
+constexpr int kOccLdsWords = 1024;  // grids up to 32768 cells keep their occupancy in LDS (4 KiB)
+
+template <bool OCC_LDS>
 __global__ __launch_bounds__(64) void astar3d_kernel(
     const uint32_t* __restrict__ occ_all, int per_query, int X, int Y, int Z, int heuristic,
     const int32_t* __restrict__ start_xyz, const int32_t* __restrict__ goal_xyz, int nq, double* __restrict__ cost_out,
@@ -74,6 +87,7 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
     const size_t words = (ncell + 31) / 32;
     const size_t spill_n = (size_t)(heap_cap > lds_cap ? heap_cap - lds_cap : 0);
     const heap16::Heap hp = heap16::make_heap(smem, lds_cap, spill_all + (size_t)worker * spill_n, spill_n);
+    lds_w32* occl = (lds_w32*)(smem + (size_t)16 * lds_cap);  // OCC_LDS: the query's bitmap
     uint8_t* cdir = cdir_all + (size_t)worker * ncell;
     double* cg = cg_all + (size_t)worker * 2 * ncell;  // closed g
     double* og = cg + ncell;                            // best pending (pushed) g
@@ -91,6 +105,8 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
         if (qi >= nq) break;
         const int q = qi;
         const uint32_t* occ = occ_all + (per_query ? (size_t)q * words : 0);
+        if (OCC_LDS)
+            for (size_t i = lane; i < words; i += 64) occl[i] = occ[i];
         for (size_t i = lane; i < ncell; i += 64) {
             cdir[i] = 0;
             og[i] = __builtin_inf();
@@ -141,26 +157,40 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
             bool coll = true;
             uint32_t ncd = 0;
             double ncg = 0.0, nog = 0.0;
-            uint32_t nlin = 0;
+            uint32_t nlin = lin;
             if (lane < 26) {
-                coll = occ3(occ, X, Y, Z, x, y, z) || occ3(occ, X, Y, Z, nx, ny, nz);
-                if (mchg == 2) {
-                    if (mdx != 0 && mdy != 0) coll = coll || occ3(occ, X, Y, Z, x + mdx, y, z) || occ3(occ, X, Y, Z, x, y + mdy, z);
-                    else if (mdx != 0 && mdz != 0) coll = coll || occ3(occ, X, Y, Z, x + mdx, y, z) || occ3(occ, X, Y, Z, x, y, z + mdz);
-                    else coll = coll || occ3(occ, X, Y, Z, x, y + mdy, z) || occ3(occ, X, Y, Z, x, y, z + mdz);
-                } else if (mchg == 3) {
-                    coll = coll || occ3(occ, X, Y, Z, x + mdx, y, z) || occ3(occ, X, Y, Z, x, y + mdy, z) ||
-                           occ3(occ, X, Y, Z, x, y, z + mdz);
+                const bool inb = (unsigned)nx < (unsigned)X && (unsigned)ny < (unsigned)Y && (unsigned)nz < (unsigned)Z;
+                if (inb) nlin = ((uint32_t)nx * (uint32_t)Y + (uint32_t)ny) * (uint32_t)Z + (uint32_t)nz;
+            }
+            if (lane <= 26) {  // one HBM round, independent of the collision test: CLOSED / pending state
+                ncd = cdir[nlin];
+                ncg = cg[nlin];
+                nog = og[nlin];
+            }
+            if (lane < 26) {
+                if (OCC_LDS) {
+#define OCC(a, b, c) occ3l(occl, X, Y, Z, a, b, c)
+                    uint32_t c = OCC(x, y, z) | OCC(nx, ny, nz);
+                    if (mchg == 2) {
+                        if (mdx != 0 && mdy != 0) c |= OCC(x + mdx, y, z) | OCC(x, y + mdy, z);
+                        else if (mdx != 0 && mdz != 0) c |= OCC(x + mdx, y, z) | OCC(x, y, z + mdz);
+                        else c |= OCC(x, y + mdy, z) | OCC(x, y, z + mdz);
+                    } else if (mchg == 3) {
+                        c |= OCC(x + mdx, y, z) | OCC(x, y + mdy, z) | OCC(x, y, z + mdz);
+                    }
+                    coll = c != 0u;
+#undef OCC
+                } else {
+                    coll = occ3(occ, X, Y, Z, x, y, z) || occ3(occ, X, Y, Z, nx, ny, nz);
+                    if (mchg == 2) {
+                        if (mdx != 0 && mdy != 0) coll = coll || occ3(occ, X, Y, Z, x + mdx, y, z) || occ3(occ, X, Y, Z, x, y + mdy, z);
+                        else if (mdx != 0 && mdz != 0) coll = coll || occ3(occ, X, Y, Z, x + mdx, y, z) || occ3(occ, X, Y, Z, x, y, z + mdz);
+                        else coll = coll || occ3(occ, X, Y, Z, x, y + mdy, z) || occ3(occ, X, Y, Z, x, y, z + mdz);
+                    } else if (mchg == 3) {
+                        coll = coll || occ3(occ, X, Y, Z, x + mdx, y, z) || occ3(occ, X, Y, Z, x, y + mdy, z) ||
+                               occ3(occ, X, Y, Z, x, y, z + mdz);
+                    }
                 }
-                if (!coll) {
-                    nlin = ((uint32_t)nx * (uint32_t)Y + (uint32_t)ny) * (uint32_t)Z + (uint32_t)nz;
-                    ncd = cdir[nlin];
-                    ncg = cg[nlin];
-                    nog = og[nlin];
-                }
-            } else if (lane == 26) {
-                ncd = cdir[lin];
-                ncg = cg[lin];
             }
             // ---- pop
             if (n > 0) {
@@ -287,7 +317,10 @@ extern "C" int pmp_astar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
     int workers = 256 * 4;
     if (workers > nq) workers = nq;
     const int per_cu = 4;
-    int lds_cap = (((160 * 1024) / per_cu - 256) / 16) & ~15;
+    const size_t words = (ncell + 31) / 32;
+    const bool occ_lds = words <= (size_t)kOccLdsWords;
+    const int occ_bytes = occ_lds ? kOccLdsWords * 4 : 0;
+    int lds_cap = (((160 * 1024) / per_cu - 256 - occ_bytes) / 16) & ~15;
     size_t hc = 26 * ncell + 8;
     if (hc > (size_t)(1 << 22)) hc = (size_t)1 << 22;
     const int heap_cap = (int)hc;
@@ -300,7 +333,8 @@ extern "C" int pmp_astar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
     if (!spill || !cdir || !cg || !queue) return PMP_ENOMEM;
     hipStream_t s = (hipStream_t)stream;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
-    hipLaunchKernelGGL(astar3d_kernel, dim3(workers), dim3(64), (size_t)lds_cap * 16, s, occ_bits, per_query, X, Y, Z,
+    auto kern = occ_lds ? astar3d_kernel<true> : astar3d_kernel<false>;
+    hipLaunchKernelGGL(kern, dim3(workers), dim3(64), (size_t)lds_cap * 16 + occ_bytes, s, occ_bits, per_query, X, Y, Z,
                        heuristic, start_xyz, goal_xyz, nq, cost, path_len, path, path_cap, n_expanded, expand, expand_cap,
                        counters, status, queue, spill, heap_cap, lds_cap, cdir, cg);
     PMP_HIP_CHECK(ctx, hipGetLastError());
