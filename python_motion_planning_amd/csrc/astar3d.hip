@@ -142,6 +142,11 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
         int n = 1;
         uint32_t seq = 1;
         int64_t npush = 1, npop = 0, niter = 0;
+#ifdef PMP_STAMPS
+        // diagnostic build: cycles in (pop + the overlapped HBM round), after-pop wait, push loop, whole query
+        uint64_t cyc_pop = 0, cyc_wait = 0, cyc_push = 0;
+        const uint64_t cyc_q0 = __builtin_amdgcn_s_memtime();
+#endif
         int nexp = 0, maxn = 1, st = PMP_NO_PATH, plen = 0;
         double goal_cost = __builtin_inf();
 
@@ -193,15 +198,38 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
                 }
             }
             // ---- pop
+#ifdef PMP_STAMPS
+            const uint64_t ts0 = __builtin_amdgcn_s_memtime();
+#endif
             if (n > 0) {
                 if (n < lds_cap) heap16::pop<Key3, false>(hp, qc, n, root, lane, pop_jl, pop_ol);
                 else heap16::pop<Key3, true>(hp, qc, n, root, lane, pop_jl, pop_ol);
             }
+#ifdef PMP_STAMPS
+            const uint64_t ts1 = __builtin_amdgcn_s_memtime();
+#endif
             // best_closed check (a_star3d.py:48-50)
             const bool sclosed = rl_u32(ncd, 26) != 0u;
             const double scg = rl_f64(ncg, 26);
+#ifdef PMP_STAMPS
+            const uint64_t ts2 = __builtin_amdgcn_s_memtime();
+            cyc_pop += ts1 - ts0;
+            cyc_wait += ts2 - ts1;
+#endif
             if (sclosed && node.g >= scg) continue;
             niter++;
+            // Neighbour decisions first (:66-75): they consume this round's loads before any store is
+            // issued below, so the compiler never has to drain those stores (vmcnt) to read them.
+            const double tg = node.g + mcost;
+            const bool ok = lane < 26 && !coll && !(ncd != 0u && tg >= ncg);
+            // The key (f, h, counter) is a total order, so only the heap's contents matter.  An entry
+            // whose cell already has a pending entry with g <= tg pops after it (f = g + h, equal
+            // g -> earlier counter) and is then skipped by the CLOSED check (:48-50): it is dead on
+            // arrival and is not inserted.  A strictly better entry is inserted and makes the old
+            // one dead instead (skipped the same way when it pops).
+            const bool live = ok && tg < nog;
+            const uint32_t okm = (uint32_t)ballot(ok);
+            uint64_t vm = ballot(live);
             if (lane == 0) {
                 if (!sclosed) {
                     if (expand_out && nexp < expand_cap) expand_out[(size_t)q * expand_cap + nexp] = lin;
@@ -244,25 +272,15 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
                 }
                 break;
             }
-            // ---- neighbours (:66-75): skip if CLOSED with g <= tentative_g, else push with counter
-            const double tg = node.g + mcost;
-            const bool ok = lane < 26 && !coll && !(ncd != 0u && tg >= ncg);
-            npush += __popcll(ballot(ok));  // the reference's pushes (:66-75)
-            // The key (f, h, counter) is a total order, so only the heap's contents matter.  An entry
-            // whose cell already has a pending entry with g <= tg pops after it (f = g + h, equal
-            // g -> earlier counter) and is then skipped by the CLOSED check (:48-50): it is dead on
-            // arrival and is not inserted.  A strictly better entry is inserted and makes the old
-            // one dead instead (skipped the same way when it pops).
-            const bool live = ok && tg < nog;
+            // ---- neighbours (:66-75): push the live ones with the reference's counters
+            npush += __popc(okm);  // the reference's pushes
             if (live) og[nlin] = tg;
-            uint64_t vm = ballot(live);
             Ent item;
             item.g = tg;
             item.a = 0u;
             item.b = ((((uint32_t)nx & 255u) << 16) | (((uint32_t)ny & 255u) << 8) | ((uint32_t)nz & 255u)) << 5 | (uint32_t)(lane < 26 ? lane : 0);
             qc.derive(item);
             bool overflow = false;
-            uint32_t okm = (uint32_t)ballot(ok);
             while (vm) {
                 const int m = __ffsll((long long)vm) - 1;
                 vm &= vm - 1;
@@ -275,6 +293,9 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
                 n += 1;
             }
             seq += (uint32_t)__popc(okm);
+#ifdef PMP_STAMPS
+            cyc_push += __builtin_amdgcn_s_memtime() - ts2;
+#endif
             if (n > maxn) maxn = n;
             if (overflow) { st = PMP_CAP_OVERFLOW; break; }
         }
@@ -286,10 +307,17 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
             path_len_out[q] = st == PMP_FOUND ? plen : 0;
             nexp_out[q] = nexp;
             if (counters) {
+#ifdef PMP_STAMPS
+                counters[4 * q + 0] = (int64_t)cyc_pop;
+                counters[4 * q + 1] = (int64_t)cyc_wait;
+                counters[4 * q + 2] = (int64_t)cyc_push;
+                counters[4 * q + 3] = (int64_t)(__builtin_amdgcn_s_memtime() - cyc_q0);
+#else
                 counters[4 * q + 0] = npush;
                 counters[4 * q + 1] = npop;
                 counters[4 * q + 2] = niter;
                 counters[4 * q + 3] = maxn;
+#endif
             }
         }
         heap16::wsync();

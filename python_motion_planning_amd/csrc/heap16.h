@@ -131,20 +131,21 @@ __device__ __forceinline__ void pop(const Heap& hp, const K& key, int n, Ent& ro
         const uint64_t mrmask = ballot(vr & K::lt(R, last));
         int cur = uni(hole), oc = 0;
         uint64_t mover = 0, movr = 0;
-        bool go = true;
+        uint32_t go = 1u;
+        // branch-free scalar walk: every step is a select, so the 6 levels are one straight-line
+        // SALU sequence (taken branches cost more than the arithmetic they skip)
 #pragma unroll
         for (int lv = 1; lv <= 6; lv++) {
             const int c = 2 * cur + 1;
             const int pl = (1 << (lv - 1)) - 1 + oc;
-            const int r = (int)((dmask >> pl) & 1ull);
+            const uint32_t r = (uint32_t)(dmask >> pl) & 1u;
             const uint64_t mm = r ? mrmask : mlmask;
-            go = go & (c < n) & (((mm >> pl) & 1ull) != 0ull);
-            if (go) {
-                mover |= 1ull << pl;
-                movr |= (uint64_t)r << pl;
-                cur = c + r;
-                oc = 2 * oc + r;
-            }
+            go = go & (uint32_t)(c < n) & ((uint32_t)(mm >> pl) & 1u);
+            const uint64_t bit = (uint64_t)go << pl;
+            mover |= bit;
+            movr |= (uint64_t)(go & r) << pl;
+            cur = go ? c + (int)r : cur;
+            oc = go ? 2 * oc + (int)r : oc;
         }
         if ((mover >> lane) & 1ull) {
             const bool rr = (movr >> lane) & 1ull;
