@@ -26,6 +26,8 @@ constexpr int kMaxObs = 256;   // per obstacle kind
 constexpr int kMaxBnd = 8;
 constexpr int kMaxA = 2048;    // collision-free improving candidates per iteration
 constexpr int kMaxT = 4096;    // candidates awaiting a collision test per phase
+constexpr int kMaxK = 1024;    // in-radius candidates kept in LDS (more spill to the HBM list)
+constexpr int kRnd = 1024;     // random doubles staged in LDS
 
 constexpr int KF_A = 1;        // c_i < G0
 constexpr int KF_VALID = 2;    // ... and collision-free
@@ -69,6 +71,11 @@ struct RrtShared {
     double ac[kMaxA];
     int tk[kMaxT];      // K entries awaiting a collision test
     double tG[kMaxT];   // ... and their G_{i-1}
+    // in-radius candidates (first kMaxK in LDS, with the node's coordinates and g loaded once)
+    int kj[kMaxK], kf[kMaxK];
+    double kd[kMaxK], kx[kMaxK], ky[kMaxK], kg[kMaxK];
+    double rbuf[kRnd];  // window of the query's random stream
+    double nearx, neary, nearg;
     int nK, nA, nT, slot;
 };
 
@@ -203,6 +210,30 @@ __device__ void block_min_di(double& v, int& i, RrtShared& S)
     __syncthreads();
 }
 
+struct KRec {
+    int j, fl;
+    double d, x, y, g;
+};
+
+// candidate k: from LDS, or (k >= kMaxK) from the HBM list plus the node arrays
+__device__ __forceinline__ KRec kget(const RrtShared& S, const KEntry* kl, const double* tx, const double* tg, int k)
+{
+    KRec r;
+    if (k < kMaxK) {
+        r.j = S.kj[k]; r.fl = S.kf[k]; r.d = S.kd[k]; r.x = S.kx[k]; r.y = S.ky[k]; r.g = S.kg[k];
+    } else {
+        const KEntry e = kl[k];
+        r.j = e.j; r.fl = e.flags; r.d = e.d; r.x = tx[2 * e.j]; r.y = tx[2 * e.j + 1]; r.g = tg[e.j];
+    }
+    return r;
+}
+
+__device__ __forceinline__ void kset_flags(RrtShared& S, KEntry* kl, int k, int fl)
+{
+    if (k < kMaxK) S.kf[k] = fl;
+    else kl[k].flags = fl;
+}
+
 template <bool STAR>
 __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
 {
@@ -239,12 +270,20 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
     int64_t cur = 0;
     int64_t c_iter = 0, c_scan = 0, c_cand = 0, c_tests = 0;  // iterations, nodes scanned, in-radius, collision tests
 
+    int64_t rb0 = 0, rb1 = 0;  // staged window [rb0, rb1) of the random stream
     for (int it = 0; it < P.sample_num; it++) {
         if (cur + 3 > A.stride) { status = PMP_CAP_OVERFLOW; break; }
+        if (cur + 3 > rb1) {
+            __syncthreads();
+            rb0 = cur;
+            rb1 = rb0 + kRnd < A.stride ? rb0 + kRnd : A.stride;
+            for (int i = tid; i < (int)(rb1 - rb0); i += kNT) S.rbuf[i] = rnd[rb0 + i];
+            __syncthreads();
+        }
         double sx = gx, sy = gy;
-        if (rnd[cur++] > P.goal_sample_rate) {
-            sx = lox + rgx * rnd[cur++];
-            sy = loy + rgy * rnd[cur++];
+        if (S.rbuf[cur++ - rb0] > P.goal_sample_rate) {
+            sx = lox + rgx * S.rbuf[cur++ - rb0];
+            sy = loy + rgy * S.rbuf[cur++ - rb0];
         }
         c_iter++;
         c_scan += n;
@@ -259,22 +298,26 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         const float m = block_min_f(best, S);
         const double band = sqrt((double)m) + 2.0 * eps;
         const float T = (float)(band * band) * 1.0001f;
-        double h = INFINITY;
+        double h = INFINITY, hx = 0.0, hy = 0.0, hg = 0.0;
         int hi = 0x7fffffff;
         if (best <= T) {
             for (int j = tid; j < n; j += kNT) {
                 const float2 p = xyf[j];
                 const float dx = p.x - sxf, dy = p.y - syf;
                 if (dx * dx + dy * dy <= T) {
-                    const double e = lp::py_hypot(tx[2 * j] - sx, tx[2 * j + 1] - sy);
-                    if (e < h) { h = e; hi = j; }  // increasing j per thread: keeps the first
+                    const double xj = tx[2 * j], yj = tx[2 * j + 1], gj = tg[j];  // one round
+                    const double e = lp::py_hypot(xj - sx, yj - sy);
+                    if (e < h) { h = e; hi = j; hx = xj; hy = yj; hg = gj; }  // increasing j: keeps the first
                 }
             }
         }
+        const int my_hi = hi;
         block_min_di(h, hi, S);
         if (h == 0.0) continue;  // node_rand.current already in sample_list
+        if (my_hi == hi) { S.nearx = hx; S.neary = hy; S.nearg = hg; }  // the owner publishes the node
+        __syncthreads();
         const int near = hi;
-        const double nx0 = tx[2 * near], ny0 = tx[2 * near + 1], gnear = tg[near];
+        const double nx0 = S.nearx, ny0 = S.neary, gnear = S.nearg;
         // ---- 3. steer + collision (rrt.py:121-129) ----
         double dist = lp::py_hypot(sx - nx0, sy - ny0);
         const double theta = atan2(sy - ny0, sx - nx0);
@@ -298,17 +341,22 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                 const float2 p = xyf[j];
                 const float dx = p.x - nxf, dy = p.y - nyf;
                 if (dx * dx + dy * dy > Tr) continue;
-                const double xj = tx[2 * j], yj = tx[2 * j + 1];
+                const double xj = tx[2 * j], yj = tx[2 * j + 1], gj = tg[j];  // one round
                 if (xj == nx && yj == ny) atomicMin(&S.slot, j);
                 const double d = lp::py_hypot(nx - xj, ny - yj);
                 if (!(d < P.radius)) continue;
                 const int k = atomicAdd(&S.nK, 1);
-                KEntry e;
-                e.j = j;
-                e.d = d;
-                e.flags = (tg[j] + d < G0) ? KF_A : 0;
-                kl[k] = e;
-                if (e.flags & KF_A) {
+                const int fl = (gj + d < G0) ? KF_A : 0;
+                if (k < kMaxK) {
+                    S.kj[k] = j; S.kf[k] = fl; S.kd[k] = d; S.kx[k] = xj; S.ky[k] = yj; S.kg[k] = gj;
+                } else {
+                    KEntry e;
+                    e.j = j;
+                    e.d = d;
+                    e.flags = fl;
+                    kl[k] = e;
+                }
+                if (fl & KF_A) {
                     const int t = atomicAdd(&S.nT, 1);
                     if (t < kMaxT) S.tk[t] = k;
                 }
@@ -324,12 +372,12 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             // ---- 4b. one wave per test: the collision-free improving set ----
             for (int t = wave; t < nT; t += kWaves) {
                 const int k = S.tk[t];
-                const KEntry e = kl[k];
-                if (collision_wave(S, nr, nc, nb, delta, tx[2 * e.j], tx[2 * e.j + 1], nx, ny)) continue;
+                const KRec e = kget(S, kl, tx, tg, k);
+                if (collision_wave(S, nr, nc, nb, delta, e.x, e.y, nx, ny)) continue;
                 if (lane == 0) {
                     const int a = atomicAdd(&S.nA, 1);
-                    if (a < kMaxA) { S.aj[a] = e.j; S.ac[a] = tg[e.j] + e.d; }
-                    kl[k].flags = KF_A | KF_VALID;
+                    if (a < kMaxA) { S.aj[a] = e.j; S.ac[a] = e.g + e.d; }
+                    kset_flags(S, kl, k, KF_A | KF_VALID);
                 }
             }
             __syncthreads();
@@ -344,16 +392,16 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             if (cb < G0) { G = cb; parent = jb; }
             // ---- 4c. rewire decisions; untested candidates queue for a collision test ----
             for (int k = tid; k < nK; k += kNT) {
-                const KEntry e = kl[k];
+                const KRec e = kget(S, kl, tx, tg, k);
                 double Gp = G0;
                 for (int a = 0; a < nA; a++)
                     if (S.aj[a] < e.j) Gp = fmin(Gp, S.ac[a]);
-                const double gj = tg[e.j];
-                if ((e.flags & KF_VALID) && Gp > gj + e.d) continue;  // node_new re-parents here
+                const double gj = e.g;
+                if ((e.fl & KF_VALID) && Gp > gj + e.d) continue;  // node_new re-parents here
                 const double c2 = Gp + e.d;
                 if (!(gj > c2)) continue;
-                if (e.flags & KF_A) {
-                    if (e.flags & KF_VALID) { tg[e.j] = c2; tpar[e.j] = slot; }
+                if (e.fl & KF_A) {
+                    if (e.fl & KF_VALID) { tg[e.j] = c2; tpar[e.j] = slot; }
                     continue;
                 }
                 const int t = atomicAdd(&S.nT, 1);
@@ -364,8 +412,8 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             if (nT2 > kMaxT) { status = PMP_CAP_OVERFLOW; break; }
             c_tests += nT2;
             for (int t = wave; t < nT2; t += kWaves) {
-                const KEntry e = kl[S.tk[t]];
-                if (collision_wave(S, nr, nc, nb, delta, tx[2 * e.j], tx[2 * e.j + 1], nx, ny)) continue;
+                const KRec e = kget(S, kl, tx, tg, S.tk[t]);
+                if (collision_wave(S, nr, nc, nb, delta, e.x, e.y, nx, ny)) continue;
                 if (lane == 0) { tg[e.j] = S.tG[t] + e.d; tpar[e.j] = slot; }
             }
             __syncthreads();  // rewires land before the insert below may overwrite a duplicate slot
