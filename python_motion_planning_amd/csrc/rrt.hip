@@ -3,10 +3,11 @@
 //
 // Per iteration (all decisions wave-uniform, results identical to the reference's sequential loop):
 //  1. sample from the query's np.random stream (generateRandomNode, rrt.py:91-103);
-//  2. nearest node = first argmin of the exact CPython hypot (rrt.py:117-118).  A coarse pass over an
-//     f32 copy of the coordinates (8 B/node) finds the minimum; only nodes within a rigorous f32
-//     error band of it are re-evaluated exactly in f64; ties resolve to the lowest index.  A zero
-//     distance means the sample is already in sample_list (rrt.py:67-68);
+//  2. nearest node = first argmin of the exact CPython hypot (rrt.py:117-118).  A coarse pass over a
+//     16-bit fixed-point copy of the coordinates (4 B/node, so 32 trees stay in an XCD's L2) finds
+//     the minimum; only nodes within a rigorous error band of it are re-evaluated exactly in f64;
+//     ties resolve to the lowest index.  A zero distance means the sample is already in
+//     sample_list (rrt.py:67-68);
 //  3. steer (hypot, atan2, cos, sin) and isCollision(new, near), the obstacle tests spread over the
 //     workgroup;
 //  4. RRT*: the sequential choose-parent/rewire scan (rrt_star.py:57-73) in parallel form.  With
@@ -56,7 +57,7 @@ struct RrtArgs {
     int64_t* draws;
     int32_t* status;
     int64_t* counters;  // nullable [nq][4]
-    float2* xyf;      // scratch [nq][cap]
+    uint32_t* xyq;    // scratch [nq][cap]: 16-bit fixed-point x | y << 16 (the coarse scan copy)
     KEntry* klist;    // scratch [nq][cap]
 };
 
@@ -251,21 +252,35 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
     double* tx = A.txy + (size_t)q * cap * 2;
     double* tg = A.tg + (size_t)q * cap;
     int32_t* tpar = A.tpar + (size_t)q * cap;
-    float2* xyf = A.xyf + (size_t)q * cap;
+    uint32_t* xyq = A.xyq + (size_t)q * cap;
     KEntry* kl = A.klist + (size_t)q * cap;
     const double* rnd = A.rnd + (size_t)q * A.stride;
     const double sx0 = A.start[2 * q], sy0 = A.start[2 * q + 1];
     const double gx = A.goal[2 * q], gy = A.goal[2 * q + 1];
+    // Coarse coordinates: every node lies in the box spanned by the map, the start and the goal
+    // (steering moves toward samples inside the map), quantised to 16 bits per axis.  A decoded
+    // value is within half a step (+ f32 rounding) of the node, so the f32 distance of the coarse
+    // copy is within eps of the exact one: candidates within 2*eps of the coarse minimum include
+    // every exact-minimum node, and the exact f64 CPython hypot decides among them.
+    const double qlo = fmin(fmin(0.0, fmin(sx0, sy0)), fmin(gx, gy));
+    const double qhi = fmax(fmax(fmax(P.x_range, P.y_range), fmax(sx0, sy0)), fmax(gx, gy));
+    const double qscale = 65535.0 / (qhi - qlo);
+    const float qinv = (float)((qhi - qlo) / 65535.0);
+    const float qlof = (float)qlo;
+    auto qenc = [&](double x, double y) -> uint32_t {
+        const double ux = fmin(fmax(rint((x - qlo) * qscale), 0.0), 65535.0);
+        const double uy = fmin(fmax(rint((y - qlo) * qscale), 0.0), 65535.0);
+        return (uint32_t)ux | ((uint32_t)uy << 16);
+    };
     if (tid == 0) {
         tx[0] = sx0; tx[1] = sy0; tg[0] = 0.0; tpar[0] = 0;
-        xyf[0] = make_float2((float)sx0, (float)sy0);
+        xyq[0] = qenc(sx0, sy0);
     }
     __syncthreads();
     const double lox = delta, rgx = (P.x_range - delta) - delta;
     const double loy = delta, rgy = (P.y_range - delta) - delta;
-    // f32 error band: coordinates of magnitude <= cmax carry <= cmax * 2^-24 rounding each
-    const double cmax = fmax(fmax(P.x_range, P.y_range), fmax(fmax(fabs(gx), fabs(gy)), fmax(fabs(sx0), fabs(sy0)))) + 1.0;
-    const double eps = 4e-6 * cmax + 1e-5;
+    // |coarse - exact| per node distance <= sqrt(2) * (half step + f32 decode rounding) + f32 arithmetic
+    const double eps = (qhi - qlo) / 65535.0 + 1e-6 * (qhi - qlo) + 2e-4;
     int n = 1, status = 1;
     int64_t cur = 0;
     int64_t c_iter = 0, c_scan = 0, c_cand = 0, c_tests = 0;  // iterations, nodes scanned, in-radius, collision tests
@@ -290,10 +305,26 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         // ---- 2. nearest ----
         const float sxf = (float)sx, syf = (float)sy;
         float best = INFINITY;
-        for (int j = tid; j < n; j += kNT) {
-            const float2 p = xyf[j];
-            const float dx = p.x - sxf, dy = p.y - syf;
-            best = fminf(best, dx * dx + dy * dy);
+        {
+            // 8 loads in flight per thread: the scan is bound by L2/MALL latency, not bandwidth
+            int j = tid;
+            for (; j + 7 * kNT < n; j += 8 * kNT) {
+                uint32_t p[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) p[u] = xyq[j + u * kNT];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const float dx = fmaf((float)(p[u] & 0xFFFFu), qinv, qlof) - sxf;
+                    const float dy = fmaf((float)(p[u] >> 16), qinv, qlof) - syf;
+                    best = fminf(best, dx * dx + dy * dy);
+                }
+            }
+            for (; j < n; j += kNT) {
+                const uint32_t p = xyq[j];
+                const float dx = fmaf((float)(p & 0xFFFFu), qinv, qlof) - sxf;
+                const float dy = fmaf((float)(p >> 16), qinv, qlof) - syf;
+                best = fminf(best, dx * dx + dy * dy);
+            }
         }
         const float m = block_min_f(best, S);
         const double band = sqrt((double)m) + 2.0 * eps;
@@ -302,8 +333,9 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         int hi = 0x7fffffff;
         if (best <= T) {
             for (int j = tid; j < n; j += kNT) {
-                const float2 p = xyf[j];
-                const float dx = p.x - sxf, dy = p.y - syf;
+                const uint32_t p = xyq[j];
+                const float dx = fmaf((float)(p & 0xFFFFu), qinv, qlof) - sxf;
+                const float dy = fmaf((float)(p >> 16), qinv, qlof) - syf;
                 if (dx * dx + dy * dy <= T) {
                     const double xj = tx[2 * j], yj = tx[2 * j + 1], gj = tg[j];  // one round
                     const double e = lp::py_hypot(xj - sx, yj - sy);
@@ -337,10 +369,19 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             const float nxf = (float)nx, nyf = (float)ny;
             const double rb = P.radius + 2.0 * eps;
             const float Tr = (float)(rb * rb) * 1.0001f;
-            for (int j = tid; j < n; j += kNT) {
-                const float2 p = xyf[j];
-                const float dx = p.x - nxf, dy = p.y - nyf;
-                if (dx * dx + dy * dy > Tr) continue;
+            for (int j0 = tid; j0 < n; j0 += 8 * kNT) {
+                uint32_t p[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) p[u] = (j0 + u * kNT < n) ? xyq[j0 + u * kNT] : 0u;
+                uint32_t hits = 0;
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const float dx = fmaf((float)(p[u] & 0xFFFFu), qinv, qlof) - nxf;
+                    const float dy = fmaf((float)(p[u] >> 16), qinv, qlof) - nyf;
+                    hits |= (uint32_t)((j0 + u * kNT < n) & (dx * dx + dy * dy <= Tr)) << u;
+                }
+              for (; hits; hits &= hits - 1) {
+                const int j = j0 + (__ffs(hits) - 1) * kNT;
                 const double xj = tx[2 * j], yj = tx[2 * j + 1], gj = tg[j];  // one round
                 if (xj == nx && yj == ny) atomicMin(&S.slot, j);
                 const double d = lp::py_hypot(nx - xj, ny - yj);
@@ -360,6 +401,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                     const int t = atomicAdd(&S.nT, 1);
                     if (t < kMaxT) S.tk[t] = k;
                 }
+              }
             }
             __syncthreads();
             const int nK = S.nK;
@@ -421,7 +463,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         // ---- 5. insert + goal test (rrt.py:70-81) ----
         if (tid == 0) {
             tx[2 * slot] = nx; tx[2 * slot + 1] = ny; tg[slot] = G; tpar[slot] = parent;
-            xyf[slot] = make_float2((float)nx, (float)ny);
+            xyq[slot] = qenc(nx, ny);
         }
         if (slot == n) {
             if (n >= cap) { status = PMP_CAP_OVERFLOW; break; }
@@ -434,7 +476,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             if (n >= cap) { status = PMP_CAP_OVERFLOW; break; }
             if (tid == 0) {
                 tx[2 * n] = gx; tx[2 * n + 1] = gy; tg[n] = G + lp::py_hypot(nx - gx, ny - gy); tpar[n] = slot;
-                xyf[n] = make_float2((float)gx, (float)gy);
+                xyq[n] = qenc(gx, gy);
             }
             n++;
             status = PMP_FOUND;
@@ -493,9 +535,9 @@ extern "C" int pmp_rrt_batch(pmp_ctx* ctx, void* stream, const pmp_rrt_params* p
         !tree_parent || !n_nodes || !cost || !path_len || (path_cap && !path_xy) || !draws || !status)
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_rrt_batch: null pointer argument");
     PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
-    float2* xyf = (float2*)pmp_scratch(ctx, SCR_AUX0, sizeof(float2) * (size_t)nq * tree_cap);
+    uint32_t* xyq = (uint32_t*)pmp_scratch(ctx, SCR_AUX0, sizeof(uint32_t) * (size_t)nq * tree_cap);
     KEntry* kl = (KEntry*)pmp_scratch(ctx, SCR_AUX1, sizeof(KEntry) * (size_t)nq * tree_cap);
-    if (!xyf || !kl) return PMP_ENOMEM;
+    if (!xyq || !kl) return PMP_ENOMEM;
     RrtArgs A;
     A.P = *p;
     A.rect = rect; A.circ = circ; A.bnd = bnd;
@@ -504,7 +546,7 @@ extern "C" int pmp_rrt_batch(pmp_ctx* ctx, void* stream, const pmp_rrt_params* p
     A.rnd = rnd; A.stride = rnd_stride; A.cap = tree_cap;
     A.txy = tree_xy; A.tg = tree_g; A.tpar = tree_parent; A.n_nodes = n_nodes;
     A.cost = cost; A.path_len = path_len; A.path = path_xy; A.path_cap = path_cap;
-    A.draws = draws; A.status = status; A.counters = counters; A.xyf = xyf; A.klist = kl;
+    A.draws = draws; A.status = status; A.counters = counters; A.xyq = xyq; A.klist = kl;
     if (p->star)
         hipLaunchKernelGGL(rrt_kernel<true>, dim3(nq), dim3(kNT), 0, (hipStream_t)stream, A);
     else
