@@ -10,8 +10,10 @@
 //  - np.sum of a column = numpy pairwise summation (leaves of <= 128 with 8 accumulators, splits at
 //    n/2 rounded down to a multiple of 8), evaluated as that exact tree.
 //  - (eval_win @ factor)[:, 2] = fma(e4, vw, fma(e3, ow, fma(e2, hw, fma(e1, 0, e0*0)))) (OpenBLAS).
-//  - sin/cos/atan2 are the device libm (<= 1 ulp from glibc): trajectories agree to the last bits and
-//    decisions are checked tie-aware in the tests.
+//  - sin/cos/atan2 are the device libm (<= 1 ulp from glibc); inside a sample's rollout cos/sin(th_k)
+//    come from a rotation recurrence (within ~2e-14 of libm over H = 30 steps): trajectories agree
+//    to ~1e-14 and decisions are checked tie-aware in the tests.
+//  - the occupancy bitmap is staged in LDS when it fits (16 KiB).
 #include "localplan.h"
 
 namespace {
@@ -44,7 +46,11 @@ __device__ inline double linsp_at(const Linsp& L, int i)
     return L.step == 0.0 ? ((double)i / L.div) * L.delta + L.a : (double)i * L.step + L.a;
 }
 
-__device__ inline bool occ_at(const uint32_t* occ, int ox, int oy, int W, int H, int cx, int cy)
+typedef __attribute__((address_space(3))) uint32_t lds_w32;
+constexpr int kOccLdsWords = 4096;  // grids up to 131072 cells keep their occupancy in LDS (16 KiB)
+
+template <class PTR>
+__device__ inline bool occ_at(PTR occ, int ox, int oy, int W, int H, int cx, int cy)
 {
     const int i = cx - ox, j = cy - oy;
     if ((unsigned)i >= (unsigned)W || (unsigned)j >= (unsigned)H) return false;
@@ -77,6 +83,7 @@ __device__ inline int pw_half(int n)
 }
 
 struct DwaShared {
+    uint32_t occ[kOccLdsWords];      // the occupancy bitmap (when it fits)
     double col[3][kMaxN];            // heading, obstacle, velocity per sample
     double leafsum[3][kMaxLeaves];
     int leaf_lo[kMaxLeaves], leaf_n[kMaxLeaves];
@@ -128,6 +135,7 @@ __device__ inline double pw_combine(const double* leafsum, int n)
     return ret;
 }
 
+template <bool OCC_LDS>
 __global__ __launch_bounds__(kThreads) void dwa_kernel(
     const uint32_t* __restrict__ occ, int ox, int oy, int W, int H, pmp_lp_params P, pmp_dwa_params D, int na,
     double* __restrict__ state, const double* __restrict__ goal, const double* __restrict__ path_xy,
@@ -140,6 +148,12 @@ __global__ __launch_bounds__(kThreads) void dwa_kernel(
     const int a = blockIdx.x;
     const int tid = threadIdx.x;
     if (a >= na) return;
+    if (OCC_LDS) {
+        const int words = (int)(((size_t)W * H + 31) / 32);
+        for (int i = tid; i < words; i += kThreads) S.occ[i] = occ[i];
+        __syncthreads();
+    }
+    const lds_w32* occl = (const lds_w32*)S.occ;
     const double* path = path_xy + 2 * (size_t)path_off[a];
     const int Pn = path_off[a + 1] - path_off[a];
     const double gl[3] = {goal[3 * a], goal[3 * a + 1], goal[3 * a + 2]};
@@ -175,10 +189,17 @@ __global__ __launch_bounds__(kThreads) void dwa_kernel(
             const double v = linsp_at(LV, c / nw), w = linsp_at(LW, c % nw);
             double x = st[0], y = st[1], th = st[2];
             double mind = INFINITY;
+            // cos/sin of th_k by rotation: th_k = th_0 + k*(dt*w) up to the rounding of the running
+            // sum (which th itself keeps exactly as the reference), so (cs, sn) stay within ~2e-14
+            // of libm's cos/sin(th_k) over the horizon -- one sincos pair per sample, not per step.
+            double sn, cs, sd, cd;
+            sincos(th, &sn, &cs);
+            sincos(dt * w, &sd, &cd);
             for (int k = 0; k < Hh; k++) {
-                double sn, cs;
-                sincos(th, &sn, &cs);
                 const double nx = x + (dt * cs) * v, ny = y + (dt * sn) * v, nth = th + dt * w;
+                const double ncs = cs * cd - sn * sd, nsn = sn * cd + cs * sd;
+                cs = ncs;
+                sn = nsn;
                 x = nx;
                 y = ny;
                 th = nth;
@@ -186,7 +207,8 @@ __global__ __launch_bounds__(kThreads) void dwa_kernel(
                 const int y0 = (int)ceil(y - R), y1 = (int)floor(y + R);
                 for (int cx = x0; cx <= x1 && cx <= x0 + 16; cx++)
                     for (int cy = y0; cy <= y1 && cy <= y0 + 16; cy++) {
-                        if (!occ_at(occ, ox, oy, W, H, cx, cy)) continue;
+                        const bool o = OCC_LDS ? occ_at(occl, ox, oy, W, H, cx, cy) : occ_at(occ, ox, oy, W, H, cx, cy);
+                        if (!o) continue;
                         const double dx = (double)cx - x, dy = (double)cy - y;
                         const double d = sqrt(dx * dx + dy * dy);
                         if (d < mind) mind = d;
@@ -310,7 +332,9 @@ extern "C" int pmp_dwa_step_batch(pmp_ctx* ctx, void* stream, const uint32_t* oc
     if (dp->nv * dp->nw > kMaxN || !(lp->dt > 0) || !(dp->predict_time >= 0))
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_dwa_step_batch: nv*nw must be <= 4096 and dt > 0");
     PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
-    hipLaunchKernelGGL(dwa_kernel, dim3(na), dim3(kThreads), sizeof(DwaShared), (hipStream_t)stream, occ_bits, ox, oy, W,
+    const bool occ_lds = ((size_t)W * H + 31) / 32 <= (size_t)kOccLdsWords;
+    auto kern = occ_lds ? dwa_kernel<true> : dwa_kernel<false>;
+    hipLaunchKernelGGL(kern, dim3(na), dim3(kThreads), sizeof(DwaShared), (hipStream_t)stream, occ_bits, ox, oy, W,
                        H, *lp, *dp, na, state, goal, path_xy, path_off, iters, u, best, status, n_steps, hist_pose, eval,
                        best_traj);
     PMP_HIP_CHECK(ctx, hipGetLastError());
