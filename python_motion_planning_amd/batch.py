@@ -28,13 +28,17 @@ def occ_bits_device(occ, torch=None):
 
 def astar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: int | None = None,
                   expand_cap: int = 0, counters: bool = False, occ_bits=None, reserve_slots: int | None = None,
-                  heap_cap: int = 0):
+                  heap_cap: int = 0, retry_overflow: bool = True):
     """Batched AStar.plan (a_star.py:39-83).
 
     occ: numpy uint8 [W, H] (or pass occ=(W, H) with a prebuilt `occ_bits` device tensor).
     starts, goals: [nq, 2] int (numpy or device tensors).
     Returns dict of device tensors: cost f64 [nq], path_len i32 [nq], path i32 [nq, path_cap]
     (cell ids x*H+y, goal first), n_expanded i32, status i32, optional expand / counters.
+
+    A query whose heap outgrows the reserved capacity stops with STATUS_CAP_OVERFLOW; with
+    retry_overflow those queries are planned again on the GPU with the full bound (8 W H + 8
+    entries) on fewer workers -- one host sync to read the statuses.
     """
     torch = _lib.device_check()
     L = _lib.load_library()
@@ -66,6 +70,19 @@ def astar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: in
                              out["n_expanded"].data_ptr(), _lib.ptr(out["expand"]), int(expand_cap),
                              _lib.ptr(out["counters"]), out["status"].data_ptr())
     _lib.check(ctx, rc, "pmp_astar2d_batch")
+    if retry_overflow:
+        redo = torch.nonzero(out["status"] == _lib.STATUS_CAP_OVERFLOW).flatten()
+        if redo.numel():
+            full = 8 * W * H + 8
+            workers = max(1, min(int(redo.numel()), 256))
+            _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, workers, full), "pmp_astar2d_reserve")
+            r = astar2d_batch((W, H), s[redo], g[redo], heuristic, path_cap, expand_cap, counters, occ_bits,
+                              retry_overflow=False)
+            for k in ("cost", "path_len", "path", "n_expanded", "status", "expand", "counters"):
+                if out[k] is not None:
+                    out[k][redo] = r[k]
+            _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, int(reserve_slots or 1024), int(heap_cap)),
+                       "pmp_astar2d_reserve")
     out["W"], out["H"] = W, H
     return out
 

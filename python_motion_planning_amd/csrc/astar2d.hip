@@ -289,12 +289,10 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
     const int pop_ol = lane + 1 - (1 << (pop_jl - 1));
 
     for (;;) {
-        int qi = 0;
-        if (lane == 0) qi = atomicAdd(queue, 1);
         // readfirstlane (not __shfl): the compiler must SEE the query index as wave-uniform, or
         // every value derived from it (coordinates, heap size, walk state) lands in VGPRs and the
         // scalar heap walk is compiled as a divergent loop.
-        qi = uni(qi);
+        const int qi = next_query(queue, lane);
         if (qi >= nq) break;
         const int q = uni(order ? order[qi] : qi);
 
@@ -314,14 +312,13 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
         const bool s_in = (unsigned)sx < (unsigned)W && (unsigned)sy < (unsigned)H;
         const bool g_in = (unsigned)qc.gx < (unsigned)W && (unsigned)qc.gy < (unsigned)H;
         if (!s_in || !g_in) {  // outside the grid: blocked -> no neighbours -> no path
-            if (lane == 0) {
-                status_out[q] = PMP_NO_PATH;
-                cost_out[q] = 0.0;
-                path_len_out[q] = 0;
-                nexp_out[q] = s_in ? 1 : 0;
-                if (counters) {
-                    counters[4 * q] = 1; counters[4 * q + 1] = 1; counters[4 * q + 2] = s_in ? 1 : 0; counters[4 * q + 3] = 1;
-                }
+            // every lane stores the same values: no lane-0-only block right before the continue
+            status_out[q] = PMP_NO_PATH;
+            cost_out[q] = 0.0;
+            path_len_out[q] = 0;
+            nexp_out[q] = s_in ? 1 : 0;
+            if (counters) {
+                counters[4 * q] = 1; counters[4 * q + 1] = 1; counters[4 * q + 2] = s_in ? 1 : 0; counters[4 * q + 3] = 1;
             }
             continue;
         }
@@ -531,11 +528,17 @@ int default_lds_cap(int workers_per_cu)
     int bytes = (160 * 1024) / workers_per_cu - 256;
     return (bytes / 12) & ~15;
 }
+// The heap never holds more than 8 * expansions + 1 <= 8 W H + 1 entries; the default cap is far
+// below that bound (C2's largest heap is ~10k entries).  A query that outgrows its cap stops with
+// PMP_CAP_OVERFLOW and the host re-runs it with a larger reservation (batch.astar2d_batch).
+size_t max_heap(int W, int H) { return 8 * (size_t)W * H + 8; }
 int default_heap_cap(int W, int H)
 {
-    size_t c = 8 * (size_t)W * H + 8;
-    return (int)(c < (size_t)(1 << 20) ? c : (size_t)(1 << 20));
+    const size_t c = max_heap(W, H);
+    return (int)(c < (size_t)(1 << 16) ? c : (size_t)(1 << 16));
 }
+// per-context scratch budget: workers are reduced to fit (heap spill + cell state + G per worker)
+constexpr size_t kScratchBudget = (size_t)64 << 30;
 
 }  // namespace
 
@@ -545,11 +548,18 @@ extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int workers, int 
     if (W < 1 || H < 1 || W > kMaxDim || H > kMaxDim || workers < 1)
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_reserve: bad dims/workers");
     if (heap_cap <= 0) heap_cap = default_heap_cap(W, H);
+    if ((size_t)heap_cap > max_heap(W, H)) heap_cap = (int)max_heap(W, H);
+    const size_t ncell = (size_t)W * H;
+    const size_t cst_words = ((ncell + 7) / 8 + 3) & ~(size_t)3;
+    {
+        const size_t per_worker = (size_t)heap_cap * 16 + cst_words * 4 + ncell * 8;
+        const size_t fit = kScratchBudget / per_worker;
+        if (fit < 1) return pmp_set_err(ctx, PMP_ENOMEM, "pmp_astar2d_reserve: one worker exceeds the scratch budget");
+        if ((size_t)workers > fit) workers = (int)fit;
+    }
     const int per_cu = (workers + 255) / 256;
     int lds_cap = default_lds_cap(per_cu < 1 ? 1 : per_cu);
     if (lds_cap > heap_cap) lds_cap = (heap_cap + 15) & ~15;
-    const size_t ncell = (size_t)W * H;
-    const size_t cst_words = ((ncell + 7) / 8 + 3) & ~(size_t)3;
     const size_t spill = heap_cap > lds_cap ? (size_t)(heap_cap - lds_cap) : 0;
     if (!pmp_scratch(ctx, SCR_HEAP, (size_t)workers * spill * 16 + 16)) return PMP_ENOMEM;
     if (!pmp_scratch(ctx, SCR_CLOSED, (size_t)workers * cst_words * 4)) return PMP_ENOMEM;

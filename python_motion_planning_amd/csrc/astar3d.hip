@@ -99,9 +99,7 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
     const double mcost = __dsqrt_rn((double)mchg);  // Planner3D.dist: math.sqrt(1|2|3)
 
     for (;;) {
-        int qi = 0;
-        if (lane == 0) qi = atomicAdd(queue, 1);
-        qi = uni(qi);
+        const int qi = next_query(queue, lane);
         if (qi >= nq) break;
         const int q = qi;
         const uint32_t* occ = occ_all + (per_query ? (size_t)q * words : 0);
@@ -120,14 +118,12 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
         qc.heur = heuristic;
         const bool s_in = (unsigned)sx < (unsigned)X && (unsigned)sy < (unsigned)Y && (unsigned)sz < (unsigned)Z;
         const bool g_in = (unsigned)qc.gx < (unsigned)X && (unsigned)qc.gy < (unsigned)Y && (unsigned)qc.gz < (unsigned)Z;
-        if (!s_in || !g_in) {
-            if (lane == 0) {
-                status_out[q] = PMP_NO_PATH;
-                cost_out[q] = __builtin_inf();
-                path_len_out[q] = 0;
-                nexp_out[q] = s_in ? 1 : 0;
-                if (counters) { counters[4 * q] = 1; counters[4 * q + 1] = 1; counters[4 * q + 2] = s_in; counters[4 * q + 3] = 1; }
-            }
+        if (!s_in || !g_in) {  // every lane stores the same values (no lane-0 block before the continue)
+            status_out[q] = PMP_NO_PATH;
+            cost_out[q] = __builtin_inf();
+            path_len_out[q] = 0;
+            nexp_out[q] = s_in ? 1 : 0;
+            if (counters) { counters[4 * q] = 1; counters[4 * q + 1] = 1; counters[4 * q + 2] = s_in; counters[4 * q + 3] = 1; }
             continue;
         }
         const uint32_t scm = (((uint32_t)sx << 16) | ((uint32_t)sy << 8) | (uint32_t)sz) << 5 | 26u;

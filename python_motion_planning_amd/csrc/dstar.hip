@@ -105,16 +105,15 @@ __global__ __launch_bounds__(64) void dstar_kernel(const uint32_t* __restrict__ 
     const double mcost = (lane & 1) ? 1.4142135623730951 : 1.0;  // Planner.dist = hypot(1, 1) / hypot(1, 0)
 
     for (;;) {
-        int qi = 0;
-        if (lane == 0) qi = atomicAdd(queue, 1);
-        qi = uni(qi);
+        const int qi = next_query(queue, lane);
         if (qi >= nq) break;
         const int q = qi;
         const int sx = start_xy[2 * q], sy = start_xy[2 * q + 1];
         const int gx = goal_xy[2 * q], gy = goal_xy[2 * q + 1];
         if ((unsigned)sx >= (unsigned)W || (unsigned)sy >= (unsigned)H || (unsigned)gx >= (unsigned)W ||
             (unsigned)gy >= (unsigned)H) {
-            if (lane == 0) { status_out[q] = PMP_REF_RAISES; cost_out[q] = 0.0; path_len_out[q] = 0; nproc_out[q] = 0; }
+            // every lane stores the same values (no lane-0 block before the continue)
+            status_out[q] = PMP_REF_RAISES; cost_out[q] = 0.0; path_len_out[q] = 0; nproc_out[q] = 0;
             continue;
         }
         const int start = sx * H + sy, goal = gx * H + gy;

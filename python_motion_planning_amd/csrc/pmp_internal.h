@@ -46,6 +46,18 @@ __device__ __forceinline__ double rl_f64(double v, int lane) {
     return __longlong_as_double(((uint64_t)hi << 32) | lo);
 }
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Next index from a persistent-worker queue, wave-uniform.  The workgroup barrier is a convergence
+// point (free for one-wave workgroups): without it the compiler may let lanes run ahead into the
+// next iteration while lane 0 is still in a lane-0-only block, and then readfirstlane would read a
+// lane that never fetched the index.
+__device__ __forceinline__ int next_query(int* queue, int lane)
+{
+    __syncthreads();
+    int qi = 0;
+    if (lane == 0) qi = atomicAdd(queue, 1);
+    return __builtin_amdgcn_readfirstlane(qi);
+}
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
 // launch-span stamps (pmp_set_timing): each worker's lane 0 folds its start / end wall-clock tick

@@ -134,9 +134,17 @@ def test_edge_cases():
     # path_cap overflow is reported, never silently truncated
     r = batch.astar2d_batch(occ, starts[:1], goals[:1], path_cap=10)
     assert int(r["status"][0]) == 2 and int(r["path_len"][0]) == 48
-    # tiny heap capacity -> status 3
-    r = batch.astar2d_batch(occ, starts[:1], goals[:1], path_cap=64, reserve_slots=1, heap_cap=4)
+    # tiny heap capacity -> status 3 from the kernel ...
+    r = batch.astar2d_batch(occ, starts[:1], goals[:1], path_cap=64, reserve_slots=1, heap_cap=4,
+                            retry_overflow=False)
     assert int(r["status"][0]) == 3
+    # ... and the host re-runs the overflowed queries with the full bound: same answers as the oracle
+    from oracle import oracle as O
+
+    r = batch.astar2d_batch(occ, starts, goals, path_cap=2048, reserve_slots=4, heap_cap=8, expand_cap=4096)
+    assert r["status"].cpu().numpy().tolist() == [0, 0, 1, 1, 1, 1]
+    ref = O.astar2d(occ, tuple(starts[0]), tuple(goals[0]))
+    assert float(r["cost"][0]) == ref["cost"] and int(r["n_expanded"][0]) == ref["n_expanded"]
     torch.cuda.synchronize()
     # restore default scratch sizing for later tests
     batch.astar2d_batch(occ, starts[:1], goals[:1], path_cap=64, reserve_slots=64, heap_cap=0)
