@@ -438,6 +438,8 @@ def main():
     ap.add_argument("--track-steps", type=int, default=5)
     ap.add_argument("--schedule", choices=["lpt", "input"], default="lpt",
                     help="A* query order across workers: longest start-goal distance first, or input order")
+    ap.add_argument("--prio", type=int, default=64,
+                    help="longest-first only: the first N (longest) queries of a batch run at raised wave priority")
     ap.add_argument("--streams", type=int, default=3,
                     help="batches in flight: consecutive steps go to different HIP streams (own scratch "
                          "context each), so one batch's long-query tail overlaps the next batch")
@@ -468,6 +470,7 @@ def main():
         ctx = L.pmp_create(torch.cuda.current_device())
         _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, args.workers, 0), "reserve")
         _lib.check(ctx, L.pmp_astar2d_set_schedule(ctx, 1 if args.schedule == "lpt" else 0), "schedule")
+        _lib.check(ctx, L.pmp_astar2d_set_priority(ctx, args.prio), "priority")
         lanes.append(dict(
             ctx=ctx, stream=torch.cuda.Stream(),
             cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
@@ -593,7 +596,7 @@ def main():
                        "pushes_per_launch": int(counters[:, 0].sum()),
                        "pops_per_launch": int(counters[:, 1].sum()),
                        "max_heap_entries": int(counters[:, 3].max()),
-                       "workers": args.workers, "streams": S},
+                       "workers": args.workers, "streams": S, "priority_queries": args.prio},
         }
         print(json.dumps(out), flush=True)
     if dist:

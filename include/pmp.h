@@ -257,6 +257,10 @@ int pmp_wall_clock_khz(pmp_ctx* ctx, int* khz);
  * first (the expansion count grows with it, so long queries stop forming a tail), 0 = input order.
  * Results are identical either way; only which worker runs which query changes. */
 int pmp_astar2d_set_schedule(pmp_ctx* ctx, int longest_first);
+/* With the longest-first schedule, the first n_high queries (the longest) run at raised wave
+ * priority, so they finish sooner and the short queries fill the issue slots they leave idle.
+ * Default 64; 0 switches it off.  Results are identical for any value. */
+int pmp_astar2d_set_priority(pmp_ctx* ctx, int n_high);
 
 /* Pre-size the A* scratch (heap of heap_cap entries per concurrent query, up to max_slots
  * concurrent queries) so that later batch calls allocate nothing (hipGraph-capturable). */

@@ -91,9 +91,25 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 // a ds_read/ds_write), positions >= lds_cap in a per-worker HBM spill reached only through buffer
 // instructions (a distinct instruction class, so the compiler can never fold the two paths into
 // one flat access that waits on both counters).
+//
+// Direction bits.  For every node p with two children the heap also keeps CPython _siftup's child
+// choice bit(p) = !(heap[2p+1] < heap[2p+2]) (Lib/heapq.py: "if rightpos < endpos and not
+// heap[childpos] < heap[rightpos]: childpos = rightpos"), so the whole sift path of a heappop is
+// known from bits alone.  Bits live in 5-level subtree blocks: the u32 block of tier t (levels
+// 5t..5t+4) rooted at node a keeps node (a's descendant r levels down, offset o) at bit (1<<r)-1+o.
+// LDS word 0 = tier 0, words 1..32 = tier 1, words 33..1056 = tier 2; tiers >= 3 (heaps of more than
+// 32767 entries) in HBM.  A bit is only meaningful while its node has two children: it is rewritten
+// whenever a push gives a node its right child or a push/pop changes one of its children, and the
+// walk ignores it for a node with one child.
+constexpr int kBitsLdsWords = 1057;
+constexpr int kBitsLdsBytes = 4240;  // 1057 words, padded to 16 B
+static_assert(kBitsLdsBytes >= 4 * kBitsLdsWords, "bit blocks overflow their LDS region");
+
 struct Heap {
     lds_f64* lg;       // LDS f[lds_cap]
     lds_u32* lcm;      // LDS cm[lds_cap]
+    lds_u32* lb;       // LDS direction-bit blocks of tiers 0..2
+    uint32_t* hb;      // HBM direction-bit blocks of tiers >= 3
     __amdgpu_buffer_rsrc_t spill;  // HBM entries {f lo, f hi, cm, 0} for positions >= lds_cap
     int lds_cap;
 
@@ -121,6 +137,32 @@ struct Heap {
         }
     }
 };
+
+// HBM word of tier t >= 3 for the block whose root has path number R (= root position + 1):
+// tier t starts after sum_{s=3}^{t-1} 32^s = (32^t - 32^3) / 31 words
+__device__ __forceinline__ size_t hb_word(int t, uint32_t R)
+{
+    const size_t base = (size_t)1 << (5 * t);
+    return (base - 32768u) / 31u + (size_t)(R - (uint32_t)base);
+}
+
+// Set the direction bit of the node at `level` whose path number (position + 1) is Pl.  Lanes may
+// share a block word, so the update is an atomic and/or (no return value: nothing waits on it).
+__device__ __forceinline__ void bit_write(const Heap& hp, int level, uint32_t Pl, uint32_t bit)
+{
+    const int t = level / 5, r = level - 5 * t;
+    const uint32_t R = Pl >> r;
+    const uint32_t m = 1u << ((1u << r) - 1u + (Pl & ((1u << r) - 1u)));
+    if (t <= 2) {
+        lds_u32* w = hp.lb + (t == 0 ? 0u : (t == 1 ? R - 31u : R - 991u));
+        if (bit) __atomic_fetch_or(w, m, __ATOMIC_RELAXED);
+        else __atomic_fetch_and(w, ~m, __ATOMIC_RELAXED);
+    } else {
+        uint32_t* w = hp.hb + hb_word(t, R);
+        if (bit) __hip_atomic_fetch_or(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else __hip_atomic_fetch_and(w, ~m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
 
 // 4-bit cell state: word i >> 3, nibble i & 7
 __device__ __forceinline__ uint32_t cst_at(const uint32_t* cst, uint32_t i) { return (cst[i >> 3] >> ((i & 7) * 4)) & 15u; }
@@ -154,105 +196,147 @@ __device__ __forceinline__ void hstore(const Heap& hp, int p, double g, uint32_t
         hp.lcm[p] = cm;
     }
 }
+// predicated load: SPILL lanes branch (a buffer load only where needed), LDS-only code loads a
+// clamped valid address unconditionally
+template <bool SPILL>
+__device__ __forceinline__ void hload_if(const Heap& hp, bool v, int p, double& g, uint32_t& cm)
+{
+    if constexpr (SPILL) {
+        g = 0.0;
+        cm = 0u;
+        if (v) hp.load(p, g, cm);
+    } else {
+        hload<false>(hp, v ? p : 0, g, cm);
+    }
+}
 
-// heappop on a heap of n (>0, already decremented) entries whose old last element sits at position
-// n; the old root has been taken by the caller.  Updates `root` (wave-uniform copy of heap[0]).
-// jl / ol: this lane's pair level (1..6) and pair offset inside a chunk (lane 63: idle).
+// heappop on a heap of n (> 0, already decremented) entries whose old last element sits at
+// position n; the old root has been taken by the caller.  Updates `root` (wave-uniform heap[0]).
+//  1. the _siftup path p_0 = 0, p_1, .., p_K (a leaf) from the direction bits: a scalar walk over
+//     prefetched block words (tiers 0/1 in one LDS round, the 32 tier-2 candidates below p_5 in a
+//     second round that overlaps the tier-1 walk);
+//  2. one round: lane i in 1..K loads heap[p_i], heap[p_{i+1}] and heap[sibling(p_i)];
+//  3. the children that move up are the prefix with !(last < heap[p_i]) (the path is sorted), so a
+//     ballot popcount m places `last` at p_m -- the array CPython's _siftup + _siftdown produce;
+//  4. lanes 1..m rewrite the bits of p_0..p_{m-1}, whose children changed.
 template <bool SPILL, int HEUR>
-__device__ __forceinline__ void heap_pop(const Heap& hp, const Q& qc, int n, Ent& root, int lane, int jl, int ol)
+__device__ __forceinline__ void heap_pop(const Heap& hp, const Q& qc, int n, Ent& root, int lane)
 {
     n = uni(n);  // wave-uniform by construction; say so, so the walk below stays on the SALU
     Ent last;
     hload<SPILL>(hp, n, last.f, last.cm);  // uniform address, but an LDS load is not known-uniform:
+    const uint32_t v01 = hp.lb[lane <= 32 ? lane : 0];  // tier-0 word (lane 0), tier-1 words (1..32)
     last.f = rl_f64(last.f, 0);            // readlane makes `last` (and the root / node derived from
     last.cm = rl_u32(last.cm, 0);          // it) SGPR values, keeping the whole walk scalar
     last.hk = key_of<HEUR>(qc, last.cm);
-    int hole = 0;
-    bool first = true;
-    for (;;) {
-        const int li = ((hole + 1) << jl) - 1 + 2 * ol;  // left child position of this lane's pair
-        const bool vl = (lane < 63) & (li < n);
-        const bool vr = (lane < 63) & (li + 1 < n);
-        Ent L, R;
-        if constexpr (SPILL) {
-            L.f = R.f = 0.0;
-            L.cm = R.cm = 0u;
-            if (vl) hload<true>(hp, li, L.f, L.cm);
-            if (vr) hload<true>(hp, li + 1, R.f, R.cm);
-        } else {  // unconditional loads from clamped (valid) addresses: no branch
-            const int a = vl ? li : 0, b = vr ? li + 1 : 0;
-            L.f = hp.lg[a];
-            L.cm = hp.lcm[a];
-            R.f = hp.lg[b];
-            R.cm = hp.lcm[b];
-        }
-        L.hk = key_of<HEUR>(qc, L.cm);
-        R.hk = key_of<HEUR>(qc, R.cm);
-        const uint64_t dmask = ballot(vr & !ent_lt(L, R));    // heapq._siftup: right unless left < right
-        const uint64_t mlmask = ballot(vl & !ent_lt(last, L));  // child may move up past `last`
-        const uint64_t mrmask = ballot(vr & !ent_lt(last, R));
-        // scalar walk through the chunk's 6 levels (all SGPR, unrolled)
-        int cur = uni(hole), oc = 0;
-        uint64_t mover = 0, movr = 0;
-        bool go = true;
-#pragma unroll
-        for (int lv = 1; lv <= 6; lv++) {
-            const int c = 2 * cur + 1;
-            const int pl = (1 << (lv - 1)) - 1 + oc;  // pair lane
-            const int r = (int)((dmask >> pl) & 1ull);
-            const uint64_t mm = r ? mrmask : mlmask;
-            go = go & (c < n) & (((mm >> pl) & 1ull) != 0ull);
-            if (go) {
-                mover |= 1ull << pl;
-                movr |= (uint64_t)r << pl;
-                cur = c + r;
-                oc = 2 * oc + r;
+
+    // ---- 1. the path.  Levels 0..D-1 are full (D = floor(log2 n)), so every node above level D-1
+    //      has two children and the walk takes D-1 unconditional steps; the last step (level D-1 ->
+    //      D) exists only below a node with a child.  Per step: c = bit, P = 2P + c (P = position + 1
+    //      of the current node), Pr = the same relative to the current block's root (bit index Pr-1).
+    const int D = 31 - __clz(n);
+    uint32_t P = 1, R1 = 0, v2 = 0;
+    int K = 0;
+    {
+        // w2 = block word << 1, so node Pr of the block (Pr = 1 at its root) is bit Pr of w2
+        uint32_t w2 = rl_u32(v01, 0) << 1, Pr = 1;
+        const int full = D - 1;
+        int lvl = 0;  // level of the current node
+        for (int t = 0; lvl < full; t++) {
+            const int steps = min(5, full - lvl);  // unconditional steps inside this block
+            for (int r = 0; r < steps; r++) Pr = 2u * Pr + ((w2 >> Pr) & 1u);
+            P = (P << steps) + Pr - (1u << steps);
+            lvl += steps;
+            if (steps < 5) break;
+            // the node reached roots the block of tier t + 1: fetch its word
+            Pr = 1u;
+            if (t == 0) {
+                w2 = rl_u32(v01, (int)P - 31) << 1;
+                R1 = P;
+                if (full >= 10) v2 = hp.lb[33 + ((R1 << 5) - 1024u) + (uint32_t)(lane & 31)];
+            } else if (t == 1) {
+                w2 = rl_u32(v2, (int)(P - (R1 << 5))) << 1;
+            } else {  // tiers >= 3 (heaps above 32767 entries): an L2-coherent read of the HBM block
+                w2 = (uint32_t)uni((int)__hip_atomic_fetch_or(hp.hb + hb_word(t + 1, P), 0u, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT)) << 1;
             }
         }
-        if ((mover >> lane) & 1ull) {  // the chosen child moves up one level
-            const bool rr = (movr >> lane) & 1ull;
-            hstore<SPILL>(hp, ((rr ? li + 1 : li) - 1) >> 1, rr ? R.f : L.f, rr ? R.cm : L.cm);
+        K = lvl;
+        // the last step: below a node at level D-1 with a child (2p + 1 < n, p = P - 1)
+        // (w2, Pr) already describe the block holding the node at level D-1
+        if (D >= 1 && 2u * P - 1u < (uint32_t)n) {
+            const uint32_t c = (2u * P < (uint32_t)n) ? ((w2 >> Pr) & 1u) : 0u;
+            P = 2u * P + c;
+            K++;
         }
-        if (first && (mover & 1ull)) {  // the child that moved into the root is the new root
-            const bool r0 = movr & 1ull;
-            root.f = rl_f64(r0 ? R.f : L.f, 0);
-            root.cm = rl_u32(r0 ? R.cm : L.cm, 0);
-            root.hk = rl_u32(r0 ? R.hk : L.hk, 0);
-        }
-        first = false;
-        hole = cur;
-        if (!go) break;
-        wave_sync_mem();
     }
-    if (lane == 0) hstore<SPILL>(hp, hole, last.f, last.cm);
-    if (hole == 0) root = last;
+
+    // ---- 2. one load round
+    const bool on = lane >= 1 && lane <= K;
+    const int sh = K - lane;
+    const int pi = on ? (int)(P >> sh) - 1 : 0;
+    const bool hasb = on && lane < K;
+    const int pn = hasb ? (int)(P >> (sh - 1)) - 1 : 0;
+    const int si = (pi & 1) ? pi + 1 : pi - 1;
+    const bool hass = on && si < n;
+    Ent A, B, S;
+    hload_if<SPILL>(hp, on, pi, A.f, A.cm);
+    hload_if<SPILL>(hp, hasb, pn, B.f, B.cm);
+    hload_if<SPILL>(hp, hass, si, S.f, S.cm);
+    A.hk = key_of<HEUR>(qc, A.cm);
+    B.hk = key_of<HEUR>(qc, B.cm);
+    S.hk = key_of<HEUR>(qc, S.cm);
+
+    // ---- 3. movers and stores
+    const int m = __popcll(ballot(on && !ent_lt(last, A)));
+    if (lane >= 1 && lane <= m) hstore<SPILL>(hp, (int)(P >> (sh + 1)) - 1, A.f, A.cm);
+    if (lane == 0) hstore<SPILL>(hp, (int)(P >> (K - m)) - 1, last.f, last.cm);
+    if (m >= 1) {
+        root.f = rl_f64(A.f, 1);
+        root.cm = rl_u32(A.cm, 1);
+        root.hk = rl_u32(A.hk, 1);
+    } else {
+        root = last;
+    }
+
+    // ---- 4. bits of p_0 .. p_{m-1}
+    if (hass && lane <= m) {
+        const Ent vn = lane < m ? B : last;  // the new heap[p_i]
+        const bool bit = (pi & 1) ? !ent_lt(vn, S) : !ent_lt(S, vn);
+        bit_write(hp, lane - 1, P >> (sh + 1), bit ? 1u : 0u);
+    }
     wave_sync_mem();
 }
 
-// heappush of `it` onto a heap of n entries (position n is free).
+// heappush of `it` onto a heap of n entries (position n is free): the ancestors a_j = parent^j(n)
+// load in one round (with the siblings of a_{j-1}, for the bits); a ballot popcount t gives how
+// many move down; lanes 1..t+1 rewrite the bits of a_1..a_{t+1}, whose children changed.
 template <bool SPILL, int HEUR>
 __device__ __forceinline__ void heap_push(const Heap& hp, const Q& qc, int n, const Ent& it, Ent& root, int lane)
 {
     n = uni(n);
-    const int np1 = n + 1;
-    const int depth = 31 - __clz(np1);  // ancestors of position n
-    const bool valid = lane < depth;
-    const int apos = valid ? (np1 >> (lane + 1)) - 1 : 0;
-    Ent a;
-    if constexpr (SPILL) {
-        a.f = 0.0;
-        a.cm = 0u;
-        if (valid) hload<true>(hp, apos, a.f, a.cm);
-    } else {
-        a.f = hp.lg[apos];
-        a.cm = hp.lcm[apos];
-    }
+    const uint32_t np1 = (uint32_t)n + 1u;
+    const int D = 31 - __clz((int)np1);  // depth of position n
+    const bool on = lane >= 1 && lane <= D;
+    const int aj = on ? (int)(np1 >> lane) - 1 : 0;
+    const int x = on ? (int)(np1 >> (lane - 1)) - 1 : 1;  // a_{j-1}
+    const int sx = (x & 1) ? x + 1 : x - 1;
+    const bool hass = on && sx < n;  // a_{j-1} = n (lane 1) has a sibling only when n is even
+    Ent a, S;
+    hload_if<SPILL>(hp, on, aj, a.f, a.cm);
+    hload_if<SPILL>(hp, hass, sx, S.f, S.cm);
     a.hk = key_of<HEUR>(qc, a.cm);
-    const int t = __popcll(ballot(valid & ent_lt(it, a)));  // the "less" set is a prefix from the parent up
-    if (lane < t) hstore<SPILL>(hp, (np1 >> lane) - 1, a.f, a.cm);
-    const int ipos = (np1 >> t) - 1;
+    S.hk = key_of<HEUR>(qc, S.cm);
+    const int t = __popcll(ballot(on && ent_lt(it, a)));  // the "less" set is a prefix from the parent up
+    if (lane >= 1 && lane <= t) hstore<SPILL>(hp, x, a.f, a.cm);
+    const int ipos = (int)(np1 >> t) - 1;
     if (lane == 0) hstore<SPILL>(hp, ipos, it.f, it.cm);
     if (ipos == 0) root = it;
+    if (hass && lane <= t + 1) {
+        const Ent vn = lane - 1 < t ? a : it;  // the new heap[a_{j-1}]
+        const bool bit = (x & 1) ? !ent_lt(vn, S) : !ent_lt(S, vn);
+        bit_write(hp, D - lane, np1 >> lane, bit ? 1u : 0u);
+    }
     wave_sync_mem();
 }
 
@@ -264,15 +348,18 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
     int32_t* __restrict__ nexp_out, uint32_t* __restrict__ expand_out, int expand_cap,
     int64_t* __restrict__ counters, int32_t* __restrict__ status_out, int* __restrict__ queue,
     uint4* __restrict__ spill_all, int heap_cap, int lds_cap, uint32_t* __restrict__ cst_all, size_t cst_words,
-    double* __restrict__ G_all, unsigned long long* __restrict__ span)
+    double* __restrict__ G_all, uint32_t* __restrict__ hbits_all, size_t hbits_words, int prio_n,
+    unsigned long long* __restrict__ span)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
     const int worker = blockIdx.x;
     span_begin(span);
     Heap hp;
-    hp.lg = (lds_f64*)(smem);
-    hp.lcm = (lds_u32*)(smem + (size_t)8 * lds_cap);
+    hp.lb = (lds_u32*)smem;
+    hp.lg = (lds_f64*)(smem + kBitsLdsBytes);
+    hp.lcm = (lds_u32*)(smem + kBitsLdsBytes + (size_t)8 * lds_cap);
+    hp.hb = hbits_all + (size_t)worker * hbits_words;
     {
         const size_t spill_n = (size_t)(heap_cap > lds_cap ? heap_cap - lds_cap : 0);
         hp.spill = __builtin_amdgcn_make_buffer_rsrc(spill_all + (size_t)worker * spill_n, 0, (int)(spill_n * 16), 0x00020000);
@@ -284,9 +371,6 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
     // lane 9 + i -> its CLOSED-state nibble
     const int blk_i = lane < 9 ? lane : (lane < 18 ? lane - 9 : 4);
     const int blk_dx = blk_i / 3 - 1, blk_dy = blk_i % 3 - 1;
-    // this lane's sibling pair inside a pop chunk: level jl = 1..6 below the hole, offset ol
-    const int pop_jl = 32 - __clz(lane + 1);
-    const int pop_ol = lane + 1 - (1 << (pop_jl - 1));
 
     for (;;) {
         // readfirstlane (not __shfl): the compiler must SEE the query index as wave-uniform, or
@@ -295,6 +379,10 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
         const int qi = next_query(queue, lane);
         if (qi >= nq) break;
         const int q = uni(order ? order[qi] : qi);
+        // the longest queries (first in the longest-first order) get issue priority on their SIMD:
+        // they set the launch's tail, the short ones fill the cycles they leave idle
+        if (qi < prio_n) __builtin_amdgcn_s_setprio(3);
+        else __builtin_amdgcn_s_setprio(0);
 
         // reset this worker's cell-state array
         {
@@ -339,7 +427,7 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
         int plen = 0;
 
 #ifdef PMP_STAMPS
-        uint64_t cyc_pop = 0, cyc_wait = 0, cyc_push = 0;
+        uint64_t cyc_pop = 0, cyc_wait = 0, cyc_push = 0, cyc_hbm = 0;
         const uint64_t cyc_q0 = __builtin_amdgcn_s_memtime();
 #endif
         while (n > 0) {
@@ -365,11 +453,17 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
             }
             double gpar = 0.0;  // G[parent] (the parent closed earlier); the start has g = 0
             if (lane == 18 && ndir < 8) gpar = G[(uint32_t)(x - c_mx[ndir]) * (uint32_t)H + (uint32_t)(y - c_my[ndir])];
+#ifdef PMP_STAMPS_SPLIT  // diagnostic: wait for the HBM round before the pop, time the two apart
+            asm volatile("s_waitcnt vmcnt(0)" ::"v"(blk_word), "v"(gpar) : "memory");
+            STAMP(tsB);
+            cyc_hbm += tsB - ts0;
+            ts0 = tsB;
+#endif
 
             // ---- heappop (a_star.py:54): `last` = heap[n] sifts down the CPython path
             if (n > 0) {
-                if (n < lds_cap) heap_pop<false, HEUR>(hp, qc, n, root, lane, pop_jl, pop_ol);
-                else heap_pop<true, HEUR>(hp, qc, n, root, lane, pop_jl, pop_ol);
+                if (n < lds_cap) heap_pop<false, HEUR>(hp, qc, n, root, lane);
+                else heap_pop<true, HEUR>(hp, qc, n, root, lane);
             }
 
             STAMP(ts1);
@@ -474,7 +568,11 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
             if (counters) {
 #ifdef PMP_STAMPS
                 counters[4 * q + 0] = (int64_t)cyc_pop;
+#ifdef PMP_STAMPS_SPLIT
+                counters[4 * q + 1] = (int64_t)cyc_hbm;
+#else
                 counters[4 * q + 1] = (int64_t)cyc_wait;
+#endif
                 counters[4 * q + 2] = (int64_t)cyc_push;
                 counters[4 * q + 3] = (int64_t)(__builtin_amdgcn_s_memtime() - cyc_q0);
 #else
@@ -524,9 +622,18 @@ __global__ void lpt_scatter(const int32_t* s, const int32_t* g, int nq, int nb, 
 int default_workers() { return 256 * 4; }
 int default_lds_cap(int workers_per_cu)
 {
-    // 160 KiB LDS per CU shared by the resident workers; 12 B per entry, keep a little slack
-    int bytes = (160 * 1024) / workers_per_cu - 256;
+    // 160 KiB LDS per CU shared by the resident workers: the direction-bit blocks, then 12 B per
+    // heap entry; keep a little slack
+    int bytes = (160 * 1024) / workers_per_cu - 256 - kBitsLdsBytes;
     return (bytes / 12) & ~15;
+}
+// HBM words of the direction-bit tiers >= 3 for heaps of up to heap_cap entries
+size_t hbits_words(int heap_cap)
+{
+    const int maxlvl = 31 - __builtin_clz((unsigned)heap_cap);
+    size_t w = 0;
+    for (int t = 3; 5 * t <= maxlvl; t++) w += (size_t)1 << (5 * t);
+    return w ? w : 1;
 }
 // The heap never holds more than 8 * expansions + 1 <= 8 W H + 1 entries; the default cap is far
 // below that bound (C2's largest heap is ~10k entries).  A query that outgrows its cap stops with
@@ -552,7 +659,7 @@ extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int workers, int 
     const size_t ncell = (size_t)W * H;
     const size_t cst_words = ((ncell + 7) / 8 + 3) & ~(size_t)3;
     {
-        const size_t per_worker = (size_t)heap_cap * 16 + cst_words * 4 + ncell * 8;
+        const size_t per_worker = (size_t)heap_cap * 16 + cst_words * 4 + ncell * 8 + hbits_words(heap_cap) * 4;
         const size_t fit = kScratchBudget / per_worker;
         if (fit < 1) return pmp_set_err(ctx, PMP_ENOMEM, "pmp_astar2d_reserve: one worker exceeds the scratch budget");
         if ((size_t)workers > fit) workers = (int)fit;
@@ -565,6 +672,7 @@ extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int workers, int 
     if (!pmp_scratch(ctx, SCR_CLOSED, (size_t)workers * cst_words * 4)) return PMP_ENOMEM;
     if (!pmp_scratch(ctx, SCR_AUX0, 256)) return PMP_ENOMEM;
     if (!pmp_scratch(ctx, SCR_G, (size_t)workers * ncell * 8)) return PMP_ENOMEM;
+    if (!pmp_scratch(ctx, SCR_BITS, (size_t)workers * hbits_words(heap_cap) * 4)) return PMP_ENOMEM;
     ctx->astar_W = W;
     ctx->astar_H = H;
     ctx->astar_workers = workers;
@@ -603,7 +711,7 @@ extern "C" int pmp_astar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
     int* queue = (int*)ctx->buf[SCR_AUX0];
     double* G = (double*)ctx->buf[SCR_G];
     hipStream_t s = (hipStream_t)stream;
-    const size_t lds = (size_t)ctx->astar_lds_cap * 12;
+    const size_t lds = (size_t)kBitsLdsBytes + (size_t)ctx->astar_lds_cap * 12;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
     int32_t* order = nullptr;
     if (ctx->astar_lpt && nq > workers) {
@@ -620,7 +728,7 @@ extern "C" int pmp_astar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
     hipLaunchKernelGGL(kern, dim3(workers), dim3(64), lds, s, occ_bits, W, H, start_xy,
                        goal_xy, (const int32_t*)order, nq, cost, path_len, path, path_cap, n_expanded, expand,
                        expand_cap, counters, status, queue, spill, ctx->astar_heap_cap, ctx->astar_lds_cap, cst, cst_words, G,
-                       ctx->span);
+                       (uint32_t*)ctx->buf[SCR_BITS], hbits_words(ctx->astar_heap_cap), order ? ctx->astar_prio_n : 0, ctx->span);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }

@@ -43,7 +43,7 @@ void pmp_destroy(pmp_ctx* ctx)
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
-    for (int i = 0; i < 8; i++)
+    for (int i = 0; i < SCR_NSLOTS; i++)
         if (ctx->buf[i]) (void)hipFree(ctx->buf[i]);
     delete ctx;
 }
@@ -70,6 +70,13 @@ int pmp_astar2d_set_schedule(pmp_ctx* ctx, int longest_first)
 {
     if (!ctx) return PMP_EINVAL;
     ctx->astar_lpt = longest_first ? 1 : 0;
+    return PMP_OK;
+}
+
+int pmp_astar2d_set_priority(pmp_ctx* ctx, int n_high)
+{
+    if (!ctx || n_high < 0) return PMP_EINVAL;
+    ctx->astar_prio_n = n_high;
     return PMP_OK;
 }
 
