@@ -424,7 +424,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--agents", type=int, default=256, help="C4 agents per GPU (control-step leg)")
     ap.add_argument("--control-steps", type=int, default=20, help="timed control steps")
-    ap.add_argument("--workers", type=int, default=2048, help="persistent A* workers (waves) per launch")
+    ap.add_argument("--workers", type=int, default=3072, help="persistent A* workers (waves) per launch")
     ap.add_argument("--legs", default="dwa,rrt,astar3d,lqr,mpc",
                     help="secondary legs to run (comma list of dwa, rrt, astar3d, lqr, mpc; 'none' for none)")
     ap.add_argument("--rrt-queries", type=int, default=256)
