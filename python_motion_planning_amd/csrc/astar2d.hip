@@ -7,12 +7,14 @@
 // per-worker HBM array) and a 4-bit-per-cell state array in HBM (0 = open, dir+1 = closed with
 // parent motion `dir`), reused across the queries it processes.
 //
-// Heap entry (12 B in LDS as SoA: f64 f[] | u32 cm[]):  cm = (x << 13 | y) << 4 | dir
-//   dir = motion index (env.py:52-55) that reached the cell from its parent, 8 = start.
+// Heap entry (12 B in LDS as SoA: f64 f[] | u32 cm[]):
+//   cm = dx << 18 | dy << 4 | dir, with (dx, dy) = goal - cell as 14-bit two's-complement fields and
+//   dir = the motion index (env.py:52-55) that reached the cell from its parent, 8 = start.  The
+//   start entry stores (dx, dy) = (0, 0): its h is 0 (planner.py:15); its real cell is the query's.
 //   f = g + h as Node.__lt__ computes it (euclidean h = hypot(dx, dy) == sqrt(d2) exactly for
 //   |d| <= 16384, pinned against CPython's vector_norm; manhattan h = |dx| + |dy|).
-//   Node.__lt__: f < f' or (f == f' and h < h'); h order == hkey order (d2, or |dx|+|dy|), and hkey
-//   is rebuilt from the cell with integer ops, so loading an entry costs no transcendental.
+//   Node.__lt__: f < f' or (f == f' and h < h'); h order == hkey order (dx^2 + dy^2, or |dx| + |dy|),
+//   four integer ops from cm, so loading an entry costs no transcendental.
 //   g of a popped node = G[parent] + motion cost (node.py:39-41), G written when the parent closed,
 //   loaded in the same HBM round as the node's 3x3 occupancy / CLOSED block.
 //
@@ -20,10 +22,11 @@
 // when not left < right -- to a leaf, then _siftdown moves it back up).  The final array equals a
 // top-down walk along that same child path that moves each chosen child up while
 // !(last < child) and drops `last` at the first child it is less than (the path is sorted, so the
-// "not less" set is a prefix).  A chunk = 6 levels below the hole: lane l < 63 loads one sibling
-// pair, decides the CPython child choice and the two "may move up" bits; three ballots give the
-// masks; the walk itself is scalar; movers store in parallel.
+// "not less" set is a prefix).  The path comes from per-node child-choice bits (below) in a scalar
+// walk of two instructions per level; one LDS round loads the path; a ballot popcount places last.
 // heappush (_siftdown): the ancestors load in one round, one ballot finds how many move down.
+// Both operations are written for a low instruction count: the kernel is issue-bound (one wave per
+// query, a few waves per SIMD), so every instruction on the heap path costs wall time.
 #include "pmp_internal.h"
 
 // Diagnostic build only (make stamps -> libpmp_hip_stamps.so): per-query cycle sums of the
@@ -39,42 +42,32 @@ namespace {
 constexpr int kMaxDim = 8192;
 constexpr double kSqrt2 = 1.4142135623730951;  // math.sqrt(2) == math.hypot(1, 1)
 
-__device__ __constant__ int c_mx[8] = {-1, -1, 0, 1, 1, 1, 0, -1};
-__device__ __constant__ int c_my[8] = {0, 1, 1, 1, 0, -1, -1, -1};
+// motions in the order of env.py:52-55: (-1,0),(-1,1),(0,1),(1,1),(1,0),(1,-1),(0,-1),(-1,-1),
+// as 2-bit fields of (m + 1)
+constexpr uint32_t kMx1 = 0x1A90u, kMy1 = 0x01A9u;
+__device__ __forceinline__ int mot_x(int d) { return (int)((kMx1 >> (2 * d)) & 3u) - 1; }
+__device__ __forceinline__ int mot_y(int d) { return (int)((kMy1 >> (2 * d)) & 3u) - 1; }
 
-struct Q {  // per-query wave-uniform constants
-    int gx, gy;
-};
-
-struct Ent {
-    double f;
-    uint32_t cm, hk;
-};
+__device__ __forceinline__ uint32_t pack_cm(int dx, int dy, int dir)
+{
+    return ((uint32_t)dx << 18) | (((uint32_t)dy & 0x3fffu) << 4) | (uint32_t)dir;
+}
+__device__ __forceinline__ int cm_dx(uint32_t cm) { return (int)cm >> 18; }
+__device__ __forceinline__ int cm_dy(uint32_t cm) { return (int)(cm << 14) >> 18; }
 
 // HEUR: 0 euclidean, 1 manhattan (GraphSearcher.h, graph_search.py:41-44) -- a template parameter,
-// so key computations carry no runtime branch.
+// so key computations carry no runtime branch.  The order key of h.
 template <int HEUR>
-__device__ __forceinline__ uint32_t hkey_raw(const Q& q, uint32_t cm)
+__device__ __forceinline__ uint32_t hkey(uint32_t cm)
 {
-    const int x = (int)(cm >> 17), y = (int)((cm >> 4) & 8191u);
-    const int dx = q.gx - x, dy = q.gy - y;
-    return HEUR == 1 ? (uint32_t)(abs(dx) + abs(dy)) : (uint32_t)(dx * dx + dy * dy);
+    const int dx = cm_dx(cm), dy = cm_dy(cm);
+    if (HEUR == 1) return (uint32_t)(abs(dx) + abs(dy));
+    return (uint32_t)(__mul24(dx, dx) + __mul24(dy, dy));
 }
-
-// h of a pushed node and its integer order key
 template <int HEUR>
-__device__ __forceinline__ double h_and_key(const Q& q, uint32_t cm, uint32_t& hk)
+__device__ __forceinline__ double h_of_key(uint32_t hk)
 {
-    hk = hkey_raw<HEUR>(q, cm);
     return HEUR == 1 ? (double)hk : __dsqrt_rn((double)hk);
-}
-
-// order key of a stored entry; the start node has h = 0 (planner.py:15)
-template <int HEUR>
-__device__ __forceinline__ uint32_t key_of(const Q& q, uint32_t cm)
-{
-    const uint32_t k = hkey_raw<HEUR>(q, cm);
-    return (cm & 15u) == 8u ? 0u : k;
 }
 
 // Node.__lt__ (node.py:51-54) -- evaluated without short-circuit branches
@@ -82,16 +75,10 @@ __device__ __forceinline__ bool key_lt(double fa, uint32_t ka, double fb, uint32
 {
     return (fa < fb) | ((fa == fb) & (ka < kb));
 }
-__device__ __forceinline__ bool ent_lt(const Ent& a, const Ent& b) { return key_lt(a.f, a.hk, b.f, b.hk); }
 
 typedef __attribute__((address_space(3))) double lds_f64;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
-// The CPython heap array: positions < lds_cap in LDS (explicit address space 3, so every access is
-// a ds_read/ds_write), positions >= lds_cap in a per-worker HBM spill reached only through buffer
-// instructions (a distinct instruction class, so the compiler can never fold the two paths into
-// one flat access that waits on both counters).
-//
 // Direction bits.  For every node p with two children the heap also keeps CPython _siftup's child
 // choice bit(p) = !(heap[2p+1] < heap[2p+2]) (Lib/heapq.py: "if rightpos < endpos and not
 // heap[childpos] < heap[rightpos]: childpos = rightpos"), so the whole sift path of a heappop is
@@ -104,39 +91,92 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 constexpr int kBitsLdsWords = 1057;
 constexpr int kBitsLdsBytes = 4240;  // 1057 words, padded to 16 B
 static_assert(kBitsLdsBytes >= 4 * kBitsLdsWords, "bit blocks overflow their LDS region");
+constexpr int kBigHeap = 32767;  // from this size on, levels >= 15 exist: bit tiers >= 3 in HBM
 
 struct Heap {
-    lds_f64* lg;       // LDS f[lds_cap]
-    lds_u32* lcm;      // LDS cm[lds_cap]
-    lds_u32* lb;       // LDS direction-bit blocks of tiers 0..2
+    lds_f64* F;        // LDS f[lds_cap]
+    lds_u32* C;        // LDS cm[lds_cap]
+    lds_u32* B;        // LDS direction-bit blocks of tiers 0..2
     uint32_t* hb;      // HBM direction-bit blocks of tiers >= 3
     __amdgpu_buffer_rsrc_t spill;  // HBM entries {f lo, f hi, cm, 0} for positions >= lds_cap
-    int lds_cap;
+    int cap;
+};
 
-    __device__ __forceinline__ void load(int p, double& g, uint32_t& cm) const
+// per lane: bit `lane` of mask ? a : b
+__device__ __forceinline__ uint32_t sel_lanes(uint64_t mask, uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"(mask));
+    return r;
+}
+
+// Entry load in two phases, so a round of several loads is issued before any value is used.
+// SPILL = false: every position touched is < cap (pure ds_read code).  SPILL: both an LDS read
+// (clamped address) and a buffer read are issued and the right one selected; a position < cap
+// gives a negative buffer offset, which is out of range and reads 0 -- no branch.
+template <bool SPILL>
+struct Ld {
+    double fl;
+    uint32_t cl;
+    uint4 v;
+    bool in;
+    __device__ __forceinline__ void issue(const Heap& h, int p)
     {
-        if (p < lds_cap) {
-            g = lg[p];
-            cm = lcm[p];
+        if constexpr (!SPILL) {
+            fl = h.F[p];
+            cl = h.C[p];
         } else {
-            const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(spill, (p - lds_cap) * 16, 0, 0));
-            g = __hiloint2double((int)v.y, (int)v.x);
-            cm = v.z;
+            in = p < h.cap;
+            const int pl = in ? p : 0;
+            v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(h.spill, (p - h.cap) * 16, 0, 0));
+            fl = h.F[pl];
+            cl = h.C[pl];
         }
     }
-    __device__ __forceinline__ void store(int p, double g, uint32_t cm) const
+    // the select as explicit v_cndmask: left to itself the compiler turns it into an LDS load
+    // predicated into the buffer load's registers, which must first wait for the buffer load
+    __device__ __forceinline__ void get(double& f, uint32_t& c) const
     {
-        if (p < lds_cap) {
-            lg[p] = g;
-            lcm[p] = cm;
+        if constexpr (!SPILL) {
+            f = fl;
+            c = cl;
         } else {
-            const uint64_t b = (uint64_t)__double_as_longlong(g);
-            const uint4 v = make_uint4((uint32_t)b, (uint32_t)(b >> 32), cm, 0u);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
-                                                   spill, (p - lds_cap) * 16, 0, 0);
+            const uint64_t m = ballot(in);
+            const uint64_t b = (uint64_t)__double_as_longlong(fl);
+            f = __hiloint2double((int)sel_lanes(m, (uint32_t)(b >> 32), v.y), (int)sel_lanes(m, (uint32_t)b, v.x));
+            c = sel_lanes(m, cl, v.z);
         }
     }
 };
+template <bool SPILL>
+__device__ __forceinline__ void hld(const Heap& h, int p, double& f, uint32_t& c)
+{
+    Ld<SPILL> l;
+    l.issue(h, p);
+    l.get(f, c);
+}
+// Entry store by the lanes with `on`; the buffer store of a lane that does not spill gets an
+// out-of-range offset and is dropped by the hardware.
+template <bool SPILL>
+__device__ __forceinline__ void hst(const Heap& h, bool on, int p, double f, uint32_t c)
+{
+    if constexpr (!SPILL) {
+        if (on) {
+            h.F[p] = f;
+            h.C[p] = c;
+        }
+    } else {
+        if (on && p < h.cap) {
+            h.F[p] = f;
+            h.C[p] = c;
+        }
+        const uint64_t b = (uint64_t)__double_as_longlong(f);
+        const uint4 v = make_uint4((uint32_t)b, (uint32_t)(b >> 32), c, 0u);
+        const int off = (on && p >= h.cap) ? (p - h.cap) * 16 : -16;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
+                                               h.spill, off, 0, 0);
+    }
+}
 
 // HBM word of tier t >= 3 for the block whose root has path number R (= root position + 1):
 // tier t starts after sum_{s=3}^{t-1} 32^s = (32^t - 32^3) / 31 words
@@ -146,26 +186,50 @@ __device__ __forceinline__ size_t hb_word(int t, uint32_t R)
     return (base - 32768u) / 31u + (size_t)(R - (uint32_t)base);
 }
 
-// Set the direction bit of the node at `level` whose path number (position + 1) is Pl.  Lanes may
-// share a block word, so the update is an atomic and/or (no return value: nothing waits on it).
-__device__ __forceinline__ void bit_write(const Heap& hp, int level, uint32_t Pl, uint32_t bit)
+// LDS atomic masked OR: word = (word & ~mask) | val, no return value (nothing waits on it).  LDS
+// operations of one wave complete in order, so later ds_reads of the word see it.
+__device__ __forceinline__ void ds_mskor(lds_u32* w, uint32_t mask, uint32_t val)
 {
-    const int t = level / 5, r = level - 5 * t;
+    asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"((uint32_t)(uintptr_t)w), "v"(mask), "v"(val) : "memory");
+}
+
+// Set the direction bit of the node at `level` whose path number (position + 1) is Pl, on the
+// lanes with `on`.  Lanes may share a block word, hence the atomics.
+template <bool BIG>
+__device__ __forceinline__ void bit_write(const Heap& h, bool on, int level, uint32_t Pl, bool bit)
+{
+    const int t = (level * 13) >> 6;  // level / 5 for level < 64
+    const int r = level - 5 * t;
     const uint32_t R = Pl >> r;
-    const uint32_t m = 1u << ((1u << r) - 1u + (Pl & ((1u << r) - 1u)));
-    if (t <= 2) {
-        lds_u32* w = hp.lb + (t == 0 ? 0u : (t == 1 ? R - 31u : R - 991u));
-        if (bit) __atomic_fetch_or(w, m, __ATOMIC_RELAXED);
-        else __atomic_fetch_and(w, ~m, __ATOMIC_RELAXED);
-    } else {
-        uint32_t* w = hp.hb + hb_word(t, R);
+    const uint32_t m = 1u << (Pl + ((1u - R) << r) - 1u);
+    const uint32_t v = bit ? m : 0u;
+    if (!BIG || t <= 2) {
+        const int off = t == 0 ? -1 : (t == 1 ? -31 : -991);
+        if (on) ds_mskor(h.B + (int)R + off, m, v);
+    } else if (on) {
+        uint32_t* w = h.hb + hb_word(t, R);
         if (bit) __hip_atomic_fetch_or(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else __hip_atomic_fetch_and(w, ~m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
-// 4-bit cell state: word i >> 3, nibble i & 7
-__device__ __forceinline__ uint32_t cst_at(const uint32_t* cst, uint32_t i) { return (cst[i >> 3] >> ((i & 7) * 4)) & 15u; }
+// Five levels of the _siftup path inside one bit block: w2 = block word << 1 (node Pr of the
+// block, Pr = 1 at its root, is bit Pr); returns Pr after five steps (32..63).  Each step is
+// SCC = bit Pr of w2; Pr = 2 Pr + SCC.  Steps past the block's last real level are harmless:
+// the caller keeps the prefix it needs (Pr >> (5 - steps)).
+__device__ __forceinline__ uint32_t walk5(uint32_t w2)
+{
+    uint32_t pr = 1;
+    asm("s_bitcmp1_b32 %1, %0\n\ts_addc_u32 %0, %0, %0\n\t"
+        "s_bitcmp1_b32 %1, %0\n\ts_addc_u32 %0, %0, %0\n\t"
+        "s_bitcmp1_b32 %1, %0\n\ts_addc_u32 %0, %0, %0\n\t"
+        "s_bitcmp1_b32 %1, %0\n\ts_addc_u32 %0, %0, %0\n\t"
+        "s_bitcmp1_b32 %1, %0\n\ts_addc_u32 %0, %0, %0"
+        : "+s"(pr)
+        : "s"(w2)
+        : "scc");
+    return pr;
+}
 
 __device__ __forceinline__ void wave_sync_mem()
 {
@@ -175,135 +239,134 @@ __device__ __forceinline__ void wave_sync_mem()
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
-// SPILL = false: every position touched is < lds_cap (pure ds_read/ds_write code, no vmcnt waits).
-template <bool SPILL>
-__device__ __forceinline__ void hload(const Heap& hp, int p, double& g, uint32_t& cm)
-{
-    if constexpr (SPILL) {
-        hp.load(p, g, cm);
-    } else {
-        g = hp.lg[p];
-        cm = hp.lcm[p];
-    }
-}
-template <bool SPILL>
-__device__ __forceinline__ void hstore(const Heap& hp, int p, double g, uint32_t cm)
-{
-    if constexpr (SPILL) {
-        hp.store(p, g, cm);
-    } else {
-        hp.lg[p] = g;
-        hp.lcm[p] = cm;
-    }
-}
-// predicated load: SPILL lanes branch (a buffer load only where needed), LDS-only code loads a
-// clamped valid address unconditionally
-template <bool SPILL>
-__device__ __forceinline__ void hload_if(const Heap& hp, bool v, int p, double& g, uint32_t& cm)
-{
-    if constexpr (SPILL) {
-        g = 0.0;
-        cm = 0u;
-        if (v) hp.load(p, g, cm);
-    } else {
-        hload<false>(hp, v ? p : 0, g, cm);
-    }
-}
-
 // heappop on a heap of n (> 0, already decremented) entries whose old last element sits at
-// position n; the old root has been taken by the caller.  Updates `root` (wave-uniform heap[0]).
-//  1. the _siftup path p_0 = 0, p_1, .., p_K (a leaf) from the direction bits: a scalar walk over
-//     prefetched block words (tiers 0/1 in one LDS round, the 32 tier-2 candidates below p_5 in a
-//     second round that overlaps the tier-1 walk);
+// position n; the old root has been taken by the caller.  Updates the wave-uniform root (heap[0]).
+//  1. the _siftup path p_0 = 0, p_1, .., p_K (a leaf) from the direction bits: tier-0/1 words come
+//     with `last` in one LDS round, the 32 tier-2 candidates in a second round issued as soon as the
+//     tier-1 block is known; the walk itself is scalar;
 //  2. one round: lane i in 1..K loads heap[p_i], heap[p_{i+1}] and heap[sibling(p_i)];
 //  3. the children that move up are the prefix with !(last < heap[p_i]) (the path is sorted), so a
 //     ballot popcount m places `last` at p_m -- the array CPython's _siftup + _siftdown produce;
 //  4. lanes 1..m rewrite the bits of p_0..p_{m-1}, whose children changed.
-template <bool SPILL, int HEUR>
-__device__ __forceinline__ void heap_pop(const Heap& hp, const Q& qc, int n, Ent& root, int lane)
+template <bool SPILL, bool BIG, int HEUR>
+__device__ __forceinline__ void heap_pop(const Heap& h, int n, double& rootf, uint32_t& rootc, int lane)
 {
-    n = uni(n);  // wave-uniform by construction; say so, so the walk below stays on the SALU
-    Ent last;
-    hload<SPILL>(hp, n, last.f, last.cm);  // uniform address, but an LDS load is not known-uniform:
-    const uint32_t v01 = hp.lb[lane <= 32 ? lane : 0];  // tier-0 word (lane 0), tier-1 words (1..32)
-    last.f = rl_f64(last.f, 0);            // readlane makes `last` (and the root / node derived from
-    last.cm = rl_u32(last.cm, 0);          // it) SGPR values, keeping the whole walk scalar
-    last.hk = key_of<HEUR>(qc, last.cm);
+    n = uni(n);
+    double lf;
+    uint32_t lc;
+    hld<SPILL>(h, n, lf, lc);  // `last`, the same address in every lane
+    const uint32_t v01 = h.B[lane <= 32 ? lane : 0];  // tier-0 word (lane 0), tier-1 words (1..32)
+    const uint32_t lk = hkey<HEUR>(lc);
 
     // ---- 1. the path.  Levels 0..D-1 are full (D = floor(log2 n)), so every node above level D-1
     //      has two children and the walk takes D-1 unconditional steps; the last step (level D-1 ->
-    //      D) exists only below a node with a child.  Per step: c = bit, P = 2P + c (P = position + 1
-    //      of the current node), Pr = the same relative to the current block's root (bit index Pr-1).
+    //      D) exists only below a node with a child.  P = path number (position + 1); (w, prel) =
+    //      the block word (<< 1) and the block-relative number of the current node.
     const int D = 31 - __clz(n);
-    uint32_t P = 1, R1 = 0, v2 = 0;
-    int K = 0;
-    {
-        // w2 = block word << 1, so node Pr of the block (Pr = 1 at its root) is bit Pr of w2
-        uint32_t w2 = rl_u32(v01, 0) << 1, Pr = 1;
-        const int full = D - 1;
-        int lvl = 0;  // level of the current node
-        for (int t = 0; lvl < full; t++) {
-            const int steps = min(5, full - lvl);  // unconditional steps inside this block
-            for (int r = 0; r < steps; r++) Pr = 2u * Pr + ((w2 >> Pr) & 1u);
-            P = (P << steps) + Pr - (1u << steps);
-            lvl += steps;
-            if (steps < 5) break;
-            // the node reached roots the block of tier t + 1: fetch its word
-            Pr = 1u;
-            if (t == 0) {
-                w2 = rl_u32(v01, (int)P - 31) << 1;
-                R1 = P;
-                if (full >= 10) v2 = hp.lb[33 + ((R1 << 5) - 1024u) + (uint32_t)(lane & 31)];
-            } else if (t == 1) {
-                w2 = rl_u32(v2, (int)(P - (R1 << 5))) << 1;
-            } else {  // tiers >= 3 (heaps above 32767 entries): an L2-coherent read of the HBM block
-                w2 = (uint32_t)uni((int)__hip_atomic_fetch_or(hp.hb + hb_word(t + 1, P), 0u, __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT)) << 1;
+    const int full = D - 1;
+    uint32_t P = 1, prel = 1, w = rl_u32(v01, 0) << 1;
+    int lvl = 0;
+    if (full > 0) {
+        const int s0 = min(5, full);
+        const uint32_t pr0 = walk5(w);
+        prel = pr0 >> (5 - s0);
+        P = prel;
+        lvl = s0;
+        if (s0 == 5) {  // P roots a tier-1 block
+            const uint32_t R1 = P;
+            uint32_t v2 = 0;
+            if (full >= 10) v2 = h.B[33 + (R1 << 5) - 1024 + (uint32_t)(lane & 31)];
+            w = rl_u32(v01, (int)R1 - 31) << 1;
+            prel = 1;
+            if (full > 5) {
+                const int s1 = min(5, full - 5);
+                const uint32_t pr1 = walk5(w);
+                prel = pr1 >> (5 - s1);
+                P = (R1 << s1) + prel - (1u << s1);
+                lvl = 5 + s1;
+                if (s1 == 5) {  // P roots a tier-2 block
+                    const uint32_t R2 = P;
+                    w = rl_u32(v2, (int)(R2 - (R1 << 5))) << 1;
+                    prel = 1;
+                    if (full > 10) {
+                        const int s2 = min(5, full - 10);
+                        const uint32_t pr2 = walk5(w);
+                        prel = pr2 >> (5 - s2);
+                        P = (R2 << s2) + prel - (1u << s2);
+                        lvl = 10 + s2;
+                        if constexpr (BIG) {
+                            // tiers >= 3 (heaps above 32767 entries): L2-coherent reads of the HBM blocks
+                            int s = s2;
+                            for (int t = 3; s == 5; t++) {
+                                w = (uint32_t)uni((int)__hip_atomic_fetch_or(h.hb + hb_word(t, P), 0u, __ATOMIC_RELAXED,
+                                                                             __HIP_MEMORY_SCOPE_AGENT)) << 1;
+                                prel = 1;
+                                if (full <= lvl) break;
+                                s = min(5, full - lvl);
+                                const uint32_t pr = walk5(w);
+                                prel = pr >> (5 - s);
+                                P = (P << s) + prel - (1u << s);
+                                lvl += s;
+                            }
+                        }
+                    }
+                }
             }
         }
-        K = lvl;
-        // the last step: below a node at level D-1 with a child (2p + 1 < n, p = P - 1)
-        // (w2, Pr) already describe the block holding the node at level D-1
-        if (D >= 1 && 2u * P - 1u < (uint32_t)n) {
-            const uint32_t c = (2u * P < (uint32_t)n) ? ((w2 >> Pr) & 1u) : 0u;
-            P = 2u * P + c;
-            K++;
-        }
     }
+    // the last step: below the node at level D-1 if it has a child (position 2P - 1 < n); the bit
+    // counts only when it also has a right child
+    if (2u * P <= (uint32_t)n) {
+        const uint32_t c = (2u * P < (uint32_t)n) ? ((w >> prel) & 1u) : 0u;
+        P = 2u * P + c;
+        lvl++;
+    }
+    const int K = lvl;
 
     // ---- 2. one load round
     const bool on = lane >= 1 && lane <= K;
-    const int sh = K - lane;
+    const int sh = on ? K - lane : 0;
     const int pi = on ? (int)(P >> sh) - 1 : 0;
     const bool hasb = on && lane < K;
     const int pn = hasb ? (int)(P >> (sh - 1)) - 1 : 0;
-    const int si = (pi & 1) ? pi + 1 : pi - 1;
+    const int si = ((pi - 1) ^ 1) + 1;  // sibling: odd (left) p -> p + 1, even (right) p -> p - 1
     const bool hass = on && si < n;
-    Ent A, B, S;
-    hload_if<SPILL>(hp, on, pi, A.f, A.cm);
-    hload_if<SPILL>(hp, hasb, pn, B.f, B.cm);
-    hload_if<SPILL>(hp, hass, si, S.f, S.cm);
-    A.hk = key_of<HEUR>(qc, A.cm);
-    B.hk = key_of<HEUR>(qc, B.cm);
-    S.hk = key_of<HEUR>(qc, S.cm);
+    double Af, Bf, Sf;
+    uint32_t Ac, Bc, Sc;
+    {
+        Ld<SPILL> la, lb, ls;
+        la.issue(h, pi);
+        lb.issue(h, pn);
+        ls.issue(h, hass ? si : 0);
+        la.get(Af, Ac);
+        lb.get(Bf, Bc);
+        ls.get(Sf, Sc);
+    }
+    const uint32_t Ak = hkey<HEUR>(Ac), Bk = hkey<HEUR>(Bc), Sk = hkey<HEUR>(Sc);
 
-    // ---- 3. movers and stores
-    const int m = __popcll(ballot(on && !ent_lt(last, A)));
-    if (lane >= 1 && lane <= m) hstore<SPILL>(hp, (int)(P >> (sh + 1)) - 1, A.f, A.cm);
-    if (lane == 0) hstore<SPILL>(hp, (int)(P >> (K - m)) - 1, last.f, last.cm);
+    // ---- 3. movers: lanes 1..m store heap[p_i] at p_{i-1}; lane 0 stores last at p_m
+    const int m = __popcll(ballot(on && !key_lt(lf, lk, Af, Ak)));
+    {
+        const bool l0 = lane == 0;
+        const bool st = l0 || (on && lane <= m);
+        const int dst = (int)(P >> (l0 ? K - m : sh + 1)) - 1;
+        hst<SPILL>(h, st, dst, l0 ? lf : Af, l0 ? lc : Ac);
+    }
     if (m >= 1) {
-        root.f = rl_f64(A.f, 1);
-        root.cm = rl_u32(A.cm, 1);
-        root.hk = rl_u32(A.hk, 1);
+        rootf = rl_f64(Af, 1);
+        rootc = rl_u32(Ac, 1);
     } else {
-        root = last;
+        rootf = rl_f64(lf, 0);
+        rootc = rl_u32(lc, 0);
     }
 
-    // ---- 4. bits of p_0 .. p_{m-1}
-    if (hass && lane <= m) {
-        const Ent vn = lane < m ? B : last;  // the new heap[p_i]
-        const bool bit = (pi & 1) ? !ent_lt(vn, S) : !ent_lt(S, vn);
-        bit_write(hp, lane - 1, P >> (sh + 1), bit ? 1u : 0u);
+    // ---- 4. bits of p_0 .. p_{m-1}: the new heap[p_i] against its sibling
+    {
+        const bool useb = lane < m;
+        const double vf = useb ? Bf : lf;
+        const uint32_t vk = useb ? Bk : lk;
+        const bool bit = (pi & 1) ? !key_lt(vf, vk, Sf, Sk) : !key_lt(Sf, Sk, vf, vk);
+        bit_write<BIG>(h, hass && lane <= m, lane - 1, P >> (sh + 1), bit);
     }
     wave_sync_mem();
 }
@@ -311,34 +374,68 @@ __device__ __forceinline__ void heap_pop(const Heap& hp, const Q& qc, int n, Ent
 // heappush of `it` onto a heap of n entries (position n is free): the ancestors a_j = parent^j(n)
 // load in one round (with the siblings of a_{j-1}, for the bits); a ballot popcount t gives how
 // many move down; lanes 1..t+1 rewrite the bits of a_1..a_{t+1}, whose children changed.
-template <bool SPILL, int HEUR>
-__device__ __forceinline__ void heap_push(const Heap& hp, const Q& qc, int n, const Ent& it, Ent& root, int lane)
+template <bool SPILL, bool BIG, int HEUR>
+__device__ __forceinline__ void heap_push(const Heap& h, int n, double itf, uint32_t itc, uint32_t itk, double& rootf,
+                                          uint32_t& rootc, int lane)
 {
     n = uni(n);
     const uint32_t np1 = (uint32_t)n + 1u;
     const int D = 31 - __clz((int)np1);  // depth of position n
     const bool on = lane >= 1 && lane <= D;
-    const int aj = on ? (int)(np1 >> lane) - 1 : 0;
-    const int x = on ? (int)(np1 >> (lane - 1)) - 1 : 1;  // a_{j-1}
-    const int sx = (x & 1) ? x + 1 : x - 1;
+    const int l1 = on ? lane : 1;
+    const int aj = (int)(np1 >> l1) - 1;        // a_j
+    const int x = (int)(np1 >> (l1 - 1)) - 1;   // a_{j-1}
+    const int sx = ((x - 1) ^ 1) + 1;
     const bool hass = on && sx < n;  // a_{j-1} = n (lane 1) has a sibling only when n is even
-    Ent a, S;
-    hload_if<SPILL>(hp, on, aj, a.f, a.cm);
-    hload_if<SPILL>(hp, hass, sx, S.f, S.cm);
-    a.hk = key_of<HEUR>(qc, a.cm);
-    S.hk = key_of<HEUR>(qc, S.cm);
-    const int t = __popcll(ballot(on && ent_lt(it, a)));  // the "less" set is a prefix from the parent up
-    if (lane >= 1 && lane <= t) hstore<SPILL>(hp, x, a.f, a.cm);
+    double Af, Sf;
+    uint32_t Ac, Sc;
+    {
+        Ld<SPILL> la, ls;
+        la.issue(h, on ? aj : 0);
+        ls.issue(h, hass ? sx : 0);
+        la.get(Af, Ac);
+        ls.get(Sf, Sc);
+    }
+    const uint32_t Ak = hkey<HEUR>(Ac), Sk = hkey<HEUR>(Sc);
+    const int t = __popcll(ballot(on && key_lt(itf, itk, Af, Ak)));  // the "less" set is a prefix from the parent up
     const int ipos = (int)(np1 >> t) - 1;
-    if (lane == 0) hstore<SPILL>(hp, ipos, it.f, it.cm);
-    if (ipos == 0) root = it;
-    if (hass && lane <= t + 1) {
-        const Ent vn = lane - 1 < t ? a : it;  // the new heap[a_{j-1}]
-        const bool bit = (x & 1) ? !ent_lt(vn, S) : !ent_lt(S, vn);
-        bit_write(hp, D - lane, np1 >> lane, bit ? 1u : 0u);
+    {
+        const bool l0 = lane == 0;
+        const bool st = l0 || (on && lane <= t);
+        hst<SPILL>(h, st, l0 ? ipos : x, l0 ? itf : Af, l0 ? itc : Ac);
+    }
+    if (ipos == 0) {
+        rootf = itf;
+        rootc = itc;
+    }
+    {
+        const bool usea = lane - 1 < t;  // the new heap[a_{j-1}]
+        const double vf = usea ? Af : itf;
+        const uint32_t vk = usea ? Ak : itk;
+        const bool bit = (x & 1) ? !key_lt(vf, vk, Sf, Sk) : !key_lt(Sf, Sk, vf, vk);
+        bit_write<BIG>(h, hass && lane <= t + 1, D - l1, np1 >> l1, bit);
     }
     wave_sync_mem();
 }
+
+template <int HEUR>
+__device__ __forceinline__ void pop_any(const Heap& h, int n, double& rootf, uint32_t& rootc, int lane)
+{
+    if (n < h.cap) heap_pop<false, false, HEUR>(h, n, rootf, rootc, lane);
+    else if (n < kBigHeap) heap_pop<true, false, HEUR>(h, n, rootf, rootc, lane);
+    else heap_pop<true, true, HEUR>(h, n, rootf, rootc, lane);
+}
+template <int HEUR>
+__device__ __forceinline__ void push_any(const Heap& h, int n, double itf, uint32_t itc, uint32_t itk, double& rootf,
+                                         uint32_t& rootc, int lane)
+{
+    if (n < h.cap) heap_push<false, false, HEUR>(h, n, itf, itc, itk, rootf, rootc, lane);
+    else if (n < kBigHeap) heap_push<true, false, HEUR>(h, n, itf, itc, itk, rootf, rootc, lane);
+    else heap_push<true, true, HEUR>(h, n, itf, itc, itk, rootf, rootc, lane);
+}
+
+// 4-bit cell state: word i >> 3, nibble i & 7
+__device__ __forceinline__ uint32_t cst_at(const uint32_t* cst, uint32_t i) { return (cst[i >> 3] >> ((i & 7) * 4)) & 15u; }
 
 template <int HEUR>
 __global__ __launch_bounds__(64) void astar2d_kernel(
@@ -356,21 +453,32 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
     const int worker = blockIdx.x;
     span_begin(span);
     Heap hp;
-    hp.lb = (lds_u32*)smem;
-    hp.lg = (lds_f64*)(smem + kBitsLdsBytes);
-    hp.lcm = (lds_u32*)(smem + kBitsLdsBytes + (size_t)8 * lds_cap);
+    hp.B = (lds_u32*)smem;
+    hp.F = (lds_f64*)(smem + kBitsLdsBytes);
+    hp.C = (lds_u32*)(smem + kBitsLdsBytes + (size_t)8 * lds_cap);
     hp.hb = hbits_all + (size_t)worker * hbits_words;
     {
         const size_t spill_n = (size_t)(heap_cap > lds_cap ? heap_cap - lds_cap : 0);
         hp.spill = __builtin_amdgcn_make_buffer_rsrc(spill_all + (size_t)worker * spill_n, 0, (int)(spill_n * 16), 0x00020000);
     }
-    hp.lds_cap = lds_cap;
+    hp.cap = lds_cap;
     uint32_t* cst = cst_all + (size_t)worker * cst_words;
     double* G = G_all + (size_t)worker * ((size_t)W * (size_t)H);
+
+    // ---- per-lane constants
     // this lane's cell of the 3x3 block: lane i < 9 -> occupancy of (x + i/3 - 1, y + i%3 - 1),
-    // lane 9 + i -> its CLOSED-state nibble
+    // lane 9 + i -> its CLOSED-state nibble, lane 18 -> G[parent]
     const int blk_i = lane < 9 ? lane : (lane < 18 ? lane - 9 : 4);
     const int blk_dx = blk_i / 3 - 1, blk_dy = blk_i % 3 - 1;
+    // motion of lane m < 8: offset, cost, and the 3x3 cells isCollision needs free
+    // (graph_search.py:66-87: both endpoints; for a diagonal both corner cells)
+    const int mo = lane & 7;
+    const int mx = mot_x(mo), my = mot_y(mo);
+    const double mcost = (mo & 1) ? kSqrt2 : 1.0;
+    const int par_off = mx * H + my;  // lane d: linear offset of motion d (parent = cell - offset)
+    uint32_t need = 16u | (1u << ((mx + 1) * 3 + (my + 1)));
+    if (mo & 1) need |= (1u << (3 + (my + 1))) | (1u << ((mx + 1) * 3 + 1));
+    const uint32_t self_bit = 1u << ((mx + 1) * 3 + (my + 1));
 
     for (;;) {
         // readfirstlane (not __shfl): the compiler must SEE the query index as wave-uniform, or
@@ -393,12 +501,10 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
         }
         wave_sync_mem();
 
-        const int sx = start_xy[2 * q], sy = start_xy[2 * q + 1];
-        Q qc;
-        qc.gx = goal_xy[2 * q];
-        qc.gy = goal_xy[2 * q + 1];
+        const int sx = uni(start_xy[2 * q]), sy = uni(start_xy[2 * q + 1]);
+        const int gx = uni(goal_xy[2 * q]), gy = uni(goal_xy[2 * q + 1]);
         const bool s_in = (unsigned)sx < (unsigned)W && (unsigned)sy < (unsigned)H;
-        const bool g_in = (unsigned)qc.gx < (unsigned)W && (unsigned)qc.gy < (unsigned)H;
+        const bool g_in = (unsigned)gx < (unsigned)W && (unsigned)gy < (unsigned)H;
         if (!s_in || !g_in) {  // outside the grid: blocked -> no neighbours -> no path
             // every lane stores the same values: no lane-0-only block right before the continue
             status_out[q] = PMP_NO_PATH;
@@ -410,13 +516,11 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
             }
             continue;
         }
-        const uint32_t goal_xy13 = ((uint32_t)qc.gx << 13) | (uint32_t)qc.gy;
 
-        Ent root;  // heap[0], kept in registers (wave-uniform)
-        root.cm = ((((uint32_t)sx << 13) | (uint32_t)sy) << 4) | 8u;  // Node(start, start, 0, 0)
-        root.hk = 0;
-        root.f = 0.0;
-        if (lane == 0) hstore<true>(hp, 0, root.f, root.cm);
+        // heap[0] in registers (wave-uniform): Node(start, start, 0, 0), key (0, h = 0)
+        double rootf = 0.0;
+        uint32_t rootc = pack_cm(0, 0, 8);
+        if (lane == 0) hst<true>(hp, true, 0, rootf, rootc);
         wave_sync_mem();
 
         int n = 1;
@@ -432,11 +536,12 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
 #endif
         while (n > 0) {
             STAMP(ts0);
-            const Ent node = root;
+            const uint32_t ncm = rootc;
             npop++;
             n -= 1;
-            const int x = (int)(node.cm >> 17), y = (int)((node.cm >> 4) & 8191u);
-            const int ndir = (int)(node.cm & 15u);
+            const int ndir = (int)(ncm & 15u);
+            const int x = ndir == 8 ? sx : gx - cm_dx(ncm);
+            const int y = ndir == 8 ? sy : gy - cm_dy(ncm);
             const uint32_t nlin = (uint32_t)x * (uint32_t)H + (uint32_t)y;
 
             // ---- HBM round, issued before the LDS pop so the two overlap: one unconditional load
@@ -452,7 +557,10 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 blk_word = *ptr;
             }
             double gpar = 0.0;  // G[parent] (the parent closed earlier); the start has g = 0
-            if (lane == 18 && ndir < 8) gpar = G[(uint32_t)(x - c_mx[ndir]) * (uint32_t)H + (uint32_t)(y - c_my[ndir])];
+            if (ndir < 8) {
+                const uint32_t plin = nlin - (uint32_t)rl_u32((uint32_t)par_off, ndir);
+                if (lane == 18) gpar = G[plin];
+            }
 #ifdef PMP_STAMPS_SPLIT  // diagnostic: wait for the HBM round before the pop, time the two apart
             asm volatile("s_waitcnt vmcnt(0)" ::"v"(blk_word), "v"(gpar) : "memory");
             STAMP(tsB);
@@ -461,10 +569,7 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
 #endif
 
             // ---- heappop (a_star.py:54): `last` = heap[n] sifts down the CPython path
-            if (n > 0) {
-                if (n < lds_cap) heap_pop<false, HEUR>(hp, qc, n, root, lane);
-                else heap_pop<true, HEUR>(hp, qc, n, root, lane);
-            }
+            if (n > 0) pop_any<HEUR>(hp, n, rootf, rootc, lane);
 
             STAMP(ts1);
             // 3x3 masks: bit k = cell (x + k/3 - 1, y + k%3 - 1); the node is k = 4
@@ -489,7 +594,7 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 expand_out[(size_t)q * expand_cap + nexp] = nlin | ((uint32_t)ndir << 28);
             nexp++;
 
-            if (node.cm >> 4 == goal_xy13) {  // goal found (a_star.py:61-64)
+            if (x == gx && y == gy) {  // goal found (a_star.py:61-64)
                 st = PMP_FOUND;
                 wave_sync_mem();
                 if (lane == 0) {  // extractPath (a_star.py:98-117): goal -> start, cost in that order
@@ -504,8 +609,8 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                         if (cx == sx && cy == sy) break;
                         const int d = (int)cst_at(cst, li) - 1;
                         cost += (d & 1) ? kSqrt2 : 1.0;
-                        cx -= c_mx[d];
-                        cy -= c_my[d];
+                        cx -= mot_x(d);
+                        cy -= mot_y(d);
                     }
                     goal_cost = cost;
                     plen = len;
@@ -514,37 +619,21 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
             }
 
             // ---- getNeighbor + the push loop in motion order; push the goal and stop (a_star.py:66-80)
-            bool nb_ok = false;
-            uint32_t nbxy = 0;
-            if (lane < 8) {
-                const int ax = c_mx[lane] + 1, ay = c_my[lane] + 1;
-                uint32_t need = 16u | (1u << (ax * 3 + ay));                     // both endpoints
-                if (lane & 1) need |= (1u << (3 + ay)) | (1u << (ax * 3 + 1));  // both corner cells
-                nb_ok = (occ9 & need) == 0u && ((cls9 >> (ax * 3 + ay)) & 1u) == 0u;
-                nbxy = ((uint32_t)(x + c_mx[lane]) << 13) | (uint32_t)(y + c_my[lane]);
-            }
+            const int ndx = gx - x - mx, ndy = gy - y - my;  // goal - neighbour of lane m
+            const bool nb_ok = lane < 8 && (occ9 & need) == 0u && (cls9 & self_bit) == 0u;
             uint64_t vm = ballot(nb_ok) & 0xffull;
-            const uint64_t gm = ballot(nb_ok && nbxy == goal_xy13) & 0xffull;
+            const uint64_t gm = ballot(nb_ok && ndx == 0 && ndy == 0) & 0xffull;
             if (gm) vm &= (gm << 1) - 1;
-            Ent item;  // node + motion (node.py:39-41), h = GraphSearcher.h (graph_search.py:41-44)
-            {
-                const int m = lane & 7;
-                item.cm = (nbxy << 4) | (uint32_t)m;
-                item.f = 0.0;
-                item.hk = 0u;
-                if (lane < 8) item.f = (gnode + ((m & 1) ? kSqrt2 : 1.0)) + h_and_key<HEUR>(qc, item.cm, item.hk);
-            }
+            // Node + motion (node.py:39-41), h = GraphSearcher.h (graph_search.py:41-44)
+            const uint32_t icm = pack_cm(ndx, ndy, mo);
+            const uint32_t ik = hkey<HEUR>(icm);
+            const double ifv = (gnode + mcost) + h_of_key<HEUR>(ik);
             bool overflow = false;
             while (vm) {
                 const int m = __ffsll((long long)vm) - 1;
                 vm &= vm - 1;
                 if (n >= heap_cap) { overflow = true; break; }
-                Ent it;
-                it.f = rl_f64(item.f, m);
-                it.cm = rl_u32(item.cm, m);
-                it.hk = rl_u32(item.hk, m);
-                if (n < lds_cap) heap_push<false, HEUR>(hp, qc, n, it, root, lane);
-                else heap_push<true, HEUR>(hp, qc, n, it, root, lane);
+                push_any<HEUR>(hp, n, rl_f64(ifv, m), rl_u32(icm, m), rl_u32(ik, m), rootf, rootc, lane);
                 n += 1;
                 npush++;
             }
