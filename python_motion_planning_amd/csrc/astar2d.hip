@@ -249,13 +249,14 @@ __device__ __forceinline__ void wave_sync_mem()
 //     ballot popcount m places `last` at p_m -- the array CPython's _siftup + _siftdown produce;
 //  4. lanes 1..m rewrite the bits of p_0..p_{m-1}, whose children changed.
 template <bool SPILL, bool BIG, int HEUR>
-__device__ __forceinline__ void heap_pop(const Heap& h, int n, double& rootf, uint32_t& rootc, int lane)
+__device__ __forceinline__ void heap_pop(const Heap& h, int n, uint32_t v01, double& lastf, uint32_t& lastc, double& rootf,
+                                         uint32_t& rootc, int lane)
 {
     n = uni(n);
-    double lf;
-    uint32_t lc;
-    hld<SPILL>(h, n, lf, lc);  // `last`, the same address in every lane
-    const uint32_t v01 = h.B[lane <= 32 ? lane : 0];  // tier-0 word (lane 0), tier-1 words (1..32)
+    // `last` = heap[n] is kept in registers by the caller (no load round); v01 = the tier-0 word
+    // (lane 0) and tier-1 words (lanes 1..32), loaded by the caller ahead of time
+    const double lf = lastf;
+    const uint32_t lc = lastc;
     const uint32_t lk = hkey<HEUR>(lc);
 
     // ---- 1. the path.  Levels 0..D-1 are full (D = floor(log2 n)), so every node above level D-1
@@ -323,10 +324,10 @@ __device__ __forceinline__ void heap_pop(const Heap& h, int n, double& rootf, ui
     }
     const int K = lvl;
 
-    // ---- 2. one load round
+    // ---- 2. one load round; lane 0 loads heap[n - 1], the next `last`
     const bool on = lane >= 1 && lane <= K;
     const int sh = on ? K - lane : 0;
-    const int pi = on ? (int)(P >> sh) - 1 : 0;
+    const int pi = on ? (int)(P >> sh) - 1 : (lane == 0 ? n - 1 : 0);
     const bool hasb = on && lane < K;
     const int pn = hasb ? (int)(P >> (sh - 1)) - 1 : 0;
     const int si = ((pi - 1) ^ 1) + 1;  // sibling: odd (left) p -> p + 1, even (right) p -> p - 1
@@ -356,8 +357,14 @@ __device__ __forceinline__ void heap_pop(const Heap& h, int n, double& rootf, ui
         rootf = rl_f64(Af, 1);
         rootc = rl_u32(Ac, 1);
     } else {
-        rootf = rl_f64(lf, 0);
-        rootc = rl_u32(lc, 0);
+        rootf = lf;
+        rootc = lc;
+    }
+    // the new last element heap[n - 1]: n - 1 has no children, so of the path it can only be the
+    // leaf p_K, which this pop rewrites only when last itself lands there
+    if (!(m == K && P == (uint32_t)n)) {
+        lastf = rl_f64(Af, 0);
+        lastc = rl_u32(Ac, 0);
     }
 
     // ---- 4. bits of p_0 .. p_{m-1}: the new heap[p_i] against its sibling
@@ -375,8 +382,8 @@ __device__ __forceinline__ void heap_pop(const Heap& h, int n, double& rootf, ui
 // load in one round (with the siblings of a_{j-1}, for the bits); a ballot popcount t gives how
 // many move down; lanes 1..t+1 rewrite the bits of a_1..a_{t+1}, whose children changed.
 template <bool SPILL, bool BIG, int HEUR>
-__device__ __forceinline__ void heap_push(const Heap& h, int n, double itf, uint32_t itc, uint32_t itk, double& rootf,
-                                          uint32_t& rootc, int lane)
+__device__ __forceinline__ void heap_push(const Heap& h, int n, double itf, uint32_t itc, uint32_t itk, double& lastf,
+                                          uint32_t& lastc, double& rootf, uint32_t& rootc, int lane)
 {
     n = uni(n);
     const uint32_t np1 = (uint32_t)n + 1u;
@@ -408,6 +415,14 @@ __device__ __forceinline__ void heap_push(const Heap& h, int n, double itf, uint
         rootf = itf;
         rootc = itc;
     }
+    // the new last element heap[n]: the item, or the parent that moved down into n
+    if (t == 0) {
+        lastf = itf;
+        lastc = itc;
+    } else {
+        lastf = rl_f64(Af, 1);
+        lastc = rl_u32(Ac, 1);
+    }
     {
         const bool usea = lane - 1 < t;  // the new heap[a_{j-1}]
         const double vf = usea ? Af : itf;
@@ -419,19 +434,20 @@ __device__ __forceinline__ void heap_push(const Heap& h, int n, double itf, uint
 }
 
 template <int HEUR>
-__device__ __forceinline__ void pop_any(const Heap& h, int n, double& rootf, uint32_t& rootc, int lane)
+__device__ __forceinline__ void pop_any(const Heap& h, int n, uint32_t v01, double& lastf, uint32_t& lastc, double& rootf,
+                                        uint32_t& rootc, int lane)
 {
-    if (n < h.cap) heap_pop<false, false, HEUR>(h, n, rootf, rootc, lane);
-    else if (n < kBigHeap) heap_pop<true, false, HEUR>(h, n, rootf, rootc, lane);
-    else heap_pop<true, true, HEUR>(h, n, rootf, rootc, lane);
+    if (n < h.cap) heap_pop<false, false, HEUR>(h, n, v01, lastf, lastc, rootf, rootc, lane);
+    else if (n < kBigHeap) heap_pop<true, false, HEUR>(h, n, v01, lastf, lastc, rootf, rootc, lane);
+    else heap_pop<true, true, HEUR>(h, n, v01, lastf, lastc, rootf, rootc, lane);
 }
 template <int HEUR>
-__device__ __forceinline__ void push_any(const Heap& h, int n, double itf, uint32_t itc, uint32_t itk, double& rootf,
-                                         uint32_t& rootc, int lane)
+__device__ __forceinline__ void push_any(const Heap& h, int n, double itf, uint32_t itc, uint32_t itk, double& lastf,
+                                         uint32_t& lastc, double& rootf, uint32_t& rootc, int lane)
 {
-    if (n < h.cap) heap_push<false, false, HEUR>(h, n, itf, itc, itk, rootf, rootc, lane);
-    else if (n < kBigHeap) heap_push<true, false, HEUR>(h, n, itf, itc, itk, rootf, rootc, lane);
-    else heap_push<true, true, HEUR>(h, n, itf, itc, itk, rootf, rootc, lane);
+    if (n < h.cap) heap_push<false, false, HEUR>(h, n, itf, itc, itk, lastf, lastc, rootf, rootc, lane);
+    else if (n < kBigHeap) heap_push<true, false, HEUR>(h, n, itf, itc, itk, lastf, lastc, rootf, rootc, lane);
+    else heap_push<true, true, HEUR>(h, n, itf, itc, itk, lastf, lastc, rootf, rootc, lane);
 }
 
 // 4-bit cell state: word i >> 3, nibble i & 7
@@ -520,6 +536,8 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
         // heap[0] in registers (wave-uniform): Node(start, start, 0, 0), key (0, h = 0)
         double rootf = 0.0;
         uint32_t rootc = pack_cm(0, 0, 8);
+        double lastf = rootf;  // heap[n - 1]
+        uint32_t lastc = rootc;
         if (lane == 0) hst<true>(hp, true, 0, rootf, rootc);
         wave_sync_mem();
 
@@ -537,6 +555,7 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
         while (n > 0) {
             STAMP(ts0);
             const uint32_t ncm = rootc;
+            const uint32_t v01 = hp.B[lane <= 32 ? lane : 0];  // bit words for the pop below
             npop++;
             n -= 1;
             const int ndir = (int)(ncm & 15u);
@@ -569,7 +588,7 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
 #endif
 
             // ---- heappop (a_star.py:54): `last` = heap[n] sifts down the CPython path
-            if (n > 0) pop_any<HEUR>(hp, n, rootf, rootc, lane);
+            if (n > 0) pop_any<HEUR>(hp, n, v01, lastf, lastc, rootf, rootc, lane);
 
             STAMP(ts1);
             // 3x3 masks: bit k = cell (x + k/3 - 1, y + k%3 - 1); the node is k = 4
@@ -633,7 +652,7 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 const int m = __ffsll((long long)vm) - 1;
                 vm &= vm - 1;
                 if (n >= heap_cap) { overflow = true; break; }
-                push_any<HEUR>(hp, n, rl_f64(ifv, m), rl_u32(icm, m), rl_u32(ik, m), rootf, rootc, lane);
+                push_any<HEUR>(hp, n, rl_f64(ifv, m), rl_u32(icm, m), rl_u32(ik, m), lastf, lastc, rootf, rootc, lane);
                 n += 1;
                 npush++;
             }
