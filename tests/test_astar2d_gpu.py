@@ -163,3 +163,27 @@ def test_unreachable_and_empty_batch():
     assert int(r["n_expanded"][0]) == O.astar2d(occ, (2, 2), (12, 12))["n_expanded"]
     r = batch.astar2d_batch(occ, np.zeros((0, 2), np.int32), np.zeros((0, 2), np.int32), path_cap=4)
     assert r["status"].numel() == 0
+
+
+def test_heap_above_32767_entries_uses_hbm_bit_tiers():
+    """A heap past 32767 entries walks levels >= 14, whose direction-bit blocks live in HBM
+    (astar2d.hip, tiers >= 3).  An open 2900x2900 grid whose goal is walled in explores every
+    cell and peaks at ~36k heap entries: counts and the closure must match the oracle exactly."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import batch
+
+    W = 2900
+    occ = np.zeros((W, W), np.uint8)
+    occ[0, :] = occ[-1, :] = occ[:, 0] = occ[:, -1] = 1
+    g = (W // 2, W // 2)
+    occ[g[0] - 1:g[0] + 2, g[1] - 1:g[1] + 2] = 1
+    occ[g] = 0
+    s = np.array([[1, 1]], np.int32)
+    ref = O.astar2d_batch(occ, s, np.array([g], np.int32))
+    assert ref["counters"][0, 3] > 32767
+    r = batch.astar2d_batch(occ, s, np.array([g], np.int32), path_cap=16, counters=True, reserve_slots=1,
+                            heap_cap=1 << 17)
+    assert int(r["status"][0]) == 1
+    assert int(r["n_expanded"][0]) == int(ref["n_expanded"][0])
+    assert r["counters"].cpu().numpy()[0].tolist() == ref["counters"][0].tolist()
+    batch.astar2d_batch(occ[:64, :64], s, s, path_cap=4, reserve_slots=64, heap_cap=0)  # default sizing again
