@@ -38,21 +38,21 @@ def lib():
         L.oracle_hypot.argtypes = [ctypes.c_double, ctypes.c_double]
         L.oracle_hypot_many.restype = None
         L.oracle_hypot_many.argtypes = [_dp, _dp, _dp, ctypes.c_int64]
-        L.oracle_astar2d.restype = ctypes.c_int
-        L.oracle_astar2d.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+        L.oracle_graph2d.restype = ctypes.c_int
+        L.oracle_graph2d.argtypes = [ctypes.c_int, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      _dp, _i32p, ctypes.c_int, _i32p, _i32p, ctypes.c_int, _i32p, _i64p]
-        L.oracle_astar3d.restype = ctypes.c_int
-        L.oracle_astar3d.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+        L.oracle_graph3d.restype = ctypes.c_int
+        L.oracle_graph3d.argtypes = [ctypes.c_int, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      _i32p, _i32p, _dp, _i32p, ctypes.c_int, _i32p, _i32p, ctypes.c_int,
                                      _i32p, _i64p]
         L.oracle_dstar2d.restype = ctypes.c_int
         L.oracle_dstar2d.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, _dp, _i32p, ctypes.c_int, _i32p,
                                      _i64p, ctypes.c_int64]
-        L.oracle_astar2d_batch.restype = ctypes.c_int
-        L.oracle_astar2d_batch.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p, _i32p,
-                                           ctypes.c_int, _dp, _i32p, ctypes.c_int, _i32p, _i32p, _i64p,
+        L.oracle_graph2d_batch.restype = ctypes.c_int
+        L.oracle_graph2d_batch.argtypes = [ctypes.c_int, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p,
+                                           _i32p, ctypes.c_int, _dp, _i32p, ctypes.c_int, _i32p, _i32p, _i64p,
                                            _i32p, ctypes.c_int]
         _lib = L
     return _lib
@@ -70,9 +70,14 @@ def hypot(a, b):
     return out
 
 
+# planners sharing the AStar loop (pmp_oracle.c oracle_graph2d / oracle_graph3d)
+ALGOS = {"astar": 0, "dijkstra": 1, "gbfs": 2}
+
+
 def astar2d(occ: np.ndarray, start, goal, heuristic: str = "euclidean", with_expand: bool = True,
-            path_cap: int | None = None, expand_cap: int | None = None):
-    """Restatement of AStar.plan (a_star.py:39-83).  occ: uint8 [W, H], occ[x, y] != 0 blocked.
+            path_cap: int | None = None, expand_cap: int | None = None, algo: str = "astar"):
+    """Restatement of AStar.plan (a_star.py:39-83); algo "dijkstra" / "gbfs" restate Dijkstra.plan
+    (dijkstra.py:36-85) / GBFS.plan (gbfs.py:36-86).  occ: uint8 [W, H], occ[x, y] != 0 blocked.
     Returns dict(status, cost, path (goal->start list of (x,y)), expand (closure order), counters)."""
     occ = np.ascontiguousarray(occ, dtype=np.uint8)
     W, H = occ.shape
@@ -84,7 +89,7 @@ def astar2d(occ: np.ndarray, start, goal, heuristic: str = "euclidean", with_exp
     plen = ctypes.c_int32(0)
     nexp = ctypes.c_int32(0)
     ctr = np.zeros(4, np.int64)
-    st = lib().oracle_astar2d(_p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0,
+    st = lib().oracle_graph2d(ALGOS[algo], _p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0,
                               int(start[0]), int(start[1]), int(goal[0]), int(goal[1]),
                               ctypes.byref(cost), _p(path, _i32p), path_cap, ctypes.byref(plen),
                               _p(expand, _i32p) if with_expand else None, expand_cap,
@@ -99,8 +104,10 @@ def astar2d(occ: np.ndarray, start, goal, heuristic: str = "euclidean", with_exp
     return out
 
 
-def astar3d(occ: np.ndarray, start, goal, heuristic: str = "euclidean", with_expand: bool = True):
-    """Restatement of AStar3D.plan (a_star3d.py:33-78).  occ: uint8 [X, Y, Z]."""
+def astar3d(occ: np.ndarray, start, goal, heuristic: str = "euclidean", with_expand: bool = True,
+            algo: str = "astar"):
+    """Restatement of AStar3D.plan (a_star3d.py:33-78); algo "dijkstra" / "gbfs" restate
+    Dijkstra3D.plan (dijkstra3d.py:39-87) / GBFS3D.plan (gbfs3d.py:34-82).  occ: uint8 [X, Y, Z]."""
     occ = np.ascontiguousarray(occ, dtype=np.uint8)
     X, Y, Z = occ.shape
     n = X * Y * Z
@@ -112,7 +119,7 @@ def astar3d(occ: np.ndarray, start, goal, heuristic: str = "euclidean", with_exp
     plen = ctypes.c_int32(0)
     nexp = ctypes.c_int32(0)
     ctr = np.zeros(4, np.int64)
-    st = lib().oracle_astar3d(_p(occ, _u8p), X, Y, Z, 1 if heuristic == "manhattan" else 0,
+    st = lib().oracle_graph3d(ALGOS[algo], _p(occ, _u8p), X, Y, Z, 1 if heuristic == "manhattan" else 0,
                               _p(s, _i32p), _p(g, _i32p), ctypes.byref(cost), _p(path, _i32p), n + 1,
                               ctypes.byref(plen), _p(expand, _i32p) if with_expand else None, n,
                               ctypes.byref(nexp), _p(ctr, _i64p))
@@ -146,8 +153,8 @@ def dstar2d(occ: np.ndarray, start, goal, max_process: int = 0):
 
 
 def astar2d_batch(occ: np.ndarray, starts, goals, heuristic: str = "euclidean", path_cap: int = 4096,
-                  nthreads: int = 0):
-    """OpenMP batch of the AStar.plan restatement (one grid, many queries)."""
+                  nthreads: int = 0, algo: str = "astar"):
+    """OpenMP batch of the AStar.plan (or Dijkstra / GBFS) restatement (one grid, many queries)."""
     occ = np.ascontiguousarray(occ, dtype=np.uint8)
     W, H = occ.shape
     s = np.ascontiguousarray(starts, np.int32).reshape(-1, 2)
@@ -156,7 +163,7 @@ def astar2d_batch(occ: np.ndarray, starts, goals, heuristic: str = "euclidean", 
     out = dict(cost=np.zeros(nq), path=np.zeros((nq, path_cap), np.int32), path_len=np.zeros(nq, np.int32),
                n_expanded=np.zeros(nq, np.int32), counters=np.zeros((nq, 4), np.int64),
                status=np.zeros(nq, np.int32))
-    lib().oracle_astar2d_batch(_p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0, _p(s, _i32p),
+    lib().oracle_graph2d_batch(ALGOS[algo], _p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0, _p(s, _i32p),
                                _p(g, _i32p), nq, _p(out["cost"], _dp), _p(out["path"], _i32p), path_cap,
                                _p(out["path_len"], _i32p), _p(out["n_expanded"], _i32p),
                                _p(out["counters"], _i64p), _p(out["status"], _i32p), int(nthreads))
@@ -485,13 +492,14 @@ def rrt_batch(star, rects, circs, X, Y, starts, goals, rnd, sample_num, max_dist
     return dict(status=st, n_nodes=nn, tree=tree)
 
 
-def astar3d_batch(occ, starts, goals, heuristic: str = "euclidean", nthreads: int = 0):
-    """AStar3D over per-query grids occ [nq, X, Y, Z] with OpenMP -> (cost [nq], status [nq])."""
+def astar3d_batch(occ, starts, goals, heuristic: str = "euclidean", nthreads: int = 0, algo: str = "astar"):
+    """AStar3D (or Dijkstra3D / GBFS3D) over per-query grids occ [nq, X, Y, Z] with OpenMP
+    -> (cost [nq], status [nq])."""
     L = lib()
     if not getattr(L, "_a3b", False):
-        L.oracle_astar3d_batch.restype = ctypes.c_int
-        L.oracle_astar3d_batch.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p, _i32p,
-                                           ctypes.c_int, _dp, _i32p, ctypes.c_int]
+        L.oracle_graph3d_batch.restype = ctypes.c_int
+        L.oracle_graph3d_batch.argtypes = [ctypes.c_int, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           _i32p, _i32p, ctypes.c_int, _dp, _i32p, ctypes.c_int]
         L._a3b = True
     occ = np.ascontiguousarray(occ, dtype=np.uint8)
     nq, X, Y, Z = occ.shape
@@ -499,6 +507,6 @@ def astar3d_batch(occ, starts, goals, heuristic: str = "euclidean", nthreads: in
     g = np.ascontiguousarray(goals, np.int32).reshape(-1, 3)
     cost = np.zeros(nq)
     st = np.zeros(nq, np.int32)
-    L.oracle_astar3d_batch(_p(occ, _u8p), X, Y, Z, 1 if heuristic == "manhattan" else 0, _p(s, _i32p), _p(g, _i32p),
-                           nq, _p(cost, _dp), _p(st, _i32p), nthreads)
+    L.oracle_graph3d_batch(ALGOS[algo], _p(occ, _u8p), X, Y, Z, 1 if heuristic == "manhattan" else 0, _p(s, _i32p),
+                           _p(g, _i32p), nq, _p(cost, _dp), _p(st, _i32p), nthreads)
     return cost, st

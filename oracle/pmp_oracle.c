@@ -159,12 +159,17 @@ static inline int collide2(const uint8_t* occ, int W, int H, int x1, int y1, int
 
 /*
  * AStar.plan  (global_planner/graph_search/a_star.py:39-83) + getNeighbor (:85-96)
- *             + extractPath (:98-117).
+ *             + extractPath (:98-117), and the two planners that share its loop:
+ *   algo 0: AStar      node_n.h = h(node_n)                            (a_star.py:71-72)
+ *   algo 1: Dijkstra   node_n.h = 0                                    (dijkstra.py:73-74)
+ *   algo 2: GBFS       node_n.h = h(node_n), node_n.g = 0              (gbfs.py:73-75)
+ * (Dijkstra/GBFS also skip neighbours in obstacles, dijkstra.py:66-67 / gbfs.py:66-67: a no-op,
+ * getNeighbor never returns one.)  All three push the start as Node(start, start, 0, 0).
  * heuristic: 0 = euclidean (math.hypot), 1 = manhattan (graph_search.py:41-44).
  * path: goal -> start order (reference does not reverse it), cell ids x*H+y.
  * expand (nullable): closure order of CLOSED (list(CLOSED.values()), :64).
  */
-int oracle_astar2d(const uint8_t* occ, int W, int H, int heuristic, int sx, int sy, int gx, int gy,
+int oracle_graph2d(int algo, const uint8_t* occ, int W, int H, int heuristic, int sx, int sy, int gx, int gy,
                    double* cost_out, int32_t* path, int path_cap, int32_t* path_len,
                    int32_t* expand, int expand_cap, int32_t* n_expanded, int64_t* counters)
 {
@@ -226,8 +231,10 @@ int oracle_astar2d(const uint8_t* occ, int W, int H, int heuristic, int sx, int 
             anode_t nb;
             nb.cell = nc;
             nb.parent = node.cell;
-            nb.g = node.g + ((m & 1) ? SQ2 : 1.0);
-            if (heuristic == 1)
+            nb.g = algo == 2 ? 0.0 : node.g + ((m & 1) ? SQ2 : 1.0);
+            if (algo == 1)
+                nb.h = 0.0;
+            else if (heuristic == 1)
                 nb.h = (double)(abs(gx - nx) + abs(gy - ny));
             else
                 nb.h = vnorm2((double)(gx - nx), (double)(gy - ny));
@@ -255,6 +262,14 @@ done:
     if (status == 0 && expand && nexp > expand_cap) status = 3;
     free(closed); free(cparent); free(heap);
     return status;
+}
+
+int oracle_astar2d(const uint8_t* occ, int W, int H, int heuristic, int sx, int sy, int gx, int gy,
+                   double* cost_out, int32_t* path, int path_cap, int32_t* path_len,
+                   int32_t* expand, int expand_cap, int32_t* n_expanded, int64_t* counters)
+{
+    return oracle_graph2d(0, occ, W, H, heuristic, sx, sy, gx, gy, cost_out, path, path_cap, path_len, expand,
+                          expand_cap, n_expanded, counters);
 }
 
 /* ------------------------------------------------------------------------------------ */
@@ -340,9 +355,14 @@ static inline int collide3(const uint8_t* occ, int X, int Y, int Z, int x1, int 
 
 /* heuristic: 0 euclidean = math.sqrt(dx**2+dy**2+dz**2) (graph_search_3d.py:40-50), 1 manhattan.
  * path: start -> goal.  expand: distinct CLOSED keys in first-insertion order.
- * Unreachable -> status 1 with cost = inf (a_star3d.py:77-78). */
-int oracle_astar3d(const uint8_t* occ, int X, int Y, int Z, int heuristic, const int32_t* s, const int32_t* g,
-                   double* cost_out, int32_t* path, int path_cap, int32_t* path_len,
+ * Unreachable -> status 1 with cost = inf (a_star3d.py:77-78).
+ * algo 0: AStar3D.  algo 1: Dijkstra3D (dijkstra3d.py:39-87): key (g, 0.0, counter), start h = 0,
+ * the same reopening rules; its getNeighbor (:89-126) adds an in-bounds test and face checks that
+ * equal isCollision's, so with out-of-grid cells blocked it is this loop with h = 0.
+ * algo 2: GBFS3D (gbfs3d.py:34-82): key (h, counter), CLOSED membership tests (:55, :74) -- this
+ * loop with every g = 0: (f, h, counter) = (h, h, counter), and `g >= closed g` is always true. */
+int oracle_graph3d(int algo, const uint8_t* occ, int X, int Y, int Z, int heuristic, const int32_t* s,
+                   const int32_t* g, double* cost_out, int32_t* path, int path_cap, int32_t* path_len,
                    int32_t* expand, int expand_cap, int32_t* n_expanded, int64_t* counters)
 {
     const int64_t ncell = (int64_t)X * Y * Z;
@@ -358,7 +378,7 @@ int oracle_astar3d(const uint8_t* occ, int X, int Y, int Z, int heuristic, const
     const int gx = g[0], gy = g[1], gz = g[2];
     const int32_t start = (s[0] * Y + s[1]) * Z + s[2], goal = (gx * Y + gy) * Z + gz;
 #define H3(x, y, z)                                                                                     \
-    (heuristic == 1 ? (double)(abs(gx - (x)) + abs(gy - (y)) + abs(gz - (z)))                         \
+    (algo == 1 ? 0.0 : heuristic == 1 ? (double)(abs(gx - (x)) + abs(gy - (y)) + abs(gz - (z)))       \
                     : sqrt((double)((gx - (x)) * (gx - (x)) + (gy - (y)) * (gy - (y)) + (gz - (z)) * (gz - (z)))))
     {
         double h0 = H3(s[0], s[1], s[2]);
@@ -415,7 +435,7 @@ int oracle_astar3d(const uint8_t* occ, int X, int Y, int Z, int heuristic, const
             if (collide3(occ, X, Y, Z, x, y, z, dx, dy, dz)) continue;
             int nx = x + dx, ny = y + dy, nz = z + dz;
             int32_t nc = (nx * Y + ny) * Z + nz;
-            double tg = node.g + sqrt((double)(dx * dx + dy * dy + dz * dz));
+            double tg = algo == 2 ? 0.0 : node.g + sqrt((double)(dx * dx + dy * dy + dz * dz));
             if (closed[nc] && tg >= cg[nc]) continue;
             double hn = H3(nx, ny, nz);
             if (n == cap) {
@@ -438,6 +458,14 @@ done3:
     if (status == 0 && expand && nclose > expand_cap) status = 3;
     free(cg); free(cparent); free(closed); free(heap);
     return status;
+}
+
+int oracle_astar3d(const uint8_t* occ, int X, int Y, int Z, int heuristic, const int32_t* s, const int32_t* g,
+                   double* cost_out, int32_t* path, int path_cap, int32_t* path_len,
+                   int32_t* expand, int expand_cap, int32_t* n_expanded, int64_t* counters)
+{
+    return oracle_graph3d(0, occ, X, Y, Z, heuristic, s, g, cost_out, path, path_cap, path_len, expand, expand_cap,
+                          n_expanded, counters);
 }
 
 /* ------------------------------------------------------------------------------------ */
@@ -611,7 +639,7 @@ ddone:
 /* Batch of 2D A* queries on one grid, OpenMP over queries (the CPU baseline of bench.py).
  * path: [nq][path_cap] goal->start cells; counters [nq][4] (push, pop, expansions, max heap).
  * nthreads <= 0: OpenMP default.  Returns the number of queries with status 0. */
-int oracle_astar2d_batch(const uint8_t* occ, int W, int H, int heuristic, const int32_t* starts,
+int oracle_graph2d_batch(int algo, const uint8_t* occ, int W, int H, int heuristic, const int32_t* starts,
                          const int32_t* goals, int nq, double* cost, int32_t* path, int path_cap,
                          int32_t* path_len, int32_t* n_expanded, int64_t* counters, int32_t* status,
                          int nthreads)
@@ -620,12 +648,21 @@ int oracle_astar2d_batch(const uint8_t* occ, int W, int H, int heuristic, const 
     if (nthreads <= 0) nthreads = omp_get_max_threads();
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) reduction(+ : found)
     for (int q = 0; q < nq; q++) {
-        status[q] = oracle_astar2d(occ, W, H, heuristic, starts[2 * q], starts[2 * q + 1], goals[2 * q],
+        status[q] = oracle_graph2d(algo, occ, W, H, heuristic, starts[2 * q], starts[2 * q + 1], goals[2 * q],
                                    goals[2 * q + 1], &cost[q], path + (int64_t)q * path_cap, path_cap,
                                    &path_len[q], NULL, 0, &n_expanded[q], counters ? counters + 4 * (int64_t)q : NULL);
         found += status[q] == 0;
     }
     return found;
+}
+
+int oracle_astar2d_batch(const uint8_t* occ, int W, int H, int heuristic, const int32_t* starts,
+                         const int32_t* goals, int nq, double* cost, int32_t* path, int path_cap,
+                         int32_t* path_len, int32_t* n_expanded, int64_t* counters, int32_t* status,
+                         int nthreads)
+{
+    return oracle_graph2d_batch(0, occ, W, H, heuristic, starts, goals, nq, cost, path, path_cap, path_len, n_expanded,
+                                counters, status, nthreads);
 }
 
 /* ==================================================================================== */
@@ -1485,7 +1522,7 @@ int oracle_rrt_batch(int star, const double* rect, int nr, const double* circ, i
 
 /* OpenMP over independent AStar3D queries with per-query occupancy occ [nq][X*Y*Z] (bench
  * cpu_baseline of config C5).  cost [nq]; status [nq]. */
-int oracle_astar3d_batch(const uint8_t* occ, int X, int Y, int Z, int heuristic, const int32_t* s,
+int oracle_graph3d_batch(int algo, const uint8_t* occ, int X, int Y, int Z, int heuristic, const int32_t* s,
                          const int32_t* g, int nq, double* cost, int32_t* status, int nthreads)
 {
     if (nthreads <= 0) nthreads = omp_get_max_threads();
@@ -1498,11 +1535,17 @@ int oracle_astar3d_batch(const uint8_t* occ, int X, int Y, int Z, int heuristic,
         int64_t ctr[4];
 #pragma omp for schedule(dynamic, 4)
         for (int q = 0; q < nq; q++) {
-            status[q] = oracle_astar3d(occ + (size_t)q * ncell, X, Y, Z, heuristic, s + 3 * q, g + 3 * q, cost + q, path,
+            status[q] = oracle_graph3d(algo, occ + (size_t)q * ncell, X, Y, Z, heuristic, s + 3 * q, g + 3 * q, cost + q, path,
                                        (int)(ncell + 1), &plen, NULL, 0, &nexp, ctr);
             found += status[q] == 0;
         }
         free(path);
     }
     return found;
+}
+
+int oracle_astar3d_batch(const uint8_t* occ, int X, int Y, int Z, int heuristic, const int32_t* s,
+                         const int32_t* g, int nq, double* cost, int32_t* status, int nthreads)
+{
+    return oracle_graph3d_batch(0, occ, X, Y, Z, heuristic, s, g, nq, cost, status, nthreads);
 }

@@ -4,7 +4,7 @@ Run in the build container only (the reference never travels to the GPU box):
 
     PYTHONDONTWRITEBYTECODE=1 MPLBACKEND=Agg python tests/golden/make_golden.py [section ...]
 
-Sections: astar_readme astar_small astar_1024 dstar astar3d rrt dwa lqr mpc hypot
+Sections: astar_readme astar_small astar_1024 dstar astar3d graph2d graph3d rrt dwa lqr mpc hypot
 Outputs are small fixtures (inputs + expected outputs) under tests/golden/.  The reference is
 imported with stubs for the modules absent from this image (osqp, pyvista), per SURVEY.md §8(c).
 """
@@ -505,8 +505,120 @@ def sec_rrt():
     print("rrt", [(c[0], c[1], c[2], r["found"], len(r["tree"]), round(r["cost"], 6)) for c, r in zip(cases, res)])
 
 
+# ----------------------------------------------------------------------------------------------
+# Dijkstra / GBFS (2D: dijkstra.py, gbfs.py; 3D: dijkstra3d.py, gbfs3d.py) -- SURVEY.md §8(f) rank 1
+def run_graph2d(args):
+    occ, start, goal, heur, algo = args
+    pmp = import_reference()
+    W, H = occ.shape
+    env = pmp.Grid(W, H)
+    env.update(obstacles_of(occ))
+    cls = dict(dijkstra=pmp.Dijkstra, gbfs=pmp.GBFS)[algo]
+    p = cls(tuple(start), tuple(goal), env, heur)
+    cost, path, expand = p.plan()
+    close_figs()
+    return dict(found=bool(path), cost=float(cost) if path else float("nan"), path=[x * H + y for (x, y) in path],
+                expand=[n.current[0] * H + n.current[1] for n in expand])
+
+
+def sec_graph2d(n=120):
+    from python_motion_planning_amd import workloads as wl
+
+    rng = np.random.default_rng(2468)
+    cases = []
+    occ = wl.readme_grid()
+    for algo in ("dijkstra", "gbfs"):
+        for heur in ("euclidean", "manhattan"):
+            cases.append((occ, (5, 5), (45, 25), heur, algo))
+    for i in range(n):
+        W = int(rng.integers(8, 81))
+        H = int(rng.integers(8, 81))
+        dens = float(rng.uniform(0.0, 0.35))
+        occ = (rng.random((W, H)) < dens).astype(np.uint8)
+        occ[:, 0] = occ[:, H - 1] = 1
+        occ[0, :] = occ[W - 1, :] = 1
+        free = np.argwhere(occ == 0)
+        if len(free) < 2:
+            occ[1, 1] = occ[W - 2, H - 2] = 0
+            free = np.argwhere(occ == 0)
+        s = free[rng.integers(len(free))]
+        g = free[rng.integers(len(free))]
+        if i % 17 == 5:
+            g = s
+        heur = "manhattan" if i % 4 == 3 else "euclidean"
+        cases.append((occ, tuple(int(v) for v in s), tuple(int(v) for v in g), heur, "gbfs" if i % 2 else "dijkstra"))
+    with Pool(8) as pool:
+        res = pool.map(run_graph2d, cases, chunksize=4)
+    dims = np.array([c[0].shape for c in cases], np.int32)
+    occ_flat, occ_off = ragged([np.packbits(c[0].ravel()) for c in cases], np.uint8)
+    path_flat, path_off = ragged([r["path"] for r in res])
+    exp_flat, exp_off = ragged([r["expand"] for r in res])
+    np.savez_compressed(
+        os.path.join(HERE, "graph2d_small.npz"),
+        dims=dims, occ_bits=occ_flat, occ_off=occ_off,
+        start=np.array([c[1] for c in cases], np.int32), goal=np.array([c[2] for c in cases], np.int32),
+        manhattan=np.array([c[3] == "manhattan" for c in cases]), algo=np.array([c[4] for c in cases]),
+        found=np.array([r["found"] for r in res]), cost=np.array([r["cost"] for r in res], np.float64),
+        path=path_flat, path_off=path_off, expand=exp_flat, expand_off=exp_off)
+    print("graph2d", sum(r["found"] for r in res), "found of", len(cases), "readme costs",
+          [r["cost"] for r in res[:4]])
+
+
+def run_graph3d(args):
+    occ, start, goal, algo = args
+    pmp = import_reference()
+    X, Y, Z = occ.shape
+    env = pmp.Grid3D(X, Y, Z)
+    env.update({(int(a), int(b), int(c)) for a, b, c in np.argwhere(occ)})
+    cls = dict(dijkstra=pmp.Dijkstra3D, gbfs=pmp.GBFS3D)[algo]
+    p = cls(tuple(start), tuple(goal), env)
+    cost, path, expand = p.plan()
+    close_figs()
+    enc = lambda t: (t[0] * Y + t[1]) * Z + t[2]  # noqa: E731
+    return dict(cost=float(cost), path=[enc(t) for t in path], expand=[enc(n.current) for n in expand])
+
+
+def sec_graph3d():
+    from python_motion_planning_amd import workloads as wl
+
+    # (a) the reference's published CSV rows for Dijkstra3D / GBFS3D (every 10th row = distinct seeds)
+    rows = []
+    with open(os.path.join(REF, "3d_pathfinding_results.csv"), newline="") as f:
+        rd = csv.reader(f)
+        next(rd)
+        for k, r in enumerate(rd):
+            if r[1] in ("dijkstra", "gbfs") and k % 10 == 0:
+                rows.append(dict(algo=r[1], scenario=r[0], cost=r[3], visited=int(r[4]),
+                                 start=list(eval(r[5])), goal=list(eval(r[6])), seed=int(r[7])))  # noqa: S307
+    with open(os.path.join(HERE, "graph3d_csv.json"), "w") as f:
+        json.dump(rows, f)
+    # (b) full reference runs (path + expand order): every scenario, both planners
+    cases = []
+    for algo in ("dijkstra", "gbfs"):
+        for name in wl.SCENARIOS_3D:
+            for seed in range(3, 100, 16):
+                s, gq = wl.bench3d_query(seed, 21, 15, 11)
+                o = wl.SCENARIOS_3D[name](21, 15, 11)
+                wl.carve_safety_bubble(o, s, 2)
+                wl.carve_safety_bubble(o, gq, 2)
+                cases.append((o, s, gq, algo))
+    with Pool(8) as pool:
+        res = pool.map(run_graph3d, cases)
+    dims = np.array([c[0].shape for c in cases], np.int32)
+    occ_flat, occ_off = ragged([np.packbits(c[0].ravel()) for c in cases], np.uint8)
+    path_flat, path_off = ragged([r["path"] for r in res])
+    exp_flat, exp_off = ragged([r["expand"] for r in res])
+    np.savez_compressed(
+        os.path.join(HERE, "graph3d_runs.npz"), dims=dims, occ_bits=occ_flat, occ_off=occ_off,
+        start=np.array([c[1] for c in cases], np.int32), goal=np.array([c[2] for c in cases], np.int32),
+        algo=np.array([c[3] for c in cases]), cost=np.array([r["cost"] for r in res]), path=path_flat,
+        path_off=path_off, expand=exp_flat, expand_off=exp_off)
+    print("graph3d csv rows", len(rows), "runs", len(res))
+
+
 SECTIONS = dict(rrt=sec_rrt, mpc=sec_mpc, dwa=sec_dwa, local_plans=sec_local_plans, lqr=sec_lqr, astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
-                dstar=sec_dstar, astar3d=sec_astar3d)
+                dstar=sec_dstar, astar3d=sec_astar3d,
+                graph2d=sec_graph2d, graph3d=sec_graph3d)
 
 if __name__ == "__main__":
     want = sys.argv[1:] or list(SECTIONS)
