@@ -71,6 +71,21 @@ int pmp_astar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int 
                       int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded,
                       uint32_t* expand, int expand_cap, int64_t* counters, int32_t* status);
 
+/* Planners that share the AStar loop (2D: a_star.py:39-83; 3D: a_star3d.py:33-78). */
+enum { PMP_ALGO_ASTAR = 0, PMP_ALGO_DIJKSTRA = 1, PMP_ALGO_GBFS = 2 };
+
+/*
+ * Batched 2D AStar / Dijkstra / GBFS.  algo = PMP_ALGO_ASTAR is pmp_astar2d_batch;
+ * PMP_ALGO_DIJKSTRA replaces Dijkstra.plan (global_planner/graph_search/dijkstra.py:36-85: node_n.h
+ * = 0, so `heuristic` is unused); PMP_ALGO_GBFS replaces GBFS.plan (gbfs.py:36-86: node_n.g = 0,
+ * ordered by h).  Same loop, CPython heap ties, goal -> start path and arguments as
+ * pmp_astar2d_batch; cost is extractPath's (a_star.py:98-117) for all three.
+ */
+int pmp_graph2d_batch(pmp_ctx* ctx, void* stream, int algo, const uint32_t* occ_bits, int W, int H, int heuristic,
+                      const int32_t* start_xy, const int32_t* goal_xy, int nq, double* cost,
+                      int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded,
+                      uint32_t* expand, int expand_cap, int64_t* counters, int32_t* status);
+
 /*
  * Batched 3D A*.  Replaces AStar3D.plan (global_planner/graph_search/a_star3d.py:33-106) with
  * GraphSearcher3D.h / isCollision (graph_search_3d.py:30-107) over Grid3D's 26 motions
@@ -84,6 +99,19 @@ int pmp_astar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int 
  */
 int pmp_astar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int per_query, int X, int Y, int Z,
                       int heuristic, const int32_t* start_xyz, const int32_t* goal_xyz, int nq, double* cost,
+                      int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded, uint32_t* expand,
+                      int expand_cap, int64_t* counters, int32_t* status);
+
+/*
+ * Batched 3D AStar3D / Dijkstra3D / GBFS3D.  algo = PMP_ALGO_ASTAR is pmp_astar3d_batch;
+ * PMP_ALGO_DIJKSTRA replaces Dijkstra3D.plan (global_planner/graph_search/dijkstra3d.py:39-87: key
+ * (g, 0.0, counter), `heuristic` unused; its getNeighbor (:89-126) equals isCollision plus an
+ * in-bounds test, and cells outside the grid are blocked here); PMP_ALGO_GBFS replaces
+ * GBFS3D.plan (gbfs3d.py:34-82: key (h, counter), CLOSED membership tests).  Same arguments as
+ * pmp_astar3d_batch; cost is extractPath's (dist along the path) for all three.
+ */
+int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uint32_t* occ_bits, int per_query, int X, int Y,
+                      int Z, int heuristic, const int32_t* start_xyz, const int32_t* goal_xyz, int nq, double* cost,
                       int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded, uint32_t* expand,
                       int expand_cap, int64_t* counters, int32_t* status);
 

@@ -23,6 +23,10 @@ SIGNATURES = {
     "pmp_version": (ctypes.c_char_p, []),
     "pmp_astar2d_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _i,
                                _vp, _vp]),
+    "pmp_graph2d_batch": (_i, [_vp, _vp, _i, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _i,
+                               _vp, _vp]),
+    "pmp_graph3d_batch": (_i, [_vp, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp,
+                               _i, _vp, _vp]),
     "pmp_astar2d_reserve": (_i, [_vp, _i, _i, _i, _i]),
     "pmp_set_timing": (_i, [_vp, _vp]),
     "pmp_wall_clock_khz": (_i, [_vp, _vp]),
@@ -118,6 +122,11 @@ class PMPError(RuntimeError):
 _lib = None
 _lock = threading.Lock()
 _ctx = {}
+
+
+# planners sharing the AStar loop (include/pmp.h PMP_ALGO_*)
+ALGO_ASTAR, ALGO_DIJKSTRA, ALGO_GBFS = 0, 1, 2
+ALGOS = {"astar": ALGO_ASTAR, "dijkstra": ALGO_DIJKSTRA, "gbfs": ALGO_GBFS}
 
 
 def load_library(path: str = LIB_PATH):

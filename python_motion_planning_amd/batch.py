@@ -28,8 +28,9 @@ def occ_bits_device(occ, torch=None):
 
 def astar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: int | None = None,
                   expand_cap: int = 0, counters: bool = False, occ_bits=None, reserve_slots: int | None = None,
-                  heap_cap: int = 0, retry_overflow: bool = True):
-    """Batched AStar.plan (a_star.py:39-83).
+                  heap_cap: int = 0, retry_overflow: bool = True, algo: str = "astar"):
+    """Batched AStar.plan (a_star.py:39-83); algo "dijkstra" / "gbfs" run Dijkstra.plan
+    (dijkstra.py:36-85) / GBFS.plan (gbfs.py:36-86) on the same kernel (pmp_graph2d_batch).
 
     occ: numpy uint8 [W, H] (or pass occ=(W, H) with a prebuilt `occ_bits` device tensor).
     starts, goals: [nq, 2] int (numpy or device tensors).
@@ -64,12 +65,12 @@ def astar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: in
     out["counters"] = torch.empty((nq, 4), dtype=torch.int64, device="cuda") if counters else None
     if reserve_slots:
         _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, int(reserve_slots), int(heap_cap)), "pmp_astar2d_reserve")
-    rc = L.pmp_astar2d_batch(ctx, _lib.stream_ptr(), occ_bits.data_ptr(), W, H,
+    rc = L.pmp_graph2d_batch(ctx, _lib.stream_ptr(), _lib.ALGOS[algo], occ_bits.data_ptr(), W, H,
                              1 if heuristic == "manhattan" else 0, s.data_ptr(), g.data_ptr(), nq,
                              out["cost"].data_ptr(), out["path_len"].data_ptr(), out["path"].data_ptr(), path_cap,
                              out["n_expanded"].data_ptr(), _lib.ptr(out["expand"]), int(expand_cap),
                              _lib.ptr(out["counters"]), out["status"].data_ptr())
-    _lib.check(ctx, rc, "pmp_astar2d_batch")
+    _lib.check(ctx, rc, "pmp_graph2d_batch")
     if retry_overflow:
         redo = torch.nonzero(out["status"] == _lib.STATUS_CAP_OVERFLOW).flatten()
         if redo.numel():
@@ -77,7 +78,7 @@ def astar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: in
             workers = max(1, min(int(redo.numel()), 256))
             _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, workers, full), "pmp_astar2d_reserve")
             r = astar2d_batch((W, H), s[redo], g[redo], heuristic, path_cap, expand_cap, counters, occ_bits,
-                              retry_overflow=False)
+                              retry_overflow=False, algo=algo)
             for k in ("cost", "path_len", "path", "n_expanded", "status", "expand", "counters"):
                 if out[k] is not None:
                     out[k][redo] = r[k]
@@ -302,8 +303,9 @@ def rrt_batch(env, starts, goals, rnd, sample_num: int, star: bool = True, max_d
 
 
 def astar3d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: int | None = None,
-                  expand_cap: int = 0, counters: bool = False):
-    """Batched AStar3D.plan (a_star3d.py:33-106).
+                  expand_cap: int = 0, counters: bool = False, algo: str = "astar"):
+    """Batched AStar3D.plan (a_star3d.py:33-106); algo "dijkstra" / "gbfs" run Dijkstra3D.plan
+    (dijkstra3d.py:39-87) / GBFS3D.plan (gbfs3d.py:34-82) on the same kernel (pmp_graph3d_batch).
 
     occ: uint8 [X, Y, Z] shared grid or [nq, X, Y, Z] per-query grids (numpy).
     Returns dict of device tensors: cost (inf if unreachable), path_len, path [nq, path_cap]
@@ -332,11 +334,11 @@ def astar3d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: in
                status=torch.empty(nq, dtype=torch.int32, device="cuda"))
     out["expand"] = torch.empty((nq, expand_cap), dtype=torch.int32, device="cuda") if expand_cap else None
     out["counters"] = torch.empty((nq, 4), dtype=torch.int64, device="cuda") if counters else None
-    rc = L.pmp_astar3d_batch(ctx, _lib.stream_ptr(), occ_bits.data_ptr(), 1 if per_query else 0, X, Y, Z,
-                             1 if heuristic == "manhattan" else 0, s.data_ptr(), g.data_ptr(), nq,
+    rc = L.pmp_graph3d_batch(ctx, _lib.stream_ptr(), _lib.ALGOS[algo], occ_bits.data_ptr(), 1 if per_query else 0,
+                             X, Y, Z, 1 if heuristic == "manhattan" else 0, s.data_ptr(), g.data_ptr(), nq,
                              out["cost"].data_ptr(), out["path_len"].data_ptr(), out["path"].data_ptr(), path_cap,
                              out["n_expanded"].data_ptr(), _lib.ptr(out["expand"]), int(expand_cap),
                              _lib.ptr(out["counters"]), out["status"].data_ptr())
-    _lib.check(ctx, rc, "pmp_astar3d_batch")
+    _lib.check(ctx, rc, "pmp_graph3d_batch")
     out["dims"] = (X, Y, Z)
     return out

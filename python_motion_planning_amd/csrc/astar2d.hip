@@ -55,11 +55,13 @@ __device__ __forceinline__ uint32_t pack_cm(int dx, int dy, int dir)
 __device__ __forceinline__ int cm_dx(uint32_t cm) { return (int)cm >> 18; }
 __device__ __forceinline__ int cm_dy(uint32_t cm) { return (int)(cm << 14) >> 18; }
 
-// HEUR: 0 euclidean, 1 manhattan (GraphSearcher.h, graph_search.py:41-44) -- a template parameter,
-// so key computations carry no runtime branch.  The order key of h.
+// HEUR: 0 euclidean, 1 manhattan (GraphSearcher.h, graph_search.py:41-44), 2 zero (Dijkstra's
+// node_n.h = 0, dijkstra.py:74) -- a template parameter, so key computations carry no runtime
+// branch.  The order key of h.
 template <int HEUR>
 __device__ __forceinline__ uint32_t hkey(uint32_t cm)
 {
+    if (HEUR == 2) return 0u;
     const int dx = cm_dx(cm), dy = cm_dy(cm);
     if (HEUR == 1) return (uint32_t)(abs(dx) + abs(dy));
     return (uint32_t)(__mul24(dx, dx) + __mul24(dy, dy));
@@ -67,7 +69,7 @@ __device__ __forceinline__ uint32_t hkey(uint32_t cm)
 template <int HEUR>
 __device__ __forceinline__ double h_of_key(uint32_t hk)
 {
-    return HEUR == 1 ? (double)hk : __dsqrt_rn((double)hk);
+    return HEUR == 2 ? 0.0 : (HEUR == 1 ? (double)hk : __dsqrt_rn((double)hk));
 }
 
 // Node.__lt__ (node.py:51-54) -- evaluated without short-circuit branches
@@ -453,7 +455,8 @@ __device__ __forceinline__ void push_any(const Heap& h, int n, double itf, uint3
 // 4-bit cell state: word i >> 3, nibble i & 7
 __device__ __forceinline__ uint32_t cst_at(const uint32_t* cst, uint32_t i) { return (cst[i >> 3] >> ((i & 7) * 4)) & 15u; }
 
-template <int HEUR>
+// GZERO: GBFS (gbfs.py:73-75) -- every pushed node gets g = 0, so f = h and G is never needed.
+template <int HEUR, bool GZERO>
 __global__ __launch_bounds__(64) void astar2d_kernel(
     const uint32_t* __restrict__ occ, int W, int H, const int32_t* __restrict__ start_xy,
     const int32_t* __restrict__ goal_xy, const int32_t* __restrict__ order, int nq, double* __restrict__ cost_out,
@@ -490,7 +493,7 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
     // (graph_search.py:66-87: both endpoints; for a diagonal both corner cells)
     const int mo = lane & 7;
     const int mx = mot_x(mo), my = mot_y(mo);
-    const double mcost = (mo & 1) ? kSqrt2 : 1.0;
+    const double mcost = GZERO ? 0.0 : ((mo & 1) ? kSqrt2 : 1.0);
     const int par_off = mx * H + my;  // lane d: linear offset of motion d (parent = cell - offset)
     uint32_t need = 16u | (1u << ((mx + 1) * 3 + (my + 1)));
     if (mo & 1) need |= (1u << (3 + (my + 1))) | (1u << ((mx + 1) * 3 + 1));
@@ -576,7 +579,7 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 blk_word = *ptr;
             }
             double gpar = 0.0;  // G[parent] (the parent closed earlier); the start has g = 0
-            if (ndir < 8) {
+            if (!GZERO && ndir < 8) {
                 const uint32_t plin = nlin - (uint32_t)rl_u32((uint32_t)par_off, ndir);
                 if (lane == 18) gpar = G[plin];
             }
@@ -606,9 +609,9 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
 
             // CLOSED[node.current] = node (a_star.py:82).  The node's state word was loaded by lane 13
             // and only this wave writes it: store it back now (fire-and-forget, off the critical path).
-            const double gnode = ndir == 8 ? 0.0 : rl_f64(gpar, 18) + ((ndir & 1) ? kSqrt2 : 1.0);
+            const double gnode = (GZERO || ndir == 8) ? 0.0 : rl_f64(gpar, 18) + ((ndir & 1) ? kSqrt2 : 1.0);
             if (lane == 13) cst[nlin >> 3] = blk_word | ((uint32_t)(ndir + 1) << blk_sh);
-            if (lane == 14) G[nlin] = gnode;
+            if (!GZERO && lane == 14) G[nlin] = gnode;
             if (lane == 0 && expand_out && nexp < expand_cap)
                 expand_out[(size_t)q * expand_cap + nexp] = nlin | ((uint32_t)ndir << 28);
             nexp++;
@@ -789,13 +792,15 @@ extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int workers, int 
     return PMP_OK;
 }
 
-extern "C" int pmp_astar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H,
+extern "C" int pmp_graph2d_batch(pmp_ctx* ctx, void* stream, int algo, const uint32_t* occ_bits, int W, int H,
                                  int heuristic, const int32_t* start_xy, const int32_t* goal_xy, int nq,
                                  double* cost, int32_t* path_len, uint32_t* path, int path_cap,
                                  int32_t* n_expanded, uint32_t* expand, int expand_cap, int64_t* counters,
                                  int32_t* status)
 {
     if (!ctx) return PMP_EINVAL;
+    if (algo < PMP_ALGO_ASTAR || algo > PMP_ALGO_GBFS)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_graph2d_batch: algo must be 0 (AStar), 1 (Dijkstra) or 2 (GBFS)");
     if (W < 1 || H < 1 || W > kMaxDim || H > kMaxDim)
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_batch: W and H must be in [1, 8192]");
     if (heuristic != 0 && heuristic != 1) return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_batch: heuristic must be 0 or 1");
@@ -832,11 +837,23 @@ extern "C" int pmp_astar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
         hipLaunchKernelGGL(lpt_scan, dim3(1), dim3(64), 0, s, nb, hist);
         hipLaunchKernelGGL(lpt_scatter, dim3((nq + 255) / 256), dim3(256), 0, s, start_xy, goal_xy, nq, nb, hist, order);
     }
-    auto kern = heuristic == 1 ? astar2d_kernel<1> : astar2d_kernel<0>;
+    auto kern = algo == PMP_ALGO_DIJKSTRA ? astar2d_kernel<2, false>
+              : algo == PMP_ALGO_GBFS     ? (heuristic == 1 ? astar2d_kernel<1, true> : astar2d_kernel<0, true>)
+                                          : (heuristic == 1 ? astar2d_kernel<1, false> : astar2d_kernel<0, false>);
     hipLaunchKernelGGL(kern, dim3(workers), dim3(64), lds, s, occ_bits, W, H, start_xy,
                        goal_xy, (const int32_t*)order, nq, cost, path_len, path, path_cap, n_expanded, expand,
                        expand_cap, counters, status, queue, spill, ctx->astar_heap_cap, ctx->astar_lds_cap, cst, cst_words, G,
                        (uint32_t*)ctx->buf[SCR_BITS], hbits_words(ctx->astar_heap_cap), order ? ctx->astar_prio_n : 0, ctx->span);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
+}
+
+extern "C" int pmp_astar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H,
+                                 int heuristic, const int32_t* start_xy, const int32_t* goal_xy, int nq,
+                                 double* cost, int32_t* path_len, uint32_t* path, int path_cap,
+                                 int32_t* n_expanded, uint32_t* expand, int expand_cap, int64_t* counters,
+                                 int32_t* status)
+{
+    return pmp_graph2d_batch(ctx, stream, PMP_ALGO_ASTAR, occ_bits, W, H, heuristic, start_xy, goal_xy, nq, cost,
+                             path_len, path, path_cap, n_expanded, expand, expand_cap, counters, status);
 }

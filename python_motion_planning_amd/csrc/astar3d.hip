@@ -31,13 +31,16 @@ using heap16::Ent;  // g = path cost, a = push counter, b = cm; derived f = g + 
 // (f, h, counter) tuple order of a_star3d.py:40,75, with f and h rebuilt from the cell
 struct Key3 {
     int gx, gy, gz;
-    int heur;  // 0 euclidean, 1 manhattan
+    int heur;  // 0 euclidean, 1 manhattan, 2 zero (Dijkstra3D: h = 0, dijkstra3d.py:34,83)
 
     __device__ __forceinline__ void derive(Ent& e) const
     {
         const int x = (int)(e.b >> 21), y = (int)((e.b >> 13) & 255u), z = (int)((e.b >> 5) & 255u);
         const int dx = abs(gx - x), dy = abs(gy - y), dz = abs(gz - z);
-        if (heur == 1) {
+        if (heur == 2) {
+            e.hk = 0u;
+            e.f = e.g;
+        } else if (heur == 1) {
             e.hk = (uint32_t)(dx + dy + dz);
             e.f = e.g + (double)e.hk;
         } else {
@@ -78,7 +81,7 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
     int32_t* __restrict__ path_len_out, uint32_t* __restrict__ path_out, int path_cap, int32_t* __restrict__ nexp_out,
     uint32_t* __restrict__ expand_out, int expand_cap, int64_t* __restrict__ counters, int32_t* __restrict__ status_out,
     int* __restrict__ queue, uint4* __restrict__ spill_all, int heap_cap, int lds_cap, uint8_t* __restrict__ cdir_all,
-    double* __restrict__ cg_all)
+    double* __restrict__ cg_all, int gzero)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
@@ -96,7 +99,10 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
     // neighbour lane m < 26: motion m (env3d.py:56-70)
     const int mdx = lane < 26 ? c_m3[lane][0] : 0, mdy = lane < 26 ? c_m3[lane][1] : 0, mdz = lane < 26 ? c_m3[lane][2] : 0;
     const int mchg = (mdx != 0) + (mdy != 0) + (mdz != 0);
-    const double mcost = __dsqrt_rn((double)mchg);  // Planner3D.dist: math.sqrt(1|2|3)
+    // Planner3D.dist: math.sqrt(1|2|3); GBFS3D pushes every node with g = 0 (gbfs3d.py:78), so its
+    // key (h, counter) is this loop's (f, h, counter) with f = 0 + h, and `g >= closed g` is always
+    // true: the CLOSED membership tests of gbfs3d.py:55,74
+    const double mcost = gzero ? 0.0 : __dsqrt_rn((double)mchg);
 
     for (;;) {
         const int qi = next_query(queue, lane);
@@ -322,12 +328,14 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
 
 }  // namespace
 
-extern "C" int pmp_astar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int per_query, int X, int Y,
-                                 int Z, int heuristic, const int32_t* start_xyz, const int32_t* goal_xyz, int nq,
+extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uint32_t* occ_bits, int per_query, int X,
+                                 int Y, int Z, int heuristic, const int32_t* start_xyz, const int32_t* goal_xyz, int nq,
                                  double* cost, int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded,
                                  uint32_t* expand, int expand_cap, int64_t* counters, int32_t* status)
 {
     if (!ctx) return PMP_EINVAL;
+    if (algo < PMP_ALGO_ASTAR || algo > PMP_ALGO_GBFS)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_graph3d_batch: algo must be 0 (AStar3D), 1 (Dijkstra3D) or 2 (GBFS3D)");
     if (X < 1 || Y < 1 || Z < 1 || X > kMaxDim3 || Y > kMaxDim3 || Z > kMaxDim3)
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar3d_batch: X, Y, Z must be in [1, 256]");
     if (heuristic != 0 && heuristic != 1) return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar3d_batch: heuristic must be 0 or 1");
@@ -359,8 +367,18 @@ extern "C" int pmp_astar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
     auto kern = occ_lds ? astar3d_kernel<true> : astar3d_kernel<false>;
     hipLaunchKernelGGL(kern, dim3(workers), dim3(64), (size_t)lds_cap * 16 + occ_bytes, s, occ_bits, per_query, X, Y, Z,
-                       heuristic, start_xyz, goal_xyz, nq, cost, path_len, path, path_cap, n_expanded, expand, expand_cap,
-                       counters, status, queue, spill, heap_cap, lds_cap, cdir, cg);
+                       algo == PMP_ALGO_DIJKSTRA ? 2 : heuristic, start_xyz, goal_xyz, nq, cost, path_len, path, path_cap,
+                       n_expanded, expand, expand_cap, counters, status, queue, spill, heap_cap, lds_cap, cdir, cg,
+                       algo == PMP_ALGO_GBFS ? 1 : 0);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
+}
+
+extern "C" int pmp_astar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int per_query, int X, int Y,
+                                 int Z, int heuristic, const int32_t* start_xyz, const int32_t* goal_xyz, int nq,
+                                 double* cost, int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded,
+                                 uint32_t* expand, int expand_cap, int64_t* counters, int32_t* status)
+{
+    return pmp_graph3d_batch(ctx, stream, PMP_ALGO_ASTAR, occ_bits, per_query, X, Y, Z, heuristic, start_xyz, goal_xyz, nq,
+                             cost, path_len, path, path_cap, n_expanded, expand, expand_cap, counters, status);
 }

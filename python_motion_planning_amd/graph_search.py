@@ -48,6 +48,8 @@ class GraphSearcher(Planner):
 class AStar(GraphSearcher):
     """A* (a_star.py:13-124) -- the OPEN/CLOSED loop runs in the gfx950 kernel astar2d.hip."""
 
+    _algo = "astar"
+
     def __str__(self) -> str:
         return "A*"
 
@@ -56,12 +58,12 @@ class AStar(GraphSearcher):
         occ = self.env.occupancy()
         W, H = occ.shape
         r = batch.astar2d_batch(occ, np.array([self.start.current]), np.array([self.goal.current]),
-                                self.heuristic_type, path_cap=W * H + 1, expand_cap=W * H)
+                                self.heuristic_type, path_cap=W * H + 1, expand_cap=W * H, algo=self._algo)
         st = int(r["status"][0])
         if st != 0:
             if st == 1:
                 return [], [], []
-            raise RuntimeError(f"A* kernel status {st}")
+            raise RuntimeError(f"{self} kernel status {st}")
         plen = int(r["path_len"][0])
         cells = r["path"][0, :plen].cpu().numpy()
         nexp = int(r["n_expanded"][0])
@@ -86,16 +88,37 @@ class AStar(GraphSearcher):
             else:
                 m = motions[d]
                 par = (cur[0] - m.x, cur[1] - m.y)
-                node = Node(cur, par, gmap[par] + m.g, self.h(Node(cur), self.goal))
+                g = 0 if self._algo == "gbfs" else gmap[par] + m.g  # gbfs.py:75: node_n.g = 0
+                h = 0 if self._algo == "dijkstra" else self.h(Node(cur), self.goal)  # dijkstra.py:74
+                node = Node(cur, par, g, h)
             gmap[cur] = node.g
             nodes.append(node)
         return nodes
 
-    @staticmethod
-    def plan_batch(occ: np.ndarray, starts, goals, heuristic_type: str = "euclidean", **kw):
+    @classmethod
+    def plan_batch(cls, occ: np.ndarray, starts, goals, heuristic_type: str = "euclidean", **kw):
         """Batched plan over one occupancy grid; returns the device-tensor dict of
         batch.astar2d_batch (cost, path_len, path goal->start, n_expanded, status)."""
-        return batch.astar2d_batch(occ, starts, goals, heuristic_type, **kw)
+        return batch.astar2d_batch(occ, starts, goals, heuristic_type, algo=cls._algo, **kw)
+
+
+class Dijkstra(AStar):
+    """Dijkstra (dijkstra.py:13-85): AStar's loop with node_n.h = 0 (:73-74), on the same kernel."""
+
+    _algo = "dijkstra"
+
+    def __str__(self) -> str:
+        return "Dijkstra"
+
+
+class GBFS(AStar):
+    """Greedy Best First Search (gbfs.py:13-86): AStar's loop with node_n.g = 0 (:73-75), so the
+    heap orders by h alone; the same kernel."""
+
+    _algo = "gbfs"
+
+    def __str__(self) -> str:
+        return "Greedy Best First Search(GBFS)"
 
 
 class DStar(GraphSearcher):
@@ -162,6 +185,8 @@ class GraphSearcher3D:
 class AStar3D(GraphSearcher3D):
     """A* for 3D grids (a_star3d.py:18-111) -- the search runs in the gfx950 kernel astar3d.hip."""
 
+    _algo = "astar"
+
     def __str__(self) -> str:
         return "A*"
 
@@ -173,7 +198,7 @@ class AStar3D(GraphSearcher3D):
         occ = self.env.occupancy()
         X, Y, Z = occ.shape
         r = batch.astar3d_batch(occ, np.array([self.start.current]), np.array([self.goal.current]),
-                                self.heuristic_type, path_cap=X * Y * Z + 1, expand_cap=X * Y * Z)
+                                self.heuristic_type, path_cap=X * Y * Z + 1, expand_cap=X * Y * Z, algo=self._algo)
         st = int(r["status"][0])
         ne = int(r["n_expanded"][0])
         ex = r["expand"][0, :ne].cpu().numpy()
@@ -181,11 +206,34 @@ class AStar3D(GraphSearcher3D):
         if st == 1:
             return float("inf"), [], expand
         if st != 0:
-            raise RuntimeError(f"AStar3D kernel status {st}")
+            raise RuntimeError(f"{self} kernel status {st}")
         cells = r["path"][0, : int(r["path_len"][0])].cpu().numpy()
         path = [(int(c) // (Y * Z), (int(c) // Z) % Y, int(c) % Z) for c in cells]
         return float(r["cost"][0]), path, expand
 
-    @staticmethod
-    def plan_batch(occ, starts, goals, heuristic_type: str = "euclidean", **kw):
-        return batch.astar3d_batch(occ, starts, goals, heuristic_type, **kw)
+    @classmethod
+    def plan_batch(cls, occ, starts, goals, heuristic_type: str = "euclidean", **kw):
+        return batch.astar3d_batch(occ, starts, goals, heuristic_type, algo=cls._algo, **kw)
+
+
+class Dijkstra3D(AStar3D):
+    """Dijkstra for 3D grids (dijkstra3d.py:18-147): key (g, 0.0, counter), start h = 0; its
+    getNeighbor (:89-126) is isCollision plus an in-bounds test.  The same kernel with h = 0."""
+
+    _algo = "dijkstra"
+
+    def __init__(self, start: tuple, goal: tuple, env) -> None:
+        super().__init__(start, goal, env, "euclidean")  # dijkstra3d.py:31 passes no heuristic
+
+    def __str__(self) -> str:
+        return "Dijkstra (3D)"
+
+
+class GBFS3D(AStar3D):
+    """Greedy Best First Search for 3D grids (gbfs3d.py:20-114): key (h, counter), CLOSED membership
+    tests.  The same kernel with every g = 0."""
+
+    _algo = "gbfs"
+
+    def __str__(self) -> str:
+        return "Greedy Best First Search (GBFS) 3D"

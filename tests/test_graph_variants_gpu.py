@@ -1,0 +1,127 @@
+"""Dijkstra / GBFS (2D: dijkstra.py, gbfs.py; 3D: dijkstra3d.py, gbfs3d.py) on the HIP kernels
+astar2d.hip / astar3d.hip (C-ABI pmp_graph2d_batch / pmp_graph3d_batch) vs the reference's own
+outputs (tests/golden/graph2d_small.npz, graph3d_csv.json, graph3d_runs.npz) and the oracle.
+
+Bar: bit-exact -- cost bits, path cells, closure (expand) order, visited counts."""
+import numpy as np
+import pytest
+
+from golden_io import grid_cases, load_json, seg
+
+pytestmark = pytest.mark.gpu
+
+
+def test_graph2d_against_reference():
+    from python_motion_planning_amd import batch
+
+    n = 0
+    for i, occ, z in grid_cases("graph2d_small.npz"):
+        W, H = occ.shape
+        heur = "manhattan" if z["manhattan"][i] else "euclidean"
+        r = batch.astar2d_batch(occ, z["start"][i][None], z["goal"][i][None], heur, path_cap=W * H + 1,
+                                expand_cap=W * H, algo=str(z["algo"][i]))
+        st = int(r["status"][0])
+        if not z["found"][i]:
+            assert st == 1, i
+            continue
+        assert st == 0, i
+        assert float(r["cost"][0]) == z["cost"][i], i
+        plen = int(r["path_len"][0])
+        assert np.array_equal(r["path"][0, :plen].cpu().numpy(), seg(z["path"], z["path_off"], i)), i
+        ne = int(r["n_expanded"][0])
+        e = (r["expand"][0, :ne].cpu().numpy().astype(np.uint32) & 0x0FFFFFFF).astype(np.int32)
+        assert np.array_equal(e, seg(z["expand"], z["expand_off"], i)), i
+        n += 1
+    assert n > 100
+
+
+def test_readme_dropin_classes():
+    import python_motion_planning_amd as pmp
+    from python_motion_planning_amd import workloads as wl
+    from oracle import oracle as O
+
+    occ = wl.readme_grid()
+    env = pmp.Grid(51, 31)
+    env.update({(int(x), int(y)) for x, y in np.argwhere(occ)})
+    for cls, algo in ((pmp.Dijkstra, "dijkstra"), (pmp.GBFS, "gbfs")):
+        for heur in ("euclidean", "manhattan"):
+            cost, path, expand = cls((5, 5), (45, 25), env, heur).plan()
+            ref = O.astar2d(occ, (5, 5), (45, 25), heur, algo=algo)
+            assert cost == ref["cost"] and path == ref["path"], (algo, heur)
+            assert [n.current[0] * 31 + n.current[1] for n in expand] == ref["expand_cells"].tolist()
+            if algo == "gbfs":
+                assert all(n.g == 0 for n in expand)
+            else:
+                assert all(n.h == 0 for n in expand)
+
+
+def test_c2_subset_against_oracle():
+    """Dijkstra / GBFS on the C2 1024x1024 grid (20 % obstacles): 24 queries each, bit-exact."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import batch, workloads as wl
+
+    occ, s, g = wl.c2_workload(4096)
+    idx = np.arange(0, 4096, 171)[:24]
+    for algo in ("dijkstra", "gbfs"):
+        r = batch.astar2d_batch(occ, s[idx], g[idx], path_cap=8192, counters=True, algo=algo)
+        ref = O.astar2d_batch(occ, s[idx], g[idx], path_cap=8192, algo=algo)
+        assert np.array_equal(r["status"].cpu().numpy(), ref["status"]), algo
+        assert np.array_equal(r["cost"].cpu().numpy(), ref["cost"]), algo
+        assert np.array_equal(r["n_expanded"].cpu().numpy(), ref["n_expanded"]), algo
+        assert np.array_equal(r["counters"].cpu().numpy(), ref["counters"]), algo
+        P = r["path"].cpu().numpy()
+        for k in range(len(idx)):
+            n = ref["path_len"][k]
+            assert np.array_equal(P[k, :n], ref["path"][k, :n]), (algo, k)
+
+
+def _csv_batch(rows):
+    from python_motion_planning_amd import workloads as wl
+
+    occ = np.zeros((len(rows), 21, 15, 11), np.uint8)
+    S = np.zeros((len(rows), 3), np.int32)
+    G = np.zeros((len(rows), 3), np.int32)
+    for i, r in enumerate(rows):
+        s, g = wl.bench3d_query(r["seed"], 21, 15, 11)
+        o = wl.SCENARIOS_3D[r["scenario"]](21, 15, 11)
+        wl.carve_safety_bubble(o, s, 2)
+        wl.carve_safety_bubble(o, g, 2)
+        occ[i], S[i], G[i] = o, s, g
+    return occ, S, G
+
+
+def test_graph3d_published_csv_rows():
+    """The 1000 Dijkstra3D / GBFS3D rows of the reference's 3d_pathfinding_results.csv."""
+    from python_motion_planning_amd import batch
+
+    rows = load_json("graph3d_csv.json")
+    for algo in ("dijkstra", "gbfs"):
+        sub = [r for r in rows if r["algo"] == algo]
+        occ, S, G = _csv_batch(sub)
+        out = batch.astar3d_batch(occ, S, G, algo=algo)
+        cost = out["cost"].cpu().numpy()
+        ne = out["n_expanded"].cpu().numpy()
+        for i, r in enumerate(sub):
+            assert repr(float(cost[i])) == r["cost"], (algo, i, r)
+            assert ne[i] == r["visited"], (algo, i, r)
+
+
+def test_graph3d_full_runs_and_dropin():
+    import python_motion_planning_amd as pmp
+    from python_motion_planning_amd import batch
+
+    for i, occ, z in grid_cases("graph3d_runs.npz"):
+        X, Y, Z = occ.shape
+        algo = str(z["algo"][i])
+        out = batch.astar3d_batch(occ, z["start"][i][None], z["goal"][i][None], expand_cap=X * Y * Z, algo=algo)
+        assert float(out["cost"][0]) == z["cost"][i], (algo, i)
+        pl = int(out["path_len"][0])
+        assert np.array_equal(out["path"][0, :pl].cpu().numpy(), seg(z["path"], z["path_off"], i)), (algo, i)
+        ne = int(out["n_expanded"][0])
+        assert np.array_equal(out["expand"][0, :ne].cpu().numpy(), seg(z["expand"], z["expand_off"], i)), (algo, i)
+        if i % 9 == 0:  # the drop-in classes on the same case
+            env = pmp.Grid3D(X, Y, Z)
+            env.update({(int(a), int(b), int(c)) for a, b, c in np.argwhere(occ)})
+            cls = pmp.Dijkstra3D if algo == "dijkstra" else pmp.GBFS3D
+            cost, path, expand = cls(tuple(z["start"][i]), tuple(z["goal"][i]), env).plan()
+            assert cost == z["cost"][i] and len(expand) == ne

@@ -52,6 +52,14 @@ def test_out_of_scope_names_raise():
     import python_motion_planning_amd as pmp
 
     with pytest.raises(NotImplementedError):
-        pmp.SearchFactory()("dijkstra", start=(1, 1), goal=(2, 2), env=None)
+        pmp.SearchFactory()("jps", start=(1, 1), goal=(2, 2), env=None)
     with pytest.raises(NotImplementedError):
         pmp.ControlFactory()("pid", start=(1, 1, 0), goal=(2, 2, 0), env=None)
+
+
+def test_factory_names_dijkstra_gbfs():
+    import python_motion_planning_amd as pmp
+
+    env = pmp.Grid(51, 31)
+    assert type(pmp.SearchFactory()("dijkstra", start=(5, 5), goal=(45, 25), env=env)).__name__ == "Dijkstra"
+    assert type(pmp.SearchFactory()("gbfs", start=(5, 5), goal=(45, 25), env=env)).__name__ == "GBFS"
