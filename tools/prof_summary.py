@@ -17,7 +17,7 @@ KERNELS = {  # short name -> regex on the demangled kernel name
     "astar2d_kernel": r"astar2d_kernel<",
     "dwa_kernel": r"dwa_kernel\(",
     "rrt_kernel": r"rrt_kernel<",
-    "astar3d_kernel": r"astar3d_kernel\(",
+    "astar3d_kernel": r"astar3d_kernel[<(]",
     "dstar_kernel": r"dstar_kernel\(",
     "track_kernel_lqr": r"track_kernel<0>",
     "track_kernel_mpc": r"track_kernel<1>",
