@@ -510,3 +510,34 @@ def astar3d_batch(occ, starts, goals, heuristic: str = "euclidean", nthreads: in
     L.oracle_graph3d_batch(ALGOS[algo], _p(occ, _u8p), X, Y, Z, 1 if heuristic == "manhattan" else 0, _p(s, _i32p),
                            _p(g, _i32p), nq, _p(cost, _dp), _p(st, _i32p), nthreads)
     return cost, st
+
+
+def theta3d(occ: np.ndarray, start, goal, lazy: bool = False, heuristic: str = "euclidean",
+            with_expand: bool = True):
+    """Restatement of ThetaStar3D.plan (theta_star3d.py:38-94) or, with lazy, LazyThetaStar3D.plan
+    (lazy_theta_star3d.py:41-112).  occ: uint8 [X, Y, Z].  Path start -> goal."""
+    L = lib()
+    if not getattr(L, "_th3", False):
+        L.oracle_theta3d.restype = ctypes.c_int
+        L.oracle_theta3d.argtypes = [ctypes.c_int, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     _i32p, _i32p, _dp, _i32p, ctypes.c_int, _i32p, _i32p, ctypes.c_int, _i32p, _i64p]
+        L._th3 = True
+    occ = np.ascontiguousarray(occ, dtype=np.uint8)
+    X, Y, Z = occ.shape
+    n = X * Y * Z
+    path = np.zeros(n + 1, np.int32)
+    expand = np.zeros(n, np.int32)
+    s = np.asarray(start, np.int32)
+    g = np.asarray(goal, np.int32)
+    cost = ctypes.c_double(0)
+    plen = ctypes.c_int32(0)
+    nexp = ctypes.c_int32(0)
+    ctr = np.zeros(4, np.int64)
+    st = L.oracle_theta3d(int(bool(lazy)), _p(occ, _u8p), X, Y, Z, 1 if heuristic == "manhattan" else 0,
+                          _p(s, _i32p), _p(g, _i32p), ctypes.byref(cost), _p(path, _i32p), n + 1, ctypes.byref(plen),
+                          _p(expand, _i32p) if with_expand else None, n, ctypes.byref(nexp), _p(ctr, _i64p))
+    out = dict(status=st, cost=cost.value, n_expanded=nexp.value, path_cells=path[: plen.value].copy(),
+               n_push=int(ctr[0]), n_pop=int(ctr[1]), n_iter=int(ctr[2]), max_heap=int(ctr[3]))
+    if with_expand:
+        out["expand_cells"] = expand[: nexp.value].copy()
+    return out

@@ -469,6 +469,185 @@ int oracle_astar3d(const uint8_t* occ, int X, int Y, int Z, int heuristic, const
 }
 
 /* ------------------------------------------------------------------------------------ */
+/* ThetaStar3D / LazyThetaStar3D (global_planner/graph_search/theta_star3d.py:38-232,      */
+/* lazy_theta_star3d.py:41-252): AStar3D's (f, h, counter) heap and reopening rules, with  */
+/* any-voxel parents.                                                                      */
+/* ------------------------------------------------------------------------------------ */
+
+/* lineOfSight (theta_star3d.py:139-213 == lazy_theta_star3d.py:158-233): integer Bresenham from a
+ * to b along the dominant axis; both endpoints must be free; every voxel after a (b included) must
+ * be in the grid and free. */
+static int los3(const uint8_t* occ, int X, int Y, int Z, int x0, int y0, int z0, int x1, int y1, int z1)
+{
+    if (occ3(occ, X, Y, Z, x0, y0, z0) || occ3(occ, X, Y, Z, x1, y1, z1)) return 0;
+    const int dx = abs(x1 - x0), dy = abs(y1 - y0), dz = abs(z1 - z0);
+    const int sx = x1 >= x0 ? 1 : -1, sy = y1 >= y0 ? 1 : -1, sz = z1 >= z0 ? 1 : -1;
+    int x = x0, y = y0, z = z0;
+    if (dx >= dy && dx >= dz) {
+        int ey = dx / 2, ez = dx / 2;
+        while (x != x1) {
+            x += sx; ey -= dy; ez -= dz;
+            if (ey < 0) { y += sy; ey += dx; }
+            if (ez < 0) { z += sz; ez += dx; }
+            if (occ3(occ, X, Y, Z, x, y, z)) return 0;
+        }
+        return 1;
+    }
+    if (dy >= dx && dy >= dz) {
+        int ex = dy / 2, ez = dy / 2;
+        while (y != y1) {
+            y += sy; ex -= dx; ez -= dz;
+            if (ex < 0) { x += sx; ex += dy; }
+            if (ez < 0) { z += sz; ez += dy; }
+            if (occ3(occ, X, Y, Z, x, y, z)) return 0;
+        }
+        return 1;
+    }
+    int ex = dz / 2, ey = dz / 2;
+    while (z != z1) {
+        z += sz; ex -= dx; ey -= dy;
+        if (ex < 0) { x += sx; ex += dz; }
+        if (ey < 0) { y += sy; ey += dz; }
+        if (occ3(occ, X, Y, Z, x, y, z)) return 0;
+    }
+    return 1;
+}
+
+/* Planner3D.dist (utils/planner/planner3d.py:22-27): math.sqrt of the integer sum of squares */
+static inline double dist3c(int64_t YZ, int Z, int32_t a, int32_t b)
+{
+    const int dx = (int)(a / YZ) - (int)(b / YZ), dy = (int)((a / Z) % (YZ / Z)) - (int)((b / Z) % (YZ / Z)),
+              dz = (int)(a % Z) - (int)(b % Z);
+    return sqrt((double)(dx * dx + dy * dy + dz * dz));
+}
+
+int oracle_theta3d(int lazy, const uint8_t* occ, int X, int Y, int Z, int heuristic, const int32_t* s,
+                   const int32_t* g, double* cost_out, int32_t* path, int path_cap, int32_t* path_len,
+                   int32_t* expand, int expand_cap, int32_t* n_expanded, int64_t* counters)
+{
+    const int64_t ncell = (int64_t)X * Y * Z, YZ = (int64_t)Y * Z;
+    double* cg = (double*)malloc(sizeof(double) * (size_t)ncell);
+    int32_t* cparent = (int32_t*)malloc(sizeof(int32_t) * (size_t)ncell);
+    uint8_t* closed = (uint8_t*)calloc((size_t)ncell, 1);
+    int64_t cap = 1024, n = 0, npush = 0, npop = 0, nexp = 0, seq = 0, nclose = 0, maxn = 1;
+    a3node_t* heap = (a3node_t*)malloc(sizeof(a3node_t) * (size_t)cap);
+    int status = 1;
+    *path_len = 0;
+    *cost_out = INFINITY;
+    if (!cg || !cparent || !closed || !heap) { free(cg); free(cparent); free(closed); free(heap); return 3; }
+    const int gx = g[0], gy = g[1], gz = g[2];
+    const int32_t start = (s[0] * Y + s[1]) * Z + s[2], goal = (gx * Y + gy) * Z + gz;
+#define H3T(x, y, z)                                                                                    \
+    (heuristic == 1 ? (double)(abs(gx - (x)) + abs(gy - (y)) + abs(gz - (z)))                         \
+                    : sqrt((double)((gx - (x)) * (gx - (x)) + (gy - (y)) * (gy - (y)) + (gz - (z)) * (gz - (z)))))
+#define CX(c) ((int)((c) / YZ))
+#define CY(c) ((int)(((c) / Z) % Y))
+#define CZ(c) ((int)((c) % Z))
+    {
+        double h0 = H3T(s[0], s[1], s[2]);
+        heap[n++] = (a3node_t){0.0 + h0, h0, 0.0, seq++, start, start};
+        npush++;
+    }
+    while (n > 0) {
+        a3node_t node;
+        n--;
+        npop++;
+        if (n > 0) {
+            node = heap[0];
+            heap[0] = heap[n];
+            a3_siftup(heap, n, 0);
+        } else {
+            node = heap[0];
+        }
+        int z = CZ(node.cell), y = CY(node.cell), x = CX(node.cell);
+        if (lazy) {
+            /* lazy_theta_star3d.py:60-71: the parent is CLOSED (it expanded this node or its parent) */
+            const int32_t p = node.parent;
+            if (!los3(occ, X, Y, Z, CX(p), CY(p), CZ(p), x, y, z)) {
+                node.g = INFINITY;
+                for (int m = 0; m < 26; m++) {
+                    int dx = M3[m][0], dy = M3[m][1], dz = M3[m][2];
+                    if (collide3(occ, X, Y, Z, x, y, z, dx, dy, dz)) continue;
+                    int32_t nc = ((x + dx) * Y + (y + dy)) * Z + (z + dz);
+                    if (!closed[nc]) continue;
+                    double ng = cg[nc] + sqrt((double)(dx * dx + dy * dy + dz * dz));
+                    if (ng < node.g) { node.g = ng; node.parent = nc; }
+                }
+            }
+        }
+        if (closed[node.cell] && node.g >= cg[node.cell]) continue;
+        if (!closed[node.cell]) {
+            if (expand && nclose < expand_cap) expand[nclose] = node.cell;
+            nclose++;
+        }
+        closed[node.cell] = 1;
+        cg[node.cell] = node.g;
+        cparent[node.cell] = node.parent;
+        nexp++;
+        if (node.cell == goal) {
+            double cost = 0.0;
+            int32_t c = goal, len = 1;
+            while (c != start) {
+                int32_t p = cparent[c];
+                cost += dist3c(YZ, Z, c, p);
+                c = p;
+                len++;
+            }
+            status = 0;
+            if (len > path_cap) status = 2;
+            else {
+                c = goal;
+                int32_t i = len - 1;
+                path[i--] = c;
+                while (c != start) { c = cparent[c]; path[i--] = c; }
+            }
+            *path_len = len;
+            *cost_out = cost;
+            break;
+        }
+        const int32_t np_ = node.parent;  /* node_p = CLOSED.get(node.parent): always present */
+        for (int m = 0; m < 26; m++) {
+            int dx = M3[m][0], dy = M3[m][1], dz = M3[m][2];
+            if (collide3(occ, X, Y, Z, x, y, z, dx, dy, dz)) continue;
+            int nx = x + dx, ny = y + dy, nz = z + dz;
+            int32_t nc = (nx * Y + ny) * Z + nz;
+            double g1 = node.g + sqrt((double)(dx * dx + dy * dy + dz * dz));
+            if (closed[nc] && g1 >= cg[nc]) continue;
+            double qg = g1;
+            int32_t qp = node.cell;
+            /* updateVertex (theta_star3d.py:102-110 with lineOfSight(q, node_p); lazy_theta_star3d.py:120-128
+             * without it) */
+            if (lazy || los3(occ, X, Y, Z, nx, ny, nz, CX(np_), CY(np_), CZ(np_))) {
+                double alt = cg[np_] + dist3c(YZ, Z, nc, np_);
+                if (alt < qg) { qg = alt; qp = np_; }
+            }
+            double hn = H3T(nx, ny, nz);
+            if (n == cap) {
+                cap *= 2;
+                a3node_t* nh = (a3node_t*)realloc(heap, sizeof(a3node_t) * (size_t)cap);
+                if (!nh) { status = 3; goto donet; }
+                heap = nh;
+            }
+            heap[n++] = (a3node_t){qg + hn, hn, qg, seq++, nc, qp};
+            npush++;
+            if (n > maxn) maxn = n;
+            a3_siftdown(heap, 0, n - 1);
+        }
+    }
+#undef H3T
+#undef CX
+#undef CY
+#undef CZ
+donet:
+    *n_expanded = (int32_t)nclose;
+    if (counters) { counters[0] = npush; counters[1] = npop; counters[2] = nexp; counters[3] = maxn; }
+    if (status == 1) { *path_len = 0; *cost_out = INFINITY; }
+    if (status == 0 && expand && nclose > expand_cap) status = 3;
+    free(cg); free(cparent); free(closed); free(heap);
+    return status;
+}
+
+/* ------------------------------------------------------------------------------------ */
 /* DStar (global_planner/graph_search/d_star.py:37-291): list-semantics OPEN.             */
 /*  min_state = first element of minimal k in list order (:220-227)                       */
 /*  delete    = list.remove -> first occurrence; sets CLOSED only if OPEN (:250-259)      */

@@ -4,7 +4,7 @@ Run in the build container only (the reference never travels to the GPU box):
 
     PYTHONDONTWRITEBYTECODE=1 MPLBACKEND=Agg python tests/golden/make_golden.py [section ...]
 
-Sections: astar_readme astar_small astar_1024 dstar astar3d graph2d graph3d rrt dwa lqr mpc hypot
+Sections: astar_readme astar_small astar_1024 dstar astar3d graph2d graph3d theta3d rrt dwa lqr mpc hypot
 Outputs are small fixtures (inputs + expected outputs) under tests/golden/.  The reference is
 imported with stubs for the modules absent from this image (osqp, pyvista), per SURVEY.md §8(c).
 """
@@ -616,9 +616,62 @@ def sec_graph3d():
     print("graph3d csv rows", len(rows), "runs", len(res))
 
 
+# ----------------------------------------------------------------------------------------------
+# ThetaStar3D / LazyThetaStar3D (theta_star3d.py, lazy_theta_star3d.py) -- SURVEY.md §8(f) rank 4
+def run_theta3d(args):
+    occ, start, goal, lazy = args
+    pmp = import_reference()
+    X, Y, Z = occ.shape
+    env = pmp.Grid3D(X, Y, Z)
+    env.update({(int(a), int(b), int(c)) for a, b, c in np.argwhere(occ)})
+    from python_motion_planning.global_planner.graph_search import LazyThetaStar3D, ThetaStar3D
+
+    p = (LazyThetaStar3D if lazy else ThetaStar3D)(tuple(start), tuple(goal), env)
+    cost, path, expand = p.plan()
+    close_figs()
+    enc = lambda t: (t[0] * Y + t[1]) * Z + t[2]  # noqa: E731
+    return dict(cost=float(cost), path=[enc(t) for t in path], expand=[enc(n.current) for n in expand])
+
+
+def sec_theta3d():
+    from python_motion_planning_amd import workloads as wl
+
+    rows = []
+    with open(os.path.join(REF, "3d_pathfinding_results.csv"), newline="") as f:
+        rd = csv.reader(f)
+        next(rd)
+        for k, r in enumerate(rd):
+            if r[1] in ("theta_star", "lazy_theta_star") and k % 10 == 0:
+                rows.append(dict(algo=r[1], scenario=r[0], cost=r[3], visited=int(r[4]),
+                                 start=list(eval(r[5])), goal=list(eval(r[6])), seed=int(r[7])))  # noqa: S307
+    with open(os.path.join(HERE, "theta3d_csv.json"), "w") as f:
+        json.dump(rows, f)
+    cases = []
+    for lazy in (False, True):
+        for name in wl.SCENARIOS_3D:
+            for seed in range(5, 100, 16):
+                s, gq = wl.bench3d_query(seed, 21, 15, 11)
+                o = wl.SCENARIOS_3D[name](21, 15, 11)
+                wl.carve_safety_bubble(o, s, 2)
+                wl.carve_safety_bubble(o, gq, 2)
+                cases.append((o, s, gq, lazy))
+    with Pool(8) as pool:
+        res = pool.map(run_theta3d, cases)
+    dims = np.array([c[0].shape for c in cases], np.int32)
+    occ_flat, occ_off = ragged([np.packbits(c[0].ravel()) for c in cases], np.uint8)
+    path_flat, path_off = ragged([r["path"] for r in res])
+    exp_flat, exp_off = ragged([r["expand"] for r in res])
+    np.savez_compressed(
+        os.path.join(HERE, "theta3d_runs.npz"), dims=dims, occ_bits=occ_flat, occ_off=occ_off,
+        start=np.array([c[1] for c in cases], np.int32), goal=np.array([c[2] for c in cases], np.int32),
+        lazy=np.array([c[3] for c in cases]), cost=np.array([r["cost"] for r in res]), path=path_flat,
+        path_off=path_off, expand=exp_flat, expand_off=exp_off)
+    print("theta3d csv rows", len(rows), "runs", len(res))
+
+
 SECTIONS = dict(rrt=sec_rrt, mpc=sec_mpc, dwa=sec_dwa, local_plans=sec_local_plans, lqr=sec_lqr, astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
                 dstar=sec_dstar, astar3d=sec_astar3d,
-                graph2d=sec_graph2d, graph3d=sec_graph3d)
+                graph2d=sec_graph2d, graph3d=sec_graph3d, theta3d=sec_theta3d)
 
 if __name__ == "__main__":
     want = sys.argv[1:] or list(SECTIONS)

@@ -326,3 +326,27 @@ def test_graph3d_runs():
         assert out["cost"] == z["cost"][i]
         assert np.array_equal(out["path_cells"], seg(z["path"], z["path_off"], i))
         assert np.array_equal(out["expand_cells"], seg(z["expand"], z["expand_off"], i))
+
+
+def test_theta3d_published_csv():
+    """The reference's published ThetaStar3D / LazyThetaStar3D rows of 3d_pathfinding_results.csv."""
+    from python_motion_planning_amd import workloads as wl
+
+    rows = load_json("theta3d_csv.json")
+    assert len(rows) == 1000
+    for r in rows:
+        s, g = wl.bench3d_query(r["seed"], 21, 15, 11)
+        occ = wl.SCENARIOS_3D[r["scenario"]](21, 15, 11)
+        wl.carve_safety_bubble(occ, s, 2)
+        wl.carve_safety_bubble(occ, g, 2)
+        out = O.theta3d(occ, s, g, lazy=r["algo"] == "lazy_theta_star", with_expand=False)
+        assert repr(out["cost"]) == r["cost"], r
+        assert out["n_expanded"] == r["visited"], r
+
+
+def test_theta3d_runs():
+    for i, occ, z in grid_cases("theta3d_runs.npz"):
+        out = O.theta3d(occ, z["start"][i], z["goal"][i], lazy=bool(z["lazy"][i]))
+        assert out["cost"] == z["cost"][i]
+        assert np.array_equal(out["path_cells"], seg(z["path"], z["path_off"], i))
+        assert np.array_equal(out["expand_cells"], seg(z["expand"], z["expand_off"], i))
