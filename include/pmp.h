@@ -72,7 +72,7 @@ int pmp_astar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int 
                       uint32_t* expand, int expand_cap, int64_t* counters, int32_t* status);
 
 /* Planners that share the AStar loop (2D: a_star.py:39-83; 3D: a_star3d.py:33-78). */
-enum { PMP_ALGO_ASTAR = 0, PMP_ALGO_DIJKSTRA = 1, PMP_ALGO_GBFS = 2 };
+enum { PMP_ALGO_ASTAR = 0, PMP_ALGO_DIJKSTRA = 1, PMP_ALGO_GBFS = 2, PMP_ALGO_THETA = 3, PMP_ALGO_LAZY_THETA = 4 };
 
 /*
  * Batched 2D AStar / Dijkstra / GBFS.  algo = PMP_ALGO_ASTAR is pmp_astar2d_batch;
@@ -107,8 +107,14 @@ int pmp_astar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int 
  * PMP_ALGO_DIJKSTRA replaces Dijkstra3D.plan (global_planner/graph_search/dijkstra3d.py:39-87: key
  * (g, 0.0, counter), `heuristic` unused; its getNeighbor (:89-126) equals isCollision plus an
  * in-bounds test, and cells outside the grid are blocked here); PMP_ALGO_GBFS replaces
- * GBFS3D.plan (gbfs3d.py:34-82: key (h, counter), CLOSED membership tests).  Same arguments as
- * pmp_astar3d_batch; cost is extractPath's (dist along the path) for all three.
+ * GBFS3D.plan (gbfs3d.py:34-82: key (h, counter), CLOSED membership tests); PMP_ALGO_THETA
+ * replaces ThetaStar3D.plan (theta_star3d.py:38-110: at each push, the expanding node's CLOSED
+ * parent becomes the neighbour's parent when lineOfSight(neighbour, parent) (Bresenham, :139-213)
+ * holds and it is cheaper); PMP_ALGO_LAZY_THETA replaces LazyThetaStar3D.plan
+ * (lazy_theta_star3d.py:41-128: that update without the test, the test deferred to the pop, where
+ * a failed line of sight re-parents the node to its best CLOSED neighbour).  Same arguments as
+ * pmp_astar3d_batch; cost is extractPath's (Planner3D.dist along the path) for all five; any-voxel
+ * parents make paths shorter than their cell counts suggest.
  */
 int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uint32_t* occ_bits, int per_query, int X, int Y,
                       int Z, int heuristic, const int32_t* start_xyz, const int32_t* goal_xyz, int nq, double* cost,

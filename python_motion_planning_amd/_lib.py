@@ -125,8 +125,9 @@ _ctx = {}
 
 
 # planners sharing the AStar loop (include/pmp.h PMP_ALGO_*)
-ALGO_ASTAR, ALGO_DIJKSTRA, ALGO_GBFS = 0, 1, 2
-ALGOS = {"astar": ALGO_ASTAR, "dijkstra": ALGO_DIJKSTRA, "gbfs": ALGO_GBFS}
+ALGO_ASTAR, ALGO_DIJKSTRA, ALGO_GBFS, ALGO_THETA, ALGO_LAZY_THETA = 0, 1, 2, 3, 4
+ALGOS = {"astar": ALGO_ASTAR, "dijkstra": ALGO_DIJKSTRA, "gbfs": ALGO_GBFS, "theta_star": ALGO_THETA,
+         "lazy_theta_star": ALGO_LAZY_THETA}
 
 
 def load_library(path: str = LIB_PATH):

@@ -74,14 +74,63 @@ __device__ __forceinline__ uint32_t occ3l(const lds_w32* occ, int X, int Y, int 
 
 constexpr int kOccLdsWords = 1024;  // grids up to 32768 cells keep their occupancy in LDS (4 KiB)
 
+// lineOfSight (theta_star3d.py:139-213 == lazy_theta_star3d.py:158-233): integer Bresenham from a to
+// b along the dominant axis; both endpoints free, every voxel after a (b included) in the grid and free.
 template <bool OCC_LDS>
+__device__ __forceinline__ bool los3d(const uint32_t* occ, const lds_w32* occl, int X, int Y, int Z, int x0, int y0,
+                                      int z0, int x1, int y1, int z1)
+{
+    auto blocked = [&](int a, int b, int c) -> bool {
+        return OCC_LDS ? occ3l(occl, X, Y, Z, a, b, c) != 0u : occ3(occ, X, Y, Z, a, b, c);
+    };
+    if (blocked(x0, y0, z0) || blocked(x1, y1, z1)) return false;
+    const int dx = abs(x1 - x0), dy = abs(y1 - y0), dz = abs(z1 - z0);
+    const int sx = x1 >= x0 ? 1 : -1, sy = y1 >= y0 ? 1 : -1, sz = z1 >= z0 ? 1 : -1;
+    // the dominant axis becomes `u`, the other two `v`, `w` (same arithmetic as the three branches)
+    const int ax = (dx >= dy && dx >= dz) ? 0 : ((dy >= dx && dy >= dz) ? 1 : 2);
+    const int du = ax == 0 ? dx : (ax == 1 ? dy : dz);
+    const int dv = ax == 0 ? dy : dx, dw = ax == 2 ? dy : dz;
+    int x = x0, y = y0, z = z0;
+    int ev = du / 2, ew = du / 2;
+    for (int k = 0; k < du; k++) {
+        if (ax == 0) x += sx;
+        else if (ax == 1) y += sy;
+        else z += sz;
+        ev -= dv;
+        ew -= dw;
+        if (ev < 0) {
+            if (ax == 0) y += sy;
+            else x += sx;
+            ev += du;
+        }
+        if (ew < 0) {
+            if (ax == 2) y += sy;
+            else z += sz;
+            ew += du;
+        }
+        if (blocked(x, y, z)) return false;
+    }
+    return true;
+}
+
+__device__ __forceinline__ double dist3(int dx, int dy, int dz)  // Planner3D.dist (planner3d.py:22-27)
+{
+    return __dsqrt_rn((double)(dx * dx + dy * dy + dz * dz));
+}
+
+// THETA: 0 = AStar3D / Dijkstra3D / GBFS3D, 1 = ThetaStar3D (theta_star3d.py:38-110), 2 =
+// LazyThetaStar3D (lazy_theta_star3d.py:41-128).  Theta modes keep any-voxel parents: a per-cell
+// CLOSED parent (cpar) and, per push, the entry's parent in a side table indexed by the push
+// counter (ppar), since an entry's parent may be its pusher's parent.
+template <bool OCC_LDS, int THETA>
 __global__ __launch_bounds__(64) void astar3d_kernel(
     const uint32_t* __restrict__ occ_all, int per_query, int X, int Y, int Z, int heuristic,
     const int32_t* __restrict__ start_xyz, const int32_t* __restrict__ goal_xyz, int nq, double* __restrict__ cost_out,
     int32_t* __restrict__ path_len_out, uint32_t* __restrict__ path_out, int path_cap, int32_t* __restrict__ nexp_out,
     uint32_t* __restrict__ expand_out, int expand_cap, int64_t* __restrict__ counters, int32_t* __restrict__ status_out,
     int* __restrict__ queue, uint4* __restrict__ spill_all, int heap_cap, int lds_cap, uint8_t* __restrict__ cdir_all,
-    double* __restrict__ cg_all, int gzero)
+    double* __restrict__ cg_all, int gzero, uint32_t* __restrict__ cpar_all, uint32_t* __restrict__ ppar_all,
+    uint32_t ppar_cap)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
@@ -94,6 +143,8 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
     uint8_t* cdir = cdir_all + (size_t)worker * ncell;
     double* cg = cg_all + (size_t)worker * 2 * ncell;  // closed g
     double* og = cg + ncell;                            // best pending (pushed) g
+    uint32_t* cpar = THETA ? cpar_all + (size_t)worker * ncell : nullptr;      // CLOSED parent cell
+    uint32_t* ppar = THETA ? ppar_all + (size_t)worker * ppar_cap : nullptr;   // parent of push #seq
     int pop_jl, pop_ol;
     heap16::pop_lane_consts(lane, pop_jl, pop_ol);
     // neighbour lane m < 26: motion m (env3d.py:56-70)
@@ -140,6 +191,7 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
         root.b = scm;
         qc.derive(root);
         if (lane == 0) heap16::store<true>(hp, 0, root);
+        if (THETA && lane == 0) ppar[0] = ((uint32_t)sx * (uint32_t)Y + (uint32_t)sy) * (uint32_t)Z + (uint32_t)sz;
         heap16::wsync();
         int n = 1;
         uint32_t seq = 1;
@@ -174,6 +226,8 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
                 ncg = cg[nlin];
                 nog = og[nlin];
             }
+            uint32_t epar = 0;  // theta: the entry's parent cell (the start's parent is the start)
+            if (THETA && lane == 27) epar = node.a < ppar_cap ? ppar[node.a] : 0u;
             if (lane < 26) {
                 if (OCC_LDS) {
 #define OCC(a, b, c) occ3l(occl, X, Y, Z, a, b, c)
@@ -213,23 +267,71 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
             // best_closed check (a_star3d.py:48-50)
             const bool sclosed = rl_u32(ncd, 26) != 0u;
             const double scg = rl_f64(ncg, 26);
+            double node_g = node.g;
+            uint32_t npar = 0;  // theta: the node's parent cell
+            if (THETA) {
+                npar = rl_u32(epar, 27);
+                if (THETA == 2) {
+                    // lazy_theta_star3d.py:60-71: no line of sight from the parent -> g = inf, then the
+                    // best CLOSED neighbour (first minimum in motion order) becomes the parent
+                    const int px = (int)(npar / ((uint32_t)Y * Z)), py = (int)((npar / (uint32_t)Z) % (uint32_t)Y),
+                              pz = (int)(npar % (uint32_t)Z);
+                    if (!los3d<OCC_LDS>(occ, occl, X, Y, Z, px, py, pz, x, y, z)) {
+                        const bool cand = lane < 26 && !coll && ncd != 0u;
+                        const double cgv = cand ? ncg + mcost : __builtin_inf();
+                        double best = cgv;  // wave min, ties to the lowest lane (= motion order)
+                        int bl = cand ? lane : 64;
+                        for (int o = 32; o >= 1; o >>= 1) {
+                            const double ob = __shfl_xor(best, o);
+                            const int ol = __shfl_xor(bl, o);
+                            if (ob < best || (ob == best && ol < bl)) { best = ob; bl = ol; }
+                        }
+                        node_g = __builtin_inf();
+                        const int bsel = uni(bl);
+                        if (bsel < 64) {
+                            const double bv = rl_f64(best, 0);
+                            if (bv < node_g) {
+                                node_g = bv;
+                                npar = rl_u32(nlin, bsel);
+                            }
+                        }
+                    }
+                }
+            }
 #ifdef PMP_STAMPS
             const uint64_t ts2 = __builtin_amdgcn_s_memtime();
             cyc_pop += ts1 - ts0;
             cyc_wait += ts2 - ts1;
 #endif
-            if (sclosed && node.g >= scg) continue;
+            if (sclosed && node_g >= scg) continue;
             niter++;
             // Neighbour decisions first (:66-75): they consume this round's loads before any store is
             // issued below, so the compiler never has to drain those stores (vmcnt) to read them.
-            const double tg = node.g + mcost;
-            const bool ok = lane < 26 && !coll && !(ncd != 0u && tg >= ncg);
+            const double g1 = node_g + mcost;
+            const bool ok = lane < 26 && !coll && !(ncd != 0u && g1 >= ncg);
+            double tg = g1;
+            uint32_t qpar = lin;
+            if (THETA) {
+                // updateVertex with node_p = CLOSED[node.parent] (theta_star3d.py:86-110 with
+                // lineOfSight(q, node_p); lazy_theta_star3d.py:104-128 without it)
+                // the reference reads CLOSED[node.parent] after inserting the node itself
+                const double gp = npar == lin ? node_g : rl_f64(lane == 0 ? cg[npar] : 0.0, 0);
+                const int px = (int)(npar / ((uint32_t)Y * Z)), py = (int)((npar / (uint32_t)Z) % (uint32_t)Y),
+                          pz = (int)(npar % (uint32_t)Z);
+                if (ok && (THETA == 2 || los3d<OCC_LDS>(occ, occl, X, Y, Z, nx, ny, nz, px, py, pz))) {
+                    const double alt = gp + dist3(nx - px, ny - py, nz - pz);
+                    if (alt < tg) {
+                        tg = alt;
+                        qpar = npar;
+                    }
+                }
+            }
             // The key (f, h, counter) is a total order, so only the heap's contents matter.  An entry
             // whose cell already has a pending entry with g <= tg pops after it (f = g + h, equal
             // g -> earlier counter) and is then skipped by the CLOSED check (:48-50): it is dead on
             // arrival and is not inserted.  A strictly better entry is inserted and makes the old
             // one dead instead (skipped the same way when it pops).
-            const bool live = ok && tg < nog;
+            const bool live = THETA == 2 ? ok : (ok && tg < nog);
             const uint32_t okm = (uint32_t)ballot(ok);
             uint64_t vm = ballot(live);
             if (lane == 0) {
@@ -237,13 +339,39 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
                     if (expand_out && nexp < expand_cap) expand_out[(size_t)q * expand_cap + nexp] = lin;
                 }
                 cdir[lin] = (uint8_t)(ndir + 1);
-                cg[lin] = node.g;
+                cg[lin] = node_g;
+                if (THETA) cpar[lin] = npar;
             }
             if (!sclosed) nexp++;
             if ((node.b >> 5) == goal_xyz24) {  // goal check (:59-63), path via CLOSED parents
                 st = PMP_FOUND;
                 heap16::wsync();
-                if (lane == 0) {
+                if (THETA && lane == 0) {  // extractPath via CLOSED parents (theta_star3d.py:217-232)
+                    uint32_t c = lin;
+                    const uint32_t st_c = ((uint32_t)sx * (uint32_t)Y + (uint32_t)sy) * (uint32_t)Z + (uint32_t)sz;
+                    int len = 1;
+                    double cost = 0.0;
+                    while (c != st_c && len <= (int)ncell) {
+                        const uint32_t p = cpar[c];
+                        const int ddx = (int)(c / ((uint32_t)Y * Z)) - (int)(p / ((uint32_t)Y * Z));
+                        const int ddy = (int)((c / (uint32_t)Z) % (uint32_t)Y) - (int)((p / (uint32_t)Z) % (uint32_t)Y);
+                        const int ddz = (int)(c % (uint32_t)Z) - (int)(p % (uint32_t)Z);
+                        cost += dist3(ddx, ddy, ddz);
+                        c = p;
+                        len++;
+                    }
+                    goal_cost = cost;
+                    plen = len;
+                    if (len <= path_cap) {
+                        uint32_t* pth = path_out + (size_t)q * path_cap;
+                        c = lin;
+                        for (int i = len - 1; i >= 0; i--) {
+                            pth[i] = c;
+                            if (i == 0) break;
+                            c = cpar[c];
+                        }
+                    }
+                } else if (!THETA && lane == 0) {
                     int cx = x, cy = y, cz = z, len = 1;
                     double cost = 0.0;
                     while (!(cx == sx && cy == sy && cz == sz)) {  // goal -> start: cost and length
@@ -276,7 +404,7 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
             }
             // ---- neighbours (:66-75): push the live ones with the reference's counters
             npush += __popc(okm);  // the reference's pushes
-            if (live) og[nlin] = tg;
+            if (live && THETA != 2) og[nlin] = tg;
             Ent item;
             item.g = tg;
             item.a = 0u;
@@ -290,6 +418,10 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
                 Ent it = heap16::rl_ent(item, m);
                 // counter = the reference's push index of this neighbour
                 it.a = seq + (uint32_t)__popc(okm & ((1u << m) - 1u));
+                if (THETA) {
+                    if (it.a >= ppar_cap) { overflow = true; break; }
+                    if (lane == 0) ppar[it.a] = rl_u32(qpar, m);
+                }
                 if (n < lds_cap) heap16::push<Key3, false>(hp, qc, n, it, root, lane);
                 else heap16::push<Key3, true>(hp, qc, n, it, root, lane);
                 n += 1;
@@ -334,8 +466,10 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
                                  uint32_t* expand, int expand_cap, int64_t* counters, int32_t* status)
 {
     if (!ctx) return PMP_EINVAL;
-    if (algo < PMP_ALGO_ASTAR || algo > PMP_ALGO_GBFS)
-        return pmp_set_err(ctx, PMP_EINVAL, "pmp_graph3d_batch: algo must be 0 (AStar3D), 1 (Dijkstra3D) or 2 (GBFS3D)");
+    if (algo < PMP_ALGO_ASTAR || algo > PMP_ALGO_LAZY_THETA)
+        return pmp_set_err(ctx, PMP_EINVAL,
+                           "pmp_graph3d_batch: algo must be 0 (AStar3D), 1 (Dijkstra3D), 2 (GBFS3D), 3 (ThetaStar3D) or "
+                           "4 (LazyThetaStar3D)");
     if (X < 1 || Y < 1 || Z < 1 || X > kMaxDim3 || Y > kMaxDim3 || Z > kMaxDim3)
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar3d_batch: X, Y, Z must be in [1, 256]");
     if (heuristic != 0 && heuristic != 1) return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar3d_batch: heuristic must be 0 or 1");
@@ -362,14 +496,23 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     uint8_t* cdir = (uint8_t*)pmp_scratch(ctx, SCR_AUX2, (size_t)workers * ncell + 16);
     double* cg = (double*)pmp_scratch(ctx, SCR_AUX3, (size_t)workers * ncell * 16 + 16);  // closed g + pending g
     int* queue = (int*)pmp_scratch(ctx, SCR_AUX0, 256);
+    const int theta = algo == PMP_ALGO_THETA ? 1 : (algo == PMP_ALGO_LAZY_THETA ? 2 : 0);
+    // theta modes: CLOSED parent per cell, and the parent of every push (indexed by the push counter)
+    const uint32_t ppar_cap = theta ? (uint32_t)(64 * ncell + 64) : 0u;
+    uint32_t* tpar = nullptr;
+    if (theta) {
+        tpar = (uint32_t*)pmp_scratch(ctx, SCR_AUX4, (size_t)workers * (ncell + ppar_cap) * 4 + 16);
+        if (!tpar) return PMP_ENOMEM;
+    }
     if (!spill || !cdir || !cg || !queue) return PMP_ENOMEM;
     hipStream_t s = (hipStream_t)stream;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
-    auto kern = occ_lds ? astar3d_kernel<true> : astar3d_kernel<false>;
+    auto kern = occ_lds ? (theta == 1 ? astar3d_kernel<true, 1> : theta == 2 ? astar3d_kernel<true, 2> : astar3d_kernel<true, 0>)
+                        : (theta == 1 ? astar3d_kernel<false, 1> : theta == 2 ? astar3d_kernel<false, 2> : astar3d_kernel<false, 0>);
     hipLaunchKernelGGL(kern, dim3(workers), dim3(64), (size_t)lds_cap * 16 + occ_bytes, s, occ_bits, per_query, X, Y, Z,
                        algo == PMP_ALGO_DIJKSTRA ? 2 : heuristic, start_xyz, goal_xyz, nq, cost, path_len, path, path_cap,
                        n_expanded, expand, expand_cap, counters, status, queue, spill, heap_cap, lds_cap, cdir, cg,
-                       algo == PMP_ALGO_GBFS ? 1 : 0);
+                       algo == PMP_ALGO_GBFS ? 1 : 0, tpar, tpar ? tpar + (size_t)workers * ncell : nullptr, ppar_cap);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }

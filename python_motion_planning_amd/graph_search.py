@@ -237,3 +237,25 @@ class GBFS3D(AStar3D):
 
     def __str__(self) -> str:
         return "Greedy Best First Search (GBFS) 3D"
+
+
+class ThetaStar3D(AStar3D):
+    """Theta* for 3D voxel grids (theta_star3d.py:24-232): AStar3D's loop where a neighbour takes the
+    expanding node's CLOSED parent as its own when lineOfSight (integer Bresenham, :139-213) allows a
+    cheaper straight segment.  Same kernel (astar3d.hip, THETA = 1); paths are any-voxel."""
+
+    _algo = "theta_star"
+
+    def __str__(self) -> str:
+        return "Theta* 3D"
+
+
+class LazyThetaStar3D(AStar3D):
+    """Lazy Theta* for 3D grids (lazy_theta_star3d.py:24-252): the parent update without the line of
+    sight test, which is deferred to the pop (a failure re-parents the node to its best CLOSED
+    neighbour).  Same kernel (astar3d.hip, THETA = 2)."""
+
+    _algo = "lazy_theta_star"
+
+    def __str__(self) -> str:
+        return "Lazy Theta* 3D"

@@ -1,6 +1,7 @@
-"""Dijkstra / GBFS (2D: dijkstra.py, gbfs.py; 3D: dijkstra3d.py, gbfs3d.py) on the HIP kernels
-astar2d.hip / astar3d.hip (C-ABI pmp_graph2d_batch / pmp_graph3d_batch) vs the reference's own
-outputs (tests/golden/graph2d_small.npz, graph3d_csv.json, graph3d_runs.npz) and the oracle.
+"""Dijkstra / GBFS (2D: dijkstra.py, gbfs.py; 3D: dijkstra3d.py, gbfs3d.py) and Theta* / Lazy Theta*
+3D (theta_star3d.py, lazy_theta_star3d.py) on the HIP kernels astar2d.hip / astar3d.hip (C-ABI
+pmp_graph2d_batch / pmp_graph3d_batch) vs the reference's own outputs (tests/golden/graph2d_small.npz,
+graph3d_csv.json, graph3d_runs.npz, theta3d_csv.json, theta3d_runs.npz) and the oracle.
 
 Bar: bit-exact -- cost bits, path cells, closure (expand) order, visited counts."""
 import numpy as np
@@ -125,3 +126,64 @@ def test_graph3d_full_runs_and_dropin():
             cls = pmp.Dijkstra3D if algo == "dijkstra" else pmp.GBFS3D
             cost, path, expand = cls(tuple(z["start"][i]), tuple(z["goal"][i]), env).plan()
             assert cost == z["cost"][i] and len(expand) == ne
+
+
+def test_theta3d_published_csv_rows():
+    """The 1000 ThetaStar3D / LazyThetaStar3D rows of the reference's 3d_pathfinding_results.csv."""
+    from python_motion_planning_amd import batch
+
+    rows = load_json("theta3d_csv.json")
+    for algo in ("theta_star", "lazy_theta_star"):
+        sub = [r for r in rows if r["algo"] == algo]
+        occ, S, G = _csv_batch(sub)
+        out = batch.astar3d_batch(occ, S, G, algo=algo)
+        cost = out["cost"].cpu().numpy()
+        ne = out["n_expanded"].cpu().numpy()
+        st = out["status"].cpu().numpy()
+        for i, r in enumerate(sub):
+            assert repr(float(cost[i])) == r["cost"], (algo, i, r, st[i])
+            assert ne[i] == r["visited"], (algo, i, r)
+
+
+def test_theta3d_full_runs_and_dropin():
+    import python_motion_planning_amd as pmp
+    from oracle import oracle as O
+    from python_motion_planning_amd import batch
+
+    for i, occ, z in grid_cases("theta3d_runs.npz"):
+        X, Y, Z = occ.shape
+        lazy = bool(z["lazy"][i])
+        algo = "lazy_theta_star" if lazy else "theta_star"
+        out = batch.astar3d_batch(occ, z["start"][i][None], z["goal"][i][None], expand_cap=X * Y * Z, counters=True,
+                                  algo=algo)
+        assert float(out["cost"][0]) == z["cost"][i], (algo, i)
+        pl = int(out["path_len"][0])
+        assert np.array_equal(out["path"][0, :pl].cpu().numpy(), seg(z["path"], z["path_off"], i)), (algo, i)
+        ne = int(out["n_expanded"][0])
+        assert np.array_equal(out["expand"][0, :ne].cpu().numpy(), seg(z["expand"], z["expand_off"], i)), (algo, i)
+        ref = O.theta3d(occ, z["start"][i], z["goal"][i], lazy=lazy, with_expand=False)
+        assert int(out["counters"][0, 0]) == ref["n_push"] and int(out["counters"][0, 2]) == ref["n_iter"], (algo, i)
+        if i % 7 == 0:
+            env = pmp.Grid3D(X, Y, Z)
+            env.update({(int(a), int(b), int(c)) for a, b, c in np.argwhere(occ)})
+            cls = pmp.LazyThetaStar3D if lazy else pmp.ThetaStar3D
+            cost, path, expand = cls(tuple(z["start"][i]), tuple(z["goal"][i]), env).plan()
+            assert cost == z["cost"][i] and len(expand) == ne
+
+
+def test_theta3d_c5_batch_against_oracle():
+    """Theta* / Lazy Theta* on the C5 door workload (26x20x16, per-query carve), 2048 queries each."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import batch, workloads as wl
+
+    occ, S, G = wl.c5_workload(2048)
+    for lazy in (False, True):
+        out = batch.astar3d_batch(occ, S, G, algo="lazy_theta_star" if lazy else "theta_star")
+        cost = out["cost"].cpu().numpy()
+        ne = out["n_expanded"].cpu().numpy()
+        pl = out["path_len"].cpu().numpy()
+        P = out["path"].cpu().numpy()
+        for q in np.random.default_rng(5).choice(2048, 120, replace=False):
+            ref = O.theta3d(occ[q], S[q], G[q], lazy=lazy, with_expand=False)
+            assert cost[q] == ref["cost"] and ne[q] == ref["n_expanded"], (lazy, q)
+            assert np.array_equal(P[q, : pl[q]], ref["path_cells"]), (lazy, q)
