@@ -195,24 +195,61 @@ __device__ __forceinline__ void ds_mskor(lds_u32* w, uint32_t mask, uint32_t val
     asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"((uint32_t)(uintptr_t)w), "v"(mask), "v"(val) : "memory");
 }
 
-// Set the direction bit of the node at `level` whose path number (position + 1) is Pl, on the
-// lanes with `on`.  Lanes may share a block word, hence the atomics.
-template <bool BIG>
-__device__ __forceinline__ void bit_write(const Heap& h, bool on, int level, uint32_t Pl, bool bit)
+// Block coordinates of a level: tier t = level / 5, r = level - 5t, mr = 2^r - 1 and the LDS word
+// offset of the tier's blocks (word = block root path number + off).
+struct Lvl {
+    int t, r;
+    uint32_t mr;
+    int off;
+};
+__device__ __forceinline__ Lvl lvl_of(int level)
 {
-    const int t = (level * 13) >> 6;  // level / 5 for level < 64
-    const int r = level - 5 * t;
-    const uint32_t R = Pl >> r;
-    const uint32_t m = 1u << (Pl + ((1u - R) << r) - 1u);
-    const uint32_t v = bit ? m : 0u;
-    if (!BIG || t <= 2) {
-        const int off = t == 0 ? -1 : (t == 1 ? -31 : -991);
-        if (on) ds_mskor(h.B + (int)R + off, m, v);
+    Lvl l;
+    l.t = (int)((uint32_t)__mul24(level, 13) >> 6);  // level / 5 for level < 64
+    l.r = level - __mul24(l.t, 5);
+    l.mr = (1u << l.r) - 1u;
+    l.off = l.t == 0 ? -1 : (l.t == 1 ? -31 : -991);
+    return l;
+}
+
+// Set the direction bit of the node whose path number (position + 1) is Pl, at the level `L`
+// describes, on the lanes with `on`; the bit value is this lane's bit of `bits`.  Lanes may share a
+// block word, hence the atomics.
+template <bool BIG>
+__device__ __forceinline__ void bit_write(const Heap& h, bool on, const Lvl& L, uint32_t Pl, uint64_t bits)
+{
+    const uint32_t R = Pl >> L.r;
+    const uint32_t m = 1u << ((Pl & L.mr) + L.mr);  // node (R's descendant, offset Pl - R 2^r) of the block
+    const uint32_t v = sel_lanes(bits, m, 0u);
+    if (!BIG || L.t <= 2) {
+        if (on) ds_mskor(h.B + (int)R + L.off, m, v);
     } else if (on) {
-        uint32_t* w = h.hb + hb_word(t, R);
-        if (bit) __hip_atomic_fetch_or(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t* w = h.hb + hb_word(L.t, R);
+        if (v) __hip_atomic_fetch_or(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else __hip_atomic_fetch_and(w, ~m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+}
+
+// Lane mask of the lanes where a < b under Node.__lt__ (node.py:51-54) on (f, h) pairs, h ordered by
+// hkey(cm); compares go straight to lane masks (no bool round trips through VGPRs).
+template <int HEUR>
+__device__ __forceinline__ uint64_t lt_mask(bool on, double fa, uint32_t ca, double fb, uint32_t cb)
+{
+    const uint64_t lt = ballot(on && fa < fb);
+    const uint64_t eq = ballot(on && fa == fb);
+    return lt | (eq & ballot(hkey<HEUR>(ca) < hkey<HEUR>(cb)));
+}
+// CPython _siftup's choice bit of a parent whose child `child` (a position) now holds (vf, vc) and
+// whose other child holds (sf, sc): bit = !(left < right).  Returns the lane mask of bits.
+template <int HEUR>
+__device__ __forceinline__ uint64_t choice_bits(int child, double vf, uint32_t vc, double sf, uint32_t sc)
+{
+    const uint64_t eq = ballot(vf == sf);
+    const uint32_t vk = hkey<HEUR>(vc), sk = hkey<HEUR>(sc);
+    const uint64_t vlt = ballot(vf < sf) | (eq & ballot(vk < sk));
+    const uint64_t slt = ballot(sf < vf) | (eq & ballot(sk < vk));
+    const uint64_t left = ballot((child & 1) != 0);  // odd positions are left children
+    return (left & ~vlt) | (~left & ~slt);
 }
 
 // Five levels of the _siftup path inside one bit block: w2 = block word << 1 (node Pr of the
@@ -252,14 +289,13 @@ __device__ __forceinline__ void wave_sync_mem()
 //  4. lanes 1..m rewrite the bits of p_0..p_{m-1}, whose children changed.
 template <bool SPILL, bool BIG, int HEUR>
 __device__ __forceinline__ void heap_pop(const Heap& h, int n, uint32_t v01, double& lastf, uint32_t& lastc, double& rootf,
-                                         uint32_t& rootc, int lane)
+                                         uint32_t& rootc, const Lvl& pl, int lane)
 {
     n = uni(n);
     // `last` = heap[n] is kept in registers by the caller (no load round); v01 = the tier-0 word
     // (lane 0) and tier-1 words (lanes 1..32), loaded by the caller ahead of time
     const double lf = lastf;
     const uint32_t lc = lastc;
-    const uint32_t lk = hkey<HEUR>(lc);
 
     // ---- 1. the path.  Levels 0..D-1 are full (D = floor(log2 n)), so every node above level D-1
     //      has two children and the walk takes D-1 unconditional steps; the last step (level D-1 ->
@@ -345,10 +381,10 @@ __device__ __forceinline__ void heap_pop(const Heap& h, int n, uint32_t v01, dou
         lb.get(Bf, Bc);
         ls.get(Sf, Sc);
     }
-    const uint32_t Ak = hkey<HEUR>(Ac), Bk = hkey<HEUR>(Bc), Sk = hkey<HEUR>(Sc);
 
     // ---- 3. movers: lanes 1..m store heap[p_i] at p_{i-1}; lane 0 stores last at p_m
-    const int m = __popcll(ballot(on && !key_lt(lf, lk, Af, Ak)));
+    const uint64_t onm = ballot(on);
+    const int m = __popcll(onm & ~lt_mask<HEUR>(on, lf, lc, Af, Ac));
     {
         const bool l0 = lane == 0;
         const bool st = l0 || (on && lane <= m);
@@ -372,10 +408,8 @@ __device__ __forceinline__ void heap_pop(const Heap& h, int n, uint32_t v01, dou
     // ---- 4. bits of p_0 .. p_{m-1}: the new heap[p_i] against its sibling
     {
         const bool useb = lane < m;
-        const double vf = useb ? Bf : lf;
-        const uint32_t vk = useb ? Bk : lk;
-        const bool bit = (pi & 1) ? !key_lt(vf, vk, Sf, Sk) : !key_lt(Sf, Sk, vf, vk);
-        bit_write<BIG>(h, hass && lane <= m, lane - 1, P >> (sh + 1), bit);
+        const uint64_t bits = choice_bits<HEUR>(pi, useb ? Bf : lf, useb ? Bc : lc, Sf, Sc);
+        bit_write<BIG>(h, hass && lane <= m, pl, P >> (sh + 1), bits);
     }
     wave_sync_mem();
 }
@@ -405,8 +439,7 @@ __device__ __forceinline__ void heap_push(const Heap& h, int n, double itf, uint
         la.get(Af, Ac);
         ls.get(Sf, Sc);
     }
-    const uint32_t Ak = hkey<HEUR>(Ac), Sk = hkey<HEUR>(Sc);
-    const int t = __popcll(ballot(on && key_lt(itf, itk, Af, Ak)));  // the "less" set is a prefix from the parent up
+    const int t = __popcll(lt_mask<HEUR>(on, itf, itc, Af, Ac));  // the "less" set is a prefix from the parent up
     const int ipos = (int)(np1 >> t) - 1;
     {
         const bool l0 = lane == 0;
@@ -427,21 +460,19 @@ __device__ __forceinline__ void heap_push(const Heap& h, int n, double itf, uint
     }
     {
         const bool usea = lane - 1 < t;  // the new heap[a_{j-1}]
-        const double vf = usea ? Af : itf;
-        const uint32_t vk = usea ? Ak : itk;
-        const bool bit = (x & 1) ? !key_lt(vf, vk, Sf, Sk) : !key_lt(Sf, Sk, vf, vk);
-        bit_write<BIG>(h, hass && lane <= t + 1, D - l1, np1 >> l1, bit);
+        const uint64_t bits = choice_bits<HEUR>(x, usea ? Af : itf, usea ? Ac : itc, Sf, Sc);
+        bit_write<BIG>(h, hass && lane <= t + 1, lvl_of(D - l1), np1 >> l1, bits);
     }
     wave_sync_mem();
 }
 
 template <int HEUR>
 __device__ __forceinline__ void pop_any(const Heap& h, int n, uint32_t v01, double& lastf, uint32_t& lastc, double& rootf,
-                                        uint32_t& rootc, int lane)
+                                        uint32_t& rootc, const Lvl& pl, int lane)
 {
-    if (n < h.cap) heap_pop<false, false, HEUR>(h, n, v01, lastf, lastc, rootf, rootc, lane);
-    else if (n < kBigHeap) heap_pop<true, false, HEUR>(h, n, v01, lastf, lastc, rootf, rootc, lane);
-    else heap_pop<true, true, HEUR>(h, n, v01, lastf, lastc, rootf, rootc, lane);
+    if (n < h.cap) heap_pop<false, false, HEUR>(h, n, v01, lastf, lastc, rootf, rootc, pl, lane);
+    else if (n < kBigHeap) heap_pop<true, false, HEUR>(h, n, v01, lastf, lastc, rootf, rootc, pl, lane);
+    else heap_pop<true, true, HEUR>(h, n, v01, lastf, lastc, rootf, rootc, pl, lane);
 }
 template <int HEUR>
 __device__ __forceinline__ void push_any(const Heap& h, int n, double itf, uint32_t itc, uint32_t itk, double& lastf,
@@ -498,6 +529,8 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
     uint32_t need = 16u | (1u << ((mx + 1) * 3 + (my + 1)));
     if (mo & 1) need |= (1u << (3 + (my + 1))) | (1u << ((mx + 1) * 3 + 1));
     const uint32_t self_bit = 1u << ((mx + 1) * 3 + (my + 1));
+    // pop lane i (1..15) rewrites the bit of the path node at level i - 1
+    const Lvl pop_lvl = lvl_of(lane >= 1 ? lane - 1 : 0);
 
     for (;;) {
         // readfirstlane (not __shfl): the compiler must SEE the query index as wave-uniform, or
@@ -591,7 +624,7 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
 #endif
 
             // ---- heappop (a_star.py:54): `last` = heap[n] sifts down the CPython path
-            if (n > 0) pop_any<HEUR>(hp, n, v01, lastf, lastc, rootf, rootc, lane);
+            if (n > 0) pop_any<HEUR>(hp, n, v01, lastf, lastc, rootf, rootc, pop_lvl, lane);
 
             STAMP(ts1);
             // 3x3 masks: bit k = cell (x + k/3 - 1, y + k%3 - 1); the node is k = 4
