@@ -18,7 +18,7 @@
 
 namespace {
 
-constexpr int kThreads = 512;
+constexpr int kThreads = 1024;  // 16 waves per agent: the FP64 rollout needs the occupancy to hide latency
 constexpr int kMaxN = 4096;    // samples per step held in LDS
 constexpr int kMaxLeaves = 128;
 
@@ -48,6 +48,18 @@ __device__ inline double linsp_at(const Linsp& L, int i)
 
 typedef __attribute__((address_space(3))) uint32_t lds_w32;
 constexpr int kOccLdsWords = 4096;  // grids up to 131072 cells keep their occupancy in LDS (16 KiB)
+
+// The occupancy bits of cells (i, j0 .. j0 + n - 1) of one grid row (x-major: consecutive j are
+// consecutive bits), n <= 32, all inside the grid: bit b of the result = cell (i, j0 + b).
+template <class PTR>
+__device__ inline uint32_t occ_run(PTR occ, int H, int i, int j0, int n)
+{
+    const uint32_t k = (uint32_t)i * (uint32_t)H + (uint32_t)j0;
+    const uint32_t w = k >> 5, sh = k & 31u;
+    uint32_t v = occ[w] >> sh;
+    if (sh + (uint32_t)n > 32u) v |= occ[w + 1] << (32u - sh);
+    return n >= 32 ? v : (v & ((1u << n) - 1u));
+}
 
 template <class PTR>
 __device__ inline bool occ_at(PTR occ, int ox, int oy, int W, int H, int cx, int cy)
@@ -188,7 +200,9 @@ __global__ __launch_bounds__(kThreads) void dwa_kernel(
         for (int c = tid; c < N; c += kThreads) {
             const double v = linsp_at(LV, c / nw), w = linsp_at(LW, c % nw);
             double x = st[0], y = st[1], th = st[2];
-            double mind = INFINITY;
+            // min over cells of sqrt(d2) == sqrt(min d2): sqrt is monotone and correctly rounded, so
+            // one square root per sample (scipy cdist: d = sqrt(dx*dx + dy*dy), no fused multiply-add)
+            double mind2 = INFINITY;
             // cos/sin of th_k by rotation: th_k = th_0 + k*(dt*w) up to the rounding of the running
             // sum (which th itself keeps exactly as the reference), so (cs, sn) stay within ~2e-14
             // of libm's cos/sin(th_k) over the horizon -- one sincos pair per sample, not per step.
@@ -205,17 +219,26 @@ __global__ __launch_bounds__(kThreads) void dwa_kernel(
                 th = nth;
                 const int x0 = (int)ceil(x - R), x1 = (int)floor(x + R);
                 const int y0 = (int)ceil(y - R), y1 = (int)floor(y + R);
-                for (int cx = x0; cx <= x1 && cx <= x0 + 16; cx++)
-                    for (int cy = y0; cy <= y1 && cy <= y0 + 16; cy++) {
-                        const bool o = OCC_LDS ? occ_at(occl, ox, oy, W, H, cx, cy) : occ_at(occ, ox, oy, W, H, cx, cy);
-                        if (!o) continue;
-                        const double dx = (double)cx - x, dy = (double)cy - y;
-                        const double d = sqrt(dx * dx + dy * dy);
-                        if (d < mind) mind = d;
+                // the stencil row by row: one bit run per row, distances only for its set bits
+                // (cells outside the grid are not obstacles)
+                const int j0 = max(y0 - oy, 0), j1 = min(min(y1, y0 + 16) - oy, H - 1);
+                if (j0 <= j1)
+                    for (int cx = x0; cx <= x1 && cx <= x0 + 16; cx++) {
+                        const int i = cx - ox;
+                        if ((unsigned)i >= (unsigned)W) continue;
+                        uint32_t run = OCC_LDS ? occ_run(occl, H, i, j0, j1 - j0 + 1) : occ_run(occ, H, i, j0, j1 - j0 + 1);
+                        while (run) {
+                            const int b = __ffs(run) - 1;
+                            run &= run - 1;
+                            const double dx = (double)cx - x, dy = (double)(oy + j0 + b) - y;
+                            const double d2 = dx * dx + dy * dy;
+                            if (d2 < mind2) mind2 = d2;
+                        }
                     }
             }
             const double ang = atan2(gy - y, gx - x);
             S.col[0][c] = lp::kPi - fabs(ang - th);
+            const double mind = sqrt(mind2);
             S.col[1][c] = mind < R ? mind : R;
             S.col[2][c] = fabs(v);
         }
