@@ -72,12 +72,16 @@ def hypot(a, b):
 
 # planners sharing the AStar loop (pmp_oracle.c oracle_graph2d / oracle_graph3d)
 ALGOS = {"astar": 0, "dijkstra": 1, "gbfs": 2}
+# 2D only: ThetaStar / LazyThetaStar on the same loop (3D Theta* is theta3d below)
+ALGOS2D = dict(ALGOS, theta_star=3, lazy_theta_star=4)
 
 
 def astar2d(occ: np.ndarray, start, goal, heuristic: str = "euclidean", with_expand: bool = True,
             path_cap: int | None = None, expand_cap: int | None = None, algo: str = "astar"):
     """Restatement of AStar.plan (a_star.py:39-83); algo "dijkstra" / "gbfs" restate Dijkstra.plan
-    (dijkstra.py:36-85) / GBFS.plan (gbfs.py:36-86).  occ: uint8 [W, H], occ[x, y] != 0 blocked.
+    (dijkstra.py:36-85) / GBFS.plan (gbfs.py:36-86), "theta_star" / "lazy_theta_star" ThetaStar.plan
+    (theta_star.py:44-94) / LazyThetaStar.plan (lazy_theta_star.py:38-101).  occ: uint8 [W, H],
+    occ[x, y] != 0 blocked.
     Returns dict(status, cost, path (goal->start list of (x,y)), expand (closure order), counters)."""
     occ = np.ascontiguousarray(occ, dtype=np.uint8)
     W, H = occ.shape
@@ -89,7 +93,7 @@ def astar2d(occ: np.ndarray, start, goal, heuristic: str = "euclidean", with_exp
     plen = ctypes.c_int32(0)
     nexp = ctypes.c_int32(0)
     ctr = np.zeros(4, np.int64)
-    st = lib().oracle_graph2d(ALGOS[algo], _p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0,
+    st = lib().oracle_graph2d(ALGOS2D[algo], _p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0,
                               int(start[0]), int(start[1]), int(goal[0]), int(goal[1]),
                               ctypes.byref(cost), _p(path, _i32p), path_cap, ctypes.byref(plen),
                               _p(expand, _i32p) if with_expand else None, expand_cap,
@@ -163,7 +167,7 @@ def astar2d_batch(occ: np.ndarray, starts, goals, heuristic: str = "euclidean", 
     out = dict(cost=np.zeros(nq), path=np.zeros((nq, path_cap), np.int32), path_len=np.zeros(nq, np.int32),
                n_expanded=np.zeros(nq, np.int32), counters=np.zeros((nq, 4), np.int64),
                status=np.zeros(nq, np.int32))
-    lib().oracle_graph2d_batch(ALGOS[algo], _p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0, _p(s, _i32p),
+    lib().oracle_graph2d_batch(ALGOS2D[algo], _p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0, _p(s, _i32p),
                                _p(g, _i32p), nq, _p(out["cost"], _dp), _p(out["path"], _i32p), path_cap,
                                _p(out["path_len"], _i32p), _p(out["n_expanded"], _i32p),
                                _p(out["counters"], _i64p), _p(out["status"], _i32p), int(nthreads))

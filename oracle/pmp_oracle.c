@@ -154,6 +154,36 @@ static inline int collide2(const uint8_t* occ, int W, int H, int x1, int y1, int
     return 0;
 }
 
+/* ThetaStar.lineOfSight (global_planner/graph_search/theta_star.py:110-171): Bresenham from
+ * (x1, y1) to (x2, y2).  tau = (d_y - d_x) / 2 is a half-integer, so `e > tau` is compared as
+ * 2e > (d_y - d_x) in integers.  Cells off the grid are not in the obstacle set (a set lookup), but
+ * a line between two in-grid endpoints never leaves the grid's bounding box anyway. */
+static int los2(const uint8_t* occ, int W, int H, int x1, int y1, int x2, int y2)
+{
+    if (occ2(occ, W, H, x1, y1) || occ2(occ, W, H, x2, y2)) return 0; /* also the range checks */
+    const int dx = abs(x2 - x1), dy = abs(y2 - y1);
+    const int sx = x2 > x1 ? 1 : (x2 < x1 ? -1 : 0), sy = y2 > y1 ? 1 : (y2 < y1 ? -1 : 0);
+    int x = x1, y = y1, e = 0;
+    if (dx > dy) {
+        const int T = dy - dx;
+        while (x != x2) {
+            if (2 * e > T) { x += sx; e -= dy; }
+            else if (2 * e < T) { y += sy; e += dx; }
+            else { x += sx; y += sy; e += dx - dy; }
+            if (x >= 0 && y >= 0 && x < W && y < H && occ[(int64_t)x * H + y]) return 0;
+        }
+    } else {
+        const int T = dx - dy;
+        while (y != y2) {
+            if (2 * e > T) { y += sy; e -= dx; }
+            else if (2 * e < T) { x += sx; e += dy; }
+            else { x += sx; y += sy; e += dy - dx; }
+            if (x >= 0 && y >= 0 && x < W && y < H && occ[(int64_t)x * H + y]) return 0;
+        }
+    }
+    return 1;
+}
+
 /* Return codes for every planner: 0 found, 1 no path, 2 path_cap overflow,
  * 3 heap/expand capacity overflow, 4 reference raises. */
 
@@ -163,8 +193,14 @@ static inline int collide2(const uint8_t* occ, int W, int H, int x1, int y1, int
  *   algo 0: AStar      node_n.h = h(node_n)                            (a_star.py:71-72)
  *   algo 1: Dijkstra   node_n.h = 0                                    (dijkstra.py:73-74)
  *   algo 2: GBFS       node_n.h = h(node_n), node_n.g = 0              (gbfs.py:73-75)
+ *   algo 3: ThetaStar  after path 1, updateVertex(CLOSED[node.parent], node_n): lineOfSight(node_n,
+ *                      parent) and parent.g + dist <= node_n.g -> path 2  (theta_star.py:44-108)
+ *   algo 4: LazyThetaStar  updateVertex without the line of sight at the push; at the pop, no
+ *                      lineOfSight(parent, node) -> g = min over CLOSED neighbours (first minimum in
+ *                      motion order), g = inf if none  (lazy_theta_star.py:38-114)
  * (Dijkstra/GBFS also skip neighbours in obstacles, dijkstra.py:66-67 / gbfs.py:66-67: a no-op,
- * getNeighbor never returns one.)  All three push the start as Node(start, start, 0, 0).
+ * getNeighbor never returns one.)  All of them push the start as Node(start, start, 0, 0).
+ * Theta*'s parents are any cell; extractPath is AStar's (hypot per hop, goal -> start).
  * heuristic: 0 = euclidean (math.hypot), 1 = manhattan (graph_search.py:41-44).
  * path: goal -> start order (reference does not reverse it), cell ids x*H+y.
  * expand (nullable): closure order of CLOSED (list(CLOSED.values()), :64).
@@ -176,13 +212,14 @@ int oracle_graph2d(int algo, const uint8_t* occ, int W, int H, int heuristic, in
     const int64_t ncell = (int64_t)W * H;
     uint8_t* closed = (uint8_t*)calloc((size_t)ncell, 1);
     int32_t* cparent = (int32_t*)malloc(sizeof(int32_t) * (size_t)ncell);
+    double* cg = algo >= 3 ? (double*)malloc(sizeof(double) * (size_t)ncell) : NULL; /* CLOSED[c].g */
     int64_t cap = 1024, n = 0, npush = 0, npop = 0, nexp = 0, maxn = 1;
     anode_t* heap = (anode_t*)malloc(sizeof(anode_t) * (size_t)cap);
     const double SQ2 = sqrt(2.0);
     int status = 1;
     *path_len = 0;
     *cost_out = 0.0;
-    if (!closed || !cparent || !heap) { free(closed); free(cparent); free(heap); return 3; }
+    if (!closed || !cparent || !heap || (algo >= 3 && !cg)) { free(closed); free(cparent); free(heap); free(cg); return 3; }
     const int32_t start = sx * H + sy, goal = gx * H + gy;
     /* start node: Node(start, start, 0, 0)  (planner.py:15) */
     heap[n++] = (anode_t){0.0, 0.0, start, start};
@@ -200,9 +237,26 @@ int oracle_graph2d(int algo, const uint8_t* occ, int W, int H, int heuristic, in
         }
         if (closed[node.cell]) continue;
         int x = node.cell / H, y = node.cell % H;
+        if (algo == 4 && closed[node.parent]) {
+            /* set vertex (lazy_theta_star.py:55-65); it runs before the CLOSED check there, but on a
+             * node that check then skips it changes nothing */
+            const int px = node.parent / H, py = node.parent % H;
+            if (!los2(occ, W, H, px, py, x, y)) {
+                node.g = INFINITY;
+                for (int m = 0; m < 8; m++) {
+                    int nx = x + MX8[m], ny = y + MY8[m];
+                    if (collide2(occ, W, H, x, y, nx, ny)) continue;
+                    int32_t nc = nx * H + ny;
+                    if (!closed[nc]) continue;
+                    const double c = cg[nc] + ((m & 1) ? SQ2 : 1.0);
+                    if (node.g > c) { node.g = c; node.parent = nc; }
+                }
+            }
+        }
         if (node.cell == goal) {
             closed[node.cell] = 1;
             cparent[node.cell] = node.parent;
+            if (cg) cg[node.cell] = node.g;
             if (expand && nexp < expand_cap) expand[nexp] = node.cell;
             nexp++;
             /* extractPath: walk parents goal -> start, cost += hypot in that order */
@@ -238,6 +292,14 @@ int oracle_graph2d(int algo, const uint8_t* occ, int W, int H, int heuristic, in
                 nb.h = (double)(abs(gx - nx) + abs(gy - ny));
             else
                 nb.h = vnorm2((double)(gx - nx), (double)(gy - ny));
+            if (algo >= 3 && closed[node.parent]) { /* updateVertex(CLOSED[node.parent], node_n) */
+                const int px = node.parent / H, py = node.parent % H;
+                const double g2 = cg[node.parent] + vnorm2((double)(px - nx), (double)(py - ny));
+                if (g2 <= nb.g && (algo == 4 || los2(occ, W, H, nx, ny, px, py))) {
+                    nb.g = g2;
+                    nb.parent = node.parent;
+                }
+            }
             if (n == cap) {
                 cap *= 2;
                 anode_t* nh = (anode_t*)realloc(heap, sizeof(anode_t) * (size_t)cap);
@@ -252,6 +314,7 @@ int oracle_graph2d(int algo, const uint8_t* occ, int W, int H, int heuristic, in
         }
         closed[node.cell] = 1;
         cparent[node.cell] = node.parent;
+        if (cg) cg[node.cell] = node.g;
         if (expand && nexp < expand_cap) expand[nexp] = node.cell;
         nexp++;
     }
@@ -260,7 +323,7 @@ done:
     if (counters) { counters[0] = npush; counters[1] = npop; counters[2] = nexp; counters[3] = maxn; }
     if (status == 1) *path_len = 0;
     if (status == 0 && expand && nexp > expand_cap) status = 3;
-    free(closed); free(cparent); free(heap);
+    free(closed); free(cparent); free(heap); free(cg);
     return status;
 }
 

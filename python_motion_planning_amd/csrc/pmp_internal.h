@@ -18,12 +18,12 @@ struct pmp_ctx {
     // longest-first only: how many of the first (longest) queries run at raised wave priority
     int astar_prio_n = 64;
     // grow-only scratch arena, one buffer per use
-    void* buf[10] = {nullptr};
-    size_t cap[10] = {0};
+    void* buf[11] = {nullptr};
+    size_t cap[11] = {0};
 };
 
 enum ScratchSlot { SCR_HEAP = 0, SCR_CLOSED = 1, SCR_PDIR = 2, SCR_G = 3, SCR_AUX0 = 4, SCR_AUX1 = 5, SCR_AUX2 = 6, SCR_AUX3 = 7,
-                   SCR_BITS = 8, SCR_AUX4 = 9, SCR_NSLOTS = 10 };
+                   SCR_BITS = 8, SCR_AUX4 = 9, SCR_PAR = 10, SCR_NSLOTS = 11 };
 
 int pmp_set_err(pmp_ctx* ctx, int code, const std::string& msg);
 // Ensure scratch buffer `slot` holds at least `bytes`; returns device pointer or nullptr (error set).

@@ -4,7 +4,7 @@ Run in the build container only (the reference never travels to the GPU box):
 
     PYTHONDONTWRITEBYTECODE=1 MPLBACKEND=Agg python tests/golden/make_golden.py [section ...]
 
-Sections: astar_readme astar_small astar_1024 dstar astar3d graph2d graph3d theta3d rrt dwa lqr mpc hypot
+Sections: astar_readme astar_small astar_1024 dstar astar3d graph2d graph3d theta3d theta2d rrt dwa lqr mpc hypot
 Outputs are small fixtures (inputs + expected outputs) under tests/golden/.  The reference is
 imported with stubs for the modules absent from this image (osqp, pyvista), per SURVEY.md §8(c).
 """
@@ -669,9 +669,73 @@ def sec_theta3d():
     print("theta3d csv rows", len(rows), "runs", len(res))
 
 
+# ----------------------------------------------------------------------------------------------
+# ThetaStar / LazyThetaStar 2D (theta_star.py, lazy_theta_star.py) -- SURVEY.md §8(f) rank 4
+def run_theta2d(args):
+    occ, start, goal, heur, algo = args
+    pmp = import_reference()
+    W, H = occ.shape
+    env = pmp.Grid(W, H)
+    env.update(obstacles_of(occ))
+    cls = dict(theta_star=pmp.ThetaStar, lazy_theta_star=pmp.LazyThetaStar)[algo]
+    p = cls(tuple(start), tuple(goal), env, heur)
+    cost, path, expand = p.plan()
+    close_figs()
+    return dict(found=bool(path), cost=float(cost) if path else float("nan"), path=[x * H + y for (x, y) in path],
+                expand=[n.current[0] * H + n.current[1] for n in expand],
+                exp_parent=[n.parent[0] * H + n.parent[1] for n in expand], exp_g=[float(n.g) for n in expand])
+
+
+def sec_theta2d(n=160):
+    from python_motion_planning_amd import workloads as wl
+
+    rng = np.random.default_rng(1357)
+    cases = []
+    occ = wl.readme_grid()
+    for algo in ("theta_star", "lazy_theta_star"):
+        for heur in ("euclidean", "manhattan"):
+            cases.append((occ, (5, 5), (45, 25), heur, algo))
+    for i in range(n):
+        big = i % 20 == 7
+        W = int(rng.integers(96, 161)) if big else int(rng.integers(8, 81))
+        H = int(rng.integers(96, 161)) if big else int(rng.integers(8, 81))
+        dens = float(rng.uniform(0.0, 0.35))
+        occ = (rng.random((W, H)) < dens).astype(np.uint8)
+        occ[:, 0] = occ[:, H - 1] = 1
+        occ[0, :] = occ[W - 1, :] = 1
+        free = np.argwhere(occ == 0)
+        if len(free) < 2:
+            occ[1, 1] = occ[W - 2, H - 2] = 0
+            free = np.argwhere(occ == 0)
+        s = free[rng.integers(len(free))]
+        g = free[rng.integers(len(free))]
+        if i % 17 == 5:
+            g = s
+        heur = "manhattan" if i % 4 == 3 else "euclidean"
+        cases.append((occ, tuple(int(v) for v in s), tuple(int(v) for v in g), heur,
+                      "lazy_theta_star" if i % 2 else "theta_star"))
+    with Pool(8) as pool:
+        res = pool.map(run_theta2d, cases, chunksize=2)
+    dims = np.array([c[0].shape for c in cases], np.int32)
+    occ_flat, occ_off = ragged([np.packbits(c[0].ravel()) for c in cases], np.uint8)
+    path_flat, path_off = ragged([r["path"] for r in res])
+    exp_flat, exp_off = ragged([r["expand"] for r in res])
+    par_flat, _ = ragged([r["exp_parent"] for r in res])
+    g_flat, _ = ragged([r["exp_g"] for r in res], np.float64)
+    np.savez_compressed(
+        os.path.join(HERE, "theta2d_small.npz"),
+        dims=dims, occ_bits=occ_flat, occ_off=occ_off,
+        start=np.array([c[1] for c in cases], np.int32), goal=np.array([c[2] for c in cases], np.int32),
+        manhattan=np.array([c[3] == "manhattan" for c in cases]), algo=np.array([c[4] for c in cases]),
+        found=np.array([r["found"] for r in res]), cost=np.array([r["cost"] for r in res], np.float64),
+        path=path_flat, path_off=path_off, expand=exp_flat, expand_off=exp_off, exp_parent=par_flat, exp_g=g_flat)
+    print("theta2d", sum(r["found"] for r in res), "found of", len(cases), "readme costs",
+          [r["cost"] for r in res[:4]])
+
+
 SECTIONS = dict(rrt=sec_rrt, mpc=sec_mpc, dwa=sec_dwa, local_plans=sec_local_plans, lqr=sec_lqr, astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
                 dstar=sec_dstar, astar3d=sec_astar3d,
-                graph2d=sec_graph2d, graph3d=sec_graph3d, theta3d=sec_theta3d)
+                graph2d=sec_graph2d, graph3d=sec_graph3d, theta3d=sec_theta3d, theta2d=sec_theta2d)
 
 if __name__ == "__main__":
     want = sys.argv[1:] or list(SECTIONS)

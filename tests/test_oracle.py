@@ -303,6 +303,23 @@ def test_graph2d_dijkstra_gbfs_against_reference():
     assert n > 100
 
 
+def test_theta2d_against_reference():
+    """ThetaStar.plan (theta_star.py:44-94) / LazyThetaStar.plan (lazy_theta_star.py:38-101): README
+    grid + random grids up to 160x160, cost bits, path and closure order as the reference produced."""
+    n = 0
+    for i, occ, z in grid_cases("theta2d_small.npz"):
+        heur = "manhattan" if z["manhattan"][i] else "euclidean"
+        r = O.astar2d(occ, z["start"][i], z["goal"][i], heur, algo=str(z["algo"][i]))
+        if not z["found"][i]:
+            assert r["status"] == 1, i
+            continue
+        assert r["status"] == 0, i
+        assert r["cost"] == z["cost"][i], i
+        assert np.array_equal(r["path_cells"], seg(z["path"], z["path_off"], i)), i
+        assert np.array_equal(r["expand_cells"], seg(z["expand"], z["expand_off"], i)), i
+        n += 1
+    assert n > 140
+
 def test_graph3d_published_csv():
     """The reference's published Dijkstra3D / GBFS3D rows of 3d_pathfinding_results.csv."""
     from python_motion_planning_amd import workloads as wl
