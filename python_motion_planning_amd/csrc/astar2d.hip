@@ -48,28 +48,37 @@ constexpr uint32_t kMx1 = 0x1A90u, kMy1 = 0x01A9u;
 __device__ __forceinline__ int mot_x(int d) { return (int)((kMx1 >> (2 * d)) & 3u) - 1; }
 __device__ __forceinline__ int mot_y(int d) { return (int)((kMy1 >> (2 * d)) & 3u) - 1; }
 
+// HEUR (a template parameter, so key computations carry no runtime branch): bits 0-1 = the
+// heuristic -- 0 euclidean, 1 manhattan (GraphSearcher.h, graph_search.py:41-44), 2 zero (Dijkstra's
+// node_n.h = 0, dijkstra.py:74); bit 2 = the Theta* entry layout: a 5-bit code instead of the 4-bit
+// dir (code 16 + dir = "path 2": the parent is the pusher's own parent, theta_star.py:104-108) and a
+// 13-bit dy field (H <= 4096).
+constexpr int kThetaLayout = 4;
+template <int HEUR> constexpr int hkind() { return HEUR & 3; }
+template <int HEUR> constexpr int dbits() { return (HEUR & kThetaLayout) ? 5 : 4; }
+template <int HEUR>
 __device__ __forceinline__ uint32_t pack_cm(int dx, int dy, int dir)
 {
-    return ((uint32_t)dx << 18) | (((uint32_t)dy & 0x3fffu) << 4) | (uint32_t)dir;
+    constexpr int S = dbits<HEUR>();
+    return ((uint32_t)dx << 18) | (((uint32_t)dy & ((1u << (18 - S)) - 1u)) << S) | (uint32_t)dir;
 }
-__device__ __forceinline__ int cm_dx(uint32_t cm) { return (int)cm >> 18; }
-__device__ __forceinline__ int cm_dy(uint32_t cm) { return (int)(cm << 14) >> 18; }
+template <int HEUR> __device__ __forceinline__ int cm_dx(uint32_t cm) { return (int)cm >> 18; }
+template <int HEUR> __device__ __forceinline__ int cm_dy(uint32_t cm) { return (int)(cm << 14) >> (14 + dbits<HEUR>()); }
+template <int HEUR> __device__ __forceinline__ int cm_dir(uint32_t cm) { return (int)(cm & ((1u << dbits<HEUR>()) - 1u)); }
 
-// HEUR: 0 euclidean, 1 manhattan (GraphSearcher.h, graph_search.py:41-44), 2 zero (Dijkstra's
-// node_n.h = 0, dijkstra.py:74) -- a template parameter, so key computations carry no runtime
-// branch.  The order key of h.
+// The order key of h.
 template <int HEUR>
 __device__ __forceinline__ uint32_t hkey(uint32_t cm)
 {
-    if (HEUR == 2) return 0u;
-    const int dx = cm_dx(cm), dy = cm_dy(cm);
-    if (HEUR == 1) return (uint32_t)(abs(dx) + abs(dy));
+    if (hkind<HEUR>() == 2) return 0u;
+    const int dx = cm_dx<HEUR>(cm), dy = cm_dy<HEUR>(cm);
+    if (hkind<HEUR>() == 1) return (uint32_t)(abs(dx) + abs(dy));
     return (uint32_t)(__mul24(dx, dx) + __mul24(dy, dy));
 }
 template <int HEUR>
 __device__ __forceinline__ double h_of_key(uint32_t hk)
 {
-    return HEUR == 2 ? 0.0 : (HEUR == 1 ? (double)hk : __dsqrt_rn((double)hk));
+    return hkind<HEUR>() == 2 ? 0.0 : (hkind<HEUR>() == 1 ? (double)hk : __dsqrt_rn((double)hk));
 }
 
 // Node.__lt__ (node.py:51-54) -- evaluated without short-circuit branches
@@ -483,11 +492,46 @@ __device__ __forceinline__ void push_any(const Heap& h, int n, double itf, uint3
     else heap_push<true, true, HEUR>(h, n, itf, itc, itk, lastf, lastc, rootf, rootc, lane);
 }
 
+// ThetaStar.lineOfSight (theta_star.py:110-171): Bresenham from (x1, y1) to (x2, y2) over the bit
+// grid; tau = (d_y - d_x) / 2 is compared as 2e against d_y - d_x.  Both endpoints are in the grid
+// (they are cells the search reached), so the line stays inside its bounding box.  The step bound
+// is never reached by the reference's loop; it only guarantees termination.
+__device__ __forceinline__ bool occ_bit(const uint32_t* occ, int H, int x, int y)
+{
+    const uint32_t ci = (uint32_t)x * (uint32_t)H + (uint32_t)y;
+    return ((occ[ci >> 5] >> (ci & 31u)) & 1u) != 0u;
+}
+__device__ bool los2d(const uint32_t* occ, int H, int x1, int y1, int x2, int y2)
+{
+    if (occ_bit(occ, H, x1, y1) || occ_bit(occ, H, x2, y2)) return false;
+    const int dx = abs(x2 - x1), dy = abs(y2 - y1);
+    const int sx = x2 > x1 ? 1 : (x2 < x1 ? -1 : 0), sy = y2 > y1 ? 1 : (y2 < y1 ? -1 : 0);
+    int x = x1, y = y1, e = 0;
+    const bool xmaj = dx > dy;
+    const int T = xmaj ? dy - dx : dx - dy;
+    const int du = xmaj ? dx : dy, dv = xmaj ? dy : dx;  // major / minor deltas
+    for (int it = 0; it <= dx + dy + 1; it++) {
+        if (xmaj ? x == x2 : y == y2) return true;
+        const bool maj = 2 * e >= T, mino = 2 * e <= T;  // e > tau: major step; e < tau: minor; equal: both
+        if (maj) {
+            if (xmaj) x += sx; else y += sy;
+        }
+        if (mino) {
+            if (xmaj) y += sy; else x += sx;
+        }
+        e += (maj ? -dv : 0) + (mino ? du : 0);
+        if (occ_bit(occ, H, x, y)) return false;
+    }
+    return false;
+}
+
 // 4-bit cell state: word i >> 3, nibble i & 7
 __device__ __forceinline__ uint32_t cst_at(const uint32_t* cst, uint32_t i) { return (cst[i >> 3] >> ((i & 7) * 4)) & 15u; }
 
 // GZERO: GBFS (gbfs.py:73-75) -- every pushed node gets g = 0, so f = h and G is never needed.
-template <int HEUR, bool GZERO>
+// THETA: 1 = ThetaStar (theta_star.py:44-108), 2 = LazyThetaStar (lazy_theta_star.py:38-114); the
+// parent of a node is any cell, kept per CLOSED cell in P_all (HEUR carries the Theta* layout).
+template <int HEUR, bool GZERO, int THETA>
 __global__ __launch_bounds__(64) void astar2d_kernel(
     const uint32_t* __restrict__ occ, int W, int H, const int32_t* __restrict__ start_xy,
     const int32_t* __restrict__ goal_xy, const int32_t* __restrict__ order, int nq, double* __restrict__ cost_out,
@@ -496,7 +540,7 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
     int64_t* __restrict__ counters, int32_t* __restrict__ status_out, int* __restrict__ queue,
     uint4* __restrict__ spill_all, int heap_cap, int lds_cap, uint32_t* __restrict__ cst_all, size_t cst_words,
     double* __restrict__ G_all, uint32_t* __restrict__ hbits_all, size_t hbits_words, int prio_n,
-    unsigned long long* __restrict__ span)
+    unsigned long long* __restrict__ span, uint32_t* __restrict__ P_all)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
@@ -514,6 +558,7 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
     hp.cap = lds_cap;
     uint32_t* cst = cst_all + (size_t)worker * cst_words;
     double* G = G_all + (size_t)worker * ((size_t)W * (size_t)H);
+    uint32_t* Pc = THETA ? P_all + (size_t)worker * ((size_t)W * (size_t)H) : nullptr;  // CLOSED parent cell
 
     // ---- per-lane constants
     // this lane's cell of the 3x3 block: lane i < 9 -> occupancy of (x + i/3 - 1, y + i%3 - 1),
@@ -571,7 +616,7 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
 
         // heap[0] in registers (wave-uniform): Node(start, start, 0, 0), key (0, h = 0)
         double rootf = 0.0;
-        uint32_t rootc = pack_cm(0, 0, 8);
+        uint32_t rootc = pack_cm<HEUR>(0, 0, 8);
         double lastf = rootf;  // heap[n - 1]
         uint32_t lastc = rootc;
         if (lane == 0) hst<true>(hp, true, 0, rootf, rootc);
@@ -594,9 +639,9 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
             const uint32_t v01 = hp.B[lane <= 32 ? lane : 0];  // bit words for the pop below
             npop++;
             n -= 1;
-            const int ndir = (int)(ncm & 15u);
-            const int x = ndir == 8 ? sx : gx - cm_dx(ncm);
-            const int y = ndir == 8 ? sy : gy - cm_dy(ncm);
+            const int ndir = cm_dir<HEUR>(ncm);
+            const int x = ndir == 8 ? sx : gx - cm_dx<HEUR>(ncm);
+            const int y = ndir == 8 ? sy : gy - cm_dy<HEUR>(ncm);
             const uint32_t nlin = (uint32_t)x * (uint32_t)H + (uint32_t)y;
 
             // ---- HBM round, issued before the LDS pop so the two overlap: one unconditional load
@@ -612,7 +657,14 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 blk_word = *ptr;
             }
             double gpar = 0.0;  // G[parent] (the parent closed earlier); the start has g = 0
-            if (!GZERO && ndir < 8) {
+            uint32_t ppar = 0u;  // Theta* path 2: the pusher's CLOSED parent
+            if (THETA) {
+                if (ndir != 8) {
+                    const uint32_t plin = nlin - (uint32_t)rl_u32((uint32_t)par_off, ndir & 7);
+                    if (lane == 18) gpar = G[plin];
+                    if (lane == 19 && ndir >= 16) ppar = Pc[plin];
+                }
+            } else if (!GZERO && ndir < 8) {
                 const uint32_t plin = nlin - (uint32_t)rl_u32((uint32_t)par_off, ndir);
                 if (lane == 18) gpar = G[plin];
             }
@@ -642,17 +694,83 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
 
             // CLOSED[node.current] = node (a_star.py:82).  The node's state word was loaded by lane 13
             // and only this wave writes it: store it back now (fire-and-forget, off the critical path).
-            const double gnode = (GZERO || ndir == 8) ? 0.0 : rl_f64(gpar, 18) + ((ndir & 1) ? kSqrt2 : 1.0);
-            if (lane == 13) cst[nlin >> 3] = blk_word | ((uint32_t)(ndir + 1) << blk_sh);
+            double gnode = (GZERO || ndir == 8) ? 0.0 : rl_f64(gpar, 18) + ((ndir & 1) ? kSqrt2 : 1.0);
+            // Theta*: the node's parent (cell, coordinates, g) and its expand-record code
+            uint32_t par_lin = nlin;
+            int px = x, py = y, ecode = ndir;
+            double gp_g = 0.0;
+            if (THETA && ndir != 8) {
+                const uint32_t pusher = nlin - (uint32_t)rl_u32((uint32_t)par_off, ndir & 7);
+                gp_g = rl_f64(gpar, 18);
+                par_lin = pusher;
+                if (ndir >= 16) {  // path 2: node.g = parent.g + dist (theta_star.py:106-108)
+                    par_lin = rl_u32(ppar, 19);
+                    double t = 0.0;
+                    if (lane == 18) t = G[par_lin];
+                    gp_g = rl_f64(t, 18);
+                }
+                px = (int)(par_lin / (uint32_t)H);
+                py = (int)(par_lin - (uint32_t)px * (uint32_t)H);
+                gnode = gp_g + ((ndir >= 16) ? __dsqrt_rn((double)((x - px) * (x - px) + (y - py) * (y - py)))
+                                             : ((ndir & 1) ? kSqrt2 : 1.0));
+                if (THETA == 2 && !los2d(occ, H, px, py, x, y)) {
+                    // set vertex (lazy_theta_star.py:55-65): the first CLOSED, collision-free
+                    // neighbour minimising its g + dist becomes the parent; g = inf if there is none
+                    const bool cand = lane < 8 && (occ9 & need) == 0u && (cls9 & self_bit) != 0u;
+                    double gn = 0.0;
+                    if (cand) gn = G[nlin + (uint32_t)par_off];
+                    const double gc = gn + mcost;
+                    uint64_t cmask = ballot(cand) & 0xffull;
+                    double best = __longlong_as_double(0x7ff0000000000000ll);
+                    int bm = -1;
+                    while (cmask) {
+                        const int m = __ffsll((long long)cmask) - 1;
+                        cmask &= cmask - 1;
+                        const double c = rl_f64(gc, m);
+                        if (best > c) { best = c; bm = m; }
+                    }
+                    gnode = best;
+                    if (bm >= 0) {
+                        gp_g = rl_f64(gn, bm);
+                        px = x + mot_x(bm);
+                        py = y + mot_y(bm);
+                        par_lin = (uint32_t)px * (uint32_t)H + (uint32_t)py;
+                        ecode = 24 + bm;
+                    } else {
+                        ecode |= 32;
+                    }
+                }
+            }
+            if (lane == 13) cst[nlin >> 3] = blk_word | ((uint32_t)(THETA ? 1 : ndir + 1) << blk_sh);
             if (!GZERO && lane == 14) G[nlin] = gnode;
+            if (THETA && lane == 15) Pc[nlin] = par_lin;
             if (lane == 0 && expand_out && nexp < expand_cap)
-                expand_out[(size_t)q * expand_cap + nexp] = nlin | ((uint32_t)ndir << 28);
+                expand_out[(size_t)q * expand_cap + nexp] = THETA ? (nlin | ((uint32_t)ecode << 26)) : (nlin | ((uint32_t)ndir << 28));
             nexp++;
 
             if (x == gx && y == gy) {  // goal found (a_star.py:61-64)
                 st = PMP_FOUND;
                 wave_sync_mem();
-                if (lane == 0) {  // extractPath (a_star.py:98-117): goal -> start, cost in that order
+                if (THETA && lane == 0) {  // extractPath via the CLOSED parents (any cell), hypot per hop
+                    uint32_t li = nlin;
+                    int cx = x, cy = y;
+                    double cost = 0.0;
+                    int len = 0;
+                    uint32_t* pth = path_out + (size_t)q * path_cap;
+                    for (;;) {
+                        if (len < path_cap) pth[len] = li;
+                        len++;
+                        if (cx == sx && cy == sy) break;
+                        const uint32_t pl = Pc[li];
+                        const int qx = (int)(pl / (uint32_t)H), qy = (int)(pl - (uint32_t)qx * (uint32_t)H);
+                        cost += __dsqrt_rn((double)((cx - qx) * (cx - qx) + (cy - qy) * (cy - qy)));
+                        cx = qx;
+                        cy = qy;
+                        li = pl;
+                    }
+                    goal_cost = cost;
+                    plen = len;
+                } else if (lane == 0) {  // extractPath (a_star.py:98-117): goal -> start, cost in that order
                     int cx = x, cy = y;
                     double cost = 0.0;
                     int len = 0;
@@ -680,9 +798,22 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
             const uint64_t gm = ballot(nb_ok && ndx == 0 && ndy == 0) & 0xffull;
             if (gm) vm &= (gm << 1) - 1;
             // Node + motion (node.py:39-41), h = GraphSearcher.h (graph_search.py:41-44)
-            const uint32_t icm = pack_cm(ndx, ndy, mo);
+            double ig = gnode + mcost;
+            int icode = mo;
+            if (THETA && ndir != 8) {
+                // updateVertex(CLOSED[node.parent], node_n) (theta_star.py:96-108; lazy_theta_star.py:
+                // 103-114 without the line of sight): path 2 when parent.g + dist <= node_n.g
+                const int nxl = x + mx, nyl = y + my;
+                const double g2 =
+                    gp_g + __dsqrt_rn((double)((px - nxl) * (px - nxl) + (py - nyl) * (py - nyl)));
+                if (lane < 8 && (vm >> lane & 1ull) && g2 <= ig && (THETA == 2 || los2d(occ, H, nxl, nyl, px, py))) {
+                    ig = g2;
+                    icode = 16 + mo;
+                }
+            }
+            const uint32_t icm = pack_cm<HEUR>(ndx, ndy, icode);
             const uint32_t ik = hkey<HEUR>(icm);
-            const double ifv = (gnode + mcost) + h_of_key<HEUR>(ik);
+            const double ifv = ig + h_of_key<HEUR>(ik);
             bool overflow = false;
             while (vm) {
                 const int m = __ffsll((long long)vm) - 1;
@@ -832,8 +963,12 @@ extern "C" int pmp_graph2d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
                                  int32_t* status)
 {
     if (!ctx) return PMP_EINVAL;
-    if (algo < PMP_ALGO_ASTAR || algo > PMP_ALGO_GBFS)
-        return pmp_set_err(ctx, PMP_EINVAL, "pmp_graph2d_batch: algo must be 0 (AStar), 1 (Dijkstra) or 2 (GBFS)");
+    if (algo < PMP_ALGO_ASTAR || algo > PMP_ALGO_LAZY_THETA)
+        return pmp_set_err(ctx, PMP_EINVAL,
+                           "pmp_graph2d_batch: algo must be 0 (AStar), 1 (Dijkstra), 2 (GBFS), 3 (ThetaStar) or 4 (LazyThetaStar)");
+    const bool theta = algo == PMP_ALGO_THETA || algo == PMP_ALGO_LAZY_THETA;
+    if (theta && H > 4096)  // the Theta* entry layout keeps a 13-bit dy (and expand records 26-bit cells)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_graph2d_batch: ThetaStar / LazyThetaStar need H <= 4096");
     if (W < 1 || H < 1 || W > kMaxDim || H > kMaxDim)
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_batch: W and H must be in [1, 8192]");
     if (heuristic != 0 && heuristic != 1) return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_batch: heuristic must be 0 or 1");
@@ -870,13 +1005,22 @@ extern "C" int pmp_graph2d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
         hipLaunchKernelGGL(lpt_scan, dim3(1), dim3(64), 0, s, nb, hist);
         hipLaunchKernelGGL(lpt_scatter, dim3((nq + 255) / 256), dim3(256), 0, s, start_xy, goal_xy, nq, nb, hist, order);
     }
-    auto kern = algo == PMP_ALGO_DIJKSTRA ? astar2d_kernel<2, false>
-              : algo == PMP_ALGO_GBFS     ? (heuristic == 1 ? astar2d_kernel<1, true> : astar2d_kernel<0, true>)
-                                          : (heuristic == 1 ? astar2d_kernel<1, false> : astar2d_kernel<0, false>);
+    uint32_t* par = nullptr;
+    if (theta) {
+        par = (uint32_t*)pmp_scratch(ctx, SCR_PAR, (size_t)workers * ncell * 4);
+        if (!par) return PMP_ENOMEM;
+    }
+    constexpr int TL = kThetaLayout;
+    auto kern = algo == PMP_ALGO_DIJKSTRA ? astar2d_kernel<2, false, 0>
+              : algo == PMP_ALGO_GBFS     ? (heuristic == 1 ? astar2d_kernel<1, true, 0> : astar2d_kernel<0, true, 0>)
+              : algo == PMP_ALGO_THETA    ? (heuristic == 1 ? astar2d_kernel<TL | 1, false, 1> : astar2d_kernel<TL, false, 1>)
+              : algo == PMP_ALGO_LAZY_THETA ? (heuristic == 1 ? astar2d_kernel<TL | 1, false, 2> : astar2d_kernel<TL, false, 2>)
+                                          : (heuristic == 1 ? astar2d_kernel<1, false, 0> : astar2d_kernel<0, false, 0>);
     hipLaunchKernelGGL(kern, dim3(workers), dim3(64), lds, s, occ_bits, W, H, start_xy,
                        goal_xy, (const int32_t*)order, nq, cost, path_len, path, path_cap, n_expanded, expand,
                        expand_cap, counters, status, queue, spill, ctx->astar_heap_cap, ctx->astar_lds_cap, cst, cst_words, G,
-                       (uint32_t*)ctx->buf[SCR_BITS], hbits_words(ctx->astar_heap_cap), order ? ctx->astar_prio_n : 0, ctx->span);
+                       (uint32_t*)ctx->buf[SCR_BITS], hbits_words(ctx->astar_heap_cap), order ? ctx->astar_prio_n : 0, ctx->span,
+                       par);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }

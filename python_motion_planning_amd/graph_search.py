@@ -121,6 +121,60 @@ class GBFS(AStar):
         return "Greedy Best First Search(GBFS)"
 
 
+class ThetaStar(AStar):
+    """Theta* (theta_star.py:13-171): AStar's loop where a neighbour takes the expanded node's parent
+    as its own when that parent sees it (Bresenham lineOfSight) and is no farther (updateVertex,
+    :96-108).  Same kernel as AStar, with any-cell parents kept per CLOSED cell."""
+
+    _algo = "theta_star"
+
+    def __str__(self) -> str:
+        return "Theta*"
+
+    def _expand_nodes(self, exp: np.ndarray, H: int) -> list:
+        """CLOSED Node objects from the kernel's (cell | code << 26) records.  code: 0-7 = path 1
+        through motion d, 8 = start, 16 + d = path 2 (the pusher's own parent), 24 + d = Lazy Theta*'s
+        re-parenting to the CLOSED neighbour in motion d; + 32 = no parent found (g = inf)."""
+        motions = self.env.motions
+        nodes, gmap, pmap = [], {}, {}
+        for e in exp.tolist():
+            cell, code = e & 0x03FFFFFF, e >> 26
+            cur = (cell // H, cell % H)
+            d = code & 7
+            m = motions[d]
+            if code == 8:
+                node = Node(cur, cur, 0, 0)
+            else:
+                base = code & 31
+                if base >= 24:
+                    par = (cur[0] + m.x, cur[1] + m.y)
+                    g = gmap[par] + m.g
+                else:
+                    pusher = (cur[0] - m.x, cur[1] - m.y)
+                    if base >= 16:
+                        par = pmap[pusher]
+                        g = gmap[par] + self.dist(Node(cur), Node(par))
+                    else:
+                        par = pusher
+                        g = gmap[par] + m.g
+                if code & 32:
+                    g = float("inf")
+                node = Node(cur, par, g, self.h(Node(cur), self.goal))
+            gmap[cur], pmap[cur] = node.g, node.parent
+            nodes.append(node)
+        return nodes
+
+
+class LazyThetaStar(ThetaStar):
+    """Lazy Theta* (lazy_theta_star.py:13-114): updateVertex without the line of sight at the push;
+    the line of sight is checked when the node pops (:55-65).  Same kernel."""
+
+    _algo = "lazy_theta_star"
+
+    def __str__(self) -> str:
+        return "Lazy Theta*"
+
+
 class DStar(GraphSearcher):
     """Dynamic A* (d_star.py:37-291) -- the static plan (processState until the start is CLOSED)
     runs in the gfx950 kernel dstar.hip with the reference's list-semantics OPEN."""

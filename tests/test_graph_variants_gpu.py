@@ -187,3 +187,62 @@ def test_theta3d_c5_batch_against_oracle():
             ref = O.theta3d(occ[q], S[q], G[q], lazy=lazy, with_expand=False)
             assert cost[q] == ref["cost"] and ne[q] == ref["n_expanded"], (lazy, q)
             assert np.array_equal(P[q, : pl[q]], ref["path_cells"]), (lazy, q)
+
+
+def test_theta2d_against_reference():
+    """ThetaStar / LazyThetaStar 2D (theta_star.py, lazy_theta_star.py) on astar2d.hip vs the reference's
+    runs (tests/golden/theta2d_small.npz): cost bits, path, closure order; the drop-in classes rebuild
+    the reference's CLOSED nodes (parent, g) from the kernel's expand records."""
+    import python_motion_planning_amd as pmp
+    from python_motion_planning_amd import batch
+
+    n = 0
+    for i, occ, z in grid_cases("theta2d_small.npz"):
+        W, H = occ.shape
+        heur = "manhattan" if z["manhattan"][i] else "euclidean"
+        algo = str(z["algo"][i])
+        r = batch.astar2d_batch(occ, z["start"][i][None], z["goal"][i][None], heur, path_cap=W * H + 1,
+                                expand_cap=W * H, algo=algo)
+        st = int(r["status"][0])
+        if not z["found"][i]:
+            assert st == 1, i
+            continue
+        assert st == 0, i
+        assert float(r["cost"][0]) == z["cost"][i], i
+        plen = int(r["path_len"][0])
+        assert np.array_equal(r["path"][0, :plen].cpu().numpy(), seg(z["path"], z["path_off"], i)), i
+        ne = int(r["n_expanded"][0])
+        e = (r["expand"][0, :ne].cpu().numpy().astype(np.uint32) & 0x03FFFFFF).astype(np.int32)
+        assert np.array_equal(e, seg(z["expand"], z["expand_off"], i)), i
+        if i % 5 == 0:  # drop-in class: the CLOSED nodes' parents and g as the reference holds them
+            env = pmp.Grid(W, H)
+            env.update({(int(a), int(b)) for a, b in np.argwhere(occ)})
+            cls = pmp.LazyThetaStar if algo == "lazy_theta_star" else pmp.ThetaStar
+            cost, path, expand = cls(tuple(z["start"][i]), tuple(z["goal"][i]), env, heur).plan()
+            assert cost == z["cost"][i] and [a * H + b for a, b in path] == seg(z["path"], z["path_off"], i).tolist()
+            par = seg(z["exp_parent"], z["expand_off"], i).tolist()
+            assert [nd.parent[0] * H + nd.parent[1] for nd in expand] == par, i
+            assert [nd.g for nd in expand] == seg(z["exp_g"], z["expand_off"], i).tolist(), i
+        n += 1
+    assert n > 140
+
+
+def test_theta2d_c2_subset_against_oracle():
+    """ThetaStar / LazyThetaStar on the C2 1024x1024 grid (20 % obstacles): 16 queries each, bit-exact
+    cost, path, closure count and push/pop counts."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import batch, workloads as wl
+
+    occ, s, g = wl.c2_workload(4096)
+    idx = np.arange(0, 4096, 257)[:16]
+    for algo in ("theta_star", "lazy_theta_star"):
+        r = batch.astar2d_batch(occ, s[idx], g[idx], path_cap=8192, counters=True, algo=algo)
+        ref = O.astar2d_batch(occ, s[idx], g[idx], path_cap=8192, algo=algo)
+        assert np.array_equal(r["status"].cpu().numpy(), ref["status"]), algo
+        assert np.array_equal(r["cost"].cpu().numpy(), ref["cost"]), algo
+        assert np.array_equal(r["n_expanded"].cpu().numpy(), ref["n_expanded"]), algo
+        assert np.array_equal(r["counters"].cpu().numpy(), ref["counters"]), algo
+        P = r["path"].cpu().numpy()
+        for k in range(len(idx)):
+            n = ref["path_len"][k]
+            assert np.array_equal(P[k, :n], ref["path"][k, :n]), (algo, k)

@@ -63,3 +63,11 @@ def test_factory_names_dijkstra_gbfs():
     env = pmp.Grid(51, 31)
     assert type(pmp.SearchFactory()("dijkstra", start=(5, 5), goal=(45, 25), env=env)).__name__ == "Dijkstra"
     assert type(pmp.SearchFactory()("gbfs", start=(5, 5), goal=(45, 25), env=env)).__name__ == "GBFS"
+
+
+def test_factory_names_theta_2d():
+    import python_motion_planning_amd as pmp
+
+    env = pmp.Grid(51, 31)
+    assert type(pmp.SearchFactory()("theta_star", start=(5, 5), goal=(45, 25), env=env)).__name__ == "ThetaStar"
+    assert type(pmp.SearchFactory()("lazy_theta_star", start=(5, 5), goal=(45, 25), env=env)).__name__ == "LazyThetaStar"
