@@ -78,8 +78,12 @@ enum { PMP_ALGO_ASTAR = 0, PMP_ALGO_DIJKSTRA = 1, PMP_ALGO_GBFS = 2, PMP_ALGO_TH
  * Batched 2D AStar / Dijkstra / GBFS.  algo = PMP_ALGO_ASTAR is pmp_astar2d_batch;
  * PMP_ALGO_DIJKSTRA replaces Dijkstra.plan (global_planner/graph_search/dijkstra.py:36-85: node_n.h
  * = 0, so `heuristic` is unused); PMP_ALGO_GBFS replaces GBFS.plan (gbfs.py:36-86: node_n.g = 0,
- * ordered by h).  Same loop, CPython heap ties, goal -> start path and arguments as
- * pmp_astar2d_batch; cost is extractPath's (a_star.py:98-117) for all three.
+ * ordered by h).  PMP_ALGO_THETA replaces ThetaStar.plan (theta_star.py:44-171: updateVertex with
+ * the Bresenham lineOfSight) and PMP_ALGO_LAZY_THETA LazyThetaStar.plan (lazy_theta_star.py:38-114:
+ * the line of sight at the pop); both need H <= 4096, and their expand records are
+ * cell | code << 26 (code 0-7 path 1 via motion d, 8 start, 16+d path 2, 24+d Lazy Theta*'s
+ * re-parenting to the CLOSED neighbour in motion d, +32 g = inf).  Same loop, CPython heap ties,
+ * goal -> start path and arguments as pmp_astar2d_batch; cost is extractPath's (a_star.py:98-117).
  */
 int pmp_graph2d_batch(pmp_ctx* ctx, void* stream, int algo, const uint32_t* occ_bits, int W, int H, int heuristic,
                       const int32_t* start_xy, const int32_t* goal_xy, int nq, double* cost,
