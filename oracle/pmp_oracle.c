@@ -1791,3 +1791,174 @@ int oracle_astar3d_batch(const uint8_t* occ, int X, int Y, int Z, int heuristic,
 {
     return oracle_graph3d_batch(0, occ, X, Y, Z, heuristic, s, g, nq, cost, status, nthreads);
 }
+
+/* ------------------------------------------------------------------------------------ */
+/* LPAStar.plan (global_planner/graph_search/lpa_star.py:78-87): computeShortestPath      */
+/* (:139-160) + extractPath (:209-230).  U is the reference's Python list, restated as   */
+/* a list: `min(U, key=key)` = first minimal element in list order, `U.remove` shifts    */
+/* the tail left, `heapq.heappush` appends and sifts by LNode.__lt__ (key list compare,  */
+/* :32-33) on whatever order the list holds.                                           */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+    int32_t* cell;
+    double *k1, *k2;
+    int64_t n;
+} ulist_t;
+
+static inline int key_lt(double a1, double a2, double b1, double b2) { return a1 < b1 || (a1 == b1 && a2 < b2); }
+
+static void u_remove(ulist_t* U, int32_t* pos, int64_t i)
+{
+    for (int64_t j = i; j + 1 < U->n; j++) {
+        U->cell[j] = U->cell[j + 1];
+        U->k1[j] = U->k1[j + 1];
+        U->k2[j] = U->k2[j + 1];
+        pos[U->cell[j]] = (int32_t)j;
+    }
+    U->n--;
+}
+
+static void u_push(ulist_t* U, int32_t* pos, int32_t c, double k1, double k2)
+{
+    int64_t p = U->n++;
+    while (p > 0) { /* Lib/heapq.py _siftdown */
+        int64_t q = (p - 1) >> 1;
+        if (!key_lt(k1, k2, U->k1[q], U->k2[q])) break;
+        U->cell[p] = U->cell[q];
+        U->k1[p] = U->k1[q];
+        U->k2[p] = U->k2[q];
+        pos[U->cell[p]] = (int32_t)p;
+        p = q;
+    }
+    U->cell[p] = c;
+    U->k1[p] = k1;
+    U->k2[p] = k2;
+    pos[c] = (int32_t)p;
+}
+
+/* GraphSearcher.h of the LPA* key (:181-194): euclidean hypot or manhattan */
+static inline double lpa_h(int heuristic, int x, int y, int gx, int gy)
+{
+    return heuristic == 1 ? (double)(abs(gx - x) + abs(gy - y)) : vnorm2((double)(gx - x), (double)(gy - y));
+}
+
+/* updateVertex (:162-179).  Returns 4 when the reference raises (KeyError off the map, or min()
+ * of an empty neighbour list). */
+static int lpa_update(const uint8_t* occ, int W, int H, int heuristic, int32_t start, int gx, int gy, double* g,
+                      double* rhs, int32_t* pos, ulist_t* U, int32_t v, int64_t* npush)
+{
+    const int x = v / H, y = v % H;
+    if (v != start) {
+        double best = INFINITY;
+        int any = 0;
+        for (int m = 0; m < 8; m++) { /* getNeighbor (:196-207): map lookup, then the obstacle filter */
+            const int ux = x + MX8[m], uy = y + MY8[m];
+            if (ux < 0 || uy < 0 || ux >= W || uy >= H) return 4;
+            if (occ[(int64_t)ux * H + uy]) continue;
+            const double c = collide2(occ, W, H, ux, uy, x, y) ? INFINITY : ((m & 1) ? sqrt(2.0) : 1.0);
+            const double val = g[ux * H + uy] + c;
+            if (!any || val < best) best = val;
+            any = 1;
+        }
+        if (!any) return 4;
+        rhs[v] = best;
+    }
+    if (pos[v] >= 0) {
+        const int64_t i = pos[v];
+        pos[v] = -1;
+        u_remove(U, pos, i);
+    }
+    if (g[v] != rhs[v]) {
+        const double mn = g[v] < rhs[v] ? g[v] : rhs[v];
+        u_push(U, pos, v, mn + lpa_h(heuristic, x, y, gx, gy), mn);
+        (*npush)++;
+    }
+    return 0;
+}
+
+/* status 0 found, 1 extractPath gave up after 1000 steps (cost kept, path empty), 4 the reference
+ * raises (U empties: min() of an empty list; or KeyError / empty neighbour list).
+ * path: start -> goal.  counters: {pushes, expansions (len(EXPAND)), path steps, max |U|}. */
+int oracle_lpastar2d(const uint8_t* occ, int W, int H, int heuristic, int sx, int sy, int gx, int gy,
+                     double* cost_out, int32_t* path, int path_cap, int32_t* path_len, int64_t* counters)
+{
+    const int64_t ncell = (int64_t)W * H;
+    double* g = (double*)malloc(sizeof(double) * (size_t)ncell);
+    double* rhs = (double*)malloc(sizeof(double) * (size_t)ncell);
+    int32_t* pos = (int32_t*)malloc(sizeof(int32_t) * (size_t)ncell);
+    ulist_t U = {(int32_t*)malloc(sizeof(int32_t) * (size_t)ncell), (double*)malloc(sizeof(double) * (size_t)ncell),
+                 (double*)malloc(sizeof(double) * (size_t)ncell), 0};
+    int64_t npush = 0, nexp = 0, maxn = 0, steps = 0;
+    int status = 0;
+    *cost_out = 0.0;
+    *path_len = 0;
+    for (int64_t i = 0; i < ncell; i++) { g[i] = INFINITY; rhs[i] = INFINITY; pos[i] = -1; }
+    const int32_t start = sx * H + sy, goal = gx * H + gy;
+    rhs[start] = 0.0; /* LNode(start, inf, 0.0, None) (:59) */
+    u_push(&U, pos, start, lpa_h(heuristic, sx, sy, gx, gy), 0.0);
+    npush++;
+    maxn = 1;
+    for (;;) {
+        if (U.n == 0) { status = 4; break; }
+        int64_t bi = 0;
+        for (int64_t i = 1; i < U.n; i++)
+            if (key_lt(U.k1[i], U.k2[i], U.k1[bi], U.k2[bi])) bi = i;
+        const double gm = g[goal] < rhs[goal] ? g[goal] : rhs[goal];
+        const double gk1 = gm + 0.0; /* calculateKey(goal): h(goal, goal) = 0 */
+        if (!key_lt(U.k1[bi], U.k2[bi], gk1, gm) && rhs[goal] == g[goal]) break;
+        const int32_t v = U.cell[bi];
+        pos[v] = -1;
+        u_remove(&U, pos, bi);
+        nexp++;
+        if (g[v] > rhs[v]) {
+            g[v] = rhs[v];
+        } else {
+            g[v] = INFINITY;
+            if ((status = lpa_update(occ, W, H, heuristic, start, gx, gy, g, rhs, pos, &U, v, &npush))) break;
+        }
+        const int x = v / H, y = v % H;
+        for (int m = 0; m < 8 && !status; m++) {
+            const int ux = x + MX8[m], uy = y + MY8[m];
+            if (ux < 0 || uy < 0 || ux >= W || uy >= H) { status = 4; break; }
+            if (occ[(int64_t)ux * H + uy]) continue;
+            status = lpa_update(occ, W, H, heuristic, start, gx, gy, g, rhs, pos, &U, ux * H + uy, &npush);
+        }
+        if (status) break;
+        if (U.n > maxn) maxn = U.n;
+    }
+    if (status == 0) { /* extractPath: greedy min-g neighbour from the goal, first minimum in motion order */
+        int32_t c = goal;
+        double cost = 0.0;
+        int64_t len = 0;
+        if (len < path_cap) path[len] = c;
+        len++;
+        while (c != start) {
+            const int x = c / H, y = c % H;
+            int bm = -1;
+            double bg = 0.0;
+            for (int m = 0; m < 8; m++) {
+                const int ux = x + MX8[m], uy = y + MY8[m];
+                if (ux < 0 || uy < 0 || ux >= W || uy >= H) { status = 4; break; }
+                if (occ[(int64_t)ux * H + uy] || collide2(occ, W, H, x, y, ux, uy)) continue;
+                if (bm < 0 || g[ux * H + uy] < bg) { bm = m; bg = g[ux * H + uy]; }
+            }
+            if (status) break;
+            if (bm < 0) { status = 4; break; }
+            cost += (bm & 1) ? sqrt(2.0) : 1.0;
+            c = (x + MX8[bm]) * H + (y + MY8[bm]);
+            if (len < path_cap) path[len] = c;
+            len++;
+            if (++steps == 1000) { status = 1; break; }
+        }
+        *cost_out = cost;
+        if (status == 0) {
+            if (len > path_cap) status = 2;
+            else
+                for (int64_t i = 0; i < len / 2; i++) { int32_t t = path[i]; path[i] = path[len - 1 - i]; path[len - 1 - i] = t; }
+            *path_len = (int32_t)len;
+        }
+    }
+    if (counters) { counters[0] = npush; counters[1] = nexp; counters[2] = steps; counters[3] = maxn; }
+    free(g); free(rhs); free(pos); free(U.cell); free(U.k1); free(U.k2);
+    return status;
+}
