@@ -1903,9 +1903,13 @@ int oracle_lpastar2d(const uint8_t* occ, int W, int H, int heuristic, int sx, in
         int64_t bi = 0;
         for (int64_t i = 1; i < U.n; i++)
             if (key_lt(U.k1[i], U.k2[i], U.k1[bi], U.k2[bi])) bi = i;
-        const double gm = g[goal] < rhs[goal] ? g[goal] : rhs[goal];
+        /* start == goal: self.goal is a separate LNode(goal, inf, inf) that map[] no longer holds
+         * (map[start] overwrote it, :62-63), so its g = rhs = inf forever and the loop only ends
+         * when U empties */
+        const double gg = start == goal ? INFINITY : g[goal], grhs = start == goal ? INFINITY : rhs[goal];
+        const double gm = gg < grhs ? gg : grhs;
         const double gk1 = gm + 0.0; /* calculateKey(goal): h(goal, goal) = 0 */
-        if (!key_lt(U.k1[bi], U.k2[bi], gk1, gm) && rhs[goal] == g[goal]) break;
+        if (!key_lt(U.k1[bi], U.k2[bi], gk1, gm) && grhs == gg) break;
         const int32_t v = U.cell[bi];
         pos[v] = -1;
         u_remove(&U, pos, bi);

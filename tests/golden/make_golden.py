@@ -4,7 +4,7 @@ Run in the build container only (the reference never travels to the GPU box):
 
     PYTHONDONTWRITEBYTECODE=1 MPLBACKEND=Agg python tests/golden/make_golden.py [section ...]
 
-Sections: astar_readme astar_small astar_1024 dstar astar3d graph2d graph3d theta3d theta2d rrt dwa lqr mpc hypot
+Sections: astar_readme astar_small astar_1024 dstar astar3d graph2d graph3d theta3d theta2d lpa rrt dwa lqr mpc hypot
 Outputs are small fixtures (inputs + expected outputs) under tests/golden/.  The reference is
 imported with stubs for the modules absent from this image (osqp, pyvista), per SURVEY.md §8(c).
 """
@@ -733,9 +733,63 @@ def sec_theta2d(n=160):
           [r["cost"] for r in res[:4]])
 
 
+# ----------------------------------------------------------------------------------------------
+# LPAStar (lpa_star.py) -- SURVEY.md §8(f) rank 3 (the initial computeShortestPath + extractPath)
+def run_lpa(args):
+    occ, start, goal, heur = args
+    pmp = import_reference()
+    W, H = occ.shape
+    env = pmp.Grid(W, H)
+    env.update(obstacles_of(occ))
+    p = pmp.LPAStar(tuple(start), tuple(goal), env, heur)
+    try:
+        cost, path, _ = p.plan()
+        err = ""
+    except (ValueError, KeyError) as e:
+        cost, path, err = float("nan"), [], type(e).__name__
+    close_figs()
+    return dict(cost=float(cost), path=[x * H + y for (x, y) in path], n_expand=len(p.EXPAND), err=err)
+
+
+def sec_lpa(n=120):
+    from python_motion_planning_amd import workloads as wl
+
+    rng = np.random.default_rng(8642)
+    cases = [(wl.readme_grid(), (5, 5), (45, 25), "euclidean"), (wl.readme_grid(), (5, 5), (45, 25), "manhattan")]
+    for i in range(n):
+        W = int(rng.integers(6, 41))
+        H = int(rng.integers(6, 41))
+        dens = float(rng.uniform(0.0, 0.35))
+        occ = (rng.random((W, H)) < dens).astype(np.uint8)
+        occ[:, 0] = occ[:, H - 1] = 1
+        occ[0, :] = occ[W - 1, :] = 1
+        free = np.argwhere(occ == 0)
+        if len(free) < 2:
+            occ[1, 1] = occ[W - 2, H - 2] = 0
+            free = np.argwhere(occ == 0)
+        s = free[rng.integers(len(free))]
+        g = free[rng.integers(len(free))]
+        if i % 19 == 4:
+            g = s
+        cases.append((occ, tuple(int(v) for v in s), tuple(int(v) for v in g), "manhattan" if i % 4 == 3 else "euclidean"))
+    with Pool(8) as pool:
+        res = pool.map(run_lpa, cases, chunksize=2)
+    dims = np.array([c[0].shape for c in cases], np.int32)
+    occ_flat, occ_off = ragged([np.packbits(c[0].ravel()) for c in cases], np.uint8)
+    path_flat, path_off = ragged([r["path"] for r in res])
+    np.savez_compressed(
+        os.path.join(HERE, "lpa_small.npz"), dims=dims, occ_bits=occ_flat, occ_off=occ_off,
+        start=np.array([c[1] for c in cases], np.int32), goal=np.array([c[2] for c in cases], np.int32),
+        manhattan=np.array([c[3] == "manhattan" for c in cases]), cost=np.array([r["cost"] for r in res]),
+        path=path_flat, path_off=path_off, n_expand=np.array([r["n_expand"] for r in res], np.int64),
+        err=np.array([r["err"] for r in res]))
+    print("lpa", sum(1 for r in res if r["path"]), "with path,", sum(1 for r in res if r["err"]), "raise, of", len(res),
+          "readme", res[0]["cost"], res[0]["n_expand"])
+
+
 SECTIONS = dict(rrt=sec_rrt, mpc=sec_mpc, dwa=sec_dwa, local_plans=sec_local_plans, lqr=sec_lqr, astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
                 dstar=sec_dstar, astar3d=sec_astar3d,
-                graph2d=sec_graph2d, graph3d=sec_graph3d, theta3d=sec_theta3d, theta2d=sec_theta2d)
+                graph2d=sec_graph2d, graph3d=sec_graph3d, theta3d=sec_theta3d, theta2d=sec_theta2d, lpa=sec_lpa)
 
 if __name__ == "__main__":
     want = sys.argv[1:] or list(SECTIONS)

@@ -320,6 +320,22 @@ def test_theta2d_against_reference():
         n += 1
     assert n > 140
 
+def test_lpastar_against_reference():
+    """LPAStar.plan (lpa_star.py:78-87, 139-230): README grid + random grids, cost bits, path,
+    len(EXPAND), and the runs where the reference raises (U empties; start == goal)."""
+    n = 0
+    for i, occ, z in grid_cases("lpa_small.npz"):
+        heur = "manhattan" if z["manhattan"][i] else "euclidean"
+        r = O.lpastar2d(occ, z["start"][i], z["goal"][i], heur)
+        assert r["n_expanded"] == z["n_expand"][i], i
+        if str(z["err"][i]):
+            assert r["status"] == 4, i
+            continue
+        path = seg(z["path"], z["path_off"], i)
+        assert r["cost"] == z["cost"][i] and np.array_equal(r["path_cells"], path), i
+        n += 1
+    assert n > 90
+
 def test_graph3d_published_csv():
     """The reference's published Dijkstra3D / GBFS3D rows of 3d_pathfinding_results.csv."""
     from python_motion_planning_amd import workloads as wl
