@@ -191,6 +191,25 @@ int pmp_dstar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int 
                       const int32_t* goal_xy, int nq, double* cost, int32_t* path_len, int32_t* path, int path_cap,
                       int64_t* n_process, int32_t* status, int64_t max_process);
 
+/*
+ * Batched LPA*.  Replaces LPAStar.plan (global_planner/graph_search/lpa_star.py:78-87): the initial
+ * computeShortestPath (:139-160) with updateVertex (:162-179), and extractPath (:209-230).  U keeps
+ * the reference's Python-list semantics (first-minimal `min(U, key)`, shifting `U.remove`,
+ * `heapq.heappush` on the list), so the expansion order, len(EXPAND) and costs are bit-exact.
+ *   occ_bits, heuristic, start_xy, goal_xy as pmp_astar2d_batch
+ *   cost [nq] f64        extractPath cost; also kept when extractPath gives up after 1000 steps
+ *   path [nq][path_cap]  cells x*H + y, start -> goal (path_cap >= 1001 covers every result)
+ *   n_expanded [nq]      len(EXPAND) of computeShortestPath
+ *   counters nullable [nq][4] i64: pushes, expansions, extractPath steps, max |U|
+ *   status [nq]          0 found, 1 extractPath gave up (1000 steps: the reference returns
+ *                        (cost, [], None)), 2 path_cap overflow, 4 the reference raises (U empties:
+ *                        ValueError from min(); a neighbour off the grid: KeyError; start == goal
+ *                        ends that way too, the goal node being detached from the map)
+ */
+int pmp_lpastar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H, int heuristic,
+                        const int32_t* start_xy, const int32_t* goal_xy, int nq, double* cost, int32_t* path_len,
+                        uint32_t* path, int path_cap, int32_t* n_expanded, int64_t* counters, int32_t* status);
+
 /* LQR settings (local_planner/lqr.py:35-38): diag Q, diag R, Riccati iteration cap and the
  * signed exit threshold of lqr.py:134.  Reference defaults: q = 1,1,1  r = 1,1  iters 100  eps 0.1. */
 typedef struct {

@@ -253,6 +253,36 @@ def dstar2d_batch(occ, starts, goals, path_cap: int | None = None, max_process: 
     return out
 
 
+def lpastar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: int = 1001, counters: bool = False,
+                    stream=None):
+    """Batched LPAStar.plan (lpa_star.py:78-87: computeShortestPath + extractPath) on one Grid.
+    occ uint8 [W, H] (x-major).  Returns dict of device tensors: cost, path_len, path [nq, path_cap]
+    (cells x*H+y, start -> goal), n_expanded (len(EXPAND)), status (1 = extractPath gave up after
+    1000 steps, 4 = the reference raises), optional counters [nq, 4]."""
+    torch = _lib.device_check()
+    L = _lib.load_library()
+    ctx = _lib.context()
+    occ = np.asarray(occ)
+    W, H = occ.shape
+    occ_bits = occ_bits_device(occ, torch)
+    s = _dev(torch, starts, torch.int32).reshape(-1, 2)
+    g = _dev(torch, goals, torch.int32).reshape(-1, 2)
+    nq = int(s.shape[0])
+    out = dict(cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
+               path_len=torch.empty(nq, dtype=torch.int32, device="cuda"),
+               path=torch.empty((nq, int(path_cap)), dtype=torch.int32, device="cuda"),
+               n_expanded=torch.empty(nq, dtype=torch.int32, device="cuda"),
+               status=torch.empty(nq, dtype=torch.int32, device="cuda"))
+    out["counters"] = torch.empty((nq, 4), dtype=torch.int64, device="cuda") if counters else None
+    rc = L.pmp_lpastar2d_batch(ctx, stream if stream is not None else _lib.stream_ptr(), occ_bits.data_ptr(), W, H,
+                               1 if heuristic == "manhattan" else 0, s.data_ptr(), g.data_ptr(), nq,
+                               out["cost"].data_ptr(), out["path_len"].data_ptr(), out["path"].data_ptr(),
+                               int(path_cap), out["n_expanded"].data_ptr(), _lib.ptr(out["counters"]),
+                               out["status"].data_ptr())
+    _lib.check(ctx, rc, "pmp_lpastar2d_batch")
+    return out
+
+
 def map_arrays(env, torch=None):
     """Map obstacle lists (env.py:83-117) -> device f64 tensors rect [nr,4], circ [nc,3], bnd [nb,4]."""
     torch = torch or _lib.device_check()

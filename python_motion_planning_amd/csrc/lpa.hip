@@ -1,0 +1,407 @@
+// Batched LPA* for gfx950: LPAStar.plan (global_planner/graph_search/lpa_star.py:78-87) =
+// computeShortestPath (:139-160) + extractPath (:209-230), bit-exact with the reference including
+// its OPEN "set" U, which is a Python list:
+//   * min(U, key=key) returns the FIRST minimal element in list order (:141);
+//   * U.remove(node) shifts the list tail left by one (:149, :173);
+//   * heapq.heappush(U, node) appends and sifts by LNode.__lt__ (key list compare, :32-33) on
+//     whatever order the list holds after the removes (:178).
+// So the kernel keeps the list itself, element for element: U = {cell, k1, k2} arrays in HBM plus
+// a per-cell position (`node in U` is pos >= 0).
+//
+// Execution model: one wave64 per query (persistent workers over an atomic queue).  The wave
+// scans U for the minimum (64 lanes, first index on ties), shifts the tail 64 elements per
+// instruction, sifts a push with one load round of the ancestors (the "less" prefix from the
+// parent up is a ballot's trailing-ones count), and evaluates a node's 8 neighbours on lanes 0..7
+// (rhs = min over them, :166-167).
+#include "pmp_internal.h"
+
+namespace {
+
+constexpr int kMaxDim = 8192;
+constexpr double kSqrt2 = 1.4142135623730951;  // math.hypot(1, 1)
+constexpr double kInf = __builtin_huge_val();
+
+// motions in the order of env.py:52-55
+__constant__ int kMX[8] = {-1, -1, 0, 1, 1, 1, 0, -1};
+__constant__ int kMY[8] = {0, 1, 1, 1, 0, -1, -1, -1};
+
+struct Q {
+    const uint32_t* occ;
+    int W, H, heur;
+    int32_t start, goal;
+    int gx, gy;
+    double* g;
+    double* rhs;
+    int32_t* pos;
+    int32_t* Uc;
+    double* Uk1;
+    double* Uk2;
+    int n;         // |U| (wave-uniform)
+    int64_t npush;
+};
+
+__device__ __forceinline__ bool occ_at(const uint32_t* occ, int H, int x, int y)
+{
+    const uint32_t ci = (uint32_t)x * (uint32_t)H + (uint32_t)y;
+    return ((occ[ci >> 5] >> (ci & 31u)) & 1u) != 0u;
+}
+__device__ __forceinline__ bool key_lt(double a1, double a2, double b1, double b2)
+{
+    return a1 < b1 || (a1 == b1 && a2 < b2);
+}
+__device__ __forceinline__ void wave_sync_mem() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+// calculateKey's h (GraphSearcher.h, graph_search.py:41-44): hypot of integer deltas == the
+// correctly rounded sqrt of the exact square sum; manhattan |dx| + |dy|
+__device__ __forceinline__ double hval(const Q& S, int x, int y)
+{
+    const int dx = S.gx - x, dy = S.gy - y;
+    return S.heur == 1 ? (double)(abs(dx) + abs(dy)) : __dsqrt_rn((double)(dx * dx + dy * dy));
+}
+
+// U.remove(U[i]): the tail moves left one slot, 64 elements per round (every lane loads before
+// any lane stores, and a round never reads what an earlier round wrote)
+__device__ void u_remove(Q& S, int i, int lane)
+{
+    for (int base = i; base < S.n - 1; base += 64) {
+        const int k = base + lane;
+        const bool on = k < S.n - 1;
+        int32_t c = 0;
+        double a = 0.0, b = 0.0;
+        if (on) {
+            c = S.Uc[k + 1];
+            a = S.Uk1[k + 1];
+            b = S.Uk2[k + 1];
+        }
+        wave_sync_mem();
+        if (on) {
+            S.Uc[k] = c;
+            S.Uk1[k] = a;
+            S.Uk2[k] = b;
+            S.pos[c] = k;
+        }
+        wave_sync_mem();
+    }
+    S.n -= 1;
+}
+
+// heapq.heappush(U, (c, k1, k2)): lane j (1..D) loads ancestor j of position n; the ancestors that
+// move down are the run of "new < ancestor" from the parent up (CPython _siftdown stops at the
+// first one that is not greater)
+__device__ void u_push(Q& S, int32_t c, double k1, double k2, int lane)
+{
+    const uint32_t np1 = (uint32_t)S.n + 1u;
+    const int D = 31 - __clz((int)np1);
+    const bool on = lane >= 1 && lane <= D;
+    const int aj = on ? (int)(np1 >> lane) - 1 : 0;
+    int32_t ac = 0;
+    double a1 = 0.0, a2 = 0.0;
+    if (on) {
+        ac = S.Uc[aj];
+        a1 = S.Uk1[aj];
+        a2 = S.Uk2[aj];
+    }
+    const uint64_t lt = ballot(on && key_lt(k1, k2, a1, a2));
+    const int t = __builtin_ctzll(~(lt >> 1));  // trailing ones from lane 1
+    wave_sync_mem();
+    if (on && lane <= t) {  // ancestor j moves to ancestor j - 1 (ancestor 0 = position n)
+        const int dst = (int)(np1 >> (lane - 1)) - 1;
+        S.Uc[dst] = ac;
+        S.Uk1[dst] = a1;
+        S.Uk2[dst] = a2;
+        S.pos[ac] = dst;
+    }
+    if (lane == 0) {
+        const int dst = (int)(np1 >> t) - 1;
+        S.Uc[dst] = c;
+        S.Uk1[dst] = k1;
+        S.Uk2[dst] = k2;
+        S.pos[c] = dst;
+    }
+    wave_sync_mem();
+    S.n += 1;
+    S.npush += 1;
+}
+
+// updateVertex (:162-179).  Returns PMP_REF_RAISES when the reference raises (KeyError: a
+// neighbour off the map; ValueError: min() of an empty neighbour list).
+__device__ int update_vertex(Q& S, int32_t v, int lane)
+{
+    const int vx = (int)((uint32_t)v / (uint32_t)S.H), vy = v - vx * S.H;
+    const int m = lane & 7;
+    double rv;
+    if (v != S.start) {
+        // getNeighbor (:196-207): map lookup (KeyError off the grid), then the obstacle filter;
+        // cost (graph_search.py:46-59): inf on isCollision(node_n, node), else hypot
+        const int ux = vx + kMX[m], uy = vy + kMY[m];
+        const bool in = (unsigned)ux < (unsigned)S.W && (unsigned)uy < (unsigned)S.H;
+        bool valid = false;
+        double val = kInf;
+        if (lane < 8 && in) {
+            const bool ou = occ_at(S.occ, S.H, ux, uy);
+            valid = !ou;
+            bool coll = ou || occ_at(S.occ, S.H, vx, vy);
+            if ((m & 1) && !coll) coll = occ_at(S.occ, S.H, ux, vy) || occ_at(S.occ, S.H, vx, uy);
+            const double gu = S.g[ux * S.H + uy];
+            val = gu + (coll ? kInf : ((m & 1) ? kSqrt2 : 1.0));
+        }
+        if (ballot(lane < 8 && !in)) return PMP_REF_RAISES;
+        if (!ballot(valid)) return PMP_REF_RAISES;
+        double best = valid ? val : kInf;
+        for (int o = 1; o < 8; o <<= 1) best = fmin(best, __shfl_xor(best, o, 64));
+        rv = __shfl(best, 0, 64);
+        if (lane == 0) S.rhs[v] = rv;
+    } else {
+        double t = 0.0;
+        if (lane == 0) t = S.rhs[v];
+        rv = __shfl(t, 0, 64);
+    }
+    double gt = 0.0;
+    int32_t pt = 0;
+    if (lane == 0) {
+        gt = S.g[v];
+        pt = S.pos[v];
+    }
+    const double gv = __shfl(gt, 0, 64);
+    const int p = uni(pt);
+    if (p >= 0) {  // `node in U`: U.remove(node)
+        if (lane == 0) S.pos[v] = -1;
+        wave_sync_mem();
+        u_remove(S, p, lane);
+    }
+    if (gv != rv) {
+        const double mn = gv < rv ? gv : rv;
+        u_push(S, v, mn + hval(S, vx, vy), mn, lane);
+    }
+    return 0;
+}
+
+__global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ occ, int W, int H, int heur,
+                                                 const int32_t* __restrict__ start_xy,
+                                                 const int32_t* __restrict__ goal_xy, int nq, double* __restrict__ cost_out,
+                                                 int32_t* __restrict__ path_len_out, uint32_t* __restrict__ path_out,
+                                                 int path_cap, int32_t* __restrict__ nexp_out,
+                                                 int64_t* __restrict__ counters, int32_t* __restrict__ status_out,
+                                                 int* __restrict__ queue, double* __restrict__ scr_f64,
+                                                 int32_t* __restrict__ scr_i32)
+{
+    const int lane = lane_id();
+    const size_t ncell = (size_t)W * (size_t)H;
+    Q S;
+    S.occ = occ;
+    S.W = W;
+    S.H = H;
+    S.heur = heur;
+    {
+        double* f = scr_f64 + (size_t)blockIdx.x * 4 * ncell;
+        int32_t* i = scr_i32 + (size_t)blockIdx.x * 2 * ncell;
+        S.g = f;
+        S.rhs = f + ncell;
+        S.Uk1 = f + 2 * ncell;
+        S.Uk2 = f + 3 * ncell;
+        S.pos = i;
+        S.Uc = i + ncell;
+    }
+    for (;;) {
+        const int q = next_query(queue, lane);
+        if (q >= nq) break;
+        const int sx = uni(start_xy[2 * q]), sy = uni(start_xy[2 * q + 1]);
+        const int gx = uni(goal_xy[2 * q]), gy = uni(goal_xy[2 * q + 1]);
+        int st = 0;
+        int64_t nexp = 0, steps = 0, maxn = 0;
+        double cost = 0.0;
+        int len = 0;
+        S.gx = gx;
+        S.gy = gy;
+        S.n = 0;
+        S.npush = 0;
+        if (!((unsigned)sx < (unsigned)W && (unsigned)sy < (unsigned)H && (unsigned)gx < (unsigned)W &&
+              (unsigned)gy < (unsigned)H)) {
+            st = PMP_REF_RAISES;  // map lookups off the grid (KeyError)
+        } else {
+            for (size_t i = lane; i < ncell; i += 64) {
+                S.g[i] = kInf;
+                S.rhs[i] = kInf;
+                S.pos[i] = -1;
+            }
+            wave_sync_mem();
+            S.start = sx * H + sy;
+            S.goal = gx * H + gy;
+            // start == goal: self.goal is a separate LNode(goal, inf, inf) that map[] no longer
+            // holds (map[start] overwrote it, :62-63): g = rhs = inf forever, the loop ends only
+            // when U empties
+            const bool detached = S.start == S.goal;
+            if (lane == 0) S.rhs[S.start] = 0.0;  // LNode(start, inf, 0.0, None) (:59)
+            wave_sync_mem();
+            u_push(S, S.start, hval(S, sx, sy), 0.0, lane);
+            maxn = 1;
+            for (;;) {
+                if (S.n == 0) { st = PMP_REF_RAISES; break; }  // min() of an empty list
+                // safety bound only (LPA* on a static grid settles every cell a bounded number of
+                // times): a runaway query stops with status 3 instead of holding the GPU
+                if (nexp > (int64_t)64 * (int64_t)ncell + 64) { st = PMP_CAP_OVERFLOW; break; }
+                // min(U, key=key): first minimal element in list order
+                double b1 = kInf, b2 = kInf;
+                int bi = 0x7fffffff;
+                for (int k = lane; k < S.n; k += 64) {
+                    const double a1 = S.Uk1[k], a2 = S.Uk2[k];
+                    if (bi == 0x7fffffff || key_lt(a1, a2, b1, b2)) { b1 = a1; b2 = a2; bi = k; }
+                }
+                for (int o = 1; o < 64; o <<= 1) {
+                    const double o1 = __shfl_xor(b1, o, 64), o2 = __shfl_xor(b2, o, 64);
+                    const int oi = __shfl_xor(bi, o, 64);
+                    const bool take = oi != 0x7fffffff &&
+                                      (bi == 0x7fffffff || key_lt(o1, o2, b1, b2) || (o1 == b1 && o2 == b2 && oi < bi));
+                    if (take) { b1 = o1; b2 = o2; bi = oi; }
+                }
+                bi = uni(bi);
+                b1 = __shfl(b1, 0, 64);
+                b2 = __shfl(b2, 0, 64);
+                double ggt = 0.0, grt = 0.0;
+                int32_t vt = 0;
+                if (lane == 0) {
+                    ggt = S.g[S.goal];
+                    grt = S.rhs[S.goal];
+                    vt = S.Uc[bi];
+                }
+                const double gg = detached ? kInf : __shfl(ggt, 0, 64);
+                const double gr = detached ? kInf : __shfl(grt, 0, 64);
+                const double gm = gg < gr ? gg : gr;
+                if (!key_lt(b1, b2, gm + 0.0, gm) && gr == gg) break;  // calculateKey(goal): h = 0
+                const int32_t v = uni(vt);
+                if (lane == 0) S.pos[v] = -1;
+                wave_sync_mem();
+                u_remove(S, bi, lane);
+                nexp++;
+                double gvt = 0.0, rvt = 0.0;
+                if (lane == 0) {
+                    gvt = S.g[v];
+                    rvt = S.rhs[v];
+                }
+                const double gv = __shfl(gvt, 0, 64), rv = __shfl(rvt, 0, 64);
+                if (gv > rv) {
+                    if (lane == 0) S.g[v] = rv;
+                    wave_sync_mem();
+                } else {
+                    if (lane == 0) S.g[v] = kInf;
+                    wave_sync_mem();
+                    if ((st = update_vertex(S, v, lane))) break;
+                }
+                const int vx = (int)((uint32_t)v / (uint32_t)H), vy = v - vx * H;
+                // getNeighbor(node) (:196-207): the list is fixed before the updates
+                uint32_t nbm = 0u;
+                {
+                    const int ux = vx + kMX[lane & 7], uy = vy + kMY[lane & 7];
+                    const bool in = (unsigned)ux < (unsigned)W && (unsigned)uy < (unsigned)H;
+                    const uint64_t bad = ballot(lane < 8 && !in);
+                    const bool ok = lane < 8 && in && !occ_at(occ, H, ux, uy);
+                    nbm = (uint32_t)ballot(ok) & 0xffu;
+                    if (bad) st = PMP_REF_RAISES;  // KeyError while the list is built: no update runs
+                }
+                if (st) break;
+                for (int m = 0; m < 8 && nbm; m++) {
+                    if (!((nbm >> m) & 1u)) continue;
+                    const int r = update_vertex(S, (vx + kMX[m]) * H + (vy + kMY[m]), lane);
+                    if (r) { st = r; break; }
+                }
+                if (st) break;
+                if (S.n > maxn) maxn = S.n;
+            }
+            if (st == 0) {
+                // extractPath (:209-230): greedy min-g neighbour from the goal, first minimum in motion
+                // order; gives up (cost kept, empty path) after 1000 steps
+                uint32_t* pth = path_out + (size_t)q * path_cap;
+                int32_t c = S.goal;
+                if (lane == 0 && len < path_cap) pth[len] = (uint32_t)c;
+                len++;
+                while (c != S.start) {
+                    const int x = (int)((uint32_t)c / (uint32_t)H), y = c - x * H;
+                    const int m = lane & 7;
+                    const int ux = x + kMX[m], uy = y + kMY[m];
+                    const bool in = (unsigned)ux < (unsigned)W && (unsigned)uy < (unsigned)H;
+                    bool valid = false;
+                    double gu = 0.0;
+                    if (lane < 8 && in) {
+                        bool coll = occ_at(occ, H, ux, uy) || occ_at(occ, H, x, y);
+                        if ((m & 1) && !coll) coll = occ_at(occ, H, ux, y) || occ_at(occ, H, x, uy);
+                        valid = !coll;
+                        gu = S.g[ux * H + uy];
+                    }
+                    if (ballot(lane < 8 && !in)) { st = PMP_REF_RAISES; break; }
+                    uint64_t vm = ballot(valid) & 0xffull;
+                    if (!vm) { st = PMP_REF_RAISES; break; }
+                    int bm = -1;
+                    double bg = 0.0;
+                    while (vm) {
+                        const int k = __ffsll((long long)vm) - 1;
+                        vm &= vm - 1;
+                        const double gk = __shfl(gu, k, 64);
+                        if (bm < 0 || gk < bg) { bm = k; bg = gk; }
+                    }
+                    cost += (bm & 1) ? kSqrt2 : 1.0;
+                    c = (x + kMX[bm]) * H + (y + kMY[bm]);
+                    if (lane == 0 && len < path_cap) pth[len] = (uint32_t)c;
+                    len++;
+                    if (++steps == 1000) { st = PMP_NO_PATH; break; }
+                }
+                wave_sync_mem();
+                if (st == 0) {
+                    if (len > path_cap) st = PMP_PATH_OVERFLOW;
+                    else  // path start -> goal (list(reversed(path)))
+                        for (int i = lane; i < len / 2; i += 64) {
+                            const uint32_t a = pth[i], b = pth[len - 1 - i];
+                            pth[i] = b;
+                            pth[len - 1 - i] = a;
+                        }
+                }
+            }
+        }
+        if (lane == 0) {
+            status_out[q] = st;
+            cost_out[q] = (st == 0 || st == PMP_NO_PATH) ? cost : 0.0;
+            path_len_out[q] = st == 0 ? len : 0;
+            nexp_out[q] = (int32_t)nexp;
+            if (counters) {
+                counters[4 * q] = S.npush;
+                counters[4 * q + 1] = nexp;
+                counters[4 * q + 2] = steps;
+                counters[4 * q + 3] = maxn;
+            }
+        }
+        wave_sync_mem();
+    }
+}
+
+}  // namespace
+
+extern "C" int pmp_lpastar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H, int heuristic,
+                                   const int32_t* start_xy, const int32_t* goal_xy, int nq, double* cost,
+                                   int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded,
+                                   int64_t* counters, int32_t* status)
+{
+    if (!ctx) return PMP_EINVAL;
+    if (W < 1 || H < 1 || W > kMaxDim || H > kMaxDim)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar2d_batch: W and H must be in [1, 8192]");
+    if (heuristic != 0 && heuristic != 1) return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar2d_batch: heuristic must be 0 or 1");
+    if (nq < 0 || path_cap < 1) return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar2d_batch: bad nq/path_cap");
+    if (nq == 0) return PMP_OK;
+    if (!occ_bits || !start_xy || !goal_xy || !cost || !path_len || !path || !n_expanded || !status)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar2d_batch: null pointer argument");
+    PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    const size_t ncell = (size_t)W * H;
+    const size_t per_worker = ncell * 40;  // g, rhs, U keys (f64) + pos, U cells (i32)
+    int workers = 256 * 4;
+    const size_t max_workers = ((size_t)16 << 30) / per_worker;  // scratch under 16 GiB
+    if ((size_t)workers > max_workers) workers = (int)(max_workers > 0 ? max_workers : 1);
+    if (workers > nq) workers = nq;
+    double* f = (double*)pmp_scratch(ctx, SCR_AUX2, (size_t)workers * ncell * 32 + 16);
+    int32_t* i32 = (int32_t*)pmp_scratch(ctx, SCR_AUX3, (size_t)workers * ncell * 8 + 16);
+    int* queue = (int*)pmp_scratch(ctx, SCR_AUX0, 256);
+    if (!f || !i32 || !queue) return PMP_ENOMEM;
+    hipStream_t s = (hipStream_t)stream;
+    PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
+    hipLaunchKernelGGL(lpa_kernel, dim3(workers), dim3(64), 0, s, occ_bits, W, H, heuristic, start_xy, goal_xy, nq, cost,
+                       path_len, path, path_cap, n_expanded, counters, status, queue, f, i32);
+    PMP_HIP_CHECK(ctx, hipGetLastError());
+    return PMP_OK;
+}

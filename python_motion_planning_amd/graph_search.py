@@ -175,6 +175,34 @@ class LazyThetaStar(ThetaStar):
         return "Lazy Theta*"
 
 
+class LPAStar(GraphSearcher):
+    """Lifelong Planning A* (lpa_star.py:39-230): plan() is the initial computeShortestPath +
+    extractPath on the gfx950 kernel lpa.hip (U with the reference's list semantics).  Interactive
+    replanning (OnPress) needs a figure and is not provided."""
+
+    def __str__(self) -> str:
+        return "Lifelong Planning A*"
+
+    def plan(self) -> tuple:
+        """Returns (cost, path start->goal, None); (cost, [], None) when extractPath gives up after
+        1000 steps; raises ValueError where the reference's min() of an empty list does."""
+        occ = self.env.occupancy()
+        W, H = occ.shape
+        r = batch.lpastar2d_batch(occ, np.array([self.start.current]), np.array([self.goal.current]),
+                                  self.heuristic_type, counters=True)
+        st = int(r["status"][0])
+        self.n_expanded = int(r["n_expanded"][0])
+        if st == 4:
+            raise ValueError("min() arg is an empty sequence (LPAStar: U emptied before the goal was consistent)")
+        if st == 1:
+            return float(r["cost"][0]), [], None
+        if st != 0:
+            raise RuntimeError(f"{self} kernel status {st}")
+        plen = int(r["path_len"][0])
+        cells = r["path"][0, :plen].cpu().numpy()
+        return float(r["cost"][0]), [(int(c) // H, int(c) % H) for c in cells], None
+
+
 class DStar(GraphSearcher):
     """Dynamic A* (d_star.py:37-291) -- the static plan (processState until the start is CLOSED)
     runs in the gfx950 kernel dstar.hip with the reference's list-semantics OPEN."""
