@@ -210,6 +210,17 @@ int pmp_lpastar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, in
                         const int32_t* start_xy, const int32_t* goal_xy, int nq, double* cost, int32_t* path_len,
                         uint32_t* path, int path_cap, int32_t* n_expanded, int64_t* counters, int32_t* status);
 
+/*
+ * Batched D* Lite.  Replaces DStarLite.plan (global_planner/graph_search/d_star_lite.py:14-187; plan()
+ * is LPAStar's): the same list-semantics U, searched from the goal (rhs = 0) toward the start with
+ * keys min(g, rhs) + h(node, start) + km (km = 0), outdated keys re-keyed at the pop (:104-106), and
+ * extractPath from the start to the goal (:156-187).  Arguments, outputs and statuses as
+ * pmp_lpastar2d_batch; start == goal raises in the reference (status 4 after one expansion).
+ */
+int pmp_dstarlite2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H, int heuristic,
+                          const int32_t* start_xy, const int32_t* goal_xy, int nq, double* cost, int32_t* path_len,
+                          uint32_t* path, int path_cap, int32_t* n_expanded, int64_t* counters, int32_t* status);
+
 /* LQR settings (local_planner/lqr.py:35-38): diag Q, diag R, Riccati iteration cap and the
  * signed exit threshold of lqr.py:134.  Reference defaults: q = 1,1,1  r = 1,1  iters 100  eps 0.1. */
 typedef struct {

@@ -547,15 +547,17 @@ def theta3d(occ: np.ndarray, start, goal, lazy: bool = False, heuristic: str = "
     return out
 
 
-def lpastar2d(occ: np.ndarray, start, goal, heuristic: str = "euclidean"):
+def lpastar2d(occ: np.ndarray, start, goal, heuristic: str = "euclidean", lite: bool = False):
     """Restatement of LPAStar.plan (lpa_star.py:78-87, computeShortestPath :139-160, extractPath
-    :209-230) with the reference's list semantics for U.  Path start -> goal.  status 4 = the
-    reference raises (ValueError from min() of an empty U / neighbour list, or KeyError)."""
+    :209-230) with the reference's list semantics for U; lite=True restates DStarLite.plan
+    (d_star_lite.py:14-187).  Path start -> goal.  status 4 = the reference raises (ValueError from
+    min() of an empty U / neighbour list, or KeyError)."""
     L = lib()
     if not getattr(L, "_lpa_set", False):
-        L.oracle_lpastar2d.restype = ctypes.c_int
-        L.oracle_lpastar2d.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                       ctypes.c_int, ctypes.c_int, _dp, _i32p, ctypes.c_int, _i32p, _i64p]
+        for fn in (L.oracle_lpastar2d, L.oracle_dstarlite2d):
+            fn.restype = ctypes.c_int
+            fn.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                           ctypes.c_int, ctypes.c_int, _dp, _i32p, ctypes.c_int, _i32p, _i64p]
         L._lpa_set = True
     occ = np.ascontiguousarray(occ, dtype=np.uint8)
     W, H = occ.shape
@@ -563,7 +565,7 @@ def lpastar2d(occ: np.ndarray, start, goal, heuristic: str = "euclidean"):
     cost = ctypes.c_double(0)
     plen = ctypes.c_int32(0)
     ctr = np.zeros(4, np.int64)
-    st = L.oracle_lpastar2d(_p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0, int(start[0]), int(start[1]),
+    st = (L.oracle_dstarlite2d if lite else L.oracle_lpastar2d)(_p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0, int(start[0]), int(start[1]),
                             int(goal[0]), int(goal[1]), ctypes.byref(cost), _p(path, _i32p), 1002, ctypes.byref(plen),
                             _p(ctr, _i64p))
     cells = path[: plen.value]

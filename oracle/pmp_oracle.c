@@ -1844,11 +1844,11 @@ static inline double lpa_h(int heuristic, int x, int y, int gx, int gy)
 
 /* updateVertex (:162-179).  Returns 4 when the reference raises (KeyError off the map, or min()
  * of an empty neighbour list). */
-static int lpa_update(const uint8_t* occ, int W, int H, int heuristic, int32_t start, int gx, int gy, double* g,
+static int lpa_update(const uint8_t* occ, int W, int H, int heuristic, int32_t src, int gx, int gy, double* g,
                       double* rhs, int32_t* pos, ulist_t* U, int32_t v, int64_t* npush)
 {
     const int x = v / H, y = v % H;
-    if (v != start) {
+    if (v != src) {
         double best = INFINITY;
         int any = 0;
         for (int m = 0; m < 8; m++) { /* getNeighbor (:196-207): map lookup, then the obstacle filter */
@@ -1878,9 +1878,13 @@ static int lpa_update(const uint8_t* occ, int W, int H, int heuristic, int32_t s
 
 /* status 0 found, 1 extractPath gave up after 1000 steps (cost kept, path empty), 4 the reference
  * raises (U empties: min() of an empty list; or KeyError / empty neighbour list).
- * path: start -> goal.  counters: {pushes, expansions (len(EXPAND)), path steps, max |U|}. */
-int oracle_lpastar2d(const uint8_t* occ, int W, int H, int heuristic, int sx, int sy, int gx, int gy,
-                     double* cost_out, int32_t* path, int path_cap, int32_t* path_len, int64_t* counters)
+ * path: start -> goal.  counters: {pushes, expansions (len(EXPAND)), path steps, max |U|}.
+ * lite = 1: DStarLite.plan (d_star_lite.py:14-187, plan() inherited from LPAStar): the search runs
+ * from the goal (rhs = 0) toward the start, keys add h(node, start) + km (km = 0 in plan()), a popped
+ * node with an outdated key is re-keyed (:104-106), updateVertex skips the goal (:131-132), and
+ * extractPath walks from the start to the goal without reversing (:156-187). */
+static int lpa_core(int lite, const uint8_t* occ, int W, int H, int heuristic, int sx, int sy, int gx, int gy,
+                    double* cost_out, int32_t* path, int path_cap, int32_t* path_len, int64_t* counters)
 {
     const int64_t ncell = (int64_t)W * H;
     double* g = (double*)malloc(sizeof(double) * (size_t)ncell);
@@ -1894,8 +1898,19 @@ int oracle_lpastar2d(const uint8_t* occ, int W, int H, int heuristic, int sx, in
     *path_len = 0;
     for (int64_t i = 0; i < ncell; i++) { g[i] = INFINITY; rhs[i] = INFINITY; pos[i] = -1; }
     const int32_t start = sx * H + sy, goal = gx * H + gy;
-    rhs[start] = 0.0; /* LNode(start, inf, 0.0, None) (:59) */
-    u_push(&U, pos, start, lpa_h(heuristic, sx, sy, gx, gy), 0.0);
+    /* src: the node created with rhs = 0; tgt: the node whose consistency ends the search and
+     * toward which h points */
+    const int32_t src = lite ? goal : start, tgt = lite ? start : goal;
+    const int tx = lite ? sx : gx, ty = lite ? sy : gy, ox = lite ? gx : sx, oy = lite ? gy : sy;
+    if (lite && start == goal) {
+        /* map[start] overwrote map[goal] (:58-59): the goal node in U is detached, its g = 0 never
+         * reaches a neighbour's rhs, so the first expansion pushes nothing and U empties */
+        free(g); free(rhs); free(pos); free(U.cell); free(U.k1); free(U.k2);
+        if (counters) { counters[0] = 1; counters[1] = 1; counters[2] = 0; counters[3] = 1; }
+        return 4;
+    }
+    rhs[src] = 0.0; /* LNode(start, inf, 0.0, None) (lpa_star.py:59); LNode(goal, inf, 0.0) (d_star_lite.py:57) */
+    u_push(&U, pos, src, lpa_h(heuristic, ox, oy, tx, ty), 0.0);
     npush++;
     maxn = 1;
     for (;;) {
@@ -1906,37 +1921,48 @@ int oracle_lpastar2d(const uint8_t* occ, int W, int H, int heuristic, int sx, in
         /* start == goal: self.goal is a separate LNode(goal, inf, inf) that map[] no longer holds
          * (map[start] overwrote it, :62-63), so its g = rhs = inf forever and the loop only ends
          * when U empties */
-        const double gg = start == goal ? INFINITY : g[goal], grhs = start == goal ? INFINITY : rhs[goal];
+        const double gg = start == goal ? INFINITY : g[tgt], grhs = start == goal ? INFINITY : rhs[tgt];
         const double gm = gg < grhs ? gg : grhs;
         const double gk1 = gm + 0.0; /* calculateKey(goal): h(goal, goal) = 0 */
         if (!key_lt(U.k1[bi], U.k2[bi], gk1, gm) && grhs == gg) break;
         const int32_t v = U.cell[bi];
+        const double vk1 = U.k1[bi], vk2 = U.k2[bi];
         pos[v] = -1;
         u_remove(&U, pos, bi);
         nexp++;
+        const int x = v / H, y = v % H;
+        if (lite) { /* node.key < calculateKey(node): re-key, push, nothing else (:104-106) */
+            const double mn = g[v] < rhs[v] ? g[v] : rhs[v];
+            const double c1 = mn + lpa_h(heuristic, x, y, tx, ty) + 0.0, c2 = mn;
+            if (key_lt(vk1, vk2, c1, c2)) {
+                u_push(&U, pos, v, c1, c2);
+                npush++;
+                if (U.n > maxn) maxn = U.n;
+                continue;
+            }
+        }
         if (g[v] > rhs[v]) {
             g[v] = rhs[v];
         } else {
             g[v] = INFINITY;
-            if ((status = lpa_update(occ, W, H, heuristic, start, gx, gy, g, rhs, pos, &U, v, &npush))) break;
+            if ((status = lpa_update(occ, W, H, heuristic, src, tx, ty, g, rhs, pos, &U, v, &npush))) break;
         }
-        const int x = v / H, y = v % H;
         for (int m = 0; m < 8 && !status; m++) {
             const int ux = x + MX8[m], uy = y + MY8[m];
             if (ux < 0 || uy < 0 || ux >= W || uy >= H) { status = 4; break; }
             if (occ[(int64_t)ux * H + uy]) continue;
-            status = lpa_update(occ, W, H, heuristic, start, gx, gy, g, rhs, pos, &U, ux * H + uy, &npush);
+            status = lpa_update(occ, W, H, heuristic, src, tx, ty, g, rhs, pos, &U, ux * H + uy, &npush);
         }
         if (status) break;
         if (U.n > maxn) maxn = U.n;
     }
-    if (status == 0) { /* extractPath: greedy min-g neighbour from the goal, first minimum in motion order */
-        int32_t c = goal;
+    if (status == 0) { /* extractPath: greedy min-g neighbour from tgt, first minimum in motion order */
+        int32_t c = tgt;
         double cost = 0.0;
         int64_t len = 0;
         if (len < path_cap) path[len] = c;
         len++;
-        while (c != start) {
+        while (c != src) {
             const int x = c / H, y = c % H;
             int bm = -1;
             double bg = 0.0;
@@ -1957,7 +1983,7 @@ int oracle_lpastar2d(const uint8_t* occ, int W, int H, int heuristic, int sx, in
         *cost_out = cost;
         if (status == 0) {
             if (len > path_cap) status = 2;
-            else
+            else if (!lite) /* LPA*: list(reversed(path)); D* Lite's path already runs start -> goal */
                 for (int64_t i = 0; i < len / 2; i++) { int32_t t = path[i]; path[i] = path[len - 1 - i]; path[len - 1 - i] = t; }
             *path_len = (int32_t)len;
         }
@@ -1965,4 +1991,16 @@ int oracle_lpastar2d(const uint8_t* occ, int W, int H, int heuristic, int sx, in
     if (counters) { counters[0] = npush; counters[1] = nexp; counters[2] = steps; counters[3] = maxn; }
     free(g); free(rhs); free(pos); free(U.cell); free(U.k1); free(U.k2);
     return status;
+}
+
+int oracle_lpastar2d(const uint8_t* occ, int W, int H, int heuristic, int sx, int sy, int gx, int gy,
+                     double* cost_out, int32_t* path, int path_cap, int32_t* path_len, int64_t* counters)
+{
+    return lpa_core(0, occ, W, H, heuristic, sx, sy, gx, gy, cost_out, path, path_cap, path_len, counters);
+}
+
+int oracle_dstarlite2d(const uint8_t* occ, int W, int H, int heuristic, int sx, int sy, int gx, int gy,
+                       double* cost_out, int32_t* path, int path_cap, int32_t* path_len, int64_t* counters)
+{
+    return lpa_core(1, occ, W, H, heuristic, sx, sy, gx, gy, cost_out, path, path_cap, path_len, counters);
 }

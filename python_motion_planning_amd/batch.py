@@ -254,8 +254,9 @@ def dstar2d_batch(occ, starts, goals, path_cap: int | None = None, max_process: 
 
 
 def lpastar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: int = 1001, counters: bool = False,
-                    stream=None):
-    """Batched LPAStar.plan (lpa_star.py:78-87: computeShortestPath + extractPath) on one Grid.
+                    stream=None, lite: bool = False):
+    """Batched LPAStar.plan (lpa_star.py:78-87: computeShortestPath + extractPath) on one Grid;
+    lite=True runs DStarLite.plan (d_star_lite.py:14-187, pmp_dstarlite2d_batch).
     occ uint8 [W, H] (x-major).  Returns dict of device tensors: cost, path_len, path [nq, path_cap]
     (cells x*H+y, start -> goal), n_expanded (len(EXPAND)), status (1 = extractPath gave up after
     1000 steps, 4 = the reference raises), optional counters [nq, 4]."""
@@ -274,12 +275,13 @@ def lpastar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: 
                n_expanded=torch.empty(nq, dtype=torch.int32, device="cuda"),
                status=torch.empty(nq, dtype=torch.int32, device="cuda"))
     out["counters"] = torch.empty((nq, 4), dtype=torch.int64, device="cuda") if counters else None
-    rc = L.pmp_lpastar2d_batch(ctx, stream if stream is not None else _lib.stream_ptr(), occ_bits.data_ptr(), W, H,
+    fn = L.pmp_dstarlite2d_batch if lite else L.pmp_lpastar2d_batch
+    rc = fn(ctx, stream if stream is not None else _lib.stream_ptr(), occ_bits.data_ptr(), W, H,
                                1 if heuristic == "manhattan" else 0, s.data_ptr(), g.data_ptr(), nq,
                                out["cost"].data_ptr(), out["path_len"].data_ptr(), out["path"].data_ptr(),
                                int(path_cap), out["n_expanded"].data_ptr(), _lib.ptr(out["counters"]),
                                out["status"].data_ptr())
-    _lib.check(ctx, rc, "pmp_lpastar2d_batch")
+    _lib.check(ctx, rc, "pmp_dstarlite2d_batch" if lite else "pmp_lpastar2d_batch")
     return out
 
 

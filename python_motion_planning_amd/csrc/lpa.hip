@@ -8,6 +8,11 @@
 // So the kernel keeps the list itself, element for element: U = {cell, k1, k2} arrays in HBM plus
 // a per-cell position (`node in U` is pos >= 0).
 //
+// DStarLite.plan (d_star_lite.py:14-187; plan() is LPAStar's) is the same loop run backwards: the
+// node created with rhs = 0 is the goal, the search ends on the start's consistency, keys add
+// h(node, start) + km (km = 0 in plan()), a popped node with an outdated key is only re-keyed
+// (:104-106), and extractPath walks start -> goal without reversing (`lite` below).
+//
 // Execution model: one wave64 per query (persistent workers over an atomic queue).  The wave
 // scans U for the minimum (64 lanes, first index on ties), shifts the tail 64 elements per
 // instruction, sifts a push with one load round of the ancestors (the "less" prefix from the
@@ -28,8 +33,8 @@ __constant__ int kMY[8] = {0, 1, 1, 1, 0, -1, -1, -1};
 struct Q {
     const uint32_t* occ;
     int W, H, heur;
-    int32_t start, goal;
-    int gx, gy;
+    int32_t src, tgt;  // src: the node created with rhs = 0; tgt: ends the search, h points at it
+    int gx, gy;        // tgt's coordinates
     double* g;
     double* rhs;
     int32_t* pos;
@@ -130,7 +135,7 @@ __device__ int update_vertex(Q& S, int32_t v, int lane)
     const int vx = (int)((uint32_t)v / (uint32_t)S.H), vy = v - vx * S.H;
     const int m = lane & 7;
     double rv;
-    if (v != S.start) {
+    if (v != S.src) {
         // getNeighbor (:196-207): map lookup (KeyError off the grid), then the obstacle filter;
         // cost (graph_search.py:46-59): inf on isCollision(node_n, node), else hypot
         const int ux = vx + kMX[m], uy = vy + kMY[m];
@@ -183,7 +188,7 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
                                                  int path_cap, int32_t* __restrict__ nexp_out,
                                                  int64_t* __restrict__ counters, int32_t* __restrict__ status_out,
                                                  int* __restrict__ queue, double* __restrict__ scr_f64,
-                                                 int32_t* __restrict__ scr_i32)
+                                                 int32_t* __restrict__ scr_i32, int lite)
 {
     const int lane = lane_id();
     const size_t ncell = (size_t)W * (size_t)H;
@@ -211,8 +216,8 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
         int64_t nexp = 0, steps = 0, maxn = 0;
         double cost = 0.0;
         int len = 0;
-        S.gx = gx;
-        S.gy = gy;
+        S.gx = lite ? sx : gx;
+        S.gy = lite ? sy : gy;
         S.n = 0;
         S.npush = 0;
         if (!((unsigned)sx < (unsigned)W && (unsigned)sy < (unsigned)H && (unsigned)gx < (unsigned)W &&
@@ -225,16 +230,22 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
                 S.pos[i] = -1;
             }
             wave_sync_mem();
-            S.start = sx * H + sy;
-            S.goal = gx * H + gy;
-            // start == goal: self.goal is a separate LNode(goal, inf, inf) that map[] no longer
-            // holds (map[start] overwrote it, :62-63): g = rhs = inf forever, the loop ends only
-            // when U empties
-            const bool detached = S.start == S.goal;
-            if (lane == 0) S.rhs[S.start] = 0.0;  // LNode(start, inf, 0.0, None) (:59)
+            const int32_t start = sx * H + sy, goal = gx * H + gy;
+            S.src = lite ? goal : start;
+            S.tgt = lite ? start : goal;
+            // start == goal: map[start] overwrote map[goal] (lpa_star.py:62-63, d_star_lite.py:58-59).
+            // LPA*: self.goal is a detached LNode(goal, inf, inf), so the loop ends only when U
+            // empties.  D* Lite: the detached node is the goal in U; its g = 0 never reaches a
+            // neighbour's rhs, so the first expansion pushes nothing and U empties.
+            const bool detached = start == goal;
+            if (lane == 0) S.rhs[S.src] = 0.0;  // LNode(start, inf, 0.0) (lpa_star.py:59) / LNode(goal, inf, 0.0)
             wave_sync_mem();
-            u_push(S, S.start, hval(S, sx, sy), 0.0, lane);
+            u_push(S, S.src, hval(S, lite ? gx : sx, lite ? gy : sy), 0.0, lane);
             maxn = 1;
+            if (lite && detached) {
+                nexp = 1;
+                S.n = 0;
+            }
             for (;;) {
                 if (S.n == 0) { st = PMP_REF_RAISES; break; }  // min() of an empty list
                 // safety bound only (LPA* on a static grid settles every cell a bounded number of
@@ -260,8 +271,8 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
                 double ggt = 0.0, grt = 0.0;
                 int32_t vt = 0;
                 if (lane == 0) {
-                    ggt = S.g[S.goal];
-                    grt = S.rhs[S.goal];
+                    ggt = S.g[S.tgt];
+                    grt = S.rhs[S.tgt];
                     vt = S.Uc[bi];
                 }
                 const double gg = detached ? kInf : __shfl(ggt, 0, 64);
@@ -279,6 +290,16 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
                     rvt = S.rhs[v];
                 }
                 const double gv = __shfl(gvt, 0, 64), rv = __shfl(rvt, 0, 64);
+                const int vx = (int)((uint32_t)v / (uint32_t)H), vy = v - vx * H;
+                if (lite) {  // node.key < calculateKey(node): re-key and push, nothing else (:104-106)
+                    const double mn = gv < rv ? gv : rv;
+                    const double c1 = mn + hval(S, vx, vy) + 0.0;
+                    if (key_lt(b1, b2, c1, mn)) {
+                        u_push(S, v, c1, mn, lane);
+                        if (S.n > maxn) maxn = S.n;
+                        continue;
+                    }
+                }
                 if (gv > rv) {
                     if (lane == 0) S.g[v] = rv;
                     wave_sync_mem();
@@ -287,7 +308,6 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
                     wave_sync_mem();
                     if ((st = update_vertex(S, v, lane))) break;
                 }
-                const int vx = (int)((uint32_t)v / (uint32_t)H), vy = v - vx * H;
                 // getNeighbor(node) (:196-207): the list is fixed before the updates
                 uint32_t nbm = 0u;
                 {
@@ -311,10 +331,10 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
                 // extractPath (:209-230): greedy min-g neighbour from the goal, first minimum in motion
                 // order; gives up (cost kept, empty path) after 1000 steps
                 uint32_t* pth = path_out + (size_t)q * path_cap;
-                int32_t c = S.goal;
+                int32_t c = S.tgt;
                 if (lane == 0 && len < path_cap) pth[len] = (uint32_t)c;
                 len++;
-                while (c != S.start) {
+                while (c != S.src) {
                     const int x = (int)((uint32_t)c / (uint32_t)H), y = c - x * H;
                     const int m = lane & 7;
                     const int ux = x + kMX[m], uy = y + kMY[m];
@@ -347,7 +367,7 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
                 wave_sync_mem();
                 if (st == 0) {
                     if (len > path_cap) st = PMP_PATH_OVERFLOW;
-                    else  // path start -> goal (list(reversed(path)))
+                    else if (!lite)  // LPA*: list(reversed(path)); D* Lite's runs start -> goal already
                         for (int i = lane; i < len / 2; i += 64) {
                             const uint32_t a = pth[i], b = pth[len - 1 - i];
                             pth[i] = b;
@@ -374,19 +394,18 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
 
 }  // namespace
 
-extern "C" int pmp_lpastar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H, int heuristic,
-                                   const int32_t* start_xy, const int32_t* goal_xy, int nq, double* cost,
-                                   int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded,
-                                   int64_t* counters, int32_t* status)
+static int lpa_batch(int lite, pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H, int heuristic,
+                     const int32_t* start_xy, const int32_t* goal_xy, int nq, double* cost, int32_t* path_len,
+                     uint32_t* path, int path_cap, int32_t* n_expanded, int64_t* counters, int32_t* status)
 {
     if (!ctx) return PMP_EINVAL;
     if (W < 1 || H < 1 || W > kMaxDim || H > kMaxDim)
-        return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar2d_batch: W and H must be in [1, 8192]");
-    if (heuristic != 0 && heuristic != 1) return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar2d_batch: heuristic must be 0 or 1");
-    if (nq < 0 || path_cap < 1) return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar2d_batch: bad nq/path_cap");
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar2d_batch / pmp_dstarlite2d_batch: W and H must be in [1, 8192]");
+    if (heuristic != 0 && heuristic != 1) return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar2d_batch / pmp_dstarlite2d_batch: heuristic must be 0 or 1");
+    if (nq < 0 || path_cap < 1) return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar2d_batch / pmp_dstarlite2d_batch: bad nq/path_cap");
     if (nq == 0) return PMP_OK;
     if (!occ_bits || !start_xy || !goal_xy || !cost || !path_len || !path || !n_expanded || !status)
-        return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar2d_batch: null pointer argument");
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar2d_batch / pmp_dstarlite2d_batch: null pointer argument");
     PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     const size_t ncell = (size_t)W * H;
     const size_t per_worker = ncell * 40;  // g, rhs, U keys (f64) + pos, U cells (i32)
@@ -401,7 +420,25 @@ extern "C" int pmp_lpastar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* o
     hipStream_t s = (hipStream_t)stream;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
     hipLaunchKernelGGL(lpa_kernel, dim3(workers), dim3(64), 0, s, occ_bits, W, H, heuristic, start_xy, goal_xy, nq, cost,
-                       path_len, path, path_cap, n_expanded, counters, status, queue, f, i32);
+                       path_len, path, path_cap, n_expanded, counters, status, queue, f, i32, lite);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
+}
+
+extern "C" int pmp_lpastar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H, int heuristic,
+                                   const int32_t* start_xy, const int32_t* goal_xy, int nq, double* cost,
+                                   int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded,
+                                   int64_t* counters, int32_t* status)
+{
+    return lpa_batch(0, ctx, stream, occ_bits, W, H, heuristic, start_xy, goal_xy, nq, cost, path_len, path, path_cap,
+                     n_expanded, counters, status);
+}
+
+extern "C" int pmp_dstarlite2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H, int heuristic,
+                                     const int32_t* start_xy, const int32_t* goal_xy, int nq, double* cost,
+                                     int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded,
+                                     int64_t* counters, int32_t* status)
+{
+    return lpa_batch(1, ctx, stream, occ_bits, W, H, heuristic, start_xy, goal_xy, nq, cost, path_len, path, path_cap,
+                     n_expanded, counters, status);
 }

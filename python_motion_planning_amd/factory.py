@@ -4,7 +4,7 @@ reference planners outside the accelerated hot path raise NotImplementedError (n
 substituted)."""
 from __future__ import annotations
 
-_SEARCH_OUT_OF_SCOPE = {"jps", "d_star_lite", "voronoi", "s_theta_star", "anya", "rrt_connect", "informed_rrt", "aco", "pso"}
+_SEARCH_OUT_OF_SCOPE = {"jps", "voronoi", "s_theta_star", "anya", "rrt_connect", "informed_rrt", "aco", "pso"}
 _CONTROL_OUT_OF_SCOPE = {"pid", "apf", "rpp"}
 
 
@@ -14,9 +14,9 @@ class SearchFactory(object):
 
         table = {"a_star": "AStar", "dijkstra": "Dijkstra", "gbfs": "GBFS", "d_star": "DStar", "rrt": "RRT",
                  "rrt_star": "RRTStar", "theta_star": "ThetaStar", "lazy_theta_star": "LazyThetaStar",
-                 "lpa_star": "LPAStar"}
+                 "lpa_star": "LPAStar", "d_star_lite": "DStarLite"}
         if planner_name in table:
-            mod = graph_search if planner_name in ("a_star", "dijkstra", "gbfs", "d_star", "theta_star", "lazy_theta_star", "lpa_star") else __import__(
+            mod = graph_search if planner_name in ("a_star", "dijkstra", "gbfs", "d_star", "theta_star", "lazy_theta_star", "lpa_star", "d_star_lite") else __import__(
                 __package__ + ".sample_search", fromlist=["x"])
             cls = getattr(mod, table[planner_name], None)
             if cls is None:

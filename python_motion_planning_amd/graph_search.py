@@ -180,6 +180,8 @@ class LPAStar(GraphSearcher):
     extractPath on the gfx950 kernel lpa.hip (U with the reference's list semantics).  Interactive
     replanning (OnPress) needs a figure and is not provided."""
 
+    _lite = False
+
     def __str__(self) -> str:
         return "Lifelong Planning A*"
 
@@ -189,7 +191,7 @@ class LPAStar(GraphSearcher):
         occ = self.env.occupancy()
         W, H = occ.shape
         r = batch.lpastar2d_batch(occ, np.array([self.start.current]), np.array([self.goal.current]),
-                                  self.heuristic_type, counters=True)
+                                  self.heuristic_type, counters=True, lite=self._lite)
         st = int(r["status"][0])
         self.n_expanded = int(r["n_expanded"][0])
         if st == 4:
@@ -201,6 +203,17 @@ class LPAStar(GraphSearcher):
         plen = int(r["path_len"][0])
         cells = r["path"][0, :plen].cpu().numpy()
         return float(r["cost"][0]), [(int(c) // H, int(c) % H) for c in cells], None
+
+
+class DStarLite(LPAStar):
+    """D* Lite (d_star_lite.py:14-187): LPAStar's plan() searched from the goal toward the start
+    (keys with h(node, start) + km, km = 0), on the same kernel (pmp_dstarlite2d_batch).  Interactive
+    replanning (OnPress) needs a figure and is not provided."""
+
+    _lite = True
+
+    def __str__(self) -> str:
+        return "D* Lite"
 
 
 class DStar(GraphSearcher):

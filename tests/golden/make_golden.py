@@ -4,7 +4,7 @@ Run in the build container only (the reference never travels to the GPU box):
 
     PYTHONDONTWRITEBYTECODE=1 MPLBACKEND=Agg python tests/golden/make_golden.py [section ...]
 
-Sections: astar_readme astar_small astar_1024 dstar astar3d graph2d graph3d theta3d theta2d lpa rrt dwa lqr mpc hypot
+Sections: astar_readme astar_small astar_1024 dstar astar3d graph2d graph3d theta3d theta2d lpa dstarlite rrt dwa lqr mpc hypot
 Outputs are small fixtures (inputs + expected outputs) under tests/golden/.  The reference is
 imported with stubs for the modules absent from this image (osqp, pyvista), per SURVEY.md §8(c).
 """
@@ -736,12 +736,13 @@ def sec_theta2d(n=160):
 # ----------------------------------------------------------------------------------------------
 # LPAStar (lpa_star.py) -- SURVEY.md §8(f) rank 3 (the initial computeShortestPath + extractPath)
 def run_lpa(args):
-    occ, start, goal, heur = args
+    occ, start, goal, heur = args[:4]
+    lite = len(args) > 4 and args[4]
     pmp = import_reference()
     W, H = occ.shape
     env = pmp.Grid(W, H)
     env.update(obstacles_of(occ))
-    p = pmp.LPAStar(tuple(start), tuple(goal), env, heur)
+    p = (pmp.DStarLite if lite else pmp.LPAStar)(tuple(start), tuple(goal), env, heur)
     try:
         cost, path, _ = p.plan()
         err = ""
@@ -751,7 +752,7 @@ def run_lpa(args):
     return dict(cost=float(cost), path=[x * H + y for (x, y) in path], n_expand=len(p.EXPAND), err=err)
 
 
-def sec_lpa(n=120):
+def sec_lpa(n=120, lite=False):
     from python_motion_planning_amd import workloads as wl
 
     rng = np.random.default_rng(8642)
@@ -772,24 +773,26 @@ def sec_lpa(n=120):
         if i % 19 == 4:
             g = s
         cases.append((occ, tuple(int(v) for v in s), tuple(int(v) for v in g), "manhattan" if i % 4 == 3 else "euclidean"))
+    cases = [c + (lite,) for c in cases]
     with Pool(8) as pool:
         res = pool.map(run_lpa, cases, chunksize=2)
     dims = np.array([c[0].shape for c in cases], np.int32)
     occ_flat, occ_off = ragged([np.packbits(c[0].ravel()) for c in cases], np.uint8)
     path_flat, path_off = ragged([r["path"] for r in res])
     np.savez_compressed(
-        os.path.join(HERE, "lpa_small.npz"), dims=dims, occ_bits=occ_flat, occ_off=occ_off,
+        os.path.join(HERE, "dstarlite_small.npz" if lite else "lpa_small.npz"), dims=dims, occ_bits=occ_flat, occ_off=occ_off,
         start=np.array([c[1] for c in cases], np.int32), goal=np.array([c[2] for c in cases], np.int32),
         manhattan=np.array([c[3] == "manhattan" for c in cases]), cost=np.array([r["cost"] for r in res]),
         path=path_flat, path_off=path_off, n_expand=np.array([r["n_expand"] for r in res], np.int64),
         err=np.array([r["err"] for r in res]))
-    print("lpa", sum(1 for r in res if r["path"]), "with path,", sum(1 for r in res if r["err"]), "raise, of", len(res),
+    print("dstarlite" if lite else "lpa", sum(1 for r in res if r["path"]), "with path,", sum(1 for r in res if r["err"]), "raise, of", len(res),
           "readme", res[0]["cost"], res[0]["n_expand"])
 
 
 SECTIONS = dict(rrt=sec_rrt, mpc=sec_mpc, dwa=sec_dwa, local_plans=sec_local_plans, lqr=sec_lqr, astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
                 dstar=sec_dstar, astar3d=sec_astar3d,
-                graph2d=sec_graph2d, graph3d=sec_graph3d, theta3d=sec_theta3d, theta2d=sec_theta2d, lpa=sec_lpa)
+                graph2d=sec_graph2d, graph3d=sec_graph3d, theta3d=sec_theta3d, theta2d=sec_theta2d, lpa=sec_lpa,
+                dstarlite=lambda: sec_lpa(lite=True))
 
 if __name__ == "__main__":
     want = sys.argv[1:] or list(SECTIONS)

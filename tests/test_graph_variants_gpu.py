@@ -248,17 +248,19 @@ def test_theta2d_c2_subset_against_oracle():
             assert np.array_equal(P[k, :n], ref["path"][k, :n]), (algo, k)
 
 
-def test_lpastar_against_reference():
-    """LPAStar.plan (lpa_star.py:78-230) on lpa.hip vs the reference's runs (tests/golden/lpa_small.npz):
-    cost bits, path, len(EXPAND), and the raising runs (status 4 / ValueError from the drop-in)."""
+@pytest.mark.parametrize("lite", [False, True])
+def test_lpastar_against_reference(lite):
+    """LPAStar.plan (lpa_star.py:78-230) / DStarLite.plan (d_star_lite.py:14-187) on lpa.hip vs the
+    reference's runs (tests/golden/lpa_small.npz, dstarlite_small.npz): cost bits, path, len(EXPAND),
+    and the raising runs (status 4 / ValueError from the drop-in)."""
     import python_motion_planning_amd as pmp
     from python_motion_planning_amd import batch
 
     n = 0
-    for i, occ, z in grid_cases("lpa_small.npz"):
+    for i, occ, z in grid_cases("dstarlite_small.npz" if lite else "lpa_small.npz"):
         W, H = occ.shape
         heur = "manhattan" if z["manhattan"][i] else "euclidean"
-        r = batch.lpastar2d_batch(occ, z["start"][i][None], z["goal"][i][None], heur)
+        r = batch.lpastar2d_batch(occ, z["start"][i][None], z["goal"][i][None], heur, lite=lite)
         st = int(r["status"][0])
         assert int(r["n_expanded"][0]) == z["n_expand"][i], i
         if str(z["err"][i]):
@@ -271,15 +273,17 @@ def test_lpastar_against_reference():
         if i % 6 == 0:
             env = pmp.Grid(W, H)
             env.update({(int(a), int(b)) for a, b in np.argwhere(occ)})
-            cost, p, _ = pmp.LPAStar(tuple(z["start"][i]), tuple(z["goal"][i]), env, heur).plan()
+            cls = pmp.DStarLite if lite else pmp.LPAStar
+            cost, p, _ = cls(tuple(z["start"][i]), tuple(z["goal"][i]), env, heur).plan()
             assert cost == z["cost"][i] and [a * H + b for a, b in p] == path.tolist(), i
         n += 1
     assert n > 90
 
 
-def test_lpastar_batch_against_oracle():
-    """256 LPA* queries on one 96x80 grid (25 % obstacles) in one launch vs the oracle: status, cost,
-    path, len(EXPAND), pushes and max |U|."""
+@pytest.mark.parametrize("lite", [False, True])
+def test_lpastar_batch_against_oracle(lite):
+    """256 LPA* / D* Lite queries on one 96x80 grid (25 % obstacles) in one launch vs the oracle:
+    status, cost, path, len(EXPAND), pushes and max |U|."""
     from oracle import oracle as O
     from python_motion_planning_amd import batch
 
@@ -290,7 +294,7 @@ def test_lpastar_batch_against_oracle():
     free = np.argwhere(occ == 0)
     S = free[rng.integers(len(free), size=256)].astype(np.int32)
     G = free[rng.integers(len(free), size=256)].astype(np.int32)
-    r = batch.lpastar2d_batch(occ, S, G, counters=True)
+    r = batch.lpastar2d_batch(occ, S, G, counters=True, lite=lite)
     st = r["status"].cpu().numpy()
     cost = r["cost"].cpu().numpy()
     ne = r["n_expanded"].cpu().numpy()
@@ -298,7 +302,7 @@ def test_lpastar_batch_against_oracle():
     P = r["path"].cpu().numpy()
     pl = r["path_len"].cpu().numpy()
     for q in range(256):
-        ref = O.lpastar2d(occ, S[q], G[q])
+        ref = O.lpastar2d(occ, S[q], G[q], lite=lite)
         assert st[q] == ref["status"] and ne[q] == ref["n_expanded"], q
         assert ctr[q, 0] == ref["n_push"] and ctr[q, 3] == ref["max_u"], q
         if ref["status"] in (0, 1):

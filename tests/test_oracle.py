@@ -320,13 +320,15 @@ def test_theta2d_against_reference():
         n += 1
     assert n > 140
 
-def test_lpastar_against_reference():
-    """LPAStar.plan (lpa_star.py:78-87, 139-230): README grid + random grids, cost bits, path,
-    len(EXPAND), and the runs where the reference raises (U empties; start == goal)."""
+@pytest.mark.parametrize("lite", [False, True])
+def test_lpastar_against_reference(lite):
+    """LPAStar.plan (lpa_star.py:78-87, 139-230) and DStarLite.plan (d_star_lite.py:14-187): README grid
+    + random grids, cost bits, path, len(EXPAND), and the runs where the reference raises (U empties;
+    start == goal)."""
     n = 0
-    for i, occ, z in grid_cases("lpa_small.npz"):
+    for i, occ, z in grid_cases("dstarlite_small.npz" if lite else "lpa_small.npz"):
         heur = "manhattan" if z["manhattan"][i] else "euclidean"
-        r = O.lpastar2d(occ, z["start"][i], z["goal"][i], heur)
+        r = O.lpastar2d(occ, z["start"][i], z["goal"][i], heur, lite=lite)
         assert r["n_expanded"] == z["n_expand"][i], i
         if str(z["err"][i]):
             assert r["status"] == 4, i
