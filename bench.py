@@ -341,6 +341,90 @@ def astar3d_leg(args, torch, dist, world, rank):
             "cpu_baseline": cpu}
 
 
+def graphs_leg(args, torch, dist, world, rank):
+    """Widened planners on the same measurement bar: ThetaStar /
+    LazyThetaStar 2D on C2 queries (1024^2 grid, astar2d.hip THETA = 1 / 2), and LPAStar / DStarLite
+    on README-grid queries (lpa.hip).  Each: plans/s over `--graph-steps` launches, HIP-event kernel
+    time, and the oracle (C restatement, OpenMP or a loop) timed on a bounded sample beside it."""
+    from python_motion_planning_amd import batch, workloads as wl
+
+    out = {}
+    occ2, s2, g2 = wl.c2_workload(4096, pair_seed=1 + rank)
+    nq = args.theta_queries
+    s2, g2 = s2[:nq], g2[:nq]
+    occ_bits = batch.occ_bits_device(occ2, torch)
+    for algo in ("theta_star", "lazy_theta_star"):
+        def run(i, algo=algo, counters=False):
+            return batch.astar2d_batch((1024, 1024), s2, g2, path_cap=8192, occ_bits=occ_bits, counters=counters,
+                                       algo=algo, retry_overflow=False)
+        r = run(0, counters=True)
+        torch.cuda.synchronize()
+        c = r["counters"].cpu().numpy()
+        elapsed, kern_ms = timed(torch, dist, run, args.graph_steps)
+        alg = astar_algorithmic_bytes(c)
+        achieved = alg / (kern_ms * 1e-3) / 1e9
+        cpu = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            from oracle import oracle as O
+
+            ns, th = min(256, nq), cpu_threads()
+            t = time.perf_counter()
+            ref = O.astar2d_batch(occ2, s2[:ns], g2[:ns], path_cap=8192, nthreads=th, algo=algo)
+            dt = time.perf_counter() - t
+            assert np.array_equal(ref["cost"], r["cost"][:ns].cpu().numpy()), f"GPU/oracle {algo} cost mismatch"
+            cpu = {"value": ns / dt, "unit": "plans/s", "cores": th, "kind": "port",
+                   "sample": f"first {ns} of the {nq} queries, C restatement (oracle/pmp_oracle.c) with OpenMP over "
+                             f"queries, {dt:.1f} s wall"}
+        out[algo + "_2d"] = {
+            "metric": f"{algo} 2D plans/sec on the C2 1024^2 grid", "value": nq * args.graph_steps * world / elapsed,
+            "unit": "plans/s", "queries_per_gpu": nq, "steps": args.graph_steps,
+            "ms_per_step": elapsed / args.graph_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": alg,
+                         "note": "A*'s 19E + 16(P+Q) bytes; the line-of-sight cells are not counted"},
+            "detail": {"expansions_per_launch": int(c[:, 2].sum()), "pushes_per_launch": int(c[:, 0].sum())},
+            "cpu_baseline": cpu}
+
+    occ = wl.readme_grid()
+    free = np.argwhere(occ == 0)
+    rng = np.random.default_rng(3 + rank)
+    nl = args.lpa_queries
+    sl = free[rng.integers(len(free), size=nl)].astype(np.int32)
+    gl = free[rng.integers(len(free), size=nl)].astype(np.int32)
+    s_d, g_d = torch.as_tensor(sl, device="cuda"), torch.as_tensor(gl, device="cuda")
+    for lite in (False, True):
+        def run(i, lite=lite, counters=False):
+            return batch.lpastar2d_batch(occ, s_d, g_d, counters=counters, lite=lite)
+        r = run(0, counters=True)
+        torch.cuda.synchronize()
+        c = r["counters"].cpu().numpy()
+        elapsed, kern_ms = timed(torch, dist, run, args.graph_steps)
+        cpu = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            from oracle import oracle as O
+
+            ns = min(512, nl)
+            t = time.perf_counter()
+            costs = [O.lpastar2d(occ, sl[q], gl[q], lite=lite)["cost"] for q in range(ns)]
+            dt = time.perf_counter() - t
+            assert np.array_equal(np.array(costs), r["cost"][:ns].cpu().numpy()), "GPU/oracle LPA* cost mismatch"
+            cpu = {"value": ns / dt, "unit": "plans/s", "cores": 1, "kind": "port",
+                   "sample": f"first {ns} of the {nl} queries, C restatement (oracle/pmp_oracle.c), one core, "
+                             f"{dt:.1f} s wall"}
+        name = "dstar_lite" if lite else "lpa_star"
+        out[name] = {
+            "metric": f"{name} plans/sec on the README 51x31 grid ({nl} random free-cell pairs)",
+            "value": nl * args.graph_steps * world / elapsed, "unit": "plans/s", "queries_per_gpu": nl,
+            "steps": args.graph_steps, "ms_per_step": elapsed / args.graph_steps * 1e3, "kernel_ms_per_launch": kern_ms,
+            "dtype": "f64", "roofline": None,
+            "roofline_note": "latency-bound list machine (U scans / shifts of a few hundred entries per expansion, "
+                             "L2-resident); no HBM or MFMA roofline applies",
+            "detail": {"expansions_per_launch": int(c[:, 1].sum()), "pushes_per_launch": int(c[:, 0].sum()),
+                       "max_U": int(c[:, 3].max())},
+            "cpu_baseline": cpu}
+    return out
+
+
 def track_leg(args, torch, dist, world, rank, kind):
     """LQR / MPC tracking (lqr.py:58-86 / mpc.py:66-94) for the C4 agents: one timed step = one launch
     running `iters` plan iterations of every agent (MPC at p = 30, m = 8, ADMM to 1e-9)."""
@@ -425,8 +509,11 @@ def main():
     ap.add_argument("--agents", type=int, default=256, help="C4 agents per GPU (control-step leg)")
     ap.add_argument("--control-steps", type=int, default=20, help="timed control steps")
     ap.add_argument("--workers", type=int, default=3072, help="persistent A* workers (waves) per launch")
-    ap.add_argument("--legs", default="dwa,rrt,astar3d,lqr,mpc",
-                    help="secondary legs to run (comma list of dwa, rrt, astar3d, lqr, mpc; 'none' for none)")
+    ap.add_argument("--legs", default="dwa,rrt,astar3d,lqr,mpc,graphs",
+                    help="secondary legs to run (comma list of dwa, rrt, astar3d, lqr, mpc, graphs; 'none' for none)")
+    ap.add_argument("--theta-queries", type=int, default=4096, help="C2 queries per Theta* / Lazy Theta* 2D launch")
+    ap.add_argument("--lpa-queries", type=int, default=4096, help="README-grid queries per LPA* / D* Lite launch")
+    ap.add_argument("--graph-steps", type=int, default=2)
     ap.add_argument("--rrt-queries", type=int, default=256)
     ap.add_argument("--rrt-samples", type=int, default=65536)
     ap.add_argument("--rrt-steps", type=int, default=4)
@@ -565,6 +652,8 @@ def main():
         secondary["lqr"] = track_leg(args, torch, dist, world, rank, "lqr")
     if "mpc" in legs:
         secondary["mpc_qp"] = track_leg(args, torch, dist, world, rank, "mpc")
+    if "graphs" in legs:
+        secondary.update(graphs_leg(args, torch, dist, world, rank))
 
     if rank == 0:
         out = {

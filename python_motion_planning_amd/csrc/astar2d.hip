@@ -510,17 +510,36 @@ __device__ bool los2d(const uint32_t* occ, int H, int x1, int y1, int x2, int y2
     const bool xmaj = dx > dy;
     const int T = xmaj ? dy - dx : dx - dy;
     const int du = xmaj ? dx : dy, dv = xmaj ? dy : dx;  // major / minor deltas
-    for (int it = 0; it <= dx + dy + 1; it++) {
-        if (xmaj ? x == x2 : y == y2) return true;
-        const bool maj = 2 * e >= T, mino = 2 * e <= T;  // e > tau: major step; e < tau: minor; equal: both
-        if (maj) {
-            if (xmaj) x += sx; else y += sy;
+    // The cells a line visits do not depend on the grid, so 8 steps are generated first and their
+    // 8 bit loads issued as one round (one memory latency per 8 cells instead of per cell); the
+    // first blocked cell in step order decides, as in the reference's loop.
+    constexpr int kB = 8;
+    for (int it = 0; it <= dx + dy + 1; it += kB) {
+        uint32_t ci[kB];
+        int nv = 0;
+#pragma unroll
+        for (int j = 0; j < kB; j++) {
+            const bool go = !(xmaj ? x == x2 : y == y2);
+            if (go) {
+                const bool maj = 2 * e >= T, mino = 2 * e <= T;  // e > tau: major; e < tau: minor; equal: both
+                if (maj) {
+                    if (xmaj) x += sx; else y += sy;
+                }
+                if (mino) {
+                    if (xmaj) y += sy; else x += sx;
+                }
+                e += (maj ? -dv : 0) + (mino ? du : 0);
+                nv++;
+            }
+            ci[j] = go ? (uint32_t)x * (uint32_t)H + (uint32_t)y : ~0u;
         }
-        if (mino) {
-            if (xmaj) y += sy; else x += sx;
-        }
-        e += (maj ? -dv : 0) + (mino ? du : 0);
-        if (occ_bit(occ, H, x, y)) return false;
+        uint32_t wv[kB];
+#pragma unroll
+        for (int j = 0; j < kB; j++) wv[j] = ci[j] != ~0u ? occ[ci[j] >> 5] : 0u;
+#pragma unroll
+        for (int j = 0; j < kB; j++)
+            if (ci[j] != ~0u && ((wv[j] >> (ci[j] & 31u)) & 1u)) return false;
+        if (nv < kB || (xmaj ? x == x2 : y == y2)) return true;
     }
     return false;
 }
