@@ -221,6 +221,24 @@ int pmp_dstarlite2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, 
                           const int32_t* start_xy, const int32_t* goal_xy, int nq, double* cost, int32_t* path_len,
                           uint32_t* path, int path_cap, int32_t* n_expanded, int64_t* counters, int32_t* status);
 
+/*
+ * Batched LPA* incremental replanning: LPAStar.plan() followed by nt LPAStar.OnPress edits
+ * (global_planner/graph_search/lpa_star.py:101-137) without the figure.  Edit p toggles the
+ * obstacle at toggles[q][p] (in-grid cells): a freed cell gets updateVertex, then its free
+ * neighbours do, and plan() runs again on the kept g / rhs / U (len(EXPAND) restarts per plan).
+ * Each worker edits its own copy of the grid; the shared occ_bits are not written.
+ *   toggles   [nq][nt][2] i32 (nt >= 1)
+ *   cost, n_expanded, status  [nq][nt + 1]: every plan's result, status as pmp_lpastar2d_batch,
+ *             -1 = not run (an earlier plan raised, which ends OnPress in the reference)
+ *   path_len [nq], path [nq][path_cap]: the last plan's path (start -> goal)
+ *   counters  nullable [nq][4] i64, cumulative over the plans (pushes, last plan's expansions and
+ *             extractPath steps, max |U|)
+ */
+int pmp_lpastar2d_replan_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H, int heuristic,
+                               const int32_t* start_xy, const int32_t* goal_xy, int nq, const int32_t* toggles, int nt,
+                               double* cost, int32_t* n_expanded, int32_t* status, int32_t* path_len, uint32_t* path,
+                               int path_cap, int64_t* counters);
+
 /* LQR settings (local_planner/lqr.py:35-38): diag Q, diag R, Riccati iteration cap and the
  * signed exit threshold of lqr.py:134.  Reference defaults: q = 1,1,1  r = 1,1  iters 100  eps 0.1. */
 typedef struct {

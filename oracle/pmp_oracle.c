@@ -1883,10 +1883,13 @@ static int lpa_update(const uint8_t* occ, int W, int H, int heuristic, int32_t s
  * from the goal (rhs = 0) toward the start, keys add h(node, start) + km (km = 0 in plan()), a popped
  * node with an outdated key is re-keyed (:104-106), updateVertex skips the goal (:131-132), and
  * extractPath walks from the start to the goal without reversing (:156-187). */
-static int lpa_core(int lite, const uint8_t* occ, int W, int H, int heuristic, int sx, int sy, int gx, int gy,
-                    double* cost_out, int32_t* path, int path_cap, int32_t* path_len, int64_t* counters)
+static int lpa_core(int lite, const uint8_t* occ_in, int W, int H, int heuristic, int sx, int sy, int gx, int gy,
+                    double* cost_out, int32_t* path, int path_cap, int32_t* path_len, int64_t* counters,
+                    const int32_t* toggles, int nt, double* rp_cost, int32_t* rp_nexp, int32_t* rp_status)
 {
     const int64_t ncell = (int64_t)W * H;
+    uint8_t* occ = (uint8_t*)malloc((size_t)ncell); /* OnPress edits the obstacle set */
+    memcpy(occ, occ_in, (size_t)ncell);
     double* g = (double*)malloc(sizeof(double) * (size_t)ncell);
     double* rhs = (double*)malloc(sizeof(double) * (size_t)ncell);
     int32_t* pos = (int32_t*)malloc(sizeof(int32_t) * (size_t)ncell);
@@ -1905,7 +1908,7 @@ static int lpa_core(int lite, const uint8_t* occ, int W, int H, int heuristic, i
     if (lite && start == goal) {
         /* map[start] overwrote map[goal] (:58-59): the goal node in U is detached, its g = 0 never
          * reaches a neighbour's rhs, so the first expansion pushes nothing and U empties */
-        free(g); free(rhs); free(pos); free(U.cell); free(U.k1); free(U.k2);
+        free(g); free(rhs); free(pos); free(U.cell); free(U.k1); free(U.k2); free(occ);
         if (counters) { counters[0] = 1; counters[1] = 1; counters[2] = 0; counters[3] = 1; }
         return 4;
     }
@@ -1913,7 +1916,33 @@ static int lpa_core(int lite, const uint8_t* occ, int W, int H, int heuristic, i
     u_push(&U, pos, src, lpa_h(heuristic, ox, oy, tx, ty), 0.0);
     npush++;
     maxn = 1;
+    /* phase 0: plan(); phase p >= 1: LPAStar.OnPress (lpa_star.py:101-137) at toggles[p - 1] */
+    for (int phase = 0; phase <= nt; phase++) {
+    if (phase > 0) {
+        nexp = 0;
+        steps = 0;
+        *cost_out = 0.0;
+        *path_len = 0;
+        const int cx = toggles[2 * phase - 2], cy = toggles[2 * phase - 1];
+        const int32_t cc = cx * H + cy;
+        if (!occ[cc]) {
+            occ[cc] = 1;
+        } else {
+            occ[cc] = 0;
+            status = lpa_update(occ, W, H, heuristic, src, tx, ty, g, rhs, pos, &U, cc, &npush);
+        }
+        for (int m = 0; m < 8 && !status; m++) { /* getNeighbor(node_change) raises before any update */
+            const int ux = cx + MX8[m], uy = cy + MY8[m];
+            if (ux < 0 || uy < 0 || ux >= W || uy >= H) status = 4;
+        }
+        for (int m = 0; m < 8 && !status; m++) {
+            const int ux = cx + MX8[m], uy = cy + MY8[m];
+            if (occ[(int64_t)ux * H + uy]) continue;
+            status = lpa_update(occ, W, H, heuristic, src, tx, ty, g, rhs, pos, &U, ux * H + uy, &npush);
+        }
+    }
     for (;;) {
+        if (status) break;
         if (U.n == 0) { status = 4; break; }
         int64_t bi = 0;
         for (int64_t i = 1; i < U.n; i++)
@@ -1988,19 +2017,44 @@ static int lpa_core(int lite, const uint8_t* occ, int W, int H, int heuristic, i
             *path_len = (int32_t)len;
         }
     }
+    if (nt > 0) {
+        rp_cost[phase] = (status == 0 || status == 1) ? *cost_out : 0.0;
+        rp_nexp[phase] = (int32_t)nexp;
+        rp_status[phase] = status;
+    }
+    if (status != 0 && status != 1) {
+        for (int p2 = phase + 1; p2 <= nt; p2++) { rp_cost[p2] = 0.0; rp_nexp[p2] = 0; rp_status[p2] = -1; }
+        break;
+    }
+    if (status == 1 && phase < nt) status = 0;
+    } /* phase */
     if (counters) { counters[0] = npush; counters[1] = nexp; counters[2] = steps; counters[3] = maxn; }
-    free(g); free(rhs); free(pos); free(U.cell); free(U.k1); free(U.k2);
+    free(g); free(rhs); free(pos); free(U.cell); free(U.k1); free(U.k2); free(occ);
     return status;
 }
 
 int oracle_lpastar2d(const uint8_t* occ, int W, int H, int heuristic, int sx, int sy, int gx, int gy,
                      double* cost_out, int32_t* path, int path_cap, int32_t* path_len, int64_t* counters)
 {
-    return lpa_core(0, occ, W, H, heuristic, sx, sy, gx, gy, cost_out, path, path_cap, path_len, counters);
+    return lpa_core(0, occ, W, H, heuristic, sx, sy, gx, gy, cost_out, path, path_cap, path_len, counters, NULL, 0,
+                    NULL, NULL, NULL);
+}
+
+/* LPAStar.plan() followed by nt OnPress edits (lpa_star.py:101-137) at toggles[nt][2]: rp_* [nt + 1]
+ * hold each plan's cost / len(EXPAND) / status (-1 = not run: an earlier plan raised); path is the
+ * last plan's. */
+int oracle_lpastar2d_replan(const uint8_t* occ, int W, int H, int heuristic, int sx, int sy, int gx, int gy,
+                            const int32_t* toggles, int nt, double* rp_cost, int32_t* rp_nexp, int32_t* rp_status,
+                            int32_t* path, int path_cap, int32_t* path_len, int64_t* counters)
+{
+    double c;
+    return lpa_core(0, occ, W, H, heuristic, sx, sy, gx, gy, &c, path, path_cap, path_len, counters, toggles, nt,
+                    rp_cost, rp_nexp, rp_status);
 }
 
 int oracle_dstarlite2d(const uint8_t* occ, int W, int H, int heuristic, int sx, int sy, int gx, int gy,
                        double* cost_out, int32_t* path, int path_cap, int32_t* path_len, int64_t* counters)
 {
-    return lpa_core(1, occ, W, H, heuristic, sx, sy, gx, gy, cost_out, path, path_cap, path_len, counters);
+    return lpa_core(1, occ, W, H, heuristic, sx, sy, gx, gy, cost_out, path, path_cap, path_len, counters, NULL, 0,
+                    NULL, NULL, NULL);
 }

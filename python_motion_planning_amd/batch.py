@@ -285,6 +285,41 @@ def lpastar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: 
     return out
 
 
+def lpastar2d_replan_batch(occ, starts, goals, toggles, heuristic: str = "euclidean", path_cap: int = 1001,
+                           counters: bool = False, stream=None):
+    """LPAStar.plan() then one LPAStar.OnPress edit (lpa_star.py:101-137) per toggle, each followed by
+    plan() on the kept state, for every query (pmp_lpastar2d_replan_batch).  toggles [nq, nt, 2].
+    Returns cost / n_expanded / status [nq, nt + 1] (status -1 = not run) and the last plan's path."""
+    torch = _lib.device_check()
+    L = _lib.load_library()
+    ctx = _lib.context()
+    occ = np.asarray(occ)
+    W, H = occ.shape
+    occ_bits = occ_bits_device(occ, torch)
+    s = _dev(torch, starts, torch.int32).reshape(-1, 2)
+    g = _dev(torch, goals, torch.int32).reshape(-1, 2)
+    nq = int(s.shape[0])
+    t = _dev(torch, toggles, torch.int32).reshape(nq, -1, 2)
+    nt = int(t.shape[1])
+    if nt < 1:
+        raise ValueError("lpastar2d_replan_batch needs at least one toggle per query")
+    if bool(((t[..., 0] < 0) | (t[..., 0] >= W) | (t[..., 1] < 0) | (t[..., 1] >= H)).any()):
+        raise ValueError("toggle cells must lie in the grid (OnPress rejects others, lpa_star.py:108-109)")
+    out = dict(cost=torch.empty((nq, nt + 1), dtype=torch.float64, device="cuda"),
+               n_expanded=torch.empty((nq, nt + 1), dtype=torch.int32, device="cuda"),
+               status=torch.empty((nq, nt + 1), dtype=torch.int32, device="cuda"),
+               path_len=torch.empty(nq, dtype=torch.int32, device="cuda"),
+               path=torch.empty((nq, int(path_cap)), dtype=torch.int32, device="cuda"))
+    out["counters"] = torch.empty((nq, 4), dtype=torch.int64, device="cuda") if counters else None
+    rc = L.pmp_lpastar2d_replan_batch(ctx, stream if stream is not None else _lib.stream_ptr(), occ_bits.data_ptr(), W, H,
+                                      1 if heuristic == "manhattan" else 0, s.data_ptr(), g.data_ptr(), nq,
+                                      t.data_ptr(), nt, out["cost"].data_ptr(), out["n_expanded"].data_ptr(),
+                                      out["status"].data_ptr(), out["path_len"].data_ptr(), out["path"].data_ptr(),
+                                      int(path_cap), _lib.ptr(out["counters"]))
+    _lib.check(ctx, rc, "pmp_lpastar2d_replan_batch")
+    return out
+
+
 def map_arrays(env, torch=None):
     """Map obstacle lists (env.py:83-117) -> device f64 tensors rect [nr,4], circ [nc,3], bnd [nb,4]."""
     torch = torch or _lib.device_check()

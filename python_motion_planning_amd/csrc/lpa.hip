@@ -188,12 +188,18 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
                                                  int path_cap, int32_t* __restrict__ nexp_out,
                                                  int64_t* __restrict__ counters, int32_t* __restrict__ status_out,
                                                  int* __restrict__ queue, double* __restrict__ scr_f64,
-                                                 int32_t* __restrict__ scr_i32, int lite)
+                                                 int32_t* __restrict__ scr_i32, int lite,
+                                                 const int32_t* __restrict__ toggles, int nt,
+                                                 double* __restrict__ rp_cost, int32_t* __restrict__ rp_nexp,
+                                                 int32_t* __restrict__ rp_status, uint32_t* __restrict__ occ_scr)
 {
     const int lane = lane_id();
     const size_t ncell = (size_t)W * (size_t)H;
+    const size_t nwords = (ncell + 31) / 32;
     Q S;
-    S.occ = occ;
+    // replanning toggles obstacles, so each worker then works on its own copy of the grid
+    uint32_t* occ_w = nt > 0 ? occ_scr + (size_t)blockIdx.x * nwords : nullptr;
+    S.occ = nt > 0 ? occ_w : occ;
     S.W = W;
     S.H = H;
     S.heur = heur;
@@ -229,6 +235,8 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
                 S.rhs[i] = kInf;
                 S.pos[i] = -1;
             }
+            if (nt > 0)
+                for (size_t i = lane; i < nwords; i += 64) occ_w[i] = occ[i];
             wave_sync_mem();
             const int32_t start = sx * H + sy, goal = gx * H + gy;
             S.src = lite ? goal : start;
@@ -246,7 +254,36 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
                 nexp = 1;
                 S.n = 0;
             }
+            // phase 0: plan(); phase p >= 1: LPAStar.OnPress (lpa_star.py:101-137) at toggles[p - 1]:
+            // flip the cell, updateVertex(cell) if it was freed, updateVertex on its free neighbours,
+            // then plan() again on the kept g / rhs / U (EXPAND restarts)
+            for (int phase = 0; phase <= nt; phase++) {
+            if (phase > 0) {
+                nexp = 0;
+                steps = 0;
+                cost = 0.0;
+                len = 0;
+                const int tx = uni(toggles[2 * ((size_t)q * nt + phase - 1)]);
+                const int ty = uni(toggles[2 * ((size_t)q * nt + phase - 1) + 1]);
+                const int32_t tc = tx * H + ty;
+                const bool was = occ_at(S.occ, H, tx, ty);
+                if (lane == 0) {
+                    if (was) occ_w[tc >> 5] &= ~(1u << (tc & 31));
+                    else occ_w[tc >> 5] |= 1u << (tc & 31);
+                }
+                wave_sync_mem();
+                if (was) st = update_vertex(S, tc, lane);
+                if (!st) {  // getNeighbor(node_change): KeyError off the grid before any update
+                    const int ux = tx + kMX[lane & 7], uy = ty + kMY[lane & 7];
+                    const bool in = (unsigned)ux < (unsigned)W && (unsigned)uy < (unsigned)H;
+                    if (ballot(lane < 8 && !in)) st = PMP_REF_RAISES;
+                    const uint32_t nbm = (uint32_t)ballot(lane < 8 && in && !occ_at(S.occ, H, ux, uy)) & 0xffu;
+                    for (int m = 0; m < 8 && !st; m++)
+                        if ((nbm >> m) & 1u) st = update_vertex(S, (tx + kMX[m]) * H + (ty + kMY[m]), lane);
+                }
+            }
             for (;;) {
+                if (st) break;
                 if (S.n == 0) { st = PMP_REF_RAISES; break; }  // min() of an empty list
                 // safety bound only (LPA* on a static grid settles every cell a bounded number of
                 // times): a runaway query stops with status 3 instead of holding the GPU
@@ -314,7 +351,7 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
                     const int ux = vx + kMX[lane & 7], uy = vy + kMY[lane & 7];
                     const bool in = (unsigned)ux < (unsigned)W && (unsigned)uy < (unsigned)H;
                     const uint64_t bad = ballot(lane < 8 && !in);
-                    const bool ok = lane < 8 && in && !occ_at(occ, H, ux, uy);
+                    const bool ok = lane < 8 && in && !occ_at(S.occ, H, ux, uy);
                     nbm = (uint32_t)ballot(ok) & 0xffu;
                     if (bad) st = PMP_REF_RAISES;  // KeyError while the list is built: no update runs
                 }
@@ -342,8 +379,8 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
                     bool valid = false;
                     double gu = 0.0;
                     if (lane < 8 && in) {
-                        bool coll = occ_at(occ, H, ux, uy) || occ_at(occ, H, x, y);
-                        if ((m & 1) && !coll) coll = occ_at(occ, H, ux, y) || occ_at(occ, H, x, uy);
+                        bool coll = occ_at(S.occ, H, ux, uy) || occ_at(S.occ, H, x, y);
+                        if ((m & 1) && !coll) coll = occ_at(S.occ, H, ux, y) || occ_at(S.occ, H, x, uy);
                         valid = !coll;
                         gu = S.g[ux * H + uy];
                     }
@@ -375,6 +412,24 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
                         }
                 }
             }
+            if (nt > 0 && lane == 0) {
+                const size_t k = (size_t)q * (nt + 1) + phase;
+                rp_cost[k] = (st == 0 || st == PMP_NO_PATH) ? cost : 0.0;
+                rp_nexp[k] = (int32_t)nexp;
+                rp_status[k] = st;
+            }
+            if (st != 0 && st != PMP_NO_PATH) {  // the reference raised: no further OnPress runs
+                if (lane == 0)
+                    for (int p2 = phase + 1; p2 <= nt; p2++) {
+                        const size_t k = (size_t)q * (nt + 1) + p2;
+                        rp_cost[k] = 0.0;
+                        rp_nexp[k] = 0;
+                        rp_status[k] = -1;
+                    }
+                break;
+            }
+            if (st == PMP_NO_PATH && phase < nt) st = 0;  // (cost, []) is a result, not a raise
+            }  // phase
         }
         if (lane == 0) {
             status_out[q] = st;
@@ -396,7 +451,9 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
 
 static int lpa_batch(int lite, pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H, int heuristic,
                      const int32_t* start_xy, const int32_t* goal_xy, int nq, double* cost, int32_t* path_len,
-                     uint32_t* path, int path_cap, int32_t* n_expanded, int64_t* counters, int32_t* status)
+                     uint32_t* path, int path_cap, int32_t* n_expanded, int64_t* counters, int32_t* status,
+                     const int32_t* toggles = nullptr, int nt = 0, double* rp_cost = nullptr, int32_t* rp_nexp = nullptr,
+                     int32_t* rp_status = nullptr)
 {
     if (!ctx) return PMP_EINVAL;
     if (W < 1 || H < 1 || W > kMaxDim || H > kMaxDim)
@@ -417,10 +474,16 @@ static int lpa_batch(int lite, pmp_ctx* ctx, void* stream, const uint32_t* occ_b
     int32_t* i32 = (int32_t*)pmp_scratch(ctx, SCR_AUX3, (size_t)workers * ncell * 8 + 16);
     int* queue = (int*)pmp_scratch(ctx, SCR_AUX0, 256);
     if (!f || !i32 || !queue) return PMP_ENOMEM;
+    uint32_t* occ_scr = nullptr;
+    if (nt > 0) {
+        occ_scr = (uint32_t*)pmp_scratch(ctx, SCR_AUX4, (size_t)workers * ((ncell + 31) / 32) * 4 + 16);
+        if (!occ_scr) return PMP_ENOMEM;
+    }
     hipStream_t s = (hipStream_t)stream;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
     hipLaunchKernelGGL(lpa_kernel, dim3(workers), dim3(64), 0, s, occ_bits, W, H, heuristic, start_xy, goal_xy, nq, cost,
-                       path_len, path, path_cap, n_expanded, counters, status, queue, f, i32, lite);
+                       path_len, path, path_cap, n_expanded, counters, status, queue, f, i32, lite, toggles, nt,
+                       rp_cost, rp_nexp, rp_status, occ_scr);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }
@@ -441,4 +504,23 @@ extern "C" int pmp_dstarlite2d_batch(pmp_ctx* ctx, void* stream, const uint32_t*
 {
     return lpa_batch(1, ctx, stream, occ_bits, W, H, heuristic, start_xy, goal_xy, nq, cost, path_len, path, path_cap,
                      n_expanded, counters, status);
+}
+
+extern "C" int pmp_lpastar2d_replan_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H,
+                                          int heuristic, const int32_t* start_xy, const int32_t* goal_xy, int nq,
+                                          const int32_t* toggles, int nt, double* cost, int32_t* n_expanded,
+                                          int32_t* status, int32_t* path_len, uint32_t* path, int path_cap,
+                                          int64_t* counters)
+{
+    if (!ctx) return PMP_EINVAL;
+    if (nt < 1 || !toggles || !cost || !n_expanded || !status)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar2d_replan_batch: need nt >= 1 toggles and the per-plan outputs");
+    if (nq > 0 && (!path_len || !path)) return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar2d_replan_batch: null path output");
+    // the last plan's cost / status / len(EXPAND) also land in the single-plan outputs; scratch for them
+    double* c1 = (double*)pmp_scratch(ctx, SCR_AUX1, (size_t)(nq > 0 ? nq : 1) * 16 + 16);
+    if (!c1) return PMP_ENOMEM;
+    int32_t* n1 = (int32_t*)(c1 + (nq > 0 ? nq : 1));
+    int32_t* s1 = n1 + (nq > 0 ? nq : 1);
+    return lpa_batch(0, ctx, stream, occ_bits, W, H, heuristic, start_xy, goal_xy, nq, c1, path_len, path, path_cap, n1,
+                     counters, s1, toggles, nt, cost, n_expanded, status);
 }

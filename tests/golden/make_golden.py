@@ -4,7 +4,7 @@ Run in the build container only (the reference never travels to the GPU box):
 
     PYTHONDONTWRITEBYTECODE=1 MPLBACKEND=Agg python tests/golden/make_golden.py [section ...]
 
-Sections: astar_readme astar_small astar_1024 dstar astar3d graph2d graph3d theta3d theta2d lpa dstarlite rrt dwa lqr mpc hypot
+Sections: astar_readme astar_small astar_1024 dstar astar3d graph2d graph3d theta3d theta2d lpa dstarlite lpa_replan rrt dwa lqr mpc hypot
 Outputs are small fixtures (inputs + expected outputs) under tests/golden/.  The reference is
 imported with stubs for the modules absent from this image (osqp, pyvista), per SURVEY.md §8(c).
 """
@@ -789,10 +789,79 @@ def sec_lpa(n=120, lite=False):
           "readme", res[0]["cost"], res[0]["n_expand"])
 
 
+# LPAStar.OnPress replanning (lpa_star.py:101-137) without the figure: the same edits on the planner
+def run_lpa_replan(args):
+    occ, start, goal, toggles = args
+    pmp = import_reference()
+    W, H = occ.shape
+    env = pmp.Grid(W, H)
+    env.update(obstacles_of(occ))
+    p = pmp.LPAStar(tuple(start), tuple(goal), env, "euclidean")
+    costs, nexp, errs, path = [], [], [], []
+    try:
+        cost, path, _ = p.plan()
+        costs.append(float(cost)); nexp.append(len(p.EXPAND)); errs.append("")
+        for (x, y) in toggles:
+            p.EXPAND = []
+            node_change = p.map[(x, y)]
+            if (x, y) not in p.obstacles:
+                p.obstacles.add((x, y))
+            else:
+                p.obstacles.remove((x, y))
+                p.updateVertex(node_change)
+            p.env.update(p.obstacles)
+            for node_n in p.getNeighbor(node_change):
+                p.updateVertex(node_n)
+            cost, path, _ = p.plan()
+            costs.append(float(cost)); nexp.append(len(p.EXPAND)); errs.append("")
+    except (ValueError, KeyError) as e:
+        costs.append(float("nan")); nexp.append(len(p.EXPAND)); errs.append(type(e).__name__)
+        path = []
+    close_figs()
+    return dict(cost=costs, nexp=nexp, err=errs, path=[x * H + y for (x, y) in path])
+
+
+def sec_lpa_replan(n=60, nt=4):
+    from python_motion_planning_amd import workloads as wl
+
+    rng = np.random.default_rng(9753)
+    cases = []
+    for i in range(n):
+        if i < 4:
+            occ = wl.readme_grid()
+        else:
+            W, H = int(rng.integers(10, 41)), int(rng.integers(10, 41))
+            occ = (rng.random((W, H)) < float(rng.uniform(0.0, 0.3))).astype(np.uint8)
+            occ[:, 0] = occ[:, -1] = 1
+            occ[0, :] = occ[-1, :] = 1
+        W, H = occ.shape
+        free = np.argwhere(occ == 0)
+        s = tuple(int(v) for v in free[rng.integers(len(free))])
+        g = tuple(int(v) for v in free[rng.integers(len(free))])
+        if i < 4:
+            s, g = (5, 5), (45, 25)
+        inner = np.argwhere(np.ones((W - 2, H - 2), bool)) + 1
+        tg = [tuple(int(v) for v in inner[rng.integers(len(inner))]) for _ in range(nt)]
+        cases.append((occ, s, g, tg))
+    with Pool(8) as pool:
+        res = pool.map(run_lpa_replan, cases, chunksize=2)
+    dims = np.array([c[0].shape for c in cases], np.int32)
+    occ_flat, occ_off = ragged([np.packbits(c[0].ravel()) for c in cases], np.uint8)
+    path_flat, path_off = ragged([r["path"] for r in res])
+    pad = lambda v, f: [list(x) + [f] * (nt + 1 - len(x)) for x in v]  # noqa: E731
+    np.savez_compressed(
+        os.path.join(HERE, "lpa_replan.npz"), dims=dims, occ_bits=occ_flat, occ_off=occ_off,
+        start=np.array([c[1] for c in cases], np.int32), goal=np.array([c[2] for c in cases], np.int32),
+        toggles=np.array([c[3] for c in cases], np.int32),
+        cost=np.array(pad([r["cost"] for r in res], float("nan"))), nexp=np.array(pad([r["nexp"] for r in res], 0)),
+        err=np.array(pad([r["err"] for r in res], "-")), path=path_flat, path_off=path_off)
+    print("lpa_replan", len(res), "cases;", sum(1 for r in res if r["err"][-1]), "raise")
+
+
 SECTIONS = dict(rrt=sec_rrt, mpc=sec_mpc, dwa=sec_dwa, local_plans=sec_local_plans, lqr=sec_lqr, astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
                 dstar=sec_dstar, astar3d=sec_astar3d,
                 graph2d=sec_graph2d, graph3d=sec_graph3d, theta3d=sec_theta3d, theta2d=sec_theta2d, lpa=sec_lpa,
-                dstarlite=lambda: sec_lpa(lite=True))
+                dstarlite=lambda: sec_lpa(lite=True), lpa_replan=sec_lpa_replan)
 
 if __name__ == "__main__":
     want = sys.argv[1:] or list(SECTIONS)

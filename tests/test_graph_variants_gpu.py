@@ -309,3 +309,42 @@ def test_lpastar_batch_against_oracle(lite):
             assert cost[q] == ref["cost"], q
         if ref["status"] == 0:
             assert np.array_equal(P[q, : pl[q]], ref["path_cells"]), q
+
+
+def test_lpastar_replan_against_reference_and_oracle():
+    """LPA* incremental replanning (pmp_lpastar2d_replan_batch: plan() + OnPress edits, lpa_star.py:101-137)
+    vs the reference's replays (tests/golden/lpa_replan.npz), all 60 cases in one launch, then a 256-query
+    batch with 6 edits each on a 64x48 grid vs the oracle."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import batch
+
+    for i, occ, z in grid_cases("lpa_replan.npz"):
+        r = batch.lpastar2d_replan_batch(occ, z["start"][i][None], z["goal"][i][None], z["toggles"][i][None])
+        st = r["status"][0].cpu().numpy()
+        ne = r["n_expanded"][0].cpu().numpy()
+        cost = r["cost"][0].cpu().numpy()
+        errs = z["err"][i].tolist()
+        for ph, e in enumerate(errs):
+            if e == "-":
+                assert st[ph] == -1, (i, ph)
+                continue
+            assert ne[ph] == z["nexp"][i][ph], (i, ph)
+            assert (st[ph] == 4) if e else (st[ph] in (0, 1) and cost[ph] == z["cost"][i][ph]), (i, ph)
+        if not any(errs):
+            pl = int(r["path_len"][0])
+            assert np.array_equal(r["path"][0, :pl].cpu().numpy(), seg(z["path"], z["path_off"], i)), i
+
+    rng = np.random.default_rng(21)
+    occ = (rng.random((64, 48)) < 0.2).astype(np.uint8)
+    occ[:, 0] = occ[:, -1] = 1
+    occ[0, :] = occ[-1, :] = 1
+    free = np.argwhere(occ == 0)
+    S = free[rng.integers(len(free), size=256)].astype(np.int32)
+    G = free[rng.integers(len(free), size=256)].astype(np.int32)
+    T = (np.argwhere(np.ones((62, 46), bool)) + 1)[rng.integers(62 * 46, size=(256, 6))].astype(np.int32)
+    r = batch.lpastar2d_replan_batch(occ, S, G, T)
+    st, ne, cost = (r[k].cpu().numpy() for k in ("status", "n_expanded", "cost"))
+    for q in range(256):
+        ref = O.lpastar2d_replan(occ, S[q], G[q], T[q])
+        assert np.array_equal(st[q], ref["status"]) and np.array_equal(ne[q], ref["n_expanded"]), q
+        assert np.array_equal(cost[q], ref["cost"]), q

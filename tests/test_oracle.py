@@ -338,6 +338,23 @@ def test_lpastar_against_reference(lite):
         n += 1
     assert n > 90
 
+def test_lpastar_replan_against_reference():
+    """LPAStar.plan() + 4 OnPress edits each (lpa_star.py:101-137, replayed without the figure): every
+    plan's cost bits and len(EXPAND), the raising plans, and the last path."""
+    for i, occ, z in grid_cases("lpa_replan.npz"):
+        r = O.lpastar2d_replan(occ, z["start"][i], z["goal"][i], z["toggles"][i])
+        for ph, e in enumerate(z["err"][i].tolist()):
+            if e == "-":
+                assert r["status"][ph] == -1, (i, ph)
+                continue
+            assert r["n_expanded"][ph] == z["nexp"][i][ph], (i, ph)
+            if e:
+                assert r["status"][ph] == 4, (i, ph)
+            else:
+                assert r["status"][ph] in (0, 1) and r["cost"][ph] == z["cost"][i][ph], (i, ph)
+        if not any(z["err"][i].tolist()[k] for k in range(len(z["err"][i]))):
+            assert np.array_equal(r["path_cells"], seg(z["path"], z["path_off"], i)), i
+
 def test_graph3d_published_csv():
     """The reference's published Dijkstra3D / GBFS3D rows of 3d_pathfinding_results.csv."""
     from python_motion_planning_amd import workloads as wl
