@@ -239,6 +239,20 @@ int pmp_lpastar2d_replan_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_b
                                double* cost, int32_t* n_expanded, int32_t* status, int32_t* path_len, uint32_t* path,
                                int path_cap, int64_t* counters);
 
+/*
+ * Batched D* Lite incremental replanning: DStarLite.plan() followed by nt DStarLite.OnPress calls
+ * (global_planner/graph_search/d_star_lite.py:61-97) without the figure: walk from the start along
+ * min-g neighbours; after the first step set km = h(step, start), apply the edit as
+ * pmp_lpastar2d_replan_batch does, computeShortestPath on the kept state, and walk on to the goal.
+ * cost[q][p] is the walk's cost and path the last walk (start -> goal); the walk has no step limit
+ * in the reference (it can loop forever), so here it stops with status 3 after 4 W H + 4 steps.
+ * Arguments and outputs otherwise as pmp_lpastar2d_replan_batch.
+ */
+int pmp_dstarlite2d_replan_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H, int heuristic,
+                                 const int32_t* start_xy, const int32_t* goal_xy, int nq, const int32_t* toggles,
+                                 int nt, double* cost, int32_t* n_expanded, int32_t* status, int32_t* path_len,
+                                 uint32_t* path, int path_cap, int64_t* counters);
+
 /* LQR settings (local_planner/lqr.py:35-38): diag Q, diag R, Riccati iteration cap and the
  * signed exit threshold of lqr.py:134.  Reference defaults: q = 1,1,1  r = 1,1  iters 100  eps 0.1. */
 typedef struct {

@@ -573,14 +573,15 @@ def lpastar2d(occ: np.ndarray, start, goal, heuristic: str = "euclidean", lite: 
                 n_push=int(ctr[0]), n_expanded=int(ctr[1]), steps=int(ctr[2]), max_u=int(ctr[3]))
 
 
-def lpastar2d_replan(occ: np.ndarray, start, goal, toggles, heuristic: str = "euclidean"):
+def lpastar2d_replan(occ: np.ndarray, start, goal, toggles, heuristic: str = "euclidean", lite: bool = False):
     """LPAStar.plan() then one LPAStar.OnPress edit (lpa_star.py:101-137) per toggle cell, each
-    followed by plan() on the kept state.  Returns per-plan cost / n_expanded / status arrays
+    followed by plan() on the kept state; lite=True: DStarLite.plan() then DStarLite.OnPress
+    (d_star_lite.py:61-97: walk, km, edit, computeShortestPath, walk on) per toggle.  Returns per-plan cost / n_expanded / status arrays
     (status -1 = not run because an earlier plan raised) and the last plan's path."""
     L = lib()
     if not getattr(L, "_lpar_set", False):
         L.oracle_lpastar2d_replan.restype = ctypes.c_int
-        L.oracle_lpastar2d_replan.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+        L.oracle_lpastar2d_replan.argtypes = [ctypes.c_int, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                               ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p, ctypes.c_int, _dp,
                                               _i32p, _i32p, _i32p, ctypes.c_int, _i32p, _i64p]
         L._lpar_set = True
@@ -594,7 +595,7 @@ def lpastar2d_replan(occ: np.ndarray, start, goal, toggles, heuristic: str = "eu
     path = np.zeros(1002, np.int32)
     plen = ctypes.c_int32(0)
     ctr = np.zeros(4, np.int64)
-    L.oracle_lpastar2d_replan(_p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0, int(start[0]), int(start[1]),
+    L.oracle_lpastar2d_replan(int(bool(lite)), _p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0, int(start[0]), int(start[1]),
                               int(goal[0]), int(goal[1]), _p(t, _i32p), nt, _p(cost, _dp), _p(nexp, _i32p),
                               _p(st, _i32p), _p(path, _i32p), 1002, ctypes.byref(plen), _p(ctr, _i64p))
     return dict(cost=cost, n_expanded=nexp, status=st, path_cells=path[: plen.value].copy())

@@ -1844,8 +1844,8 @@ static inline double lpa_h(int heuristic, int x, int y, int gx, int gy)
 
 /* updateVertex (:162-179).  Returns 4 when the reference raises (KeyError off the map, or min()
  * of an empty neighbour list). */
-static int lpa_update(const uint8_t* occ, int W, int H, int heuristic, int32_t src, int gx, int gy, double* g,
-                      double* rhs, int32_t* pos, ulist_t* U, int32_t v, int64_t* npush)
+static int lpa_update(const uint8_t* occ, int W, int H, int heuristic, int32_t src, int gx, int gy, double km,
+                      double* g, double* rhs, int32_t* pos, ulist_t* U, int32_t v, int64_t* npush)
 {
     const int x = v / H, y = v % H;
     if (v != src) {
@@ -1870,10 +1870,26 @@ static int lpa_update(const uint8_t* occ, int W, int H, int heuristic, int32_t s
     }
     if (g[v] != rhs[v]) {
         const double mn = g[v] < rhs[v] ? g[v] : rhs[v];
-        u_push(U, pos, v, mn + lpa_h(heuristic, x, y, gx, gy), mn);
+        u_push(U, pos, v, mn + lpa_h(heuristic, x, y, gx, gy) + km, mn);
         (*npush)++;
     }
     return 0;
+}
+
+/* one greedy step of extractPath / D* Lite's OnPress walk: first minimal-g neighbour in motion order
+ * among the free ones isCollision allows; -1 where the reference raises */
+static int lpa_greedy(const uint8_t* occ, int W, int H, const double* g, int32_t c)
+{
+    const int x = c / H, y = c % H;
+    int bm = -1;
+    double bg = 0.0;
+    for (int m = 0; m < 8; m++) {
+        const int ux = x + MX8[m], uy = y + MY8[m];
+        if (ux < 0 || uy < 0 || ux >= W || uy >= H) return -1;
+        if (occ[(int64_t)ux * H + uy] || collide2(occ, W, H, x, y, ux, uy)) continue;
+        if (bm < 0 || g[ux * H + uy] < bg) { bm = m; bg = g[ux * H + uy]; }
+    }
+    return bm;
 }
 
 /* status 0 found, 1 extractPath gave up after 1000 steps (cost kept, path empty), 4 the reference
@@ -1916,20 +1932,50 @@ static int lpa_core(int lite, const uint8_t* occ_in, int W, int H, int heuristic
     u_push(&U, pos, src, lpa_h(heuristic, ox, oy, tx, ty), 0.0);
     npush++;
     maxn = 1;
-    /* phase 0: plan(); phase p >= 1: LPAStar.OnPress (lpa_star.py:101-137) at toggles[p - 1] */
+    /* phase 0: plan(); phase p >= 1: OnPress at toggles[p - 1] -- LPAStar's (lpa_star.py:101-137):
+     * edit, then plan(); DStarLite's (d_star_lite.py:61-97): walk from the start along min-g
+     * neighbours, after the first step set km = h(step, start), edit, computeShortestPath, walk on */
+    double km = 0.0, wcost = 0.0;
+    int32_t wcur = tgt;
+    int64_t wlen = 0;
     for (int phase = 0; phase <= nt; phase++) {
+    int walk_only = 0;
     if (phase > 0) {
         nexp = 0;
         steps = 0;
         *cost_out = 0.0;
         *path_len = 0;
+        if (lite) {
+            wcur = tgt;
+            wcost = 0.0;
+            wlen = 0;
+            if (wlen < path_cap) path[wlen] = wcur;
+            wlen++;
+            if (wcur == src) {
+                walk_only = 1;
+            } else {
+                const int bm = lpa_greedy(occ, W, H, g, wcur);
+                if (bm < 0) status = 4;
+                else {
+                    const int x = wcur / H, y = wcur % H;
+                    wcost += (bm & 1) ? sqrt(2.0) : 1.0;
+                    wcur = (x + MX8[bm]) * H + (y + MY8[bm]);
+                    if (wlen < path_cap) path[wlen] = wcur;
+                    wlen++;
+                    steps++;
+                    km = lpa_h(heuristic, x + MX8[bm], y + MY8[bm], sx, sy);
+                }
+            }
+        }
+    }
+    if (phase > 0 && !walk_only && !status) {
         const int cx = toggles[2 * phase - 2], cy = toggles[2 * phase - 1];
         const int32_t cc = cx * H + cy;
         if (!occ[cc]) {
             occ[cc] = 1;
         } else {
             occ[cc] = 0;
-            status = lpa_update(occ, W, H, heuristic, src, tx, ty, g, rhs, pos, &U, cc, &npush);
+            status = lpa_update(occ, W, H, heuristic, src, tx, ty, km, g, rhs, pos, &U, cc, &npush);
         }
         for (int m = 0; m < 8 && !status; m++) { /* getNeighbor(node_change) raises before any update */
             const int ux = cx + MX8[m], uy = cy + MY8[m];
@@ -1938,11 +1984,11 @@ static int lpa_core(int lite, const uint8_t* occ_in, int W, int H, int heuristic
         for (int m = 0; m < 8 && !status; m++) {
             const int ux = cx + MX8[m], uy = cy + MY8[m];
             if (occ[(int64_t)ux * H + uy]) continue;
-            status = lpa_update(occ, W, H, heuristic, src, tx, ty, g, rhs, pos, &U, ux * H + uy, &npush);
+            status = lpa_update(occ, W, H, heuristic, src, tx, ty, km, g, rhs, pos, &U, ux * H + uy, &npush);
         }
     }
     for (;;) {
-        if (status) break;
+        if (status || walk_only) break;
         if (U.n == 0) { status = 4; break; }
         int64_t bi = 0;
         for (int64_t i = 1; i < U.n; i++)
@@ -1952,7 +1998,7 @@ static int lpa_core(int lite, const uint8_t* occ_in, int W, int H, int heuristic
          * when U empties */
         const double gg = start == goal ? INFINITY : g[tgt], grhs = start == goal ? INFINITY : rhs[tgt];
         const double gm = gg < grhs ? gg : grhs;
-        const double gk1 = gm + 0.0; /* calculateKey(goal): h(goal, goal) = 0 */
+        const double gk1 = gm + 0.0 + km; /* calculateKey(tgt): h(tgt, tgt) = 0 */
         if (!key_lt(U.k1[bi], U.k2[bi], gk1, gm) && grhs == gg) break;
         const int32_t v = U.cell[bi];
         const double vk1 = U.k1[bi], vk2 = U.k2[bi];
@@ -1962,7 +2008,7 @@ static int lpa_core(int lite, const uint8_t* occ_in, int W, int H, int heuristic
         const int x = v / H, y = v % H;
         if (lite) { /* node.key < calculateKey(node): re-key, push, nothing else (:104-106) */
             const double mn = g[v] < rhs[v] ? g[v] : rhs[v];
-            const double c1 = mn + lpa_h(heuristic, x, y, tx, ty) + 0.0, c2 = mn;
+            const double c1 = mn + lpa_h(heuristic, x, y, tx, ty) + km, c2 = mn;
             if (key_lt(vk1, vk2, c1, c2)) {
                 u_push(&U, pos, v, c1, c2);
                 npush++;
@@ -1974,18 +2020,34 @@ static int lpa_core(int lite, const uint8_t* occ_in, int W, int H, int heuristic
             g[v] = rhs[v];
         } else {
             g[v] = INFINITY;
-            if ((status = lpa_update(occ, W, H, heuristic, src, tx, ty, g, rhs, pos, &U, v, &npush))) break;
+            if ((status = lpa_update(occ, W, H, heuristic, src, tx, ty, km, g, rhs, pos, &U, v, &npush))) break;
         }
         for (int m = 0; m < 8 && !status; m++) {
             const int ux = x + MX8[m], uy = y + MY8[m];
             if (ux < 0 || uy < 0 || ux >= W || uy >= H) { status = 4; break; }
             if (occ[(int64_t)ux * H + uy]) continue;
-            status = lpa_update(occ, W, H, heuristic, src, tx, ty, g, rhs, pos, &U, ux * H + uy, &npush);
+            status = lpa_update(occ, W, H, heuristic, src, tx, ty, km, g, rhs, pos, &U, ux * H + uy, &npush);
         }
         if (status) break;
         if (U.n > maxn) maxn = U.n;
     }
-    if (status == 0) { /* extractPath: greedy min-g neighbour from tgt, first minimum in motion order */
+    if (status == 0 && lite && phase > 0) { /* the rest of OnPress's walk: no step limit (a bound here) */
+        while (wcur != src) {
+            const int bm = lpa_greedy(occ, W, H, g, wcur);
+            if (bm < 0) { status = 4; break; }
+            const int x = wcur / H, y = wcur % H;
+            wcost += (bm & 1) ? sqrt(2.0) : 1.0;
+            wcur = (x + MX8[bm]) * H + (y + MY8[bm]);
+            if (wlen < path_cap) path[wlen] = wcur;
+            wlen++;
+            if (++steps > 4 * ncell + 4) { status = 3; break; }
+        }
+        *cost_out = wcost;
+        if (status == 0) {
+            if (wlen > path_cap) status = 2;
+            *path_len = (int32_t)wlen;
+        }
+    } else if (status == 0) { /* extractPath: greedy min-g neighbour from tgt, first minimum in motion order */
         int32_t c = tgt;
         double cost = 0.0;
         int64_t len = 0;
@@ -2043,12 +2105,12 @@ int oracle_lpastar2d(const uint8_t* occ, int W, int H, int heuristic, int sx, in
 /* LPAStar.plan() followed by nt OnPress edits (lpa_star.py:101-137) at toggles[nt][2]: rp_* [nt + 1]
  * hold each plan's cost / len(EXPAND) / status (-1 = not run: an earlier plan raised); path is the
  * last plan's. */
-int oracle_lpastar2d_replan(const uint8_t* occ, int W, int H, int heuristic, int sx, int sy, int gx, int gy,
+int oracle_lpastar2d_replan(int lite, const uint8_t* occ, int W, int H, int heuristic, int sx, int sy, int gx, int gy,
                             const int32_t* toggles, int nt, double* rp_cost, int32_t* rp_nexp, int32_t* rp_status,
                             int32_t* path, int path_cap, int32_t* path_len, int64_t* counters)
 {
     double c;
-    return lpa_core(0, occ, W, H, heuristic, sx, sy, gx, gy, &c, path, path_cap, path_len, counters, toggles, nt,
+    return lpa_core(lite, occ, W, H, heuristic, sx, sy, gx, gy, &c, path, path_cap, path_len, counters, toggles, nt,
                     rp_cost, rp_nexp, rp_status);
 }
 

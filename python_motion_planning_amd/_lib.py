@@ -44,6 +44,8 @@ SIGNATURES = {
     "pmp_dstarlite2d_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     "pmp_lpastar2d_replan_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _i,
                                         _vp]),
+    "pmp_dstarlite2d_replan_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _i,
+                                          _vp]),
     "pmp_rrt_batch": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _i, _vp, _i, _vp, _vp, _i, _vp, ctypes.c_int64, _i, _vp, _vp,
                            _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     "pmp_track_step_batch": (_i, [_vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp,

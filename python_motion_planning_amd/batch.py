@@ -286,9 +286,10 @@ def lpastar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: 
 
 
 def lpastar2d_replan_batch(occ, starts, goals, toggles, heuristic: str = "euclidean", path_cap: int = 1001,
-                           counters: bool = False, stream=None):
+                           counters: bool = False, stream=None, lite: bool = False):
     """LPAStar.plan() then one LPAStar.OnPress edit (lpa_star.py:101-137) per toggle, each followed by
-    plan() on the kept state, for every query (pmp_lpastar2d_replan_batch).  toggles [nq, nt, 2].
+    plan() on the kept state, for every query (pmp_lpastar2d_replan_batch); lite=True: DStarLite.plan()
+    then DStarLite.OnPress per toggle (d_star_lite.py:61-97, pmp_dstarlite2d_replan_batch).  toggles [nq, nt, 2].
     Returns cost / n_expanded / status [nq, nt + 1] (status -1 = not run) and the last plan's path."""
     torch = _lib.device_check()
     L = _lib.load_library()
@@ -311,12 +312,13 @@ def lpastar2d_replan_batch(occ, starts, goals, toggles, heuristic: str = "euclid
                path_len=torch.empty(nq, dtype=torch.int32, device="cuda"),
                path=torch.empty((nq, int(path_cap)), dtype=torch.int32, device="cuda"))
     out["counters"] = torch.empty((nq, 4), dtype=torch.int64, device="cuda") if counters else None
-    rc = L.pmp_lpastar2d_replan_batch(ctx, stream if stream is not None else _lib.stream_ptr(), occ_bits.data_ptr(), W, H,
+    fn = L.pmp_dstarlite2d_replan_batch if lite else L.pmp_lpastar2d_replan_batch
+    rc = fn(ctx, stream if stream is not None else _lib.stream_ptr(), occ_bits.data_ptr(), W, H,
                                       1 if heuristic == "manhattan" else 0, s.data_ptr(), g.data_ptr(), nq,
                                       t.data_ptr(), nt, out["cost"].data_ptr(), out["n_expanded"].data_ptr(),
                                       out["status"].data_ptr(), out["path_len"].data_ptr(), out["path"].data_ptr(),
                                       int(path_cap), _lib.ptr(out["counters"]))
-    _lib.check(ctx, rc, "pmp_lpastar2d_replan_batch")
+    _lib.check(ctx, rc, "pmp_dstarlite2d_replan_batch" if lite else "pmp_lpastar2d_replan_batch")
     return out
 
 

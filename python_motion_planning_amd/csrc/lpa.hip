@@ -43,6 +43,7 @@ struct Q {
     double* Uk2;
     int n;         // |U| (wave-uniform)
     int64_t npush;
+    double km;     // D* Lite's key offset (0 in plan(), set by OnPress)
 };
 
 __device__ __forceinline__ bool occ_at(const uint32_t* occ, int H, int x, int y)
@@ -176,9 +177,65 @@ __device__ int update_vertex(Q& S, int32_t v, int lane)
     }
     if (gv != rv) {
         const double mn = gv < rv ? gv : rv;
-        u_push(S, v, mn + hval(S, vx, vy), mn, lane);
+        u_push(S, v, mn + hval(S, vx, vy) + S.km, mn, lane);
     }
     return 0;
+}
+
+// One greedy step of extractPath (lpa_star.py:209-230) / D* Lite's OnPress walk (d_star_lite.py:
+// 73-83): the first minimal-g neighbour in motion order among the free ones that isCollision allows.
+// Returns the motion, or -1 where the reference raises (KeyError off the grid, min() of nothing).
+__device__ int greedy_step(const Q& S, int32_t c, int lane)
+{
+    const int H = S.H;
+    const int x = (int)((uint32_t)c / (uint32_t)H), y = c - x * H;
+    const int m = lane & 7;
+    const int ux = x + kMX[m], uy = y + kMY[m];
+    const bool in = (unsigned)ux < (unsigned)S.W && (unsigned)uy < (unsigned)H;
+    bool valid = false;
+    double gu = 0.0;
+    if (lane < 8 && in) {
+        bool coll = occ_at(S.occ, H, ux, uy) || occ_at(S.occ, H, x, y);
+        if ((m & 1) && !coll) coll = occ_at(S.occ, H, ux, y) || occ_at(S.occ, H, x, uy);
+        valid = !coll;
+        gu = S.g[ux * H + uy];
+    }
+    if (ballot(lane < 8 && !in)) return -1;
+    uint64_t vm = ballot(valid) & 0xffull;
+    int bm = -1;
+    double bg = 0.0;
+    while (vm) {
+        const int k = __ffsll((long long)vm) - 1;
+        vm &= vm - 1;
+        const double gk = __shfl(gu, k, 64);
+        if (bm < 0 || gk < bg) { bm = k; bg = gk; }
+    }
+    return bm;
+}
+
+// OnPress's obstacle edit at (tx, ty) (lpa_star.py:113-122 == d_star_lite.py:85-93): flip the cell in
+// the worker's grid, updateVertex the cell if it was freed, then its free neighbours
+__device__ int toggle_cell(Q& S, uint32_t* occ_w, int tx, int ty, int lane)
+{
+    const int H = S.H;
+    const int32_t tc = tx * H + ty;
+    const bool was = occ_at(S.occ, H, tx, ty);
+    if (lane == 0) {
+        if (was) occ_w[tc >> 5] &= ~(1u << (tc & 31));
+        else occ_w[tc >> 5] |= 1u << (tc & 31);
+    }
+    wave_sync_mem();
+    int st = 0;
+    if (was) st = update_vertex(S, tc, lane);
+    if (!st) {  // getNeighbor(node_change): KeyError off the grid before any update
+        const int ux = tx + kMX[lane & 7], uy = ty + kMY[lane & 7];
+        const bool in = (unsigned)ux < (unsigned)S.W && (unsigned)uy < (unsigned)H;
+        if (ballot(lane < 8 && !in)) st = PMP_REF_RAISES;
+        const uint32_t nbm = (uint32_t)ballot(lane < 8 && in && !occ_at(S.occ, H, ux, uy)) & 0xffu;
+        for (int m = 0; m < 8 && !st; m++)
+            if ((nbm >> m) & 1u) st = update_vertex(S, (tx + kMX[m]) * H + (ty + kMY[m]), lane);
+    }
+    return st;
 }
 
 __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ occ, int W, int H, int heur,
@@ -226,6 +283,7 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
         S.gy = lite ? sy : gy;
         S.n = 0;
         S.npush = 0;
+        S.km = 0.0;
         if (!((unsigned)sx < (unsigned)W && (unsigned)sy < (unsigned)H && (unsigned)gx < (unsigned)W &&
               (unsigned)gy < (unsigned)H)) {
             st = PMP_REF_RAISES;  // map lookups off the grid (KeyError)
@@ -258,6 +316,9 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
             // flip the cell, updateVertex(cell) if it was freed, updateVertex on its free neighbours,
             // then plan() again on the kept g / rhs / U (EXPAND restarts)
             for (int phase = 0; phase <= nt; phase++) {
+            // D* Lite's OnPress (d_star_lite.py:61-97): walk from the start along min-g neighbours; after
+            // the first step set km = h(step, start), edit the cell, computeShortestPath, walk on
+            int32_t wcur = S.tgt;
             if (phase > 0) {
                 nexp = 0;
                 steps = 0;
@@ -265,21 +326,32 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
                 len = 0;
                 const int tx = uni(toggles[2 * ((size_t)q * nt + phase - 1)]);
                 const int ty = uni(toggles[2 * ((size_t)q * nt + phase - 1) + 1]);
-                const int32_t tc = tx * H + ty;
-                const bool was = occ_at(S.occ, H, tx, ty);
-                if (lane == 0) {
-                    if (was) occ_w[tc >> 5] &= ~(1u << (tc & 31));
-                    else occ_w[tc >> 5] |= 1u << (tc & 31);
-                }
-                wave_sync_mem();
-                if (was) st = update_vertex(S, tc, lane);
-                if (!st) {  // getNeighbor(node_change): KeyError off the grid before any update
-                    const int ux = tx + kMX[lane & 7], uy = ty + kMY[lane & 7];
-                    const bool in = (unsigned)ux < (unsigned)W && (unsigned)uy < (unsigned)H;
-                    if (ballot(lane < 8 && !in)) st = PMP_REF_RAISES;
-                    const uint32_t nbm = (uint32_t)ballot(lane < 8 && in && !occ_at(S.occ, H, ux, uy)) & 0xffu;
-                    for (int m = 0; m < 8 && !st; m++)
-                        if ((nbm >> m) & 1u) st = update_vertex(S, (tx + kMX[m]) * H + (ty + kMY[m]), lane);
+                if (lite) {
+                    uint32_t* pth = path_out + (size_t)q * path_cap;
+                    if (lane == 0 && len < path_cap) pth[len] = (uint32_t)wcur;
+                    len++;
+                    if (wcur != S.src) {
+                        const int bm = greedy_step(S, wcur, lane);
+                        if (bm < 0) {
+                            st = PMP_REF_RAISES;
+                        } else {
+                            cost += (bm & 1) ? kSqrt2 : 1.0;
+                            const int x = (int)((uint32_t)wcur / (uint32_t)H), y = wcur - x * H;
+                            wcur = (x + kMX[bm]) * H + (y + kMY[bm]);
+                            if (lane == 0 && len < path_cap) pth[len] = (uint32_t)wcur;
+                            len++;
+                            steps++;
+                            // km = h(cur_start, new_start) with new_start = self.start
+                            const int cx = x + kMX[bm], cy = y + kMY[bm];
+                            S.km = S.heur == 1 ? (double)(abs(sx - cx) + abs(sy - cy))
+                                               : __dsqrt_rn((double)((sx - cx) * (sx - cx) + (sy - cy) * (sy - cy)));
+                            st = toggle_cell(S, occ_w, tx, ty, lane);
+                        }
+                    } else {
+                        st = -2;  // the walk never starts: no edit, no search (marker, cleared below)
+                    }
+                } else {
+                    st = toggle_cell(S, occ_w, tx, ty, lane);
                 }
             }
             for (;;) {
@@ -315,7 +387,7 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
                 const double gg = detached ? kInf : __shfl(ggt, 0, 64);
                 const double gr = detached ? kInf : __shfl(grt, 0, 64);
                 const double gm = gg < gr ? gg : gr;
-                if (!key_lt(b1, b2, gm + 0.0, gm) && gr == gg) break;  // calculateKey(goal): h = 0
+                if (!key_lt(b1, b2, gm + 0.0 + S.km, gm) && gr == gg) break;  // calculateKey(tgt): h = 0
                 const int32_t v = uni(vt);
                 if (lane == 0) S.pos[v] = -1;
                 wave_sync_mem();
@@ -330,7 +402,7 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
                 const int vx = (int)((uint32_t)v / (uint32_t)H), vy = v - vx * H;
                 if (lite) {  // node.key < calculateKey(node): re-key and push, nothing else (:104-106)
                     const double mn = gv < rv ? gv : rv;
-                    const double c1 = mn + hval(S, vx, vy) + 0.0;
+                    const double c1 = mn + hval(S, vx, vy) + S.km;
                     if (key_lt(b1, b2, c1, mn)) {
                         u_push(S, v, c1, mn, lane);
                         if (S.n > maxn) maxn = S.n;
@@ -364,42 +436,29 @@ __global__ __launch_bounds__(64) void lpa_kernel(const uint32_t* __restrict__ oc
                 if (st) break;
                 if (S.n > maxn) maxn = S.n;
             }
-            if (st == 0) {
-                // extractPath (:209-230): greedy min-g neighbour from the goal, first minimum in motion
-                // order; gives up (cost kept, empty path) after 1000 steps
+            if (st == -2) st = 0;  // D* Lite walk that starts at the goal: cost 0, path [start]
+            else if (st == 0) {
+                // extractPath (:209-230): greedy min-g neighbour from tgt, first minimum in motion order;
+                // gives up (cost kept, empty path) after 1000 steps.  D* Lite's OnPress walk continues
+                // from where its first step left it, with no step limit (a bound of its own here).
+                const bool onpress = lite && phase > 0;
                 uint32_t* pth = path_out + (size_t)q * path_cap;
-                int32_t c = S.tgt;
-                if (lane == 0 && len < path_cap) pth[len] = (uint32_t)c;
-                len++;
+                int32_t c = onpress ? wcur : S.tgt;
+                if (!onpress) {
+                    if (lane == 0 && len < path_cap) pth[len] = (uint32_t)c;
+                    len++;
+                }
                 while (c != S.src) {
-                    const int x = (int)((uint32_t)c / (uint32_t)H), y = c - x * H;
-                    const int m = lane & 7;
-                    const int ux = x + kMX[m], uy = y + kMY[m];
-                    const bool in = (unsigned)ux < (unsigned)W && (unsigned)uy < (unsigned)H;
-                    bool valid = false;
-                    double gu = 0.0;
-                    if (lane < 8 && in) {
-                        bool coll = occ_at(S.occ, H, ux, uy) || occ_at(S.occ, H, x, y);
-                        if ((m & 1) && !coll) coll = occ_at(S.occ, H, ux, y) || occ_at(S.occ, H, x, uy);
-                        valid = !coll;
-                        gu = S.g[ux * H + uy];
-                    }
-                    if (ballot(lane < 8 && !in)) { st = PMP_REF_RAISES; break; }
-                    uint64_t vm = ballot(valid) & 0xffull;
-                    if (!vm) { st = PMP_REF_RAISES; break; }
-                    int bm = -1;
-                    double bg = 0.0;
-                    while (vm) {
-                        const int k = __ffsll((long long)vm) - 1;
-                        vm &= vm - 1;
-                        const double gk = __shfl(gu, k, 64);
-                        if (bm < 0 || gk < bg) { bm = k; bg = gk; }
-                    }
+                    const int bm = greedy_step(S, c, lane);
+                    if (bm < 0) { st = PMP_REF_RAISES; break; }
                     cost += (bm & 1) ? kSqrt2 : 1.0;
+                    const int x = (int)((uint32_t)c / (uint32_t)H), y = c - x * H;
                     c = (x + kMX[bm]) * H + (y + kMY[bm]);
                     if (lane == 0 && len < path_cap) pth[len] = (uint32_t)c;
                     len++;
-                    if (++steps == 1000) { st = PMP_NO_PATH; break; }
+                    ++steps;
+                    if (!onpress && steps == 1000) { st = PMP_NO_PATH; break; }
+                    if (onpress && steps > (int64_t)4 * (int64_t)ncell + 4) { st = PMP_CAP_OVERFLOW; break; }
                 }
                 wave_sync_mem();
                 if (st == 0) {
@@ -506,11 +565,10 @@ extern "C" int pmp_dstarlite2d_batch(pmp_ctx* ctx, void* stream, const uint32_t*
                      n_expanded, counters, status);
 }
 
-extern "C" int pmp_lpastar2d_replan_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H,
-                                          int heuristic, const int32_t* start_xy, const int32_t* goal_xy, int nq,
-                                          const int32_t* toggles, int nt, double* cost, int32_t* n_expanded,
-                                          int32_t* status, int32_t* path_len, uint32_t* path, int path_cap,
-                                          int64_t* counters)
+static int replan_batch(int lite, pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H, int heuristic,
+                        const int32_t* start_xy, const int32_t* goal_xy, int nq, const int32_t* toggles, int nt,
+                        double* cost, int32_t* n_expanded, int32_t* status, int32_t* path_len, uint32_t* path,
+                        int path_cap, int64_t* counters)
 {
     if (!ctx) return PMP_EINVAL;
     if (nt < 1 || !toggles || !cost || !n_expanded || !status)
@@ -521,6 +579,26 @@ extern "C" int pmp_lpastar2d_replan_batch(pmp_ctx* ctx, void* stream, const uint
     if (!c1) return PMP_ENOMEM;
     int32_t* n1 = (int32_t*)(c1 + (nq > 0 ? nq : 1));
     int32_t* s1 = n1 + (nq > 0 ? nq : 1);
-    return lpa_batch(0, ctx, stream, occ_bits, W, H, heuristic, start_xy, goal_xy, nq, c1, path_len, path, path_cap, n1,
-                     counters, s1, toggles, nt, cost, n_expanded, status);
+    return lpa_batch(lite, ctx, stream, occ_bits, W, H, heuristic, start_xy, goal_xy, nq, c1, path_len, path, path_cap,
+                     n1, counters, s1, toggles, nt, cost, n_expanded, status);
+}
+
+extern "C" int pmp_lpastar2d_replan_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H,
+                                          int heuristic, const int32_t* start_xy, const int32_t* goal_xy, int nq,
+                                          const int32_t* toggles, int nt, double* cost, int32_t* n_expanded,
+                                          int32_t* status, int32_t* path_len, uint32_t* path, int path_cap,
+                                          int64_t* counters)
+{
+    return replan_batch(0, ctx, stream, occ_bits, W, H, heuristic, start_xy, goal_xy, nq, toggles, nt, cost, n_expanded,
+                        status, path_len, path, path_cap, counters);
+}
+
+extern "C" int pmp_dstarlite2d_replan_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H,
+                                            int heuristic, const int32_t* start_xy, const int32_t* goal_xy, int nq,
+                                            const int32_t* toggles, int nt, double* cost, int32_t* n_expanded,
+                                            int32_t* status, int32_t* path_len, uint32_t* path, int path_cap,
+                                            int64_t* counters)
+{
+    return replan_batch(1, ctx, stream, occ_bits, W, H, heuristic, start_xy, goal_xy, nq, toggles, nt, cost, n_expanded,
+                        status, path_len, path, path_cap, counters);
 }

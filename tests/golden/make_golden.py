@@ -4,7 +4,7 @@ Run in the build container only (the reference never travels to the GPU box):
 
     PYTHONDONTWRITEBYTECODE=1 MPLBACKEND=Agg python tests/golden/make_golden.py [section ...]
 
-Sections: astar_readme astar_small astar_1024 dstar astar3d graph2d graph3d theta3d theta2d lpa dstarlite lpa_replan rrt dwa lqr mpc hypot
+Sections: astar_readme astar_small astar_1024 dstar astar3d graph2d graph3d theta3d theta2d lpa dstarlite lpa_replan dstarlite_replan rrt dwa lqr mpc hypot
 Outputs are small fixtures (inputs + expected outputs) under tests/golden/.  The reference is
 imported with stubs for the modules absent from this image (osqp, pyvista), per SURVEY.md §8(c).
 """
@@ -790,18 +790,56 @@ def sec_lpa(n=120, lite=False):
 
 
 # LPAStar.OnPress replanning (lpa_star.py:101-137) without the figure: the same edits on the planner
+def dstarlite_onpress(p, x, y):
+    """DStarLite.OnPress (d_star_lite.py:61-97) without the figure and the prints."""
+    cur_start, new_start = p.start, p.start
+    update_start = True
+    cost, count = 0, 0
+    path = [p.start.current]
+    p.EXPAND = []
+    while cur_start != p.goal:
+        neighbors = [node_n for node_n in p.getNeighbor(cur_start) if not p.isCollision(cur_start, node_n)]
+        next_node = min(neighbors, key=lambda n: n.g)
+        path.append(next_node.current)
+        cost += p.cost(cur_start, next_node)
+        count += 1
+        cur_start = next_node
+        if count > 20000:
+            raise RuntimeError("walk does not end")
+        if update_start:
+            update_start = False
+            p.km = p.h(cur_start, new_start)
+            new_start = cur_start
+            node_change = p.map[(x, y)]
+            if (x, y) not in p.obstacles:
+                p.obstacles.add((x, y))
+            else:
+                p.obstacles.remove((x, y))
+                p.updateVertex(node_change)
+            p.env.update(p.obstacles)
+            for node_n in p.getNeighbor(node_change):
+                p.updateVertex(node_n)
+            p.computeShortestPath()
+    return cost, path
+
+
 def run_lpa_replan(args):
-    occ, start, goal, toggles = args
+    occ, start, goal, toggles = args[:4]
+    lite = len(args) > 4 and args[4]
     pmp = import_reference()
     W, H = occ.shape
     env = pmp.Grid(W, H)
     env.update(obstacles_of(occ))
-    p = pmp.LPAStar(tuple(start), tuple(goal), env, "euclidean")
+    p = (pmp.DStarLite if lite else pmp.LPAStar)(tuple(start), tuple(goal), env, "euclidean")
     costs, nexp, errs, path = [], [], [], []
     try:
         cost, path, _ = p.plan()
         costs.append(float(cost)); nexp.append(len(p.EXPAND)); errs.append("")
         for (x, y) in toggles:
+            if lite:
+                cost, path = dstarlite_onpress(p, x, y)
+                costs.append(float(cost)); nexp.append(len(p.EXPAND)); errs.append("")
+                continue
             p.EXPAND = []
             node_change = p.map[(x, y)]
             if (x, y) not in p.obstacles:
@@ -814,14 +852,14 @@ def run_lpa_replan(args):
                 p.updateVertex(node_n)
             cost, path, _ = p.plan()
             costs.append(float(cost)); nexp.append(len(p.EXPAND)); errs.append("")
-    except (ValueError, KeyError) as e:
+    except (ValueError, KeyError, RuntimeError) as e:
         costs.append(float("nan")); nexp.append(len(p.EXPAND)); errs.append(type(e).__name__)
         path = []
     close_figs()
     return dict(cost=costs, nexp=nexp, err=errs, path=[x * H + y for (x, y) in path])
 
 
-def sec_lpa_replan(n=60, nt=4):
+def sec_lpa_replan(n=60, nt=4, lite=False):
     from python_motion_planning_amd import workloads as wl
 
     rng = np.random.default_rng(9753)
@@ -842,7 +880,7 @@ def sec_lpa_replan(n=60, nt=4):
             s, g = (5, 5), (45, 25)
         inner = np.argwhere(np.ones((W - 2, H - 2), bool)) + 1
         tg = [tuple(int(v) for v in inner[rng.integers(len(inner))]) for _ in range(nt)]
-        cases.append((occ, s, g, tg))
+        cases.append((occ, s, g, tg, lite))
     with Pool(8) as pool:
         res = pool.map(run_lpa_replan, cases, chunksize=2)
     dims = np.array([c[0].shape for c in cases], np.int32)
@@ -850,18 +888,19 @@ def sec_lpa_replan(n=60, nt=4):
     path_flat, path_off = ragged([r["path"] for r in res])
     pad = lambda v, f: [list(x) + [f] * (nt + 1 - len(x)) for x in v]  # noqa: E731
     np.savez_compressed(
-        os.path.join(HERE, "lpa_replan.npz"), dims=dims, occ_bits=occ_flat, occ_off=occ_off,
+        os.path.join(HERE, "dstarlite_replan.npz" if lite else "lpa_replan.npz"), dims=dims, occ_bits=occ_flat, occ_off=occ_off,
         start=np.array([c[1] for c in cases], np.int32), goal=np.array([c[2] for c in cases], np.int32),
         toggles=np.array([c[3] for c in cases], np.int32),
         cost=np.array(pad([r["cost"] for r in res], float("nan"))), nexp=np.array(pad([r["nexp"] for r in res], 0)),
         err=np.array(pad([r["err"] for r in res], "-")), path=path_flat, path_off=path_off)
-    print("lpa_replan", len(res), "cases;", sum(1 for r in res if r["err"][-1]), "raise")
+    print("dstarlite_replan" if lite else "lpa_replan", len(res), "cases;", sum(1 for r in res if r["err"][-1]), "raise")
 
 
 SECTIONS = dict(rrt=sec_rrt, mpc=sec_mpc, dwa=sec_dwa, local_plans=sec_local_plans, lqr=sec_lqr, astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
                 dstar=sec_dstar, astar3d=sec_astar3d,
                 graph2d=sec_graph2d, graph3d=sec_graph3d, theta3d=sec_theta3d, theta2d=sec_theta2d, lpa=sec_lpa,
-                dstarlite=lambda: sec_lpa(lite=True), lpa_replan=sec_lpa_replan)
+                dstarlite=lambda: sec_lpa(lite=True), lpa_replan=sec_lpa_replan,
+                dstarlite_replan=lambda: sec_lpa_replan(lite=True))
 
 if __name__ == "__main__":
     want = sys.argv[1:] or list(SECTIONS)
