@@ -422,6 +422,38 @@ def graphs_leg(args, torch, dist, world, rank):
             "detail": {"expansions_per_launch": int(c[:, 1].sum()), "pushes_per_launch": int(c[:, 0].sum()),
                        "max_U": int(c[:, 3].max())},
             "cpu_baseline": cpu}
+
+    # incremental replanning: plan() + 4 OnPress obstacle edits per query, each followed by a re-plan
+    nt = 4
+    inner = np.argwhere(np.ones((occ.shape[0] - 2, occ.shape[1] - 2), bool)) + 1
+    T = inner[rng.integers(len(inner), size=(nl, nt))].astype(np.int32)
+    t_d = torch.as_tensor(T, device="cuda")
+    for lite in (False, True):
+        def run(i, lite=lite):
+            return batch.lpastar2d_replan_batch(occ, s_d, g_d, t_d, lite=lite)
+        r = run(0)
+        torch.cuda.synchronize()
+        ne = r["n_expanded"].cpu().numpy()
+        elapsed, kern_ms = timed(torch, dist, run, args.graph_steps)
+        cpu = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            from oracle import oracle as O
+
+            ns = min(256, nl)
+            t = time.perf_counter()
+            refc = [O.lpastar2d_replan(occ, sl[q], gl[q], T[q], lite=lite)["cost"] for q in range(ns)]
+            dt = time.perf_counter() - t
+            assert np.array_equal(np.array(refc), r["cost"][:ns].cpu().numpy()), "GPU/oracle replan cost mismatch"
+            cpu = {"value": ns * (nt + 1) / dt, "unit": "plans/s", "cores": 1, "kind": "port",
+                   "sample": f"first {ns} of the {nl} sessions ({nt} edits each), C restatement, one core, {dt:.1f} s wall"}
+        name = ("dstar_lite" if lite else "lpa_star") + "_replan"
+        out[name] = {
+            "metric": f"{name} plans/sec (plan() + {nt} OnPress edits per session, README grid, {nl} sessions)",
+            "value": nl * (nt + 1) * args.graph_steps * world / elapsed, "unit": "plans/s", "sessions_per_gpu": nl,
+            "steps": args.graph_steps, "ms_per_step": elapsed / args.graph_steps * 1e3,
+            "kernel_ms_per_launch": kern_ms, "dtype": "f64", "roofline": None,
+            "roofline_note": "latency-bound list machine, as lpa_star",
+            "detail": {"expansions_per_launch": int(np.maximum(ne, 0).sum())}, "cpu_baseline": cpu}
     return out
 
 
