@@ -599,3 +599,24 @@ def lpastar2d_replan(occ: np.ndarray, start, goal, toggles, heuristic: str = "eu
                               int(goal[0]), int(goal[1]), _p(t, _i32p), nt, _p(cost, _dp), _p(nexp, _i32p),
                               _p(st, _i32p), _p(path, _i32p), 1002, ctypes.byref(plen), _p(ctr, _i64p))
     return dict(cost=cost, n_expanded=nexp, status=st, path_cells=path[: plen.value].copy())
+
+
+def lpastar2d_batch(occ: np.ndarray, starts, goals, heuristic: str = "euclidean", lite: bool = False,
+                    nthreads: int = 0):
+    """OpenMP batch of the LPAStar.plan (or, lite, DStarLite.plan) restatement: cost, status, n_expanded."""
+    L = lib()
+    if not getattr(L, "_lpab_set", False):
+        L.oracle_lpastar2d_batch.restype = None
+        L.oracle_lpastar2d_batch.argtypes = [ctypes.c_int, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p,
+                                             _i32p, ctypes.c_int, _dp, _i32p, _i32p, ctypes.c_int]
+        L._lpab_set = True
+    occ = np.ascontiguousarray(occ, dtype=np.uint8)
+    W, H = occ.shape
+    s = np.ascontiguousarray(starts, np.int32).reshape(-1, 2)
+    g = np.ascontiguousarray(goals, np.int32).reshape(-1, 2)
+    nq = len(s)
+    out = dict(cost=np.zeros(nq), status=np.zeros(nq, np.int32), n_expanded=np.zeros(nq, np.int32))
+    L.oracle_lpastar2d_batch(int(bool(lite)), _p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0, _p(s, _i32p),
+                             _p(g, _i32p), nq, _p(out["cost"], _dp), _p(out["status"], _i32p),
+                             _p(out["n_expanded"], _i32p), int(nthreads))
+    return out

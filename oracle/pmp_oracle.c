@@ -2120,3 +2120,20 @@ int oracle_dstarlite2d(const uint8_t* occ, int W, int H, int heuristic, int sx, 
     return lpa_core(1, occ, W, H, heuristic, sx, sy, gx, gy, cost_out, path, path_cap, path_len, counters, NULL, 0,
                     NULL, NULL, NULL);
 }
+
+/* OpenMP batch of the LPAStar / DStarLite restatement (one grid, many queries; the bench's CPU
+ * baseline).  Outputs per query: cost, status, n_expanded. */
+void oracle_lpastar2d_batch(int lite, const uint8_t* occ, int W, int H, int heuristic, const int32_t* starts,
+                            const int32_t* goals, int nq, double* cost, int32_t* status, int32_t* n_expanded,
+                            int nthreads)
+{
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int q = 0; q < nq; q++) {
+        int32_t path[1002], plen;
+        int64_t ctr[4];
+        status[q] = lpa_core(lite, occ, W, H, heuristic, starts[2 * q], starts[2 * q + 1], goals[2 * q], goals[2 * q + 1],
+                             &cost[q], path, 1002, &plen, ctr, NULL, 0, NULL, NULL, NULL);
+        n_expanded[q] = (int32_t)ctr[1];
+    }
+}

@@ -525,7 +525,9 @@ static int lpa_batch(int lite, pmp_ctx* ctx, void* stream, const uint32_t* occ_b
     PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     const size_t ncell = (size_t)W * H;
     const size_t per_worker = ncell * 40;  // g, rhs, U keys (f64) + pos, U cells (i32)
-    int workers = 256 * 4;
+    // one wave per query up to 16 per CU: each query is a dependent chain of short U scans and
+    // shifts (L2-latency bound), so more resident waves hide more of it
+    int workers = 256 * 16;
     const size_t max_workers = ((size_t)16 << 30) / per_worker;  // scratch under 16 GiB
     if ((size_t)workers > max_workers) workers = (int)(max_workers > 0 ? max_workers : 1);
     if (workers > nq) workers = nq;
