@@ -356,7 +356,7 @@ def graphs_leg(args, torch, dist, world, rank):
     for algo in ("theta_star", "lazy_theta_star"):
         def run(i, algo=algo, counters=False):
             return batch.astar2d_batch((1024, 1024), s2, g2, path_cap=8192, occ_bits=occ_bits, counters=counters,
-                                       algo=algo, retry_overflow=False)
+                                       algo=algo, retry_overflow=False, reserve_slots=args.workers)
         r = run(0, counters=True)
         torch.cuda.synchronize()
         c = r["counters"].cpu().numpy()
