@@ -550,7 +550,8 @@ def main():
     ap.add_argument("--legs", default="dwa,rrt,astar3d,lqr,mpc,graphs",
                     help="secondary legs to run (comma list of dwa, rrt, astar3d, lqr, mpc, graphs; 'none' for none)")
     ap.add_argument("--theta-queries", type=int, default=4096, help="C2 queries per Theta* / Lazy Theta* 2D launch")
-    ap.add_argument("--lpa-queries", type=int, default=4096, help="README-grid queries per LPA* / D* Lite launch")
+    ap.add_argument("--lpa-queries", type=int, default=16384,
+                    help="README-grid queries per LPA* / D* Lite launch (4 per worker wave: the queue balances the tail)")
     ap.add_argument("--graph-steps", type=int, default=2)
     ap.add_argument("--rrt-queries", type=int, default=256)
     ap.add_argument("--rrt-samples", type=int, default=65536)
