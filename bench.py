@@ -535,6 +535,41 @@ def track_leg(args, torch, dist, world, rank, kind):
             "cpu_baseline": cpu}
 
 
+def dry_run(args, rank, world):
+    """--dry-run: the multi-rank plumbing without a GPU.  Ranks come from launch_ranks (or
+    torch.distributed.run), join a gloo group, take their longest-first round-robin share of one
+    96-query batch on a 64^2 grid, plan it with the CPU oracle standing in for the kernels, and
+    all_gather the records; rank 0 checks the gathered batch against one single-process oracle run
+    and prints a JSON line of the bench's shape (n_gpus = world)."""
+    import torch  # noqa: F401  (torch.distributed)
+
+    from oracle import oracle as O
+    from python_motion_planning_amd import shard, workloads as wl
+
+    dist = shard.init("gloo")
+    occ, starts, goals = wl.c2_workload(nq=96, W=64, H=64, pair_seed=6)
+
+    def plan(s, g):
+        r = O.astar2d_batch(occ, s, g, path_cap=4096, nthreads=1)
+        return {"cost": torch.as_tensor(r["cost"]), "status": torch.as_tensor(r["status"]),
+                "n_expanded": torch.as_tensor(r["n_expanded"]), "path_len": torch.as_tensor(r["path_len"])}
+
+    shard.barrier(dist)
+    t0 = time.perf_counter()
+    out = shard.run_sharded(dist, plan, starts, goals)
+    shard.barrier(dist)
+    (elapsed,) = shard.max_over_ranks(dist, [time.perf_counter() - t0])
+    if rank == 0:
+        ref = O.astar2d_batch(occ, starts, goals, path_cap=4096, nthreads=1)
+        equal = all(np.array_equal(out[k].numpy(), ref[k]) for k in ("cost", "status", "n_expanded", "path_len"))
+        print(json.dumps({"metric": "dry run: A* plans/sec (CPU oracle stand-in, 64^2 grid, 96 queries)",
+                          "value": 96 / elapsed, "unit": "plans/s", "n_gpus": world, "steps": 1, "warmup": 0,
+                          "scaling": "strong", "dry_run": True, "gathered_equal_single_rank": equal,
+                          "higher_is_better": True}), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -569,21 +604,43 @@ def main():
     ap.add_argument("--streams", type=int, default=3,
                     help="batches in flight: consecutive steps go to different HIP streams (own scratch "
                          "context each), so one batch's long-query tail overlaps the next batch")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: every rank plans its own --nq batch; strong: one --nq batch dealt over the ranks "
+                         "(longest-first round-robin) with an all_gather of the results")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: exercise the rank launcher, the strong-scaling deal and the result all_gather "
+                         "over gloo with the CPU oracle standing in for the kernels (tests/test_multirank.py)")
     args = ap.parse_args()
-
-    import torch
 
     from python_motion_planning_amd import shard
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # a bare `python bench.py --gpus N`: start the N rank processes here, before anything touches
+        # a GPU, and leave with their exit code (rank 0 prints the JSON line)
+        sys.exit(shard.launch_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
     rank, world, local = shard.env_rank()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        return dry_run(args, rank, world)
+
+    import torch
+
     dist = shard.init("nccl")  # RCCL over xGMI; None for a single process
     if dist is None:
         torch.cuda.set_device(0)
 
     from python_motion_planning_amd import _lib, batch, workloads as wl
 
-    nq = args.nq
-    occ, starts, goals = wl.c2_workload(nq=nq, pair_seed=1 + rank)
+    if args.scaling == "strong":
+        # one fixed batch (the C2 pairs of default_rng(1)) dealt longest-first round-robin over the ranks
+        occ, starts_all, goals_all = wl.c2_workload(nq=args.nq, pair_seed=1)
+        mine = shard.lpt_deal(shard.octile(starts_all, goals_all), world, rank)
+        starts, goals = starts_all[mine], goals_all[mine]
+    else:
+        occ, starts, goals = wl.c2_workload(nq=args.nq, pair_seed=1 + rank)
+        mine = np.arange(args.nq)
+    nq = len(starts)
     W, H = occ.shape
     L = _lib.load_library()
     occ_bits = batch.occ_bits_device(occ, torch)
@@ -660,8 +717,18 @@ def main():
     span_ms = float(np.mean((sp[:, 1] - sp[:, 0]).astype(np.float64)) / khz.value)
     elapsed, kern_ms, span_ms = shard.max_over_ranks(dist, [elapsed, kern_ms, span_ms], "cuda")
 
-    plans = nq * args.steps * world
+    plans = (args.nq if args.scaling == "strong" else nq * world) * args.steps
     value = plans / elapsed
+    gathered = None
+    if args.scaling == "strong" and dist is not None:
+        # the survey's end-of-run result exchange: every rank's records into the full batch, input order
+        g = shard.all_gather_rows(dist, mine, {"cost": lanes[0]["cost"], "status": lanes[0]["status"],
+                                               "n_expanded": lanes[0]["nexp"]}, args.nq, device="cuda")
+        gathered = {"queries": args.nq, "found": int((g["status"] == 0).sum().item()),
+                    "sum_expansions": int(g["n_expanded"].sum().item())}
+    counters_all = shard.all_gather_rows(dist, mine, {"c": torch.as_tensor(counters, device="cuda")},
+                                         args.nq, device="cuda")["c"].cpu().numpy() if (
+        args.scaling == "strong" and dist is not None) else counters
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
 
     cpu = None
@@ -696,7 +763,8 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": "A* plans/sec on 1024^2 grid (4096 random start/goal pairs per GPU)",
+            "metric": "A* plans/sec on 1024^2 grid (4096 random start/goal pairs per GPU)" if args.scaling == "weak"
+                      else f"A* plans/sec on 1024^2 grid ({args.nq} random start/goal pairs over {world} GPUs)",
             "value": value,
             "unit": "plans/s",
             "n_gpus": world,
@@ -704,11 +772,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (SURVEY.md §8(d) C2 generator: default_rng(0) 20% obstacles, default_rng(1+rank) pairs)",
-            "config": {"workload": "C2 batched A* 1024x1024 Grid, 4096 start/goal pairs per GPU, euclidean",
+            "config": {"workload": "C2 batched A* 1024x1024 Grid, 4096 start/goal pairs per GPU, euclidean"
+                                   if args.scaling == "weak" else
+                                   f"C2 batched A* 1024x1024 Grid, one {args.nq}-pair batch split over the GPUs",
                        "grid": [W, H], "queries_per_gpu": nq, "parallelism": f"query-sharded x{world}"},
             "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                       "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -724,6 +794,8 @@ def main():
                        "pushes_per_launch": int(counters[:, 0].sum()),
                        "pops_per_launch": int(counters[:, 1].sum()),
                        "max_heap_entries": int(counters[:, 3].max()),
+                       "expansions_all_ranks_per_step": int(counters_all[:, 2].sum()) if args.scaling == "strong" else None,
+                       "strong_scaling_gather": gathered,
                        "workers": args.workers, "streams": S, "priority_queries": args.prio},
         }
         print(json.dumps(out), flush=True)

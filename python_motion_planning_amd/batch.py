@@ -88,6 +88,44 @@ def astar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: in
     return out
 
 
+_RECORDS = ("cost", "path_len", "path", "n_expanded", "status")
+
+
+def astar2d_sharded(occ, starts, goals, dist=None, path_cap: int | None = None, algo: str = "astar", **kw):
+    """One batch of 2D grid queries split over all ranks of the process group `dist` (one GPU each):
+    every rank plans its longest-first round-robin share on its own GPU with astar2d_batch and every
+    rank returns the full batch's records (cost, path_len, path, n_expanded, status) in input order,
+    gathered with one all_gather per field over RCCL.  dist=None: one rank."""
+    from . import shard
+
+    torch = _lib.device_check()
+    occ_np = np.asarray(occ)
+    occ_bits = occ_bits_device(occ_np, torch)
+    shape = (int(occ_np.shape[0]), int(occ_np.shape[1]))
+
+    def plan(s, g):
+        r = astar2d_batch(shape, s, g, path_cap=path_cap, occ_bits=occ_bits, algo=algo, **kw)
+        return {k: r[k] for k in _RECORDS}
+
+    return shard.run_sharded(dist, plan, np.asarray(starts), np.asarray(goals), device="cuda")
+
+
+def astar3d_sharded(occ, starts, goals, dist=None, path_cap: int | None = None, algo: str = "astar", **kw):
+    """astar2d_sharded for AStar3D (C5: 8192 queries over the node's GPUs).  occ: shared [X,Y,Z] or
+    per-query [nq,X,Y,Z] grids (per-query grids are sliced with the rank's queries)."""
+    from . import shard
+
+    _lib.device_check()
+    occ_np = np.asarray(occ)
+    s_all, g_all = np.asarray(starts), np.asarray(goals)
+    per_query = occ_np.ndim == 4
+    world = dist.get_world_size() if dist is not None else 1
+    rank = dist.get_rank() if dist is not None else 0
+    idx = shard.lpt_deal(shard.octile(s_all, g_all), world, rank)
+    r = astar3d_batch(occ_np[idx] if per_query else occ_np, s_all[idx], g_all[idx], path_cap=path_cap, algo=algo, **kw)
+    return shard.all_gather_rows(dist, idx, {k: r[k] for k in _RECORDS}, len(s_all), device="cuda")
+
+
 def obstacle_grid(obstacles):
     """Obstacle set of (x, y) integer tuples -> (ox, oy, occ[W, H]) covering its bounding box."""
     if not obstacles:

@@ -80,3 +80,56 @@ def test_single_process_defaults(monkeypatch):
     assert shard.env_rank() == (0, 1, 0)
     assert shard.init("gloo") is None
     assert shard.max_over_ranks(None, [1.5, 2]) == [1.5, 2.0]
+
+
+def _bench_json(*argv):
+    import json
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), *argv], capture_output=True, text=True,
+                       timeout=300, env=env, cwd=repo)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 prints exactly one line
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_gpus_flag_spawns_ranks(n):
+    """`python bench.py --gpus N` (no torch.distributed.run around it) starts N ranks itself; the
+    strong-scaling deal + all_gather over those ranks reproduces the single-rank batch."""
+    out = _bench_json("--gpus", str(n), "--dry-run")
+    assert out["n_gpus"] == n and out["scaling"] == "strong"
+    assert out["gathered_equal_single_rank"] is True
+
+
+def test_bench_rejects_world_mismatch():
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=repo)
+    assert p.returncode != 0 and "WORLD_SIZE=1" in (p.stderr + p.stdout)
+
+
+def test_lpt_deal_and_local_gather():
+    import torch
+
+    from python_motion_planning_amd import shard
+
+    work = np.array([5.0, 1.0, 9.0, 3.0, 7.0, 2.0, 8.0])
+    parts = [shard.lpt_deal(work, 3, r) for r in range(3)]
+    # the longest three go one to each rank, then the next three, ...
+    assert sorted(np.concatenate(parts).tolist()) == list(range(7))
+    assert [sorted(work[p].tolist(), reverse=True)[0] for p in parts] == [9.0, 8.0, 7.0]
+    assert max(len(p) for p in parts) - min(len(p) for p in parts) <= 1
+    # octile distance: max + (sqrt2 - 1) min in 2D
+    assert np.allclose(shard.octile(np.array([[0, 0]]), np.array([[3, 4]])), [4 + (np.sqrt(2) - 1) * 3])
+    idx = np.array([4, 0, 2])
+    g = shard.all_gather_rows(None, idx, {"v": torch.tensor([40.0, 0.5, 20.0])}, 5)
+    assert g["v"].tolist() == [0.5, 0.0, 20.0, 0.0, 40.0]
