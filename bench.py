@@ -25,6 +25,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+L2_PEAK_GBS = 34500.0  # MI355X L2, 8 XCDs x 4 MiB, aggregate (MI355X_MICROARCH.md, L2 per XCD)
 
 
 def astar_algorithmic_bytes(counters: np.ndarray) -> float:
@@ -84,30 +85,48 @@ def control_leg(args, torch, dist, world, rank):
     K = args.control_steps
     elapsed, kern_ms = timed(torch, dist, lambda i: step(), K)
     steps_done = na * K * world
-    # ~8.2 MFLOP per agent-step in the stencil formulation
-    flops_per_step = 4096 * 30 * (12 + 2 * 20) + 4096 * 30 * 9 * 6 + 4096 * 20
+    # SURVEY.md §8(d) C4 in the stencil formulation, transcendental calls not counted: per sample and
+    # step 12 flops of rollout (x, y, th updates) + a 3x3 stencil of 6 flops per cell; 20 per sample
+    # for normalisation and scoring -> 8.2 MFLOP per agent-step
+    flops_per_step = 4096 * 30 * 12 + 4096 * 30 * 9 * 6 + 4096 * 20
     achieved_tf = flops_per_step * na / (kern_ms * 1e-3) / 1e12
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as O
 
-        threads = min(16, os.cpu_count() or 1)
-        ns = min(64, na)
+        threads = cpu_threads()
         obs = np.argwhere(occ).astype(np.float64)
-        xs, offs = batch.pack_paths(paths[:ns])
-        t = time.perf_counter()
-        O.dwa_step_batch(obs, xs, offs, goals[:ns], states[:ns], nthreads=threads)
-        dt = time.perf_counter() - t
-        cpu = {"value": ns / dt, "unit": "agent-steps/s", "cores": threads, "kind": "port",
-               "sample": f"first {ns} C4 agents, one step each, C restatement of DWA.evaluation (brute-force "
-                         f"cdist like the reference) with OpenMP over agents, {dt:.1f} s wall"}
+        xs, offs = batch.pack_paths(paths)
+
+        # the kernel's formulation on the CPU (obstacle term over the cells within R): all cores, 1 core
+        def run(nth, k=na):
+            return lambda i: O.dwa_step_batch(obs, xs, offs[: k + 1], goals[:k], states[:k], nthreads=nth, grid=occ)
+        reps, dt = timed_cpu(run(threads), args.cpu_seconds)
+        ns1 = min(16, na)
+        reps1, dt1 = timed_cpu(run(1, ns1), 2.0)
+        # the reference's own formulation (cdist over all 215 obstacles per trajectory point): all cores
+        nb = min(32, na)
+        xb, ob = batch.pack_paths(paths[:nb])
+        repsb, dtb = timed_cpu(lambda i: O.dwa_step_batch(obs, xb, ob, goals[:nb], states[:nb], nthreads=threads),
+                               2.0)
+        cpu = {"value": na * reps / dt, "unit": "agent-steps/s", "cores": threads, "kind": "port",
+               "host": host_cpu(),
+               "sample": f"all {na} C4 agents x {reps} steps, C restatement of DWA.evaluation with the obstacle "
+                         f"term over the cells within the inflation radius (the kernel's formulation; identical "
+                         f"values), OpenMP over agents, {dt:.1f} s wall",
+               "one_core": {"value": ns1 * reps1 / dt1, "sample": f"{ns1} agents x {reps1} steps, {dt1:.1f} s"},
+               "reference_formulation": {"value": nb * repsb / dtb, "cores": threads,
+                                         "sample": f"{nb} agents x {repsb} steps, cdist over every obstacle like "
+                                                   f"dwa.py:164, {dtb:.1f} s"}}
     return {"metric": "MPC steps/sec (H=30, 4096 samples): sampled-rollout control step (DWA form)",
             "value": steps_done / elapsed, "unit": "agent-steps/s", "agents_per_gpu": na, "steps": K,
             "ms_per_step": elapsed / K * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
             "config": {"workload": "C4: README 51x31 grid, 64x64 (v,w) samples, H=30, weights 0.2/0.1/0.05"},
             "roofline": with_traffic({"bound": "fp64-valu", "achieved": achieved_tf, "peak": 78.6, "unit": "TFLOP/s",
                                       "frac": achieved_tf / 78.6, "traffic": None,
-                                      "flops_per_agent_step": flops_per_step}, "dwa_kernel"),
+                                      "flops_per_agent_step": flops_per_step,
+                                      "flops_note": "SURVEY.md 8(d) stencil formulation, sin/cos/atan2 not counted"},
+                                     "dwa_kernel"),
             "cpu_baseline": cpu}
 
 
@@ -165,7 +184,35 @@ def timed(torch, dist, fn, steps, stream=None):
 
 
 def cpu_threads():
-    return min(16, os.cpu_count() or 1)
+    """Every core this process may run on (its affinity mask): the CPU baselines' thread count."""
+    return len(os.sched_getaffinity(0))
+
+
+def host_cpu():
+    """The CPU-baseline host as the bench sees it: model, os.cpu_count() (the machine) and the
+    affinity mask (the cores this job may use; gpurun boxes hand a share of the machine)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"model": model, "os_cpu_count": os.cpu_count(), "affinity_cores": cpu_threads()}
+
+
+def timed_cpu(fn, min_seconds):
+    """Run fn() until at least min_seconds of wall time have passed; returns (calls, seconds)."""
+    t = time.perf_counter()
+    reps = 0
+    while True:
+        fn(reps)
+        reps += 1
+        dt = time.perf_counter() - t
+        if dt >= min_seconds:
+            return reps, dt
 
 
 def rrt_leg(args, torch, dist, world, rank):
@@ -242,8 +289,11 @@ def rrt_leg(args, torch, dist, world, rank):
     from python_motion_planning_amd import shard
 
     elapsed, kern_ms = shard.max_over_ranks(dist, [elapsed, kern_ms], "cuda")
-    # per plan sum_i 16 n_i (node coordinates scanned) + 8 k_i (g of in-radius nodes)
-    alg_bytes = float(16.0 * ctr[:, 1].sum() + 8.0 * ctr[:, 2].sum())
+    # the bytes the kernel loads: 4 B per node scanned (the 16-bit fixed-point
+    # coordinate copy of the coarse nearest / radius scans) + 24 B per in-radius candidate (exact
+    # f64 x, y and g).  The trees (4 B x 65,537 nodes per query) stay in L2 / Infinity Cache, so the
+    # roof is the L2 bandwidth (MI355X_MICROARCH.md: ~34.5 TB/s aggregate)
+    alg_bytes = float(4.0 * ctr[:, 1].sum() + 24.0 * ctr[:, 2].sum())
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -265,9 +315,12 @@ def rrt_leg(args, torch, dist, world, rank):
             "streams": len(lanes),
             "config": {"workload": "C3: Map(512,512), 40 rects + 40 circles (default_rng(7)), (5,5)->(505,505), "
                                    "65536 samples, max_dist 0.5, r 10, goal rate 0.05"},
-            "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                                      "algorithmic_bytes_per_launch": alg_bytes}, "rrt_kernel"),
+            "roofline": with_traffic({"bound": "l2", "achieved": achieved, "peak": L2_PEAK_GBS, "unit": "GB/s",
+                                      "frac": achieved / L2_PEAK_GBS, "traffic": None,
+                                      "algorithmic_bytes_per_launch": alg_bytes,
+                                      "bytes_note": "4 B per node scanned + 24 B per in-radius candidate, as loaded; "
+                                                    "traffic = HBM bytes (PMC), far below: the trees are cache-resident"},
+                                     "rrt_kernel"),
             "detail": {"found": int((status == 0).sum()), "mean_nodes": float(out["n_nodes"].float().mean().item()),
                        "iterations_per_launch": int(ctr[:, 0].sum()), "nodes_scanned_per_launch": int(ctr[:, 1].sum()),
                        "collision_tests_per_launch": int(ctr[:, 3].sum())},
@@ -445,13 +498,18 @@ def graphs_leg(args, torch, dist, world, rank):
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             from oracle import oracle as O
 
-            ns = min(256, nl)
-            t = time.perf_counter()
-            refc = [O.lpastar2d_replan(occ, sl[q], gl[q], T[q], lite=lite)["cost"] for q in range(ns)]
-            dt = time.perf_counter() - t
-            assert np.array_equal(np.array(refc), r["cost"][:ns].cpu().numpy()), "GPU/oracle replan cost mismatch"
-            cpu = {"value": ns * (nt + 1) / dt, "unit": "plans/s", "cores": 1, "kind": "port",
-                   "sample": f"first {ns} of the {nl} sessions ({nt} edits each), C restatement, one core, {dt:.1f} s wall"}
+            th = cpu_threads()
+            ref = O.lpastar2d_replan_batch(occ, sl, gl, T, lite=lite, nthreads=th)
+            assert np.array_equal(ref["cost"], r["cost"].cpu().numpy()), "GPU/oracle replan cost mismatch"
+            reps, dt = timed_cpu(lambda i: O.lpastar2d_replan_batch(occ, sl, gl, T, lite=lite, nthreads=th), 2.0)
+            ns1 = min(2048, nl)
+            reps1, dt1 = timed_cpu(lambda i: O.lpastar2d_replan_batch(occ, sl[:ns1], gl[:ns1], T[:ns1], lite=lite,
+                                                                      nthreads=1), 2.0)
+            cpu = {"value": nl * (nt + 1) * reps / dt, "unit": "plans/s", "cores": th, "kind": "port",
+                   "sample": f"all {nl} sessions ({nt} edits each) x {reps}, C restatement with OpenMP over "
+                             f"sessions, {dt:.1f} s wall",
+                   "one_core": {"value": ns1 * (nt + 1) * reps1 / dt1,
+                                "sample": f"{ns1} sessions x {reps1}, {dt1:.1f} s"}}
         name = ("dstar_lite" if lite else "lpa_star") + "_replan"
         out[name] = {
             "metric": f"{name} plans/sec (plan() + {nt} OnPress edits per session, README grid, {nl} sessions)",
@@ -460,6 +518,62 @@ def graphs_leg(args, torch, dist, world, rank):
             "kernel_ms_per_launch": kern_ms, "dtype": "f64", "roofline": None,
             "roofline_note": "latency-bound list machine, as lpa_star",
             "detail": {"expansions_per_launch": int(np.maximum(ne, 0).sum())}, "cpu_baseline": cpu}
+    return out
+
+
+def dstar_leg(args, torch, dist, world, rank):
+    """DStar.plan (d_star.py:75-156, processState loop over the list-semantics OPEN) on C2-style grids:
+    10 % random obstacles, boundary walls, start/goal pairs from the largest free component, at 256^2
+    and 512^2 (SURVEY.md §6 measured the reference there).  One timed step = one launch over the
+    rank's queries."""
+    from python_motion_planning_amd import batch, workloads as wl
+
+    out = {}
+    for W, nq in ((256, args.dstar_queries), (512, args.dstar_queries)):
+        occ, s, g = wl.c2_workload(nq=nq, W=W, H=W, density=0.1, grid_seed=4, pair_seed=5 + rank)
+        s_d, g_d = torch.as_tensor(s, device="cuda"), torch.as_tensor(g, device="cuda")
+
+        def run(i):
+            return batch.dstar2d_batch(occ, s_d, g_d, path_cap=4 * W)
+
+        r = run(0)
+        torch.cuda.synchronize()
+        npr = r["n_process"].cpu().numpy()
+        st = r["status"].cpu().numpy()
+        elapsed, kern_ms = timed(torch, dist, run, args.dstar_steps)
+        # algorithmic bytes per processState: the 3x3 block of cell states (h, k f64 + tag / parent:
+        # 24 B each) read + ~2 OPEN entries (16 B) inserted / removed
+        alg = float(npr.sum()) * (9 * 24 + 2 * 16)
+        achieved = alg / (kern_ms * 1e-3) / 1e9
+        cpu = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            from oracle import oracle as O
+
+            th = cpu_threads()
+            ns = min(nq, 4 * th)
+            ref = O.dstar2d_batch(occ, s[:ns], g[:ns], nthreads=th)
+            assert np.array_equal(ref["cost"], r["cost"][:ns].cpu().numpy()), "GPU/oracle D* cost mismatch"
+            assert np.array_equal(ref["n_process"], npr[:ns]), "GPU/oracle D* processState-count mismatch"
+            reps, dt = timed_cpu(lambda i: O.dstar2d_batch(occ, s[:ns], g[:ns], nthreads=th), 2.0)
+            reps1, dt1 = timed_cpu(lambda i: O.dstar2d_batch(occ, s[:2], g[:2], nthreads=1), 1.0)
+            cpu = {"value": ns * reps / dt, "unit": "plans/s", "cores": th, "kind": "port",
+                   "sample": f"first {ns} of the {nq} queries x {reps}, C restatement of DStar (list OPEN, "
+                             f"first-minimum scans like d_star.py:220-259) with OpenMP over queries, {dt:.1f} s wall",
+                   "one_core": {"value": 2 * reps1 / dt1, "sample": f"2 queries x {reps1}, {dt1:.1f} s"}}
+        out[f"dstar_{W}"] = {
+            "metric": f"DStar plans/sec on a {W}x{W} grid (10% obstacles, {nq} random start/goal pairs)",
+            "value": nq * args.dstar_steps * world / elapsed, "unit": "plans/s", "queries_per_gpu": nq,
+            "steps": args.dstar_steps, "ms_per_step": elapsed / args.dstar_steps * 1e3, "kernel_ms_per_launch": kern_ms,
+            "dtype": "f64",
+            "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                                      "algorithmic_bytes_per_launch": alg,
+                                      "bytes_note": "248 B per processState (3x3 cell states 9 x 24 B + 2 OPEN "
+                                                    "entries x 16 B); latency-bound, one wave per query"},
+                                     "dstar_kernel"),
+            "detail": {"process_state_per_launch": int(npr.sum()), "max_process_state_query": int(npr.max()),
+                       "statuses": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))}},
+            "cpu_baseline": cpu}
     return out
 
 
@@ -582,8 +696,11 @@ def main():
     ap.add_argument("--agents", type=int, default=256, help="C4 agents per GPU (control-step leg)")
     ap.add_argument("--control-steps", type=int, default=20, help="timed control steps")
     ap.add_argument("--workers", type=int, default=3072, help="persistent A* workers (waves) per launch")
-    ap.add_argument("--legs", default="dwa,rrt,astar3d,lqr,mpc,graphs",
-                    help="secondary legs to run (comma list of dwa, rrt, astar3d, lqr, mpc, graphs; 'none' for none)")
+    ap.add_argument("--legs", default="dwa,rrt,astar3d,lqr,mpc,graphs,dstar",
+                    help="secondary legs to run (comma list of dwa, rrt, astar3d, lqr, mpc, graphs, dstar; 'none' "
+                         "for none)")
+    ap.add_argument("--dstar-queries", type=int, default=1024, help="queries per D* launch (256^2 and 512^2 grids)")
+    ap.add_argument("--dstar-steps", type=int, default=1)
     ap.add_argument("--theta-queries", type=int, default=4096, help="C2 queries per Theta* / Lazy Theta* 2D launch")
     ap.add_argument("--lpa-queries", type=int, default=16384,
                     help="README-grid queries per LPA* / D* Lite launch (4 per worker wave: the queue balances the tail)")
@@ -735,16 +852,22 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as O
 
-        threads = min(16, os.cpu_count() or 1)
+        threads = cpu_threads()
         ns = min(args.cpu_sample, nq)
         O.lib()
         t = time.perf_counter()
         ref = O.astar2d_batch(occ, starts[:ns], goals[:ns], path_cap=path_cap, nthreads=threads)
         dt = time.perf_counter() - t
         assert np.array_equal(ref["cost"], cost[:ns].cpu().numpy()), "GPU/oracle cost mismatch"
-        cpu = {"value": ns / dt, "unit": "plans/s", "cores": threads, "kind": "port",
+        # one core: every 32nd query of the batch (the same mix of short and long queries)
+        sub = np.arange(0, nq, 32)[: max(1, args.cpu_sample // 32)]
+        t = time.perf_counter()
+        O.astar2d_batch(occ, starts[sub], goals[sub], path_cap=path_cap, nthreads=1)
+        dt1 = time.perf_counter() - t
+        cpu = {"value": ns / dt, "unit": "plans/s", "cores": threads, "kind": "port", "host": host_cpu(),
                "sample": f"first {ns} of the 4096 C2 pairs, C restatement (oracle/pmp_oracle.c) with OpenMP over "
-                         f"queries, {dt:.1f} s wall"}
+                         f"queries on every core of the affinity mask, {dt:.1f} s wall",
+               "one_core": {"value": len(sub) / dt1, "sample": f"every 32nd pair ({len(sub)}), {dt1:.1f} s"}}
 
     legs = [x for x in args.legs.split(",") if x and x != "none"]
     secondary = {}
@@ -760,6 +883,8 @@ def main():
         secondary["mpc_qp"] = track_leg(args, torch, dist, world, rank, "mpc")
     if "graphs" in legs:
         secondary.update(graphs_leg(args, torch, dist, world, rank))
+    if "dstar" in legs:
+        secondary.update(dstar_leg(args, torch, dist, world, rank))
 
     if rank == 0:
         out = {

@@ -156,6 +156,25 @@ def dstar2d(occ: np.ndarray, start, goal, max_process: int = 0):
                 path=[(int(c) // H, int(c) % H) for c in cells], path_cells=cells.copy())
 
 
+def dstar2d_batch(occ: np.ndarray, starts, goals, nthreads: int = 0):
+    """OpenMP batch of the DStar.plan restatement: cost, status, n_process per query."""
+    L = lib()
+    if not getattr(L, "_dsb_set", False):
+        L.oracle_dstar2d_batch.restype = None
+        L.oracle_dstar2d_batch.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, _i32p, _i32p, ctypes.c_int, _dp, _i32p,
+                                           _i64p, ctypes.c_int]
+        L._dsb_set = True
+    occ = np.ascontiguousarray(occ, dtype=np.uint8)
+    W, H = occ.shape
+    s = np.ascontiguousarray(starts, np.int32).reshape(-1, 2)
+    g = np.ascontiguousarray(goals, np.int32).reshape(-1, 2)
+    nq = len(s)
+    out = dict(cost=np.zeros(nq), status=np.zeros(nq, np.int32), n_process=np.zeros(nq, np.int64))
+    L.oracle_dstar2d_batch(_p(occ, _u8p), W, H, _p(s, _i32p), _p(g, _i32p), nq, _p(out["cost"], _dp),
+                           _p(out["status"], _i32p), _p(out["n_process"], _i64p), int(nthreads))
+    return out
+
+
 def astar2d_batch(occ: np.ndarray, starts, goals, heuristic: str = "euclidean", path_cap: int = 4096,
                   nthreads: int = 0, algo: str = "astar"):
     """OpenMP batch of the AStar.plan (or Dijkstra / GBFS) restatement (one grid, many queries)."""
@@ -401,8 +420,27 @@ def track_batch(kind, path_xy, path_off, goals, states, u_p=None, iters=1, param
 
 
 def dwa_step_batch(obstacles, path_xy, path_off, goals, states, params=None, nv=64, nw=64, predict_time=3.0,
-                   v_res=0.05, w_res=0.05, weights=(0.2, 0.1, 0.05), inflation=1.0, nthreads=0):
+                   v_res=0.05, w_res=0.05, weights=(0.2, 0.1, 0.05), inflation=1.0, nthreads=0, grid=None):
+    """OpenMP batch of one DWA.plan iteration per agent.  grid: optional uint8 [W, H] occupancy of the
+    same obstacles -- the obstacle term is then taken over the cells within the inflation radius
+    (identical values; the CPU form of the kernel's stencil) instead of the reference's loop over
+    every obstacle."""
     L = _lp_lib()
+    L.oracle_dwa_set_grid.restype = None
+    L.oracle_dwa_set_grid.argtypes = [_u8p, ctypes.c_int, ctypes.c_int]
+    if grid is not None:
+        grid = np.ascontiguousarray(grid, dtype=np.uint8)
+        L.oracle_dwa_set_grid(_p(grid, _u8p), grid.shape[0], grid.shape[1])
+    try:
+        return _dwa_step_batch(L, obstacles, path_xy, path_off, goals, states, params, nv, nw, predict_time,
+                               v_res, w_res, weights, inflation, nthreads)
+    finally:
+        if grid is not None:
+            L.oracle_dwa_set_grid(None, 0, 0)
+
+
+def _dwa_step_batch(L, obstacles, path_xy, path_off, goals, states, params, nv, nw, predict_time, v_res, w_res,
+                    weights, inflation, nthreads):
     if not getattr(L, "_dwab", False):
         L.oracle_dwa_step_batch.restype = ctypes.c_int
         L.oracle_dwa_step_batch.argtypes = [_dp, ctypes.c_int, _dp, _i32p, _dp, _dp, ctypes.c_int,
@@ -619,4 +657,29 @@ def lpastar2d_batch(occ: np.ndarray, starts, goals, heuristic: str = "euclidean"
     L.oracle_lpastar2d_batch(int(bool(lite)), _p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0, _p(s, _i32p),
                              _p(g, _i32p), nq, _p(out["cost"], _dp), _p(out["status"], _i32p),
                              _p(out["n_expanded"], _i32p), int(nthreads))
+    return out
+
+
+def lpastar2d_replan_batch(occ: np.ndarray, starts, goals, toggles, heuristic: str = "euclidean", lite: bool = False,
+                           nthreads: int = 0):
+    """OpenMP batch of lpastar2d_replan: toggles [nq, nt, 2]; returns cost / n_expanded / status [nq, nt + 1]."""
+    L = lib()
+    if not getattr(L, "_lparb_set", False):
+        L.oracle_lpastar2d_replan_batch.restype = None
+        L.oracle_lpastar2d_replan_batch.argtypes = [ctypes.c_int, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                    _i32p, _i32p, ctypes.c_int, _i32p, ctypes.c_int, _dp, _i32p,
+                                                    _i32p, ctypes.c_int]
+        L._lparb_set = True
+    occ = np.ascontiguousarray(occ, dtype=np.uint8)
+    W, H = occ.shape
+    s = np.ascontiguousarray(starts, np.int32).reshape(-1, 2)
+    g = np.ascontiguousarray(goals, np.int32).reshape(-1, 2)
+    nq = len(s)
+    t = np.ascontiguousarray(toggles, np.int32).reshape(nq, -1, 2)
+    nt = t.shape[1]
+    out = dict(cost=np.zeros((nq, nt + 1)), n_expanded=np.zeros((nq, nt + 1), np.int32),
+               status=np.zeros((nq, nt + 1), np.int32))
+    L.oracle_lpastar2d_replan_batch(int(bool(lite)), _p(occ, _u8p), W, H, 1 if heuristic == "manhattan" else 0,
+                                    _p(s, _i32p), _p(g, _i32p), nq, _p(t, _i32p), nt, _p(out["cost"], _dp),
+                                    _p(out["n_expanded"], _i32p), _p(out["status"], _i32p), int(nthreads))
     return out

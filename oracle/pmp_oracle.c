@@ -1073,6 +1073,33 @@ void oracle_dwa_window(double v, double w, const lp_params_t* P, double vr[4])
  * obs: [nobs][2] (integer obstacle cells as doubles).  nv/nw > 0 override int((v1-v0)/v_res).
  * out: eval3 [N][3] = eval_win @ factor (v, w, score); best = argmax; best_traj [H][5].
  * Returns N (0 = the reference would raise on the empty window). */
+/* Optional stencil form of the obstacle term (CPU-baseline variant, not the reference's loop): with a
+ * grid set, min(min cdist(obstacles, traj), R) is taken over the occupied cells within R of each
+ * trajectory point instead of over every obstacle.  Only cells with |dx|, |dy| <= R can be closer
+ * than R, and min(sqrt(d2)) == sqrt(min(d2)), so the result is identical.  Set before a batch,
+ * read-only during it; oracle_dwa_set_grid(NULL, ...) restores the brute-force loop. */
+static const uint8_t* g_dwa_grid = NULL;
+static int g_dwa_W = 0, g_dwa_H = 0;
+void oracle_dwa_set_grid(const uint8_t* occ, int W, int H)
+{
+    g_dwa_grid = occ;
+    g_dwa_W = W;
+    g_dwa_H = H;
+}
+
+static double dwa_stencil_d2(double x, double y, double R, double mind2)
+{
+    const int x0 = (int)ceil(x - R), x1 = (int)floor(x + R), y0 = (int)ceil(y - R), y1 = (int)floor(y + R);
+    for (int cx = x0 < 0 ? 0 : x0; cx <= x1 && cx < g_dwa_W; cx++)
+        for (int cy = y0 < 0 ? 0 : y0; cy <= y1 && cy < g_dwa_H; cy++)
+            if (g_dwa_grid[(size_t)cx * g_dwa_H + cy]) {
+                const double dx = (double)cx - x, dy = (double)cy - y;
+                const double d2 = dx * dx + dy * dy;
+                if (d2 < mind2) mind2 = d2;
+            }
+    return mind2;
+}
+
 int oracle_dwa_eval(const double* obs, int nobs, const double st[5], const double goal[2], const double vr[4],
                     double v_res, double w_res, int nv, int nw, double predict_time, double dt, double hw,
                     double ow, double vw, double R, double* eval3, int* best, double* best_traj)
@@ -1089,16 +1116,21 @@ int oracle_dwa_eval(const double* obs, int nobs, const double st[5], const doubl
     for (int c = 0; c < N; c++) {
         const double v = vs[c / nw], w = ws[c % nw];
         double x = st[0], y = st[1], th = st[2];
-        double mind = INFINITY;
+        double mind = INFINITY, mind2 = INFINITY;
         for (int k = 0; k < H; k++) {
             const double nx = x + (dt * cos(th)) * v, ny = y + (dt * sin(th)) * v, nth = th + dt * w;
             x = nx; y = ny; th = nth;
+            if (g_dwa_grid) {
+                mind2 = dwa_stencil_d2(x, y, R, mind2);
+                continue;
+            }
             for (int o = 0; o < nobs; o++) {
                 const double dx = obs[2 * o] - x, dy = obs[2 * o + 1] - y;
                 const double d = sqrt(dx * dx + dy * dy);
                 if (d < mind) mind = d;
             }
         }
+        if (g_dwa_grid) mind = sqrt(mind2);
         const double theta = atan2(goal[1] - y, goal[0] - x);
         ew[5 * c + 0] = v;
         ew[5 * c + 1] = w;
@@ -2135,5 +2167,43 @@ void oracle_lpastar2d_batch(int lite, const uint8_t* occ, int W, int H, int heur
         status[q] = lpa_core(lite, occ, W, H, heuristic, starts[2 * q], starts[2 * q + 1], goals[2 * q], goals[2 * q + 1],
                              &cost[q], path, 1002, &plen, ctr, NULL, 0, NULL, NULL, NULL);
         n_expanded[q] = (int32_t)ctr[1];
+    }
+}
+
+/* OpenMP batch of the replanning restatement (plan() + nt OnPress edits per session, one toggle
+ * list of nt cells per query): the bench's CPU baseline.  rp_* [nq][nt + 1] as in
+ * oracle_lpastar2d_replan. */
+void oracle_lpastar2d_replan_batch(int lite, const uint8_t* occ, int W, int H, int heuristic, const int32_t* starts,
+                                   const int32_t* goals, int nq, const int32_t* toggles, int nt, double* rp_cost,
+                                   int32_t* rp_nexp, int32_t* rp_status, int nthreads)
+{
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int q = 0; q < nq; q++) {
+        int32_t path[1002], plen;
+        int64_t ctr[4];
+        double c;
+        const size_t o = (size_t)q * (size_t)(nt + 1);
+        lpa_core(lite, occ, W, H, heuristic, starts[2 * q], starts[2 * q + 1], goals[2 * q], goals[2 * q + 1], &c, path,
+                 1002, &plen, ctr, toggles + (size_t)q * 2 * (size_t)nt, nt, rp_cost + o, rp_nexp + o, rp_status + o);
+    }
+}
+
+/* OpenMP batch of the DStar restatement (one grid, many queries; the bench's CPU baseline):
+ * cost, status, n_process per query. */
+void oracle_dstar2d_batch(const uint8_t* occ, int W, int H, const int32_t* starts, const int32_t* goals, int nq,
+                          double* cost, int32_t* status, int64_t* n_process, int nthreads)
+{
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel
+    {
+        int32_t* path = (int32_t*)malloc(sizeof(int32_t) * ((size_t)W * H + 1));
+#pragma omp for schedule(dynamic, 1)
+        for (int q = 0; q < nq; q++) {
+            int32_t plen;
+            status[q] = oracle_dstar2d(occ, W, H, starts[2 * q], starts[2 * q + 1], goals[2 * q], goals[2 * q + 1],
+                                       &cost[q], path, W * H + 1, &plen, &n_process[q], 0);
+        }
+        free(path);
     }
 }

@@ -162,11 +162,14 @@ def device_check():
 
 
 def context(device: int | None = None):
-    """Per-(thread, device) pmp_ctx."""
+    """Per-(thread, device, current stream) pmp_ctx.  A context's scratch (work queue, per-worker
+    state) belongs to the launches of one stream: keyed by the stream too, launches the caller puts
+    on different torch streams never share scratch, and every batch call allocates its tensors and
+    launches on the same current stream, so the caching allocator orders their reuse."""
     torch = device_check()
     L = load_library()
     dev = torch.cuda.current_device() if device is None else int(device)
-    key = (threading.get_ident(), dev)
+    key = (threading.get_ident(), dev, torch.cuda.current_stream(dev).cuda_stream)
     c = _ctx.get(key)
     if c is None:
         c = L.pmp_create(dev)

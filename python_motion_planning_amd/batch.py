@@ -148,7 +148,7 @@ def pack_paths(paths):
 
 
 def dwa_step_batch(grid, lp_params, dwa_params, state, goal, path_xy, path_off, iters: int = 1,
-                   want_eval: bool = False, want_traj: bool = False, want_hist: bool = False, stream=None):
+                   want_eval: bool = False, want_traj: bool = False, want_hist: bool = False):
     """Batched DWA.plan iterations (dwa.py:72-93) on the gfx950 kernel dwa.hip.
 
     grid: (ox, oy, occ[W, H]) from obstacle_grid() (or with occ already a device bit tensor plus W, H).
@@ -178,7 +178,7 @@ def dwa_step_batch(grid, lp_params, dwa_params, state, goal, path_xy, path_off, 
     out["eval"] = torch.zeros((na, 4096, 3), dtype=torch.float64, device="cuda") if want_eval else None
     out["best_traj"] = (torch.zeros((na, iters, max(H_steps, 1), 5), dtype=torch.float64, device="cuda")
                         if want_traj else None)
-    rc = L.pmp_dwa_step_batch(ctx, stream if stream is not None else _lib.stream_ptr(), occ_bits.data_ptr(),
+    rc = L.pmp_dwa_step_batch(ctx, _lib.stream_ptr(), occ_bits.data_ptr(),
                               ox, oy, W, H, ctypes.byref(lp_params), ctypes.byref(dwa_params), na, state.data_ptr(),
                               goal.data_ptr(), path_xy.data_ptr(), path_off.data_ptr(), int(iters),
                               out["u"].data_ptr(), out["best"].data_ptr(), out["status"].data_ptr(),
@@ -188,7 +188,7 @@ def dwa_step_batch(grid, lp_params, dwa_params, state, goal, path_xy, path_off, 
     return out
 
 
-def lqr_control_batch(lp_params, lqr_params, s, s_d, u_r, robot_vw, stream=None):
+def lqr_control_batch(lp_params, lqr_params, s, s_d, u_r, robot_vw):
     """Batched LQR.lqrControl (lqr.py:103-145).  s, s_d [n,3], u_r [n,2], robot_vw [n,2] (the
     robot's current v, w).  Returns u [n,2] (device tensor)."""
     torch = _lib.device_check()
@@ -200,14 +200,14 @@ def lqr_control_batch(lp_params, lqr_params, s, s_d, u_r, robot_vw, stream=None)
     u_r = _dev(torch, u_r, torch.float64).reshape(-1, 2)
     vw = _dev(torch, robot_vw, torch.float64).reshape(-1, 2)
     u = torch.empty((n, 2), dtype=torch.float64, device="cuda")
-    rc = L.pmp_lqr_control_batch(ctx, stream if stream is not None else _lib.stream_ptr(), ctypes.byref(lp_params),
+    rc = L.pmp_lqr_control_batch(ctx, _lib.stream_ptr(), ctypes.byref(lp_params),
                                  ctypes.byref(lqr_params), n, s.data_ptr(), s_d.data_ptr(), u_r.data_ptr(),
                                  vw.data_ptr(), u.data_ptr())
     _lib.check(ctx, rc, "pmp_lqr_control_batch")
     return u
 
 
-def mpc_control_batch(lp_params, mpc_params, s, s_d, u_r, u_p, robot_vw, want_qp: bool = False, stream=None):
+def mpc_control_batch(lp_params, mpc_params, s, s_d, u_r, u_p, robot_vw, want_qp: bool = False):
     """Batched MPC.mpcControl (mpc.py:111-214).  u_p [n,2] device tensor updated in place (the new
     u_p the reference returns).  Returns dict: u [n,2], iters, status, and with want_qp the assembled
     QP (H [n,2m,2m], g [n,2m], lu [n,2,4m]) and its solution du [n,2m]."""
@@ -225,7 +225,7 @@ def mpc_control_batch(lp_params, mpc_params, s, s_d, u_r, u_p, robot_vw, want_qp
                status=torch.empty(n, dtype=torch.int32, device="cuda"))
     out.update(H=torch.zeros((n, nv, nv), **f64), g=torch.zeros((n, nv), **f64), lu=torch.zeros((n, 2, 2 * nv), **f64),
                du=torch.zeros((n, nv), **f64)) if want_qp else out.update(H=None, g=None, lu=None, du=None)
-    rc = L.pmp_mpc_control_batch(ctx, stream if stream is not None else _lib.stream_ptr(), ctypes.byref(lp_params),
+    rc = L.pmp_mpc_control_batch(ctx, _lib.stream_ptr(), ctypes.byref(lp_params),
                                  ctypes.byref(mpc_params), n, s.data_ptr(), s_d.data_ptr(), u_r.data_ptr(),
                                  u_p.data_ptr(), vw.data_ptr(), out["u"].data_ptr(), _lib.ptr(out["H"]),
                                  _lib.ptr(out["g"]), _lib.ptr(out["lu"]), _lib.ptr(out["du"]), out["iters"].data_ptr(),
@@ -235,7 +235,7 @@ def mpc_control_batch(lp_params, mpc_params, s, s_d, u_r, u_p, robot_vw, want_qp
 
 
 def track_step_batch(kind: str, lp_params, state, goal, path_xy, path_off, iters: int = 1, lqr_params=None,
-                     mpc_params=None, u_p=None, want_hist: bool = False, stream=None):
+                     mpc_params=None, u_p=None, want_hist: bool = False):
     """Batched LQR.plan / MPC.plan iterations (lqr.py:58-86, mpc.py:66-94), kind "lqr" or "mpc".
     state [na,5] f64 device tensor (updated in place); u_p [na,2] device tensor (MPC, in place).
     Returns dict of device tensors (u, status, n_steps, admm_iters, optional hist_pose)."""
@@ -254,7 +254,7 @@ def track_step_batch(kind: str, lp_params, state, goal, path_xy, path_off, iters
                n_steps=torch.empty(na, dtype=torch.int32, device="cuda"),
                admm_iters=torch.empty(na, dtype=torch.int32, device="cuda"))
     out["hist_pose"] = torch.zeros((na, iters, 3), dtype=torch.float64, device="cuda") if want_hist else None
-    rc = L.pmp_track_step_batch(ctx, stream if stream is not None else _lib.stream_ptr(), k, ctypes.byref(lp_params),
+    rc = L.pmp_track_step_batch(ctx, _lib.stream_ptr(), k, ctypes.byref(lp_params),
                                 ctypes.byref(lqr_params) if lqr_params is not None else None,
                                 ctypes.byref(mpc_params) if mpc_params is not None else None, na, state.data_ptr(),
                                 _lib.ptr(u_p), goal.data_ptr(), path_xy.data_ptr(), path_off.data_ptr(), int(iters),
@@ -264,7 +264,7 @@ def track_step_batch(kind: str, lp_params, state, goal, path_xy, path_off, iters
     return out
 
 
-def dstar2d_batch(occ, starts, goals, path_cap: int | None = None, max_process: int = 0, stream=None):
+def dstar2d_batch(occ, starts, goals, path_cap: int | None = None, max_process: int = 0):
     """Batched DStar.plan (d_star.py:75-156) on one Grid.  occ uint8 [W, H] (x-major).
     Returns dict of device tensors: cost, path_len, path [nq, path_cap] (cells x*H+y, start -> goal),
     n_process (processState calls), status (4 = the reference raises: start unreachable)."""
@@ -283,7 +283,7 @@ def dstar2d_batch(occ, starts, goals, path_cap: int | None = None, max_process: 
                path=torch.empty((nq, path_cap), dtype=torch.int32, device="cuda"),
                n_process=torch.empty(nq, dtype=torch.int64, device="cuda"),
                status=torch.empty(nq, dtype=torch.int32, device="cuda"))
-    rc = L.pmp_dstar2d_batch(ctx, stream if stream is not None else _lib.stream_ptr(), occ_bits.data_ptr(), W, H,
+    rc = L.pmp_dstar2d_batch(ctx, _lib.stream_ptr(), occ_bits.data_ptr(), W, H,
                              s.data_ptr(), g.data_ptr(), nq, out["cost"].data_ptr(), out["path_len"].data_ptr(),
                              out["path"].data_ptr(), path_cap, out["n_process"].data_ptr(), out["status"].data_ptr(),
                              int(max_process))
@@ -292,7 +292,7 @@ def dstar2d_batch(occ, starts, goals, path_cap: int | None = None, max_process: 
 
 
 def lpastar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: int = 1001, counters: bool = False,
-                    stream=None, lite: bool = False):
+                    lite: bool = False):
     """Batched LPAStar.plan (lpa_star.py:78-87: computeShortestPath + extractPath) on one Grid;
     lite=True runs DStarLite.plan (d_star_lite.py:14-187, pmp_dstarlite2d_batch).
     occ uint8 [W, H] (x-major).  Returns dict of device tensors: cost, path_len, path [nq, path_cap]
@@ -314,7 +314,7 @@ def lpastar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: 
                status=torch.empty(nq, dtype=torch.int32, device="cuda"))
     out["counters"] = torch.empty((nq, 4), dtype=torch.int64, device="cuda") if counters else None
     fn = L.pmp_dstarlite2d_batch if lite else L.pmp_lpastar2d_batch
-    rc = fn(ctx, stream if stream is not None else _lib.stream_ptr(), occ_bits.data_ptr(), W, H,
+    rc = fn(ctx, _lib.stream_ptr(), occ_bits.data_ptr(), W, H,
                                1 if heuristic == "manhattan" else 0, s.data_ptr(), g.data_ptr(), nq,
                                out["cost"].data_ptr(), out["path_len"].data_ptr(), out["path"].data_ptr(),
                                int(path_cap), out["n_expanded"].data_ptr(), _lib.ptr(out["counters"]),
@@ -324,7 +324,7 @@ def lpastar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: 
 
 
 def lpastar2d_replan_batch(occ, starts, goals, toggles, heuristic: str = "euclidean", path_cap: int = 1001,
-                           counters: bool = False, stream=None, lite: bool = False):
+                           counters: bool = False, lite: bool = False):
     """LPAStar.plan() then one LPAStar.OnPress edit (lpa_star.py:101-137) per toggle, each followed by
     plan() on the kept state, for every query (pmp_lpastar2d_replan_batch); lite=True: DStarLite.plan()
     then DStarLite.OnPress per toggle (d_star_lite.py:61-97, pmp_dstarlite2d_replan_batch).  toggles [nq, nt, 2].
@@ -351,7 +351,7 @@ def lpastar2d_replan_batch(occ, starts, goals, toggles, heuristic: str = "euclid
                path=torch.empty((nq, int(path_cap)), dtype=torch.int32, device="cuda"))
     out["counters"] = torch.empty((nq, 4), dtype=torch.int64, device="cuda") if counters else None
     fn = L.pmp_dstarlite2d_replan_batch if lite else L.pmp_lpastar2d_replan_batch
-    rc = fn(ctx, stream if stream is not None else _lib.stream_ptr(), occ_bits.data_ptr(), W, H,
+    rc = fn(ctx, _lib.stream_ptr(), occ_bits.data_ptr(), W, H,
                                       1 if heuristic == "manhattan" else 0, s.data_ptr(), g.data_ptr(), nq,
                                       t.data_ptr(), nt, out["cost"].data_ptr(), out["n_expanded"].data_ptr(),
                                       out["status"].data_ptr(), out["path_len"].data_ptr(), out["path"].data_ptr(),
@@ -373,7 +373,7 @@ def map_arrays(env, torch=None):
 
 def rrt_batch(env, starts, goals, rnd, sample_num: int, star: bool = True, max_dist: float = 0.5,
               radius: float = 10.0, goal_sample_rate: float = 0.05, delta: float = 0.5, path_cap: int | None = None,
-              counters: bool = False, stream=None):
+              counters: bool = False):
     """Batched RRT / RRT* plans (rrt.py:49-151, rrt_star.py:43-76) on one Map.
     rnd: [nq, stride] f64 random streams (RandomState.random_sample order; 3*sample_num+1 per query).
     Returns dict of device tensors: tree_xy [nq,cap,2], tree_g, tree_parent, n_nodes, cost, path_len,
@@ -398,7 +398,7 @@ def rrt_batch(env, starts, goals, rnd, sample_num: int, star: bool = True, max_d
                counters=torch.zeros((nq, 4), dtype=torch.int64, device="cuda") if counters else None)
     P = _lib.RRTParams(float(env.x_range), float(env.y_range), float(delta), float(max_dist), float(radius),
                        float(goal_sample_rate), int(sample_num), int(bool(star)))
-    rc = L.pmp_rrt_batch(ctx, stream if stream is not None else _lib.stream_ptr(), ctypes.byref(P), rect.data_ptr(),
+    rc = L.pmp_rrt_batch(ctx, _lib.stream_ptr(), ctypes.byref(P), rect.data_ptr(),
                          int(rect.shape[0]), circ.data_ptr(), int(circ.shape[0]), bnd.data_ptr(), int(bnd.shape[0]),
                          s.data_ptr(), g.data_ptr(), nq, rnd.data_ptr(), int(rnd.shape[1]), cap,
                          out["tree_xy"].data_ptr(), out["tree_g"].data_ptr(), out["tree_parent"].data_ptr(),

@@ -14,6 +14,7 @@
 // The heap engine is heap16.h (LDS + HBM spill, wave-parallel pop/push).
 // One wave64 per query (persistent workers pulling an atomic queue); per-worker HBM state:
 // u8 closed-dir per cell (0 = open, dir+1 = closed) + f64 closed g per cell, reset per query.
+#include <algorithm>
 #include "heap16.h"
 
 namespace {
@@ -458,6 +459,9 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
     }
 }
 
+// per-context scratch budget of the 3D planners (heap spill + closed state + Theta* parents per worker)
+constexpr size_t kScratchBudget3 = (size_t)32 << 30;
+
 }  // namespace
 
 extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uint32_t* occ_bits, int per_query, int X,
@@ -492,13 +496,21 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     const int heap_cap = (int)hc;
     if (lds_cap > heap_cap) lds_cap = (heap_cap + 15) & ~15;
     const size_t spill_n = heap_cap > lds_cap ? (size_t)(heap_cap - lds_cap) : 0;
+    const int theta = algo == PMP_ALGO_THETA ? 1 : (algo == PMP_ALGO_LAZY_THETA ? 2 : 0);
+    // theta modes: CLOSED parent per cell, and the parent of every push (indexed by the push counter;
+    // a query that pushes more stops with PMP_CAP_OVERFLOW)
+    const uint32_t ppar_cap = theta ? (uint32_t)std::min<size_t>(64 * ncell + 64, (size_t)1 << 24) : 0u;
+    {
+        // per-context scratch budget: fewer workers (each pulls more queries) rather than ENOMEM
+        const size_t per_worker = spill_n * 16 + ncell + ncell * 16 + (theta ? ((size_t)ncell + ppar_cap) * 4 : 0);
+        const size_t fit = kScratchBudget3 / per_worker;
+        if (fit < 1) return pmp_set_err(ctx, PMP_ENOMEM, "pmp_graph3d_batch: one worker exceeds the scratch budget");
+        if ((size_t)workers > fit) workers = (int)fit;
+    }
     uint4* spill = (uint4*)pmp_scratch(ctx, SCR_AUX1, (size_t)workers * spill_n * 16 + 16);
     uint8_t* cdir = (uint8_t*)pmp_scratch(ctx, SCR_AUX2, (size_t)workers * ncell + 16);
     double* cg = (double*)pmp_scratch(ctx, SCR_AUX3, (size_t)workers * ncell * 16 + 16);  // closed g + pending g
     int* queue = (int*)pmp_scratch(ctx, SCR_AUX0, 256);
-    const int theta = algo == PMP_ALGO_THETA ? 1 : (algo == PMP_ALGO_LAZY_THETA ? 2 : 0);
-    // theta modes: CLOSED parent per cell, and the parent of every push (indexed by the push counter)
-    const uint32_t ppar_cap = theta ? (uint32_t)(64 * ncell + 64) : 0u;
     uint32_t* tpar = nullptr;
     if (theta) {
         tpar = (uint32_t*)pmp_scratch(ctx, SCR_AUX4, (size_t)workers * (ncell + ppar_cap) * 4 + 16);

@@ -18,7 +18,11 @@
 
 namespace {
 
-constexpr int kThreads = 1024;  // 16 waves per agent: the FP64 rollout needs the occupancy to hide latency
+#ifndef PMP_DWA_THREADS
+#define PMP_DWA_THREADS 768
+#endif
+constexpr int kThreads = PMP_DWA_THREADS;  // 12 waves per agent (3 per SIMD): <= 168 VGPRs, no scratch spills; 16 waves
+                                           // spill to scratch, 8 hide less latency (tools/dwa_ab.sh)
 constexpr int kMaxN = 4096;    // samples per step held in LDS
 constexpr int kMaxLeaves = 128;
 
@@ -99,52 +103,48 @@ struct DwaShared {
     double col[3][kMaxN];            // heading, obstacle, velocity per sample
     double leafsum[3][kMaxLeaves];
     int leaf_lo[kMaxLeaves], leaf_n[kMaxLeaves];
-    double redd[kThreads];
-    int redi[kThreads];
+    double redd[kThreads / 64];
+    int redi[kThreads / 64];
     double sums[3];
+    double sn0, cs0;                 // sin / cos of the agent's heading
     double pt[2], theta, kappa;
     int nleaves;
 };
 
-// pairwise tree over the leaves (in left-to-right order) for a column of n samples
-__device__ inline double pw_combine(const double* leafsum, int n)
+// numpy's pairwise tree for n <= kMaxN samples is at most kPwDepth splits deep (n > 128 splits at
+// pw_half(n); checked over every n <= 4096), so both walks below are compile-time recursions that
+// the compiler flattens into registers -- no per-lane stack arrays, no scratch memory.
+constexpr int kPwDepth = 6;
+
+// the leaves of the tree for [lo, lo + n), in left-to-right order
+template <int D>
+__device__ inline void pw_leaves(int lo, int n, int* leaf_lo, int* leaf_n, int& nl)
 {
-    int ns[16], stage[16];
-    double left[16];
-    int sp = 0, leaf = 0;
-    ns[0] = n;
-    stage[0] = 0;
-    bool have = false;
-    double ret = 0.0;
-    while (sp >= 0) {
-        if (have) {
-            if (stage[sp] == 1) {  // left child done -> descend right
-                left[sp] = ret;
-                stage[sp] = 2;
-                have = false;
-                const int n2 = pw_half(ns[sp]);
-                ns[sp + 1] = ns[sp] - n2;
-                stage[sp + 1] = 0;
-                sp++;
-            } else {  // both done
-                ret = left[sp] + ret;
-                sp--;
-            }
-            continue;
-        }
-        const int nn = ns[sp];
-        if (nn <= 128) {
-            ret = leafsum[leaf++];
-            have = true;
-            sp--;
-            continue;
-        }
-        stage[sp] = 1;
-        ns[sp + 1] = pw_half(nn);
-        stage[sp + 1] = 0;
-        sp++;
+    if (D == 0 || n <= 128) {
+        leaf_lo[nl] = lo;
+        leaf_n[nl] = n;
+        nl++;
+        return;
     }
-    return ret;
+    if constexpr (D > 0) {
+        const int n2 = pw_half(n);
+        pw_leaves<D - 1>(lo, n2, leaf_lo, leaf_n, nl);
+        pw_leaves<D - 1>(lo + n2, n - n2, leaf_lo, leaf_n, nl);
+    }
+}
+
+// the tree's value from its leaf sums (left + right at every split, as numpy combines them)
+template <int D>
+__device__ inline double pw_combine(const double* leafsum, int n, int& leaf)
+{
+    if (D == 0 || n <= 128) return leafsum[leaf++];
+    if constexpr (D > 0) {
+        const int n2 = pw_half(n);
+        const double l = pw_combine<D - 1>(leafsum, n2, leaf);
+        const double r = pw_combine<D - 1>(leafsum, n - n2, leaf);
+        return l + r;
+    }
+    return 0.0;
 }
 
 template <bool OCC_LDS>
@@ -196,70 +196,73 @@ __global__ __launch_bounds__(kThreads) void dwa_kernel(
         if (nv <= 0 || nw <= 0 || N > kMaxN) { status = PMP_REF_RAISES; break; }
         const Linsp LV = make_linsp(vr0, vr1, nv), LW = make_linsp(vr2, vr3, nw);
 
-        // evaluation: one sample per thread per round (dwa.py:152-174)
+        // evaluation (dwa.py:152-174) in three passes over the samples, one sample per thread per
+        // round, so each pass carries only its own libm code (one pass with sincos, rollout and
+        // atan2 together needs more registers than 16 waves per CU leave): (1) the rotation of one
+        // step, sin / cos(dt * w) -> col[1], col[2]; (2) the H-step rollout -> end x, y and the
+        // stencil's min d2 (a thread reads and rewrites only its own sample's slots);
+        // (3) heading / obstacle / velocity.
+        if (tid == 0) sincos(st[2], &S.sn0, &S.cs0);
+        for (int c = tid; c < N; c += kThreads) sincos(dt * linsp_at(LW, c % nw), &S.col[1][c], &S.col[2][c]);
+        __syncthreads();
+        const double sn0 = S.sn0, cs0 = S.cs0;
         for (int c = tid; c < N; c += kThreads) {
-            const double v = linsp_at(LV, c / nw), w = linsp_at(LW, c % nw);
-            double x = st[0], y = st[1], th = st[2];
+            const double v = linsp_at(LV, c / nw);
+            double x = st[0], y = st[1];
             // min over cells of sqrt(d2) == sqrt(min d2): sqrt is monotone and correctly rounded, so
             // one square root per sample (scipy cdist: d = sqrt(dx*dx + dy*dy), no fused multiply-add)
             double mind2 = INFINITY;
             // cos/sin of th_k by rotation: th_k = th_0 + k*(dt*w) up to the rounding of the running
-            // sum (which th itself keeps exactly as the reference), so (cs, sn) stay within ~2e-14
+            // sum (which pass 3 recomputes exactly as the reference), so (cs, sn) stay within ~2e-14
             // of libm's cos/sin(th_k) over the horizon -- one sincos pair per sample, not per step.
-            double sn, cs, sd, cd;
-            sincos(th, &sn, &cs);
-            sincos(dt * w, &sd, &cd);
+            double sn = sn0, cs = cs0;
+            const double sd = S.col[1][c], cd = S.col[2][c];
             for (int k = 0; k < Hh; k++) {
-                const double nx = x + (dt * cs) * v, ny = y + (dt * sn) * v, nth = th + dt * w;
+                const double nx = x + (dt * cs) * v, ny = y + (dt * sn) * v;
                 const double ncs = cs * cd - sn * sd, nsn = sn * cd + cs * sd;
                 cs = ncs;
                 sn = nsn;
                 x = nx;
                 y = ny;
-                th = nth;
                 const int x0 = (int)ceil(x - R), x1 = (int)floor(x + R);
                 const int y0 = (int)ceil(y - R), y1 = (int)floor(y + R);
                 // the stencil row by row: one bit run per row, distances only for its set bits
-                // (cells outside the grid are not obstacles)
-                const int j0 = max(y0 - oy, 0), j1 = min(min(y1, y0 + 16) - oy, H - 1);
-                if (j0 <= j1)
-                    for (int cx = x0; cx <= x1 && cx <= x0 + 16; cx++) {
+                // (cells outside the grid are not obstacles); rows of up to 32 cells per run, so any
+                // inflation radius is covered
+                const int j0 = max(y0 - oy, 0), j1 = min(y1 - oy, H - 1);
+                for (int jc = j0; jc <= j1; jc += 32)
+                    for (int cx = x0; cx <= x1; cx++) {
                         const int i = cx - ox;
                         if ((unsigned)i >= (unsigned)W) continue;
-                        uint32_t run = OCC_LDS ? occ_run(occl, H, i, j0, j1 - j0 + 1) : occ_run(occ, H, i, j0, j1 - j0 + 1);
+                        const int nrun = min(32, j1 - jc + 1);
+                        uint32_t run = OCC_LDS ? occ_run(occl, H, i, jc, nrun) : occ_run(occ, H, i, jc, nrun);
                         while (run) {
                             const int b = __ffs(run) - 1;
                             run &= run - 1;
-                            const double dx = (double)cx - x, dy = (double)(oy + j0 + b) - y;
+                            const double dx = (double)cx - x, dy = (double)(oy + jc + b) - y;
                             const double d2 = dx * dx + dy * dy;
                             if (d2 < mind2) mind2 = d2;
                         }
                     }
             }
-            const double ang = atan2(gy - y, gx - x);
+            S.col[0][c] = x;
+            S.col[1][c] = mind2;
+            S.col[2][c] = y;
+        }
+        for (int c = tid; c < N; c += kThreads) {
+            const double v = linsp_at(LV, c / nw), w = linsp_at(LW, c % nw);
+            double th = st[2];
+            for (int k = 0; k < Hh; k++) th = th + dt * w;
+            const double ang = atan2(gy - S.col[2][c], gx - S.col[0][c]);
             S.col[0][c] = lp::kPi - fabs(ang - th);
-            const double mind = sqrt(mind2);
+            const double mind = sqrt(S.col[1][c]);
             S.col[1][c] = mind < R ? mind : R;
             S.col[2][c] = fabs(v);
         }
         // normalisation sums (dwa.py:176-181): numpy pairwise tree, leaves in parallel
         if (tid == 0) {
-            int stk_lo[32], stk_n[32], sp = 0, nl = 0;
-            stk_lo[0] = 0;
-            stk_n[0] = N;
-            while (sp >= 0) {
-                const int lo = stk_lo[sp], n = stk_n[sp];
-                sp--;
-                if (n <= 128) {
-                    S.leaf_lo[nl] = lo;
-                    S.leaf_n[nl] = n;
-                    nl++;
-                } else {
-                    const int n2 = pw_half(n);
-                    sp++; stk_lo[sp] = lo + n2; stk_n[sp] = n - n2;  // right pushed first
-                    sp++; stk_lo[sp] = lo; stk_n[sp] = n2;           // left popped first
-                }
-            }
+            int nl = 0;
+            pw_leaves<kPwDepth>(0, N, S.leaf_lo, S.leaf_n, nl);
             S.nleaves = nl;
         }
         __syncthreads();
@@ -269,7 +272,10 @@ __global__ __launch_bounds__(kThreads) void dwa_kernel(
             S.leafsum[cidx][l] = pw_leaf(&S.col[cidx][S.leaf_lo[l]], S.leaf_n[l]);
         }
         __syncthreads();
-        if (tid < 3) S.sums[tid] = 0.0 + pw_combine(S.leafsum[tid], N);
+        if (tid < 3) {
+            int leaf = 0;
+            S.sums[tid] = 0.0 + pw_combine<kPwDepth>(S.leafsum[tid], N, leaf);
+        }
         __syncthreads();
         const double s0 = S.sums[0], s1 = S.sums[1], s2 = S.sums[2];
         // scores and first-index argmax (dwa.py:183-190, :89)
@@ -289,19 +295,8 @@ __global__ __launch_bounds__(kThreads) void dwa_kernel(
             }
             if (sc > bs || bi == 0x7fffffff) { bs = sc; bi = c; }
         }
-        S.redd[tid] = bs;
-        S.redi[tid] = bi;
-        __syncthreads();
-        for (int s = kThreads / 2; s > 0; s >>= 1) {
-            if (tid < s) {
-                const double od = S.redd[tid + s];
-                const int oi = S.redi[tid + s];
-                if (od > S.redd[tid] || (od == S.redd[tid] && oi < S.redi[tid])) { S.redd[tid] = od; S.redi[tid] = oi; }
-            }
-            __syncthreads();
-        }
-        best = S.redi[0];
-        __syncthreads();
+        lp::block_best<false>(bs, bi, S.redd, S.redi);
+        best = bi;
         u0 = linsp_at(LV, best / nw);
         u1 = linsp_at(LW, best % nw);
         if (tid == 0 && hist_pose) {

@@ -152,9 +152,45 @@ __device__ inline int lookahead_tail(const double* path, int P, double rx, doubl
     return 0;
 }
 
+// Block-wide first-index best of (v, i): the minimum (MIN) or maximum of v, ties to the lowest i.
+// Butterflies inside each wave, then one LDS round over the waves' results: `redd` / `redi` need
+// blockDim.x / 64 entries.  Every thread returns the block's result.
+template <bool MIN>
+__device__ inline void block_best(double& v, int& i, double* redd, int* redi)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(v, o);
+        const int oi = __shfl_xor(i, o);
+        const bool take = MIN ? (ov < v || (ov == v && oi < i)) : (ov > v || (ov == v && oi < i));
+        if (take) {
+            v = ov;
+            i = oi;
+        }
+    }
+    const int nw = (int)(blockDim.x >> 6);
+    __syncthreads();  // the previous use of redd / redi is read everywhere
+    if ((threadIdx.x & 63) == 0) {
+        redd[threadIdx.x >> 6] = v;
+        redi[threadIdx.x >> 6] = i;
+    }
+    __syncthreads();
+    v = redd[0];
+    i = redi[0];
+    for (int k = 1; k < nw; k++) {
+        const double ov = redd[k];
+        const int oi = redi[k];
+        const bool take = MIN ? (ov < v || (ov == v && oi < i)) : (ov > v || (ov == v && oi < i));
+        if (take) {
+            v = ov;
+            i = oi;
+        }
+    }
+}
+
 // getLookaheadPoint (local_planner.py:103-170) for one agent, computed by a whole workgroup:
 // the distance scan, first-index argmin and the first-beyond-lookahead search are block-parallel,
-// the tail runs on thread 0.  `red` is >= 2*nthreads ints/doubles of LDS scratch.
+// the tail runs on thread 0.  `redd` / `redi` hold >= blockDim.x / 64 entries of LDS.
 __device__ inline int lookahead_block(const double* path, int P, double rx, double ry, double v, const pmp_lp_params& Pm,
                                       double* pt, double* theta, double* kappa, double* redd, int* redi)
 {
@@ -167,33 +203,18 @@ __device__ inline int lookahead_block(const double* path, int P, double rx, doub
         const double d = py_hypot(rx - path[2 * i], ry - path[2 * i + 1]);
         if (d < bd) { bd = d; bi = i; }  // strided in increasing i: keeps the first minimum
     }
-    redd[tid] = bd;
-    redi[tid] = bi;
-    __syncthreads();
-    for (int s = nt / 2; s > 0; s >>= 1) {
-        if (tid < s) {
-            const double od = redd[tid + s];
-            const int oi = redi[tid + s];
-            if (od < redd[tid] || (od == redd[tid] && oi < redi[tid])) { redd[tid] = od; redi[tid] = oi; }
-        }
-        __syncthreads();
-    }
-    const int idx_closest = redi[0];
-    __syncthreads();
+    block_best<true>(bd, bi, redd, redi);
+    const int idx_closest = bi;
     // first i >= idx_closest with dist >= L
     int fi = 0x7fffffff;
     for (int i = idx_closest + tid; i < P; i += nt) {
         if (py_hypot(rx - path[2 * i], ry - path[2 * i + 1]) >= L) { fi = i; break; }
     }
-    redi[tid] = fi;
-    __syncthreads();
-    for (int s = nt / 2; s > 0; s >>= 1) {
-        if (tid < s && redi[tid + s] < redi[tid]) redi[tid] = redi[tid + s];
-        __syncthreads();
-    }
-    const int first = redi[0];
-    __syncthreads();
+    double fd = 0.0;
+    block_best<true>(fd, fi, redd, redi);
+    const int first = fi;
     int st = 0;
+    __syncthreads();
     if (tid == 0) {
         const int idx_goal = first == 0x7fffffff ? P - 1 : first;
         st = lookahead_tail(path, P, rx, ry, L, idx_goal, pt, theta, kappa);

@@ -108,3 +108,37 @@ def test_c4_batch_against_oracle():
             continue
         vr = O.dwa_window(states[i, 3], states[i, 4])
         assert vr[0] - 1e-12 <= u[i, 0] <= vr[1] + 1e-12 and vr[2] - 1e-12 <= u[i, 1] <= vr[3] + 1e-12
+
+
+@pytest.mark.parametrize("inflation", [3.0, 9.5, 20.0])
+def test_large_inflation_against_oracle(inflation):
+    """The obstacle stencil covers any inflation radius (dwa.py:162-164: min(cdist(...), R) over all
+    obstacles): radii above 8 cells need several bit runs per stencil row."""
+    import torch
+
+    from oracle import oracle as O
+    from python_motion_planning_amd import _lib, batch, workloads as wl
+
+    occ, states, goals = wl.c4_workload(16, seed=5)
+    r = batch.astar2d_batch(occ, states[:, :2].astype(np.int32), np.tile([45, 25], (16, 1)).astype(np.int32),
+                            path_cap=2048)
+    pl, P = r["path_len"].cpu().numpy(), r["path"].cpu().numpy()
+    H = occ.shape[1]
+    paths = [np.column_stack([P[i, : pl[i]][::-1] // H, P[i, : pl[i]][::-1] % H]).astype(np.float64)
+             for i in range(16)]
+    xy, off = batch.pack_paths(paths)
+    lp = _lib.LPParams.from_params(_pmp().LocalPlanner.DEFAULTS)
+    dp = _lib.DWAParams(0.2, 0.1, 0.05, 3.0, inflation, 0.05, 0.05, 32, 32)
+    grid = batch.obstacle_grid({(int(a), int(b)) for a, b in np.argwhere(occ)})
+    st_d = torch.tensor(states, dtype=torch.float64, device="cuda")
+    out = batch.dwa_step_batch(grid, lp, dp, st_d, goals, xy, off, iters=1)
+    status = out["status"].cpu().numpy()
+    new_st, u = st_d.cpu().numpy(), out["u"].cpu().numpy()
+    obs = np.argwhere(occ).astype(np.float64)
+    for i in range(16):
+        rc, ost, ou = O.dwa_step(obs, paths[i], goals[i], states[i], nv=32, nw=32, predict_time=3.0,
+                                 inflation=inflation)
+        assert rc == status[i], i
+        if rc == 0:
+            np.testing.assert_allclose(new_st[i], ost, rtol=1e-12, atol=1e-14)
+            np.testing.assert_allclose(u[i], ou, rtol=1e-12, atol=1e-14)
