@@ -183,9 +183,31 @@ def timed(torch, dist, fn, steps, stream=None):
     return elapsed, kern_ms
 
 
+def cgroup_cpus():
+    """CPUs granted by the cgroup CPU quota (cgroup v2 cpu.max or v1 cfs quota), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else max(1, int(-(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else max(1, -(-q // per))
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_threads():
-    """Every core this process may run on (its affinity mask): the CPU baselines' thread count."""
-    return len(os.sched_getaffinity(0))
+    """The CPU baselines' thread count: every core this job may use -- its affinity mask, capped by
+    the cgroup CPU quota (a gpurun box hands the job a share of the machine: more threads than the
+    quota only time-slice against each other)."""
+    n = len(os.sched_getaffinity(0))
+    q = cgroup_cpus()
+    return min(n, q) if q else n
 
 
 def host_cpu():
@@ -200,7 +222,8 @@ def host_cpu():
                     break
     except OSError:
         pass
-    return {"model": model, "os_cpu_count": os.cpu_count(), "affinity_cores": cpu_threads()}
+    return {"model": model, "os_cpu_count": os.cpu_count(), "affinity_cores": len(os.sched_getaffinity(0)),
+            "cgroup_quota_cpus": cgroup_cpus(), "threads_used": cpu_threads()}
 
 
 def timed_cpu(fn, min_seconds):

@@ -192,6 +192,52 @@ int pmp_dstar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int 
                       int64_t* n_process, int32_t* status, int64_t max_process);
 
 /*
+ * Batched D* with OnPress replanning.  Replaces DStar.plan followed by npress DStar.OnPress(event)
+ * calls (d_star.py:102-134) without the figure: an in-grid press on a free cell adds the obstacle,
+ * walks from the start along the parents (the walk's path excludes the goal, as there) and runs
+ * modify() (:262-274) -- processState on the kept OPEN / cell states -- where an edge collides.
+ *   presses [nq][npress][2]       the pressed cells (x, y)
+ *   cost, path_len, n_process, status [nq][npress + 1]; path [nq][npress + 1][path_cap]
+ *       round 0 = plan() as pmp_dstar2d_batch; round r: the walk's cost / cells / len(EXPAND);
+ *       status 0 walked to the goal, 1 the press changed nothing (off the grid or already an
+ *       obstacle: len(EXPAND) is kept), 2 path_cap overflow, 3 a cap or a loop the reference never
+ *       leaves (4*W*H+4 steps, or modify() on an empty OPEN), 4 the reference raises (a parentless
+ *       node: KeyError, reported with path_len -1; OPEN emptied: AttributeError), -1 not run (an
+ *       earlier call raised or capped)
+ * pmp_dstar2d_batch is this call with npress = 0.
+ */
+int pmp_dstar2d_onpress_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H,
+                              const int32_t* start_xy, const int32_t* goal_xy, int nq, const int32_t* presses, int npress,
+                              double* cost, int32_t* path_len, int32_t* path, int path_cap, int64_t* n_process,
+                              int32_t* status, int64_t max_process);
+
+/*
+ * Batched 3D D* with dynamic obstacles.  Replaces DStar3D (global_planner/graph_search/d_star3d.py:60-281):
+ * plan() (:100-109: processState until OPEN empties or the start is CLOSED, then extractPath
+ * :153-166) followed by nrounds apply_dynamic_obstacles(newly_blocked) calls (:115-149: block the
+ * voxels, walk from the start along the parents, modify() + processState where an edge collides).
+ * OPEN keeps the reference's list semantics (append when absent, first-minimal k), so every round's
+ * len(EXPAND), cost and path are bit-exact, including the inf costs of the asymmetric isCollision.
+ *   occ_bits, per_query, X, Y, Z, start_xyz, goal_xyz as pmp_graph3d_batch (X, Y, Z <= 256)
+ *   blocks [nq][nrounds][nblk][3]  voxels newly blocked per round (outside the grid: ignored); may be
+ *                                  NULL when nrounds == 0 or nblk == 0
+ *   cost, path_len, n_process, status [nq][nrounds + 1]  per round, 0 = plan(): cost (may be inf),
+ *                                  len(EXPAND) of that call, status 0 reached the goal, 1 the walk met
+ *                                  a parentless voxel (plan: unreachable; the reference returns the
+ *                                  partial path), 2 path_cap overflow, 3 cap (max_process, heap, or the
+ *                                  4*X*Y*Z+4 walk bound the reference lacks), 4 endpoints off the grid
+ *   path [nq][nrounds + 1][path_cap]  voxel ids (x*Y + y)*Z + z, start -> goal (round 0: extractPath's
+ *                                  path; rounds: apply_dynamic_obstacles' path, the goal appended when
+ *                                  reached)
+ *   expand [nq][expand_cap]        nullable: plan()'s EXPAND as voxel ids, in order (duplicates kept)
+ *   max_process                    0 = unbounded, else a processState cap per round
+ */
+int pmp_dstar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int per_query, int X, int Y, int Z,
+                      const int32_t* start_xyz, const int32_t* goal_xyz, int nq, const int32_t* blocks, int nrounds,
+                      int nblk, double* cost, int32_t* path_len, int32_t* path, int path_cap, int64_t* n_process,
+                      int32_t* status, int32_t* expand, int expand_cap, int64_t max_process);
+
+/*
  * Batched LPA*.  Replaces LPAStar.plan (global_planner/graph_search/lpa_star.py:78-87): the initial
  * computeShortestPath (:139-160) with updateVertex (:162-179), and extractPath (:209-230).  U keeps
  * the reference's Python-list semantics (first-minimal `min(U, key)`, shifting `U.remove`,

@@ -683,3 +683,61 @@ def lpastar2d_replan_batch(occ: np.ndarray, starts, goals, toggles, heuristic: s
                                     _p(s, _i32p), _p(g, _i32p), nq, _p(t, _i32p), nt, _p(out["cost"], _dp),
                                     _p(out["n_expanded"], _i32p), _p(out["status"], _i32p), int(nthreads))
     return out
+
+
+def dstar3d(occ: np.ndarray, start, goal, blocks=None, path_cap: int = 0, max_process: int = 0):
+    """Restatement of DStar3D.plan (d_star3d.py:100-109) followed by one apply_dynamic_obstacles
+    (:115-149) per entry of blocks [nrounds][nblk][3] (voxels outside the grid are ignored).
+    Returns per round (0 = plan): cost, status (0 reached the goal, 1 stopped at a parentless node,
+    3 cap), n_process (len(EXPAND)), path (voxel ids x*Y*Z + y*Z + z, start -> goal)."""
+    L = lib()
+    if not getattr(L, "_d3_set", False):
+        L.oracle_dstar3d.restype = ctypes.c_int
+        L.oracle_dstar3d.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p, _i32p, _i32p, ctypes.c_int,
+                                     ctypes.c_int, _dp, _i32p, _i64p, _i32p, ctypes.c_int, _i32p, ctypes.c_int64]
+        L._d3_set = True
+    occ = np.ascontiguousarray(occ, dtype=np.uint8)
+    X, Y, Z = occ.shape
+    b = np.zeros((0, 0, 3), np.int32) if blocks is None else np.ascontiguousarray(blocks, np.int32)
+    nr, nb = (b.shape[0], b.shape[1]) if b.size else (len(b), 0)
+    path_cap = path_cap or X * Y * Z + 1
+    s = np.ascontiguousarray(start, np.int32)
+    g = np.ascontiguousarray(goal, np.int32)
+    cost = np.zeros(nr + 1)
+    st = np.zeros(nr + 1, np.int32)
+    npr = np.zeros(nr + 1, np.int64)
+    path = np.zeros((nr + 1, path_cap), np.int32)
+    plen = np.zeros(nr + 1, np.int32)
+    rc = L.oracle_dstar3d(_p(occ, _u8p), X, Y, Z, _p(s, _i32p), _p(g, _i32p), _p(b, _i32p) if b.size else None, nr, nb,
+                          _p(cost, _dp), _p(st, _i32p), _p(npr, _i64p), _p(path, _i32p), path_cap, _p(plen, _i32p),
+                          int(max_process))
+    return dict(rc=rc, cost=cost, status=st, n_process=npr,
+                paths=[path[r, : min(plen[r], path_cap)].copy() for r in range(nr + 1)], path_len=plen)
+
+
+def dstar2d_onpress(occ: np.ndarray, start, goal, presses, path_cap: int = 0, max_process: int = 0):
+    """Restatement of DStar.plan followed by one OnPress per press (x, y) (d_star.py:75-134).
+    Returns per call (0 = plan): cost, status (include/pmp.h pmp_dstar2d_onpress_batch), n_process
+    (len(EXPAND)), paths (cells x*H + y; plan: start -> goal, presses: the walk without the goal)."""
+    L = lib()
+    if not getattr(L, "_d2p_set", False):
+        L.oracle_dstar2d_onpress.restype = ctypes.c_int
+        L.oracle_dstar2d_onpress.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, _i32p, ctypes.c_int, _dp, _i32p, ctypes.c_int, _i32p, _i64p,
+                                             _i32p, ctypes.c_int64]
+        L._d2p_set = True
+    occ = np.ascontiguousarray(occ, dtype=np.uint8)
+    W, H = occ.shape
+    pr = np.ascontiguousarray(presses, np.int32).reshape(-1, 2)
+    n = len(pr)
+    path_cap = path_cap or 4 * W * H + 8
+    cost = np.zeros(n + 1)
+    st = np.zeros(n + 1, np.int32)
+    npr = np.zeros(n + 1, np.int64)
+    plen = np.zeros(n + 1, np.int32)
+    path = np.zeros((n + 1, path_cap), np.int32)
+    L.oracle_dstar2d_onpress(_p(occ, _u8p), W, H, int(start[0]), int(start[1]), int(goal[0]), int(goal[1]),
+                             _p(pr, _i32p), n, _p(cost, _dp), _p(path, _i32p), path_cap, _p(plen, _i32p), _p(npr, _i64p),
+                             _p(st, _i32p), int(max_process))
+    return dict(cost=cost, status=st, n_process=npr, path_len=plen,
+                paths=[path[r, : max(0, min(plen[r], path_cap))].copy() for r in range(n + 1)])

@@ -725,6 +725,7 @@ typedef struct {
     uint8_t* t;
     int32_t* open;
     int64_t nopen, capopen;
+    int32_t goal_slot, goal_cell; /* start == goal: the goal object lives in slot W*H (d_star.py:66-68) */
 } dstate_t;
 
 static int d_insert(dstate_t* S, int32_t c, double hnew)
@@ -776,106 +777,18 @@ static int d_neighbors(const uint8_t* occ, int W, int H, int32_t c, int32_t* out
 /* Returns status; *n_process = number of processState calls (len(EXPAND)).
  * path: start -> goal (d_star.py:136-156). status 4 = reference raises AttributeError
  * (OPEN empties: min_k on None at :234). */
+int oracle_dstar2d_onpress(const uint8_t* occ_in, int W, int H, int sx, int sy, int gx, int gy, const int32_t* presses,
+                           int npress, double* cost, int32_t* path, int path_cap, int32_t* plen, int64_t* nproc,
+                           int32_t* status, int64_t max_process);
+
 int oracle_dstar2d(const uint8_t* occ, int W, int H, int sx, int sy, int gx, int gy, double* cost_out,
                    int32_t* path, int path_cap, int32_t* path_len, int64_t* n_process, int64_t max_process)
 {
-    const int64_t ncell = (int64_t)W * H;
-    dstate_t S;
-    S.h = (double*)malloc(sizeof(double) * (size_t)ncell);
-    S.k = (double*)malloc(sizeof(double) * (size_t)ncell);
-    S.parent = (int32_t*)malloc(sizeof(int32_t) * (size_t)ncell);
-    S.t = (uint8_t*)malloc((size_t)ncell);
-    S.capopen = 1024;
-    S.nopen = 0;
-    S.open = (int32_t*)malloc(sizeof(int32_t) * (size_t)S.capopen);
-    int status = 0;
-    *path_len = 0;
-    *cost_out = 0.0;
-    *n_process = 0;
-    for (int64_t i = 0; i < ncell; i++) {
-        S.h[i] = INFINITY;
-        S.k[i] = INFINITY;
-        S.parent[i] = -1;
-        S.t[i] = T_NEW;
-    }
-    const int32_t start = sx * H + sy, goal = gx * H + gy;
-    S.h[goal] = 0.0; /* DNode(goal, None, 'NEW', 0, inf) (:58) */
-    d_insert(&S, goal, 0.0);
-    int32_t nb[8];
-    double nc[8];
-    int64_t np = 0;
-    for (;;) {
-        /* processState (:158-218) */
-        int64_t pos = d_minpos(&S);
-        np++;
-        if (pos < 0) { status = 4; break; } /* unreachable in practice: OPEN non-empty here */
-        int32_t x = S.open[pos];
-        double k_old = S.k[x];
-        if (S.t[x] == T_OPEN) S.t[x] = T_CLOSED;
-        memmove(&S.open[pos], &S.open[pos + 1], sizeof(int32_t) * (size_t)(S.nopen - pos - 1));
-        S.nopen--;
-        int nn;
-        if (k_old < S.h[x]) {
-            nn = d_neighbors(occ, W, H, x, nb, nc);
-            for (int i = 0; i < nn; i++) {
-                int32_t y = nb[i];
-                if (S.h[y] <= k_old && S.h[x] > S.h[y] + nc[i]) {
-                    S.parent[x] = y;
-                    S.h[x] = S.h[y] + nc[i];
-                }
-            }
-        }
-        nn = d_neighbors(occ, W, H, x, nb, nc);
-        if (k_old == S.h[x]) {
-            for (int i = 0; i < nn; i++) {
-                int32_t y = nb[i];
-                if (S.t[y] == T_NEW || (S.parent[y] == x && S.h[y] != S.h[x] + nc[i]) ||
-                    (S.parent[y] != x && S.h[y] > S.h[x] + nc[i])) {
-                    S.parent[y] = x;
-                    if (d_insert(&S, y, S.h[x] + nc[i])) { status = 3; goto ddone; }
-                }
-            }
-        } else {
-            for (int i = 0; i < nn; i++) {
-                int32_t y = nb[i];
-                if (S.t[y] == T_NEW || (S.parent[y] == x && S.h[y] != S.h[x] + nc[i])) {
-                    S.parent[y] = x;
-                    if (d_insert(&S, y, S.h[x] + nc[i])) { status = 3; goto ddone; }
-                } else if (S.parent[y] != x && S.h[y] > S.h[x] + nc[i]) {
-                    if (d_insert(&S, x, S.h[x])) { status = 3; goto ddone; }
-                } else if (S.parent[y] != x && S.h[x] > S.h[y] + nc[i] && S.t[y] == T_CLOSED && S.h[y] > k_old) {
-                    if (d_insert(&S, y, S.h[y])) { status = 3; goto ddone; }
-                }
-            }
-        }
-        if (S.nopen == 0) { status = 4; break; } /* return self.min_k -> None.k raises */
-        if (S.t[start] == T_CLOSED) break;
-        if (max_process > 0 && np >= max_process) { status = 3; break; }
-    }
-    if (status == 0) {
-        double cost = 0.0;
-        int32_t c = start;
-        int32_t len = 0;
-        if (len < path_cap) path[len] = c; else status = 2;
-        len++;
-        while (c != goal) {
-            int32_t p = S.parent[c];
-            if (p < 0) { status = 4; break; } /* closed_list[None] -> KeyError in reference */
-            int cx = c / H, cy = c % H, px = p / H, py = p % H;
-            if (collide2(occ, W, H, cx, cy, px, py)) cost += INFINITY;
-            else cost += vnorm2((double)(px - cx), (double)(py - cy));
-            c = p;
-            if (len < path_cap) path[len] = c; else status = 2;
-            len++;
-            if (len > ncell + 1) { status = 4; break; } /* parent cycle: reference loops forever */
-        }
-        *path_len = len;
-        *cost_out = cost;
-    }
-ddone:
-    *n_process = np;
-    free(S.h); free(S.k); free(S.parent); free(S.t); free(S.open);
-    return status;
+    /* DStar.plan: the OnPress restatement with no presses (one processState loop for both) */
+    int32_t st;
+    oracle_dstar2d_onpress(occ, W, H, sx, sy, gx, gy, NULL, 0, cost_out, path, path_cap, path_len, n_process, &st,
+                           max_process);
+    return st;
 }
 
 /* Batch of 2D A* queries on one grid, OpenMP over queries (the CPU baseline of bench.py).
@@ -2206,4 +2119,408 @@ void oracle_dstar2d_batch(const uint8_t* occ, int W, int H, const int32_t* start
         }
         free(path);
     }
+}
+
+/* ============================================================================================
+ * DStar3D (global_planner/graph_search/d_star3d.py:60-281): plan() (:100-109) followed by
+ * nrounds apply_dynamic_obstacles() calls (:115-149).  OPEN is restated as the reference's Python
+ * list: append only when the node is not in it (:245-246; Node3D equality is by coordinates and
+ * "in OPEN" <=> t == OPEN throughout), min_state = the FIRST minimal k in list order (:220-225),
+ * delete = list.remove (:248-253).  getNeighbor (:266-280) keeps in-map voxels with
+ * isCollision(node, n) false; isCollision (graph_search_3d.py:66-107) is asymmetric for three-axis
+ * diagonals.  `p in self.obstacles` is false outside the grid (only in-grid voxels are tested).
+ * start == goal: map[start] = self.start detaches the goal object (:89-90): slot ncell.
+ * ============================================================================================ */
+typedef struct {
+    double *h, *k;
+    int32_t* parent;
+    uint8_t* t;
+    int32_t* open;
+    int64_t nopen, capopen;
+    uint8_t* occ; /* working copy (apply_dynamic_obstacles adds voxels) */
+    int X, Y, Z, ncell, goal_slot, goal_cell;
+    int64_t np;
+} d3_t;
+
+static inline int d3_occ(const d3_t* S, int x, int y, int z)
+{
+    if (x < 0 || y < 0 || z < 0 || x >= S->X || y >= S->Y || z >= S->Z) return 0;
+    return S->occ[((int64_t)x * S->Y + y) * S->Z + z] != 0;
+}
+static inline void d3_xyz(const d3_t* S, int c, int* x, int* y, int* z)
+{
+    *z = c % S->Z;
+    *y = (c / S->Z) % S->Y;
+    *x = c / (S->Z * S->Y);
+}
+static inline int d3_coord(const d3_t* S, int slot) { return slot == S->goal_slot ? S->goal_cell : slot; }
+/* isCollision(node1, node2) on voxel ids */
+static int d3_coll(const d3_t* S, int a, int b)
+{
+    int x1, y1, z1, x2, y2, z2;
+    d3_xyz(S, a, &x1, &y1, &z1);
+    d3_xyz(S, b, &x2, &y2, &z2);
+    if (d3_occ(S, x1, y1, z1) || d3_occ(S, x2, y2, z2)) return 1;
+    const int dx = x2 - x1, dy = y2 - y1, dz = z2 - z1;
+    const int ax = abs(dx) > abs(dy) ? abs(dx) : abs(dy);
+    if ((ax > abs(dz) ? ax : abs(dz)) > 1) return 0;
+    const int ch = (dx != 0) + (dy != 0) + (dz != 0);
+    if (ch <= 1) return 0;
+    if (ch == 2) {
+        if (dx != 0 && dy != 0) return d3_occ(S, x1 + dx, y1, z1) || d3_occ(S, x1, y1 + dy, z1);
+        if (dx != 0 && dz != 0) return d3_occ(S, x1 + dx, y1, z1) || d3_occ(S, x1, y1, z1 + dz);
+        return d3_occ(S, x1, y1 + dy, z1) || d3_occ(S, x1, y1, z1 + dz);
+    }
+    return d3_occ(S, x1 + dx, y1, z1) || d3_occ(S, x1, y1 + dy, z1) || d3_occ(S, x1, y1, z1 + dz);
+}
+/* GraphSearcher3D.cost: inf on collision, else Planner3D.dist (math.sqrt of the squared deltas) */
+static double d3_cost(const d3_t* S, int a, int b)
+{
+    if (d3_coll(S, a, b)) return INFINITY;
+    int x1, y1, z1, x2, y2, z2;
+    d3_xyz(S, a, &x1, &y1, &z1);
+    d3_xyz(S, b, &x2, &y2, &z2);
+    const double dx = x2 - x1, dy = y2 - y1, dz = z2 - z1;
+    return sqrt(dx * dx + dy * dy + dz * dz);
+}
+/* insert (:233-246) */
+static void d3_insert(d3_t* S, int slot, double h_new)
+{
+    if (S->t[slot] == T_NEW) S->k[slot] = h_new;
+    else if (S->t[slot] == T_OPEN) S->k[slot] = S->k[slot] < h_new ? S->k[slot] : h_new;
+    else if (S->t[slot] == T_CLOSED) S->k[slot] = S->h[slot] < h_new ? S->h[slot] : h_new;
+    const int in_open = S->t[slot] == T_OPEN;
+    S->h[slot] = h_new;
+    S->t[slot] = T_OPEN;
+    if (!in_open) {
+        if (S->nopen == S->capopen) {
+            S->capopen *= 2;
+            S->open = (int32_t*)realloc(S->open, sizeof(int32_t) * (size_t)S->capopen);
+        }
+        S->open[S->nopen++] = slot;
+    }
+}
+/* min_state (:220-225): first minimal k; returns the list index or -1 */
+static int64_t d3_min_state(const d3_t* S)
+{
+    if (S->nopen == 0) return -1;
+    int64_t bi = 0;
+    for (int64_t i = 1; i < S->nopen; i++)
+        if (S->k[S->open[i]] < S->k[S->open[bi]]) bi = i;
+    return bi;
+}
+/* the neighbours of slot X (getNeighbor :266-280) as voxel ids, in motion order */
+static int d3_neighbors(const d3_t* S, int Xs, int* nb)
+{
+    const int c = d3_coord(S, Xs);
+    int x, y, z, n = 0;
+    d3_xyz(S, c, &x, &y, &z);
+    for (int m = 0; m < 26; m++) {
+        const int nx = x + M3[m][0], ny = y + M3[m][1], nz = z + M3[m][2];
+        if (nx < 0 || ny < 0 || nz < 0 || nx >= S->X || ny >= S->Y || nz >= S->Z) continue;
+        const int v = (nx * S->Y + ny) * S->Z + nz;
+        if (!d3_coll(S, c, v)) nb[n++] = v;
+    }
+    return n;
+}
+/* processState (:168-218); returns the new min k or -1 */
+static double d3_process(d3_t* S)
+{
+    const int64_t mi = d3_min_state(S);
+    if (mi < 0) return -1.0;
+    const int Xs = S->open[mi];
+    S->np++;
+    const double k_old = S->k[Xs];
+    /* delete (:248-253) */
+    if (S->t[Xs] == T_OPEN) S->t[Xs] = T_CLOSED;
+    memmove(S->open + mi, S->open + mi + 1, sizeof(int32_t) * (size_t)(S->nopen - mi - 1));
+    S->nopen--;
+    const int Xc = d3_coord(S, Xs);
+    int nb[26];
+    const int nn = d3_neighbors(S, Xs, nb);
+    if (k_old < S->h[Xs])
+        for (int i = 0; i < nn; i++) {
+            const int n = nb[i];
+            const double c = d3_cost(S, Xc, n);
+            if (S->h[n] <= k_old && S->h[Xs] > S->h[n] + c) {
+                S->parent[Xs] = n;
+                S->h[Xs] = S->h[n] + c;
+            }
+        }
+    if (k_old == S->h[Xs]) {
+        for (int i = 0; i < nn; i++) {
+            const int n = nb[i];
+            const double c = d3_cost(S, Xc, n);
+            if (S->t[n] == T_NEW || (S->parent[n] == Xc && S->h[n] != S->h[Xs] + c) ||
+                (S->parent[n] != Xc && S->h[n] > S->h[Xs] + c)) {
+                S->parent[n] = Xc;
+                d3_insert(S, n, S->h[Xs] + c);
+            }
+        }
+    } else {
+        for (int i = 0; i < nn; i++) {
+            const int n = nb[i];
+            const double c = d3_cost(S, Xc, n);
+            if (S->t[n] == T_NEW || (S->parent[n] == Xc && S->h[n] != S->h[Xs] + c)) {
+                S->parent[n] = Xc;
+                d3_insert(S, n, S->h[Xs] + c);
+            } else if (S->parent[n] != Xc && S->h[n] > S->h[Xs] + c) {
+                d3_insert(S, Xs, S->h[Xs]);
+            } else if (S->parent[n] != Xc && S->h[Xs] > S->h[n] + c && S->t[n] == T_CLOSED && S->h[n] > k_old) {
+                d3_insert(S, n, S->h[n]);
+            }
+        }
+    }
+    const int64_t s = d3_min_state(S);
+    return s >= 0 ? S->k[S->open[s]] : -1.0;
+}
+/* modify (:255-264) */
+static void d3_modify(d3_t* S, int node, double h_new, int64_t max_process)
+{
+    if (S->t[node] == T_CLOSED) d3_insert(S, node, h_new);
+    for (;;) {
+        const double k_min = d3_process(S);
+        if (k_min < 0 || k_min >= S->h[node]) break;
+        if (max_process > 0 && S->np >= max_process) break;
+    }
+}
+
+/* Returns 0, or 3 when a cap was hit.  Per round r (0 = plan): cost[r], status[r] (0 reached the
+ * goal, 1 stopped at a node without parent, 3 step / processState cap), nproc[r] = len(EXPAND),
+ * path[r * path_cap ..] (voxel ids, start -> goal) and plen[r]. */
+int oracle_dstar3d(const uint8_t* occ_in, int X, int Y, int Z, const int32_t* s, const int32_t* g,
+                   const int32_t* blocks, int nrounds, int nblk, double* cost, int32_t* status, int64_t* nproc,
+                   int32_t* path, int path_cap, int32_t* plen, int64_t max_process)
+{
+    d3_t S;
+    S.X = X; S.Y = Y; S.Z = Z;
+    S.ncell = X * Y * Z;
+    const int start = (s[0] * Y + s[1]) * Z + s[2];
+    S.goal_cell = (g[0] * Y + g[1]) * Z + g[2];
+    S.goal_slot = start == S.goal_cell ? S.ncell : S.goal_cell;
+    const int ns = S.ncell + 1;
+    S.h = (double*)malloc(sizeof(double) * ns);
+    S.k = (double*)malloc(sizeof(double) * ns);
+    S.parent = (int32_t*)malloc(sizeof(int32_t) * ns);
+    S.t = (uint8_t*)malloc(ns);
+    S.occ = (uint8_t*)malloc(S.ncell);
+    memcpy(S.occ, occ_in, S.ncell);
+    S.capopen = 1024;
+    S.nopen = 0;
+    S.open = (int32_t*)malloc(sizeof(int32_t) * S.capopen);
+    S.np = 0;
+    for (int i = 0; i < ns; i++) {
+        S.h[i] = INFINITY; S.k[i] = INFINITY; S.parent[i] = -1; S.t[i] = T_NEW;
+    }
+    S.h[S.goal_slot] = 0.0;
+    d3_insert(&S, S.goal_slot, 0.0);
+    int rc = 0;
+    /* plan (:100-109) */
+    for (;;) {
+        const double kmin = d3_process(&S);
+        if (kmin < 0) break;
+        if (S.t[start] == T_CLOSED) break;
+        if (max_process > 0 && S.np >= max_process) { rc = 3; break; }
+    }
+    const int64_t bound = 4 * (int64_t)S.ncell + 4;
+    for (int r = 0; r <= nrounds; r++) {
+        int32_t* pth = path + (size_t)r * path_cap;
+        int n = 0, st = 0;
+        double c = 0.0;
+        if (r > 0) {
+            const int32_t* b = blocks + ((size_t)(r - 1) * nblk) * 3;
+            for (int i = 0; i < nblk; i++)
+                if (b[3 * i] >= 0 && b[3 * i] < X && b[3 * i + 1] >= 0 && b[3 * i + 1] < Y && b[3 * i + 2] >= 0 &&
+                    b[3 * i + 2] < Z)
+                    S.occ[((int64_t)b[3 * i] * Y + b[3 * i + 1]) * Z + b[3 * i + 2]] = 1;
+            S.np = 0;
+        }
+        int node = start;
+        int64_t steps = 0;
+        if (rc == 0) {
+            if (r == 0) { if (n < path_cap) pth[n] = start; n++; }
+            while (node != S.goal_cell) {
+                if (++steps > bound) { st = 3; break; }
+                if (S.parent[node] < 0) {
+                    if (r > 0) d3_modify(&S, node, S.h[S.goal_slot] + d3_cost(&S, node, S.goal_cell), max_process);
+                    st = 1;
+                    break;
+                }
+                const int p = S.parent[node];
+                const int pslot = p == S.goal_cell ? S.goal_slot : p;
+                if (r > 0 && d3_coll(&S, node, p)) {
+                    d3_modify(&S, node, S.h[pslot] + d3_cost(&S, node, p), max_process);
+                    if (max_process > 0 && S.np >= max_process) { st = 3; break; }
+                    continue;
+                }
+                if (r > 0) { if (n < path_cap) pth[n] = node; n++; }
+                c += d3_cost(&S, node, p);
+                node = p;
+                if (r == 0) { if (n < path_cap) pth[n] = node; n++; }
+            }
+            if (r > 0 && st == 0 && node == S.goal_cell) { if (n < path_cap) pth[n] = node; n++; }
+        } else {
+            st = 3;
+        }
+        if (st == 3) rc = 3;
+        cost[r] = c;
+        status[r] = st;
+        nproc[r] = S.np;
+        plen[r] = n;
+    }
+    free(S.h); free(S.k); free(S.parent); free(S.t); free(S.open); free(S.occ);
+    return rc;
+}
+
+/* ============================================================================================
+ * DStar.plan (d_star.py:75-89) followed by npress OnPress(event) calls (:102-134) without the
+ * figure.  processState (:158-218) with the list-semantics OPEN of oracle_dstar2d; OnPress adds the
+ * obstacle (a free in-grid cell only), resets EXPAND, walks from the start along the parents
+ * (path without the goal) and calls modify (:262-274) where an edge collides.
+ * Per call r (0 = plan): cost[r], plen[r], path[r * path_cap ..], nproc[r] = len(EXPAND) (a None
+ * appended by processState on an empty OPEN counts), status[r]: 0 done, 1 the press did nothing,
+ * 2 path_cap overflow, 3 a loop the reference never leaves (4*W*H+4 walk steps, or modify on an
+ * empty OPEN) or max_process, 4 the reference raises, -1 not run.
+ * ============================================================================================ */
+/* returns 0 = OPEN empty on entry (-1), 1 = processed, OPEN non-empty, 2 = processed, OPEN empty
+ * (min_k raises), 3 = allocation failure */
+static int d2_process(dstate_t* S, const uint8_t* occ, int W, int H, int64_t* np)
+{
+    int64_t pos = d_minpos(S);
+    (*np)++;
+    if (pos < 0) return 0;
+    int32_t x = S->open[pos];
+    double k_old = S->k[x];
+    if (S->t[x] == T_OPEN) S->t[x] = T_CLOSED;
+    memmove(&S->open[pos], &S->open[pos + 1], sizeof(int32_t) * (size_t)(S->nopen - pos - 1));
+    S->nopen--;
+    const int32_t xc = x == S->goal_slot ? S->goal_cell : x; /* node.current */
+    int32_t nb[8];
+    double nc[8];
+    int nn = d_neighbors(occ, W, H, xc, nb, nc);
+    if (k_old < S->h[x])
+        for (int i = 0; i < nn; i++) {
+            int32_t y = nb[i];
+            if (S->h[y] <= k_old && S->h[x] > S->h[y] + nc[i]) { S->parent[x] = y; S->h[x] = S->h[y] + nc[i]; }
+        }
+    if (k_old == S->h[x]) {
+        for (int i = 0; i < nn; i++) {
+            int32_t y = nb[i];
+            if (S->t[y] == T_NEW || (S->parent[y] == xc && S->h[y] != S->h[x] + nc[i]) ||
+                (S->parent[y] != xc && S->h[y] > S->h[x] + nc[i])) {
+                S->parent[y] = xc;
+                if (d_insert(S, y, S->h[x] + nc[i])) return 3;
+            }
+        }
+    } else {
+        for (int i = 0; i < nn; i++) {
+            int32_t y = nb[i];
+            if (S->t[y] == T_NEW || (S->parent[y] == xc && S->h[y] != S->h[x] + nc[i])) {
+                S->parent[y] = xc;
+                if (d_insert(S, y, S->h[x] + nc[i])) return 3;
+            } else if (S->parent[y] != xc && S->h[y] > S->h[x] + nc[i]) {
+                if (d_insert(S, x, S->h[x])) return 3;
+            } else if (S->parent[y] != xc && S->h[x] > S->h[y] + nc[i] && S->t[y] == T_CLOSED && S->h[y] > k_old) {
+                if (d_insert(S, y, S->h[y])) return 3;
+            }
+        }
+    }
+    return S->nopen == 0 ? 2 : 1;
+}
+
+int oracle_dstar2d_onpress(const uint8_t* occ_in, int W, int H, int sx, int sy, int gx, int gy, const int32_t* presses,
+                           int npress, double* cost, int32_t* path, int path_cap, int32_t* plen, int64_t* nproc,
+                           int32_t* status, int64_t max_process)
+{
+    const int64_t ncell = (int64_t)W * H;
+    uint8_t* occ = (uint8_t*)malloc((size_t)ncell);
+    memcpy(occ, occ_in, (size_t)ncell);
+    dstate_t S;
+    const int64_t ns = ncell + 1;
+    S.h = (double*)malloc(sizeof(double) * (size_t)ns);
+    S.k = (double*)malloc(sizeof(double) * (size_t)ns);
+    S.parent = (int32_t*)malloc(sizeof(int32_t) * (size_t)ns);
+    S.t = (uint8_t*)malloc((size_t)ns);
+    S.capopen = 1024;
+    S.nopen = 0;
+    S.open = (int32_t*)malloc(sizeof(int32_t) * (size_t)S.capopen);
+    for (int64_t i = 0; i < ns; i++) { S.h[i] = INFINITY; S.k[i] = INFINITY; S.parent[i] = -1; S.t[i] = T_NEW; }
+    const int32_t start = sx * H + sy, goal = gx * H + gy;
+    S.goal_cell = goal;
+    S.goal_slot = start == goal ? (int32_t)ncell : goal;
+    S.h[S.goal_slot] = 0.0; /* DNode(goal, None, 'NEW', 0, inf) (:58) */
+    d_insert(&S, S.goal_slot, 0.0);
+    int64_t np = 0;
+    int st = 0;
+    for (;;) {
+        const int ps = d2_process(&S, occ, W, H, &np);
+        if (ps == 3) { st = 3; break; }
+        if (ps != 1) { st = 4; break; }
+        if (S.t[start] == T_CLOSED) break;
+        if (max_process > 0 && np >= max_process) { st = 3; break; }
+    }
+    for (int r = 0; r <= npress; r++) {
+        int32_t* pth = path + (size_t)r * path_cap;
+        int n = 0, rst = st;
+        double c = 0.0;
+        if (r == 0) {
+            if (st == 0) {
+                int32_t x = start;
+                pth[n++] = x;
+                while (x != goal) {
+                    int32_t p = S.parent[x];
+                    if (p < 0 || n > ncell) { rst = 4; break; }
+                    const int cx = x / H, cy = x % H, px = p / H, py = p % H;
+                    c += collide2(occ, W, H, cx, cy, px, py) ? INFINITY : ((cx != px && cy != py) ? sqrt(2.0) : 1.0);
+                    x = p;
+                    if (n < path_cap) pth[n] = x;
+                    n++;
+                }
+                if (rst == 0 && n > path_cap) rst = 2;
+            }
+        } else if (st != 0) {
+            rst = -1;
+        } else {
+            const int px = presses[2 * (r - 1)], py = presses[2 * (r - 1) + 1];
+            if (px < 0 || px > W - 1 || py < 0 || py > H - 1 || occ[(int64_t)px * H + py]) {
+                rst = 1;
+            } else {
+                occ[(int64_t)px * H + py] = 1;
+                np = 0;
+                int32_t node = start;
+                int64_t steps = 0;
+                while (node != goal) {
+                    if (++steps > 4 * ncell + 4) { rst = 3; break; }
+                    const int32_t p = S.parent[node];
+                    if (p < 0) { rst = 4; n = -1; break; } /* self.map[None]: KeyError */
+                    const int cx = node / H, cy = node % H, qx = p / H, qy = p % H;
+                    if (collide2(occ, W, H, cx, cy, qx, qy)) {
+                        if (S.t[node] == T_CLOSED && d_insert(&S, node, S.h[p] + INFINITY)) { rst = 3; break; }
+                        for (;;) {
+                            const int ps = d2_process(&S, occ, W, H, &np);
+                            if (ps == 3) { rst = 3; break; }
+                            if (ps == 2) { rst = 4; break; }
+                            if (ps == 0) { rst = 3; break; } /* -1 >= node.h never holds: endless loop */
+                            if (max_process > 0 && np >= max_process) { rst = 3; break; }
+                            if (S.k[S.open[d_minpos(&S)]] >= S.h[node]) break;
+                        }
+                        if (rst != 0) break;
+                        continue;
+                    }
+                    if (n < path_cap) pth[n] = node;
+                    n++;
+                    c += (cx != qx && cy != qy) ? sqrt(2.0) : 1.0;
+                    node = p;
+                }
+                if (rst == 0 && n > path_cap) rst = 2;
+            }
+            if (rst == 3 || rst == 4) st = rst;
+        }
+        cost[r] = c;
+        plen[r] = n;
+        status[r] = rst;
+        nproc[r] = rst == -1 ? 0 : np;
+    }
+    free(occ); free(S.h); free(S.k); free(S.parent); free(S.t); free(S.open);
+    return st;
 }

@@ -40,6 +40,10 @@ SIGNATURES = {
     "pmp_mpc_control_batch": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _vp]),
     "pmp_dstar2d_batch": (_i, [_vp, _vp, _vp, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, ctypes.c_int64]),
+    "pmp_dstar2d_onpress_batch": (_i, [_vp, _vp, _vp, _i, _i, _vp, _vp, _i, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp,
+                                       ctypes.c_int64]),
+    "pmp_dstar3d_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _i, _vp, _vp, _vp, _i, _vp, _vp,
+                               _vp, _i, ctypes.c_int64]),
     "pmp_lpastar2d_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     "pmp_dstarlite2d_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     "pmp_lpastar2d_replan_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _i,

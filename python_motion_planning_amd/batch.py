@@ -291,6 +291,38 @@ def dstar2d_batch(occ, starts, goals, path_cap: int | None = None, max_process: 
     return out
 
 
+def dstar2d_onpress_batch(occ, starts, goals, presses, path_cap: int | None = None, max_process: int = 0):
+    """Batched DStar.plan followed by one DStar.OnPress per press (d_star.py:75-134) on one Grid,
+    pmp_dstar2d_onpress_batch.  presses [nq, npress, 2] int cells (x, y).
+    Returns dict of device tensors, per call r (0 = plan): cost [nq, R], path_len [nq, R],
+    path [nq, R, path_cap] (cells x*H+y; plan start -> goal, presses the walk without the goal),
+    n_process [nq, R] (len(EXPAND)), status [nq, R] (include/pmp.h)."""
+    torch = _lib.device_check()
+    L = _lib.load_library()
+    ctx = _lib.context()
+    occ = np.asarray(occ)
+    W, H = occ.shape
+    occ_bits = occ_bits_device(occ, torch)
+    s = _dev(torch, starts, torch.int32).reshape(-1, 2)
+    g = _dev(torch, goals, torch.int32).reshape(-1, 2)
+    nq = int(s.shape[0])
+    pr = _dev(torch, presses, torch.int32)
+    if pr.dim() != 3 or pr.shape[0] != nq or pr.shape[2] != 2:
+        raise ValueError("presses must be [nq, npress, 2]")
+    R = int(pr.shape[1]) + 1
+    path_cap = 4 * W * H + 8 if path_cap is None else int(path_cap)
+    i32 = dict(dtype=torch.int32, device="cuda")
+    out = dict(cost=torch.empty((nq, R), dtype=torch.float64, device="cuda"), path_len=torch.empty((nq, R), **i32),
+               path=torch.empty((nq, R, path_cap), **i32),
+               n_process=torch.empty((nq, R), dtype=torch.int64, device="cuda"), status=torch.empty((nq, R), **i32))
+    rc = L.pmp_dstar2d_onpress_batch(ctx, _lib.stream_ptr(), occ_bits.data_ptr(), W, H, s.data_ptr(), g.data_ptr(), nq,
+                                     pr.data_ptr(), R - 1, out["cost"].data_ptr(), out["path_len"].data_ptr(),
+                                     out["path"].data_ptr(), path_cap, out["n_process"].data_ptr(),
+                                     out["status"].data_ptr(), int(max_process))
+    _lib.check(ctx, rc, "pmp_dstar2d_onpress_batch")
+    return out
+
+
 def lpastar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: int = 1001, counters: bool = False,
                     lite: bool = False):
     """Batched LPAStar.plan (lpa_star.py:78-87: computeShortestPath + extractPath) on one Grid;
@@ -447,5 +479,48 @@ def astar3d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: in
                              out["n_expanded"].data_ptr(), _lib.ptr(out["expand"]), int(expand_cap),
                              _lib.ptr(out["counters"]), out["status"].data_ptr())
     _lib.check(ctx, rc, "pmp_graph3d_batch")
+    out["dims"] = (X, Y, Z)
+    return out
+
+
+def dstar3d_batch(occ, starts, goals, blocks=None, path_cap: int | None = None, expand_cap: int = 0,
+                  max_process: int = 0):
+    """Batched DStar3D (d_star3d.py:60-281): plan() and then one apply_dynamic_obstacles() per round
+    of `blocks` [nq, nrounds, nblk, 3] (int voxels; outside the grid = ignored), on pmp_dstar3d_batch.
+
+    occ: uint8 [X, Y, Z] shared grid or [nq, X, Y, Z] per-query grids (numpy).
+    Returns dict of device tensors, per round r (0 = plan): cost [nq, R], path_len [nq, R],
+    path [nq, R, path_cap] (voxels (x*Y+y)*Z+z, start -> goal), n_process [nq, R] (len(EXPAND)),
+    status [nq, R] (include/pmp.h), optional expand [nq, expand_cap] (plan()'s EXPAND voxels)."""
+    torch = _lib.device_check()
+    L = _lib.load_library()
+    ctx = _lib.context()
+    occ = np.asarray(occ)
+    per_query = occ.ndim == 4
+    X, Y, Z = occ.shape[-3:]
+    words = np.stack([pack_bits(o) for o in occ]) if per_query else pack_bits(occ)
+    occ_bits = torch.as_tensor(np.ascontiguousarray(words).view(np.int32), device="cuda")
+    s = _dev(torch, starts, torch.int32).reshape(-1, 3)
+    g = _dev(torch, goals, torch.int32).reshape(-1, 3)
+    nq = int(s.shape[0])
+    if blocks is None:
+        nr, nb, b = 0, 0, None
+    else:
+        b = _dev(torch, blocks, torch.int32)
+        if b.dim() != 4 or b.shape[0] != nq or b.shape[3] != 3:
+            raise ValueError("blocks must be [nq, nrounds, nblk, 3]")
+        nr, nb = int(b.shape[1]), int(b.shape[2])
+    R = nr + 1
+    path_cap = min(X * Y * Z + 1, 1 << 16) if path_cap is None else int(path_cap)
+    i32 = dict(dtype=torch.int32, device="cuda")
+    out = dict(cost=torch.empty((nq, R), dtype=torch.float64, device="cuda"), path_len=torch.empty((nq, R), **i32),
+               path=torch.empty((nq, R, path_cap), **i32),
+               n_process=torch.empty((nq, R), dtype=torch.int64, device="cuda"), status=torch.empty((nq, R), **i32))
+    out["expand"] = torch.empty((nq, expand_cap), **i32) if expand_cap else None
+    rc = L.pmp_dstar3d_batch(ctx, _lib.stream_ptr(), occ_bits.data_ptr(), 1 if per_query else 0, X, Y, Z, s.data_ptr(),
+                             g.data_ptr(), nq, _lib.ptr(b), nr, nb, out["cost"].data_ptr(), out["path_len"].data_ptr(),
+                             out["path"].data_ptr(), path_cap, out["n_process"].data_ptr(), out["status"].data_ptr(),
+                             _lib.ptr(out["expand"]), int(expand_cap), int(max_process))
+    _lib.check(ctx, rc, "pmp_dstar3d_batch")
     out["dims"] = (X, Y, Z)
     return out

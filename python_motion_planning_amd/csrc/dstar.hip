@@ -1,4 +1,4 @@
-// Batched D* (static plan) for gfx950, exact with DStar.plan (global_planner/graph_search/d_star.py:75-291)
+// Batched D* (plan + OnPress replanning) for gfx950, exact with DStar.plan (global_planner/graph_search/d_star.py:75-291)
 // over Grid with GraphSearcher.isCollision (graph_search.py:61-87).
 //
 // The reference's OPEN is a Python list: insert appends (duplicates allowed, :236-248), min_state is
@@ -9,6 +9,9 @@
 //   per cell (32 B): h, k, first/last remaining entry, parent cell, entry count | tag << 24;
 //   per entry: the next entry of the same node (a FIFO per node, positions = append counter);
 //   a lazy min-heap (heap16.h) of (k, first position, cell), validated on pop against the cell.
+// plan() is followed by any number of OnPress(x, y) calls (:102-134) without the figure: add the
+// obstacle to the worker's copy of the grid, walk from the start along the parents and modify()
+// (:262-274) where an edge collides -- processState on the kept OPEN / cell states.
 // processState (:158-218) runs on one wave: lanes 0..7 are the 8 motions (env.py:52-55) in order,
 // the RAISE scan is a scalar loop, the LOWER/else decisions are per lane, and appended entries
 // take their positions by lane-order prefix counts, exactly the reference's append order.
@@ -81,40 +84,318 @@ __device__ __forceinline__ DCell rl_cell(const DCell& v, int lane)
     return r;
 }
 
-__global__ __launch_bounds__(64) void dstar_kernel(const uint32_t* __restrict__ occ, int W, int H,
+// Per-query search state of one wave (wave-uniform scalars)
+struct Search2 {
+    heap16::Heap hp;
+    DCell* cells;
+    int32_t* nxt;
+    int heap_cap, lds_cap, entry_cap;
+    int n;              // heap elements (valid + stale)
+    int64_t open;       // len(OPEN) (entries, duplicates included)
+    int ne;             // entries appended so far (list positions)
+    int64_t np;         // processState calls (len(EXPAND), a None entry included)
+    Ent root;
+    int start;
+    int goal_slot, goal_cell;  // start == goal: the goal object lives in slot W*H (d_star.py:66-68)
+    bool start_closed;  // self.start.t == 'CLOSED'
+    bool overflow;
+};
+
+// processState outcome: EMPTY = OPEN was empty (the reference appends None to EXPAND, returns -1),
+// DONE = processed and OPEN is non-empty (min_k is S.root after clean_top), EMPTIED = processed and
+// OPEN is empty (the reference's `return self.min_k` raises AttributeError), OVER = a cap was hit
+enum { PS_EMPTY = 0, PS_DONE = 1, PS_EMPTIED = 2, PS_OVER = 3 };
+
+struct D2 {
+    const uint32_t* occ;  // the shared grid, or the worker's working copy (OnPress adds obstacles)
+    int W, H;
+    Search2& S;
+    int lane, pop_jl, pop_ol;
+    int mdx, mdy;
+    double mcost;
+    KeyD key;
+
+    __device__ __forceinline__ void push(const Ent& it0)
+    {
+        if (S.n >= S.heap_cap) { S.overflow = true; return; }
+        Ent it = it0;
+        key.derive(it);
+        if (S.n == 0) {
+            if (lane == 0) heap16::store<true>(S.hp, 0, it);
+            S.root = it;
+            heap16::wsync();
+        } else if (S.n < S.lds_cap) {
+            heap16::push<KeyD, false>(S.hp, key, S.n, it, S.root, lane);
+        } else {
+            heap16::push<KeyD, true>(S.hp, key, S.n, it, S.root, lane);
+        }
+        S.n += 1;
+    }
+
+    __device__ __forceinline__ void pop_top()
+    {
+        S.n -= 1;
+        if (S.n > 0) {
+            if (S.n < S.lds_cap) heap16::pop<KeyD, false>(S.hp, key, S.n, S.root, lane, pop_jl, pop_ol);
+            else heap16::pop<KeyD, true>(S.hp, key, S.n, S.root, lane, pop_jl, pop_ol);
+        }
+    }
+
+    // drop heap tops that do not match their cell's (k, first entry); S.root is then min_state
+    __device__ __forceinline__ void clean_top()
+    {
+        while (S.open > 0 && S.n > 0) {
+            const DCell c = load_cell(S.cells, (int)S.root.b);
+            if (cnt_of(c.cnt_t) > 0 && (uint32_t)c.first == S.root.a && c.k == S.root.g) return;
+            pop_top();
+        }
+    }
+
+    // insert(node, h_new) (:236-248) on a wave-uniform cell: always appends an entry
+    __device__ __forceinline__ void insert_uniform(int X, double hnew)
+    {
+        if (S.ne + 1 > S.entry_cap) { S.overflow = true; return; }
+        DCell c = load_cell(S.cells, X);
+        const uint32_t t = tag_of(c.cnt_t);
+        if (t == T_NEW) c.k = hnew;
+        else if (t == T_OPEN) c.k = fmin(c.k, hnew);
+        else c.k = fmin(c.h, hnew);
+        c.h = hnew;
+        const int e = S.ne++;
+        const uint32_t cnt = cnt_of(c.cnt_t);
+        if (lane == 0) {
+            if (cnt == 0) c.first = e;
+            else S.nxt[c.last] = e;
+            S.nxt[e] = -1;
+        }
+        if (cnt == 0) c.first = e;
+        c.last = e;
+        c.cnt_t = (T_OPEN << 24) | (cnt + 1u);
+        if (lane == 0) store_cell(S.cells, X, c);
+        S.open += 1;
+        if (X == S.start) S.start_closed = false;
+        heap16::wsync();
+        Ent it;
+        it.g = c.k;
+        it.a = (uint32_t)c.first;
+        it.b = (uint32_t)X;
+        push(it);
+    }
+
+    __device__ __forceinline__ int process_state()
+    {
+        // ---- min_state: the earliest entry of the node minimising (k, first entry) ----
+        clean_top();
+        S.np++;  // EXPAND.append(node), None included (:165-167)
+        if (S.open == 0) return PS_EMPTY;
+        if (S.n == 0) return PS_OVER;  // cannot happen while S.open > 0
+        const Ent top = S.root;
+        pop_top();
+        DCell xc = load_cell(S.cells, (int)top.b);
+        const int X = (int)top.b;
+        const int Xc = X == S.goal_slot ? S.goal_cell : X;  // node.current
+        const double k_old = xc.k;
+        // delete (:250-259): CLOSED if OPEN, drop the first entry
+        {
+            uint32_t tg = tag_of(xc.cnt_t);
+            if (tg == T_OPEN) tg = T_CLOSED;
+            const int e = xc.first;
+            xc.first = S.nxt[e];
+            xc.cnt_t = (tg << 24) | (cnt_of(xc.cnt_t) - 1u);
+            if (cnt_of(xc.cnt_t) == 0) xc.last = -1;
+            S.open -= 1;
+        }
+        // ---- neighbours (getNeighbor, :276-291): lanes 0..7 in motion order ----
+        const int x = Xc / H, y = Xc % H;
+        const int nx = x + mdx, ny = y + mdy;
+        bool nb = false;
+        DCell yc;
+        yc.h = yc.k = 0.0;
+        yc.first = yc.last = yc.parent = -1;
+        yc.cnt_t = 0;
+        int Y = 0;
+        if (lane < 8) {
+            bool coll = occ2(occ, W, H, x, y) || occ2(occ, W, H, nx, ny);
+            if (mdx != 0 && mdy != 0) coll = coll || occ2(occ, W, H, x, ny) || occ2(occ, W, H, nx, y);
+            nb = !coll;
+            if (nb) {
+                Y = nx * H + ny;
+                yc = load_cell(S.cells, Y);
+            }
+        }
+        const uint64_t nbm = ballot(nb) & 0xFFull;
+        // RAISE (:177-183): scalar scan in motion order
+        double hX = xc.h;
+        int pX = xc.parent;
+        if (k_old < hX) {
+            for (uint64_t m = nbm; m; m &= m - 1) {
+                const int l = __ffsll((long long)m) - 1;
+                const double hy = rl_f64(yc.h, l);
+                const double c = (l & 1) ? 1.4142135623730951 : 1.0;
+                if (hy <= k_old && hX > hy + c) {
+                    pX = (int)rl_u32((uint32_t)Y, l);
+                    hX = hy + c;
+                }
+            }
+        }
+        // LOWER / else (:185-217): one decision per lane; kind 1 = insert(node_n, h_new), 2 = insert(node, h)
+        int kind = 0;
+        double hnew = 0.0;
+        bool setpar = false;
+        if (nb) {
+            const uint32_t ty = tag_of(yc.cnt_t);
+            const bool par_is_x = yc.parent == Xc;
+            const double hc = hX + mcost;
+            if (k_old == hX) {
+                if (ty == T_NEW || (par_is_x && yc.h != hc) || (!par_is_x && yc.h > hc)) {
+                    kind = 1; hnew = hc; setpar = true;
+                }
+            } else {
+                if (ty == T_NEW || (par_is_x && yc.h != hc)) {
+                    kind = 1; hnew = hc; setpar = true;
+                } else if (!par_is_x && yc.h > hc) {
+                    kind = 2;
+                } else if (!par_is_x && hX > yc.h + mcost && ty == T_CLOSED && yc.h > k_old) {
+                    kind = 1; hnew = yc.h;
+                }
+            }
+        }
+        const uint64_t insm = ballot(kind != 0);
+        const int nins = __popcll(insm);
+        if (S.ne + nins > S.entry_cap) return PS_OVER;
+        const int myE = S.ne + __popcll(insm & ((1ull << lane) - 1ull));
+        // insert(node_n, h_new) (:236-248) for lanes of kind 1 (distinct cells, independent)
+        if (kind == 1) {
+            const uint32_t ty = tag_of(yc.cnt_t);
+            if (ty == T_NEW) yc.k = hnew;
+            else if (ty == T_OPEN) yc.k = fmin(yc.k, hnew);
+            else yc.k = fmin(yc.h, hnew);
+            yc.h = hnew;
+            if (setpar) yc.parent = Xc;
+            const uint32_t cnt = cnt_of(yc.cnt_t);
+            if (cnt == 0) yc.first = myE;
+            else S.nxt[yc.last] = myE;
+            S.nxt[myE] = -1;
+            yc.last = myE;
+            yc.cnt_t = (T_OPEN << 24) | (cnt + 1u);
+            store_cell(S.cells, Y, yc);
+        }
+        // insert(node, node.h) for lanes of kind 2, in lane order (node is CLOSED here, so
+        // k = min(h, h) = h the first time and min(k, h) = h after)
+        const uint64_t xm = ballot(kind == 2);
+        if (xm) {
+            if (lane == 0) {
+                uint32_t cnt = cnt_of(xc.cnt_t);
+                for (uint64_t m = xm; m; m &= m - 1) {
+                    const int l = __ffsll((long long)m) - 1;
+                    const int e = S.ne + __popcll(insm & ((1ull << l) - 1ull));
+                    if (cnt == 0) xc.first = e;
+                    else S.nxt[xc.last] = e;
+                    S.nxt[e] = -1;
+                    xc.last = e;
+                    cnt++;
+                }
+                xc.cnt_t = (T_OPEN << 24) | cnt;
+            }
+            xc.first = (int32_t)rl_u32((uint32_t)xc.first, 0);
+            xc.last = (int32_t)rl_u32((uint32_t)xc.last, 0);
+            xc.cnt_t = rl_u32(xc.cnt_t, 0);
+            xc.k = hX;
+        }
+        xc.h = hX;
+        xc.parent = pX;
+        if (lane == 0) store_cell(S.cells, X, xc);
+        S.ne += nins;
+        S.open += nins;
+        heap16::wsync();
+        // heap pushes: every re-keyed cell (stale elements are skipped on pop)
+        for (uint64_t pm = ballot(kind == 1); pm && !S.overflow; pm &= pm - 1) {
+            const int l = __ffsll((long long)pm) - 1;
+            Ent it;
+            it.g = rl_f64(yc.k, l);
+            it.a = rl_u32((uint32_t)yc.first, l);
+            it.b = rl_u32((uint32_t)Y, l);
+            push(it);
+        }
+        if (!S.overflow && cnt_of(xc.cnt_t) > 0) {
+            Ent it;
+            it.g = xc.k;
+            it.a = (uint32_t)xc.first;
+            it.b = (uint32_t)X;
+            push(it);
+        }
+        if (S.overflow) return PS_OVER;
+        // start.t after this processState
+        if (X == S.start) S.start_closed = tag_of(xc.cnt_t) == T_CLOSED;
+        if (ballot(kind == 1 && Y == S.start)) S.start_closed = false;
+        return S.open == 0 ? PS_EMPTIED : PS_DONE;
+    }
+};
+
+__device__ __forceinline__ bool coll2(const uint32_t* occ, int W, int H, int a, int b)
+{
+    const int x1 = a / H, y1 = a % H, x2 = b / H, y2 = b % H;
+    bool c = occ2(occ, W, H, x1, y1) || occ2(occ, W, H, x2, y2);
+    if (x1 != x2 && y1 != y2) c = c || occ2(occ, W, H, x1, y2) || occ2(occ, W, H, x2, y1);
+    return c;
+}
+
+// GraphSearcher.cost (graph_search.py:46-59): inf on collision, else Planner.dist of neighbours
+__device__ __forceinline__ double cost2(const uint32_t* occ, int W, int H, int a, int b)
+{
+    if (coll2(occ, W, H, a, b)) return __builtin_inf();
+    return (a / H != b / H && a % H != b % H) ? 1.4142135623730951 : 1.0;
+}
+
+// DStar.plan (:75-89) and then npress OnPress(x, y) calls (:102-134) per query.  Round r (0 = plan)
+// writes cost / path / len(EXPAND) / status at [q][r]; presses at [q][npress][2].
+__global__ __launch_bounds__(64) void dstar_kernel(const uint32_t* __restrict__ occ_in, int W, int H,
                                                    const int32_t* __restrict__ start_xy, const int32_t* __restrict__ goal_xy,
-                                                   int nq, double* __restrict__ cost_out, int32_t* __restrict__ path_len_out,
+                                                   int nq, const int32_t* __restrict__ presses, int npress,
+                                                   double* __restrict__ cost_out, int32_t* __restrict__ path_len_out,
                                                    int32_t* __restrict__ path_out, int path_cap,
                                                    int64_t* __restrict__ nproc_out, int32_t* __restrict__ status_out,
                                                    int64_t max_process, int* __restrict__ queue, uint4* __restrict__ spill_all,
                                                    int heap_cap, int lds_cap, DCell* __restrict__ cells_all,
-                                                   int32_t* __restrict__ next_all, int entry_cap)
+                                                   int32_t* __restrict__ next_all, int entry_cap, uint32_t* __restrict__ occw_all)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
     const int worker = blockIdx.x;
     const int ncell = W * H;
+    const int words = (ncell + 31) / 32;
     const size_t spill_n = (size_t)(heap_cap > lds_cap ? heap_cap - lds_cap : 0);
-    const heap16::Heap hp = heap16::make_heap(smem, lds_cap, spill_all + (size_t)worker * spill_n, spill_n);
-    DCell* cells = cells_all + (size_t)worker * ncell;
-    int32_t* nxt = next_all + (size_t)worker * entry_cap;
-    int pop_jl, pop_ol;
-    heap16::pop_lane_consts(lane, pop_jl, pop_ol);
-    const KeyD key;
-    const int mdx = c_dmx[lane & 7], mdy = c_dmy[lane & 7];
-    const double mcost = (lane & 1) ? 1.4142135623730951 : 1.0;  // Planner.dist = hypot(1, 1) / hypot(1, 0)
+    Search2 S;
+    S.hp = heap16::make_heap(smem, lds_cap, spill_all + (size_t)worker * spill_n, spill_n);
+    S.cells = cells_all + (size_t)worker * (size_t)(ncell + 1);
+    S.nxt = next_all + (size_t)worker * entry_cap;
+    S.heap_cap = heap_cap;
+    S.lds_cap = lds_cap;
+    S.entry_cap = entry_cap;
+    uint32_t* occw = npress > 0 ? occw_all + (size_t)worker * (size_t)words : nullptr;
+    D2 d{npress > 0 ? (const uint32_t*)occw : occ_in, W, H, S, lane, 0, 0, c_dmx[lane & 7], c_dmy[lane & 7],
+         (lane & 1) ? 1.4142135623730951 : 1.0, KeyD()};  // Planner.dist = hypot(1, 1) / hypot(1, 0)
+    heap16::pop_lane_consts(lane, d.pop_jl, d.pop_ol);
+    const int R1 = npress + 1;
 
     for (;;) {
-        const int qi = next_query(queue, lane);
-        if (qi >= nq) break;
-        const int q = qi;
-        const int sx = start_xy[2 * q], sy = start_xy[2 * q + 1];
-        const int gx = goal_xy[2 * q], gy = goal_xy[2 * q + 1];
+        const int q = next_query(queue, lane);
+        if (q >= nq) break;
+        const int sx = uni(start_xy[2 * q]), sy = uni(start_xy[2 * q + 1]);
+        const int gx = uni(goal_xy[2 * q]), gy = uni(goal_xy[2 * q + 1]);
         if ((unsigned)sx >= (unsigned)W || (unsigned)sy >= (unsigned)H || (unsigned)gx >= (unsigned)W ||
             (unsigned)gy >= (unsigned)H) {
             // every lane stores the same values (no lane-0 block before the continue)
-            status_out[q] = PMP_REF_RAISES; cost_out[q] = 0.0; path_len_out[q] = 0; nproc_out[q] = 0;
+            for (int r = 0; r < R1; r++) {
+                status_out[(size_t)q * R1 + r] = r == 0 ? PMP_REF_RAISES : -1;
+                cost_out[(size_t)q * R1 + r] = 0.0;
+                path_len_out[(size_t)q * R1 + r] = 0;
+                nproc_out[(size_t)q * R1 + r] = 0;
+            }
             continue;
+        }
+        if (occw) {
+            for (int w = lane; w < words; w += 64) occw[w] = occ_in[w];
         }
         const int start = sx * H + sy, goal = gx * H + gy;
         // DStar.__init__ (:55-70): every cell NEW with h = k = inf, goal h = 0, insert(goal, 0)
@@ -124,242 +405,113 @@ __global__ __launch_bounds__(64) void dstar_kernel(const uint32_t* __restrict__ 
             v.k = __builtin_inf();
             v.first = v.last = v.parent = -1;
             v.cnt_t = T_NEW << 24;
-            for (int c = lane; c < ncell; c += 64) store_cell(cells, c, v);
+            for (int c = lane; c <= ncell; c += 64) store_cell(S.cells, c, v);
             heap16::wsync();
             if (lane == 0) {
                 v.h = 0.0;
-                v.k = 0.0;
-                v.first = v.last = 0;
-                v.cnt_t = (T_OPEN << 24) | 1u;
-                store_cell(cells, goal, v);
-                nxt[0] = -1;
+                store_cell(S.cells, start == goal ? ncell : goal, v);
             }
-        }
-        Ent root;
-        root.g = 0.0;
-        root.a = 0u;
-        root.b = (uint32_t)goal;
-        key.derive(root);
-        if (lane == 0) heap16::store<true>(hp, 0, root);
-        heap16::wsync();
-        int n = 1;               // heap elements (valid + stale)
-        int64_t open_total = 1;  // len(OPEN)
-        int ne = 1;              // entries appended so far (list positions)
-        int64_t np = 0;
-        int st = PMP_FOUND;
-        bool start_closed = false;
-
-        for (;;) {
-            // ---- min_state: pop until an element matches its cell's (k, first) ----
-            Ent top;
-            DCell xc;
-            for (;;) {
-                top = root;
-                n -= 1;
-                if (n > 0) {
-                    if (n < lds_cap) heap16::pop<KeyD, false>(hp, key, n, root, lane, pop_jl, pop_ol);
-                    else heap16::pop<KeyD, true>(hp, key, n, root, lane, pop_jl, pop_ol);
-                }
-                xc = load_cell(cells, (int)top.b);
-                if (cnt_of(xc.cnt_t) > 0 && (uint32_t)xc.first == top.a && xc.k == top.g) break;
-                if (n == 0) { st = PMP_CAP_OVERFLOW; break; }  // cannot happen while open_total > 0
-            }
-            if (st != PMP_FOUND) break;
-            np++;
-            const int X = (int)top.b;
-            const double k_old = xc.k;
-            // delete (:250-259): CLOSED if OPEN, drop the first entry
-            {
-                uint32_t tg = tag_of(xc.cnt_t);
-                if (tg == T_OPEN) tg = T_CLOSED;
-                const int e = xc.first;
-                xc.first = nxt[e];
-                xc.cnt_t = (tg << 24) | (cnt_of(xc.cnt_t) - 1u);
-                if (cnt_of(xc.cnt_t) == 0) xc.last = -1;
-                open_total -= 1;
-            }
-            // ---- neighbours (getNeighbor, :276-291): lanes 0..7 in motion order ----
-            const int x = X / H, y = X % H;
-            const int nx = x + mdx, ny = y + mdy;
-            bool nb = false;
-            DCell yc;
-            yc.h = yc.k = 0.0;
-            yc.first = yc.last = yc.parent = -1;
-            yc.cnt_t = 0;
-            int Y = 0;
-            if (lane < 8) {
-                bool coll = occ2(occ, W, H, x, y) || occ2(occ, W, H, nx, ny);
-                if (mdx != 0 && mdy != 0) coll = coll || occ2(occ, W, H, x, ny) || occ2(occ, W, H, nx, y);
-                nb = !coll;
-                if (nb) {
-                    Y = nx * H + ny;
-                    yc = load_cell(cells, Y);
-                }
-            }
-            const uint64_t nbm = ballot(nb) & 0xFFull;
-            // RAISE (:177-183): scalar scan in motion order
-            double hX = xc.h;
-            int pX = xc.parent;
-            if (k_old < hX) {
-                for (uint64_t m = nbm; m; m &= m - 1) {
-                    const int l = __ffsll((long long)m) - 1;
-                    const double hy = rl_f64(yc.h, l);
-                    const double c = (l & 1) ? 1.4142135623730951 : 1.0;
-                    if (hy <= k_old && hX > hy + c) {
-                        pX = (int)rl_u32((uint32_t)Y, l);
-                        hX = hy + c;
-                    }
-                }
-            }
-            // LOWER / else (:185-217): one decision per lane; kind 1 = insert(node_n, h_new), 2 = insert(node, h)
-            int kind = 0;
-            double hnew = 0.0;
-            bool setpar = false;
-            if (nb) {
-                const uint32_t ty = tag_of(yc.cnt_t);
-                const bool par_is_x = yc.parent == X;
-                const double hc = hX + mcost;
-                if (k_old == hX) {
-                    if (ty == T_NEW || (par_is_x && yc.h != hc) || (!par_is_x && yc.h > hc)) {
-                        kind = 1; hnew = hc; setpar = true;
-                    }
-                } else {
-                    if (ty == T_NEW || (par_is_x && yc.h != hc)) {
-                        kind = 1; hnew = hc; setpar = true;
-                    } else if (!par_is_x && yc.h > hc) {
-                        kind = 2;
-                    } else if (!par_is_x && hX > yc.h + mcost && ty == T_CLOSED && yc.h > k_old) {
-                        kind = 1; hnew = yc.h;
-                    }
-                }
-            }
-            const uint64_t insm = ballot(kind != 0);
-            const int nins = __popcll(insm);
-            if (ne + nins > entry_cap) { st = PMP_CAP_OVERFLOW; break; }
-            const int myE = ne + __popcll(insm & ((1ull << lane) - 1ull));
-            // insert(node_n, h_new) (:236-248) for lanes of kind 1 (distinct cells, independent)
-            if (kind == 1) {
-                const uint32_t ty = tag_of(yc.cnt_t);
-                if (ty == T_NEW) yc.k = hnew;
-                else if (ty == T_OPEN) yc.k = fmin(yc.k, hnew);
-                else yc.k = fmin(yc.h, hnew);
-                yc.h = hnew;
-                if (setpar) yc.parent = X;
-                const uint32_t cnt = cnt_of(yc.cnt_t);
-                if (cnt == 0) yc.first = myE;
-                else nxt[yc.last] = myE;
-                nxt[myE] = -1;
-                yc.last = myE;
-                yc.cnt_t = (T_OPEN << 24) | (cnt + 1u);
-                store_cell(cells, Y, yc);
-            }
-            // insert(node, node.h) for lanes of kind 2, in lane order (node is CLOSED here, so
-            // k = min(h, h) = h the first time and min(k, h) = h after)
-            const uint64_t xm = ballot(kind == 2);
-            if (xm) {
-                if (lane == 0) {
-                    uint32_t cnt = cnt_of(xc.cnt_t);
-                    for (uint64_t m = xm; m; m &= m - 1) {
-                        const int l = __ffsll((long long)m) - 1;
-                        const int e = ne + __popcll(insm & ((1ull << l) - 1ull));
-                        if (cnt == 0) xc.first = e;
-                        else nxt[xc.last] = e;
-                        nxt[e] = -1;
-                        xc.last = e;
-                        cnt++;
-                    }
-                    xc.cnt_t = (T_OPEN << 24) | cnt;
-                }
-                xc.first = (int32_t)rl_u32((uint32_t)xc.first, 0);
-                xc.last = (int32_t)rl_u32((uint32_t)xc.last, 0);
-                xc.cnt_t = rl_u32(xc.cnt_t, 0);
-                xc.k = hX;
-            }
-            xc.h = hX;
-            xc.parent = pX;
-            if (lane == 0) store_cell(cells, X, xc);
-            ne += nins;
-            open_total += nins;
             heap16::wsync();
-            // heap pushes: every re-keyed cell (stale elements are skipped on pop)
-            uint64_t pm = ballot(kind == 1);
-            bool overflow = false;
-            while (pm) {
-                const int l = __ffsll((long long)pm) - 1;
-                pm &= pm - 1;
-                if (n >= heap_cap) { overflow = true; break; }
-                Ent it;
-                it.g = rl_f64(yc.k, l);
-                it.a = rl_u32((uint32_t)yc.first, l);
-                it.b = rl_u32((uint32_t)Y, l);
-                key.derive(it);
-                if (n == 0) {
-                    if (lane == 0) heap16::store<true>(hp, 0, it);
-                    root = it;
-                    heap16::wsync();
-                } else if (n < lds_cap) {
-                    heap16::push<KeyD, false>(hp, key, n, it, root, lane);
-                } else {
-                    heap16::push<KeyD, true>(hp, key, n, it, root, lane);
-                }
-                n += 1;
-            }
-            if (!overflow && cnt_of(xc.cnt_t) > 0) {
-                if (n >= heap_cap) {
-                    overflow = true;
-                } else {
-                    Ent it;
-                    it.g = xc.k;
-                    it.a = (uint32_t)xc.first;
-                    it.b = (uint32_t)X;
-                    key.derive(it);
-                    if (n == 0) {
-                        if (lane == 0) heap16::store<true>(hp, 0, it);
-                        root = it;
-                        heap16::wsync();
-                    } else if (n < lds_cap) {
-                        heap16::push<KeyD, false>(hp, key, n, it, root, lane);
-                    } else {
-                        heap16::push<KeyD, true>(hp, key, n, it, root, lane);
-                    }
-                    n += 1;
-                }
-            }
-            if (overflow) { st = PMP_CAP_OVERFLOW; break; }
-            // start.t after this processState
-            if (X == start) start_closed = tag_of(xc.cnt_t) == T_CLOSED;
-            if (ballot(kind == 1 && Y == start)) start_closed = false;
-            if (open_total == 0) { st = PMP_REF_RAISES; break; }  // return self.min_k on an empty OPEN
-            if (start_closed) break;
-            if (max_process > 0 && np >= max_process) { st = PMP_CAP_OVERFLOW; break; }
         }
-        heap16::wsync();
-        if (lane == 0) {
-            int plen = 0;
+        S.n = 0;
+        S.open = 0;
+        S.ne = 0;
+        S.np = 0;
+        S.start = start;
+        S.goal_cell = goal;
+        S.goal_slot = start == goal ? ncell : goal;
+        S.start_closed = false;
+        S.overflow = false;
+        d.insert_uniform(S.goal_slot, 0.0);
+        // ---- plan(): processState until the start is CLOSED (:84-87)
+        int st = PMP_FOUND;
+        for (;;) {
+            const int ps = d.process_state();
+            if (ps == PS_OVER) { st = PMP_CAP_OVERFLOW; break; }
+            if (ps != PS_DONE) { st = PMP_REF_RAISES; break; }  // min_k of an empty OPEN (:234)
+            if (S.start_closed) break;
+            if (max_process > 0 && S.np >= max_process) { st = PMP_CAP_OVERFLOW; break; }
+        }
+        for (int r = 0; r <= npress; r++) {
+            int rst = st;
             double cost = 0.0;
-            if (st == PMP_FOUND) {
-                // extractPath (:136-156): start -> goal through parents, cost via GraphSearcher.cost
-                int32_t* pth = path_out + (size_t)q * path_cap;
-                int c = start;
-                pth[0] = c;
-                plen = 1;
-                while (c != goal) {
-                    const int p = load_cell(cells, c).parent;
-                    if (p < 0 || plen > ncell) { st = PMP_REF_RAISES; break; }
-                    const int cx = c / H, cy = c % H, px = p / H, py = p % H;
-                    bool coll = occ2(occ, W, H, cx, cy) || occ2(occ, W, H, px, py);
-                    if (cx != px && cy != py) coll = coll || occ2(occ, W, H, cx, py) || occ2(occ, W, H, px, cy);
-                    cost += coll ? __builtin_inf() : ((cx != px && cy != py) ? 1.4142135623730951 : 1.0);
-                    c = p;
-                    if (plen < path_cap) pth[plen] = c;
-                    plen++;
+            int plen = 0;
+            int32_t* pth = path_out + ((size_t)q * R1 + r) * (size_t)path_cap;
+            if (r == 0) {
+                if (st == PMP_FOUND && lane == 0) {
+                    // extractPath (:136-156): start -> goal through parents, cost via GraphSearcher.cost
+                    int c = start;
+                    pth[0] = c;
+                    plen = 1;
+                    while (c != goal) {
+                        const int p = load_cell(S.cells, c).parent;
+                        if (p < 0 || plen > ncell) { rst = PMP_REF_RAISES; break; }
+                        cost += cost2(d.occ, W, H, c, p);
+                        c = p;
+                        if (plen < path_cap) pth[plen] = c;
+                        plen++;
+                    }
+                    if (rst == PMP_FOUND && plen > path_cap) rst = PMP_PATH_OVERFLOW;
                 }
-                if (st == PMP_FOUND && plen > path_cap) st = PMP_PATH_OVERFLOW;
+                rst = uni(rst);
+            } else if (st != PMP_FOUND) {
+                rst = -1;  // not run: an earlier call raised or hit a cap
+            } else {
+                // OnPress(x, y) (:102-134) without the figure
+                const int px = uni(presses[((size_t)q * npress + (r - 1)) * 2]);
+                const int py = uni(presses[((size_t)q * npress + (r - 1)) * 2 + 1]);
+                if (px < 0 || px > W - 1 || py < 0 || py > H - 1 || occ2(d.occ, W, H, px, py)) {
+                    rst = PMP_NO_PATH;  // "Please choose right area!" / already an obstacle: nothing happens
+                } else {
+                    heap16::wsync();
+                    if (lane == 0) {
+                        const uint32_t c = (uint32_t)(px * H + py);
+                        occw[c >> 5] |= 1u << (c & 31);
+                    }
+                    heap16::wsync();
+                    S.np = 0;  // self.EXPAND = []
+                    int node = start;
+                    const int64_t bound = 4 * (int64_t)ncell + 4;
+                    int64_t steps = 0;
+                    while (node != goal) {
+                        if (++steps > bound) { rst = PMP_CAP_OVERFLOW; break; }
+                        const int p = load_cell(S.cells, node).parent;
+                        if (p < 0) { rst = PMP_REF_RAISES; plen = -1; break; }  // self.map[None]: KeyError
+                        if (coll2(d.occ, W, H, node, p)) {
+                            // modify(node, node_parent) (:262-274): cost is inf (they collide)
+                            if (tag_of(load_cell(S.cells, node).cnt_t) == T_CLOSED)
+                                d.insert_uniform(node, load_cell(S.cells, p).h + __builtin_inf());
+                            for (;;) {
+                                const int ps = S.overflow ? PS_OVER : d.process_state();
+                                if (ps == PS_OVER) { rst = PMP_CAP_OVERFLOW; break; }
+                                if (ps == PS_EMPTIED) { rst = PMP_REF_RAISES; break; }
+                                // an OPEN empty on entry makes processState return -1 forever: the
+                                // reference's loop never ends
+                                if (ps == PS_EMPTY) { rst = PMP_CAP_OVERFLOW; break; }
+                                if (max_process > 0 && S.np >= max_process) { rst = PMP_CAP_OVERFLOW; break; }
+                                // k_min >= node.h
+                                d.clean_top();
+                                if (S.root.g >= load_cell(S.cells, node).h) break;
+                            }
+                            if (rst != PMP_FOUND) break;
+                            continue;
+                        }
+                        if (lane == 0 && plen < path_cap) pth[plen] = node;
+                        plen++;
+                        cost += cost2(d.occ, W, H, node, p);
+                        node = p;
+                    }
+                    if (rst == PMP_FOUND && plen > path_cap) rst = PMP_PATH_OVERFLOW;
+                    plen = uni(plen);
+                }
+                if (rst == PMP_REF_RAISES || rst == PMP_CAP_OVERFLOW) st = rst;
             }
-            status_out[q] = st;
-            cost_out[q] = cost;
-            path_len_out[q] = plen;
-            nproc_out[q] = np;
+            if (lane == 0) {
+                status_out[(size_t)q * R1 + r] = rst;
+                cost_out[(size_t)q * R1 + r] = cost;
+                path_len_out[(size_t)q * R1 + r] = plen;
+                nproc_out[(size_t)q * R1 + r] = rst == -1 ? 0 : S.np;  // a no-op press keeps EXPAND
+            }
         }
         heap16::wsync();
     }
@@ -367,20 +519,22 @@ __global__ __launch_bounds__(64) void dstar_kernel(const uint32_t* __restrict__ 
 
 }  // namespace
 
-extern "C" int pmp_dstar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H,
-                                 const int32_t* start_xy, const int32_t* goal_xy, int nq, double* cost,
-                                 int32_t* path_len, int32_t* path, int path_cap, int64_t* n_process, int32_t* status,
-                                 int64_t max_process)
+extern "C" int pmp_dstar2d_onpress_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H,
+                                         const int32_t* start_xy, const int32_t* goal_xy, int nq, const int32_t* presses,
+                                         int npress, double* cost, int32_t* path_len, int32_t* path, int path_cap,
+                                         int64_t* n_process, int32_t* status, int64_t max_process)
 {
     if (!ctx) return PMP_EINVAL;
     if (W < 1 || H < 1 || (int64_t)W * H > (1 << 26))
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_dstar2d_batch: W*H must be in [1, 2^26]");
-    if (nq < 0 || path_cap < 1) return pmp_set_err(ctx, PMP_EINVAL, "pmp_dstar2d_batch: bad nq/path_cap");
+    if (nq < 0 || path_cap < 1 || npress < 0 || (npress > 0 && !presses))
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_dstar2d_batch: bad nq/path_cap/npress/presses");
     if (nq == 0) return PMP_OK;
     if (!occ_bits || !start_xy || !goal_xy || !cost || !path_len || !path || !n_process || !status)
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_dstar2d_batch: null pointer argument");
     PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     const size_t ncell = (size_t)W * H;
+    const size_t words = (ncell + 31) / 32;
     // per worker: 32 B cell state + 4 entries (16 B) + 4 heap elements (64 B) per cell, over the LDS part
     const size_t hc = 4 * ncell + 64;
     const int heap_cap = (int)(hc > (size_t)(1 << 26) ? (size_t)(1 << 26) : hc);
@@ -389,21 +543,32 @@ extern "C" int pmp_dstar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
     int lds_cap = (((160 * 1024) / per_cu - 256) / 16) & ~15;
     if (lds_cap > heap_cap) lds_cap = (heap_cap + 15) & ~15;
     const size_t spill_n = heap_cap > lds_cap ? (size_t)(heap_cap - lds_cap) : 0;
-    const size_t per_worker = ncell * sizeof(DCell) + (size_t)entry_cap * 4 + spill_n * 16 + 4096;
+    const size_t per_worker = (ncell + 1) * sizeof(DCell) + (size_t)entry_cap * 4 + spill_n * 16 + 4096 +
+                              (npress > 0 ? words * 4 : 0);
     int workers = 256 * per_cu;
     const size_t max_workers = ((size_t)16 << 30) / per_worker;  // keep the scratch under 16 GiB
     if ((size_t)workers > max_workers) workers = (int)(max_workers > 0 ? max_workers : 1);
     if (workers > nq) workers = nq;
     uint4* spill = (uint4*)pmp_scratch(ctx, SCR_AUX1, (size_t)workers * spill_n * 16 + 16);
-    DCell* cells = (DCell*)pmp_scratch(ctx, SCR_AUX2, (size_t)workers * ncell * sizeof(DCell) + 16);
+    DCell* cells = (DCell*)pmp_scratch(ctx, SCR_AUX2, (size_t)workers * (ncell + 1) * sizeof(DCell) + 16);
     int32_t* nxt = (int32_t*)pmp_scratch(ctx, SCR_AUX3, (size_t)workers * entry_cap * 4 + 16);
     int* queue = (int*)pmp_scratch(ctx, SCR_AUX0, 256);
-    if (!spill || !cells || !nxt || !queue) return PMP_ENOMEM;
+    uint32_t* occw = npress > 0 ? (uint32_t*)pmp_scratch(ctx, SCR_AUX4, (size_t)workers * words * 4 + 16) : nullptr;
+    if (!spill || !cells || !nxt || !queue || (npress > 0 && !occw)) return PMP_ENOMEM;
     hipStream_t s = (hipStream_t)stream;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
     hipLaunchKernelGGL(dstar_kernel, dim3(workers), dim3(64), (size_t)lds_cap * 16, s, occ_bits, W, H, start_xy, goal_xy,
-                       nq, cost, path_len, path, path_cap, n_process, status, max_process, queue, spill, heap_cap, lds_cap,
-                       cells, nxt, entry_cap);
+                       nq, presses, npress, cost, path_len, path, path_cap, n_process, status, max_process, queue, spill,
+                       heap_cap, lds_cap, cells, nxt, entry_cap, occw);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
+}
+
+extern "C" int pmp_dstar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H,
+                                 const int32_t* start_xy, const int32_t* goal_xy, int nq, double* cost,
+                                 int32_t* path_len, int32_t* path, int path_cap, int64_t* n_process, int32_t* status,
+                                 int64_t max_process)
+{
+    return pmp_dstar2d_onpress_batch(ctx, stream, occ_bits, W, H, start_xy, goal_xy, nq, nullptr, 0, cost, path_len, path,
+                                     path_cap, n_process, status, max_process);
 }

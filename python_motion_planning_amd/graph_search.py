@@ -231,6 +231,7 @@ class DStar(GraphSearcher):
         """(cost, path start->goal, None) (d_star.py:75-89); raises AttributeError when the start is
         unreachable, like the reference (min_k of an empty OPEN, :234)."""
         occ = self.env.occupancy()
+        self._occ0, self._presses = occ, []
         W, H = occ.shape
         r = batch.dstar2d_batch(occ, np.array([self.start.current]), np.array([self.goal.current]))
         st = int(r["status"][0])
@@ -245,9 +246,47 @@ class DStar(GraphSearcher):
     def run(self):
         return self.plan()
 
+    def OnPress(self, event) -> None:
+        """Mouse callback (d_star.py:102-134) without the figure: a press on a free in-grid cell adds
+        the obstacle and repairs the plan from the start's back-pointer chain; the walk's cost and
+        path (which stops before the goal, as the reference's) are kept in self.cost / self.path and
+        len(self.EXPAND) is the processState count of that repair.  The kernel is stateless, so the
+        plan and every earlier press are replayed on the device."""
+        x, y = int(event.xdata), int(event.ydata)
+        if x < 0 or x > self.env.x_range - 1 or y < 0 or y > self.env.y_range - 1:
+            print("Please choose right area!")
+            return
+        if (x, y) in self.obstacles:
+            return
+        print("Add obstacle at: ({}, {})".format(x, y))
+        if not hasattr(self, "_occ0"):
+            self._occ0, self._presses = self.env.occupancy(), []
+        self.obstacles.add((x, y))
+        self.env.update(self.obstacles)
+        self._presses.append((x, y))
+        W, H = self._occ0.shape
+        r = batch.dstar2d_onpress_batch(self._occ0, np.array([self.start.current]), np.array([self.goal.current]),
+                                        np.array([self._presses], np.int32))
+        k = len(self._presses)
+        st = int(r["status"][0, k])
+        if st == 4:
+            if int(r["path_len"][0, k]) < 0:
+                raise KeyError(None)  # self.map[node.parent] of a parentless node
+            raise AttributeError("'NoneType' object has no attribute 'k'")  # min_k of an emptied OPEN
+        if st not in (0, 1):
+            raise RuntimeError(f"D* kernel status {st} (a walk or repair the reference never finishes)")
+        n = int(r["path_len"][0, k])
+        self.cost = float(r["cost"][0, k])
+        self.path = [(int(c) // H, int(c) % H) for c in r["path"][0, k, :n].cpu().numpy()]
+        self.EXPAND = [None] * int(r["n_process"][0, k])
+
     @staticmethod
     def plan_batch(occ: np.ndarray, starts, goals, **kw):
         return batch.dstar2d_batch(occ, starts, goals, **kw)
+
+    @staticmethod
+    def onpress_batch(occ: np.ndarray, starts, goals, presses, **kw):
+        return batch.dstar2d_onpress_batch(occ, starts, goals, presses, **kw)
 
 
 class GraphSearcher3D:
@@ -354,3 +393,93 @@ class LazyThetaStar3D(AStar3D):
 
     def __str__(self) -> str:
         return "Lazy Theta* 3D"
+
+
+class DNode3D:
+    """D* bookkeeping node of DStar3D (d_star3d.py:21-57): coordinates in `current`, parent
+    coordinates, tag t, h and k.  Equality and hashing by coordinates (Node3D, node3d.py:43-57)."""
+
+    __slots__ = ("current", "parent", "t", "h", "k")
+
+    def __init__(self, current, parent, t, h, k) -> None:
+        self.current, self.parent, self.t, self.h, self.k = current, parent, t, h, k
+
+    def __eq__(self, other) -> bool:
+        return isinstance(other, DNode3D) and self.current == other.current
+
+    def __hash__(self) -> int:
+        return hash(self.current)
+
+    def __repr__(self) -> str:
+        return f"DNode3D(current={self.current}, parent={self.parent}, t={self.t}, h={self.h}, k={self.k})"
+
+
+class DStar3D(GraphSearcher3D):
+    """Dynamic A* in 3D voxel grids (d_star3d.py:60-281).  plan() and apply_dynamic_obstacles() run
+    in the gfx950 kernel dstar3d.hip with the reference's list-semantics OPEN.  The kernel is
+    stateless, so the planner keeps the history of blocked-voxel batches and every call replays the
+    plan and the earlier rounds on the device (the reference's in-place state is a function of that
+    history)."""
+
+    def __init__(self, start: tuple, goal: tuple, env) -> None:
+        super().__init__(start, goal, env, None)
+        self._rounds = []
+        self.EXPAND = []
+        self._occ0 = None
+
+    def __str__(self) -> str:
+        return "Dynamic A* (D*) 3D"
+
+    def _run(self, want_expand: bool):
+        occ = self._occ0
+        X, Y, Z = occ.shape
+        nb = max((len(r) for r in self._rounds), default=0)
+        blocks = None
+        if self._rounds:
+            blocks = np.full((1, len(self._rounds), max(nb, 1), 3), -1, np.int32)
+            for i, r in enumerate(self._rounds):
+                if r:
+                    blocks[0, i, : len(r)] = np.asarray(r, np.int32).reshape(-1, 3)
+        r = batch.dstar3d_batch(occ, np.array([self.start.current]), np.array([self.goal.current]), blocks,
+                                path_cap=4 * X * Y * Z + 8, expand_cap=(8 * X * Y * Z + 8) if want_expand else 0)
+        st = r["status"][0].cpu().numpy()
+        if (st >= 2).any():
+            raise RuntimeError(f"{self} kernel status {st.tolist()}")
+        return r
+
+    def _cells(self, r, k):
+        X, Y, Z = r["dims"]
+        n = int(r["path_len"][0, k])
+        return [(int(c) // (Y * Z), (int(c) // Z) % Y, int(c) % Z) for c in r["path"][0, k, :n].cpu().numpy()]
+
+    def plan(self) -> tuple:
+        """(cost, path start->goal, EXPAND) (d_star3d.py:100-109).  An unreachable start gives
+        (0.0, [start], EXPAND), as the reference's extractPath breaks at the parentless start.
+        EXPAND: one DNode3D per processState, `current` set (state fields not materialised)."""
+        self._occ0 = self.env.occupancy()
+        self._rounds = []
+        r = self._run(True)
+        ne = int(r["n_process"][0, 0])
+        X, Y, Z = r["dims"]
+        ex = r["expand"][0, :ne].cpu().numpy()
+        self.EXPAND = [DNode3D((int(c) // (Y * Z), (int(c) // Z) % Y, int(c) % Z), None, None, None, None) for c in ex]
+        return float(r["cost"][0, 0]), self._cells(r, 0), list(self.EXPAND)
+
+    def apply_dynamic_obstacles(self, newly_blocked) -> tuple:
+        """Block the voxels and repair from the start's back-pointer chain (d_star3d.py:115-149).
+        Returns (cost, path); self.EXPAND holds this call's processState count."""
+        if self._occ0 is None:
+            self.plan()
+        blk = [tuple(int(v) for v in t) for t in newly_blocked]
+        for v in blk:
+            self.obstacles.add(v)
+        self.env.update(self.obstacles)
+        self._rounds.append(blk)
+        r = self._run(False)
+        k = len(self._rounds)
+        self.EXPAND = [None] * int(r["n_process"][0, k])
+        return float(r["cost"][0, k]), self._cells(r, k)
+
+    @staticmethod
+    def plan_batch(occ, starts, goals, blocks=None, **kw):
+        return batch.dstar3d_batch(occ, starts, goals, blocks, **kw)

@@ -896,11 +896,198 @@ def sec_lpa_replan(n=60, nt=4, lite=False):
     print("dstarlite_replan" if lite else "lpa_replan", len(res), "cases;", sum(1 for r in res if r["err"][-1]), "raise")
 
 
+# ----------------------------------------------------------------------------------------------
+# DStar3D plan + apply_dynamic_obstacles (d_star3d.py:100-149) -- SURVEY.md §8(f) rank 3
+def run_dstar3d(args):
+    occ, start, goal, rounds = args
+    pmp = import_reference()
+    X, Y, Z = occ.shape
+    env = pmp.Grid3D(X, Y, Z)
+    env.update({(int(a), int(b), int(c)) for a, b, c in np.argwhere(occ)})
+    p = pmp.DStar3D(tuple(start), tuple(goal), env)
+    enc = lambda t: (t[0] * Y + t[1]) * Z + t[2]  # noqa: E731
+    cost, path, expand = p.plan()
+    out = dict(cost=[float(cost)], path=[[enc(t) for t in path]], nexp=[len(expand)])
+    for blk in rounds:
+        cost, path = p.apply_dynamic_obstacles([tuple(int(v) for v in b) for b in blk])
+        out["cost"].append(float(cost))
+        out["path"].append([enc(t) for t in path])
+        out["nexp"].append(len(p.EXPAND))
+    close_figs()
+    return out
+
+
+def sec_dstar3d(n_per=8, nr=3):
+    from python_motion_planning_amd import workloads as wl
+
+    rng = np.random.default_rng(4242)
+    cases = []
+    for name in wl.SCENARIOS_3D:
+        for j in range(n_per):
+            X, Y, Z = (21, 15, 11) if j % 4 else (26, 20, 16)
+            seed = int(rng.integers(1000))
+            s, g = wl.bench3d_query(seed, X, Y, Z)
+            o = wl.SCENARIOS_3D[name](X, Y, Z)
+            wl.carve_safety_bubble(o, s, 2 if X == 21 else 1)
+            wl.carve_safety_bubble(o, g, 2 if X == 21 else 1)
+            inner = np.argwhere(o[1:-1, 1:-1, 1:-1] == 0) + 1
+            rounds = []
+            for _ in range(nr):
+                blk = [inner[rng.integers(len(inner))] for _ in range(3)]
+                rounds.append([[int(v) for v in b] for b in blk])
+            cases.append((o, s, g, rounds))
+    # blocks on the planned path (forces the modify / processState repair): taken from a first plan
+    res = []
+    with Pool(8) as pool:
+        first = pool.map(run_dstar3d, [(c[0], c[1], c[2], []) for c in cases])
+        jobs = []
+        for c, f in zip(cases, first):
+            o, s, g, rounds = c
+            X, Y, Z = o.shape
+            path = f["path"][0]
+            if len(path) > 3:
+                v = path[len(path) // 2]
+                rounds[0][0] = [v // (Y * Z), (v // Z) % Y, v % Z]
+            jobs.append(pool.apply_async(run_dstar3d, (c,)))
+        keep = []
+        for c, j in zip(cases, jobs):
+            try:
+                res.append(j.get(timeout=120))
+                keep.append(c)
+            except Exception as e:  # a walk that never ends in the reference (no step bound there)
+                print("dstar3d case dropped:", type(e).__name__)
+        cases = keep
+    dims = np.array([c[0].shape for c in cases], np.int32)
+    occ_flat, occ_off = ragged([np.packbits(c[0].ravel()) for c in cases], np.uint8)
+    paths = [p for r in res for p in r["path"]]
+    path_flat, path_off = ragged(paths)
+    np.savez_compressed(
+        os.path.join(HERE, "dstar3d_runs.npz"), dims=dims, occ_bits=occ_flat, occ_off=occ_off,
+        start=np.array([c[1] for c in cases], np.int32), goal=np.array([c[2] for c in cases], np.int32),
+        blocks=np.array([c[3] for c in cases], np.int32), cost=np.array([r["cost"] for r in res]),
+        nexp=np.array([r["nexp"] for r in res], np.int64), path=path_flat, path_off=path_off)
+    # the reference's published CSV rows for DStar3D (every 10th row = distinct seeds, 120 inf rows in all)
+    rows = []
+    with open(os.path.join(REF, "3d_pathfinding_results.csv"), newline="") as f:
+        rd = csv.reader(f)
+        next(rd)
+        for k, r in enumerate(rd):
+            if r[1] == "dstar" and k % 10 == 0:
+                rows.append(dict(algo=r[1], scenario=r[0], cost=r[3], visited=int(r[4]),
+                                 start=list(eval(r[5])), goal=list(eval(r[6])), seed=int(r[7])))  # noqa: S307
+    with open(os.path.join(HERE, "dstar3d_csv.json"), "w") as f:
+        json.dump(rows, f)
+    print("dstar3d runs", len(res), "csv rows", len(rows), "inf rounds",
+          sum(1 for r in res for c in r["cost"] if math.isinf(c)))
+
+
+# ----------------------------------------------------------------------------------------------
+# DStar.plan + OnPress(event) (d_star.py:75-134): the reference's own OnPress with a stand-in event
+# and a recording plot (the walk's path / cost are what it hands to plot.animation)
+def run_dstar_onpress(args):
+    occ, start, goal, presses = args
+    pmp = import_reference()
+    import contextlib
+    import io
+
+    W, H = occ.shape
+    env = pmp.Grid(W, H)
+    env.update(obstacles_of(occ))
+    p = pmp.DStar(tuple(start), tuple(goal), env)
+    out = dict(cost=[], path=[], nexp=[], kind=[])
+    try:
+        cost, path, _ = p.plan()
+    except Exception as e:  # noqa: BLE001  unreachable start: AttributeError (d_star.py:234)
+        out["cost"].append(float("nan")); out["path"].append([]); out["nexp"].append(len(p.EXPAND))
+        out["kind"].append(type(e).__name__)
+        close_figs()
+        return out
+    out["cost"].append(float(cost)); out["path"].append([x * H + y for (x, y) in path])
+    out["nexp"].append(len(p.EXPAND)); out["kind"].append("")
+    p.plot = unittest.mock.MagicMock()
+    for (x, y) in presses:
+        ev = types.SimpleNamespace(xdata=float(x) + 0.25, ydata=float(y) + 0.25)
+        p.plot.animation.reset_mock()
+        try:
+            with contextlib.redirect_stdout(io.StringIO()):
+                p.OnPress(ev)
+        except Exception as e:  # noqa: BLE001  KeyError on a parentless node, AttributeError on an emptied OPEN
+            out["cost"].append(float("nan")); out["path"].append([]); out["nexp"].append(len(p.EXPAND))
+            out["kind"].append(type(e).__name__)
+            break
+        if p.plot.animation.called:
+            wpath, _, wcost, _ = p.plot.animation.call_args[0]
+            out["cost"].append(float(wcost)); out["path"].append([x * H + y for (x, y) in wpath])
+            out["nexp"].append(len(p.EXPAND)); out["kind"].append("")
+        else:
+            out["cost"].append(0.0); out["path"].append([]); out["nexp"].append(len(p.EXPAND)); out["kind"].append("noop")
+    close_figs()
+    return out
+
+
+def sec_dstar_onpress(n=48, npress=4):
+    from python_motion_planning_amd import workloads as wl
+
+    rng = np.random.default_rng(31337)
+    cases = []
+    for i in range(n):
+        if i < 6:
+            occ = wl.readme_grid()
+            s, g = ((5, 5), (45, 25)) if i < 3 else tuple(tuple(int(v) for v in np.argwhere(occ == 0)[rng.integers(
+                (occ == 0).sum())]) for _ in range(2))
+        else:
+            W, H = int(rng.integers(10, 41)), int(rng.integers(10, 41))
+            occ = wl.random_grid(W, H, float(rng.uniform(0.0, 0.25)), int(rng.integers(1 << 30)))
+            free = np.argwhere(occ == 0)
+            s = tuple(int(v) for v in free[rng.integers(len(free))])
+            g = tuple(int(v) for v in free[rng.integers(len(free))])
+        cases.append([occ, s, g, None])
+    res = []
+    with Pool(8) as pool:
+        first = pool.map(run_dstar_onpress, [(c[0], c[1], c[2], []) for c in cases])
+        jobs = []
+        for c, f in zip(cases, first):
+            occ, s, g, _ = c
+            W, H = occ.shape
+            path = f["path"][0]
+            pr = []
+            for k in range(npress):
+                if path and k < 2 and len(path) > 4:  # on the planned path: forces the modify / processState repair
+                    v = path[int(rng.integers(1, len(path) - 1))]
+                    pr.append((v // H, v % H))
+                else:  # anywhere (off-path, obstacles and off-grid presses included)
+                    pr.append((int(rng.integers(-1, W + 1)), int(rng.integers(-1, H + 1))))
+            c[3] = pr
+            jobs.append(pool.apply_async(run_dstar_onpress, (tuple(c),)))
+        keep = []
+        for c, j in zip(cases, jobs):
+            try:
+                res.append(j.get(timeout=60))
+                keep.append(c)
+            except Exception as e:  # noqa: BLE001  an OnPress walk that never ends in the reference
+                print("dstar onpress case dropped:", type(e).__name__)
+        cases = keep
+    R = npress + 1
+    pad = lambda v, f: list(v) + [f] * (R - len(v))  # noqa: E731
+    dims = np.array([c[0].shape for c in cases], np.int32)
+    occ_flat, occ_off = ragged([np.packbits(c[0].ravel()) for c in cases], np.uint8)
+    path_flat, path_off = ragged([p for r in res for p in pad(r["path"], [])])
+    np.savez_compressed(
+        os.path.join(HERE, "dstar_onpress.npz"), dims=dims, occ_bits=occ_flat, occ_off=occ_off,
+        start=np.array([c[1] for c in cases], np.int32), goal=np.array([c[2] for c in cases], np.int32),
+        presses=np.array([c[3] for c in cases], np.int32),
+        cost=np.array([pad(r["cost"], float("nan")) for r in res]), nexp=np.array([pad(r["nexp"], -1) for r in res]),
+        kind=np.array([pad(r["kind"], "-") for r in res]), path=path_flat, path_off=path_off)
+    kinds = [k for r in res for k in r["kind"]]
+    print("dstar_onpress", len(res), "cases;", {k: kinds.count(k) for k in set(kinds)})
+
+
 SECTIONS = dict(rrt=sec_rrt, mpc=sec_mpc, dwa=sec_dwa, local_plans=sec_local_plans, lqr=sec_lqr, astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
                 dstar=sec_dstar, astar3d=sec_astar3d,
                 graph2d=sec_graph2d, graph3d=sec_graph3d, theta3d=sec_theta3d, theta2d=sec_theta2d, lpa=sec_lpa,
                 dstarlite=lambda: sec_lpa(lite=True), lpa_replan=sec_lpa_replan,
-                dstarlite_replan=lambda: sec_lpa_replan(lite=True))
+                dstarlite_replan=lambda: sec_lpa_replan(lite=True), dstar3d=sec_dstar3d,
+                dstar_onpress=sec_dstar_onpress)
 
 if __name__ == "__main__":
     want = sys.argv[1:] or list(SECTIONS)

@@ -1,0 +1,126 @@
+"""HIP DStar3D (dstar3d.hip via the C-ABI): plan() and apply_dynamic_obstacles() rounds against the
+reference's published CSV rows, replayed reference runs and the oracle (d_star3d.py:60-281).
+
+Bar: bit-exact -- every round's cost (inf included), len(EXPAND) and path."""
+import math
+
+import numpy as np
+import pytest
+
+from golden_io import grid_cases, load_json, seg
+
+pytestmark = pytest.mark.gpu
+
+
+def _csv_batch(rows):
+    from python_motion_planning_amd import workloads as wl
+
+    occ = np.zeros((len(rows), 21, 15, 11), np.uint8)
+    S = np.zeros((len(rows), 3), np.int32)
+    G = np.zeros((len(rows), 3), np.int32)
+    for i, r in enumerate(rows):
+        s, g = wl.bench3d_query(r["seed"], 21, 15, 11)
+        o = wl.SCENARIOS_3D[r["scenario"]](21, 15, 11)
+        wl.carve_safety_bubble(o, s, 2)
+        wl.carve_safety_bubble(o, g, 2)
+        occ[i], S[i], G[i] = o, s, g
+    return occ, S, G
+
+
+def test_dstar3d_published_csv_rows():
+    """The 500 distinct DStar3D rows of 3d_pathfinding_results.csv (120 of the 5,000 rows are inf)."""
+    from python_motion_planning_amd import batch
+
+    rows = load_json("dstar3d_csv.json")
+    occ, S, G = _csv_batch(rows)
+    out = batch.dstar3d_batch(occ, S, G)
+    cost = out["cost"][:, 0].cpu().numpy()
+    npr = out["n_process"][:, 0].cpu().numpy()
+    n_inf = 0
+    for i, r in enumerate(rows):
+        assert repr(float(cost[i])) == r["cost"], (i, r)
+        assert npr[i] == r["visited"], (i, r)
+        n_inf += math.isinf(cost[i])
+    assert n_inf > 0
+
+
+def _same(a, b):
+    return a == b or (math.isinf(a) and math.isinf(b) and (a > 0) == (b > 0))
+
+
+def test_dstar3d_dynamic_obstacles_against_reference():
+    """39 replayed reference sessions: plan() + 3 apply_dynamic_obstacles() rounds each (the first
+    round blocks a voxel of the planned path), one launch per session."""
+    from python_motion_planning_amd import batch
+
+    n = 0
+    for i, occ, z in grid_cases("dstar3d_runs.npz"):
+        R = z["blocks"].shape[1] + 1
+        out = batch.dstar3d_batch(occ, z["start"][i][None], z["goal"][i][None], z["blocks"][i][None])
+        st = out["status"][0].cpu().numpy()
+        assert (st <= 1).all(), (i, st)
+        for r in range(R):
+            assert _same(float(out["cost"][0, r]), float(z["cost"][i][r])), (i, r)
+            assert int(out["n_process"][0, r]) == z["nexp"][i][r], (i, r)
+            pl = int(out["path_len"][0, r])
+            assert np.array_equal(out["path"][0, r, :pl].cpu().numpy(), seg(z["path"], z["path_off"], i * R + r)), (i, r)
+        n += 1
+    assert n >= 30
+
+
+def test_dstar3d_c5_batch_against_oracle():
+    """C5 shape (26x20x16 door, per-query safety bubbles): 384 queries in one launch, 2 rounds of 4
+    random blocked voxels each, every output against the oracle."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import batch, workloads as wl
+
+    occ, s, g = wl.c5_workload(384)
+    rng = np.random.default_rng(11)
+    X, Y, Z = occ.shape[1:]
+    blocks = np.stack([rng.integers(1, [X - 1, Y - 1, Z - 1], size=(2, 4, 3)) for _ in range(len(s))]).astype(np.int32)
+    out = batch.dstar3d_batch(occ, s, g, blocks, expand_cap=X * Y * Z * 4)
+    cost, npr = out["cost"].cpu().numpy(), out["n_process"].cpu().numpy()
+    st, pl, path = out["status"].cpu().numpy(), out["path_len"].cpu().numpy(), out["path"].cpu().numpy()
+    for q in range(len(s)):
+        ref = O.dstar3d(occ[q], s[q], g[q], blocks[q])
+        for r in range(3):
+            assert st[q, r] == ref["status"][r], (q, r)
+            assert _same(cost[q, r], ref["cost"][r]), (q, r)
+            assert npr[q, r] == ref["n_process"][r], (q, r)
+            assert np.array_equal(path[q, r, : pl[q, r]], ref["paths"][r]), (q, r)
+
+
+def test_dstar3d_dropin_sequence():
+    """The drop-in class: plan() then apply_dynamic_obstacles() calls, as the reference object."""
+    import python_motion_planning_amd as pmp
+
+    for i, occ, z in grid_cases("dstar3d_runs.npz"):
+        if i % 6:
+            continue
+        X, Y, Z = occ.shape
+        env = pmp.Grid3D(X, Y, Z)
+        env.update({(int(a), int(b), int(c)) for a, b, c in np.argwhere(occ)})
+        p = pmp.DStar3D(tuple(int(v) for v in z["start"][i]), tuple(int(v) for v in z["goal"][i]), env)
+        cost, path, expand = p.plan()
+        R = z["blocks"].shape[1] + 1
+        enc = lambda t: (t[0] * Y + t[1]) * Z + t[2]  # noqa: E731
+        assert _same(cost, float(z["cost"][i][0])) and len(expand) == z["nexp"][i][0]
+        assert [enc(t) for t in path] == seg(z["path"], z["path_off"], i * R).tolist()
+        for r in range(1, R):
+            cost, path = p.apply_dynamic_obstacles([tuple(int(v) for v in b) for b in z["blocks"][i][r - 1]])
+            assert _same(cost, float(z["cost"][i][r])) and len(p.EXPAND) == z["nexp"][i][r], (i, r)
+            assert [enc(t) for t in path] == seg(z["path"], z["path_off"], i * R + r).tolist(), (i, r)
+
+
+def test_dstar3d_start_equals_goal_and_off_grid():
+    """start == goal detaches the goal object (d_star3d.py:89-90); endpoints off the grid -> status 4."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import batch, workloads as wl
+
+    occ = wl.SCENARIOS_3D["door"](21, 15, 11)
+    s = np.array([[5, 5, 5], [30, 5, 5]], np.int32)
+    g = np.array([[5, 5, 5], [3, 3, 3]], np.int32)
+    out = batch.dstar3d_batch(occ, s, g)
+    ref = O.dstar3d(occ, s[0], g[0])
+    assert int(out["n_process"][0, 0]) == ref["n_process"][0] and float(out["cost"][0, 0]) == ref["cost"][0]
+    assert int(out["status"][1, 0]) == 4

@@ -62,3 +62,103 @@ def test_dstar_dropin_readme():
     o = O.dstar2d(wl.readme_grid(), (5, 5), (45, 25))
     assert none is None and cost == o["cost"] and path == o["path"]
     assert path[0] == (5, 5) and path[-1] == (45, 25)
+
+
+def test_dstar_512_against_oracle():
+    """A 512^2 grid (10 % obstacles, the bench's D* leg workload) -- the survey measured the
+    reference there (239,070 processState calls, 31 s)."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import batch, workloads as wl
+
+    occ, s, g = wl.c2_workload(nq=16, W=512, H=512, density=0.1, grid_seed=4, pair_seed=5)
+    r = batch.dstar2d_batch(occ, s, g, path_cap=2048)
+    ref = O.dstar2d_batch(occ, s, g, nthreads=8)
+    assert np.array_equal(r["status"].cpu().numpy(), ref["status"])
+    assert np.array_equal(r["n_process"].cpu().numpy(), ref["n_process"])
+    assert np.array_equal(r["cost"].cpu().numpy(), ref["cost"])
+
+
+def _kind_status(k):
+    return {"": 0, "noop": 1, "AttributeError": 4, "KeyError": 4, "-": -1}[k]
+
+
+def test_dstar_onpress_against_reference():
+    """48 sessions of the reference's own DStar.OnPress (stand-in event, recording plot): plan + 4
+    presses each, two of them on the planned path; every call's status, cost, walk and len(EXPAND)."""
+    from golden_io import load_npz
+    from python_motion_planning_amd import batch
+
+    z = load_npz("dstar_onpress.npz")
+    R = z["presses"].shape[1] + 1
+    n_walk = 0
+    for i, occ, _ in grid_cases("dstar_onpress.npz"):
+        out = batch.dstar2d_onpress_batch(occ, z["start"][i][None], z["goal"][i][None], z["presses"][i][None])
+        st, npr = out["status"][0].cpu().numpy(), out["n_process"][0].cpu().numpy()
+        cost, pl, path = out["cost"][0].cpu().numpy(), out["path_len"][0].cpu().numpy(), out["path"][0].cpu().numpy()
+        for r in range(R):
+            k = str(z["kind"][i][r])
+            assert st[r] == _kind_status(k), (i, r, k, st)
+            if k in ("", "noop"):
+                assert npr[r] == z["nexp"][i][r], (i, r)
+            if k == "":
+                assert cost[r] == z["cost"][i][r], (i, r)
+                assert np.array_equal(path[r, : pl[r]], seg(z["path"], z["path_off"], i * R + r)), (i, r)
+                n_walk += r > 0
+    assert n_walk >= 100
+
+
+def test_dstar_onpress_batch_against_oracle():
+    """128 sessions on a 128^2 grid, 3 presses each on cells of the planned path: the repairs run
+    processState on the kept state; every output against the oracle."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import batch, workloads as wl
+
+    occ, s, g = wl.c2_workload(nq=128, W=128, H=128, density=0.15, grid_seed=21, pair_seed=22)
+    r0 = batch.dstar2d_batch(occ, s, g)
+    pl0, p0 = r0["path_len"].cpu().numpy(), r0["path"].cpu().numpy()
+    rng = np.random.default_rng(23)
+    presses = np.zeros((128, 3, 2), np.int32)
+    for q in range(128):
+        cells = p0[q, 1 : max(2, pl0[q] - 1)]
+        for k in range(3):
+            c = int(cells[rng.integers(len(cells))]) if len(cells) else 0
+            presses[q, k] = (c // 128, c % 128)
+    out = batch.dstar2d_onpress_batch(occ, s, g, presses)
+    st, npr = out["status"].cpu().numpy(), out["n_process"].cpu().numpy()
+    cost, pl, path = out["cost"].cpu().numpy(), out["path_len"].cpu().numpy(), out["path"].cpu().numpy()
+    repaired = 0
+    for q in range(128):
+        ref = O.dstar2d_onpress(occ, s[q], g[q], presses[q])
+        for r in range(4):
+            assert st[q, r] == ref["status"][r] and npr[q, r] == ref["n_process"][r], (q, r)
+            assert cost[q, r] == ref["cost"][r] and pl[q, r] == ref["path_len"][r], (q, r)
+            assert np.array_equal(path[q, r, : max(pl[q, r], 0)], ref["paths"][r]), (q, r)
+            repaired += r > 0 and npr[q, r] > 0
+    assert repaired > 100
+
+
+def test_dstar_onpress_dropin():
+    """The drop-in DStar.OnPress(event) sequence on the README grid equals the reference session."""
+    import types
+
+    import python_motion_planning_amd as pmp
+    from golden_io import load_npz
+
+    z = load_npz("dstar_onpress.npz")
+    R = z["presses"].shape[1] + 1
+    for i, occ, _ in grid_cases("dstar_onpress.npz"):
+        if i >= 3:
+            break
+        W, H = occ.shape
+        env = pmp.Grid(W, H)
+        env.update({(int(x), int(y)) for x, y in np.argwhere(occ)})
+        p = pmp.DStar(tuple(int(v) for v in z["start"][i]), tuple(int(v) for v in z["goal"][i]), env)
+        p.plan()
+        for r in range(1, R):
+            x, y = (int(v) for v in z["presses"][i][r - 1])
+            p.OnPress(types.SimpleNamespace(xdata=x + 0.25, ydata=y + 0.25))
+            k = str(z["kind"][i][r])
+            assert len(p.EXPAND) == z["nexp"][i][r] or k == "noop", (i, r)
+            if k == "":
+                assert p.cost == z["cost"][i][r]
+                assert [c[0] * H + c[1] for c in p.path] == seg(z["path"], z["path_off"], i * R + r).tolist()

@@ -404,3 +404,66 @@ def test_theta3d_runs():
         assert out["cost"] == z["cost"][i]
         assert np.array_equal(out["path_cells"], seg(z["path"], z["path_off"], i))
         assert np.array_equal(out["expand_cells"], seg(z["expand"], z["expand_off"], i))
+
+
+def _csv3d_case(r):
+    from python_motion_planning_amd import workloads as wl
+
+    s, g = wl.bench3d_query(r["seed"], 21, 15, 11)
+    o = wl.SCENARIOS_3D[r["scenario"]](21, 15, 11)
+    wl.carve_safety_bubble(o, s, 2)
+    wl.carve_safety_bubble(o, g, 2)
+    return o, s, g
+
+
+def test_dstar3d_published_csv():
+    """All 500 distinct DStar3D rows of the reference's 3d_pathfinding_results.csv: cost repr
+    (including the inf rows of the asymmetric isCollision) and len(EXPAND)."""
+    rows = load_json("dstar3d_csv.json")
+    assert len(rows) == 500 and any(r["cost"] == "inf" for r in rows)
+    for r in rows:
+        o, s, g = _csv3d_case(r)
+        res = O.dstar3d(o, s, g)
+        assert repr(float(res["cost"][0])) == r["cost"], r
+        assert res["n_process"][0] == r["visited"], r
+
+
+def test_dstar3d_dynamic_obstacles_against_reference():
+    """plan() + 3 apply_dynamic_obstacles() rounds per case, replayed from reference runs: cost,
+    path and len(EXPAND) of every round."""
+    n = 0
+    for i, occ, z in grid_cases("dstar3d_runs.npz"):
+        res = O.dstar3d(occ, z["start"][i], z["goal"][i], z["blocks"][i])
+        R = z["blocks"].shape[1] + 1
+        for r in range(R):
+            assert res["cost"][r] == z["cost"][i][r] or (math.isinf(res["cost"][r]) and math.isinf(z["cost"][i][r])), (i, r)
+            assert res["n_process"][r] == z["nexp"][i][r], (i, r)
+            assert np.array_equal(res["paths"][r], seg(z["path"], z["path_off"], i * R + r)), (i, r)
+        n += 1
+    assert n >= 30
+
+
+def test_dstar_onpress_against_reference():
+    """DStar.plan + 4 OnPress(event) calls per session, replayed from the reference's own OnPress
+    (stand-in event, recording plot): every call's cost, walk path, len(EXPAND); raises and no-op
+    presses where the reference has them."""
+    z = load_npz("dstar_onpress.npz")
+    R = z["presses"].shape[1] + 1
+    kinds = set()
+    for i, occ, _ in grid_cases("dstar_onpress.npz"):
+        res = O.dstar2d_onpress(occ, z["start"][i], z["goal"][i], z["presses"][i])
+        for r in range(R):
+            k = str(z["kind"][i][r])
+            kinds.add(k)
+            if k == "-":
+                assert res["status"][r] == -1, (i, r)
+                continue
+            if k in ("AttributeError", "KeyError"):
+                assert res["status"][r] == 4, (i, r)
+                continue
+            assert res["status"][r] == (1 if k == "noop" else 0), (i, r, res["status"])
+            assert res["n_process"][r] == z["nexp"][i][r], (i, r)
+            if k == "":
+                assert res["cost"][r] == z["cost"][i][r], (i, r)
+                assert np.array_equal(res["paths"][r], seg(z["path"], z["path_off"], i * R + r)), (i, r)
+    assert {"", "noop"} <= kinds
