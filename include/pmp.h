@@ -238,6 +238,24 @@ int pmp_dstar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int 
                       int32_t* status, int32_t* expand, int expand_cap, int64_t max_process);
 
 /*
+ * Batched 3D LPA* with apply_change rounds.  Replaces LPAStar3D (global_planner/graph_search/
+ * lpa_star3d.py:40-225): plan() (:78-82: computeShortestPath :127-145, extractPath :185-225, the
+ * greedy min-g walk from the goal that gives (cost, []) when stuck or after 100000 steps) followed by
+ * nr apply_change(coord, blocked) calls (:93-124), each re-planning on the kept g / rhs / U.  U keeps
+ * the reference's list semantics, so every call's len(EXPAND), cost and path are bit-exact.
+ *   occ_bits, per_query, X, Y, Z, heuristic, start_xyz, goal_xyz as pmp_graph3d_batch
+ *   changes [nq][nr][4]      (x, y, z, mode): mode 0 = blocked None (toggle), 1 = True, 2 = False
+ *   cost, path_len, n_expanded, status [nq][nr + 1]; path [nq][nr + 1][path_cap] (voxels, start -> goal)
+ *       status 0 path, 1 the reference's empty path (cost kept), 2 path_cap overflow, 3 max_expansions
+ *       (0 = unbounded) hit, 4 endpoints off the grid, -1 not run (an earlier call hit a cap)
+ *   counters [nq][4] nullable: U pushes, expansions (all calls), 0, max |U|
+ */
+int pmp_lpastar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int per_query, int X, int Y, int Z,
+                        int heuristic, const int32_t* start_xyz, const int32_t* goal_xyz, int nq, const int32_t* changes,
+                        int nr, double* cost, int32_t* path_len, int32_t* path, int path_cap, int64_t* n_expanded,
+                        int32_t* status, int64_t* counters, int64_t max_expansions);
+
+/*
  * Batched LPA*.  Replaces LPAStar.plan (global_planner/graph_search/lpa_star.py:78-87): the initial
  * computeShortestPath (:139-160) with updateVertex (:162-179), and extractPath (:209-230).  U keeps
  * the reference's Python-list semantics (first-minimal `min(U, key)`, shifting `U.remove`,

@@ -741,3 +741,34 @@ def dstar2d_onpress(occ: np.ndarray, start, goal, presses, path_cap: int = 0, ma
                              _p(st, _i32p), int(max_process))
     return dict(cost=cost, status=st, n_process=npr, path_len=plen,
                 paths=[path[r, : max(0, min(plen[r], path_cap))].copy() for r in range(n + 1)])
+
+
+def lpastar3d(occ: np.ndarray, start, goal, changes=None, heuristic: str = "euclidean", path_cap: int = 0,
+              max_exp: int = 0):
+    """Restatement of LPAStar3D.plan (lpa_star3d.py:78-82) followed by one apply_change per row of
+    changes [nr][4] = (x, y, z, mode) (mode 0 toggle = blocked None, 1 block, 2 free; :93-124).
+    Returns per call (0 = plan): cost, status (0 path, 1 empty path, 2 overflow, 3 cap, -1 not run),
+    n_expanded (len(EXPAND)), paths (voxel ids, start -> goal)."""
+    L = lib()
+    if not getattr(L, "_l3_set", False):
+        L.oracle_lpastar3d.restype = ctypes.c_int
+        L.oracle_lpastar3d.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p, _i32p,
+                                       _i32p, ctypes.c_int, _dp, _i32p, _i64p, _i32p, ctypes.c_int, _i32p,
+                                       ctypes.c_int64]
+        L._l3_set = True
+    occ = np.ascontiguousarray(occ, dtype=np.uint8)
+    X, Y, Z = occ.shape
+    ch = np.zeros((0, 4), np.int32) if changes is None else np.ascontiguousarray(changes, np.int32).reshape(-1, 4)
+    nr = len(ch)
+    path_cap = path_cap or X * Y * Z + 1
+    cost = np.zeros(nr + 1)
+    st = np.zeros(nr + 1, np.int32)
+    ne = np.zeros(nr + 1, np.int64)
+    plen = np.zeros(nr + 1, np.int32)
+    path = np.zeros((nr + 1, path_cap), np.int32)
+    L.oracle_lpastar3d(_p(occ, _u8p), X, Y, Z, 1 if heuristic == "manhattan" else 0,
+                       _p(np.ascontiguousarray(start, np.int32), _i32p), _p(np.ascontiguousarray(goal, np.int32), _i32p),
+                       _p(ch, _i32p) if nr else None, nr, _p(cost, _dp), _p(st, _i32p), _p(ne, _i64p), _p(path, _i32p),
+                       path_cap, _p(plen, _i32p), int(max_exp))
+    return dict(cost=cost, status=st, n_expanded=ne, path_len=plen,
+                paths=[path[r, : min(plen[r], path_cap)].copy() for r in range(nr + 1)])

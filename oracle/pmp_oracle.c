@@ -2524,3 +2524,232 @@ int oracle_dstar2d_onpress(const uint8_t* occ_in, int W, int H, int sx, int sy, 
     free(occ); free(S.h); free(S.k); free(S.parent); free(S.t); free(S.open);
     return st;
 }
+
+/* ============================================================================================
+ * LPAStar3D (global_planner/graph_search/lpa_star3d.py:40-225): plan() (:78-82) = computeShortest
+ * Path (:127-145) + extractPath (:185-225), and apply_change(coord, blocked) (:93-124) rounds.
+ * U is restated as the reference's Python list: min(U, key) = the first minimal key (list `<`,
+ * :130), U.remove = first occurrence (coordinate equality; the list never holds a node twice),
+ * heapq.heappush = append + CPython _siftdown under LNode3D.__lt__ (key list compare, :38-40) on
+ * whatever order the list has.  getNeighbor (:160-182): in the map and the endpoint not an
+ * obstacle (no edge test); updateVertex's cost(n, node) uses isCollision(n, node) (asymmetric).
+ * start == goal: map[goal] overwrites map[start] (:62-63), so the start object lives in slot ncell.
+ * ============================================================================================ */
+typedef struct {
+    int32_t c;
+    double k1, k2;
+} l3ent_t;
+
+typedef struct {
+    double *g, *rhs;
+    l3ent_t* U;
+    int64_t n, cap;
+    d3_t geo; /* X, Y, Z, ncell, occ, goal_slot (unused), goal_cell */
+    int start_slot, start_cell, goal;
+    int heur;
+    int64_t nexp;
+} l3_t;
+
+static inline int l3_lt(const l3ent_t* a, const l3ent_t* b) { return a->k1 < b->k1 || (a->k1 == b->k1 && a->k2 < b->k2); }
+static inline int l3_coord(const l3_t* S, int slot) { return slot == S->start_slot ? S->start_cell : slot; }
+static double l3_h(const l3_t* S, int c)
+{
+    int x, y, z, gx, gy, gz;
+    d3_xyz(&S->geo, c, &x, &y, &z);
+    d3_xyz(&S->geo, S->goal, &gx, &gy, &gz);
+    const int dx = abs(gx - x), dy = abs(gy - y), dz = abs(gz - z);
+    if (S->heur == 1) return (double)(dx + dy + dz);
+    return sqrt((double)(dx * dx + dy * dy + dz * dz));
+}
+/* getNeighbor (:160-182): slots of the in-map, non-obstacle neighbours of voxel c, motion order */
+static int l3_neighbors(const l3_t* S, int c, int* nb)
+{
+    int x, y, z, k = 0;
+    d3_xyz(&S->geo, c, &x, &y, &z);
+    for (int m = 0; m < 26; m++) {
+        const int nx = x + M3[m][0], ny = y + M3[m][1], nz = z + M3[m][2];
+        if (nx < 0 || ny < 0 || nz < 0 || nx >= S->geo.X || ny >= S->geo.Y || nz >= S->geo.Z) continue;
+        if (d3_occ(&S->geo, nx, ny, nz)) continue;
+        nb[k++] = (nx * S->geo.Y + ny) * S->geo.Z + nz;
+    }
+    return k;
+}
+static void l3_push(l3_t* S, int32_t c, double k1, double k2)
+{
+    if (S->n == S->cap) {
+        S->cap *= 2;
+        S->U = (l3ent_t*)realloc(S->U, sizeof(l3ent_t) * (size_t)S->cap);
+    }
+    l3ent_t it = {c, k1, k2};
+    int64_t pos = S->n++;
+    while (pos > 0) { /* heapq._siftdown(heap, 0, pos) */
+        const int64_t parent = (pos - 1) >> 1;
+        if (l3_lt(&it, &S->U[parent])) {
+            S->U[pos] = S->U[parent];
+            pos = parent;
+            continue;
+        }
+        break;
+    }
+    S->U[pos] = it;
+}
+static void l3_remove_at(l3_t* S, int64_t i)
+{
+    memmove(S->U + i, S->U + i + 1, sizeof(l3ent_t) * (size_t)(S->n - i - 1));
+    S->n--;
+}
+static int64_t l3_find(const l3_t* S, int32_t slot)
+{
+    for (int64_t i = 0; i < S->n; i++)
+        if (l3_coord(S, S->U[i].c) == l3_coord(S, slot)) return i; /* Node3D equality: coordinates */
+    return -1;
+}
+/* updateVertex (:147-158) */
+static void l3_update(l3_t* S, int32_t slot)
+{
+    const int c = l3_coord(S, slot);
+    if (c != S->start_cell) { /* node != self.start: coordinate equality */
+        int nb[26];
+        const int k = l3_neighbors(S, c, nb);
+        if (k) {
+            double best = INFINITY;
+            for (int i = 0; i < k; i++) {
+                const double v = S->g[nb[i]] + d3_cost(&S->geo, nb[i], c);
+                if (i == 0 || v < best) best = v;
+            }
+            S->rhs[slot] = best;
+        } else {
+            S->rhs[slot] = INFINITY;
+        }
+    }
+    const int64_t p = l3_find(S, slot);
+    if (p >= 0) l3_remove_at(S, p);
+    if (S->g[slot] != S->rhs[slot]) {
+        const double m = S->g[slot] < S->rhs[slot] ? S->g[slot] : S->rhs[slot];
+        l3_push(S, slot, m + l3_h(S, c), m);
+    }
+}
+/* computeShortestPath (:127-145) */
+static int l3_compute(l3_t* S, int64_t max_exp)
+{
+    while (S->n > 0) {
+        int64_t bi = 0;
+        for (int64_t i = 1; i < S->n; i++)
+            if (l3_lt(&S->U[i], &S->U[bi])) bi = i;
+        const int gs = S->goal;
+        const double gm = S->g[gs] < S->rhs[gs] ? S->g[gs] : S->rhs[gs];
+        const l3ent_t gk = {0, gm + l3_h(S, S->goal), gm};
+        if (!l3_lt(&S->U[bi], &gk) && S->rhs[gs] == S->g[gs]) break;
+        const int32_t v = S->U[bi].c;
+        l3_remove_at(S, bi);
+        S->nexp++;
+        if (max_exp > 0 && S->nexp > max_exp) return 3;
+        if (S->g[v] > S->rhs[v]) {
+            S->g[v] = S->rhs[v];
+        } else {
+            S->g[v] = INFINITY;
+            l3_update(S, v);
+        }
+        int nb[26];
+        const int k = l3_neighbors(S, l3_coord(S, v), nb);
+        for (int i = 0; i < k; i++) l3_update(S, nb[i]);
+    }
+    return 0;
+}
+/* extractPath (:185-225): greedy min-g neighbours from the goal; (cost, []) when stuck or after
+ * 100000 steps.  Returns the path length written (start -> goal) or -1 for an empty path. */
+static int64_t l3_extract(const l3_t* S, double* cost, int32_t* path, int64_t path_cap)
+{
+    int node = S->goal;
+    double c = 0.0;
+    int64_t n = 0, safety = 0;
+    int32_t* tmp = (int32_t*)malloc(sizeof(int32_t) * 100002);
+    tmp[n++] = node;
+    while (node != S->start_cell) {
+        int nb[26], cand[26], k = l3_neighbors(S, node, nb), nc = 0;
+        for (int i = 0; i < k; i++)
+            if (!d3_coll(&S->geo, node, nb[i])) cand[nc++] = nb[i];
+        if (!nc) { *cost = c; free(tmp); return -1; }
+        int best = cand[0];
+        for (int i = 1; i < nc; i++)
+            if (S->g[cand[i]] < S->g[best]) best = cand[i];
+        c += d3_cost(&S->geo, node, best);
+        node = best;
+        tmp[n++] = node;
+        if (++safety >= 100000) { *cost = c; free(tmp); return -1; }
+    }
+    *cost = c;
+    for (int64_t i = 0; i < n && i < path_cap; i++) path[i] = tmp[n - 1 - i];
+    free(tmp);
+    return n;
+}
+
+/* changes [nr][4] = (x, y, z, mode): mode 0 toggle (blocked=None), 1 block, 2 free.  Per call r
+ * (0 = plan): cost[r], plen[r] (0 = the reference's empty path), path[r * path_cap ..],
+ * nexp[r] = len(EXPAND), status[r]: 0 path, 1 empty path, 2 path_cap overflow, 3 cap. */
+int oracle_lpastar3d(const uint8_t* occ_in, int X, int Y, int Z, int heuristic, const int32_t* s, const int32_t* g,
+                     const int32_t* changes, int nr, double* cost, int32_t* status, int64_t* nexp, int32_t* path,
+                     int path_cap, int32_t* plen, int64_t max_exp)
+{
+    l3_t S;
+    S.geo.X = X; S.geo.Y = Y; S.geo.Z = Z;
+    S.geo.ncell = X * Y * Z;
+    S.geo.occ = (uint8_t*)malloc(S.geo.ncell);
+    memcpy(S.geo.occ, occ_in, S.geo.ncell);
+    S.heur = heuristic;
+    S.start_cell = (s[0] * Y + s[1]) * Z + s[2];
+    S.goal = (g[0] * Y + g[1]) * Z + g[2];
+    S.start_slot = S.start_cell == S.goal ? S.geo.ncell : S.start_cell;
+    S.geo.goal_slot = -1;
+    S.geo.goal_cell = -1;
+    const int ns = S.geo.ncell + 1;
+    S.g = (double*)malloc(sizeof(double) * ns);
+    S.rhs = (double*)malloc(sizeof(double) * ns);
+    for (int i = 0; i < ns; i++) { S.g[i] = INFINITY; S.rhs[i] = INFINITY; }
+    S.rhs[S.start_slot] = 0.0; /* LNode3D(start, inf, 0.0) */
+    S.cap = 1024;
+    S.n = 0;
+    S.U = (l3ent_t*)malloc(sizeof(l3ent_t) * (size_t)S.cap);
+    l3_push(&S, S.start_slot, 0.0 + l3_h(&S, S.start_cell), 0.0); /* calculateKey(start) */
+    int rc = 0;
+    for (int r = 0; r <= nr; r++) {
+        S.nexp = 0; /* EXPAND.clear() in apply_change; empty at construction */
+        int st = 0;
+        if (r > 0) {
+            const int32_t* ch = changes + (size_t)(r - 1) * 4;
+            const int cx = ch[0], cy = ch[1], cz = ch[2], mode = ch[3];
+            const int in = cx >= 0 && cy >= 0 && cz >= 0 && cx < X && cy < Y && cz < Z;
+            const int cell = in ? (cx * Y + cy) * Z + cz : -1;
+            const int is_obs = in && S.geo.occ[cell];
+            if (in) {
+                if (mode == 0) {
+                    if (is_obs) { S.geo.occ[cell] = 0; l3_update(&S, cell); }
+                    else S.geo.occ[cell] = 1;
+                } else if (mode == 1) {
+                    S.geo.occ[cell] = 1;
+                } else if (is_obs) {
+                    S.geo.occ[cell] = 0;
+                    l3_update(&S, cell);
+                }
+                int nb[26];
+                const int k = l3_neighbors(&S, cell, nb);
+                for (int i = 0; i < k; i++) l3_update(&S, nb[i]);
+            }
+        }
+        if (l3_compute(&S, max_exp)) st = 3;
+        double c = 0.0;
+        int64_t n = 0;
+        if (st == 0) {
+            n = l3_extract(&S, &c, path + (size_t)r * path_cap, path_cap);
+            if (n < 0) { st = 1; n = 0; }
+            else if (n > path_cap) st = 2;
+        }
+        cost[r] = c;
+        status[r] = st;
+        nexp[r] = S.nexp;
+        plen[r] = (int32_t)n;
+        if (st == 3) { rc = 3; for (int q = r + 1; q <= nr; q++) status[q] = -1; break; }
+    }
+    free(S.geo.occ); free(S.g); free(S.rhs); free(S.U);
+    return rc;
+}

@@ -44,6 +44,8 @@ SIGNATURES = {
                                        ctypes.c_int64]),
     "pmp_dstar3d_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _i, _vp, _vp, _vp, _i, _vp, _vp,
                                _vp, _i, ctypes.c_int64]),
+    "pmp_lpastar3d_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _vp, _vp, _vp, _i, _vp,
+                                 _vp, _vp, ctypes.c_int64]),
     "pmp_lpastar2d_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     "pmp_dstarlite2d_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     "pmp_lpastar2d_replan_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _i,

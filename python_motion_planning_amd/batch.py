@@ -524,3 +524,46 @@ def dstar3d_batch(occ, starts, goals, blocks=None, path_cap: int | None = None, 
     _lib.check(ctx, rc, "pmp_dstar3d_batch")
     out["dims"] = (X, Y, Z)
     return out
+
+
+def lpastar3d_batch(occ, starts, goals, changes=None, heuristic: str = "euclidean", path_cap: int | None = None,
+                    counters: bool = False, max_expansions: int = 0):
+    """Batched LPAStar3D (lpa_star3d.py:40-225): plan() and then one apply_change() per row of
+    `changes` [nq, nr, 4] = (x, y, z, mode) with mode 0 = blocked None (toggle), 1 = True, 2 = False,
+    on pmp_lpastar3d_batch.  occ: uint8 [X, Y, Z] shared or [nq, X, Y, Z] per-query grids.
+    Returns dict of device tensors per call r (0 = plan): cost [nq, R], path_len [nq, R],
+    path [nq, R, path_cap] (voxels (x*Y+y)*Z+z, start -> goal), n_expanded [nq, R] (len(EXPAND)),
+    status [nq, R] (include/pmp.h), optional counters [nq, 4]."""
+    torch = _lib.device_check()
+    L = _lib.load_library()
+    ctx = _lib.context()
+    occ = np.asarray(occ)
+    per_query = occ.ndim == 4
+    X, Y, Z = occ.shape[-3:]
+    words = np.stack([pack_bits(o) for o in occ]) if per_query else pack_bits(occ)
+    occ_bits = torch.as_tensor(np.ascontiguousarray(words).view(np.int32), device="cuda")
+    s = _dev(torch, starts, torch.int32).reshape(-1, 3)
+    g = _dev(torch, goals, torch.int32).reshape(-1, 3)
+    nq = int(s.shape[0])
+    if changes is None:
+        nr, ch = 0, None
+    else:
+        ch = _dev(torch, changes, torch.int32)
+        if ch.dim() != 3 or ch.shape[0] != nq or ch.shape[2] != 4:
+            raise ValueError("changes must be [nq, nr, 4]")
+        nr = int(ch.shape[1])
+    R = nr + 1
+    path_cap = min(X * Y * Z + 1, 1 << 16) if path_cap is None else int(path_cap)
+    i32 = dict(dtype=torch.int32, device="cuda")
+    out = dict(cost=torch.empty((nq, R), dtype=torch.float64, device="cuda"), path_len=torch.empty((nq, R), **i32),
+               path=torch.empty((nq, R, path_cap), **i32),
+               n_expanded=torch.empty((nq, R), dtype=torch.int64, device="cuda"), status=torch.empty((nq, R), **i32))
+    out["counters"] = torch.empty((nq, 4), dtype=torch.int64, device="cuda") if counters else None
+    rc = L.pmp_lpastar3d_batch(ctx, _lib.stream_ptr(), occ_bits.data_ptr(), 1 if per_query else 0, X, Y, Z,
+                               1 if heuristic == "manhattan" else 0, s.data_ptr(), g.data_ptr(), nq, _lib.ptr(ch), nr,
+                               out["cost"].data_ptr(), out["path_len"].data_ptr(), out["path"].data_ptr(), path_cap,
+                               out["n_expanded"].data_ptr(), out["status"].data_ptr(), _lib.ptr(out["counters"]),
+                               int(max_expansions))
+    _lib.check(ctx, rc, "pmp_lpastar3d_batch")
+    out["dims"] = (X, Y, Z)
+    return out

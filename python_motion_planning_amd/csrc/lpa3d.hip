@@ -1,0 +1,620 @@
+// Batched LPA* in 3D for gfx950, exact with LPAStar3D (global_planner/graph_search/lpa_star3d.py:40-225):
+// plan() (:78-82: computeShortestPath :127-145 + extractPath :185-225) and any number of
+// apply_change(coord, blocked) rounds (:93-124) per query, over Grid3D with GraphSearcher3D's
+// asymmetric isCollision (graph_search_3d.py:66-107).
+//
+// U is the reference's Python list, kept element for element:
+//   * min(U, key) = the FIRST minimal key in list order (list `<` on [k1, k2], :130);
+//   * U.remove(node) shifts the tail left (the list never holds a node twice: updateVertex removes
+//     before it pushes, :154-157);
+//   * heapq.heappush appends and sifts with CPython _siftdown on whatever order the list has.
+// U lives in LDS (one wave per query, 8 per CU; positions past the LDS share spill to HBM), so the
+// scans, shifts and sifts are LDS rounds.  g / rhs per voxel stay in HBM.
+//
+// One expansion touches one 5x5x5 block: updateVertex never changes g, so after the expanded
+// node's own g update every rhs the expansion recomputes (the node's and its 26 neighbours') reads
+// g values of that block, staged in LDS in two load rounds, and the 27 rhs minima (26 candidates
+// each, cost(n, node) with isCollision(n, node)) are computed lane-parallel.  The membership of the
+// 27 voxels in U comes from one scan; the sequential remove / push of updateVertex in motion order
+// (:145, :154-157) then only adjusts the 27 tracked positions (a remove shifts the ones past it, a
+// push's sift moves its ancestor chain).
+//
+// start == goal: map[goal] overwrites map[start] (:62-63), the start object is detached, and the
+// reference's result is fixed: plan() expands it once and returns (0.0, [goal]); every
+// apply_change then expands nothing.
+#include "pmp_internal.h"
+
+namespace {
+
+constexpr int kMaxDim = 256;
+constexpr double kInf = __builtin_huge_val();
+
+__device__ __constant__ int8_t c_m[26][3] = {
+    {-1, 0, 0}, {-1, 1, 0}, {0, 1, 0}, {1, 1, 0}, {1, 0, 0}, {1, -1, 0}, {0, -1, 0}, {-1, -1, 0},
+    {0, 0, 1}, {0, 0, -1},
+    {-1, 0, 1}, {-1, 1, 1}, {0, 1, 1}, {1, 1, 1}, {1, 0, 1}, {1, -1, 1}, {0, -1, 1}, {-1, -1, 1},
+    {-1, 0, -1}, {-1, 1, -1}, {0, 1, -1}, {1, 1, -1}, {1, 0, -1}, {1, -1, -1}, {0, -1, -1}, {-1, -1, -1}};
+
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) int32_t lds_i32;
+typedef __attribute__((address_space(3))) double lds_f64;
+
+__device__ __forceinline__ void wsync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+__device__ __forceinline__ bool key_lt(double a1, double a2, double b1, double b2)
+{
+    return a1 < b1 || (a1 == b1 && a2 < b2);
+}
+
+struct Geo {
+    int X, Y, Z;
+    __device__ __forceinline__ bool in(int x, int y, int z) const
+    {
+        return (unsigned)x < (unsigned)X && (unsigned)y < (unsigned)Y && (unsigned)z < (unsigned)Z;
+    }
+    __device__ __forceinline__ int id(int x, int y, int z) const { return (x * Y + y) * Z + z; }
+    __device__ __forceinline__ void xyz(int c, int& x, int& y, int& z) const
+    {
+        z = c % Z;
+        const int r = c / Z;
+        y = r % Y;
+        x = r / Y;
+    }
+};
+
+// working occupancy (apply_change edits it): LDS when it fits, else the worker's HBM copy;
+// `p in self.obstacles` is false outside the grid
+struct Occ {
+    lds_u32* l;
+    uint32_t* g;
+    bool lds;
+    Geo geo;
+    __device__ __forceinline__ bool at(int x, int y, int z) const
+    {
+        if (!geo.in(x, y, z)) return false;
+        const uint32_t c = (uint32_t)geo.id(x, y, z);
+        const uint32_t w = lds ? l[c >> 5] : g[c >> 5];
+        return (w >> (c & 31)) & 1u;
+    }
+    // isCollision(node1 = (x1,y1,z1), node2) for neighbouring voxels
+    __device__ __forceinline__ bool coll(int x1, int y1, int z1, int x2, int y2, int z2) const
+    {
+        if (at(x1, y1, z1) || at(x2, y2, z2)) return true;
+        const int dx = x2 - x1, dy = y2 - y1, dz = z2 - z1;
+        const int ch = (dx != 0) + (dy != 0) + (dz != 0);
+        if (ch <= 1) return false;
+        if (ch == 2) {
+            if (dx != 0 && dy != 0) return at(x1 + dx, y1, z1) || at(x1, y1 + dy, z1);
+            if (dx != 0 && dz != 0) return at(x1 + dx, y1, z1) || at(x1, y1, z1 + dz);
+            return at(x1, y1 + dy, z1) || at(x1, y1, z1 + dz);
+        }
+        return at(x1 + dx, y1, z1) || at(x1, y1 + dy, z1) || at(x1, y1, z1 + dz);
+    }
+};
+
+__device__ __forceinline__ double dist_unit(int dx, int dy, int dz)  // Planner3D.dist of a motion
+{
+    return __dsqrt_rn((double)(dx * dx + dy * dy + dz * dz));
+}
+
+// U: positions < cap in LDS, the rest in the worker's HBM arrays
+struct UList {
+    lds_i32* lc;
+    lds_f64* l1;
+    lds_f64* l2;
+    int32_t* gc;
+    double* g1;
+    double* g2;
+    int cap;
+    int n;
+    __device__ __forceinline__ void ld(int k, int32_t& c, double& a, double& b) const
+    {
+        if (k < cap) {
+            c = lc[k];
+            a = l1[k];
+            b = l2[k];
+        } else {
+            c = gc[k - cap];
+            a = g1[k - cap];
+            b = g2[k - cap];
+        }
+    }
+    __device__ __forceinline__ void st(int k, int32_t c, double a, double b) const
+    {
+        if (k < cap) {
+            lc[k] = c;
+            l1[k] = a;
+            l2[k] = b;
+        } else {
+            gc[k - cap] = c;
+            g1[k - cap] = a;
+            g2[k - cap] = b;
+        }
+    }
+};
+
+// The 27 tracked voxels of the current block (lane b < 27 = block voxel b, 26 = the centre): their
+// U positions follow every remove / push
+struct Track {
+    int pos;  // per lane: this lane's voxel's index in U, -1 = not in U
+};
+
+struct L3 {
+    Geo geo;
+    Occ occ;
+    UList U;
+    double* g;
+    double* rhs;
+    lds_f64* cube;  // 125 g values of the 5x5x5 block around the centre
+    int lane;
+    int start, goal;  // voxel ids
+    int gx, gy, gz;
+    int heur;
+    int64_t nexp;
+    int64_t npush;
+    int maxn;
+
+    __device__ __forceinline__ double hval(int x, int y, int z) const
+    {
+        const int dx = abs(gx - x), dy = abs(gy - y), dz = abs(gz - z);
+        return heur == 1 ? (double)(dx + dy + dz) : __dsqrt_rn((double)(dx * dx + dy * dy + dz * dz));
+    }
+
+    // U.remove(U[i]): the tail moves left one slot; 4 elements per lane per round (all loads of a
+    // round before its stores; a round never reads what an earlier round wrote)
+    __device__ __forceinline__ void remove_at(int i, Track& t)
+    {
+        for (int base = i; base < U.n - 1; base += 256) {
+            int32_t c[4];
+            double a[4], b[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int k = base + lane + 64 * j;
+                if (k < U.n - 1) U.ld(k + 1, c[j], a[j], b[j]);
+            }
+            wsync();
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int k = base + lane + 64 * j;
+                if (k < U.n - 1) U.st(k, c[j], a[j], b[j]);
+            }
+            wsync();
+        }
+        U.n -= 1;
+        if (t.pos == i) t.pos = -1;
+        else if (t.pos > i) t.pos -= 1;
+    }
+
+    // heapq.heappush(U, node): lane j (1..D) loads ancestor j of position n; the ancestors that move
+    // down are the run of "new < ancestor" from the parent up (_siftdown stops at the first one that
+    // is not greater).  `me` = this lane tracks the pushed voxel.
+    __device__ __forceinline__ void push(int32_t c, double k1, double k2, Track& t, bool me)
+    {
+        const uint32_t np1 = (uint32_t)U.n + 1u;
+        const int D = 31 - __clz((int)np1);
+        const bool on = lane >= 1 && lane <= D;
+        const int aj = on ? (int)(np1 >> lane) - 1 : 0;
+        int32_t ac = 0;
+        double a1 = 0.0, a2 = 0.0;
+        if (on) U.ld(aj, ac, a1, a2);
+        const uint64_t lt = ballot(on && key_lt(k1, k2, a1, a2));
+        const int s = __builtin_ctzll(~(lt >> 1));  // trailing ones from lane 1
+        wsync();
+        if (on && lane <= s) U.st((int)(np1 >> (lane - 1)) - 1, ac, a1, a2);
+        const int dst = (int)(np1 >> s) - 1;
+        if (lane == 0) U.st(dst, c, k1, k2);
+        wsync();
+        // tracked positions: ancestor j (1..s) -> ancestor j-1
+        if (t.pos >= 0) {
+            const int p1 = t.pos + 1;
+            const int depth = 31 - __clz(np1) - (31 - __clz(p1));  // levels from p to position n
+            if (depth >= 1 && depth <= s && ((int)(np1 >> depth) == p1)) t.pos = (int)(np1 >> (depth - 1)) - 1;
+        }
+        if (me) t.pos = dst;
+        U.n += 1;
+        npush += 1;
+        if (U.n > maxn) maxn = U.n;
+    }
+
+    // updateVertex over the 3x3x3 block of `center` (:147-158): optionally the centre first (its own
+    // updateVertex), then getNeighbor(center) in motion order.  The 5x5x5 g block is staged first;
+    // g does not change inside.
+    __device__ void update_block(int center, bool do_center)
+    {
+        int cx, cy, cz;
+        geo.xyz(center, cx, cy, cz);
+        // ---- stage g of the 5x5x5 block (inf outside the map)
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const int b = lane + 64 * r;
+            double v = kInf;
+            if (b < 125) {
+                const int x = cx + b / 25 - 2, y = cy + (b / 5) % 5 - 2, z = cz + b % 5 - 2;
+                if (geo.in(x, y, z)) v = g[geo.id(x, y, z)];
+                cube[b] = v;
+            }
+        }
+        // ---- this lane's block voxel: lanes 0..25 = motion m, lane 26 = the centre
+        const int m = lane < 26 ? lane : 0;
+        const int dx = lane < 26 ? c_m[m][0] : 0, dy = lane < 26 ? c_m[m][1] : 0, dz = lane < 26 ? c_m[m][2] : 0;
+        const int px = cx + dx, py = cy + dy, pz = cz + dz;
+        const bool mine = lane <= 26 && geo.in(px, py, pz);
+        const int P = mine ? geo.id(px, py, pz) : 0;
+        // the centre's getNeighbor(center): in the map, endpoint free
+        const bool is_nb = lane < 26 && mine && !occ.at(px, py, pz);
+        double rv = 0.0;
+        if (mine) rv = rhs[P];
+        wsync();
+        // ---- rhs of the lane's voxel: min over its getNeighbor of g + cost(n, voxel) (:150-153)
+        if (mine && P != start) {
+            double best = kInf;
+            bool any = false;
+            for (int u = 0; u < 26; u++) {
+                const int qx = px + c_m[u][0], qy = py + c_m[u][1], qz = pz + c_m[u][2];
+                if (!geo.in(qx, qy, qz) || occ.at(qx, qy, qz)) continue;
+                any = true;
+                const double gq = cube[(qx - cx + 2) * 25 + (qy - cy + 2) * 5 + (qz - cz + 2)];
+                const double c = occ.coll(qx, qy, qz, px, py, pz) ? kInf
+                                                                  : dist_unit(px - qx, py - qy, pz - qz);
+                best = fmin(best, gq + c);
+            }
+            rv = any ? best : kInf;
+        }
+        const double gv = mine ? cube[(dx + 2) * 25 + (dy + 2) * 5 + (dz + 2)] : 0.0;
+        // ---- U positions of the 27 voxels: one scan
+        Track t;
+        t.pos = -1;
+        for (int base = 0; base < U.n; base += 64) {
+            const int k = base + lane;
+            int32_t c = -1;
+            double a, b;
+            if (k < U.n) U.ld(k, c, a, b);
+            // block index of c relative to the centre, or -1
+            int bi = -1;
+            if (c >= 0) {
+                int x, y, z;
+                geo.xyz(c, x, y, z);
+                const int ex = x - cx, ey = y - cy, ez = z - cz;
+                if (ex >= -1 && ex <= 1 && ey >= -1 && ey <= 1 && ez >= -1 && ez <= 1) bi = (ex + 1) * 9 + (ey + 1) * 3 + (ez + 1);
+            }
+            uint64_t hits = ballot(bi >= 0);
+            while (hits) {
+                const int l = __ffsll((long long)hits) - 1;
+                hits &= hits - 1;
+                const int hb = __builtin_amdgcn_readlane(bi, l);
+                const int myb = (dx + 1) * 9 + (dy + 1) * 3 + (dz + 1);
+                if (lane <= 26 && myb == hb) t.pos = base + l;
+            }
+        }
+        // ---- updateVertex in the reference's order: the centre (if asked), then each neighbour
+        const uint64_t nbm = ballot(is_nb);
+        const int nsteps = (do_center ? 1 : 0) + __popcll(nbm);
+        uint64_t rem = nbm;
+        for (int sidx = 0; sidx < nsteps; sidx++) {
+            int who;
+            if (do_center && sidx == 0) {
+                who = 26;
+            } else {
+                who = __ffsll((long long)rem) - 1;
+                rem &= rem - 1;
+            }
+            const int Pw = __builtin_amdgcn_readlane(P, who);
+            const double rw = rl_f64(rv, who);
+            const double gw = rl_f64(gv, who);
+            if (Pw != start && lane == 0) rhs[Pw] = rw;
+            const int pw = __builtin_amdgcn_readlane(t.pos, who);
+            if (pw >= 0) remove_at(pw, t);
+            if (gw != rw) {
+                int x, y, z;
+                geo.xyz(Pw, x, y, z);
+                const double mn = gw < rw ? gw : rw;
+                push(Pw, mn + hval(x, y, z), mn, t, lane == who);
+            }
+        }
+        wsync();
+    }
+};
+
+__global__ __launch_bounds__(64) void lpa3d_kernel(
+    const uint32_t* __restrict__ occ_all, int per_query, int X, int Y, int Z, int heur,
+    const int32_t* __restrict__ start_xyz, const int32_t* __restrict__ goal_xyz, int nq,
+    const int32_t* __restrict__ changes, int nr, double* __restrict__ cost_out, int32_t* __restrict__ plen_out,
+    int32_t* __restrict__ path_out, int path_cap, int64_t* __restrict__ nexp_out, int32_t* __restrict__ status_out,
+    int64_t* __restrict__ counters, int64_t max_exp, int* __restrict__ queue, double* __restrict__ scr_f64,
+    int32_t* __restrict__ scr_i32, uint32_t* __restrict__ occ_scr, int words, int occ_lds, int ucap)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = lane_id();
+    const int ncell = X * Y * Z;
+    L3 S;
+    S.geo = Geo{X, Y, Z};
+    S.lane = lane;
+    S.heur = heur;
+    // LDS: cube (125 f64, 1000 B -> 1024), U keys (2 x ucap f64), U cells (ucap i32), occupancy bits
+    S.cube = (lds_f64*)smem;
+    S.U.l1 = (lds_f64*)(smem + 1024);
+    S.U.l2 = (lds_f64*)(smem + 1024 + (size_t)8 * ucap);
+    S.U.lc = (lds_i32*)(smem + 1024 + (size_t)16 * ucap);
+    S.U.cap = ucap;
+    S.occ.l = (lds_u32*)(smem + 1024 + (size_t)20 * ucap);
+    S.occ.lds = occ_lds != 0;
+    S.occ.g = occ_scr + (size_t)blockIdx.x * (size_t)words;
+    S.occ.geo = S.geo;
+    {
+        const size_t spill = (size_t)ncell + 1;
+        double* f = scr_f64 + (size_t)blockIdx.x * (2 * (size_t)ncell + 2 * spill);
+        S.g = f;
+        S.rhs = f + ncell;
+        S.U.g1 = f + 2 * (size_t)ncell;
+        S.U.g2 = S.U.g1 + spill;
+        S.U.gc = scr_i32 + (size_t)blockIdx.x * spill;
+    }
+    const int R1 = nr + 1;
+
+    for (;;) {
+        const int q = next_query(queue, lane);
+        if (q >= nq) break;
+        const int sx = uni(start_xyz[3 * q]), sy = uni(start_xyz[3 * q + 1]), sz = uni(start_xyz[3 * q + 2]);
+        const int gx = uni(goal_xyz[3 * q]), gy = uni(goal_xyz[3 * q + 1]), gz = uni(goal_xyz[3 * q + 2]);
+        const bool in = S.geo.in(sx, sy, sz) && S.geo.in(gx, gy, gz);
+        if (!in) {  // endpoints outside the map: not supported (every lane stores the same values)
+            for (int r = 0; r < R1; r++) {
+                status_out[(size_t)q * R1 + r] = PMP_REF_RAISES;
+                cost_out[(size_t)q * R1 + r] = 0.0;
+                plen_out[(size_t)q * R1 + r] = 0;
+                nexp_out[(size_t)q * R1 + r] = 0;
+            }
+            continue;
+        }
+        S.start = S.geo.id(sx, sy, sz);
+        S.goal = S.geo.id(gx, gy, gz);
+        S.gx = gx;
+        S.gy = gy;
+        S.gz = gz;
+        S.npush = 0;
+        S.maxn = 0;
+        if (S.start == S.goal) {
+            for (int r = 0; r < R1; r++) {
+                status_out[(size_t)q * R1 + r] = 0;
+                cost_out[(size_t)q * R1 + r] = 0.0;
+                plen_out[(size_t)q * R1 + r] = 1;
+                nexp_out[(size_t)q * R1 + r] = r == 0 ? 1 : 0;
+                path_out[((size_t)q * R1 + r) * (size_t)path_cap] = S.goal;
+            }
+            if (counters && lane == 0) {
+                counters[4 * q] = 1; counters[4 * q + 1] = 1; counters[4 * q + 2] = 0; counters[4 * q + 3] = 1;
+            }
+            continue;
+        }
+        // working occupancy, g = rhs = inf, rhs(start) = 0 (LNode3D(start, inf, 0.0), :58)
+        {
+            const uint32_t* src = occ_all + (per_query ? (size_t)q * (size_t)words : 0);
+            for (int w = lane; w < words; w += 64) {
+                if (S.occ.lds) S.occ.l[w] = src[w];
+                else S.occ.g[w] = src[w];
+            }
+            for (int c = lane; c < ncell; c += 64) {
+                S.g[c] = kInf;
+                S.rhs[c] = c == S.start ? 0.0 : kInf;
+            }
+        }
+        wsync();
+        S.U.n = 0;
+        {
+            Track t;
+            t.pos = -1;
+            S.push(S.start, 0.0 + S.hval(sx, sy, sz), 0.0, t, false);  // calculateKey(start)
+        }
+        int st = 0;
+        int64_t tot_exp = 0;
+        for (int r = 0; r <= nr; r++) {
+            S.nexp = 0;
+            if (r > 0 && st != 0 && st != PMP_NO_PATH) {
+                if (lane == 0) {
+                    status_out[(size_t)q * R1 + r] = -1;
+                    cost_out[(size_t)q * R1 + r] = 0.0;
+                    plen_out[(size_t)q * R1 + r] = 0;
+                    nexp_out[(size_t)q * R1 + r] = 0;
+                }
+                continue;
+            }
+            st = 0;
+            if (r > 0) {
+                // apply_change(coord, blocked) (:93-124)
+                const int32_t* ch = changes + ((size_t)q * nr + (r - 1)) * 4;
+                const int cx = uni(ch[0]), cy = uni(ch[1]), cz = uni(ch[2]), mode = uni(ch[3]);
+                if (S.geo.in(cx, cy, cz)) {
+                    const int cell = S.geo.id(cx, cy, cz);
+                    const bool is_obs = S.occ.at(cx, cy, cz);
+                    bool freed = false;
+                    if (mode == 0) freed = is_obs;
+                    else if (mode == 2) freed = is_obs;
+                    const bool block = (mode == 0 && !is_obs) || mode == 1;
+                    wsync();
+                    if (lane == 0 && (freed || block)) {
+                        const uint32_t bit = 1u << (cell & 31);
+                        if (S.occ.lds) {
+                            if (freed) S.occ.l[cell >> 5] &= ~bit;
+                            else S.occ.l[cell >> 5] |= bit;
+                        } else {
+                            if (freed) S.occ.g[cell >> 5] &= ~bit;
+                            else S.occ.g[cell >> 5] |= bit;
+                        }
+                    }
+                    wsync();
+                    // updateVertex(map[coord]) when freed, then getNeighbor(changed)'s updateVertex
+                    S.update_block(cell, freed);
+                }
+            }
+            // ---- computeShortestPath (:127-145)
+            for (;;) {
+                if (S.U.n == 0) break;
+                if (max_exp > 0 && S.nexp >= max_exp) { st = PMP_CAP_OVERFLOW; break; }
+                double gg = 0.0, gr = 0.0;
+                if (lane == 0) {
+                    gg = S.g[S.goal];
+                    gr = S.rhs[S.goal];
+                }
+                // min(U, key): first minimal key in list order
+                double b1 = kInf, b2 = kInf;
+                int bi = 0x7fffffff;
+                for (int k = lane; k < S.U.n; k += 64) {
+                    int32_t c;
+                    double a1, a2;
+                    S.U.ld(k, c, a1, a2);
+                    if (bi == 0x7fffffff || key_lt(a1, a2, b1, b2)) { b1 = a1; b2 = a2; bi = k; }
+                }
+                for (int o = 1; o < 64; o <<= 1) {
+                    const double o1 = __shfl_xor(b1, o, 64), o2 = __shfl_xor(b2, o, 64);
+                    const int oi = __shfl_xor(bi, o, 64);
+                    const bool take = oi != 0x7fffffff &&
+                                      (bi == 0x7fffffff || key_lt(o1, o2, b1, b2) || (o1 == b1 && o2 == b2 && oi < bi));
+                    if (take) { b1 = o1; b2 = o2; bi = oi; }
+                }
+                bi = uni(bi);
+                b1 = rl_f64(b1, 0);
+                b2 = rl_f64(b2, 0);
+                gg = rl_f64(gg, 0);
+                gr = rl_f64(gr, 0);
+                const double gm = gg < gr ? gg : gr;
+                // node.key >= calculateKey(goal) and goal.rhs == goal.g (:131-133); h(goal, goal) = 0
+                if (!key_lt(b1, b2, gm + 0.0, gm) && gr == gg) break;
+                int32_t vt = 0;
+                if (lane == 0) {
+                    double a, b;
+                    S.U.ld(bi, vt, a, b);
+                }
+                const int v = uni(vt);
+                {
+                    Track t;
+                    t.pos = -1;
+                    S.remove_at(bi, t);
+                }
+                S.nexp++;
+                double gvt = 0.0, rvt = 0.0;
+                if (lane == 0) {
+                    gvt = S.g[v];
+                    rvt = S.rhs[v];
+                }
+                const double gv = rl_f64(gvt, 0), rv = rl_f64(rvt, 0);
+                const bool over = gv > rv;
+                if (lane == 0) S.g[v] = over ? rv : kInf;
+                wsync();
+                // over-consistent: g = rhs; else g = inf and updateVertex(node); then the neighbours
+                S.update_block(v, !over);
+            }
+            // ---- extractPath (:185-225): greedy min-g free neighbour from the goal
+            double cost = 0.0;
+            int len = 0;
+            int32_t* pth = path_out + ((size_t)q * R1 + r) * (size_t)path_cap;
+            if (st == 0) {
+                int node = S.goal;
+                if (lane == 0 && len < path_cap) pth[len] = node;
+                len++;
+                int safety = 0;
+                while (node != S.start) {
+                    int x, y, z;
+                    S.geo.xyz(node, x, y, z);
+                    const int m = lane < 26 ? lane : 0;
+                    const int nx = x + c_m[m][0], ny = y + c_m[m][1], nz = z + c_m[m][2];
+                    bool ok = lane < 26 && S.geo.in(nx, ny, nz) && !S.occ.at(nx, ny, nz) &&
+                              !S.occ.coll(x, y, z, nx, ny, nz);
+                    double gn = kInf;
+                    if (ok) gn = S.g[S.geo.id(nx, ny, nz)];
+                    uint64_t vm = ballot(ok);
+                    if (!vm) { st = PMP_NO_PATH; break; }
+                    int bm = -1;
+                    double bg = 0.0;
+                    while (vm) {
+                        const int k = __ffsll((long long)vm) - 1;
+                        vm &= vm - 1;
+                        const double gk = rl_f64(gn, k);
+                        if (bm < 0 || gk < bg) { bm = k; bg = gk; }
+                    }
+                    cost += dist_unit(c_m[bm][0], c_m[bm][1], c_m[bm][2]);
+                    node = S.geo.id(x + c_m[bm][0], y + c_m[bm][1], z + c_m[bm][2]);
+                    if (lane == 0 && len < path_cap) pth[len] = node;
+                    len++;
+                    if (++safety >= 100000) { st = PMP_NO_PATH; break; }
+                }
+                wsync();
+                if (st == 0) {
+                    if (len > path_cap) st = PMP_PATH_OVERFLOW;
+                    else  // path.reverse()
+                        for (int i = lane; i < len / 2; i += 64) {
+                            const int32_t a = pth[i], b = pth[len - 1 - i];
+                            pth[i] = b;
+                            pth[len - 1 - i] = a;
+                        }
+                }
+            }
+            tot_exp += S.nexp;
+            if (lane == 0) {
+                status_out[(size_t)q * R1 + r] = st;
+                cost_out[(size_t)q * R1 + r] = cost;
+                plen_out[(size_t)q * R1 + r] = st == 0 || st == PMP_PATH_OVERFLOW ? len : 0;
+                nexp_out[(size_t)q * R1 + r] = S.nexp;
+            }
+            wsync();
+        }
+        if (counters && lane == 0) {
+            counters[4 * q] = S.npush;
+            counters[4 * q + 1] = tot_exp;
+            counters[4 * q + 2] = 0;
+            counters[4 * q + 3] = S.maxn;
+        }
+        wsync();
+    }
+}
+
+constexpr int kOccLdsWords = 2048;                 // grids up to 65536 voxels: occupancy in LDS
+constexpr size_t kScratchBudget = (size_t)16 << 30;
+
+}  // namespace
+
+extern "C" int pmp_lpastar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int per_query, int X, int Y,
+                                   int Z, int heuristic, const int32_t* start_xyz, const int32_t* goal_xyz, int nq,
+                                   const int32_t* changes, int nr, double* cost, int32_t* path_len, int32_t* path,
+                                   int path_cap, int64_t* n_expanded, int32_t* status, int64_t* counters,
+                                   int64_t max_expansions)
+{
+    if (!ctx) return PMP_EINVAL;
+    if (X < 1 || Y < 1 || Z < 1 || X > kMaxDim || Y > kMaxDim || Z > kMaxDim)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar3d_batch: X, Y, Z must be in [1, 256]");
+    if (heuristic != 0 && heuristic != 1) return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar3d_batch: heuristic must be 0 or 1");
+    if (nq < 0 || path_cap < 1 || nr < 0 || (nr > 0 && !changes))
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar3d_batch: bad nq/path_cap/nr/changes");
+    if (nq == 0) return PMP_OK;
+    if (!occ_bits || !start_xyz || !goal_xyz || !cost || !path_len || !path || !n_expanded || !status)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar3d_batch: null pointer argument");
+    PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    const size_t ncell = (size_t)X * Y * Z;
+    const int words = (int)((ncell + 31) / 32);
+    const bool occ_lds = words <= kOccLdsWords;
+    // 8 waves per CU: 20 KiB of LDS each for the g block, U (20 B per entry) and the occupancy
+    const int per_cu = 8;
+    const int occ_bytes = occ_lds ? ((words * 4 + 15) & ~15) : 0;
+    int ucap = (((160 * 1024) / per_cu - 1024 - occ_bytes) / 20) & ~15;
+    if (ucap < 64) ucap = 64;
+    if ((size_t)ucap > ncell + 1) ucap = (int)((ncell + 1 + 15) & ~(size_t)15);
+    const size_t lds = 1024 + (size_t)20 * ucap + occ_bytes;
+    const size_t spill = ncell + 1;
+    const size_t per_worker = (2 * ncell + 2 * spill) * 8 + spill * 4 + (occ_lds ? 0 : (size_t)words * 4) + 256;
+    int workers = 256 * per_cu;
+    const size_t fit = kScratchBudget / per_worker;
+    if (fit < 1) return pmp_set_err(ctx, PMP_ENOMEM, "pmp_lpastar3d_batch: one worker exceeds the scratch budget");
+    if ((size_t)workers > fit) workers = (int)fit;
+    if (workers > nq) workers = nq;
+    double* f = (double*)pmp_scratch(ctx, SCR_AUX2, (size_t)workers * (2 * ncell + 2 * spill) * 8 + 16);
+    int32_t* i32 = (int32_t*)pmp_scratch(ctx, SCR_AUX3, (size_t)workers * spill * 4 + 16);
+    uint32_t* occw = (uint32_t*)pmp_scratch(ctx, SCR_AUX4, occ_lds ? 16 : (size_t)workers * words * 4 + 16);
+    int* queue = (int*)pmp_scratch(ctx, SCR_AUX0, 256);
+    if (!f || !i32 || !occw || !queue) return PMP_ENOMEM;
+    hipStream_t s = (hipStream_t)stream;
+    PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
+    hipLaunchKernelGGL(lpa3d_kernel, dim3(workers), dim3(64), lds, s, occ_bits, per_query, X, Y, Z, heuristic, start_xyz,
+                       goal_xyz, nq, changes, nr, cost, path_len, path, path_cap, n_expanded, status, counters,
+                       max_expansions, queue, f, i32, occw, words, occ_lds ? 1 : 0, ucap);
+    PMP_HIP_CHECK(ctx, hipGetLastError());
+    return PMP_OK;
+}

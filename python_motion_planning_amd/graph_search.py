@@ -483,3 +483,85 @@ class DStar3D(GraphSearcher3D):
     @staticmethod
     def plan_batch(occ, starts, goals, blocks=None, **kw):
         return batch.dstar3d_batch(occ, starts, goals, blocks, **kw)
+
+
+class LNode3D:
+    """LPA* node of LPAStar3D (lpa_star3d.py:13-43): coordinates in `current`, g, rhs, key."""
+
+    __slots__ = ("current", "g", "rhs", "key", "parent")
+
+    def __init__(self, current, g, rhs, key) -> None:
+        self.current, self.g, self.rhs, self.key, self.parent = current, g, rhs, key, None
+
+    def __eq__(self, other) -> bool:
+        return isinstance(other, LNode3D) and self.current == other.current
+
+    def __hash__(self) -> int:
+        return hash(self.current)
+
+
+class LPAStar3D(GraphSearcher3D):
+    """Lifelong Planning A* on 3D voxel grids (lpa_star3d.py:40-225): plan() and apply_change() run
+    in the gfx950 kernel lpa3d.hip with the reference's list-semantics U.  The kernel is stateless,
+    so the planner keeps the history of changes and every call replays plan() and the earlier
+    changes on the device (the reference's kept g / rhs / U are a function of that history)."""
+
+    def __init__(self, start: tuple, goal: tuple, env, heuristic_type: str = "euclidean") -> None:
+        super().__init__(start, goal, env, heuristic_type)
+        self.EXPAND = []
+        self._changes = []
+        self._occ0 = None
+
+    def __str__(self) -> str:
+        return "Lifelong Planning A* 3D"
+
+    def _call(self):
+        ch = np.asarray(self._changes, np.int32).reshape(1, -1, 4) if self._changes else None
+        X, Y, Z = self._occ0.shape
+        r = batch.lpastar3d_batch(self._occ0, np.array([self.start.current]), np.array([self.goal.current]), ch,
+                                  self.heuristic_type, path_cap=X * Y * Z + 1)
+        k = len(self._changes)
+        st = int(r["status"][0, k])
+        if st not in (0, 1):
+            raise RuntimeError(f"{self} kernel status {st}")
+        n = int(r["path_len"][0, k])
+        cells = r["path"][0, k, :n].cpu().numpy()
+        path = [(int(c) // (Y * Z), (int(c) // Z) % Y, int(c) % Z) for c in cells]
+        self.EXPAND = [None] * int(r["n_expanded"][0, k])
+        return float(r["cost"][0, k]), path, self.EXPAND
+
+    def plan(self) -> tuple:
+        """(cost, path start->goal, EXPAND) (lpa_star3d.py:78-82); (cost, [], EXPAND) when the greedy
+        extraction finds no path.  EXPAND holds len(EXPAND) placeholders (the node objects are not
+        materialised).  A second plan() without changes expands nothing and keeps EXPAND, as there."""
+        if self._occ0 is None:
+            self._occ0 = self.env.occupancy()
+            return self._call()
+        # a no-op round: computeShortestPath on the kept state; plan() does not clear EXPAND
+        prev = list(self.EXPAND)
+        self._changes.append((-1, -1, -1, 0))
+        cost, path, new = self._call()
+        self.EXPAND = prev + new
+        return cost, path, self.EXPAND
+
+    def apply_change(self, coord: tuple, blocked=None) -> tuple:
+        """Toggle / set the voxel and re-plan incrementally (lpa_star3d.py:93-124)."""
+        if self._occ0 is None:
+            self.plan()
+        c = tuple(int(v) for v in coord)
+        if blocked is None:
+            if c in self.obstacles:
+                self.obstacles.remove(c)
+            else:
+                self.obstacles.add(c)
+        elif blocked:
+            self.obstacles.add(c)
+        elif c in self.obstacles:
+            self.obstacles.remove(c)
+        self.env.update(self.obstacles)
+        self._changes.append((c[0], c[1], c[2], 0 if blocked is None else (1 if blocked else 2)))
+        return self._call()
+
+    @staticmethod
+    def plan_batch(occ, starts, goals, changes=None, **kw):
+        return batch.lpastar3d_batch(occ, starts, goals, changes, **kw)

@@ -1082,12 +1082,101 @@ def sec_dstar_onpress(n=48, npress=4):
     print("dstar_onpress", len(res), "cases;", {k: kinds.count(k) for k in set(kinds)})
 
 
+# ----------------------------------------------------------------------------------------------
+# LPAStar3D plan + apply_change (lpa_star3d.py:78-124) -- SURVEY.md §8(f) rank 3
+def run_lpastar3d(args):
+    occ, start, goal, changes = args
+    pmp = import_reference()
+    X, Y, Z = occ.shape
+    env = pmp.Grid3D(X, Y, Z)
+    env.update({(int(a), int(b), int(c)) for a, b, c in np.argwhere(occ)})
+    p = pmp.LPAStar3D(tuple(start), tuple(goal), env)
+    enc = lambda t: (t[0] * Y + t[1]) * Z + t[2]  # noqa: E731
+    cost, path, expand = p.plan()
+    out = dict(cost=[float(cost)], path=[[enc(t) for t in path]], nexp=[len(expand)])
+    for (x, y, z, mode) in changes:
+        blocked = None if mode == 0 else (mode == 1)
+        cost, path, expand = p.apply_change((int(x), int(y), int(z)), blocked)
+        out["cost"].append(float(cost))
+        out["path"].append([enc(t) for t in path])
+        out["nexp"].append(len(expand))
+    close_figs()
+    return out
+
+
+def sec_lpastar3d(n_per=8, nr=4):
+    from python_motion_planning_amd import workloads as wl
+
+    rng = np.random.default_rng(5151)
+    cases = []
+    for name in wl.SCENARIOS_3D:
+        for j in range(n_per):
+            X, Y, Z = (21, 15, 11) if j % 4 else (26, 20, 16)
+            seed = int(rng.integers(1000))
+            s, g = wl.bench3d_query(seed, X, Y, Z)
+            if j == 7 and name == "empty":
+                g = s  # start == goal: map[goal] overwrites map[start] (lpa_star3d.py:62-63)
+            o = wl.SCENARIOS_3D[name](X, Y, Z)
+            wl.carve_safety_bubble(o, s, 2 if X == 21 else 1)
+            wl.carve_safety_bubble(o, g, 2 if X == 21 else 1)
+            cases.append([o, s, g, None])
+    res = []
+    with Pool(8) as pool:
+        first = pool.map(run_lpastar3d, [(c[0], c[1], c[2], []) for c in cases])
+        jobs = []
+        for c, f in zip(cases, first):
+            o, s, g, _ = c
+            X, Y, Z = o.shape
+            path = f["path"][0]
+            ch = []
+            for k in range(nr):
+                if k < 2 and len(path) > 3:  # block a voxel of the current path
+                    v = path[int(rng.integers(1, len(path) - 1))]
+                    ch.append([v // (Y * Z), (v // Z) % Y, v % Z, 1 if k == 0 else 0])
+                elif k == 2:  # free an obstacle voxel (the wall or a scenario block)
+                    obs = np.argwhere(o)
+                    v = obs[rng.integers(len(obs))]
+                    ch.append([int(v[0]), int(v[1]), int(v[2]), 2])
+                else:  # toggle anywhere (off-grid included)
+                    ch.append([int(rng.integers(-1, X + 1)), int(rng.integers(0, Y)), int(rng.integers(0, Z)), 0])
+            c[3] = ch
+            jobs.append(pool.apply_async(run_lpastar3d, (tuple(c),)))
+        keep = []
+        for c, j in zip(cases, jobs):
+            try:
+                res.append(j.get(timeout=180))
+                keep.append(c)
+            except Exception as e:  # noqa: BLE001
+                print("lpastar3d case dropped:", type(e).__name__, e)
+        cases = keep
+    dims = np.array([c[0].shape for c in cases], np.int32)
+    occ_flat, occ_off = ragged([np.packbits(c[0].ravel()) for c in cases], np.uint8)
+    path_flat, path_off = ragged([p for r in res for p in r["path"]])
+    np.savez_compressed(
+        os.path.join(HERE, "lpastar3d_runs.npz"), dims=dims, occ_bits=occ_flat, occ_off=occ_off,
+        start=np.array([c[1] for c in cases], np.int32), goal=np.array([c[2] for c in cases], np.int32),
+        changes=np.array([c[3] for c in cases], np.int32), cost=np.array([r["cost"] for r in res]),
+        nexp=np.array([r["nexp"] for r in res], np.int64), path=path_flat, path_off=path_off)
+    rows = []
+    with open(os.path.join(REF, "3d_pathfinding_results.csv"), newline="") as f:
+        rd = csv.reader(f)
+        next(rd)
+        for k, r in enumerate(rd):
+            if r[1] == "lpastar" and k % 10 == 0:
+                rows.append(dict(algo=r[1], scenario=r[0], cost=r[3], visited=int(r[4]),
+                                 start=list(eval(r[5])), goal=list(eval(r[6])), seed=int(r[7])))  # noqa: S307
+    with open(os.path.join(HERE, "lpastar3d_csv.json"), "w") as f:
+        json.dump(rows, f)
+    print("lpastar3d runs", len(res), "csv rows", len(rows), "empty paths",
+          sum(1 for r in res for p in r["path"] if not p))
+
+
 SECTIONS = dict(rrt=sec_rrt, mpc=sec_mpc, dwa=sec_dwa, local_plans=sec_local_plans, lqr=sec_lqr, astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
                 dstar=sec_dstar, astar3d=sec_astar3d,
                 graph2d=sec_graph2d, graph3d=sec_graph3d, theta3d=sec_theta3d, theta2d=sec_theta2d, lpa=sec_lpa,
                 dstarlite=lambda: sec_lpa(lite=True), lpa_replan=sec_lpa_replan,
                 dstarlite_replan=lambda: sec_lpa_replan(lite=True), dstar3d=sec_dstar3d,
-                dstar_onpress=sec_dstar_onpress)
+                dstar_onpress=sec_dstar_onpress, lpastar3d=sec_lpastar3d)
 
 if __name__ == "__main__":
     want = sys.argv[1:] or list(SECTIONS)

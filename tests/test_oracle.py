@@ -467,3 +467,29 @@ def test_dstar_onpress_against_reference():
                 assert res["cost"][r] == z["cost"][i][r], (i, r)
                 assert np.array_equal(res["paths"][r], seg(z["path"], z["path_off"], i * R + r)), (i, r)
     assert {"", "noop"} <= kinds
+
+
+def test_lpastar3d_published_csv():
+    """All 500 distinct LPAStar3D rows of 3d_pathfinding_results.csv: cost repr and len(EXPAND)."""
+    rows = load_json("lpastar3d_csv.json")
+    assert len(rows) == 500
+    for r in rows:
+        o, s, g = _csv3d_case(r)
+        res = O.lpastar3d(o, s, g)
+        assert repr(float(res["cost"][0])) == r["cost"], r
+        assert res["n_expanded"][0] == r["visited"], r
+
+
+def test_lpastar3d_apply_change_against_reference():
+    """plan() + 4 apply_change() calls per case (block on the path, toggle, free an obstacle, toggle
+    anywhere), replayed from reference runs: every call's cost, path and len(EXPAND)."""
+    n = 0
+    for i, occ, z in grid_cases("lpastar3d_runs.npz"):
+        res = O.lpastar3d(occ, z["start"][i], z["goal"][i], z["changes"][i])
+        R = z["changes"].shape[1] + 1
+        for r in range(R):
+            assert res["cost"][r] == z["cost"][i][r], (i, r)
+            assert res["n_expanded"][r] == z["nexp"][i][r], (i, r)
+            assert np.array_equal(res["paths"][r], seg(z["path"], z["path_off"], i * R + r)), (i, r)
+        n += 1
+    assert n >= 38
