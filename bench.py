@@ -600,6 +600,140 @@ def dstar_leg(args, torch, dist, world, rank):
     return out
 
 
+def dyn3d_leg(args, torch, dist, world, rank):
+    """The 3D incremental planners on the C5 workload (Grid3D(26,20,16) door, per-query safety
+    bubbles, random.seed(i) pairs): DStar3D (d_star3d.py:100-149, dstar3d.hip) and LPAStar3D
+    (lpa_star3d.py:78-124, lpa3d.hip), each as plan() alone and as a replanning session (plan() + 2
+    dynamic-obstacle calls: DStar3D.apply_dynamic_obstacles of 2 voxels, LPAStar3D.apply_change
+    blocking a voxel).  One timed step = one launch over the rank's queries."""
+    from python_motion_planning_amd import batch, workloads as wl
+
+    nq = args.dyn3d_queries
+    occ, s, g = wl.c5_workload(nq, first_seed=rank * nq)
+    X, Y, Z = occ.shape[1:]
+    rng = np.random.default_rng(40 + rank)
+    inner = rng.integers(1, [X - 1, Y - 1, Z - 1], size=(nq, 2, 2, 3)).astype(np.int32)
+    changes = np.concatenate([inner[:, :, 0, :], np.ones((nq, 2, 1), np.int32)], axis=2)
+    s_d, g_d = torch.as_tensor(s, device="cuda"), torch.as_tensor(g, device="cuda")
+    out = {}
+    for kind, rounds in (("dstar3d", None), ("dstar3d", inner), ("lpastar3d", None), ("lpastar3d", changes)):
+        rd = None if rounds is None else torch.as_tensor(rounds, device="cuda")
+
+        def run(i, kind=kind, rd=rd):
+            if kind == "dstar3d":
+                return batch.dstar3d_batch(occ, s_d, g_d, rd, path_cap=X * Y * Z + 1)
+            return batch.lpastar3d_batch(occ, s_d, g_d, rd, path_cap=X * Y * Z + 1)
+
+        r = run(0)
+        torch.cuda.synchronize()
+        nkey = "n_process" if kind == "dstar3d" else "n_expanded"
+        nexp = r[nkey].cpu().numpy()
+        st = r["status"].cpu().numpy()
+        elapsed, kern_ms = timed(torch, dist, run, args.dyn3d_steps)
+        R = 1 if rounds is None else rounds.shape[1] + 1
+        cpu = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            from oracle import oracle as O
+
+            th = cpu_threads()
+            ns = min(nq, 64 * th)
+            ref = O.graph3d_dynamic_batch(kind, occ[:ns], s[:ns], g[:ns], None if rounds is None else rounds[:ns],
+                                          nthreads=th)
+            assert np.array_equal(ref["n"], nexp[:ns]), f"GPU/oracle {kind} expansion-count mismatch"
+            assert np.array_equal(ref["cost"], r["cost"][:ns].cpu().numpy()), f"GPU/oracle {kind} cost mismatch"
+            reps, dt = timed_cpu(lambda i: O.graph3d_dynamic_batch(kind, occ[:ns], s[:ns], g[:ns],
+                                                                   None if rounds is None else rounds[:ns], nthreads=th),
+                                 2.0)
+            reps1, dt1 = timed_cpu(lambda i: O.graph3d_dynamic_batch(kind, occ[:16], s[:16], g[:16],
+                                                                     None if rounds is None else rounds[:16],
+                                                                     nthreads=1), 1.0)
+            cpu = {"value": ns * R * reps / dt, "unit": "plans/s", "cores": th, "kind": "port",
+                   "sample": f"first {ns} of the {nq} queries x {reps}, C restatement (list-semantics OPEN / U, "
+                             f"as the reference) with OpenMP over queries, {dt:.1f} s wall",
+                   "one_core": {"value": 16 * R * reps1 / dt1, "sample": f"16 queries x {reps1}, {dt1:.1f} s"}}
+        name = kind + ("" if rounds is None else "_replan")
+        out[name] = {
+            "metric": f"{kind} plans/sec on C5 (Grid3D 26x20x16 door, {nq} queries"
+                      + ("" if rounds is None else f", plan + {R - 1} dynamic-obstacle calls per session") + ")",
+            "value": nq * R * args.dyn3d_steps * world / elapsed, "unit": "plans/s", "queries_per_gpu": nq,
+            "steps": args.dyn3d_steps, "ms_per_step": elapsed / args.dyn3d_steps * 1e3, "kernel_ms_per_launch": kern_ms,
+            "dtype": "f64", "roofline": None,
+            "roofline_note": "latency-bound list machines (OPEN / U with Python-list semantics); no HBM or MFMA "
+                             "roofline applies",
+            "detail": {"expansions_per_launch": int(np.maximum(nexp, 0).sum()),
+                       "statuses": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))}},
+            "cpu_baseline": cpu}
+    return out
+
+
+def latency_leg(args, torch, dist, world, rank):
+    """Single-query latency of the drop-in AStar.plan() end to end (the
+    set -> bit-grid ingestion, the kernel, the path / CLOSED-Node marshalling): C1 (the README
+    query, 51x31, 579 expansions) and one C2 query (1024^2 grid given as a 213k-tuple obstacle set).
+    Median wall time of repeated calls, with the parts timed separately; the reference measured
+    14.8-26.8 ms for C1 and 2.76 s mean per C2 query in CPython."""
+    import python_motion_planning_amd as pmp
+    from python_motion_planning_amd import batch, workloads as wl
+
+    out = {}
+    cases = [("c1_readme", wl.readme_grid(), (5, 5), (45, 25), 50)]
+    occ2, s2, g2 = wl.c2_workload(nq=64)
+    # a C2 query of median length: the 32nd longest of 64 by octile distance
+    from python_motion_planning_amd import shard
+
+    k = int(np.argsort(shard.octile(s2, g2))[32])
+    cases.append(("c2_1024_one_query", occ2, tuple(int(v) for v in s2[k]), tuple(int(v) for v in g2[k]), 5))
+    for name, occ, s, g, reps in cases:
+        W, H = occ.shape
+        env = pmp.Grid(W, H)
+        env.update({(int(x), int(y)) for x, y in np.argwhere(occ)})
+        planner = pmp.AStar(s, g, env)
+        planner.plan()  # warm: library, context, allocator
+        torch.cuda.synchronize()
+        walls, ingest, kern, nodes = [], [], [], []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            cost, path, expand = planner.plan()
+            walls.append(time.perf_counter() - t0)
+        for _ in range(min(reps, 5)):
+            t0 = time.perf_counter()
+            words = env.occupancy_words()
+            t1 = time.perf_counter()
+            occ_bits = torch.as_tensor(words.view(np.int32), device="cuda")
+            r = batch.astar2d_batch((W, H), np.array([s]), np.array([g]), path_cap=W * H + 1, expand_cap=W * H,
+                                    occ_bits=occ_bits)
+            ne = int(r["n_expanded"][0])
+            t2 = time.perf_counter()
+            exp = r["expand"][0, :ne].cpu().numpy().astype(np.uint32)
+            planner._expand_nodes(exp, H)
+            t3 = time.perf_counter()
+            ingest.append(t1 - t0)
+            kern.append(t2 - t1)
+            nodes.append(t3 - t2)
+        cpu = None
+        if rank == 0 and not args.no_cpu_baseline:
+            from oracle import oracle as O
+
+            t0 = time.perf_counter()
+            n1 = 0
+            while True:
+                O.astar2d(occ, s, g)
+                n1 += 1
+                if time.perf_counter() - t0 > 1.0:
+                    break
+            cpu = {"value": (time.perf_counter() - t0) / n1 * 1e3, "unit": "ms", "cores": 1, "kind": "port",
+                   "sample": f"{n1} calls of the C restatement (oracle/pmp_oracle.c astar2d with the CLOSED order)"}
+        out[name] = {"metric": f"drop-in AStar.plan() latency, {name}", "value": float(np.median(walls)) * 1e3,
+                     "unit": "ms", "higher_is_better": False, "calls": reps, "expansions": len(expand),
+                     "parts_ms": {"set_to_bitgrid": float(np.median(ingest)) * 1e3,
+                                  "kernel_and_sync": float(np.median(kern)) * 1e3,
+                                  "closed_node_list": float(np.median(nodes)) * 1e3},
+                     "reference_python_ms": "14.8-26.8 (SURVEY.md §6)" if name == "c1_readme" else
+                                            "2760 mean per C2 query (SURVEY.md §6)",
+                     "cpu_baseline": cpu}
+    return out
+
+
 def track_leg(args, torch, dist, world, rank, kind):
     """LQR / MPC tracking (lqr.py:58-86 / mpc.py:66-94) for the C4 agents: one timed step = one launch
     running `iters` plan iterations of every agent (MPC at p = 30, m = 8, ADMM to 1e-9)."""
@@ -719,9 +853,11 @@ def main():
     ap.add_argument("--agents", type=int, default=256, help="C4 agents per GPU (control-step leg)")
     ap.add_argument("--control-steps", type=int, default=20, help="timed control steps")
     ap.add_argument("--workers", type=int, default=3072, help="persistent A* workers (waves) per launch")
-    ap.add_argument("--legs", default="dwa,rrt,astar3d,lqr,mpc,graphs,dstar",
-                    help="secondary legs to run (comma list of dwa, rrt, astar3d, lqr, mpc, graphs, dstar; 'none' "
-                         "for none)")
+    ap.add_argument("--legs", default="dwa,rrt,astar3d,lqr,mpc,graphs,dstar,dyn3d,latency",
+                    help="secondary legs to run (comma list of dwa, rrt, astar3d, lqr, mpc, graphs, dstar, dyn3d, "
+                         "latency; 'none' for none)")
+    ap.add_argument("--dyn3d-queries", type=int, default=8192, help="C5 queries per DStar3D / LPAStar3D launch")
+    ap.add_argument("--dyn3d-steps", type=int, default=2)
     ap.add_argument("--dstar-queries", type=int, default=1024, help="queries per D* launch (256^2 and 512^2 grids)")
     ap.add_argument("--dstar-steps", type=int, default=1)
     ap.add_argument("--theta-queries", type=int, default=4096, help="C2 queries per Theta* / Lazy Theta* 2D launch")
@@ -908,6 +1044,10 @@ def main():
         secondary.update(graphs_leg(args, torch, dist, world, rank))
     if "dstar" in legs:
         secondary.update(dstar_leg(args, torch, dist, world, rank))
+    if "dyn3d" in legs:
+        secondary.update(dyn3d_leg(args, torch, dist, world, rank))
+    if "latency" in legs:
+        secondary.update(latency_leg(args, torch, dist, world, rank))
 
     if rank == 0:
         out = {

@@ -772,3 +772,39 @@ def lpastar3d(occ: np.ndarray, start, goal, changes=None, heuristic: str = "eucl
                        path_cap, _p(plen, _i32p), int(max_exp))
     return dict(cost=cost, status=st, n_expanded=ne, path_len=plen,
                 paths=[path[r, : min(plen[r], path_cap)].copy() for r in range(nr + 1)])
+
+
+def graph3d_dynamic_batch(kind: str, occ, starts, goals, rounds=None, heuristic: str = "euclidean", nthreads: int = 0):
+    """OpenMP batch of the DStar3D (kind "dstar3d", rounds = blocks [nq, nr, nblk, 3]) or LPAStar3D
+    (kind "lpastar3d", rounds = changes [nq, nr, 4]) restatement over per-query [nq, X, Y, Z] or
+    shared [X, Y, Z] grids.  Returns cost / status / n [nq, nr + 1] (n = len(EXPAND))."""
+    L = lib()
+    if not getattr(L, "_g3db_set", False):
+        L.oracle_dstar3d_batch.restype = None
+        L.oracle_dstar3d_batch.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p, _i32p,
+                                           ctypes.c_int, _i32p, ctypes.c_int, ctypes.c_int, _dp, _i32p, _i64p,
+                                           ctypes.c_int]
+        L.oracle_lpastar3d_batch.restype = None
+        L.oracle_lpastar3d_batch.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, _i32p, _i32p, ctypes.c_int, _i32p, ctypes.c_int, _dp, _i32p,
+                                             _i64p, ctypes.c_int]
+        L._g3db_set = True
+    occ = np.ascontiguousarray(occ, dtype=np.uint8)
+    per_query = occ.ndim == 4
+    X, Y, Z = occ.shape[-3:]
+    s = np.ascontiguousarray(starts, np.int32).reshape(-1, 3)
+    g = np.ascontiguousarray(goals, np.int32).reshape(-1, 3)
+    nq = len(s)
+    rd = None if rounds is None else np.ascontiguousarray(rounds, np.int32)
+    nr = 0 if rd is None else rd.shape[1]
+    out = dict(cost=np.zeros((nq, nr + 1)), status=np.zeros((nq, nr + 1), np.int32), n=np.zeros((nq, nr + 1), np.int64))
+    if kind == "dstar3d":
+        nb = 0 if rd is None else rd.shape[2]
+        L.oracle_dstar3d_batch(_p(occ, _u8p), int(per_query), X, Y, Z, _p(s, _i32p), _p(g, _i32p), nq,
+                               _p(rd, _i32p) if rd is not None else None, nr, nb, _p(out["cost"], _dp),
+                               _p(out["status"], _i32p), _p(out["n"], _i64p), int(nthreads))
+    else:
+        L.oracle_lpastar3d_batch(_p(occ, _u8p), int(per_query), X, Y, Z, 1 if heuristic == "manhattan" else 0,
+                                 _p(s, _i32p), _p(g, _i32p), nq, _p(rd, _i32p) if rd is not None else None, nr,
+                                 _p(out["cost"], _dp), _p(out["status"], _i32p), _p(out["n"], _i64p), int(nthreads))
+    return out

@@ -2753,3 +2753,46 @@ int oracle_lpastar3d(const uint8_t* occ_in, int X, int Y, int Z, int heuristic, 
     free(S.geo.occ); free(S.g); free(S.rhs); free(S.U);
     return rc;
 }
+
+/* OpenMP batches of the DStar3D / LPAStar3D restatements over per-query grids occ[nq][X*Y*Z]
+ * (plan + nr rounds of changes; the bench's CPU baselines): per query and call cost, status,
+ * len(EXPAND) at [q * (nr + 1) + r]. */
+void oracle_dstar3d_batch(const uint8_t* occ, int per_query, int X, int Y, int Z, const int32_t* s, const int32_t* g,
+                          int nq, const int32_t* blocks, int nr, int nblk, double* cost, int32_t* status, int64_t* nproc,
+                          int nthreads)
+{
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+    const size_t nc = (size_t)X * Y * Z;
+#pragma omp parallel
+    {
+        int32_t* path = (int32_t*)malloc(sizeof(int32_t) * (nc + 1) * (size_t)(nr + 1));
+        int32_t* plen = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nr + 1));
+#pragma omp for schedule(dynamic, 4)
+        for (int q = 0; q < nq; q++)
+            oracle_dstar3d(occ + (per_query ? (size_t)q * nc : 0), X, Y, Z, s + 3 * q, g + 3 * q,
+                           blocks ? blocks + (size_t)q * nr * nblk * 3 : NULL, nr, nblk, cost + (size_t)q * (nr + 1),
+                           status + (size_t)q * (nr + 1), nproc + (size_t)q * (nr + 1), path, (int)nc + 1, plen, 0);
+        free(path);
+        free(plen);
+    }
+}
+
+void oracle_lpastar3d_batch(const uint8_t* occ, int per_query, int X, int Y, int Z, int heuristic, const int32_t* s,
+                            const int32_t* g, int nq, const int32_t* changes, int nr, double* cost, int32_t* status,
+                            int64_t* nexp, int nthreads)
+{
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+    const size_t nc = (size_t)X * Y * Z;
+#pragma omp parallel
+    {
+        int32_t* path = (int32_t*)malloc(sizeof(int32_t) * (nc + 1) * (size_t)(nr + 1));
+        int32_t* plen = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nr + 1));
+#pragma omp for schedule(dynamic, 4)
+        for (int q = 0; q < nq; q++)
+            oracle_lpastar3d(occ + (per_query ? (size_t)q * nc : 0), X, Y, Z, heuristic, s + 3 * q, g + 3 * q,
+                             changes ? changes + (size_t)q * nr * 4 : NULL, nr, cost + (size_t)q * (nr + 1),
+                             status + (size_t)q * (nr + 1), nexp + (size_t)q * (nr + 1), path, (int)nc + 1, plen, 0);
+        free(path);
+        free(plen);
+    }
+}

@@ -11,6 +11,8 @@ from math import sqrt
 
 import numpy as np
 
+from . import _hostio  # native set -> bit-grid marshalling (csrc/hostio.c); no Python fallback
+
 
 class Node:
     """utils/environment/node.py:8-84 -- search node (current, parent, g, h)."""
@@ -147,15 +149,19 @@ class Grid(Env):
         return cKDTree(np.array(list(self.obstacles)))
 
     # ---- kernel-facing views ------------------------------------------------------------------
+    def occupancy_words(self) -> np.ndarray:
+        """The kernels' bit-packed x-major occupancy (uint32 words, bit c of word c >> 5 for cell
+        c = x*H + y) of the in-range obstacle cells, from one native pass over the set."""
+        W, H = self.x_range, self.y_range
+        words = np.empty((W * H + 31) // 32, np.uint32)
+        _hostio.set_to_words(self.obstacles or (), (W, H), words)
+        return words
+
     def occupancy(self) -> np.ndarray:
         """uint8 [x_range, y_range], occ[x, y] = 1 for (x, y) in obstacles (in-range cells)."""
-        occ = np.zeros((self.x_range, self.y_range), np.uint8)
-        if self.obstacles:
-            a = np.fromiter((c for t in self.obstacles for c in t), np.int64,
-                            count=2 * len(self.obstacles)).reshape(-1, 2)
-            m = (a[:, 0] >= 0) & (a[:, 0] < self.x_range) & (a[:, 1] >= 0) & (a[:, 1] < self.y_range)
-            occ[a[m, 0], a[m, 1]] = 1
-        return occ
+        W, H = self.x_range, self.y_range
+        bits = np.unpackbits(self.occupancy_words().view(np.uint8), bitorder="little")
+        return bits[: W * H].reshape(W, H)
 
     @classmethod
     def from_occupancy(cls, occ: np.ndarray) -> "Grid":
@@ -238,14 +244,18 @@ class Grid3D(Env3D):
     def update(self, obstacles):
         self.obstacles = obstacles
 
+    def occupancy_words(self) -> np.ndarray:
+        """Bit-packed occupancy (cell (x*Y + y)*Z + z) of the in-range obstacle voxels (native pass)."""
+        X, Y, Z = self.x_range, self.y_range, self.z_range
+        words = np.empty((X * Y * Z + 31) // 32, np.uint32)
+        _hostio.set_to_words(self.obstacles or (), (X, Y, Z), words)
+        return words
+
     def occupancy(self) -> np.ndarray:
-        occ = np.zeros((self.x_range, self.y_range, self.z_range), np.uint8)
-        if self.obstacles:
-            a = np.fromiter((c for t in self.obstacles for c in t), np.int64,
-                            count=3 * len(self.obstacles)).reshape(-1, 3)
-            m = np.all((a >= 0) & (a < np.array([self.x_range, self.y_range, self.z_range])), axis=1)
-            occ[a[m, 0], a[m, 1], a[m, 2]] = 1
-        return occ
+        """uint8 [x_range, y_range, z_range] of the in-range obstacle voxels."""
+        X, Y, Z = self.x_range, self.y_range, self.z_range
+        bits = np.unpackbits(self.occupancy_words().view(np.uint8), bitorder="little")
+        return bits[: X * Y * Z].reshape(X, Y, Z)
 
 
 class Map3D(Env3D):

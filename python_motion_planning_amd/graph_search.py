@@ -6,12 +6,35 @@ plan() keeps the reference's signature and return convention; plan_batch() is th
 from __future__ import annotations
 
 import math
+from collections.abc import Sequence
 
 import numpy as np
 
 from . import batch
 from .env import Grid, Node
 from .planner import Planner
+
+
+class LazyExpand(Sequence):
+    """The CLOSED Node list of a plan, built on first access (AStar.lazy_expand = True): len() is
+    known without building it."""
+
+    def __init__(self, build, n: int) -> None:
+        self._build, self._n, self._nodes = build, n, None
+
+    def _get(self) -> list:
+        if self._nodes is None:
+            self._nodes = self._build()
+        return self._nodes
+
+    def __len__(self) -> int:
+        return self._n
+
+    def __getitem__(self, i):
+        return self._get()[i]
+
+    def __eq__(self, other) -> bool:
+        return list(self._get()) == list(other)
 
 
 class GraphSearcher(Planner):
@@ -53,47 +76,56 @@ class AStar(GraphSearcher):
     def __str__(self) -> str:
         return "A*"
 
+    #: return the CLOSED Node list lazily (materialised on first use); the reference builds it eagerly
+    lazy_expand = False
+
     def plan(self) -> tuple:
-        """Returns (cost, path goal->start, expand list of Node) or ([], [], []) (a_star.py:39-83)."""
-        occ = self.env.occupancy()
-        W, H = occ.shape
-        r = batch.astar2d_batch(occ, np.array([self.start.current]), np.array([self.goal.current]),
-                                self.heuristic_type, path_cap=W * H + 1, expand_cap=W * H, algo=self._algo)
-        st = int(r["status"][0])
+        """Returns (cost, path goal->start, expand list of Node) or ([], [], []) (a_star.py:39-83).
+
+        The Grid's obstacle set is bit-packed natively (no per-call Python loop); the path and
+        CLOSED-record buffers are sized for the common case and the query re-runs with exact sizes
+        only when one overflows."""
+        import torch
+
+        W, H = self.env.x_range, self.env.y_range
+        occ_bits = torch.as_tensor(self.env.occupancy_words().view(np.int32), device="cuda")
+        s, g = np.array([self.start.current]), np.array([self.goal.current])
+        path_cap, expand_cap = min(W * H + 1, 1 << 14), min(W * H, 1 << 18)
+        while True:
+            r = batch.astar2d_batch((W, H), s, g, self.heuristic_type, path_cap=path_cap, expand_cap=expand_cap,
+                                    algo=self._algo, occ_bits=occ_bits)
+            st, nexp, plen = (int(v) for v in torch.stack([r["status"][0], r["n_expanded"][0],
+                                                            r["path_len"][0]]).cpu().tolist())
+            if st == 2 or nexp > expand_cap:  # PMP_PATH_OVERFLOW / truncated CLOSED records: exact sizes
+                path_cap, expand_cap = max(path_cap, plen), max(expand_cap, nexp)
+                continue
+            break
         if st != 0:
             if st == 1:
                 return [], [], []
             raise RuntimeError(f"{self} kernel status {st}")
-        plen = int(r["path_len"][0])
         cells = r["path"][0, :plen].cpu().numpy()
-        nexp = int(r["n_expanded"][0])
         exp = r["expand"][0, :nexp].cpu().numpy().astype(np.uint32)
         path = [(int(c) // H, int(c) % H) for c in cells]
         cost = 0
         for a, b in zip(path[:-1], path[1:]):
             cost += math.hypot(b[0] - a[0], b[1] - a[1])
+        if self.lazy_expand:
+            return cost, path, LazyExpand(lambda: self._expand_nodes(exp, H), nexp)
         return cost, path, self._expand_nodes(exp, H)
 
     def _expand_nodes(self, exp: np.ndarray, H: int) -> list:
         """Rebuild the reference's CLOSED Node objects (current, parent, g, h) from the kernel's
-        closure-ordered (cell | parent_dir << 28) records; g is re-accumulated exactly as
-        Node.__add__ does (node.py:39-41)."""
+        closure-ordered (cell | parent_dir << 28) records, natively (csrc/hostio.c): g accumulated
+        with Python's `+` on the motion costs as Node.__add__ does (node.py:39-41), h as
+        GraphSearcher.h; Dijkstra's h = 0 (dijkstra.py:74), GBFS's g = 0 (gbfs.py:75)."""
+        from ._hostio import expand_nodes
+
+        manhattan = self.heuristic_type == "manhattan"
+        kind = {"astar": 1 if manhattan else 0, "dijkstra": 2, "gbfs": 4 if manhattan else 3}[self._algo]
         motions = self.env.motions
-        nodes, gmap = [], {}
-        for e in exp.tolist():
-            cell, d = e & 0x0FFFFFFF, e >> 28
-            cur = (cell // H, cell % H)
-            if d == 8:
-                node = Node(cur, cur, 0, 0)
-            else:
-                m = motions[d]
-                par = (cur[0] - m.x, cur[1] - m.y)
-                g = 0 if self._algo == "gbfs" else gmap[par] + m.g  # gbfs.py:75: node_n.g = 0
-                h = 0 if self._algo == "dijkstra" else self.h(Node(cur), self.goal)  # dijkstra.py:74
-                node = Node(cur, par, g, h)
-            gmap[cur] = node.g
-            nodes.append(node)
-        return nodes
+        return expand_nodes(np.ascontiguousarray(exp, np.uint32), len(exp), H, [(m.x, m.y) for m in motions],
+                            [m.g for m in motions], self.goal.current, kind, Node)
 
     @classmethod
     def plan_batch(cls, occ: np.ndarray, starts, goals, heuristic_type: str = "euclidean", **kw):

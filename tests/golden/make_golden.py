@@ -1171,12 +1171,36 @@ def sec_lpastar3d(n_per=8, nr=4):
           sum(1 for r in res for p in r["path"] if not p))
 
 
+# ----------------------------------------------------------------------------------------------
+# the CLOSED Node objects AStar / Dijkstra / GBFS return (a_star.py:64): current, parent, g, h with
+# their Python types (g stays int while every step is straight) -- pins the native marshalling
+def sec_astar_nodes():
+    from python_motion_planning_amd import workloads as wl
+
+    pmp = import_reference()
+    occ = wl.readme_grid()
+    env = pmp.Grid(51, 31)
+    env.update(obstacles_of(occ))
+    out = []
+    for name, cls in (("astar", pmp.AStar), ("dijkstra", pmp.Dijkstra), ("gbfs", pmp.GBFS)):
+        for heur in ("euclidean", "manhattan"):
+            cost, path, expand = cls((5, 5), (45, 25), env, heur).plan()
+            out.append(dict(algo=name, heuristic=heur, cost=repr(cost),
+                            nodes=[[list(n.current), list(n.parent), repr(n.g), type(n.g).__name__, repr(n.h),
+                                    type(n.h).__name__] for n in expand]))
+    close_figs()
+    with open(os.path.join(HERE, "astar_nodes.json"), "w") as f:
+        json.dump(out, f)
+    print("astar nodes", [(o["algo"], o["heuristic"], len(o["nodes"])) for o in out])
+
+
 SECTIONS = dict(rrt=sec_rrt, mpc=sec_mpc, dwa=sec_dwa, local_plans=sec_local_plans, lqr=sec_lqr, astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
                 dstar=sec_dstar, astar3d=sec_astar3d,
                 graph2d=sec_graph2d, graph3d=sec_graph3d, theta3d=sec_theta3d, theta2d=sec_theta2d, lpa=sec_lpa,
                 dstarlite=lambda: sec_lpa(lite=True), lpa_replan=sec_lpa_replan,
                 dstarlite_replan=lambda: sec_lpa_replan(lite=True), dstar3d=sec_dstar3d,
-                dstar_onpress=sec_dstar_onpress, lpastar3d=sec_lpastar3d)
+                dstar_onpress=sec_dstar_onpress, lpastar3d=sec_lpastar3d,
+                astar_nodes=sec_astar_nodes)
 
 if __name__ == "__main__":
     want = sys.argv[1:] or list(SECTIONS)
