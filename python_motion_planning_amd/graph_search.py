@@ -85,8 +85,9 @@ class AStar(GraphSearcher):
         The Grid's obstacle set is bit-packed natively (no per-call Python loop); the path and
         CLOSED-record buffers are sized for the common case and the query re-runs with exact sizes
         only when one overflows."""
-        import torch
+        from . import _lib
 
+        torch = _lib.device_check()  # no CPU fallback: raises PMPError without a HIP device
         W, H = self.env.x_range, self.env.y_range
         occ_bits = torch.as_tensor(self.env.occupancy_words().view(np.int32), device="cuda")
         s, g = np.array([self.start.current]), np.array([self.goal.current])
