@@ -126,7 +126,7 @@ class AStar(GraphSearcher):
         kind = {"astar": 1 if manhattan else 0, "dijkstra": 2, "gbfs": 4 if manhattan else 3}[self._algo]
         motions = self.env.motions
         return expand_nodes(np.ascontiguousarray(exp, np.uint32), len(exp), H, [(m.x, m.y) for m in motions],
-                            [m.g for m in motions], self.goal.current, kind, Node)
+                            [m.g for m in motions], tuple(int(v) for v in self.goal.current), kind, Node)
 
     @classmethod
     def plan_batch(cls, occ: np.ndarray, starts, goals, heuristic_type: str = "euclidean", **kw):
