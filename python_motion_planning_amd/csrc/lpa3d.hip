@@ -35,6 +35,13 @@ __device__ __constant__ int8_t c_m[26][3] = {
     {-1, 0, 1}, {-1, 1, 1}, {0, 1, 1}, {1, 1, 1}, {1, 0, 1}, {1, -1, 1}, {0, -1, 1}, {-1, -1, 1},
     {-1, 0, -1}, {-1, 1, -1}, {0, 1, -1}, {1, 1, -1}, {1, 0, -1}, {1, -1, -1}, {0, -1, -1}, {-1, -1, -1}};
 
+// the same table as a compile-time constant (indexed only by unrolled loop counters)
+constexpr int8_t kM[26][3] = {
+    {-1, 0, 0}, {-1, 1, 0}, {0, 1, 0}, {1, 1, 0}, {1, 0, 0}, {1, -1, 0}, {0, -1, 0}, {-1, -1, 0},
+    {0, 0, 1}, {0, 0, -1},
+    {-1, 0, 1}, {-1, 1, 1}, {0, 1, 1}, {1, 1, 1}, {1, 0, 1}, {1, -1, 1}, {0, -1, 1}, {-1, -1, 1},
+    {-1, 0, -1}, {-1, 1, -1}, {0, 1, -1}, {1, 1, -1}, {1, 0, -1}, {1, -1, -1}, {0, -1, -1}, {-1, -1, -1}};
+
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) int32_t lds_i32;
 typedef __attribute__((address_space(3))) double lds_f64;
@@ -46,8 +53,19 @@ __device__ __forceinline__ bool key_lt(double a1, double a2, double b1, double b
     return a1 < b1 || (a1 == b1 && a2 < b2);
 }
 
+// c / d for 0 <= c < 2^24 through an f32 reciprocal (error <= 1 before the correction): a handful
+// of instructions instead of an integer division
+__device__ __forceinline__ int fdiv(int c, int d, float inv)
+{
+    int q = (int)((float)c * inv);
+    const int r = c - q * d;
+    q += (r >= d) - (r < 0);
+    return q;
+}
+
 struct Geo {
     int X, Y, Z;
+    float invY, invZ;
     __device__ __forceinline__ bool in(int x, int y, int z) const
     {
         return (unsigned)x < (unsigned)X && (unsigned)y < (unsigned)Y && (unsigned)z < (unsigned)Z;
@@ -55,11 +73,18 @@ struct Geo {
     __device__ __forceinline__ int id(int x, int y, int z) const { return (x * Y + y) * Z + z; }
     __device__ __forceinline__ void xyz(int c, int& x, int& y, int& z) const
     {
-        z = c % Z;
-        const int r = c / Z;
-        y = r % Y;
-        x = r / Y;
+        const int r = fdiv(c, Z, invZ);
+        z = c - r * Z;
+        x = fdiv(r, Y, invY);
+        y = r - x * Y;
     }
+};
+
+// 125-bit masks over the 5x5x5 block around a centre (bit (x*5 + y)*5 + z of block coordinates
+// 0..4), wave-uniform: "in the map" and "an obstacle"
+struct Mask125 {
+    uint64_t lo, hi;
+    __device__ __forceinline__ bool at(int b) const { return b < 64 ? (lo >> b) & 1ull : (hi >> (b - 64)) & 1ull; }
 };
 
 // working occupancy (apply_change edits it): LDS when it fits, else the worker's HBM copy;
@@ -107,9 +132,11 @@ struct UList {
     double* g2;
     int cap;
     int n;
+    // SP = false: every position touched is < cap (pure LDS code, no vector-memory waits)
+    template <bool SP>
     __device__ __forceinline__ void ld(int k, int32_t& c, double& a, double& b) const
     {
-        if (k < cap) {
+        if (!SP || k < cap) {
             c = lc[k];
             a = l1[k];
             b = l2[k];
@@ -119,9 +146,10 @@ struct UList {
             b = g2[k - cap];
         }
     }
+    template <bool SP>
     __device__ __forceinline__ void st(int k, int32_t c, double a, double b) const
     {
-        if (k < cap) {
+        if (!SP || k < cap) {
             lc[k] = c;
             l1[k] = a;
             l2[k] = b;
@@ -153,6 +181,13 @@ struct L3 {
     int64_t nexp;
     int64_t npush;
     int maxn;
+    double goal_g, goal_rhs;  // the goal's g / rhs, kept in registers for the termination test
+#ifdef PMP_STAMPS
+    uint64_t cyc[4];  // diagnostic build: min scan, g block + rhs minima, membership scan, updates
+#define LSTAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define LSTAMP(v)
+#endif
 
     __device__ __forceinline__ double hval(int x, int y, int z) const
     {
@@ -162,7 +197,8 @@ struct L3 {
 
     // U.remove(U[i]): the tail moves left one slot; 4 elements per lane per round (all loads of a
     // round before its stores; a round never reads what an earlier round wrote)
-    __device__ __forceinline__ void remove_at(int i, Track& t)
+    template <bool SP>
+    __device__ __forceinline__ void remove_at_t(int i)
     {
         for (int base = i; base < U.n - 1; base += 256) {
             int32_t c[4];
@@ -170,16 +206,21 @@ struct L3 {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int k = base + lane + 64 * j;
-                if (k < U.n - 1) U.ld(k + 1, c[j], a[j], b[j]);
+                if (k < U.n - 1) U.template ld<SP>(k + 1, c[j], a[j], b[j]);
             }
             wsync();
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int k = base + lane + 64 * j;
-                if (k < U.n - 1) U.st(k, c[j], a[j], b[j]);
+                if (k < U.n - 1) U.template st<SP>(k, c[j], a[j], b[j]);
             }
             wsync();
         }
+    }
+    __device__ __forceinline__ void remove_at(int i, Track& t)
+    {
+        if (U.n <= U.cap) remove_at_t<false>(i);
+        else remove_at_t<true>(i);
         U.n -= 1;
         if (t.pos == i) t.pos = -1;
         else if (t.pos > i) t.pos -= 1;
@@ -188,22 +229,29 @@ struct L3 {
     // heapq.heappush(U, node): lane j (1..D) loads ancestor j of position n; the ancestors that move
     // down are the run of "new < ancestor" from the parent up (_siftdown stops at the first one that
     // is not greater).  `me` = this lane tracks the pushed voxel.
-    __device__ __forceinline__ void push(int32_t c, double k1, double k2, Track& t, bool me)
+    template <bool SP>
+    __device__ __forceinline__ int push_t(int32_t c, double k1, double k2, uint32_t np1, int& s)
     {
-        const uint32_t np1 = (uint32_t)U.n + 1u;
         const int D = 31 - __clz((int)np1);
         const bool on = lane >= 1 && lane <= D;
         const int aj = on ? (int)(np1 >> lane) - 1 : 0;
         int32_t ac = 0;
         double a1 = 0.0, a2 = 0.0;
-        if (on) U.ld(aj, ac, a1, a2);
+        if (on) U.template ld<SP>(aj, ac, a1, a2);
         const uint64_t lt = ballot(on && key_lt(k1, k2, a1, a2));
-        const int s = __builtin_ctzll(~(lt >> 1));  // trailing ones from lane 1
+        s = __builtin_ctzll(~(lt >> 1));  // trailing ones from lane 1
         wsync();
-        if (on && lane <= s) U.st((int)(np1 >> (lane - 1)) - 1, ac, a1, a2);
+        if (on && lane <= s) U.template st<SP>((int)(np1 >> (lane - 1)) - 1, ac, a1, a2);
         const int dst = (int)(np1 >> s) - 1;
-        if (lane == 0) U.st(dst, c, k1, k2);
+        if (lane == 0) U.template st<SP>(dst, c, k1, k2);
         wsync();
+        return dst;
+    }
+    __device__ __forceinline__ void push(int32_t c, double k1, double k2, Track& t, bool me)
+    {
+        const uint32_t np1 = (uint32_t)U.n + 1u;
+        int s;
+        const int dst = U.n < U.cap ? push_t<false>(c, k1, k2, np1, s) : push_t<true>(c, k1, k2, np1, s);
         // tracked positions: ancestor j (1..s) -> ancestor j-1
         if (t.pos >= 0) {
             const int p1 = t.pos + 1;
@@ -218,9 +266,12 @@ struct L3 {
 
     // updateVertex over the 3x3x3 block of `center` (:147-158): optionally the centre first (its own
     // updateVertex), then getNeighbor(center) in motion order.  The 5x5x5 g block is staged first;
-    // g does not change inside.
-    __device__ void update_block(int center, bool do_center)
+    // g does not change inside.  expand: the centre was just popped -- computeShortestPath's
+    // over/under-consistency step (:136-141) runs here on the staged g / rhs: g = rhs, or g = inf
+    // and the centre's own updateVertex.  The g / rhs stores go out after the block's updates.
+    __device__ void update_block(int center, bool do_center, bool expand = false)
     {
+        LSTAMP(t0);
         int cx, cy, cz;
         geo.xyz(center, cx, cy, cz);
         // ---- stage g of the 5x5x5 block (inf outside the map)
@@ -234,6 +285,27 @@ struct L3 {
                 cube[b] = v;
             }
         }
+        // ---- block masks: in the map / obstacle, as wave-uniform bits
+        Mask125 inm, obm;
+        {
+            bool i0 = false, o0 = false, i1 = false, o1 = false;
+            {
+                const int b = lane;
+                const int x = cx + b / 25 - 2, y = cy + (b / 5) % 5 - 2, z = cz + b % 5 - 2;
+                i0 = geo.in(x, y, z);
+                o0 = i0 && occ.at(x, y, z);
+            }
+            if (lane < 61) {
+                const int b = lane + 64;
+                const int x = cx + b / 25 - 2, y = cy + (b / 5) % 5 - 2, z = cz + b % 5 - 2;
+                i1 = geo.in(x, y, z);
+                o1 = i1 && occ.at(x, y, z);
+            }
+            inm.lo = ballot(i0);
+            inm.hi = ballot(i1);
+            obm.lo = ballot(o0);
+            obm.hi = ballot(o1);
+        }
         // ---- this lane's block voxel: lanes 0..25 = motion m, lane 26 = the centre
         const int m = lane < 26 ? lane : 0;
         const int dx = lane < 26 ? c_m[m][0] : 0, dy = lane < 26 ? c_m[m][1] : 0, dz = lane < 26 ? c_m[m][2] : 0;
@@ -245,30 +317,63 @@ struct L3 {
         double rv = 0.0;
         if (mine) rv = rhs[P];
         wsync();
+        double gnew = 0.0;  // the popped centre's new g (expand)
+        if (expand) {
+            const double g0 = cube[62], r0 = rl_f64(rv, 26);
+            const bool over = g0 > r0;
+            gnew = over ? r0 : kInf;
+            do_center = !over;
+            if (lane == 0) cube[62] = gnew;
+            if (center == goal) goal_g = gnew;
+            wsync();
+        }
         // ---- rhs of the lane's voxel: min over its getNeighbor of g + cost(n, voxel) (:150-153)
         if (mine && P != start) {
+            // block coordinates of the voxel (1..3) and of its neighbours (0..4): every occupancy
+            // test of isCollision(n, voxel) falls inside the block
+            const int ax = dx + 2, ay = dy + 2, az = dz + 2;
+            const bool pblk = obm.at((ax * 5 + ay) * 5 + az);
             double best = kInf;
             bool any = false;
+#pragma unroll
             for (int u = 0; u < 26; u++) {
-                const int qx = px + c_m[u][0], qy = py + c_m[u][1], qz = pz + c_m[u][2];
-                if (!geo.in(qx, qy, qz) || occ.at(qx, qy, qz)) continue;
+                const int ex = kM[u][0], ey = kM[u][1], ez = kM[u][2];  // compile-time after unrolling
+                const int qx = ax + ex, qy = ay + ey, qz = az + ez;
+                const int qb = (qx * 5 + qy) * 5 + qz;
+                if (!inm.at(qb) || obm.at(qb)) continue;  // getNeighbor: in the map, endpoint free
                 any = true;
-                const double gq = cube[(qx - cx + 2) * 25 + (qy - cy + 2) * 5 + (qz - cz + 2)];
-                const double c = occ.coll(qx, qy, qz, px, py, pz) ? kInf
-                                                                  : dist_unit(px - qx, py - qy, pz - qz);
-                best = fmin(best, gq + c);
+                // isCollision(n = q, voxel): the voxel blocked, or the face cells next to q toward it
+                const int mx = -ex, my = -ey, mz = -ez;  // q -> voxel
+                const int ch = (mx != 0) + (my != 0) + (mz != 0);
+                bool c = pblk;
+                if (!c && ch == 2) {
+                    if (mx != 0 && my != 0) c = obm.at(((qx + mx) * 5 + qy) * 5 + qz) || obm.at((qx * 5 + qy + my) * 5 + qz);
+                    else if (mx != 0 && mz != 0) c = obm.at(((qx + mx) * 5 + qy) * 5 + qz) || obm.at((qx * 5 + qy) * 5 + qz + mz);
+                    else c = obm.at((qx * 5 + qy + my) * 5 + qz) || obm.at((qx * 5 + qy) * 5 + qz + mz);
+                } else if (!c && ch == 3) {
+                    c = obm.at(((qx + mx) * 5 + qy) * 5 + qz) || obm.at((qx * 5 + qy + my) * 5 + qz) ||
+                        obm.at((qx * 5 + qy) * 5 + qz + mz);
+                }
+                const double gq = cube[qb];
+                best = fmin(best, gq + (c ? kInf : (ch == 1 ? 1.0 : (ch == 2 ? 1.4142135623730951 : 1.7320508075688772))));
             }
             rv = any ? best : kInf;
         }
         const double gv = mine ? cube[(dx + 2) * 25 + (dy + 2) * 5 + (dz + 2)] : 0.0;
+        const double hv = mine ? hval(px, py, pz) : 0.0;  // calculateKey's h, lane-parallel
+        LSTAMP(t1);
         // ---- U positions of the 27 voxels: one scan
         Track t;
         t.pos = -1;
+        const bool usp = U.n > U.cap;
         for (int base = 0; base < U.n; base += 64) {
             const int k = base + lane;
             int32_t c = -1;
             double a, b;
-            if (k < U.n) U.ld(k, c, a, b);
+            if (k < U.n) {
+                if (usp) U.template ld<true>(k, c, a, b);
+                else U.template ld<false>(k, c, a, b);
+            }
             // block index of c relative to the centre, or -1
             int bi = -1;
             if (c >= 0) {
@@ -286,6 +391,7 @@ struct L3 {
                 if (lane <= 26 && myb == hb) t.pos = base + l;
             }
         }
+        LSTAMP(t2);
         // ---- updateVertex in the reference's order: the centre (if asked), then each neighbour
         const uint64_t nbm = ballot(is_nb);
         const int nsteps = (do_center ? 1 : 0) + __popcll(nbm);
@@ -301,17 +407,27 @@ struct L3 {
             const int Pw = __builtin_amdgcn_readlane(P, who);
             const double rw = rl_f64(rv, who);
             const double gw = rl_f64(gv, who);
-            if (Pw != start && lane == 0) rhs[Pw] = rw;
+            if (Pw == goal) goal_rhs = rw;
             const int pw = __builtin_amdgcn_readlane(t.pos, who);
             if (pw >= 0) remove_at(pw, t);
             if (gw != rw) {
-                int x, y, z;
-                geo.xyz(Pw, x, y, z);
                 const double mn = gw < rw ? gw : rw;
-                push(Pw, mn + hval(x, y, z), mn, t, lane == who);
+                push(Pw, mn + rl_f64(hv, who), mn, t, lane == who);
             }
         }
+        // deferred stores: the updated voxels' rhs (the start keeps its own), the centre's new g
+        {
+            const bool upd = mine && P != start && (is_nb || (lane == 26 && do_center));
+            if (upd) rhs[P] = rv;
+            if (expand && lane == 0) g[center] = gnew;
+        }
         wsync();
+#ifdef PMP_STAMPS
+        LSTAMP(t3);
+        cyc[1] += t1 - t0;
+        cyc[2] += t2 - t1;
+        cyc[3] += t3 - t2;
+#endif
     }
 };
 
@@ -327,7 +443,7 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
     const int lane = lane_id();
     const int ncell = X * Y * Z;
     L3 S;
-    S.geo = Geo{X, Y, Z};
+    S.geo = Geo{X, Y, Z, 1.0f / (float)Y, 1.0f / (float)Z};
     S.lane = lane;
     S.heur = heur;
     // LDS: cube (125 f64, 1000 B -> 1024), U keys (2 x ucap f64), U cells (ucap i32), occupancy bits
@@ -373,6 +489,9 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
         S.gz = gz;
         S.npush = 0;
         S.maxn = 0;
+#ifdef PMP_STAMPS
+        S.cyc[0] = S.cyc[1] = S.cyc[2] = S.cyc[3] = 0;
+#endif
         if (S.start == S.goal) {
             for (int r = 0; r < R1; r++) {
                 status_out[(size_t)q * R1 + r] = 0;
@@ -400,6 +519,8 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
         }
         wsync();
         S.U.n = 0;
+        S.goal_g = kInf;
+        S.goal_rhs = kInf;  // LNode3D(goal, inf, inf) (:59); goal != start here
         {
             Track t;
             t.pos = -1;
@@ -449,19 +570,20 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
             // ---- computeShortestPath (:127-145)
             for (;;) {
                 if (S.U.n == 0) break;
+#ifdef PMP_STAMPS
+                const uint64_t ts = __builtin_amdgcn_s_memtime();
+#endif
                 if (max_exp > 0 && S.nexp >= max_exp) { st = PMP_CAP_OVERFLOW; break; }
-                double gg = 0.0, gr = 0.0;
-                if (lane == 0) {
-                    gg = S.g[S.goal];
-                    gr = S.rhs[S.goal];
-                }
+                const double gg = S.goal_g, gr = S.goal_rhs;
                 // min(U, key): first minimal key in list order
                 double b1 = kInf, b2 = kInf;
                 int bi = 0x7fffffff;
+                const bool usp = S.U.n > S.U.cap;
                 for (int k = lane; k < S.U.n; k += 64) {
                     int32_t c;
                     double a1, a2;
-                    S.U.ld(k, c, a1, a2);
+                    if (usp) S.U.template ld<true>(k, c, a1, a2);
+                    else S.U.template ld<false>(k, c, a1, a2);
                     if (bi == 0x7fffffff || key_lt(a1, a2, b1, b2)) { b1 = a1; b2 = a2; bi = k; }
                 }
                 for (int o = 1; o < 64; o <<= 1) {
@@ -474,15 +596,17 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
                 bi = uni(bi);
                 b1 = rl_f64(b1, 0);
                 b2 = rl_f64(b2, 0);
-                gg = rl_f64(gg, 0);
-                gr = rl_f64(gr, 0);
                 const double gm = gg < gr ? gg : gr;
                 // node.key >= calculateKey(goal) and goal.rhs == goal.g (:131-133); h(goal, goal) = 0
+#ifdef PMP_STAMPS
+                S.cyc[0] += __builtin_amdgcn_s_memtime() - ts;
+#endif
                 if (!key_lt(b1, b2, gm + 0.0, gm) && gr == gg) break;
                 int32_t vt = 0;
                 if (lane == 0) {
                     double a, b;
-                    S.U.ld(bi, vt, a, b);
+                    if (usp) S.U.template ld<true>(bi, vt, a, b);
+                    else S.U.template ld<false>(bi, vt, a, b);
                 }
                 const int v = uni(vt);
                 {
@@ -491,17 +615,8 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
                     S.remove_at(bi, t);
                 }
                 S.nexp++;
-                double gvt = 0.0, rvt = 0.0;
-                if (lane == 0) {
-                    gvt = S.g[v];
-                    rvt = S.rhs[v];
-                }
-                const double gv = rl_f64(gvt, 0), rv = rl_f64(rvt, 0);
-                const bool over = gv > rv;
-                if (lane == 0) S.g[v] = over ? rv : kInf;
-                wsync();
                 // over-consistent: g = rhs; else g = inf and updateVertex(node); then the neighbours
-                S.update_block(v, !over);
+                S.update_block(v, false, true);
             }
             // ---- extractPath (:185-225): greedy min-g free neighbour from the goal
             double cost = 0.0;
@@ -558,10 +673,14 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
             wsync();
         }
         if (counters && lane == 0) {
+#ifdef PMP_STAMPS
+            for (int k = 0; k < 4; k++) counters[4 * q + k] = (int64_t)S.cyc[k];
+#else
             counters[4 * q] = S.npush;
             counters[4 * q + 1] = tot_exp;
             counters[4 * q + 2] = 0;
             counters[4 * q + 3] = S.maxn;
+#endif
         }
         wsync();
     }
