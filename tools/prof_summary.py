@@ -19,6 +19,9 @@ KERNELS = {  # short name -> regex on the demangled kernel name
     "rrt_kernel": r"rrt_kernel<",
     "astar3d_kernel": r"astar3d_kernel[<(]",
     "dstar_kernel": r"dstar_kernel\(",
+    "dstar3d_kernel": r"dstar3d_kernel<",
+    "lpa_kernel": r"lpa_kernel\(",
+    "lpa3d_kernel": r"lpa3d_kernel\(",
     "track_kernel_lqr": r"track_kernel<0>",
     "track_kernel_mpc": r"track_kernel<1>",
 }
@@ -79,6 +82,25 @@ def main(src, dst):
                         "calibration) and WRITE_SIZE as is; Infinity-Cache hits are counted by these counters")
     with open(os.path.join(dst, "pmc_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1, sort_keys=True)
+    # MFMA utilisation pass (rocprofv3's MfmaUtil expression: SQ_VALU_MFMA_BUSY_CYCLES summed over the
+    # chip / (GRBM_GUI_ACTIVE x SIMDs), per dispatch)
+    path = os.path.join(src, "prof_mfma", "run_results.db")
+    if os.path.exists(path):
+        d = sqlite3.connect(path)
+        mf = {}
+        for name, cn, n, avg in d.execute("select kernel_name, counter_name, count(*), avg(value) from "
+                                          "counters_collection group by kernel_name, counter_name"):
+            mf.setdefault(short(name), {})[cn] = avg
+            mf[short(name)]["dispatches"] = n
+        simds = 256 * 4
+        for k, e in mf.items():
+            if e.get("GRBM_GUI_ACTIVE"):
+                e["mfma_util_pct"] = 100.0 * e.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (e["GRBM_GUI_ACTIVE"] * simds)
+        mf["_note"] = ("per-dispatch averages of the separate --pmc pass; mfma_util_pct = SQ_VALU_MFMA_BUSY_CYCLES / "
+                       "(GRBM_GUI_ACTIVE x 1024 SIMDs) x 100 (rocprofv3 MfmaUtil)")
+        with open(os.path.join(dst, "pmc_mfma.json"), "w") as f:
+            json.dump(mf, f, indent=1, sort_keys=True)
+        print("mfma", {k: v.get("mfma_util_pct") for k, v in mf.items() if not k.startswith("_")})
     for n, c, t, a, p in rows[:8]:
         print(f"{short(n):24s} calls {c:5d} avg {a / 1e6:12.3f} ms  {p:6.2f} %")
     print(json.dumps({k: v.get("hbm_bytes_per_dispatch") for k, v in traffic.items() if not k.startswith("_")}))
