@@ -877,9 +877,13 @@ def main():
                     help="A* query order across workers: longest start-goal distance first, or input order")
     ap.add_argument("--prio", type=int, default=64,
                     help="longest-first only: the first N (longest) queries of a batch run at raised wave priority")
-    ap.add_argument("--streams", type=int, default=3,
+    ap.add_argument("--streams", type=int, default=4,
                     help="batches in flight: consecutive steps go to different HIP streams (own scratch "
                          "context each), so one batch's long-query tail overlaps the next batch")
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="HIP hardware queues per process (GPU_MAX_HW_QUEUES, <= 32), set before the GPU is "
+                         "touched: with HIP's default of 4 a fourth batch in flight shares a queue with "
+                         "another and serialises behind it")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="weak: every rank plans its own --nq batch; strong: one --nq batch dealt over the ranks "
                          "(longest-first round-robin) with an all_gather of the results")
@@ -900,6 +904,9 @@ def main():
     if args.dry_run:
         return dry_run(args, rank, world)
 
+    # must be in the environment before the HIP runtime initialises (the first torch.cuda call)
+    if "GPU_MAX_HW_QUEUES" not in os.environ:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(4, args.hw_queues)))
     import torch
 
     dist = shard.init("nccl")  # RCCL over xGMI; None for a single process
@@ -1007,6 +1014,13 @@ def main():
         args.scaling == "strong" and dist is not None) else counters
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
 
+    # the headline's scratch (about 30 GB per batch in flight) is not needed by the other legs
+    torch.cuda.synchronize()
+    cost = cost.cpu()
+    for b in lanes:
+        L.pmp_destroy(b["ctx"])
+    lanes.clear()
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as O
@@ -1017,7 +1031,7 @@ def main():
         t = time.perf_counter()
         ref = O.astar2d_batch(occ, starts[:ns], goals[:ns], path_cap=path_cap, nthreads=threads)
         dt = time.perf_counter() - t
-        assert np.array_equal(ref["cost"], cost[:ns].cpu().numpy()), "GPU/oracle cost mismatch"
+        assert np.array_equal(ref["cost"], cost[:ns].numpy()), "GPU/oracle cost mismatch"
         # one core: every 32nd query of the batch (the same mix of short and long queries)
         sub = np.arange(0, nq, 32)[: max(1, args.cpu_sample // 32)]
         t = time.perf_counter()
@@ -1084,7 +1098,8 @@ def main():
                        "max_heap_entries": int(counters[:, 3].max()),
                        "expansions_all_ranks_per_step": int(counters_all[:, 2].sum()) if args.scaling == "strong" else None,
                        "strong_scaling_gather": gathered,
-                       "workers": args.workers, "streams": S, "priority_queries": args.prio},
+                       "workers": args.workers, "streams": S, "priority_queries": args.prio,
+                       "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
         }
         print(json.dumps(out), flush=True)
     if dist:
