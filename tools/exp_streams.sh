@@ -1,9 +1,8 @@
-# dev experiment: A* headline vs batches in flight (streams), HIP hardware queues and workers
+# dev experiment: A* headline vs persistent workers per launch (LDS heap share per worker), 4 batches in flight
 set -e
 mkdir -p gpurun_out
-: > gpurun_out/streams3.log
-for cfg in "4 3 3072" "8 3 3072" "8 4 3072" "8 5 3072" "8 4 2560" "8 5 2560"; do
-  set -- $cfg
-  echo "hwq=$1 streams=$2 workers=$3" >> gpurun_out/streams3.log
-  GPU_MAX_HW_QUEUES=$1 timeout -k 10 150 python -u bench.py --legs none --no-cpu-baseline --steps 20 --warmup $2 --streams $2 --workers $3 >> gpurun_out/streams3.log 2>&1
+: > gpurun_out/workers.log
+for w in 2048 2560 3072 3328; do
+  echo "workers=$w" >> gpurun_out/workers.log
+  timeout -k 10 150 python -u bench.py --legs none --no-cpu-baseline --steps 20 --warmup 4 --workers $w >> gpurun_out/workers.log 2>&1
 done
