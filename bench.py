@@ -883,7 +883,7 @@ def main():
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="HIP hardware queues per process (GPU_MAX_HW_QUEUES, <= 32), set before the GPU is "
                          "touched: with HIP's default of 4 a fourth batch in flight shares a queue with "
-                         "another and serialises behind it")
+                         "another and serialises behind it (0: keep the environment's value)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="weak: every rank plans its own --nq batch; strong: one --nq batch dealt over the ranks "
                          "(longest-first round-robin) with an all_gather of the results")
@@ -905,7 +905,8 @@ def main():
         return dry_run(args, rank, world)
 
     # must be in the environment before the HIP runtime initialises (the first torch.cuda call)
-    if "GPU_MAX_HW_QUEUES" not in os.environ:
+    # (the GPU box exports GPU_MAX_HW_QUEUES=4, HIP's default: override it; --hw-queues 0 keeps it)
+    if args.hw_queues > 0:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(4, args.hw_queues)))
     import torch
 
