@@ -411,6 +411,39 @@ int pmp_rrt_batch(pmp_ctx* ctx, void* stream, const pmp_rrt_params* p, const dou
                   int32_t* path_len, double* path_xy, int path_cap, int64_t* draws, int32_t* status,
                   int64_t* counters);
 
+/* TrajectoryConstraints (trajectory/trajectory_base.py:30-45) and TimeOptimalTrajectory3D's
+ * path_resolution (trajectory/time_optimal_trajectory.py:17-29) */
+typedef struct {
+    double max_velocity[3];
+    double max_acceleration[3];
+    double min_time_step;
+    double path_resolution;
+} pmp_totp_params;
+
+/*
+ * Batched time-optimal trajectories (config 5's step after 3D planning, examples/3d_example.py:93-128).
+ * Replaces TimeOptimalTrajectory3D(path, constraints, path_resolution).generate()
+ * (trajectory/time_optimal_trajectory.py:260-302): arc-length parameterisation with scipy's
+ * not-a-knot CubicSpline per axis (:41-74), forward / backward velocity integration (:162-226, the
+ * reference's sign handling for q' < 0 included), s_ddot and time profiles (:228-258), sampling at
+ * t = 0, dt, ... (+ total_time) through interp1d (:304-335), yaw / yaw rate
+ * (trajectory_base.py:245-261).  Values match the reference to rounding.
+ *   path_xyz [sum n][3] f64, path_off [nq + 1] i32   waypoints per path (reference order)
+ *   max_waypoints  >= every path's n (sizes LDS; <= 480)
+ *   s_values, s_dot, s_ddot, time_profile [nq][sample_cap]; n_samples [nq] = max(int(L / res), 100)
+ *   points [nq][point_cap][12]: time, position[3], velocity[3], acceleration[3], yaw, yaw rate
+ *       (NaN where the reference leaves None); n_points [nq]; total_time [nq]
+ *   status [nq]  0 ok, 2 sample_cap or point_cap too small (the counts are still reported),
+ *                3 path longer than max_waypoints, 4 the reference raises (< 2 waypoints, or
+ *                repeated consecutive waypoints: scipy needs strictly increasing knots)
+ *   eval_t [n_eval] nullable: instead of generate()'s sampling, evaluate(t) (:304-335) at these times
+ *       (yaw / yaw rate NaN, as evaluate leaves them)
+ */
+int pmp_totp3d_batch(pmp_ctx* ctx, void* stream, const pmp_totp_params* prm, int nq, const double* path_xyz,
+                     const int32_t* path_off, int max_waypoints, int sample_cap, double* s_values, double* s_dot,
+                     double* s_ddot, double* time_profile, int32_t* n_samples, int point_cap, double* points,
+                     int32_t* n_points, double* total_time, int32_t* status, const double* eval_t, int n_eval);
+
 /* Launch-span recording for profiling: while set, every A* 2D launch of this context folds its
  * workers' first start and last end wall-clock ticks into span[0] (atomic min) and span[1] (atomic
  * max); the caller initialises span to {UINT64_MAX, 0}.  NULL switches it off. */

@@ -808,3 +808,46 @@ def graph3d_dynamic_batch(kind: str, occ, starts, goals, rounds=None, heuristic:
                                  _p(s, _i32p), _p(g, _i32p), nq, _p(rd, _i32p) if rd is not None else None, nr,
                                  _p(out["cost"], _dp), _p(out["status"], _i32p), _p(out["n"], _i64p), int(nthreads))
     return out
+
+
+class TotpParams(ctypes.Structure):
+    """totp_params_t: TrajectoryConstraints (trajectory_base.py) + path_resolution"""
+    _fields_ = [("vmax", ctypes.c_double * 3), ("amax", ctypes.c_double * 3), ("tstep", ctypes.c_double),
+                ("res", ctypes.c_double)]
+
+    @classmethod
+    def make(cls, vmax=(2.0, 2.0, 2.0), amax=(1.0, 1.0, 1.0), tstep=0.01, res=0.01):
+        return cls((ctypes.c_double * 3)(*vmax), (ctypes.c_double * 3)(*amax), tstep, res)
+
+
+def totp3d_batch(paths, params: TotpParams, sample_cap: int = 0, point_cap: int = 0, nthreads: int = 0):
+    """TimeOptimalTrajectory3D(path, constraints, path_resolution).generate() for every path
+    (time_optimal_trajectory.py:8-353) with OpenMP over paths.  Caps of 0 size the buffers from a
+    first pass.  Returns profiles [nq, sample_cap] + n_samples, points [nq, point_cap, 12] (time,
+    position, velocity, acceleration, yaw, yaw rate; NaN = None) + n_points, total_time, status."""
+    L = lib()
+    if not getattr(L, "_totp", False):
+        L.oracle_totp3d_batch.restype = ctypes.c_int
+        L.oracle_totp3d_batch.argtypes = [_dp, _i64p, ctypes.c_int, ctypes.POINTER(TotpParams), ctypes.c_int, _dp, _dp,
+                                          _dp, _dp, _i32p, ctypes.c_int, _dp, _i32p, _dp, _i32p, ctypes.c_int]
+        L._totp = True
+    flat = np.ascontiguousarray(np.concatenate([np.asarray(p, np.float64).reshape(-1, 3) for p in paths]))
+    off = np.zeros(len(paths) + 1, np.int64)
+    off[1:] = np.cumsum([len(p) for p in paths])
+    nq = len(paths)
+
+    def run(sc, pc):
+        out = dict(s_values=np.zeros((nq, sc)), s_dot=np.zeros((nq, sc)), s_ddot=np.zeros((nq, sc)),
+                   time=np.zeros((nq, sc)), n_samples=np.zeros(nq, np.int32), points=np.zeros((nq, pc, 12)),
+                   n_points=np.zeros(nq, np.int32), total_time=np.zeros(nq), status=np.zeros(nq, np.int32))
+        L.oracle_totp3d_batch(_p(flat, _dp), _p(off, _i64p), nq, ctypes.byref(params), sc, _p(out["s_values"], _dp),
+                              _p(out["s_dot"], _dp), _p(out["s_ddot"], _dp), _p(out["time"], _dp),
+                              _p(out["n_samples"], _i32p), pc, _p(out["points"], _dp), _p(out["n_points"], _i32p),
+                              _p(out["total_time"], _dp), _p(out["status"], _i32p), nthreads)
+        return out
+
+    if sample_cap <= 0 or point_cap <= 0:
+        first = run(1, 1)
+        sample_cap = sample_cap if sample_cap > 0 else max(1, int(first["n_samples"].max()))
+        point_cap = point_cap if point_cap > 0 else max(1, int(first["n_points"].max()))
+    return run(sample_cap, point_cap)

@@ -2796,3 +2796,381 @@ void oracle_lpastar3d_batch(const uint8_t* occ, int per_query, int X, int Y, int
         free(plen);
     }
 }
+
+/* ==================================================================================== */
+/* TimeOptimalTrajectory3D (trajectory/time_optimal_trajectory.py:8-353,                 */
+/* trajectory_base.py:245-261): scipy CubicSpline per axis, forward/backward velocity     */
+/* integration, interp1d sampling, yaw / yaw rate.                                         */
+/* ==================================================================================== */
+
+typedef struct {
+    double vmax[3], amax[3];  /* TrajectoryConstraints.max_velocity / max_acceleration */
+    double tstep;             /* TrajectoryConstraints.min_time_step */
+    double res;               /* path_resolution */
+} totp_params_t;
+
+/* scipy CubicSpline(x, y) with bc 'not-a-knot' (scipy/interpolate/_cubic.py CubicSpline.__init__,
+   scipy 1.15): first derivatives s[] at the knots.  n == 2: both ends take the slope; n == 3: the
+   parabola system solved by LU with partial pivoting (LAPACK dgesv); n >= 4: the tridiagonal system
+   with the not-a-knot end rows, banded LU with partial pivoting (LAPACK dgbtf2: multipliers by the
+   reciprocal pivot) and the column-oriented banded back substitution (dtbsv). */
+static void cspline_slopes(const double* x, const double* y, int n, double* s, double* w /* 5n */)
+{
+    double* dx = w;
+    double* sl = w + n;
+    for (int i = 0; i + 1 < n; i++) {
+        dx[i] = x[i + 1] - x[i];
+        sl[i] = (y[i + 1] - y[i]) / dx[i];
+    }
+    if (n == 2) {
+        s[0] = sl[0];
+        s[1] = sl[0];
+        return;
+    }
+    if (n == 3) {
+        double A[3][3] = {{1.0, 1.0, 0.0}, {dx[1], 2.0 * (dx[0] + dx[1]), dx[0]}, {0.0, 1.0, 1.0}};
+        double b[3] = {2.0 * sl[0], 3.0 * (dx[0] * sl[1] + dx[1] * sl[0]), 2.0 * sl[1]};
+        for (int k = 0; k < 3; k++) {
+            int p = k;
+            for (int r = k + 1; r < 3; r++)
+                if (fabs(A[r][k]) > fabs(A[p][k])) p = r;
+            if (p != k) {
+                for (int c = 0; c < 3; c++) { double t = A[k][c]; A[k][c] = A[p][c]; A[p][c] = t; }
+                double t = b[k]; b[k] = b[p]; b[p] = t;
+            }
+            const double rinv = 1.0 / A[k][k];
+            for (int r = k + 1; r < 3; r++) {
+                const double m = A[r][k] * rinv;
+                for (int c = k + 1; c < 3; c++) A[r][c] -= m * A[k][c];
+                b[r] -= m * b[k];
+            }
+        }
+        for (int k = 2; k >= 0; k--) {
+            s[k] = b[k] / A[k][k];
+            for (int r = 0; r < k; r++) b[r] -= s[k] * A[r][k];
+        }
+        return;
+    }
+    /* rows: L = sub-diagonal (col i-1), D = diagonal, U1 = col i+1, U2 = col i+2 (pivoting fill) */
+    double* D = w + 2 * n;
+    double* U1 = w + 3 * n;
+    double* U2 = w + 4 * n;
+    double Lk1;  /* the sub-diagonal entry of the row below the current pivot row */
+    double* b = s;
+    for (int i = 1; i + 1 < n; i++) {
+        D[i] = 2.0 * (dx[i - 1] + dx[i]);
+        U1[i] = dx[i - 1];
+        U2[i] = 0.0;
+        b[i] = 3.0 * (dx[i] * sl[i - 1] + dx[i - 1] * sl[i]);
+    }
+    {
+        const double d = x[2] - x[0];
+        D[0] = dx[1];
+        U1[0] = d;
+        U2[0] = 0.0;
+        b[0] = ((dx[0] + 2.0 * d) * dx[1] * sl[0] + (dx[0] * dx[0]) * sl[1]) / d;
+    }
+    double Lnm1;
+    {
+        const double d = x[n - 1] - x[n - 3];
+        D[n - 1] = dx[n - 3];
+        Lnm1 = d;
+        U1[n - 1] = 0.0;
+        U2[n - 1] = 0.0;
+        b[n - 1] = ((dx[n - 2] * dx[n - 2]) * sl[n - 3] + (2.0 * d + dx[n - 2]) * dx[n - 3] * sl[n - 2]) / d;
+    }
+    for (int k = 0; k + 1 < n; k++) {
+        Lk1 = (k + 1 == n - 1) ? Lnm1 : dx[k + 1];  /* A[k+1][k] (A[-1, :-2] = dx[1:]) */
+        if (fabs(Lk1) > fabs(D[k])) {  /* swap rows k and k+1 (columns k .. k+2) */
+            const double t0 = D[k], t1 = U1[k], t2 = U2[k], tb = b[k];
+            D[k] = Lk1; U1[k] = D[k + 1]; U2[k] = U1[k + 1]; b[k] = b[k + 1];
+            Lk1 = t0; D[k + 1] = t1; U1[k + 1] = t2; b[k + 1] = tb;
+        }
+        const double m = Lk1 * (1.0 / D[k]);
+        D[k + 1] -= m * U1[k];
+        if (k + 2 < n) U1[k + 1] -= m * U2[k];
+        b[k + 1] -= m * b[k];
+    }
+    for (int j = n - 1; j >= 0; j--) {
+        if (b[j] != 0.0) {
+            b[j] = b[j] / D[j];
+            const double t = b[j];
+            if (j >= 1) b[j - 1] -= t * U1[j - 1];
+            if (j >= 2) b[j - 2] -= t * U2[j - 2];
+        }
+    }
+}
+
+/* PPoly evaluation (scipy/interpolate/_ppoly.pyx find_interval_ascending + evaluate_poly1 with
+   dx = 0): interval i with x[i] <= v < x[i+1] (the last closed), then sum_k c[K-1-k] (v - x[i])^k
+   with the power built by repeated products.  c: K coefficient rows of n-1 segments. */
+static int pp_interval(const double* x, int n, double v)
+{
+    if (!(x[0] <= v && v <= x[n - 1])) return v < x[0] ? 0 : n - 2;
+    if (v == x[n - 1]) return n - 2;
+    int lo = 0, hi = n - 2;
+    if (v < x[lo + 1]) hi = lo;
+    while (lo < hi) {
+        const int mid = (hi + lo) / 2;
+        if (v < x[mid]) hi = mid;
+        else if (v >= x[mid + 1]) lo = mid + 1;
+        else { lo = mid; break; }
+    }
+    return lo;
+}
+
+/* position, first and second derivative of one axis at v: the CubicSpline and its derivative(1) /
+   derivative(2) PPolys (coefficients [3c0, 2c1, c2] and [6c0, 2c1], PPoly.derivative's rising
+   factorials) */
+static void pp_eval3(const double* c /* [4][n-1] */, const double* x, int n, double v, double* p, double* d1, double* d2)
+{
+    const int i = pp_interval(x, n, v), m = n - 1;
+    const double s = v - x[i];
+    const double c0 = c[i], c1 = c[m + i], c2 = c[2 * m + i], c3 = c[3 * m + i];
+    const double s2 = s * s, s3 = s2 * s;
+    *p = ((c3 + c2 * s) + c1 * s2) + c0 * s3;
+    *d1 = (c2 + (2.0 * c1) * s) + (3.0 * c0) * s2;
+    *d2 = (2.0 * c1) + (6.0 * c0) * s;
+}
+
+typedef struct {
+    int n;              /* waypoints */
+    double L;           /* path_length */
+    const double* arc;  /* arc lengths [n] */
+    const double* c;    /* per axis [4][n-1] */
+} totp_path_t;
+
+/* _evaluate_path (time_optimal_trajectory.py:76-94): s clipped to [0, L] */
+static void totp_eval(const totp_path_t* P, double s, double pos[3], double q1[3], double q2[3])
+{
+    if (s < 0.0) s = 0.0;
+    if (s > P->L) s = P->L;
+    for (int d = 0; d < 3; d++) pp_eval3(P->c + (size_t)d * 4 * (P->n - 1), P->arc, P->n, s, &pos[d], &q1[d], &q2[d]);
+}
+
+/* _compute_max_velocity (:96-118) */
+static double totp_vmax(const totp_path_t* P, const totp_params_t* T, double s)
+{
+    double pos[3], q1[3], q2[3];
+    totp_eval(P, s, pos, q1, q2);
+    double best = 0.0;
+    int any = 0;
+    for (int d = 0; d < 3; d++)
+        if (fabs(q1[d]) > 1e-10) {
+            const double v = T->vmax[d] / fabs(q1[d]);
+            if (!any || v < best) best = v;
+            any = 1;
+        }
+    if (!any) {
+        best = T->vmax[0];
+        for (int d = 1; d < 3; d++) if (T->vmax[d] < best) best = T->vmax[d];
+    }
+    return best;
+}
+
+/* _compute_max_acceleration (:120-160), including the reference's sign handling for q' < 0 */
+static void totp_amax(const totp_path_t* P, const totp_params_t* T, double s, double sd, double* smax, double* smin)
+{
+    double pos[3], q1[3], q2[3];
+    totp_eval(P, s, pos, q1, q2);
+    double hi = INFINITY, lo = -INFINITY;
+    for (int d = 0; d < 3; d++)
+        if (fabs(q1[d]) > 1e-10) {
+            const double cen = q2[d] * sd * sd;
+            const double a = T->amax[d];
+            const double fw = (a - cen) / q1[d], bw = (-a - cen) / q1[d];
+            if (q1[d] > 0) {
+                if (fw < hi) hi = fw;
+                if (bw > lo) lo = bw;
+            } else {
+                if (-bw < hi) hi = -bw;
+                if (-fw > lo) lo = -fw;
+            }
+        }
+    *smax = hi;
+    *smin = lo;
+}
+
+static double py_min(double a, double b) { return b < a ? b : a; }
+static double np_sq(double a) { return a * a; }
+
+/* One TimeOptimalTrajectory3D(path, constraints, path_resolution).generate().  Profiles of
+   n_samples = max(int(L / res), 100) entries go to s_values / s_dot / s_ddot / time (up to
+   sample_cap), trajectory points (time, position[3], velocity[3], acceleration[3], yaw, yaw rate;
+   NaN for None) to pts (up to point_cap rows of 12).  Returns 0, 2 (a cap was too small: the
+   counts are still reported) or 4 (fewer than 2 waypoints: the reference raises ValueError). */
+int oracle_totp3d(const double* path, int n, const totp_params_t* T, int sample_cap, double* s_values, double* s_dot,
+                  double* s_ddot, double* time_prof, int* n_samples, int point_cap, double* pts, int* n_points,
+                  double* total_time)
+{
+    *n_samples = 0;
+    *n_points = 0;
+    *total_time = 0.0;
+    if (n < 2) return 4;
+    double* arc = (double*)malloc(sizeof(double) * n);
+    double* c = (double*)malloc(sizeof(double) * 12 * (n - 1));
+    double* w = (double*)malloc(sizeof(double) * 5 * n);
+    double* y = (double*)malloc(sizeof(double) * n);
+    double* sl = (double*)malloc(sizeof(double) * n);
+    /* _parameterize_path (:41-74): cumulative arc length, np.linalg.norm = sqrt(dot) */
+    arc[0] = 0.0;
+    for (int i = 1; i < n; i++) {
+        const double a = path[3 * i] - path[3 * i - 3], b = path[3 * i + 1] - path[3 * i - 2], e = path[3 * i + 2] - path[3 * i - 1];
+        arc[i] = arc[i - 1] + sqrt((a * a + b * b) + e * e);
+    }
+    const double L = arc[n - 1];
+    for (int i = 0; i + 1 < n; i++)
+        if (!(arc[i + 1] - arc[i] > 0.0)) {  /* scipy: `x` must be strictly increasing (ValueError) */
+            free(arc); free(c); free(w); free(y); free(sl);
+            return 4;
+        }
+    for (int d = 0; d < 3; d++) {
+        for (int i = 0; i < n; i++) y[i] = path[3 * i + d];
+        cspline_slopes(arc, y, n, sl, w);
+        /* CubicHermiteSpline coefficients (scipy/interpolate/_cubic.py) */
+        double* cd = c + (size_t)d * 4 * (n - 1);
+        for (int i = 0; i + 1 < n; i++) {
+            const double dx = arc[i + 1] - arc[i], slope = (y[i + 1] - y[i]) / dx;
+            const double t = ((sl[i] + sl[i + 1]) - 2.0 * slope) / dx;
+            cd[i] = t / dx;
+            cd[(n - 1) + i] = (slope - sl[i]) / dx - t;
+            cd[2 * (n - 1) + i] = sl[i];
+            cd[3 * (n - 1) + i] = y[i];
+        }
+    }
+    totp_path_t P = {n, L, arc, c};
+    int ns = (int)(L / T->res);
+    if (ns < 100) ns = 100;
+    *n_samples = ns;
+    double* sv = (double*)malloc(sizeof(double) * ns);
+    double* sd = (double*)malloc(sizeof(double) * ns);
+    double* sdd = (double*)malloc(sizeof(double) * ns);
+    double* tp = (double*)malloc(sizeof(double) * ns);
+    np_linspace(0.0, L, ns, sv);
+    /* _forward_integration (:162-195) */
+    sd[0] = 0.0;
+    for (int i = 1; i < ns; i++) {
+        const double ds = sv[i] - sv[i - 1], smid = (sv[i] + sv[i - 1]) / 2.0;
+        const double vc = totp_vmax(&P, T, smid);
+        double smax, smin;
+        totp_amax(&P, T, sv[i - 1], sd[i - 1], &smax, &smin);
+        if (smax > 0) {
+            const double v2 = np_sq(sd[i - 1]) + 2.0 * smax * ds;
+            sd[i] = py_min(sqrt(v2 > 0 ? v2 : 0.0), vc);
+        } else {
+            sd[i] = py_min(sd[i - 1], vc);
+        }
+    }
+    /* _backward_integration (:197-226) */
+    sd[ns - 1] = 0.0;
+    for (int i = ns - 2; i >= 0; i--) {
+        const double ds = sv[i + 1] - sv[i];
+        double smax, smin;
+        totp_amax(&P, T, sv[i + 1], sd[i + 1], &smax, &smin);
+        if (smin < 0) {
+            const double v2 = np_sq(sd[i + 1]) - 2.0 * smin * ds;
+            sd[i] = py_min(sd[i], sqrt(v2 > 0 ? v2 : 0.0));
+        }
+    }
+    /* _compute_velocity_profile (:228-258) */
+    for (int i = 0; i < ns; i++) sdd[i] = 0.0;
+    for (int i = 1; i + 1 < ns; i++) {
+        const double ds = sv[i + 1] - sv[i - 1];
+        if (ds > 0) sdd[i] = (np_sq(sd[i + 1]) - np_sq(sd[i - 1])) / (2.0 * ds);
+    }
+    tp[0] = 0.0;
+    for (int i = 1; i < ns; i++) {
+        const double ds = sv[i] - sv[i - 1], avg = (sd[i] + sd[i - 1]) / 2.0;
+        const double dt = avg > 1e-10 ? ds / avg : ds / 0.1;
+        tp[i] = tp[i - 1] + dt;
+    }
+    const double total = tp[ns - 1];
+    *total_time = total;
+    int rc = 0;
+    if (ns <= sample_cap) {
+        memcpy(s_values, sv, sizeof(double) * ns);
+        memcpy(s_dot, sd, sizeof(double) * ns);
+        memcpy(s_ddot, sdd, sizeof(double) * ns);
+        memcpy(time_prof, tp, sizeof(double) * ns);
+    } else {
+        rc = 2;
+    }
+    /* generate (:260-302): t = 0, dt, ... <= total_time, then total_time if the last is short */
+    int np_ = 0;
+    double t = 0.0, last_t = -1.0;
+    for (;;) {
+        int last = 0;
+        double tq;
+        if (t <= total) {
+            tq = t;
+        } else if (np_ > 0 && last_t < total) {
+            tq = total;
+            last = 1;
+        } else {
+            break;
+        }
+        if (np_ < point_cap) {
+            /* evaluate (:304-335): interp1d linear (searchsorted left, clipped to [1, n-1]) */
+            const double tc = tq < 0 ? 0 : (tq > total ? total : tq);
+            int hi = 0;
+            {
+                int lo_ = 0, hi_ = ns;
+                while (lo_ < hi_) { const int mid = (lo_ + hi_) / 2; if (tp[mid] < tc) lo_ = mid + 1; else hi_ = mid; }
+                hi = lo_;
+            }
+            if (hi < 1) hi = 1;
+            if (hi > ns - 1) hi = ns - 1;
+            const int lo = hi - 1;
+            const double xl = tp[lo], xh = tp[hi], dxl = tc - xl;
+            const double s = (sv[hi] - sv[lo]) / (xh - xl) * dxl + sv[lo];
+            const double sdt = (sd[hi] - sd[lo]) / (xh - xl) * dxl + sd[lo];
+            const double sddt = (sdd[hi] - sdd[lo]) / (xh - xl) * dxl + sdd[lo];
+            double pos[3], q1[3], q2[3];
+            totp_eval(&P, s, pos, q1, q2);
+            double* o = pts + (size_t)np_ * 12;
+            o[0] = tc;
+            for (int d = 0; d < 3; d++) {
+                o[1 + d] = pos[d];
+                o[4 + d] = q1[d] * sdt;
+                o[7 + d] = q2[d] * np_sq(sdt) + q1[d] * sddt;
+            }
+            /* compute_yaw_from_velocity (trajectory_base.py:245-261) */
+            o[10] = sqrt(o[4] * o[4] + o[5] * o[5]) > 1e-6 ? atan2(o[5], o[4]) : NAN;
+            o[11] = NAN;
+            if (np_ > 0) {
+                const double* pr = o - 12;
+                const double dtp = o[0] - pr[0];
+                if (dtp > 0 && !isnan(o[10]) && !isnan(pr[10])) {
+                    double dy = o[10] - pr[10];
+                    while (dy > PI_) dy -= 2.0 * PI_;
+                    while (dy < -PI_) dy += 2.0 * PI_;
+                    o[11] = dy / dtp;
+                }
+            }
+        }
+        np_++;
+        last_t = tq;
+        if (last) break;
+        t += T->tstep;
+    }
+    *n_points = np_;
+    if (np_ > point_cap) rc = 2;
+    free(arc); free(c); free(w); free(y); free(sl); free(sv); free(sd); free(sdd); free(tp);
+    return rc;
+}
+
+/* batch over paths (path_off: waypoint offsets, nq + 1) with OpenMP over queries; per-query caps */
+int oracle_totp3d_batch(const double* path, const int64_t* path_off, int nq, const totp_params_t* T, int sample_cap,
+                        double* s_values, double* s_dot, double* s_ddot, double* time_prof, int* n_samples, int point_cap,
+                        double* pts, int* n_points, double* total_time, int* status, int nthreads)
+{
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int q = 0; q < nq; q++) {
+        const size_t so = (size_t)q * sample_cap;
+        status[q] = oracle_totp3d(path + 3 * path_off[q], (int)(path_off[q + 1] - path_off[q]), T, sample_cap,
+                                  s_values + so, s_dot + so, s_ddot + so, time_prof + so, &n_samples[q], point_cap,
+                                  pts + (size_t)q * point_cap * 12, &n_points[q], &total_time[q]);
+    }
+    return 0;
+}

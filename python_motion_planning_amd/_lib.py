@@ -56,6 +56,8 @@ SIGNATURES = {
                            _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     "pmp_track_step_batch": (_i, [_vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp,
                                   _vp]),
+    "pmp_totp3d_batch": (_i, [_vp, _vp, _vp, _i, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp,
+                              _vp, _i]),
 }
 
 
@@ -120,6 +122,20 @@ class RRTParams(ctypes.Structure):
     _fields_ = [("x_range", ctypes.c_double), ("y_range", ctypes.c_double), ("delta", ctypes.c_double),
                 ("max_dist", ctypes.c_double), ("radius", ctypes.c_double), ("goal_sample_rate", ctypes.c_double),
                 ("sample_num", ctypes.c_int32), ("star", ctypes.c_int32)]
+
+
+class TotpParams(ctypes.Structure):
+    """pmp_totp_params == TrajectoryConstraints (trajectory/trajectory_base.py:30-45) max_velocity,
+    max_acceleration, min_time_step + TimeOptimalTrajectory3D's path_resolution."""
+    _fields_ = [("max_velocity", ctypes.c_double * 3), ("max_acceleration", ctypes.c_double * 3),
+                ("min_time_step", ctypes.c_double), ("path_resolution", ctypes.c_double)]
+
+    @classmethod
+    def make(cls, max_velocity=(2.0, 2.0, 2.0), max_acceleration=(1.0, 1.0, 1.0), min_time_step: float = 0.01,
+             path_resolution: float = 0.01):
+        return cls((ctypes.c_double * 3)(*[float(v) for v in max_velocity]),
+                   (ctypes.c_double * 3)(*[float(v) for v in max_acceleration]), float(min_time_step),
+                   float(path_resolution))
 
 
 TRACK_LQR, TRACK_MPC = 0, 1

@@ -567,3 +567,70 @@ def lpastar3d_batch(occ, starts, goals, changes=None, heuristic: str = "euclidea
     _lib.check(ctx, rc, "pmp_lpastar3d_batch")
     out["dims"] = (X, Y, Z)
     return out
+
+
+def totp3d_batch(paths, params, point_cap: int | None = None, eval_t=None, retry_overflow: bool = True):
+    """Batched TimeOptimalTrajectory3D(path, constraints, path_resolution).generate()
+    (trajectory/time_optimal_trajectory.py:260-302) on pmp_totp3d_batch.  paths: list of [n, 3]
+    waypoint arrays (reference order); params: _lib.TotpParams.  With eval_t (1-D times), evaluate(t)
+    (:304-335) at those times instead of generate()'s sampling.
+    Returns dict of device tensors: s_values / s_dot / s_ddot / time [nq, sample_cap], n_samples,
+    points [nq, point_cap, 12] (time, position, velocity, acceleration, yaw, yaw rate; NaN = None),
+    n_points, total_time, status (include/pmp.h).  Queries whose points overflow the first cap are
+    re-run with their exact count when retry_overflow."""
+    torch = _lib.device_check()
+    L = _lib.load_library()
+    ctx = _lib.context()
+    arrs = [np.asarray(p, np.float64).reshape(-1, 3) for p in paths]
+    nq = len(arrs)
+    off = np.zeros(nq + 1, np.int32)
+    off[1:] = np.cumsum([len(a) for a in arrs])
+    nmax = max(2, max((len(a) for a in arrs), default=2))
+    # n_samples = max(int(L / res), 100) with L summed in the kernel's (the reference's) order
+    res = float(params.path_resolution)
+    ns = [max(int(np.cumsum(np.sqrt(np.sum(np.diff(a, axis=0) ** 2, axis=1)))[-1] / res), 100) if len(a) > 1 else 1
+          for a in arrs]
+    sample_cap = max(ns, default=1) + 1
+    flat = torch.as_tensor(np.concatenate(arrs) if nq else np.zeros((0, 3)), device="cuda")
+    off_d = torch.as_tensor(off, device="cuda")
+    et = None if eval_t is None else torch.as_tensor(np.asarray(eval_t, np.float64).ravel(), device="cuda")
+    n_eval = 0 if et is None else int(et.numel())
+    if point_cap is None:
+        point_cap = n_eval + 1 if et is not None else 2048
+
+    def launch(idx_paths, offs, pc):
+        m = len(offs) - 1
+        f64 = dict(dtype=torch.float64, device="cuda")
+        i32 = dict(dtype=torch.int32, device="cuda")
+        o = dict(s_values=torch.empty((m, sample_cap), **f64), s_dot=torch.empty((m, sample_cap), **f64),
+                 s_ddot=torch.empty((m, sample_cap), **f64), time=torch.empty((m, sample_cap), **f64),
+                 n_samples=torch.empty(m, **i32), points=torch.empty((m, pc, 12), **f64), n_points=torch.empty(m, **i32),
+                 total_time=torch.empty(m, **f64), status=torch.empty(m, **i32))
+        if m:
+            rc = L.pmp_totp3d_batch(ctx, _lib.stream_ptr(), ctypes.byref(params), m, idx_paths.data_ptr(),
+                                    offs.data_ptr(), nmax, sample_cap, o["s_values"].data_ptr(), o["s_dot"].data_ptr(),
+                                    o["s_ddot"].data_ptr(), o["time"].data_ptr(), o["n_samples"].data_ptr(), pc,
+                                    o["points"].data_ptr(), o["n_points"].data_ptr(), o["total_time"].data_ptr(),
+                                    o["status"].data_ptr(), _lib.ptr(et), n_eval)
+            _lib.check(ctx, rc, "pmp_totp3d_batch")
+        return o
+
+    out = launch(flat, off_d, int(point_cap))
+    if retry_overflow and nq:
+        st = out["status"].cpu().numpy()
+        npt = out["n_points"].cpu().numpy()
+        redo = np.nonzero((st == _lib.STATUS_PATH_OVERFLOW) & (npt > point_cap))[0]
+        if len(redo):
+            pc = int(npt[redo].max())
+            sub = [arrs[i] for i in redo]
+            so = np.zeros(len(sub) + 1, np.int32)
+            so[1:] = np.cumsum([len(a) for a in sub])
+            r = launch(torch.as_tensor(np.concatenate(sub), device="cuda"), torch.as_tensor(so, device="cuda"), pc)
+            big = torch.full((nq, pc, 12), float("nan"), dtype=torch.float64, device="cuda")
+            big[:, : int(point_cap)] = out["points"]
+            idx = torch.as_tensor(redo, device="cuda", dtype=torch.long)
+            big[idx] = r["points"]
+            out["points"] = big
+            for k in ("s_values", "s_dot", "s_ddot", "time", "n_samples", "n_points", "total_time", "status"):
+                out[k][idx] = r[k]
+    return out

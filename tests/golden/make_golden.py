@@ -4,7 +4,7 @@ Run in the build container only (the reference never travels to the GPU box):
 
     PYTHONDONTWRITEBYTECODE=1 MPLBACKEND=Agg python tests/golden/make_golden.py [section ...]
 
-Sections: astar_readme astar_small astar_1024 dstar astar3d graph2d graph3d theta3d theta2d lpa dstarlite lpa_replan dstarlite_replan rrt dwa lqr mpc hypot
+Sections: astar_readme astar_small astar_1024 dstar astar3d graph2d graph3d theta3d theta2d lpa dstarlite lpa_replan dstarlite_replan rrt dwa lqr mpc hypot totp
 Outputs are small fixtures (inputs + expected outputs) under tests/golden/.  The reference is
 imported with stubs for the modules absent from this image (osqp, pyvista), per SURVEY.md §8(c).
 """
@@ -1194,13 +1194,79 @@ def sec_astar_nodes():
     print("astar nodes", [(o["algo"], o["heuristic"], len(o["nodes"])) for o in out])
 
 
+# ----------------------------------------------------------------------------------------------
+# TimeOptimalTrajectory3D (trajectory/time_optimal_trajectory.py:8-353) on C5 paths: the 3d_example
+# set-up (examples/3d_example.py:104-128: constraints, path_resolution 0.05, path from AStar3D.plan)
+# plus the defaults (2 / 1 m/s(^2), resolution 0.01) and the 2- and 3-waypoint special cases of
+# scipy's CubicSpline
+def run_totp(args):
+    path, vmax, amax, tstep, res = args
+    pmp = import_reference()
+    from python_motion_planning.trajectory import TimeOptimalTrajectory3D, TrajectoryConstraints
+
+    cons = None if vmax is None else TrajectoryConstraints(max_velocity=np.array(vmax), max_acceleration=np.array(amax),
+                                                           min_time_step=tstep)
+    tr = TimeOptimalTrajectory3D(path=[tuple(p) for p in path], constraints=cons, path_resolution=res)
+    pts = tr.generate()
+    nan = float("nan")
+    return dict(total_time=float(tr.total_time), s_values=np.asarray(tr.s_values, np.float64),
+                s_dot=np.asarray(tr.s_dot_profile, np.float64), s_ddot=np.asarray(tr.s_ddot_profile, np.float64),
+                time=np.asarray(tr.time_profile, np.float64),
+                pts=np.array([[q.time, *q.position, *q.velocity, *q.acceleration,
+                               nan if q.yaw is None else q.yaw, nan if q.yaw_rate is None else q.yaw_rate]
+                              for q in pts], np.float64))
+
+
+def sec_totp():
+    from python_motion_planning_amd import workloads as wl
+
+    pmp = import_reference()
+    ex = ([2.0, 2.0, 1.5], [1.5, 1.5, 1.0], 0.05, 0.05)  # 3d_example.py:104-109, :124-128
+    cases = []
+    for seed in range(32):
+        s, gq = wl.bench3d_query(seed, 26, 20, 16)
+        o = wl.SCENARIOS_3D["door"](26, 20, 16)
+        wl.carve_safety_bubble(o, s, 1)
+        wl.carve_safety_bubble(o, gq, 1)
+        env = pmp.Grid3D(26, 20, 16)
+        env.update({(int(a), int(b), int(c)) for a, b, c in np.argwhere(o)})
+        cost, path, _ = pmp.AStar3D(tuple(s), tuple(gq), env).plan()
+        close_figs()
+        if len(path) >= 2:
+            cases.append((np.array(path, np.float64),) + (ex if seed % 4 else (None, None, None, 0.01)))
+    # scipy CubicSpline special cases (n = 2: line, n = 3: parabola) and a short diagonal run
+    cases.append((np.array([[1, 1, 1], [2, 2, 1]], np.float64),) + ex)
+    cases.append((np.array([[1, 1, 1], [2, 2, 1], [3, 2, 2]], np.float64),) + ex)
+    cases.append((np.array([[5, 5, 5], [4, 4, 4], [3, 3, 3], [2, 3, 3], [1, 3, 4]], np.float64),) + ex)
+    cases.append((np.array([[5, 5, 5], [4, 4, 4], [3, 3, 3], [2, 3, 3], [1, 3, 4]], np.float64), None, None, None, 0.01))
+    with Pool(8) as pool:
+        res = pool.map(run_totp, cases)
+    path_flat, path_off = ragged([c[0] for c in cases], np.float64)
+    prof_off = np.concatenate([[0], np.cumsum([len(r["s_values"]) for r in res])]).astype(np.int64)
+    # trajectory points: all of them up to 1500 per case, else every 10th and the last (fixture size);
+    # pts_idx = the point's index in the reference's list, n_pts = the list's length
+    keep = [np.arange(len(r["pts"])) if len(r["pts"]) <= 1500 else
+            np.unique(np.append(np.arange(0, len(r["pts"]), 10), len(r["pts"]) - 1)) for r in res]
+    pts_off = np.concatenate([[0], np.cumsum([len(k) for k in keep])]).astype(np.int64)
+    cons = np.array([(c[1] or [2.0] * 3) + (c[2] or [1.0] * 3) + [c[3] if c[3] is not None else 0.01, c[4]]
+                     for c in cases], np.float64)
+    np.savez_compressed(
+        os.path.join(HERE, "totp.npz"), path=path_flat.reshape(-1, 3), path_off=path_off, cons=cons,
+        total_time=np.array([r["total_time"] for r in res]), prof_off=prof_off,
+        s_values=np.concatenate([r["s_values"] for r in res]), s_dot=np.concatenate([r["s_dot"] for r in res]),
+        s_ddot=np.concatenate([r["s_ddot"] for r in res]), time=np.concatenate([r["time"] for r in res]),
+        pts_off=pts_off, pts=np.concatenate([r["pts"][k] for r, k in zip(res, keep)]),
+        pts_idx=np.concatenate(keep).astype(np.int32), n_pts=np.array([len(r["pts"]) for r in res], np.int32))
+    print("totp cases", len(cases), "samples", prof_off[-1], "points", pts_off[-1])
+
+
 SECTIONS = dict(rrt=sec_rrt, mpc=sec_mpc, dwa=sec_dwa, local_plans=sec_local_plans, lqr=sec_lqr, astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
                 dstar=sec_dstar, astar3d=sec_astar3d,
                 graph2d=sec_graph2d, graph3d=sec_graph3d, theta3d=sec_theta3d, theta2d=sec_theta2d, lpa=sec_lpa,
                 dstarlite=lambda: sec_lpa(lite=True), lpa_replan=sec_lpa_replan,
                 dstarlite_replan=lambda: sec_lpa_replan(lite=True), dstar3d=sec_dstar3d,
                 dstar_onpress=sec_dstar_onpress, lpastar3d=sec_lpastar3d,
-                astar_nodes=sec_astar_nodes)
+                astar_nodes=sec_astar_nodes, totp=sec_totp)
 
 if __name__ == "__main__":
     want = sys.argv[1:] or list(SECTIONS)

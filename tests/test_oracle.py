@@ -493,3 +493,21 @@ def test_lpastar3d_apply_change_against_reference():
             assert np.array_equal(res["paths"][r], seg(z["path"], z["path_off"], i * R + r)), (i, r)
         n += 1
     assert n >= 38
+
+
+def test_totp_against_reference():
+    """TimeOptimalTrajectory3D restatement vs 36 reference runs (C5 AStar3D paths with the
+    3d_example constraints and with the defaults, the 2- and 3-waypoint spline cases)."""
+    from golden_io import totp_cases, totp_compare
+
+    for i, path, (vmax, amax, tstep, res), z in totp_cases():
+        r = O.totp3d_batch([path], O.TotpParams.make(vmax, amax, tstep, res))
+        assert r["status"][0] == 0
+        totp_compare(z, i, r["n_samples"][0], {k: r[k][0] for k in ("s_values", "s_dot", "s_ddot", "time")},
+                     r["n_points"][0], r["points"][0][: r["n_points"][0]], r["total_time"][0], rtol=1e-11)
+
+
+def test_totp_raises_like_reference():
+    prm = O.TotpParams.make()
+    r = O.totp3d_batch([np.array([[1.0, 1.0, 1.0]]), np.array([[1.0, 1.0, 1.0], [1.0, 1.0, 1.0], [2.0, 1.0, 1.0]])], prm)
+    assert list(r["status"]) == [4, 4]
