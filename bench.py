@@ -154,6 +154,23 @@ def with_traffic(roof: dict, kernel: str) -> dict:
     return roof
 
 
+def with_mfma(roof: dict, kernel: str) -> dict:
+    """MFMA utilisation of `kernel` from the newest committed profiles/r*/pmc_mfma.json (the separate
+    rocprofv3 --pmc pass of SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE, tools/profile_round.sh):
+    busy cycles over 1024 SIMDs x the dispatch's GPU cycles, in percent (rocprofv3's MfmaUtil)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_mfma.json")))
+    roof["mfma_util_pct"] = None
+    if files:
+        with open(files[-1]) as f:
+            d = json.load(f).get(kernel) or {}
+        if d.get("mfma_util_pct") is not None:
+            roof["mfma_util_pct"] = float(d["mfma_util_pct"])
+            roof["mfma_source"] = f"{os.path.relpath(files[-1], REPO)} [{kernel}]"
+    return roof
+
+
 def timed(torch, dist, fn, steps, stream=None):
     """Barrier + sync, run `steps` launches with HIP events around each (on `stream`), barrier +
     sync; returns (wall seconds, max over ranks; mean event ms per launch)."""
@@ -405,6 +422,7 @@ def astar3d_leg(args, torch, dist, world, rank):
         cpu = {"value": nq * reps / dt, "unit": "plans/s", "cores": th, "kind": "port",
                "sample": f"all {nq} C5 queries, repeated {reps}x, C restatement of AStar3D (oracle/pmp_oracle.c) "
                          f"with OpenMP over queries, {dt:.1f} s wall"}
+    traj = totp3d_leg(args, torch, dist, world, rank, plen, path, (X, Y, Z)) if "totp" in args.legs.split(",") else None
     return {"metric": "3D A* plans/sec, Grid3D(26,20,16) door scenario, 8192 queries", "value": nq * args.a3_steps * world / elapsed,
             "unit": "plans/s", "queries_per_gpu": nq, "steps": args.a3_steps,
             "ms_per_step": elapsed / args.a3_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
@@ -414,6 +432,83 @@ def astar3d_leg(args, torch, dist, world, rank):
                                       "algorithmic_bytes_per_launch": alg_bytes}, "astar3d_kernel"),
             "detail": {"expansions_per_launch": int(c[:, 2].sum()), "reference_pushes_per_launch": int(c[:, 0].sum()),
                        "heap_pops_per_launch": int(c[:, 1].sum()), "max_heap_entries": int(c[:, 3].max())},
+            "cpu_baseline": cpu, "trajectory": traj}
+
+
+def totp3d_leg(args, torch, dist, world, rank, plen, path, dims):
+    """C5's step after planning (examples/3d_example.py:93-128): TimeOptimalTrajectory3D.generate() on
+    every path the 3D A* leg planned, with the example's constraints (max velocity 2 / 2 / 1.5,
+    max acceleration 1.5 / 1.5 / 1.0, time step 0.05, path_resolution 0.05).  One step = one launch
+    over all the paths; the oracle (C restatement, OpenMP) timed on the same paths beside it."""
+    from python_motion_planning_amd import _lib, batch
+
+    X, Y, Z = dims
+    pl = plen.cpu().numpy()
+    P = path.cpu().numpy()
+    paths = []
+    for q in range(len(pl)):
+        v = P[q, : pl[q]].astype(np.int64)
+        if len(v) >= 2:
+            paths.append(np.stack([v // (Y * Z), (v // Z) % Y, v % Z], axis=1).astype(np.float64))
+    cons = dict(max_velocity=(2.0, 2.0, 1.5), max_acceleration=(1.5, 1.5, 1.0), min_time_step=0.05,
+                path_resolution=0.05)
+    prm = _lib.TotpParams.make(**cons)
+    first = batch.totp3d_batch(paths, prm)
+    torch.cuda.synchronize()
+    n_pts = first["n_points"].cpu().numpy()
+    n_smp = first["n_samples"].cpu().numpy()
+    assert (first["status"].cpu().numpy() == 0).all()
+    pc = int(n_pts.max())
+    L = _lib.load_library()
+    ctx = _lib.context()
+    npath = len(paths)
+    off = np.zeros(npath + 1, np.int32)
+    off[1:] = np.cumsum([len(a) for a in paths])
+    flat = torch.as_tensor(np.concatenate(paths), device="cuda")
+    off_d = torch.as_tensor(off, device="cuda")
+    nmax = int(max(len(a) for a in paths))
+    sc = int(first["s_values"].shape[1])
+    out = {k: torch.empty_like(first[k]) for k in ("s_values", "s_dot", "s_ddot", "time", "n_samples", "n_points",
+                                                   "total_time", "status")}
+    pts = torch.empty((npath, pc, 12), dtype=torch.float64, device="cuda")
+
+    def run(i):
+        rc = L.pmp_totp3d_batch(ctx, _lib.stream_ptr(), ctypes.byref(prm), npath, flat.data_ptr(), off_d.data_ptr(),
+                                nmax, sc, out["s_values"].data_ptr(), out["s_dot"].data_ptr(), out["s_ddot"].data_ptr(),
+                                out["time"].data_ptr(), out["n_samples"].data_ptr(), pc, pts.data_ptr(),
+                                out["n_points"].data_ptr(), out["total_time"].data_ptr(), out["status"].data_ptr(),
+                                None, 0)
+        if rc:
+            _lib.check(ctx, rc, "pmp_totp3d_batch")
+
+    elapsed, kern_ms = timed(torch, dist, run, args.a3_steps)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+
+        th = cpu_threads()
+        op = O.TotpParams.make(cons["max_velocity"], cons["max_acceleration"], cons["min_time_step"],
+                               cons["path_resolution"])
+        ref = O.totp3d_batch(paths, op, sample_cap=sc, point_cap=pc, nthreads=th)
+        assert np.array_equal(ref["n_points"], out["n_points"].cpu().numpy()), "GPU/oracle trajectory length mismatch"
+        np.testing.assert_allclose(ref["total_time"], out["total_time"].cpu().numpy(), rtol=1e-9)
+        reps, dt = timed_cpu(lambda r: O.totp3d_batch(paths, op, sample_cap=sc, point_cap=pc, nthreads=th),
+                             args.cpu_seconds)
+        sub = paths[: max(1, npath // 16)]
+        reps1, dt1 = timed_cpu(lambda r: O.totp3d_batch(sub, op, sample_cap=sc, point_cap=pc, nthreads=1), 1.0)
+        cpu = {"value": npath * reps / dt, "unit": "trajectories/s", "cores": th, "kind": "port", "host": host_cpu(),
+               "sample": f"all {npath} C5 paths x {reps}, C restatement of TimeOptimalTrajectory3D.generate() "
+                         f"(oracle/pmp_oracle.c) with OpenMP over paths, {dt:.1f} s wall",
+               "one_core": {"value": len(sub) * reps1 / dt1, "sample": f"{len(sub)} paths x {reps1}, {dt1:.1f} s"}}
+    return {"metric": "C5 time-optimal trajectories/sec (TimeOptimalTrajectory3D.generate on the 3D A* paths)",
+            "value": npath * args.a3_steps * world / elapsed, "unit": "trajectories/s", "paths_per_gpu": npath,
+            "steps": args.a3_steps, "ms_per_step": elapsed / args.a3_steps * 1e3, "kernel_ms_per_launch": kern_ms,
+            "dtype": "f64", "config": {"workload": "C5 paths, 3d_example.py constraints, path_resolution 0.05"},
+            "roofline": None,
+            "roofline_note": "latency-bound: two sequential velocity recurrences per path (each step depends on the "
+                             "last through the centripetal term), one wave per path; no HBM or MFMA roofline applies",
+            "detail": {"samples_per_launch": int(n_smp.sum()), "points_per_launch": int(n_pts.sum()),
+                       "max_points": pc},
             "cpu_baseline": cpu}
 
 
@@ -799,9 +894,10 @@ def track_leg(args, torch, dist, world, rank, kind):
             "unit": "agent-steps/s", "agents_per_gpu": na, "iterations_per_launch": iters, "steps": args.track_steps,
             "ms_per_step": elapsed / args.track_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
             "config": {"workload": f"C4 agents on the README grid, {iters} LQR/MPC plan iterations per launch"},
-            "roofline": with_traffic({"bound": "fp64-valu", "achieved": achieved_tf, "peak": 78.6, "unit": "TFLOP/s",
-                                      "frac": achieved_tf / 78.6, "traffic": None},
-                                     "track_kernel_lqr" if kind == "lqr" else "track_kernel_mpc"),
+            "roofline": with_mfma(with_traffic({"bound": "fp64-valu", "achieved": achieved_tf, "peak": 78.6,
+                                                "unit": "TFLOP/s", "frac": achieved_tf / 78.6, "traffic": None},
+                                               "track_kernel_lqr" if kind == "lqr" else "track_kernel_mpc"),
+                                  "track_kernel_lqr" if kind == "lqr" else "track_kernel_mpc"),
             "detail": {"agent_steps_per_launch": stepped, "admm_iterations_per_launch": admm},
             "cpu_baseline": cpu}
 
@@ -853,9 +949,9 @@ def main():
     ap.add_argument("--agents", type=int, default=256, help="C4 agents per GPU (control-step leg)")
     ap.add_argument("--control-steps", type=int, default=20, help="timed control steps")
     ap.add_argument("--workers", type=int, default=3072, help="persistent A* workers (waves) per launch")
-    ap.add_argument("--legs", default="dwa,rrt,astar3d,lqr,mpc,graphs,dstar,dyn3d,latency",
-                    help="secondary legs to run (comma list of dwa, rrt, astar3d, lqr, mpc, graphs, dstar, dyn3d, "
-                         "latency; 'none' for none)")
+    ap.add_argument("--legs", default="dwa,rrt,astar3d,totp,lqr,mpc,graphs,dstar,dyn3d,latency",
+                    help="secondary legs to run (comma list of dwa, rrt, astar3d, totp (C5 trajectories on the "
+                         "astar3d leg's paths), lqr, mpc, graphs, dstar, dyn3d, latency; 'none' for none)")
     ap.add_argument("--dyn3d-queries", type=int, default=8192, help="C5 queries per DStar3D / LPAStar3D launch")
     ap.add_argument("--dyn3d-steps", type=int, default=2)
     ap.add_argument("--dstar-queries", type=int, default=1024, help="queries per D* launch (256^2 and 512^2 grids)")

@@ -24,6 +24,7 @@ KERNELS = {  # short name -> regex on the demangled kernel name
     "lpa3d_kernel": r"lpa3d_kernel\(",
     "track_kernel_lqr": r"track_kernel<0>",
     "track_kernel_mpc": r"track_kernel<1>",
+    "totp3d_kernel": r"totp3d_kernel\(",
 }
 
 
