@@ -239,6 +239,21 @@ __device__ __forceinline__ void bit_write(const Heap& h, bool on, const Lvl& L, 
     }
 }
 
+// bit_write for one wave-uniform bit value, by lane 0 (any heap size)
+__device__ __forceinline__ void bit_write1(const Heap& h, int lane, const Lvl& L, uint32_t Pl, bool bit)
+{
+    const uint32_t R = Pl >> L.r;
+    const uint32_t m = 1u << ((Pl & L.mr) + L.mr);
+    if (lane != 0) return;
+    if (L.t <= 2) {
+        ds_mskor(h.B + (int)R + L.off, m, bit ? m : 0u);
+    } else {
+        uint32_t* w = h.hb + hb_word(L.t, R);
+        if (bit) __hip_atomic_fetch_or(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else __hip_atomic_fetch_and(w, ~m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // Lane mask of the lanes where a < b under Node.__lt__ (node.py:51-54) on (f, h) pairs, h ordered by
 // hkey(cm); compares go straight to lane masks (no bool round trips through VGPRs).
 template <int HEUR>
@@ -296,9 +311,19 @@ __device__ __forceinline__ void wave_sync_mem()
 //  3. the children that move up are the prefix with !(last < heap[p_i]) (the path is sorted), so a
 //     ballot popcount m places `last` at p_m -- the array CPython's _siftup + _siftdown produce;
 //  4. lanes 1..m rewrite the bits of p_0..p_{m-1}, whose children changed.
+// What a pop wrote, for callers that hold heap values loaded before it (the parent window): the
+// leaf's path number P and level K, the mover count m (p_{j-1} <- A_j for j <= m, p_m <- last) and
+// lane j's A_j = heap[p_j] before the pop.
+struct PopOut {
+    uint32_t P;
+    int K, m;
+    double Af;
+    uint32_t Ac;
+};
+
 template <bool SPILL, bool BIG, int HEUR>
 __device__ __forceinline__ void heap_pop(const Heap& h, int n, uint32_t v01, double& lastf, uint32_t& lastc, double& rootf,
-                                         uint32_t& rootc, const Lvl& pl, int lane)
+                                         uint32_t& rootc, const Lvl& pl, int lane, PopOut& po)
 {
     n = uni(n);
     // `last` = heap[n] is kept in registers by the caller (no load round); v01 = the tier-0 word
@@ -420,6 +445,11 @@ __device__ __forceinline__ void heap_pop(const Heap& h, int n, uint32_t v01, dou
         const uint64_t bits = choice_bits<HEUR>(pi, useb ? Bf : lf, useb ? Bc : lc, Sf, Sc);
         bit_write<BIG>(h, hass && lane <= m, pl, P >> (sh + 1), bits);
     }
+    po.P = P;
+    po.K = K;
+    po.m = m;
+    po.Af = Af;
+    po.Ac = Ac;
     wave_sync_mem();
 }
 
@@ -428,7 +458,8 @@ __device__ __forceinline__ void heap_pop(const Heap& h, int n, uint32_t v01, dou
 // many move down; lanes 1..t+1 rewrite the bits of a_1..a_{t+1}, whose children changed.
 template <bool SPILL, bool BIG, int HEUR>
 __device__ __forceinline__ void heap_push(const Heap& h, int n, double itf, uint32_t itc, uint32_t itk, double& lastf,
-                                          uint32_t& lastc, double& rootf, uint32_t& rootc, int lane)
+                                          uint32_t& lastc, double& rootf, uint32_t& rootc, int lane, int& t_out,
+                                          double& a1f, uint32_t& a1c)
 {
     n = uni(n);
     const uint32_t np1 = (uint32_t)n + 1u;
@@ -450,6 +481,10 @@ __device__ __forceinline__ void heap_push(const Heap& h, int n, double itf, uint
     }
     const int t = __popcll(lt_mask<HEUR>(on, itf, itc, Af, Ac));  // the "less" set is a prefix from the parent up
     const int ipos = (int)(np1 >> t) - 1;
+    // the new heap[a_1] (the parent): the item when it stops there, else a_2's old entry
+    t_out = t;
+    a1f = t >= 2 ? rl_f64(Af, 2) : itf;
+    a1c = t >= 2 ? rl_u32(Ac, 2) : itc;
     {
         const bool l0 = lane == 0;
         const bool st = l0 || (on && lane <= t);
@@ -477,20 +512,30 @@ __device__ __forceinline__ void heap_push(const Heap& h, int n, double itf, uint
 
 template <int HEUR>
 __device__ __forceinline__ void pop_any(const Heap& h, int n, uint32_t v01, double& lastf, uint32_t& lastc, double& rootf,
-                                        uint32_t& rootc, const Lvl& pl, int lane)
+                                        uint32_t& rootc, const Lvl& pl, int lane, PopOut& po)
 {
-    if (n < h.cap) heap_pop<false, false, HEUR>(h, n, v01, lastf, lastc, rootf, rootc, pl, lane);
-    else if (n < kBigHeap) heap_pop<true, false, HEUR>(h, n, v01, lastf, lastc, rootf, rootc, pl, lane);
-    else heap_pop<true, true, HEUR>(h, n, v01, lastf, lastc, rootf, rootc, pl, lane);
+    if (n < h.cap) heap_pop<false, false, HEUR>(h, n, v01, lastf, lastc, rootf, rootc, pl, lane, po);
+    else if (n < kBigHeap) heap_pop<true, false, HEUR>(h, n, v01, lastf, lastc, rootf, rootc, pl, lane, po);
+    else heap_pop<true, true, HEUR>(h, n, v01, lastf, lastc, rootf, rootc, pl, lane, po);
 }
 template <int HEUR>
 __device__ __forceinline__ void push_any(const Heap& h, int n, double itf, uint32_t itc, uint32_t itk, double& lastf,
-                                         uint32_t& lastc, double& rootf, uint32_t& rootc, int lane)
+                                         uint32_t& lastc, double& rootf, uint32_t& rootc, int lane, int& t,
+                                         double& a1f, uint32_t& a1c)
 {
-    if (n < h.cap) heap_push<false, false, HEUR>(h, n, itf, itc, itk, lastf, lastc, rootf, rootc, lane);
-    else if (n < kBigHeap) heap_push<true, false, HEUR>(h, n, itf, itc, itk, lastf, lastc, rootf, rootc, lane);
-    else heap_push<true, true, HEUR>(h, n, itf, itc, itk, lastf, lastc, rootf, rootc, lane);
+    if (n < h.cap) heap_push<false, false, HEUR>(h, n, itf, itc, itk, lastf, lastc, rootf, rootc, lane, t, a1f, a1c);
+    else if (n < kBigHeap) heap_push<true, false, HEUR>(h, n, itf, itc, itk, lastf, lastc, rootf, rootc, lane, t, a1f, a1c);
+    else heap_push<true, true, HEUR>(h, n, itf, itc, itk, lastf, lastc, rootf, rootc, lane, t, a1f, a1c);
 }
+
+// Parent window.  On a spilled heap (size after the pop n1 >= lds_cap) the pushes of one expansion
+// take positions n1 .. n1 + 7, whose parents are the (at most 5) positions (n1 - 1) / 2 + 0..4.
+// Lanes kWin0..kWin0+4 load them in the expansion's first memory round, next to the 3x3 block, and
+// keep them current through the pop (patched from PopOut) and the pushes.  A push whose item is not
+// less than its parent -- 73 % of C2's pushes -- then needs no memory round: CPython's _siftdown
+// stops at once (t = 0), the item is stored at position n, and the parent's choice bit, when n is a
+// right child, compares the item with heap[n - 1] = `last`, already in registers.
+constexpr int kWin0 = 24;
 
 // ThetaStar.lineOfSight (theta_star.py:110-171): Bresenham from (x1, y1) to (x2, y2) over the bit
 // grid; tau = (d_y - d_x) / 2 is compared as 2e against d_y - d_x.  Both endpoints are in the grid
@@ -687,6 +732,14 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 const uint32_t plin = nlin - (uint32_t)rl_u32((uint32_t)par_off, ndir);
                 if (lane == 18) gpar = G[plin];
             }
+            // the parent window, loaded in the same round (before the pop; patched after it)
+            const int n1 = n;  // the heap size after this pop
+            const bool use_win = n1 >= hp.cap;
+            const int wlo = (n1 - 1) >> 1;
+            const int wpos = wlo + (lane - kWin0);
+            const bool won = lane >= kWin0 && lane < kWin0 + 5;
+            Ld<true> wld;
+            if (use_win) wld.issue(hp, won ? wpos : 0);
 #ifdef PMP_STAMPS_SPLIT  // diagnostic: wait for the HBM round before the pop, time the two apart
             asm volatile("s_waitcnt vmcnt(0)" ::"v"(blk_word), "v"(gpar) : "memory");
             STAMP(tsB);
@@ -695,7 +748,10 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
 #endif
 
             // ---- heappop (a_star.py:54): `last` = heap[n] sifts down the CPython path
-            if (n > 0) pop_any<HEUR>(hp, n, v01, lastf, lastc, rootf, rootc, pop_lvl, lane);
+            PopOut po;
+            const double oldlf = lastf;
+            const uint32_t oldlc = lastc;
+            if (n > 0) pop_any<HEUR>(hp, n, v01, lastf, lastc, rootf, rootc, pop_lvl, lane, po);
 
             STAMP(ts1);
             // 3x3 masks: bit k = cell (x + k/3 - 1, y + k%3 - 1); the node is k = 4
@@ -710,6 +766,21 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
             }
 #endif
             if (cls9 & 16u) continue;  // node.current in CLOSED (a_star.py:57-58)
+
+            // the parent window after the pop: p_{j-1} <- A_j (j <= m), p_m <- the old last
+            double wf = 0.0;
+            uint32_t wc = 0u;
+            if (use_win) {
+                wld.get(wf, wc);
+                const int lw = 31 - __clz(wpos + 1);  // level of this lane's position
+                const int src = min(lw + 1, 63);
+                const double af = __shfl(po.Af, src);
+                const uint32_t ac = (uint32_t)__shfl((int)po.Ac, src);
+                if (won && lw <= po.m && (int)(po.P >> (po.K - lw)) - 1 == wpos) {
+                    wf = lw == po.m ? oldlf : af;
+                    wc = lw == po.m ? oldlc : ac;
+                }
+            }
 
             // CLOSED[node.current] = node (a_star.py:82).  The node's state word was loaded by lane 13
             // and only this wave writes it: store it back now (fire-and-forget, off the critical path).
@@ -838,7 +909,40 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 const int m = __ffsll((long long)vm) - 1;
                 vm &= vm - 1;
                 if (n >= heap_cap) { overflow = true; break; }
-                push_any<HEUR>(hp, n, rl_f64(ifv, m), rl_u32(icm, m), rl_u32(ik, m), lastf, lastc, rootf, rootc, lane);
+                const double itf = rl_f64(ifv, m);
+                const uint32_t itc = rl_u32(icm, m), itk = rl_u32(ik, m);
+                if (use_win) {
+                    const int wl = kWin0 + (((n - 1) >> 1) - wlo);  // the lane holding heap[parent(n)]
+                    const double pf = rl_f64(wf, wl);
+                    const uint32_t pc = rl_u32(wc, wl);
+                    if (!key_lt(itf, itk, pf, hkey<HEUR>(pc))) {
+                        // t = 0: heap[n] = item; a right child (n even) sets its parent's bit against
+                        // its left sibling heap[n - 1] = last
+                        if ((n & 1) == 0) {
+                            const uint32_t np1 = (uint32_t)n + 1u;
+                            const bool bit = !key_lt(lastf, hkey<HEUR>(lastc), itf, itk);
+                            bit_write1(hp, lane, lvl_of(30 - __clz((int)np1)), np1 >> 1, bit);
+                        }
+                        hst<true>(hp, lane == 0, n, itf, itc);
+                        lastf = itf;
+                        lastc = itc;
+                        wave_sync_mem();
+                    } else {
+                        int t;
+                        double a1f;
+                        uint32_t a1c;
+                        push_any<HEUR>(hp, n, itf, itc, itk, lastf, lastc, rootf, rootc, lane, t, a1f, a1c);
+                        if (lane == wl) {
+                            wf = a1f;
+                            wc = a1c;
+                        }
+                    }
+                } else {
+                    int t;
+                    double a1f;
+                    uint32_t a1c;
+                    push_any<HEUR>(hp, n, itf, itc, itk, lastf, lastc, rootf, rootc, lane, t, a1f, a1c);
+                }
                 n += 1;
                 npush++;
             }
