@@ -370,7 +370,7 @@ def rrt_leg(args, torch, dist, world, rank):
 def astar3d_leg(args, torch, dist, world, rank):
     """C5: AStar3D on Grid3D(26,20,16) door scenario, 8192 queries per GPU (random.seed(i) pairs,
     safety bubbles carved per query, so each query has its own occupancy)."""
-    from python_motion_planning_amd import _lib, batch, workloads as wl
+    from python_motion_planning_amd import _lib, batch, shard, workloads as wl
 
     nq = args.a3_queries
     occ, s, g = wl.c5_workload(nq, first_seed=rank * nq)
@@ -380,26 +380,54 @@ def astar3d_leg(args, torch, dist, world, rank):
     s_d = torch.as_tensor(s, device="cuda")
     g_d = torch.as_tensor(g, device="cuda")
     L = _lib.load_library()
-    ctx = _lib.context()
     cap = X * Y * Z + 1
-    cost = torch.empty(nq, dtype=torch.float64, device="cuda")
-    plen = torch.empty(nq, dtype=torch.int32, device="cuda")
-    path = torch.empty((nq, cap), dtype=torch.int32, device="cuda")
-    nexp = torch.empty(nq, dtype=torch.int32, device="cuda")
-    st = torch.empty(nq, dtype=torch.int32, device="cuda")
+    # batches in flight (own stream + pmp_ctx each): a launch lasts as long as its longest query (the
+    # longest-first schedule starts it first), and the next launch's workers fill the CUs the
+    # finished ones free
+    lanes = []
+    for _ in range(max(1, args.a3_streams)):
+        ctx = L.pmp_create(torch.cuda.current_device())
+        _lib.check(ctx, L.pmp_graph3d_set_workers(ctx, args.a3_workers_per_cu), "workers")
+        lanes.append(dict(ctx=ctx, stream=torch.cuda.Stream(),
+                          cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
+                          plen=torch.empty(nq, dtype=torch.int32, device="cuda"),
+                          path=torch.empty((nq, cap), dtype=torch.int32, device="cuda"),
+                          nexp=torch.empty(nq, dtype=torch.int32, device="cuda"),
+                          st=torch.empty(nq, dtype=torch.int32, device="cuda")))
     ctr = torch.empty((nq, 4), dtype=torch.int64, device="cuda")
 
     def run(i, counters=None):
-        rc = L.pmp_astar3d_batch(ctx, _lib.stream_ptr(), occ_d.data_ptr(), 1, X, Y, Z, 0, s_d.data_ptr(), g_d.data_ptr(),
-                                 nq, cost.data_ptr(), plen.data_ptr(), path.data_ptr(), cap, nexp.data_ptr(), None, 0,
-                                 counters, st.data_ptr())
+        b = lanes[i % len(lanes)]
+        rc = L.pmp_astar3d_batch(b["ctx"], b["stream"].cuda_stream, occ_d.data_ptr(), 1, X, Y, Z, 0, s_d.data_ptr(),
+                                 g_d.data_ptr(), nq, b["cost"].data_ptr(), b["plen"].data_ptr(), b["path"].data_ptr(), cap,
+                                 b["nexp"].data_ptr(), None, 0, counters, b["st"].data_ptr())
         if rc:
-            _lib.check(ctx, rc, "pmp_astar3d_batch")
+            _lib.check(b["ctx"], rc, "pmp_astar3d_batch")
 
     run(0, ctr.data_ptr())
+    for i in range(1, len(lanes)):
+        run(i)
     torch.cuda.synchronize()
     c = ctr.cpu().numpy()
-    elapsed, kern_ms = timed(torch, dist, run, args.a3_steps)
+    cost, plen, path = lanes[0]["cost"], lanes[0]["plen"], lanes[0]["path"]
+    for b in lanes[1:]:
+        assert torch.equal(b["cost"], cost) and torch.equal(b["st"], lanes[0]["st"])
+    shard.barrier(dist)
+    torch.cuda.synchronize()
+    evs = []
+    t0 = time.perf_counter()
+    for i in range(args.a3_steps):
+        b = lanes[i % len(lanes)]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(b["stream"])
+        run(i)
+        e1.record(b["stream"])
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    shard.barrier(dist)
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(e) for a, e in evs]))
+    elapsed, kern_ms = shard.max_over_ranks(dist, [elapsed, kern_ms], "cuda")
     # per plan 55*E3 + 16*(P3 + Q3), with P3 the reference's pushes and Q3 <= P3
     # (every pushed entry popped at most once): 55*E3 + 32*P3
     alg_bytes = float(np.sum(55.0 * c[:, 2] + 32.0 * c[:, 0]))
@@ -423,9 +451,13 @@ def astar3d_leg(args, torch, dist, world, rank):
                "sample": f"all {nq} C5 queries, repeated {reps}x, C restatement of AStar3D (oracle/pmp_oracle.c) "
                          f"with OpenMP over queries, {dt:.1f} s wall"}
     traj = totp3d_leg(args, torch, dist, world, rank, plen, path, (X, Y, Z)) if "totp" in args.legs.split(",") else None
+    torch.cuda.synchronize()
+    for b in lanes:  # the lanes' scratch (about 15 GB each) is not needed by the other legs
+        L.pmp_destroy(b["ctx"])
     return {"metric": "3D A* plans/sec, Grid3D(26,20,16) door scenario, 8192 queries", "value": nq * args.a3_steps * world / elapsed,
             "unit": "plans/s", "queries_per_gpu": nq, "steps": args.a3_steps,
             "ms_per_step": elapsed / args.a3_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
+            "streams": len(lanes), "workers_per_cu": args.a3_workers_per_cu,
             "config": {"workload": "C5: Grid3D(26,20,16) door, random.seed(i) pairs, safety bubbles r=1, euclidean"},
             "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                       "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -966,7 +998,9 @@ def main():
     ap.add_argument("--rrt-streams", type=int, default=3, help="RRT* batches in flight (own stream + context each)")
     ap.add_argument("--rrt-cpu-sample", type=int, default=16)
     ap.add_argument("--a3-queries", type=int, default=8192)
-    ap.add_argument("--a3-steps", type=int, default=3)
+    ap.add_argument("--a3-steps", type=int, default=32)
+    ap.add_argument("--a3-streams", type=int, default=4, help="3D A* batches in flight (own stream + context each)")
+    ap.add_argument("--a3-workers-per-cu", type=int, default=16, help="3D A* persistent workers per CU")
     ap.add_argument("--track-iters", type=int, default=20)
     ap.add_argument("--track-steps", type=int, default=5)
     ap.add_argument("--schedule", choices=["lpt", "input"], default="lpt",

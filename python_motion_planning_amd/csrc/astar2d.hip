@@ -528,14 +528,7 @@ __device__ __forceinline__ void push_any(const Heap& h, int n, double itf, uint3
     else heap_push<true, true, HEUR>(h, n, itf, itc, itk, lastf, lastc, rootf, rootc, lane, t, a1f, a1c);
 }
 
-// Parent window.  On a spilled heap (size after the pop n1 >= lds_cap) the pushes of one expansion
-// take positions n1 .. n1 + 7, whose parents are the (at most 5) positions (n1 - 1) / 2 + 0..4.
-// Lanes kWin0..kWin0+4 load them in the expansion's first memory round, next to the 3x3 block, and
-// keep them current through the pop (patched from PopOut) and the pushes.  A push whose item is not
-// less than its parent -- 73 % of C2's pushes -- then needs no memory round: CPython's _siftdown
-// stops at once (t = 0), the item is stored at position n, and the parent's choice bit, when n is a
-// right child, compares the item with heap[n - 1] = `last`, already in registers.
-constexpr int kWin0 = 24;
+
 
 // ThetaStar.lineOfSight (theta_star.py:110-171): Bresenham from (x1, y1) to (x2, y2) over the bit
 // grid; tau = (d_y - d_x) / 2 is compared as 2e against d_y - d_x.  Both endpoints are in the grid
@@ -732,14 +725,6 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 const uint32_t plin = nlin - (uint32_t)rl_u32((uint32_t)par_off, ndir);
                 if (lane == 18) gpar = G[plin];
             }
-            // the parent window, loaded in the same round (before the pop; patched after it)
-            const int n1 = n;  // the heap size after this pop
-            const bool use_win = n1 >= hp.cap;
-            const int wlo = (n1 - 1) >> 1;
-            const int wpos = wlo + (lane - kWin0);
-            const bool won = lane >= kWin0 && lane < kWin0 + 5;
-            Ld<true> wld;
-            if (use_win) wld.issue(hp, won ? wpos : 0);
 #ifdef PMP_STAMPS_SPLIT  // diagnostic: wait for the HBM round before the pop, time the two apart
             asm volatile("s_waitcnt vmcnt(0)" ::"v"(blk_word), "v"(gpar) : "memory");
             STAMP(tsB);
@@ -749,8 +734,6 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
 
             // ---- heappop (a_star.py:54): `last` = heap[n] sifts down the CPython path
             PopOut po;
-            const double oldlf = lastf;
-            const uint32_t oldlc = lastc;
             if (n > 0) pop_any<HEUR>(hp, n, v01, lastf, lastc, rootf, rootc, pop_lvl, lane, po);
 
             STAMP(ts1);
@@ -767,20 +750,6 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
 #endif
             if (cls9 & 16u) continue;  // node.current in CLOSED (a_star.py:57-58)
 
-            // the parent window after the pop: p_{j-1} <- A_j (j <= m), p_m <- the old last
-            double wf = 0.0;
-            uint32_t wc = 0u;
-            if (use_win) {
-                wld.get(wf, wc);
-                const int lw = 31 - __clz(wpos + 1);  // level of this lane's position
-                const int src = min(lw + 1, 63);
-                const double af = __shfl(po.Af, src);
-                const uint32_t ac = (uint32_t)__shfl((int)po.Ac, src);
-                if (won && lw <= po.m && (int)(po.P >> (po.K - lw)) - 1 == wpos) {
-                    wf = lw == po.m ? oldlf : af;
-                    wc = lw == po.m ? oldlc : ac;
-                }
-            }
 
             // CLOSED[node.current] = node (a_star.py:82).  The node's state word was loaded by lane 13
             // and only this wave writes it: store it back now (fire-and-forget, off the critical path).
@@ -911,32 +880,23 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 if (n >= heap_cap) { overflow = true; break; }
                 const double itf = rl_f64(ifv, m);
                 const uint32_t itc = rl_u32(icm, m), itk = rl_u32(ik, m);
-                if (use_win) {
-                    const int wl = kWin0 + (((n - 1) >> 1) - wlo);  // the lane holding heap[parent(n)]
-                    const double pf = rl_f64(wf, wl);
-                    const uint32_t pc = rl_u32(wc, wl);
-                    if (!key_lt(itf, itk, pf, hkey<HEUR>(pc))) {
-                        // t = 0: heap[n] = item; a right child (n even) sets its parent's bit against
-                        // its left sibling heap[n - 1] = last
-                        if ((n & 1) == 0) {
-                            const uint32_t np1 = (uint32_t)n + 1u;
-                            const bool bit = !key_lt(lastf, hkey<HEUR>(lastc), itf, itk);
-                            bit_write1(hp, lane, lvl_of(30 - __clz((int)np1)), np1 >> 1, bit);
-                        }
-                        hst<true>(hp, lane == 0, n, itf, itc);
-                        lastf = itf;
-                        lastc = itc;
-                        wave_sync_mem();
-                    } else {
-                        int t;
-                        double a1f;
-                        uint32_t a1c;
-                        push_any<HEUR>(hp, n, itf, itc, itk, lastf, lastc, rootf, rootc, lane, t, a1f, a1c);
-                        if (lane == wl) {
-                            wf = a1f;
-                            wc = a1c;
-                        }
-                    }
+                // CPython's _siftdown stops at once when the item is not less than its parent (73 % of
+                // C2's pushes): probe the parent first, and run the full push only when it moves
+                double pf;
+                uint32_t pc;
+                hld<true>(hp, n > 0 ? (n - 1) >> 1 : 0, pf, pc);
+                pf = rl_f64(pf, 0);
+                pc = rl_u32(pc, 0);
+                if (n > 0 && !key_lt(itf, itk, pf, hkey<HEUR>(pc))) {
+                    // t = 0: heap[n] = item; a right child (n even) sets its parent's bit against its
+                    // left sibling heap[n - 1] = last
+                    if ((n & 1) == 0)
+                        bit_write1(hp, lane, lvl_of(30 - __clz(n + 1)), ((uint32_t)n + 1u) >> 1,
+                                   !key_lt(lastf, hkey<HEUR>(lastc), itf, itk));
+                    hst<true>(hp, lane == 0, n, itf, itc);
+                    lastf = itf;
+                    lastc = itc;
+                    wave_sync_mem();
                 } else {
                     int t;
                     double a1f;

@@ -131,7 +131,7 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
     uint32_t* __restrict__ expand_out, int expand_cap, int64_t* __restrict__ counters, int32_t* __restrict__ status_out,
     int* __restrict__ queue, uint4* __restrict__ spill_all, int heap_cap, int lds_cap, uint8_t* __restrict__ cdir_all,
     double* __restrict__ cg_all, int gzero, uint32_t* __restrict__ cpar_all, uint32_t* __restrict__ ppar_all,
-    uint32_t ppar_cap)
+    uint32_t ppar_cap, const int32_t* __restrict__ order, int prio_n)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
@@ -159,7 +159,11 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
     for (;;) {
         const int qi = next_query(queue, lane);
         if (qi >= nq) break;
-        const int q = qi;
+        const int q = uni(order ? order[qi] : qi);
+        // the longest queries (first in the longest-first order) run at raised priority: they set the
+        // launch's tail, the short ones fill the issue slots they leave idle
+        if (qi < prio_n) __builtin_amdgcn_s_setprio(3);
+        else __builtin_amdgcn_s_setprio(0);
         const uint32_t* occ = occ_all + (per_query ? (size_t)q * words : 0);
         if (OCC_LDS)
             for (size_t i = lane; i < words; i += 64) occl[i] = occ[i];
@@ -459,6 +463,33 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
     }
 }
 
+// ---- longest-first schedule: counting sort of the queries by descending start-goal distance ----
+__device__ __forceinline__ int lpt3_key(const int32_t* s, const int32_t* g, int q)
+{
+    const int dx = s[3 * q] - g[3 * q], dy = s[3 * q + 1] - g[3 * q + 1], dz = s[3 * q + 2] - g[3 * q + 2];
+    return (int)__dsqrt_rn((double)(dx * dx + dy * dy + dz * dz));
+}
+__global__ void lpt3_hist(const int32_t* s, const int32_t* g, int nq, int nb, int* hist)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nq) atomicAdd(&hist[min(lpt3_key(s, g, q), nb - 1)], 1);
+}
+__global__ void lpt3_scan(int nb, int* hist)  // offsets[k] = queries with a larger key; one thread
+{
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    int run = 0;
+    for (int k = nb - 1; k >= 0; k--) {
+        const int c = hist[k];
+        hist[k] = run;
+        run += c;
+    }
+}
+__global__ void lpt3_scatter(const int32_t* s, const int32_t* g, int nq, int nb, int* offs, int32_t* order)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nq) order[atomicAdd(&offs[min(lpt3_key(s, g, q), nb - 1)], 1)] = q;
+}
+
 // per-context scratch budget of the 3D planners (heap spill + closed state + Theta* parents per worker)
 constexpr size_t kScratchBudget3 = (size_t)32 << 30;
 
@@ -484,9 +515,12 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar3d_batch: null pointer argument");
     PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     const size_t ncell = (size_t)X * Y * Z;
-    int workers = 256 * 4;
+    // workers per CU: the configured count (default 16: C5's 8192-query batches run fastest at 16-24,
+    // tools/astar3d_sweep.py), but no more than the batch fills, so small batches get a larger LDS
+    // heap share per worker
+    const int per_cu = std::max(1, std::min(ctx->a3_per_cu > 0 ? ctx->a3_per_cu : 16, (nq + 255) / 256));
+    int workers = 256 * per_cu;
     if (workers > nq) workers = nq;
-    const int per_cu = 4;
     const size_t words = (ncell + 31) / 32;
     const bool occ_lds = words <= (size_t)kOccLdsWords;
     const int occ_bytes = occ_lds ? kOccLdsWords * 4 : 0;
@@ -519,12 +553,24 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     if (!spill || !cdir || !cg || !queue) return PMP_ENOMEM;
     hipStream_t s = (hipStream_t)stream;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
+    int32_t* order = nullptr;
+    if (ctx->astar_lpt && nq > workers) {
+        const int nb = (int)ceil(sqrt((double)X * X + (double)Y * Y + (double)Z * Z)) + 1;
+        int* hist = (int*)pmp_scratch(ctx, SCR_PDIR, sizeof(int) * ((size_t)nb + (size_t)nq));
+        if (!hist) return PMP_ENOMEM;
+        order = hist + nb;
+        PMP_HIP_CHECK(ctx, hipMemsetAsync(hist, 0, sizeof(int) * (size_t)nb, s));
+        hipLaunchKernelGGL(lpt3_hist, dim3((nq + 255) / 256), dim3(256), 0, s, start_xyz, goal_xyz, nq, nb, hist);
+        hipLaunchKernelGGL(lpt3_scan, dim3(1), dim3(64), 0, s, nb, hist);
+        hipLaunchKernelGGL(lpt3_scatter, dim3((nq + 255) / 256), dim3(256), 0, s, start_xyz, goal_xyz, nq, nb, hist, order);
+    }
     auto kern = occ_lds ? (theta == 1 ? astar3d_kernel<true, 1> : theta == 2 ? astar3d_kernel<true, 2> : astar3d_kernel<true, 0>)
                         : (theta == 1 ? astar3d_kernel<false, 1> : theta == 2 ? astar3d_kernel<false, 2> : astar3d_kernel<false, 0>);
     hipLaunchKernelGGL(kern, dim3(workers), dim3(64), (size_t)lds_cap * 16 + occ_bytes, s, occ_bits, per_query, X, Y, Z,
                        algo == PMP_ALGO_DIJKSTRA ? 2 : heuristic, start_xyz, goal_xyz, nq, cost, path_len, path, path_cap,
                        n_expanded, expand, expand_cap, counters, status, queue, spill, heap_cap, lds_cap, cdir, cg,
-                       algo == PMP_ALGO_GBFS ? 1 : 0, tpar, tpar ? tpar + (size_t)workers * ncell : nullptr, ppar_cap);
+                       algo == PMP_ALGO_GBFS ? 1 : 0, tpar, tpar ? tpar + (size_t)workers * ncell : nullptr, ppar_cap,
+                       (const int32_t*)order, order ? ctx->astar_prio_n : 0);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }

@@ -18,3 +18,6 @@ ne = ref["n_expanded"].cpu().numpy().astype(np.float64)
 print(f"per expansion cycles: pop {st[:, 0].sum() / ne.sum():.0f}  after-pop wait {st[:, 1].sum() / ne.sum():.0f}  "
       f"push loop {st[:, 2].sum() / ne.sum():.0f}  total {st[:, 3].sum() / ne.sum():.0f}; "
       f"per query total {st[:, 3].mean():.0f} cycles, expansions {ne.mean():.0f}")
+i = int(np.argmax(st[:, 3]))
+print(f"slowest query {i}: {st[i, 3]:.0f} cycles, {ne[i]:.0f} expansions ({st[i, 3] / max(ne[i], 1):.0f} per expansion; "
+      f"pop {st[i, 0] / max(ne[i], 1):.0f} wait {st[i, 1] / max(ne[i], 1):.0f} push {st[i, 2] / max(ne[i], 1):.0f})")

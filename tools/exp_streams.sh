@@ -1,8 +1,8 @@
-# dev experiment: A* headline vs persistent workers per launch (LDS heap share per worker), 4 batches in flight
+# dev experiment: A* headline vs batches in flight (one stream + scratch context each)
 set -e
 mkdir -p gpurun_out
-: > gpurun_out/workers.log
-for w in 2048 2560 3072 3328; do
-  echo "workers=$w" >> gpurun_out/workers.log
-  timeout -k 10 150 python -u bench.py --legs none --no-cpu-baseline --steps 20 --warmup 4 --workers $w >> gpurun_out/workers.log 2>&1
+: > gpurun_out/streams.log
+for s in ${STREAMS:-4 6 4 6}; do
+  echo "streams=$s" >> gpurun_out/streams.log
+  timeout -k 10 200 python -u bench.py --legs none --no-cpu-baseline --steps 12 --warmup 6 --streams $s >> gpurun_out/streams.log 2>&1
 done

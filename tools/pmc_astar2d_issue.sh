@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC issue/latency breakdown of the A* 2D kernel on the C2 batch (tools/astar2d_one.py MODE=batch).
 R=${GRAFT_REPO_ROOT:-/root/repo}
-OUT=$R/gpurun_out/pmc_issue
+OUT=${OUT:-$R/gpurun_out/pmc_issue}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 S1="SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_IFETCH SQ_IFETCH_LEVEL SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INST_LEVEL_VMEM"
