@@ -129,7 +129,7 @@ __device__ __forceinline__ double max16(double t)
 
 // Minv = (H + sigma I + rho A'A)^-1, row v in this lane (rows/cols >= n are the identity).
 // A'A[2k+c][2k'+c'] = [c == c'] (m - max(k, k')) + [2k+c == 2k'+c'].
-__device__ __forceinline__ void build_inverse(const double (&Hrow)[16], int v, int n, int m, double sigma, double rho,
+__device__ __forceinline__ void build_inverse(const double* Hrow, int v, int n, int m, double sigma, double rho,
                                               double (&Inv)[16])
 {
     double Mr[16];
@@ -138,7 +138,7 @@ __device__ __forceinline__ void build_inverse(const double (&Hrow)[16], int v, i
         const bool act = v < n && c < n;
         const int kv = v >> 1, kc = c >> 1;
         const double t = ((v & 1) == (c & 1)) ? (double)(m - (kv > kc ? kv : kc)) : 0.0;
-        double val = Hrow[c] + rho * (t + (c == v ? 1.0 : 0.0)) + (c == v ? sigma : 0.0);
+        double val = (act ? Hrow[c] : 0.0) + rho * (t + (c == v ? 1.0 : 0.0)) + (c == v ? sigma : 0.0);
         Mr[c] = act ? val : (c == v ? 1.0 : 0.0);
         Inv[c] = c == v ? 1.0 : 0.0;
     }
@@ -242,10 +242,9 @@ __device__ MpcResult mpc_control_wave(const double* s, const double* sd, const d
         qplu[v] = l1; qplu[n + v] = l2;
         qplu[2 * n + v] = h1; qplu[3 * n + v] = h2;
     }
-    double Hrow[16];
-#pragma unroll
-    for (int c = 0; c < 16; c++) Hrow[c] = act && c < n ? Hs[v * 16 + c] : 0.0;
-    __syncthreads();  // Hs is reused by the caller
+    // this lane's row of H stays in LDS through the ADMM (read by the inverse builds and the residual
+    // checks): 32 fewer live VGPRs than a register copy, so the tracking kernel fits 2 waves per SIMD
+    const double* Hrow = Hs + 16 * (v & 15);
 
     // ---- ADMM ----
     double rho = M.rho;
@@ -284,7 +283,7 @@ __device__ MpcResult mpc_control_wave(const double* s, const double* sd, const d
         const double ax1 = prefix16(x, v), ax2 = x;
         double hx = 0.0;
 #pragma unroll
-        for (int c = 0; c < 16; c++) hx += Hrow[c] * rl_f64(x, c);
+        for (int c = 0; c < 16; c++) hx += (act && c < n ? Hrow[c] : 0.0) * rl_f64(x, c);
         const double aty = suffix16(y1, v) + y2;
         const double prim = max16(act ? fmax(fabs(ax1 - z1), fabs(ax2 - z2)) : 0.0);
         const double dual = max16(act ? fabs((hx + gv) + aty) : 0.0);
@@ -303,6 +302,7 @@ __device__ MpcResult mpc_control_wave(const double* s, const double* sd, const d
             }
         }
     }
+    __syncthreads();  // Hs is reused by the caller
     if (duo && act) duo[v] = x;
     const double du0 = rl_f64(x, 0), du1 = rl_f64(x, 1);
     const double uu0 = (du0 + p0) + ur[0], uu1 = (du1 + p1) + ur[1];
