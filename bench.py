@@ -387,7 +387,7 @@ def astar3d_leg(args, torch, dist, world, rank):
     lanes = []
     for _ in range(max(1, args.a3_streams)):
         ctx = L.pmp_create(torch.cuda.current_device())
-        _lib.check(ctx, L.pmp_graph3d_set_workers(ctx, args.a3_workers_per_cu), "workers")
+        _lib.check(ctx, L.pmp_set_workers_per_cu(ctx, args.a3_workers_per_cu), "workers")
         lanes.append(dict(ctx=ctx, stream=torch.cuda.Stream(),
                           cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
                           plen=torch.empty(nq, dtype=torch.int32, device="cuda"),
@@ -676,21 +676,62 @@ def dstar_leg(args, torch, dist, world, rank):
     10 % random obstacles, boundary walls, start/goal pairs from the largest free component, at 256^2
     and 512^2 (SURVEY.md §6 measured the reference there).  One timed step = one launch over the
     rank's queries."""
-    from python_motion_planning_amd import batch, workloads as wl
+    from python_motion_planning_amd import _lib, batch, shard, workloads as wl
 
+    L = _lib.load_library()
     out = {}
     for W, nq in ((256, args.dstar_queries), (512, args.dstar_queries)):
         occ, s, g = wl.c2_workload(nq=nq, W=W, H=W, density=0.1, grid_seed=4, pair_seed=5 + rank)
         s_d, g_d = torch.as_tensor(s, device="cuda"), torch.as_tensor(g, device="cuda")
+        bits = batch.occ_bits_device(occ, torch)
+        # batches in flight (own stream + pmp_ctx each): one wave per query, so a launch lasts as long
+        # as its longest query and the next launch's workers fill the CUs the finished ones free
+        lanes = []
+        for _ in range(max(1, args.dstar_streams)):
+            lanes.append(dict(ctx=L.pmp_create(torch.cuda.current_device()), stream=torch.cuda.Stream(),
+                              cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
+                              plen=torch.empty(nq, dtype=torch.int32, device="cuda"),
+                              path=torch.empty((nq, 4 * W), dtype=torch.int32, device="cuda"),
+                              npr=torch.empty(nq, dtype=torch.int64, device="cuda"),
+                              st=torch.empty(nq, dtype=torch.int32, device="cuda")))
 
         def run(i):
-            return batch.dstar2d_batch(occ, s_d, g_d, path_cap=4 * W)
+            b = lanes[i % len(lanes)]
+            rc = L.pmp_dstar2d_batch(b["ctx"], b["stream"].cuda_stream, bits.data_ptr(), W, W, s_d.data_ptr(),
+                                     g_d.data_ptr(), nq, b["cost"].data_ptr(), b["plen"].data_ptr(), b["path"].data_ptr(),
+                                     4 * W, b["npr"].data_ptr(), b["st"].data_ptr(), 0)
+            if rc:
+                _lib.check(b["ctx"], rc, "pmp_dstar2d_batch")
 
-        r = run(0)
+        for i in range(len(lanes)):
+            run(i)
         torch.cuda.synchronize()
+        r = {"cost": lanes[0]["cost"], "n_process": lanes[0]["npr"], "status": lanes[0]["st"]}
+        for b in lanes[1:]:
+            assert torch.equal(b["cost"], r["cost"]) and torch.equal(b["npr"], r["n_process"])
         npr = r["n_process"].cpu().numpy()
         st = r["status"].cpu().numpy()
-        elapsed, kern_ms = timed(torch, dist, run, args.dstar_steps)
+        shard.barrier(dist)
+        torch.cuda.synchronize()
+        evs = []
+        t0 = time.perf_counter()
+        for i in range(args.dstar_steps):
+            b = lanes[i % len(lanes)]
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(b["stream"])
+            run(i)
+            e1.record(b["stream"])
+            evs.append((e0, e1))
+        torch.cuda.synchronize()
+        shard.barrier(dist)
+        elapsed = time.perf_counter() - t0
+        kern_ms = float(np.mean([a.elapsed_time(e) for a, e in evs]))
+        elapsed, kern_ms = shard.max_over_ranks(dist, [elapsed, kern_ms], "cuda")
+        r = {k: v.clone() for k, v in r.items()}
+        torch.cuda.synchronize()
+        for b in lanes:
+            L.pmp_destroy(b["ctx"])
+        lanes.clear()
         # algorithmic bytes per processState: the 3x3 block of cell states (h, k f64 + tag / parent:
         # 24 B each) read + ~2 OPEN entries (16 B) inserted / removed
         alg = float(npr.sum()) * (9 * 24 + 2 * 16)
@@ -714,7 +755,7 @@ def dstar_leg(args, torch, dist, world, rank):
             "metric": f"DStar plans/sec on a {W}x{W} grid (10% obstacles, {nq} random start/goal pairs)",
             "value": nq * args.dstar_steps * world / elapsed, "unit": "plans/s", "queries_per_gpu": nq,
             "steps": args.dstar_steps, "ms_per_step": elapsed / args.dstar_steps * 1e3, "kernel_ms_per_launch": kern_ms,
-            "dtype": "f64",
+            "dtype": "f64", "streams": args.dstar_streams,
             "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                       "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                                       "algorithmic_bytes_per_launch": alg,
@@ -987,7 +1028,8 @@ def main():
     ap.add_argument("--dyn3d-queries", type=int, default=8192, help="C5 queries per DStar3D / LPAStar3D launch")
     ap.add_argument("--dyn3d-steps", type=int, default=2)
     ap.add_argument("--dstar-queries", type=int, default=1024, help="queries per D* launch (256^2 and 512^2 grids)")
-    ap.add_argument("--dstar-steps", type=int, default=1)
+    ap.add_argument("--dstar-steps", type=int, default=6)
+    ap.add_argument("--dstar-streams", type=int, default=3, help="D* batches in flight (own stream + context each)")
     ap.add_argument("--theta-queries", type=int, default=4096, help="C2 queries per Theta* / Lazy Theta* 2D launch")
     ap.add_argument("--lpa-queries", type=int, default=16384,
                     help="README-grid queries per LPA* / D* Lite launch (4 per worker wave: the queue balances the tail)")

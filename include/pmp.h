@@ -459,12 +459,14 @@ int pmp_astar2d_set_schedule(pmp_ctx* ctx, int longest_first);
  * Default 64; 0 switches it off.  Results are identical for any value. */
 int pmp_astar2d_set_priority(pmp_ctx* ctx, int n_high);
 
-/* 3D planners (pmp_graph3d_batch): persistent workers (one wave each) per CU; 0 = the default (16),
- * capped at ceil(nq / 256) so a small batch gets fewer workers with a larger LDS share each.
- * Fewer workers leave each a larger LDS share of its heap (fewer spilled positions), more workers
- * hide more latency.  The longest-first schedule and its raised priority (pmp_astar2d_set_schedule,
- * pmp_astar2d_set_priority) apply to the 3D planners as well.  Results are identical for any value. */
-int pmp_graph3d_set_workers(pmp_ctx* ctx, int per_cu);
+/* Persistent workers (one wave each) per CU of the one-wave-per-query planners: pmp_graph3d_batch
+ * (default 16) and pmp_dstar2d_batch / pmp_dstar2d_onpress_batch (default 8); 0 = the default.
+ * Each launch caps it at ceil(nq / 256), so a small batch gets fewer workers with a larger LDS share
+ * each.  Fewer workers leave each a larger LDS share of its heap (fewer spilled positions), more
+ * workers hide more latency.  The longest-first schedule and its raised priority
+ * (pmp_astar2d_set_schedule, pmp_astar2d_set_priority) apply to these planners as well.  Results are
+ * identical for any value. */
+int pmp_set_workers_per_cu(pmp_ctx* ctx, int per_cu);
 
 /* Pre-size the A* scratch (heap of heap_cap entries per concurrent query, up to max_slots
  * concurrent queries) so that later batch calls allocate nothing (hipGraph-capturable). */

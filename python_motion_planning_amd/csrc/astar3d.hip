@@ -518,7 +518,7 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     // workers per CU: the configured count (default 16: C5's 8192-query batches run fastest at 16-24,
     // tools/astar3d_sweep.py), but no more than the batch fills, so small batches get a larger LDS
     // heap share per worker
-    const int per_cu = std::max(1, std::min(ctx->a3_per_cu > 0 ? ctx->a3_per_cu : 16, (nq + 255) / 256));
+    const int per_cu = std::max(1, std::min(ctx->workers_per_cu > 0 ? ctx->workers_per_cu : 16, (nq + 255) / 256));
     int workers = 256 * per_cu;
     if (workers > nq) workers = nq;
     const size_t words = (ncell + 31) / 32;

@@ -15,6 +15,7 @@
 // processState (:158-218) runs on one wave: lanes 0..7 are the 8 motions (env.py:52-55) in order,
 // the RAISE scan is a scalar loop, the LOWER/else decisions are per lane, and appended entries
 // take their positions by lane-order prefix counts, exactly the reference's append order.
+#include <algorithm>
 #include "heap16.h"
 
 namespace {
@@ -539,14 +540,14 @@ extern "C" int pmp_dstar2d_onpress_batch(pmp_ctx* ctx, void* stream, const uint3
     const size_t hc = 4 * ncell + 64;
     const int heap_cap = (int)(hc > (size_t)(1 << 26) ? (size_t)(1 << 26) : hc);
     const int entry_cap = heap_cap;
-    const int per_cu = 4;
+    const int per_cu = std::max(1, std::min(ctx->workers_per_cu > 0 ? ctx->workers_per_cu : 8, (nq + 255) / 256));
     int lds_cap = (((160 * 1024) / per_cu - 256) / 16) & ~15;
     if (lds_cap > heap_cap) lds_cap = (heap_cap + 15) & ~15;
     const size_t spill_n = heap_cap > lds_cap ? (size_t)(heap_cap - lds_cap) : 0;
     const size_t per_worker = (ncell + 1) * sizeof(DCell) + (size_t)entry_cap * 4 + spill_n * 16 + 4096 +
                               (npress > 0 ? words * 4 : 0);
     int workers = 256 * per_cu;
-    const size_t max_workers = ((size_t)16 << 30) / per_worker;  // keep the scratch under 16 GiB
+    const size_t max_workers = ((size_t)48 << 30) / per_worker;  // keep the scratch under 48 GiB
     if ((size_t)workers > max_workers) workers = (int)(max_workers > 0 ? max_workers : 1);
     if (workers > nq) workers = nq;
     uint4* spill = (uint4*)pmp_scratch(ctx, SCR_AUX1, (size_t)workers * spill_n * 16 + 16);

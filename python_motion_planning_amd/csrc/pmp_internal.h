@@ -17,8 +17,8 @@ struct pmp_ctx {
     int astar_lpt = 1;
     // longest-first only: how many of the first (longest) queries run at raised wave priority
     int astar_prio_n = 64;
-    // 3D planners (pmp_graph3d_batch): persistent workers per CU (0 = the default, 4)
-    int a3_per_cu = 0;
+    // one-wave-per-query planners (3D A* family, D*): persistent workers per CU (0 = each one's default)
+    int workers_per_cu = 0;
     // grow-only scratch arena, one buffer per use
     void* buf[11] = {nullptr};
     size_t cap[11] = {0};

@@ -1,4 +1,4 @@
-"""Dev probe: C5 3D A* throughput vs persistent workers per CU (pmp_graph3d_set_workers) and batches
+"""Dev probe: C5 3D A* throughput vs persistent workers per CU (pmp_set_workers_per_cu) and batches
 in flight (one stream + context each), checked against the first configuration's costs."""
 import os
 import sys
@@ -25,7 +25,7 @@ for pc in [int(x) for x in os.environ.get("PER_CU", "4,8,16").split(",")]:
         lanes = []
         for _ in range(S):
             ctx = L.pmp_create(0)
-            _lib.check(ctx, L.pmp_graph3d_set_workers(ctx, pc), "workers")
+            _lib.check(ctx, L.pmp_set_workers_per_cu(ctx, pc), "workers")
             lanes.append(dict(ctx=ctx, st=torch.cuda.Stream(), cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
                               plen=torch.empty(nq, dtype=torch.int32, device="cuda"),
                               path=torch.empty((nq, cap), dtype=torch.int32, device="cuda"),
