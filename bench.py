@@ -549,21 +549,66 @@ def graphs_leg(args, torch, dist, world, rank):
     LazyThetaStar 2D on C2 queries (1024^2 grid, astar2d.hip THETA = 1 / 2), and LPAStar / DStarLite
     on README-grid queries (lpa.hip).  Each: plans/s over `--graph-steps` launches, HIP-event kernel
     time, and the oracle (C restatement, OpenMP or a loop) timed on a bounded sample beside it."""
-    from python_motion_planning_amd import batch, workloads as wl
+    from python_motion_planning_amd import _lib, batch, shard, workloads as wl
 
+    L = _lib.load_library()
     out = {}
     occ2, s2, g2 = wl.c2_workload(4096, pair_seed=1 + rank)
     nq = args.theta_queries
     s2, g2 = s2[:nq], g2[:nq]
     occ_bits = batch.occ_bits_device(occ2, torch)
+    s2d, g2d = torch.as_tensor(s2, device="cuda"), torch.as_tensor(g2, device="cuda")
     for algo in ("theta_star", "lazy_theta_star"):
-        def run(i, algo=algo, counters=False):
-            return batch.astar2d_batch((1024, 1024), s2, g2, path_cap=8192, occ_bits=occ_bits, counters=counters,
-                                       algo=algo, retry_overflow=False, reserve_slots=args.workers)
-        r = run(0, counters=True)
+        # batches in flight as in the headline (own stream + pmp_ctx each)
+        lanes = []
+        for _ in range(max(1, args.theta_streams)):
+            ctx = L.pmp_create(torch.cuda.current_device())
+            _lib.check(ctx, L.pmp_astar2d_reserve(ctx, 1024, 1024, args.workers, 0), "reserve")
+            lanes.append(dict(ctx=ctx, stream=torch.cuda.Stream(),
+                              cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
+                              plen=torch.empty(nq, dtype=torch.int32, device="cuda"),
+                              path=torch.empty((nq, 8192), dtype=torch.int32, device="cuda"),
+                              nexp=torch.empty(nq, dtype=torch.int32, device="cuda"),
+                              st=torch.empty(nq, dtype=torch.int32, device="cuda")))
+        ctr = torch.empty((nq, 4), dtype=torch.int64, device="cuda")
+
+        def run(i, algo=algo, counters=None):
+            b = lanes[i % len(lanes)]
+            rc = L.pmp_graph2d_batch(b["ctx"], b["stream"].cuda_stream, _lib.ALGOS[algo], occ_bits.data_ptr(), 1024, 1024,
+                                     0, s2d.data_ptr(), g2d.data_ptr(), nq, b["cost"].data_ptr(), b["plen"].data_ptr(),
+                                     b["path"].data_ptr(), 8192, b["nexp"].data_ptr(), None, 0, counters,
+                                     b["st"].data_ptr())
+            if rc:
+                _lib.check(b["ctx"], rc, "pmp_graph2d_batch")
+
+        run(0, counters=ctr.data_ptr())
+        for i in range(1, len(lanes)):
+            run(i)
         torch.cuda.synchronize()
-        c = r["counters"].cpu().numpy()
-        elapsed, kern_ms = timed(torch, dist, run, args.graph_steps)
+        r = {"cost": lanes[0]["cost"].clone(), "status": lanes[0]["st"].clone()}
+        assert (r["status"] == 0).all(), f"unexpected {algo} statuses"
+        for b in lanes[1:]:
+            assert torch.equal(b["cost"], r["cost"])
+        c = ctr.cpu().numpy()
+        shard.barrier(dist)
+        torch.cuda.synchronize()
+        evs = []
+        t0 = time.perf_counter()
+        for i in range(args.graph_steps):
+            b = lanes[i % len(lanes)]
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(b["stream"])
+            run(i)
+            e1.record(b["stream"])
+            evs.append((e0, e1))
+        torch.cuda.synchronize()
+        shard.barrier(dist)
+        elapsed = time.perf_counter() - t0
+        kern_ms = float(np.mean([a.elapsed_time(e) for a, e in evs]))
+        elapsed, kern_ms = shard.max_over_ranks(dist, [elapsed, kern_ms], "cuda")
+        for b in lanes:  # their scratch (about 40 GB each with the Theta* parents) is not needed later
+            L.pmp_destroy(b["ctx"])
+        lanes.clear()
         alg = astar_algorithmic_bytes(c)
         achieved = alg / (kern_ms * 1e-3) / 1e9
         cpu = None
@@ -580,7 +625,7 @@ def graphs_leg(args, torch, dist, world, rank):
                              f"queries, {dt:.1f} s wall"}
         out[algo + "_2d"] = {
             "metric": f"{algo} 2D plans/sec on the C2 1024^2 grid", "value": nq * args.graph_steps * world / elapsed,
-            "unit": "plans/s", "queries_per_gpu": nq, "steps": args.graph_steps,
+            "unit": "plans/s", "queries_per_gpu": nq, "steps": args.graph_steps, "streams": args.theta_streams,
             "ms_per_step": elapsed / args.graph_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": alg,
@@ -774,7 +819,7 @@ def dyn3d_leg(args, torch, dist, world, rank):
     (lpa_star3d.py:78-124, lpa3d.hip), each as plan() alone and as a replanning session (plan() + 2
     dynamic-obstacle calls: DStar3D.apply_dynamic_obstacles of 2 voxels, LPAStar3D.apply_change
     blocking a voxel).  One timed step = one launch over the rank's queries."""
-    from python_motion_planning_amd import batch, workloads as wl
+    from python_motion_planning_amd import batch, shard, workloads as wl
 
     nq = args.dyn3d_queries
     occ, s, g = wl.c5_workload(nq, first_seed=rank * nq)
@@ -783,21 +828,45 @@ def dyn3d_leg(args, torch, dist, world, rank):
     inner = rng.integers(1, [X - 1, Y - 1, Z - 1], size=(nq, 2, 2, 3)).astype(np.int32)
     changes = np.concatenate([inner[:, :, 0, :], np.ones((nq, 2, 1), np.int32)], axis=2)
     s_d, g_d = torch.as_tensor(s, device="cuda"), torch.as_tensor(g, device="cuda")
+    # the grids packed once (device words), outside the timed region
+    bits = torch.as_tensor(np.ascontiguousarray(np.stack([batch.pack_bits(o) for o in occ])).view(np.int32),
+                           device="cuda")
+    # batches in flight: consecutive launches on different streams (the per-stream contexts of
+    # _lib.context), so the next launch's workers fill the CUs the finished ones free
+    streams = [torch.cuda.Stream() for _ in range(max(1, args.dyn3d_streams))]
     out = {}
     for kind, rounds in (("dstar3d", None), ("dstar3d", inner), ("lpastar3d", None), ("lpastar3d", changes)):
         rd = None if rounds is None else torch.as_tensor(rounds, device="cuda")
 
         def run(i, kind=kind, rd=rd):
-            if kind == "dstar3d":
-                return batch.dstar3d_batch(occ, s_d, g_d, rd, path_cap=X * Y * Z + 1)
-            return batch.lpastar3d_batch(occ, s_d, g_d, rd, path_cap=X * Y * Z + 1)
+            with torch.cuda.stream(streams[i % len(streams)]):
+                if kind == "dstar3d":
+                    return batch.dstar3d_batch(occ.shape, s_d, g_d, rd, path_cap=X * Y * Z + 1, occ_bits=bits)
+                return batch.lpastar3d_batch(occ.shape, s_d, g_d, rd, path_cap=X * Y * Z + 1, occ_bits=bits)
 
         r = run(0)
+        for i in range(1, len(streams)):
+            run(i)
         torch.cuda.synchronize()
         nkey = "n_process" if kind == "dstar3d" else "n_expanded"
         nexp = r[nkey].cpu().numpy()
         st = r["status"].cpu().numpy()
-        elapsed, kern_ms = timed(torch, dist, run, args.dyn3d_steps)
+        shard.barrier(dist)
+        torch.cuda.synchronize()
+        evs = []
+        t0 = time.perf_counter()
+        for i in range(args.dyn3d_steps):
+            sm = streams[i % len(streams)]
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(sm)
+            run(i)
+            e1.record(sm)
+            evs.append((e0, e1))
+        torch.cuda.synchronize()
+        shard.barrier(dist)
+        elapsed = time.perf_counter() - t0
+        kern_ms = float(np.mean([a.elapsed_time(e) for a, e in evs]))
+        elapsed, kern_ms = shard.max_over_ranks(dist, [elapsed, kern_ms], "cuda")
         R = 1 if rounds is None else rounds.shape[1] + 1
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -907,7 +976,7 @@ def track_leg(args, torch, dist, world, rank, kind):
     running `iters` plan iterations of every agent (MPC at p = 30, m = 8, ADMM to 1e-9)."""
     from python_motion_planning_amd import _lib, batch, local_planner, workloads as wl
 
-    na, iters = args.agents, args.track_iters
+    na, iters = args.track_agents, args.track_iters
     occ, states, goals = wl.c4_workload(na, seed=2 + rank)
     r = batch.astar2d_batch(occ, states[:, :2].astype(np.int32), np.tile([45, 25], (na, 1)).astype(np.int32),
                             path_cap=2048)
@@ -966,7 +1035,8 @@ def track_leg(args, torch, dist, world, rank, kind):
     return {"metric": f"{name} tracking agent-steps/sec", "value": stepped * args.track_steps * world / elapsed,
             "unit": "agent-steps/s", "agents_per_gpu": na, "iterations_per_launch": iters, "steps": args.track_steps,
             "ms_per_step": elapsed / args.track_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
-            "config": {"workload": f"C4 agents on the README grid, {iters} LQR/MPC plan iterations per launch"},
+            "config": {"workload": f"C4 agents on the README grid ({na} per launch), {iters} LQR/MPC plan iterations "
+                                   f"per launch"},
             "roofline": with_mfma(with_traffic({"bound": "fp64-valu", "achieved": achieved_tf, "peak": 78.6,
                                                 "unit": "TFLOP/s", "frac": achieved_tf / 78.6, "traffic": None},
                                                "track_kernel_lqr" if kind == "lqr" else "track_kernel_mpc"),
@@ -1026,14 +1096,16 @@ def main():
                     help="secondary legs to run (comma list of dwa, rrt, astar3d, totp (C5 trajectories on the "
                          "astar3d leg's paths), lqr, mpc, graphs, dstar, dyn3d, latency; 'none' for none)")
     ap.add_argument("--dyn3d-queries", type=int, default=8192, help="C5 queries per DStar3D / LPAStar3D launch")
-    ap.add_argument("--dyn3d-steps", type=int, default=2)
+    ap.add_argument("--dyn3d-steps", type=int, default=8)
+    ap.add_argument("--dyn3d-streams", type=int, default=4, help="DStar3D / LPAStar3D batches in flight")
     ap.add_argument("--dstar-queries", type=int, default=1024, help="queries per D* launch (256^2 and 512^2 grids)")
     ap.add_argument("--dstar-steps", type=int, default=6)
+    ap.add_argument("--theta-streams", type=int, default=3, help="Theta* 2D batches in flight (own stream + context each)")
     ap.add_argument("--dstar-streams", type=int, default=3, help="D* batches in flight (own stream + context each)")
     ap.add_argument("--theta-queries", type=int, default=4096, help="C2 queries per Theta* / Lazy Theta* 2D launch")
     ap.add_argument("--lpa-queries", type=int, default=16384,
                     help="README-grid queries per LPA* / D* Lite launch (4 per worker wave: the queue balances the tail)")
-    ap.add_argument("--graph-steps", type=int, default=2)
+    ap.add_argument("--graph-steps", type=int, default=6)
     ap.add_argument("--rrt-queries", type=int, default=256)
     ap.add_argument("--rrt-samples", type=int, default=65536)
     ap.add_argument("--rrt-steps", type=int, default=4)
@@ -1043,6 +1115,8 @@ def main():
     ap.add_argument("--a3-steps", type=int, default=32)
     ap.add_argument("--a3-streams", type=int, default=4, help="3D A* batches in flight (own stream + context each)")
     ap.add_argument("--a3-workers-per-cu", type=int, default=16, help="3D A* persistent workers per CU")
+    ap.add_argument("--track-agents", type=int, default=2048,
+                    help="agents per LQR / MPC tracking launch (one wave each; C4's 256 leave 3 of 4 SIMDs idle)")
     ap.add_argument("--track-iters", type=int, default=20)
     ap.add_argument("--track-steps", type=int, default=5)
     ap.add_argument("--schedule", choices=["lpt", "input"], default="lpt",

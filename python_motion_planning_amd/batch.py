@@ -484,22 +484,19 @@ def astar3d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: in
 
 
 def dstar3d_batch(occ, starts, goals, blocks=None, path_cap: int | None = None, expand_cap: int = 0,
-                  max_process: int = 0):
+                  max_process: int = 0, occ_bits=None):
     """Batched DStar3D (d_star3d.py:60-281): plan() and then one apply_dynamic_obstacles() per round
     of `blocks` [nq, nrounds, nblk, 3] (int voxels; outside the grid = ignored), on pmp_dstar3d_batch.
 
     occ: uint8 [X, Y, Z] shared grid or [nq, X, Y, Z] per-query grids (numpy).
     Returns dict of device tensors, per round r (0 = plan): cost [nq, R], path_len [nq, R],
     path [nq, R, path_cap] (voxels (x*Y+y)*Z+z, start -> goal), n_process [nq, R] (len(EXPAND)),
-    status [nq, R] (include/pmp.h), optional expand [nq, expand_cap] (plan()'s EXPAND voxels)."""
+    status [nq, R] (include/pmp.h), optional expand [nq, expand_cap] (plan()'s EXPAND voxels).
+    occ_bits: optional device words of `occ` already packed (occ may then be just its shape)."""
     torch = _lib.device_check()
     L = _lib.load_library()
     ctx = _lib.context()
-    occ = np.asarray(occ)
-    per_query = occ.ndim == 4
-    X, Y, Z = occ.shape[-3:]
-    words = np.stack([pack_bits(o) for o in occ]) if per_query else pack_bits(occ)
-    occ_bits = torch.as_tensor(np.ascontiguousarray(words).view(np.int32), device="cuda")
+    occ_bits, per_query, (X, Y, Z) = _occ3d_bits(torch, occ, occ_bits)
     s = _dev(torch, starts, torch.int32).reshape(-1, 3)
     g = _dev(torch, goals, torch.int32).reshape(-1, 3)
     nq = int(s.shape[0])
@@ -526,22 +523,31 @@ def dstar3d_batch(occ, starts, goals, blocks=None, path_cap: int | None = None, 
     return out
 
 
+def _occ3d_bits(torch, occ, occ_bits=None):
+    """(device words, per_query, (X, Y, Z)) of a shared [X, Y, Z] or per-query [nq, X, Y, Z] grid; with
+    occ_bits given, `occ` only supplies the shape."""
+    shape = tuple(occ) if isinstance(occ, tuple) else np.asarray(occ).shape
+    per_query = len(shape) == 4
+    if occ_bits is None:
+        occ = np.asarray(occ)
+        words = np.stack([pack_bits(o) for o in occ]) if per_query else pack_bits(occ)
+        occ_bits = torch.as_tensor(np.ascontiguousarray(words).view(np.int32), device="cuda")
+    return occ_bits, per_query, tuple(int(d) for d in shape[-3:])
+
+
 def lpastar3d_batch(occ, starts, goals, changes=None, heuristic: str = "euclidean", path_cap: int | None = None,
-                    counters: bool = False, max_expansions: int = 0):
+                    counters: bool = False, max_expansions: int = 0, occ_bits=None):
     """Batched LPAStar3D (lpa_star3d.py:40-225): plan() and then one apply_change() per row of
     `changes` [nq, nr, 4] = (x, y, z, mode) with mode 0 = blocked None (toggle), 1 = True, 2 = False,
     on pmp_lpastar3d_batch.  occ: uint8 [X, Y, Z] shared or [nq, X, Y, Z] per-query grids.
     Returns dict of device tensors per call r (0 = plan): cost [nq, R], path_len [nq, R],
     path [nq, R, path_cap] (voxels (x*Y+y)*Z+z, start -> goal), n_expanded [nq, R] (len(EXPAND)),
-    status [nq, R] (include/pmp.h), optional counters [nq, 4]."""
+    status [nq, R] (include/pmp.h), optional counters [nq, 4].
+    occ_bits: optional device words of `occ` already packed (occ may then be just its shape)."""
     torch = _lib.device_check()
     L = _lib.load_library()
     ctx = _lib.context()
-    occ = np.asarray(occ)
-    per_query = occ.ndim == 4
-    X, Y, Z = occ.shape[-3:]
-    words = np.stack([pack_bits(o) for o in occ]) if per_query else pack_bits(occ)
-    occ_bits = torch.as_tensor(np.ascontiguousarray(words).view(np.int32), device="cuda")
+    occ_bits, per_query, (X, Y, Z) = _occ3d_bits(torch, occ, occ_bits)
     s = _dev(torch, starts, torch.int32).reshape(-1, 3)
     g = _dev(torch, goals, torch.int32).reshape(-1, 3)
     nq = int(s.shape[0])

@@ -495,6 +495,23 @@ constexpr size_t kScratchBudget3 = (size_t)32 << 30;
 
 }  // namespace
 
+int pmp_lpt_order3d(pmp_ctx* ctx, hipStream_t s, const int32_t* start_xyz, const int32_t* goal_xyz, int nq, int X,
+                    int Y, int Z, int workers, int32_t** order)
+{
+    *order = nullptr;
+    if (!ctx->astar_lpt || nq <= workers) return PMP_OK;
+    const int nb = (int)ceil(sqrt((double)X * X + (double)Y * Y + (double)Z * Z)) + 1;
+    int* hist = (int*)pmp_scratch(ctx, SCR_PDIR, sizeof(int) * ((size_t)nb + (size_t)nq));
+    if (!hist) return PMP_ENOMEM;
+    int32_t* ord = hist + nb;
+    PMP_HIP_CHECK(ctx, hipMemsetAsync(hist, 0, sizeof(int) * (size_t)nb, s));
+    hipLaunchKernelGGL(lpt3_hist, dim3((nq + 255) / 256), dim3(256), 0, s, start_xyz, goal_xyz, nq, nb, hist);
+    hipLaunchKernelGGL(lpt3_scan, dim3(1), dim3(64), 0, s, nb, hist);
+    hipLaunchKernelGGL(lpt3_scatter, dim3((nq + 255) / 256), dim3(256), 0, s, start_xyz, goal_xyz, nq, nb, hist, ord);
+    *order = ord;
+    return PMP_OK;
+}
+
 extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uint32_t* occ_bits, int per_query, int X,
                                  int Y, int Z, int heuristic, const int32_t* start_xyz, const int32_t* goal_xyz, int nq,
                                  double* cost, int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded,
@@ -554,15 +571,9 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     hipStream_t s = (hipStream_t)stream;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
     int32_t* order = nullptr;
-    if (ctx->astar_lpt && nq > workers) {
-        const int nb = (int)ceil(sqrt((double)X * X + (double)Y * Y + (double)Z * Z)) + 1;
-        int* hist = (int*)pmp_scratch(ctx, SCR_PDIR, sizeof(int) * ((size_t)nb + (size_t)nq));
-        if (!hist) return PMP_ENOMEM;
-        order = hist + nb;
-        PMP_HIP_CHECK(ctx, hipMemsetAsync(hist, 0, sizeof(int) * (size_t)nb, s));
-        hipLaunchKernelGGL(lpt3_hist, dim3((nq + 255) / 256), dim3(256), 0, s, start_xyz, goal_xyz, nq, nb, hist);
-        hipLaunchKernelGGL(lpt3_scan, dim3(1), dim3(64), 0, s, nb, hist);
-        hipLaunchKernelGGL(lpt3_scatter, dim3((nq + 255) / 256), dim3(256), 0, s, start_xyz, goal_xyz, nq, nb, hist, order);
+    {
+        const int rc = pmp_lpt_order3d(ctx, s, start_xyz, goal_xyz, nq, X, Y, Z, workers, &order);
+        if (rc) return rc;
     }
     auto kern = occ_lds ? (theta == 1 ? astar3d_kernel<true, 1> : theta == 2 ? astar3d_kernel<true, 2> : astar3d_kernel<true, 0>)
                         : (theta == 1 ? astar3d_kernel<false, 1> : theta == 2 ? astar3d_kernel<false, 2> : astar3d_kernel<false, 0>);

@@ -363,7 +363,7 @@ __global__ __launch_bounds__(64) void dstar3d_kernel(
     int64_t* __restrict__ nproc_out, int32_t* __restrict__ status_out, int32_t* __restrict__ expand_out, int expand_cap,
     int64_t max_process, int* __restrict__ queue,
     uint4* __restrict__ spill_all, int heap_cap, int lds_cap, DC3* __restrict__ cells_all, uint32_t* __restrict__ occw_all,
-    int words)
+    int words, const int32_t* __restrict__ order, int prio_n)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
@@ -394,8 +394,12 @@ __global__ __launch_bounds__(64) void dstar3d_kernel(
     const int R1 = nrounds + 1;
 
     for (;;) {
-        const int q = next_query(queue, lane);
-        if (q >= nq) break;
+        const int qi = next_query(queue, lane);
+        if (qi >= nq) break;
+        const int q = uni(order ? order[qi] : qi);
+        // longest queries first, at raised priority (they set the launch's tail)
+        if (qi < prio_n) __builtin_amdgcn_s_setprio(3);
+        else __builtin_amdgcn_s_setprio(0);
         const int sx = uni(start_xyz[3 * q]), sy = uni(start_xyz[3 * q + 1]), sz = uni(start_xyz[3 * q + 2]);
         const int gx = uni(goal_xyz[3 * q]), gy = uni(goal_xyz[3 * q + 1]), gz = uni(goal_xyz[3 * q + 2]);
         const bool in = (unsigned)sx < (unsigned)X && (unsigned)sy < (unsigned)Y && (unsigned)sz < (unsigned)Z &&
@@ -566,7 +570,7 @@ extern "C" int pmp_dstar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
     const size_t ncell = (size_t)X * Y * Z;
     const int words = (int)((ncell + 31) / 32);
     const bool lds_occ = words <= kOccLdsWords;
-    const int per_cu = 4;
+    const int per_cu = std::max(1, std::min(ctx->workers_per_cu > 0 ? ctx->workers_per_cu : 4, (nq + 255) / 256));
     const int occ_bytes = lds_occ ? ((words * 4 + 15) & ~15) : 0;
     // heap: one valid element per OPEN voxel plus stale ones; 8 pushes per voxel bound the total
     const size_t hc = std::min<size_t>(8 * (ncell + 1) + 64, (size_t)1 << 26);
@@ -587,10 +591,16 @@ extern "C" int pmp_dstar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
     if (!spill || !cells || !queue || (!lds_occ && !occw)) return PMP_ENOMEM;
     hipStream_t s = (hipStream_t)stream;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
+    int32_t* order = nullptr;
+    {
+        const int rc = pmp_lpt_order3d(ctx, s, start_xyz, goal_xyz, nq, X, Y, Z, workers, &order);
+        if (rc) return rc;
+    }
     auto kern = lds_occ ? dstar3d_kernel<true> : dstar3d_kernel<false>;
     hipLaunchKernelGGL(kern, dim3(workers), dim3(64), (size_t)lds_cap * 16 + occ_bytes, s, occ_bits, per_query, X, Y, Z,
                        start_xyz, goal_xyz, nq, blocks, nrounds, nblk, cost, path_len, path, path_cap, n_process, status,
-                       expand, expand_cap, max_process, queue, spill, heap_cap, lds_cap, cells, occw, words);
+                       expand, expand_cap, max_process, queue, spill, heap_cap, lds_cap, cells, occw, words,
+                       (const int32_t*)order, order ? ctx->astar_prio_n : 0);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }

@@ -22,6 +22,7 @@
 // start == goal: map[goal] overwrites map[start] (:62-63), the start object is detached, and the
 // reference's result is fixed: plan() expands it once and returns (0.0, [goal]); every
 // apply_change then expands nothing.
+#include <algorithm>
 #include "pmp_internal.h"
 
 namespace {
@@ -437,7 +438,8 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
     const int32_t* __restrict__ changes, int nr, double* __restrict__ cost_out, int32_t* __restrict__ plen_out,
     int32_t* __restrict__ path_out, int path_cap, int64_t* __restrict__ nexp_out, int32_t* __restrict__ status_out,
     int64_t* __restrict__ counters, int64_t max_exp, int* __restrict__ queue, double* __restrict__ scr_f64,
-    int32_t* __restrict__ scr_i32, uint32_t* __restrict__ occ_scr, int words, int occ_lds, int ucap)
+    int32_t* __restrict__ scr_i32, uint32_t* __restrict__ occ_scr, int words, int occ_lds, int ucap,
+    const int32_t* __restrict__ order, int prio_n)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
@@ -468,8 +470,12 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
     const int R1 = nr + 1;
 
     for (;;) {
-        const int q = next_query(queue, lane);
-        if (q >= nq) break;
+        const int qi = next_query(queue, lane);
+        if (qi >= nq) break;
+        const int q = uni(order ? order[qi] : qi);
+        // longest queries first, at raised priority (they set the launch's tail)
+        if (qi < prio_n) __builtin_amdgcn_s_setprio(3);
+        else __builtin_amdgcn_s_setprio(0);
         const int sx = uni(start_xyz[3 * q]), sy = uni(start_xyz[3 * q + 1]), sz = uni(start_xyz[3 * q + 2]);
         const int gx = uni(goal_xyz[3 * q]), gy = uni(goal_xyz[3 * q + 1]), gz = uni(goal_xyz[3 * q + 2]);
         const bool in = S.geo.in(sx, sy, sz) && S.geo.in(gx, gy, gz);
@@ -711,7 +717,7 @@ extern "C" int pmp_lpastar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* o
     const int words = (int)((ncell + 31) / 32);
     const bool occ_lds = words <= kOccLdsWords;
     // 8 waves per CU: 20 KiB of LDS each for the g block, U (20 B per entry) and the occupancy
-    const int per_cu = 8;
+    const int per_cu = std::max(1, std::min(ctx->workers_per_cu > 0 ? ctx->workers_per_cu : 8, (nq + 255) / 256));
     const int occ_bytes = occ_lds ? ((words * 4 + 15) & ~15) : 0;
     int ucap = (((160 * 1024) / per_cu - 1024 - occ_bytes) / 20) & ~15;
     if (ucap < 64) ucap = 64;
@@ -731,9 +737,15 @@ extern "C" int pmp_lpastar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* o
     if (!f || !i32 || !occw || !queue) return PMP_ENOMEM;
     hipStream_t s = (hipStream_t)stream;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
+    int32_t* order = nullptr;
+    {
+        const int rc = pmp_lpt_order3d(ctx, s, start_xyz, goal_xyz, nq, X, Y, Z, workers, &order);
+        if (rc) return rc;
+    }
     hipLaunchKernelGGL(lpa3d_kernel, dim3(workers), dim3(64), lds, s, occ_bits, per_query, X, Y, Z, heuristic, start_xyz,
                        goal_xyz, nq, changes, nr, cost, path_len, path, path_cap, n_expanded, status, counters,
-                       max_expansions, queue, f, i32, occw, words, occ_lds ? 1 : 0, ucap);
+                       max_expansions, queue, f, i32, occw, words, occ_lds ? 1 : 0, ucap, (const int32_t*)order,
+                       order ? ctx->astar_prio_n : 0);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }

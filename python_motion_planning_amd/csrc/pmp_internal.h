@@ -31,6 +31,12 @@ int pmp_set_err(pmp_ctx* ctx, int code, const std::string& msg);
 // Ensure scratch buffer `slot` holds at least `bytes`; returns device pointer or nullptr (error set).
 void* pmp_scratch(pmp_ctx* ctx, int slot, size_t bytes);
 
+// Longest-first order of a 3D batch (descending start-goal distance, counting sort on `s`) in the
+// context's SCR_PDIR scratch; *order = nullptr when the schedule is off or every query has its own
+// worker (nq <= workers).  Shared by the one-wave-per-query 3D planners (astar3d.hip).
+int pmp_lpt_order3d(pmp_ctx* ctx, hipStream_t s, const int32_t* start_xyz, const int32_t* goal_xyz, int nq, int X,
+                    int Y, int Z, int workers, int32_t** order);
+
 #define PMP_HIP_CHECK(ctx, call)                                                                     \
     do {                                                                                             \
         hipError_t _e = (call);                                                                      \
