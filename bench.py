@@ -171,9 +171,13 @@ def with_mfma(roof: dict, kernel: str) -> dict:
     return roof
 
 
-def timed(torch, dist, fn, steps, stream=None):
-    """Barrier + sync, run `steps` launches with HIP events around each (on `stream`), barrier +
-    sync; returns (wall seconds, max over ranks; mean event ms per launch)."""
+def timed(torch, dist, fn, steps, stream=None, streams=None):
+    """Barrier + sync, run `steps` launches with HIP events around each (on `stream`; or, with
+    `streams`, launch i runs with streams[i % len] current: batches in flight, each on its own
+    stream and so its own per-stream pmp_ctx), barrier + sync; returns (wall seconds, max over
+    ranks; mean event ms per launch)."""
+    import contextlib
+
     from python_motion_planning_amd import shard
 
     shard.barrier(dist)
@@ -181,16 +185,18 @@ def timed(torch, dist, fn, steps, stream=None):
     evs = []
     t0 = time.perf_counter()
     for i in range(steps):
+        sm = streams[i % len(streams)] if streams else stream
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        if stream is None:
+        if sm is None:
             e0.record()
         else:
-            e0.record(stream)
-        fn(i)
-        if stream is None:
+            e0.record(sm)
+        with (torch.cuda.stream(sm) if streams else contextlib.nullcontext()):
+            fn(i)
+        if sm is None:
             e1.record()
         else:
-            e1.record(stream)
+            e1.record(sm)
         evs.append((e0, e1))
     torch.cuda.synchronize()
     shard.barrier(dist)
@@ -640,13 +646,17 @@ def graphs_leg(args, torch, dist, world, rank):
     sl = free[rng.integers(len(free), size=nl)].astype(np.int32)
     gl = free[rng.integers(len(free), size=nl)].astype(np.int32)
     s_d, g_d = torch.as_tensor(sl, device="cuda"), torch.as_tensor(gl, device="cuda")
+    lpa_streams = [torch.cuda.Stream() for _ in range(max(1, args.lpa_streams))]
     for lite in (False, True):
         def run(i, lite=lite, counters=False):
             return batch.lpastar2d_batch(occ, s_d, g_d, counters=counters, lite=lite)
         r = run(0, counters=True)
+        for sm in lpa_streams:  # each stream's context and scratch, before the timed region
+            with torch.cuda.stream(sm):
+                run(0)
         torch.cuda.synchronize()
         c = r["counters"].cpu().numpy()
-        elapsed, kern_ms = timed(torch, dist, run, args.graph_steps)
+        elapsed, kern_ms = timed(torch, dist, run, args.graph_steps, streams=lpa_streams)
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             from oracle import oracle as O
@@ -685,10 +695,13 @@ def graphs_leg(args, torch, dist, world, rank):
     for lite in (False, True):
         def run(i, lite=lite):
             return batch.lpastar2d_replan_batch(occ, s_d, g_d, t_d, lite=lite)
+        for sm in lpa_streams:
+            with torch.cuda.stream(sm):
+                run(0)
         r = run(0)
         torch.cuda.synchronize()
         ne = r["n_expanded"].cpu().numpy()
-        elapsed, kern_ms = timed(torch, dist, run, args.graph_steps)
+        elapsed, kern_ms = timed(torch, dist, run, args.graph_steps, streams=lpa_streams)
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             from oracle import oracle as O
@@ -1100,6 +1113,7 @@ def main():
     ap.add_argument("--dyn3d-streams", type=int, default=4, help="DStar3D / LPAStar3D batches in flight")
     ap.add_argument("--dstar-queries", type=int, default=1024, help="queries per D* launch (256^2 and 512^2 grids)")
     ap.add_argument("--dstar-steps", type=int, default=6)
+    ap.add_argument("--lpa-streams", type=int, default=3, help="LPA* / D* Lite 2D batches in flight")
     ap.add_argument("--theta-streams", type=int, default=3, help="Theta* 2D batches in flight (own stream + context each)")
     ap.add_argument("--dstar-streams", type=int, default=3, help="D* batches in flight (own stream + context each)")
     ap.add_argument("--theta-queries", type=int, default=4096, help="C2 queries per Theta* / Lazy Theta* 2D launch")
