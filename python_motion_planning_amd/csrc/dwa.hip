@@ -1,5 +1,6 @@
-// Batched DWA control step for gfx950 (local_planner/dwa.py:72-212): one 512-thread workgroup
-// per agent, one lane per (v, w) sample, H-step rollout, obstacle cost from an occupancy stencil,
+// Batched DWA control step for gfx950 (local_planner/dwa.py:72-212): one 768-thread workgroup
+// (12 waves) per agent, one lane per (v, w) sample (the 4096 samples in passes over the threads),
+// H-step rollout, obstacle cost from an occupancy stencil,
 // numpy-exact normalisation and scoring, first-index argmax, Robot.kinematic.
 //
 // Numerics follow the reference operation by operation (-ffp-contract=off):
