@@ -14,6 +14,7 @@ import sys
 
 KERNELS = {  # short name -> regex on the demangled kernel name
     "lpt_hist": r"lpt_hist\(", "lpt_scan": r"lpt_scan\(", "lpt_scatter": r"lpt_scatter\(",
+    "lpt3_hist": r"lpt3_hist\(", "lpt3_scan": r"lpt3_scan\(", "lpt3_scatter": r"lpt3_scatter\(",
     "astar2d_kernel": r"astar2d_kernel<",
     "dwa_kernel": r"dwa_kernel\(",
     "rrt_kernel": r"rrt_kernel<",

@@ -10,9 +10,9 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 700 rocprofv3 --kernel-trace --stats -d $OUT/prof_kt -o run -- python3 $R/bench.py \
     > $OUT/bench_prof.json 2> $OUT/bench_prof.err
 timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE -d $OUT/prof_fetch -o run -- python3 $R/bench.py --no-cpu-baseline \
-    --steps 3 --warmup 1 --rrt-steps 1 --a3-steps 1 --track-steps 1 --control-steps 2 > $OUT/bench_fetch.json 2> $OUT/bench_fetch.err
+    --steps 3 --warmup 1 --rrt-steps 1 --a3-steps 2 --track-steps 1 --control-steps 2 --graph-steps 2 --dstar-steps 2 --dyn3d-steps 2 > $OUT/bench_fetch.json 2> $OUT/bench_fetch.err
 timeout -k 10 500 rocprofv3 --pmc WRITE_SIZE -d $OUT/prof_write -o run -- python3 $R/bench.py --no-cpu-baseline \
-    --steps 3 --warmup 1 --rrt-steps 1 --a3-steps 1 --track-steps 1 --control-steps 2 > $OUT/bench_write.json 2> $OUT/bench_write.err
+    --steps 3 --warmup 1 --rrt-steps 1 --a3-steps 2 --track-steps 1 --control-steps 2 --graph-steps 2 --dstar-steps 2 --dyn3d-steps 2 > $OUT/bench_write.json 2> $OUT/bench_write.err
 # MFMA utilisation of the MPC QP kernel (track_kernel<1>, v_mfma_f64_16x16x4_f64): its own pass
 timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES SQ_BUSY_CYCLES -d $OUT/prof_mfma -o run \
     -- python3 $R/bench.py --no-cpu-baseline --legs mpc --steps 1 --warmup 1 --track-steps 2 \
