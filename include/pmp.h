@@ -460,7 +460,7 @@ int pmp_astar2d_set_schedule(pmp_ctx* ctx, int longest_first);
 int pmp_astar2d_set_priority(pmp_ctx* ctx, int n_high);
 
 /* Persistent workers (one wave each) per CU of the one-wave-per-query planners: pmp_graph3d_batch
- * (default 16) and pmp_dstar2d_batch / pmp_dstar2d_onpress_batch (default 8); 0 = the default.
+ * (default 16) and pmp_dstar2d_batch / pmp_dstar2d_onpress_batch (default 16); 0 = the default.
  * Each launch caps it at ceil(nq / 256), so a small batch gets fewer workers with a larger LDS share
  * each.  Fewer workers leave each a larger LDS share of its heap (fewer spilled positions), more
  * workers hide more latency.  The longest-first schedule and its raised priority
