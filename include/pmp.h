@@ -459,8 +459,9 @@ int pmp_astar2d_set_schedule(pmp_ctx* ctx, int longest_first);
  * Default 64; 0 switches it off.  Results are identical for any value. */
 int pmp_astar2d_set_priority(pmp_ctx* ctx, int n_high);
 
-/* Persistent workers (one wave each) per CU of the one-wave-per-query planners: pmp_graph3d_batch
- * (default 16) and pmp_dstar2d_batch / pmp_dstar2d_onpress_batch (default 16); 0 = the default.
+/* Persistent workers (one wave each) per CU of the one-wave-per-query planners: pmp_graph3d_batch,
+ * pmp_dstar2d_batch / pmp_dstar2d_onpress_batch, pmp_dstar3d_batch and pmp_lpastar3d_batch (default 16
+ * each); 0 = the default.
  * Each launch caps it at ceil(nq / 256), so a small batch gets fewer workers with a larger LDS share
  * each.  Fewer workers leave each a larger LDS share of its heap (fewer spilled positions), more
  * workers hide more latency.  The longest-first schedule and its raised priority

@@ -570,7 +570,7 @@ extern "C" int pmp_dstar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
     const size_t ncell = (size_t)X * Y * Z;
     const int words = (int)((ncell + 31) / 32);
     const bool lds_occ = words <= kOccLdsWords;
-    const int per_cu = std::max(1, std::min(ctx->workers_per_cu > 0 ? ctx->workers_per_cu : 4, (nq + 255) / 256));
+    const int per_cu = std::max(1, std::min(ctx->workers_per_cu > 0 ? ctx->workers_per_cu : 16, (nq + 255) / 256));
     const int occ_bytes = lds_occ ? ((words * 4 + 15) & ~15) : 0;
     // heap: one valid element per OPEN voxel plus stale ones; 8 pushes per voxel bound the total
     const size_t hc = std::min<size_t>(8 * (ncell + 1) + 64, (size_t)1 << 26);

@@ -716,8 +716,9 @@ extern "C" int pmp_lpastar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* o
     const size_t ncell = (size_t)X * Y * Z;
     const int words = (int)((ncell + 31) / 32);
     const bool occ_lds = words <= kOccLdsWords;
-    // 8 waves per CU: 20 KiB of LDS each for the g block, U (20 B per entry) and the occupancy
-    const int per_cu = std::max(1, std::min(ctx->workers_per_cu > 0 ? ctx->workers_per_cu : 8, (nq + 255) / 256));
+    // up to 16 waves per CU (tools/dyn3d_sweep.py): the LDS share of each holds the g block, U (20 B per
+    // entry, the rest spills) and the occupancy
+    const int per_cu = std::max(1, std::min(ctx->workers_per_cu > 0 ? ctx->workers_per_cu : 16, (nq + 255) / 256));
     const int occ_bytes = occ_lds ? ((words * 4 + 15) & ~15) : 0;
     int ucap = (((160 * 1024) / per_cu - 1024 - occ_bytes) / 20) & ~15;
     if (ucap < 64) ucap = 64;
