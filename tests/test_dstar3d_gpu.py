@@ -3,6 +3,7 @@ reference's published CSV rows, replayed reference runs and the oracle (d_star3d
 
 Bar: bit-exact -- every round's cost (inf included), len(EXPAND) and path."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -124,3 +125,23 @@ def test_dstar3d_start_equals_goal_and_off_grid():
     ref = O.dstar3d(occ, s[0], g[0])
     assert int(out["n_process"][0, 0]) == ref["n_process"][0] and float(out["cost"][0, 0]) == ref["cost"][0]
     assert int(out["status"][1, 0]) == 4
+
+
+@pytest.mark.gpu
+def test_dstar3d_longest_first_schedule_full_c5():
+    """All 8192 C5 queries with 1 worker per CU (256 workers): the longest-first order and the
+    raised priority of the longest queries are active; costs and len(EXPAND) equal the oracle's."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import _lib, batch, workloads as wl
+
+    occ, s, g = wl.c5_workload(8192)
+    L, ctx = _lib.load_library(), _lib.context()
+    _lib.check(ctx, L.pmp_set_workers_per_cu(ctx, 1), "workers")
+    try:
+        out = batch.dstar3d_batch(occ, s, g)
+    finally:
+        _lib.check(ctx, L.pmp_set_workers_per_cu(ctx, 0), "workers")
+    ref = O.graph3d_dynamic_batch("dstar3d", occ, s, g, None, nthreads=min(16, os.cpu_count() or 1))
+    cost = out["cost"][:, 0].cpu().numpy()
+    assert np.array_equal(out["n_process"][:, 0].cpu().numpy(), ref["n"][:, 0])
+    assert all(_same(a, b) for a, b in zip(cost, ref["cost"][:, 0]))

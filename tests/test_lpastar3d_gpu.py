@@ -2,6 +2,8 @@
 reference's published CSV rows, replayed reference runs and the oracle (lpa_star3d.py:40-225).
 
 Bar: bit-exact -- every call's cost, len(EXPAND) and path."""
+import os
+
 import numpy as np
 import pytest
 
@@ -108,3 +110,22 @@ def test_lpastar3d_dropin_sequence():
             cost, path, expand = p.apply_change((x, y, zz), None if mode == 0 else mode == 1)
             assert cost == z["cost"][i][r] and len(expand) == z["nexp"][i][r], (i, r)
             assert [enc(t) for t in path] == seg(z["path"], z["path_off"], i * R + r).tolist(), (i, r)
+
+
+@pytest.mark.gpu
+def test_lpastar3d_longest_first_schedule_full_c5():
+    """All 8192 C5 queries with 1 worker per CU (256 workers): the longest-first order and the
+    raised priority of the longest queries are active; costs and len(EXPAND) equal the oracle's."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import _lib, batch, workloads as wl
+
+    occ, s, g = wl.c5_workload(8192)
+    L, ctx = _lib.load_library(), _lib.context()
+    _lib.check(ctx, L.pmp_set_workers_per_cu(ctx, 1), "workers")
+    try:
+        out = batch.lpastar3d_batch(occ, s, g)
+    finally:
+        _lib.check(ctx, L.pmp_set_workers_per_cu(ctx, 0), "workers")
+    ref = O.graph3d_dynamic_batch("lpastar3d", occ, s, g, None, nthreads=min(16, os.cpu_count() or 1))
+    assert np.array_equal(out["n_expanded"][:, 0].cpu().numpy(), ref["n"][:, 0])
+    assert np.array_equal(out["cost"][:, 0].cpu().numpy(), ref["cost"][:, 0])
