@@ -750,6 +750,18 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
 #endif
             if (cls9 & 16u) continue;  // node.current in CLOSED (a_star.py:57-58)
 
+            // The parents of the positions this expansion's pushes can take (n .. n + 7) load in one
+            // round now, under the neighbour computation below, instead of one probe round per push.
+            // Valid while the 8 positions share a depth: a push that sifts up (t >= 1) rewrites only
+            // the ancestors of its position, and of those only its parent is the parent of another
+            // position of the batch (its right sibling's), which is refreshed below.
+            const int n0 = n;
+            const bool pcache = n0 > 0 && (31 - __clz(n0 + 1)) == (31 - __clz(n0 + 8));
+            double pf8 = 0.0;
+            uint32_t pc8 = 0u;
+            Ld<true> pld;
+            if (pcache) pld.issue(hp, lane < 8 ? ((n0 + lane - 1) >> 1) : 0);
+
 
             // CLOSED[node.current] = node (a_star.py:82).  The node's state word was loaded by lane 13
             // and only this wave writes it: store it back now (fire-and-forget, off the critical path).
@@ -874,6 +886,7 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
             const uint32_t ik = hkey<HEUR>(icm);
             const double ifv = ig + h_of_key<HEUR>(ik);
             bool overflow = false;
+            if (pcache) pld.get(pf8, pc8);
             while (vm) {
                 const int m = __ffsll((long long)vm) - 1;
                 vm &= vm - 1;
@@ -881,12 +894,17 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 const double itf = rl_f64(ifv, m);
                 const uint32_t itc = rl_u32(icm, m), itk = rl_u32(ik, m);
                 // CPython's _siftdown stops at once when the item is not less than its parent (73 % of
-                // C2's pushes): probe the parent first, and run the full push only when it moves
+                // C2's pushes): compare with the parent first, and run the full push only when it moves
                 double pf;
                 uint32_t pc;
-                hld<true>(hp, n > 0 ? (n - 1) >> 1 : 0, pf, pc);
-                pf = rl_f64(pf, 0);
-                pc = rl_u32(pc, 0);
+                if (pcache) {
+                    pf = rl_f64(pf8, n - n0);
+                    pc = rl_u32(pc8, n - n0);
+                } else {
+                    hld<true>(hp, n > 0 ? (n - 1) >> 1 : 0, pf, pc);
+                    pf = rl_f64(pf, 0);
+                    pc = rl_u32(pc, 0);
+                }
                 if (n > 0 && !key_lt(itf, itk, pf, hkey<HEUR>(pc))) {
                     // t = 0: heap[n] = item; a right child (n even) sets its parent's bit against its
                     // left sibling heap[n - 1] = last
@@ -902,6 +920,11 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                     double a1f;
                     uint32_t a1c;
                     push_any<HEUR>(hp, n, itf, itc, itk, lastf, lastc, rootf, rootc, lane, t, a1f, a1c);
+                    // a left child's right sibling (the next position) has the same parent, now a1
+                    if (pcache && (n & 1) && lane == n - n0 + 1) {
+                        pf8 = a1f;
+                        pc8 = a1c;
+                    }
                 }
                 n += 1;
                 npush++;
