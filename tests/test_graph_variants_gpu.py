@@ -312,6 +312,37 @@ def test_lpastar_batch_against_oracle(lite):
 
 
 @pytest.mark.parametrize("lite", [False, True])
+def test_lpastar_long_lists(lite):
+    """Lists far longer than the README grid's: 24 queries on a 256^2 grid (10 % obstacles), some
+    with |U| > 496, against the oracle (status, cost, path, len(EXPAND), pushes, max |U|)."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import batch
+
+    rng = np.random.default_rng(12)
+    occ = (rng.random((256, 256)) < 0.1).astype(np.uint8)
+    occ[:, 0] = occ[:, -1] = 1
+    occ[0, :] = occ[-1, :] = 1
+    free = np.argwhere(occ == 0)
+    S = free[rng.integers(len(free), size=24)].astype(np.int32)
+    G = free[rng.integers(len(free), size=24)].astype(np.int32)
+    r = batch.lpastar2d_batch(occ, S, G, counters=True, lite=lite)
+    st, cost = r["status"].cpu().numpy(), r["cost"].cpu().numpy()
+    ne, ctr = r["n_expanded"].cpu().numpy(), r["counters"].cpu().numpy()
+    P, pl = r["path"].cpu().numpy(), r["path_len"].cpu().numpy()
+    long_lists = 0
+    for q in range(len(S)):
+        ref = O.lpastar2d(occ, S[q], G[q], lite=lite)
+        long_lists += ref["max_u"] > 496
+        assert st[q] == ref["status"] and ne[q] == ref["n_expanded"], q
+        assert ctr[q, 0] == ref["n_push"] and ctr[q, 3] == ref["max_u"], q
+        if ref["status"] in (0, 1):
+            assert cost[q] == ref["cost"], q
+        if ref["status"] == 0:
+            assert np.array_equal(P[q, : pl[q]], ref["path_cells"]), q
+    assert long_lists > 0
+
+
+@pytest.mark.parametrize("lite", [False, True])
 def test_lpastar_replan_against_reference_and_oracle(lite):
     """LPA* incremental replanning (pmp_lpastar2d_replan_batch: plan() + OnPress edits, lpa_star.py:101-137)
     vs the reference's replays (tests/golden/lpa_replan.npz), all 60 cases in one launch, then a 256-query
