@@ -14,6 +14,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "liboracle.so")
+# tests/test_oracle_sanitized.py points this at the ASan/UBSan build (make -C oracle san)
+_SAN_PATH = os.environ.get("PMP_ORACLE_LIB")
 _lib = None
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -32,8 +34,11 @@ def build(force: bool = False) -> str:
 def lib():
     global _lib
     if _lib is None:
-        build()
-        L = ctypes.CDLL(_LIB_PATH)
+        if _SAN_PATH:
+            L = ctypes.CDLL(_SAN_PATH)
+        else:
+            build()
+            L = ctypes.CDLL(_LIB_PATH)
         L.oracle_hypot.restype = ctypes.c_double
         L.oracle_hypot.argtypes = [ctypes.c_double, ctypes.c_double]
         L.oracle_hypot_many.restype = None

@@ -55,10 +55,11 @@ def launch_ranks(n: int, argv=None, extra_env=None) -> int:
     return bad[0] if bad else 0
 
 
-def init(backend: str = "nccl"):
-    """Initialise the process group when WORLD_SIZE > 1; returns the torch.distributed module or None."""
+def init(backend: str = "nccl", always: bool = False):
+    """Initialise the process group when WORLD_SIZE > 1 (or at any world size with always=True, which
+    the 1-GPU tests use to drive the RCCL branch); returns the torch.distributed module or None."""
     rank, world, local = env_rank()
-    if world <= 1:
+    if world <= 1 and not always:
         return None
     import torch
     import torch.distributed as dist
