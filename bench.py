@@ -1128,12 +1128,12 @@ def main():
                          "astar3d leg's paths), lqr, mpc, graphs, dstar, dyn3d, latency; 'none' for none)")
     ap.add_argument("--dyn3d-queries", type=int, default=8192, help="C5 queries per DStar3D / LPAStar3D launch")
     ap.add_argument("--dyn3d-steps", type=int, default=8)
-    ap.add_argument("--dyn3d-streams", type=int, default=4, help="DStar3D / LPAStar3D batches in flight")
+    ap.add_argument("--dyn3d-streams", type=int, default=6, help="DStar3D / LPAStar3D batches in flight")
     ap.add_argument("--dstar-queries", type=int, default=4096, help="queries per D* launch (256^2 and 512^2 grids)")
     ap.add_argument("--dstar-steps", type=int, default=4)
     ap.add_argument("--lpa-streams", type=int, default=3, help="LPA* / D* Lite 2D batches in flight")
     ap.add_argument("--theta-streams", type=int, default=3, help="Theta* 2D batches in flight (own stream + context each)")
-    ap.add_argument("--dstar-streams", type=int, default=2, help="D* batches in flight (own stream + context each)")
+    ap.add_argument("--dstar-streams", type=int, default=3, help="D* batches in flight (own stream + context each)")
     ap.add_argument("--theta-queries", type=int, default=4096, help="C2 queries per Theta* / Lazy Theta* 2D launch")
     ap.add_argument("--lpa-queries", type=int, default=16384,
                     help="README-grid queries per LPA* / D* Lite launch (4 per worker wave: the queue balances the tail)")
@@ -1145,7 +1145,7 @@ def main():
     ap.add_argument("--rrt-cpu-sample", type=int, default=16)
     ap.add_argument("--a3-queries", type=int, default=8192)
     ap.add_argument("--a3-steps", type=int, default=32)
-    ap.add_argument("--a3-streams", type=int, default=4, help="3D A* batches in flight (own stream + context each)")
+    ap.add_argument("--a3-streams", type=int, default=6, help="3D A* batches in flight (own stream + context each)")
     ap.add_argument("--a3-workers-per-cu", type=int, default=16, help="3D A* persistent workers per CU")
     ap.add_argument("--track-agents", type=int, default=2048,
                     help="agents per LQR / MPC tracking launch (one wave each; C4's 256 leave 3 of 4 SIMDs idle)")
