@@ -582,7 +582,9 @@ def graphs_leg(args, torch, dist, world, rank):
         lanes = []
         for _ in range(max(1, args.theta_streams)):
             ctx = L.pmp_create(torch.cuda.current_device())
-            _lib.check(ctx, L.pmp_astar2d_reserve(ctx, 1024, 1024, args.workers, 0), "reserve")
+            _lib.check(ctx, L.pmp_astar2d_reserve(ctx, 1024, 1024, args.theta_workers, 0), "reserve")
+            if args.theta_residency:
+                _lib.check(ctx, L.pmp_astar2d_set_residency(ctx, args.theta_residency), "residency")
             lanes.append(dict(ctx=ctx, stream=pool_stream(torch, len(lanes)),
                               cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
                               plen=torch.empty(nq, dtype=torch.int32, device="cuda"),
@@ -1114,7 +1116,7 @@ def dry_run(args, rank, world):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--nq", type=int, default=4096)
     ap.add_argument("--cpu-sample", type=int, default=4096, help="queries in the CPU-baseline sample")
@@ -1122,15 +1124,20 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--agents", type=int, default=256, help="C4 agents per GPU (control-step leg)")
     ap.add_argument("--control-steps", type=int, default=20, help="timed control steps")
-    ap.add_argument("--workers", type=int, default=3072, help="persistent A* workers (waves) per launch")
+    ap.add_argument("--workers", type=int, default=768, help="persistent A* workers (waves) per launch")
+    ap.add_argument("--theta-workers", type=int, default=3072, help="persistent Theta* 2D workers per launch")
+    ap.add_argument("--theta-residency", type=int, default=0, help="Theta* 2D workers resident per CU (as --residency)")
+    ap.add_argument("--residency", type=int, default=18,
+                    help="A* workers resident per CU over all batches in flight (sets each worker's LDS heap "
+                         "share; 0 = one launch's own workers / 256)")
     ap.add_argument("--legs", default="dwa,rrt,astar3d,totp,lqr,mpc,graphs,dstar,dyn3d,latency",
                     help="secondary legs to run (comma list of dwa, rrt, astar3d, totp (C5 trajectories on the "
                          "astar3d leg's paths), lqr, mpc, graphs, dstar, dyn3d, latency; 'none' for none)")
     ap.add_argument("--dyn3d-queries", type=int, default=8192, help="C5 queries per DStar3D / LPAStar3D launch")
-    ap.add_argument("--dyn3d-steps", type=int, default=8)
+    ap.add_argument("--dyn3d-steps", type=int, default=24)
     ap.add_argument("--dyn3d-streams", type=int, default=6, help="DStar3D / LPAStar3D batches in flight")
     ap.add_argument("--dstar-queries", type=int, default=4096, help="queries per D* launch (256^2 and 512^2 grids)")
-    ap.add_argument("--dstar-steps", type=int, default=4)
+    ap.add_argument("--dstar-steps", type=int, default=9)
     ap.add_argument("--lpa-streams", type=int, default=3, help="LPA* / D* Lite 2D batches in flight")
     ap.add_argument("--theta-streams", type=int, default=3, help="Theta* 2D batches in flight (own stream + context each)")
     ap.add_argument("--dstar-streams", type=int, default=3, help="D* batches in flight (own stream + context each)")
@@ -1155,7 +1162,7 @@ def main():
                     help="A* query order across workers: longest start-goal distance first, or input order")
     ap.add_argument("--prio", type=int, default=64,
                     help="longest-first only: the first N (longest) queries of a batch run at raised wave priority")
-    ap.add_argument("--streams", type=int, default=4,
+    ap.add_argument("--streams", type=int, default=6,
                     help="batches in flight: consecutive steps go to different HIP streams (own scratch "
                          "context each), so one batch's long-query tail overlaps the next batch")
     ap.add_argument("--hw-queues", type=int, default=8,
@@ -1216,6 +1223,8 @@ def main():
         _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, args.workers, 0), "reserve")
         _lib.check(ctx, L.pmp_astar2d_set_schedule(ctx, 1 if args.schedule == "lpt" else 0), "schedule")
         _lib.check(ctx, L.pmp_astar2d_set_priority(ctx, args.prio), "priority")
+        if args.residency:
+            _lib.check(ctx, L.pmp_astar2d_set_residency(ctx, args.residency), "residency")
         lanes.append(dict(
             ctx=ctx, stream=pool_stream(torch, len(lanes)),
             cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
@@ -1363,7 +1372,11 @@ def main():
                        "grid": [W, H], "queries_per_gpu": nq, "parallelism": f"query-sharded x{world}"},
             "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                       "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                                      "algorithmic_bytes_per_launch": bytes_per_launch}, "astar2d_kernel"),
+                                      "algorithmic_bytes_per_launch": bytes_per_launch,
+                                      # the batches in flight overlap: bytes of one batch per step interval
+                                      "achieved_aggregate": bytes_per_launch / (elapsed / args.steps) / 1e9,
+                                      "frac_aggregate": bytes_per_launch / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS},
+                                     "astar2d_kernel"),
             "cpu_baseline": cpu,
             "secondary": secondary,
             "detail": {"kernel_ms_per_launch": kern_ms,
@@ -1378,6 +1391,7 @@ def main():
                        "expansions_all_ranks_per_step": int(counters_all[:, 2].sum()) if args.scaling == "strong" else None,
                        "strong_scaling_gather": gathered,
                        "workers": args.workers, "streams": S, "priority_queries": args.prio,
+                       "resident_per_cu": args.residency or (args.workers + 255) // 256,
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
         }
         print(json.dumps(out), flush=True)

@@ -458,6 +458,13 @@ int pmp_astar2d_set_schedule(pmp_ctx* ctx, int longest_first);
  * priority, so they finish sooner and the short queries fill the issue slots they leave idle.
  * Default 64; 0 switches it off.  Results are identical for any value. */
 int pmp_astar2d_set_priority(pmp_ctx* ctx, int n_high);
+/* A* 2D workers resident per CU across all the launches that run at once (default 0 = this
+ * context's own launch alone: ceil(max_slots / 256) of pmp_astar2d_reserve).  The LDS share of each
+ * worker's heap is 160 KiB / per_cu, so several batches in flight with fewer workers each (e.g. 6
+ * contexts x 512 workers) set 12 here to stay resident together: every batch's longest queries then
+ * start at once instead of behind the earlier batches.  Re-sizes the reserved scratch (call after
+ * pmp_astar2d_reserve).  Results are identical for any value. */
+int pmp_astar2d_set_residency(pmp_ctx* ctx, int per_cu);
 
 /* Persistent workers (one wave each) per CU of the one-wave-per-query planners: pmp_graph3d_batch,
  * pmp_dstar2d_batch / pmp_dstar2d_onpress_batch, pmp_dstar3d_batch and pmp_lpastar3d_batch (default 16

@@ -1045,7 +1045,7 @@ extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int workers, int 
         if (fit < 1) return pmp_set_err(ctx, PMP_ENOMEM, "pmp_astar2d_reserve: one worker exceeds the scratch budget");
         if ((size_t)workers > fit) workers = (int)fit;
     }
-    const int per_cu = (workers + 255) / 256;
+    const int per_cu = ctx->astar_resident_per_cu > 0 ? ctx->astar_resident_per_cu : (workers + 255) / 256;
     int lds_cap = default_lds_cap(per_cu < 1 ? 1 : per_cu);
     if (lds_cap > heap_cap) lds_cap = (heap_cap + 15) & ~15;
     const size_t spill = heap_cap > lds_cap ? (size_t)(heap_cap - lds_cap) : 0;
@@ -1060,6 +1060,15 @@ extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int workers, int 
     ctx->astar_heap_cap = heap_cap;
     ctx->astar_lds_cap = lds_cap;
     return PMP_OK;
+}
+
+extern "C" int pmp_astar2d_set_residency(pmp_ctx* ctx, int per_cu)
+{
+    if (!ctx) return PMP_EINVAL;
+    if (per_cu < 0 || per_cu > 32) return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_set_residency: per_cu must be in [0, 32]");
+    ctx->astar_resident_per_cu = per_cu;
+    if (ctx->astar_W == 0) return PMP_OK;  // applied by the next reserve
+    return pmp_astar2d_reserve(ctx, ctx->astar_W, ctx->astar_H, ctx->astar_workers, ctx->astar_heap_cap);
 }
 
 extern "C" int pmp_graph2d_batch(pmp_ctx* ctx, void* stream, int algo, const uint32_t* occ_bits, int W, int H,

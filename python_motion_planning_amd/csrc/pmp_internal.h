@@ -17,6 +17,8 @@ struct pmp_ctx {
     int astar_lpt = 1;
     // longest-first only: how many of the first (longest) queries run at raised wave priority
     int astar_prio_n = 64;
+    // A* 2D workers resident per CU over all concurrent launches (0 = ceil(workers / 256)): sets the LDS heap share
+    int astar_resident_per_cu = 0;
     // one-wave-per-query planners (3D A* family, D*): persistent workers per CU (0 = each one's default)
     int workers_per_cu = 0;
     // grow-only scratch arena, one buffer per use

@@ -187,3 +187,49 @@ def test_heap_above_32767_entries_uses_hbm_bit_tiers():
     assert int(r["n_expanded"][0]) == int(ref["n_expanded"][0])
     assert r["counters"].cpu().numpy()[0].tolist() == ref["counters"][0].tolist()
     batch.astar2d_batch(occ[:64, :64], s, s, path_cap=4, reserve_slots=64, heap_cap=0)  # default sizing again
+
+
+def test_residency_batches_in_flight():
+    """The bench's headline schedule: several contexts, each a smaller persistent-worker launch on
+    its own stream with the LDS heap share of 18 resident workers per CU (pmp_astar2d_set_residency,
+    368 LDS positions, the rest of each heap spilled), all in flight together.  Every batch equals
+    the oracle's CLOSED order / cost / path."""
+    import torch
+
+    from oracle import oracle as O
+    from python_motion_planning_amd import _lib, batch, workloads as wl
+
+    occ, s, g = wl.c2_workload(nq=96, W=256, H=256, pair_seed=21)
+    W, H = occ.shape
+    L = _lib.load_library()
+    bits = batch.occ_bits_device(occ, torch)
+    s_d, g_d = torch.as_tensor(s, device="cuda"), torch.as_tensor(g, device="cuda")
+    nq, pc = len(s), 4096
+    lanes = []
+    for _ in range(3):
+        ctx = L.pmp_create(torch.cuda.current_device())
+        _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, 32, 0), "reserve")
+        _lib.check(ctx, L.pmp_astar2d_set_residency(ctx, 18), "residency")
+        assert L.pmp_astar2d_set_residency(ctx, 33) != 0
+        lanes.append(dict(ctx=ctx, stream=torch.cuda.Stream(),
+                          out=[torch.empty(nq, dtype=torch.float64, device="cuda"),
+                               torch.empty(nq, dtype=torch.int32, device="cuda"),
+                               torch.empty((nq, pc), dtype=torch.int32, device="cuda"),
+                               torch.empty(nq, dtype=torch.int32, device="cuda"),
+                               torch.empty(nq, dtype=torch.int32, device="cuda")]))
+    torch.cuda.synchronize()
+    for b in lanes:
+        c, pl, p, ne, st = b["out"]
+        rc = L.pmp_astar2d_batch(b["ctx"], b["stream"].cuda_stream, bits.data_ptr(), W, H, 0, s_d.data_ptr(),
+                                 g_d.data_ptr(), nq, c.data_ptr(), pl.data_ptr(), p.data_ptr(), pc, ne.data_ptr(),
+                                 None, 0, None, st.data_ptr())
+        _lib.check(b["ctx"], rc, "pmp_astar2d_batch")
+    torch.cuda.synchronize()
+    ref = O.astar2d_batch(occ, s, g, path_cap=pc)
+    for b in lanes:
+        c, pl, p, ne, st = (t.cpu().numpy() for t in b["out"])
+        assert (st == ref["status"]).all()
+        assert (c == ref["cost"]).all() and (ne == ref["n_expanded"]).all() and (pl == ref["path_len"]).all()
+        for q in range(nq):
+            assert (p[q, : pl[q]] == ref["path"][q, : pl[q]]).all()
+        L.pmp_destroy(b["ctx"])
