@@ -29,7 +29,20 @@ KERNELS = {  # short name -> regex on the demangled kernel name
 }
 
 
+# the 2D graph kernel's template <HEUR, GZERO, THETA> (astar2d.hip): one short name per planner, so the
+# headline's traffic is never taken from the Theta* launches of the same kernel template
+_G2D = re.compile(r"astar2d_kernel<(\d+), (true|false), (\d)>")
+
+
 def short(name):
+    m = _G2D.search(name)
+    if m:
+        heur, gzero, theta = int(m.group(1)), m.group(2) == "true", int(m.group(3))
+        if theta:
+            return "theta2d_kernel" if theta == 1 else "lazy_theta2d_kernel"
+        if gzero:
+            return "gbfs2d_kernel"
+        return "dijkstra2d_kernel" if (heur & 3) == 2 else "astar2d_kernel"
     for k, rx in KERNELS.items():
         if re.search(rx, name):
             return k
@@ -38,7 +51,15 @@ def short(name):
 
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
-    db = sqlite3.connect(os.path.join(src, "prof_kt", "run_results.db"))
+    kt = os.path.join(src, "prof_kt", "run_results.db")
+    rows = []
+    if os.path.exists(kt):
+        rows = kernel_stats(kt, dst)
+    traffic_and_mfma(src, dst, rows)
+
+
+def kernel_stats(kt, dst):
+    db = sqlite3.connect(kt)
     # one row per (kernel, grid size): a planner launched with different batch sizes (e.g. the small
     # A* batches that build the control legs' global paths) gets separate statistics
     rows = list(db.execute("select name, grid_x, count(*), sum(duration), avg(duration), min(duration), max(duration) "
@@ -53,10 +74,14 @@ def main(src, dst):
     with open(os.path.join(dst, "astar2d_dispatches.csv"), "w", newline="") as f:
         w = csv.writer(f)
         w.writerow(["dispatch", "grid_threads", "duration_ns"])
-        for i, (g, d) in enumerate(db.execute("select grid_x, duration from kernels where name like '%astar2d_kernel%' "
-                                             "order by start")):
-            w.writerow([i, g, d])
-    rows = [(n, c, t, a, 100.0 * t / tot) for n, g, c, t, a, mn, mx in rows]
+        for i, (n, g, d) in enumerate(db.execute("select name, grid_x, duration from kernels where name like "
+                                                "'%astar2d_kernel%' order by start")):
+            if short(n) == "astar2d_kernel":
+                w.writerow([i, g, d])
+    return [(n, c, t, a, 100.0 * t / tot) for n, g, c, t, a, mn, mx in rows]
+
+
+def traffic_and_mfma(src, dst, rows):
     traffic = {}
     for counter, sub in (("FETCH_SIZE", "prof_fetch"), ("WRITE_SIZE", "prof_write")):
         path = os.path.join(src, sub, "run_results.db")

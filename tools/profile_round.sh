@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-/root/repo}
 OUT=$R/gpurun_out
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 700 rocprofv3 --kernel-trace --stats -d $OUT/prof_kt -o run -- python3 $R/bench.py \
+[ "${SKIP_KT:-0}" = 1 ] || timeout -k 10 700 rocprofv3 --kernel-trace --stats -d $OUT/prof_kt -o run -- python3 $R/bench.py \
     > $OUT/bench_prof.json 2> $OUT/bench_prof.err
 timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE -d $OUT/prof_fetch -o run -- python3 $R/bench.py --no-cpu-baseline \
     --steps 3 --warmup 1 --rrt-steps 1 --a3-steps 2 --track-steps 1 --control-steps 2 --graph-steps 2 --dstar-steps 2 --dyn3d-steps 2 > $OUT/bench_fetch.json 2> $OUT/bench_fetch.err
