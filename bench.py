@@ -407,6 +407,7 @@ def astar3d_leg(args, torch, dist, world, rank):
     for _ in range(max(1, args.a3_streams)):
         ctx = L.pmp_create(torch.cuda.current_device())
         _lib.check(ctx, L.pmp_set_workers_per_cu(ctx, args.a3_workers_per_cu), "workers")
+        _lib.check(ctx, L.pmp_set_resident_per_cu(ctx, args.a3_residency), "residency")
         lanes.append(dict(ctx=ctx, stream=pool_stream(torch, len(lanes)),
                           cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
                           plen=torch.empty(nq, dtype=torch.int32, device="cuda"),
@@ -476,7 +477,7 @@ def astar3d_leg(args, torch, dist, world, rank):
     return {"metric": "3D A* plans/sec, Grid3D(26,20,16) door scenario, 8192 queries", "value": nq * args.a3_steps * world / elapsed,
             "unit": "plans/s", "queries_per_gpu": nq, "steps": args.a3_steps,
             "ms_per_step": elapsed / args.a3_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
-            "streams": len(lanes), "workers_per_cu": args.a3_workers_per_cu,
+            "streams": len(lanes), "workers_per_cu": args.a3_workers_per_cu, "resident_per_cu": args.a3_residency,
             "config": {"workload": "C5: Grid3D(26,20,16) door, random.seed(i) pairs, safety bubbles r=1, euclidean"},
             "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                       "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -761,7 +762,10 @@ def dstar_leg(args, torch, dist, world, rank):
         # as its longest query and the next launch's workers fill the CUs the finished ones free
         lanes = []
         for _ in range(max(1, args.dstar_streams)):
-            lanes.append(dict(ctx=L.pmp_create(torch.cuda.current_device()), stream=pool_stream(torch, len(lanes)),
+            ctx = L.pmp_create(torch.cuda.current_device())
+            _lib.check(ctx, L.pmp_set_workers_per_cu(ctx, args.dstar_workers_per_cu), "workers")
+            _lib.check(ctx, L.pmp_set_resident_per_cu(ctx, args.dstar_residency), "residency")
+            lanes.append(dict(ctx=ctx, stream=pool_stream(torch, len(lanes)),
                               cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
                               plen=torch.empty(nq, dtype=torch.int32, device="cuda"),
                               path=torch.empty((nq, 4 * W), dtype=torch.int32, device="cuda"),
@@ -1154,6 +1158,11 @@ def main():
     ap.add_argument("--a3-steps", type=int, default=32)
     ap.add_argument("--a3-streams", type=int, default=6, help="3D A* batches in flight (own stream + context each)")
     ap.add_argument("--a3-workers-per-cu", type=int, default=16, help="3D A* persistent workers per CU")
+    ap.add_argument("--a3-residency", type=int, default=0,
+                    help="3D A* workers resident per CU over all batches in flight (LDS share; 0 = per launch)")
+    ap.add_argument("--dstar-workers-per-cu", type=int, default=0, help="D* persistent workers per CU (0 = default)")
+    ap.add_argument("--dstar-residency", type=int, default=0,
+                    help="D* workers resident per CU over all batches in flight (LDS share; 0 = per launch)")
     ap.add_argument("--track-agents", type=int, default=2048,
                     help="agents per LQR / MPC tracking launch (one wave each; C4's 256 leave 3 of 4 SIMDs idle)")
     ap.add_argument("--track-iters", type=int, default=20)

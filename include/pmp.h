@@ -475,6 +475,12 @@ int pmp_astar2d_set_residency(pmp_ctx* ctx, int per_cu);
  * (pmp_astar2d_set_schedule, pmp_astar2d_set_priority) apply to these planners as well.  Results are
  * identical for any value. */
 int pmp_set_workers_per_cu(pmp_ctx* ctx, int per_cu);
+/* Workers resident per CU over all the launches that run at once, for pmp_graph3d_batch,
+ * pmp_dstar2d_batch / pmp_dstar2d_onpress_batch and pmp_dstar3d_batch: each worker's LDS heap share
+ * is sized for max(this, the launch's own workers per CU), so several batches in flight with few
+ * workers each stay resident together (as pmp_astar2d_set_residency for A* 2D); 0 = the launch's own
+ * count.  Results are identical for any value. */
+int pmp_set_resident_per_cu(pmp_ctx* ctx, int per_cu);
 
 /* Pre-size the A* scratch (heap of heap_cap entries per concurrent query, up to max_slots
  * concurrent queries) so that later batch calls allocate nothing (hipGraph-capturable). */

@@ -541,7 +541,7 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     const size_t words = (ncell + 31) / 32;
     const bool occ_lds = words <= (size_t)kOccLdsWords;
     const int occ_bytes = occ_lds ? kOccLdsWords * 4 : 0;
-    int lds_cap = (((160 * 1024) / per_cu - 256 - occ_bytes) / 16) & ~15;
+    int lds_cap = (((160 * 1024) / pmp_lds_share(ctx, per_cu) - 256 - occ_bytes) / 16) & ~15;
     size_t hc = 26 * ncell + 8;
     if (hc > (size_t)(1 << 22)) hc = (size_t)1 << 22;
     const int heap_cap = (int)hc;

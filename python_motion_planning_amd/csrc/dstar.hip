@@ -541,7 +541,7 @@ extern "C" int pmp_dstar2d_onpress_batch(pmp_ctx* ctx, void* stream, const uint3
     const int heap_cap = (int)(hc > (size_t)(1 << 26) ? (size_t)(1 << 26) : hc);
     const int entry_cap = heap_cap;
     const int per_cu = std::max(1, std::min(ctx->workers_per_cu > 0 ? ctx->workers_per_cu : 16, (nq + 255) / 256));
-    int lds_cap = (((160 * 1024) / per_cu - 256) / 16) & ~15;
+    int lds_cap = (((160 * 1024) / pmp_lds_share(ctx, per_cu) - 256) / 16) & ~15;
     if (lds_cap > heap_cap) lds_cap = (heap_cap + 15) & ~15;
     const size_t spill_n = heap_cap > lds_cap ? (size_t)(heap_cap - lds_cap) : 0;
     const size_t per_worker = (ncell + 1) * sizeof(DCell) + (size_t)entry_cap * 4 + spill_n * 16 + 4096 +

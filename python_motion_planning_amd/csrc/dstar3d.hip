@@ -575,7 +575,7 @@ extern "C" int pmp_dstar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
     // heap: one valid element per OPEN voxel plus stale ones; 8 pushes per voxel bound the total
     const size_t hc = std::min<size_t>(8 * (ncell + 1) + 64, (size_t)1 << 26);
     const int heap_cap = (int)hc;
-    int lds_cap = (((160 * 1024) / per_cu - 256 - occ_bytes) / 16) & ~15;
+    int lds_cap = (((160 * 1024) / pmp_lds_share(ctx, per_cu) - 256 - occ_bytes) / 16) & ~15;
     if (lds_cap > heap_cap) lds_cap = (heap_cap + 15) & ~15;
     const size_t spill_n = heap_cap > lds_cap ? (size_t)(heap_cap - lds_cap) : 0;
     const size_t per_worker = (ncell + 1) * sizeof(DC3) + spill_n * 16 + (lds_occ ? 0 : (size_t)words * 4) + 256;

@@ -80,6 +80,13 @@ int pmp_astar2d_set_priority(pmp_ctx* ctx, int n_high)
     return PMP_OK;
 }
 
+int pmp_set_resident_per_cu(pmp_ctx* ctx, int per_cu)
+{
+    if (!ctx || per_cu < 0 || per_cu > 32) return PMP_EINVAL;
+    ctx->resident_per_cu = per_cu;
+    return PMP_OK;
+}
+
 int pmp_set_workers_per_cu(pmp_ctx* ctx, int per_cu)
 {
     if (!ctx || per_cu < 0 || per_cu > 32) return PMP_EINVAL;

@@ -21,6 +21,9 @@ struct pmp_ctx {
     int astar_resident_per_cu = 0;
     // one-wave-per-query planners (3D A* family, D*): persistent workers per CU (0 = each one's default)
     int workers_per_cu = 0;
+    // ... and the workers resident per CU over all concurrent launches, which sets their LDS share
+    // (0 = this launch's own workers per CU; pmp_set_resident_per_cu)
+    int resident_per_cu = 0;
     // grow-only scratch arena, one buffer per use
     void* buf[11] = {nullptr};
     size_t cap[11] = {0};
@@ -30,6 +33,8 @@ enum ScratchSlot { SCR_HEAP = 0, SCR_CLOSED = 1, SCR_PDIR = 2, SCR_G = 3, SCR_AU
                    SCR_BITS = 8, SCR_AUX4 = 9, SCR_PAR = 10, SCR_NSLOTS = 11 };
 
 int pmp_set_err(pmp_ctx* ctx, int code, const std::string& msg);
+// Workers per CU whose LDS shares a launch of `per_cu` workers per CU must fit beside
+inline int pmp_lds_share(const pmp_ctx* ctx, int per_cu) { return ctx->resident_per_cu > per_cu ? ctx->resident_per_cu : per_cu; }
 // Ensure scratch buffer `slot` holds at least `bytes`; returns device pointer or nullptr (error set).
 void* pmp_scratch(pmp_ctx* ctx, int slot, size_t bytes);
 
