@@ -1129,8 +1129,8 @@ def main():
     ap.add_argument("--agents", type=int, default=256, help="C4 agents per GPU (control-step leg)")
     ap.add_argument("--control-steps", type=int, default=20, help="timed control steps")
     ap.add_argument("--workers", type=int, default=768, help="persistent A* workers (waves) per launch")
-    ap.add_argument("--theta-workers", type=int, default=3072, help="persistent Theta* 2D workers per launch")
-    ap.add_argument("--theta-residency", type=int, default=0, help="Theta* 2D workers resident per CU (as --residency)")
+    ap.add_argument("--theta-workers", type=int, default=768, help="persistent Theta* 2D workers per launch")
+    ap.add_argument("--theta-residency", type=int, default=18, help="Theta* 2D workers resident per CU (as --residency)")
     ap.add_argument("--residency", type=int, default=18,
                     help="A* workers resident per CU over all batches in flight (sets each worker's LDS heap "
                          "share; 0 = one launch's own workers / 256)")
@@ -1143,12 +1143,12 @@ def main():
     ap.add_argument("--dstar-queries", type=int, default=4096, help="queries per D* launch (256^2 and 512^2 grids)")
     ap.add_argument("--dstar-steps", type=int, default=9)
     ap.add_argument("--lpa-streams", type=int, default=3, help="LPA* / D* Lite 2D batches in flight")
-    ap.add_argument("--theta-streams", type=int, default=3, help="Theta* 2D batches in flight (own stream + context each)")
+    ap.add_argument("--theta-streams", type=int, default=6, help="Theta* 2D batches in flight (own stream + context each)")
     ap.add_argument("--dstar-streams", type=int, default=3, help="D* batches in flight (own stream + context each)")
     ap.add_argument("--theta-queries", type=int, default=4096, help="C2 queries per Theta* / Lazy Theta* 2D launch")
     ap.add_argument("--lpa-queries", type=int, default=16384,
                     help="README-grid queries per LPA* / D* Lite launch (4 per worker wave: the queue balances the tail)")
-    ap.add_argument("--graph-steps", type=int, default=6)
+    ap.add_argument("--graph-steps", type=int, default=12)
     ap.add_argument("--rrt-queries", type=int, default=256)
     ap.add_argument("--rrt-samples", type=int, default=65536)
     ap.add_argument("--rrt-steps", type=int, default=4)
@@ -1157,8 +1157,8 @@ def main():
     ap.add_argument("--a3-queries", type=int, default=8192)
     ap.add_argument("--a3-steps", type=int, default=32)
     ap.add_argument("--a3-streams", type=int, default=6, help="3D A* batches in flight (own stream + context each)")
-    ap.add_argument("--a3-workers-per-cu", type=int, default=16, help="3D A* persistent workers per CU")
-    ap.add_argument("--a3-residency", type=int, default=0,
+    ap.add_argument("--a3-workers-per-cu", type=int, default=4, help="3D A* persistent workers per CU")
+    ap.add_argument("--a3-residency", type=int, default=24,
                     help="3D A* workers resident per CU over all batches in flight (LDS share; 0 = per launch)")
     ap.add_argument("--dstar-workers-per-cu", type=int, default=0, help="D* persistent workers per CU (0 = default)")
     ap.add_argument("--dstar-residency", type=int, default=0,
