@@ -69,6 +69,7 @@ def control_leg(args, torch, dist, world, rank):
     best = torch.empty(na, dtype=torch.int32, device="cuda")
     status = torch.empty(na, dtype=torch.int32, device="cuda")
     nst = torch.empty(na, dtype=torch.int32, device="cuda")
+    _LABEL[0] = "mpc_sampled_dwa"
 
     def step():
         rc = L.pmp_dwa_step_batch(ctx, _lib.stream_ptr(), occ_bits.data_ptr(), ox, oy, gocc.shape[0], gocc.shape[1],
@@ -84,6 +85,15 @@ def control_leg(args, torch, dist, world, rank):
     st.copy_(st0)
     K = args.control_steps
     elapsed, kern_ms = timed(torch, dist, lambda i: step(), K)
+    # the timed work checked: an untimed replay of the same K steps from the same states must end in
+    # the same agent states and controls (the first step's evaluation is pinned to the oracle by
+    # tests/test_dwa_gpu.py)
+    ref_out = {"state": st.clone(), "u": u.clone(), "best": best.clone(), "status": status.clone()}
+    st.copy_(st0)
+    for _ in range(K):
+        step()
+    torch.cuda.synchronize()
+    checked = check_timed("dwa", ref_out, [{"state": st, "u": u, "best": best, "status": status}])
     steps_done = na * K * world
     # SURVEY.md §8(d) C4 in the stencil formulation, transcendental calls not counted: per sample and
     # step 12 flops of rollout (x, y, th updates) + a 3x3 stencil of 6 flops per cell; 20 per sample
@@ -118,39 +128,120 @@ def control_leg(args, torch, dist, world, rank):
                "reference_formulation": {"value": nb * repsb / dtb, "cores": threads,
                                          "sample": f"{nb} agents x {repsb} steps, cdist over every obstacle like "
                                                    f"dwa.py:164, {dtb:.1f} s"}}
+    _LABEL[0] = "setup"
     return {"metric": "MPC steps/sec (H=30, 4096 samples): sampled-rollout control step (DWA form)",
             "value": steps_done / elapsed, "unit": "agent-steps/s", "agents_per_gpu": na, "steps": K,
             "ms_per_step": elapsed / K * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
+            "timed_launches_checked": checked,
             "config": {"workload": "C4: README 51x31 grid, 64x64 (v,w) samples, H=30, weights 0.2/0.1/0.05"},
             "roofline": with_traffic({"bound": "fp64-valu", "achieved": achieved_tf, "peak": 78.6, "unit": "TFLOP/s",
                                       "frac": achieved_tf / 78.6, "traffic": None,
                                       "flops_per_agent_step": flops_per_step,
                                       "flops_note": "SURVEY.md 8(d) stencil formulation, sin/cos/atan2 not counted"},
-                                     "dwa_kernel"),
+                                     "dwa_kernel", "mpc_sampled_dwa"),
             "cpu_baseline": cpu}
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per dispatch of `kernel` from the newest committed profiles/r*/pmc_traffic.json: the
-    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench (tools/profile_round.sh,
-    summarised by tools/prof_summary.py with the guide's gfx950 correction).  (bytes, source) or
-    (None, None) when no summary is committed."""
+# ---- launch manifest -------------------------------------------------------------------------
+# Which workload (leg) made each dispatch of each kernel, in launch order, so the rocprofv3 kernel
+# trace and PMC passes can be keyed per (kernel, workload) (tools/prof_summary.py): every C-ABI
+# planner call is counted through a wrapper on the library, under the label of the leg running.
+_MANIFEST = []  # [label, kernel short name, dispatches], consecutive equal (label, kernel) merged
+_LABEL = ["setup"]
+_G2D = {0: "astar2d_kernel", 1: "dijkstra2d_kernel", 2: "gbfs2d_kernel", 3: "theta2d_kernel", 4: "lazy_theta2d_kernel"}
+ENTRY_KERNEL = {  # C-ABI entry -> (short name of the kernel it launches, as tools/prof_summary.short)
+    "pmp_astar2d_batch": lambda a: "astar2d_kernel",
+    "pmp_graph2d_batch": lambda a: _G2D[int(a[2])],
+    "pmp_astar3d_batch": lambda a: "astar3d_kernel",
+    "pmp_graph3d_batch": lambda a: "astar3d_kernel",
+    "pmp_dstar2d_batch": lambda a: "dstar_kernel",
+    "pmp_dstar2d_onpress_batch": lambda a: "dstar_kernel",
+    "pmp_dstar3d_batch": lambda a: "dstar3d_kernel",
+    "pmp_lpastar3d_batch": lambda a: "lpa3d_kernel",
+    "pmp_lpastar2d_batch": lambda a: "lpa_kernel",
+    "pmp_dstarlite2d_batch": lambda a: "lpa_kernel",
+    "pmp_lpastar2d_replan_batch": lambda a: "lpa_kernel",
+    "pmp_dstarlite2d_replan_batch": lambda a: "lpa_kernel",
+    "pmp_dwa_step_batch": lambda a: "dwa_kernel",
+    "pmp_rrt_batch": lambda a: "rrt_kernel",
+    "pmp_totp3d_batch": lambda a: "totp3d_kernel",
+    "pmp_track_step_batch": lambda a: "track_kernel_lqr" if int(a[2]) == 0 else "track_kernel_mpc",
+    "pmp_lqr_control_batch": lambda a: "lqr_control_kernel",
+    "pmp_mpc_control_batch": lambda a: "mpc_control_kernel",
+}
+
+
+def count_launches(L):
+    """Wrap the planner entry points of the (singleton) library object so every successful call is
+    logged in _MANIFEST under the current label.  Idempotent."""
+    if getattr(L, "_pmp_counted", False):
+        return L
+    for name, kern in ENTRY_KERNEL.items():
+        fn = getattr(L, name)
+
+        def wrapped(*a, _fn=fn, _k=kern):
+            rc = _fn(*a)
+            if rc == 0:
+                k = _k(a)
+                if _MANIFEST and _MANIFEST[-1][0] == _LABEL[0] and _MANIFEST[-1][1] == k:
+                    _MANIFEST[-1][2] += 1
+                else:
+                    _MANIFEST.append([_LABEL[0], k, 1])
+            return rc
+        setattr(L, name, wrapped)
+    L._pmp_counted = True
+    return L
+
+
+class leg_label:
+    """with leg_label("dstar_256"): ... -- the launches inside belong to that workload."""
+
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        self.prev = _LABEL[0]
+        _LABEL[0] = self.name
+
+    def __exit__(self, *exc):
+        _LABEL[0] = self.prev
+
+
+def _newest_profile(fname):
     import glob
 
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_traffic.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        d = json.load(f).get(kernel) or {}
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", fname)),
+                   key=lambda p: int(os.path.basename(os.path.dirname(p))[1:] or 0))
+    return files[-1] if files else None
+
+
+def pmc_traffic(workload: str, kernel: str):
+    """HBM bytes per dispatch of `kernel` in the leg `workload`, from the newest committed
+    profiles/r*/pmc_traffic.json (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, keyed per
+    (kernel, workload) through the bench's launch manifest by tools/prof_summary.py, gfx950
+    correction applied).  A summary entry whose kernel or workload does not match is refused.
+    (bytes, source) or (None, reason)."""
+    path = _newest_profile("pmc_traffic.json")
+    if not path:
+        return None, "no committed pmc_traffic.json"
+    with open(path) as f:
+        d = json.load(f).get("workloads", {}).get(workload)
+    src = os.path.relpath(path, REPO)
+    if not d:
+        return None, f"{src} has no entry for workload {workload}"
+    if d.get("kernel") != kernel:
+        return None, f"{src} [{workload}] is kernel {d.get('kernel')}, not {kernel}: refused"
     b = d.get("hbm_bytes_per_dispatch")
-    return (float(b) if b is not None else None), os.path.relpath(files[-1], REPO)
+    return (float(b) if b is not None else None), f"{src} [{workload}: {kernel}]"
 
 
-def with_traffic(roof: dict, kernel: str) -> dict:
-    t, src = pmc_traffic(kernel)
+def with_traffic(roof: dict, kernel: str, workload: str) -> dict:
+    t, src = pmc_traffic(workload, kernel)
     roof["traffic"] = t
-    if src:
-        roof["traffic_source"] = f"{src} [{kernel}]"
+    roof["traffic_source"] = src
+    alg = roof.get("algorithmic_bytes_per_launch")
+    if t and alg:
+        roof["traffic_over_algorithmic"] = t / alg
     return roof
 
 
@@ -158,16 +249,14 @@ def with_mfma(roof: dict, kernel: str) -> dict:
     """MFMA utilisation of `kernel` from the newest committed profiles/r*/pmc_mfma.json (the separate
     rocprofv3 --pmc pass of SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE, tools/profile_round.sh):
     busy cycles over 1024 SIMDs x the dispatch's GPU cycles, in percent (rocprofv3's MfmaUtil)."""
-    import glob
-
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_mfma.json")))
+    path = _newest_profile("pmc_mfma.json")
     roof["mfma_util_pct"] = None
-    if files:
-        with open(files[-1]) as f:
+    if path:
+        with open(path) as f:
             d = json.load(f).get(kernel) or {}
         if d.get("mfma_util_pct") is not None:
             roof["mfma_util_pct"] = float(d["mfma_util_pct"])
-            roof["mfma_source"] = f"{os.path.relpath(files[-1], REPO)} [{kernel}]"
+            roof["mfma_source"] = f"{os.path.relpath(path, REPO)} [{kernel}]"
     return roof
 
 
@@ -184,11 +273,12 @@ def pool_stream(torch, i):
     return _STREAM_POOL[i]
 
 
-def timed(torch, dist, fn, steps, stream=None, streams=None):
+def timed(torch, dist, fn, steps, stream=None, streams=None, last=None):
     """Barrier + sync, run `steps` launches with HIP events around each (on `stream`; or, with
     `streams`, launch i runs with streams[i % len] current: batches in flight, each on its own
     stream and so its own per-stream pmp_ctx), barrier + sync; returns (wall seconds, max over
-    ranks; mean event ms per launch)."""
+    ranks; mean event ms per launch).  With a list `last`, the return values of the final launch
+    on each stream are appended to it (for the check of the timed work, `check_timed`)."""
     import contextlib
 
     from python_motion_planning_amd import shard
@@ -196,6 +286,7 @@ def timed(torch, dist, fn, steps, stream=None, streams=None):
     shard.barrier(dist)
     torch.cuda.synchronize()
     evs = []
+    rets = {}
     t0 = time.perf_counter()
     for i in range(steps):
         sm = streams[i % len(streams)] if streams else stream
@@ -205,7 +296,9 @@ def timed(torch, dist, fn, steps, stream=None, streams=None):
         else:
             e0.record(sm)
         with (torch.cuda.stream(sm) if streams else contextlib.nullcontext()):
-            fn(i)
+            r = fn(i)
+        if last is not None:
+            rets[i % len(streams) if streams else 0] = r
         if sm is None:
             e1.record()
         else:
@@ -216,7 +309,66 @@ def timed(torch, dist, fn, steps, stream=None, streams=None):
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     elapsed, kern_ms = shard.max_over_ranks(dist, [elapsed, kern_ms], "cuda")
+    if last is not None:
+        last.extend(rets.values())
     return elapsed, kern_ms
+
+
+LPA_BYTES_NOTE = ("LPA* / D* Lite: per expansion the 3x3 block of (g, rhs) 9 x 16 B + 9 B occupancy + 8 B g write "
+                  "= 161 B; per U insertion 20 B (k1, k2 f64 + cell)")
+
+
+def lpa_bytes(expansions, pushes) -> float:
+    """Algorithmic bytes of the LPA* / D* Lite 2D list machine (lpa_star.py:39-230, d_star_lite.py:14-187):
+    161 B per expansion + 20 B per U insertion (LPA_BYTES_NOTE)."""
+    return 161.0 * float(expansions) + 20.0 * float(pushes)
+
+
+def hbm_roof(alg_bytes, kern_ms, note):
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None, "algorithmic_bytes_per_launch": alg_bytes, "bytes_note": note}
+
+
+def dyn3d_roof(kind, n, pushes, kern_ms):
+    """DStar3D (d_star3d.py:60-281): per processState the 3x3x3 block of voxel states (h, k f64 + tag /
+    parent: 27 x 24 B) + 27 B occupancy + 2 OPEN entries x 16 B = 707 B.  LPAStar3D
+    (lpa_star3d.py:40-225): per expansion 27 x 16 B (g, rhs) + 27 B occupancy + 8 B g write = 467 B,
+    + 20 B per U insertion (counted by the kernel; when absent, one per expansion)."""
+    if kind == "dstar3d":
+        return hbm_roof(707.0 * n, kern_ms, "707 B per processState (27 x 24 B voxel states + 27 B occupancy + 2 OPEN "
+                                            "entries x 16 B)")
+    p = n if pushes is None else pushes
+    return hbm_roof(467.0 * n + 20.0 * p, kern_ms, "467 B per expansion (27 x 16 B g/rhs + 27 B occupancy + 8 B write) "
+                                                   "+ 20 B per U insertion")
+
+
+def poison(bufs):
+    """Overwrite output buffers before a timed region (NaN / -1), so that check_timed proves the
+    timed launches wrote them."""
+    for t in bufs:
+        if t.is_floating_point():
+            t.fill_(float("nan"))
+        else:
+            t.fill_(-1)
+
+
+def check_timed(name, ref: dict, outs) -> int:
+    """The work of the timed launches is checked, not trusted: every stream's last timed output
+    equals the warmup launch's (which the legs check against the oracle / invariants) field for
+    field.  Returns the number of launches checked; raises on a mismatch."""
+    import torch
+
+    n = 0
+    for o in outs:
+        for k, v in ref.items():
+            got = o[k]
+            if not torch.equal(got.to(v.device), v):
+                raise AssertionError(f"{name}: timed launch output '{k}' differs from the warmup launch's")
+        n += 1
+    if n == 0:
+        raise AssertionError(f"{name}: no timed output to check")
+    return n
 
 
 def cgroup_cpus():
@@ -328,6 +480,10 @@ def rrt_leg(args, torch, dist, world, rank):
     torch.cuda.synchronize()
     for b in lanes:
         assert torch.equal(b["nn"], out["n_nodes"]) and torch.equal(b["st"], out["status"])
+    rkeys = ("nn", "st", "cost", "plen", "draws")
+    ref_out = {k: lanes[0][k].clone() for k in rkeys}
+    for b in lanes:
+        poison([b[k] for k in rkeys])
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -348,12 +504,16 @@ def rrt_leg(args, torch, dist, world, rank):
     from python_motion_planning_amd import shard
 
     elapsed, kern_ms = shard.max_over_ranks(dist, [elapsed, kern_ms], "cuda")
+    checked = check_timed("rrt_star", ref_out, lanes[: min(len(lanes), args.rrt_steps)])
     # the bytes the kernel loads: 4 B per node scanned (the 16-bit fixed-point
     # coordinate copy of the coarse nearest / radius scans) + 24 B per in-radius candidate (exact
     # f64 x, y and g).  The trees (4 B x 65,537 nodes per query) stay in L2 / Infinity Cache, so the
     # roof is the L2 bandwidth (MI355X_MICROARCH.md: ~34.5 TB/s aggregate)
     alg_bytes = float(4.0 * ctr[:, 1].sum() + 24.0 * ctr[:, 2].sum())
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    # SURVEY.md §8(d)'s own accounting: 16 B of xy per node scanned + 8 B of g per in-radius node
+    sv_bytes = float(16.0 * ctr[:, 1].sum() + 8.0 * ctr[:, 2].sum())
+    sv_gbs = sv_bytes / (kern_ms * 1e-3) / 1e9
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as O
@@ -371,15 +531,19 @@ def rrt_leg(args, torch, dist, world, rank):
     return {"metric": "RRT* plans/sec on 512x512 Map, 65536 samples", "value": nq * args.rrt_steps * world / elapsed,
             "unit": "plans/s", "queries_per_gpu": nq, "steps": args.rrt_steps,
             "ms_per_step": elapsed / args.rrt_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
-            "streams": len(lanes),
+            "streams": len(lanes), "timed_launches_checked": checked,
             "config": {"workload": "C3: Map(512,512), 40 rects + 40 circles (default_rng(7)), (5,5)->(505,505), "
                                    "65536 samples, max_dist 0.5, r 10, goal rate 0.05"},
             "roofline": with_traffic({"bound": "l2", "achieved": achieved, "peak": L2_PEAK_GBS, "unit": "GB/s",
                                       "frac": achieved / L2_PEAK_GBS, "traffic": None,
                                       "algorithmic_bytes_per_launch": alg_bytes,
                                       "bytes_note": "4 B per node scanned + 24 B per in-radius candidate, as loaded; "
-                                                    "traffic = HBM bytes (PMC), far below: the trees are cache-resident"},
-                                     "rrt_kernel"),
+                                                    "traffic = HBM bytes (PMC), far below: the trees are cache-resident",
+                                      "survey_8d": {"bytes_per_launch": sv_bytes, "achieved": sv_gbs,
+                                                    "frac_l2": sv_gbs / L2_PEAK_GBS, "frac_hbm": sv_gbs / HBM_PEAK_GBS,
+                                                    "note": "SURVEY.md 8(d): 16 B xy per node scanned + 8 B g per "
+                                                            "in-radius node"}},
+                                     "rrt_kernel", "rrt_star"),
             "detail": {"found": int((status == 0).sum()), "mean_nodes": float(out["n_nodes"].float().mean().item()),
                        "iterations_per_launch": int(ctr[:, 0].sum()), "nodes_scanned_per_launch": int(ctr[:, 1].sum()),
                        "collision_tests_per_launch": int(ctr[:, 3].sum())},
@@ -393,6 +557,7 @@ def astar3d_leg(args, torch, dist, world, rank):
 
     nq = args.a3_queries
     occ, s, g = wl.c5_workload(nq, first_seed=rank * nq)
+    _LABEL[0] = "astar3d"
     X, Y, Z = occ.shape[1:]
     words = np.stack([batch.pack_bits(o) for o in occ])
     occ_d = torch.as_tensor(np.ascontiguousarray(words).view(np.int32), device="cuda")
@@ -432,6 +597,10 @@ def astar3d_leg(args, torch, dist, world, rank):
     cost, plen, path = lanes[0]["cost"], lanes[0]["plen"], lanes[0]["path"]
     for b in lanes[1:]:
         assert torch.equal(b["cost"], cost) and torch.equal(b["st"], lanes[0]["st"])
+    akeys = ("cost", "plen", "nexp", "st")
+    ref_out = {k: lanes[0][k].clone() for k in akeys}
+    for b in lanes:
+        poison([b[k] for k in akeys])
     shard.barrier(dist)
     torch.cuda.synchronize()
     evs = []
@@ -448,6 +617,8 @@ def astar3d_leg(args, torch, dist, world, rank):
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(e) for a, e in evs]))
     elapsed, kern_ms = shard.max_over_ranks(dist, [elapsed, kern_ms], "cuda")
+    checked = check_timed("astar3d", ref_out, lanes[: min(len(lanes), args.a3_steps)])
+    cost = ref_out["cost"]
     # per plan 55*E3 + 16*(P3 + Q3), with P3 the reference's pushes and Q3 <= P3
     # (every pushed entry popped at most once): 55*E3 + 32*P3
     alg_bytes = float(np.sum(55.0 * c[:, 2] + 32.0 * c[:, 0]))
@@ -470,18 +641,20 @@ def astar3d_leg(args, torch, dist, world, rank):
         cpu = {"value": nq * reps / dt, "unit": "plans/s", "cores": th, "kind": "port",
                "sample": f"all {nq} C5 queries, repeated {reps}x, C restatement of AStar3D (oracle/pmp_oracle.c) "
                          f"with OpenMP over queries, {dt:.1f} s wall"}
+    _LABEL[0] = "totp3d"
     traj = totp3d_leg(args, torch, dist, world, rank, plen, path, (X, Y, Z)) if "totp" in args.legs.split(",") else None
+    _LABEL[0] = "setup"
     torch.cuda.synchronize()
     for b in lanes:  # the lanes' scratch (about 15 GB each) is not needed by the other legs
         L.pmp_destroy(b["ctx"])
     return {"metric": "3D A* plans/sec, Grid3D(26,20,16) door scenario, 8192 queries", "value": nq * args.a3_steps * world / elapsed,
             "unit": "plans/s", "queries_per_gpu": nq, "steps": args.a3_steps,
             "ms_per_step": elapsed / args.a3_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
-            "streams": len(lanes), "workers_per_cu": args.a3_workers_per_cu, "resident_per_cu": args.a3_residency,
+            "streams": len(lanes), "timed_launches_checked": checked, "workers_per_cu": args.a3_workers_per_cu, "resident_per_cu": args.a3_residency,
             "config": {"workload": "C5: Grid3D(26,20,16) door, random.seed(i) pairs, safety bubbles r=1, euclidean"},
             "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                       "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                                      "algorithmic_bytes_per_launch": alg_bytes}, "astar3d_kernel"),
+                                      "algorithmic_bytes_per_launch": alg_bytes}, "astar3d_kernel", "astar3d"),
             "detail": {"expansions_per_launch": int(c[:, 2].sum()), "reference_pushes_per_launch": int(c[:, 0].sum()),
                        "heap_pops_per_launch": int(c[:, 1].sum()), "max_heap_entries": int(c[:, 3].max())},
             "cpu_baseline": cpu, "trajectory": traj}
@@ -579,10 +752,12 @@ def graphs_leg(args, torch, dist, world, rank):
     occ_bits = batch.occ_bits_device(occ2, torch)
     s2d, g2d = torch.as_tensor(s2, device="cuda"), torch.as_tensor(g2, device="cuda")
     for algo in ("theta_star", "lazy_theta_star"):
+        _LABEL[0] = algo + "_2d"
         # batches in flight as in the headline (own stream + pmp_ctx each)
         lanes = []
         for _ in range(max(1, args.theta_streams)):
             ctx = L.pmp_create(torch.cuda.current_device())
+            _lib.check(ctx, L.pmp_astar2d_set_engine(ctx, 0, 0), "engine")  # Theta*: one query per wave
             _lib.check(ctx, L.pmp_astar2d_reserve(ctx, 1024, 1024, args.theta_workers, 0), "reserve")
             if args.theta_residency:
                 _lib.check(ctx, L.pmp_astar2d_set_residency(ctx, args.theta_residency), "residency")
@@ -611,6 +786,10 @@ def graphs_leg(args, torch, dist, world, rank):
         assert (r["status"] == 0).all(), f"unexpected {algo} statuses"
         for b in lanes[1:]:
             assert torch.equal(b["cost"], r["cost"])
+        gkeys = ("cost", "plen", "nexp", "st")
+        ref_out = {k: lanes[0][k].clone() for k in gkeys}
+        for b in lanes:
+            poison([b[k] for k in gkeys])
         c = ctr.cpu().numpy()
         shard.barrier(dist)
         torch.cuda.synchronize()
@@ -628,6 +807,7 @@ def graphs_leg(args, torch, dist, world, rank):
         elapsed = time.perf_counter() - t0
         kern_ms = float(np.mean([a.elapsed_time(e) for a, e in evs]))
         elapsed, kern_ms = shard.max_over_ranks(dist, [elapsed, kern_ms], "cuda")
+        checked = check_timed(algo, ref_out, lanes[: min(len(lanes), args.graph_steps)])
         for b in lanes:  # their scratch (about 40 GB each with the Theta* parents) is not needed later
             L.pmp_destroy(b["ctx"])
         lanes.clear()
@@ -648,10 +828,12 @@ def graphs_leg(args, torch, dist, world, rank):
         out[algo + "_2d"] = {
             "metric": f"{algo} 2D plans/sec on the C2 1024^2 grid", "value": nq * args.graph_steps * world / elapsed,
             "unit": "plans/s", "queries_per_gpu": nq, "steps": args.graph_steps, "streams": args.theta_streams,
+            "timed_launches_checked": checked,
             "ms_per_step": elapsed / args.graph_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": alg,
-                         "note": "A*'s 19E + 16(P+Q) bytes; the line-of-sight cells are not counted"},
+            "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                      "frac": achieved / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": alg,
+                                      "note": "A*'s 19E + 16(P+Q) bytes; the line-of-sight cells are not counted"},
+                                     "theta2d_kernel" if algo == "theta_star" else "lazy_theta2d_kernel", algo + "_2d"),
             "detail": {"expansions_per_launch": int(c[:, 2].sum()), "pushes_per_launch": int(c[:, 0].sum())},
             "cpu_baseline": cpu}
 
@@ -664,6 +846,8 @@ def graphs_leg(args, torch, dist, world, rank):
     s_d, g_d = torch.as_tensor(sl, device="cuda"), torch.as_tensor(gl, device="cuda")
     lpa_streams = [pool_stream(torch, i) for i in range(max(1, args.lpa_streams))]
     for lite in (False, True):
+        _LABEL[0] = "dstar_lite" if lite else "lpa_star"
+
         def run(i, lite=lite, counters=False):
             return batch.lpastar2d_batch(occ, s_d, g_d, counters=counters, lite=lite)
         r = run(0, counters=True)
@@ -672,7 +856,9 @@ def graphs_leg(args, torch, dist, world, rank):
                 run(0)
         torch.cuda.synchronize()
         c = r["counters"].cpu().numpy()
-        elapsed, kern_ms = timed(torch, dist, run, args.graph_steps, streams=lpa_streams)
+        last = []
+        elapsed, kern_ms = timed(torch, dist, run, args.graph_steps, streams=lpa_streams, last=last)
+        checked = check_timed("lpa", {k: r[k] for k in ("cost", "n_expanded", "status", "path_len")}, last)
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             from oracle import oracle as O
@@ -692,13 +878,15 @@ def graphs_leg(args, torch, dist, world, rank):
                    "sample": f"all {nl} queries, repeated {reps}x, C restatement (oracle/pmp_oracle.c) with OpenMP "
                              f"over queries, {dt:.1f} s wall"}
         name = "dstar_lite" if lite else "lpa_star"
+        alg = lpa_bytes(c[:, 1].sum(), c[:, 0].sum())
         out[name] = {
             "metric": f"{name} plans/sec on the README 51x31 grid ({nl} random free-cell pairs)",
             "value": nl * args.graph_steps * world / elapsed, "unit": "plans/s", "queries_per_gpu": nl,
             "steps": args.graph_steps, "ms_per_step": elapsed / args.graph_steps * 1e3, "kernel_ms_per_launch": kern_ms,
-            "dtype": "f64", "roofline": None,
+            "timed_launches_checked": checked, "dtype": "f64",
+            "roofline": with_traffic(hbm_roof(alg, kern_ms, LPA_BYTES_NOTE), "lpa_kernel", name),
             "roofline_note": "latency-bound list machine (U scans / shifts of a few hundred entries per expansion, "
-                             "L2-resident); no HBM or MFMA roofline applies",
+                             "L2-resident): a small frac is the expected reading",
             "detail": {"expansions_per_launch": int(c[:, 1].sum()), "pushes_per_launch": int(c[:, 0].sum()),
                        "max_U": int(c[:, 3].max())},
             "cpu_baseline": cpu}
@@ -709,15 +897,20 @@ def graphs_leg(args, torch, dist, world, rank):
     T = inner[rng.integers(len(inner), size=(nl, nt))].astype(np.int32)
     t_d = torch.as_tensor(T, device="cuda")
     for lite in (False, True):
-        def run(i, lite=lite):
-            return batch.lpastar2d_replan_batch(occ, s_d, g_d, t_d, lite=lite)
+        _LABEL[0] = ("dstar_lite" if lite else "lpa_star") + "_replan"
+
+        def run(i, lite=lite, counters=False):
+            return batch.lpastar2d_replan_batch(occ, s_d, g_d, t_d, lite=lite, counters=counters)
         for sm in lpa_streams:
             with torch.cuda.stream(sm):
                 run(0)
-        r = run(0)
+        r = run(0, counters=True)
         torch.cuda.synchronize()
         ne = r["n_expanded"].cpu().numpy()
-        elapsed, kern_ms = timed(torch, dist, run, args.graph_steps, streams=lpa_streams)
+        cr = r["counters"].cpu().numpy()
+        last = []
+        elapsed, kern_ms = timed(torch, dist, run, args.graph_steps, streams=lpa_streams, last=last)
+        checked = check_timed("lpa_replan", {k: r[k] for k in ("cost", "n_expanded", "status", "path_len")}, last)
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             from oracle import oracle as O
@@ -739,9 +932,12 @@ def graphs_leg(args, torch, dist, world, rank):
             "metric": f"{name} plans/sec (plan() + {nt} OnPress edits per session, README grid, {nl} sessions)",
             "value": nl * (nt + 1) * args.graph_steps * world / elapsed, "unit": "plans/s", "sessions_per_gpu": nl,
             "steps": args.graph_steps, "ms_per_step": elapsed / args.graph_steps * 1e3,
-            "kernel_ms_per_launch": kern_ms, "dtype": "f64", "roofline": None,
+            "kernel_ms_per_launch": kern_ms, "timed_launches_checked": checked, "dtype": "f64",
+            "roofline": with_traffic(hbm_roof(lpa_bytes(cr[:, 1].sum(), cr[:, 0].sum()), kern_ms, LPA_BYTES_NOTE),
+                                     "lpa_kernel", name),
             "roofline_note": "latency-bound list machine, as lpa_star",
             "detail": {"expansions_per_launch": int(np.maximum(ne, 0).sum())}, "cpu_baseline": cpu}
+    _LABEL[0] = "setup"
     return out
 
 
@@ -756,6 +952,7 @@ def dstar_leg(args, torch, dist, world, rank):
     out = {}
     for W, nq in ((256, args.dstar_queries), (512, args.dstar_queries)):
         occ, s, g = wl.c2_workload(nq=nq, W=W, H=W, density=0.1, grid_seed=4, pair_seed=5 + rank)
+        _LABEL[0] = f"dstar_{W}"
         s_d, g_d = torch.as_tensor(s, device="cuda"), torch.as_tensor(g, device="cuda")
         bits = batch.occ_bits_device(occ, torch)
         # batches in flight (own stream + pmp_ctx each): one wave per query, so a launch lasts as long
@@ -788,6 +985,10 @@ def dstar_leg(args, torch, dist, world, rank):
             assert torch.equal(b["cost"], r["cost"]) and torch.equal(b["npr"], r["n_process"])
         npr = r["n_process"].cpu().numpy()
         st = r["status"].cpu().numpy()
+        dkeys = ("cost", "plen", "npr", "st")
+        ref_out = {k: lanes[0][k].clone() for k in dkeys}
+        for b in lanes:
+            poison([b[k] for k in dkeys])
         shard.barrier(dist)
         torch.cuda.synchronize()
         evs = []
@@ -804,7 +1005,8 @@ def dstar_leg(args, torch, dist, world, rank):
         elapsed = time.perf_counter() - t0
         kern_ms = float(np.mean([a.elapsed_time(e) for a, e in evs]))
         elapsed, kern_ms = shard.max_over_ranks(dist, [elapsed, kern_ms], "cuda")
-        r = {k: v.clone() for k, v in r.items()}
+        checked = check_timed(f"dstar_{W}", ref_out, lanes[: min(len(lanes), args.dstar_steps)])
+        r = {"cost": ref_out["cost"], "n_process": ref_out["npr"], "status": ref_out["st"]}
         torch.cuda.synchronize()
         for b in lanes:
             L.pmp_destroy(b["ctx"])
@@ -832,16 +1034,17 @@ def dstar_leg(args, torch, dist, world, rank):
             "metric": f"DStar plans/sec on a {W}x{W} grid (10% obstacles, {nq} random start/goal pairs)",
             "value": nq * args.dstar_steps * world / elapsed, "unit": "plans/s", "queries_per_gpu": nq,
             "steps": args.dstar_steps, "ms_per_step": elapsed / args.dstar_steps * 1e3, "kernel_ms_per_launch": kern_ms,
-            "dtype": "f64", "streams": args.dstar_streams,
+            "dtype": "f64", "streams": args.dstar_streams, "timed_launches_checked": checked,
             "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                       "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                                       "algorithmic_bytes_per_launch": alg,
                                       "bytes_note": "248 B per processState (3x3 cell states 9 x 24 B + 2 OPEN "
                                                     "entries x 16 B); latency-bound, one wave per query"},
-                                     "dstar_kernel"),
+                                     "dstar_kernel", f"dstar_{W}"),
             "detail": {"process_state_per_launch": int(npr.sum()), "max_process_state_query": int(npr.max()),
                        "statuses": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))}},
             "cpu_baseline": cpu}
+    _LABEL[0] = "setup"
     return out
 
 
@@ -868,20 +1071,24 @@ def dyn3d_leg(args, torch, dist, world, rank):
     streams = [pool_stream(torch, i) for i in range(max(1, args.dyn3d_streams))]
     out = {}
     for kind, rounds in (("dstar3d", None), ("dstar3d", inner), ("lpastar3d", None), ("lpastar3d", changes)):
+        _LABEL[0] = kind + ("" if rounds is None else "_replan")
         rd = None if rounds is None else torch.as_tensor(rounds, device="cuda")
 
-        def run(i, kind=kind, rd=rd):
+        def run(i, kind=kind, rd=rd, counters=False):
             with torch.cuda.stream(streams[i % len(streams)]):
                 if kind == "dstar3d":
                     return batch.dstar3d_batch(occ.shape, s_d, g_d, rd, path_cap=X * Y * Z + 1, occ_bits=bits)
-                return batch.lpastar3d_batch(occ.shape, s_d, g_d, rd, path_cap=X * Y * Z + 1, occ_bits=bits)
+                return batch.lpastar3d_batch(occ.shape, s_d, g_d, rd, path_cap=X * Y * Z + 1, occ_bits=bits,
+                                             counters=counters)
 
-        r = run(0)
+        r = run(0, counters=True)
         torch.cuda.synchronize()
         nkey = "n_process" if kind == "dstar3d" else "n_expanded"
         nexp = r[nkey].cpu().numpy()
+        pushes = int(r["counters"][:, 0].sum().item()) if r.get("counters") is not None else None
         st = r["status"].cpu().numpy()
         cost0 = r["cost"].cpu().numpy()
+        ref_out = {k: r[k].clone() for k in ("cost", nkey, "status", "path_len")}
         del r
         # one untimed launch per stream whose outputs are freed: the timed launches then reuse those
         # blocks from the stream's caching-allocator pool instead of allocating (and synchronising)
@@ -891,12 +1098,13 @@ def dyn3d_leg(args, torch, dist, world, rank):
         shard.barrier(dist)
         torch.cuda.synchronize()
         evs = []
+        lastr = {}
         t0 = time.perf_counter()
         for i in range(args.dyn3d_steps):
             sm = streams[i % len(streams)]
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(sm)
-            run(i)
+            lastr[i % len(streams)] = run(i)
             e1.record(sm)
             evs.append((e0, e1))
         torch.cuda.synchronize()
@@ -904,6 +1112,8 @@ def dyn3d_leg(args, torch, dist, world, rank):
         elapsed = time.perf_counter() - t0
         kern_ms = float(np.mean([a.elapsed_time(e) for a, e in evs]))
         elapsed, kern_ms = shard.max_over_ranks(dist, [elapsed, kern_ms], "cuda")
+        checked = check_timed(kind, ref_out, list(lastr.values()))
+        del lastr
         R = 1 if rounds is None else rounds.shape[1] + 1
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -930,13 +1140,17 @@ def dyn3d_leg(args, torch, dist, world, rank):
             "metric": f"{kind} plans/sec on C5 (Grid3D 26x20x16 door, {nq} queries"
                       + ("" if rounds is None else f", plan + {R - 1} dynamic-obstacle calls per session") + ")",
             "value": nq * R * args.dyn3d_steps * world / elapsed, "unit": "plans/s", "queries_per_gpu": nq,
+            "timed_launches_checked": checked,
             "steps": args.dyn3d_steps, "ms_per_step": elapsed / args.dyn3d_steps * 1e3, "kernel_ms_per_launch": kern_ms,
-            "dtype": "f64", "roofline": None,
-            "roofline_note": "latency-bound list machines (OPEN / U with Python-list semantics); no HBM or MFMA "
-                             "roofline applies",
+            "dtype": "f64",
+            "roofline": with_traffic(dyn3d_roof(kind, int(np.maximum(nexp, 0).sum()), pushes, kern_ms),
+                                     "dstar3d_kernel" if kind == "dstar3d" else "lpa3d_kernel", name),
+            "roofline_note": "latency-bound list machines (OPEN / U with Python-list semantics): a small frac is "
+                             "the expected reading",
             "detail": {"expansions_per_launch": int(np.maximum(nexp, 0).sum()),
                        "statuses": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))}},
             "cpu_baseline": cpu}
+    _LABEL[0] = "setup"
     return out
 
 
@@ -958,6 +1172,7 @@ def latency_leg(args, torch, dist, world, rank):
     k = int(np.argsort(shard.octile(s2, g2))[32])
     cases.append(("c2_1024_one_query", occ2, tuple(int(v) for v in s2[k]), tuple(int(v) for v in g2[k]), 5))
     for name, occ, s, g, reps in cases:
+        _LABEL[0] = name
         W, H = occ.shape
         env = pmp.Grid(W, H)
         env.update({(int(x), int(y)) for x, y in np.argwhere(occ)})
@@ -1005,6 +1220,7 @@ def latency_leg(args, torch, dist, world, rank):
                      "reference_python_ms": "14.8-26.8 (SURVEY.md §6)" if name == "c1_readme" else
                                             "2760 mean per C2 query (SURVEY.md §6)",
                      "cpu_baseline": cpu}
+    _LABEL[0] = "setup"
     return out
 
 
@@ -1030,17 +1246,24 @@ def track_leg(args, torch, dist, world, rank, kind):
     gd = torch.tensor(goals, dtype=torch.float64, device="cuda")
     xyd = torch.tensor(xy, dtype=torch.float64, device="cuda")
     offd = torch.tensor(off, dtype=torch.int32, device="cuda")
+    _LABEL[0] = "lqr" if kind == "lqr" else "mpc_qp"
     o = batch.track_step_batch(kind, lp, st, gd, xyd, offd, iters=iters, u_p=up, **kw)
     torch.cuda.synchronize()
     stepped = int(o["n_steps"].sum().item())
     admm = int(o["admm_iters"].sum().item())
 
+    ref_out = {"u": o["u"].clone(), "n_steps": o["n_steps"].clone(), "admm_iters": o["admm_iters"].clone(),
+               "state": st.clone(), "u_p": up.clone()}
+
     def run(i):
         st.copy_(st0)
         up.zero_()
-        batch.track_step_batch(kind, lp, st, gd, xyd, offd, iters=iters, u_p=up, **kw)
+        r = batch.track_step_batch(kind, lp, st, gd, xyd, offd, iters=iters, u_p=up, **kw)
+        return {"u": r["u"], "n_steps": r["n_steps"], "admm_iters": r["admm_iters"], "state": st, "u_p": up}
 
-    elapsed, kern_ms = timed(torch, dist, run, args.track_steps)
+    last = []
+    elapsed, kern_ms = timed(torch, dist, run, args.track_steps, last=last)
+    checked = check_timed(kind, ref_out, last)
     if kind == "mpc":
         # per ADMM iteration ~ 16x16 inverse matvec (512) + scans/projections (~150); assembly 2*16*16*3p (MFMA)
         flops = admm * 662.0 + stepped * 2 * 16 * 16 * 90
@@ -1068,6 +1291,7 @@ def track_leg(args, torch, dist, world, rank, kind):
         cpu = {"value": tot / dt, "unit": "agent-steps/s", "cores": th, "kind": "port",
                "sample": f"all {na} C4 agents x {iters} plan iterations, repeated {reps}x, C restatement "
                          f"(oracle/pmp_oracle.c) with OpenMP over agents, {dt:.1f} s wall"}
+    _LABEL[0] = "setup"
     name = "LQR" if kind == "lqr" else "MPC (p=30, m=8, ADMM QP)"
     return {"metric": f"{name} tracking agent-steps/sec", "value": stepped * args.track_steps * world / elapsed,
             "unit": "agent-steps/s", "agents_per_gpu": na, "iterations_per_launch": iters, "steps": args.track_steps,
@@ -1076,10 +1300,81 @@ def track_leg(args, torch, dist, world, rank, kind):
                                    f"per launch"},
             "roofline": with_mfma(with_traffic({"bound": "fp64-valu", "achieved": achieved_tf, "peak": 78.6,
                                                 "unit": "TFLOP/s", "frac": achieved_tf / 78.6, "traffic": None},
-                                               "track_kernel_lqr" if kind == "lqr" else "track_kernel_mpc"),
+                                               "track_kernel_lqr" if kind == "lqr" else "track_kernel_mpc",
+                                               "lqr" if kind == "lqr" else "mpc_qp"),
                                   "track_kernel_lqr" if kind == "lqr" else "track_kernel_mpc"),
+            "timed_launches_checked": checked,
             "detail": {"agent_steps_per_launch": stepped, "admm_iterations_per_launch": admm},
             "cpu_baseline": cpu}
+
+
+def _sig(v, n=4):
+    """A number rounded to n significant digits (the compact line's precision)."""
+    if v is None or not isinstance(v, (int, float)) or v == 0 or v != v:
+        return v
+    return float(f"{v:.{n}g}")
+
+
+def compact_leg(rec: dict) -> dict:
+    """One secondary leg in the headline line: value, unit, roofline frac and CPU-baseline value
+    (the full record goes to the detail file)."""
+    roof = rec.get("roofline") or {}
+    cpu = rec.get("cpu_baseline") or {}
+    out = {"value": _sig(rec.get("value")), "unit": rec.get("unit"), "frac": _sig(roof.get("frac"), 3),
+           "cpu": _sig(cpu.get("value"))}
+    if roof.get("traffic") and roof.get("algorithmic_bytes_per_launch"):
+        out["traffic_x"] = _sig(roof["traffic"] / roof["algorithmic_bytes_per_launch"], 3)
+    if rec.get("timed_launches_checked") is not None:
+        out["checked"] = rec["timed_launches_checked"]
+    return out
+
+
+def write_detail(args, out: dict):
+    """The full per-leg records (every field of every leg) as JSON: --detail-out, default
+    gpurun_out/bench_detail.json (merged back from a GPU box by gpurun).  Returns the path or None."""
+    path = args.detail_out or os.path.join(REPO, "gpurun_out", "bench_detail.json")
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+        return os.path.relpath(path, REPO)
+    except OSError:
+        return None
+
+
+def headline_line(out: dict, detail_path) -> dict:
+    """The driver-parsed last stdout line (<= 4 KB): the headline with its roofline and CPU baseline,
+    and a compact map of the secondary legs."""
+    roof = dict(out["roofline"])
+    roof = {k: (_sig(v) if isinstance(v, float) else v) for k, v in roof.items()}
+    cpu = out["cpu_baseline"]
+    if cpu:
+        host = cpu.get("host") or {}
+        cpu = {"value": _sig(cpu["value"]), "unit": cpu["unit"], "cores": cpu["cores"], "kind": cpu["kind"],
+               "sample": cpu["sample"], "cpu_model": host.get("model"),
+               "one_core": _sig((cpu.get("one_core") or {}).get("value"))}
+    d = out["detail"]
+    line = {k: out[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")}
+    line["roofline"] = roof
+    line["cpu_baseline"] = cpu
+    line["detail"] = {"kernel_ms_per_launch": _sig(d["kernel_ms_per_launch"]), "streams": d["streams"],
+                      "engine": d["engine"],
+                      "expansions_per_launch": d["expansions_per_launch"],
+                      "timed_launches_checked": d["timed_launches_checked"], "detail_file": detail_path}
+    line["secondary"] = {k: compact_leg(v) for k, v in out["secondary"].items()}
+    s = json.dumps(line)
+    # keep the line inside the driver's window whatever the leg set: drop optional fields first
+    for drop in (("secondary", "traffic_x"), ("secondary", "checked"), ("cpu_baseline", "sample")):
+        if len(s) <= 4000:
+            break
+        if drop[0] == "secondary":
+            for v in line["secondary"].values():
+                v.pop(drop[1], None)
+        elif line.get("cpu_baseline"):
+            line["cpu_baseline"].pop(drop[1], None)
+        s = json.dumps(line)
+    return line
 
 
 def dry_run(args, rank, world):
@@ -1128,12 +1423,17 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--agents", type=int, default=256, help="C4 agents per GPU (control-step leg)")
     ap.add_argument("--control-steps", type=int, default=20, help="timed control steps")
-    ap.add_argument("--workers", type=int, default=768, help="persistent A* workers (waves) per launch")
+    ap.add_argument("--engine", type=int, default=1, choices=[0, 1],
+                    help="A* 2D engine: 1 = four queries per wave (astar2d_mq.hip), 0 = one query per wave (astar2d.hip)")
+    ap.add_argument("--t2lds", type=int, default=0, help="multi-query engine: level-10..14 heap bits in LDS (1) or HBM (0)")
+    ap.add_argument("--workers", type=int, default=0,
+                    help="A* queries in flight per launch (persistent 16-lane groups on engine 1, waves on engine 0); "
+                         "0 = the engine's default")
     ap.add_argument("--theta-workers", type=int, default=768, help="persistent Theta* 2D workers per launch")
     ap.add_argument("--theta-residency", type=int, default=18, help="Theta* 2D workers resident per CU (as --residency)")
-    ap.add_argument("--residency", type=int, default=18,
-                    help="A* workers resident per CU over all batches in flight (sets each worker's LDS heap "
-                         "share; 0 = one launch's own workers / 256)")
+    ap.add_argument("--residency", type=int, default=0,
+                    help="A* queries resident per CU over all batches in flight (sets each one's LDS heap share; "
+                         "0 = the engine's default)")
     ap.add_argument("--legs", default="dwa,rrt,astar3d,totp,lqr,mpc,graphs,dstar,dyn3d,latency",
                     help="secondary legs to run (comma list of dwa, rrt, astar3d, totp (C5 trajectories on the "
                          "astar3d leg's paths), lqr, mpc, graphs, dstar, dyn3d, latency; 'none' for none)")
@@ -1181,10 +1481,19 @@ def main():
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="weak: every rank plans its own --nq batch; strong: one --nq batch dealt over the ranks "
                          "(longest-first round-robin) with an all_gather of the results")
+    ap.add_argument("--detail-out", default=None,
+                    help="file for the full per-leg records (default gpurun_out/bench_detail.json); stdout's last "
+                         "line is the compact headline")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the rank launcher, the strong-scaling deal and the result all_gather "
                          "over gloo with the CPU oracle standing in for the kernels (tests/test_multirank.py)")
     args = ap.parse_args()
+    # engine defaults (tools/sweep_residency.sh): engine 1 -- 6 x 2048 groups in flight, 48 per CU;
+    # engine 0 -- 6 x 768 waves, 18 per CU (round 2)
+    if not args.workers:
+        args.workers = 2048 if args.engine == 1 else 768
+    if not args.residency:
+        args.residency = 48 if args.engine == 1 else 18
 
     from python_motion_planning_amd import shard
 
@@ -1220,7 +1529,8 @@ def main():
         mine = np.arange(args.nq)
     nq = len(starts)
     W, H = occ.shape
-    L = _lib.load_library()
+    L = count_launches(_lib.load_library())
+    _LABEL[0] = "astar2d_c2"
     occ_bits = batch.occ_bits_device(occ, torch)
     s_d = torch.as_tensor(starts, device="cuda")
     g_d = torch.as_tensor(goals, device="cuda")
@@ -1229,6 +1539,7 @@ def main():
     lanes = []
     for _ in range(S):
         ctx = L.pmp_create(torch.cuda.current_device())
+        _lib.check(ctx, L.pmp_astar2d_set_engine(ctx, args.engine, args.t2lds), "engine")
         _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, args.workers, 0), "reserve")
         _lib.check(ctx, L.pmp_astar2d_set_schedule(ctx, 1 if args.schedule == "lpt" else 0), "schedule")
         _lib.check(ctx, L.pmp_astar2d_set_priority(ctx, args.prio), "priority")
@@ -1265,6 +1576,10 @@ def main():
         assert (st == 0).all(), f"unexpected statuses {np.unique(st)}"
         assert torch.equal(b["cost"], cost)
     bytes_per_launch = astar_algorithmic_bytes(counters)
+    ref_out = {k: lanes[0][k].clone() for k in ("cost", "plen", "nexp", "status")}
+    for b in lanes:
+        poison([b["cost"], b["plen"], b["nexp"], b["status"]])
+    torch.cuda.synchronize()
 
     # timed region.  kernel_ms = HIP events on each launch's own stream: with several batches in
     # flight this includes the time a dispatch waits for CUs held by the other streams' persistent
@@ -1295,6 +1610,7 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     sp = spans.cpu().numpy().view(np.uint64)
     span_ms = float(np.mean((sp[:, 1] - sp[:, 0]).astype(np.float64)) / khz.value)
+    timed_checked = check_timed("astar2d", ref_out, lanes[: min(S, args.steps)])
     elapsed, kern_ms, span_ms = shard.max_over_ranks(dist, [elapsed, kern_ms, span_ms], "cuda")
 
     plans = (args.nq if args.scaling == "strong" else nq * world) * args.steps
@@ -1313,7 +1629,7 @@ def main():
 
     # the headline's scratch (about 30 GB per batch in flight) is not needed by the other legs
     torch.cuda.synchronize()
-    cost = cost.cpu()
+    cost = ref_out["cost"].cpu()
     for b in lanes:
         L.pmp_destroy(b["ctx"])
     lanes.clear()
@@ -1339,14 +1655,18 @@ def main():
                          f"queries on every core of the affinity mask, {dt:.1f} s wall",
                "one_core": {"value": len(sub) / dt1, "sample": f"every 32nd pair ({len(sub)}), {dt1:.1f} s"}}
 
+    _LABEL[0] = "setup"
     legs = [x for x in args.legs.split(",") if x and x != "none"]
     secondary = {}
     if "dwa" in legs:
         secondary["mpc_sampled_dwa"] = control_leg(args, torch, dist, world, rank)
     if "rrt" in legs:
-        secondary["rrt_star"] = rrt_leg(args, torch, dist, world, rank)
+        with leg_label("rrt_star"):
+            secondary["rrt_star"] = rrt_leg(args, torch, dist, world, rank)
     if "astar3d" in legs:
         secondary["astar3d"] = astar3d_leg(args, torch, dist, world, rank)
+        if secondary["astar3d"].get("trajectory"):
+            secondary["totp3d"] = secondary["astar3d"].pop("trajectory")
     if "lqr" in legs:
         secondary["lqr"] = track_leg(args, torch, dist, world, rank, "lqr")
     if "mpc" in legs:
@@ -1385,7 +1705,7 @@ def main():
                                       # the batches in flight overlap: bytes of one batch per step interval
                                       "achieved_aggregate": bytes_per_launch / (elapsed / args.steps) / 1e9,
                                       "frac_aggregate": bytes_per_launch / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS},
-                                     "astar2d_kernel"),
+                                     "astar2d_kernel", "astar2d_c2"),
             "cpu_baseline": cpu,
             "secondary": secondary,
             "detail": {"kernel_ms_per_launch": kern_ms,
@@ -1399,11 +1719,17 @@ def main():
                        "max_heap_entries": int(counters[:, 3].max()),
                        "expansions_all_ranks_per_step": int(counters_all[:, 2].sum()) if args.scaling == "strong" else None,
                        "strong_scaling_gather": gathered,
-                       "workers": args.workers, "streams": S, "priority_queries": args.prio,
-                       "resident_per_cu": args.residency or (args.workers + 255) // 256,
-                       "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
+                       "engine": "multi-query (4 per wave, astar2d_mq.hip)" if args.engine == 1 else
+                                 "one query per wave (astar2d.hip)", "t2_lds": args.t2lds,
+                       "queries_in_flight_per_launch": args.workers, "streams": S, "priority_queries": args.prio,
+                       "resident_per_cu": args.residency,
+                       "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                       "timed_launches_checked": timed_checked},
+            "launch_manifest": _MANIFEST,
         }
-        print(json.dumps(out), flush=True)
+        path = write_detail(args, out)
+        line = json.dumps(headline_line(out, path))
+        print(line, flush=True)
     if dist:
         dist.destroy_process_group()
 

@@ -458,13 +458,23 @@ int pmp_astar2d_set_schedule(pmp_ctx* ctx, int longest_first);
  * priority, so they finish sooner and the short queries fill the issue slots they leave idle.
  * Default 64; 0 switches it off.  Results are identical for any value. */
 int pmp_astar2d_set_priority(pmp_ctx* ctx, int n_high);
-/* A* 2D workers resident per CU across all the launches that run at once (default 0 = this
- * context's own launch alone: ceil(max_slots / 256) of pmp_astar2d_reserve).  The LDS share of each
- * worker's heap is 160 KiB / per_cu, so several batches in flight with fewer workers each (e.g. 6
- * contexts x 512 workers) set 12 here to stay resident together: every batch's longest queries then
- * start at once instead of behind the earlier batches.  Re-sizes the reserved scratch (call after
- * pmp_astar2d_reserve).  Results are identical for any value. */
+/* A* 2D queries resident per CU across all the launches that run at once, in [0, 128] (default 0 =
+ * this context's own launch alone: ceil(max_slots / 256) of pmp_astar2d_reserve).  The LDS share of
+ * each query's heap is 160 KiB / per_cu, so several batches in flight with fewer queries each (e.g.
+ * 6 contexts x 2048 queries on the multi-query engine) set 48 here to stay resident together: every
+ * batch's longest queries then start at once instead of behind the earlier batches.  A share too
+ * small for the engine's fixed LDS needs is refused (PMP_EINVAL).  Re-sizes the reserved scratch
+ * (call after pmp_astar2d_reserve).  Results are identical for any accepted value. */
 int pmp_astar2d_set_residency(pmp_ctx* ctx, int per_cu);
+
+/* A* 2D engine of the context (replaces nothing in the reference: a scheduling knob of
+ * AStar.plan / Dijkstra.plan / GBFS.plan, a_star.py:39-83).  engine 1 (default): four queries per
+ * wave, one per 16-lane row, for A* / Dijkstra / GBFS whose heaps stay within 32,767 entries (a
+ * query that outgrows it reports PMP_CAP_OVERFLOW; re-reserving with a larger heap_cap selects
+ * engine 0); t2_lds = keep its level-10..14 heap direction bits in LDS (1) or HBM (0).  engine 0:
+ * one query per wave (also Theta* / Lazy Theta*, and heaps of any size).  Results are identical.
+ * Applies to the next launch (re-reserves the scratch geometry when one is set). */
+int pmp_astar2d_set_engine(pmp_ctx* ctx, int engine, int t2_lds);
 
 /* Persistent workers (one wave each) per CU of the one-wave-per-query planners: pmp_graph3d_batch,
  * pmp_dstar2d_batch / pmp_dstar2d_onpress_batch, pmp_dstar3d_batch and pmp_lpastar3d_batch (default 16

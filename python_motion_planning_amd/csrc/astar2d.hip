@@ -972,8 +972,9 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
 // ---- longest-first schedule: counting sort of the queries by descending start-goal distance ----
 __device__ __forceinline__ int lpt_key(const int32_t* s, const int32_t* g, int q)
 {
-    const int dx = s[2 * q] - g[2 * q], dy = s[2 * q + 1] - g[2 * q + 1];
-    return (int)__dsqrt_rn((double)dx * dx + (double)dy * dy);  // expansions grow ~ with distance^2
+    const double dx = (double)s[2 * q] - g[2 * q], dy = (double)s[2 * q + 1] - g[2 * q + 1];
+    const double d = __dsqrt_rn(dx * dx + dy * dy);  // expansions grow ~ with distance^2
+    return d < 2147483647.0 ? (int)d : 2147483647;  // callers clamp to the histogram's last bin
 }
 
 __global__ void lpt_hist(const int32_t* s, const int32_t* g, int nq, int nb, int* hist)
@@ -1004,9 +1005,9 @@ int default_workers() { return 256 * 4; }
 int default_lds_cap(int workers_per_cu)
 {
     // 160 KiB LDS per CU shared by the resident workers: the direction-bit blocks, then 12 B per
-    // heap entry; keep a little slack
+    // heap entry; keep a little slack (< 16: the share is too small, the caller refuses)
     int bytes = (160 * 1024) / workers_per_cu - 256 - kBitsLdsBytes;
-    return (bytes / 12) & ~15;
+    return bytes < 16 * 12 ? 0 : (bytes / 12) & ~15;
 }
 // HBM words of the direction-bit tiers >= 3 for heaps of up to heap_cap entries
 size_t hbits_words(int heap_cap)
@@ -1028,8 +1029,27 @@ int default_heap_cap(int W, int H)
 // per-context scratch budget: workers are reduced to fit (heap spill + cell state + G per worker)
 constexpr size_t kScratchBudget = (size_t)64 << 30;
 
+// longest-first order of a batch in the context's SCR_PDIR scratch (counting sort, descending
+// start-goal distance)
+int lpt_order2d(pmp_ctx* ctx, hipStream_t s, const int32_t* start_xy, const int32_t* goal_xy, int nq, int W, int H,
+                int32_t** order)
+{
+    const int nb = (int)ceil(sqrt((double)W * W + (double)H * H)) + 1;
+    int* hist = (int*)pmp_scratch(ctx, SCR_PDIR, sizeof(int) * ((size_t)nb + (size_t)nq));
+    if (!hist) return PMP_ENOMEM;
+    *order = hist + nb;
+    PMP_HIP_CHECK(ctx, hipMemsetAsync(hist, 0, sizeof(int) * (size_t)nb, s));
+    hipLaunchKernelGGL(lpt_hist, dim3((nq + 255) / 256), dim3(256), 0, s, start_xy, goal_xy, nq, nb, hist);
+    hipLaunchKernelGGL(lpt_scan, dim3(1), dim3(64), 0, s, nb, hist);
+    hipLaunchKernelGGL(lpt_scatter, dim3((nq + 255) / 256), dim3(256), 0, s, start_xy, goal_xy, nq, nb, hist, *order);
+    return PMP_OK;
+}
+
 }  // namespace
 
+// The multi-query engine (astar2d_mq.hip) serves A* / Dijkstra / GBFS when the context selects it
+// and the reserved heap capacity fits its limit (a query that outgrows it is re-run by the host with
+// the full bound, which selects this file's engine).
 extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int workers, int heap_cap)
 {
     if (!ctx) return PMP_EINVAL;
@@ -1037,6 +1057,29 @@ extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int workers, int 
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_reserve: bad dims/workers");
     if (heap_cap <= 0) heap_cap = default_heap_cap(W, H);
     if ((size_t)heap_cap > max_heap(W, H)) heap_cap = (int)max_heap(W, H);
+    if (ctx->astar_engine == 1 && heap_cap <= 65536 && heap_cap > pmp_astar2d_mq_cap())
+        heap_cap = pmp_astar2d_mq_cap();  // the default capacity on the multi-query engine
+    if (ctx->astar_engine == 1 && heap_cap <= pmp_astar2d_mq_cap()) {
+        // workers = queries in flight (16-lane groups, 4 per wave); scratch is taken at launch
+        const size_t per_slot = (size_t)W * H * 9 + (size_t)pmp_astar2d_mq_cap() * 16 + 4096 + 256;
+        const size_t fit = kScratchBudget / per_slot;
+        if (fit < 4) return pmp_set_err(ctx, PMP_ENOMEM, "pmp_astar2d_reserve: one wave exceeds the scratch budget");
+        if ((size_t)workers > fit) workers = (int)(fit & ~(size_t)3);
+        const int per_cu = ctx->astar_resident_per_cu > 0 ? ctx->astar_resident_per_cu : (workers + 255) / 256;
+        int lds_cap = pmp_astar2d_mq_lds_cap(per_cu, ctx->astar_mq_t2lds != 0);
+        if (lds_cap > heap_cap) lds_cap = (heap_cap + 15) & ~15;
+        if (lds_cap < 16)
+            return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_reserve: residency leaves no LDS heap share");
+        if (!pmp_scratch(ctx, SCR_AUX0, 256)) return PMP_ENOMEM;
+        ctx->astar_W = W;
+        ctx->astar_H = H;
+        ctx->astar_workers = workers;
+        ctx->astar_heap_cap = heap_cap;
+        ctx->astar_lds_cap = lds_cap;
+        ctx->astar_reserved_mq = 1;
+        return PMP_OK;
+    }
+    ctx->astar_reserved_mq = 0;
     const size_t ncell = (size_t)W * H;
     const size_t cst_words = ((ncell + 7) / 8 + 3) & ~(size_t)3;
     {
@@ -1047,6 +1090,8 @@ extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int workers, int 
     }
     const int per_cu = ctx->astar_resident_per_cu > 0 ? ctx->astar_resident_per_cu : (workers + 255) / 256;
     int lds_cap = default_lds_cap(per_cu < 1 ? 1 : per_cu);
+    if (lds_cap < 16)  // the share cannot hold the bit blocks and a minimal heap: refuse, never wrap
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_reserve: residency leaves no LDS heap share (one query per wave)");
     if (lds_cap > heap_cap) lds_cap = (heap_cap + 15) & ~15;
     const size_t spill = heap_cap > lds_cap ? (size_t)(heap_cap - lds_cap) : 0;
     if (!pmp_scratch(ctx, SCR_HEAP, (size_t)workers * spill * 16 + 16)) return PMP_ENOMEM;
@@ -1062,10 +1107,23 @@ extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int workers, int 
     return PMP_OK;
 }
 
+extern "C" int pmp_astar2d_set_engine(pmp_ctx* ctx, int engine, int t2_lds)
+{
+    if (!ctx) return PMP_EINVAL;
+    if (engine != 0 && engine != 1)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_set_engine: engine must be 0 (one query per wave) or 1 (multi-query)");
+    ctx->astar_engine = engine;
+    ctx->astar_mq_t2lds = t2_lds ? 1 : 0;
+    if (ctx->astar_W == 0) return PMP_OK;
+    return pmp_astar2d_reserve(ctx, ctx->astar_W, ctx->astar_H, ctx->astar_workers, 0);
+}
+
 extern "C" int pmp_astar2d_set_residency(pmp_ctx* ctx, int per_cu)
 {
     if (!ctx) return PMP_EINVAL;
-    if (per_cu < 0 || per_cu > 32) return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_set_residency: per_cu must be in [0, 32]");
+    // queries resident per CU: at most 32 one-query waves, or 128 queries of 32 four-query waves
+    if (per_cu < 0 || per_cu > 128)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_set_residency: per_cu must be in [0, 128]");
     ctx->astar_resident_per_cu = per_cu;
     if (ctx->astar_W == 0) return PMP_OK;  // applied by the next reserve
     return pmp_astar2d_reserve(ctx, ctx->astar_W, ctx->astar_H, ctx->astar_workers, ctx->astar_heap_cap);
@@ -1094,9 +1152,32 @@ extern "C" int pmp_graph2d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_batch: null pointer argument");
     PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     if (!(ctx->astar_W == W && ctx->astar_H == H)) {
-        int workers = default_workers();
+        int workers = ctx->astar_engine == 1 ? 4 * default_workers() : default_workers();
         if (workers > nq) workers = nq;
         int rc = pmp_astar2d_reserve(ctx, W, H, workers, 0);
+        if (rc) return rc;
+    }
+    if (!theta && ctx->astar_reserved_mq) {
+        const int groups = ctx->astar_workers < nq ? ctx->astar_workers : nq;
+        int* queue = (int*)ctx->buf[SCR_AUX0];
+        hipStream_t s = (hipStream_t)stream;
+        PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
+        int32_t* order = nullptr;
+        if (ctx->astar_lpt && nq > groups) {
+            const int rc = lpt_order2d(ctx, s, start_xy, goal_xy, nq, W, H, &order);
+            if (rc) return rc;
+        }
+        return pmp_astar2d_mq_launch(ctx, s, algo, occ_bits, W, H, heuristic, start_xy, goal_xy, order, nq, cost,
+                                     path_len, path, path_cap, n_expanded, expand, expand_cap, counters, status, queue);
+    }
+    if (ctx->astar_reserved_mq) {
+        // Theta* on a context reserved for the multi-query engine: this engine's scratch
+        const int e = ctx->astar_engine;
+        ctx->astar_engine = 0;
+        int workers = default_workers();
+        if (workers > nq) workers = nq;
+        const int rc = pmp_astar2d_reserve(ctx, W, H, workers, 0);
+        ctx->astar_engine = e;
         if (rc) return rc;
     }
     const int workers = ctx->astar_workers < nq ? ctx->astar_workers : nq;
@@ -1111,14 +1192,8 @@ extern "C" int pmp_graph2d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
     int32_t* order = nullptr;
     if (ctx->astar_lpt && nq > workers) {
-        const int nb = (int)ceil(sqrt((double)W * W + (double)H * H)) + 1;
-        int* hist = (int*)pmp_scratch(ctx, SCR_PDIR, sizeof(int) * ((size_t)nb + (size_t)nq));
-        if (!hist) return PMP_ENOMEM;
-        order = hist + nb;
-        PMP_HIP_CHECK(ctx, hipMemsetAsync(hist, 0, sizeof(int) * (size_t)nb, s));
-        hipLaunchKernelGGL(lpt_hist, dim3((nq + 255) / 256), dim3(256), 0, s, start_xy, goal_xy, nq, nb, hist);
-        hipLaunchKernelGGL(lpt_scan, dim3(1), dim3(64), 0, s, nb, hist);
-        hipLaunchKernelGGL(lpt_scatter, dim3((nq + 255) / 256), dim3(256), 0, s, start_xy, goal_xy, nq, nb, hist, order);
+        const int rc = lpt_order2d(ctx, s, start_xy, goal_xy, nq, W, H, &order);
+        if (rc) return rc;
     }
     uint32_t* par = nullptr;
     if (theta) {

@@ -1,0 +1,723 @@
+// Batched 2D A* (and Dijkstra / GBFS) for gfx950, several queries per wave: bit-exact with the
+// reference AStar.plan (global_planner/graph_search/a_star.py:39-83) including CPython heapq's tie
+// behaviour (Lib/heapq.py heappush/_siftdown, heappop/_siftup) under Node.__lt__
+// (utils/environment/node.py:51-54) -- the same algorithm as astar2d.hip, laid out differently.
+//
+// Why a second engine.  astar2d.hip runs one query per wave: every per-query value (heap size,
+// sift path, root, last) is wave-uniform and lives in SGPRs, so the heap walk is scalar code.  The
+// scalar unit is one per CU, shared by its 4 SIMDs, and the PMC issue breakdown of that kernel
+// (profiles/r2/pmc_astar2d_issue.txt: 129 SALU + 112 VALU per heap operation) puts it at ~90 % of
+// the per-SIMD scalar issue rate while the vector pipes idle at ~40 %.  Here a wave runs FOUR
+// queries, one per 16-lane DPP row ("group"); every per-query value lives in VGPRs (equal across
+// its row), so the walk, the compares and the placements are vector instructions serving four
+// queries at once, and the scalar unit only runs the loop.  Cross-lane traffic stays inside a row:
+// DPP row_newbcast (lane k of my row), DPP row_ror reductions, ds_bpermute for a variable lane, and
+// 16-bit slices of ballots.
+//
+// Per group (query) state, identical in its 16 lanes: the query, the heap size n, heap[0] (root)
+// and heap[n-1] (last) in registers, the pending pushes of the current expansion (a motion mask)
+// and the parents of the positions those pushes take (prefetched with the expansion).
+//
+// Heap storage per group: positions < lds_cap in LDS (f64 f[], u32 cm[] as SoA), the rest in a
+// per-group HBM spill (16 B entries) read and written through one buffer descriptor per wave;
+// CPython _siftup's child-choice ("direction") bits in 5-level blocks, tiers 0-1 in LDS and tier 2
+// (levels 10-14) in LDS (T2LDS) or HBM.  Heaps are limited to kMqCap entries (levels 0-14); a
+// query that outgrows it stops with PMP_CAP_OVERFLOW and the host re-runs it on astar2d.hip.
+//
+// Cell state: one byte per cell per group, (epoch << 4) | (parent motion + 1) for a CLOSED cell,
+// where the epoch (1..15) numbers the group's queries, so a new query needs no reset of the 1 MiB
+// array except every 15th query.  g of a CLOSED cell in a per-group f64 array (as astar2d.hip).
+#include "pmp_internal.h"
+
+namespace {
+
+constexpr double kSqrt2 = 1.4142135623730951;  // math.sqrt(2) == math.hypot(1, 1)
+constexpr int kMqCap = 32767;                   // positions 0..32766: levels 0..14
+constexpr int kBits01 = 144;                    // LDS bytes of bit tiers 0-1 (33 words) per group
+constexpr int kT2Words = 1024;                  // tier-2 bit blocks (levels 10-14) per group
+
+// motions in the order of env.py:52-55: (-1,0),(-1,1),(0,1),(1,1),(1,0),(1,-1),(0,-1),(-1,-1)
+constexpr uint32_t kMx1 = 0x1A90u, kMy1 = 0x01A9u;
+__device__ __forceinline__ int mot_x(int d) { return (int)((kMx1 >> (2 * d)) & 3u) - 1; }
+__device__ __forceinline__ int mot_y(int d) { return (int)((kMy1 >> (2 * d)) & 3u) - 1; }
+
+// HEUR: 0 euclidean, 1 manhattan (GraphSearcher.h, graph_search.py:41-44), 2 zero (Dijkstra)
+template <int HEUR>
+__device__ __forceinline__ uint32_t pack_cm(int dx, int dy, int dir)
+{
+    return ((uint32_t)dx << 18) | (((uint32_t)dy & 0x3FFFu) << 4) | (uint32_t)dir;
+}
+__device__ __forceinline__ int cm_dx(uint32_t cm) { return (int)cm >> 18; }
+__device__ __forceinline__ int cm_dy(uint32_t cm) { return (int)(cm << 14) >> 18; }
+__device__ __forceinline__ int cm_dir(uint32_t cm) { return (int)(cm & 15u); }
+template <int HEUR>
+__device__ __forceinline__ uint32_t hkey(uint32_t cm)
+{
+    if (HEUR == 2) return 0u;
+    const int dx = cm_dx(cm), dy = cm_dy(cm);
+    if (HEUR == 1) return (uint32_t)(abs(dx) + abs(dy));
+    return (uint32_t)(__mul24(dx, dx) + __mul24(dy, dy));
+}
+template <int HEUR>
+__device__ __forceinline__ double h_of_key(uint32_t hk)
+{
+    return HEUR == 2 ? 0.0 : (HEUR == 1 ? (double)hk : __dsqrt_rn((double)hk));
+}
+// Node.__lt__ (node.py:51-54)
+__device__ __forceinline__ bool key_lt(double fa, uint32_t ka, double fb, uint32_t kb)
+{
+    return (fa < fb) | ((fa == fb) & (ka < kb));
+}
+
+typedef __attribute__((address_space(3))) double lds_f64;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// ---- row (16-lane group) primitives ----------------------------------------------------------
+template <int K>
+__device__ __forceinline__ uint32_t bc(uint32_t v)  // lane K of my row
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + K, 0xF, 0xF, false);
+}
+template <int K>
+__device__ __forceinline__ int bci(int v) { return (int)bc<K>((uint32_t)v); }
+template <int K>
+__device__ __forceinline__ double bcf(double v)
+{
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    return __longlong_as_double(((uint64_t)bc<K>((uint32_t)(b >> 32)) << 32) | bc<K>((uint32_t)b));
+}
+__device__ __forceinline__ uint32_t ror_or(uint32_t v)  // OR over my row
+{
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xF, 0xF, false);
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xF, 0xF, false);
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);
+    return v;
+}
+// value of absolute lane `src` (same row), any src per lane
+__device__ __forceinline__ uint32_t bp(uint32_t v, int src) { return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v); }
+__device__ __forceinline__ double bpf(double v, int src)
+{
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    return __longlong_as_double(((uint64_t)bp((uint32_t)(b >> 32), src) << 32) | bp((uint32_t)b, src));
+}
+// my row's 16 bits of a ballot
+__device__ __forceinline__ uint32_t rbits(bool p, int gb) { return (uint32_t)(__ballot(p) >> gb) & 0xFFFFu; }
+
+// per lane: bit `lane` of mask ? a : b, as one v_cndmask (see astar2d.hip Ld::get)
+__device__ __forceinline__ uint32_t sel_lanes(uint64_t mask, uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"(mask));
+    return r;
+}
+__device__ __forceinline__ void ds_mskor(lds_u32* w, uint32_t mask, uint32_t val)
+{
+    asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"((uint32_t)(uintptr_t)w), "v"(mask), "v"(val) : "memory");
+}
+__device__ __forceinline__ void wave_sync_mem() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+// ---- heap storage of one group ------------------------------------------------------------------
+struct GHeap {
+    lds_f64* F;      // LDS f[cap]
+    lds_u32* C;      // LDS cm[cap]
+    lds_u32* B;      // LDS bit words: tier 0 (word 0), tier 1 (words 1..32)[, tier 2 (words 33..1056)]
+    uint32_t* T2;    // HBM tier-2 words (when not in LDS)
+    __amdgpu_buffer_rsrc_t spill;  // the wave's spill region (4 groups)
+    uint32_t soff;   // this group's byte offset in it
+    int cap;
+};
+constexpr uint32_t kOOR = 0x80000000u;  // a buffer offset beyond any spill region: loads 0, stores dropped
+
+struct Ld {
+    double fl;
+    uint32_t cl;
+    uint4 v;
+    bool in;
+    __device__ __forceinline__ void issue(const GHeap& h, int p)
+    {
+        in = p < h.cap;
+        const int pl = in ? p : 0;
+        const uint32_t off = in ? kOOR : h.soff + (uint32_t)(p - h.cap) * 16u;
+        v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(h.spill, off, 0, 0));
+        fl = h.F[pl];
+        cl = h.C[pl];
+    }
+    __device__ __forceinline__ void get(double& f, uint32_t& c) const
+    {
+        const uint64_t m = __ballot(in);
+        const uint64_t b = (uint64_t)__double_as_longlong(fl);
+        f = __hiloint2double((int)sel_lanes(m, (uint32_t)(b >> 32), v.y), (int)sel_lanes(m, (uint32_t)b, v.x));
+        c = sel_lanes(m, cl, v.z);
+    }
+};
+__device__ __forceinline__ void hst(const GHeap& h, bool on, int p, double f, uint32_t c)
+{
+    if (on && p < h.cap) {
+        h.F[p] = f;
+        h.C[p] = c;
+    }
+    const uint64_t b = (uint64_t)__double_as_longlong(f);
+    const uint4 v = make_uint4((uint32_t)b, (uint32_t)(b >> 32), c, 0u);
+    const uint32_t off = (on && p >= h.cap) ? h.soff + (uint32_t)(p - h.cap) * 16u : kOOR;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
+                                           h.spill, off, 0, 0);
+}
+
+// ---- direction bits (astar2d.hip: bit(p) = !(heap[2p+1] < heap[2p+2]) for nodes with two children,
+// 5-level blocks; node Pl (path number) at level L: tier t = L / 5, r = L - 5t, block root R = Pl >> r,
+// bit (Pl & (2^r - 1)) + 2^r - 1 of the block word)
+__device__ __forceinline__ uint32_t walk5(uint32_t w2)  // five steps from a block root, w2 = word << 1
+{
+    uint32_t pr = 1;
+#pragma unroll
+    for (int i = 0; i < 5; i++) pr = (pr << 1) | ((w2 >> pr) & 1u);
+    return pr;
+}
+template <bool T2LDS>
+__device__ __forceinline__ uint32_t t2_load(const GHeap& h, uint32_t R2)
+{
+    if (T2LDS) return h.B[33 + (R2 - 1024u)];
+    return __hip_atomic_load(h.T2 + (R2 - 1024u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// set (on lanes with `on`) the bit of node Pl at `level` to `bit`
+template <bool T2LDS>
+__device__ __forceinline__ void bit_set(const GHeap& h, bool on, int level, uint32_t Pl, bool bit)
+{
+    const int t = (int)((uint32_t)__mul24(level, 13) >> 6);  // level / 5 for level < 64
+    const int r = level - 5 * t;
+    const uint32_t mr = (1u << r) - 1u;
+    const uint32_t R = Pl >> r;
+    const uint32_t m = 1u << ((Pl & mr) + mr);
+    if (!on) return;
+    if (t == 0) {
+        ds_mskor(h.B, m, bit ? m : 0u);
+    } else if (t == 1) {
+        ds_mskor(h.B + (R - 31u), m, bit ? m : 0u);
+    } else if (T2LDS) {
+        ds_mskor(h.B + (33u + R - 1024u), m, bit ? m : 0u);
+    } else {
+        uint32_t* w = h.T2 + (R - 1024u);
+        if (bit) __hip_atomic_fetch_or(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else __hip_atomic_fetch_and(w, ~m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+// CPython _siftup's choice bit of the parent of `child` (a position) whose new content is v and
+// whose sibling holds s: bit = !(left < right), odd positions are left children
+template <int HEUR>
+__device__ __forceinline__ bool choice_bit(int child, double vf, uint32_t vc, double sf, uint32_t sc)
+{
+    const uint32_t vk = hkey<HEUR>(vc), sk = hkey<HEUR>(sc);
+    return (child & 1) ? !key_lt(vf, vk, sf, sk) : !key_lt(sf, sk, vf, vk);
+}
+
+// heappop on a group's heap of n (> 0, already decremented) entries whose old last element (in
+// registers) sits at position n; the old root has been taken.  Same steps as astar2d.hip
+// heap_pop, per row: the _siftup path from the bits, one load round (lane i in 1..K: heap[p_i],
+// heap[p_{i+1}], sibling(p_i); lane 0: heap[n - 1]), a popcount placing `last`, the stores and
+// the bit rewrites of p_0..p_{m-1}.
+template <bool T2LDS, int HEUR>
+__device__ __forceinline__ void heap_pop(const GHeap& h, int n, double& lastf, uint32_t& lastc, double& rootf,
+                                         uint32_t& rootc, int gl, int gb)
+{
+    const double lf = lastf;
+    const uint32_t lc = lastc;
+    // ---- the path: levels 0..D-1 are full; `full` = D - 1 unconditional steps, then the last step
+    const int D = 31 - __clz(n);
+    const int full = D - 1 < 0 ? 0 : D - 1;
+    const uint32_t w0 = h.B[0] << 1;
+    const uint32_t pr0 = walk5(w0);                 // level-5 node (32..63) along the tier-0 bits
+    uint32_t w1 = 0u, w2 = 0u, pr1 = 32u, pr2 = 32u;
+    if (full >= 5) {
+        w1 = h.B[pr0 - 31u] << 1;
+        pr1 = walk5(w1);
+    }
+    const uint32_t R2 = (pr0 << 5) + pr1 - 32u;     // level-10 node (1024..2047)
+    if (full >= 10) {
+        w2 = t2_load<T2LDS>(h, R2) << 1;
+        pr2 = walk5(w2);
+    }
+    const int tf = full >= 10 ? 2 : (full >= 5 ? 1 : 0);
+    const int rf = full - 5 * tf;
+    const uint32_t wt = tf == 2 ? w2 : (tf == 1 ? w1 : w0);
+    const uint32_t prt = tf == 2 ? pr2 : (tf == 1 ? pr1 : pr0);
+    const uint32_t Rt = tf == 2 ? R2 : (tf == 1 ? pr0 : 1u);
+    const uint32_t prel = prt >> (5 - rf);
+    uint32_t P = (Rt << rf) + prel - (1u << rf);
+    int K = D - 1 < 0 ? 0 : D - 1;
+    if (2u * P <= (uint32_t)n) {
+        const uint32_t c = (2u * P < (uint32_t)n) ? ((wt >> prel) & 1u) : 0u;
+        P = 2u * P + c;
+        K++;
+    }
+    // ---- one load round
+    const bool on = gl >= 1 && gl <= K;
+    const int sh = on ? K - gl : 0;
+    const int pi = on ? (int)(P >> sh) - 1 : (gl == 0 ? n - 1 : 0);
+    const bool hasb = on && gl < K;
+    const int pn = hasb ? (int)(P >> (sh - 1)) - 1 : 0;
+    const int si = ((pi - 1) ^ 1) + 1;
+    const bool hass = on && si < n;
+    double Af, Bf, Sf;
+    uint32_t Ac, Bc, Sc;
+    {
+        Ld la, lb, ls;
+        la.issue(h, pi);
+        lb.issue(h, pn);
+        ls.issue(h, hass ? si : 0);
+        la.get(Af, Ac);
+        lb.get(Bf, Bc);
+        ls.get(Sf, Sc);
+    }
+    // ---- movers: the path prefix with !(last < heap[p_i])
+    const int m = __popc(rbits(on && !key_lt(lf, hkey<HEUR>(lc), Af, hkey<HEUR>(Ac)), gb));
+    {
+        const bool l0 = gl == 0;
+        const bool st = l0 || (on && gl <= m);
+        const int dst = (int)(P >> (l0 ? K - m : sh + 1)) - 1;
+        hst(h, st, dst, l0 ? lf : Af, l0 ? lc : Ac);
+    }
+    const double a1f = bcf<1>(Af), a0f = bcf<0>(Af);
+    const uint32_t a1c = bc<1>(Ac), a0c = bc<0>(Ac);
+    rootf = m >= 1 ? a1f : lf;
+    rootc = m >= 1 ? a1c : lc;
+    if (!(m == K && P == (uint32_t)n)) {
+        lastf = a0f;
+        lastc = a0c;
+    }
+    // ---- bits of p_0 .. p_{m-1}
+    {
+        const bool useb = gl < m;
+        const bool bit = choice_bit<HEUR>(pi, useb ? Bf : lf, useb ? Bc : lc, Sf, Sc);
+        bit_set<T2LDS>(h, hass && gl <= m, gl - 1, P >> (sh + 1), bit);
+    }
+    wave_sync_mem();
+}
+
+// heappush (_siftdown) of `it` onto a group's heap of n entries: ancestors a_j = parent^j(n) in
+// one round (lane j), a popcount t of the ancestors that move down, the stores, the bits of
+// a_1..a_{t+1}.  Returns t; a1 = the new heap[parent(n)].
+template <bool T2LDS, int HEUR>
+__device__ __forceinline__ int heap_push(const GHeap& h, int n, double itf, uint32_t itc, uint32_t itk, double& lastf,
+                                         uint32_t& lastc, double& rootf, uint32_t& rootc, int gl, int gb, double& a1f,
+                                         uint32_t& a1c)
+{
+    const uint32_t np1 = (uint32_t)n + 1u;
+    const int D = 31 - __clz((int)np1);  // depth of position n
+    const bool on = gl >= 1 && gl <= D;
+    const int l1 = on ? gl : 1;
+    const int aj = (int)(np1 >> l1) - 1;
+    const int x = (int)(np1 >> (l1 - 1)) - 1;
+    const int sx = ((x - 1) ^ 1) + 1;
+    const bool hass = on && sx < n;
+    double Af, Sf;
+    uint32_t Ac, Sc;
+    {
+        Ld la, ls;
+        la.issue(h, on ? aj : 0);
+        ls.issue(h, hass ? sx : 0);
+        la.get(Af, Ac);
+        ls.get(Sf, Sc);
+    }
+    const int t = __popc(rbits(on && key_lt(itf, itk, Af, hkey<HEUR>(Ac)), gb));
+    const int ipos = (int)(np1 >> t) - 1;
+    const double A1f = bcf<1>(Af), A2f = bcf<2>(Af);
+    const uint32_t A1c = bc<1>(Ac), A2c = bc<2>(Ac);
+    a1f = t >= 2 ? A2f : itf;
+    a1c = t >= 2 ? A2c : itc;
+    {
+        const bool l0 = gl == 0;
+        const bool st = l0 || (on && gl <= t);
+        hst(h, st, l0 ? ipos : x, l0 ? itf : Af, l0 ? itc : Ac);
+    }
+    if (ipos == 0) {
+        rootf = itf;
+        rootc = itc;
+    }
+    lastf = t == 0 ? itf : A1f;
+    lastc = t == 0 ? itc : A1c;
+    {
+        const bool usea = gl - 1 < t;
+        const bool bit = choice_bit<HEUR>(x, usea ? Af : itf, usea ? Ac : itc, Sf, Sc);
+        bit_set<T2LDS>(h, hass && gl <= t + 1, D - l1, np1 >> l1, bit);
+    }
+    wave_sync_mem();
+    return t;
+}
+
+// one byte per cell: (epoch << 4) | (motion + 1) for a cell CLOSED during query `epoch`
+__device__ __forceinline__ bool closed_byte(uint32_t b, uint32_t ep) { return (b >> 4) == ep && (b & 15u) != 0u; }
+
+// GZERO: GBFS (gbfs.py:73-75) -- every pushed node has g = 0, f = h.
+template <int HEUR, bool GZERO, bool T2LDS>
+__global__ __launch_bounds__(64) void astar2d_mq_kernel(
+    const uint32_t* __restrict__ occ, int W, int H, const int32_t* __restrict__ start_xy,
+    const int32_t* __restrict__ goal_xy, const int32_t* __restrict__ order, int nq, double* __restrict__ cost_out,
+    int32_t* __restrict__ path_len_out, uint32_t* __restrict__ path_out, int path_cap,
+    int32_t* __restrict__ nexp_out, uint32_t* __restrict__ expand_out, int expand_cap,
+    int64_t* __restrict__ counters, int32_t* __restrict__ status_out, int* __restrict__ queue,
+    uint4* __restrict__ spill_all, int spill_n, int heap_cap, int lds_cap, int region, uint8_t* __restrict__ cst_all,
+    size_t cst_bytes, double* __restrict__ G_all, uint32_t* __restrict__ t2_all, uint32_t* __restrict__ epoch_all,
+    int prio_n, unsigned long long* __restrict__ span)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = lane_id();
+    const int gl = lane & 15, gb = lane & 48, grp = lane >> 4;
+    const size_t slot = (size_t)blockIdx.x * 4u + (size_t)grp;
+    span_begin(span);
+    GHeap hp;
+    {
+        unsigned char* base = smem + (size_t)grp * (size_t)region;
+        hp.B = (lds_u32*)base;
+        const int bits_b = T2LDS ? kBits01 + 4 * kT2Words : kBits01;
+        hp.F = (lds_f64*)(base + bits_b);
+        hp.C = (lds_u32*)(base + bits_b + (size_t)8 * lds_cap);
+        hp.T2 = t2_all + slot * kT2Words;
+        hp.spill = __builtin_amdgcn_make_buffer_rsrc(spill_all + (size_t)blockIdx.x * 4u * (size_t)spill_n, 0,
+                                                     (int)(4u * (uint32_t)spill_n * 16u), 0x00020000);
+        hp.soff = (uint32_t)grp * (uint32_t)spill_n * 16u;
+        hp.cap = lds_cap;
+    }
+    uint8_t* cst = cst_all + slot * cst_bytes;
+    double* G = G_all + slot * ((size_t)W * (size_t)H);
+
+    // per-lane constants: lane m < 8 of a row is motion m (offset, cost, isCollision's cells)
+    const int mo = gl & 7;
+    const int mx = mot_x(mo), my = mot_y(mo);
+    const double mcost = GZERO ? 0.0 : ((mo & 1) ? kSqrt2 : 1.0);
+    uint32_t need = 16u | (1u << ((mx + 1) * 3 + (my + 1)));
+    if (mo & 1) need |= (1u << (3 + (my + 1))) | (1u << ((mx + 1) * 3 + 1));
+    const uint32_t self_bit = 1u << ((mx + 1) * 3 + (my + 1));
+    // the 3x3 round: lanes 0..8 occupancy of cell (x + i/3 - 1, y + i%3 - 1); lanes 9..11 the
+    // cell-state bytes of row i - 9; lane 12 G[parent]
+    const int blk_dx = gl < 9 ? gl / 3 - 1 : (gl < 12 ? gl - 10 : 0);
+    const int blk_dy = gl < 9 ? gl % 3 - 1 : 0;
+
+    // group state (equal across the row)
+    uint32_t ep = epoch_all[slot];
+    bool need_q = true, done = false;
+    int q = 0, qi = 0, sx = 0, sy = 0, gx = 0, gy = 0;
+    int n = 0, nexp = 0, maxn = 0, n0 = 0;
+    int64_t npush = 0, npop = 0;
+    double rootf = 0.0, lastf = 0.0;
+    uint32_t rootc = 0u, lastc = 0u;
+    uint32_t pend = 0u;     // pending pushes of the current expansion (motion mask)
+    bool pc_ok = false;     // parents of n0 .. n0 + 7 held by lanes 0..7 (pf8, pc8)
+    double pf8 = 0.0, ifv = 0.0;
+    uint32_t pc8 = 0u, icm = 0u;
+    Ld pld;
+    pld.in = true;
+    pld.fl = 0.0;
+    pld.cl = 0u;
+    pld.v = make_uint4(0u, 0u, 0u, 0u);
+
+    for (;;) {
+        // ---- groups without a query take the next one (or retire)
+        const bool fetch_any = __ballot(need_q && !done) != 0ull;
+        if (need_q && !done) {
+            int v = 0;
+            if (gl == 0) v = atomicAdd(queue, 1);
+            qi = bci<0>(v);
+            if (qi >= nq) {
+                done = true;
+            } else {
+                q = order ? order[qi] : qi;
+                sx = start_xy[2 * q];
+                sy = start_xy[2 * q + 1];
+                gx = goal_xy[2 * q];
+                gy = goal_xy[2 * q + 1];
+                const bool s_in = (unsigned)sx < (unsigned)W && (unsigned)sy < (unsigned)H;
+                const bool g_in = (unsigned)gx < (unsigned)W && (unsigned)gy < (unsigned)H;
+                if (!s_in || !g_in) {  // outside the grid: blocked -> no neighbours -> no path
+                    if (gl == 0) {
+                        status_out[q] = PMP_NO_PATH;
+                        cost_out[q] = 0.0;
+                        path_len_out[q] = 0;
+                        nexp_out[q] = s_in ? 1 : 0;
+                        if (counters) {
+                            counters[4 * q] = 1; counters[4 * q + 1] = 1;
+                            counters[4 * q + 2] = s_in ? 1 : 0; counters[4 * q + 3] = 1;
+                        }
+                    }
+                } else {
+                    // next epoch; every 15th query (and a fresh slot, epoch 0) clears the cell states
+                    if (ep == 0u || ep >= 15u) {
+                        uint4* c4 = reinterpret_cast<uint4*>(cst);
+                        const size_t n4 = cst_bytes / 16;
+                        for (size_t i = gl; i < n4; i += 16) c4[i] = make_uint4(0u, 0u, 0u, 0u);
+                        ep = 1u;
+                    } else {
+                        ep++;
+                    }
+                    // heap[0] = Node(start, start, 0, 0), key (0, h = 0)
+                    rootf = 0.0;
+                    rootc = pack_cm<HEUR>(0, 0, 8);
+                    lastf = rootf;
+                    lastc = rootc;
+                    hst(hp, gl == 0, 0, rootf, rootc);
+                    n = 1;
+                    npush = 1;
+                    npop = 0;
+                    nexp = 0;
+                    maxn = 1;
+                    pend = 0u;
+                    pc_ok = false;
+                    need_q = false;
+                }
+            }
+            wave_sync_mem();
+        }
+        if (fetch_any) {
+            // the longest queries (first in the longest-first order) get issue priority
+            if (__ballot(!done && !need_q && qi < prio_n)) __builtin_amdgcn_s_setprio(3);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+        if (__ballot(!done) == 0ull) break;
+        const bool act = !done && !need_q;
+
+        // ---- heappop + expansion (a_star.py:53-82) for the groups with no pending push
+        int st = -1;  // >= 0: the query ends this iteration with this status
+        double goal_cost = 0.0;
+        int plen = 0;
+        const bool dopop = act && pend == 0u && n > 0;
+        if (act && pend == 0u && n == 0) st = PMP_NO_PATH;  // OPEN exhausted (a_star.py:83)
+        if (dopop) {
+            const uint32_t ncm = rootc;
+            npop++;
+            n -= 1;
+            const int ndir = cm_dir(ncm);
+            const int x = ndir == 8 ? sx : gx - cm_dx(ncm);
+            const int y = ndir == 8 ? sy : gy - cm_dy(ncm);
+            const uint32_t nlin = (uint32_t)x * (uint32_t)H + (uint32_t)y;
+            // the 3x3 round, issued before the LDS pop so the two overlap
+            uint32_t blk_w = 0u, blk_w2 = 0u;
+            int blk_sh = 0;
+            bool blk_in = false;
+            double gpar = 0.0;
+            {
+                const int cx = x + blk_dx, cy = y + blk_dy;
+                if (gl < 9) {
+                    blk_in = (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
+                    const uint32_t ci = blk_in ? (uint32_t)cx * (uint32_t)H + (uint32_t)cy : 0u;
+                    blk_sh = (int)(ci & 31u);
+                    blk_w = occ[ci >> 5];
+                } else if (gl < 12) {
+                    blk_in = (unsigned)cx < (unsigned)W;
+                    // bytes of (cx, y-1 .. y+1) inside the 8-byte window at a0 (4-aligned)
+                    const uint32_t lo = blk_in ? (uint32_t)cx * (uint32_t)H + (uint32_t)(y > 0 ? y - 1 : 0) : 0u;
+                    const uint32_t a0 = lo & ~3u;
+                    blk_sh = (int)((uint32_t)cx * (uint32_t)H + (uint32_t)y - 1u - a0);  // byte of cell y-1 (may be -1)
+                    const uint32_t* p32 = reinterpret_cast<const uint32_t*>(cst + a0);
+                    blk_w = p32[0];
+                    blk_w2 = p32[1];
+                } else if (gl == 12 && !GZERO && ndir < 8) {
+                    gpar = G[nlin - (uint32_t)(mot_x(ndir) * H + mot_y(ndir))];
+                }
+            }
+            if (n > 0) heap_pop<T2LDS, HEUR>(hp, n, lastf, lastc, rootf, rootc, gl, gb);
+            // 3x3 masks: bit k = cell (x + k/3 - 1, y + k%3 - 1)
+            const uint32_t occ9 = rbits(gl < 9 && (!blk_in || ((blk_w >> blk_sh) & 1u)), gb) & 0x1FFu;
+            uint32_t row = 0u;
+            if (gl >= 9 && gl < 12 && blk_in) {
+                const uint64_t win = ((uint64_t)blk_w2 << 32) | blk_w;
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const int cy = y - 1 + k;
+                    const int bo = blk_sh + k < 0 ? 0 : blk_sh + k;
+                    if ((unsigned)cy < (unsigned)H && closed_byte((uint32_t)(win >> (8 * bo)) & 0xFFu, ep)) row |= 1u << k;
+                }
+            }
+            const uint32_t cls9 = bc<9>(row) | (bc<10>(row) << 3) | (bc<11>(row) << 6);
+            const double gp = bcf<12>(gpar);
+            if (!(cls9 & 16u)) {  // node.current not in CLOSED (a_star.py:57-58)
+                const double gnode = (GZERO || ndir == 8) ? 0.0 : gp + ((ndir & 1) ? kSqrt2 : 1.0);
+                // CLOSED[node.current] = node (a_star.py:82)
+                if (gl == 0) cst[nlin] = (uint8_t)((ep << 4) | (uint32_t)(ndir + 1));
+                if (!GZERO && gl == 1) G[nlin] = gnode;
+                if (gl == 2 && expand_out && nexp < expand_cap)
+                    expand_out[(size_t)q * expand_cap + nexp] = nlin | ((uint32_t)ndir << 28);
+                nexp++;
+                if (x == gx && y == gy) {  // goal (a_star.py:61-64): extractPath, goal -> start
+                    st = PMP_FOUND;
+                    wave_sync_mem();
+                    if (gl == 0) {
+                        int cx = x, cy = y;
+                        double cost = 0.0;
+                        int len = 0;
+                        uint32_t* pth = path_out + (size_t)q * path_cap;
+                        for (;;) {
+                            const uint32_t li = (uint32_t)cx * (uint32_t)H + (uint32_t)cy;
+                            if (len < path_cap) pth[len] = li;
+                            len++;
+                            if (cx == sx && cy == sy) break;
+                            const int d = (int)(cst[li] & 15u) - 1;
+                            cost += (d & 1) ? kSqrt2 : 1.0;
+                            cx -= mot_x(d);
+                            cy -= mot_y(d);
+                        }
+                        goal_cost = cost;
+                        plen = len;
+                    }
+                } else {
+                    // getNeighbor in motion order; push the goal and stop (a_star.py:66-80)
+                    const int ndx = gx - x - mx, ndy = gy - y - my;
+                    const bool nb_ok = gl < 8 && (occ9 & need) == 0u && (cls9 & self_bit) == 0u;
+                    uint32_t vm = rbits(nb_ok, gb) & 0xFFu;
+                    const uint32_t gm = rbits(nb_ok && ndx == 0 && ndy == 0, gb) & 0xFFu;
+                    if (gm) vm &= (gm << 1) - 1u;
+                    const double ig = gnode + mcost;
+                    icm = pack_cm<HEUR>(ndx, ndy, mo);
+                    ifv = ig + h_of_key<HEUR>(hkey<HEUR>(icm));
+                    pend = vm;
+                    // the parents of the positions the pushes take (n .. n + 7), one round, valid
+                    // while those positions share a depth (astar2d.hip)
+                    n0 = n;
+                    pc_ok = vm != 0u && n > 0 && (31 - __clz(n + 1)) == (31 - __clz(n + 8));
+                    if (pc_ok) pld.issue(hp, gl < 8 ? ((n + gl - 1) >> 1) : 0);
+                }
+            }
+        }
+
+        // ---- one push per group with pending pushes (not in the iteration that expanded)
+        const bool dopush = act && !dopop && pend != 0u;
+        if (dopush) {
+            const int m = __ffs((int)pend) - 1;
+            pend &= pend - 1u;
+            if (n >= heap_cap) {
+                st = PMP_CAP_OVERFLOW;
+            } else {
+                const double itf = bpf(ifv, gb + m);
+                const uint32_t itc = bp(icm, gb + m);
+                const uint32_t itk = hkey<HEUR>(itc);
+                double pf, dummyf;
+                uint32_t pc, dummyc;
+                pld.get(dummyf, dummyc);
+                pf8 = dummyf;
+                pc8 = dummyc;
+                pf = bpf(pf8, gb + (n - n0));
+                pc = bp(pc8, gb + (n - n0));
+                if (pc_ok && !key_lt(itf, itk, pf, hkey<HEUR>(pc))) {
+                    // trivial push: heap[n] = item; a right child sets its parent's bit against
+                    // its left sibling heap[n - 1] = last
+                    const uint32_t np1 = (uint32_t)n + 1u;
+                    bit_set<T2LDS>(hp, gl == 0 && (n & 1) == 0, 30 - __clz(n + 1), np1 >> 1,
+                                   !key_lt(lastf, hkey<HEUR>(lastc), itf, itk));
+                    hst(hp, gl == 0, n, itf, itc);
+                    lastf = itf;
+                    lastc = itc;
+                    wave_sync_mem();
+                } else {
+                    double a1f;
+                    uint32_t a1c;
+                    heap_push<T2LDS, HEUR>(hp, n, itf, itc, itk, lastf, lastc, rootf, rootc, gl, gb, a1f, a1c);
+                    // a left child's right sibling (the next position) has the same parent, now a1
+                    if (pc_ok && (n & 1) && gl == n - n0 + 1) {
+                        pld.fl = a1f;
+                        pld.cl = a1c;
+                        pld.in = true;
+                        pld.v = make_uint4(0u, 0u, 0u, 0u);
+                    }
+                }
+                n += 1;
+                npush++;
+                if (n > maxn) maxn = n;
+            }
+        }
+
+        // ---- the groups whose query ended: results, then a new query next iteration
+        if (st >= 0) {
+            if (gl == 0) {
+                int s = st;
+                if (s == PMP_FOUND && plen > path_cap) s = PMP_PATH_OVERFLOW;
+                status_out[q] = s;
+                cost_out[q] = st == PMP_FOUND ? goal_cost : 0.0;
+                path_len_out[q] = st == PMP_FOUND ? plen : 0;
+                nexp_out[q] = nexp;
+                if (counters) {
+                    counters[4 * q + 0] = npush;
+                    counters[4 * q + 1] = npop;
+                    counters[4 * q + 2] = nexp;
+                    counters[4 * q + 3] = maxn;
+                }
+            }
+            need_q = true;
+            pend = 0u;
+        }
+    }
+    if (gl == 0) epoch_all[slot] = ep;
+    span_end(span);
+}
+
+size_t mq_cst_bytes(int W, int H) { return (((size_t)W * H + 8 + 255) & ~(size_t)255); }
+
+}  // namespace
+
+// The multi-query engine's launch (called by pmp_graph2d_batch for A* / Dijkstra / GBFS when the
+// context's heap capacity fits kMqCap).  ctx->astar_workers = group slots (queries in flight) of
+// one launch; the LDS share per group comes from the residency (groups per CU over all launches in
+// flight).
+int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t* occ_bits, int W, int H, int heuristic,
+                          const int32_t* start_xy, const int32_t* goal_xy, const int32_t* order, int nq, double* cost,
+                          int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded, uint32_t* expand,
+                          int expand_cap, int64_t* counters, int32_t* status, int* queue)
+{
+    const int groups = ctx->astar_workers < nq ? ctx->astar_workers : nq;
+    const int waves = (groups + 3) / 4;
+    const int lds_cap = ctx->astar_lds_cap;
+    const bool t2lds = ctx->astar_mq_t2lds != 0;
+    const int bits_b = t2lds ? kBits01 + 4 * kT2Words : kBits01;
+    const int region = bits_b + 12 * lds_cap;
+    const int heap_cap = ctx->astar_heap_cap < kMqCap ? ctx->astar_heap_cap : kMqCap;
+    const int spill_n = heap_cap > lds_cap ? heap_cap - lds_cap : 1;
+    const size_t cst_bytes = mq_cst_bytes(W, H);
+    const size_t ncell = (size_t)W * H;
+    const size_t slots = (size_t)waves * 4;
+    uint4* spill = (uint4*)pmp_scratch(ctx, SCR_MQ_SPILL, slots * (size_t)spill_n * 16 + 16);
+    uint8_t* cstp = (uint8_t*)pmp_scratch(ctx, SCR_MQ_CST, slots * cst_bytes + 16);
+    double* G = (double*)pmp_scratch(ctx, SCR_MQ_G, slots * ncell * 8 + 16);
+    uint32_t* t2 = (uint32_t*)pmp_scratch(ctx, SCR_MQ_T2, slots * kT2Words * 4 + 16);
+    const bool fresh_epochs = ctx->cap[SCR_MQ_EPOCH] < slots * 4 || ctx->astar_mq_epoch_slots < slots ||
+                              ctx->astar_mq_cst_bytes != cst_bytes;
+    uint32_t* ep = (uint32_t*)pmp_scratch(ctx, SCR_MQ_EPOCH, slots * 4 + 16);
+    if (!spill || !cstp || !G || !t2 || !ep) return PMP_ENOMEM;
+    if (fresh_epochs) {  // new or re-laid-out cell-state arrays: every slot clears at its first query
+        PMP_HIP_CHECK(ctx, hipMemsetAsync(ep, 0, slots * 4 + 16, s));
+        ctx->astar_mq_epoch_slots = slots;
+        ctx->astar_mq_cst_bytes = cst_bytes;
+    }
+    const size_t lds = (size_t)region * 4;
+    const int prio = order ? ctx->astar_prio_n : 0;
+#define MQ_LAUNCH(HE, GZ, T2)                                                                                       \
+    hipLaunchKernelGGL((astar2d_mq_kernel<HE, GZ, T2>), dim3(waves), dim3(64), lds, s, occ_bits, W, H, start_xy,    \
+                       goal_xy, order, nq, cost, path_len, path, path_cap, n_expanded, expand, expand_cap, counters, \
+                       status, queue, spill, spill_n, heap_cap, lds_cap, region, cstp, cst_bytes, G, t2, ep, prio,   \
+                       ctx->span)
+    const int he = algo == PMP_ALGO_DIJKSTRA ? 2 : heuristic;
+    const bool gz = algo == PMP_ALGO_GBFS;
+    if (t2lds) {
+        if (gz) { if (he == 1) MQ_LAUNCH(1, true, true); else MQ_LAUNCH(0, true, true); }
+        else if (he == 2) MQ_LAUNCH(2, false, true);
+        else if (he == 1) MQ_LAUNCH(1, false, true);
+        else MQ_LAUNCH(0, false, true);
+    } else {
+        if (gz) { if (he == 1) MQ_LAUNCH(1, true, false); else MQ_LAUNCH(0, true, false); }
+        else if (he == 2) MQ_LAUNCH(2, false, false);
+        else if (he == 1) MQ_LAUNCH(1, false, false);
+        else MQ_LAUNCH(0, false, false);
+    }
+#undef MQ_LAUNCH
+    PMP_HIP_CHECK(ctx, hipGetLastError());
+    return PMP_OK;
+}
+
+// LDS heap positions per group for `per_cu` groups resident per CU (each CU's 160 KiB shared)
+int pmp_astar2d_mq_lds_cap(int per_cu, bool t2lds)
+{
+    const int bits_b = t2lds ? kBits01 + 4 * kT2Words : kBits01;
+    // a workgroup is one wave = 4 groups, and may hold at most the CU's 160 KiB
+    int bytes = (160 * 1024) / (per_cu < 4 ? 4 : per_cu) - 160 - bits_b;
+    int cap = (bytes / 12) & ~15;
+    if (cap > kMqCap) cap = kMqCap & ~15;
+    return cap;
+}
+int pmp_astar2d_mq_cap() { return kMqCap; }

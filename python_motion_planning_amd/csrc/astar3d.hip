@@ -466,8 +466,12 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
 // ---- longest-first schedule: counting sort of the queries by descending start-goal distance ----
 __device__ __forceinline__ int lpt3_key(const int32_t* s, const int32_t* g, int q)
 {
-    const int dx = s[3 * q] - g[3 * q], dy = s[3 * q + 1] - g[3 * q + 1], dz = s[3 * q + 2] - g[3 * q + 2];
-    return (int)__dsqrt_rn((double)(dx * dx + dy * dy + dz * dz));
+    // in double (endpoints may lie far outside the grid: the kernels report those queries, this
+    // pre-pass must only stay in range), clamped to the histogram [0, nb - 1] by the callers
+    const double dx = (double)s[3 * q] - g[3 * q], dy = (double)s[3 * q + 1] - g[3 * q + 1],
+                 dz = (double)s[3 * q + 2] - g[3 * q + 2];
+    const double d = __dsqrt_rn(dx * dx + dy * dy + dz * dz);
+    return d < 2147483647.0 ? (int)d : 2147483647;
 }
 __global__ void lpt3_hist(const int32_t* s, const int32_t* g, int nq, int nb, int* hist)
 {
@@ -539,9 +543,16 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     int workers = 256 * per_cu;
     if (workers > nq) workers = nq;
     const size_t words = (ncell + 31) / 32;
-    const bool occ_lds = words <= (size_t)kOccLdsWords;
-    const int occ_bytes = occ_lds ? kOccLdsWords * 4 : 0;
-    int lds_cap = (((160 * 1024) / pmp_lds_share(ctx, per_cu) - 256 - occ_bytes) / 16) & ~15;
+    bool occ_lds = words <= (size_t)kOccLdsWords;
+    int occ_bytes = occ_lds ? kOccLdsWords * 4 : 0;
+    int lds_cap = pmp_heap_lds_cap(ctx, per_cu, occ_bytes, 16);
+    if (lds_cap < kMinLdsHeap && occ_lds) {  // the LDS share cannot hold the occupancy too: keep it in HBM
+        occ_lds = false;
+        occ_bytes = 0;
+        lds_cap = pmp_heap_lds_cap(ctx, per_cu, 0, 16);
+    }
+    if (lds_cap < kMinLdsHeap)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_graph3d_batch: workers / resident per CU leave no LDS heap share");
     size_t hc = 26 * ncell + 8;
     if (hc > (size_t)(1 << 22)) hc = (size_t)1 << 22;
     const int heap_cap = (int)hc;

@@ -569,13 +569,20 @@ extern "C" int pmp_dstar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ
     PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     const size_t ncell = (size_t)X * Y * Z;
     const int words = (int)((ncell + 31) / 32);
-    const bool lds_occ = words <= kOccLdsWords;
+    bool lds_occ = words <= kOccLdsWords;
     const int per_cu = std::max(1, std::min(ctx->workers_per_cu > 0 ? ctx->workers_per_cu : 16, (nq + 255) / 256));
-    const int occ_bytes = lds_occ ? ((words * 4 + 15) & ~15) : 0;
+    int occ_bytes = lds_occ ? ((words * 4 + 15) & ~15) : 0;
     // heap: one valid element per OPEN voxel plus stale ones; 8 pushes per voxel bound the total
     const size_t hc = std::min<size_t>(8 * (ncell + 1) + 64, (size_t)1 << 26);
     const int heap_cap = (int)hc;
-    int lds_cap = (((160 * 1024) / pmp_lds_share(ctx, per_cu) - 256 - occ_bytes) / 16) & ~15;
+    int lds_cap = pmp_heap_lds_cap(ctx, per_cu, occ_bytes, 16);
+    if (lds_cap < kMinLdsHeap && lds_occ) {  // the LDS share cannot hold the occupancy too: keep it in HBM
+        lds_occ = false;
+        occ_bytes = 0;
+        lds_cap = pmp_heap_lds_cap(ctx, per_cu, 0, 16);
+    }
+    if (lds_cap < kMinLdsHeap)
+        return pmp_set_err(ctx, PMP_EINVAL, "pmp_dstar3d_batch: workers / resident per CU leave no LDS heap share");
     if (lds_cap > heap_cap) lds_cap = (heap_cap + 15) & ~15;
     const size_t spill_n = heap_cap > lds_cap ? (size_t)(heap_cap - lds_cap) : 0;
     const size_t per_worker = (ncell + 1) * sizeof(DC3) + spill_n * 16 + (lds_occ ? 0 : (size_t)words * 4) + 256;

@@ -82,14 +82,16 @@ int pmp_astar2d_set_priority(pmp_ctx* ctx, int n_high)
 
 int pmp_set_resident_per_cu(pmp_ctx* ctx, int per_cu)
 {
-    if (!ctx || per_cu < 0 || per_cu > 32) return PMP_EINVAL;
+    if (!ctx) return PMP_EINVAL;
+    if (per_cu < 0 || per_cu > 32) return pmp_set_err(ctx, PMP_EINVAL, "pmp_set_resident_per_cu: per_cu must be in [0, 32]");
     ctx->resident_per_cu = per_cu;
     return PMP_OK;
 }
 
 int pmp_set_workers_per_cu(pmp_ctx* ctx, int per_cu)
 {
-    if (!ctx || per_cu < 0 || per_cu > 32) return PMP_EINVAL;
+    if (!ctx) return PMP_EINVAL;
+    if (per_cu < 0 || per_cu > 32) return pmp_set_err(ctx, PMP_EINVAL, "pmp_set_workers_per_cu: per_cu must be in [0, 32]");
     ctx->workers_per_cu = per_cu;
     return PMP_OK;
 }

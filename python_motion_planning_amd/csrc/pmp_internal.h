@@ -24,17 +24,36 @@ struct pmp_ctx {
     // ... and the workers resident per CU over all concurrent launches, which sets their LDS share
     // (0 = this launch's own workers per CU; pmp_set_resident_per_cu)
     int resident_per_cu = 0;
+    // A* 2D engine: 1 = several queries per wave (astar2d_mq.hip) for A* / Dijkstra / GBFS whose heaps fit
+    // its capacity, 0 = one query per wave (astar2d.hip) always; the multi-query engine's tier-2
+    // direction bits in LDS (1) or HBM (0); the geometry its per-slot epochs were written for
+    int astar_engine = 1;
+    int astar_mq_t2lds = 0;
+    int astar_reserved_mq = 0;  // the current reservation (pmp_astar2d_reserve) is the multi-query engine's
+    size_t astar_mq_epoch_slots = 0, astar_mq_cst_bytes = 0;
     // grow-only scratch arena, one buffer per use
-    void* buf[11] = {nullptr};
-    size_t cap[11] = {0};
+    void* buf[16] = {nullptr};
+    size_t cap[16] = {0};
 };
 
 enum ScratchSlot { SCR_HEAP = 0, SCR_CLOSED = 1, SCR_PDIR = 2, SCR_G = 3, SCR_AUX0 = 4, SCR_AUX1 = 5, SCR_AUX2 = 6, SCR_AUX3 = 7,
-                   SCR_BITS = 8, SCR_AUX4 = 9, SCR_PAR = 10, SCR_NSLOTS = 11 };
+                   SCR_BITS = 8, SCR_AUX4 = 9, SCR_PAR = 10, SCR_MQ_SPILL = 11, SCR_MQ_CST = 12, SCR_MQ_G = 13,
+                   SCR_MQ_T2 = 14, SCR_MQ_EPOCH = 15, SCR_NSLOTS = 16 };
 
 int pmp_set_err(pmp_ctx* ctx, int code, const std::string& msg);
 // Workers per CU whose LDS shares a launch of `per_cu` workers per CU must fit beside
 inline int pmp_lds_share(const pmp_ctx* ctx, int per_cu) { return ctx->resident_per_cu > per_cu ? ctx->resident_per_cu : per_cu; }
+// Heap positions kept in LDS (a multiple of 16) when each of the `pmp_lds_share` workers of a CU
+// gets an equal share of its 160 KiB and `fixed_bytes` of that share hold other LDS data (occupancy
+// bits, ...).  Below kMinLdsHeap the share cannot hold the kernel's fixed LDS needs: the caller
+// moves the fixed data to HBM or refuses the launch (never a negative size: the dynamic LDS size
+// would wrap and the kernel would address outside its allocation).
+constexpr int kMinLdsHeap = 16;
+inline int pmp_heap_lds_cap(const pmp_ctx* ctx, int per_cu, int fixed_bytes, int entry_bytes)
+{
+    const int bytes = (160 * 1024) / pmp_lds_share(ctx, per_cu) - 256 - fixed_bytes;
+    return bytes < kMinLdsHeap * entry_bytes ? 0 : (bytes / entry_bytes) & ~15;
+}
 // Ensure scratch buffer `slot` holds at least `bytes`; returns device pointer or nullptr (error set).
 void* pmp_scratch(pmp_ctx* ctx, int slot, size_t bytes);
 
@@ -43,6 +62,14 @@ void* pmp_scratch(pmp_ctx* ctx, int slot, size_t bytes);
 // worker (nq <= workers).  Shared by the one-wave-per-query 3D planners (astar3d.hip).
 int pmp_lpt_order3d(pmp_ctx* ctx, hipStream_t s, const int32_t* start_xyz, const int32_t* goal_xyz, int nq, int X,
                     int Y, int Z, int workers, int32_t** order);
+
+// The multi-query A* 2D engine (astar2d_mq.hip), driven by pmp_graph2d_batch (astar2d.hip).
+int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t* occ_bits, int W, int H, int heuristic,
+                          const int32_t* start_xy, const int32_t* goal_xy, const int32_t* order, int nq, double* cost,
+                          int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded, uint32_t* expand,
+                          int expand_cap, int64_t* counters, int32_t* status, int* queue);
+int pmp_astar2d_mq_lds_cap(int per_cu, bool t2lds);
+int pmp_astar2d_mq_cap();
 
 #define PMP_HIP_CHECK(ctx, call)                                                                     \
     do {                                                                                             \

@@ -38,8 +38,11 @@ def launch_ranks(n: int, argv=None, extra_env=None) -> int:
     """Run `python <argv>` as n rank processes on this node (one per GPU) and wait for all of them.
 
     Called before anything touches the GPU.  Children inherit stdout/stderr, so rank 0's output is
-    the program's output.  Returns 0 when every rank exits 0, else the first failing exit code (a
-    failing rank makes the others' collectives fail too, so all of them end)."""
+    the program's output.  The children are polled: on the first non-zero exit the survivors (which
+    may be blocked in a collective waiting for the dead rank, up to the process-group timeout) are
+    terminated, and that exit code is returned; 0 when every rank exits 0."""
+    import time
+
     argv = list(sys.argv if argv is None else argv)
     port = str(_free_port())
     procs = []
@@ -50,9 +53,23 @@ def launch_ranks(n: int, argv=None, extra_env=None) -> int:
         if extra_env:
             env.update(extra_env)
         procs.append(subprocess.Popen([sys.executable] + argv, env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [c for c in rcs if c != 0]
-    return bad[0] if bad else 0
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [c for c in rcs if c is not None and c != 0]
+        if bad:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            return bad[0]
+        if all(c == 0 for c in rcs):
+            return 0
+        time.sleep(0.05)
 
 
 def init(backend: str = "nccl", always: bool = False):
@@ -158,16 +175,19 @@ def all_gather_rows(dist, idx, rows: dict, n: int, device="cpu") -> dict:
     return out
 
 
-def run_sharded(dist, plan_fn, starts, goals, device="cpu", work=None):
+def run_sharded(dist, plan_fn, starts, goals, device="cpu", work=None, per_query=None):
     """Strong-scaling split of ONE batch of queries over the ranks of `dist`, plus the result gather.
 
     Each rank takes its lpt_deal share of the queries (by octile distance unless `work` is given),
-    calls plan_fn(local_starts, local_goals) -> dict of [n_local, ...] tensors, and all ranks return
-    the full-batch records in the input order.  Equal to plan_fn(starts, goals) on one rank."""
+    calls plan_fn(local_starts, local_goals, **local_per_query) -> dict of [n_local, ...] tensors,
+    and all ranks return the full-batch records in the input order.  `per_query` holds further
+    per-query inputs (e.g. C5's per-query occupancy grids), sliced like the starts.  Equal to
+    plan_fn(starts, goals, **per_query) on one rank."""
     n = len(starts)
     world = dist.get_world_size() if dist is not None else 1
     rank = dist.get_rank() if dist is not None else 0
     w = octile(starts, goals) if work is None else work
     idx = lpt_deal(w, world, rank)
-    rows = plan_fn(np.asarray(starts)[idx], np.asarray(goals)[idx])
+    extra = {k: np.asarray(v)[idx] for k, v in (per_query or {}).items()}
+    rows = plan_fn(np.asarray(starts)[idx], np.asarray(goals)[idx], **extra)
     return all_gather_rows(dist, idx, rows, n, device)

@@ -17,6 +17,21 @@ def _pmp():
     return pmp
 
 
+# (engine, tier-2 bits in LDS): 1 = four queries per wave (astar2d_mq.hip, the default), 0 = one
+# query per wave (astar2d.hip); both must give the reference's answers bit for bit
+ENGINES = [(1, 0), (1, 1), (0, 0)]
+
+
+@pytest.fixture(params=ENGINES, ids=["mq", "mq_t2lds", "wave"])
+def engine(request):
+    from python_motion_planning_amd import _lib
+
+    L, ctx = _lib.load_library(), _lib.context()
+    _lib.check(ctx, L.pmp_astar2d_set_engine(ctx, *request.param), "engine")
+    yield request.param
+    _lib.check(ctx, L.pmp_astar2d_set_engine(ctx, 1, 0), "engine")
+
+
 def test_readme_dropin_class():
     pmp = _pmp()
     fx = load_json("astar_readme.json")
@@ -38,7 +53,7 @@ def test_readme_dropin_class():
     assert expand[0].current == (5, 5) and expand[0].parent == (5, 5) and expand[0].g == 0
 
 
-def test_small_grids_against_reference():
+def test_small_grids_against_reference(engine):
     from python_motion_planning_amd import batch
 
     for i, occ, z in grid_cases("astar_small.npz"):
@@ -60,7 +75,7 @@ def test_small_grids_against_reference():
         assert np.array_equal(e, seg(z["expand"], z["expand_off"], i)), i
 
 
-def test_c2_subset_against_reference():
+def test_c2_subset_against_reference(engine):
     from python_motion_planning_amd import batch, workloads as wl
 
     z = load_npz("astar_1024.npz")
@@ -119,7 +134,7 @@ def test_c2_full_batch_against_oracle_and_properties():
     assert (ctr[:, 2] == ne).all() and (ctr[:, 1] <= ctr[:, 0]).all()
 
 
-def test_edge_cases():
+def test_edge_cases(engine):
     import torch
 
     from python_motion_planning_amd import batch, workloads as wl
@@ -150,7 +165,7 @@ def test_edge_cases():
     batch.astar2d_batch(occ, starts[:1], goals[:1], path_cap=64, reserve_slots=64, heap_cap=0)
 
 
-def test_unreachable_and_empty_batch():
+def test_unreachable_and_empty_batch(engine):
     from python_motion_planning_amd import batch
 
     occ = np.zeros((16, 16), np.uint8)
@@ -189,7 +204,8 @@ def test_heap_above_32767_entries_uses_hbm_bit_tiers():
     batch.astar2d_batch(occ[:64, :64], s, s, path_cap=4, reserve_slots=64, heap_cap=0)  # default sizing again
 
 
-def test_residency_batches_in_flight():
+@pytest.mark.parametrize("eng,per_cu", [(1, 48), (1, 18), (0, 18)])
+def test_residency_batches_in_flight(eng, per_cu):
     """The bench's headline schedule: several contexts, each a smaller persistent-worker launch on
     its own stream with the LDS heap share of 18 resident workers per CU (pmp_astar2d_set_residency,
     368 LDS positions, the rest of each heap spilled), all in flight together.  Every batch equals
@@ -208,9 +224,10 @@ def test_residency_batches_in_flight():
     lanes = []
     for _ in range(3):
         ctx = L.pmp_create(torch.cuda.current_device())
+        _lib.check(ctx, L.pmp_astar2d_set_engine(ctx, eng, 0), "engine")
         _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, 32, 0), "reserve")
-        _lib.check(ctx, L.pmp_astar2d_set_residency(ctx, 18), "residency")
-        assert L.pmp_astar2d_set_residency(ctx, 33) != 0
+        _lib.check(ctx, L.pmp_astar2d_set_residency(ctx, per_cu), "residency")
+        assert L.pmp_astar2d_set_residency(ctx, 129) != 0
         lanes.append(dict(ctx=ctx, stream=torch.cuda.Stream(),
                           out=[torch.empty(nq, dtype=torch.float64, device="cuda"),
                                torch.empty(nq, dtype=torch.int32, device="cuda"),

@@ -145,3 +145,36 @@ def test_dstar3d_longest_first_schedule_full_c5():
     cost = out["cost"][:, 0].cpu().numpy()
     assert np.array_equal(out["n_process"][:, 0].cpu().numpy(), ref["n"][:, 0])
     assert all(_same(a, b) for a, b in zip(cost, ref["cost"][:, 0]))
+
+
+def test_small_lds_share_falls_back_to_hbm_occupancy():
+    """with 32 workers resident per CU a 40x40x25 grid's occupancy (5,000 B) no longer fits
+    beside an LDS heap; DStar3D and AStar3D then keep the occupancy in HBM (never a negative LDS heap
+    size), and the results still equal the oracle's."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import _lib, batch
+
+    rng = np.random.default_rng(21)
+    X, Y, Z = 40, 40, 25
+    base = (rng.random((X, Y, Z)) < 0.12).astype(np.uint8)
+    base[[0, -1], :, :] = 1
+    base[:, [0, -1], :] = 1
+    base[:, :, [0, -1]] = 1
+    free = np.argwhere(base == 0)
+    nq = 24
+    s = free[rng.integers(len(free), size=nq)].astype(np.int32)
+    g = free[rng.integers(len(free), size=nq)].astype(np.int32)
+    occ = np.repeat(base[None], nq, axis=0)
+    L, ctx = _lib.load_library(), _lib.context()
+    _lib.check(ctx, L.pmp_set_resident_per_cu(ctx, 32), "resident")
+    try:
+        d = batch.dstar3d_batch(occ, s, g)
+        a = batch.astar3d_batch(occ, s, g)
+    finally:
+        _lib.check(ctx, L.pmp_set_resident_per_cu(ctx, 0), "resident")
+    ref_d = O.graph3d_dynamic_batch("dstar3d", occ, s, g, None, nthreads=8)
+    assert np.array_equal(d["n_process"][:, 0].cpu().numpy(), ref_d["n"][:, 0])
+    assert all(_same(x, y) for x, y in zip(d["cost"][:, 0].cpu().numpy(), ref_d["cost"][:, 0]))
+    cost, st = O.astar3d_batch(occ, s, g, nthreads=8)
+    assert np.array_equal(a["status"].cpu().numpy(), st)
+    assert np.array_equal(a["cost"].cpu().numpy(), cost)

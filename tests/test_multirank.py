@@ -72,6 +72,77 @@ def test_two_ranks_gloo(tmp_path):
     assert [shard.shard_range(r, 3, 10) for r in range(3)] == [(0, 4), (4, 7), (7, 10)]
 
 
+def _c2_small():
+    from python_motion_planning_amd import workloads as wl
+
+    return wl.c2_workload(nq=72, W=96, H=96, pair_seed=11)
+
+
+def _c5_small():
+    from python_motion_planning_amd import workloads as wl
+
+    return wl.c5_workload(nq=40, first_seed=100)
+
+
+def _plan2d(s, g, occ):
+    import torch
+
+    from oracle import oracle as O
+
+    r = O.astar2d_batch(occ, s, g, path_cap=2048, nthreads=1)
+    return {k: torch.as_tensor(r[k]) for k in ("cost", "status", "n_expanded", "path_len", "path")}
+
+
+def _plan3d(s, g, occ):
+    import torch
+
+    from oracle import oracle as O
+
+    cost, st = O.astar3d_batch(occ, s, g, nthreads=1)
+    return {"cost": torch.as_tensor(cost), "status": torch.as_tensor(st)}
+
+
+def _sharded_main(rank, world, port, outdir):
+    """One rank of the strong-scaling path (shard.run_sharded): lpt_deal share -> the per-rank planner
+    (the oracle standing in for this rank's GPU) -> all_gather_rows into input order."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from python_motion_planning_amd import shard
+
+    dist = shard.init("gloo")
+    occ, s, g = _c2_small()
+    r2 = shard.run_sharded(dist, lambda a, b: _plan2d(a, b, occ), s, g)
+    occ3, s3, g3 = _c5_small()
+    r3 = shard.run_sharded(dist, lambda a, b, occ: _plan3d(a, b, occ), s3, g3, per_query={"occ": occ3})
+    mine = shard.lpt_deal(shard.octile(s, g), world, rank)
+    np.savez(os.path.join(outdir, f"sharded{rank}.npz"), mine=mine,
+             **{"c2_" + k: v.numpy() for k, v in r2.items()}, **{"c5_" + k: v.numpy() for k, v in r3.items()})
+    dist.destroy_process_group()
+
+
+def test_two_ranks_run_sharded_gather(tmp_path):
+    """world-size-2 gloo ranks through shard.run_sharded (lpt_deal + all_gather_rows): every rank's
+    gathered records equal one single-process run's, in input order, for a C2-style batch (96^2
+    grid, 72 queries) and a C5 batch (per-query 3D grids, 40 queries)."""
+    world = 2
+    mp.start_processes(_sharded_main, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    z = [np.load(tmp_path / f"sharded{r}.npz") for r in range(world)]
+    occ, s, g = _c2_small()
+    ref2 = {k: v.numpy() for k, v in _plan2d(s, g, occ).items()}
+    occ3, s3, g3 = _c5_small()
+    ref3 = {k: v.numpy() for k, v in _plan3d(s3, g3, occ3).items()}
+    assert (ref2["status"] == 0).all() and (ref3["status"] == 0).all()
+    for r in range(world):
+        for k, v in ref2.items():
+            assert np.array_equal(z[r]["c2_" + k], v), (r, k)
+        for k, v in ref3.items():
+            assert np.array_equal(z[r]["c5_" + k], v), (r, k)
+    # the deal really split the batch: disjoint, covering, both ranks busy
+    m0, m1 = z[0]["mine"], z[1]["mine"]
+    assert len(m0) and len(m1) and not set(m0) & set(m1) and len(m0) + len(m1) == len(s)
+
+
 def test_single_process_defaults(monkeypatch):
     from python_motion_planning_amd import shard
 

@@ -1,9 +1,16 @@
 """Summarise a round's rocprofv3 databases (tools/profile_round.sh) into profiles/<round>/:
-  kernel_stats.csv   -- rocprofv3 --kernel-trace --stats of the default bench command
-  pmc_traffic.json   -- per-kernel FETCH_SIZE / WRITE_SIZE per dispatch from the two --pmc passes,
-                        with the gfx950 correction of MI355X_MICROARCH.md (FETCH_SIZE counts half the
-                        bytes of wide streaming reads: doubled; WRITE_SIZE as is; both in KiB)
-usage: python tools/prof_summary.py gpurun_out profiles/r1
+  kernel_stats.csv            -- rocprofv3 --kernel-trace --stats of the default bench command, per kernel
+  kernel_stats_workloads.csv  -- the same dispatches keyed per (workload, kernel) through the bench's
+                                 launch manifest (bench.py: every C-ABI planner call is logged under
+                                 the label of the leg that made it, in launch order)
+  pmc_traffic.json            -- FETCH_SIZE / WRITE_SIZE per dispatch from the two --pmc passes, keyed
+                                 per workload the same way ("workloads"), with the gfx950 correction of
+                                 MI355X_MICROARCH.md (FETCH_SIZE counts half the bytes of wide streaming
+                                 reads: doubled; WRITE_SIZE as is; both in KiB)
+  pmc_mfma.json               -- MFMA busy cycles of the MPC pass
+A kernel whose dispatch count in a database differs from its manifest total is not attributed (its
+workload entries are left out, so bench.py reports traffic null rather than a mis-keyed number).
+usage: python tools/prof_summary.py gpurun_out profiles/r3
 """
 import csv
 import json
@@ -15,23 +22,25 @@ import sys
 KERNELS = {  # short name -> regex on the demangled kernel name
     "lpt_hist": r"lpt_hist\(", "lpt_scan": r"lpt_scan\(", "lpt_scatter": r"lpt_scatter\(",
     "lpt3_hist": r"lpt3_hist\(", "lpt3_scan": r"lpt3_scan\(", "lpt3_scatter": r"lpt3_scatter\(",
-    "astar2d_kernel": r"astar2d_kernel<",
-    "dwa_kernel": r"dwa_kernel\(",
-    "rrt_kernel": r"rrt_kernel<",
-    "astar3d_kernel": r"astar3d_kernel[<(]",
-    "dstar_kernel": r"dstar_kernel\(",
-    "dstar3d_kernel": r"dstar3d_kernel<",
-    "lpa_kernel": r"lpa_kernel\(",
-    "lpa3d_kernel": r"lpa3d_kernel\(",
+    "dwa_kernel": r"\bdwa_kernel[<(]",
+    "rrt_kernel": r"\brrt_kernel[<(]",
+    "astar3d_kernel": r"\bastar3d_kernel[<(]",
+    "dstar_kernel": r"\bdstar_kernel[<(]",
+    "dstar3d_kernel": r"\bdstar3d_kernel[<(]",
+    "lpa_kernel": r"\blpa_kernel[<(]",
+    "lpa3d_kernel": r"\blpa3d_kernel[<(]",
     "track_kernel_lqr": r"track_kernel<0>",
     "track_kernel_mpc": r"track_kernel<1>",
-    "totp3d_kernel": r"totp3d_kernel\(",
+    "lqr_control_kernel": r"\blqr_control_kernel[<(]",
+    "mpc_control_kernel": r"\bmpc_control_kernel[<(]",
+    "totp3d_kernel": r"\btotp3d_kernel[<(]",
 }
 
 
-# the 2D graph kernel's template <HEUR, GZERO, THETA> (astar2d.hip): one short name per planner, so the
+# the 2D graph kernels' template <HEUR, GZERO, THETA> (astar2d.hip): one short name per planner, so the
 # headline's traffic is never taken from the Theta* launches of the same kernel template
 _G2D = re.compile(r"astar2d_kernel<(\d+), (true|false), (\d)>")
+_MQ = re.compile(r"astar2d_mq_kernel<(\d+), (true|false), (true|false)>")
 
 
 def short(name):
@@ -43,22 +52,54 @@ def short(name):
         if gzero:
             return "gbfs2d_kernel"
         return "dijkstra2d_kernel" if (heur & 3) == 2 else "astar2d_kernel"
+    m = _MQ.search(name)
+    if m:  # the multi-query engine <HEUR, GZERO, T2LDS>: same short names as the one-query-per-wave kernel
+        heur, gzero = int(m.group(1)), m.group(2) == "true"
+        return "gbfs2d_kernel" if gzero else ("dijkstra2d_kernel" if heur == 2 else "astar2d_kernel")
     for k, rx in KERNELS.items():
         if re.search(rx, name):
             return k
     return name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:60]
 
 
+def load_manifest(path):
+    """[label, kernel, dispatches] in launch order, from a bench detail file (bench.py --detail-out)."""
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get("launch_manifest")
+
+
+def attribute(seq, manifest):
+    """seq: [(short kernel name, record)] in dispatch order.  Returns ({label: [(kernel, record), ...]},
+    {kernel: (seen, expected)} for the kernels that could not be attributed)."""
+    by_k = {}
+    for k, rec in seq:
+        by_k.setdefault(k, []).append(rec)
+    want = {}
+    for label, k, n in manifest:
+        want[k] = want.get(k, 0) + n
+    bad = {k: (len(by_k.get(k, [])), n) for k, n in want.items() if len(by_k.get(k, [])) != n}
+    pos = {k: 0 for k in want}
+    out = {}
+    for label, k, n in manifest:
+        recs = by_k.get(k, [])[pos[k]: pos[k] + n]
+        pos[k] += n
+        if k in bad:
+            continue
+        out.setdefault(label, []).extend((k, r) for r in recs)
+    return out, bad
+
+
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
     kt = os.path.join(src, "prof_kt", "run_results.db")
-    rows = []
     if os.path.exists(kt):
-        rows = kernel_stats(kt, dst)
-    traffic_and_mfma(src, dst, rows)
+        kernel_stats(kt, dst, load_manifest(os.path.join(src, "prof_kt", "detail.json")))
+    traffic_and_mfma(src, dst)
 
 
-def kernel_stats(kt, dst):
+def kernel_stats(kt, dst, manifest):
     db = sqlite3.connect(kt)
     # one row per (kernel, grid size): a planner launched with different batch sizes (e.g. the small
     # A* batches that build the control legs' global paths) gets separate statistics
@@ -70,45 +111,86 @@ def kernel_stats(kt, dst):
         w.writerow(["kernel", "grid_threads", "calls", "total_ns", "avg_ns", "min_ns", "max_ns", "percent"])
         for n, g, c, t, a, mn, mx in rows:
             w.writerow([short(n), g, c, f"{t:.0f}", f"{a:.0f}", f"{mn:.0f}", f"{mx:.0f}", f"{100.0 * t / tot:.3f}"])
-    # per-dispatch durations of the headline kernel, in launch order (warmups first)
+    seq = [(short(n), d) for n, d in db.execute("select name, duration from kernels order by start")]
     with open(os.path.join(dst, "astar2d_dispatches.csv"), "w", newline="") as f:
         w = csv.writer(f)
-        w.writerow(["dispatch", "grid_threads", "duration_ns"])
-        for i, (n, g, d) in enumerate(db.execute("select name, grid_x, duration from kernels where name like "
-                                                "'%astar2d_kernel%' order by start")):
-            if short(n) == "astar2d_kernel":
-                w.writerow([i, g, d])
-    return [(n, c, t, a, 100.0 * t / tot) for n, g, c, t, a, mn, mx in rows]
+        w.writerow(["dispatch", "duration_ns"])
+        for i, (k, d) in enumerate(x for x in seq if x[0] == "astar2d_kernel"):
+            w.writerow([i, d])
+    if manifest:
+        per, bad = attribute(seq, manifest)
+        with open(os.path.join(dst, "kernel_stats_workloads.csv"), "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["workload", "kernel", "dispatches", "avg_ns", "min_ns", "max_ns"])
+            for label, recs in per.items():
+                for k in sorted({k for k, _ in recs}):
+                    d = [r for kk, r in recs if kk == k]
+                    w.writerow([label, k, len(d), f"{sum(d) / len(d):.0f}", f"{min(d):.0f}", f"{max(d):.0f}"])
+        if bad:
+            print("kernel trace: not attributed (seen, manifest):", bad)
+    for n, g, c, t, a, mn, mx in rows[:8]:
+        print(f"{short(n):24s} calls {c:5d} avg {a / 1e6:12.3f} ms  {100.0 * t / tot:6.2f} %")
 
 
-def traffic_and_mfma(src, dst, rows):
-    traffic = {}
+def pmc_dispatches(path, counter):
+    """[(short kernel name, value)] per dispatch in dispatch order for one counter of a --pmc pass."""
+    d = sqlite3.connect(path)
+    cols = [r[1] for r in d.execute("pragma table_info(counters_collection)")]
+    order = "dispatch_id" if "dispatch_id" in cols else ("correlation_id" if "correlation_id" in cols else None)
+    if order:
+        q = (f"select kernel_name, sum(value) from counters_collection where counter_name = ? group by {order} "
+             f"order by {order}")
+    else:
+        q = "select kernel_name, value from counters_collection where counter_name = ? order by rowid"
+    return [(short(n), v) for n, v in d.execute(q, (counter,))], cols
+
+
+def traffic_and_mfma(src, dst):
+    kernels, workloads, unattributed = {}, {}, {}
     for counter, sub in (("FETCH_SIZE", "prof_fetch"), ("WRITE_SIZE", "prof_write")):
         path = os.path.join(src, sub, "run_results.db")
         if not os.path.exists(path):
             continue
-        d = sqlite3.connect(path)
-        # the largest launch configuration of each kernel (the bench leg's own batch)
-        for name, n, mean_kb in d.execute(
-                "select kernel_name, count(*), avg(value) from counters_collection c where counter_name = ? "
-                "and grid_size = (select max(grid_size) from counters_collection c2 where c2.kernel_name = "
-                "c.kernel_name and c2.counter_name = c.counter_name) group by kernel_name", (counter,)):
-            k = short(name)
-            e = traffic.setdefault(k, {})
-            e[f"{counter}_kib_per_dispatch"] = mean_kb
-            e["dispatches"] = n
-    for k, e in traffic.items():
+        seq, cols = pmc_dispatches(path, counter)
+        print(sub, "counters_collection columns:", cols)
+        for k in {k for k, _ in seq}:
+            v = [x for kk, x in seq if kk == k]
+            e = kernels.setdefault(k, {})
+            e[f"{counter}_kib_per_dispatch"] = sum(v) / len(v)
+            e[f"{counter}_dispatches"] = len(v)
+        manifest = load_manifest(os.path.join(src, sub, "detail.json"))
+        if not manifest:
+            continue
+        per, bad = attribute(seq, manifest)
+        unattributed[counter] = bad
+        for label, recs in per.items():
+            ks = {k for k, _ in recs}
+            # a workload's own kernel: the one the leg is about (the setup A* path batches of the
+            # control legs are labelled "setup", not with the leg's name)
+            for k in ks:
+                v = [x for kk, x in recs if kk == k]
+                key = label if len(ks) == 1 else f"{label}:{k}"
+                e = workloads.setdefault(key, {"kernel": k})
+                e[f"{counter}_kib_per_dispatch"] = sum(v) / len(v)
+                e[f"{counter}_dispatches"] = len(v)
+    for e in list(kernels.values()) + list(workloads.values()):
         fb = e.get("FETCH_SIZE_kib_per_dispatch")
         wb = e.get("WRITE_SIZE_kib_per_dispatch")
         e["read_bytes_per_dispatch"] = None if fb is None else 2.0 * fb * 1024.0
         e["write_bytes_per_dispatch"] = None if wb is None else wb * 1024.0
         e["hbm_bytes_per_dispatch"] = (None if fb is None or wb is None
                                        else e["read_bytes_per_dispatch"] + e["write_bytes_per_dispatch"])
-    traffic["_note"] = ("FETCH_SIZE doubled per MI355X_MICROARCH.md (calibrated for 16 B/lane streaming reads; "
-                        "the planners' reads are scattered 4-16 B accesses, for which the guide gives no "
-                        "calibration) and WRITE_SIZE as is; Infinity-Cache hits are counted by these counters")
-    with open(os.path.join(dst, "pmc_traffic.json"), "w") as f:
-        json.dump(traffic, f, indent=1, sort_keys=True)
+    out = {"workloads": workloads, "kernels": kernels, "unattributed": unattributed,
+           "_note": ("per dispatch, keyed per workload through the bench's launch manifest; FETCH_SIZE doubled per "
+                     "MI355X_MICROARCH.md (calibrated for 16 B/lane streaming reads; the planners' reads are "
+                     "scattered 4-16 B accesses, for which the guide gives no calibration) and WRITE_SIZE as is; "
+                     "Infinity-Cache hits are counted by these counters")}
+    if kernels:
+        with open(os.path.join(dst, "pmc_traffic.json"), "w") as f:
+            json.dump(out, f, indent=1, sort_keys=True)
+        print(json.dumps({k: v.get("hbm_bytes_per_dispatch") for k, v in workloads.items()}))
+        if any(unattributed.values()):
+            print("pmc: not attributed (seen, manifest):", unattributed)
     # MFMA utilisation pass (rocprofv3's MfmaUtil expression: SQ_VALU_MFMA_BUSY_CYCLES summed over the
     # chip / (GRBM_GUI_ACTIVE x SIMDs), per dispatch)
     path = os.path.join(src, "prof_mfma", "run_results.db")
@@ -128,9 +210,6 @@ def traffic_and_mfma(src, dst, rows):
         with open(os.path.join(dst, "pmc_mfma.json"), "w") as f:
             json.dump(mf, f, indent=1, sort_keys=True)
         print("mfma", {k: v.get("mfma_util_pct") for k, v in mf.items() if not k.startswith("_")})
-    for n, c, t, a, p in rows[:8]:
-        print(f"{short(n):24s} calls {c:5d} avg {a / 1e6:12.3f} ms  {p:6.2f} %")
-    print(json.dumps({k: v.get("hbm_bytes_per_dispatch") for k, v in traffic.items() if not k.startswith("_")}))
 
 
 if __name__ == "__main__":
