@@ -564,52 +564,59 @@ def astar3d_leg(args, torch, dist, world, rank):
     s_d = torch.as_tensor(s, device="cuda")
     g_d = torch.as_tensor(g, device="cuda")
     L = _lib.load_library()
-    cap = X * Y * Z + 1
-    # batches in flight (own stream + pmp_ctx each): a launch lasts as long as its longest query (the
-    # longest-first schedule starts it first), and the next launch's workers fill the CUs the
-    # finished ones free
+    cap = 512  # C5 paths are far shorter (the kernel reports PMP_PATH_OVERFLOW otherwise)
+    # Batches per launch (as the headline): B of the steps' batches per launch, streamed through the
+    # launch's persistent workers longest first; B = 1 with several streams = batches in flight.
+    B = max(1, min(args.a3_batches_per_launch or args.a3_steps, args.a3_steps))
+    nlaunch = -(-args.a3_steps // B)
+    S = max(1, min(args.a3_streams, nlaunch))
+    occ_r, s_r, g_r = occ_d.repeat(B, 1), s_d.repeat(B, 1), g_d.repeat(B, 1)
+    wpc = args.a3_workers_per_cu if B == 1 else args.a3_residency
     lanes = []
-    for _ in range(max(1, args.a3_streams)):
+    for _ in range(S):
         ctx = L.pmp_create(torch.cuda.current_device())
-        _lib.check(ctx, L.pmp_set_workers_per_cu(ctx, args.a3_workers_per_cu), "workers")
+        _lib.check(ctx, L.pmp_set_workers_per_cu(ctx, wpc), "workers")
         _lib.check(ctx, L.pmp_set_resident_per_cu(ctx, args.a3_residency), "residency")
         lanes.append(dict(ctx=ctx, stream=pool_stream(torch, len(lanes)),
-                          cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
-                          plen=torch.empty(nq, dtype=torch.int32, device="cuda"),
-                          path=torch.empty((nq, cap), dtype=torch.int32, device="cuda"),
-                          nexp=torch.empty(nq, dtype=torch.int32, device="cuda"),
-                          st=torch.empty(nq, dtype=torch.int32, device="cuda")))
-    ctr = torch.empty((nq, 4), dtype=torch.int64, device="cuda")
+                          cost=torch.empty(B * nq, dtype=torch.float64, device="cuda"),
+                          plen=torch.empty(B * nq, dtype=torch.int32, device="cuda"),
+                          path=torch.empty((B * nq, cap), dtype=torch.int32, device="cuda"),
+                          nexp=torch.empty(B * nq, dtype=torch.int32, device="cuda"),
+                          st=torch.empty(B * nq, dtype=torch.int32, device="cuda")))
+    ctr = torch.empty((B * nq, 4), dtype=torch.int64, device="cuda")
 
-    def run(i, counters=None):
+    def run(i, nb, counters=None):
         b = lanes[i % len(lanes)]
-        rc = L.pmp_astar3d_batch(b["ctx"], b["stream"].cuda_stream, occ_d.data_ptr(), 1, X, Y, Z, 0, s_d.data_ptr(),
-                                 g_d.data_ptr(), nq, b["cost"].data_ptr(), b["plen"].data_ptr(), b["path"].data_ptr(), cap,
-                                 b["nexp"].data_ptr(), None, 0, counters, b["st"].data_ptr())
+        rc = L.pmp_astar3d_batch(b["ctx"], b["stream"].cuda_stream, occ_r.data_ptr(), 1, X, Y, Z, 0, s_r.data_ptr(),
+                                 g_r.data_ptr(), nq * nb, b["cost"].data_ptr(), b["plen"].data_ptr(),
+                                 b["path"].data_ptr(), cap, b["nexp"].data_ptr(), None, 0, counters, b["st"].data_ptr())
         if rc:
             _lib.check(b["ctx"], rc, "pmp_astar3d_batch")
 
-    run(0, ctr.data_ptr())
+    wb = max(1, min(B, 2))
+    run(0, wb, ctr.data_ptr())
     for i in range(1, len(lanes)):
-        run(i)
+        run(i, wb)
     torch.cuda.synchronize()
-    c = ctr.cpu().numpy()
-    cost, plen, path = lanes[0]["cost"], lanes[0]["plen"], lanes[0]["path"]
-    for b in lanes[1:]:
-        assert torch.equal(b["cost"], cost) and torch.equal(b["st"], lanes[0]["st"])
+    c = ctr[:nq].cpu().numpy()
     akeys = ("cost", "plen", "nexp", "st")
-    ref_out = {k: lanes[0][k].clone() for k in akeys}
+    ref_out = {k: lanes[0][k][:nq].clone() for k in akeys}
+    assert np.isin(ref_out["st"].cpu().numpy(), (0, 1)).all(), "unexpected 3D A* statuses"
+    plen, path = ref_out["plen"], lanes[0]["path"][:nq].clone()
     for b in lanes:
+        for j in range(wb):
+            assert torch.equal(b["cost"][j * nq:(j + 1) * nq], ref_out["cost"])
         poison([b[k] for k in akeys])
     shard.barrier(dist)
     torch.cuda.synchronize()
     evs = []
+    nbs = [min(B, args.a3_steps - i * B) for i in range(nlaunch)]
     t0 = time.perf_counter()
-    for i in range(args.a3_steps):
+    for i in range(nlaunch):
         b = lanes[i % len(lanes)]
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(b["stream"])
-        run(i)
+        run(i, nbs[i])
         e1.record(b["stream"])
         evs.append((e0, e1))
     torch.cuda.synchronize()
@@ -617,11 +624,15 @@ def astar3d_leg(args, torch, dist, world, rank):
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(e) for a, e in evs]))
     elapsed, kern_ms = shard.max_over_ranks(dist, [elapsed, kern_ms], "cuda")
-    checked = check_timed("astar3d", ref_out, lanes[: min(len(lanes), args.a3_steps)])
+    outs = []
+    for li, b in enumerate(lanes[: min(S, nlaunch)]):
+        last_nb = nbs[max(i for i in range(nlaunch) if i % S == li)]
+        outs += [{k: b[k][j * nq:(j + 1) * nq] for k in akeys} for j in range(last_nb)]
+    checked = check_timed("astar3d", ref_out, outs)
     cost = ref_out["cost"]
     # per plan 55*E3 + 16*(P3 + Q3), with P3 the reference's pushes and Q3 <= P3
     # (every pushed entry popped at most once): 55*E3 + 32*P3
-    alg_bytes = float(np.sum(55.0 * c[:, 2] + 32.0 * c[:, 0]))
+    alg_bytes = float(np.sum(55.0 * c[:, 2] + 32.0 * c[:, 0])) * float(np.mean(nbs))
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -650,13 +661,14 @@ def astar3d_leg(args, torch, dist, world, rank):
     return {"metric": "3D A* plans/sec, Grid3D(26,20,16) door scenario, 8192 queries", "value": nq * args.a3_steps * world / elapsed,
             "unit": "plans/s", "queries_per_gpu": nq, "steps": args.a3_steps,
             "ms_per_step": elapsed / args.a3_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
-            "streams": len(lanes), "timed_launches_checked": checked, "workers_per_cu": args.a3_workers_per_cu, "resident_per_cu": args.a3_residency,
+            "streams": len(lanes), "batches_per_launch": B, "timed_launches_checked": checked,
+            "workers_per_cu": wpc, "resident_per_cu": args.a3_residency,
             "config": {"workload": "C5: Grid3D(26,20,16) door, random.seed(i) pairs, safety bubbles r=1, euclidean"},
             "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                       "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                                       "algorithmic_bytes_per_launch": alg_bytes}, "astar3d_kernel", "astar3d"),
-            "detail": {"expansions_per_launch": int(c[:, 2].sum()), "reference_pushes_per_launch": int(c[:, 0].sum()),
-                       "heap_pops_per_launch": int(c[:, 1].sum()), "max_heap_entries": int(c[:, 3].max())},
+            "detail": {"expansions_per_batch": int(c[:, 2].sum()), "reference_pushes_per_batch": int(c[:, 0].sum()),
+                       "heap_pops_per_batch": int(c[:, 1].sum()), "max_heap_entries": int(c[:, 3].max())},
             "cpu_baseline": cpu, "trajectory": traj}
 
 
@@ -1360,7 +1372,8 @@ def headline_line(out: dict, detail_path) -> dict:
     line["cpu_baseline"] = cpu
     line["detail"] = {"kernel_ms_per_launch": _sig(d["kernel_ms_per_launch"]), "streams": d["streams"],
                       "engine": d["engine"],
-                      "expansions_per_launch": d["expansions_per_launch"],
+                      "batches_per_launch": d["batches_per_launch"],
+                      "expansions_per_batch": d["expansions_per_batch"],
                       "timed_launches_checked": d["timed_launches_checked"], "detail_file": detail_path}
     line["secondary"] = {k: compact_leg(v) for k, v in out["secondary"].items()}
     s = json.dumps(line)
@@ -1425,7 +1438,8 @@ def main():
     ap.add_argument("--control-steps", type=int, default=20, help="timed control steps")
     ap.add_argument("--engine", type=int, default=1, choices=[0, 1],
                     help="A* 2D engine: 1 = four queries per wave (astar2d_mq.hip), 0 = one query per wave (astar2d.hip)")
-    ap.add_argument("--t2lds", type=int, default=0, help="multi-query engine: level-10..14 heap bits in LDS (1) or HBM (0)")
+    ap.add_argument("--t2lds", type=int, default=1,
+                    help="multi-query engine: level-10..12 heap bits in LDS (1; heaps <= 16383) or level-10..14 in HBM (0)")
     ap.add_argument("--workers", type=int, default=0,
                     help="A* queries in flight per launch (persistent 16-lane groups on engine 1, waves on engine 0); "
                          "0 = the engine's default")
@@ -1457,6 +1471,8 @@ def main():
     ap.add_argument("--a3-queries", type=int, default=8192)
     ap.add_argument("--a3-steps", type=int, default=32)
     ap.add_argument("--a3-streams", type=int, default=6, help="3D A* batches in flight (own stream + context each)")
+    ap.add_argument("--a3-batches-per-launch", type=int, default=0,
+                    help="3D A* batches per launch (0 = all the timed steps in one launch)")
     ap.add_argument("--a3-workers-per-cu", type=int, default=4, help="3D A* persistent workers per CU")
     ap.add_argument("--a3-residency", type=int, default=24,
                     help="3D A* workers resident per CU over all batches in flight (LDS share; 0 = per launch)")
@@ -1471,6 +1487,9 @@ def main():
                     help="A* query order across workers: longest start-goal distance first, or input order")
     ap.add_argument("--prio", type=int, default=64,
                     help="longest-first only: the first N (longest) queries of a batch run at raised wave priority")
+    ap.add_argument("--batches-per-launch", type=int, default=0,
+                    help="batches (steps) one launch plans, streamed through its persistent workers longest first; "
+                         "0 = all the timed steps in one launch (engine 1) or one per launch (engine 0)")
     ap.add_argument("--streams", type=int, default=6,
                     help="batches in flight: consecutive steps go to different HIP streams (own scratch "
                          "context each), so one batch's long-query tail overlaps the next batch")
@@ -1491,9 +1510,11 @@ def main():
     # engine defaults (tools/sweep_residency.sh): engine 1 -- 6 x 2048 groups in flight, 48 per CU;
     # engine 0 -- 6 x 768 waves, 18 per CU (round 2)
     if not args.workers:
-        args.workers = 2048 if args.engine == 1 else 768
+        args.workers = 8192 if args.engine == 1 else 768
     if not args.residency:
-        args.residency = 48 if args.engine == 1 else 18
+        args.residency = 32 if args.engine == 1 else 18
+    if not args.batches_per_launch and args.engine == 0:
+        args.batches_per_launch = 1
 
     from python_motion_planning_amd import shard
 
@@ -1535,7 +1556,16 @@ def main():
     s_d = torch.as_tensor(starts, device="cuda")
     g_d = torch.as_tensor(goals, device="cuda")
     path_cap = 4096
-    S = max(1, args.streams)
+    # Batches per launch (B): the steps' batches go to the planner B at a time, each launch's
+    # persistent workers streaming through its B x 4096 queries longest first (continuous batching:
+    # a query of batch k+1 starts as soon as a worker frees up, instead of behind batch k's longest
+    # query).  B = 1 with several streams is the round-2 schedule (one launch per batch, batches in
+    # flight on their own streams).  Every batch keeps its own outputs; every timed batch is checked.
+    B = max(1, min(args.batches_per_launch or args.steps, args.steps))
+    nlaunch = -(-args.steps // B)
+    S = max(1, min(args.streams, nlaunch))
+    s_rep = s_d.repeat(B, 1)
+    g_rep = g_d.repeat(B, 1)
     lanes = []
     for _ in range(S):
         ctx = L.pmp_create(torch.cuda.current_device())
@@ -1547,45 +1577,47 @@ def main():
             _lib.check(ctx, L.pmp_astar2d_set_residency(ctx, args.residency), "residency")
         lanes.append(dict(
             ctx=ctx, stream=pool_stream(torch, len(lanes)),
-            cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
-            plen=torch.empty(nq, dtype=torch.int32, device="cuda"),
-            path=torch.empty((nq, path_cap), dtype=torch.int32, device="cuda"),
-            nexp=torch.empty(nq, dtype=torch.int32, device="cuda"),
-            status=torch.empty(nq, dtype=torch.int32, device="cuda")))
-    ctr = torch.empty((nq, 4), dtype=torch.int64, device="cuda")
+            cost=torch.empty(B * nq, dtype=torch.float64, device="cuda"),
+            plen=torch.empty(B * nq, dtype=torch.int32, device="cuda"),
+            path=torch.empty((B * nq, path_cap), dtype=torch.int32, device="cuda"),
+            nexp=torch.empty(B * nq, dtype=torch.int32, device="cuda"),
+            status=torch.empty(B * nq, dtype=torch.int32, device="cuda")))
+    ctr = torch.empty((B * nq, 4), dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
 
-    def step(i, counters=None):
+    def step(i, nb, counters=None):
+        """Launch i (on lane i % S): nb batches of the nq pairs, as one call of the C-ABI."""
         b = lanes[i % S]
-        rc = L.pmp_astar2d_batch(b["ctx"], b["stream"].cuda_stream, occ_bits.data_ptr(), W, H, 0, s_d.data_ptr(),
-                                 g_d.data_ptr(), nq, b["cost"].data_ptr(), b["plen"].data_ptr(), b["path"].data_ptr(),
-                                 path_cap, b["nexp"].data_ptr(), None, 0, counters, b["status"].data_ptr())
+        rc = L.pmp_astar2d_batch(b["ctx"], b["stream"].cuda_stream, occ_bits.data_ptr(), W, H, 0, s_rep.data_ptr(),
+                                 g_rep.data_ptr(), nq * nb, b["cost"].data_ptr(), b["plen"].data_ptr(),
+                                 b["path"].data_ptr(), path_cap, b["nexp"].data_ptr(), None, 0, counters,
+                                 b["status"].data_ptr())
         if rc:
             _lib.check(b["ctx"], rc, "pmp_astar2d_batch")
         return b
 
-    # warmup: every stream once (the first pass also records the deterministic push/pop/expansion counts)
-    step(0, ctr.data_ptr())
-    for i in range(1, max(args.warmup, S)):
-        step(i)
+    # warmup: every lane once (the first launch also records the deterministic push/pop/expansion counts)
+    wb = max(1, min(B, args.warmup))
+    step(0, wb, ctr.data_ptr())
+    for i in range(1, S):
+        step(i, wb)
     torch.cuda.synchronize()
-    counters = ctr.cpu().numpy()
-    cost = lanes[0]["cost"]
+    counters = ctr[:nq].cpu().numpy()
+    ref_out = {k: lanes[0][k][:nq].clone() for k in ("cost", "plen", "nexp", "status")}
+    st0 = ref_out["status"].cpu().numpy()
+    assert (st0 == 0).all(), f"unexpected statuses {np.unique(st0)}"
     for b in lanes:
-        st = b["status"].cpu().numpy()
-        assert (st == 0).all(), f"unexpected statuses {np.unique(st)}"
-        assert torch.equal(b["cost"], cost)
-    bytes_per_launch = astar_algorithmic_bytes(counters)
-    ref_out = {k: lanes[0][k].clone() for k in ("cost", "plen", "nexp", "status")}
+        for j in range(wb):
+            assert torch.equal(b["cost"][j * nq:(j + 1) * nq], ref_out["cost"])
+    bytes_per_batch = astar_algorithmic_bytes(counters)
     for b in lanes:
         poison([b["cost"], b["plen"], b["nexp"], b["status"]])
     torch.cuda.synchronize()
 
-    # timed region.  kernel_ms = HIP events on each launch's own stream: with several batches in
-    # flight this includes the time a dispatch waits for CUs held by the other streams' persistent
-    # workers, exactly as rocprofv3's dispatch duration does.  Each launch also records its device
-    # execution span (first worker start .. last worker end, pmp_set_timing) for the detail block.
-    spans = torch.empty((args.steps, 2), dtype=torch.int64, device="cuda")
+    # timed region.  kernel_ms = HIP events on each launch's own stream (= rocprofv3's dispatch
+    # duration).  Each launch also records its device execution span (first worker start .. last
+    # worker end, pmp_set_timing) for the detail block.
+    spans = torch.empty((nlaunch, 2), dtype=torch.int64, device="cuda")
     spans[:, 0] = -1  # UINT64_MAX
     spans[:, 1] = 0
     khz = ctypes.c_int(0)
@@ -1593,13 +1625,14 @@ def main():
     shard.barrier(dist)
     torch.cuda.synchronize()
     evs = []
+    nbs = [min(B, args.steps - i * B) for i in range(nlaunch)]
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(nlaunch):
         b = lanes[i % S]
         L.pmp_set_timing(b["ctx"], spans[i].data_ptr())
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(b["stream"])
-        step(i)
+        step(i, nbs[i])
         e1.record(b["stream"])
         evs.append((e0, e1))
     torch.cuda.synchronize()
@@ -1610,16 +1643,21 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     sp = spans.cpu().numpy().view(np.uint64)
     span_ms = float(np.mean((sp[:, 1] - sp[:, 0]).astype(np.float64)) / khz.value)
-    timed_checked = check_timed("astar2d", ref_out, lanes[: min(S, args.steps)])
+    # every batch of the last launch on every lane equals the warmup's first batch
+    outs = []
+    for li, b in enumerate(lanes[: min(S, nlaunch)]):
+        last_nb = nbs[max(i for i in range(nlaunch) if i % S == li)]
+        outs += [{k: b[k][j * nq:(j + 1) * nq] for k in ("cost", "plen", "nexp", "status")} for j in range(last_nb)]
+    timed_checked = check_timed("astar2d", ref_out, outs)
     elapsed, kern_ms, span_ms = shard.max_over_ranks(dist, [elapsed, kern_ms, span_ms], "cuda")
-
+    bytes_per_launch = bytes_per_batch * float(np.mean(nbs))
     plans = (args.nq if args.scaling == "strong" else nq * world) * args.steps
     value = plans / elapsed
     gathered = None
     if args.scaling == "strong" and dist is not None:
         # the survey's end-of-run result exchange: every rank's records into the full batch, input order
-        g = shard.all_gather_rows(dist, mine, {"cost": lanes[0]["cost"], "status": lanes[0]["status"],
-                                               "n_expanded": lanes[0]["nexp"]}, args.nq, device="cuda")
+        g = shard.all_gather_rows(dist, mine, {"cost": ref_out["cost"], "status": ref_out["status"],
+                                               "n_expanded": ref_out["nexp"]}, args.nq, device="cuda")
         gathered = {"queries": args.nq, "found": int((g["status"] == 0).sum().item()),
                     "sum_expansions": int(g["n_expanded"].sum().item())}
     counters_all = shard.all_gather_rows(dist, mine, {"c": torch.as_tensor(counters, device="cuda")},
@@ -1702,9 +1740,9 @@ def main():
             "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                       "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                                       "algorithmic_bytes_per_launch": bytes_per_launch,
-                                      # the batches in flight overlap: bytes of one batch per step interval
-                                      "achieved_aggregate": bytes_per_launch / (elapsed / args.steps) / 1e9,
-                                      "frac_aggregate": bytes_per_launch / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS},
+                                      # launches in flight overlap: bytes of one batch per step interval
+                                      "achieved_aggregate": bytes_per_batch / (elapsed / args.steps) / 1e9,
+                                      "frac_aggregate": bytes_per_batch / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS},
                                      "astar2d_kernel", "astar2d_c2"),
             "cpu_baseline": cpu,
             "secondary": secondary,
@@ -1712,7 +1750,8 @@ def main():
                        "kernel_ms_source": "HIP events on the launch's stream (= rocprofv3 dispatch duration)",
                        "execution_span_ms_per_launch": span_ms, "schedule": args.schedule,
                        "algorithmic_bytes_per_launch": bytes_per_launch,
-                       "expansions_per_launch": int(counters[:, 2].sum()),
+                       "batches_per_launch": B, "launches": nlaunch,
+                       "expansions_per_batch": int(counters[:, 2].sum()),
                        "max_expansions_query": int(counters[:, 2].max()),
                        "pushes_per_launch": int(counters[:, 0].sum()),
                        "pops_per_launch": int(counters[:, 1].sum()),

@@ -1028,6 +1028,9 @@ int default_heap_cap(int W, int H)
 }
 // per-context scratch budget: workers are reduced to fit (heap spill + cell state + G per worker)
 constexpr size_t kScratchBudget = (size_t)64 << 30;
+// the multi-query engine keeps 3-4x more queries in flight (9.5 MB of cell state, g and heap spill
+// each at 1024^2): its per-context budget
+constexpr size_t kScratchBudgetMq = (size_t)160 << 30;
 
 // longest-first order of a batch in the context's SCR_PDIR scratch (counting sort, descending
 // start-goal distance)
@@ -1057,12 +1060,12 @@ extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int workers, int 
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_reserve: bad dims/workers");
     if (heap_cap <= 0) heap_cap = default_heap_cap(W, H);
     if ((size_t)heap_cap > max_heap(W, H)) heap_cap = (int)max_heap(W, H);
-    if (ctx->astar_engine == 1 && heap_cap <= 65536 && heap_cap > pmp_astar2d_mq_cap())
-        heap_cap = pmp_astar2d_mq_cap();  // the default capacity on the multi-query engine
-    if (ctx->astar_engine == 1 && heap_cap <= pmp_astar2d_mq_cap()) {
+    if (ctx->astar_engine == 1 && heap_cap <= 65536 && heap_cap > pmp_astar2d_mq_cap(ctx->astar_mq_t2lds != 0))
+        heap_cap = pmp_astar2d_mq_cap(ctx->astar_mq_t2lds != 0);  // the default capacity on the multi-query engine
+    if (ctx->astar_engine == 1 && heap_cap <= pmp_astar2d_mq_cap(ctx->astar_mq_t2lds != 0)) {
         // workers = queries in flight (16-lane groups, 4 per wave); scratch is taken at launch
-        const size_t per_slot = (size_t)W * H * 9 + (size_t)pmp_astar2d_mq_cap() * 16 + 4096 + 256;
-        const size_t fit = kScratchBudget / per_slot;
+        const size_t per_slot = (size_t)W * H * 9 + (size_t)pmp_astar2d_mq_cap(ctx->astar_mq_t2lds != 0) * 16 + 4096 + 256;
+        const size_t fit = kScratchBudgetMq / per_slot;
         if (fit < 4) return pmp_set_err(ctx, PMP_ENOMEM, "pmp_astar2d_reserve: one wave exceeds the scratch budget");
         if ((size_t)workers > fit) workers = (int)(fit & ~(size_t)3);
         const int per_cu = ctx->astar_resident_per_cu > 0 ? ctx->astar_resident_per_cu : (workers + 255) / 256;

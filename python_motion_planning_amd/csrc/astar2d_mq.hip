@@ -29,12 +29,22 @@
 // array except every 15th query.  g of a CLOSED cell in a per-group f64 array (as astar2d.hip).
 #include "pmp_internal.h"
 
+// Diagnostic build only (make stamps): per-query cycle sums of the iteration's sections go to
+// counters[4q + 0..3] = {pop (issue to stores), expansion, push rounds, whole query} instead of the counts.
+#ifdef PMP_STAMPS
+#define MQ_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define MQ_STAMP(v)
+#endif
+
 namespace {
 
 constexpr double kSqrt2 = 1.4142135623730951;  // math.sqrt(2) == math.hypot(1, 1)
-constexpr int kMqCap = 32767;                   // positions 0..32766: levels 0..14
+constexpr int kMqCap = 32767;                   // positions 0..32766: levels 0..14 (tier 2 in HBM)
+constexpr int kMqCapT2L = 16383;                // positions 0..16382: levels 0..13 (tier 2 in LDS)
 constexpr int kBits01 = 144;                    // LDS bytes of bit tiers 0-1 (33 words) per group
-constexpr int kT2Words = 1024;                  // tier-2 bit blocks (levels 10-14) per group
+constexpr int kT2Words = 1024;                  // HBM tier-2 bit blocks (levels 10-14) per group
+constexpr int kT2LBytes = 1024;                 // LDS tier-2 bit blocks (levels 10-12, 7 bits each) per group
 
 // motions in the order of env.py:52-55: (-1,0),(-1,1),(0,1),(1,1),(1,0),(1,-1),(0,-1),(-1,-1)
 constexpr uint32_t kMx1 = 0x1A90u, kMy1 = 0x01A9u;
@@ -121,7 +131,7 @@ __device__ __forceinline__ void wave_sync_mem() { __builtin_amdgcn_fence(__ATOMI
 struct GHeap {
     lds_f64* F;      // LDS f[cap]
     lds_u32* C;      // LDS cm[cap]
-    lds_u32* B;      // LDS bit words: tier 0 (word 0), tier 1 (words 1..32)[, tier 2 (words 33..1056)]
+    lds_u32* B;      // LDS bit words: tier 0 (word 0), tier 1 (words 1..32)[, tier-2 bytes from word 36]
     uint32_t* T2;    // HBM tier-2 words (when not in LDS)
     __amdgpu_buffer_rsrc_t spill;  // the wave's spill region (4 groups)
     uint32_t soff;   // this group's byte offset in it
@@ -166,18 +176,49 @@ __device__ __forceinline__ void hst(const GHeap& h, bool on, int p, double f, ui
 
 // ---- direction bits (astar2d.hip: bit(p) = !(heap[2p+1] < heap[2p+2]) for nodes with two children,
 // 5-level blocks; node Pl (path number) at level L: tier t = L / 5, r = L - 5t, block root R = Pl >> r,
-// bit (Pl & (2^r - 1)) + 2^r - 1 of the block word)
-__device__ __forceinline__ uint32_t walk5(uint32_t w2)  // five steps from a block root, w2 = word << 1
-{
-    uint32_t pr = 1;
-#pragma unroll
-    for (int i = 0; i < 5; i++) pr = (pr << 1) | ((w2 >> pr) & 1u);
-    return pr;
-}
+// bit (Pl & (2^r - 1)) + 2^r - 1 of the block word).  With the tier-2 blocks in LDS (T2LDS) heaps stop
+// at level 13, so tier 2 only holds the bits of levels 10-12: 7 bits per block, one byte each.
+//
+// A walk through a block is found without a dependent chain: the bits define exactly one leaf whose
+// path they agree with, so each lane tests two candidate leaves of a 5-level block (one of a 3-level
+// block) against masks fixed per lane (Walk), and the row's ballot names the leaf.
+struct Walk {
+    uint32_t MA, VA, MB, VB, M3, V3;  // leaves gl and gl + 16 of a 5-level block; leaf gl & 7 of a 3-level one
+    __device__ __forceinline__ static void leaf(int L, int lev, uint32_t& M, uint32_t& V)
+    {
+        uint32_t pr = 1;
+        M = V = 0u;
+        for (int k = 0; k < lev; k++) {
+            const uint32_t b = (uint32_t)(L >> (lev - 1 - k)) & 1u;
+            M |= 1u << pr;
+            V |= b << pr;
+            pr = 2u * pr + b;
+        }
+    }
+    __device__ __forceinline__ void init(int gl)
+    {
+        leaf(gl, 5, MA, VA);
+        leaf(gl + 16, 5, MB, VB);
+        leaf(gl & 7, 3, M3, V3);
+    }
+    // path number (block-relative) after five / three steps from the block root; w2 = block word << 1
+    __device__ __forceinline__ uint32_t five(uint32_t w2, int gb) const
+    {
+        const uint32_t a = rbits((w2 & MA) == VA, gb), b = rbits((w2 & MB) == VB, gb);
+        return 32u + (uint32_t)(__ffs((int)(a | (b << 16))) - 1);
+    }
+    __device__ __forceinline__ uint32_t three(uint32_t w2, int gb) const
+    {
+        return 8u + (uint32_t)(__ffs((int)(rbits((w2 & M3) == V3, gb) & 0xFFu)) - 1);
+    }
+};
 template <bool T2LDS>
 __device__ __forceinline__ uint32_t t2_load(const GHeap& h, uint32_t R2)
 {
-    if (T2LDS) return h.B[33 + (R2 - 1024u)];
+    if (T2LDS) {
+        const uint32_t b = R2 - 1024u;
+        return (h.B[36u + (b >> 2)] >> (8u * (b & 3u))) & 0x7Fu;
+    }
     return __hip_atomic_load(h.T2 + (R2 - 1024u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // set (on lanes with `on`) the bit of node Pl at `level` to `bit`
@@ -195,7 +236,8 @@ __device__ __forceinline__ void bit_set(const GHeap& h, bool on, int level, uint
     } else if (t == 1) {
         ds_mskor(h.B + (R - 31u), m, bit ? m : 0u);
     } else if (T2LDS) {
-        ds_mskor(h.B + (33u + R - 1024u), m, bit ? m : 0u);
+        const uint32_t b = R - 1024u, sh = 8u * (b & 3u);
+        ds_mskor(h.B + (36u + (b >> 2)), m << sh, bit ? (m << sh) : 0u);
     } else {
         uint32_t* w = h.T2 + (R - 1024u);
         if (bit) __hip_atomic_fetch_or(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -216,9 +258,19 @@ __device__ __forceinline__ bool choice_bit(int child, double vf, uint32_t vc, do
 // heap_pop, per row: the _siftup path from the bits, one load round (lane i in 1..K: heap[p_i],
 // heap[p_{i+1}], sibling(p_i); lane 0: heap[n - 1]), a popcount placing `last`, the stores and
 // the bit rewrites of p_0..p_{m-1}.
+// What a pop wrote, for values loaded before it (the parents prefetched for the expansion's pushes):
+// the leaf's path number P and level K, the mover count m (p_{i-1} <- A_i for i <= m, p_m <- last)
+// and lane i's A_i = heap[p_i] before the pop.
+struct PopOut {
+    uint32_t P;
+    int K, m;
+    double Af;
+    uint32_t Ac;
+};
+
 template <bool T2LDS, int HEUR>
-__device__ __forceinline__ void heap_pop(const GHeap& h, int n, double& lastf, uint32_t& lastc, double& rootf,
-                                         uint32_t& rootc, int gl, int gb)
+__device__ __forceinline__ void heap_pop(const GHeap& h, const Walk& wk, int n, double& lastf, uint32_t& lastc,
+                                         double& rootf, uint32_t& rootc, int gl, int gb, PopOut& po)
 {
     const double lf = lastf;
     const uint32_t lc = lastc;
@@ -226,23 +278,23 @@ __device__ __forceinline__ void heap_pop(const GHeap& h, int n, double& lastf, u
     const int D = 31 - __clz(n);
     const int full = D - 1 < 0 ? 0 : D - 1;
     const uint32_t w0 = h.B[0] << 1;
-    const uint32_t pr0 = walk5(w0);                 // level-5 node (32..63) along the tier-0 bits
-    uint32_t w1 = 0u, w2 = 0u, pr1 = 32u, pr2 = 32u;
+    const uint32_t pr0 = wk.five(w0, gb);           // level-5 node (32..63) along the tier-0 bits
+    uint32_t w1 = 0u, w2 = 0u, pr1 = 32u, pr2 = T2LDS ? 8u : 32u;
     if (full >= 5) {
         w1 = h.B[pr0 - 31u] << 1;
-        pr1 = walk5(w1);
+        pr1 = wk.five(w1, gb);
     }
     const uint32_t R2 = (pr0 << 5) + pr1 - 32u;     // level-10 node (1024..2047)
     if (full >= 10) {
         w2 = t2_load<T2LDS>(h, R2) << 1;
-        pr2 = walk5(w2);
+        pr2 = T2LDS ? wk.three(w2, gb) : wk.five(w2, gb);
     }
     const int tf = full >= 10 ? 2 : (full >= 5 ? 1 : 0);
     const int rf = full - 5 * tf;
     const uint32_t wt = tf == 2 ? w2 : (tf == 1 ? w1 : w0);
     const uint32_t prt = tf == 2 ? pr2 : (tf == 1 ? pr1 : pr0);
     const uint32_t Rt = tf == 2 ? R2 : (tf == 1 ? pr0 : 1u);
-    const uint32_t prel = prt >> (5 - rf);
+    const uint32_t prel = prt >> ((tf == 2 && T2LDS ? 3 : 5) - rf);
     uint32_t P = (Rt << rf) + prel - (1u << rf);
     int K = D - 1 < 0 ? 0 : D - 1;
     if (2u * P <= (uint32_t)n) {
@@ -291,6 +343,11 @@ __device__ __forceinline__ void heap_pop(const GHeap& h, int n, double& lastf, u
         const bool bit = choice_bit<HEUR>(pi, useb ? Bf : lf, useb ? Bc : lc, Sf, Sc);
         bit_set<T2LDS>(h, hass && gl <= m, gl - 1, P >> (sh + 1), bit);
     }
+    po.P = P;
+    po.K = K;
+    po.m = m;
+    po.Af = Af;
+    po.Ac = Ac;
     wave_sync_mem();
 }
 
@@ -369,7 +426,7 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
     {
         unsigned char* base = smem + (size_t)grp * (size_t)region;
         hp.B = (lds_u32*)base;
-        const int bits_b = T2LDS ? kBits01 + 4 * kT2Words : kBits01;
+        const int bits_b = T2LDS ? kBits01 + kT2LBytes : kBits01;
         hp.F = (lds_f64*)(base + bits_b);
         hp.C = (lds_u32*)(base + bits_b + (size_t)8 * lds_cap);
         hp.T2 = t2_all + slot * kT2Words;
@@ -381,6 +438,8 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
     uint8_t* cst = cst_all + slot * cst_bytes;
     double* G = G_all + slot * ((size_t)W * (size_t)H);
 
+    Walk wk;
+    wk.init(gl);
     // per-lane constants: lane m < 8 of a row is motion m (offset, cost, isCollision's cells)
     const int mo = gl & 7;
     const int mx = mot_x(mo), my = mot_y(mo);
@@ -397,20 +456,20 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
     uint32_t ep = epoch_all[slot];
     bool need_q = true, done = false;
     int q = 0, qi = 0, sx = 0, sy = 0, gx = 0, gy = 0;
-    int n = 0, nexp = 0, maxn = 0, n0 = 0;
+    int n = 0, nexp = 0, maxn = 0;
     int64_t npush = 0, npop = 0;
+#ifdef PMP_STAMPS
+    uint64_t cy_pop = 0, cy_exp = 0, cy_push = 0, cy_q0 = 0;
+#endif
     double rootf = 0.0, lastf = 0.0;
     uint32_t rootc = 0u, lastc = 0u;
-    uint32_t pend = 0u;     // pending pushes of the current expansion (motion mask)
-    bool pc_ok = false;     // parents of n0 .. n0 + 7 held by lanes 0..7 (pf8, pc8)
-    double pf8 = 0.0, ifv = 0.0;
-    uint32_t pc8 = 0u, icm = 0u;
-    Ld pld;
-    pld.in = true;
-    pld.fl = 0.0;
-    pld.cl = 0u;
-    pld.v = make_uint4(0u, 0u, 0u, 0u);
 
+    // One iteration: every group with a query pops once (a_star.py:54) and expands the node
+    // (a_star.py:57-82); then rounds of pushes (a_star.py:76-80) run until every group has pushed the
+    // whole expansion: per round, the leading run of "trivial" pushes (the item is not less than its
+    // parent, so CPython's _siftdown stops at once: 73 % of C2's pushes) is stored in one step, then
+    // the next item, which moves, is pushed by the full sift.  The parents of the positions the
+    // pushes take are loaded before the pop (with the 3x3 round) and patched with what the pop wrote.
     for (;;) {
         // ---- groups without a query take the next one (or retire)
         const bool fetch_any = __ballot(need_q && !done) != 0ull;
@@ -458,10 +517,12 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
                     n = 1;
                     npush = 1;
                     npop = 0;
+#ifdef PMP_STAMPS
+                    cy_pop = cy_exp = cy_push = 0;
+                    cy_q0 = __builtin_amdgcn_s_memtime();
+#endif
                     nexp = 0;
                     maxn = 1;
-                    pend = 0u;
-                    pc_ok = false;
                     need_q = false;
                 }
             }
@@ -474,22 +535,29 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
         }
         if (__ballot(!done) == 0ull) break;
         const bool act = !done && !need_q;
+        MQ_STAMP(t0);
 
-        // ---- heappop + expansion (a_star.py:53-82) for the groups with no pending push
         int st = -1;  // >= 0: the query ends this iteration with this status
         double goal_cost = 0.0;
         int plen = 0;
-        const bool dopop = act && pend == 0u && n > 0;
-        if (act && pend == 0u && n == 0) st = PMP_NO_PATH;  // OPEN exhausted (a_star.py:83)
-        if (dopop) {
+        uint32_t pend = 0u;   // the expansion's pushes still to do (motion mask, in motion order)
+        double ifv = 0.0;     // lane m < 8: the item of motion m (f, code)
+        uint32_t icm = 0u;
+        bool pc_ok = false;   // lanes 0..7 hold heap[parent(n0 + lane)] (pf8, pc8)
+        double pf8 = 0.0;
+        uint32_t pc8 = 0u;
+        int n0 = 0;
+        if (act && n == 0) st = PMP_NO_PATH;  // OPEN exhausted (a_star.py:83)
+        if (act && n > 0) {
+            // ---- heappop (a_star.py:54), with the 3x3 round and the parent prefetch issued first
             const uint32_t ncm = rootc;
             npop++;
             n -= 1;
+            n0 = n;
             const int ndir = cm_dir(ncm);
             const int x = ndir == 8 ? sx : gx - cm_dx(ncm);
             const int y = ndir == 8 ? sy : gy - cm_dy(ncm);
             const uint32_t nlin = (uint32_t)x * (uint32_t)H + (uint32_t)y;
-            // the 3x3 round, issued before the LDS pop so the two overlap
             uint32_t blk_w = 0u, blk_w2 = 0u;
             int blk_sh = 0;
             bool blk_in = false;
@@ -514,8 +582,42 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
                     gpar = G[nlin - (uint32_t)(mot_x(ndir) * H + mot_y(ndir))];
                 }
             }
-            if (n > 0) heap_pop<T2LDS, HEUR>(hp, n, lastf, lastc, rootf, rootc, gl, gb);
-            // 3x3 masks: bit k = cell (x + k/3 - 1, y + k%3 - 1)
+            // the pushes take positions n0, n0 + 1, ...: their parents, while all 8 share a depth
+            pc_ok = n0 > 0 && (31 - __clz(n0 + 1)) == (31 - __clz(n0 + 8));
+            const int pp = (n0 + (gl & 7) - 1) >> 1;
+            Ld pld;
+            pld.issue(hp, pc_ok && gl < 8 ? pp : 0);
+            PopOut po;
+            po.K = -1;
+            po.m = -1;
+            po.P = 0u;
+            po.Af = 0.0;
+            po.Ac = 0u;
+            const double lf0 = lastf;  // the old last element, which the pop places at p_m
+            const uint32_t lc0 = lastc;
+            if (n > 0) heap_pop<T2LDS, HEUR>(hp, wk, n, lastf, lastc, rootf, rootc, gl, gb, po);
+            pld.get(pf8, pc8);
+            {
+                // patch the prefetched parents: the pop moved heap[p_{L+1}] into path node p_L (L < m)
+                // and the old last element into p_m
+                const int L = 31 - __clz(pp + 1);
+                const bool onp = pc_ok && gl < 8 && po.K >= 0 && L >= 0 && L <= po.m &&
+                                 (int)(po.P >> (po.K - L)) - 1 == pp;
+                const int src = gb + (L + 1 < 16 ? L + 1 : 15);
+                const double af = bpf(po.Af, src);
+                const uint32_t ac = bp(po.Ac, src);
+                if (onp) {
+                    pf8 = L < po.m ? af : lf0;
+                    pc8 = L < po.m ? ac : lc0;
+                }
+            }
+#ifdef PMP_STAMPS
+            {
+                const uint64_t t1 = __builtin_amdgcn_s_memtime();
+                cy_pop += t1 - t0;
+            }
+#endif
+            // ---- 3x3 masks: bit k = cell (x + k/3 - 1, y + k%3 - 1)
             const uint32_t occ9 = rbits(gl < 9 && (!blk_in || ((blk_w >> blk_sh) & 1u)), gb) & 0x1FFu;
             uint32_t row = 0u;
             if (gl >= 9 && gl < 12 && blk_in) {
@@ -568,61 +670,79 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
                     const double ig = gnode + mcost;
                     icm = pack_cm<HEUR>(ndx, ndy, mo);
                     ifv = ig + h_of_key<HEUR>(hkey<HEUR>(icm));
-                    pend = vm;
-                    // the parents of the positions the pushes take (n .. n + 7), one round, valid
-                    // while those positions share a depth (astar2d.hip)
-                    n0 = n;
-                    pc_ok = vm != 0u && n > 0 && (31 - __clz(n + 1)) == (31 - __clz(n + 8));
-                    if (pc_ok) pld.issue(hp, gl < 8 ? ((n + gl - 1) >> 1) : 0);
+                    if (n + __popc(vm) > heap_cap) st = PMP_CAP_OVERFLOW;  // a push would find n >= heap_cap
+                    else pend = vm;
                 }
             }
         }
 
-        // ---- one push per group with pending pushes (not in the iteration that expanded)
-        const bool dopush = act && !dopop && pend != 0u;
-        if (dopush) {
-            const int m = __ffs((int)pend) - 1;
-            pend &= pend - 1u;
-            if (n >= heap_cap) {
-                st = PMP_CAP_OVERFLOW;
-            } else {
-                const double itf = bpf(ifv, gb + m);
-                const uint32_t itc = bp(icm, gb + m);
-                const uint32_t itk = hkey<HEUR>(itc);
-                double pf, dummyf;
-                uint32_t pc, dummyc;
-                pld.get(dummyf, dummyc);
-                pf8 = dummyf;
-                pc8 = dummyc;
-                pf = bpf(pf8, gb + (n - n0));
-                pc = bp(pc8, gb + (n - n0));
-                if (pc_ok && !key_lt(itf, itk, pf, hkey<HEUR>(pc))) {
-                    // trivial push: heap[n] = item; a right child sets its parent's bit against
-                    // its left sibling heap[n - 1] = last
-                    const uint32_t np1 = (uint32_t)n + 1u;
-                    bit_set<T2LDS>(hp, gl == 0 && (n & 1) == 0, 30 - __clz(n + 1), np1 >> 1,
-                                   !key_lt(lastf, hkey<HEUR>(lastc), itf, itk));
-                    hst(hp, gl == 0, n, itf, itc);
-                    lastf = itf;
-                    lastc = itc;
+        MQ_STAMP(t2);
+#ifdef PMP_STAMPS
+        if (act && n0 >= 0) cy_exp += t2 - t0;
+#endif
+        // ---- push rounds (a_star.py:76-80) until every group has pushed its expansion
+        while (__ballot(pend != 0u) != 0ull) {
+            if (pend != 0u) {
+                const uint32_t mine = (pend >> mo) & 1u;  // lane m < 8: my item is pending
+                const uint32_t below = pend & ((1u << mo) - 1u);
+                const int rank = __popc(below);
+                const int pos = n + rank;
+                const uint32_t ik = hkey<HEUR>(icm);
+                // the leading run of trivial pushes (needs the parents; a small heap has none cached)
+                uint32_t run = 0u;
+                if (pc_ok) {
+                    const int pl = gb + (pos - n0 < 8 ? pos - n0 : 7);
+                    const double pf = bpf(pf8, pl);
+                    const uint32_t pc = bp(pc8, pl);
+                    const bool triv = gl < 8 && mine && !key_lt(ifv, ik, pf, hkey<HEUR>(pc));
+                    const uint32_t tm = rbits(triv, gb) & 0xFFu;
+                    const uint32_t nt = pend & ~tm;
+                    run = nt ? pend & ((nt & (0u - nt)) - 1u) : pend;
+                }
+                if (run != 0u) {
+                    // store the run: heap[pos] = item; a right child sets its parent's bit against its
+                    // left sibling (the previous item of the run, or `last`)
+                    const bool inrun = gl < 8 && ((run >> mo) & 1u);
+                    const int prev = below ? 31 - __clz(below) : 0;
+                    const double lfp = bpf(ifv, gb + prev);
+                    const uint32_t lcp = bp(icm, gb + prev);
+                    const double leftf = rank == 0 ? lastf : lfp;
+                    const uint32_t leftc = rank == 0 ? lastc : lcp;
+                    bit_set<T2LDS>(hp, inrun && (pos & 1) == 0 && pos > 0, 30 - __clz(pos + 1), (uint32_t)(pos + 1) >> 1,
+                                   !key_lt(leftf, hkey<HEUR>(leftc), ifv, ik));
+                    hst(hp, inrun, pos, ifv, icm);
+                    const int top = 31 - __clz(run);
+                    lastf = bpf(ifv, gb + top);
+                    lastc = bp(icm, gb + top);
+                    const int k = __popc(run);
+                    n += k;
+                    npush += k;
+                    pend &= ~run;
                     wave_sync_mem();
-                } else {
+                }
+                if (pend != 0u) {
+                    // the first remaining item moves up: the full _siftdown
+                    const int m = __ffs((int)pend) - 1;
+                    pend &= pend - 1u;
+                    const double itf = bpf(ifv, gb + m);
+                    const uint32_t itc = bp(icm, gb + m);
                     double a1f;
                     uint32_t a1c;
-                    heap_push<T2LDS, HEUR>(hp, n, itf, itc, itk, lastf, lastc, rootf, rootc, gl, gb, a1f, a1c);
+                    heap_push<T2LDS, HEUR>(hp, n, itf, itc, hkey<HEUR>(itc), lastf, lastc, rootf, rootc, gl, gb, a1f, a1c);
                     // a left child's right sibling (the next position) has the same parent, now a1
                     if (pc_ok && (n & 1) && gl == n - n0 + 1) {
-                        pld.fl = a1f;
-                        pld.cl = a1c;
-                        pld.in = true;
-                        pld.v = make_uint4(0u, 0u, 0u, 0u);
+                        pf8 = a1f;
+                        pc8 = a1c;
                     }
+                    n += 1;
+                    npush++;
                 }
-                n += 1;
-                npush++;
-                if (n > maxn) maxn = n;
             }
         }
+        if (n > maxn) maxn = n;
+#ifdef PMP_STAMPS
+        if (act) cy_push += __builtin_amdgcn_s_memtime() - t2;
+#endif
 
         // ---- the groups whose query ended: results, then a new query next iteration
         if (st >= 0) {
@@ -634,14 +754,20 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
                 path_len_out[q] = st == PMP_FOUND ? plen : 0;
                 nexp_out[q] = nexp;
                 if (counters) {
+#ifdef PMP_STAMPS
+                    counters[4 * q + 0] = (int64_t)cy_pop;
+                    counters[4 * q + 1] = (int64_t)(cy_exp - cy_pop);
+                    counters[4 * q + 2] = (int64_t)cy_push;
+                    counters[4 * q + 3] = (int64_t)(__builtin_amdgcn_s_memtime() - cy_q0);
+#else
                     counters[4 * q + 0] = npush;
                     counters[4 * q + 1] = npop;
                     counters[4 * q + 2] = nexp;
                     counters[4 * q + 3] = maxn;
+#endif
                 }
             }
             need_q = true;
-            pend = 0u;
         }
     }
     if (gl == 0) epoch_all[slot] = ep;
@@ -665,9 +791,10 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
     const int waves = (groups + 3) / 4;
     const int lds_cap = ctx->astar_lds_cap;
     const bool t2lds = ctx->astar_mq_t2lds != 0;
-    const int bits_b = t2lds ? kBits01 + 4 * kT2Words : kBits01;
+    const int bits_b = t2lds ? kBits01 + kT2LBytes : kBits01;
     const int region = bits_b + 12 * lds_cap;
-    const int heap_cap = ctx->astar_heap_cap < kMqCap ? ctx->astar_heap_cap : kMqCap;
+    const int cap_max = t2lds ? kMqCapT2L : kMqCap;
+    const int heap_cap = ctx->astar_heap_cap < cap_max ? ctx->astar_heap_cap : cap_max;
     const int spill_n = heap_cap > lds_cap ? heap_cap - lds_cap : 1;
     const size_t cst_bytes = mq_cst_bytes(W, H);
     const size_t ncell = (size_t)W * H;
@@ -713,11 +840,11 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
 // LDS heap positions per group for `per_cu` groups resident per CU (each CU's 160 KiB shared)
 int pmp_astar2d_mq_lds_cap(int per_cu, bool t2lds)
 {
-    const int bits_b = t2lds ? kBits01 + 4 * kT2Words : kBits01;
+    const int bits_b = t2lds ? kBits01 + kT2LBytes : kBits01;
     // a workgroup is one wave = 4 groups, and may hold at most the CU's 160 KiB
     int bytes = (160 * 1024) / (per_cu < 4 ? 4 : per_cu) - 160 - bits_b;
     int cap = (bytes / 12) & ~15;
     if (cap > kMqCap) cap = kMqCap & ~15;
     return cap;
 }
-int pmp_astar2d_mq_cap() { return kMqCap; }
+int pmp_astar2d_mq_cap(bool t2lds) { return t2lds ? kMqCapT2L : kMqCap; }

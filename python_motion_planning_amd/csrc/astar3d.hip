@@ -544,7 +544,8 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     if (workers > nq) workers = nq;
     const size_t words = (ncell + 31) / 32;
     bool occ_lds = words <= (size_t)kOccLdsWords;
-    int occ_bytes = occ_lds ? kOccLdsWords * 4 : 0;
+    // the query's bitmap in LDS takes its own size (C5: 260 words), the rest of the share is heap
+    int occ_bytes = occ_lds ? (int)((words * 4 + 15) & ~(size_t)15) : 0;
     int lds_cap = pmp_heap_lds_cap(ctx, per_cu, occ_bytes, 16);
     if (lds_cap < kMinLdsHeap && occ_lds) {  // the LDS share cannot hold the occupancy too: keep it in HBM
         occ_lds = false;

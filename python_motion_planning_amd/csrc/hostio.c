@@ -12,6 +12,7 @@
  */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
+#include <structmember.h>
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
@@ -103,42 +104,87 @@ static PyObject* set_to_words(PyObject* self, PyObject* args)
     return PyLong_FromLongLong(count);
 }
 
-/* open-addressing map cell -> g (a new reference) */
+/* open-addressing map cell -> (g, current tuple) of a CLOSED node (new references) */
 typedef struct {
     uint32_t* key;
-    PyObject** val;
+    PyObject** val;  /* g */
+    PyObject** cur;  /* the node's current tuple: the parent tuple of the nodes it closes */
     size_t mask;
 } gmap_t;
 
-static PyObject* gmap_get(const gmap_t* m, uint32_t k)
+static Py_ssize_t gmap_find(const gmap_t* m, uint32_t k)
 {
     size_t i = ((size_t)k * 0x9E3779B1u) & m->mask;
     while (m->val[i]) {
-        if (m->key[i] == k) return m->val[i];
+        if (m->key[i] == k) return (Py_ssize_t)i;
         i = (i + 1) & m->mask;
     }
-    return NULL;
+    return -1;
 }
 
-static void gmap_put(gmap_t* m, uint32_t k, PyObject* v) /* steals v */
+static void gmap_put(gmap_t* m, uint32_t k, PyObject* g, PyObject* cur) /* new references taken */
 {
     size_t i = ((size_t)k * 0x9E3779B1u) & m->mask;
     while (m->val[i]) {
         if (m->key[i] == k) {
             Py_DECREF(m->val[i]);
-            m->val[i] = v;
+            Py_DECREF(m->cur[i]);
+            m->val[i] = g;
+            m->cur[i] = cur;
             return;
         }
         i = (i + 1) & m->mask;
     }
     m->key[i] = k;
-    m->val[i] = v;
+    m->val[i] = g;
+    m->cur[i] = cur;
+}
+
+static PyObject* pair(long long a, long long b)
+{
+    PyObject* t = PyTuple_New(2);
+    if (!t) return NULL;
+    PyObject* x = PyLong_FromLongLong(a);
+    PyObject* y = x ? PyLong_FromLongLong(b) : NULL;
+    if (!y) {
+        Py_XDECREF(x);
+        Py_DECREF(t);
+        return NULL;
+    }
+    PyTuple_SET_ITEM(t, 0, x);
+    PyTuple_SET_ITEM(t, 1, y);
+    return t;
+}
+
+/* Byte offsets of the __slots__ members current, parent, g, h of node_cls (object members of its
+ * instance layout), or 0 when the class does not keep them as plain slots: then every node is built by
+ * calling the class. */
+static int slot_offsets(PyObject* cls, Py_ssize_t off[4])
+{
+    static const char* names[4] = {"current", "parent", "g", "h"};
+    if (!PyType_Check(cls)) return 0;
+    for (int k = 0; k < 4; k++) {
+        PyObject* d = PyObject_GetAttrString(cls, names[k]);
+        if (!d) {
+            PyErr_Clear();
+            return 0;
+        }
+        const int ok = Py_IS_TYPE(d, &PyMemberDescr_Type) &&
+                       ((PyMemberDescrObject*)d)->d_member->type == T_OBJECT_EX;
+        off[k] = ok ? ((PyMemberDescrObject*)d)->d_member->offset : 0;
+        Py_DECREF(d);
+        if (!ok) return 0;
+    }
+    return 1;
 }
 
 /* expand_nodes(records uint32 buffer, n, H, motions_xy (8 (dx, dy) tuples), motion_g (8 objects),
  *              goal (gx, gy), kind, node_cls) -> list of node_cls(current, parent, g, h)
  * kind: 0 AStar euclidean, 1 AStar manhattan, 2 Dijkstra (h = 0), 3 GBFS euclidean (g = 0),
- *       4 GBFS manhattan.  Record: cell | dir << 28, dir 8 = the start (parent = itself, g = h = 0). */
+ *       4 GBFS manhattan.  Record: cell | dir << 28, dir 8 = the start (parent = itself, g = h = 0).
+ * The drop-in Node keeps its fields in __slots__, so the objects are allocated and filled directly
+ * (the attributes node_cls.__init__ would set, without running it per node); a node's parent tuple is
+ * the CLOSED parent's own current tuple (equal, as the reference's). */
 static PyObject* expand_nodes(PyObject* self, PyObject* args)
 {
     PyObject *rec_o, *mxy, *mg_o, *goal_o, *cls;
@@ -183,19 +229,25 @@ static PyObject* expand_nodes(PyObject* self, PyObject* args)
             return NULL;
         }
     }
+    Py_ssize_t off[4];
+    const int direct = slot_offsets(cls, off);
+    PyTypeObject* tp = (PyTypeObject*)cls;
     size_t cap = 16;
     while (cap < 2 * (size_t)n + 2) cap <<= 1;
     gmap_t gm;
     gm.key = (uint32_t*)PyMem_Calloc(cap, sizeof(uint32_t));
     gm.val = (PyObject**)PyMem_Calloc(cap, sizeof(PyObject*));
+    gm.cur = (PyObject**)PyMem_Calloc(cap, sizeof(PyObject*));
     gm.mask = cap - 1;
     PyObject* zero = PyLong_FromLong(0);
     PyObject* list = PyList_New(n);
-    int ok = gm.key && gm.val && zero && list;
+    int ok = gm.key && gm.val && gm.cur && zero && list;
+    /* tens of thousands of new container objects: no cyclic-GC passes while they are made */
+    const int gc_was = PyGC_Disable();
     for (Py_ssize_t i = 0; ok && i < n; i++) {
         const uint32_t e = rec[i], cell = e & 0x0FFFFFFFu, d = e >> 28;
         const long long x = cell / (uint32_t)H, y = cell % (uint32_t)H;
-        PyObject* cur = Py_BuildValue("(LL)", x, y);
+        PyObject* cur = pair(x, y);
         PyObject *par = NULL, *g = NULL, *h = NULL;
         if (!cur) { ok = 0; break; }
         if (d == 8) {
@@ -207,14 +259,26 @@ static PyObject* expand_nodes(PyObject* self, PyObject* args)
             Py_INCREF(h);
         } else if (d < 8) {
             const long long px = x - mx[d], py = y - my[d];
-            par = Py_BuildValue("(LL)", px, py);
+            const Py_ssize_t pi = gmap_find(&gm, (uint32_t)(px * H + py));
+            if (pi >= 0) {
+                par = gm.cur[pi];
+                Py_INCREF(par);
+            } else {
+                par = pair(px, py);
+            }
             if (kind == 3 || kind == 4) {  /* gbfs.py:75: node_n.g = 0 */
                 g = zero;
                 Py_INCREF(g);
+            } else if (pi >= 0) {
+                /* Python's `+` (node.py:39-41), with the int / float cases done here */
+                PyObject *ga = gm.val[pi], *gb = mg[d];
+                if (PyFloat_CheckExact(ga) && (PyFloat_CheckExact(gb) || PyLong_CheckExact(gb)))
+                    g = PyFloat_FromDouble(PyFloat_AS_DOUBLE(ga) +
+                                           (PyFloat_CheckExact(gb) ? PyFloat_AS_DOUBLE(gb) : PyLong_AsDouble(gb)));
+                else
+                    g = PyNumber_Add(ga, gb);
             } else {
-                PyObject* gp = gmap_get(&gm, (uint32_t)(px * H + py));
-                g = gp ? PyNumber_Add(gp, mg[d]) : NULL;
-                if (!gp && !PyErr_Occurred()) PyErr_SetString(PyExc_RuntimeError, "expand record before its parent");
+                if (!PyErr_Occurred()) PyErr_SetString(PyExc_RuntimeError, "expand record before its parent");
             }
             if (kind == 2) {  /* dijkstra.py:74: node_n.h = 0 */
                 h = zero;
@@ -228,10 +292,25 @@ static PyObject* expand_nodes(PyObject* self, PyObject* args)
         } else {
             PyErr_SetString(PyExc_ValueError, "bad expand record");
         }
-        PyObject* node = (par && g && h) ? PyObject_CallFunctionObjArgs(cls, cur, par, g, h, NULL) : NULL;
+        PyObject* node = NULL;
+        if (par && g && h) {
+            if (direct) {
+                node = tp->tp_alloc(tp, 0);
+                if (node) {
+                    PyObject* v[4] = {cur, par, g, h};
+                    for (int k = 0; k < 4; k++) {
+                        Py_INCREF(v[k]);
+                        *(PyObject**)((char*)node + off[k]) = v[k];
+                    }
+                }
+            } else {
+                node = PyObject_CallFunctionObjArgs(cls, cur, par, g, h, NULL);
+            }
+        }
         if (node) {
             Py_INCREF(g);
-            gmap_put(&gm, cell, g);
+            Py_INCREF(cur);
+            gmap_put(&gm, cell, g, cur);
             PyList_SET_ITEM(list, i, node);
         } else {
             ok = 0;
@@ -241,10 +320,15 @@ static PyObject* expand_nodes(PyObject* self, PyObject* args)
         Py_XDECREF(g);
         Py_XDECREF(h);
     }
+    if (gc_was) PyGC_Enable();
     if (gm.val)
-        for (size_t i = 0; i < cap; i++) Py_XDECREF(gm.val[i]);
+        for (size_t i = 0; i < cap; i++) {
+            Py_XDECREF(gm.val[i]);
+            if (gm.cur) Py_XDECREF(gm.cur[i]);
+        }
     PyMem_Free(gm.key);
     PyMem_Free(gm.val);
+    PyMem_Free(gm.cur);
     Py_XDECREF(zero);
     for (int d = 0; d < 8; d++) Py_DECREF(mg[d]);
     PyBuffer_Release(&buf);

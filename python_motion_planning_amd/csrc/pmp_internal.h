@@ -69,7 +69,7 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
                           int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded, uint32_t* expand,
                           int expand_cap, int64_t* counters, int32_t* status, int* queue);
 int pmp_astar2d_mq_lds_cap(int per_cu, bool t2lds);
-int pmp_astar2d_mq_cap();
+int pmp_astar2d_mq_cap(bool t2lds);
 
 #define PMP_HIP_CHECK(ctx, call)                                                                     \
     do {                                                                                             \
