@@ -1436,8 +1436,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--agents", type=int, default=256, help="C4 agents per GPU (control-step leg)")
     ap.add_argument("--control-steps", type=int, default=20, help="timed control steps")
-    ap.add_argument("--engine", type=int, default=1, choices=[0, 1],
-                    help="A* 2D engine: 1 = four queries per wave (astar2d_mq.hip), 0 = one query per wave (astar2d.hip)")
+    ap.add_argument("--engine", type=int, default=1, choices=[0, 1, 2],
+                    help="A* 2D engine: 1 = four queries per wave (astar2d_mq.hip) for the C2 batches, 2 = that for "
+                         "every batch, 0 = one query per wave (astar2d.hip)")
     ap.add_argument("--t2lds", type=int, default=1,
                     help="multi-query engine: level-10..12 heap bits in LDS (1; heaps <= 16383) or level-10..14 in HBM (0)")
     ap.add_argument("--workers", type=int, default=0,
@@ -1510,9 +1511,9 @@ def main():
     # engine defaults (tools/sweep_residency.sh): engine 1 -- 6 x 2048 groups in flight, 48 per CU;
     # engine 0 -- 6 x 768 waves, 18 per CU (round 2)
     if not args.workers:
-        args.workers = 8192 if args.engine == 1 else 768
+        args.workers = 8192 if args.engine else 768
     if not args.residency:
-        args.residency = 32 if args.engine == 1 else 18
+        args.residency = 32 if args.engine else 18
     if not args.batches_per_launch and args.engine == 0:
         args.batches_per_launch = 1
 
@@ -1758,7 +1759,7 @@ def main():
                        "max_heap_entries": int(counters[:, 3].max()),
                        "expansions_all_ranks_per_step": int(counters_all[:, 2].sum()) if args.scaling == "strong" else None,
                        "strong_scaling_gather": gathered,
-                       "engine": "multi-query (4 per wave, astar2d_mq.hip)" if args.engine == 1 else
+                       "engine": "multi-query (4 per wave, astar2d_mq.hip)" if args.engine else
                                  "one query per wave (astar2d.hip)", "t2_lds": args.t2lds,
                        "queries_in_flight_per_launch": args.workers, "streams": S, "priority_queries": args.prio,
                        "resident_per_cu": args.residency,

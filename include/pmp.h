@@ -468,12 +468,15 @@ int pmp_astar2d_set_priority(pmp_ctx* ctx, int n_high);
 int pmp_astar2d_set_residency(pmp_ctx* ctx, int per_cu);
 
 /* A* 2D engine of the context (replaces nothing in the reference: a scheduling knob of
- * AStar.plan / Dijkstra.plan / GBFS.plan, a_star.py:39-83).  engine 1 (default): four queries per
- * wave, one per 16-lane row, for A* / Dijkstra / GBFS whose heaps stay within 32,767 entries (a
- * query that outgrows it reports PMP_CAP_OVERFLOW; re-reserving with a larger heap_cap selects
- * engine 0); t2_lds = keep its level-10..14 heap direction bits in LDS (1) or HBM (0).  engine 0:
- * one query per wave (also Theta* / Lazy Theta*, and heaps of any size).  Results are identical.
- * Applies to the next launch (re-reserves the scratch geometry when one is set). */
+ * AStar.plan / Dijkstra.plan / GBFS.plan, a_star.py:39-83).  engine 2: four queries per wave, one
+ * per 16-lane row, for A* / Dijkstra / GBFS whose heaps stay within 32,767 entries (a query that
+ * outgrows it reports PMP_CAP_OVERFLOW; re-reserving with a larger heap_cap selects engine 0);
+ * t2_lds = keep its level-10..14 heap direction bits in LDS (1) or HBM (0).  engine 0: one query per
+ * wave (also Theta* / Lazy Theta*, and heaps of any size); on grids whose occupancy, cell state and
+ * g fit in a wave's LDS share beside its heap (the README grid: 14 KB) all of them live in LDS.
+ * engine 1 (default): engine 2 for batches of >= 1024 queries on grids too large for that, engine 0
+ * otherwise (a single query's latency: the drop-in AStar.plan).  Results are identical.  Applies to
+ * the next launch (re-reserves the scratch geometry when one is set). */
 int pmp_astar2d_set_engine(pmp_ctx* ctx, int engine, int t2_lds);
 
 /* Persistent workers (one wave each) per CU of the one-wave-per-query planners: pmp_graph3d_batch,

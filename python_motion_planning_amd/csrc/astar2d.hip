@@ -583,12 +583,31 @@ __device__ bool los2d(const uint32_t* occ, int H, int x1, int y1, int x2, int y2
 }
 
 // 4-bit cell state: word i >> 3, nibble i & 7
-__device__ __forceinline__ uint32_t cst_at(const uint32_t* cst, uint32_t i) { return (cst[i >> 3] >> ((i & 7) * 4)) & 15u; }
+template <typename P>
+__device__ __forceinline__ uint32_t cst_at(P cst, uint32_t i) { return (cst[i >> 3] >> ((i & 7) * 4)) & 15u; }
+
+// LDSG (small grids): the worker's occupancy bits, cell-state nibbles and G live in its LDS share
+// behind the heap, so an expansion's 3x3 round, G[parent] and the CLOSED write are LDS accesses (one
+// query's latency is a chain of these rounds: the drop-in single-query path)
+template <bool LDSG> struct GridMem {
+    typedef const uint32_t* Occ;
+    typedef uint32_t* Cst;
+    typedef double* Gv;
+};
+template <> struct GridMem<true> {
+    typedef const lds_u32* Occ;
+    typedef lds_u32* Cst;
+    typedef lds_f64* Gv;
+};
+// LDS bytes of the LDSG grid block (occupancy words, state words, G), each part 16-B aligned
+__host__ __device__ constexpr size_t ldsg_occ_bytes(size_t ncell) { return (((ncell + 31) / 32) * 4 + 15) & ~(size_t)15; }
+__host__ __device__ constexpr size_t ldsg_cst_words(size_t ncell) { return ((ncell + 7) / 8 + 3) & ~(size_t)3; }
+__host__ __device__ constexpr size_t ldsg_bytes(size_t ncell) { return ldsg_occ_bytes(ncell) + ldsg_cst_words(ncell) * 4 + ncell * 8; }
 
 // GZERO: GBFS (gbfs.py:73-75) -- every pushed node gets g = 0, so f = h and G is never needed.
 // THETA: 1 = ThetaStar (theta_star.py:44-108), 2 = LazyThetaStar (lazy_theta_star.py:38-114); the
 // parent of a node is any cell, kept per CLOSED cell in P_all (HEUR carries the Theta* layout).
-template <int HEUR, bool GZERO, int THETA>
+template <int HEUR, bool GZERO, int THETA, bool LDSG = false>
 __global__ __launch_bounds__(64) void astar2d_kernel(
     const uint32_t* __restrict__ occ, int W, int H, const int32_t* __restrict__ start_xy,
     const int32_t* __restrict__ goal_xy, const int32_t* __restrict__ order, int nq, double* __restrict__ cost_out,
@@ -613,8 +632,24 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
         hp.spill = __builtin_amdgcn_make_buffer_rsrc(spill_all + (size_t)worker * spill_n, 0, (int)(spill_n * 16), 0x00020000);
     }
     hp.cap = lds_cap;
-    uint32_t* cst = cst_all + (size_t)worker * cst_words;
-    double* G = G_all + (size_t)worker * ((size_t)W * (size_t)H);
+    typename GridMem<LDSG>::Occ occg;
+    typename GridMem<LDSG>::Cst cst;
+    typename GridMem<LDSG>::Gv G;
+    if constexpr (LDSG) {
+        // grid block after the heap: occupancy (copied once per worker), state words, G
+        const size_t ncell = (size_t)W * (size_t)H;
+        unsigned char* gb = smem + kBitsLdsBytes + (size_t)12 * lds_cap;
+        lds_u32* ow = (lds_u32*)gb;
+        const uint32_t nw = (uint32_t)((ncell + 31) / 32);
+        for (uint32_t i = lane; i < nw; i += 64) ow[i] = occ[i];
+        occg = ow;
+        cst = (lds_u32*)(gb + ldsg_occ_bytes(ncell));
+        G = (lds_f64*)(gb + ldsg_occ_bytes(ncell) + ldsg_cst_words(ncell) * 4);
+    } else {
+        occg = occ;
+        cst = cst_all + (size_t)worker * cst_words;
+        G = G_all + (size_t)worker * ((size_t)W * (size_t)H);
+    }
     uint32_t* Pc = THETA ? P_all + (size_t)worker * ((size_t)W * (size_t)H) : nullptr;  // CLOSED parent cell
 
     // ---- per-lane constants
@@ -647,7 +682,9 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
         else __builtin_amdgcn_s_setprio(0);
 
         // reset this worker's cell-state array
-        {
+        if constexpr (LDSG) {
+            for (size_t i = lane; i < cst_words; i += 64) cst[i] = 0u;
+        } else {
             uint4* c4 = reinterpret_cast<uint4*>(cst);
             const size_t n4 = cst_words / 4;
             for (size_t i = lane; i < n4; i += 64) c4[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -709,7 +746,7 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 const int cx = x + blk_dx, cy = y + blk_dy;
                 blk_in = lane < 18 && (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
                 const uint32_t ci = blk_in ? (uint32_t)cx * (uint32_t)H + (uint32_t)cy : 0u;
-                const uint32_t* ptr = lane < 9 ? occ + (ci >> 5) : cst + (ci >> 3);
+                const auto ptr = lane < 9 ? occg + (ci >> 5) : cst + (ci >> 3);
                 blk_sh = lane < 9 ? (ci & 31u) : (ci & 7u) * 4u;
                 blk_word = *ptr;
             }
@@ -1053,16 +1090,15 @@ int lpt_order2d(pmp_ctx* ctx, hipStream_t s, const int32_t* start_xy, const int3
 // The multi-query engine (astar2d_mq.hip) serves A* / Dijkstra / GBFS when the context selects it
 // and the reserved heap capacity fits its limit (a query that outgrows it is re-run by the host with
 // the full bound, which selects this file's engine).
-extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int workers, int heap_cap)
+static int astar2d_reserve_impl(pmp_ctx* ctx, int W, int H, int workers, int heap_cap)
 {
-    if (!ctx) return PMP_EINVAL;
     if (W < 1 || H < 1 || W > kMaxDim || H > kMaxDim || workers < 1)
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_reserve: bad dims/workers");
     if (heap_cap <= 0) heap_cap = default_heap_cap(W, H);
     if ((size_t)heap_cap > max_heap(W, H)) heap_cap = (int)max_heap(W, H);
-    if (ctx->astar_engine == 1 && heap_cap <= 65536 && heap_cap > pmp_astar2d_mq_cap(ctx->astar_mq_t2lds != 0))
+    if (ctx->astar_engine >= 1 && heap_cap <= 65536 && heap_cap > pmp_astar2d_mq_cap(ctx->astar_mq_t2lds != 0))
         heap_cap = pmp_astar2d_mq_cap(ctx->astar_mq_t2lds != 0);  // the default capacity on the multi-query engine
-    if (ctx->astar_engine == 1 && heap_cap <= pmp_astar2d_mq_cap(ctx->astar_mq_t2lds != 0)) {
+    if (ctx->astar_engine >= 1 && heap_cap <= pmp_astar2d_mq_cap(ctx->astar_mq_t2lds != 0)) {
         // workers = queries in flight (16-lane groups, 4 per wave); scratch is taken at launch
         const size_t per_slot = (size_t)W * H * 9 + (size_t)pmp_astar2d_mq_cap(ctx->astar_mq_t2lds != 0) * 16 + 4096 + 256;
         const size_t fit = kScratchBudgetMq / per_slot;
@@ -1110,15 +1146,25 @@ extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int workers, int 
     return PMP_OK;
 }
 
+extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int workers, int heap_cap)
+{
+    if (!ctx) return PMP_EINVAL;
+    const int rc = astar2d_reserve_impl(ctx, W, H, workers, heap_cap);
+    if (rc == PMP_OK) ctx->astar_auto = 0;  // the host's own geometry: launches keep it
+    return rc;
+}
+
 extern "C" int pmp_astar2d_set_engine(pmp_ctx* ctx, int engine, int t2_lds)
 {
     if (!ctx) return PMP_EINVAL;
-    if (engine != 0 && engine != 1)
-        return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_set_engine: engine must be 0 (one query per wave) or 1 (multi-query)");
+    if (engine < 0 || engine > 2)
+        return pmp_set_err(ctx, PMP_EINVAL,
+                           "pmp_astar2d_set_engine: engine must be 0 (one query per wave), 1 (multi-query for large "
+                           "batches) or 2 (multi-query always)");
     ctx->astar_engine = engine;
     ctx->astar_mq_t2lds = t2_lds ? 1 : 0;
     if (ctx->astar_W == 0) return PMP_OK;
-    return pmp_astar2d_reserve(ctx, ctx->astar_W, ctx->astar_H, ctx->astar_workers, 0);
+    return astar2d_reserve_impl(ctx, ctx->astar_W, ctx->astar_H, ctx->astar_workers, 0);
 }
 
 extern "C" int pmp_astar2d_set_residency(pmp_ctx* ctx, int per_cu)
@@ -1129,8 +1175,17 @@ extern "C" int pmp_astar2d_set_residency(pmp_ctx* ctx, int per_cu)
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_set_residency: per_cu must be in [0, 128]");
     ctx->astar_resident_per_cu = per_cu;
     if (ctx->astar_W == 0) return PMP_OK;  // applied by the next reserve
-    return pmp_astar2d_reserve(ctx, ctx->astar_W, ctx->astar_H, ctx->astar_workers, ctx->astar_heap_cap);
+    return astar2d_reserve_impl(ctx, ctx->astar_W, ctx->astar_H, ctx->astar_workers, ctx->astar_heap_cap);
 }
+
+namespace {
+// Batches below this size run on the one-query-per-wave engine even on a multi-query context: with
+// fewer queries than the chip has waves, a query's own latency sets the launch time, and a wave
+// serves one query faster than a quarter of one.
+constexpr int kMqMinBatch = 1024;
+// The LDSG variant needs at least this many heap positions in LDS beside the grid block.
+constexpr int kLdsgMinHeap = 64;
+}  // namespace
 
 extern "C" int pmp_graph2d_batch(pmp_ctx* ctx, void* stream, int algo, const uint32_t* occ_bits, int W, int H,
                                  int heuristic, const int32_t* start_xy, const int32_t* goal_xy, int nq,
@@ -1154,13 +1209,48 @@ extern "C" int pmp_graph2d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     if (!occ_bits || !start_xy || !goal_xy || !cost || !path_len || !path || !n_expanded || !status)
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_batch: null pointer argument");
     PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
-    if (!(ctx->astar_W == W && ctx->astar_H == H)) {
-        int workers = ctx->astar_engine == 1 ? 4 * default_workers() : default_workers();
-        if (workers > nq) workers = nq;
-        int rc = pmp_astar2d_reserve(ctx, W, H, workers, 0);
-        if (rc) return rc;
+    {
+        // a geometry made here (not by the host's pmp_astar2d_reserve) follows the batches: sized to
+        // the first batch, it grows when a larger one arrives
+        const int auto_w = ctx->astar_engine >= 1 ? 4 * default_workers() : default_workers();
+        const bool grow = ctx->astar_auto && ctx->astar_workers < nq && ctx->astar_workers < auto_w;
+        if (!(ctx->astar_W == W && ctx->astar_H == H) || grow) {
+            const int rc = astar2d_reserve_impl(ctx, W, H, nq < auto_w ? nq : auto_w, 0);
+            if (rc) return rc;
+            ctx->astar_auto = 1;
+        }
     }
-    if (!theta && ctx->astar_reserved_mq) {
+    const size_t ncell = (size_t)W * H;
+    const size_t cst_words = ((ncell + 7) / 8 + 3) & ~(size_t)3;
+    const int heap_cap = ctx->astar_heap_cap;
+    // one-query-per-wave launch geometry: the reservation's, or on a multi-query reservation this
+    // engine's defaults for the batch
+    int workers, per_cu, lds_cap;
+    if (!ctx->astar_reserved_mq) {
+        workers = ctx->astar_workers < nq ? ctx->astar_workers : nq;
+        per_cu = ctx->astar_resident_per_cu > 0 ? ctx->astar_resident_per_cu : (ctx->astar_workers + 255) / 256;
+        lds_cap = ctx->astar_lds_cap;
+    } else {
+        workers = default_workers() < nq ? default_workers() : nq;
+        per_cu = ctx->astar_resident_per_cu > 0 ? ctx->astar_resident_per_cu : (workers + 255) / 256;
+        if (per_cu > 32) per_cu = 32;
+        lds_cap = default_lds_cap(per_cu);
+        if (lds_cap < 16)
+            return pmp_set_err(ctx, PMP_EINVAL, "pmp_graph2d_batch: residency leaves no LDS heap share (one query per wave)");
+        if (lds_cap > heap_cap) lds_cap = (heap_cap + 15) & ~15;
+    }
+    // small grids: the grid block in LDS when the share holds it beside a useful heap
+    bool ldsg = false;
+    if (!theta) {
+        const long long share = (long long)(160 * 1024) / (per_cu < 1 ? 1 : per_cu) - 256;
+        long long cap_g = (share - kBitsLdsBytes - (long long)ldsg_bytes(ncell)) / 12;
+        cap_g &= ~15ll;
+        if (cap_g >= kLdsgMinHeap) {
+            ldsg = true;
+            lds_cap = cap_g > heap_cap ? (heap_cap + 15) & ~15 : (int)cap_g;
+        }
+    }
+    if (!theta && ctx->astar_reserved_mq && (ctx->astar_engine == 2 || (!ldsg && nq >= kMqMinBatch))) {
         const int groups = ctx->astar_workers < nq ? ctx->astar_workers : nq;
         int* queue = (int*)ctx->buf[SCR_AUX0];
         hipStream_t s = (hipStream_t)stream;
@@ -1173,25 +1263,22 @@ extern "C" int pmp_graph2d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
         return pmp_astar2d_mq_launch(ctx, s, algo, occ_bits, W, H, heuristic, start_xy, goal_xy, order, nq, cost,
                                      path_len, path, path_cap, n_expanded, expand, expand_cap, counters, status, queue);
     }
-    if (ctx->astar_reserved_mq) {
-        // Theta* on a context reserved for the multi-query engine: this engine's scratch
-        const int e = ctx->astar_engine;
-        ctx->astar_engine = 0;
-        int workers = default_workers();
-        if (workers > nq) workers = nq;
-        const int rc = pmp_astar2d_reserve(ctx, W, H, workers, 0);
-        ctx->astar_engine = e;
-        if (rc) return rc;
+    // this engine's scratch for the launch (grow-only: no-ops on its own reservation)
+    const size_t spill = heap_cap > lds_cap ? (size_t)(heap_cap - lds_cap) : 0;
+    if (!pmp_scratch(ctx, SCR_HEAP, (size_t)workers * spill * 16 + 16)) return PMP_ENOMEM;
+    if (!pmp_scratch(ctx, SCR_BITS, (size_t)workers * hbits_words(heap_cap) * 4)) return PMP_ENOMEM;
+    if (!pmp_scratch(ctx, SCR_AUX0, 256)) return PMP_ENOMEM;
+    uint32_t* cst = nullptr;
+    double* G = nullptr;
+    if (!ldsg) {
+        cst = (uint32_t*)pmp_scratch(ctx, SCR_CLOSED, (size_t)workers * cst_words * 4);
+        G = (double*)pmp_scratch(ctx, SCR_G, (size_t)workers * ncell * 8);
+        if (!cst || !G) return PMP_ENOMEM;
     }
-    const int workers = ctx->astar_workers < nq ? ctx->astar_workers : nq;
-    const size_t ncell = (size_t)W * H;
-    const size_t cst_words = ((ncell + 7) / 8 + 3) & ~(size_t)3;
-    uint4* spill = (uint4*)ctx->buf[SCR_HEAP];
-    uint32_t* cst = (uint32_t*)ctx->buf[SCR_CLOSED];
+    uint4* spill_p = (uint4*)ctx->buf[SCR_HEAP];
     int* queue = (int*)ctx->buf[SCR_AUX0];
-    double* G = (double*)ctx->buf[SCR_G];
     hipStream_t s = (hipStream_t)stream;
-    const size_t lds = (size_t)kBitsLdsBytes + (size_t)ctx->astar_lds_cap * 12;
+    const size_t lds = (size_t)kBitsLdsBytes + (size_t)lds_cap * 12 + (ldsg ? ldsg_bytes(ncell) : 0);
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
     int32_t* order = nullptr;
     if (ctx->astar_lpt && nq > workers) {
@@ -1209,10 +1296,14 @@ extern "C" int pmp_graph2d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
               : algo == PMP_ALGO_THETA    ? (heuristic == 1 ? astar2d_kernel<TL | 1, false, 1> : astar2d_kernel<TL, false, 1>)
               : algo == PMP_ALGO_LAZY_THETA ? (heuristic == 1 ? astar2d_kernel<TL | 1, false, 2> : astar2d_kernel<TL, false, 2>)
                                           : (heuristic == 1 ? astar2d_kernel<1, false, 0> : astar2d_kernel<0, false, 0>);
+    if (ldsg)
+        kern = algo == PMP_ALGO_DIJKSTRA ? astar2d_kernel<2, false, 0, true>
+             : algo == PMP_ALGO_GBFS     ? (heuristic == 1 ? astar2d_kernel<1, true, 0, true> : astar2d_kernel<0, true, 0, true>)
+                                         : (heuristic == 1 ? astar2d_kernel<1, false, 0, true> : astar2d_kernel<0, false, 0, true>);
     hipLaunchKernelGGL(kern, dim3(workers), dim3(64), lds, s, occ_bits, W, H, start_xy,
                        goal_xy, (const int32_t*)order, nq, cost, path_len, path, path_cap, n_expanded, expand,
-                       expand_cap, counters, status, queue, spill, ctx->astar_heap_cap, ctx->astar_lds_cap, cst, cst_words, G,
-                       (uint32_t*)ctx->buf[SCR_BITS], hbits_words(ctx->astar_heap_cap), order ? ctx->astar_prio_n : 0, ctx->span,
+                       expand_cap, counters, status, queue, spill_p, heap_cap, lds_cap, cst, cst_words, G,
+                       (uint32_t*)ctx->buf[SCR_BITS], hbits_words(heap_cap), order ? ctx->astar_prio_n : 0, ctx->span,
                        par);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;

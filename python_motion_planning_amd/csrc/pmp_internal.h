@@ -24,12 +24,14 @@ struct pmp_ctx {
     // ... and the workers resident per CU over all concurrent launches, which sets their LDS share
     // (0 = this launch's own workers per CU; pmp_set_resident_per_cu)
     int resident_per_cu = 0;
-    // A* 2D engine: 1 = several queries per wave (astar2d_mq.hip) for A* / Dijkstra / GBFS whose heaps fit
-    // its capacity, 0 = one query per wave (astar2d.hip) always; the multi-query engine's tier-2
+    // A* 2D engine: 2 = several queries per wave (astar2d_mq.hip) for A* / Dijkstra / GBFS whose heaps fit
+    // its capacity, 1 = that for large batches on large grids, 0 = one query per wave (astar2d.hip)
+    // always (pmp_astar2d_set_engine); the multi-query engine's tier-2
     // direction bits in LDS (1) or HBM (0); the geometry its per-slot epochs were written for
     int astar_engine = 1;
     int astar_mq_t2lds = 0;
     int astar_reserved_mq = 0;  // the current reservation (pmp_astar2d_reserve) is the multi-query engine's
+    int astar_auto = 0;         // ... and was made by a launch (not the host): it grows with the batches
     size_t astar_mq_epoch_slots = 0, astar_mq_cst_bytes = 0;
     // grow-only scratch arena, one buffer per use
     void* buf[16] = {nullptr};

@@ -17,12 +17,13 @@ def _pmp():
     return pmp
 
 
-# (engine, tier-2 bits in LDS): 1 = four queries per wave (astar2d_mq.hip, the default), 0 = one
-# query per wave (astar2d.hip); both must give the reference's answers bit for bit
-ENGINES = [(1, 0), (1, 1), (0, 0)]
+# (engine, tier-2 bits in LDS): 2 = four queries per wave (astar2d_mq.hip) for every batch, 0 = one
+# query per wave (astar2d.hip; grid state in LDS on small grids), 1 = the default choice between them
+# by batch and grid size; all must give the reference's answers bit for bit
+ENGINES = [(2, 0), (2, 1), (0, 0), (1, 0)]
 
 
-@pytest.fixture(params=ENGINES, ids=["mq", "mq_t2lds", "wave"])
+@pytest.fixture(params=ENGINES, ids=["mq", "mq_t2lds", "wave", "auto"])
 def engine(request):
     from python_motion_planning_amd import _lib
 
@@ -204,7 +205,7 @@ def test_heap_above_32767_entries_uses_hbm_bit_tiers():
     batch.astar2d_batch(occ[:64, :64], s, s, path_cap=4, reserve_slots=64, heap_cap=0)  # default sizing again
 
 
-@pytest.mark.parametrize("eng,per_cu", [(1, 48), (1, 18), (0, 18)])
+@pytest.mark.parametrize("eng,per_cu", [(2, 48), (2, 18), (0, 18), (0, 1)])
 def test_residency_batches_in_flight(eng, per_cu):
     """The bench's headline schedule: several contexts, each a smaller persistent-worker launch on
     its own stream with the LDS heap share of 18 resident workers per CU (pmp_astar2d_set_residency,
@@ -216,6 +217,10 @@ def test_residency_batches_in_flight(eng, per_cu):
     from python_motion_planning_amd import _lib, batch, workloads as wl
 
     occ, s, g = wl.c2_workload(nq=96, W=256, H=256, pair_seed=21)
+    if per_cu == 1:  # a 60x60 grid: the one-query-per-wave engine keeps the grid state in LDS
+        occ, s, g = occ[:60, :60].copy(), np.clip(s, 1, 58).astype(np.int32), np.clip(g, 1, 58).astype(np.int32)
+        occ[s[:, 0], s[:, 1]] = 0
+        occ[g[:, 0], g[:, 1]] = 0
     W, H = occ.shape
     L = _lib.load_library()
     bits = batch.occ_bits_device(occ, torch)

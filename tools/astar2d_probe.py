@@ -13,11 +13,17 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from python_motion_planning_amd import _lib, batch, workloads as wl  # noqa: E402
 
 torch.cuda.set_device(0)
+mode = os.environ.get("MODE", "batch")
 occ, s, g = wl.c2_workload(4096)
 ref = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "c2_counters.npy"))
-mode = os.environ.get("MODE", "batch")
+if mode == "c1":  # the README query alone (the drop-in latency case): counters from the oracle's C1 run
+    occ, s, g = wl.readme_grid(), np.array([[5, 5]], np.int32), np.array([[45, 25]], np.int32)
+    ref = np.array([[2314, 1890, 579, 438]], np.int64)
+W, H = occ.shape
 engine, t2 = int(os.environ.get("ENGINE", "1")), int(os.environ.get("T2LDS", "0"))
-if mode == "longest":
+if mode == "c1":
+    idx = np.zeros(1, np.int64)
+elif mode == "longest":
     idx = np.argsort(-ref[:, 2])[:1]
 elif mode == "longest4":
     idx = np.argsort(-ref[:, 2])[:4]
@@ -27,7 +33,7 @@ w = int(os.environ.get("WORKERS", "2048" if engine == 1 else "768"))
 w = min(w, len(idx))
 L, ctx = _lib.load_library(), _lib.context()
 _lib.check(ctx, L.pmp_astar2d_set_engine(ctx, engine, t2), "engine")
-_lib.check(ctx, L.pmp_astar2d_reserve(ctx, 1024, 1024, w, 0), "reserve")
+_lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, w, 0), "reserve")
 res = int(os.environ.get("RESIDENCY", "0"))
 if res:
     _lib.check(ctx, L.pmp_astar2d_set_residency(ctx, res), "residency")
@@ -35,7 +41,7 @@ bits = batch.occ_bits_device(occ, torch)
 for rep in range(int(os.environ.get("REPS", "2"))):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    r = batch.astar2d_batch((1024, 1024), s[idx], g[idx], path_cap=4096, counters=True, occ_bits=bits,
+    r = batch.astar2d_batch((W, H), s[idx], g[idx], path_cap=4096, counters=True, occ_bits=bits,
                             retry_overflow=False)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0

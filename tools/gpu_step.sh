@@ -1,4 +1,3 @@
-# one GPU call: the GPU test suite, then the default bench
+# one GPU call: PMC issue breakdown of the C1 single query (engine 0, LDS grid)
 cd $GRAFT_REPO_ROOT
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r3_gputest6.log 2>&1 && \
-timeout -k 10 700 python bench.py --detail-out gpurun_out/r3_bench6_detail.json > gpurun_out/r3_bench6.json 2> gpurun_out/r3_bench6.err
+ENGINE=0 MODE=c1 TAG=c1 timeout -k 10 500 bash tools/pmc_probe.sh > gpurun_out/r3_pmc_c1.log 2>&1
