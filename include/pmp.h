@@ -347,8 +347,9 @@ int pmp_lqr_control_batch(pmp_ctx* ctx, void* stream, const pmp_lp_params* lp, c
                           const double* s, const double* s_d, const double* u_r, const double* robot_vw, double* u);
 
 /*
- * Batched MPC.mpcControl (local_planner/mpc.py:111-214), one wave64 per call: QP assembly
- * (S_u'QS_u on the f64 MFMA 16x16x4), ADMM solve, u = du0 + u_p + u_r, regularisation.
+ * Batched MPC.mpcControl (local_planner/mpc.py:111-214), four calls per wave64 (one per 16-lane
+ * row): QP assembly (S_u'QS_u on the f64 MFMA 16x16x4, one pass per row's agent), ADMM solve on the
+ * row (DPP broadcasts and scans), u = du0 + u_p + u_r, regularisation.
  *   u_p [n][2] in/out  carried control error (returned as u - u_r, before regularisation)
  *   qp_H [n][2m][2m], qp_g [n][2m], qp_lu [n][2][4m], du [n][2m]   nullable: the assembled QP and its solution
  *   admm_iters, admm_status [n] i32  nullable: iterations, 0 converged / 1 iteration limit
@@ -362,8 +363,8 @@ int pmp_mpc_control_batch(pmp_ctx* ctx, void* stream, const pmp_lp_params* lp, c
 #define PMP_TRACK_MPC 1
 /*
  * Batched tracking-controller plan iterations: `iters` iterations of LQR.plan (lqr.py:58-86,
- * kind PMP_TRACK_LQR) or MPC.plan (mpc.py:66-94, kind PMP_TRACK_MPC) per agent, one wave64 per
- * agent: reachGoal, getLookaheadPoint, the rotate/move branch, lqrControl / mpcControl,
+ * kind PMP_TRACK_LQR) or MPC.plan (mpc.py:66-94, kind PMP_TRACK_MPC) per agent, four agents per
+ * wave64 (one per 16-lane row): reachGoal, getLookaheadPoint, the rotate/move branch, lqrControl / mpcControl,
  * Robot.kinematic.  Arrays as pmp_dwa_step_batch, plus
  *   u_p [na][2] f64 in/out   MPC's carried u_p (start a plan with zeros); unused for LQR
  *   admm_iters [na] i32      nullable; ADMM iterations summed over this call's steps

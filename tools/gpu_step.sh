@@ -1,3 +1,5 @@
-# one GPU call: PMC issue breakdown of the C1 single query (engine 0, LDS grid)
+# one GPU call: tracking tests (four agents per wave), then the lqr/mpc legs at 2048 and 8192 agents
 cd $GRAFT_REPO_ROOT
-ENGINE=0 MODE=c1 TAG=c1 timeout -k 10 500 bash tools/pmc_probe.sh > gpurun_out/r3_pmc_c1.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_track_gpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/r3_trk1.log 2>&1 && \
+timeout -k 10 300 python bench.py --legs lqr,mpc --no-cpu-baseline --steps 1 --warmup 1 --detail-out gpurun_out/r3_trk1_2048.json > /dev/null 2> gpurun_out/r3_trk1.err && \
+timeout -k 10 300 python bench.py --legs lqr,mpc --no-cpu-baseline --steps 1 --warmup 1 --track-agents 8192 --detail-out gpurun_out/r3_trk1_8192.json > /dev/null 2>> gpurun_out/r3_trk1.err
