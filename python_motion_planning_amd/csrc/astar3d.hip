@@ -5,9 +5,10 @@
 // The reference heap holds tuples (f, h, counter, node) -> a TOTAL order, so the pop sequence is
 // the sorted order of (f, h, counter) whatever the heap shape; the kernel keeps a binary heap in
 // LDS (spilling deep positions to HBM) with the same key:
-//   entry = {f64 g, u32 seq (push counter), u32 cm = (x<<16 | y<<8 | z) << 5 | dir}   (16 B)
-//   f = g + h recomputed on load with h = math.sqrt(dx**2+dy**2+dz**2) of integers (exactly the
-//   reference's tentative_g + node_n.h), hkey = d2 (sqrt of integers is monotone and exact).
+//   entry = {f64 g, f64 f, u32 seq (push counter), u32 cm = (x<<16 | y<<8 | z) << 5 | dir}
+//   (24 B in LDS, 32 B spill records); f = g + h computed once at the push with
+//   h = math.sqrt(dx**2+dy**2+dz**2) of integers (exactly the reference's tentative_g + node_n.h),
+//   hkey = d2 rebuilt from the cell on load (sqrt of integers is monotone and exact).
 // Reopening semantics are the reference's: a pop is skipped if CLOSED holds the cell with g <= node.g
 // (:48-50), a neighbour is skipped if CLOSED holds it with g <= tentative_g (:68-70), CLOSED is
 // (over)written before the goal test (:52-63).  Path is reversed to start -> goal (:105).
@@ -29,25 +30,25 @@ __device__ __constant__ int8_t c_m3[26][3] = {
 
 using heap16::Ent;  // g = path cost, a = push counter, b = cm; derived f = g + h, hk = h order key
 
-// (f, h, counter) tuple order of a_star3d.py:40,75, with f and h rebuilt from the cell
+// (f, h, counter) tuple order of a_star3d.py:40,75.  f = tentative_g + h is computed once, at the
+// push (set_f), and stored beside the entry; h's order key (an integer) is rebuilt from the cell.
 struct Key3 {
+    static constexpr bool kStoredF = true;
     int gx, gy, gz;
     int heur;  // 0 euclidean, 1 manhattan, 2 zero (Dijkstra3D: h = 0, dijkstra3d.py:34,83)
 
-    __device__ __forceinline__ void derive(Ent& e) const
+    __device__ __forceinline__ uint32_t hkey(uint32_t b) const
     {
-        const int x = (int)(e.b >> 21), y = (int)((e.b >> 13) & 255u), z = (int)((e.b >> 5) & 255u);
+        const int x = (int)(b >> 21), y = (int)((b >> 13) & 255u), z = (int)((b >> 5) & 255u);
         const int dx = abs(gx - x), dy = abs(gy - y), dz = abs(gz - z);
-        if (heur == 2) {
-            e.hk = 0u;
-            e.f = e.g;
-        } else if (heur == 1) {
-            e.hk = (uint32_t)(dx + dy + dz);
-            e.f = e.g + (double)e.hk;
-        } else {
-            e.hk = (uint32_t)(dx * dx + dy * dy + dz * dz);
-            e.f = e.g + __dsqrt_rn((double)e.hk);
-        }
+        return heur == 2 ? 0u : (heur == 1 ? (uint32_t)(dx + dy + dz) : (uint32_t)(dx * dx + dy * dy + dz * dz));
+    }
+    __device__ __forceinline__ void derive(Ent& e) const { e.hk = hkey(e.b); }
+    // f = g + h exactly as node_n.g + node_n.h (math.sqrt of the integer square sum for euclidean)
+    __device__ __forceinline__ void set_f(Ent& e) const
+    {
+        e.hk = hkey(e.b);
+        e.f = heur == 2 ? e.g : (heur == 1 ? e.g + (double)e.hk : e.g + __dsqrt_rn((double)e.hk));
     }
 
     static __device__ __forceinline__ bool lt(const Ent& a, const Ent& b)
@@ -139,8 +140,9 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
     const size_t ncell = (size_t)X * Y * Z;
     const size_t words = (ncell + 31) / 32;
     const size_t spill_n = (size_t)(heap_cap > lds_cap ? heap_cap - lds_cap : 0);
-    const heap16::Heap hp = heap16::make_heap(smem, lds_cap, spill_all + (size_t)worker * spill_n, spill_n);
-    lds_w32* occl = (lds_w32*)(smem + (size_t)16 * lds_cap);  // OCC_LDS: the query's bitmap
+    const heap16::Heap hp =
+        heap16::make_heap<true>(smem, lds_cap, spill_all + (size_t)worker * spill_n * 2, spill_n);  // 32 B records
+    lds_w32* occl = (lds_w32*)(smem + (size_t)heap16::lds_entry_bytes<true>() * lds_cap);  // OCC_LDS: the query's bitmap
     uint8_t* cdir = cdir_all + (size_t)worker * ncell;
     double* cg = cg_all + (size_t)worker * 2 * ncell;  // closed g
     double* og = cg + ncell;                            // best pending (pushed) g
@@ -194,8 +196,8 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
         root.g = 0.0;
         root.a = 0u;
         root.b = scm;
-        qc.derive(root);
-        if (lane == 0) heap16::store<true>(hp, 0, root);
+        qc.set_f(root);
+        if (lane == 0) heap16::store<true, true>(hp, 0, root);
         if (THETA && lane == 0) ppar[0] = ((uint32_t)sx * (uint32_t)Y + (uint32_t)sy) * (uint32_t)Z + (uint32_t)sz;
         heap16::wsync();
         int n = 1;
@@ -414,7 +416,7 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
             item.g = tg;
             item.a = 0u;
             item.b = ((((uint32_t)nx & 255u) << 16) | (((uint32_t)ny & 255u) << 8) | ((uint32_t)nz & 255u)) << 5 | (uint32_t)(lane < 26 ? lane : 0);
-            qc.derive(item);
+            qc.set_f(item);
             bool overflow = false;
             while (vm) {
                 const int m = __ffsll((long long)vm) - 1;
@@ -546,11 +548,12 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     bool occ_lds = words <= (size_t)kOccLdsWords;
     // the query's bitmap in LDS takes its own size (C5: 260 words), the rest of the share is heap
     int occ_bytes = occ_lds ? (int)((words * 4 + 15) & ~(size_t)15) : 0;
-    int lds_cap = pmp_heap_lds_cap(ctx, per_cu, occ_bytes, 16);
+    constexpr int kEnt = heap16::lds_entry_bytes<true>(), kSpill = heap16::spill_entry_bytes<true>();
+    int lds_cap = pmp_heap_lds_cap(ctx, per_cu, occ_bytes, kEnt);
     if (lds_cap < kMinLdsHeap && occ_lds) {  // the LDS share cannot hold the occupancy too: keep it in HBM
         occ_lds = false;
         occ_bytes = 0;
-        lds_cap = pmp_heap_lds_cap(ctx, per_cu, 0, 16);
+        lds_cap = pmp_heap_lds_cap(ctx, per_cu, 0, kEnt);
     }
     if (lds_cap < kMinLdsHeap)
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_graph3d_batch: workers / resident per CU leave no LDS heap share");
@@ -565,12 +568,12 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     const uint32_t ppar_cap = theta ? (uint32_t)std::min<size_t>(64 * ncell + 64, (size_t)1 << 24) : 0u;
     {
         // per-context scratch budget: fewer workers (each pulls more queries) rather than ENOMEM
-        const size_t per_worker = spill_n * 16 + ncell + ncell * 16 + (theta ? ((size_t)ncell + ppar_cap) * 4 : 0);
+        const size_t per_worker = spill_n * kSpill + ncell + ncell * 16 + (theta ? ((size_t)ncell + ppar_cap) * 4 : 0);
         const size_t fit = kScratchBudget3 / per_worker;
         if (fit < 1) return pmp_set_err(ctx, PMP_ENOMEM, "pmp_graph3d_batch: one worker exceeds the scratch budget");
         if ((size_t)workers > fit) workers = (int)fit;
     }
-    uint4* spill = (uint4*)pmp_scratch(ctx, SCR_AUX1, (size_t)workers * spill_n * 16 + 16);
+    uint4* spill = (uint4*)pmp_scratch(ctx, SCR_AUX1, (size_t)workers * spill_n * kSpill + 16);
     uint8_t* cdir = (uint8_t*)pmp_scratch(ctx, SCR_AUX2, (size_t)workers * ncell + 16);
     double* cg = (double*)pmp_scratch(ctx, SCR_AUX3, (size_t)workers * ncell * 16 + 16);  // closed g + pending g
     int* queue = (int*)pmp_scratch(ctx, SCR_AUX0, 256);
@@ -589,7 +592,7 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     }
     auto kern = occ_lds ? (theta == 1 ? astar3d_kernel<true, 1> : theta == 2 ? astar3d_kernel<true, 2> : astar3d_kernel<true, 0>)
                         : (theta == 1 ? astar3d_kernel<false, 1> : theta == 2 ? astar3d_kernel<false, 2> : astar3d_kernel<false, 0>);
-    hipLaunchKernelGGL(kern, dim3(workers), dim3(64), (size_t)lds_cap * 16 + occ_bytes, s, occ_bits, per_query, X, Y, Z,
+    hipLaunchKernelGGL(kern, dim3(workers), dim3(64), (size_t)lds_cap * kEnt + occ_bytes, s, occ_bits, per_query, X, Y, Z,
                        algo == PMP_ALGO_DIJKSTRA ? 2 : heuristic, start_xyz, goal_xyz, nq, cost, path_len, path, path_cap,
                        n_expanded, expand, expand_cap, counters, status, queue, spill, heap_cap, lds_cap, cdir, cg,
                        algo == PMP_ALGO_GBFS ? 1 : 0, tpar, tpar ? tpar + (size_t)workers * ncell : nullptr, ppar_cap,

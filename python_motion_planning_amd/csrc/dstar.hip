@@ -34,6 +34,7 @@ struct __attribute__((aligned(16))) DCell {
 using heap16::Ent;  // g = k, a = first entry position, b = cell
 
 struct KeyD {
+    static constexpr bool kStoredF = false;
     __device__ __forceinline__ void derive(Ent& e) const { e.f = e.g; e.hk = 0u; }
     static __device__ __forceinline__ bool lt(const Ent& x, const Ent& y)
     {

@@ -69,6 +69,7 @@ __device__ __forceinline__ void store_c(DC3* cells, int c, const DC3& v)
 using heap16::Ent;  // g = k, a = list position, b = slot
 
 struct KeyD {
+    static constexpr bool kStoredF = false;
     __device__ __forceinline__ void derive(Ent& e) const { e.f = e.g; e.hk = 0u; }
     static __device__ __forceinline__ bool lt(const Ent& x, const Ent& y)
     {

@@ -9,7 +9,8 @@
 //   push: the ancestors load in one round; the "less than the new item" set is a prefix of the
 //         root path, so a ballot popcount gives the sift-up distance.
 // The key is supplied by a policy type K: K::derive(e) fills e.f / e.hk from the stored fields and
-// K::lt(x, y) is the strict order.
+// K::lt(x, y) is the strict order.  K::kStoredF: f is stored beside the entry (24 B in LDS: g, f, a,
+// b; 32 B spill records) instead of derived on every load, so a key costs no square root.
 #pragma once
 #include "pmp_internal.h"
 
@@ -27,50 +28,71 @@ struct Ent {
 
 struct Heap {
     lds_f64* lg;
+    lds_f64* lf;  // stored-f heaps only
     lds_u32* la;
     lds_u32* lb;
-    __amdgpu_buffer_rsrc_t spill;  // {g lo, g hi, a, b} for positions >= lds_cap
+    __amdgpu_buffer_rsrc_t spill;  // {g lo, g hi, a, b} (+ {f lo, f hi} with stored f) for positions >= lds_cap
     int lds_cap;
 };
 
+// LDS and spill bytes per entry
+template <bool SF> constexpr int lds_entry_bytes() { return SF ? 24 : 16; }
+template <bool SF> constexpr int spill_entry_bytes() { return SF ? 32 : 16; }
+
+template <bool SF = false>
 __device__ __forceinline__ Heap make_heap(unsigned char* smem, int lds_cap, uint4* spill_base, size_t spill_n)
 {
     Heap hp;
     hp.lg = (lds_f64*)smem;
-    hp.la = (lds_u32*)(smem + (size_t)8 * lds_cap);
-    hp.lb = (lds_u32*)(smem + (size_t)12 * lds_cap);
+    hp.lf = SF ? (lds_f64*)(smem + (size_t)8 * lds_cap) : nullptr;
+    hp.la = (lds_u32*)(smem + (size_t)(SF ? 16 : 8) * lds_cap);
+    hp.lb = (lds_u32*)(smem + (size_t)(SF ? 20 : 12) * lds_cap);
     hp.lds_cap = lds_cap;
-    hp.spill = __builtin_amdgcn_make_buffer_rsrc(spill_base, 0, (int)(spill_n * 16), 0x00020000);
+    hp.spill = __builtin_amdgcn_make_buffer_rsrc(spill_base, 0, (int)(spill_n * spill_entry_bytes<SF>()), 0x00020000);
     return hp;
 }
 
-template <bool SPILL>
+template <bool SPILL, bool SF = false>
 __device__ __forceinline__ void load(const Heap& hp, int p, Ent& e)
 {
     if (!SPILL || p < hp.lds_cap) {
         e.g = hp.lg[p];
+        if (SF) e.f = hp.lf[p];
         e.a = hp.la[p];
         e.b = hp.lb[p];
     } else {
-        const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(hp.spill, (p - hp.lds_cap) * 16, 0, 0));
+        const int off = (p - hp.lds_cap) * spill_entry_bytes<SF>();
+        const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(hp.spill, off, 0, 0));
         e.g = __hiloint2double((int)v.y, (int)v.x);
         e.a = v.z;
         e.b = v.w;
+        if (SF) {
+            const uint2 w = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(hp.spill, off + 16, 0, 0));
+            e.f = __hiloint2double((int)w.y, (int)w.x);
+        }
     }
 }
 
-template <bool SPILL>
+template <bool SPILL, bool SF = false>
 __device__ __forceinline__ void store(const Heap& hp, int p, const Ent& e)
 {
     if (!SPILL || p < hp.lds_cap) {
         hp.lg[p] = e.g;
+        if (SF) hp.lf[p] = e.f;
         hp.la[p] = e.a;
         hp.lb[p] = e.b;
     } else {
+        const int off = (p - hp.lds_cap) * spill_entry_bytes<SF>();
         const uint64_t bits = (uint64_t)__double_as_longlong(e.g);
         const uint4 v = make_uint4((uint32_t)bits, (uint32_t)(bits >> 32), e.a, e.b);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
-                                               hp.spill, (p - hp.lds_cap) * 16, 0, 0);
+                                               hp.spill, off, 0, 0);
+        if (SF) {
+            const uint64_t fb = (uint64_t)__double_as_longlong(e.f);
+            const uint2 w = make_uint2((uint32_t)fb, (uint32_t)(fb >> 32));
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int, w),
+                                                  hp.spill, off + 16, 0, 0);
+        }
     }
 }
 
@@ -100,10 +122,12 @@ __device__ __forceinline__ void pop_lane_consts(int lane, int& jl, int& ol)
 template <class K, bool SPILL>
 __device__ __forceinline__ void pop(const Heap& hp, const K& key, int n, Ent& root, int lane, int jl, int ol)
 {
+    constexpr bool SF = K::kStoredF;
     n = uni(n);
     Ent last;
-    load<SPILL>(hp, n, last);
+    load<SPILL, SF>(hp, n, last);
     last.g = rl_f64(last.g, 0);
+    if (SF) last.f = rl_f64(last.f, 0);
     last.a = rl_u32(last.a, 0);
     last.b = rl_u32(last.b, 0);
     key.derive(last);
@@ -115,14 +139,15 @@ __device__ __forceinline__ void pop(const Heap& hp, const K& key, int n, Ent& ro
         const bool vr = (lane < 63) & (li + 1 < n);
         Ent L, R;
         L.g = R.g = 0.0;
+        L.f = R.f = 0.0;
         L.a = R.a = 0u;
         L.b = R.b = 0u;
         if constexpr (SPILL) {
-            if (vl) load<true>(hp, li, L);
-            if (vr) load<true>(hp, li + 1, R);
+            if (vl) load<true, SF>(hp, li, L);
+            if (vr) load<true, SF>(hp, li + 1, R);
         } else {
-            load<false>(hp, vl ? li : 0, L);
-            load<false>(hp, vr ? li + 1 : 0, R);
+            load<false, SF>(hp, vl ? li : 0, L);
+            load<false, SF>(hp, vr ? li + 1 : 0, R);
         }
         key.derive(L);
         key.derive(R);
@@ -149,7 +174,7 @@ __device__ __forceinline__ void pop(const Heap& hp, const K& key, int n, Ent& ro
         }
         if ((mover >> lane) & 1ull) {
             const bool rr = (movr >> lane) & 1ull;
-            store<SPILL>(hp, ((rr ? li + 1 : li) - 1) >> 1, rr ? R : L);
+            store<SPILL, SF>(hp, ((rr ? li + 1 : li) - 1) >> 1, rr ? R : L);
         }
         if (first && (mover & 1ull)) root = rl_ent((movr & 1ull) ? R : L, 0);
         first = false;
@@ -157,7 +182,7 @@ __device__ __forceinline__ void pop(const Heap& hp, const K& key, int n, Ent& ro
         if (!go) break;
         wsync();
     }
-    if (lane == 0) store<SPILL>(hp, hole, last);
+    if (lane == 0) store<SPILL, SF>(hp, hole, last);
     if (hole == 0) root = last;
     wsync();
 }
@@ -166,6 +191,7 @@ __device__ __forceinline__ void pop(const Heap& hp, const K& key, int n, Ent& ro
 template <class K, bool SPILL>
 __device__ __forceinline__ void push(const Heap& hp, const K& key, int n, const Ent& it, Ent& root, int lane)
 {
+    constexpr bool SF = K::kStoredF;
     n = uni(n);
     const int np1 = n + 1;
     const int depth = 31 - __clz(np1);
@@ -173,17 +199,18 @@ __device__ __forceinline__ void push(const Heap& hp, const K& key, int n, const 
     const int apos = valid ? (np1 >> (lane + 1)) - 1 : 0;
     Ent a;
     a.g = 0.0;
+    a.f = 0.0;
     a.a = a.b = 0u;
     if constexpr (SPILL) {
-        if (valid) load<true>(hp, apos, a);
+        if (valid) load<true, SF>(hp, apos, a);
     } else {
-        load<false>(hp, apos, a);
+        load<false, SF>(hp, apos, a);
     }
     key.derive(a);
     const int t = __popcll(ballot(valid & K::lt(it, a)));
-    if (lane < t) store<SPILL>(hp, (np1 >> lane) - 1, a);
+    if (lane < t) store<SPILL, SF>(hp, (np1 >> lane) - 1, a);
     const int ipos = (np1 >> t) - 1;
-    if (lane == 0) store<SPILL>(hp, ipos, it);
+    if (lane == 0) store<SPILL, SF>(hp, ipos, it);
     if (ipos == 0) root = it;
     wsync();
 }

@@ -208,6 +208,13 @@ __device__ __forceinline__ double max16(double t)
     return t;
 }
 
+// Where the ADMM keeps the inverse: LDS (column-major, 16 loads per x-update, 32 fewer live VGPRs)
+// or registers (one row per lane).  A build-time switch for A/B runs (-DPMP_MPC_INV_LDS=0|1).
+#ifndef PMP_MPC_INV_LDS
+#define PMP_MPC_INV_LDS 1
+#endif
+constexpr bool kInvLds = PMP_MPC_INV_LDS != 0;
+
 // Minv = (H + sigma I + rho A'A)^-1, row v in this lane (rows/cols >= n are the identity).
 // A'A[2k+c][2k'+c'] = [c == c'] (m - max(k, k')) + [2k+c == 2k'+c'].
 // In-place Gauss-Jordan without pivoting (the matrix is SPD): at step k the pivot row goes through
@@ -216,7 +223,7 @@ __device__ __forceinline__ double max16(double t)
 // operations, value for value, as eliminating on M and I side by side.  k is a run-time loop: the
 // elimination keeps only its own row live (an unrolled one lets the scheduler hoist every broadcast).
 __device__ __forceinline__ void build_inverse(const double* Hrow, int v, int n, int m, double sigma, double rho,
-                                              double* Icol, double* prow)
+                                              double* Icol, double* prow, double (&Ireg)[16])
 {
     double A[16];
     // opaque to the optimiser: nothing of the build is hoisted out of the ADMM loop around it (the
@@ -254,7 +261,10 @@ __device__ __forceinline__ void build_inverse(const double* Hrow, int v, int n, 
     // the inverse, column-major for the agent (column c at Icol[16 c]): the x-update's loads of one
     // column by the row's 16 lanes are one contiguous 128 B
 #pragma unroll
-    for (int c = 0; c < 16; c++) Icol[16 * c + v] = A[c];
+    for (int c = 0; c < 16; c++) {
+        if (kInvLds) Icol[16 * c + v] = A[c];
+        else Ireg[c] = A[c];
+    }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
@@ -311,7 +321,7 @@ __device__ MpcResult mpc_rows(bool need, const MpcIn& I, double& up0, double& up
         const double P0 = rl_f64(p0, L0), P1 = rl_f64(p1, L0);
         v4d acc = {0.0, 0.0, 0.0, 0.0};
         double gp = 0.0;
-#pragma unroll 2
+
         for (int k0 = 0; k0 < R3; k0 += 4) {
             const int r = k0 + kq;
             double sv = 0.0, yv = 0.0, qv = 0.0;
@@ -383,7 +393,8 @@ __device__ MpcResult mpc_rows(bool need, const MpcIn& I, double& up0, double& up
         // ---- ADMM (the OSQP algorithm, unscaled), the row's agent: rows finish independently
         double rho = M.rho;
         const double sigma = M.sigma, alpha = M.alpha;
-        build_inverse(Hrow, v, n, m, sigma, rho, Icol, prow);
+        double Ireg[16];
+        build_inverse(Hrow, v, n, m, sigma, rho, Icol, prow, Ireg);
         double z1 = 0.0, z2 = 0.0, y1 = 0.0, y2 = 0.0;
         int status = 1, it = 0, cnt_c = 0, cnt_a = 0;
         while (it < M.max_iter) {
@@ -396,7 +407,7 @@ __device__ MpcResult mpc_rows(bool need, const MpcIn& I, double& up0, double& up
             double xt = 0.0;
             for16([&](auto cc) {
                 constexpr int c = decltype(cc)::value;
-                xt += Icol[16 * c + v] * bc16<c>(rhs);
+                xt += (kInvLds ? Icol[16 * c + v] : Ireg[c]) * bc16<c>(rhs);
             });
             xt = act ? xt : 0.0;
             const double zt1 = prefix16(xt);
@@ -436,7 +447,8 @@ __device__ MpcResult mpc_rows(bool need, const MpcIn& I, double& up0, double& up
                 const double rn = lp::clampd(rho * sqrt(pn / (dn + 1e-30)), 1e-6, 1e6);
                 if (rn > rho * M.adaptive_tol || rn < rho / M.adaptive_tol) {
                     rho = rn;
-                    build_inverse(Hrow, v, n, m, sigma, rho, Icol, prow);
+                    double Ireg[16];
+        build_inverse(Hrow, v, n, m, sigma, rho, Icol, prow, Ireg);
                 }
             }
         }
