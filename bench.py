@@ -1480,8 +1480,8 @@ def main():
     ap.add_argument("--dstar-workers-per-cu", type=int, default=0, help="D* persistent workers per CU (0 = default)")
     ap.add_argument("--dstar-residency", type=int, default=0,
                     help="D* workers resident per CU over all batches in flight (LDS share; 0 = per launch)")
-    ap.add_argument("--track-agents", type=int, default=8192,
-                    help="agents per LQR / MPC tracking launch (four per wave, one per 16-lane row: 2048 waves)")
+    ap.add_argument("--track-agents", type=int, default=32768,
+                    help="agents per LQR / MPC tracking launch (four per wave, one per 16-lane row: 8192 waves)")
     ap.add_argument("--track-iters", type=int, default=20)
     ap.add_argument("--track-steps", type=int, default=5)
     ap.add_argument("--schedule", choices=["lpt", "input"], default="lpt",

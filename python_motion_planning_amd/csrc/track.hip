@@ -208,10 +208,11 @@ __device__ __forceinline__ double max16(double t)
     return t;
 }
 
-// Where the ADMM keeps the inverse: LDS (column-major, 16 loads per x-update, 32 fewer live VGPRs)
-// or registers (one row per lane).  A build-time switch for A/B runs (-DPMP_MPC_INV_LDS=0|1).
+// Where the ADMM keeps the inverse: registers (one row per lane, the default) or LDS (column-major,
+// 16 loads per x-update, 32 fewer live VGPRs: 26.2M vs 32.7M agent-steps/s at 8192 agents on the
+// same box).  A build-time switch for A/B runs (-DPMP_MPC_INV_LDS=0|1, make invlds).
 #ifndef PMP_MPC_INV_LDS
-#define PMP_MPC_INV_LDS 1
+#define PMP_MPC_INV_LDS 0
 #endif
 constexpr bool kInvLds = PMP_MPC_INV_LDS != 0;
 
@@ -225,7 +226,8 @@ constexpr bool kInvLds = PMP_MPC_INV_LDS != 0;
 __device__ __forceinline__ void build_inverse(const double* Hrow, int v, int n, int m, double sigma, double rho,
                                               double* Icol, double* prow, double (&Ireg)[16])
 {
-    double A[16];
+    double Aloc[16];
+    double (&A)[16] = kInvLds ? Aloc : Ireg;  // the register build eliminates in place
     // opaque to the optimiser: nothing of the build is hoisted out of the ADMM loop around it (the
     // hoisted H row and per-column constants would stay live through every iteration)
     asm volatile("" : "+v"(v) : : "memory");
@@ -260,10 +262,9 @@ __device__ __forceinline__ void build_inverse(const double* Hrow, int v, int n, 
     }
     // the inverse, column-major for the agent (column c at Icol[16 c]): the x-update's loads of one
     // column by the row's 16 lanes are one contiguous 128 B
+    if (kInvLds) {
 #pragma unroll
-    for (int c = 0; c < 16; c++) {
-        if (kInvLds) Icol[16 * c + v] = A[c];
-        else Ireg[c] = A[c];
+        for (int c = 0; c < 16; c++) Icol[16 * c + v] = A[c];
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
@@ -283,7 +284,7 @@ constexpr int kRows = 4;  // agents per wave
 // (an H per row, then a pivot row per row, then an inverse per row at a 264-double stride: the
 // four rows' column loads fall in different LDS bank windows)
 constexpr int kInvStride = 264;
-constexpr int kMpcLds = kRows * 256 + kRows * 16 + kRows * kInvStride;
+constexpr int kMpcLds = kRows * 256 + kRows * 16 + (kInvLds ? kRows * kInvStride : 0);
 
 // MPC.mpcControl (mpc.py:111-214) for the agents of the wave's four rows, called by the whole wave
 // (the MFMA needs all lanes); `need` (row-uniform) selects the rows whose agent solves now, the other
@@ -447,8 +448,7 @@ __device__ MpcResult mpc_rows(bool need, const MpcIn& I, double& up0, double& up
                 const double rn = lp::clampd(rho * sqrt(pn / (dn + 1e-30)), 1e-6, 1e6);
                 if (rn > rho * M.adaptive_tol || rn < rho / M.adaptive_tol) {
                     rho = rn;
-                    double Ireg[16];
-        build_inverse(Hrow, v, n, m, sigma, rho, Icol, prow, Ireg);
+                    build_inverse(Hrow, v, n, m, sigma, rho, Icol, prow, Ireg);
                 }
             }
         }
