@@ -676,6 +676,143 @@ __global__ __launch_bounds__(kWave) void track_kernel(pmp_lp_params P, pmp_lqr_p
     }
 }
 
+// MPC.plan split at the solve, so each part keeps its own register budget (the fused loop needs the
+// lookahead's and the ADMM's registers at once: 1 wave per SIMD).  Per iteration `it`:
+// track_mpc_step (the kinematics of iteration it-1 for the agents that moved, then iteration it's
+// reachGoal / getLookaheadPoint / rotate-or-track branch) and track_mpc_solve (mpcControl for the
+// agents whose branch needs it); a last track_mpc_step (it = iters) applies the final kinematics.
+// Per-agent carry between the launches: the MPC inputs (10 doubles), a flag word and the ADMM count.
+enum : int { kLive = 1, kSolve = 2, kMove = 4 };
+struct TrackCarry {
+    double* in;    // [na][10]: s[3], sd[3], ur[2], rv, rw
+    int32_t* flag;  // [na]
+    int32_t* admm;  // [na]
+};
+
+__global__ __launch_bounds__(kWave) void track_mpc_step(pmp_lp_params P, int na, int it, int iters,
+                                                        double* __restrict__ state, const double* __restrict__ goal,
+                                                        const double* __restrict__ path_xy,
+                                                        const int32_t* __restrict__ path_off, double* __restrict__ u_out,
+                                                        int32_t* __restrict__ status_out, int32_t* __restrict__ nsteps_out,
+                                                        double* __restrict__ hist_pose, int32_t* __restrict__ admm_out,
+                                                        TrackCarry C)
+{
+    const int v = threadIdx.x & 15;
+    const int a = blockIdx.x * kRows + (threadIdx.x >> 4);
+    if (a >= na) return;  // row-uniform: no cross-row work below
+    const double dt = P.dt;
+    double st[5];
+    for (int k = 0; k < 5; k++) st[k] = state[5 * a + k];
+    int flag, status, steps;
+    double u0, u1;
+    if (it == 0) {
+        flag = kLive;
+        status = steps = 0;
+        u0 = st[3];
+        u1 = st[4];
+    } else {
+        flag = C.flag[a];
+        status = status_out[a];
+        steps = nsteps_out[a];
+        u0 = u_out[2 * a];
+        u1 = u_out[2 * a + 1];
+    }
+    if (flag & kMove) {  // Robot.kinematic -> lookforward (agent.py:68-116) of iteration it - 1
+        if (v == 0 && hist_pose) {
+            double* hp = hist_pose + ((size_t)a * iters + (it - 1)) * 3;
+            hp[0] = st[0]; hp[1] = st[1]; hp[2] = st[2];
+        }
+        double sn, cs;
+        sincos(st[2], &sn, &cs);
+        const double nx = st[0] + (dt * cs) * u0, ny = st[1] + (dt * sn) * u0, nth = st[2] + dt * u1;
+        st[0] = nx; st[1] = ny; st[2] = nth; st[3] = u0; st[4] = u1;
+        steps++;
+    }
+    flag &= kLive;
+    double in[10];
+    if (it < iters && (flag & kLive)) {
+        const double* path = path_xy + 2 * (size_t)path_off[a];
+        const int Pn = path_off[a + 1] - path_off[a];
+        const double gl[3] = {goal[3 * a], goal[3 * a + 1], goal[3 * a + 2]};
+        if (lp::reach_goal(st, gl, P)) {
+            status = PMP_FOUND + 1;
+            flag = 0;
+        } else {
+            double pt[2] = {0, 0}, theta = 0, kappa = 0;
+            if (lookahead_row(path, Pn, st[0], st[1], st[3], P, pt, &theta, &kappa)) {
+                status = PMP_REF_RAISES;
+                flag = 0;
+            } else {
+                // calculate velocity command (mpc.py:75-91)
+                double e_theta = lp::regularize_angle(st[2] - gl[2]);
+                const double angreg_w = st[4];
+#define ANGREG(wd) lp::clampd(angreg_w + lp::clampd((wd) - angreg_w, P.min_w_inc, P.max_w_inc), P.min_w, P.max_w)
+                if (!(lp::py_hypot(gl[0] - st[0], gl[1] - st[1]) > P.goal_dist_tol)) {
+                    u0 = 0.0;
+                    u1 = fabs(e_theta) > P.rotate_tol ? ANGREG(e_theta / dt) : 0.0;
+                } else {
+                    e_theta = lp::regularize_angle(atan2(pt[1] - st[1], pt[0] - st[0]) - st[2]);
+                    if (fabs(e_theta) > P.rotate_tol) {
+                        u0 = 0.0;
+                        u1 = ANGREG(e_theta / dt);
+                    } else {
+                        in[0] = st[0]; in[1] = st[1]; in[2] = st[2];
+                        in[3] = pt[0]; in[4] = pt[1]; in[5] = theta;
+                        in[6] = st[3]; in[7] = st[3] * kappa;
+                        in[8] = st[3]; in[9] = st[4];
+                        flag |= kSolve;
+                    }
+                }
+#undef ANGREG
+                flag |= kMove;
+            }
+        }
+    }
+    if (v == 0) {
+        for (int k = 0; k < 5; k++) state[5 * a + k] = st[k];
+        u_out[2 * a] = u0;
+        u_out[2 * a + 1] = u1;
+        status_out[a] = status;
+        nsteps_out[a] = steps;
+        C.flag[a] = flag;
+        if (flag & kSolve)
+            for (int k = 0; k < 10; k++) C.in[10 * (size_t)a + k] = in[k];
+        if (it == 0) C.admm[a] = 0;
+        if (it == iters && admm_out) admm_out[a] = C.admm[a];
+    }
+}
+
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void track_mpc_solve(pmp_lp_params P, pmp_mpc_params M, int na,
+                                                         double* __restrict__ u_p, double* __restrict__ u_out,
+                                                         TrackCarry C)
+{
+    __shared__ double Hs[kMpcLds];
+    const int v = threadIdx.x & 15;
+    const int ai = blockIdx.x * kRows + (threadIdx.x >> 4);
+    const bool valid = ai < na;
+    const int a = valid ? ai : na - 1;
+    const bool solve = valid && (C.flag[a] & kSolve) != 0;
+    if (!ballot(solve)) return;  // wave-uniform
+    MpcIn I;
+    const double* in = C.in + 10 * (size_t)a;
+    if (solve) {
+        for (int k = 0; k < 3; k++) { I.s[k] = in[k]; I.sd[k] = in[3 + k]; }
+        I.ur[0] = in[6]; I.ur[1] = in[7]; I.rv = in[8]; I.rw = in[9];
+    } else {  // rows not solving carry harmless inputs through the wave-wide assembly
+        for (int k = 0; k < 3; k++) { I.s[k] = 0.0; I.sd[k] = 0.0; }
+        I.ur[0] = I.ur[1] = I.rv = I.rw = 0.0;
+    }
+    double up0 = u_p[2 * a], up1 = u_p[2 * a + 1];
+    const MpcResult R = mpc_rows(solve, I, up0, up1, P, M, Hs, nullptr, nullptr, nullptr, nullptr);
+    if (solve && v == 0) {
+        u_p[2 * a] = up0;
+        u_p[2 * a + 1] = up1;
+        u_out[2 * a] = R.u0;
+        u_out[2 * a + 1] = R.u1;
+        C.admm[a] += R.iters;
+    }
+}
+
 int check_mpc(pmp_ctx* ctx, const pmp_mpc_params* mp, const char* who)
 {
     if (mp->m < 1 || mp->m > 8 || mp->p < 1 || mp->p > 4096 || mp->max_iter < 1 || !(mp->rho > 0) ||
@@ -744,9 +881,23 @@ extern "C" int pmp_track_step_batch(pmp_ctx* ctx, void* stream, int kind, const 
     if (kind == PMP_TRACK_LQR)
         hipLaunchKernelGGL(track_kernel<PMP_TRACK_LQR>, dim3((na + kRows - 1) / kRows), dim3(kWave), 0, (hipStream_t)stream, *lp, L, M, na,
                            state, u_p, goal, path_xy, path_off, iters, u, status, n_steps, hist_pose, admm_iters);
-    else
-        hipLaunchKernelGGL(track_kernel<PMP_TRACK_MPC>, dim3((na + kRows - 1) / kRows), dim3(kWave), 0, (hipStream_t)stream, *lp, L, M, na,
-                           state, u_p, goal, path_xy, path_off, iters, u, status, n_steps, hist_pose, admm_iters);
+    else {
+        // MPC: 2 iters + 1 launches (track_mpc_step / track_mpc_solve per iteration, a last step)
+        TrackCarry C;
+        const size_t nb = (size_t)na;
+        char* scr = (char*)pmp_scratch(ctx, SCR_AUX4, nb * 80 + nb * 8 + 64);
+        if (!scr) return PMP_ENOMEM;
+        C.in = (double*)scr;
+        C.flag = (int32_t*)(scr + nb * 80);
+        C.admm = C.flag + nb;
+        const dim3 grid((na + kRows - 1) / kRows);
+        hipStream_t s = (hipStream_t)stream;
+        for (int it = 0; it <= iters; it++) {
+            hipLaunchKernelGGL(track_mpc_step, grid, dim3(kWave), 0, s, *lp, na, it, iters, state, goal, path_xy, path_off,
+                               u, status, n_steps, hist_pose, admm_iters, C);
+            if (it < iters) hipLaunchKernelGGL(track_mpc_solve, grid, dim3(kWave), 0, s, *lp, M, na, u_p, u, C);
+        }
+    }
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }

@@ -1,7 +1,5 @@
-# one GPU call: register-inverse build under the tracking tests + mpc leg, then the LDS default's mpc leg
+# one GPU call: tracking tests with the split MPC (step / solve kernels), then the mpc leg at 8192 / 32768 agents
 cd $GRAFT_REPO_ROOT
-export PMPR=$GRAFT_REPO_ROOT/python_motion_planning_amd/libpmp_hip_invreg.so
-PMP_HIP_LIB=$PMPR timeout -k 10 300 python -u -m pytest tests/test_track_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r3_t12.log 2>&1 && \
-PMP_HIP_LIB=$PMPR timeout -k 10 300 python bench.py --legs mpc --no-cpu-baseline --steps 2 --warmup 1 --detail-out gpurun_out/r3_b12r.json > /dev/null 2> gpurun_out/r3_b12.err && \
-timeout -k 10 300 python bench.py --legs mpc --no-cpu-baseline --steps 2 --warmup 1 --detail-out gpurun_out/r3_b12l.json > /dev/null 2>> gpurun_out/r3_b12.err && \
-PMP_HIP_LIB=$PMPR timeout -k 10 300 python bench.py --legs mpc --no-cpu-baseline --steps 2 --warmup 1 --track-agents 32768 --detail-out gpurun_out/r3_b12r32.json > /dev/null 2>> gpurun_out/r3_b12.err
+timeout -k 10 300 python -u -m pytest tests/test_track_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r3_t13.log 2>&1 && \
+timeout -k 10 300 python bench.py --legs mpc --no-cpu-baseline --steps 2 --warmup 1 --track-agents 8192 --detail-out gpurun_out/r3_b13a.json > /dev/null 2> gpurun_out/r3_b13.err && \
+timeout -k 10 300 python bench.py --legs mpc --no-cpu-baseline --steps 2 --warmup 1 --detail-out gpurun_out/r3_b13b.json > /dev/null 2>> gpurun_out/r3_b13.err
