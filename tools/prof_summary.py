@@ -31,6 +31,8 @@ KERNELS = {  # short name -> regex on the demangled kernel name
     "lpa3d_kernel": r"\blpa3d_kernel[<(]",
     "track_kernel_lqr": r"track_kernel<0>",
     "track_kernel_mpc": r"track_kernel<1>",
+    "track_mpc_step": r"\btrack_mpc_step\(",
+    "track_mpc_solve": r"\btrack_mpc_solve\(",
     "lqr_control_kernel": r"\blqr_control_kernel[<(]",
     "mpc_control_kernel": r"\bmpc_control_kernel[<(]",
     "totp3d_kernel": r"\btotp3d_kernel[<(]",

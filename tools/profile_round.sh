@@ -3,21 +3,27 @@
 # separate PMC passes (FETCH_SIZE, WRITE_SIZE cannot share a pass on gfx950) of a shorter bench, then
 # the MFMA pass of the MPC leg.  Each pass writes the bench's launch manifest (--detail-out) beside
 # its database, so tools/prof_summary.py keys every dispatch by its workload.
-# Outputs under gpurun_out/; summarise with `python tools/prof_summary.py gpurun_out profiles/<round>`.
+# The PMC passes keep the default per-launch batch counts of the multi-batch legs (the A* headline's
+# 20 batches in one launch, 3D A*'s 32), so a dispatch there is the same work as in the default run;
+# the other legs are shortened (fewer launches of the same size).
+# Outputs under gpurun_out/; the summary is written on the box (ROUND=r3 -> gpurun_out/profiles_r3)
+# and the databases are deleted (they would exceed gpurun_out's 64 MiB).
 set -e
 R=${GRAFT_REPO_ROOT:-/root/repo}
 OUT=$R/gpurun_out
 mkdir -p $OUT/prof_kt $OUT/prof_fetch $OUT/prof_write $OUT/prof_mfma
 cd /tmp && export TMPDIR=/tmp
-SHORT="--no-cpu-baseline --steps 3 --warmup 1 --rrt-steps 1 --a3-steps 2 --track-steps 1 --control-steps 2 --graph-steps 2 --dstar-steps 2 --dyn3d-steps 2"
+SHORT="--no-cpu-baseline --warmup 1 --rrt-steps 1 --track-steps 1 --control-steps 2 --graph-steps 2 --dstar-steps 2 --dyn3d-steps 2"
 [ "${SKIP_KT:-0}" = 1 ] || timeout -k 10 700 rocprofv3 --kernel-trace --stats -d $OUT/prof_kt -o run -- python3 $R/bench.py \
     --detail-out $OUT/prof_kt/detail.json > $OUT/bench_prof.json 2> $OUT/bench_prof.err
 timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE -d $OUT/prof_fetch -o run -- python3 $R/bench.py $SHORT \
     --detail-out $OUT/prof_fetch/detail.json > $OUT/bench_fetch.json 2> $OUT/bench_fetch.err
 timeout -k 10 500 rocprofv3 --pmc WRITE_SIZE -d $OUT/prof_write -o run -- python3 $R/bench.py $SHORT \
     --detail-out $OUT/prof_write/detail.json > $OUT/bench_write.json 2> $OUT/bench_write.err
-# MFMA utilisation of the MPC tracking kernel (track_kernel<1>): its own pass
+# MFMA utilisation of the MPC tracking kernels (track_mpc_solve carries the assembly): its own pass
 timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES SQ_BUSY_CYCLES -d $OUT/prof_mfma -o run \
     -- python3 $R/bench.py --no-cpu-baseline --legs mpc --steps 1 --warmup 1 --track-steps 2 \
     --detail-out $OUT/prof_mfma/detail.json > $OUT/bench_mfma.json 2> $OUT/bench_mfma.err
+python3 $R/tools/prof_summary.py $OUT $OUT/profiles_${ROUND:-r3} > $OUT/prof_summary.log 2>&1
+rm -rf $OUT/prof_kt/*/ $OUT/prof_fetch/*/ $OUT/prof_write/*/ $OUT/prof_mfma/*/ $OUT/prof_kt/*.db $OUT/prof_fetch/*.db $OUT/prof_write/*.db $OUT/prof_mfma/*.db
 echo profile-done
