@@ -1,3 +1,3 @@
-# one GPU call: the round's profile (kernel trace of the default bench, FETCH / WRITE / MFMA passes), summarised on the box
+# one GPU call: A* 2D traffic attribution across engines / LDS heap shares
 cd $GRAFT_REPO_ROOT
-ROUND=r3 timeout -k 10 1500 bash tools/profile_round.sh > gpurun_out/r3_profile.log 2>&1
+timeout -k 10 1000 bash tools/traffic_probe.sh mq32:2:1:8192:32 mq8:2:1:2048:8 mq4:2:1:1024:4 w18:0:0:768:18 w4:0:0:1024:4 > gpurun_out/r3_traffic.log 2>&1
