@@ -768,55 +768,63 @@ def graphs_leg(args, torch, dist, world, rank):
     s2, g2 = s2[:nq], g2[:nq]
     occ_bits = batch.occ_bits_device(occ2, torch)
     s2d, g2d = torch.as_tensor(s2, device="cuda"), torch.as_tensor(g2, device="cuda")
+    # Batches per launch (as the headline): B of the steps' batches per launch, streamed through the
+    # launch's persistent workers longest first; B = 1 with several streams = batches in flight.
+    B = max(1, min(args.theta_batches_per_launch or args.graph_steps, args.graph_steps))
+    nlaunch = -(-args.graph_steps // B)
+    S = max(1, min(args.theta_streams, nlaunch))
+    s_rep, g_rep = s2d.repeat(B, 1), g2d.repeat(B, 1)
+    tw = args.theta_workers if B == 1 else 256 * args.theta_residency
     for algo in ("theta_star", "lazy_theta_star"):
-        _LABEL[0] = algo + "_2d"
-        # batches in flight as in the headline (own stream + pmp_ctx each)
+        _LABEL[0] = algo + "_2d_warmup"
         lanes = []
-        for _ in range(max(1, args.theta_streams)):
+        for _ in range(S):
             ctx = L.pmp_create(torch.cuda.current_device())
             _lib.check(ctx, L.pmp_astar2d_set_engine(ctx, 0, 0), "engine")  # Theta*: one query per wave
-            _lib.check(ctx, L.pmp_astar2d_reserve(ctx, 1024, 1024, args.theta_workers, 0), "reserve")
+            _lib.check(ctx, L.pmp_astar2d_reserve(ctx, 1024, 1024, tw, 0), "reserve")
             if args.theta_residency:
                 _lib.check(ctx, L.pmp_astar2d_set_residency(ctx, args.theta_residency), "residency")
             lanes.append(dict(ctx=ctx, stream=pool_stream(torch, len(lanes)),
-                              cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
-                              plen=torch.empty(nq, dtype=torch.int32, device="cuda"),
-                              path=torch.empty((nq, 8192), dtype=torch.int32, device="cuda"),
-                              nexp=torch.empty(nq, dtype=torch.int32, device="cuda"),
-                              st=torch.empty(nq, dtype=torch.int32, device="cuda")))
+                              cost=torch.empty(B * nq, dtype=torch.float64, device="cuda"),
+                              plen=torch.empty(B * nq, dtype=torch.int32, device="cuda"),
+                              path=torch.empty((B * nq, 8192), dtype=torch.int32, device="cuda"),
+                              nexp=torch.empty(B * nq, dtype=torch.int32, device="cuda"),
+                              st=torch.empty(B * nq, dtype=torch.int32, device="cuda")))
         ctr = torch.empty((nq, 4), dtype=torch.int64, device="cuda")
 
-        def run(i, algo=algo, counters=None):
+        def run(i, nb, algo=algo, counters=None):
             b = lanes[i % len(lanes)]
             rc = L.pmp_graph2d_batch(b["ctx"], b["stream"].cuda_stream, _lib.ALGOS[algo], occ_bits.data_ptr(), 1024, 1024,
-                                     0, s2d.data_ptr(), g2d.data_ptr(), nq, b["cost"].data_ptr(), b["plen"].data_ptr(),
-                                     b["path"].data_ptr(), 8192, b["nexp"].data_ptr(), None, 0, counters,
-                                     b["st"].data_ptr())
+                                     0, s_rep.data_ptr(), g_rep.data_ptr(), nq * nb, b["cost"].data_ptr(),
+                                     b["plen"].data_ptr(), b["path"].data_ptr(), 8192, b["nexp"].data_ptr(), None, 0,
+                                     counters, b["st"].data_ptr())
             if rc:
                 _lib.check(b["ctx"], rc, "pmp_graph2d_batch")
 
-        run(0, counters=ctr.data_ptr())
+        run(0, 1, counters=ctr.data_ptr())
         for i in range(1, len(lanes)):
-            run(i)
+            run(i, 1)
         torch.cuda.synchronize()
-        r = {"cost": lanes[0]["cost"].clone(), "status": lanes[0]["st"].clone()}
+        _LABEL[0] = algo + "_2d"
+        r = {"cost": lanes[0]["cost"][:nq].clone(), "status": lanes[0]["st"][:nq].clone()}
         assert (r["status"] == 0).all(), f"unexpected {algo} statuses"
         for b in lanes[1:]:
-            assert torch.equal(b["cost"], r["cost"])
+            assert torch.equal(b["cost"][:nq], r["cost"])
         gkeys = ("cost", "plen", "nexp", "st")
-        ref_out = {k: lanes[0][k].clone() for k in gkeys}
+        ref_out = {k: lanes[0][k][:nq].clone() for k in gkeys}
         for b in lanes:
             poison([b[k] for k in gkeys])
         c = ctr.cpu().numpy()
         shard.barrier(dist)
         torch.cuda.synchronize()
         evs = []
+        nbs = [min(B, args.graph_steps - i * B) for i in range(nlaunch)]
         t0 = time.perf_counter()
-        for i in range(args.graph_steps):
+        for i in range(nlaunch):
             b = lanes[i % len(lanes)]
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(b["stream"])
-            run(i)
+            run(i, nbs[i])
             e1.record(b["stream"])
             evs.append((e0, e1))
         torch.cuda.synchronize()
@@ -824,11 +832,15 @@ def graphs_leg(args, torch, dist, world, rank):
         elapsed = time.perf_counter() - t0
         kern_ms = float(np.mean([a.elapsed_time(e) for a, e in evs]))
         elapsed, kern_ms = shard.max_over_ranks(dist, [elapsed, kern_ms], "cuda")
-        checked = check_timed(algo, ref_out, lanes[: min(len(lanes), args.graph_steps)])
+        outs = []
+        for li, b in enumerate(lanes[: min(S, nlaunch)]):
+            last_nb = nbs[max(i for i in range(nlaunch) if i % S == li)]
+            outs += [{k: b[k][j * nq:(j + 1) * nq] for k in gkeys} for j in range(last_nb)]
+        checked = check_timed(algo, ref_out, outs)
         for b in lanes:  # their scratch (about 40 GB each with the Theta* parents) is not needed later
             L.pmp_destroy(b["ctx"])
         lanes.clear()
-        alg = astar_algorithmic_bytes(c)
+        alg = astar_algorithmic_bytes(c) * float(np.mean(nbs))
         achieved = alg / (kern_ms * 1e-3) / 1e9
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -844,14 +856,15 @@ def graphs_leg(args, torch, dist, world, rank):
                              f"queries, {dt:.1f} s wall"}
         out[algo + "_2d"] = {
             "metric": f"{algo} 2D plans/sec on the C2 1024^2 grid", "value": nq * args.graph_steps * world / elapsed,
-            "unit": "plans/s", "queries_per_gpu": nq, "steps": args.graph_steps, "streams": args.theta_streams,
+            "unit": "plans/s", "queries_per_gpu": nq, "steps": args.graph_steps, "streams": S,
+            "batches_per_launch": B, "workers": tw, "resident_per_cu": args.theta_residency,
             "timed_launches_checked": checked,
             "ms_per_step": elapsed / args.graph_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
             "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                       "frac": achieved / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": alg,
                                       "note": "A*'s 19E + 16(P+Q) bytes; the line-of-sight cells are not counted"},
                                      "theta2d_kernel" if algo == "theta_star" else "lazy_theta2d_kernel", algo + "_2d"),
-            "detail": {"expansions_per_launch": int(c[:, 2].sum()), "pushes_per_launch": int(c[:, 0].sum())},
+            "detail": {"expansions_per_batch": int(c[:, 2].sum()), "pushes_per_batch": int(c[:, 0].sum())},
             "cpu_baseline": cpu}
 
     occ = wl.readme_grid()
@@ -969,52 +982,58 @@ def dstar_leg(args, torch, dist, world, rank):
     out = {}
     for W, nq in ((256, args.dstar_queries), (512, args.dstar_queries)):
         occ, s, g = wl.c2_workload(nq=nq, W=W, H=W, density=0.1, grid_seed=4, pair_seed=5 + rank)
-        _LABEL[0] = f"dstar_{W}"
+        _LABEL[0] = f"dstar_{W}_warmup"
         s_d, g_d = torch.as_tensor(s, device="cuda"), torch.as_tensor(g, device="cuda")
         bits = batch.occ_bits_device(occ, torch)
-        # batches in flight (own stream + pmp_ctx each): one wave per query, so a launch lasts as long
-        # as its longest query and the next launch's workers fill the CUs the finished ones free
+        # B batches per launch (continuous batching, as the headline), or B = 1 with batches in flight
+        # on their own streams (own pmp_ctx each)
+        B = max(1, min(args.dstar_batches_per_launch or args.dstar_steps, args.dstar_steps))
+        nlaunch = -(-args.dstar_steps // B)
+        S = max(1, min(args.dstar_streams, nlaunch))
+        s_rep, g_rep = s_d.repeat(B, 1), g_d.repeat(B, 1)
         lanes = []
-        for _ in range(max(1, args.dstar_streams)):
+        for _ in range(S):
             ctx = L.pmp_create(torch.cuda.current_device())
             _lib.check(ctx, L.pmp_set_workers_per_cu(ctx, args.dstar_workers_per_cu), "workers")
             _lib.check(ctx, L.pmp_set_resident_per_cu(ctx, args.dstar_residency), "residency")
             lanes.append(dict(ctx=ctx, stream=pool_stream(torch, len(lanes)),
-                              cost=torch.empty(nq, dtype=torch.float64, device="cuda"),
-                              plen=torch.empty(nq, dtype=torch.int32, device="cuda"),
-                              path=torch.empty((nq, 4 * W), dtype=torch.int32, device="cuda"),
-                              npr=torch.empty(nq, dtype=torch.int64, device="cuda"),
-                              st=torch.empty(nq, dtype=torch.int32, device="cuda")))
+                              cost=torch.empty(B * nq, dtype=torch.float64, device="cuda"),
+                              plen=torch.empty(B * nq, dtype=torch.int32, device="cuda"),
+                              path=torch.empty((B * nq, 4 * W), dtype=torch.int32, device="cuda"),
+                              npr=torch.empty(B * nq, dtype=torch.int64, device="cuda"),
+                              st=torch.empty(B * nq, dtype=torch.int32, device="cuda")))
 
-        def run(i):
+        def run(i, nb):
             b = lanes[i % len(lanes)]
-            rc = L.pmp_dstar2d_batch(b["ctx"], b["stream"].cuda_stream, bits.data_ptr(), W, W, s_d.data_ptr(),
-                                     g_d.data_ptr(), nq, b["cost"].data_ptr(), b["plen"].data_ptr(), b["path"].data_ptr(),
-                                     4 * W, b["npr"].data_ptr(), b["st"].data_ptr(), 0)
+            rc = L.pmp_dstar2d_batch(b["ctx"], b["stream"].cuda_stream, bits.data_ptr(), W, W, s_rep.data_ptr(),
+                                     g_rep.data_ptr(), nq * nb, b["cost"].data_ptr(), b["plen"].data_ptr(),
+                                     b["path"].data_ptr(), 4 * W, b["npr"].data_ptr(), b["st"].data_ptr(), 0)
             if rc:
                 _lib.check(b["ctx"], rc, "pmp_dstar2d_batch")
 
         for i in range(len(lanes)):
-            run(i)
+            run(i, 1)
         torch.cuda.synchronize()
-        r = {"cost": lanes[0]["cost"], "n_process": lanes[0]["npr"], "status": lanes[0]["st"]}
+        _LABEL[0] = f"dstar_{W}"
+        r = {"cost": lanes[0]["cost"][:nq], "n_process": lanes[0]["npr"][:nq], "status": lanes[0]["st"][:nq]}
         for b in lanes[1:]:
-            assert torch.equal(b["cost"], r["cost"]) and torch.equal(b["npr"], r["n_process"])
+            assert torch.equal(b["cost"][:nq], r["cost"]) and torch.equal(b["npr"][:nq], r["n_process"])
         npr = r["n_process"].cpu().numpy()
         st = r["status"].cpu().numpy()
         dkeys = ("cost", "plen", "npr", "st")
-        ref_out = {k: lanes[0][k].clone() for k in dkeys}
+        ref_out = {k: lanes[0][k][:nq].clone() for k in dkeys}
         for b in lanes:
             poison([b[k] for k in dkeys])
         shard.barrier(dist)
         torch.cuda.synchronize()
         evs = []
+        nbs = [min(B, args.dstar_steps - i * B) for i in range(nlaunch)]
         t0 = time.perf_counter()
-        for i in range(args.dstar_steps):
+        for i in range(nlaunch):
             b = lanes[i % len(lanes)]
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(b["stream"])
-            run(i)
+            run(i, nbs[i])
             e1.record(b["stream"])
             evs.append((e0, e1))
         torch.cuda.synchronize()
@@ -1022,7 +1041,11 @@ def dstar_leg(args, torch, dist, world, rank):
         elapsed = time.perf_counter() - t0
         kern_ms = float(np.mean([a.elapsed_time(e) for a, e in evs]))
         elapsed, kern_ms = shard.max_over_ranks(dist, [elapsed, kern_ms], "cuda")
-        checked = check_timed(f"dstar_{W}", ref_out, lanes[: min(len(lanes), args.dstar_steps)])
+        outs = []
+        for li, b in enumerate(lanes[: min(S, nlaunch)]):
+            last_nb = nbs[max(i for i in range(nlaunch) if i % S == li)]
+            outs += [{k: b[k][j * nq:(j + 1) * nq] for k in dkeys} for j in range(last_nb)]
+        checked = check_timed(f"dstar_{W}", ref_out, outs)
         r = {"cost": ref_out["cost"], "n_process": ref_out["npr"], "status": ref_out["st"]}
         torch.cuda.synchronize()
         for b in lanes:
@@ -1030,7 +1053,7 @@ def dstar_leg(args, torch, dist, world, rank):
         lanes.clear()
         # algorithmic bytes per processState: the 3x3 block of cell states (h, k f64 + tag / parent:
         # 24 B each) read + ~2 OPEN entries (16 B) inserted / removed
-        alg = float(npr.sum()) * (9 * 24 + 2 * 16)
+        alg = float(npr.sum()) * (9 * 24 + 2 * 16) * float(np.mean(nbs))
         achieved = alg / (kern_ms * 1e-3) / 1e9
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -1051,7 +1074,7 @@ def dstar_leg(args, torch, dist, world, rank):
             "metric": f"DStar plans/sec on a {W}x{W} grid (10% obstacles, {nq} random start/goal pairs)",
             "value": nq * args.dstar_steps * world / elapsed, "unit": "plans/s", "queries_per_gpu": nq,
             "steps": args.dstar_steps, "ms_per_step": elapsed / args.dstar_steps * 1e3, "kernel_ms_per_launch": kern_ms,
-            "dtype": "f64", "streams": args.dstar_streams, "timed_launches_checked": checked,
+            "dtype": "f64", "streams": S, "batches_per_launch": B, "timed_launches_checked": checked,
             "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                       "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                                       "algorithmic_bytes_per_launch": alg,
@@ -1083,20 +1106,28 @@ def dyn3d_leg(args, torch, dist, world, rank):
     # the grids packed once (device words), outside the timed region
     bits = torch.as_tensor(np.ascontiguousarray(np.stack([batch.pack_bits(o) for o in occ])).view(np.int32),
                            device="cuda")
-    # batches in flight: consecutive launches on different streams (the per-stream contexts of
-    # _lib.context), so the next launch's workers fill the CUs the finished ones free
-    streams = [pool_stream(torch, i) for i in range(max(1, args.dyn3d_streams))]
+    # B batches per launch (continuous batching through the launch's persistent workers, longest
+    # first), or B = 1 with batches in flight: consecutive launches on different streams (the
+    # per-stream contexts of _lib.context), so the next launch's workers fill the CUs the finished ones free
+    B = max(1, min(args.dyn3d_batches_per_launch or args.dyn3d_steps, args.dyn3d_steps))
+    nlaunch = -(-args.dyn3d_steps // B)
+    streams = [pool_stream(torch, i) for i in range(max(1, min(args.dyn3d_streams, nlaunch)))]
+    s_rep, g_rep, bits_rep = s_d.repeat(B, 1), g_d.repeat(B, 1), bits.repeat(B, 1)
     out = {}
     for kind, rounds in (("dstar3d", None), ("dstar3d", inner), ("lpastar3d", None), ("lpastar3d", changes)):
-        _LABEL[0] = kind + ("" if rounds is None else "_replan")
+        _LABEL[0] = kind + ("" if rounds is None else "_replan") + "_warmup"
         rd = None if rounds is None else torch.as_tensor(rounds, device="cuda")
+        rd_rep = None if rd is None else rd.repeat(B, *([1] * (rd.dim() - 1)))
 
-        def run(i, kind=kind, rd=rd, counters=False):
+        def run(i, nb=1, kind=kind, rd_rep=rd_rep, counters=False):
+            m = nq * nb
+            r_ = None if rd_rep is None else rd_rep[:m]
             with torch.cuda.stream(streams[i % len(streams)]):
                 if kind == "dstar3d":
-                    return batch.dstar3d_batch(occ.shape, s_d, g_d, rd, path_cap=X * Y * Z + 1, occ_bits=bits)
-                return batch.lpastar3d_batch(occ.shape, s_d, g_d, rd, path_cap=X * Y * Z + 1, occ_bits=bits,
-                                             counters=counters)
+                    return batch.dstar3d_batch(occ.shape, s_rep[:m], g_rep[:m], r_, path_cap=X * Y * Z + 1,
+                                               occ_bits=bits_rep[:m])
+                return batch.lpastar3d_batch(occ.shape, s_rep[:m], g_rep[:m], r_, path_cap=X * Y * Z + 1,
+                                             occ_bits=bits_rep[:m], counters=counters)
 
         r = run(0, counters=True)
         torch.cuda.synchronize()
@@ -1109,19 +1140,21 @@ def dyn3d_leg(args, torch, dist, world, rank):
         del r
         # one untimed launch per stream whose outputs are freed: the timed launches then reuse those
         # blocks from the stream's caching-allocator pool instead of allocating (and synchronising)
+        nbs = [min(B, args.dyn3d_steps - i * B) for i in range(nlaunch)]
         for i in range(len(streams)):
-            run(i)
+            run(i, nbs[i])
         torch.cuda.synchronize()
+        _LABEL[0] = kind + ("" if rounds is None else "_replan")
         shard.barrier(dist)
         torch.cuda.synchronize()
         evs = []
         lastr = {}
         t0 = time.perf_counter()
-        for i in range(args.dyn3d_steps):
+        for i in range(nlaunch):
             sm = streams[i % len(streams)]
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(sm)
-            lastr[i % len(streams)] = run(i)
+            lastr[i % len(streams)] = (run(i, nbs[i]), nbs[i])
             e1.record(sm)
             evs.append((e0, e1))
         torch.cuda.synchronize()
@@ -1129,8 +1162,9 @@ def dyn3d_leg(args, torch, dist, world, rank):
         elapsed = time.perf_counter() - t0
         kern_ms = float(np.mean([a.elapsed_time(e) for a, e in evs]))
         elapsed, kern_ms = shard.max_over_ranks(dist, [elapsed, kern_ms], "cuda")
-        checked = check_timed(kind, ref_out, list(lastr.values()))
-        del lastr
+        outs = [{k: rr[k][j * nq:(j + 1) * nq] for k in ref_out} for rr, nb_ in lastr.values() for j in range(nb_)]
+        checked = check_timed(kind, ref_out, outs)
+        del lastr, outs
         R = 1 if rounds is None else rounds.shape[1] + 1
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -1160,11 +1194,13 @@ def dyn3d_leg(args, torch, dist, world, rank):
             "timed_launches_checked": checked,
             "steps": args.dyn3d_steps, "ms_per_step": elapsed / args.dyn3d_steps * 1e3, "kernel_ms_per_launch": kern_ms,
             "dtype": "f64",
-            "roofline": with_traffic(dyn3d_roof(kind, int(np.maximum(nexp, 0).sum()), pushes, kern_ms),
+            "roofline": with_traffic(dyn3d_roof(kind, int(np.maximum(nexp, 0).sum() * np.mean(nbs)),
+                                                None if pushes is None else int(pushes * np.mean(nbs)), kern_ms),
                                      "dstar3d_kernel" if kind == "dstar3d" else "lpa3d_kernel", name),
             "roofline_note": "latency-bound list machines (OPEN / U with Python-list semantics): a small frac is "
                              "the expected reading",
-            "detail": {"expansions_per_launch": int(np.maximum(nexp, 0).sum()),
+            "streams": len(streams), "batches_per_launch": B,
+            "detail": {"expansions_per_batch": int(np.maximum(nexp, 0).sum()),
                        "statuses": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))}},
             "cpu_baseline": cpu}
     _LABEL[0] = "setup"
@@ -1450,7 +1486,9 @@ def main():
                     help="A* queries in flight per launch (persistent 16-lane groups on engine 1, waves on engine 0); "
                          "0 = the engine's default")
     ap.add_argument("--theta-workers", type=int, default=768, help="persistent Theta* 2D workers per launch")
-    ap.add_argument("--theta-residency", type=int, default=18, help="Theta* 2D workers resident per CU (as --residency)")
+    ap.add_argument("--theta-residency", type=int, default=24,
+                    help="Theta* 2D workers resident per CU (as --residency; with one multi-batch launch: 256 x this "
+                         "many workers; 12 / 18 / 24 / 28 / 32: 8.5 / 11.3 / 11.9 / 11.85 / 11.75 k plans/s)")
     ap.add_argument("--residency", type=int, default=0,
                     help="A* queries resident per CU over all batches in flight (sets each one's LDS heap share; "
                          "0 = the engine's default)")
@@ -1459,13 +1497,23 @@ def main():
                          "astar3d leg's paths), lqr, mpc, graphs, dstar, dyn3d, latency; 'none' for none)")
     ap.add_argument("--dyn3d-queries", type=int, default=8192, help="C5 queries per DStar3D / LPAStar3D launch")
     ap.add_argument("--dyn3d-steps", type=int, default=24)
-    ap.add_argument("--dyn3d-streams", type=int, default=6, help="DStar3D / LPAStar3D batches in flight")
-    ap.add_argument("--dstar-queries", type=int, default=4096, help="queries per D* launch (256^2 and 512^2 grids)")
+    ap.add_argument("--dyn3d-streams", type=int, default=4, help="DStar3D / LPAStar3D launches in flight")
+    ap.add_argument("--dyn3d-batches-per-launch", type=int, default=6,
+                    help="DStar3D / LPAStar3D batches per launch (0 = all the timed steps in one launch; LPAStar3D "
+                         "169 k / 315 k / 321 k plans/s at 1 x 6 streams / 24 x 1 / 6 x 4)")
+    ap.add_argument("--dstar-queries", type=int, default=4096, help="queries per D* batch (256^2 and 512^2 grids)")
+    ap.add_argument("--dstar-batches-per-launch", type=int, default=1,
+                    help="D* batches per launch (0 = all the timed steps in one launch; 1 = one per launch on "
+                         "--dstar-streams: faster here, 4,180 vs 2,650-3,090 plans/s at 512^2, D* has no "
+                         "longest-first order)")
     ap.add_argument("--dstar-steps", type=int, default=9)
     ap.add_argument("--lpa-streams", type=int, default=3, help="LPA* / D* Lite 2D batches in flight")
     ap.add_argument("--theta-streams", type=int, default=6, help="Theta* 2D batches in flight (own stream + context each)")
     ap.add_argument("--dstar-streams", type=int, default=3, help="D* batches in flight (own stream + context each)")
-    ap.add_argument("--theta-queries", type=int, default=4096, help="C2 queries per Theta* / Lazy Theta* 2D launch")
+    ap.add_argument("--theta-queries", type=int, default=4096, help="C2 queries per Theta* / Lazy Theta* 2D batch")
+    ap.add_argument("--theta-batches-per-launch", type=int, default=0,
+                    help="Theta* 2D batches per launch (0 = all the timed steps in one launch, streamed through "
+                         "256 x --theta-residency persistent workers; 1 = one batch per launch on --theta-streams)")
     ap.add_argument("--lpa-queries", type=int, default=16384,
                     help="README-grid queries per LPA* / D* Lite launch (4 per worker wave: the queue balances the tail)")
     ap.add_argument("--graph-steps", type=int, default=12)

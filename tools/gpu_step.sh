@@ -1,3 +1,6 @@
-# one GPU call: A* 2D traffic attribution across engines / LDS heap shares
+# one GPU call: dyn3d legs, one batch per launch on 6 streams vs all 24 batches in one launch / 6 per launch
 cd $GRAFT_REPO_ROOT
-timeout -k 10 1000 bash tools/traffic_probe.sh mq32:2:1:8192:32 mq8:2:1:2048:8 mq4:2:1:1024:4 w18:0:0:768:18 w4:0:0:1024:4 > gpurun_out/r3_traffic.log 2>&1
+B="python bench.py --no-cpu-baseline --steps 1 --warmup 1 --legs dyn3d"
+timeout -k 10 400 $B --detail-out gpurun_out/r3_b16a.json > /dev/null 2> gpurun_out/r3_b16.err && \
+timeout -k 10 400 $B --dyn3d-batches-per-launch 0 --detail-out gpurun_out/r3_b16b.json > /dev/null 2>> gpurun_out/r3_b16.err && \
+timeout -k 10 400 $B --dyn3d-batches-per-launch 6 --dyn3d-streams 4 --detail-out gpurun_out/r3_b16c.json > /dev/null 2>> gpurun_out/r3_b16.err
