@@ -1514,8 +1514,9 @@ def main():
     ap.add_argument("--theta-batches-per-launch", type=int, default=0,
                     help="Theta* 2D batches per launch (0 = all the timed steps in one launch, streamed through "
                          "256 x --theta-residency persistent workers; 1 = one batch per launch on --theta-streams)")
-    ap.add_argument("--lpa-queries", type=int, default=16384,
-                    help="README-grid queries per LPA* / D* Lite launch (4 per worker wave: the queue balances the tail)")
+    ap.add_argument("--lpa-queries", type=int, default=65536,
+                    help="README-grid queries per LPA* / D* Lite launch (4 per worker wave: the queue balances the "
+                         "tail; 16,384 / 65,536 per launch: 1.11 M / 1.19 M plans/s, replanning 4.16 M / 4.81 M)")
     ap.add_argument("--graph-steps", type=int, default=12)
     ap.add_argument("--rrt-queries", type=int, default=256)
     ap.add_argument("--rrt-samples", type=int, default=65536)
