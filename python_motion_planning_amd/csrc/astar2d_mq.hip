@@ -558,29 +558,34 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
             const int x = ndir == 8 ? sx : gx - cm_dx(ncm);
             const int y = ndir == 8 ? sy : gy - cm_dy(ncm);
             const uint32_t nlin = (uint32_t)x * (uint32_t)H + (uint32_t)y;
-            uint32_t blk_w = 0u, blk_w2 = 0u;
-            int blk_sh = 0;
-            bool blk_in = false;
-            double gpar = 0.0;
+            // Every lane issues all three loads (lanes that need none read index 0): no branch per lane
+            // class, so no load destination is zero-filled under another exec mask -- that WAW on a
+            // register with a load in flight made the compiler wait for each load in turn (three
+            // serialised HBM round trips per pop before the heap's own load round).
+            uint32_t blk_w, blk_w2;
+            int blk_sh;
+            bool blk_in;
+            double gpar;
             {
                 const int cx = x + blk_dx, cy = y + blk_dy;
-                if (gl < 9) {
-                    blk_in = (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
-                    const uint32_t ci = blk_in ? (uint32_t)cx * (uint32_t)H + (uint32_t)cy : 0u;
-                    blk_sh = (int)(ci & 31u);
-                    blk_w = occ[ci >> 5];
-                } else if (gl < 12) {
-                    blk_in = (unsigned)cx < (unsigned)W;
-                    // bytes of (cx, y-1 .. y+1) inside the 8-byte window at a0 (4-aligned)
-                    const uint32_t lo = blk_in ? (uint32_t)cx * (uint32_t)H + (uint32_t)(y > 0 ? y - 1 : 0) : 0u;
-                    const uint32_t a0 = lo & ~3u;
-                    blk_sh = (int)((uint32_t)cx * (uint32_t)H + (uint32_t)y - 1u - a0);  // byte of cell y-1 (may be -1)
-                    const uint32_t* p32 = reinterpret_cast<const uint32_t*>(cst + a0);
-                    blk_w = p32[0];
-                    blk_w2 = p32[1];
-                } else if (gl == 12 && !GZERO && ndir < 8) {
-                    gpar = G[nlin - (uint32_t)(mot_x(ndir) * H + mot_y(ndir))];
-                }
+                const bool is_occ = gl < 9, is_cst = gl >= 9 && gl < 12;
+                const bool in_occ = (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
+                const bool in_cst = (unsigned)cx < (unsigned)W;
+                const uint32_t ci = (is_occ && in_occ) ? (uint32_t)cx * (uint32_t)H + (uint32_t)cy : 0u;
+                // cell-state lanes: bytes of (cx, y-1 .. y+1) inside the 8-byte window at a0 (4-aligned)
+                const uint32_t lo =
+                    (is_cst && in_cst) ? (uint32_t)cx * (uint32_t)H + (uint32_t)(y > 0 ? y - 1 : 0) : 0u;
+                const uint32_t a0 = lo & ~3u;
+                const uint32_t gi =
+                    (!GZERO && gl == 12 && ndir < 8) ? nlin - (uint32_t)(mot_x(ndir) * H + mot_y(ndir)) : 0u;
+                const uint32_t ow = occ[ci >> 5];
+                const uint32_t* p32 = reinterpret_cast<const uint32_t*>(cst + a0);
+                const uint32_t c0 = p32[0], c1 = p32[1];
+                gpar = GZERO ? 0.0 : G[gi];
+                blk_in = is_occ ? in_occ : (is_cst && in_cst);
+                blk_sh = is_occ ? (int)(ci & 31u) : (int)((uint32_t)cx * (uint32_t)H + (uint32_t)y - 1u - a0);  // cst: byte of cell y-1 (may be -1)
+                blk_w = is_occ ? ow : c0;
+                blk_w2 = c1;
             }
             // the pushes take positions n0, n0 + 1, ...: their parents, while all 8 share a depth
             pc_ok = n0 > 0 && (31 - __clz(n0 + 1)) == (31 - __clz(n0 + 8));
