@@ -602,7 +602,7 @@ def astar3d_leg(args, torch, dist, world, rank):
     for i in range(1, len(lanes)):
         run(i, wb)
     torch.cuda.synchronize()
-    _LABEL[0] = "astar3d"
+    _LABEL[0] = f"astar3d_x{B}"  # keyed by batches per launch: a profile of other launches is refused
     c = ctr[:nq].cpu().numpy()
     akeys = ("cost", "plen", "nexp", "st")
     ref_out = {k: lanes[0][k][:nq].clone() for k in akeys}
@@ -671,7 +671,7 @@ def astar3d_leg(args, torch, dist, world, rank):
             "config": {"workload": "C5: Grid3D(26,20,16) door, random.seed(i) pairs, safety bubbles r=1, euclidean"},
             "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                       "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                                      "algorithmic_bytes_per_launch": alg_bytes}, "astar3d_kernel", "astar3d"),
+                                      "algorithmic_bytes_per_launch": alg_bytes}, "astar3d_kernel", f"astar3d_x{B}"),
             "detail": {"expansions_per_batch": int(c[:, 2].sum()), "reference_pushes_per_batch": int(c[:, 0].sum()),
                        "heap_pops_per_batch": int(c[:, 1].sum()), "max_heap_entries": int(c[:, 3].max())},
             "cpu_baseline": cpu, "trajectory": traj}
@@ -805,7 +805,7 @@ def graphs_leg(args, torch, dist, world, rank):
         for i in range(1, len(lanes)):
             run(i, 1)
         torch.cuda.synchronize()
-        _LABEL[0] = algo + "_2d"
+        _LABEL[0] = f"{algo}_2d_x{B}"
         r = {"cost": lanes[0]["cost"][:nq].clone(), "status": lanes[0]["st"][:nq].clone()}
         assert (r["status"] == 0).all(), f"unexpected {algo} statuses"
         for b in lanes[1:]:
@@ -863,7 +863,7 @@ def graphs_leg(args, torch, dist, world, rank):
             "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                       "frac": achieved / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": alg,
                                       "note": "A*'s 19E + 16(P+Q) bytes; the line-of-sight cells are not counted"},
-                                     "theta2d_kernel" if algo == "theta_star" else "lazy_theta2d_kernel", algo + "_2d"),
+                                     "theta2d_kernel" if algo == "theta_star" else "lazy_theta2d_kernel", f"{algo}_2d_x{B}"),
             "detail": {"expansions_per_batch": int(c[:, 2].sum()), "pushes_per_batch": int(c[:, 0].sum())},
             "cpu_baseline": cpu}
 
@@ -1144,7 +1144,7 @@ def dyn3d_leg(args, torch, dist, world, rank):
         for i in range(len(streams)):
             run(i, nbs[i])
         torch.cuda.synchronize()
-        _LABEL[0] = kind + ("" if rounds is None else "_replan")
+        _LABEL[0] = kind + ("" if rounds is None else "_replan") + f"_x{B}"
         shard.barrier(dist)
         torch.cuda.synchronize()
         evs = []
@@ -1196,7 +1196,7 @@ def dyn3d_leg(args, torch, dist, world, rank):
             "dtype": "f64",
             "roofline": with_traffic(dyn3d_roof(kind, int(np.maximum(nexp, 0).sum() * np.mean(nbs)),
                                                 None if pushes is None else int(pushes * np.mean(nbs)), kern_ms),
-                                     "dstar3d_kernel" if kind == "dstar3d" else "lpa3d_kernel", name),
+                                     "dstar3d_kernel" if kind == "dstar3d" else "lpa3d_kernel", f"{name}_x{B}"),
             "roofline_note": "latency-bound list machines (OPEN / U with Python-list semantics): a small frac is "
                              "the expected reading",
             "streams": len(streams), "batches_per_launch": B,
@@ -1659,7 +1659,7 @@ def main():
     for i in range(1, S):
         step(i, wb)
     torch.cuda.synchronize()
-    _LABEL[0] = "astar2d_c2"
+    _LABEL[0] = f"astar2d_c2_x{B}"  # keyed by batches per launch: a profile of other launches is refused
     counters = ctr[:nq].cpu().numpy()
     ref_out = {k: lanes[0][k][:nq].clone() for k in ("cost", "plen", "nexp", "status")}
     st0 = ref_out["status"].cpu().numpy()
@@ -1801,7 +1801,7 @@ def main():
                                       # launches in flight overlap: bytes of one batch per step interval
                                       "achieved_aggregate": bytes_per_batch / (elapsed / args.steps) / 1e9,
                                       "frac_aggregate": bytes_per_batch / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS},
-                                     "astar2d_kernel", "astar2d_c2"),
+                                     "astar2d_kernel", f"astar2d_c2_x{B}"),
             "cpu_baseline": cpu,
             "secondary": secondary,
             "detail": {"kernel_ms_per_launch": kern_ms,

@@ -139,7 +139,10 @@ struct Ld {
         } else {
             in = p < h.cap;
             const int pl = in ? p : 0;
-            v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(h.spill, (p - h.cap) * 16, 0, 0));
+            // 12 of the entry's 16 bytes: a b128 load left a 4th destination register that the compiler
+            // reused for the LDS load below, a write-after-write that waited for the HBM load at once
+            const auto w = __builtin_amdgcn_raw_buffer_load_b96(h.spill, (p - h.cap) * 16, 0, 0);
+            v = make_uint4(w[0], w[1], w[2], 0u);
             fl = h.F[pl];
             cl = h.C[pl];
         }

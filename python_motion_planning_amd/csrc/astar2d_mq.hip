@@ -96,6 +96,15 @@ __device__ __forceinline__ double bcf(double v)
     const uint64_t b = (uint64_t)__double_as_longlong(v);
     return __longlong_as_double(((uint64_t)bc<K>((uint32_t)(b >> 32)) << 32) | bc<K>((uint32_t)b));
 }
+__device__ __forceinline__ uint32_t shl1(uint32_t v)  // lane + 1 of my row (row_shl:1; lane 15 gets 0)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x101, 0xF, 0xF, false);
+}
+__device__ __forceinline__ double shl1f(double v)
+{
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    return __longlong_as_double(((uint64_t)shl1((uint32_t)(b >> 32)) << 32) | shl1((uint32_t)b));
+}
 __device__ __forceinline__ uint32_t ror_or(uint32_t v)  // OR over my row
 {
     v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xF, 0xF, false);
@@ -306,21 +315,20 @@ __device__ __forceinline__ void heap_pop(const GHeap& h, const Walk& wk, int n, 
     const bool on = gl >= 1 && gl <= K;
     const int sh = on ? K - gl : 0;
     const int pi = on ? (int)(P >> sh) - 1 : (gl == 0 ? n - 1 : 0);
-    const bool hasb = on && gl < K;
-    const int pn = hasb ? (int)(P >> (sh - 1)) - 1 : 0;
     const int si = ((pi - 1) ^ 1) + 1;
     const bool hass = on && si < n;
-    double Af, Bf, Sf;
-    uint32_t Ac, Bc, Sc;
+    double Af, Sf;
+    uint32_t Ac, Sc;
     {
-        Ld la, lb, ls;
+        Ld la, ls;
         la.issue(h, pi);
-        lb.issue(h, pn);
         ls.issue(h, hass ? si : 0);
         la.get(Af, Ac);
-        lb.get(Bf, Bc);
         ls.get(Sf, Sc);
     }
+    // heap[p_{i+1}] is lane i+1's load (DPP row_shl:1; lanes 1..K-1 use it, K <= 14 stays in the row)
+    const double Bf = shl1f(Af);
+    const uint32_t Bc = shl1(Ac);
     // ---- movers: the path prefix with !(last < heap[p_i])
     const int m = __popc(rbits(on && !key_lt(lf, hkey<HEUR>(lc), Af, hkey<HEUR>(Ac)), gb));
     {
