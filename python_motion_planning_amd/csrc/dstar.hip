@@ -42,11 +42,13 @@ struct KeyD {
     }
 };
 
-__device__ __forceinline__ bool occ2(const uint32_t* occ, int W, int H, int x, int y)
+// branch-free: the word is loaded for any (x, y) (index 0 outside the grid), so the several
+// occupancy reads of one collision test issue together instead of one round trip each
+__device__ __forceinline__ uint32_t occ2(const uint32_t* occ, int W, int H, int x, int y)
 {
-    if ((unsigned)x >= (unsigned)W || (unsigned)y >= (unsigned)H) return true;
-    const uint32_t c = (uint32_t)x * (uint32_t)H + (uint32_t)y;
-    return (occ[c >> 5] >> (c & 31)) & 1u;
+    const bool in = (unsigned)x < (unsigned)W && (unsigned)y < (unsigned)H;
+    const uint32_t c = in ? (uint32_t)x * (uint32_t)H + (uint32_t)y : 0u;
+    return (in ? 0u : 1u) | ((occ[c >> 5] >> (c & 31)) & 1u);
 }
 
 __device__ __forceinline__ DCell load_cell(const DCell* cells, int c)
@@ -143,14 +145,20 @@ struct D2 {
         }
     }
 
-    // drop heap tops that do not match their cell's (k, first entry); S.root is then min_state
-    __device__ __forceinline__ void clean_top()
+    // drop heap tops that do not match their cell's (k, first entry); S.root is then min_state and
+    // `c` its cell (valid when the loop returned early)
+    __device__ __forceinline__ void clean_top(DCell& c)
     {
         while (S.open > 0 && S.n > 0) {
-            const DCell c = load_cell(S.cells, (int)S.root.b);
+            c = load_cell(S.cells, (int)S.root.b);
             if (cnt_of(c.cnt_t) > 0 && (uint32_t)c.first == S.root.a && c.k == S.root.g) return;
             pop_top();
         }
+    }
+    __device__ __forceinline__ void clean_top()
+    {
+        DCell c;
+        clean_top(c);
     }
 
     // insert(node, h_new) (:236-248) on a wave-uniform cell: always appends an entry
@@ -187,14 +195,24 @@ struct D2 {
     __device__ __forceinline__ int process_state()
     {
         // ---- min_state: the earliest entry of the node minimising (k, first entry) ----
-        clean_top();
+        DCell xc;  // the popped node's cell: clean_top's load (the heap pop does not touch cells)
+        clean_top(xc);
         S.np++;  // EXPAND.append(node), None included (:165-167)
         if (S.open == 0) return PS_EMPTY;
         if (S.n == 0) return PS_OVER;  // cannot happen while S.open > 0
         const Ent top = S.root;
-        pop_top();
-        DCell xc = load_cell(S.cells, (int)top.b);
         const int X = (int)top.b;
+        // the neighbours' cells load now, beside the heap pop (lanes 0..7, any in-grid neighbour;
+        // getNeighbor's collision test only decides below whether a lane uses its cell)
+        const int Xc0 = X == S.goal_slot ? S.goal_cell : X;
+        const int x = Xc0 / H, y = Xc0 % H;
+        const int nx = x + mdx, ny = y + mdy;
+        const bool nin = lane < 8 && (unsigned)nx < (unsigned)W && (unsigned)ny < (unsigned)H;
+        const int Y = nin ? nx * H + ny : 0;
+        DCell yc = load_cell(S.cells, Y);
+        uint32_t coll = occ2(occ, W, H, x, y) | occ2(occ, W, H, nx, ny);
+        if (mdx != 0 && mdy != 0) coll = coll | occ2(occ, W, H, x, ny) | occ2(occ, W, H, nx, y);
+        pop_top();
         const int Xc = X == S.goal_slot ? S.goal_cell : X;  // node.current
         const double k_old = xc.k;
         // delete (:250-259): CLOSED if OPEN, drop the first entry
@@ -208,23 +226,7 @@ struct D2 {
             S.open -= 1;
         }
         // ---- neighbours (getNeighbor, :276-291): lanes 0..7 in motion order ----
-        const int x = Xc / H, y = Xc % H;
-        const int nx = x + mdx, ny = y + mdy;
-        bool nb = false;
-        DCell yc;
-        yc.h = yc.k = 0.0;
-        yc.first = yc.last = yc.parent = -1;
-        yc.cnt_t = 0;
-        int Y = 0;
-        if (lane < 8) {
-            bool coll = occ2(occ, W, H, x, y) || occ2(occ, W, H, nx, ny);
-            if (mdx != 0 && mdy != 0) coll = coll || occ2(occ, W, H, x, ny) || occ2(occ, W, H, nx, y);
-            nb = !coll;
-            if (nb) {
-                Y = nx * H + ny;
-                yc = load_cell(S.cells, Y);
-            }
-        }
+        const bool nb = lane < 8 && coll == 0u;
         const uint64_t nbm = ballot(nb) & 0xFFull;
         // RAISE (:177-183): scalar scan in motion order
         double hX = xc.h;
@@ -337,8 +339,8 @@ struct D2 {
 __device__ __forceinline__ bool coll2(const uint32_t* occ, int W, int H, int a, int b)
 {
     const int x1 = a / H, y1 = a % H, x2 = b / H, y2 = b % H;
-    bool c = occ2(occ, W, H, x1, y1) || occ2(occ, W, H, x2, y2);
-    if (x1 != x2 && y1 != y2) c = c || occ2(occ, W, H, x1, y2) || occ2(occ, W, H, x2, y1);
+    uint32_t c = occ2(occ, W, H, x1, y1) | occ2(occ, W, H, x2, y2);
+    if (x1 != x2 && y1 != y2) c = c | occ2(occ, W, H, x1, y2) | occ2(occ, W, H, x2, y1);
     return c;
 }
 

@@ -87,11 +87,12 @@ struct Occ {
     uint32_t* g;
     int X, Y, Z;
     __device__ __forceinline__ uint32_t word(uint32_t w) const { return LDS ? l[w] : g[w]; }
-    __device__ __forceinline__ bool at(int x, int y, int z) const
+    // branch-free (word 0 read outside the grid), so a collision test's reads issue together
+    __device__ __forceinline__ uint32_t at(int x, int y, int z) const
     {
-        if ((unsigned)x >= (unsigned)X || (unsigned)y >= (unsigned)Y || (unsigned)z >= (unsigned)Z) return false;
-        const uint32_t c = ((uint32_t)x * (uint32_t)Y + (uint32_t)y) * (uint32_t)Z + (uint32_t)z;
-        return (word(c >> 5) >> (c & 31)) & 1u;
+        const bool in = (unsigned)x < (unsigned)X && (unsigned)y < (unsigned)Y && (unsigned)z < (unsigned)Z;
+        const uint32_t c = in ? ((uint32_t)x * (uint32_t)Y + (uint32_t)y) * (uint32_t)Z + (uint32_t)z : 0u;
+        return in ? (word(c >> 5) >> (c & 31)) & 1u : 0u;
     }
     __device__ __forceinline__ void set(uint32_t c) const
     {
@@ -99,19 +100,17 @@ struct Occ {
         else atomicOr(&g[c >> 5], 1u << (c & 31));
     }
     // GraphSearcher3D.isCollision(node1 = a, node2 = b) (graph_search_3d.py:66-107)
+    // All five reads are issued at once.  For a two-axis diagonal the third face cell is node1
+    // itself (its delta is 0), already part of the first test, so OR-ing all three face cells
+    // equals the reference's case split.
     __device__ __forceinline__ bool coll(int x1, int y1, int z1, int x2, int y2, int z2) const
     {
-        if (at(x1, y1, z1) || at(x2, y2, z2)) return true;
         const int dx = x2 - x1, dy = y2 - y1, dz = z2 - z1;
-        if (max(abs(dx), max(abs(dy), abs(dz))) > 1) return false;
+        const uint32_t ends = at(x1, y1, z1) | at(x2, y2, z2);
+        const uint32_t faces = at(x1 + dx, y1, z1) | at(x1, y1 + dy, z1) | at(x1, y1, z1 + dz);
+        const bool adj = max(abs(dx), max(abs(dy), abs(dz))) <= 1;
         const int ch = (dx != 0) + (dy != 0) + (dz != 0);
-        if (ch <= 1) return false;
-        if (ch == 2) {
-            if (dx != 0 && dy != 0) return at(x1 + dx, y1, z1) || at(x1, y1 + dy, z1);
-            if (dx != 0 && dz != 0) return at(x1 + dx, y1, z1) || at(x1, y1, z1 + dz);
-            return at(x1, y1 + dy, z1) || at(x1, y1, z1 + dz);
-        }
-        return at(x1 + dx, y1, z1) || at(x1, y1 + dy, z1) || at(x1, y1, z1 + dz);
+        return (ends | ((adj && ch >= 2) ? faces : 0u)) != 0u;
     }
 };
 
@@ -198,13 +197,19 @@ struct D3 {
     }
 
     // drop stale heap tops; afterwards S.root is the min_state (when S.open > 0)
-    __device__ __forceinline__ void clean_top()
+    // `c` = the root's cell when the loop returns early
+    __device__ __forceinline__ void clean_top(DC3& c)
     {
         while (S.open > 0 && S.n > 0) {
-            const DC3 c = load_c(S.cells, (int)S.root.b);
+            c = load_c(S.cells, (int)S.root.b);
             if (valid(S.root, c)) return;
             pop_top();
         }
+    }
+    __device__ __forceinline__ void clean_top()
+    {
+        DC3 c;
+        clean_top(c);
     }
 
     // insert(node, h_new) (:233-246) for a node in slot `slot` with state c, wave-uniform
@@ -229,12 +234,21 @@ struct D3 {
     // processState (:168-218).  Returns false when OPEN is empty (the reference's -1).
     __device__ __forceinline__ bool process_state()
     {
-        clean_top();
+        DC3 xc;  // the popped node's cell: clean_top's load (the heap pop does not touch cells)
+        clean_top(xc);
         if (S.open == 0) return false;
         const Ent top = S.root;
-        pop_top();
         const int Xs = (int)top.b;
-        DC3 xc = load_c(S.cells, Xs);
+        // the neighbours' cells load now, beside the heap pop and the collision reads
+        int x, y, z;
+        geo.xyz(coord_of(Xs), x, y, z);
+        const int nx = x + mdx, ny = y + mdy, nz = z + mdz;
+        const bool nin =
+            lane < 26 && (unsigned)nx < (unsigned)geo.X && (unsigned)ny < (unsigned)geo.Y && (unsigned)nz < (unsigned)geo.Z;
+        const int Yc = nin ? geo.id(nx, ny, nz) : 0;
+        DC3 yc = load_c(S.cells, Yc);
+        const bool nb = nin && !occ.coll(x, y, z, nx, ny, nz);
+        pop_top();
         if (S.ex && lane == 0 && S.np < S.ex_cap) S.ex[S.np] = coord_of(Xs);
         S.np += 1;
         const double k_old = xc.k;
@@ -242,23 +256,7 @@ struct D3 {
         xc.t = T_CLOSED;
         S.open -= 1;
         const int Xc = coord_of(Xs);
-        int x, y, z;
-        geo.xyz(Xc, x, y, z);
-        // getNeighbor: the voxel must be in the map and isCollision(node, n) false
-        const int nx = x + mdx, ny = y + mdy, nz = z + mdz;
-        bool nb = false;
-        int Yc = 0;
-        DC3 yc;
-        yc.h = yc.k = 0.0;
-        yc.parent = -1;
-        yc.pos = yc.t = yc.pad = 0u;
-        if (lane < 26 && (unsigned)nx < (unsigned)geo.X && (unsigned)ny < (unsigned)geo.Y && (unsigned)nz < (unsigned)geo.Z) {
-            nb = !occ.coll(x, y, z, nx, ny, nz);
-            if (nb) {
-                Yc = geo.id(nx, ny, nz);
-                yc = load_c(S.cells, Yc);
-            }
-        }
+        // getNeighbor: the voxel must be in the map and isCollision(node, n) false (nb above)
         // RAISE (:185-189): running strict minimum in motion order == first minimum of the candidates
         double hX = xc.h;
         int pX = xc.parent;

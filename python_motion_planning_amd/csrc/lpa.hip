@@ -135,22 +135,25 @@ __device__ int update_vertex(Q& S, int32_t v, int lane)
 {
     const int vx = (int)((uint32_t)v / (uint32_t)S.H), vy = v - vx * S.H;
     const int m = lane & 7;
+    // Every read of this call issues up front, unconditionally (in-grid addresses on every lane):
+    // the neighbour's occupancy words and g, and v's g / rhs / U position -- one round trip where
+    // short-circuit tests and lane-0 blocks made several.
+    const int ux = vx + kMX[m], uy = vy + kMY[m];
+    const bool in = (unsigned)ux < (unsigned)S.W && (unsigned)uy < (unsigned)S.H;
+    const bool act = lane < 8 && in;
+    const int uxs = act ? ux : vx, uys = act ? uy : vy;
+    const bool ou = occ_at(S.occ, S.H, uxs, uys), ov = occ_at(S.occ, S.H, vx, vy);
+    const bool oa = occ_at(S.occ, S.H, uxs, vy), ob = occ_at(S.occ, S.H, vx, uys);
+    const double gu = S.g[uxs * S.H + uys];
+    const double gv = S.g[v], rsrc = S.rhs[v];
+    const int p = S.pos[v];
     double rv;
     if (v != S.src) {
         // getNeighbor (:196-207): map lookup (KeyError off the grid), then the obstacle filter;
         // cost (graph_search.py:46-59): inf on isCollision(node_n, node), else hypot
-        const int ux = vx + kMX[m], uy = vy + kMY[m];
-        const bool in = (unsigned)ux < (unsigned)S.W && (unsigned)uy < (unsigned)S.H;
-        bool valid = false;
-        double val = kInf;
-        if (lane < 8 && in) {
-            const bool ou = occ_at(S.occ, S.H, ux, uy);
-            valid = !ou;
-            bool coll = ou || occ_at(S.occ, S.H, vx, vy);
-            if ((m & 1) && !coll) coll = occ_at(S.occ, S.H, ux, vy) || occ_at(S.occ, S.H, vx, uy);
-            const double gu = S.g[ux * S.H + uy];
-            val = gu + (coll ? kInf : ((m & 1) ? kSqrt2 : 1.0));
-        }
+        const bool valid = act && !ou;
+        const bool coll = ou | ov | ((m & 1) ? (oa | ob) : false);
+        const double val = act ? gu + (coll ? kInf : ((m & 1) ? kSqrt2 : 1.0)) : kInf;
         if (ballot(lane < 8 && !in)) return PMP_REF_RAISES;
         if (!ballot(valid)) return PMP_REF_RAISES;
         double best = valid ? val : kInf;
@@ -158,22 +161,13 @@ __device__ int update_vertex(Q& S, int32_t v, int lane)
         rv = __shfl(best, 0, 64);
         if (lane == 0) S.rhs[v] = rv;
     } else {
-        double t = 0.0;
-        if (lane == 0) t = S.rhs[v];
-        rv = __shfl(t, 0, 64);
+        rv = rsrc;
     }
-    double gt = 0.0;
-    int32_t pt = 0;
-    if (lane == 0) {
-        gt = S.g[v];
-        pt = S.pos[v];
-    }
-    const double gv = __shfl(gt, 0, 64);
-    const int p = uni(pt);
-    if (p >= 0) {  // `node in U`: U.remove(node)
+    const int pu = uni(p);  // the same word on every lane
+    if (pu >= 0) {  // `node in U`: U.remove(node)
         if (lane == 0) S.pos[v] = -1;
         wave_sync_mem();
-        u_remove(S, p, lane);
+        u_remove(S, pu, lane);
     }
     if (gv != rv) {
         const double mn = gv < rv ? gv : rv;
@@ -192,14 +186,13 @@ __device__ int greedy_step(const Q& S, int32_t c, int lane)
     const int m = lane & 7;
     const int ux = x + kMX[m], uy = y + kMY[m];
     const bool in = (unsigned)ux < (unsigned)S.W && (unsigned)uy < (unsigned)H;
-    bool valid = false;
-    double gu = 0.0;
-    if (lane < 8 && in) {
-        bool coll = occ_at(S.occ, H, ux, uy) || occ_at(S.occ, H, x, y);
-        if ((m & 1) && !coll) coll = occ_at(S.occ, H, ux, y) || occ_at(S.occ, H, x, uy);
-        valid = !coll;
-        gu = S.g[ux * H + uy];
-    }
+    // all reads issued together (in-grid addresses on every lane)
+    const bool act = lane < 8 && in;
+    const int uxs = act ? ux : x, uys = act ? uy : y;
+    const bool o1 = occ_at(S.occ, H, uxs, uys), o2 = occ_at(S.occ, H, x, y);
+    const bool o3 = occ_at(S.occ, H, uxs, y), o4 = occ_at(S.occ, H, x, uys);
+    const double gu = S.g[uxs * H + uys];
+    const bool valid = act && !(o1 | o2 | ((m & 1) ? (o3 | o4) : false));
     if (ballot(lane < 8 && !in)) return -1;
     uint64_t vm = ballot(valid) & 0xffull;
     int bm = -1;
