@@ -275,17 +275,28 @@ struct L3 {
         LSTAMP(t0);
         int cx, cy, cz;
         geo.xyz(center, cx, cy, cz);
-        // ---- stage g of the 5x5x5 block (inf outside the map)
-#pragma unroll
-        for (int r = 0; r < 2; r++) {
-            const int b = lane + 64 * r;
-            double v = kInf;
-            if (b < 125) {
-                const int x = cx + b / 25 - 2, y = cy + (b / 5) % 5 - 2, z = cz + b % 5 - 2;
-                if (geo.in(x, y, z)) v = g[geo.id(x, y, z)];
-                cube[b] = v;
-            }
+        // ---- stage g of the 5x5x5 block (inf outside the map).  Every HBM read of the block (g, and
+        //      rhs of the lane's voxel below) issues first, unconditionally on in-map addresses, and
+        //      the LDS stores follow: one round trip instead of a wait per load.
+        double gb0, gb1;
+        bool gin0, gin1;
+        {
+            const int x0 = cx + lane / 25 - 2, y0 = cy + (lane / 5) % 5 - 2, z0 = cz + lane % 5 - 2;
+            const int b1 = lane + 64;
+            const int x1 = cx + b1 / 25 - 2, y1 = cy + (b1 / 5) % 5 - 2, z1 = cz + b1 % 5 - 2;
+            gin0 = geo.in(x0, y0, z0);
+            gin1 = b1 < 125 && geo.in(x1, y1, z1);
+            gb0 = g[gin0 ? geo.id(x0, y0, z0) : center];
+            gb1 = g[gin1 ? geo.id(x1, y1, z1) : center];
         }
+        const int m = lane < 26 ? lane : 0;
+        const int dx = lane < 26 ? c_m[m][0] : 0, dy = lane < 26 ? c_m[m][1] : 0, dz = lane < 26 ? c_m[m][2] : 0;
+        const int px = cx + dx, py = cy + dy, pz = cz + dz;
+        const bool mine = lane <= 26 && geo.in(px, py, pz);
+        const int P = mine ? geo.id(px, py, pz) : 0;
+        const double rvl = rhs[mine ? P : center];
+        cube[lane] = gin0 ? gb0 : kInf;
+        if (lane < 61) cube[lane + 64] = gin1 ? gb1 : kInf;
         // ---- block masks: in the map / obstacle, as wave-uniform bits
         Mask125 inm, obm;
         {
@@ -307,16 +318,10 @@ struct L3 {
             obm.lo = ballot(o0);
             obm.hi = ballot(o1);
         }
-        // ---- this lane's block voxel: lanes 0..25 = motion m, lane 26 = the centre
-        const int m = lane < 26 ? lane : 0;
-        const int dx = lane < 26 ? c_m[m][0] : 0, dy = lane < 26 ? c_m[m][1] : 0, dz = lane < 26 ? c_m[m][2] : 0;
-        const int px = cx + dx, py = cy + dy, pz = cz + dz;
-        const bool mine = lane <= 26 && geo.in(px, py, pz);
-        const int P = mine ? geo.id(px, py, pz) : 0;
+        // ---- this lane's block voxel (above): lanes 0..25 = motion m, lane 26 = the centre
         // the centre's getNeighbor(center): in the map, endpoint free
         const bool is_nb = lane < 26 && mine && !occ.at(px, py, pz);
-        double rv = 0.0;
-        if (mine) rv = rhs[P];
+        double rv = mine ? rvl : 0.0;
         wsync();
         double gnew = 0.0;  // the popped centre's new g (expand)
         if (expand) {
