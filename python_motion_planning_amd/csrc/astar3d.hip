@@ -221,20 +221,22 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
             // ---- HBM round (issued before the pop): neighbour collision + CLOSED state, node's CLOSED state
             const int nx = x + mdx, ny = y + mdy, nz = z + mdz;
             bool coll = true;
-            uint32_t ncd = 0;
-            double ncg = 0.0, nog = 0.0;
             uint32_t nlin = lin;
             if (lane < 26) {
                 const bool inb = (unsigned)nx < (unsigned)X && (unsigned)ny < (unsigned)Y && (unsigned)nz < (unsigned)Z;
                 if (inb) nlin = ((uint32_t)nx * (uint32_t)Y + (uint32_t)ny) * (uint32_t)Z + (uint32_t)nz;
             }
-            if (lane <= 26) {  // one HBM round, independent of the collision test: CLOSED / pending state
-                ncd = cdir[nlin];
-                ncg = cg[nlin];
-                nog = og[nlin];
-            }
-            uint32_t epar = 0;  // theta: the entry's parent cell (the start's parent is the start)
-            if (THETA && lane == 27) epar = node.a < ppar_cap ? ppar[node.a] : 0u;
+            // one HBM round, independent of the collision test: CLOSED / pending state (lanes 0..25 the
+            // neighbours, 26 the node).  Every lane loads (lanes > 26 the node's cell): a zero fill of
+            // the destinations on the other lanes made the compiler drain vmcnt -- every store of the
+            // previous expansion included -- at the top of each iteration.
+            const uint32_t ncd = cdir[nlin];
+            const double ncg = cg[nlin];
+            const double nog = og[nlin];
+            // theta: the entry's parent cell (the start's parent is the start); read by lane 27 below,
+            // loaded on every lane (no zero-filled destination, see above)
+            uint32_t epar = 0;
+            if (THETA) epar = ppar[node.a < ppar_cap ? node.a : 0u];
             if (lane < 26) {
                 if (OCC_LDS) {
 #define OCC(a, b, c) occ3l(occl, X, Y, Z, a, b, c)
