@@ -5,7 +5,8 @@
 # its database, so tools/prof_summary.py keys every dispatch by its workload.
 # The PMC passes keep the default per-launch batch counts of the multi-batch legs (the A* headline's
 # 20 batches in one launch, 3D A*'s 32), so a dispatch there is the same work as in the default run;
-# the other legs are shortened (fewer launches of the same size).
+# (Theta* 12 and DStar3D / LPAStar3D 6 batches per launch too); the other legs are shortened (fewer
+# launches of the same size).
 # Outputs under gpurun_out/; the summary is written on the box (ROUND=r3 -> gpurun_out/profiles_r3)
 # and the databases are deleted (they would exceed gpurun_out's 64 MiB).
 set -e
@@ -13,7 +14,7 @@ R=${GRAFT_REPO_ROOT:-/root/repo}
 OUT=$R/gpurun_out
 mkdir -p $OUT/prof_kt $OUT/prof_fetch $OUT/prof_write $OUT/prof_mfma
 cd /tmp && export TMPDIR=/tmp
-SHORT="--no-cpu-baseline --warmup 1 --rrt-steps 1 --track-steps 1 --control-steps 2 --graph-steps 2 --dstar-steps 2 --dyn3d-steps 2"
+SHORT="--no-cpu-baseline --warmup 1 --rrt-steps 1 --track-steps 1 --control-steps 2 --graph-steps 12 --dstar-steps 2 --dyn3d-steps 6"
 # PASSES=kt / pmc / all (two gpurun calls fit the per-call limit better than one)
 P=${PASSES:-all}
 [ "$P" = pmc ] || timeout -k 10 700 rocprofv3 --kernel-trace --stats -d $OUT/prof_kt -o run -- python3 $R/bench.py \
