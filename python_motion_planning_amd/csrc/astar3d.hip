@@ -150,6 +150,7 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
     uint32_t* ppar = THETA ? ppar_all + (size_t)worker * ppar_cap : nullptr;   // parent of push #seq
     int pop_jl, pop_ol;
     heap16::pop_lane_consts(lane, pop_jl, pop_ol);
+    const heap16::Walk6 pop_w = heap16::walk6_consts(lane, pop_jl, pop_ol);
     // neighbour lane m < 26: motion m (env3d.py:56-70)
     const int mdx = lane < 26 ? c_m3[lane][0] : 0, mdy = lane < 26 ? c_m3[lane][1] : 0, mdz = lane < 26 ? c_m3[lane][2] : 0;
     const int mchg = (mdx != 0) + (mdy != 0) + (mdz != 0);
@@ -267,8 +268,8 @@ __global__ __launch_bounds__(64) void astar3d_kernel(
             const uint64_t ts0 = __builtin_amdgcn_s_memtime();
 #endif
             if (n > 0) {
-                if (n < lds_cap) heap16::pop<Key3, false>(hp, qc, n, root, lane, pop_jl, pop_ol);
-                else heap16::pop<Key3, true>(hp, qc, n, root, lane, pop_jl, pop_ol);
+                if (n < lds_cap) heap16::pop<Key3, false, true>(hp, qc, n, root, lane, pop_jl, pop_ol, pop_w);
+                else heap16::pop<Key3, true, true>(hp, qc, n, root, lane, pop_jl, pop_ol, pop_w);
             }
 #ifdef PMP_STAMPS
             const uint64_t ts1 = __builtin_amdgcn_s_memtime();

@@ -117,10 +117,32 @@ __device__ __forceinline__ void pop_lane_consts(int lane, int& jl, int& ol)
     ol = lane + 1 - (1 << (jl - 1));
 }
 
+// Lane-parallel form of the 6-level walk (pop<..., PAR = true>): lane l < 63 owns sibling pair l
+// (level jl, offset ol) and knows its strict ancestor pairs (`anc`) and which child of each leads to
+// it (`dir`).  The walk visits the pair iff every ancestor chose the child toward it and that child
+// moved up (it is < last); so "visited and my chosen child moves" is a handful of 64-bit mask tests
+// per lane instead of the 6-step scalar chain (the scalar unit is shared by the CU's four SIMDs).
+struct Walk6 {
+    uint64_t anc, dir;
+};
+__device__ __forceinline__ Walk6 walk6_consts(int lane, int jl, int ol)
+{
+    Walk6 w{0ull, 0ull};
+    if (lane < 63)
+        for (int i = 1; i < jl; i++) {
+            const int idx = (1 << (i - 1)) - 1 + (ol >> (jl - i));
+            w.anc |= 1ull << idx;
+            w.dir |= (uint64_t)((ol >> (jl - i - 1)) & 1) << idx;
+        }
+    return w;
+}
+
 // Extract-min on a heap whose size was already decremented to n (> 0); the old last element sits
-// at position n.  `root` receives the new minimum (wave-uniform).
-template <class K, bool SPILL>
-__device__ __forceinline__ void pop(const Heap& hp, const K& key, int n, Ent& root, int lane, int jl, int ol)
+// at position n.  `root` receives the new minimum (wave-uniform).  PAR: the walk over each 6-level
+// chunk is evaluated lane-parallel from `w` (same result as the scalar walk).
+template <class K, bool SPILL, bool PAR = false>
+__device__ __forceinline__ void pop(const Heap& hp, const K& key, int n, Ent& root, int lane, int jl, int ol,
+                                    const Walk6& w = Walk6{0ull, 0ull})
 {
     constexpr bool SF = K::kStoredF;
     n = uni(n);
@@ -157,6 +179,15 @@ __device__ __forceinline__ void pop(const Heap& hp, const K& key, int n, Ent& ro
         int cur = uni(hole), oc = 0;
         uint64_t mover = 0, movr = 0;
         uint32_t go = 1u;
+        if constexpr (PAR) {
+            // chosen child of each pair moves up (< last; validity is in the masks)
+            const uint64_t cl = (dmask & mrmask) | (~dmask & mlmask);
+            const bool vis = lane < 63 && ((dmask ^ w.dir) & w.anc) == 0ull && (cl & w.anc) == w.anc;
+            mover = ballot(vis && ((cl >> lane) & 1ull));
+            movr = mover & dmask;
+            go = (mover >> 31) != 0ull ? 1u : 0u;  // a level-6 pair (indices 31..62) moved
+            if (mover) cur = __builtin_amdgcn_readlane(li + (int)((dmask >> lane) & 1ull), 63 - __clzll((long long)mover));
+        } else {
         // branch-free scalar walk: every step is a select, so the 6 levels are one straight-line
         // SALU sequence (taken branches cost more than the arithmetic they skip)
 #pragma unroll
@@ -171,6 +202,7 @@ __device__ __forceinline__ void pop(const Heap& hp, const K& key, int n, Ent& ro
             movr |= (uint64_t)(go & r) << pl;
             cur = go ? c + (int)r : cur;
             oc = go ? 2 * oc + (int)r : oc;
+        }
         }
         if ((mover >> lane) & 1ull) {
             const bool rr = (movr >> lane) & 1ull;
