@@ -118,6 +118,7 @@ struct D2 {
     int mdx, mdy;
     double mcost;
     KeyD key;
+    heap16::Walk6 pop_w{0ull, 0ull};  // set after construction (walk6_consts)
 
     __device__ __forceinline__ void push(const Ent& it0)
     {
@@ -140,8 +141,8 @@ struct D2 {
     {
         S.n -= 1;
         if (S.n > 0) {
-            if (S.n < S.lds_cap) heap16::pop<KeyD, false>(S.hp, key, S.n, S.root, lane, pop_jl, pop_ol);
-            else heap16::pop<KeyD, true>(S.hp, key, S.n, S.root, lane, pop_jl, pop_ol);
+            if (S.n < S.lds_cap) heap16::pop<KeyD, false, true>(S.hp, key, S.n, S.root, lane, pop_jl, pop_ol, pop_w);
+            else heap16::pop<KeyD, true, true>(S.hp, key, S.n, S.root, lane, pop_jl, pop_ol, pop_w);
         }
     }
 
@@ -380,6 +381,7 @@ __global__ __launch_bounds__(64) void dstar_kernel(const uint32_t* __restrict__ 
     D2 d{npress > 0 ? (const uint32_t*)occw : occ_in, W, H, S, lane, 0, 0, c_dmx[lane & 7], c_dmy[lane & 7],
          (lane & 1) ? 1.4142135623730951 : 1.0, KeyD()};  // Planner.dist = hypot(1, 1) / hypot(1, 0)
     heap16::pop_lane_consts(lane, d.pop_jl, d.pop_ol);
+    d.pop_w = heap16::walk6_consts(lane, d.pop_jl, d.pop_ol);
     const int R1 = npress + 1;
 
     for (;;) {

@@ -159,6 +159,7 @@ struct D3 {
     int mdx, mdy, mdz;
     double mcost;
     KeyD key;
+    heap16::Walk6 pop_w{0ull, 0ull};  // set after construction (walk6_consts)
 
     __device__ __forceinline__ int coord_of(int slot) const { return slot == S.goal_slot ? S.goal_cell : slot; }
 
@@ -186,8 +187,8 @@ struct D3 {
     {
         S.n -= 1;
         if (S.n > 0) {
-            if (S.n < S.lds_cap) heap16::pop<KeyD, false>(S.hp, key, S.n, S.root, lane, pop_jl, pop_ol);
-            else heap16::pop<KeyD, true>(S.hp, key, S.n, S.root, lane, pop_jl, pop_ol);
+            if (S.n < S.lds_cap) heap16::pop<KeyD, false, true>(S.hp, key, S.n, S.root, lane, pop_jl, pop_ol, pop_w);
+            else heap16::pop<KeyD, true, true>(S.hp, key, S.n, S.root, lane, pop_jl, pop_ol, pop_w);
         }
     }
 
@@ -383,6 +384,7 @@ __global__ __launch_bounds__(64) void dstar3d_kernel(
     const Geo geo{X, Y, Z};
     D3<LDS> d{occ, geo, S, lane, 0, 0, 0, 0, 0, 0.0, KeyD()};
     heap16::pop_lane_consts(lane, d.pop_jl, d.pop_ol);
+    d.pop_w = heap16::walk6_consts(lane, d.pop_jl, d.pop_ol);
     {
         const int l = lane < 26 ? lane : 0;
         d.mdx = c_m[l][0];
