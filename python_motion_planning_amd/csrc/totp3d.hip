@@ -180,7 +180,7 @@ __device__ __forceinline__ double lin(double L, int ns, int i)
 
 __device__ __forceinline__ double sq(double a) { return a * a; }
 
-__global__ __launch_bounds__(64) void totp3d_kernel(pmp_totp_params T, int nq, const double* __restrict__ path,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void totp3d_kernel(pmp_totp_params T, int nq, const double* __restrict__ path,
                                                     const int32_t* __restrict__ off, int nmax, int sample_cap,
                                                     double* __restrict__ sv_out, double* __restrict__ sd_out,
                                                     double* __restrict__ sdd_out, double* __restrict__ tp_out,
