@@ -354,7 +354,7 @@ __device__ __forceinline__ double cost2(const uint32_t* occ, int W, int H, int a
 
 // DStar.plan (:75-89) and then npress OnPress(x, y) calls (:102-134) per query.  Round r (0 = plan)
 // writes cost / path / len(EXPAND) / status at [q][r]; presses at [q][npress][2].
-__global__ __launch_bounds__(64) void dstar_kernel(const uint32_t* __restrict__ occ_in, int W, int H,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void dstar_kernel(const uint32_t* __restrict__ occ_in, int W, int H,
                                                    const int32_t* __restrict__ start_xy, const int32_t* __restrict__ goal_xy,
                                                    int nq, const int32_t* __restrict__ presses, int npress,
                                                    double* __restrict__ cost_out, int32_t* __restrict__ path_len_out,
