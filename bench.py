@@ -1094,7 +1094,7 @@ def dyn3d_leg(args, torch, dist, world, rank):
     (lpa_star3d.py:78-124, lpa3d.hip), each as plan() alone and as a replanning session (plan() + 2
     dynamic-obstacle calls: DStar3D.apply_dynamic_obstacles of 2 voxels, LPAStar3D.apply_change
     blocking a voxel).  One timed step = one launch over the rank's queries."""
-    from python_motion_planning_amd import batch, shard, workloads as wl
+    from python_motion_planning_amd import _lib, batch, shard, workloads as wl
 
     nq = args.dyn3d_queries
     occ, s, g = wl.c5_workload(nq, first_seed=rank * nq)
@@ -1123,6 +1123,9 @@ def dyn3d_leg(args, torch, dist, world, rank):
             m = nq * nb
             r_ = None if rd_rep is None else rd_rep[:m]
             with torch.cuda.stream(streams[i % len(streams)]):
+                if kind == "lpastar3d" and args.lpa3d_workers_per_cu:
+                    _lib.check(_lib.context(), _lib.load_library().pmp_set_workers_per_cu(
+                        _lib.context(), args.lpa3d_workers_per_cu), "workers")
                 if kind == "dstar3d":
                     return batch.dstar3d_batch(occ.shape, s_rep[:m], g_rep[:m], r_, path_cap=X * Y * Z + 1,
                                                occ_bits=bits_rep[:m])
@@ -1498,6 +1501,8 @@ def main():
     ap.add_argument("--dyn3d-queries", type=int, default=8192, help="C5 queries per DStar3D / LPAStar3D launch")
     ap.add_argument("--dyn3d-steps", type=int, default=24)
     ap.add_argument("--dyn3d-streams", type=int, default=4, help="DStar3D / LPAStar3D launches in flight")
+    ap.add_argument("--lpa3d-workers-per-cu", type=int, default=0,
+                    help="LPAStar3D persistent workers per CU (0 = the library default)")
     ap.add_argument("--dyn3d-batches-per-launch", type=int, default=6,
                     help="DStar3D / LPAStar3D batches per launch (0 = all the timed steps in one launch; LPAStar3D "
                          "169 k / 315 k / 321 k plans/s at 1 x 6 streams / 24 x 1 / 6 x 4)")
