@@ -875,6 +875,11 @@ def graphs_leg(args, torch, dist, world, rank):
     gl = free[rng.integers(len(free), size=nl)].astype(np.int32)
     s_d, g_d = torch.as_tensor(sl, device="cuda"), torch.as_tensor(gl, device="cuda")
     lpa_streams = [pool_stream(torch, i) for i in range(max(1, args.lpa_streams))]
+    if args.lpa_workers_per_cu:
+        for sm in [torch.cuda.current_stream()] + lpa_streams:
+            with torch.cuda.stream(sm):
+                _lib.check(_lib.context(), _lib.load_library().pmp_set_workers_per_cu(
+                    _lib.context(), args.lpa_workers_per_cu), "workers")
     for lite in (False, True):
         _LABEL[0] = "dstar_lite" if lite else "lpa_star"
 
@@ -1501,6 +1506,8 @@ def main():
     ap.add_argument("--dyn3d-queries", type=int, default=8192, help="C5 queries per DStar3D / LPAStar3D launch")
     ap.add_argument("--dyn3d-steps", type=int, default=24)
     ap.add_argument("--dyn3d-streams", type=int, default=4, help="DStar3D / LPAStar3D launches in flight")
+    ap.add_argument("--lpa-workers-per-cu", type=int, default=0,
+                    help="LPA* / D* Lite 2D persistent workers per CU (0 = the library default)")
     ap.add_argument("--lpa3d-workers-per-cu", type=int, default=0,
                     help="LPAStar3D persistent workers per CU (0 = the library default)")
     ap.add_argument("--dyn3d-batches-per-launch", type=int, default=6,
