@@ -332,11 +332,21 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         double h = INFINITY, hx = 0.0, hy = 0.0, hg = 0.0;
         int hi = 0x7fffffff;
         if (best <= T) {
-            for (int j = tid; j < n; j += kNT) {
-                const uint32_t p = xyq[j];
-                const float dx = fmaf((float)(p & 0xFFFFu), qinv, qlof) - sxf;
-                const float dy = fmaf((float)(p >> 16), qinv, qlof) - syf;
-                if (dx * dx + dy * dy <= T) {
+            // 8 loads in flight per thread, as the scan above (one at a time made this pass a chain
+            // of n / 512 dependent L2 round trips per iteration)
+            for (int j0 = tid; j0 < n; j0 += 8 * kNT) {
+                uint32_t p[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) p[u] = (j0 + u * kNT < n) ? xyq[j0 + u * kNT] : 0u;
+                uint32_t hits = 0;
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const float dx = fmaf((float)(p[u] & 0xFFFFu), qinv, qlof) - sxf;
+                    const float dy = fmaf((float)(p[u] >> 16), qinv, qlof) - syf;
+                    hits |= (uint32_t)((j0 + u * kNT < n) & (dx * dx + dy * dy <= T)) << u;
+                }
+                for (; hits; hits &= hits - 1) {  // increasing j within the thread
+                    const int j = j0 + (__ffs(hits) - 1) * kNT;
                     const double xj = tx[2 * j], yj = tx[2 * j + 1], gj = tg[j];  // one round
                     const double e = lp::py_hypot(xj - sx, yj - sy);
                     if (e < h) { h = e; hi = j; hx = xj; hy = yj; hg = gj; }  // increasing j: keeps the first
