@@ -353,12 +353,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void lp
                 // safety bound only (LPA* on a static grid settles every cell a bounded number of
                 // times): a runaway query stops with status 3 instead of holding the GPU
                 if (nexp > (int64_t)64 * (int64_t)ncell + 64) { st = PMP_CAP_OVERFLOW; break; }
-                // min(U, key=key): first minimal element in list order
+                // the target's g / rhs (read after the scan) issue first, beside it
+                const double ggt = S.g[S.tgt], grt = S.rhs[S.tgt];
+                // min(U, key=key): first minimal element in list order; 2 entries per lane in flight
+                // (increasing k per lane, as the one-at-a-time loop)
                 double b1 = kInf, b2 = kInf;
                 int bi = 0x7fffffff;
-                for (int k = lane; k < S.n; k += 64) {
-                    const double a1 = S.Uk1[k], a2 = S.Uk2[k];
-                    if (bi == 0x7fffffff || key_lt(a1, a2, b1, b2)) { b1 = a1; b2 = a2; bi = k; }
+                for (int k0 = lane; k0 < S.n; k0 += 128) {
+                    double a1[2], a2[2];
+#pragma unroll
+                    for (int u = 0; u < 2; u++) {
+                        const int k = k0 + 64 * u < S.n ? k0 + 64 * u : k0;
+                        a1[u] = S.Uk1[k];
+                        a2[u] = S.Uk2[k];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 2; u++)
+                        if (k0 + 64 * u < S.n && (bi == 0x7fffffff || key_lt(a1[u], a2[u], b1, b2))) {
+                            b1 = a1[u]; b2 = a2[u]; bi = k0 + 64 * u;
+                        }
                 }
                 for (int o = 1; o < 64; o <<= 1) {
                     const double o1 = __shfl_xor(b1, o, 64), o2 = __shfl_xor(b2, o, 64);
@@ -370,28 +383,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void lp
                 bi = uni(bi);
                 b1 = __shfl(b1, 0, 64);
                 b2 = __shfl(b2, 0, 64);
-                double ggt = 0.0, grt = 0.0;
-                int32_t vt = 0;
-                if (lane == 0) {
-                    ggt = S.g[S.tgt];
-                    grt = S.rhs[S.tgt];
-                    vt = S.Uc[bi];
-                }
-                const double gg = detached ? kInf : __shfl(ggt, 0, 64);
-                const double gr = detached ? kInf : __shfl(grt, 0, 64);
+                const int32_t vt = S.Uc[bi];  // every lane the same word
+                const double gg = detached ? kInf : ggt;
+                const double gr = detached ? kInf : grt;
                 const double gm = gg < gr ? gg : gr;
                 if (!key_lt(b1, b2, gm + 0.0 + S.km, gm) && gr == gg) break;  // calculateKey(tgt): h = 0
                 const int32_t v = uni(vt);
+                // v's g / rhs (not touched by the list shift) load before it, on every lane
+                const double gv = S.g[v], rv = S.rhs[v];
                 if (lane == 0) S.pos[v] = -1;
                 wave_sync_mem();
                 u_remove(S, bi, lane);
                 nexp++;
-                double gvt = 0.0, rvt = 0.0;
-                if (lane == 0) {
-                    gvt = S.g[v];
-                    rvt = S.rhs[v];
-                }
-                const double gv = __shfl(gvt, 0, 64), rv = __shfl(rvt, 0, 64);
                 const int vx = (int)((uint32_t)v / (uint32_t)H), vy = v - vx * H;
                 if (lite) {  // node.key < calculateKey(node): re-key and push, nothing else (:104-106)
                     const double mn = gv < rv ? gv : rv;
