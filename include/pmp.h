@@ -482,7 +482,7 @@ int pmp_astar2d_set_engine(pmp_ctx* ctx, int engine, int t2_lds);
 
 /* Persistent workers (one wave each) per CU of the one-wave-per-query planners: pmp_graph3d_batch,
  * pmp_dstar2d_batch / pmp_dstar2d_onpress_batch, pmp_dstar3d_batch and pmp_lpastar3d_batch (default 16
- * each); 0 = the default.
+ * each), and the LPA* / D* Lite 2D entry points (default 24); 0 = the default.
  * Each launch caps it at ceil(nq / 256), so a small batch gets fewer workers with a larger LDS share
  * each.  Fewer workers leave each a larger LDS share of its heap (fewer spilled positions), more
  * workers hide more latency.  The longest-first schedule and its raised priority
