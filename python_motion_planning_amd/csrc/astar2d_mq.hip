@@ -255,6 +255,10 @@ __device__ __forceinline__ void bit_set(const GHeap& h, bool on, int level, uint
 }
 // CPython _siftup's choice bit of the parent of `child` (a position) whose new content is v and
 // whose sibling holds s: bit = !(left < right), odd positions are left children
+__device__ __forceinline__ bool choice_bit_k(int child, double vf, uint32_t vk, double sf, uint32_t sk)
+{
+    return (child & 1) ? !key_lt(vf, vk, sf, sk) : !key_lt(sf, sk, vf, vk);
+}
 template <int HEUR>
 __device__ __forceinline__ bool choice_bit(int child, double vf, uint32_t vc, double sf, uint32_t sc)
 {
@@ -278,11 +282,11 @@ struct PopOut {
 };
 
 template <bool T2LDS, int HEUR>
-__device__ __forceinline__ void heap_pop(const GHeap& h, const Walk& wk, int n, double& lastf, uint32_t& lastc,
+__device__ __forceinline__ void heap_pop(const GHeap& h, const Walk& wk, int n, double& lastf, uint32_t& lastc, uint32_t& lastk,
                                          double& rootf, uint32_t& rootc, int gl, int gb, PopOut& po)
 {
     const double lf = lastf;
-    const uint32_t lc = lastc;
+    const uint32_t lc = lastc, lk = lastk;  // lastk = hkey(lastc), kept beside it
     // ---- the path: levels 0..D-1 are full; `full` = D - 1 unconditional steps, then the last step
     const int D = 31 - __clz(n);
     const int full = D - 1 < 0 ? 0 : D - 1;
@@ -328,9 +332,10 @@ __device__ __forceinline__ void heap_pop(const GHeap& h, const Walk& wk, int n, 
     }
     // heap[p_{i+1}] is lane i+1's load (DPP row_shl:1; lanes 1..K-1 use it, K <= 14 stays in the row)
     const double Bf = shl1f(Af);
-    const uint32_t Bc = shl1(Ac);
     // ---- movers: the path prefix with !(last < heap[p_i])
-    const int m = __popc(rbits(on && !key_lt(lf, hkey<HEUR>(lc), Af, hkey<HEUR>(Ac)), gb));
+    const uint32_t Ak = hkey<HEUR>(Ac);
+    const uint32_t Bk = shl1(Ak);
+    const int m = __popc(rbits(on && !key_lt(lf, lk, Af, Ak), gb));
     {
         const bool l0 = gl == 0;
         const bool st = l0 || (on && gl <= m);
@@ -344,11 +349,12 @@ __device__ __forceinline__ void heap_pop(const GHeap& h, const Walk& wk, int n, 
     if (!(m == K && P == (uint32_t)n)) {
         lastf = a0f;
         lastc = a0c;
+        lastk = bc<0>(Ak);
     }
     // ---- bits of p_0 .. p_{m-1}
     {
         const bool useb = gl < m;
-        const bool bit = choice_bit<HEUR>(pi, useb ? Bf : lf, useb ? Bc : lc, Sf, Sc);
+        const bool bit = choice_bit_k(pi, useb ? Bf : lf, useb ? Bk : lk, Sf, hkey<HEUR>(Sc));
         bit_set<T2LDS>(h, hass && gl <= m, gl - 1, P >> (sh + 1), bit);
     }
     po.P = P;
@@ -364,7 +370,7 @@ __device__ __forceinline__ void heap_pop(const GHeap& h, const Walk& wk, int n, 
 // a_1..a_{t+1}.  Returns t; a1 = the new heap[parent(n)].
 template <bool T2LDS, int HEUR>
 __device__ __forceinline__ int heap_push(const GHeap& h, int n, double itf, uint32_t itc, uint32_t itk, double& lastf,
-                                         uint32_t& lastc, double& rootf, uint32_t& rootc, int gl, int gb, double& a1f,
+                                         uint32_t& lastc, uint32_t& lastk, double& rootf, uint32_t& rootc, int gl, int gb, double& a1f,
                                          uint32_t& a1c)
 {
     const uint32_t np1 = (uint32_t)n + 1u;
@@ -384,7 +390,8 @@ __device__ __forceinline__ int heap_push(const GHeap& h, int n, double itf, uint
         la.get(Af, Ac);
         ls.get(Sf, Sc);
     }
-    const int t = __popc(rbits(on && key_lt(itf, itk, Af, hkey<HEUR>(Ac)), gb));
+    const uint32_t Ak = hkey<HEUR>(Ac);
+    const int t = __popc(rbits(on && key_lt(itf, itk, Af, Ak), gb));
     const int ipos = (int)(np1 >> t) - 1;
     const double A1f = bcf<1>(Af), A2f = bcf<2>(Af);
     const uint32_t A1c = bc<1>(Ac), A2c = bc<2>(Ac);
@@ -401,9 +408,10 @@ __device__ __forceinline__ int heap_push(const GHeap& h, int n, double itf, uint
     }
     lastf = t == 0 ? itf : A1f;
     lastc = t == 0 ? itc : A1c;
+    lastk = t == 0 ? itk : bc<1>(Ak);
     {
         const bool usea = gl - 1 < t;
-        const bool bit = choice_bit<HEUR>(x, usea ? Af : itf, usea ? Ac : itc, Sf, Sc);
+        const bool bit = choice_bit_k(x, usea ? Af : itf, usea ? Ak : itk, Sf, hkey<HEUR>(Sc));
         bit_set<T2LDS>(h, hass && gl <= t + 1, D - l1, np1 >> l1, bit);
     }
     wave_sync_mem();
@@ -470,7 +478,7 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
     uint64_t cy_pop = 0, cy_exp = 0, cy_push = 0, cy_q0 = 0;
 #endif
     double rootf = 0.0, lastf = 0.0;
-    uint32_t rootc = 0u, lastc = 0u;
+    uint32_t rootc = 0u, lastc = 0u, lastk = 0u;  // lastk = hkey(lastc)
 
     // One iteration: every group with a query pops once (a_star.py:54) and expands the node
     // (a_star.py:57-82); then rounds of pushes (a_star.py:76-80) run until every group has pushed the
@@ -521,6 +529,7 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
                     rootc = pack_cm<HEUR>(0, 0, 8);
                     lastf = rootf;
                     lastc = rootc;
+                    lastk = hkey<HEUR>(rootc);
                     hst(hp, gl == 0, 0, rootf, rootc);
                     n = 1;
                     npush = 1;
@@ -608,7 +617,7 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
             po.Ac = 0u;
             const double lf0 = lastf;  // the old last element, which the pop places at p_m
             const uint32_t lc0 = lastc;
-            if (n > 0) heap_pop<T2LDS, HEUR>(hp, wk, n, lastf, lastc, rootf, rootc, gl, gb, po);
+            if (n > 0) heap_pop<T2LDS, HEUR>(hp, wk, n, lastf, lastc, lastk, rootf, rootc, gl, gb, po);
             pld.get(pf8, pc8);
             {
                 // patch the prefetched parents: the pop moved heap[p_{L+1}] into path node p_L (L < m)
@@ -718,15 +727,16 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
                     const bool inrun = gl < 8 && ((run >> mo) & 1u);
                     const int prev = below ? 31 - __clz(below) : 0;
                     const double lfp = bpf(ifv, gb + prev);
-                    const uint32_t lcp = bp(icm, gb + prev);
+                    const uint32_t lkp = bp(ik, gb + prev);
                     const double leftf = rank == 0 ? lastf : lfp;
-                    const uint32_t leftc = rank == 0 ? lastc : lcp;
+                    const uint32_t leftk = rank == 0 ? lastk : lkp;
                     bit_set<T2LDS>(hp, inrun && (pos & 1) == 0 && pos > 0, 30 - __clz(pos + 1), (uint32_t)(pos + 1) >> 1,
-                                   !key_lt(leftf, hkey<HEUR>(leftc), ifv, ik));
+                                   !key_lt(leftf, leftk, ifv, ik));
                     hst(hp, inrun, pos, ifv, icm);
                     const int top = 31 - __clz(run);
                     lastf = bpf(ifv, gb + top);
                     lastc = bp(icm, gb + top);
+                    lastk = bp(ik, gb + top);
                     const int k = __popc(run);
                     n += k;
                     npush += k;
@@ -741,7 +751,8 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
                     const uint32_t itc = bp(icm, gb + m);
                     double a1f;
                     uint32_t a1c;
-                    heap_push<T2LDS, HEUR>(hp, n, itf, itc, hkey<HEUR>(itc), lastf, lastc, rootf, rootc, gl, gb, a1f, a1c);
+                    heap_push<T2LDS, HEUR>(hp, n, itf, itc, bp(ik, gb + m), lastf, lastc, lastk, rootf, rootc, gl, gb, a1f,
+                                           a1c);
                     // a left child's right sibling (the next position) has the same parent, now a1
                     if (pc_ok && (n & 1) && gl == n - n0 + 1) {
                         pf8 = a1f;
