@@ -643,13 +643,15 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
             const uint32_t occ9 = rbits(gl < 9 && (!blk_in || ((blk_w >> blk_sh) & 1u)), gb) & 0x1FFu;
             uint32_t row = 0u;
             if (gl >= 9 && gl < 12 && blk_in) {
+                // the bytes of cells y-1, y, y+1 as bytes 0..2 of v (blk_sh = -1 when y = 0: byte 0 is
+                // then off the grid and masked below), tested together: a byte is CLOSED in this
+                // query when its high nibble is the epoch and its low nibble (motion + 1) is nonzero
                 const uint64_t win = ((uint64_t)blk_w2 << 32) | blk_w;
-#pragma unroll
-                for (int k = 0; k < 3; k++) {
-                    const int cy = y - 1 + k;
-                    const int bo = blk_sh + k < 0 ? 0 : blk_sh + k;
-                    if ((unsigned)cy < (unsigned)H && closed_byte((uint32_t)(win >> (8 * bo)) & 0xFFu, ep)) row |= 1u << k;
-                }
+                const uint32_t v = blk_sh < 0 ? (blk_w << 8) : (uint32_t)(win >> (8 * blk_sh));
+                const uint32_t lo = v & 0x0F0F0Fu, eq = ((v >> 4) & 0x0F0F0Fu) ^ (ep * 0x010101u);
+                const uint32_t m = (lo + 0x7F7F7Fu) & ~(eq + 0x7F7F7Fu) & 0x808080u;
+                row = ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u);
+                row &= (y > 0 ? 1u : 0u) | 2u | (y + 1 < H ? 4u : 0u);
             }
             const uint32_t cls9 = bc<9>(row) | (bc<10>(row) << 3) | (bc<11>(row) << 6);
             const double gp = bcf<12>(gpar);
