@@ -1277,7 +1277,9 @@ def latency_leg(args, torch, dist, world, rank):
                      "unit": "ms", "higher_is_better": False, "calls": reps, "expansions": len(expand),
                      "parts_ms": {"set_to_bitgrid": float(np.median(ingest)) * 1e3,
                                   "kernel_and_sync": float(np.median(kern)) * 1e3,
-                                  "closed_node_list": float(np.median(nodes)) * 1e3},
+                                  "closed_node_list": float(np.median(nodes)) * 1e3,
+                                  "note": "plan() packs the set while the kernel runs on the Grid's last upload "
+                                          "(re-run if the set changed); one pinned D2H per query"},
                      "reference_python_ms": "14.8-26.8 (SURVEY.md §6)" if name == "c1_readme" else
                                             "2760 mean per C2 query (SURVEY.md §6)",
                      "cpu_baseline": cpu}

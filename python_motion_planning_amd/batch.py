@@ -88,6 +88,58 @@ def astar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: in
     return out
 
 
+_ONE = {}
+
+
+class SingleQuery:
+    """One drop-in query (AStar.plan, a_star.py:39-83) with one host round trip: start/goal go up in
+    one pinned copy, the kernel writes (status, n_expanded, path_len | path | CLOSED records) into one
+    int32 device block, and the block comes back in one pinned copy and one stream sync.  The
+    buffers are kept per (context, capacities) and reused call after call."""
+
+    def __init__(self, torch, path_cap: int, expand_cap: int) -> None:
+        self.path_cap, self.expand_cap = path_cap, expand_cap
+        n = 4 + path_cap + expand_cap
+        self.dev = torch.empty(n, dtype=torch.int32, device="cuda")
+        self.host = torch.empty(n, dtype=torch.int32, pin_memory=True)
+        self.sg_host = torch.empty(4, dtype=torch.int32, pin_memory=True)
+        self.sg_dev = torch.empty(4, dtype=torch.int32, device="cuda")
+        self.cost = torch.empty(1, dtype=torch.float64, device="cuda")
+
+    def launch(self, torch, W: int, H: int, occ_bits, start, goal, heuristic: str, algo: str) -> None:
+        L, ctx = _lib.load_library(), _lib.context()
+        self.sg_host.numpy()[:] = (start[0], start[1], goal[0], goal[1])
+        self.sg_dev.copy_(self.sg_host, non_blocking=True)
+        d, pc = self.dev.data_ptr(), self.path_cap
+        rc = L.pmp_graph2d_batch(ctx, _lib.stream_ptr(), _lib.ALGOS[algo], occ_bits.data_ptr(), W, H,
+                                 1 if heuristic == "manhattan" else 0, self.sg_dev.data_ptr(),
+                                 self.sg_dev.data_ptr() + 8, 1, self.cost.data_ptr(), d + 8, d + 16, pc, d + 4,
+                                 d + 16 + 4 * pc, self.expand_cap, None, d)
+        _lib.check(ctx, rc, "pmp_graph2d_batch")
+        self.host.copy_(self.dev, non_blocking=True)
+        self.event = torch.cuda.Event()
+        self.event.record()
+
+    def result(self):
+        """(status, n_expanded, path cells goal->start, CLOSED records) as numpy, after the sync."""
+        self.event.synchronize()
+        h = self.host.numpy()
+        st, nexp, plen = int(h[0]), int(h[1]), int(h[2])
+        path = h[4: 4 + min(max(plen, 0), self.path_cap)].copy()
+        exp = h[4 + self.path_cap: 4 + self.path_cap + min(max(nexp, 0), self.expand_cap)].view(np.uint32).copy()
+        return st, nexp, plen, path, exp
+
+
+def single_query(torch, path_cap: int, expand_cap: int) -> SingleQuery:
+    key = (_lib.context(), path_cap, expand_cap)
+    q = _ONE.get(key)
+    if q is None:
+        if len(_ONE) > 16:
+            _ONE.clear()
+        q = _ONE[key] = SingleQuery(torch, path_cap, expand_cap)
+    return q
+
+
 _RECORDS = ("cost", "path_len", "path", "n_expanded", "status")
 
 

@@ -54,6 +54,35 @@ def test_readme_dropin_class():
     assert expand[0].current == (5, 5) and expand[0].parent == (5, 5) and expand[0].g == 0
 
 
+def test_dropin_obstacle_set_changes_between_calls():
+    """plan() launches on the Grid's last uploaded bit grid while it packs the obstacle set again:
+    an obstacle added or removed between two calls must re-run the query on the new set."""
+    from oracle import oracle as O
+
+    pmp = _pmp()
+    fx = load_json("astar_readme.json")
+    env = pmp.Grid(51, 31)
+    for x, y in fx["obstacles"]:
+        env.obstacles.add((x, y))
+    env.update(env.obstacles)
+    planner = pmp.AStar((5, 5), (45, 25), env)
+    cost0, path0, _ = planner.plan()
+    block = path0[len(path0) // 2]
+    for step in range(3):
+        if step == 1:
+            env.obstacles.add(block)  # in place: same set object, same Grid
+        elif step == 2:
+            env.obstacles.discard(block)
+        cost, path, expand = planner.plan()
+        ref = O.astar2d(env.occupancy(), (5, 5), (45, 25))
+        assert ref["status"] == 0 and cost == ref["cost"] and path == ref["path"], step
+        assert [n.current[0] * 31 + n.current[1] for n in expand] == ref["expand_cells"].tolist(), step
+        if step != 1:
+            assert cost == cost0 and path == path0
+        else:
+            assert block not in path
+
+
 def test_small_grids_against_reference(engine):
     from python_motion_planning_amd import batch
 
