@@ -7,8 +7,11 @@ Headline step = one pass of the hot path over one batch: 4096 start/goal pairs o
 (SURVEY.md §8(d) generator), inputs resident in HBM, outputs (cost, path, n_expanded, status)
 written to HBM.  Secondary legs (--legs): the H=30 x 4096-sample control step (C4, DWA form), RRT*
 on the C3 512^2 map (65,536 samples), 3D A* on C5 (8192 queries), and the LQR / MPC tracking steps
-on the C4 agents.  Multi-GPU: weak scaling, every rank runs its own shard (rank-offset seeds) of
-every leg; no collective on the data path.  Rank 0 prints one JSON line.
+on the C4 agents.  Multi-GPU: --scaling weak (default), every rank runs its own shard (rank-offset
+seeds) of every leg; --scaling strong, one fixed batch per leg is dealt over the ranks (C2 pairs and
+C5 queries longest-first round-robin, C4 agents round-robin) and the records are all_gathered back
+into input order at the end (rank 0 checks them against a replay of the whole batch on its GPU).  No
+collective on the data path.  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -35,23 +38,60 @@ def astar_algorithmic_bytes(counters: np.ndarray) -> float:
     return float(np.sum(19.0 * E + 16.0 * (P + Q)))
 
 
+def c4_share(args, na, world, rank):
+    """C4 agents of this rank: weak scaling, `na` agents of its own (default_rng(2 + rank)); strong
+    scaling, its round-robin share of one fixed set of `na` agents (default_rng(2)).  Returns
+    (occ, states, goals, indices into the fixed set or None)."""
+    from python_motion_planning_amd import shard, workloads as wl
+
+    if args.scaling == "strong":
+        occ, states, goals = wl.c4_workload(na, seed=2)
+        mine = shard.lpt_deal(np.ones(na), world, rank)  # equal work per agent: round-robin
+        return occ, states[mine], goals[mine], mine
+    occ, states, goals = wl.c4_workload(na, seed=2 + rank)
+    return occ, states, goals, None
+
+
+def dwa_inputs(torch, occ, states, goals):
+    """The C4 agents' global paths (start -> goal): A* from each agent's cell to (45, 25) on the GPU."""
+    from python_motion_planning_amd import batch
+
+    na = len(states)
+    r = batch.astar2d_batch(occ, states[:, :2].astype(np.int32), np.tile([45, 25], (na, 1)).astype(np.int32),
+                            path_cap=2048)
+    pl, P = r["path_len"].cpu().numpy(), r["path"].cpu().numpy()
+    Hg = occ.shape[1]
+    paths = [np.column_stack([P[i, : pl[i]][::-1] // Hg, P[i, : pl[i]][::-1] % Hg]).astype(np.float64)
+             for i in range(na)]
+    return paths
+
+
+def control_replay(args, torch, occ, states, goals, K):
+    """K DWA steps of all the given agents in one launch each (untimed): the strong-scaling check."""
+    from python_motion_planning_amd import _lib, batch, local_planner
+
+    paths = dwa_inputs(torch, occ, states, goals)
+    xy, off = batch.pack_paths(paths)
+    lp = _lib.LPParams.from_params(local_planner.LocalPlanner.DEFAULTS)
+    dp = _lib.DWAParams(0.2, 0.1, 0.05, 3.0, 1.0, 0.05, 0.05, 64, 64)
+    grid = batch.obstacle_grid({(int(a), int(b)) for a, b in np.argwhere(occ)})
+    st = torch.tensor(states, dtype=torch.float64, device="cuda")
+    o = None
+    for _ in range(K):
+        o = batch.dwa_step_batch(grid, lp, dp, st, goals, xy, off)
+    torch.cuda.synchronize()
+    return {"state": st, "u": o["u"], "best": o["best"]}
+
+
 def control_leg(args, torch, dist, world, rank):
     """BASELINE.json's second metric: MPC-style sampled control steps/s at H=30 x 4096 samples (C4):
     256 agents per GPU on the README grid, each step = one DWA.plan iteration (dwa.py:72-93) with a
     64 x 64 (v, w) window, predict_time 3.0 (H = 30).  One timed step = one launch over all agents."""
-    from python_motion_planning_amd import _lib, batch, local_planner, workloads as wl
+    from python_motion_planning_amd import _lib, batch, local_planner, shard
 
-    na = args.agents
-    occ, states, goals = wl.c4_workload(na, seed=2 + rank)
-    r = batch.astar2d_batch(occ, states[:, :2].astype(np.int32), np.tile([45, 25], (na, 1)).astype(np.int32),
-                            path_cap=2048)
-    pl = r["path_len"].cpu().numpy()
-    P = r["path"].cpu().numpy()
-    Hg = occ.shape[1]
-    paths = []
-    for i in range(na):
-        cells = P[i, : pl[i]][::-1]
-        paths.append(np.column_stack([cells // Hg, cells % Hg]).astype(np.float64))
+    occ, states, goals, mine = c4_share(args, args.agents, world, rank)
+    na = len(states)
+    paths = dwa_inputs(torch, occ, states, goals)
     xy, off = batch.pack_paths(paths)
     lp = _lib.LPParams.from_params(local_planner.LocalPlanner.DEFAULTS)
     dp = _lib.DWAParams(0.2, 0.1, 0.05, 3.0, 1.0, 0.05, 0.05, 64, 64)
@@ -94,7 +134,18 @@ def control_leg(args, torch, dist, world, rank):
         step()
     torch.cuda.synchronize()
     checked = check_timed("dwa", ref_out, [{"state": st, "u": u, "best": best, "status": status}])
-    steps_done = na * K * world
+    steps_done = (args.agents if args.scaling == "strong" else na * world) * K
+    gathered = None
+    if args.scaling == "strong":
+        # the fixed agent set's records from every rank, in agent order; rank 0 replays all the agents
+        # on its own GPU (untimed) and compares
+        g = shard.all_gather_rows(dist, mine, {k: ref_out[k] for k in ("state", "u", "best")}, args.agents,
+                                  device="cuda")
+        gathered = {"agents": args.agents, "agents_this_rank": na}
+        if rank == 0:
+            occ1, st1, gl1, _ = c4_share(args, args.agents, 1, 0)
+            full = control_replay(args, torch, occ1, st1, gl1, K)
+            gathered["gathered_equal_single_rank"] = all(torch.equal(g[k], full[k]) for k in ("state", "u", "best"))
     # SURVEY.md §8(d) C4 in the stencil formulation, transcendental calls not counted: per sample and
     # step 12 flops of rollout (x, y, th updates) + a 3x3 stencil of 6 flops per cell; 20 per sample
     # for normalisation and scoring -> 8.2 MFLOP per agent-step
@@ -131,6 +182,7 @@ def control_leg(args, torch, dist, world, rank):
     _LABEL[0] = "setup"
     return {"metric": "MPC steps/sec (H=30, 4096 samples): sampled-rollout control step (DWA form)",
             "value": steps_done / elapsed, "unit": "agent-steps/s", "agents_per_gpu": na, "steps": K,
+            "scaling": args.scaling, "strong_scaling_gather": gathered,
             "ms_per_step": elapsed / K * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
             "timed_launches_checked": checked,
             "config": {"workload": "C4: README 51x31 grid, 64x64 (v,w) samples, H=30, weights 0.2/0.1/0.05"},
@@ -558,8 +610,14 @@ def astar3d_leg(args, torch, dist, world, rank):
     safety bubbles carved per query, so each query has its own occupancy)."""
     from python_motion_planning_amd import _lib, batch, shard, workloads as wl
 
-    nq = args.a3_queries
-    occ, s, g = wl.c5_workload(nq, first_seed=rank * nq)
+    if args.scaling == "strong":  # one fixed 8192-query batch dealt longest-first round-robin
+        occ_all, s_all, g_all = wl.c5_workload(args.a3_queries, first_seed=0)
+        mine = shard.lpt_deal(shard.octile(s_all, g_all), world, rank)
+        occ, s, g = occ_all[mine], s_all[mine], g_all[mine]
+    else:
+        occ, s, g = wl.c5_workload(args.a3_queries, first_seed=rank * args.a3_queries)
+        mine = None
+    nq = len(s)
     _LABEL[0] = "astar3d"
     X, Y, Z = occ.shape[1:]
     words = np.stack([batch.pack_bits(o) for o in occ])
@@ -635,6 +693,18 @@ def astar3d_leg(args, torch, dist, world, rank):
         outs += [{k: b[k][j * nq:(j + 1) * nq] for k in akeys} for j in range(last_nb)]
     checked = check_timed("astar3d", ref_out, outs)
     cost = ref_out["cost"]
+    gathered = None
+    if args.scaling == "strong":
+        # the fixed batch's records from every rank in input order; rank 0 plans the whole batch on its
+        # own GPU (untimed) and compares
+        gk = ("cost", "st", "nexp", "plen")
+        gth = shard.all_gather_rows(dist, mine, {k: ref_out[k] for k in gk}, args.a3_queries, device="cuda")
+        gathered = {"queries": args.a3_queries, "queries_this_rank": nq}
+        if rank == 0:
+            full = batch.astar3d_batch(occ_all, s_all, g_all, path_cap=cap)
+            torch.cuda.synchronize()
+            gathered["gathered_equal_single_rank"] = all(
+                torch.equal(gth[k], full[f]) for k, f in zip(gk, ("cost", "status", "n_expanded", "path_len")))
     # per plan 55*E3 + 16*(P3 + Q3), with P3 the reference's pushes and Q3 <= P3
     # (every pushed entry popped at most once): 55*E3 + 32*P3
     alg_bytes = float(np.sum(55.0 * c[:, 2] + 32.0 * c[:, 0])) * float(np.mean(nbs))
@@ -663,8 +733,10 @@ def astar3d_leg(args, torch, dist, world, rank):
     torch.cuda.synchronize()
     for b in lanes:  # the lanes' scratch (about 15 GB each) is not needed by the other legs
         L.pmp_destroy(b["ctx"])
-    return {"metric": "3D A* plans/sec, Grid3D(26,20,16) door scenario, 8192 queries", "value": nq * args.a3_steps * world / elapsed,
+    plans = (args.a3_queries if args.scaling == "strong" else nq * world) * args.a3_steps
+    return {"metric": "3D A* plans/sec, Grid3D(26,20,16) door scenario, 8192 queries", "value": plans / elapsed,
             "unit": "plans/s", "queries_per_gpu": nq, "steps": args.a3_steps,
+            "scaling": args.scaling, "strong_scaling_gather": gathered,
             "ms_per_step": elapsed / args.a3_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
             "streams": len(lanes), "batches_per_launch": B, "timed_launches_checked": checked,
             "workers_per_cu": wpc, "resident_per_cu": args.a3_residency,
@@ -1290,16 +1362,12 @@ def latency_leg(args, torch, dist, world, rank):
 def track_leg(args, torch, dist, world, rank, kind):
     """LQR / MPC tracking (lqr.py:58-86 / mpc.py:66-94) for the C4 agents: one timed step = one launch
     running `iters` plan iterations of every agent (MPC at p = 30, m = 8, ADMM to 1e-9)."""
-    from python_motion_planning_amd import _lib, batch, local_planner, workloads as wl
+    from python_motion_planning_amd import _lib, batch, local_planner, shard
 
-    na, iters = args.track_agents, args.track_iters
-    occ, states, goals = wl.c4_workload(na, seed=2 + rank)
-    r = batch.astar2d_batch(occ, states[:, :2].astype(np.int32), np.tile([45, 25], (na, 1)).astype(np.int32),
-                            path_cap=2048)
-    pl, P = r["path_len"].cpu().numpy(), r["path"].cpu().numpy()
-    Hg = occ.shape[1]
-    paths = [np.column_stack([P[i, : pl[i]][::-1] // Hg, P[i, : pl[i]][::-1] % Hg]).astype(np.float64)
-             for i in range(na)]
+    iters = args.track_iters
+    occ, states, goals, mine = c4_share(args, args.track_agents, world, rank)
+    na = len(states)
+    paths = dwa_inputs(torch, occ, states, goals)
     xy, off = batch.pack_paths(paths)
     lp = _lib.LPParams.from_params(local_planner.LocalPlanner.DEFAULTS)
     kw = dict(lqr_params=_lib.LQRParams.make()) if kind == "lqr" else dict(mpc_params=_lib.MPCParams.make(p=30))
@@ -1327,6 +1395,27 @@ def track_leg(args, torch, dist, world, rank, kind):
     last = []
     elapsed, kern_ms = timed(torch, dist, run, args.track_steps, last=last)
     checked = check_timed(kind, ref_out, last)
+    gathered = None
+    steps_all = stepped * world
+    if args.scaling == "strong":
+        # the fixed agent set's records from every rank in agent order; rank 0 replays all the agents on
+        # its own GPU (untimed, one launch) and compares
+        g = shard.all_gather_rows(dist, mine, {k: ref_out[k] for k in ("u", "n_steps", "state", "u_p")},
+                                  args.track_agents, device="cuda")
+        steps_all = int(g["n_steps"].sum().item())
+        gathered = {"agents": args.track_agents, "agents_this_rank": na, "agent_steps": steps_all}
+        if rank == 0:
+            occ1, st1, gl1, _ = c4_share(args, args.track_agents, 1, 0)
+            xy1, off1 = batch.pack_paths(dwa_inputs(torch, occ1, st1, gl1))
+            st1d = torch.tensor(st1, dtype=torch.float64, device="cuda")
+            up1 = torch.zeros((len(st1), 2), dtype=torch.float64, device="cuda")
+            o1 = batch.track_step_batch(kind, lp, st1d, torch.tensor(gl1, dtype=torch.float64, device="cuda"),
+                                        torch.tensor(xy1, dtype=torch.float64, device="cuda"),
+                                        torch.tensor(off1, dtype=torch.int32, device="cuda"), iters=iters, u_p=up1,
+                                        **kw)
+            torch.cuda.synchronize()
+            full = {"u": o1["u"], "n_steps": o1["n_steps"], "state": st1d, "u_p": up1}
+            gathered["gathered_equal_single_rank"] = all(torch.equal(g[k], full[k]) for k in full)
     if kind == "mpc":
         # per ADMM iteration ~ 16x16 inverse matvec (512) + scans/projections (~150); assembly 2*16*16*3p (MFMA)
         flops = admm * 662.0 + stepped * 2 * 16 * 16 * 90
@@ -1356,8 +1445,9 @@ def track_leg(args, torch, dist, world, rank, kind):
                          f"(oracle/pmp_oracle.c) with OpenMP over agents, {dt:.1f} s wall"}
     _LABEL[0] = "setup"
     name = "LQR" if kind == "lqr" else "MPC (p=30, m=8, ADMM QP)"
-    return {"metric": f"{name} tracking agent-steps/sec", "value": stepped * args.track_steps * world / elapsed,
+    return {"metric": f"{name} tracking agent-steps/sec", "value": steps_all * args.track_steps / elapsed,
             "unit": "agent-steps/s", "agents_per_gpu": na, "iterations_per_launch": iters, "steps": args.track_steps,
+            "scaling": args.scaling, "strong_scaling_gather": gathered,
             "ms_per_step": elapsed / args.track_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
             "config": {"workload": f"C4 agents on the README grid ({na} per launch), {iters} LQR/MPC plan iterations "
                                    f"per launch"},
@@ -1443,14 +1533,16 @@ def headline_line(out: dict, detail_path) -> dict:
 
 def dry_run(args, rank, world):
     """--dry-run: the multi-rank plumbing without a GPU.  Ranks come from launch_ranks (or
-    torch.distributed.run), join a gloo group, take their longest-first round-robin share of one
-    96-query batch on a 64^2 grid, plan it with the CPU oracle standing in for the kernels, and
-    all_gather the records; rank 0 checks the gathered batch against one single-process oracle run
-    and prints a JSON line of the bench's shape (n_gpus = world)."""
+    torch.distributed.run) and join a gloo group.  Each strong-scaling workload is dealt over the ranks
+    exactly as the GPU legs deal it -- C2 (96 queries, 64^2 grid) and C5 (48 per-query 3D grids)
+    longest-first round-robin by octile distance, the C4 agents (12 DWA, 16 LQR) round-robin
+    (c4_share) -- planned with the CPU oracle standing in for the kernels, and all_gathered; rank 0
+    checks every gathered record set against one single-process oracle run and prints a JSON line of
+    the bench's shape (n_gpus = world)."""
     import torch  # noqa: F401  (torch.distributed)
 
     from oracle import oracle as O
-    from python_motion_planning_amd import shard, workloads as wl
+    from python_motion_planning_amd import batch, shard, workloads as wl
 
     dist = shard.init("gloo")
     occ, starts, goals = wl.c2_workload(nq=96, W=64, H=64, pair_seed=6)
@@ -1460,18 +1552,55 @@ def dry_run(args, rank, world):
         return {"cost": torch.as_tensor(r["cost"]), "status": torch.as_tensor(r["status"]),
                 "n_expanded": torch.as_tensor(r["n_expanded"]), "path_len": torch.as_tensor(r["path_len"])}
 
+    occ3, s3, g3 = wl.c5_workload(48, first_seed=0)
+
+    def plan3(s, g, occ):
+        cost, st = O.astar3d_batch(occ, s, g, nthreads=1)
+        return {"cost": torch.as_tensor(cost), "status": torch.as_tensor(st)}
+
+    def c4_paths(occ4, states):
+        r = O.astar2d_batch(occ4, states[:, :2].astype(np.int32), np.tile([45, 25], (len(states), 1)).astype(np.int32),
+                            path_cap=2048, nthreads=1)
+        H4 = occ4.shape[1]
+        paths = [np.column_stack([r["path"][i, : r["path_len"][i]][::-1] // H4,
+                                  r["path"][i, : r["path_len"][i]][::-1] % H4]).astype(np.float64)
+                 for i in range(len(states))]
+        return batch.pack_paths(paths)
+
+    def dwa(occ4, states, goals4):
+        xy, off = c4_paths(occ4, states)
+        st, u, status = O.dwa_step_batch(np.argwhere(occ4).astype(np.float64), xy, off, goals4, states, nthreads=1,
+                                         grid=occ4)
+        return {"state": torch.as_tensor(st), "u": torch.as_tensor(u), "status": torch.as_tensor(status)}
+
+    def lqr(occ4, states, goals4):
+        xy, off = c4_paths(occ4, states)
+        st, up, u, status, nst, _ = O.track_batch("lqr", xy, off, goals4, states, iters=5, nthreads=1)
+        return {"state": torch.as_tensor(st), "u": torch.as_tensor(u), "n_steps": torch.as_tensor(nst)}
+
     shard.barrier(dist)
     t0 = time.perf_counter()
     out = shard.run_sharded(dist, plan, starts, goals)
     shard.barrier(dist)
     (elapsed,) = shard.max_over_ranks(dist, [time.perf_counter() - t0])
+    out3 = shard.run_sharded(dist, plan3, s3, g3, per_query={"occ": occ3})
+    c4 = {}
+    for name, fn, na in (("c4_dwa", dwa, 12), ("c4_lqr", lqr, 16)):
+        occ4, st4, gl4, mine = c4_share(args, na, world, rank)
+        c4[name] = shard.all_gather_rows(dist, mine, fn(occ4, st4, gl4), na)
     if rank == 0:
         ref = O.astar2d_batch(occ, starts, goals, path_cap=4096, nthreads=1)
-        equal = all(np.array_equal(out[k].numpy(), ref[k]) for k in ("cost", "status", "n_expanded", "path_len"))
+        eq = {"c2": all(np.array_equal(out[k].numpy(), ref[k]) for k in ("cost", "status", "n_expanded", "path_len"))}
+        ref3 = plan3(s3, g3, occ3)
+        eq["c5"] = all(torch.equal(out3[k], ref3[k]) for k in ref3)
+        for name, fn, na in (("c4_dwa", dwa, 12), ("c4_lqr", lqr, 16)):
+            occ4, st4, gl4, _ = c4_share(args, na, 1, 0)
+            ref4 = fn(occ4, st4, gl4)
+            eq[name] = all(torch.equal(c4[name][k], ref4[k]) for k in ref4)
         print(json.dumps({"metric": "dry run: A* plans/sec (CPU oracle stand-in, 64^2 grid, 96 queries)",
                           "value": 96 / elapsed, "unit": "plans/s", "n_gpus": world, "steps": 1, "warmup": 0,
-                          "scaling": "strong", "dry_run": True, "gathered_equal_single_rank": equal,
-                          "higher_is_better": True}), flush=True)
+                          "scaling": "strong", "dry_run": True, "gathered_equal_single_rank": all(eq.values()),
+                          "gathered_equal": eq, "higher_is_better": True}), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

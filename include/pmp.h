@@ -499,6 +499,12 @@ int pmp_set_resident_per_cu(pmp_ctx* ctx, int per_cu);
 /* Pre-size the A* scratch (heap of heap_cap entries per concurrent query, up to max_slots
  * concurrent queries) so that later batch calls allocate nothing (hipGraph-capturable). */
 int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int max_slots, int heap_cap);
+/* The A* 2D scratch geometry in force: out[0..5] = {W, H, max_slots, heap_cap, multi-query engine
+ * reserved (1/0), sized by the launches (1) or by pmp_astar2d_reserve (0)}; all 0 before any. */
+int pmp_astar2d_geometry(pmp_ctx* ctx, int32_t* out6);
+/* Forget the host's pmp_astar2d_reserve geometry: the next launch sizes the scratch for its own
+ * batch and later larger batches grow it, as on a fresh context (allocated scratch is kept). */
+int pmp_astar2d_reserve_auto(pmp_ctx* ctx);
 
 #ifdef __cplusplus
 }

@@ -28,6 +28,8 @@ SIGNATURES = {
     "pmp_graph3d_batch": (_i, [_vp, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp,
                                _i, _vp, _vp]),
     "pmp_astar2d_reserve": (_i, [_vp, _i, _i, _i, _i]),
+    "pmp_astar2d_geometry": (_i, [_vp, _vp]),
+    "pmp_astar2d_reserve_auto": (_i, [_vp]),
     "pmp_set_timing": (_i, [_vp, _vp]),
     "pmp_wall_clock_khz": (_i, [_vp, _vp]),
     "pmp_astar2d_set_schedule": (_i, [_vp, _i]),

@@ -76,14 +76,19 @@ def astar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: in
         if redo.numel():
             full = 8 * W * H + 8
             workers = max(1, min(int(redo.numel()), 256))
+            geo = np.zeros(6, np.int32)  # the geometry in force, restored after the re-run
+            _lib.check(ctx, L.pmp_astar2d_geometry(ctx, geo.ctypes.data), "pmp_astar2d_geometry")
             _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, workers, full), "pmp_astar2d_reserve")
             r = astar2d_batch((W, H), s[redo], g[redo], heuristic, path_cap, expand_cap, counters, occ_bits,
                               retry_overflow=False, algo=algo)
             for k in ("cost", "path_len", "path", "n_expanded", "status", "expand", "counters"):
                 if out[k] is not None:
                     out[k][redo] = r[k]
-            _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, int(reserve_slots or 1024), int(heap_cap)),
-                       "pmp_astar2d_reserve")
+            if geo[5] or not geo[0]:  # sized by the launches: keep it that way (grows with the batches)
+                _lib.check(ctx, L.pmp_astar2d_reserve_auto(ctx), "pmp_astar2d_reserve_auto")
+            else:  # the host's own reservation
+                _lib.check(ctx, L.pmp_astar2d_reserve(ctx, int(geo[0]), int(geo[1]), int(geo[2]), int(geo[3])),
+                           "pmp_astar2d_reserve")
     out["W"], out["H"] = W, H
     return out
 

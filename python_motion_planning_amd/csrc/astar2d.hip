@@ -1097,13 +1097,18 @@ static int astar2d_reserve_impl(pmp_ctx* ctx, int W, int H, int workers, int hea
 {
     if (W < 1 || H < 1 || W > kMaxDim || H > kMaxDim || workers < 1)
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_astar2d_reserve: bad dims/workers");
-    if (heap_cap <= 0) heap_cap = default_heap_cap(W, H);
+    const int mq_cap = pmp_astar2d_mq_cap(ctx->astar_mq_t2lds != 0);
+    const bool dflt = heap_cap <= 0;
+    if (dflt) heap_cap = default_heap_cap(W, H);
     if ((size_t)heap_cap > max_heap(W, H)) heap_cap = (int)max_heap(W, H);
-    if (ctx->astar_engine >= 1 && heap_cap <= 65536 && heap_cap > pmp_astar2d_mq_cap(ctx->astar_mq_t2lds != 0))
-        heap_cap = pmp_astar2d_mq_cap(ctx->astar_mq_t2lds != 0);  // the default capacity on the multi-query engine
-    if (ctx->astar_engine >= 1 && heap_cap <= pmp_astar2d_mq_cap(ctx->astar_mq_t2lds != 0)) {
+    // the default capacity on the multi-query engine is its limit; a capacity the host asked for (an
+    // explicit one, or the full bound of an overflow re-run) is kept and, above that limit, reserves
+    // the one-query-per-wave engine instead
+    ctx->astar_heap_cap_wave = heap_cap;  // small batches on a multi-query reservation (pmp_graph2d_batch)
+    if (ctx->astar_engine >= 1 && dflt && heap_cap > mq_cap) heap_cap = mq_cap;
+    if (ctx->astar_engine >= 1 && heap_cap <= mq_cap) {
         // workers = queries in flight (16-lane groups, 4 per wave); scratch is taken at launch
-        const size_t per_slot = (size_t)W * H * 9 + (size_t)pmp_astar2d_mq_cap(ctx->astar_mq_t2lds != 0) * 16 + 4096 + 256;
+        const size_t per_slot = (size_t)W * H * 9 + (size_t)mq_cap * 16 + 4096 + 256;
         const size_t fit = kScratchBudgetMq / per_slot;
         if (fit < 4) return pmp_set_err(ctx, PMP_ENOMEM, "pmp_astar2d_reserve: one wave exceeds the scratch budget");
         if ((size_t)workers > fit) workers = (int)(fit & ~(size_t)3);
@@ -1155,6 +1160,26 @@ extern "C" int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int workers, int 
     const int rc = astar2d_reserve_impl(ctx, W, H, workers, heap_cap);
     if (rc == PMP_OK) ctx->astar_auto = 0;  // the host's own geometry: launches keep it
     return rc;
+}
+
+extern "C" int pmp_astar2d_geometry(pmp_ctx* ctx, int32_t* out6)
+{
+    if (!ctx || !out6) return PMP_EINVAL;
+    out6[0] = ctx->astar_W;
+    out6[1] = ctx->astar_H;
+    out6[2] = ctx->astar_workers;
+    out6[3] = ctx->astar_heap_cap;
+    out6[4] = ctx->astar_reserved_mq;
+    out6[5] = ctx->astar_auto;
+    return PMP_OK;
+}
+
+extern "C" int pmp_astar2d_reserve_auto(pmp_ctx* ctx)
+{
+    if (!ctx) return PMP_EINVAL;
+    ctx->astar_W = ctx->astar_H = 0;  // the next launch reserves for its batch (pmp_graph2d_batch)
+    ctx->astar_auto = 1;
+    return PMP_OK;
 }
 
 extern "C" int pmp_astar2d_set_engine(pmp_ctx* ctx, int engine, int t2_lds)
@@ -1225,15 +1250,16 @@ extern "C" int pmp_graph2d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     }
     const size_t ncell = (size_t)W * H;
     const size_t cst_words = ((ncell + 7) / 8 + 3) & ~(size_t)3;
-    const int heap_cap = ctx->astar_heap_cap;
     // one-query-per-wave launch geometry: the reservation's, or on a multi-query reservation this
-    // engine's defaults for the batch
+    // engine's defaults for the batch (with the heap capacity asked for, or this engine's default: not the multi-query limit)
+    int heap_cap = ctx->astar_heap_cap;
     int workers, per_cu, lds_cap;
     if (!ctx->astar_reserved_mq) {
         workers = ctx->astar_workers < nq ? ctx->astar_workers : nq;
         per_cu = ctx->astar_resident_per_cu > 0 ? ctx->astar_resident_per_cu : (ctx->astar_workers + 255) / 256;
         lds_cap = ctx->astar_lds_cap;
     } else {
+        heap_cap = ctx->astar_heap_cap_wave;
         workers = default_workers() < nq ? default_workers() : nq;
         per_cu = ctx->astar_resident_per_cu > 0 ? ctx->astar_resident_per_cu : (workers + 255) / 256;
         if (per_cu > 32) per_cu = 32;

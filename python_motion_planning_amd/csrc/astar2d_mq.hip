@@ -143,10 +143,14 @@ struct GHeap {
     lds_u32* B;      // LDS bit words: tier 0 (word 0), tier 1 (words 1..32)[, tier-2 bytes from word 36]
     uint32_t* T2;    // HBM tier-2 words (when not in LDS)
     __amdgpu_buffer_rsrc_t spill;  // the wave's spill region (4 groups)
-    uint32_t soff;   // this group's byte offset in it
+    uint32_t sbase;  // byte offset of heap position 0 in the spill region (mod 2^32): positions >= cap are spilled
     int cap;
 };
 constexpr uint32_t kOOR = 0x80000000u;  // a buffer offset beyond any spill region: loads 0, stores dropped
+#ifndef PMP_MQ_SPILL_SHIFT
+#define PMP_MQ_SPILL_SHIFT 1
+#endif
+constexpr int kSpillShift = PMP_MQ_SPILL_SHIFT;  // empty slots in front of position cap
 
 struct Ld {
     double fl;
@@ -157,7 +161,7 @@ struct Ld {
     {
         in = p < h.cap;
         const int pl = in ? p : 0;
-        const uint32_t off = in ? kOOR : h.soff + (uint32_t)(p - h.cap) * 16u;
+        const uint32_t off = in ? kOOR : h.sbase + (uint32_t)p * 16u;
         v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(h.spill, off, 0, 0));
         fl = h.F[pl];
         cl = h.C[pl];
@@ -178,7 +182,7 @@ __device__ __forceinline__ void hst(const GHeap& h, bool on, int p, double f, ui
     }
     const uint64_t b = (uint64_t)__double_as_longlong(f);
     const uint4 v = make_uint4((uint32_t)b, (uint32_t)(b >> 32), c, 0u);
-    const uint32_t off = (on && p >= h.cap) ? h.soff + (uint32_t)(p - h.cap) * 16u : kOOR;
+    const uint32_t off = (on && p >= h.cap) ? h.sbase + (uint32_t)p * 16u : kOOR;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
                                            h.spill, off, 0, 0);
 }
@@ -448,7 +452,9 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
         hp.T2 = t2_all + slot * kT2Words;
         hp.spill = __builtin_amdgcn_make_buffer_rsrc(spill_all + (size_t)blockIdx.x * 4u * (size_t)spill_n, 0,
                                                      (int)(4u * (uint32_t)spill_n * 16u), 0x00020000);
-        hp.soff = (uint32_t)grp * (uint32_t)spill_n * 16u;
+        // sibling pairs (2k+1, 2k+2) share a 32-B aligned slot pair (one line) when the spill's first
+        // slot holds position cap - kSpillShift (cap is a multiple of 16, spill_n is even)
+        hp.sbase = (uint32_t)grp * (uint32_t)spill_n * 16u + (uint32_t)(kSpillShift - lds_cap) * 16u;
         hp.cap = lds_cap;
     }
     uint8_t* cst = cst_all + slot * cst_bytes;
@@ -821,7 +827,7 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
     const int region = bits_b + 12 * lds_cap;
     const int cap_max = t2lds ? kMqCapT2L : kMqCap;
     const int heap_cap = ctx->astar_heap_cap < cap_max ? ctx->astar_heap_cap : cap_max;
-    const int spill_n = heap_cap > lds_cap ? heap_cap - lds_cap : 1;
+    const int spill_n = ((heap_cap > lds_cap ? heap_cap - lds_cap : 1) + kSpillShift + 1) & ~1;
     const size_t cst_bytes = mq_cst_bytes(W, H);
     const size_t ncell = (size_t)W * H;
     const size_t slots = (size_t)waves * 4;

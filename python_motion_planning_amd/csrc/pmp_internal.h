@@ -30,6 +30,7 @@ struct pmp_ctx {
     // direction bits in LDS (1) or HBM (0); the geometry its per-slot epochs were written for
     int astar_engine = 1;
     int astar_mq_t2lds = 0;
+    int astar_heap_cap_wave = 0;  // heap capacity of one-query-per-wave launches on a multi-query reservation
     int astar_reserved_mq = 0;  // the current reservation (pmp_astar2d_reserve) is the multi-query engine's
     int astar_auto = 0;         // ... and was made by a launch (not the host): it grows with the batches
     size_t astar_mq_epoch_slots = 0, astar_mq_cst_bytes = 0;

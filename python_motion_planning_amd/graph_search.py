@@ -112,6 +112,9 @@ class AStar(GraphSearcher):
                 continue
             break
         if st == _lib.STATUS_CAP_OVERFLOW:  # heap outgrew the reservation: the batch path's full-bound re-plan
+            # sized for any outcome (a path visits a cell at most once, a cell closes at most once): the
+            # full search may close more cells than the overflowed run had reached
+            path_cap, expand_cap = W * H + 1, W * H
             r = batch.astar2d_batch((W, H), np.array([s]), np.array([g]), self.heuristic_type, path_cap=path_cap,
                                     expand_cap=expand_cap, algo=self._algo, occ_bits=cached[2])
             st, nexp, plen = (int(v) for v in torch.stack([r["status"][0], r["n_expanded"][0],

@@ -195,6 +195,53 @@ def test_edge_cases(engine):
     batch.astar2d_batch(occ, starts[:1], goals[:1], path_cap=64, reserve_slots=64, heap_cap=0)
 
 
+def test_explicit_heap_cap_and_overflow_retry_keep_geometry():
+    """An explicit heap_cap above the multi-query engine's limit is kept (the one-query engine is
+    reserved for it, not the limit); a batch's overflow re-run restores the geometry in force: the
+    host's reservation, or launch-sized (auto) scratch on a context the host never reserved."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import _lib, batch
+
+    L, ctx = _lib.load_library(), _lib.context()
+
+    def geometry():
+        geo = np.zeros(6, np.int32)
+        _lib.check(ctx, L.pmp_astar2d_geometry(ctx, geo.ctypes.data), "geometry")
+        return geo.tolist()
+
+    W = 70
+    occ = np.zeros((W, W), np.uint8)
+    occ[0, :] = occ[-1, :] = occ[:, 0] = occ[:, -1] = 1
+    occ[30, 5:60] = 1
+    starts = np.array([[3, 3], [60, 60], [10, 50]], np.int32)
+    goals = np.array([[65, 65], [2, 2], [50, 10]], np.int32)
+    ref = O.astar2d_batch(occ, starts, goals, path_cap=W * W + 1)
+    try:
+        _lib.check(ctx, L.pmp_astar2d_set_engine(ctx, 1, 1), "engine")  # multi-query limit 16383
+        limit = 16383
+        _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, W, 4, limit + 1000), "reserve")
+        assert geometry()[3] == limit + 1000 and geometry()[4] == 0  # kept; one-query engine
+        _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, W, 4096, 0), "reserve")
+        assert geometry()[3] == limit and geometry()[4] == 1  # the default is the limit
+        # a tiny explicit cap overflows every query; the re-run (full bound 8 W H + 8 = 39,208 > the
+        # limit) must not be cut back to the limit, and the host's geometry comes back afterwards
+        r = batch.astar2d_batch(occ, starts, goals, path_cap=W * W + 1, reserve_slots=4, heap_cap=8)
+        assert np.array_equal(r["status"].cpu().numpy(), ref["status"])
+        assert np.array_equal(r["cost"].cpu().numpy(), ref["cost"])
+        assert np.array_equal(r["n_expanded"].cpu().numpy(), ref["n_expanded"])
+        geo = geometry()
+        assert geo[:4] == [W, W, 4, 8] and geo[5] == 0
+        # a launch-sized context stays launch-sized after a re-run
+        _lib.check(ctx, L.pmp_astar2d_reserve_auto(ctx), "reserve_auto")
+        assert geometry()[0] == 0
+        r = batch.astar2d_batch(occ, starts, goals, path_cap=W * W + 1)
+        assert np.array_equal(r["cost"].cpu().numpy(), ref["cost"])
+        assert geometry()[5] == 1
+    finally:
+        _lib.check(ctx, L.pmp_astar2d_set_engine(ctx, 1, 0), "engine")
+        _lib.check(ctx, L.pmp_astar2d_reserve_auto(ctx), "reserve_auto")
+
+
 def test_unreachable_and_empty_batch(engine):
     from python_motion_planning_amd import batch
 

@@ -170,10 +170,13 @@ def _bench_json(*argv):
 
 @pytest.mark.parametrize("n", [2, 3])
 def test_bench_gpus_flag_spawns_ranks(n):
-    """`python bench.py --gpus N` (no torch.distributed.run around it) starts N ranks itself; the
-    strong-scaling deal + all_gather over those ranks reproduces the single-rank batch."""
-    out = _bench_json("--gpus", str(n), "--dry-run")
+    """`python bench.py --gpus N --scaling strong` (no torch.distributed.run around it) starts N ranks
+    itself; the strong-scaling deal + all_gather over those ranks reproduces the single-rank records
+    for every strong-scaling workload: the C2 batch, the C5 batch (BASELINE config 5: queries sharded
+    over the GPUs) and the C4 agents (config 4: sharded by agent), DWA and LQR steps."""
+    out = _bench_json("--gpus", str(n), "--dry-run", "--scaling", "strong")
     assert out["n_gpus"] == n and out["scaling"] == "strong"
+    assert out["gathered_equal"] == {"c2": True, "c5": True, "c4_dwa": True, "c4_lqr": True}
     assert out["gathered_equal_single_rank"] is True
 
 
