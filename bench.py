@@ -1416,9 +1416,18 @@ def track_leg(args, torch, dist, world, rank, kind):
             torch.cuda.synchronize()
             full = {"u": o1["u"], "n_steps": o1["n_steps"], "state": st1d, "u_p": up1}
             gathered["gathered_equal_single_rank"] = all(torch.equal(g[k], full[k]) for k in full)
+    mfma = None
     if kind == "mpc":
         # per ADMM iteration ~ 16x16 inverse matvec (512) + scans/projections (~150); assembly 2*16*16*3p (MFMA)
         flops = admm * 662.0 + stepped * 2 * 16 * 16 * 90
+        # the assembly's matrix-core work (track.hip mpc_rows): per agent-step ceil(3p / 16) row blocks
+        # x (2 MFMAs of y = S_x x + 4 K-slices x 2 MFMAs of H and g), 16 x 16 x 4 x 2 flops each
+        mfma_flops = stepped * (-(-90 // 16)) * 10 * 16 * 16 * 4 * 2.0
+        mfma_tf = mfma_flops / (kern_ms * 1e-3) / 1e12
+        mfma = {"mfma_tflops": mfma_tf, "mfma_frac_of_fp64_peak": mfma_tf / 78.6,
+                "mfma_flops_per_agent_step": (-(-90 // 16)) * 10 * 16 * 16 * 4 * 2,
+                "note": "H = S_u' Q S_u, y = S_x x, g = (S_u' Q) y on v_mfma_f64_16x16x4_f64; the ADMM runs on "
+                        "the VALU (one 16x16 inverse per agent)"}
     else:
         flops = stepped * 1200.0  # 3x3 Riccati update, 2x2 inverse, K e (lqr.py:116-141)
     achieved_tf = flops / (kern_ms * 1e-3) / 1e12
@@ -1456,7 +1465,7 @@ def track_leg(args, torch, dist, world, rank, kind):
                                                "track_kernel_lqr" if kind == "lqr" else "track_mpc_solve",
                                                "lqr" if kind == "lqr" else "mpc_qp"),
                                   "track_kernel_lqr" if kind == "lqr" else "track_mpc_solve"),
-            "timed_launches_checked": checked,
+            "timed_launches_checked": checked, "mfma": mfma,
             "detail": {"agent_steps_per_launch": stepped, "admm_iterations_per_launch": admm},
             "cpu_baseline": cpu}
 
@@ -1479,6 +1488,10 @@ def compact_leg(rec: dict) -> dict:
         out["traffic_x"] = _sig(roof["traffic"] / roof["algorithmic_bytes_per_launch"], 3)
     if rec.get("timed_launches_checked") is not None:
         out["checked"] = rec["timed_launches_checked"]
+    if roof.get("mfma_util_pct") is not None:  # rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES pass (profiles/)
+        out["mfma_util_pct"] = _sig(roof["mfma_util_pct"], 3)
+    if rec.get("mfma"):  # the matrix-core share of the leg's own arithmetic, live
+        out["mfma_tflops"] = _sig(rec["mfma"]["mfma_tflops"], 3)
     return out
 
 

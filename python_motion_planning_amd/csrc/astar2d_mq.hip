@@ -140,6 +140,7 @@ __device__ __forceinline__ void wave_sync_mem() { __builtin_amdgcn_fence(__ATOMI
 struct GHeap {
     lds_f64* F;      // LDS f[cap]
     lds_u32* C;      // LDS cm[cap]
+    lds_u32* K;      // LDS hkey[cap] (kKeys)
     lds_u32* B;      // LDS bit words: tier 0 (word 0), tier 1 (words 1..32)[, tier-2 bytes from word 36]
     uint32_t* T2;    // HBM tier-2 words (when not in LDS)
     __amdgpu_buffer_rsrc_t spill;  // the wave's spill region (4 groups)
@@ -151,10 +152,17 @@ constexpr uint32_t kOOR = 0x80000000u;  // a buffer offset beyond any spill regi
 #define PMP_MQ_SPILL_SHIFT 1
 #endif
 constexpr int kSpillShift = PMP_MQ_SPILL_SHIFT;  // empty slots in front of position cap
+// Keep each entry's h order key (hkey) beside it: an LDS array (16 B per LDS position instead of 12)
+// and the spill record's fourth word, so loaded entries need no key rebuild (A/B switch)
+#ifndef PMP_MQ_KEYS
+#define PMP_MQ_KEYS 0
+#endif
+constexpr bool kKeys = PMP_MQ_KEYS != 0;
+constexpr int kEntLds = kKeys ? 16 : 12;  // LDS bytes per heap position
 
 struct Ld {
     double fl;
-    uint32_t cl;
+    uint32_t cl, kl;
     uint4 v;
     bool in;
     __device__ __forceinline__ void issue(const GHeap& h, int p)
@@ -165,23 +173,28 @@ struct Ld {
         v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(h.spill, off, 0, 0));
         fl = h.F[pl];
         cl = h.C[pl];
+        if (kKeys) kl = h.K[pl];
     }
-    __device__ __forceinline__ void get(double& f, uint32_t& c) const
+    // the entry (f, code) and its h order key
+    template <int HEUR>
+    __device__ __forceinline__ void get(double& f, uint32_t& c, uint32_t& k) const
     {
         const uint64_t m = __ballot(in);
         const uint64_t b = (uint64_t)__double_as_longlong(fl);
         f = __hiloint2double((int)sel_lanes(m, (uint32_t)(b >> 32), v.y), (int)sel_lanes(m, (uint32_t)b, v.x));
         c = sel_lanes(m, cl, v.z);
+        k = kKeys ? sel_lanes(m, kl, v.w) : hkey<HEUR>(c);
     }
 };
-__device__ __forceinline__ void hst(const GHeap& h, bool on, int p, double f, uint32_t c)
+__device__ __forceinline__ void hst(const GHeap& h, bool on, int p, double f, uint32_t c, uint32_t k)
 {
     if (on && p < h.cap) {
         h.F[p] = f;
         h.C[p] = c;
+        if (kKeys) h.K[p] = k;
     }
     const uint64_t b = (uint64_t)__double_as_longlong(f);
-    const uint4 v = make_uint4((uint32_t)b, (uint32_t)(b >> 32), c, 0u);
+    const uint4 v = make_uint4((uint32_t)b, (uint32_t)(b >> 32), c, kKeys ? k : 0u);
     const uint32_t off = (on && p >= h.cap) ? h.sbase + (uint32_t)p * 16u : kOOR;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
                                            h.spill, off, 0, 0);
@@ -282,7 +295,7 @@ struct PopOut {
     uint32_t P;
     int K, m;
     double Af;
-    uint32_t Ac;
+    uint32_t Ac, Ak;
 };
 
 template <bool T2LDS, int HEUR>
@@ -326,25 +339,24 @@ __device__ __forceinline__ void heap_pop(const GHeap& h, const Walk& wk, int n, 
     const int si = ((pi - 1) ^ 1) + 1;
     const bool hass = on && si < n;
     double Af, Sf;
-    uint32_t Ac, Sc;
+    uint32_t Ac, Sc, Ak, Sk;
     {
         Ld la, ls;
         la.issue(h, pi);
         ls.issue(h, hass ? si : 0);
-        la.get(Af, Ac);
-        ls.get(Sf, Sc);
+        la.get<HEUR>(Af, Ac, Ak);
+        ls.get<HEUR>(Sf, Sc, Sk);
     }
     // heap[p_{i+1}] is lane i+1's load (DPP row_shl:1; lanes 1..K-1 use it, K <= 14 stays in the row)
     const double Bf = shl1f(Af);
     // ---- movers: the path prefix with !(last < heap[p_i])
-    const uint32_t Ak = hkey<HEUR>(Ac);
     const uint32_t Bk = shl1(Ak);
     const int m = __popc(rbits(on && !key_lt(lf, lk, Af, Ak), gb));
     {
         const bool l0 = gl == 0;
         const bool st = l0 || (on && gl <= m);
         const int dst = (int)(P >> (l0 ? K - m : sh + 1)) - 1;
-        hst(h, st, dst, l0 ? lf : Af, l0 ? lc : Ac);
+        hst(h, st, dst, l0 ? lf : Af, l0 ? lc : Ac, l0 ? lk : Ak);
     }
     const double a1f = bcf<1>(Af), a0f = bcf<0>(Af);
     const uint32_t a1c = bc<1>(Ac), a0c = bc<0>(Ac);
@@ -358,7 +370,7 @@ __device__ __forceinline__ void heap_pop(const GHeap& h, const Walk& wk, int n, 
     // ---- bits of p_0 .. p_{m-1}
     {
         const bool useb = gl < m;
-        const bool bit = choice_bit_k(pi, useb ? Bf : lf, useb ? Bk : lk, Sf, hkey<HEUR>(Sc));
+        const bool bit = choice_bit_k(pi, useb ? Bf : lf, useb ? Bk : lk, Sf, Sk);
         bit_set<T2LDS>(h, hass && gl <= m, gl - 1, P >> (sh + 1), bit);
     }
     po.P = P;
@@ -366,6 +378,7 @@ __device__ __forceinline__ void heap_pop(const GHeap& h, const Walk& wk, int n, 
     po.m = m;
     po.Af = Af;
     po.Ac = Ac;
+    po.Ak = Ak;
     wave_sync_mem();
 }
 
@@ -375,7 +388,7 @@ __device__ __forceinline__ void heap_pop(const GHeap& h, const Walk& wk, int n, 
 template <bool T2LDS, int HEUR>
 __device__ __forceinline__ int heap_push(const GHeap& h, int n, double itf, uint32_t itc, uint32_t itk, double& lastf,
                                          uint32_t& lastc, uint32_t& lastk, double& rootf, uint32_t& rootc, int gl, int gb, double& a1f,
-                                         uint32_t& a1c)
+                                         uint32_t& a1c, uint32_t& a1k)
 {
     const uint32_t np1 = (uint32_t)n + 1u;
     const int D = 31 - __clz((int)np1);  // depth of position n
@@ -386,25 +399,25 @@ __device__ __forceinline__ int heap_push(const GHeap& h, int n, double itf, uint
     const int sx = ((x - 1) ^ 1) + 1;
     const bool hass = on && sx < n;
     double Af, Sf;
-    uint32_t Ac, Sc;
+    uint32_t Ac, Sc, Ak, Sk;
     {
         Ld la, ls;
         la.issue(h, on ? aj : 0);
         ls.issue(h, hass ? sx : 0);
-        la.get(Af, Ac);
-        ls.get(Sf, Sc);
+        la.get<HEUR>(Af, Ac, Ak);
+        ls.get<HEUR>(Sf, Sc, Sk);
     }
-    const uint32_t Ak = hkey<HEUR>(Ac);
     const int t = __popc(rbits(on && key_lt(itf, itk, Af, Ak), gb));
     const int ipos = (int)(np1 >> t) - 1;
     const double A1f = bcf<1>(Af), A2f = bcf<2>(Af);
     const uint32_t A1c = bc<1>(Ac), A2c = bc<2>(Ac);
     a1f = t >= 2 ? A2f : itf;
     a1c = t >= 2 ? A2c : itc;
+    a1k = t >= 2 ? bc<2>(Ak) : itk;
     {
         const bool l0 = gl == 0;
         const bool st = l0 || (on && gl <= t);
-        hst(h, st, l0 ? ipos : x, l0 ? itf : Af, l0 ? itc : Ac);
+        hst(h, st, l0 ? ipos : x, l0 ? itf : Af, l0 ? itc : Ac, l0 ? itk : Ak);
     }
     if (ipos == 0) {
         rootf = itf;
@@ -415,7 +428,7 @@ __device__ __forceinline__ int heap_push(const GHeap& h, int n, double itf, uint
     lastk = t == 0 ? itk : bc<1>(Ak);
     {
         const bool usea = gl - 1 < t;
-        const bool bit = choice_bit_k(x, usea ? Af : itf, usea ? Ak : itk, Sf, hkey<HEUR>(Sc));
+        const bool bit = choice_bit_k(x, usea ? Af : itf, usea ? Ak : itk, Sf, Sk);
         bit_set<T2LDS>(h, hass && gl <= t + 1, D - l1, np1 >> l1, bit);
     }
     wave_sync_mem();
@@ -449,6 +462,7 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
         const int bits_b = T2LDS ? kBits01 + kT2LBytes : kBits01;
         hp.F = (lds_f64*)(base + bits_b);
         hp.C = (lds_u32*)(base + bits_b + (size_t)8 * lds_cap);
+        hp.K = (lds_u32*)(base + bits_b + (size_t)12 * lds_cap);
         hp.T2 = t2_all + slot * kT2Words;
         hp.spill = __builtin_amdgcn_make_buffer_rsrc(spill_all + (size_t)blockIdx.x * 4u * (size_t)spill_n, 0,
                                                      (int)(4u * (uint32_t)spill_n * 16u), 0x00020000);
@@ -536,7 +550,7 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
                     lastf = rootf;
                     lastc = rootc;
                     lastk = hkey<HEUR>(rootc);
-                    hst(hp, gl == 0, 0, rootf, rootc);
+                    hst(hp, gl == 0, 0, rootf, rootc, lastk);
                     n = 1;
                     npush = 1;
                     npop = 0;
@@ -568,7 +582,7 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
         uint32_t icm = 0u;
         bool pc_ok = false;   // lanes 0..7 hold heap[parent(n0 + lane)] (pf8, pc8)
         double pf8 = 0.0;
-        uint32_t pc8 = 0u;
+        uint32_t pc8 = 0u, pk8 = 0u;
         int n0 = 0;
         if (act && n == 0) st = PMP_NO_PATH;  // OPEN exhausted (a_star.py:83)
         if (act && n > 0) {
@@ -622,9 +636,9 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
             po.Af = 0.0;
             po.Ac = 0u;
             const double lf0 = lastf;  // the old last element, which the pop places at p_m
-            const uint32_t lc0 = lastc;
+            const uint32_t lc0 = lastc, lk0 = lastk;
             if (n > 0) heap_pop<T2LDS, HEUR>(hp, wk, n, lastf, lastc, lastk, rootf, rootc, gl, gb, po);
-            pld.get(pf8, pc8);
+            pld.get<HEUR>(pf8, pc8, pk8);
             {
                 // patch the prefetched parents: the pop moved heap[p_{L+1}] into path node p_L (L < m)
                 // and the old last element into p_m
@@ -633,10 +647,11 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
                                  (int)(po.P >> (po.K - L)) - 1 == pp;
                 const int src = gb + (L + 1 < 16 ? L + 1 : 15);
                 const double af = bpf(po.Af, src);
-                const uint32_t ac = bp(po.Ac, src);
+                const uint32_t ac = bp(po.Ac, src), ak = bp(po.Ak, src);
                 if (onp) {
                     pf8 = L < po.m ? af : lf0;
                     pc8 = L < po.m ? ac : lc0;
+                    pk8 = L < po.m ? ak : lk0;
                 }
             }
 #ifdef PMP_STAMPS
@@ -723,8 +738,8 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
                 if (pc_ok) {
                     const int pl = gb + (pos - n0 < 8 ? pos - n0 : 7);
                     const double pf = bpf(pf8, pl);
-                    const uint32_t pc = bp(pc8, pl);
-                    const bool triv = gl < 8 && mine && !key_lt(ifv, ik, pf, hkey<HEUR>(pc));
+                    const uint32_t pk = bp(pk8, pl);
+                    const bool triv = gl < 8 && mine && !key_lt(ifv, ik, pf, pk);
                     const uint32_t tm = rbits(triv, gb) & 0xFFu;
                     const uint32_t nt = pend & ~tm;
                     run = nt ? pend & ((nt & (0u - nt)) - 1u) : pend;
@@ -740,7 +755,7 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
                     const uint32_t leftk = rank == 0 ? lastk : lkp;
                     bit_set<T2LDS>(hp, inrun && (pos & 1) == 0 && pos > 0, 30 - __clz(pos + 1), (uint32_t)(pos + 1) >> 1,
                                    !key_lt(leftf, leftk, ifv, ik));
-                    hst(hp, inrun, pos, ifv, icm);
+                    hst(hp, inrun, pos, ifv, icm, ik);
                     const int top = 31 - __clz(run);
                     lastf = bpf(ifv, gb + top);
                     lastc = bp(icm, gb + top);
@@ -758,13 +773,14 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
                     const double itf = bpf(ifv, gb + m);
                     const uint32_t itc = bp(icm, gb + m);
                     double a1f;
-                    uint32_t a1c;
+                    uint32_t a1c, a1k;
                     heap_push<T2LDS, HEUR>(hp, n, itf, itc, bp(ik, gb + m), lastf, lastc, lastk, rootf, rootc, gl, gb, a1f,
-                                           a1c);
+                                           a1c, a1k);
                     // a left child's right sibling (the next position) has the same parent, now a1
                     if (pc_ok && (n & 1) && gl == n - n0 + 1) {
                         pf8 = a1f;
                         pc8 = a1c;
+                        pk8 = a1k;
                     }
                     n += 1;
                     npush++;
@@ -824,7 +840,7 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
     const int lds_cap = ctx->astar_lds_cap;
     const bool t2lds = ctx->astar_mq_t2lds != 0;
     const int bits_b = t2lds ? kBits01 + kT2LBytes : kBits01;
-    const int region = bits_b + 12 * lds_cap;
+    const int region = bits_b + kEntLds * lds_cap;
     const int cap_max = t2lds ? kMqCapT2L : kMqCap;
     const int heap_cap = ctx->astar_heap_cap < cap_max ? ctx->astar_heap_cap : cap_max;
     const int spill_n = ((heap_cap > lds_cap ? heap_cap - lds_cap : 1) + kSpillShift + 1) & ~1;
@@ -875,7 +891,7 @@ int pmp_astar2d_mq_lds_cap(int per_cu, bool t2lds)
     const int bits_b = t2lds ? kBits01 + kT2LBytes : kBits01;
     // a workgroup is one wave = 4 groups, and may hold at most the CU's 160 KiB
     int bytes = (160 * 1024) / (per_cu < 4 ? 4 : per_cu) - 160 - bits_b;
-    int cap = (bytes / 12) & ~15;
+    int cap = (bytes / kEntLds) & ~15;
     if (cap > kMqCap) cap = kMqCap & ~15;
     return cap;
 }

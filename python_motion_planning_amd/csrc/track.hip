@@ -12,10 +12,11 @@
 //  - QP assembly in closed form.  A3 = I + N with N^2 = 0 (N = column 2 of lqr/mpc's A), so
 //    A3^k = I + kN and the blocks of S_u are G_n = C A5^n B5 = sum_{k<=n} A3^k B3
 //    = (n+1) B3 + n(n+1)/2 N B3; S_x's block i is [I + (i+1)N | G_i].
-//  - H = S_u' Qbar S_u on the f64 MFMA (v_mfma_f64_16x16x4_f64), one pass per agent of the wave:
-//    lane l holds S_u[r = 4t + l/16][col = l%16] of the t-th K-slice, A = q_r * S_u, B = S_u; the 3p
-//    rows of S_u are the K dimension, so one 16x16 accumulator tile is the whole of H.
-//    g = S_u' Qbar S_x x rides along on the VALU.
+//  - H = S_u' Qbar S_u, y = S_x x and g = (S_u' Qbar) y on the f64 MFMA (v_mfma_f64_16x16x4_f64),
+//    one pass per agent of the wave: lane l holds S_u[r = 4t + l/16][col = l%16] of the t-th K-slice,
+//    A = q_r * S_u, B = S_u (H) or y (g); the 3p rows of S_u are the K dimension, so one 16x16
+//    accumulator tile is the whole of H.  y comes out of a 16-row block MFMA of S_x against x already
+//    in the B layout of the g product.
 //  - ADMM (the OSQP algorithm, unscaled), on the agent's row: lane v owns variable v and constraint
 //    rows v (the cumulative-sum rows of kron(tril(1_m), I2)) and 2m+v (the identity rows).  A x is
 //    a stride-2 prefix scan, A'y a stride-2 suffix scan (DPP row_shr / row_shl); the x-update
@@ -306,9 +307,15 @@ __device__ MpcResult mpc_rows(bool need, const MpcIn& I, double& up0, double& up
     const double p0 = up0, p1 = up1;
     const uint64_t needm = ballot(need);
 
-    // ---- H = S_u' Qbar S_u (MFMA f64 16x16x4, one pass per agent of the wave) and g = S_u' Qbar S_x x.
-    //      Lane l holds S_u[r = 4t + l/16][col = l%16] of the t-th K-slice; the agent's closed-form
-    //      parameters are broadcast from its row.
+    // ---- H = S_u' Qbar S_u + R and g = (S_u' Qbar)(S_x x) (mpc.py:181-182, the reference's association:
+    //      S_u' Q first, then times the vector S_x x - Yr, Yr = 0), all three products on the f64 MFMA
+    //      (v_mfma_f64_16x16x4_f64), one pass per agent of the wave over 16-row blocks of S_u / S_x:
+    //       - y = S_x[16 rows] x: A = the block of S_x (lane l: row l%16, column l/16, then 4 + l/16),
+    //         B = x in every column, so register t of lane l holds y[4t + l/16] -- exactly the B operand
+    //         the g product needs at the block's t-th K-slice;
+    //       - per K-slice (4 rows r = 4t + l/16): A = q_r S_u[r][l%16] (S_u' Qbar), B = S_u[r][l%16]
+    //         into the H tile, B = y into the g tile (every column of it holds g).
+    //      The agent's closed-form parameters are broadcast from its row.
     const int col = lane & 15, kq = lane >> 4;
     const int jb = col >> 1, cb = col & 1;
     const int R3 = 3 * p;
@@ -320,38 +327,68 @@ __device__ MpcResult mpc_rows(bool need, const MpcIn& I, double& up0, double& up
         const double A0 = rl_f64(a0, L0), A1 = rl_f64(a1, L0), B00 = rl_f64(b00, L0), B10 = rl_f64(b10, L0);
         const double E0 = rl_f64(e0, L0), E1 = rl_f64(e1, L0), E2 = rl_f64(e2, L0);
         const double P0 = rl_f64(p0, L0), P1 = rl_f64(p1, L0);
-        v4d acc = {0.0, 0.0, 0.0, 0.0};
-        double gp = 0.0;
+        // x = [e_x, e_y, e_theta, u_p0, u_p1] (mpc.py:128-134): row k of the B operand, k = l/16 (+ 4)
+        const double xk0 = kq == 0 ? E0 : (kq == 1 ? E1 : (kq == 2 ? E2 : P0));
+        const double xk1 = kq == 0 ? P1 : 0.0;
+        v4d acc = {0.0, 0.0, 0.0, 0.0}, accg = {0.0, 0.0, 0.0, 0.0};
 
-        for (int k0 = 0; k0 < R3; k0 += 4) {
-            const int r = k0 + kq;
-            double sv = 0.0, yv = 0.0, qv = 0.0;
-            if (r < R3) {
-                const int i = r / 3, d = r - 3 * i;
-                qv = d == 0 ? M.q[0] : (d == 1 ? M.q[1] : M.q[2]);
-                const double n1 = (double)(i + 1), tri = 0.5 * (double)i * (double)(i + 1);
-                if (d == 0)
-                    yv = ((E0 + (n1 * A0) * E2) + (n1 * B00) * P0) + (tri * A0 * dt) * P1;
-                else if (d == 1)
-                    yv = ((E1 + (n1 * A1) * E2) + (n1 * B10) * P0) + (tri * A1 * dt) * P1;
-                else
-                    yv = E2 + (n1 * dt) * P1;
-                if (col < n && jb <= i) {
-                    const int nn = i - jb;
-                    const double m1 = (double)(nn + 1), tr = 0.5 * (double)nn * (double)(nn + 1);
-                    if (cb == 0)
-                        sv = d == 0 ? m1 * B00 : (d == 1 ? m1 * B10 : 0.0);
-                    else
-                        sv = d == 0 ? tr * A0 * dt : (d == 1 ? tr * A1 * dt : m1 * dt);
+        for (int r0 = 0; r0 < R3; r0 += 16) {
+            v4d y = {0.0, 0.0, 0.0, 0.0};
+            {
+                // S_x's block i (rows 3i .. 3i + 2) = C A^(i+1) = [I + (i+1) N | G_i]:
+                //   [1, 0, (i+1) A02, (i+1) B00, i(i+1)/2 A02 dt], [0, 1, (i+1) A12, (i+1) B10, i(i+1)/2 A12 dt],
+                //   [0, 0, 1, 0, (i+1) dt]
+                const int r = r0 + col;
+                double s0 = 0.0, s1 = 0.0;  // S_x[r][kq], S_x[r][4 + kq]
+                if (r < R3) {
+                    const int i = r / 3, d = r - 3 * i;
+                    const double n1 = (double)(i + 1), tri = 0.5 * (double)i * (double)(i + 1);
+                    if (d == 0) {
+                        s0 = kq == 0 ? 1.0 : (kq == 1 ? 0.0 : (kq == 2 ? n1 * A0 : n1 * B00));
+                        s1 = kq == 0 ? (tri * A0 * dt) : 0.0;
+                    } else if (d == 1) {
+                        s0 = kq == 0 ? 0.0 : (kq == 1 ? 1.0 : (kq == 2 ? n1 * A1 : n1 * B10));
+                        s1 = kq == 0 ? (tri * A1 * dt) : 0.0;
+                    } else {
+                        s0 = kq == 2 ? 1.0 : 0.0;
+                        s1 = kq == 0 ? n1 * dt : 0.0;
+                    }
                 }
+                y = __builtin_amdgcn_mfma_f64_16x16x4f64(s0, xk0, y, 0, 0, 0);
+                y = __builtin_amdgcn_mfma_f64_16x16x4f64(s1, xk1, y, 0, 0, 0);
             }
-            const double av = qv * sv;
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, sv, acc, 0, 0, 0);
-            gp += av * yv;
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const int r = r0 + 4 * t + kq;
+                double sv = 0.0, qv = 0.0;
+                if (r < R3) {
+                    const int i = r / 3, d = r - 3 * i;
+                    qv = d == 0 ? M.q[0] : (d == 1 ? M.q[1] : M.q[2]);
+                    if (col < n && jb <= i) {
+                        const int nn = i - jb;
+                        const double m1 = (double)(nn + 1), tr = 0.5 * (double)nn * (double)(nn + 1);
+                        if (cb == 0)
+                            sv = d == 0 ? m1 * B00 : (d == 1 ? m1 * B10 : 0.0);
+                        else
+                            sv = d == 0 ? tr * A0 * dt : (d == 1 ? tr * A1 * dt : m1 * dt);
+                    }
+                }
+                const double av = qv * sv;
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, sv, acc, 0, 0, 0);
+                accg = __builtin_amdgcn_mfma_f64_16x16x4f64(av, y[t], accg, 0, 0, 0);
+            }
         }
-        gp += __shfl_xor(gp, 16);
-        gp += __shfl_xor(gp, 32);
-        if (row == j) gv = gp;
+        // g tile: register t of lane l holds g[l/16 + 4t] (every column); lane v of row j takes g[v]
+        {
+            const int src = 16 * (col & 3) + col;
+            double gg = 0.0;
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const double w = __shfl(accg[t], src);
+                if ((col >> 2) == t) gg = w;
+            }
+            if (row == j) gv = gg;
+        }
         // D layout of v_mfma_f64_16x16x4_f64: col = lane & 15, row = lane/16 + 4*reg
         double* Hs = Hs_all + 256 * j;
 #pragma unroll
