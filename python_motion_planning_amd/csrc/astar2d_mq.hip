@@ -100,6 +100,15 @@ __device__ __forceinline__ uint32_t shl1(uint32_t v)  // lane + 1 of my row (row
 {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x101, 0xF, 0xF, false);
 }
+__device__ __forceinline__ uint32_t shr1(uint32_t v)  // lane - 1 of my row (row_shr:1; lane 0 gets 0)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
+}
+__device__ __forceinline__ double shr1f(double v)
+{
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    return __longlong_as_double(((uint64_t)shr1((uint32_t)(b >> 32)) << 32) | shr1((uint32_t)b));
+}
 __device__ __forceinline__ double shl1f(double v)
 {
     const uint64_t b = (uint64_t)__double_as_longlong(v);
@@ -158,6 +167,12 @@ constexpr int kSpillShift = PMP_MQ_SPILL_SHIFT;  // empty slots in front of posi
 #define PMP_MQ_KEYS 0
 #endif
 constexpr bool kKeys = PMP_MQ_KEYS != 0;
+// The unified step (astar2d_mqu_kernel: one heap operation per group per step) or the lock-step
+// pop + push rounds (astar2d_mq_kernel)
+#ifndef PMP_MQ_UNIFIED
+#define PMP_MQ_UNIFIED 0
+#endif
+constexpr bool kMqUnified = PMP_MQ_UNIFIED != 0;
 constexpr int kEntLds = kKeys ? 16 : 12;  // LDS bytes per heap position
 
 struct Ld {
@@ -822,6 +837,475 @@ __global__ __launch_bounds__(64) void astar2d_mq_kernel(
     span_end(span);
 }
 
+// ---- the unified step (PMP_MQ_UNIFIED) ---------------------------------------------------------
+// Each step every group runs ONE heap operation: a pop (with the 3x3 round and the expansion) when
+// it has no pushes pending, else the next pending push; the leading run of trivial pushes is stored
+// first in the same step (and a group whose run empties its pushes pops in that step).  The lock-step
+// kernel above waits, after every pop, for push rounds in which the groups without pushes (61 % of
+// pops are stale) idle: 1.44 rounds per iteration, a memory round trip each.  Here a group's pop and
+// push are one path operation of the same code (path_op), so a step costs about one such operation
+// and every group advances in it.
+
+// _siftup's leaf for a heappop on a heap of n (> 0) entries: path number P (1-based) and level K
+template <bool T2LDS>
+__device__ __forceinline__ void pop_leaf(const GHeap& h, const Walk& wk, int n, int gb, uint32_t& P, int& K)
+{
+    const int D = 31 - __clz(n);
+    const int full = D - 1 < 0 ? 0 : D - 1;
+    const uint32_t w0 = h.B[0] << 1;
+    const uint32_t pr0 = wk.five(w0, gb);  // level-5 node (32..63) along the tier-0 bits
+    uint32_t w1 = 0u, w2 = 0u, pr1 = 32u, pr2 = T2LDS ? 8u : 32u;
+    if (full >= 5) {
+        w1 = h.B[pr0 - 31u] << 1;
+        pr1 = wk.five(w1, gb);
+    }
+    const uint32_t R2 = (pr0 << 5) + pr1 - 32u;  // level-10 node (1024..2047)
+    if (full >= 10) {
+        w2 = t2_load<T2LDS>(h, R2) << 1;
+        pr2 = T2LDS ? wk.three(w2, gb) : wk.five(w2, gb);
+    }
+    const int tf = full >= 10 ? 2 : (full >= 5 ? 1 : 0);
+    const int rf = full - 5 * tf;
+    const uint32_t wt = tf == 2 ? w2 : (tf == 1 ? w1 : w0);
+    const uint32_t prt = tf == 2 ? pr2 : (tf == 1 ? pr1 : pr0);
+    const uint32_t Rt = tf == 2 ? R2 : (tf == 1 ? pr0 : 1u);
+    const uint32_t prel = prt >> ((tf == 2 && T2LDS ? 3 : 5) - rf);
+    P = (Rt << rf) + prel - (1u << rf);
+    K = D - 1 < 0 ? 0 : D - 1;
+    if (2u * P <= (uint32_t)n) {
+        const uint32_t c = (2u * P < (uint32_t)n) ? ((wt >> prel) & 1u) : 0u;
+        P = 2u * P + c;
+        K++;
+    }
+}
+
+// One heap operation of a group on the path q_L = (Q >> (Kd - L)) - 1, L = 0..Kd (lane L <-> level L):
+//  pop  (heap already shrunk to n; X = the old last element; the path = _siftup's, root to leaf):
+//       the prefix of levels 1..b with !(X < heap[q_L]) moves up one level, X lands at level b;
+//  push (X = the item at position n = q_Kd; the path = its ancestors, _siftdown): the levels
+//       b..Kd-1 with X < heap[q_L] move down one level, X lands at level b.
+// One load round (lane L: heap[q_L] and its sibling; lane 15 of a pop: heap[n - 1], the new last),
+// a ballot for b, the stores, the bits of the changed levels' parents.  Returns b; lane L's new
+// heap[q_L] in (nf, nc, nk) (for the caller's cached parents).
+template <bool T2LDS, int HEUR>
+__device__ __forceinline__ int path_op(const GHeap& h, bool on, bool pop, uint32_t Q, int Kd, int n, double Xf, uint32_t Xc,
+                                       uint32_t Xk, int gl, int gb, double& lastf, uint32_t& lastc, uint32_t& lastk,
+                                       double& rootf, uint32_t& rootc, double& nf, uint32_t& nc, uint32_t& nk)
+{
+    const bool lvl = gl <= Kd;
+    const int q = lvl ? (int)(Q >> (Kd - gl)) - 1 : 0;
+    const bool lda = on && (pop ? (gl >= 1 && lvl) : gl < Kd);
+    const int ai = lda ? q : ((on && pop && gl == 15) ? n - 1 : 0);
+    const int si = ((q - 1) ^ 1) + 1;
+    const bool hass = on && gl >= 1 && lvl && si < n;
+    double Vf, Sf;
+    uint32_t Vc, Sc, Vk, Sk;
+    {
+        Ld la, ls;
+        la.issue(h, ai);
+        ls.issue(h, hass ? si : 0);
+        la.get<HEUR>(Vf, Vc, Vk);
+        ls.get<HEUR>(Sf, Sc, Sk);
+    }
+    // the boundary level b
+    const bool lt = key_lt(Xf, Xk, Vf, Vk);
+    const int cnt = __popc(rbits(lda && (pop ? !lt : lt), gb));
+    const int b = pop ? cnt : Kd - cnt;
+    // new contents: a pop shifts levels 1..b up one (lane L takes lane L+1's), a push shifts levels
+    // b..Kd-1 down one (lane L takes lane L-1's); X at level b
+    const double upf = shl1f(Vf), dnf = shr1f(Vf);
+    const uint32_t upc = shl1(Vc), upk = shl1(Vk), dnc = shr1(Vc), dnk = shr1(Vk);
+    const bool atb = gl == b, shift = pop ? gl < b : (gl > b && lvl);
+    nf = atb ? Xf : (shift ? (pop ? upf : dnf) : Vf);
+    nc = atb ? Xc : (shift ? (pop ? upc : dnc) : Vc);
+    nk = atb ? Xk : (shift ? (pop ? upk : dnk) : Vk);
+    hst(h, on && (pop ? gl <= b : (gl >= b && lvl)), q, nf, nc, nk);
+    // the bits of the changed levels' parents: lane L (>= 1) sets its parent's from its new content
+    // and its sibling's
+    {
+        const bool upd = hass && (pop ? gl <= b : gl >= b);
+        const bool bit = choice_bit_k(q, nf, nk, Sf, Sk);
+        bit_set<T2LDS>(h, upd, gl - 1, Q >> (Kd - gl + 1), bit);
+    }
+    if (on) {
+        const double r0f = bcf<0>(nf);
+        const uint32_t r0c = bc<0>(nc);
+        rootf = r0f;
+        rootc = r0c;
+        // the last element: a pop's heap[n - 1] unless X landed on it (the path's leaf, b == Kd); a
+        // push's new heap[n] (level Kd)
+        const int src = gb + (pop ? 15 : Kd);
+        const double lf = bpf(pop ? Vf : nf, src);
+        const uint32_t lc = bp(pop ? Vc : nc, src), lk = bp(pop ? Vk : nk, src);
+        if (!(pop && b == Kd && Q == (uint32_t)n)) {
+            lastf = lf;
+            lastc = lc;
+            lastk = lk;
+        }
+    }
+    wave_sync_mem();
+    return b;
+}
+
+template <int HEUR, bool GZERO, bool T2LDS>
+__global__ __launch_bounds__(64) void astar2d_mqu_kernel(
+    const uint32_t* __restrict__ occ, int W, int H, const int32_t* __restrict__ start_xy,
+    const int32_t* __restrict__ goal_xy, const int32_t* __restrict__ order, int nq, double* __restrict__ cost_out,
+    int32_t* __restrict__ path_len_out, uint32_t* __restrict__ path_out, int path_cap,
+    int32_t* __restrict__ nexp_out, uint32_t* __restrict__ expand_out, int expand_cap,
+    int64_t* __restrict__ counters, int32_t* __restrict__ status_out, int* __restrict__ queue,
+    uint4* __restrict__ spill_all, int spill_n, int heap_cap, int lds_cap, int region, uint8_t* __restrict__ cst_all,
+    size_t cst_bytes, double* __restrict__ G_all, uint32_t* __restrict__ t2_all, uint32_t* __restrict__ epoch_all,
+    int prio_n, unsigned long long* __restrict__ span)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = lane_id();
+    const int gl = lane & 15, gb = lane & 48, grp = lane >> 4;
+    const size_t slot = (size_t)blockIdx.x * 4u + (size_t)grp;
+    span_begin(span);
+    GHeap hp;
+    {
+        unsigned char* base = smem + (size_t)grp * (size_t)region;
+        hp.B = (lds_u32*)base;
+        const int bits_b = T2LDS ? kBits01 + kT2LBytes : kBits01;
+        hp.F = (lds_f64*)(base + bits_b);
+        hp.C = (lds_u32*)(base + bits_b + (size_t)8 * lds_cap);
+        hp.K = (lds_u32*)(base + bits_b + (size_t)12 * lds_cap);
+        hp.T2 = t2_all + slot * kT2Words;
+        hp.spill = __builtin_amdgcn_make_buffer_rsrc(spill_all + (size_t)blockIdx.x * 4u * (size_t)spill_n, 0,
+                                                     (int)(4u * (uint32_t)spill_n * 16u), 0x00020000);
+        hp.sbase = (uint32_t)grp * (uint32_t)spill_n * 16u + (uint32_t)(kSpillShift - lds_cap) * 16u;
+        hp.cap = lds_cap;
+    }
+    uint8_t* cst = cst_all + slot * cst_bytes;
+    double* G = G_all + slot * ((size_t)W * (size_t)H);
+
+    Walk wk;
+    wk.init(gl);
+    // per-lane constants: lane m < 8 of a row is motion m (offset, cost, isCollision's cells)
+    const int mo = gl & 7;
+    const int mx = mot_x(mo), my = mot_y(mo);
+    const double mcost = GZERO ? 0.0 : ((mo & 1) ? kSqrt2 : 1.0);
+    uint32_t need = 16u | (1u << ((mx + 1) * 3 + (my + 1)));
+    if (mo & 1) need |= (1u << (3 + (my + 1))) | (1u << ((mx + 1) * 3 + 1));
+    const uint32_t self_bit = 1u << ((mx + 1) * 3 + (my + 1));
+    // the 3x3 round: lanes 0..8 occupancy of cell (x + i/3 - 1, y + i%3 - 1); lanes 9..11 the
+    // cell-state bytes of row i - 9; lane 12 G[parent]
+    const int blk_dx = gl < 9 ? gl / 3 - 1 : (gl < 12 ? gl - 10 : 0);
+    const int blk_dy = gl < 9 ? gl % 3 - 1 : 0;
+
+    // group state (equal across the row)
+    uint32_t ep = epoch_all[slot];
+    bool need_q = true, done = false;
+    int q = 0, qi = 0, sx = 0, sy = 0, gx = 0, gy = 0;
+    int n = 0, nexp = 0, maxn = 0;
+    int64_t npush = 0, npop = 0;
+    double rootf = 0.0, lastf = 0.0;
+    uint32_t rootc = 0u, lastc = 0u, lastk = 0u;  // lastk = hkey(lastc)
+    // the pushes of the last expansion still to do (motion mask, in motion order) and their items
+    // (lane m < 8: motion m); lanes 0..7 hold heap[parent(n0 + lane)] while pc_ok
+    uint32_t pend = 0u;
+    double ifv = 0.0;
+    uint32_t icm = 0u, ikk = 0u;
+    bool pc_ok = false;
+    double pf8 = 0.0;
+    uint32_t pk8 = 0u;
+    int n0 = 0;
+
+    for (;;) {
+        // ---- groups without a query take the next one (or retire)
+        const bool fetch_any = __ballot(need_q && !done) != 0ull;
+        if (need_q && !done) {
+            int v = 0;
+            if (gl == 0) v = atomicAdd(queue, 1);
+            qi = bci<0>(v);
+            if (qi >= nq) {
+                done = true;
+            } else {
+                q = order ? order[qi] : qi;
+                sx = start_xy[2 * q];
+                sy = start_xy[2 * q + 1];
+                gx = goal_xy[2 * q];
+                gy = goal_xy[2 * q + 1];
+                const bool s_in = (unsigned)sx < (unsigned)W && (unsigned)sy < (unsigned)H;
+                const bool g_in = (unsigned)gx < (unsigned)W && (unsigned)gy < (unsigned)H;
+                if (!s_in || !g_in) {  // outside the grid: blocked -> no neighbours -> no path
+                    if (gl == 0) {
+                        status_out[q] = PMP_NO_PATH;
+                        cost_out[q] = 0.0;
+                        path_len_out[q] = 0;
+                        nexp_out[q] = s_in ? 1 : 0;
+                        if (counters) {
+                            counters[4 * q] = 1; counters[4 * q + 1] = 1;
+                            counters[4 * q + 2] = s_in ? 1 : 0; counters[4 * q + 3] = 1;
+                        }
+                    }
+                } else {
+                    // next epoch; every 15th query (and a fresh slot, epoch 0) clears the cell states
+                    if (ep == 0u || ep >= 15u) {
+                        uint4* c4 = reinterpret_cast<uint4*>(cst);
+                        const size_t n4 = cst_bytes / 16;
+                        for (size_t i = gl; i < n4; i += 16) c4[i] = make_uint4(0u, 0u, 0u, 0u);
+                        ep = 1u;
+                    } else {
+                        ep++;
+                    }
+                    // heap[0] = Node(start, start, 0, 0), key (0, h = 0)
+                    rootf = 0.0;
+                    rootc = pack_cm<HEUR>(0, 0, 8);
+                    lastf = rootf;
+                    lastc = rootc;
+                    lastk = hkey<HEUR>(rootc);
+                    hst(hp, gl == 0, 0, rootf, rootc, lastk);
+                    n = 1;
+                    npush = 1;
+                    npop = 0;
+                    nexp = 0;
+                    maxn = 1;
+                    pend = 0u;
+                    pc_ok = false;
+                    need_q = false;
+                }
+            }
+            wave_sync_mem();
+        }
+        if (fetch_any) {
+            // the longest queries (first in the longest-first order) get issue priority
+            if (__ballot(!done && !need_q && qi < prio_n)) __builtin_amdgcn_s_setprio(3);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+        if (__ballot(!done) == 0ull) break;
+        const bool act = !done && !need_q;
+
+        // ---- 1. the leading run of trivial pushes (the item is not less than its parent, so
+        //      CPython's _siftdown stops at once): stored in one step
+        if (act && pend != 0u && pc_ok) {
+            const uint32_t mine = (pend >> mo) & 1u;  // lane m < 8: my item is pending
+            const uint32_t below = pend & ((1u << mo) - 1u);
+            const int rank = __popc(below);
+            const int pos = n + rank;
+            const int pl = gb + (pos - n0 < 8 ? pos - n0 : 7);
+            const double pf = bpf(pf8, pl);
+            const uint32_t pk = bp(pk8, pl);
+            const bool triv = gl < 8 && mine && !key_lt(ifv, ikk, pf, pk);
+            const uint32_t tm = rbits(triv, gb) & 0xFFu;
+            const uint32_t nt = pend & ~tm;
+            const uint32_t run = nt ? pend & ((nt & (0u - nt)) - 1u) : pend;
+            if (run != 0u) {
+                // heap[pos] = item; a right child sets its parent's bit against its left sibling (the
+                // previous item of the run, or `last`)
+                const bool inrun = gl < 8 && ((run >> mo) & 1u);
+                const int prev = below ? 31 - __clz(below) : 0;
+                const double lfp = bpf(ifv, gb + prev);
+                const uint32_t lkp = bp(ikk, gb + prev);
+                const double leftf = rank == 0 ? lastf : lfp;
+                const uint32_t leftk = rank == 0 ? lastk : lkp;
+                bit_set<T2LDS>(hp, inrun && (pos & 1) == 0 && pos > 0, 30 - __clz(pos + 1), (uint32_t)(pos + 1) >> 1,
+                               !key_lt(leftf, leftk, ifv, ikk));
+                hst(hp, inrun, pos, ifv, icm, ikk);
+                const int top = 31 - __clz(run);
+                lastf = bpf(ifv, gb + top);
+                lastc = bp(icm, gb + top);
+                lastk = bp(ikk, gb + top);
+                const int k = __popc(run);
+                n += k;
+                npush += k;
+                pend &= ~run;
+                wave_sync_mem();
+            }
+        }
+
+        // ---- 2. this step's heap operation: the next pending push, else a pop
+        const bool push = act && pend != 0u;
+        int st = -1;  // >= 0: the query ends this step with this status
+        double goal_cost = 0.0;
+        int plen = 0;
+        if (act && !push && n == 0) st = PMP_NO_PATH;  // OPEN exhausted (a_star.py:83)
+        const bool pop = act && !push && n > 0;
+        double Xf = lastf;
+        uint32_t Xc = lastc, Xk = lastk;
+        uint32_t Q = 0u;
+        int Kd = 0;
+        int popn = 0;  // the popped node (pop): its code, and the 3x3 round's loads
+        uint32_t ncm = rootc;
+        int x = 0, y = 0;
+        uint32_t nlin = 0u;
+        uint32_t blk_w = 0u, blk_w2 = 0u;
+        int blk_sh = 0;
+        bool blk_in = false;
+        double gpar = 0.0;
+        Ld pld;
+        if (push) {
+            const int m = __ffs((int)pend) - 1;
+            Xf = bpf(ifv, gb + m);
+            Xc = bp(icm, gb + m);
+            Xk = bp(ikk, gb + m);
+            Q = (uint32_t)n + 1u;
+            Kd = 31 - __clz((int)Q);
+        }
+        if (pop) {
+            // ---- heappop (a_star.py:54), with the 3x3 round and the parent prefetch issued first
+            npop++;
+            n -= 1;
+            n0 = n;
+            popn = 1;
+            const int ndir = cm_dir(ncm);
+            x = ndir == 8 ? sx : gx - cm_dx(ncm);
+            y = ndir == 8 ? sy : gy - cm_dy(ncm);
+            nlin = (uint32_t)x * (uint32_t)H + (uint32_t)y;
+            // every lane issues all three loads (lanes that need none read index 0): no branch per
+            // lane class, so no load destination is zero-filled under another exec mask
+            {
+                const int cx = x + blk_dx, cy = y + blk_dy;
+                const bool is_occ = gl < 9, is_cst = gl >= 9 && gl < 12;
+                const bool in_occ = (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
+                const bool in_cst = (unsigned)cx < (unsigned)W;
+                const uint32_t ci = (is_occ && in_occ) ? (uint32_t)cx * (uint32_t)H + (uint32_t)cy : 0u;
+                const uint32_t lo =
+                    (is_cst && in_cst) ? (uint32_t)cx * (uint32_t)H + (uint32_t)(y > 0 ? y - 1 : 0) : 0u;
+                const uint32_t a0 = lo & ~3u;
+                const uint32_t gi =
+                    (!GZERO && gl == 12 && ndir < 8) ? nlin - (uint32_t)(mot_x(ndir) * H + mot_y(ndir)) : 0u;
+                const uint32_t ow = occ[ci >> 5];
+                const uint32_t* p32 = reinterpret_cast<const uint32_t*>(cst + a0);
+                const uint32_t c0 = p32[0], c1 = p32[1];
+                gpar = GZERO ? 0.0 : G[gi];
+                blk_in = is_occ ? in_occ : (is_cst && in_cst);
+                blk_sh = is_occ ? (int)(ci & 31u) : (int)((uint32_t)cx * (uint32_t)H + (uint32_t)y - 1u - a0);
+                blk_w = is_occ ? ow : c0;
+                blk_w2 = c1;
+            }
+            // the pushes will take positions n0, n0 + 1, ...: their parents, while all 8 share a depth
+            pc_ok = n0 > 0 && (31 - __clz(n0 + 1)) == (31 - __clz(n0 + 8));
+            if (n > 0) pop_leaf<T2LDS>(hp, wk, n, gb, Q, Kd);
+        }
+        const int pp = (n0 + (gl & 7) - 1) >> 1;  // lanes 0..7: parent of position n0 + lane
+        pld.issue(hp, pop && pc_ok && gl < 8 ? pp : 0);
+        const bool op = push || (pop && n > 0);
+        double nf = 0.0;
+        uint32_t nc = 0u, nk = 0u;
+        int b = 0;
+        b = path_op<T2LDS, HEUR>(hp, op, pop, Q, Kd, n, Xf, Xc, Xk, gl, gb, lastf, lastc, lastk, rootf, rootc, nf, nc,
+                                 nk);
+        {
+            double f8;
+            uint32_t c8, k8;
+            pld.get<HEUR>(f8, c8, k8);
+            if (pop) {
+                pf8 = f8;
+                pk8 = k8;
+            }
+        }
+        // the cached parents (lanes 0..7: heap[parent(n0 + lane)]) after the operation: a position on
+        // the path at a level the operation rewrote now holds that level's new content
+        if (op && pc_ok) {
+            const int Lp = 31 - __clz(pp + 1);
+            const bool onpath = gl < 8 && Lp <= Kd && (int)(Q >> (Kd - Lp)) - 1 == pp &&
+                                (pop ? Lp <= b : Lp >= b);
+            const int src = gb + (Lp < 16 ? Lp : 15);
+            const double af = bpf(nf, src);
+            const uint32_t ak = bp(nk, src);
+            if (onpath) {
+                pf8 = af;
+                pk8 = ak;
+            }
+        }
+        if (push) {
+            pend &= pend - 1u;
+            n += 1;
+            npush++;
+        }
+
+        // ---- 3. the popped node: 3x3 masks (bit k = cell (x + k/3 - 1, y + k%3 - 1)), CLOSED test,
+        //      goal test, getNeighbor (a_star.py:57-82)
+        if (popn) {
+            const uint32_t occ9 = rbits(gl < 9 && (!blk_in || ((blk_w >> blk_sh) & 1u)), gb) & 0x1FFu;
+            uint32_t row = 0u;
+            if (gl >= 9 && gl < 12 && blk_in) {
+                // the bytes of cells y-1, y, y+1 as bytes 0..2 of v (blk_sh = -1 when y = 0: byte 0 is
+                // then off the grid and masked below), tested together: a byte is CLOSED in this
+                // query when its high nibble is the epoch and its low nibble (motion + 1) is nonzero
+                const uint64_t win = ((uint64_t)blk_w2 << 32) | blk_w;
+                const uint32_t v = blk_sh < 0 ? (blk_w << 8) : (uint32_t)(win >> (8 * blk_sh));
+                const uint32_t lo = v & 0x0F0F0Fu, eq = ((v >> 4) & 0x0F0F0Fu) ^ (ep * 0x010101u);
+                const uint32_t m = (lo + 0x7F7F7Fu) & ~(eq + 0x7F7F7Fu) & 0x808080u;
+                row = ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u);
+                row &= (y > 0 ? 1u : 0u) | 2u | (y + 1 < H ? 4u : 0u);
+            }
+            const uint32_t cls9 = bc<9>(row) | (bc<10>(row) << 3) | (bc<11>(row) << 6);
+            const double gp = bcf<12>(gpar);
+            if (!(cls9 & 16u)) {  // node.current not in CLOSED (a_star.py:57-58)
+                const int ndir = cm_dir(ncm);
+                const double gnode = (GZERO || ndir == 8) ? 0.0 : gp + ((ndir & 1) ? kSqrt2 : 1.0);
+                // CLOSED[node.current] = node (a_star.py:82)
+                if (gl == 0) cst[nlin] = (uint8_t)((ep << 4) | (uint32_t)(ndir + 1));
+                if (!GZERO && gl == 1) G[nlin] = gnode;
+                if (gl == 2 && expand_out && nexp < expand_cap)
+                    expand_out[(size_t)q * expand_cap + nexp] = nlin | ((uint32_t)ndir << 28);
+                nexp++;
+                if (x == gx && y == gy) {  // goal (a_star.py:61-64): extractPath, goal -> start
+                    st = PMP_FOUND;
+                    wave_sync_mem();
+                    if (gl == 0) {
+                        int cx = x, cy = y;
+                        double cost = 0.0;
+                        int len = 0;
+                        uint32_t* pth = path_out + (size_t)q * path_cap;
+                        for (;;) {
+                            const uint32_t li = (uint32_t)cx * (uint32_t)H + (uint32_t)cy;
+                            if (len < path_cap) pth[len] = li;
+                            len++;
+                            if (cx == sx && cy == sy) break;
+                            const int d = (int)(cst[li] & 15u) - 1;
+                            cost += (d & 1) ? kSqrt2 : 1.0;
+                            cx -= mot_x(d);
+                            cy -= mot_y(d);
+                        }
+                        goal_cost = cost;
+                        plen = len;
+                    }
+                } else {
+                    // getNeighbor in motion order; push the goal and stop (a_star.py:66-80)
+                    const int ndx = gx - x - mx, ndy = gy - y - my;
+                    const bool nb_ok = gl < 8 && (occ9 & need) == 0u && (cls9 & self_bit) == 0u;
+                    uint32_t vm = rbits(nb_ok, gb) & 0xFFu;
+                    const uint32_t gm = rbits(nb_ok && ndx == 0 && ndy == 0, gb) & 0xFFu;
+                    if (gm) vm &= (gm << 1) - 1u;
+                    const double ig = gnode + mcost;
+                    icm = pack_cm<HEUR>(ndx, ndy, mo);
+                    ikk = hkey<HEUR>(icm);
+                    ifv = ig + h_of_key<HEUR>(ikk);
+                    if (n + __popc(vm) > heap_cap) st = PMP_CAP_OVERFLOW;  // a push would find n >= heap_cap
+                    else pend = vm;
+                }
+            }
+        }
+        if (n > maxn) maxn = n;
+
+        // ---- the groups whose query ended: results, then a new query next step
+        if (st >= 0) {
+            if (gl == 0) {
+                int s = st;
+                if (s == PMP_FOUND && plen > path_cap) s = PMP_PATH_OVERFLOW;
+                status_out[q] = s;
+                cost_out[q] = st == PMP_FOUND ? goal_cost : 0.0;
+                path_len_out[q] = st == PMP_FOUND ? plen : 0;
+                nexp_out[q] = nexp;
+                if (counters) {
+                    counters[4 * q + 0] = npush;
+                    counters[4 * q + 1] = npop;
+                    counters[4 * q + 2] = nexp;
+                    counters[4 * q + 3] = maxn;
+                }
+            }
+            pend = 0u;
+            need_q = true;
+        }
+    }
+    if (gl == 0) epoch_all[slot] = ep;
+    span_end(span);
+}
+
 size_t mq_cst_bytes(int W, int H) { return (((size_t)W * H + 8 + 255) & ~(size_t)255); }
 
 }  // namespace
@@ -863,7 +1347,7 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
     const size_t lds = (size_t)region * 4;
     const int prio = order ? ctx->astar_prio_n : 0;
 #define MQ_LAUNCH(HE, GZ, T2)                                                                                       \
-    hipLaunchKernelGGL((astar2d_mq_kernel<HE, GZ, T2>), dim3(waves), dim3(64), lds, s, occ_bits, W, H, start_xy,    \
+    hipLaunchKernelGGL((kMqUnified ? astar2d_mqu_kernel<HE, GZ, T2> : astar2d_mq_kernel<HE, GZ, T2>), dim3(waves), dim3(64), lds, s, occ_bits, W, H, start_xy,    \
                        goal_xy, order, nq, cost, path_len, path, path_cap, n_expanded, expand, expand_cap, counters, \
                        status, queue, spill, spill_n, heap_cap, lds_cap, region, cstp, cst_bytes, G, t2, ep, prio,   \
                        ctx->span)

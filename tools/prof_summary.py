@@ -42,7 +42,7 @@ KERNELS = {  # short name -> regex on the demangled kernel name
 # the 2D graph kernels' template <HEUR, GZERO, THETA> (astar2d.hip): one short name per planner, so the
 # headline's traffic is never taken from the Theta* launches of the same kernel template
 _G2D = re.compile(r"astar2d_kernel<(\d+), (true|false), (\d)(?:, (?:true|false))?>")  # 4th: LDS grid state
-_MQ = re.compile(r"astar2d_mq_kernel<(\d+), (true|false), (true|false)>")
+_MQ = re.compile(r"astar2d_mqu?_kernel<(\d+), (true|false), (true|false)>")
 
 
 def short(name):
