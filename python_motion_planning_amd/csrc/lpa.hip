@@ -5,8 +5,10 @@
 //   * U.remove(node) shifts the list tail left by one (:149, :173);
 //   * heapq.heappush(U, node) appends and sifts by LNode.__lt__ (key list compare, :32-33) on
 //     whatever order the list holds after the removes (:178).
-// So the kernel keeps the list itself, element for element: U = {cell, k1, k2} arrays in HBM plus
-// a per-cell position (`node in U` is pos >= 0).
+// So the kernel keeps the list itself, element for element: U = {cell, k1, k2} arrays in LDS (the
+// wave's share; a list that outgrows it moves to HBM arrays for the rest of its query).  `node in U`
+// and U.remove's search are a scan of the cells (a node is in U at most once: updateVertex removes
+// it before pushing it again).
 //
 // DStarLite.plan (d_star_lite.py:14-187; plan() is LPAStar's) is the same loop run backwards: the
 // node created with rhs = 0 is the goal, the search ends on the start's consistency, keys add
@@ -30,6 +32,9 @@ constexpr double kInf = __builtin_huge_val();
 __constant__ int kMX[8] = {-1, -1, 0, 1, 1, 1, 0, -1};
 __constant__ int kMY[8] = {0, 1, 1, 1, 0, -1, -1, -1};
 
+typedef __attribute__((address_space(3))) double lds_f64;
+typedef __attribute__((address_space(3))) int32_t lds_i32;
+
 struct Q {
     const uint32_t* occ;
     int W, H, heur;
@@ -37,10 +42,14 @@ struct Q {
     int gx, gy;        // tgt's coordinates
     double* g;
     double* rhs;
-    int32_t* pos;
-    int32_t* Uc;
+    int32_t* Uc;   // U in HBM (a list past the LDS share)
     double* Uk1;
     double* Uk2;
+    lds_i32* Lc;   // U in LDS
+    lds_f64* L1;
+    lds_f64* L2;
+    int cap;       // LDS entries
+    bool lds;      // U is in LDS (wave-uniform)
     int n;         // |U| (wave-uniform)
     int64_t npush;
     double km;     // D* Lite's key offset (0 in plan(), set by OnPress)
@@ -65,6 +74,34 @@ __device__ __forceinline__ double hval(const Q& S, int x, int y)
     return S.heur == 1 ? (double)(abs(dx) + abs(dy)) : __dsqrt_rn((double)(dx * dx + dy * dy));
 }
 
+// list entry k of U, wherever the list lives
+__device__ __forceinline__ int32_t u_c(const Q& S, int k) { return S.lds ? S.Lc[k] : S.Uc[k]; }
+__device__ __forceinline__ double u_k1(const Q& S, int k) { return S.lds ? S.L1[k] : S.Uk1[k]; }
+__device__ __forceinline__ double u_k2(const Q& S, int k) { return S.lds ? S.L2[k] : S.Uk2[k]; }
+__device__ __forceinline__ void u_set(const Q& S, int k, int32_t c, double a, double b)
+{
+    if (S.lds) {
+        S.Lc[k] = c;
+        S.L1[k] = a;
+        S.L2[k] = b;
+    } else {
+        S.Uc[k] = c;
+        S.Uk1[k] = a;
+        S.Uk2[k] = b;
+    }
+}
+
+// position of node v in U, or -1 (`node in U`, list.index)
+__device__ __forceinline__ int u_find(const Q& S, int32_t v, int lane)
+{
+    for (int k0 = 0; k0 < S.n; k0 += 64) {
+        const int k = k0 + lane;
+        const uint64_t m = ballot(k < S.n && u_c(S, k < S.n ? k : 0) == v);
+        if (m) return k0 + __ffsll((long long)m) - 1;
+    }
+    return -1;
+}
+
 // U.remove(U[i]): the tail moves left one slot, 64 elements per round (every lane loads before
 // any lane stores, and a round never reads what an earlier round wrote)
 __device__ void u_remove(Q& S, int i, int lane)
@@ -75,17 +112,12 @@ __device__ void u_remove(Q& S, int i, int lane)
         int32_t c = 0;
         double a = 0.0, b = 0.0;
         if (on) {
-            c = S.Uc[k + 1];
-            a = S.Uk1[k + 1];
-            b = S.Uk2[k + 1];
+            c = u_c(S, k + 1);
+            a = u_k1(S, k + 1);
+            b = u_k2(S, k + 1);
         }
         wave_sync_mem();
-        if (on) {
-            S.Uc[k] = c;
-            S.Uk1[k] = a;
-            S.Uk2[k] = b;
-            S.pos[c] = k;
-        }
+        if (on) u_set(S, k, c, a, b);
         wave_sync_mem();
     }
     S.n -= 1;
@@ -96,6 +128,15 @@ __device__ void u_remove(Q& S, int i, int lane)
 // first one that is not greater)
 __device__ void u_push(Q& S, int32_t c, double k1, double k2, int lane)
 {
+    if (S.lds && S.n + 1 > S.cap) {  // the list outgrows the LDS share: to HBM for the rest of the query
+        for (int k = lane; k < S.n; k += 64) {
+            S.Uc[k] = S.Lc[k];
+            S.Uk1[k] = S.L1[k];
+            S.Uk2[k] = S.L2[k];
+        }
+        S.lds = false;
+        wave_sync_mem();
+    }
     const uint32_t np1 = (uint32_t)S.n + 1u;
     const int D = 31 - __clz((int)np1);
     const bool on = lane >= 1 && lane <= D;
@@ -103,27 +144,15 @@ __device__ void u_push(Q& S, int32_t c, double k1, double k2, int lane)
     int32_t ac = 0;
     double a1 = 0.0, a2 = 0.0;
     if (on) {
-        ac = S.Uc[aj];
-        a1 = S.Uk1[aj];
-        a2 = S.Uk2[aj];
+        ac = u_c(S, aj);
+        a1 = u_k1(S, aj);
+        a2 = u_k2(S, aj);
     }
     const uint64_t lt = ballot(on && key_lt(k1, k2, a1, a2));
     const int t = __builtin_ctzll(~(lt >> 1));  // trailing ones from lane 1
     wave_sync_mem();
-    if (on && lane <= t) {  // ancestor j moves to ancestor j - 1 (ancestor 0 = position n)
-        const int dst = (int)(np1 >> (lane - 1)) - 1;
-        S.Uc[dst] = ac;
-        S.Uk1[dst] = a1;
-        S.Uk2[dst] = a2;
-        S.pos[ac] = dst;
-    }
-    if (lane == 0) {
-        const int dst = (int)(np1 >> t) - 1;
-        S.Uc[dst] = c;
-        S.Uk1[dst] = k1;
-        S.Uk2[dst] = k2;
-        S.pos[c] = dst;
-    }
+    if (on && lane <= t) u_set(S, (int)(np1 >> (lane - 1)) - 1, ac, a1, a2);  // ancestor j to j - 1 (0 = position n)
+    if (lane == 0) u_set(S, (int)(np1 >> t) - 1, c, k1, k2);
     wave_sync_mem();
     S.n += 1;
     S.npush += 1;
@@ -146,7 +175,7 @@ __device__ int update_vertex(Q& S, int32_t v, int lane)
     const bool oa = occ_at(S.occ, S.H, uxs, vy), ob = occ_at(S.occ, S.H, vx, uys);
     const double gu = S.g[uxs * S.H + uys];
     const double gv = S.g[v], rsrc = S.rhs[v];
-    const int p = S.pos[v];
+    const int p = u_find(S, v, lane);
     double rv;
     if (v != S.src) {
         // getNeighbor (:196-207): map lookup (KeyError off the grid), then the obstacle filter;
@@ -163,12 +192,8 @@ __device__ int update_vertex(Q& S, int32_t v, int lane)
     } else {
         rv = rsrc;
     }
-    const int pu = uni(p);  // the same word on every lane
-    if (pu >= 0) {  // `node in U`: U.remove(node)
-        if (lane == 0) S.pos[v] = -1;
-        wave_sync_mem();
-        u_remove(S, pu, lane);
-    }
+    const int pu = uni(p);
+    if (pu >= 0) u_remove(S, pu, lane);  // `node in U`: U.remove(node)
     if (gv != rv) {
         const double mn = gv < rv ? gv : rv;
         u_push(S, v, mn + hval(S, vx, vy) + S.km, mn, lane);
@@ -241,8 +266,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void lp
                                                  int32_t* __restrict__ scr_i32, int lite,
                                                  const int32_t* __restrict__ toggles, int nt,
                                                  double* __restrict__ rp_cost, int32_t* __restrict__ rp_nexp,
-                                                 int32_t* __restrict__ rp_status, uint32_t* __restrict__ occ_scr)
+                                                 int32_t* __restrict__ rp_status, uint32_t* __restrict__ occ_scr, int ucap)
 {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
     const size_t ncell = (size_t)W * (size_t)H;
     const size_t nwords = (ncell + 31) / 32;
@@ -260,8 +286,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void lp
         S.rhs = f + ncell;
         S.Uk1 = f + 2 * ncell;
         S.Uk2 = f + 3 * ncell;
-        S.pos = i;
-        S.Uc = i + ncell;
+        S.Uc = i;
+        S.L1 = (lds_f64*)smem;
+        S.L2 = (lds_f64*)(smem + (size_t)8 * ucap);
+        S.Lc = (lds_i32*)(smem + (size_t)16 * ucap);
+        S.cap = ucap;
     }
     for (;;) {
         const int q = next_query(queue, lane);
@@ -275,6 +304,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void lp
         S.gx = lite ? sx : gx;
         S.gy = lite ? sy : gy;
         S.n = 0;
+        S.lds = true;
         S.npush = 0;
         S.km = 0.0;
         if (!((unsigned)sx < (unsigned)W && (unsigned)sy < (unsigned)H && (unsigned)gx < (unsigned)W &&
@@ -284,7 +314,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void lp
             for (size_t i = lane; i < ncell; i += 64) {
                 S.g[i] = kInf;
                 S.rhs[i] = kInf;
-                S.pos[i] = -1;
             }
             if (nt > 0)
                 for (size_t i = lane; i < nwords; i += 64) occ_w[i] = occ[i];
@@ -364,8 +393,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void lp
 #pragma unroll
                     for (int u = 0; u < 2; u++) {
                         const int k = k0 + 64 * u < S.n ? k0 + 64 * u : k0;
-                        a1[u] = S.Uk1[k];
-                        a2[u] = S.Uk2[k];
+                        a1[u] = u_k1(S, k);
+                        a2[u] = u_k2(S, k);
                     }
 #pragma unroll
                     for (int u = 0; u < 2; u++)
@@ -383,7 +412,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void lp
                 bi = uni(bi);
                 b1 = __shfl(b1, 0, 64);
                 b2 = __shfl(b2, 0, 64);
-                const int32_t vt = S.Uc[bi];  // every lane the same word
+                const int32_t vt = u_c(S, bi);  // every lane the same word
                 const double gg = detached ? kInf : ggt;
                 const double gr = detached ? kInf : grt;
                 const double gm = gg < gr ? gg : gr;
@@ -391,8 +420,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void lp
                 const int32_t v = uni(vt);
                 // v's g / rhs (not touched by the list shift) load before it, on every lane
                 const double gv = S.g[v], rv = S.rhs[v];
-                if (lane == 0) S.pos[v] = -1;
-                wave_sync_mem();
                 u_remove(S, bi, lane);
                 nexp++;
                 const int vx = (int)((uint32_t)v / (uint32_t)H), vy = v - vx * H;
@@ -520,7 +547,7 @@ static int lpa_batch(int lite, pmp_ctx* ctx, void* stream, const uint32_t* occ_b
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_lpastar2d_batch / pmp_dstarlite2d_batch: null pointer argument");
     PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     const size_t ncell = (size_t)W * H;
-    const size_t per_worker = ncell * 40;  // g, rhs, U keys (f64) + pos, U cells (i32)
+    const size_t per_worker = ncell * 36;  // g, rhs, U keys (f64) + U cells (i32); U itself in LDS until it outgrows it
     // one wave per query, 24 per CU by default (the kernel is capped at 80 VGPRs for 6 waves per
     // SIMD): each query is a dependent chain of short U scans and shifts (L2-latency bound), so more
     // resident waves hide more of it (16 -> 24 per CU: LPA* 1.46 M -> 1.55 M plans/s, replanning
@@ -530,7 +557,7 @@ static int lpa_batch(int lite, pmp_ctx* ctx, void* stream, const uint32_t* occ_b
     if ((size_t)workers > max_workers) workers = (int)(max_workers > 0 ? max_workers : 1);
     if (workers > nq) workers = nq;
     double* f = (double*)pmp_scratch(ctx, SCR_AUX2, (size_t)workers * ncell * 32 + 16);
-    int32_t* i32 = (int32_t*)pmp_scratch(ctx, SCR_AUX3, (size_t)workers * ncell * 8 + 16);
+    int32_t* i32 = (int32_t*)pmp_scratch(ctx, SCR_AUX3, (size_t)workers * ncell * 4 + 16);
     int* queue = (int*)pmp_scratch(ctx, SCR_AUX0, 256);
     if (!f || !i32 || !queue) return PMP_ENOMEM;
     uint32_t* occ_scr = nullptr;
@@ -540,9 +567,13 @@ static int lpa_batch(int lite, pmp_ctx* ctx, void* stream, const uint32_t* occ_b
     }
     hipStream_t s = (hipStream_t)stream;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
-    hipLaunchKernelGGL(lpa_kernel, dim3(workers), dim3(64), 0, s, occ_bits, W, H, heuristic, start_xy, goal_xy, nq, cost,
-                       path_len, path, path_cap, n_expanded, counters, status, queue, f, i32, lite, toggles, nt,
-                       rp_cost, rp_nexp, rp_status, occ_scr);
+    // U's LDS share: the CU's 160 KiB over its resident workers, 20 B per list entry
+    const int per_cu = (workers + 255) / 256;
+    int ucap = ((160 * 1024) / (per_cu < 1 ? 1 : per_cu) / 20) & ~15;
+    if (ucap > 4096) ucap = 4096;
+    hipLaunchKernelGGL(lpa_kernel, dim3(workers), dim3(64), (size_t)ucap * 20, s, occ_bits, W, H, heuristic, start_xy,
+                       goal_xy, nq, cost, path_len, path, path_cap, n_expanded, counters, status, queue, f, i32, lite,
+                       toggles, nt, rp_cost, rp_nexp, rp_status, occ_scr, ucap);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }
