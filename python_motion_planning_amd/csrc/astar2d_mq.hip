@@ -18,6 +18,16 @@
 // and heap[n-1] (last) in registers, the pending pushes of the current expansion (a motion mask)
 // and the parents of the positions those pushes take (prefetched with the expansion).
 //
+// The step (round 4): every group runs ONE heap operation per step -- a pop (with the 3x3 round and
+// the expansion) when it has no pushes pending, else its next push -- in one code path for both
+// (path_op): CPython's heappop and heappush are both a rotation of one root-to-node path, so a step
+// costs one such operation whatever the mix.  The round-3 kernel ran every group's pop and then
+// push rounds in lock step; 61 % of pops are stale and push nothing, so its 1.44 push rounds per
+// iteration (a memory round trip each) left 64 % of the groups idle.  Alone the change was neutral
+// (12.7 k plans/s either way: fewer waits, more scalar control); with 128 VGPRs it allows four waves
+// per SIMD, and 56 queries resident per CU (128 LDS heap positions each) reach 16.4 k plans/s where
+// the lock-step kernel lost throughput past 32.
+//
 // Heap storage per group: positions < lds_cap in LDS (f64 f[], u32 cm[] as SoA), the rest in a
 // per-group HBM spill (16 B entries) read and written through one buffer descriptor per wave;
 // CPython _siftup's child-choice ("direction") bits in 5-level blocks, tiers 0-1 in LDS and tier 2
@@ -28,14 +38,6 @@
 // where the epoch (1..15) numbers the group's queries, so a new query needs no reset of the 1 MiB
 // array except every 15th query.  g of a CLOSED cell in a per-group f64 array (as astar2d.hip).
 #include "pmp_internal.h"
-
-// Diagnostic build only (make stamps): per-query cycle sums of the iteration's sections go to
-// counters[4q + 0..3] = {pop (issue to stores), expansion, push rounds, whole query} instead of the counts.
-#ifdef PMP_STAMPS
-#define MQ_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#else
-#define MQ_STAMP(v)
-#endif
 
 namespace {
 
@@ -167,12 +169,6 @@ constexpr int kSpillShift = PMP_MQ_SPILL_SHIFT;  // empty slots in front of posi
 #define PMP_MQ_KEYS 0
 #endif
 constexpr bool kKeys = PMP_MQ_KEYS != 0;
-// The unified step (astar2d_mqu_kernel: one heap operation per group per step) or the lock-step
-// pop + push rounds (astar2d_mq_kernel)
-#ifndef PMP_MQ_UNIFIED
-#define PMP_MQ_UNIFIED 0
-#endif
-constexpr bool kMqUnified = PMP_MQ_UNIFIED != 0;
 constexpr int kEntLds = kKeys ? 16 : 12;  // LDS bytes per heap position
 
 struct Ld {
@@ -270,15 +266,19 @@ __device__ __forceinline__ void bit_set(const GHeap& h, bool on, int level, uint
     const int r = level - 5 * t;
     const uint32_t mr = (1u << r) - 1u;
     const uint32_t R = Pl >> r;
-    const uint32_t m = 1u << ((Pl & mr) + mr);
+    uint32_t m = 1u << ((Pl & mr) + mr);
+    if (T2LDS) {  // every tier in LDS: one masked write at a computed word, no branch per tier
+        const uint32_t b2 = R - 1024u;
+        const uint32_t widx = t == 0 ? 0u : (t == 1 ? R - 31u : 36u + (b2 >> 2));
+        m = t == 2 ? m << (8u * (b2 & 3u)) : m;
+        if (on) ds_mskor(h.B + widx, m, bit ? m : 0u);
+        return;
+    }
     if (!on) return;
     if (t == 0) {
         ds_mskor(h.B, m, bit ? m : 0u);
     } else if (t == 1) {
         ds_mskor(h.B + (R - 31u), m, bit ? m : 0u);
-    } else if (T2LDS) {
-        const uint32_t b = R - 1024u, sh = 8u * (b & 3u);
-        ds_mskor(h.B + (36u + (b >> 2)), m << sh, bit ? (m << sh) : 0u);
     } else {
         uint32_t* w = h.T2 + (R - 1024u);
         if (bit) __hip_atomic_fetch_or(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -291,560 +291,13 @@ __device__ __forceinline__ bool choice_bit_k(int child, double vf, uint32_t vk, 
 {
     return (child & 1) ? !key_lt(vf, vk, sf, sk) : !key_lt(sf, sk, vf, vk);
 }
-template <int HEUR>
-__device__ __forceinline__ bool choice_bit(int child, double vf, uint32_t vc, double sf, uint32_t sc)
-{
-    const uint32_t vk = hkey<HEUR>(vc), sk = hkey<HEUR>(sc);
-    return (child & 1) ? !key_lt(vf, vk, sf, sk) : !key_lt(sf, sk, vf, vk);
-}
-
-// heappop on a group's heap of n (> 0, already decremented) entries whose old last element (in
-// registers) sits at position n; the old root has been taken.  Same steps as astar2d.hip
-// heap_pop, per row: the _siftup path from the bits, one load round (lane i in 1..K: heap[p_i],
-// heap[p_{i+1}], sibling(p_i); lane 0: heap[n - 1]), a popcount placing `last`, the stores and
-// the bit rewrites of p_0..p_{m-1}.
-// What a pop wrote, for values loaded before it (the parents prefetched for the expansion's pushes):
-// the leaf's path number P and level K, the mover count m (p_{i-1} <- A_i for i <= m, p_m <- last)
-// and lane i's A_i = heap[p_i] before the pop.
-struct PopOut {
-    uint32_t P;
-    int K, m;
-    double Af;
-    uint32_t Ac, Ak;
-};
-
-template <bool T2LDS, int HEUR>
-__device__ __forceinline__ void heap_pop(const GHeap& h, const Walk& wk, int n, double& lastf, uint32_t& lastc, uint32_t& lastk,
-                                         double& rootf, uint32_t& rootc, int gl, int gb, PopOut& po)
-{
-    const double lf = lastf;
-    const uint32_t lc = lastc, lk = lastk;  // lastk = hkey(lastc), kept beside it
-    // ---- the path: levels 0..D-1 are full; `full` = D - 1 unconditional steps, then the last step
-    const int D = 31 - __clz(n);
-    const int full = D - 1 < 0 ? 0 : D - 1;
-    const uint32_t w0 = h.B[0] << 1;
-    const uint32_t pr0 = wk.five(w0, gb);           // level-5 node (32..63) along the tier-0 bits
-    uint32_t w1 = 0u, w2 = 0u, pr1 = 32u, pr2 = T2LDS ? 8u : 32u;
-    if (full >= 5) {
-        w1 = h.B[pr0 - 31u] << 1;
-        pr1 = wk.five(w1, gb);
-    }
-    const uint32_t R2 = (pr0 << 5) + pr1 - 32u;     // level-10 node (1024..2047)
-    if (full >= 10) {
-        w2 = t2_load<T2LDS>(h, R2) << 1;
-        pr2 = T2LDS ? wk.three(w2, gb) : wk.five(w2, gb);
-    }
-    const int tf = full >= 10 ? 2 : (full >= 5 ? 1 : 0);
-    const int rf = full - 5 * tf;
-    const uint32_t wt = tf == 2 ? w2 : (tf == 1 ? w1 : w0);
-    const uint32_t prt = tf == 2 ? pr2 : (tf == 1 ? pr1 : pr0);
-    const uint32_t Rt = tf == 2 ? R2 : (tf == 1 ? pr0 : 1u);
-    const uint32_t prel = prt >> ((tf == 2 && T2LDS ? 3 : 5) - rf);
-    uint32_t P = (Rt << rf) + prel - (1u << rf);
-    int K = D - 1 < 0 ? 0 : D - 1;
-    if (2u * P <= (uint32_t)n) {
-        const uint32_t c = (2u * P < (uint32_t)n) ? ((wt >> prel) & 1u) : 0u;
-        P = 2u * P + c;
-        K++;
-    }
-    // ---- one load round
-    const bool on = gl >= 1 && gl <= K;
-    const int sh = on ? K - gl : 0;
-    const int pi = on ? (int)(P >> sh) - 1 : (gl == 0 ? n - 1 : 0);
-    const int si = ((pi - 1) ^ 1) + 1;
-    const bool hass = on && si < n;
-    double Af, Sf;
-    uint32_t Ac, Sc, Ak, Sk;
-    {
-        Ld la, ls;
-        la.issue(h, pi);
-        ls.issue(h, hass ? si : 0);
-        la.get<HEUR>(Af, Ac, Ak);
-        ls.get<HEUR>(Sf, Sc, Sk);
-    }
-    // heap[p_{i+1}] is lane i+1's load (DPP row_shl:1; lanes 1..K-1 use it, K <= 14 stays in the row)
-    const double Bf = shl1f(Af);
-    // ---- movers: the path prefix with !(last < heap[p_i])
-    const uint32_t Bk = shl1(Ak);
-    const int m = __popc(rbits(on && !key_lt(lf, lk, Af, Ak), gb));
-    {
-        const bool l0 = gl == 0;
-        const bool st = l0 || (on && gl <= m);
-        const int dst = (int)(P >> (l0 ? K - m : sh + 1)) - 1;
-        hst(h, st, dst, l0 ? lf : Af, l0 ? lc : Ac, l0 ? lk : Ak);
-    }
-    const double a1f = bcf<1>(Af), a0f = bcf<0>(Af);
-    const uint32_t a1c = bc<1>(Ac), a0c = bc<0>(Ac);
-    rootf = m >= 1 ? a1f : lf;
-    rootc = m >= 1 ? a1c : lc;
-    if (!(m == K && P == (uint32_t)n)) {
-        lastf = a0f;
-        lastc = a0c;
-        lastk = bc<0>(Ak);
-    }
-    // ---- bits of p_0 .. p_{m-1}
-    {
-        const bool useb = gl < m;
-        const bool bit = choice_bit_k(pi, useb ? Bf : lf, useb ? Bk : lk, Sf, Sk);
-        bit_set<T2LDS>(h, hass && gl <= m, gl - 1, P >> (sh + 1), bit);
-    }
-    po.P = P;
-    po.K = K;
-    po.m = m;
-    po.Af = Af;
-    po.Ac = Ac;
-    po.Ak = Ak;
-    wave_sync_mem();
-}
-
-// heappush (_siftdown) of `it` onto a group's heap of n entries: ancestors a_j = parent^j(n) in
-// one round (lane j), a popcount t of the ancestors that move down, the stores, the bits of
-// a_1..a_{t+1}.  Returns t; a1 = the new heap[parent(n)].
-template <bool T2LDS, int HEUR>
-__device__ __forceinline__ int heap_push(const GHeap& h, int n, double itf, uint32_t itc, uint32_t itk, double& lastf,
-                                         uint32_t& lastc, uint32_t& lastk, double& rootf, uint32_t& rootc, int gl, int gb, double& a1f,
-                                         uint32_t& a1c, uint32_t& a1k)
-{
-    const uint32_t np1 = (uint32_t)n + 1u;
-    const int D = 31 - __clz((int)np1);  // depth of position n
-    const bool on = gl >= 1 && gl <= D;
-    const int l1 = on ? gl : 1;
-    const int aj = (int)(np1 >> l1) - 1;
-    const int x = (int)(np1 >> (l1 - 1)) - 1;
-    const int sx = ((x - 1) ^ 1) + 1;
-    const bool hass = on && sx < n;
-    double Af, Sf;
-    uint32_t Ac, Sc, Ak, Sk;
-    {
-        Ld la, ls;
-        la.issue(h, on ? aj : 0);
-        ls.issue(h, hass ? sx : 0);
-        la.get<HEUR>(Af, Ac, Ak);
-        ls.get<HEUR>(Sf, Sc, Sk);
-    }
-    const int t = __popc(rbits(on && key_lt(itf, itk, Af, Ak), gb));
-    const int ipos = (int)(np1 >> t) - 1;
-    const double A1f = bcf<1>(Af), A2f = bcf<2>(Af);
-    const uint32_t A1c = bc<1>(Ac), A2c = bc<2>(Ac);
-    a1f = t >= 2 ? A2f : itf;
-    a1c = t >= 2 ? A2c : itc;
-    a1k = t >= 2 ? bc<2>(Ak) : itk;
-    {
-        const bool l0 = gl == 0;
-        const bool st = l0 || (on && gl <= t);
-        hst(h, st, l0 ? ipos : x, l0 ? itf : Af, l0 ? itc : Ac, l0 ? itk : Ak);
-    }
-    if (ipos == 0) {
-        rootf = itf;
-        rootc = itc;
-    }
-    lastf = t == 0 ? itf : A1f;
-    lastc = t == 0 ? itc : A1c;
-    lastk = t == 0 ? itk : bc<1>(Ak);
-    {
-        const bool usea = gl - 1 < t;
-        const bool bit = choice_bit_k(x, usea ? Af : itf, usea ? Ak : itk, Sf, Sk);
-        bit_set<T2LDS>(h, hass && gl <= t + 1, D - l1, np1 >> l1, bit);
-    }
-    wave_sync_mem();
-    return t;
-}
-
-// one byte per cell: (epoch << 4) | (motion + 1) for a cell CLOSED during query `epoch`
-__device__ __forceinline__ bool closed_byte(uint32_t b, uint32_t ep) { return (b >> 4) == ep && (b & 15u) != 0u; }
-
-// GZERO: GBFS (gbfs.py:73-75) -- every pushed node has g = 0, f = h.
-template <int HEUR, bool GZERO, bool T2LDS>
-__global__ __launch_bounds__(64) void astar2d_mq_kernel(
-    const uint32_t* __restrict__ occ, int W, int H, const int32_t* __restrict__ start_xy,
-    const int32_t* __restrict__ goal_xy, const int32_t* __restrict__ order, int nq, double* __restrict__ cost_out,
-    int32_t* __restrict__ path_len_out, uint32_t* __restrict__ path_out, int path_cap,
-    int32_t* __restrict__ nexp_out, uint32_t* __restrict__ expand_out, int expand_cap,
-    int64_t* __restrict__ counters, int32_t* __restrict__ status_out, int* __restrict__ queue,
-    uint4* __restrict__ spill_all, int spill_n, int heap_cap, int lds_cap, int region, uint8_t* __restrict__ cst_all,
-    size_t cst_bytes, double* __restrict__ G_all, uint32_t* __restrict__ t2_all, uint32_t* __restrict__ epoch_all,
-    int prio_n, unsigned long long* __restrict__ span)
-{
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int lane = lane_id();
-    const int gl = lane & 15, gb = lane & 48, grp = lane >> 4;
-    const size_t slot = (size_t)blockIdx.x * 4u + (size_t)grp;
-    span_begin(span);
-    GHeap hp;
-    {
-        unsigned char* base = smem + (size_t)grp * (size_t)region;
-        hp.B = (lds_u32*)base;
-        const int bits_b = T2LDS ? kBits01 + kT2LBytes : kBits01;
-        hp.F = (lds_f64*)(base + bits_b);
-        hp.C = (lds_u32*)(base + bits_b + (size_t)8 * lds_cap);
-        hp.K = (lds_u32*)(base + bits_b + (size_t)12 * lds_cap);
-        hp.T2 = t2_all + slot * kT2Words;
-        hp.spill = __builtin_amdgcn_make_buffer_rsrc(spill_all + (size_t)blockIdx.x * 4u * (size_t)spill_n, 0,
-                                                     (int)(4u * (uint32_t)spill_n * 16u), 0x00020000);
-        // sibling pairs (2k+1, 2k+2) share a 32-B aligned slot pair (one line) when the spill's first
-        // slot holds position cap - kSpillShift (cap is a multiple of 16, spill_n is even)
-        hp.sbase = (uint32_t)grp * (uint32_t)spill_n * 16u + (uint32_t)(kSpillShift - lds_cap) * 16u;
-        hp.cap = lds_cap;
-    }
-    uint8_t* cst = cst_all + slot * cst_bytes;
-    double* G = G_all + slot * ((size_t)W * (size_t)H);
-
-    Walk wk;
-    wk.init(gl);
-    // per-lane constants: lane m < 8 of a row is motion m (offset, cost, isCollision's cells)
-    const int mo = gl & 7;
-    const int mx = mot_x(mo), my = mot_y(mo);
-    const double mcost = GZERO ? 0.0 : ((mo & 1) ? kSqrt2 : 1.0);
-    uint32_t need = 16u | (1u << ((mx + 1) * 3 + (my + 1)));
-    if (mo & 1) need |= (1u << (3 + (my + 1))) | (1u << ((mx + 1) * 3 + 1));
-    const uint32_t self_bit = 1u << ((mx + 1) * 3 + (my + 1));
-    // the 3x3 round: lanes 0..8 occupancy of cell (x + i/3 - 1, y + i%3 - 1); lanes 9..11 the
-    // cell-state bytes of row i - 9; lane 12 G[parent]
-    const int blk_dx = gl < 9 ? gl / 3 - 1 : (gl < 12 ? gl - 10 : 0);
-    const int blk_dy = gl < 9 ? gl % 3 - 1 : 0;
-
-    // group state (equal across the row)
-    uint32_t ep = epoch_all[slot];
-    bool need_q = true, done = false;
-    int q = 0, qi = 0, sx = 0, sy = 0, gx = 0, gy = 0;
-    int n = 0, nexp = 0, maxn = 0;
-    int64_t npush = 0, npop = 0;
-#ifdef PMP_STAMPS
-    uint64_t cy_pop = 0, cy_exp = 0, cy_push = 0, cy_q0 = 0;
-#endif
-    double rootf = 0.0, lastf = 0.0;
-    uint32_t rootc = 0u, lastc = 0u, lastk = 0u;  // lastk = hkey(lastc)
-
-    // One iteration: every group with a query pops once (a_star.py:54) and expands the node
-    // (a_star.py:57-82); then rounds of pushes (a_star.py:76-80) run until every group has pushed the
-    // whole expansion: per round, the leading run of "trivial" pushes (the item is not less than its
-    // parent, so CPython's _siftdown stops at once: 73 % of C2's pushes) is stored in one step, then
-    // the next item, which moves, is pushed by the full sift.  The parents of the positions the
-    // pushes take are loaded before the pop (with the 3x3 round) and patched with what the pop wrote.
-    for (;;) {
-        // ---- groups without a query take the next one (or retire)
-        const bool fetch_any = __ballot(need_q && !done) != 0ull;
-        if (need_q && !done) {
-            int v = 0;
-            if (gl == 0) v = atomicAdd(queue, 1);
-            qi = bci<0>(v);
-            if (qi >= nq) {
-                done = true;
-            } else {
-                q = order ? order[qi] : qi;
-                sx = start_xy[2 * q];
-                sy = start_xy[2 * q + 1];
-                gx = goal_xy[2 * q];
-                gy = goal_xy[2 * q + 1];
-                const bool s_in = (unsigned)sx < (unsigned)W && (unsigned)sy < (unsigned)H;
-                const bool g_in = (unsigned)gx < (unsigned)W && (unsigned)gy < (unsigned)H;
-                if (!s_in || !g_in) {  // outside the grid: blocked -> no neighbours -> no path
-                    if (gl == 0) {
-                        status_out[q] = PMP_NO_PATH;
-                        cost_out[q] = 0.0;
-                        path_len_out[q] = 0;
-                        nexp_out[q] = s_in ? 1 : 0;
-                        if (counters) {
-                            counters[4 * q] = 1; counters[4 * q + 1] = 1;
-                            counters[4 * q + 2] = s_in ? 1 : 0; counters[4 * q + 3] = 1;
-                        }
-                    }
-                } else {
-                    // next epoch; every 15th query (and a fresh slot, epoch 0) clears the cell states
-                    if (ep == 0u || ep >= 15u) {
-                        uint4* c4 = reinterpret_cast<uint4*>(cst);
-                        const size_t n4 = cst_bytes / 16;
-                        for (size_t i = gl; i < n4; i += 16) c4[i] = make_uint4(0u, 0u, 0u, 0u);
-                        ep = 1u;
-                    } else {
-                        ep++;
-                    }
-                    // heap[0] = Node(start, start, 0, 0), key (0, h = 0)
-                    rootf = 0.0;
-                    rootc = pack_cm<HEUR>(0, 0, 8);
-                    lastf = rootf;
-                    lastc = rootc;
-                    lastk = hkey<HEUR>(rootc);
-                    hst(hp, gl == 0, 0, rootf, rootc, lastk);
-                    n = 1;
-                    npush = 1;
-                    npop = 0;
-#ifdef PMP_STAMPS
-                    cy_pop = cy_exp = cy_push = 0;
-                    cy_q0 = __builtin_amdgcn_s_memtime();
-#endif
-                    nexp = 0;
-                    maxn = 1;
-                    need_q = false;
-                }
-            }
-            wave_sync_mem();
-        }
-        if (fetch_any) {
-            // the longest queries (first in the longest-first order) get issue priority
-            if (__ballot(!done && !need_q && qi < prio_n)) __builtin_amdgcn_s_setprio(3);
-            else __builtin_amdgcn_s_setprio(0);
-        }
-        if (__ballot(!done) == 0ull) break;
-        const bool act = !done && !need_q;
-        MQ_STAMP(t0);
-
-        int st = -1;  // >= 0: the query ends this iteration with this status
-        double goal_cost = 0.0;
-        int plen = 0;
-        uint32_t pend = 0u;   // the expansion's pushes still to do (motion mask, in motion order)
-        double ifv = 0.0;     // lane m < 8: the item of motion m (f, code)
-        uint32_t icm = 0u;
-        bool pc_ok = false;   // lanes 0..7 hold heap[parent(n0 + lane)] (pf8, pc8)
-        double pf8 = 0.0;
-        uint32_t pc8 = 0u, pk8 = 0u;
-        int n0 = 0;
-        if (act && n == 0) st = PMP_NO_PATH;  // OPEN exhausted (a_star.py:83)
-        if (act && n > 0) {
-            // ---- heappop (a_star.py:54), with the 3x3 round and the parent prefetch issued first
-            const uint32_t ncm = rootc;
-            npop++;
-            n -= 1;
-            n0 = n;
-            const int ndir = cm_dir(ncm);
-            const int x = ndir == 8 ? sx : gx - cm_dx(ncm);
-            const int y = ndir == 8 ? sy : gy - cm_dy(ncm);
-            const uint32_t nlin = (uint32_t)x * (uint32_t)H + (uint32_t)y;
-            // Every lane issues all three loads (lanes that need none read index 0): no branch per lane
-            // class, so no load destination is zero-filled under another exec mask -- that WAW on a
-            // register with a load in flight made the compiler wait for each load in turn (three
-            // serialised HBM round trips per pop before the heap's own load round).
-            uint32_t blk_w, blk_w2;
-            int blk_sh;
-            bool blk_in;
-            double gpar;
-            {
-                const int cx = x + blk_dx, cy = y + blk_dy;
-                const bool is_occ = gl < 9, is_cst = gl >= 9 && gl < 12;
-                const bool in_occ = (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
-                const bool in_cst = (unsigned)cx < (unsigned)W;
-                const uint32_t ci = (is_occ && in_occ) ? (uint32_t)cx * (uint32_t)H + (uint32_t)cy : 0u;
-                // cell-state lanes: bytes of (cx, y-1 .. y+1) inside the 8-byte window at a0 (4-aligned)
-                const uint32_t lo =
-                    (is_cst && in_cst) ? (uint32_t)cx * (uint32_t)H + (uint32_t)(y > 0 ? y - 1 : 0) : 0u;
-                const uint32_t a0 = lo & ~3u;
-                const uint32_t gi =
-                    (!GZERO && gl == 12 && ndir < 8) ? nlin - (uint32_t)(mot_x(ndir) * H + mot_y(ndir)) : 0u;
-                const uint32_t ow = occ[ci >> 5];
-                const uint32_t* p32 = reinterpret_cast<const uint32_t*>(cst + a0);
-                const uint32_t c0 = p32[0], c1 = p32[1];
-                gpar = GZERO ? 0.0 : G[gi];
-                blk_in = is_occ ? in_occ : (is_cst && in_cst);
-                blk_sh = is_occ ? (int)(ci & 31u) : (int)((uint32_t)cx * (uint32_t)H + (uint32_t)y - 1u - a0);  // cst: byte of cell y-1 (may be -1)
-                blk_w = is_occ ? ow : c0;
-                blk_w2 = c1;
-            }
-            // the pushes take positions n0, n0 + 1, ...: their parents, while all 8 share a depth
-            pc_ok = n0 > 0 && (31 - __clz(n0 + 1)) == (31 - __clz(n0 + 8));
-            const int pp = (n0 + (gl & 7) - 1) >> 1;
-            Ld pld;
-            pld.issue(hp, pc_ok && gl < 8 ? pp : 0);
-            PopOut po;
-            po.K = -1;
-            po.m = -1;
-            po.P = 0u;
-            po.Af = 0.0;
-            po.Ac = 0u;
-            const double lf0 = lastf;  // the old last element, which the pop places at p_m
-            const uint32_t lc0 = lastc, lk0 = lastk;
-            if (n > 0) heap_pop<T2LDS, HEUR>(hp, wk, n, lastf, lastc, lastk, rootf, rootc, gl, gb, po);
-            pld.get<HEUR>(pf8, pc8, pk8);
-            {
-                // patch the prefetched parents: the pop moved heap[p_{L+1}] into path node p_L (L < m)
-                // and the old last element into p_m
-                const int L = 31 - __clz(pp + 1);
-                const bool onp = pc_ok && gl < 8 && po.K >= 0 && L >= 0 && L <= po.m &&
-                                 (int)(po.P >> (po.K - L)) - 1 == pp;
-                const int src = gb + (L + 1 < 16 ? L + 1 : 15);
-                const double af = bpf(po.Af, src);
-                const uint32_t ac = bp(po.Ac, src), ak = bp(po.Ak, src);
-                if (onp) {
-                    pf8 = L < po.m ? af : lf0;
-                    pc8 = L < po.m ? ac : lc0;
-                    pk8 = L < po.m ? ak : lk0;
-                }
-            }
-#ifdef PMP_STAMPS
-            {
-                const uint64_t t1 = __builtin_amdgcn_s_memtime();
-                cy_pop += t1 - t0;
-            }
-#endif
-            // ---- 3x3 masks: bit k = cell (x + k/3 - 1, y + k%3 - 1)
-            const uint32_t occ9 = rbits(gl < 9 && (!blk_in || ((blk_w >> blk_sh) & 1u)), gb) & 0x1FFu;
-            uint32_t row = 0u;
-            if (gl >= 9 && gl < 12 && blk_in) {
-                // the bytes of cells y-1, y, y+1 as bytes 0..2 of v (blk_sh = -1 when y = 0: byte 0 is
-                // then off the grid and masked below), tested together: a byte is CLOSED in this
-                // query when its high nibble is the epoch and its low nibble (motion + 1) is nonzero
-                const uint64_t win = ((uint64_t)blk_w2 << 32) | blk_w;
-                const uint32_t v = blk_sh < 0 ? (blk_w << 8) : (uint32_t)(win >> (8 * blk_sh));
-                const uint32_t lo = v & 0x0F0F0Fu, eq = ((v >> 4) & 0x0F0F0Fu) ^ (ep * 0x010101u);
-                const uint32_t m = (lo + 0x7F7F7Fu) & ~(eq + 0x7F7F7Fu) & 0x808080u;
-                row = ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u);
-                row &= (y > 0 ? 1u : 0u) | 2u | (y + 1 < H ? 4u : 0u);
-            }
-            const uint32_t cls9 = bc<9>(row) | (bc<10>(row) << 3) | (bc<11>(row) << 6);
-            const double gp = bcf<12>(gpar);
-            if (!(cls9 & 16u)) {  // node.current not in CLOSED (a_star.py:57-58)
-                const double gnode = (GZERO || ndir == 8) ? 0.0 : gp + ((ndir & 1) ? kSqrt2 : 1.0);
-                // CLOSED[node.current] = node (a_star.py:82)
-                if (gl == 0) cst[nlin] = (uint8_t)((ep << 4) | (uint32_t)(ndir + 1));
-                if (!GZERO && gl == 1) G[nlin] = gnode;
-                if (gl == 2 && expand_out && nexp < expand_cap)
-                    expand_out[(size_t)q * expand_cap + nexp] = nlin | ((uint32_t)ndir << 28);
-                nexp++;
-                if (x == gx && y == gy) {  // goal (a_star.py:61-64): extractPath, goal -> start
-                    st = PMP_FOUND;
-                    wave_sync_mem();
-                    if (gl == 0) {
-                        int cx = x, cy = y;
-                        double cost = 0.0;
-                        int len = 0;
-                        uint32_t* pth = path_out + (size_t)q * path_cap;
-                        for (;;) {
-                            const uint32_t li = (uint32_t)cx * (uint32_t)H + (uint32_t)cy;
-                            if (len < path_cap) pth[len] = li;
-                            len++;
-                            if (cx == sx && cy == sy) break;
-                            const int d = (int)(cst[li] & 15u) - 1;
-                            cost += (d & 1) ? kSqrt2 : 1.0;
-                            cx -= mot_x(d);
-                            cy -= mot_y(d);
-                        }
-                        goal_cost = cost;
-                        plen = len;
-                    }
-                } else {
-                    // getNeighbor in motion order; push the goal and stop (a_star.py:66-80)
-                    const int ndx = gx - x - mx, ndy = gy - y - my;
-                    const bool nb_ok = gl < 8 && (occ9 & need) == 0u && (cls9 & self_bit) == 0u;
-                    uint32_t vm = rbits(nb_ok, gb) & 0xFFu;
-                    const uint32_t gm = rbits(nb_ok && ndx == 0 && ndy == 0, gb) & 0xFFu;
-                    if (gm) vm &= (gm << 1) - 1u;
-                    const double ig = gnode + mcost;
-                    icm = pack_cm<HEUR>(ndx, ndy, mo);
-                    ifv = ig + h_of_key<HEUR>(hkey<HEUR>(icm));
-                    if (n + __popc(vm) > heap_cap) st = PMP_CAP_OVERFLOW;  // a push would find n >= heap_cap
-                    else pend = vm;
-                }
-            }
-        }
-
-        MQ_STAMP(t2);
-#ifdef PMP_STAMPS
-        if (act && n0 >= 0) cy_exp += t2 - t0;
-#endif
-        // ---- push rounds (a_star.py:76-80) until every group has pushed its expansion
-        while (__ballot(pend != 0u) != 0ull) {
-            if (pend != 0u) {
-                const uint32_t mine = (pend >> mo) & 1u;  // lane m < 8: my item is pending
-                const uint32_t below = pend & ((1u << mo) - 1u);
-                const int rank = __popc(below);
-                const int pos = n + rank;
-                const uint32_t ik = hkey<HEUR>(icm);
-                // the leading run of trivial pushes (needs the parents; a small heap has none cached)
-                uint32_t run = 0u;
-                if (pc_ok) {
-                    const int pl = gb + (pos - n0 < 8 ? pos - n0 : 7);
-                    const double pf = bpf(pf8, pl);
-                    const uint32_t pk = bp(pk8, pl);
-                    const bool triv = gl < 8 && mine && !key_lt(ifv, ik, pf, pk);
-                    const uint32_t tm = rbits(triv, gb) & 0xFFu;
-                    const uint32_t nt = pend & ~tm;
-                    run = nt ? pend & ((nt & (0u - nt)) - 1u) : pend;
-                }
-                if (run != 0u) {
-                    // store the run: heap[pos] = item; a right child sets its parent's bit against its
-                    // left sibling (the previous item of the run, or `last`)
-                    const bool inrun = gl < 8 && ((run >> mo) & 1u);
-                    const int prev = below ? 31 - __clz(below) : 0;
-                    const double lfp = bpf(ifv, gb + prev);
-                    const uint32_t lkp = bp(ik, gb + prev);
-                    const double leftf = rank == 0 ? lastf : lfp;
-                    const uint32_t leftk = rank == 0 ? lastk : lkp;
-                    bit_set<T2LDS>(hp, inrun && (pos & 1) == 0 && pos > 0, 30 - __clz(pos + 1), (uint32_t)(pos + 1) >> 1,
-                                   !key_lt(leftf, leftk, ifv, ik));
-                    hst(hp, inrun, pos, ifv, icm, ik);
-                    const int top = 31 - __clz(run);
-                    lastf = bpf(ifv, gb + top);
-                    lastc = bp(icm, gb + top);
-                    lastk = bp(ik, gb + top);
-                    const int k = __popc(run);
-                    n += k;
-                    npush += k;
-                    pend &= ~run;
-                    wave_sync_mem();
-                }
-                if (pend != 0u) {
-                    // the first remaining item moves up: the full _siftdown
-                    const int m = __ffs((int)pend) - 1;
-                    pend &= pend - 1u;
-                    const double itf = bpf(ifv, gb + m);
-                    const uint32_t itc = bp(icm, gb + m);
-                    double a1f;
-                    uint32_t a1c, a1k;
-                    heap_push<T2LDS, HEUR>(hp, n, itf, itc, bp(ik, gb + m), lastf, lastc, lastk, rootf, rootc, gl, gb, a1f,
-                                           a1c, a1k);
-                    // a left child's right sibling (the next position) has the same parent, now a1
-                    if (pc_ok && (n & 1) && gl == n - n0 + 1) {
-                        pf8 = a1f;
-                        pc8 = a1c;
-                        pk8 = a1k;
-                    }
-                    n += 1;
-                    npush++;
-                }
-            }
-        }
-        if (n > maxn) maxn = n;
-#ifdef PMP_STAMPS
-        if (act) cy_push += __builtin_amdgcn_s_memtime() - t2;
-#endif
-
-        // ---- the groups whose query ended: results, then a new query next iteration
-        if (st >= 0) {
-            if (gl == 0) {
-                int s = st;
-                if (s == PMP_FOUND && plen > path_cap) s = PMP_PATH_OVERFLOW;
-                status_out[q] = s;
-                cost_out[q] = st == PMP_FOUND ? goal_cost : 0.0;
-                path_len_out[q] = st == PMP_FOUND ? plen : 0;
-                nexp_out[q] = nexp;
-                if (counters) {
-#ifdef PMP_STAMPS
-                    counters[4 * q + 0] = (int64_t)cy_pop;
-                    counters[4 * q + 1] = (int64_t)(cy_exp - cy_pop);
-                    counters[4 * q + 2] = (int64_t)cy_push;
-                    counters[4 * q + 3] = (int64_t)(__builtin_amdgcn_s_memtime() - cy_q0);
-#else
-                    counters[4 * q + 0] = npush;
-                    counters[4 * q + 1] = npop;
-                    counters[4 * q + 2] = nexp;
-                    counters[4 * q + 3] = maxn;
-#endif
-                }
-            }
-            need_q = true;
-        }
-    }
-    if (gl == 0) epoch_all[slot] = ep;
-    span_end(span);
-}
-
-// ---- the unified step (PMP_MQ_UNIFIED) ---------------------------------------------------------
+// ---- the step ---------------------------------------------------------------------------------
 // Each step every group runs ONE heap operation: a pop (with the 3x3 round and the expansion) when
 // it has no pushes pending, else the next pending push; the leading run of trivial pushes is stored
-// first in the same step (and a group whose run empties its pushes pops in that step).  The lock-step
-// kernel above waits, after every pop, for push rounds in which the groups without pushes (61 % of
-// pops are stale) idle: 1.44 rounds per iteration, a memory round trip each.  Here a group's pop and
-// push are one path operation of the same code (path_op), so a step costs about one such operation
-// and every group advances in it.
+// first in the same step (and a group whose run empties its pushes pops in that step).  A group's
+// pop and push are one path operation of the same code (path_op), so a step costs about one such
+// operation and every group advances in it (tests/test_heap_path_form.py checks the path form
+// against Lib/heapq).
 
 // _siftup's leaf for a heappop on a heap of n (> 0) entries: path number P (1-based) and level K
 template <bool T2LDS>
@@ -948,7 +401,8 @@ __device__ __forceinline__ int path_op(const GHeap& h, bool on, bool pop, uint32
 }
 
 template <int HEUR, bool GZERO, bool T2LDS>
-__global__ __launch_bounds__(64) void astar2d_mqu_kernel(
+// <= 128 VGPRs: four waves per SIMD, up to 64 queries resident per CU
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void astar2d_mqu_kernel(
     const uint32_t* __restrict__ occ, int W, int H, const int32_t* __restrict__ start_xy,
     const int32_t* __restrict__ goal_xy, const int32_t* __restrict__ order, int nq, double* __restrict__ cost_out,
     int32_t* __restrict__ path_len_out, uint32_t* __restrict__ path_out, int path_cap,
@@ -1347,7 +801,7 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
     const size_t lds = (size_t)region * 4;
     const int prio = order ? ctx->astar_prio_n : 0;
 #define MQ_LAUNCH(HE, GZ, T2)                                                                                       \
-    hipLaunchKernelGGL((kMqUnified ? astar2d_mqu_kernel<HE, GZ, T2> : astar2d_mq_kernel<HE, GZ, T2>), dim3(waves), dim3(64), lds, s, occ_bits, W, H, start_xy,    \
+    hipLaunchKernelGGL((astar2d_mqu_kernel<HE, GZ, T2>), dim3(waves), dim3(64), lds, s, occ_bits, W, H, start_xy,    \
                        goal_xy, order, nq, cost, path_len, path, path_cap, n_expanded, expand, expand_cap, counters, \
                        status, queue, spill, spill_n, heap_cap, lds_cap, region, cstp, cst_bytes, G, t2, ep, prio,   \
                        ctx->span)
