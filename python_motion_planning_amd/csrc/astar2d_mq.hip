@@ -156,6 +156,8 @@ struct GHeap {
     uint32_t* T2;    // HBM tier-2 words (when not in LDS)
     __amdgpu_buffer_rsrc_t spill;  // the wave's spill region (4 groups)
     uint32_t sbase;  // byte offset of heap position 0 in the spill region (mod 2^32): positions >= cap are spilled
+    uint32_t gbase;  // kBlocks: this group's byte offset in the wave's spill region
+    int L0;          // kBlocks: level of position cap (the first level with spilled positions)
     int cap;
 };
 constexpr uint32_t kOOR = 0x80000000u;  // a buffer offset beyond any spill region: loads 0, stores dropped
@@ -170,6 +172,31 @@ constexpr int kSpillShift = PMP_MQ_SPILL_SHIFT;  // empty slots in front of posi
 #endif
 constexpr bool kKeys = PMP_MQ_KEYS != 0;
 constexpr int kEntLds = kKeys ? 16 : 12;  // LDS bytes per heap position
+// Spill layout: two-level blocks (default): from level L0 (position cap's level) down, bands of two
+// levels; the block of a node Q at the level above a band holds Q's two children and four
+// grandchildren (6 x 16 B in one 128-B line), so a path and its siblings touch one line per two
+// spilled levels instead of one per level (round 4, same-box A/B: 15.5 k -> 16.6-17.1 k plans/s,
+// FETCH -18 %, WRITE -14 %).  PMP_MQ_BLOCKS=0: position order, sibling pairs 32-B aligned.
+#ifndef PMP_MQ_BLOCKS
+#define PMP_MQ_BLOCKS 1
+#endif
+constexpr bool kBlocks = PMP_MQ_BLOCKS != 0;
+
+// byte offset of spilled heap position p (>= cap) in the wave's spill region
+__device__ __forceinline__ uint32_t spill_off(const GHeap& h, int p)
+{
+    if (!kBlocks) return h.sbase + (uint32_t)p * 16u;
+    const uint32_t u = (uint32_t)p + 1u;
+    const int lam = (31 - __clz((int)u)) - h.L0;  // level below L0 (>= 0 for a spilled position)
+    const int o = lam & 1, b = lam >> 1;
+    const uint32_t Q = u >> (o + 1);  // 1-based index of the block's node at the level above the band
+    // blocks before band b: 2^(L0-1) (4^b - 1) / 3; band b's first node index 2^(L0+2b-1):
+    // blk = Q - 2^(L0-1) (2 4^b + 1) / 3, and (2 4^b + 1) / 3 = 1, 3, 11, 43, 171 for b = 0..4
+    const uint32_t kb = (uint32_t)(0xAB2B0B0301ull >> (8 * b)) & 0xFFu;
+    const uint32_t blk = Q - (kb << (h.L0 - 1));
+    const uint32_t slot = (u & ((2u << o) - 1u)) + 2u * (uint32_t)o;
+    return h.gbase + blk * 128u + slot * 16u;
+}
 
 struct Ld {
     double fl;
@@ -180,7 +207,7 @@ struct Ld {
     {
         in = p < h.cap;
         const int pl = in ? p : 0;
-        const uint32_t off = in ? kOOR : h.sbase + (uint32_t)p * 16u;
+        const uint32_t off = in ? kOOR : spill_off(h, p);
         v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(h.spill, off, 0, 0));
         fl = h.F[pl];
         cl = h.C[pl];
@@ -206,7 +233,7 @@ __device__ __forceinline__ void hst(const GHeap& h, bool on, int p, double f, ui
     }
     const uint64_t b = (uint64_t)__double_as_longlong(f);
     const uint4 v = make_uint4((uint32_t)b, (uint32_t)(b >> 32), c, kKeys ? k : 0u);
-    const uint32_t off = (on && p >= h.cap) ? h.sbase + (uint32_t)p * 16u : kOOR;
+    const uint32_t off = (on && p >= h.cap) ? spill_off(h, p) : kOOR;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
                                            h.spill, off, 0, 0);
 }
@@ -380,21 +407,21 @@ __device__ __forceinline__ int path_op(const GHeap& h, bool on, bool pop, uint32
         const bool bit = choice_bit_k(q, nf, nk, Sf, Sk);
         bit_set<T2LDS>(h, upd, gl - 1, Q >> (Kd - gl + 1), bit);
     }
-    if (on) {
+    {
+        // selects, not a branch (every lane computes them): root = level 0's new content; the last
+        // element: a pop's heap[n - 1] unless X landed on it (the path's leaf, b == Kd); a push's new
+        // heap[n] (level Kd)
         const double r0f = bcf<0>(nf);
         const uint32_t r0c = bc<0>(nc);
-        rootf = r0f;
-        rootc = r0c;
-        // the last element: a pop's heap[n - 1] unless X landed on it (the path's leaf, b == Kd); a
-        // push's new heap[n] (level Kd)
         const int src = gb + (pop ? 15 : Kd);
         const double lf = bpf(pop ? Vf : nf, src);
         const uint32_t lc = bp(pop ? Vc : nc, src), lk = bp(pop ? Vk : nk, src);
-        if (!(pop && b == Kd && Q == (uint32_t)n)) {
-            lastf = lf;
-            lastc = lc;
-            lastk = lk;
-        }
+        const bool setl = on && !(pop && b == Kd && Q == (uint32_t)n);
+        rootf = on ? r0f : rootf;
+        rootc = on ? r0c : rootc;
+        lastf = setl ? lf : lastf;
+        lastc = setl ? lc : lastc;
+        lastk = setl ? lk : lastk;
     }
     wave_sync_mem();
     return b;
@@ -429,6 +456,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void as
         hp.spill = __builtin_amdgcn_make_buffer_rsrc(spill_all + (size_t)blockIdx.x * 4u * (size_t)spill_n, 0,
                                                      (int)(4u * (uint32_t)spill_n * 16u), 0x00020000);
         hp.sbase = (uint32_t)grp * (uint32_t)spill_n * 16u + (uint32_t)(kSpillShift - lds_cap) * 16u;
+        hp.gbase = (uint32_t)grp * (uint32_t)spill_n * 16u;
+        hp.L0 = 31 - __clz(lds_cap + 1);
         hp.cap = lds_cap;
     }
     uint8_t* cst = cst_all + slot * cst_bytes;
@@ -645,10 +674,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void as
             double f8;
             uint32_t c8, k8;
             pld.get<HEUR>(f8, c8, k8);
-            if (pop) {
-                pf8 = f8;
-                pk8 = k8;
-            }
+            pf8 = pop ? f8 : pf8;
+            pk8 = pop ? k8 : pk8;
         }
         // the cached parents (lanes 0..7: heap[parent(n0 + lane)]) after the operation: a position on
         // the path at a level the operation rewrote now holds that level's new content
@@ -659,16 +686,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void as
             const int src = gb + (Lp < 16 ? Lp : 15);
             const double af = bpf(nf, src);
             const uint32_t ak = bp(nk, src);
-            if (onpath) {
-                pf8 = af;
-                pk8 = ak;
-            }
+            pf8 = onpath ? af : pf8;
+            pk8 = onpath ? ak : pk8;
         }
-        if (push) {
-            pend &= pend - 1u;
-            n += 1;
-            npush++;
-        }
+        pend = push ? pend & (pend - 1u) : pend;
+        n += push ? 1 : 0;
+        npush += push ? 1 : 0;
 
         // ---- 3. the popped node: 3x3 masks (bit k = cell (x + k/3 - 1, y + k%3 - 1)), CLOSED test,
         //      goal test, getNeighbor (a_star.py:57-82)
@@ -781,7 +804,14 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
     const int region = bits_b + kEntLds * lds_cap;
     const int cap_max = t2lds ? kMqCapT2L : kMqCap;
     const int heap_cap = ctx->astar_heap_cap < cap_max ? ctx->astar_heap_cap : cap_max;
-    const int spill_n = ((heap_cap > lds_cap ? heap_cap - lds_cap : 1) + kSpillShift + 1) & ~1;
+    int spill_n = ((heap_cap > lds_cap ? heap_cap - lds_cap : 1) + kSpillShift + 1) & ~1;
+    if (kBlocks) {  // 16-B units of the group's blocks: bands of two levels from L0 to the deepest level
+        const int L0 = 31 - __builtin_clz((unsigned)lds_cap + 1u);
+        const int Lmax = 31 - __builtin_clz((unsigned)(heap_cap > 1 ? heap_cap : 2));
+        const int B = Lmax >= L0 ? (Lmax - L0) / 2 + 1 : 1;
+        const size_t blocks = ((size_t)1 << (L0 - 1)) * ((((size_t)1 << (2 * B)) - 1) / 3);
+        spill_n = (int)(blocks * 8);
+    }
     const size_t cst_bytes = mq_cst_bytes(W, H);
     const size_t ncell = (size_t)W * H;
     const size_t slots = (size_t)waves * 4;
