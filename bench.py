@@ -1718,14 +1718,14 @@ def main():
                     help="no GPU: exercise the rank launcher, the strong-scaling deal and the result all_gather "
                          "over gloo with the CPU oracle standing in for the kernels (tests/test_multirank.py)")
     args = ap.parse_args()
-    # engine defaults: engine 1 (multi-query, one heap operation per group per step) -- 14,336 groups
-    # in flight, 56 per CU = 3.5 waves per SIMD (round 4 sweep, same box: 32 / 40 / 48 / 56 / 64 per
-    # CU: 12.7 k / 13.7 k / 15.9 k / 16.4 k / 13.9 k plans/s; 64 leaves 96 LDS heap positions);
-    # engine 0 -- 768 waves, 18 per CU (round 2)
+    # engine defaults: engine 1 (multi-query, one heap operation per group per step, two-level spill
+    # blocks) -- 15,360 groups in flight, 60 per CU = 3.75 waves per SIMD (round 4, same box,
+    # alternating, three rounds: 56 / 60 / 64 per CU 17.38-17.41 k / 17.70-17.82 k / 16.69-18.06 k
+    # plans/s; before the block layout 56 was best); engine 0 -- 768 waves, 18 per CU (round 2)
     if not args.workers:
-        args.workers = 14336 if args.engine else 768
+        args.workers = 15360 if args.engine else 768
     if not args.residency:
-        args.residency = 56 if args.engine else 18
+        args.residency = 60 if args.engine else 18
     if not args.batches_per_launch and args.engine == 0:
         args.batches_per_launch = 1
 

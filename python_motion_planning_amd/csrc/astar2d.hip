@@ -1105,6 +1105,7 @@ static int astar2d_reserve_impl(pmp_ctx* ctx, int W, int H, int workers, int hea
     // explicit one, or the full bound of an overflow re-run) is kept and, above that limit, reserves
     // the one-query-per-wave engine instead
     ctx->astar_heap_cap_wave = heap_cap;  // small batches on a multi-query reservation (pmp_graph2d_batch)
+    ctx->astar_cap_explicit = dflt ? 0 : 1;
     if (ctx->astar_engine >= 1 && dflt && heap_cap > mq_cap) heap_cap = mq_cap;
     if (ctx->astar_engine >= 1 && heap_cap <= mq_cap) {
         // workers = queries in flight (16-lane groups, 4 per wave); scratch is taken at launch
@@ -1185,10 +1186,10 @@ extern "C" int pmp_astar2d_reserve_auto(pmp_ctx* ctx)
 extern "C" int pmp_astar2d_set_engine(pmp_ctx* ctx, int engine, int t2_lds)
 {
     if (!ctx) return PMP_EINVAL;
-    if (engine < 0 || engine > 2)
+    if (engine < 0 || engine > 3)
         return pmp_set_err(ctx, PMP_EINVAL,
                            "pmp_astar2d_set_engine: engine must be 0 (one query per wave), 1 (multi-query for large "
-                           "batches) or 2 (multi-query always)");
+                           "batches, single-query for small ones), 2 (multi-query always) or 3 (single-query always)");
     ctx->astar_engine = engine;
     ctx->astar_mq_t2lds = t2_lds ? 1 : 0;
     if (ctx->astar_W == 0) return PMP_OK;
@@ -1211,6 +1212,9 @@ namespace {
 // fewer queries than the chip has waves, a query's own latency sets the launch time, and a wave
 // serves one query faster than a quarter of one.
 constexpr int kMqMinBatch = 1024;
+// Batches up to this size run on the single-query engine (one query per workgroup with a CU's LDS)
+// when it holds the heap: fewer queries than CUs, so each query's latency is the launch time.
+constexpr int kSqMaxBatch = 256;
 // The LDSG variant needs at least this many heap positions in LDS beside the grid block.
 constexpr int kLdsgMinHeap = 64;
 }  // namespace
@@ -1278,6 +1282,17 @@ extern "C" int pmp_graph2d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
             ldsg = true;
             lds_cap = cap_g > heap_cap ? (heap_cap + 15) & ~15 : (int)cap_g;
         }
+    }
+    if (!theta && (ctx->astar_engine == 3 || (ctx->astar_engine == 1 && nq <= kSqMaxBatch))) {
+        // the single-query engine, when its LDS holds the heap capacity asked for (the default
+        // capacity is cut to what it holds: a query that outgrows it reports PMP_CAP_OVERFLOW and the
+        // host re-runs it with the full bound, which lands on this file's engine)
+        const int sq_cap = pmp_astar2d_sq_cap(W, H);
+        const int want = ctx->astar_reserved_mq ? ctx->astar_heap_cap_wave : ctx->astar_heap_cap;
+        if (sq_cap > 0 && (!ctx->astar_cap_explicit || want <= sq_cap))
+            return pmp_astar2d_sq_launch(ctx, (hipStream_t)stream, algo, occ_bits, W, H, heuristic, start_xy, goal_xy, nq,
+                                         want < sq_cap ? want : sq_cap, cost, path_len, path, path_cap, n_expanded,
+                                         expand, expand_cap, counters, status);
     }
     if (!theta && ctx->astar_reserved_mq && (ctx->astar_engine == 2 || (!ldsg && nq >= kMqMinBatch))) {
         const int groups = ctx->astar_workers < nq ? ctx->astar_workers : nq;

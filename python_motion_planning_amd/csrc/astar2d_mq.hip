@@ -47,6 +47,7 @@ constexpr int kMqCapT2L = 16383;                // positions 0..16382: levels 0.
 constexpr int kBits01 = 144;                    // LDS bytes of bit tiers 0-1 (33 words) per group
 constexpr int kT2Words = 1024;                  // HBM tier-2 bit blocks (levels 10-14) per group
 constexpr int kT2LBytes = 1024;                 // LDS tier-2 bit blocks (levels 10-12, 7 bits each) per group
+constexpr int kMqLoneMax = 256;                 // batches up to this size: one query per wave (lone)
 
 // motions in the order of env.py:52-55: (-1,0),(-1,1),(0,1),(1,1),(1,0),(1,-1),(0,-1),(-1,-1)
 constexpr uint32_t kMx1 = 0x1A90u, kMy1 = 0x01A9u;
@@ -437,7 +438,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void as
     int64_t* __restrict__ counters, int32_t* __restrict__ status_out, int* __restrict__ queue,
     uint4* __restrict__ spill_all, int spill_n, int heap_cap, int lds_cap, int region, uint8_t* __restrict__ cst_all,
     size_t cst_bytes, double* __restrict__ G_all, uint32_t* __restrict__ t2_all, uint32_t* __restrict__ epoch_all,
-    int prio_n, unsigned long long* __restrict__ span)
+    int prio_n, int lone, unsigned long long* __restrict__ span)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
@@ -446,7 +447,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void as
     span_begin(span);
     GHeap hp;
     {
-        unsigned char* base = smem + (size_t)grp * (size_t)region;
+        // lone: group 0 alone, with the wave's whole LDS (the other groups retire at once and alias it)
+        unsigned char* base = smem + (lone ? (size_t)0 : (size_t)grp * (size_t)region);
         hp.B = (lds_u32*)base;
         const int bits_b = T2LDS ? kBits01 + kT2LBytes : kBits01;
         hp.F = (lds_f64*)(base + bits_b);
@@ -479,7 +481,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void as
 
     // group state (equal across the row)
     uint32_t ep = epoch_all[slot];
-    bool need_q = true, done = false;
+    bool need_q = true, done = lone && grp != 0;
     int q = 0, qi = 0, sx = 0, sy = 0, gx = 0, gy = 0;
     int n = 0, nexp = 0, maxn = 0;
     int64_t npush = 0, npop = 0;
@@ -787,6 +789,30 @@ size_t mq_cst_bytes(int W, int H) { return (((size_t)W * H + 8 + 255) & ~(size_t
 
 }  // namespace
 
+// Per-slot query state shared by the multi-query and the single-query engines: cell-state bytes
+// ((epoch << 4) | motion + 1), G, and the slot's epoch.  Any launch may use any slot under the epoch
+// protocol; a new layout (more slots, another grid size) resets every epoch, so each slot clears its
+// cell states at its first query.
+int pmp_astar2d_slot_scratch(pmp_ctx* ctx, hipStream_t s, size_t slots, int W, int H, uint8_t** cst, size_t* cst_bytes,
+                             double** G, uint32_t** ep)
+{
+    const size_t cb = mq_cst_bytes(W, H);
+    const size_t ncell = (size_t)W * H;
+    *cst = (uint8_t*)pmp_scratch(ctx, SCR_MQ_CST, slots * cb + 16);
+    *G = (double*)pmp_scratch(ctx, SCR_MQ_G, slots * ncell * 8 + 16);
+    const bool fresh_epochs = ctx->cap[SCR_MQ_EPOCH] < slots * 4 || ctx->astar_mq_epoch_slots < slots ||
+                              ctx->astar_mq_cst_bytes != cb;
+    *ep = (uint32_t*)pmp_scratch(ctx, SCR_MQ_EPOCH, slots * 4 + 16);
+    if (!*cst || !*G || !*ep) return PMP_ENOMEM;
+    if (fresh_epochs) {
+        PMP_HIP_CHECK(ctx, hipMemsetAsync(*ep, 0, slots * 4 + 16, s));
+        ctx->astar_mq_epoch_slots = slots;
+        ctx->astar_mq_cst_bytes = cb;
+    }
+    *cst_bytes = cb;
+    return PMP_OK;
+}
+
 // The multi-query engine's launch (called by pmp_graph2d_batch for A* / Dijkstra / GBFS when the
 // context's heap capacity fits kMqCap).  ctx->astar_workers = group slots (queries in flight) of
 // one launch; the LDS share per group comes from the residency (groups per CU over all launches in
@@ -797,13 +823,20 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
                           int expand_cap, int64_t* counters, int32_t* status, int* queue)
 {
     const int groups = ctx->astar_workers < nq ? ctx->astar_workers : nq;
-    const int waves = (groups + 3) / 4;
-    const int lds_cap = ctx->astar_lds_cap;
     const bool t2lds = ctx->astar_mq_t2lds != 0;
     const int bits_b = t2lds ? kBits01 + kT2LBytes : kBits01;
-    const int region = bits_b + kEntLds * lds_cap;
     const int cap_max = t2lds ? kMqCapT2L : kMqCap;
     const int heap_cap = ctx->astar_heap_cap < cap_max ? ctx->astar_heap_cap : cap_max;
+    // lone: fewer queries than CUs -- one query per wave, in group 0, with the CU's whole LDS as its
+    // heap share (the drop-in single query: latency, not throughput)
+    const bool lone = nq <= kMqLoneMax;
+    const int waves = lone ? nq : (groups + 3) / 4;
+    int lds_cap = ctx->astar_lds_cap;
+    if (lone) {
+        lds_cap = ((160 * 1024 - 256 - bits_b) / kEntLds) & ~15;
+        if (lds_cap > heap_cap) lds_cap = (heap_cap + 15) & ~15;
+    }
+    const int region = bits_b + kEntLds * lds_cap;
     int spill_n = ((heap_cap > lds_cap ? heap_cap - lds_cap : 1) + kSpillShift + 1) & ~1;
     if (kBlocks) {  // 16-B units of the group's blocks: bands of two levels from L0 to the deepest level
         const int L0 = 31 - __builtin_clz((unsigned)lds_cap + 1u);
@@ -812,29 +845,25 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
         const size_t blocks = ((size_t)1 << (L0 - 1)) * ((((size_t)1 << (2 * B)) - 1) / 3);
         spill_n = (int)(blocks * 8);
     }
-    const size_t cst_bytes = mq_cst_bytes(W, H);
-    const size_t ncell = (size_t)W * H;
     const size_t slots = (size_t)waves * 4;
     uint4* spill = (uint4*)pmp_scratch(ctx, SCR_MQ_SPILL, slots * (size_t)spill_n * 16 + 16);
-    uint8_t* cstp = (uint8_t*)pmp_scratch(ctx, SCR_MQ_CST, slots * cst_bytes + 16);
-    double* G = (double*)pmp_scratch(ctx, SCR_MQ_G, slots * ncell * 8 + 16);
     uint32_t* t2 = (uint32_t*)pmp_scratch(ctx, SCR_MQ_T2, slots * kT2Words * 4 + 16);
-    const bool fresh_epochs = ctx->cap[SCR_MQ_EPOCH] < slots * 4 || ctx->astar_mq_epoch_slots < slots ||
-                              ctx->astar_mq_cst_bytes != cst_bytes;
-    uint32_t* ep = (uint32_t*)pmp_scratch(ctx, SCR_MQ_EPOCH, slots * 4 + 16);
-    if (!spill || !cstp || !G || !t2 || !ep) return PMP_ENOMEM;
-    if (fresh_epochs) {  // new or re-laid-out cell-state arrays: every slot clears at its first query
-        PMP_HIP_CHECK(ctx, hipMemsetAsync(ep, 0, slots * 4 + 16, s));
-        ctx->astar_mq_epoch_slots = slots;
-        ctx->astar_mq_cst_bytes = cst_bytes;
+    if (!spill || !t2) return PMP_ENOMEM;
+    uint8_t* cstp;
+    size_t cst_bytes;
+    double* G;
+    uint32_t* ep;
+    {
+        const int rc = pmp_astar2d_slot_scratch(ctx, s, slots, W, H, &cstp, &cst_bytes, &G, &ep);
+        if (rc) return rc;
     }
-    const size_t lds = (size_t)region * 4;
+    const size_t lds = (size_t)region * (lone ? 1 : 4);
     const int prio = order ? ctx->astar_prio_n : 0;
 #define MQ_LAUNCH(HE, GZ, T2)                                                                                       \
     hipLaunchKernelGGL((astar2d_mqu_kernel<HE, GZ, T2>), dim3(waves), dim3(64), lds, s, occ_bits, W, H, start_xy,    \
                        goal_xy, order, nq, cost, path_len, path, path_cap, n_expanded, expand, expand_cap, counters, \
                        status, queue, spill, spill_n, heap_cap, lds_cap, region, cstp, cst_bytes, G, t2, ep, prio,   \
-                       ctx->span)
+                       lone ? 1 : 0, ctx->span)
     const int he = algo == PMP_ALGO_DIJKSTRA ? 2 : heuristic;
     const bool gz = algo == PMP_ALGO_GBFS;
     if (t2lds) {

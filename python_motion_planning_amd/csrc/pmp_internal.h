@@ -25,12 +25,14 @@ struct pmp_ctx {
     // (0 = this launch's own workers per CU; pmp_set_resident_per_cu)
     int resident_per_cu = 0;
     // A* 2D engine: 2 = several queries per wave (astar2d_mq.hip) for A* / Dijkstra / GBFS whose heaps fit
-    // its capacity, 1 = that for large batches on large grids, 0 = one query per wave (astar2d.hip)
-    // always (pmp_astar2d_set_engine); the multi-query engine's tier-2
+    // its capacity, 1 = that for large batches on large grids and the single-query engine
+    // (astar2d_sq.hip) for batches of at most 256, 3 = the single-query engine whenever it holds the
+    // heap, 0 = one query per wave (astar2d.hip) always (pmp_astar2d_set_engine); the multi-query engine's tier-2
     // direction bits in LDS (1) or HBM (0); the geometry its per-slot epochs were written for
     int astar_engine = 1;
     int astar_mq_t2lds = 0;
     int astar_heap_cap_wave = 0;  // heap capacity of one-query-per-wave launches on a multi-query reservation
+    int astar_cap_explicit = 0;   // the reservation's heap capacity was asked for (not the default)
     int astar_reserved_mq = 0;  // the current reservation (pmp_astar2d_reserve) is the multi-query engine's
     int astar_auto = 0;         // ... and was made by a launch (not the host): it grows with the batches
     size_t astar_mq_epoch_slots = 0, astar_mq_cst_bytes = 0;
@@ -72,6 +74,15 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
                           int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded, uint32_t* expand,
                           int expand_cap, int64_t* counters, int32_t* status, int* queue);
 int pmp_astar2d_mq_lds_cap(int per_cu, bool t2lds);
+int pmp_astar2d_slot_scratch(pmp_ctx* ctx, hipStream_t s, size_t slots, int W, int H, uint8_t** cst, size_t* cst_bytes,
+                             double** G, uint32_t** ep);
+// The single-query A* 2D engine (astar2d_sq.hip): one query per workgroup, the CU's LDS its heap.
+// Returns the heap capacity it can hold for this grid (0: not this engine's grid) / launches.
+int pmp_astar2d_sq_cap(int W, int H);
+int pmp_astar2d_sq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t* occ_bits, int W, int H, int heuristic,
+                          const int32_t* start_xy, const int32_t* goal_xy, int nq, int heap_cap, double* cost,
+                          int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded, uint32_t* expand,
+                          int expand_cap, int64_t* counters, int32_t* status);
 int pmp_astar2d_mq_cap(bool t2lds);
 
 #define PMP_HIP_CHECK(ctx, call)                                                                     \

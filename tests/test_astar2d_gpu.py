@@ -18,12 +18,13 @@ def _pmp():
 
 
 # (engine, tier-2 bits in LDS): 2 = four queries per wave (astar2d_mq.hip) for every batch, 0 = one
-# query per wave (astar2d.hip; grid state in LDS on small grids), 1 = the default choice between them
+# query per wave (astar2d.hip; grid state in LDS on small grids), 3 = one query per workgroup with the
+# heap in LDS and its choice bits in registers (astar2d_sq.hip), 1 = the default choice between them
 # by batch and grid size; all must give the reference's answers bit for bit
-ENGINES = [(2, 0), (2, 1), (0, 0), (1, 0)]
+ENGINES = [(2, 0), (2, 1), (0, 0), (3, 0), (1, 0)]
 
 
-@pytest.fixture(params=ENGINES, ids=["mq", "mq_t2lds", "wave", "auto"])
+@pytest.fixture(params=ENGINES, ids=["mq", "mq_t2lds", "wave", "sq", "auto"])
 def engine(request):
     from python_motion_planning_amd import _lib
 

@@ -1,7 +1,7 @@
 """Dev probe: one A* 2D launch on the C2 workload, timed, for engine A/B and PMC passes.
 ENGINE=1|0 (multi-query / one query per wave), T2LDS=0|1, WORKERS (queries in flight), RESIDENCY
 (per CU; 0 = the launch's own), MODE=batch (4096 queries) | longest (the longest C2 query alone) |
-longest4 (the 4 longest, one wave on engine 1).  Prints the launch time and the ops count."""
+longest4 (the 4 longest, one wave on engine 1) | c2med (one median C2 query) | c1.  Prints the launch time and the ops count."""
 import os
 import sys
 import time
@@ -25,6 +25,9 @@ if mode == "c1":
     idx = np.zeros(1, np.int64)
 elif mode == "longest":
     idx = np.argsort(-ref[:, 2])[:1]
+elif mode == "c2med":  # a C2 query of median start-goal distance (the bench's latency row picks likewise)
+    from python_motion_planning_amd import shard
+    idx = np.argsort(shard.octile(s, g))[2048:2049]
 elif mode == "longest4":
     idx = np.argsort(-ref[:, 2])[:4]
 else:
