@@ -173,6 +173,31 @@ __device__ __forceinline__ void sq_bits(SqHeap& h, const SqLane& c, uint32_t Q, 
     }
 }
 
+// Set the choice bit of one node (1-based u, wave-uniform) -- a trivial push's parent
+__device__ __forceinline__ void sq_bit1(SqHeap& h, uint32_t u, uint32_t bit)
+{
+    const int l = 31 - __clz((int)u);
+    if (l <= 5) {
+        h.t0 = lane_id() == (int)u ? bit : h.t0;
+    } else if (l <= 11) {
+        const int r = l - 6;
+        const int j = (int)(u >> r) - 64;
+        const uint32_t k = (1u << r) | (u & ((1u << r) - 1u));
+        const uint64_t w = rl64(h.w1, j);
+        h.w1 = wl64(h.w1, (w & ~(1ull << k)) | ((uint64_t)bit << k), j);
+    } else {
+        const int j = (int)(u >> 6) - 64;
+        const uint32_t i = u & 63u;
+        const uint64_t w = rl64(h.w2, j);
+        h.w2 = wl64(h.w2, (w & ~(1ull << i)) | ((uint64_t)bit << i), j);
+    }
+}
+__device__ __forceinline__ double uni_f64(double v)
+{
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    return __longlong_as_double(((uint64_t)(uint32_t)uni((int)(b >> 32)) << 32) | (uint32_t)uni((int)(uint32_t)b));
+}
+
 // One heap operation on the path q_L = (Q >> (Kd - L)) - 1 (lane L <-> level L, row 0):
 //  pop  (heap already shrunk to n; X = the old last element): the prefix of levels 1..b with
 //       !(X < heap[q_L]) moves up one level, X lands at level b; lane 15 loads the new last;
@@ -194,6 +219,7 @@ __device__ __forceinline__ void sq_op(SqHeap& h, const SqLane& c, uint32_t Q, in
     const uint32_t Vc = h.C[ai];
     const double Sf = h.F[hass ? si : 0];
     const uint32_t Sc = h.C[hass ? si : 0];
+    __builtin_amdgcn_sched_barrier(0);  // all four loads in flight before the first use
     const uint32_t Vk = hkey<HEUR>(Vc);
     // the boundary level b
     const bool lt = key_lt(Xf, Xk, Vf, Vk);
@@ -461,9 +487,26 @@ __global__ __launch_bounds__(64) void astar2d_sq_kernel(
             vm &= vm - 1ull;
             const double Xf = rl_f64(ifv, m);
             const uint32_t Xc = rl_u32(icm, m);
-            const uint32_t Q = (uint32_t)n + 1u;
-            const int Kd = 31 - __clz((int)Q);
-            sq_op<false, HEUR>(hp, c, Q, Kd, n, Xf, Xc, rootf, rootc, lastf, lastc);
+            // CPython's _siftdown stops at once when the item is not less than its parent (most
+            // pushes): store it, and set its parent's bit against its left sibling (= last)
+            const int pp = n > 0 ? (n - 1) >> 1 : 0;
+            const double pf = uni_f64(hp.F[pp]);
+            const uint32_t pc = (uint32_t)uni((int)hp.C[pp]);
+            const uint32_t Xk = hkey<HEUR>(Xc);
+            if (n > 0 && !key_lt(Xf, Xk, pf, hkey<HEUR>(pc))) {
+                if (lane == 0) {
+                    hp.F[n] = Xf;
+                    hp.C[n] = Xc;
+                }
+                if ((n & 1) == 0) sq_bit1(hp, (uint32_t)pp + 1u, !key_lt(lastf, hkey<HEUR>(lastc), Xf, Xk) ? 1u : 0u);
+                lastf = Xf;
+                lastc = Xc;
+                wave_sync_mem();
+            } else {
+                const uint32_t Q = (uint32_t)n + 1u;
+                const int Kd = 31 - __clz((int)Q);
+                sq_op<false, HEUR>(hp, c, Q, Kd, n, Xf, Xc, rootf, rootc, lastf, lastc);
+            }
             n++;
             npush++;
         }

@@ -131,8 +131,27 @@ class SqHeap:
         else:
             self.last = new[Kd]
 
+    # ---- sq_bit1: one node's bit (a trivial push's parent)
+    def bit1(self, u, bit):
+        lv = u.bit_length() - 1
+        if lv <= 5:
+            self.t0[u] = bit
+        elif lv <= 11:
+            r = lv - 6
+            j, k = (u >> r) - 64, (1 << r) | (u & ((1 << r) - 1))
+            self.w1[j] = (self.w1[j] & ~(1 << k)) | (bit << k)
+        else:
+            j, i = (u >> 6) - 64, u & 63
+            self.w2[j] = (self.w2[j] & ~(1 << i)) | (bit << i)
+
     def push(self, x):
         n = len(self.a)
+        if n > 0 and not lt(x, self.a[(n - 1) >> 1]):  # the kernel's trivial-push path
+            self.a.append(x)
+            if n % 2 == 0:
+                self.bit1(((n - 1) >> 1) + 1, int(not lt(self.last, x)))
+            self.last = x
+            return
         Q = n + 1
         self.op(False, Q, Q.bit_length() - 1, n, x)
 

@@ -11,7 +11,7 @@ VO=$R/build/var_$NAME
 mkdir -p $VO
 make -s -C $C -j8
 objs=()
-for f in pmp_ctx astar2d astar2d_mq astar3d dwa track rrt dstar dstar3d lpa lpa3d totp3d; do
+for f in pmp_ctx astar2d astar2d_mq astar2d_sq astar3d dwa track rrt dstar dstar3d lpa lpa3d totp3d; do
   hit=0
   for s in "$@"; do [ "$s" = "$f.hip" ] && hit=1; done
   if [ $hit = 1 ]; then
