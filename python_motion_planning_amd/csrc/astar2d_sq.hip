@@ -482,6 +482,50 @@ __global__ __launch_bounds__(64) void astar2d_sq_kernel(
             st = PMP_CAP_OVERFLOW;
             break;
         }
+        // The leading run of trivial pushes (CPython's _siftdown stops at once: the item is not less
+        // than its parent, a position < n the run does not change) is stored together: the parents
+        // of the positions n, n + 1, ... load in one LDS round
+        if (vm && n > 0) {
+            const uint32_t below = (uint32_t)vm & ((1u << mo) - 1u);
+            const int pos = n + __popc(below);
+            const int pp = (pos - 1) >> 1;
+            const bool mine = lane < 8 && ((vm >> mo) & 1ull);
+            const double pf = hp.F[mine ? pp : 0];
+            const uint32_t pc = hp.C[mine ? pp : 0];
+            const uint32_t ik = hkey<HEUR>(icm);
+            const bool triv = mine && pp < n && !key_lt(ifv, ik, pf, hkey<HEUR>(pc));
+            const uint64_t nt = vm & ~(__ballot(triv) & 0xFFull);
+            const uint64_t run = nt ? vm & ((nt & (0ull - nt)) - 1ull) : vm;
+            if (run) {
+                const bool inrun = lane < 8 && ((run >> mo) & 1ull);
+                if (inrun) {
+                    hp.F[pos] = ifv;
+                    hp.C[pos] = icm;
+                }
+                // a right child (even position) sets its parent's bit against its left sibling: the
+                // previous item of the run, or `last` for the first
+                const int prev = below ? 31 - __clz(below) : 0;
+                const double pvf = __shfl(ifv, prev);
+                const uint32_t pvc = (uint32_t)__shfl((int)icm, prev);
+                const double leftf = below ? pvf : lastf;
+                const uint32_t leftk = below ? hkey<HEUR>(pvc) : hkey<HEUR>(lastc);
+                const uint64_t rb = __ballot(inrun && !key_lt(leftf, leftk, ifv, ik));
+                uint64_t rc = __ballot(inrun && (pos & 1) == 0);
+                while (rc) {
+                    const int m = __ffsll((long long)rc) - 1;
+                    rc &= rc - 1ull;
+                    sq_bit1(hp, (uint32_t)__builtin_amdgcn_readlane(pp, m) + 1u, (uint32_t)((rb >> m) & 1ull));
+                }
+                const int top = 63 - __clzll((long long)run);
+                lastf = rl_f64(ifv, top);
+                lastc = rl_u32(icm, top);
+                const int k = __popcll(run);
+                n += k;
+                npush += k;
+                vm &= ~run;
+                wave_sync_mem();
+            }
+        }
         while (vm) {
             const int m = __ffsll((long long)vm) - 1;
             vm &= vm - 1ull;

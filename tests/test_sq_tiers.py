@@ -155,6 +155,29 @@ class SqHeap:
         Q = n + 1
         self.op(False, Q, Q.bit_length() - 1, n, x)
 
+    def push_batch(self, items):
+        """An expansion's pushes in motion order: the leading run of trivial ones (each item not
+        less than its parent, a position < n) stored together, then one by one (the kernel's batch)."""
+        n = len(self.a)
+        k = 0
+        if n > 0:
+            for i, x in enumerate(items):
+                pos = n + i
+                pp = (pos - 1) >> 1
+                if pp >= n or lt(x, self.a[pp]):
+                    break
+                k += 1
+            for i in range(k):
+                pos = n + i
+                self.a.append(items[i])
+                if pos % 2 == 0:
+                    left = self.last if i == 0 else items[i - 1]
+                    self.bit1(((pos - 1) >> 1) + 1, int(not lt(left, items[i])))
+            if k:
+                self.last = items[k - 1]
+        for x in items[k:]:
+            self.push(x)
+
     def pop(self):
         root = self.a[0]
         last = self.a.pop()
@@ -187,11 +210,19 @@ def run(seed, steps, p_pop, grow_to=None):
             r = heapq.heappop(ref)
             m = h.pop()
             assert r is m, (seed, step)
-        else:
+        elif rng.random() < 0.5:
             it = Item(float(rng.randint(0, 40)), rng.randint(0, 3), tag)
             tag += 1
             heapq.heappush(ref, it)
             h.push(it)
+        else:  # an expansion's batch of up to 8 pushes
+            items = []
+            for _ in range(rng.randint(1, 8)):
+                items.append(Item(float(rng.randint(0, 40)), rng.randint(0, 3), tag))
+                tag += 1
+            for it in items:
+                heapq.heappush(ref, it)
+            h.push_batch(items)
         assert len(ref) == len(h.a), (seed, step)
         if ref:
             assert h.root is ref[0] and h.last is ref[-1], (seed, step)
