@@ -475,9 +475,12 @@ int pmp_astar2d_set_residency(pmp_ctx* ctx, int per_cu);
  * t2_lds = keep its level-10..14 heap direction bits in LDS (1) or HBM (0).  engine 0: one query per
  * wave (also Theta* / Lazy Theta*, and heaps of any size); on grids whose occupancy, cell state and
  * g fit in a wave's LDS share beside its heap (the README grid: 14 KB) all of them live in LDS.
- * engine 1 (default): engine 2 for batches of >= 1024 queries on grids too large for that, engine 0
- * otherwise (a single query's latency: the drop-in AStar.plan).  Results are identical.  Applies to
- * the next launch (re-reserves the scratch geometry when one is set). */
+ * engine 3: one query per workgroup with the CU's whole LDS as its heap (up to 13,440 entries beside
+ * no grid; a query that outgrows it reports PMP_CAP_OVERFLOW) and the heap's choice bits in
+ * registers -- a single query's latency (the drop-in AStar.plan).  engine 1 (default): engine 3 for
+ * batches of <= 256 queries whose heap capacity it holds, engine 2 for batches of >= 1024 queries on
+ * grids too large for engine 0's LDS grid block, engine 0 otherwise.  Results are identical.
+ * Applies to the next launch (re-reserves the scratch geometry when one is set). */
 int pmp_astar2d_set_engine(pmp_ctx* ctx, int engine, int t2_lds);
 
 /* Persistent workers (one wave each) per CU of the one-wave-per-query planners: pmp_graph3d_batch,
