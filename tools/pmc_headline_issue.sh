@@ -1,7 +1,8 @@
 #!/bin/bash
-# PMC issue breakdown of the A* 2D multi-query kernel at the headline geometry (8192 groups = 2 waves
-# per SIMD, 32 queries resident per CU, tier-2 bits in LDS), REPEAT batches of the C2 queries in one
-# launch (tools/astar2d_probe.py).  Usage: [LIB=libpmp_hip_x.so] bash tools/pmc_headline_issue.sh tag
+# PMC issue breakdown of the A* 2D multi-query kernel at the headline geometry (W_=15360 groups, RES=60
+# queries resident per CU, tier-2 bits in LDS), REPEAT batches of the C2 queries in one launch
+# (tools/astar2d_probe.py); MODE=c1 ENGINE=3 KERN=sq: the single-query engine on the README query.
+# Usage: [LIB=libpmp_hip_x.so] bash tools/pmc_headline_issue.sh tag
 R=${GRAFT_REPO_ROOT:-/root/repo}
 TAG=${1:-head}
 OUT=$R/gpurun_out/pmc_issue_$TAG
@@ -13,15 +14,15 @@ S2="SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INS
 i=0
 for set in "$S1" "$S2"; do
   i=$((i+1))
-  ENGINE=1 T2LDS=1 WORKERS=8192 RESIDENCY=32 MODE=batch REPEAT=${REPEAT:-4} REPS=1 timeout -s KILL 150 rocprofv3 --pmc $set -d $OUT/p$i -o run -- python3 $R/tools/astar2d_probe.py > $OUT/p$i.log 2>&1 || { echo "pass $i failed rc=$?"; tail -5 $OUT/p$i.log; exit 1; }
+  ENGINE=${ENGINE:-1} T2LDS=1 WORKERS=${W_:-15360} RESIDENCY=${RES:-60} MODE=${MODE:-batch} REPEAT=${REPEAT:-4} REPS=1 timeout -s KILL 150 rocprofv3 --pmc $set -d $OUT/p$i -o run -- python3 $R/tools/astar2d_probe.py > $OUT/p$i.log 2>&1 || { echo "pass $i failed rc=$?"; tail -5 $OUT/p$i.log; exit 1; }
 done
-python3 - $OUT <<'PY'
+python3 - $OUT ${KERN:-mq} <<'PY'
 import glob, re, sqlite3, sys
-out = sys.argv[1]
+out, kern = sys.argv[1], sys.argv[2]
 vals = {}
 for db in sorted(glob.glob(f"{out}/p*/**/*.db", recursive=True)):
     d = sqlite3.connect(db)
-    for name, s in d.execute("select counter_name, sum(value) from counters_collection where kernel_name like '%mq%' group by counter_name"):
+    for name, s in d.execute("select counter_name, sum(value) from counters_collection where kernel_name like ? group by counter_name", (f"%{kern}%",)):
         vals[name] = s
 m = re.search(r"\((\d+) plans/s\).*pushes (\d+) pops (\d+) exp (\d+)", open(f"{out}/p1.log").read())
 pl, P, Q, E = map(int, m.groups())

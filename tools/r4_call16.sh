@@ -9,3 +9,8 @@ timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke(); print('smo
 tail -1 gpurun_out/c16/smoke.log
 timeout -k 10 500 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/c16/bench.jsonl 2> gpurun_out/c16/bench.err || { tail -20 gpurun_out/c16/bench.err; exit 1; }
 tail -c 600 gpurun_out/c16/bench.jsonl
+# 3D A* residency sweep (C5, the astar3d leg alone)
+for res in 24 20 28 32; do
+  timeout -k 10 200 python3 bench.py --legs astar3d --no-cpu-baseline --steps 1 --warmup 1 --a3-residency $res > gpurun_out/c16/a3_$res.json 2> gpurun_out/c16/a3_$res.err || { tail -5 gpurun_out/c16/a3_$res.err; exit 1; }
+  python3 -c "import json; d=json.loads(open('gpurun_out/c16/a3_$res.json').read().strip().splitlines()[-1]); print('a3 residency $res', d['secondary']['astar3d'])"
+done
