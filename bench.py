@@ -1685,8 +1685,9 @@ def main():
     ap.add_argument("--a3-batches-per-launch", type=int, default=0,
                     help="3D A* batches per launch (0 = all the timed steps in one launch)")
     ap.add_argument("--a3-workers-per-cu", type=int, default=4, help="3D A* persistent workers per CU")
-    ap.add_argument("--a3-residency", type=int, default=24,
-                    help="3D A* workers resident per CU over all batches in flight (LDS share; 0 = per launch)")
+    ap.add_argument("--a3-residency", type=int, default=20,
+                    help="3D A* workers resident per CU over all batches in flight (LDS share; 0 = per launch); "
+                         "round 4 sweep, one box: 20 / 24 / 28 / 32 -> 1.848 / 1.816 / 1.810 / 1.794 M plans/s")
     ap.add_argument("--dstar-workers-per-cu", type=int, default=0, help="D* persistent workers per CU (0 = default)")
     ap.add_argument("--dstar-residency", type=int, default=0,
                     help="D* workers resident per CU over all batches in flight (LDS share; 0 = per launch)")
