@@ -124,8 +124,11 @@ __device__ __forceinline__ double dist3(int dx, int dy, int dz)  // Planner3D.di
 // LazyThetaStar3D (lazy_theta_star3d.py:41-128).  Theta modes keep any-voxel parents: a per-cell
 // CLOSED parent (cpar) and, per push, the entry's parent in a side table indexed by the push
 // counter (ppar), since an entry's parent may be its pusher's parent.
+#ifndef PMP_A3_WAVES
+#define PMP_A3_WAVES 5  // waves per SIMD the A* / Dijkstra / GBFS variants are compiled for (A/B switch)
+#endif
 template <bool OCC_LDS, int THETA>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ? 5 : 4))) void astar3d_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ? PMP_A3_WAVES : 4))) void astar3d_kernel(
     const uint32_t* __restrict__ occ_all, int per_query, int X, int Y, int Z, int heuristic,
     const int32_t* __restrict__ start_xyz, const int32_t* __restrict__ goal_xyz, int nq, double* __restrict__ cost_out,
     int32_t* __restrict__ path_len_out, uint32_t* __restrict__ path_out, int path_cap, int32_t* __restrict__ nexp_out,
