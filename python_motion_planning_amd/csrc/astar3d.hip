@@ -36,6 +36,13 @@ struct Key3 {
     static constexpr bool kStoredF = true;
     int gx, gy, gz;
     int heur;  // 0 euclidean, 1 manhattan, 2 zero (Dijkstra3D: h = 0, dijkstra3d.py:34,83)
+    int Y, Z;  // grid dims for cell(): the decrease-key position map
+
+    __device__ __forceinline__ uint32_t cell(const Ent& e) const
+    {
+        const uint32_t x = e.b >> 21, y = (e.b >> 13) & 255u, z = (e.b >> 5) & 255u;
+        return (x * (uint32_t)Y + y) * (uint32_t)Z + z;
+    }
 
     __device__ __forceinline__ uint32_t hkey(uint32_t b) const
     {
@@ -135,7 +142,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
     uint32_t* __restrict__ expand_out, int expand_cap, int64_t* __restrict__ counters, int32_t* __restrict__ status_out,
     int* __restrict__ queue, uint4* __restrict__ spill_all, int heap_cap, int lds_cap, uint8_t* __restrict__ cdir_all,
     double* __restrict__ cg_all, int gzero, uint32_t* __restrict__ cpar_all, uint32_t* __restrict__ ppar_all,
-    uint32_t ppar_cap, const int32_t* __restrict__ order, int prio_n)
+    uint32_t ppar_cap, const int32_t* __restrict__ order, int prio_n, uint32_t* __restrict__ hpos_all)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
@@ -143,8 +150,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
     const size_t ncell = (size_t)X * Y * Z;
     const size_t words = (ncell + 31) / 32;
     const size_t spill_n = (size_t)(heap_cap > lds_cap ? heap_cap - lds_cap : 0);
-    const heap16::Heap hp =
+    heap16::Heap hp =
         heap16::make_heap<true>(smem, lds_cap, spill_all + (size_t)worker * spill_n * 2, spill_n);  // 32 B records
+    // A* / Dijkstra / GBFS: one entry per pending cell -- an improved g replaces the cell's entry in
+    // place (decrease-key through the cell -> position map) instead of leaving a dead duplicate that
+    // would pop later and be skipped.  The key is a total order, so the live entries pop in the same
+    // order either way; the heap is smaller and those stale pops are gone.
+    constexpr bool POS = THETA == 0;
+    if (POS) hp.hpos = hpos_all + (size_t)worker * ncell;
     lds_w32* occl = (lds_w32*)(smem + (size_t)heap16::lds_entry_bytes<true>() * lds_cap);  // OCC_LDS: the query's bitmap
     uint8_t* cdir = cdir_all + (size_t)worker * ncell;
     double* cg = cg_all + (size_t)worker * 2 * ncell;  // closed g
@@ -176,6 +189,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
         for (size_t i = lane; i < ncell; i += 64) {
             cdir[i] = 0;
             og[i] = __builtin_inf();
+            if (POS) hp.hpos[i] = heap16::kNoPos;
         }
         heap16::wsync();
         const int sx = start_xyz[3 * q], sy = start_xyz[3 * q + 1], sz = start_xyz[3 * q + 2];
@@ -184,6 +198,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
         qc.gy = goal_xyz[3 * q + 1];
         qc.gz = goal_xyz[3 * q + 2];
         qc.heur = heuristic;
+        qc.Y = Y;
+        qc.Z = Z;
         const bool s_in = (unsigned)sx < (unsigned)X && (unsigned)sy < (unsigned)Y && (unsigned)sz < (unsigned)Z;
         const bool g_in = (unsigned)qc.gx < (unsigned)X && (unsigned)qc.gy < (unsigned)Y && (unsigned)qc.gz < (unsigned)Z;
         if (!s_in || !g_in) {  // every lane stores the same values (no lane-0 block before the continue)
@@ -202,6 +218,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
         root.b = scm;
         qc.set_f(root);
         if (lane == 0) heap16::store<true, true>(hp, 0, root);
+        if (POS && lane == 0) hp.hpos[((uint32_t)sx * (uint32_t)Y + (uint32_t)sy) * (uint32_t)Z + (uint32_t)sz] = 0u;
         if (THETA && lane == 0) ppar[0] = ((uint32_t)sx * (uint32_t)Y + (uint32_t)sy) * (uint32_t)Z + (uint32_t)sz;
         heap16::wsync();
         int n = 1;
@@ -241,6 +258,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
             // loaded on every lane (no zero-filled destination, see above)
             uint32_t epar = 0;
             if (THETA) epar = ppar[node.a < ppar_cap ? node.a : 0u];
+            // POS: the neighbour's pending entry position (before this expansion's operations)
+            uint32_t npos = heap16::kNoPos;
+            if (POS) npos = hp.hpos[nlin];
             if (lane < 26) {
                 if (OCC_LDS) {
 #define OCC(a, b, c) occ3l(occl, X, Y, Z, a, b, c)
@@ -270,9 +290,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
 #ifdef PMP_STAMPS
             const uint64_t ts0 = __builtin_amdgcn_s_memtime();
 #endif
+            int hole = 0;
             if (n > 0) {
-                if (n < lds_cap) heap16::pop<Key3, false, true>(hp, qc, n, root, lane, pop_jl, pop_ol, pop_w);
-                else heap16::pop<Key3, true, true>(hp, qc, n, root, lane, pop_jl, pop_ol, pop_w);
+                if (n < lds_cap) hole = heap16::pop<Key3, false, true, POS>(hp, qc, n, root, lane, pop_jl, pop_ol, pop_w);
+                else hole = heap16::pop<Key3, true, true, POS>(hp, qc, n, root, lane, pop_jl, pop_ol, pop_w);
+            }
+            if (POS) {
+                // the popped entry left the heap; the pop moved the path below the root up one level
+                // and the old last entry (position n) to the hole
+                if (lane == 0) hp.hpos[lin] = heap16::kNoPos;
+                if (n > 0 && npos != heap16::kNoPos) {
+                    const int d = heap16::level_of(hole) - heap16::level_of((int)npos);
+                    if (npos == (uint32_t)n) npos = (uint32_t)hole;
+                    else if (npos != 0u && d >= 0 && (((uint32_t)hole + 1u) >> d) == npos + 1u) npos = (npos - 1u) >> 1;
+                }
             }
 #ifdef PMP_STAMPS
             const uint64_t ts1 = __builtin_amdgcn_s_memtime();
@@ -427,7 +458,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
             while (vm) {
                 const int m = __ffsll((long long)vm) - 1;
                 vm &= vm - 1;
-                if (n >= heap_cap) { overflow = true; break; }
                 Ent it = heap16::rl_ent(item, m);
                 // counter = the reference's push index of this neighbour
                 it.a = seq + (uint32_t)__popc(okm & ((1u << m) - 1u));
@@ -435,9 +465,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
                     if (it.a >= ppar_cap) { overflow = true; break; }
                     if (lane == 0) ppar[it.a] = rl_u32(qpar, m);
                 }
-                if (n < lds_cap) heap16::push<Key3, false>(hp, qc, n, it, root, lane);
-                else heap16::push<Key3, true>(hp, qc, n, it, root, lane);
-                n += 1;
+                const uint32_t pm = POS ? rl_u32(npos, m) : heap16::kNoPos;
+                int p0 = n;
+                if (pm != heap16::kNoPos) p0 = (int)pm;  // decrease-key of the cell's pending entry
+                else if (n >= heap_cap) { overflow = true; break; }
+                int ip;
+                if (p0 < lds_cap) ip = heap16::sift_up<Key3, false, POS>(hp, qc, p0, it, root, lane);
+                else ip = heap16::sift_up<Key3, true, POS>(hp, qc, p0, it, root, lane);
+                if (pm == heap16::kNoPos) n += 1;
+                if (POS && npos != heap16::kNoPos) {
+                    // the ancestors of p0 from ip down moved one level toward p0
+                    const int d = heap16::level_of(p0) - heap16::level_of((int)npos);
+                    if (d >= 1 && (((uint32_t)p0 + 1u) >> d) == npos + 1u && heap16::level_of((int)npos) >= heap16::level_of(ip))
+                        npos = (((uint32_t)p0 + 1u) >> (d - 1)) - 1u;
+                }
             }
             seq += (uint32_t)__popc(okm);
 #ifdef PMP_STAMPS
@@ -574,7 +615,7 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     const uint32_t ppar_cap = theta ? (uint32_t)std::min<size_t>(64 * ncell + 64, (size_t)1 << 24) : 0u;
     {
         // per-context scratch budget: fewer workers (each pulls more queries) rather than ENOMEM
-        const size_t per_worker = spill_n * kSpill + ncell + ncell * 16 + (theta ? ((size_t)ncell + ppar_cap) * 4 : 0);
+        const size_t per_worker = spill_n * kSpill + ncell + ncell * 16 + (theta ? ((size_t)ncell + ppar_cap) * 4 : ncell * 4);
         const size_t fit = kScratchBudget3 / per_worker;
         if (fit < 1) return pmp_set_err(ctx, PMP_ENOMEM, "pmp_graph3d_batch: one worker exceeds the scratch budget");
         if ((size_t)workers > fit) workers = (int)fit;
@@ -583,11 +624,9 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     uint8_t* cdir = (uint8_t*)pmp_scratch(ctx, SCR_AUX2, (size_t)workers * ncell + 16);
     double* cg = (double*)pmp_scratch(ctx, SCR_AUX3, (size_t)workers * ncell * 16 + 16);  // closed g + pending g
     int* queue = (int*)pmp_scratch(ctx, SCR_AUX0, 256);
-    uint32_t* tpar = nullptr;
-    if (theta) {
-        tpar = (uint32_t*)pmp_scratch(ctx, SCR_AUX4, (size_t)workers * (ncell + ppar_cap) * 4 + 16);
-        if (!tpar) return PMP_ENOMEM;
-    }
+    uint32_t* tpar = nullptr;  // theta: CLOSED parents + push parents; otherwise the heap position map
+    tpar = (uint32_t*)pmp_scratch(ctx, SCR_AUX4, (size_t)workers * (theta ? ncell + ppar_cap : ncell) * 4 + 16);
+    if (!tpar) return PMP_ENOMEM;
     if (!spill || !cdir || !cg || !queue) return PMP_ENOMEM;
     hipStream_t s = (hipStream_t)stream;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
@@ -601,8 +640,8 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     hipLaunchKernelGGL(kern, dim3(workers), dim3(64), (size_t)lds_cap * kEnt + occ_bytes, s, occ_bits, per_query, X, Y, Z,
                        algo == PMP_ALGO_DIJKSTRA ? 2 : heuristic, start_xyz, goal_xyz, nq, cost, path_len, path, path_cap,
                        n_expanded, expand, expand_cap, counters, status, queue, spill, heap_cap, lds_cap, cdir, cg,
-                       algo == PMP_ALGO_GBFS ? 1 : 0, tpar, tpar ? tpar + (size_t)workers * ncell : nullptr, ppar_cap,
-                       (const int32_t*)order, order ? ctx->astar_prio_n : 0);
+                       algo == PMP_ALGO_GBFS ? 1 : 0, theta ? tpar : nullptr, theta ? tpar + (size_t)workers * ncell : nullptr,
+                       ppar_cap, (const int32_t*)order, order ? ctx->astar_prio_n : 0, theta ? nullptr : tpar);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }
