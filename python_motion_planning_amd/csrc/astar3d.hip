@@ -38,15 +38,18 @@ struct Key3 {
     int heur;  // 0 euclidean, 1 manhattan, 2 zero (Dijkstra3D: h = 0, dijkstra3d.py:34,83)
     int Y, Z;  // grid dims for cell(): the decrease-key position map
 
+    // an entry pushed beside a pending entry of its cell with the same f (below) is not tracked
+    static constexpr uint32_t kUntracked = 1u << 29;
+    static __device__ __forceinline__ bool tracked(const Ent& e) { return !(e.b & kUntracked); }
     __device__ __forceinline__ uint32_t cell(const Ent& e) const
     {
-        const uint32_t x = e.b >> 21, y = (e.b >> 13) & 255u, z = (e.b >> 5) & 255u;
+        const uint32_t x = (e.b >> 21) & 255u, y = (e.b >> 13) & 255u, z = (e.b >> 5) & 255u;
         return (x * (uint32_t)Y + y) * (uint32_t)Z + z;
     }
 
     __device__ __forceinline__ uint32_t hkey(uint32_t b) const
     {
-        const int x = (int)(b >> 21), y = (int)((b >> 13) & 255u), z = (int)((b >> 5) & 255u);
+        const int x = (int)((b >> 21) & 255u), y = (int)((b >> 13) & 255u), z = (int)((b >> 5) & 255u);
         const int dx = abs(gx - x), dy = abs(gy - y), dz = abs(gz - z);
         return heur == 2 ? 0u : (heur == 1 ? (uint32_t)(dx + dy + dz) : (uint32_t)(dx * dx + dy * dy + dz * dz));
     }
@@ -236,7 +239,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
             const Ent node = root;
             npop++;
             n -= 1;
-            const int x = (int)(node.b >> 21), y = (int)((node.b >> 13) & 255u), z = (int)((node.b >> 5) & 255u);
+            const int x = (int)((node.b >> 21) & 255u), y = (int)((node.b >> 13) & 255u), z = (int)((node.b >> 5) & 255u);
             const int ndir = (int)(node.b & 31u);
             const uint32_t lin = ((uint32_t)x * (uint32_t)Y + (uint32_t)y) * (uint32_t)Z + (uint32_t)z;
             // ---- HBM round (issued before the pop): neighbour collision + CLOSED state, node's CLOSED state
@@ -387,7 +390,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
                 if (THETA) cpar[lin] = npar;
             }
             if (!sclosed) nexp++;
-            if ((node.b >> 5) == goal_xyz24) {  // goal check (:59-63), path via CLOSED parents
+            if (((node.b >> 5) & 0xFFFFFFu) == goal_xyz24) {  // goal check (:59-63), path via CLOSED parents
                 st = PMP_FOUND;
                 heap16::wsync();
                 if (THETA && lane == 0) {  // extractPath via CLOSED parents (theta_star3d.py:217-232)
@@ -454,6 +457,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
             item.a = 0u;
             item.b = ((((uint32_t)nx & 255u) << 16) | (((uint32_t)ny & 255u) << 8) | ((uint32_t)nz & 255u)) << 5 | (uint32_t)(lane < 26 ? lane : 0);
             qc.set_f(item);
+            bool fbelow = false;  // POS: item.f < f of the cell's pending entry (g = nog)
+            if (POS) {
+                Ent pend = item;
+                pend.g = nog;
+                qc.set_f(pend);
+                fbelow = item.f < pend.f;
+            }
             bool overflow = false;
             while (vm) {
                 const int m = __ffsll((long long)vm) - 1;
@@ -465,14 +475,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
                     if (it.a >= ppar_cap) { overflow = true; break; }
                     if (lane == 0) ppar[it.a] = rl_u32(qpar, m);
                 }
+                // decrease-key only when the new f is strictly below the pending entry's (nog + h): with
+                // equal f the reference's older entry pops first (smaller counter) and expands the cell
+                // with its g, then the newer one expands it again -- so it is pushed beside it instead,
+                // untracked (its moves leave the position map alone)
                 const uint32_t pm = POS ? rl_u32(npos, m) : heap16::kNoPos;
+                const bool dk = POS && pm != heap16::kNoPos && rl_u32(fbelow ? 1u : 0u, m) != 0u;
                 int p0 = n;
-                if (pm != heap16::kNoPos) p0 = (int)pm;  // decrease-key of the cell's pending entry
+                if (dk) p0 = (int)pm;
                 else if (n >= heap_cap) { overflow = true; break; }
+                if (POS && !dk && pm != heap16::kNoPos) it.b |= Key3::kUntracked;
                 int ip;
                 if (p0 < lds_cap) ip = heap16::sift_up<Key3, false, POS>(hp, qc, p0, it, root, lane);
                 else ip = heap16::sift_up<Key3, true, POS>(hp, qc, p0, it, root, lane);
-                if (pm == heap16::kNoPos) n += 1;
+                if (!dk) n += 1;
                 if (POS && npos != heap16::kNoPos) {
                     // the ancestors of p0 from ip down moved one level toward p0
                     const int d = heap16::level_of(p0) - heap16::level_of((int)npos);

@@ -41,7 +41,8 @@ constexpr uint32_t kNoPos = 0xFFFFFFFFu;
 template <class K, bool POS>
 __device__ __forceinline__ void note(const Heap& hp, const K& key, const Ent& e, int p)
 {
-    if constexpr (POS) hp.hpos[key.cell(e)] = (uint32_t)p;
+    if constexpr (POS)
+        if (K::tracked(e)) hp.hpos[key.cell(e)] = (uint32_t)p;
 }
 __device__ __forceinline__ int level_of(int p) { return 31 - __clz(p + 1); }
 
