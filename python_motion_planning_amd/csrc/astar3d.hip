@@ -134,6 +134,9 @@ __device__ __forceinline__ double dist3(int dx, int dy, int dz)  // Planner3D.di
 // LazyThetaStar3D (lazy_theta_star3d.py:41-128).  Theta modes keep any-voxel parents: a per-cell
 // CLOSED parent (cpar) and, per push, the entry's parent in a side table indexed by the push
 // counter (ppar), since an entry's parent may be its pusher's parent.
+#ifndef PMP_A3_DKEY
+#define PMP_A3_DKEY 0
+#endif
 #ifndef PMP_A3_WAVES
 #define PMP_A3_WAVES 5  // waves per SIMD the A* / Dijkstra / GBFS variants are compiled for (A/B switch)
 #endif
@@ -155,11 +158,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
     const size_t spill_n = (size_t)(heap_cap > lds_cap ? heap_cap - lds_cap : 0);
     heap16::Heap hp =
         heap16::make_heap<true>(smem, lds_cap, spill_all + (size_t)worker * spill_n * 2, spill_n);  // 32 B records
-    // A* / Dijkstra / GBFS: one entry per pending cell -- an improved g replaces the cell's entry in
-    // place (decrease-key through the cell -> position map) instead of leaving a dead duplicate that
-    // would pop later and be skipped.  The key is a total order, so the live entries pop in the same
-    // order either way; the heap is smaller and those stale pops are gone.
-    constexpr bool POS = THETA == 0;
+    // PMP_A3_DKEY (A/B switch, off): A* / Dijkstra / GBFS keep one entry per pending cell -- an
+    // improved g replaces the cell's entry in place (decrease-key through a cell -> position map)
+    // instead of leaving a dead duplicate that would pop later and be skipped.  The key is a total
+    // order, so the live entries pop in the same order either way (parity green); the heap is smaller
+    // and those stale pops are gone, but the map's stores and corrections cost more issue slots than
+    // the pops they save on this issue-bound loop (round 4, same box: 1.71 M vs 1.84 M plans/s).
+    constexpr bool POS = THETA == 0 && PMP_A3_DKEY != 0;
     if (POS) hp.hpos = hpos_all + (size_t)worker * ncell;
     lds_w32* occl = (lds_w32*)(smem + (size_t)heap16::lds_entry_bytes<true>() * lds_cap);  // OCC_LDS: the query's bitmap
     uint8_t* cdir = cdir_all + (size_t)worker * ncell;
@@ -631,7 +636,8 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     const uint32_t ppar_cap = theta ? (uint32_t)std::min<size_t>(64 * ncell + 64, (size_t)1 << 24) : 0u;
     {
         // per-context scratch budget: fewer workers (each pulls more queries) rather than ENOMEM
-        const size_t per_worker = spill_n * kSpill + ncell + ncell * 16 + (theta ? ((size_t)ncell + ppar_cap) * 4 : ncell * 4);
+        const size_t per_worker = spill_n * kSpill + ncell + ncell * 16 +
+                                  (theta ? ((size_t)ncell + ppar_cap) * 4 : (PMP_A3_DKEY ? ncell * 4 : 0));
         const size_t fit = kScratchBudget3 / per_worker;
         if (fit < 1) return pmp_set_err(ctx, PMP_ENOMEM, "pmp_graph3d_batch: one worker exceeds the scratch budget");
         if ((size_t)workers > fit) workers = (int)fit;
@@ -640,9 +646,11 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     uint8_t* cdir = (uint8_t*)pmp_scratch(ctx, SCR_AUX2, (size_t)workers * ncell + 16);
     double* cg = (double*)pmp_scratch(ctx, SCR_AUX3, (size_t)workers * ncell * 16 + 16);  // closed g + pending g
     int* queue = (int*)pmp_scratch(ctx, SCR_AUX0, 256);
-    uint32_t* tpar = nullptr;  // theta: CLOSED parents + push parents; otherwise the heap position map
-    tpar = (uint32_t*)pmp_scratch(ctx, SCR_AUX4, (size_t)workers * (theta ? ncell + ppar_cap : ncell) * 4 + 16);
-    if (!tpar) return PMP_ENOMEM;
+    uint32_t* tpar = nullptr;  // theta: CLOSED parents + push parents; PMP_A3_DKEY: the heap position map
+    if (theta || PMP_A3_DKEY) {
+        tpar = (uint32_t*)pmp_scratch(ctx, SCR_AUX4, (size_t)workers * (theta ? ncell + ppar_cap : ncell) * 4 + 16);
+        if (!tpar) return PMP_ENOMEM;
+    }
     if (!spill || !cdir || !cg || !queue) return PMP_ENOMEM;
     hipStream_t s = (hipStream_t)stream;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
