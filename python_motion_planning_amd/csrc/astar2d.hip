@@ -1289,7 +1289,9 @@ extern "C" int pmp_graph2d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
         // host re-runs it with the full bound, which lands on this file's engine)
         const int sq_cap = pmp_astar2d_sq_cap(W, H);
         const int want = ctx->astar_reserved_mq ? ctx->astar_heap_cap_wave : ctx->astar_heap_cap;
-        if (sq_cap > 0 && (!ctx->astar_cap_explicit || want <= sq_cap))
+        // one query slot (cell states + G, unless the grid sits in LDS) per query of the batch
+        const bool fits = (size_t)nq * (ncell * 9 + 256) <= kScratchBudgetMq;
+        if (sq_cap > 0 && fits && (!ctx->astar_cap_explicit || want <= sq_cap))
             return pmp_astar2d_sq_launch(ctx, (hipStream_t)stream, algo, occ_bits, W, H, heuristic, start_xy, goal_xy, nq,
                                          want < sq_cap ? want : sq_cap, cost, path_len, path, path_cap, n_expanded,
                                          expand, expand_cap, counters, status);
