@@ -121,3 +121,49 @@ def test_decrease_key_positions_and_order():
                 assert h.pos[e[1]] == p
                 if p:
                     assert not (e[0] < h.a[(p - 1) >> 1][0])
+
+
+def test_batch_store_then_sift_up_below_parent():
+    """astar3d.hip's batch: an expansion's live items stored at n, n + 1, ... together, then only the
+    ones below their (pre-batch) parent -- or whose parent is another new item -- sift up, in position
+    order.  The result must be a valid heap holding every entry, and the skipped items must still be
+    not below their parents at the end (a sift-up only lowers the parents of later positions)."""
+    import heapq
+
+    rng = random.Random(5)
+    for trial in range(300):
+        h = PosHeap()
+        ref = []
+        ctr = 0
+        for _ in range(rng.randint(0, 60)):
+            ctr += 1
+            e = ((rng.randint(0, 30), ctr), ctr)
+            h.sift_up(len(h.a), e)
+            heapq.heappush(ref, e)
+        for _ in range(20):
+            n0 = len(h.a)
+            k = rng.randint(1, 26)
+            items = []
+            for _ in range(k):
+                ctr += 1
+                items.append(((rng.randint(0, 30), ctr), ctr))
+            below = []
+            for r, e in enumerate(items):
+                pos, pp = n0 + r, (n0 + r - 1) >> 1
+                below.append(not (pos > 0 and pp < n0) or e[0] < h.a[pp][0])
+            for e in items:
+                h.a.append(e)
+                h.pos[e[1]] = len(h.a) - 1
+            for r, e in enumerate(items):
+                if below[r]:
+                    h.sift_up(n0 + r, e)
+            for e in items:
+                heapq.heappush(ref, e)
+            assert sorted(h.a) == sorted(ref)
+            for p in range(1, len(h.a)):
+                assert not (h.a[p][0] < h.a[(p - 1) >> 1][0]), (trial, p)
+            for _ in range(rng.randint(0, 10)):
+                if h.a:
+                    a, _ = h.pop()
+                    b = heapq.heappop(ref)
+                    assert a == b
