@@ -479,33 +479,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
                 // parent (an entry from before this batch; else assumed below) sift up afterwards, in
                 // position order -- a sift-up only lowers the parents of the later ones, so an item
                 // found not below its parent stays so.  Most pushes cost no heap operation of their own.
-                const int k = __popcll(vm);
-                if (n + k > heap_cap) {
+                if (n + __popcll(vm) > heap_cap) {
                     overflow = true;
                 } else {
-                    const bool mine = (vm >> lane) & 1ull;
-                    const int rank = __popcll(vm & ((1ull << lane) - 1ull));
-                    const int pos = n + rank, pp = (pos - 1) >> 1;
                     Ent it = item;
                     it.a = seq + (uint32_t)__popc(okm & ((1u << (lane & 31)) - 1u));
-                    const bool hasp = mine && pos > 0 && pp < n;
-                    Ent par;
-                    heap16::load<true, true>(hp, hasp ? pp : 0, par);
-                    qc.derive(par);
-                    const bool below = !hasp || Key3::lt(it, par);
-                    if (mine) heap16::store<true, true>(hp, pos, it);
-                    heap16::wsync();
-                    const int n0 = n;
-                    n += k;
-                    uint64_t sm = ballot(mine && below);
-                    while (sm) {
-                        const int m = __ffsll((long long)sm) - 1;
-                        sm &= sm - 1ull;
-                        const Ent x = heap16::rl_ent(it, m);
-                        const int p0 = n0 + __popcll(vm & ((1ull << m) - 1ull));
-                        if (p0 < lds_cap) heap16::sift_up<Key3, false>(hp, qc, p0, x, root, lane);
-                        else heap16::sift_up<Key3, true>(hp, qc, p0, x, root, lane);
-                    }
+                    n = heap16::push_batch(hp, qc, n, vm, it, root, lane);
                 }
                 vm = 0;
             }

@@ -313,14 +313,22 @@ struct D2 {
         S.ne += nins;
         S.open += nins;
         heap16::wsync();
-        // heap pushes: every re-keyed cell (stale elements are skipped on pop)
-        for (uint64_t pm = ballot(kind == 1); pm && !S.overflow; pm &= pm - 1) {
-            const int l = __ffsll((long long)pm) - 1;
-            Ent it;
-            it.g = rl_f64(yc.k, l);
-            it.a = rl_u32((uint32_t)yc.first, l);
-            it.b = rl_u32((uint32_t)Y, l);
-            push(it);
+        // heap pushes: every re-keyed cell (stale elements are skipped on pop), stored together and
+        // sifted up only where below the parent (heap16::push_batch; the key is a total order)
+        {
+            const uint64_t pm = ballot(kind == 1);
+            if (pm) {
+                if (S.n + __popcll(pm) > S.heap_cap) {
+                    S.overflow = true;
+                } else {
+                    Ent it;
+                    it.g = yc.k;
+                    it.a = (uint32_t)yc.first;
+                    it.b = (uint32_t)Y;
+                    key.derive(it);
+                    S.n = heap16::push_batch(S.hp, key, S.n, pm, it, S.root, lane);
+                }
+            }
         }
         if (!S.overflow && cnt_of(xc.cnt_t) > 0) {
             Ent it;

@@ -326,9 +326,20 @@ struct D3 {
         S.ne += (uint32_t)nap;
         S.open += nap;
         heap16::wsync();
-        for (uint64_t pm = ballot(pushme); pm && !S.overflow; pm &= pm - 1) {
-            const int l = __ffsll((long long)pm) - 1;
-            push(rl_f64(yc.k, l), rl_u32(yc.pos, l), (int)rl_u32((uint32_t)Yc, l));
+        {  // stored together, sifted up only where below the parent (heap16::push_batch: total order)
+            const uint64_t pm = ballot(pushme);
+            if (pm) {
+                if (S.n + __popcll(pm) > S.heap_cap) {
+                    S.overflow = true;
+                } else {
+                    Ent it;
+                    it.g = yc.k;
+                    it.a = yc.pos;
+                    it.b = (uint32_t)Yc;
+                    key.derive(it);
+                    S.n = heap16::push_batch(S.hp, key, S.n, pm, it, S.root, lane);
+                }
+            }
         }
         if (k2 && !S.overflow) push(xc.k, xc.pos, Xs);
         return true;

@@ -281,4 +281,36 @@ __device__ __forceinline__ int push(const Heap& hp, const K& key, int n, const E
     return sift_up<K, SPILL, POS>(hp, key, n, it, root, lane);
 }
 
+// Push the items of the lanes in pm (wave-uniform mask; each lane's `it` derived) into a heap of n
+// entries, for a total order (the heap's shape is free): all stored together at n, n + 1, ... (lane
+// order) in one round, then only the ones below their pre-batch parent (or whose parent is another
+// new item) sift up, in position order -- a sift-up only lowers the parents of later positions, so
+// an item found not below its parent stays valid.  Returns the new size.
+template <class K>
+__device__ __forceinline__ int push_batch(const Heap& hp, const K& key, int n, uint64_t pm, const Ent& it, Ent& root,
+                                          int lane)
+{
+    constexpr bool SF = K::kStoredF;
+    n = uni(n);
+    const bool mine = (pm >> lane) & 1ull;
+    const int pos = n + __popcll(pm & ((1ull << lane) - 1ull)), pp = (pos - 1) >> 1;
+    const bool hasp = mine && pos > 0 && pp < n;
+    Ent par;
+    load<true, SF>(hp, hasp ? pp : 0, par);
+    key.derive(par);
+    const bool below = !hasp || K::lt(it, par);
+    if (mine) store<true, SF>(hp, pos, it);
+    wsync();
+    uint64_t sm = ballot(mine && below);
+    while (sm) {
+        const int m = __ffsll((long long)sm) - 1;
+        sm &= sm - 1ull;
+        const Ent x = rl_ent(it, m);
+        const int p0 = n + __popcll(pm & ((1ull << m) - 1ull));
+        if (p0 < hp.lds_cap) sift_up<K, false>(hp, key, p0, x, root, lane);
+        else sift_up<K, true>(hp, key, p0, x, root, lane);
+    }
+    return n + __popcll(pm);
+}
+
 }  // namespace heap16
