@@ -7,7 +7,9 @@
 //         next 6 levels, three ballots give "right child is smaller" and "child < last" per pair,
 //         the walk over those masks is scalar, and the movers store in parallel;
 //   push: the ancestors load in one round; the "less than the new item" set is a prefix of the
-//         root path, so a ballot popcount gives the sift-up distance.
+//         root path, so a ballot popcount gives the sift-up distance;
+//   push_batch: an expansion's pushes stored together, only those below their parent sifted up;
+//   sift_up from any position (a decrease-key, with the POS position map).
 // The key is supplied by a policy type K: K::derive(e) fills e.f / e.hk from the stored fields and
 // K::lt(x, y) is the strict order.  K::kStoredF: f is stored beside the entry (24 B in LDS: g, f, a,
 // b; 32 B spill records) instead of derived on every load, so a key costs no square root.
