@@ -125,13 +125,47 @@ def test_c2_subset_against_reference(engine):
         assert hashlib.sha1(e.tobytes()).hexdigest() == str(z["expand_sha1"][i]), i
 
 
-def test_c2_full_batch_against_oracle_and_properties():
-    """All 4096 C2 queries in one launch: a seeded 256-query sample bit-exact vs the oracle,
-    and size-independent properties on every query."""
-    from oracle import oracle as O
-    from python_motion_planning_amd import batch, workloads as wl
+_C2_REF = {}
 
-    occ, starts, goals = wl.c2_workload(nq=4096)
+
+def _c2_oracle():
+    """The oracle on all 4096 C2 queries (OpenMP over the host's cores; a few seconds), computed once."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import workloads as wl
+
+    if not _C2_REF:
+        occ, starts, goals = wl.c2_workload(nq=4096)
+        _C2_REF.update(occ=occ, starts=starts, goals=goals,
+                       ref=O.astar2d_batch(occ, starts, goals, path_cap=4096))
+    return _C2_REF
+
+
+def _assert_c2_equal(ref, r, copies=1):
+    nq = len(ref["cost"])
+    cost = r["cost"].cpu().numpy()
+    ne = r["n_expanded"].cpu().numpy()
+    pl = r["path_len"].cpu().numpy()
+    P = r["path"].cpu().numpy()
+    ctr = r["counters"].cpu().numpy() if r.get("counters") is not None else None
+    for c in range(copies):
+        sl = slice(c * nq, (c + 1) * nq)
+        assert (r["status"].cpu().numpy()[sl] == 0).all()
+        assert np.array_equal(ref["cost"], cost[sl])
+        assert np.array_equal(ref["n_expanded"], ne[sl])
+        assert np.array_equal(ref["path_len"], pl[sl])
+        if ctr is not None:
+            assert np.array_equal(ref["counters"][:, :2], ctr[sl, :2])  # pushes and pops
+        for q in range(nq):
+            assert np.array_equal(ref["path"][q, : ref["path_len"][q]], P[c * nq + q, : pl[c * nq + q]]), (c, q)
+
+
+def test_c2_full_batch_against_oracle_and_properties():
+    """All 4096 C2 queries in one launch, every one bit-exact vs the oracle (cost bits, expansion and
+    heap-operation counts, path), and size-independent properties on every query."""
+    from python_motion_planning_amd import batch
+
+    c2 = _c2_oracle()
+    occ, starts, goals, ref = c2["occ"], c2["starts"], c2["goals"], c2["ref"]
     W, H = occ.shape
     r = batch.astar2d_batch(occ, starts, goals, path_cap=4096, counters=True)
     st = r["status"].cpu().numpy()
@@ -141,13 +175,7 @@ def test_c2_full_batch_against_oracle_and_properties():
     P = r["path"].cpu().numpy()
     ne = r["n_expanded"].cpu().numpy()
     ctr = r["counters"].cpu().numpy()
-    sample = np.random.default_rng(5).choice(4096, 256, replace=False)
-    ref = O.astar2d_batch(occ, starts[sample], goals[sample], path_cap=4096)
-    assert np.array_equal(ref["cost"], cost[sample])
-    assert np.array_equal(ref["n_expanded"], ne[sample])
-    assert np.array_equal(ref["counters"][:, :2], ctr[sample, :2])  # pushes and pops
-    for k, q in enumerate(sample):
-        assert np.array_equal(ref["path"][k, : ref["path_len"][k]], P[q, : pl[q]])
+    _assert_c2_equal(ref, r)
     # properties on every query
     sq2 = 2.0 ** 0.5
     for q in range(4096):
@@ -332,3 +360,28 @@ def test_residency_batches_in_flight(eng, per_cu):
         for q in range(nq):
             assert (p[q, : pl[q]] == ref["path"][q, : pl[q]]).all()
         L.pmp_destroy(b["ctx"])
+
+
+def test_c2_headline_schedule_against_oracle():
+    """The bench's headline schedule (engine 2, 15,360 groups = 60 per CU, several batches streamed
+    through one launch longest first): two copies of the 4096 C2 queries in one launch, every query
+    bit-exact vs the oracle."""
+    import torch
+
+    from python_motion_planning_amd import _lib, batch
+
+    c2 = _c2_oracle()
+    occ, starts, goals, ref = c2["occ"], c2["starts"], c2["goals"], c2["ref"]
+    W, H = occ.shape
+    L, ctx = _lib.load_library(), _lib.context()
+    try:
+        _lib.check(ctx, L.pmp_astar2d_set_engine(ctx, 1, 1), "engine")
+        _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, 15360, 0), "reserve")
+        _lib.check(ctx, L.pmp_astar2d_set_residency(ctx, 60), "residency")
+        r = batch.astar2d_batch(occ, np.tile(starts, (2, 1)), np.tile(goals, (2, 1)), path_cap=4096, counters=True)
+        torch.cuda.synchronize()
+        _assert_c2_equal(ref, r, copies=2)
+    finally:
+        _lib.check(ctx, L.pmp_astar2d_set_residency(ctx, 0), "residency")
+        _lib.check(ctx, L.pmp_astar2d_set_engine(ctx, 1, 0), "engine")
+        _lib.check(ctx, L.pmp_astar2d_reserve_auto(ctx), "reserve_auto")

@@ -62,7 +62,8 @@ def test_dropin_class():
 
 
 def test_c5_batch_against_oracle():
-    """C5: 8192 door-scenario queries on 26x20x16 (per-query carve) in one launch."""
+    """C5: 8192 door-scenario queries on 26x20x16 (per-query carve) in one launch, every one against
+    the oracle (status, cost bits, expansions, path, the reference's push count)."""
     from oracle import oracle as O
     from python_motion_planning_amd import batch, workloads as wl
 
@@ -74,7 +75,7 @@ def test_c5_batch_against_oracle():
     pl = out["path_len"].cpu().numpy()
     P = out["path"].cpu().numpy()
     ctr = out["counters"].cpu().numpy()
-    for q in np.random.default_rng(3).choice(8192, 300, replace=False):
+    for q in range(8192):  # every query against the oracle
         ref = O.astar3d(occ[q], S[q], G[q], with_expand=False)
         assert st[q] == ref["status"] and cost[q] == ref["cost"] and ne[q] == ref["n_expanded"], q
         assert np.array_equal(P[q, : pl[q]], ref["path_cells"]), q

@@ -68,7 +68,7 @@ def test_dwa_plan_dropin_against_reference():
 
 
 def test_c4_batch_against_oracle():
-    """C4: 256 agents x 4096 samples x H=30, one step; a sample of agents checked against the oracle,
+    """C4: 256 agents x 4096 samples x H=30, one step; every agent checked against the oracle, and
     properties on all."""
     import torch
 
@@ -95,7 +95,7 @@ def test_c4_batch_against_oracle():
     new_st = st_d.cpu().numpy()
     u = out["u"].cpu().numpy()
     obs = np.argwhere(occ).astype(np.float64)
-    for i in np.random.default_rng(0).choice(256, 12, replace=False):
+    for i in range(256):  # every agent against the oracle
         rc, ost, ou = O.dwa_step(obs, ref_paths[i], goals[i], states[i], nv=64, nw=64, predict_time=3.0)
         assert rc == status[i], i
         if rc != 0:
