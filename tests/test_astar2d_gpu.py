@@ -385,3 +385,24 @@ def test_c2_headline_schedule_against_oracle():
         _lib.check(ctx, L.pmp_astar2d_set_residency(ctx, 0), "residency")
         _lib.check(ctx, L.pmp_astar2d_set_engine(ctx, 1, 0), "engine")
         _lib.check(ctx, L.pmp_astar2d_reserve_auto(ctx), "reserve_auto")
+
+
+def test_dropin_heap_beyond_single_query_capacity():
+    """The drop-in AStar.plan() on a query whose heap (16,913 entries) outgrows the single-query
+    engine's LDS heap: the kernel reports PMP_CAP_OVERFLOW and plan() re-runs it with the full bound
+    (graph_search.AStar.plan) -- the answer, path and CLOSED order still equal the oracle's."""
+    from oracle import oracle as O
+
+    pmp = _pmp()
+    W = 1400
+    occ = np.zeros((W, W), np.uint8)
+    occ[0, :] = occ[-1, :] = occ[:, 0] = occ[:, -1] = 1
+    occ[W // 2, 1:W - 40] = 1  # a wall across most of the grid: A* floods the near half first
+    s, g = (W // 4, W // 2), (3 * W // 4, W // 2)
+    ref = O.astar2d(occ, s, g)
+    assert ref["status"] == 0 and ref["max_heap"] > 13440  # beyond the single-query engine's LDS heap
+    env = pmp.Grid(W, W)
+    env.update({(int(a), int(b)) for a, b in np.argwhere(occ)})
+    cost, path, expand = pmp.AStar(s, g, env).plan()
+    assert cost == ref["cost"] and path == ref["path"]
+    assert [n.current[0] * W + n.current[1] for n in expand] == ref["expand_cells"].tolist()
