@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4, call 21 / 24 (final head): the full GPU suite, smoke(), the driver's bench command, then the
+# round 4, calls 21 / 24 / 31 (final head): the full GPU suite, smoke(), the driver's bench command, then the
 # round profile's kernel-trace pass
 R=${GRAFT_REPO_ROOT:-/root/repo}
 cd $R
