@@ -589,15 +589,20 @@ def rrt_leg(args, torch, dist, world, rank):
             "streams": len(lanes), "timed_launches_checked": checked,
             "config": {"workload": "C3: Map(512,512), 40 rects + 40 circles (default_rng(7)), (5,5)->(505,505), "
                                    "65536 samples, max_dist 0.5, r 10, goal rate 0.05"},
-            "roofline": with_traffic({"bound": "l2", "achieved": achieved, "peak": L2_PEAK_GBS, "unit": "GB/s",
-                                      "frac": achieved / L2_PEAK_GBS, "traffic": None,
-                                      "algorithmic_bytes_per_launch": alg_bytes,
-                                      "bytes_note": "4 B per node scanned + 24 B per in-radius candidate, as loaded; "
-                                                    "traffic = HBM bytes (PMC), far below: the trees are cache-resident",
-                                      "survey_8d": {"bytes_per_launch": sv_bytes, "achieved": sv_gbs,
-                                                    "frac_l2": sv_gbs / L2_PEAK_GBS, "frac_hbm": sv_gbs / HBM_PEAK_GBS,
-                                                    "note": "SURVEY.md 8(d): 16 B xy per node scanned + 8 B g per "
-                                                            "in-radius node"}},
+            # frac on SURVEY.md 8(d)'s algorithmic bytes (the line's model, "bytes_model"), against the L2
+            # roof (the trees are L2 / Infinity-Cache resident); the kernel's own loads beside it
+            "roofline": with_traffic({"bound": "l2", "achieved": sv_gbs, "peak": L2_PEAK_GBS, "unit": "GB/s",
+                                      "frac": sv_gbs / L2_PEAK_GBS, "traffic": None,
+                                      "algorithmic_bytes_per_launch": sv_bytes,
+                                      "bytes_model": "8d: 16 B xy/node scanned + 8 B g/in-radius node",
+                                      "frac_hbm": sv_gbs / HBM_PEAK_GBS,
+                                      "bytes_note": "SURVEY.md 8(d): 16 B xy per node scanned + 8 B g per in-radius "
+                                                    "node; traffic = HBM bytes (PMC), far below: the trees are "
+                                                    "cache-resident",
+                                      "as_loaded": {"bytes_per_launch": alg_bytes, "achieved": achieved,
+                                                    "frac_l2": achieved / L2_PEAK_GBS,
+                                                    "note": "the kernel's own loads: 4 B per node scanned (16-bit "
+                                                            "fixed-point coarse copy) + 24 B per in-radius candidate"}},
                                      "rrt_kernel", "rrt_star"),
             "detail": {"found": int((status == 0).sum()), "mean_nodes": float(out["n_nodes"].float().mean().item()),
                        "iterations_per_launch": int(ctr[:, 0].sum()), "nodes_scanned_per_launch": int(ctr[:, 1].sum()),
@@ -1378,8 +1383,16 @@ def track_leg(args, torch, dist, world, rank, kind):
     xyd = torch.tensor(xy, dtype=torch.float64, device="cuda")
     offd = torch.tensor(off, dtype=torch.int32, device="cuda")
     _LABEL[0] = "lqr" if kind == "lqr" else "mpc_qp"
+    # the first (untimed) launch also counts the QP solves it runs (pmp_set_stats): the MFMA work of
+    # a launch is one assembly pass per solve, not per agent-step (rotation steps solve nothing)
+    solves_d = torch.zeros(1, dtype=torch.int64, device="cuda")
+    sctx = _lib.context()
+    L = _lib.load_library()
+    _lib.check(sctx, L.pmp_set_stats(sctx, solves_d.data_ptr()), "pmp_set_stats")
     o = batch.track_step_batch(kind, lp, st, gd, xyd, offd, iters=iters, u_p=up, **kw)
     torch.cuda.synchronize()
+    _lib.check(sctx, L.pmp_set_stats(sctx, None), "pmp_set_stats")
+    qp_solves = int(solves_d.item())
     stepped = int(o["n_steps"].sum().item())
     admm = int(o["admm_iters"].sum().item())
 
@@ -1419,15 +1432,20 @@ def track_leg(args, torch, dist, world, rank, kind):
     mfma = None
     if kind == "mpc":
         # per ADMM iteration ~ 16x16 inverse matvec (512) + scans/projections (~150); assembly 2*16*16*3p (MFMA)
-        flops = admm * 662.0 + stepped * 2 * 16 * 16 * 90
-        # the assembly's matrix-core work (track.hip mpc_rows): per agent-step ceil(3p / 16) row blocks
+        flops = admm * 662.0 + qp_solves * 2 * 16 * 16 * 90
+        # the assembly's matrix-core work (track.hip mpc_rows): per QP solve ceil(3p / 16) row blocks
         # x (2 MFMAs of y = S_x x + 4 K-slices x 2 MFMAs of H and g), 16 x 16 x 4 x 2 flops each
-        mfma_flops = stepped * (-(-90 // 16)) * 10 * 16 * 16 * 4 * 2.0
+        per_solve = (-(-90 // 16)) * 10
+        mfma_flops = qp_solves * per_solve * 16 * 16 * 4 * 2.0
         mfma_tf = mfma_flops / (kern_ms * 1e-3) / 1e12
         mfma = {"mfma_tflops": mfma_tf, "mfma_frac_of_fp64_peak": mfma_tf / 78.6,
-                "mfma_flops_per_agent_step": (-(-90 // 16)) * 10 * 16 * 16 * 4 * 2,
-                "note": "H = S_u' Q S_u, y = S_x x, g = (S_u' Q) y on v_mfma_f64_16x16x4_f64; the ADMM runs on "
-                        "the VALU (one 16x16 inverse per agent)"}
+                "mfma_util_pct_analytic": 100.0 * mfma_tf / 78.6,
+                "qp_solves_per_launch": qp_solves, "mfma_instructions_per_launch": qp_solves * per_solve,
+                "mfma_flops_per_qp_solve": per_solve * 16 * 16 * 4 * 2,
+                "note": "H = S_u' Q S_u, y = S_x x, g = (S_u' Q) y on v_mfma_f64_16x16x4_f64, one assembly per QP "
+                        "solve (pmp_set_stats count); the ADMM runs on the VALU (one 16x16 inverse per agent). "
+                        "mfma_tflops is over the whole launch (track_mpc_step + track_mpc_solve kernels); "
+                        "roofline.mfma_util_pct is the rocprofv3 busy-cycle figure of track_mpc_solve alone"}
     else:
         flops = stepped * 1200.0  # 3x3 Riccati update, 2x2 inverse, K e (lqr.py:116-141)
     achieved_tf = flops / (kern_ms * 1e-3) / 1e12
@@ -1492,6 +1510,10 @@ def compact_leg(rec: dict) -> dict:
         out["mfma_util_pct"] = _sig(roof["mfma_util_pct"], 3)
     if rec.get("mfma"):  # the matrix-core share of the leg's own arithmetic, live
         out["mfma_tflops"] = _sig(rec["mfma"]["mfma_tflops"], 3)
+        # the same work as a percentage of the f64 MFMA peak, comparable with mfma_util_pct
+        out["mfma_util_pct_analytic"] = _sig(rec["mfma"]["mfma_util_pct_analytic"], 3)
+    if roof.get("bytes_model"):
+        out["bytes_model"] = roof["bytes_model"]
     return out
 
 
@@ -1867,6 +1889,10 @@ def main():
         outs += [{k: b[k][j * nq:(j + 1) * nq] for k in ("cost", "plen", "nexp", "status")} for j in range(last_nb)]
     timed_checked = check_timed("astar2d", ref_out, outs)
     elapsed, kern_ms, span_ms = shard.max_over_ranks(dist, [elapsed, kern_ms, span_ms], "cuda")
+    # the ranks plan different pair sets (weak: default_rng(1 + rank); strong: dealt shares): the roofline
+    # is per GPU, on the mean over ranks of each rank's own algorithmic bytes against the max-over-ranks
+    # kernel time
+    bytes_per_batch = shard.sum_over_ranks(dist, [bytes_per_batch], "cuda")[0] / world
     bytes_per_launch = bytes_per_batch * float(np.mean(nbs))
     plans = (args.nq if args.scaling == "strong" else nq * world) * args.steps
     value = plans / elapsed
@@ -1970,8 +1996,9 @@ def main():
                        "batches_per_launch": B, "launches": nlaunch,
                        "expansions_per_batch": int(counters[:, 2].sum()),
                        "max_expansions_query": int(counters[:, 2].max()),
-                       "pushes_per_launch": int(counters[:, 0].sum()),
-                       "pops_per_launch": int(counters[:, 1].sum()),
+                       "pushes_per_batch": int(counters[:, 0].sum()),
+                       "pops_per_batch": int(counters[:, 1].sum()),
+                       "algorithmic_bytes_note": "per GPU: mean over ranks of each rank's own batch bytes",
                        "max_heap_entries": int(counters[:, 3].max()),
                        "expansions_all_ranks_per_step": int(counters_all[:, 2].sum()) if args.scaling == "strong" else None,
                        "strong_scaling_gather": gathered,

@@ -152,7 +152,10 @@ typedef struct {
  * evaluation (dwa.py:137-190: H-step Robot.lookforward rollout of every (v, w) sample, heading /
  * obstacle (cdist, capped at the inflation radius) / velocity, numpy pairwise-sum normalisation,
  * eval_win @ factor, first-index argmax) and Robot.kinematic (utils/agent/agent.py:68-116).
- * One workgroup per agent; agents never interact.
+ * One workgroup per agent, or -- with fewer agents than CUs and a fixed window (nv, nw > 0) -- k
+ * workgroups per agent, each on a leaf-aligned part of numpy's pairwise-sum tree over the samples,
+ * the last to finish combining the leaf sums in the tree's order and taking the argmax (the same bits
+ * as one workgroup; pmp_dwa_set_split).  Agents never interact.
  *   occ_bits [ceil(W*H/32)] u32  obstacle cells, cell (ox + i, oy + j) at bit i*H + j
  *   state    [na][5] f64  in/out  x, y, theta, v, w
  *   goal     [na][3] f64          goal pose
@@ -343,6 +346,12 @@ typedef struct {
  *   robot_vw [n][2] the robot's current (v, w) for linear/angularRegularization (local_planner.py:172-206)
  *   u [n][2]        regularised control
  */
+/* Workgroups per agent of pmp_dwa_step_batch: 0 (default) = auto (the device's CUs over the agents,
+ * at most 16, only for fixed windows nv, nw > 0), 1 = one workgroup per agent, k = k parts (reduced
+ * to the sample tree's leaf count; a part holds at most 1024 samples).  Results are identical for
+ * every setting. */
+int pmp_dwa_set_split(pmp_ctx* ctx, int parts);
+
 int pmp_lqr_control_batch(pmp_ctx* ctx, void* stream, const pmp_lp_params* lp, const pmp_lqr_params* lq, int n,
                           const double* s, const double* s_d, const double* u_r, const double* robot_vw, double* u);
 
@@ -449,6 +458,11 @@ int pmp_totp3d_batch(pmp_ctx* ctx, void* stream, const pmp_totp_params* prm, int
  * workers' first start and last end wall-clock ticks into span[0] (atomic min) and span[1] (atomic
  * max); the caller initialises span to {UINT64_MAX, 0}.  NULL switches it off. */
 int pmp_set_timing(pmp_ctx* ctx, uint64_t* span);
+/* Work counters for profiling: while set, every MPC pmp_track_step_batch launch of this context adds
+ * the number of QP solves it ran (agent-iterations whose MPC.plan branch called mpcControl,
+ * mpc.py:85-91) into stats[0] (atomic add; the caller zeroes it).  The matrix-core work of a launch
+ * is that count x ceil(3p / 16) x 10 v_mfma_f64_16x16x4 instructions.  NULL switches it off. */
+int pmp_set_stats(pmp_ctx* ctx, int64_t* stats);
 /* Rate of the wall-clock ticks above, in kHz. */
 int pmp_wall_clock_khz(pmp_ctx* ctx, int* khz);
 /* A* 2D query scheduling across the persistent workers: 1 (default) = longest start-goal distance
@@ -475,13 +489,16 @@ int pmp_astar2d_set_residency(pmp_ctx* ctx, int per_cu);
  * t2_lds = keep its level-10..14 heap direction bits in LDS (1) or HBM (0).  engine 0: one query per
  * wave (also Theta* / Lazy Theta*, and heaps of any size); on grids whose occupancy, cell state and
  * g fit in a wave's LDS share beside its heap (the README grid: 14 KB) all of them live in LDS.
- * engine 3: one query per workgroup with the CU's whole LDS as its heap (up to 13,440 entries beside
- * no grid; a query that outgrows it reports PMP_CAP_OVERFLOW) and the heap's choice bits in
+ * engine 3: one query per workgroup with the CU's whole LDS as its heap (pmp_astar2d_sq_cap entries:
+ * 13,632 beside no grid; a query that outgrows it reports PMP_CAP_OVERFLOW) and the heap's choice bits in
  * registers -- a single query's latency (the drop-in AStar.plan).  engine 1 (default): engine 3 for
  * batches of <= 256 queries whose heap capacity it holds, engine 2 for batches of >= 1024 queries on
  * grids too large for engine 0's LDS grid block, engine 0 otherwise.  Results are identical.
  * Applies to the next launch (re-reserves the scratch geometry when one is set). */
 int pmp_astar2d_set_engine(pmp_ctx* ctx, int engine, int t2_lds);
+/* Heap entries engine 3 holds for a W x H grid (its LDS beside the grid block it keeps in LDS on
+ * small grids); 0 = the grid leaves too little for the engine.  No device call. */
+int pmp_astar2d_sq_cap(int W, int H);
 
 /* Persistent workers (one wave each) per CU of the one-wave-per-query planners: pmp_graph3d_batch,
  * pmp_dstar2d_batch / pmp_dstar2d_onpress_batch, pmp_dstar3d_batch and pmp_lpastar3d_batch (default 16
@@ -502,8 +519,11 @@ int pmp_set_resident_per_cu(pmp_ctx* ctx, int per_cu);
 /* Pre-size the A* scratch (heap of heap_cap entries per concurrent query, up to max_slots
  * concurrent queries) so that later batch calls allocate nothing (hipGraph-capturable). */
 int pmp_astar2d_reserve(pmp_ctx* ctx, int W, int H, int max_slots, int heap_cap);
-/* The A* 2D scratch geometry in force: out[0..5] = {W, H, max_slots, heap_cap, multi-query engine
- * reserved (1/0), sized by the launches (1) or by pmp_astar2d_reserve (0)}; all 0 before any. */
+/* The A* 2D scratch geometry in force: out[0..5] = {W, H, max_slots, heap_cap in force, flags,
+ * sized by the launches (1) or by pmp_astar2d_reserve (0)}; all 0 before any.  flags: bit 0 the
+ * multi-query engine is reserved, bit 1 heap_cap was the caller's own (pmp_astar2d_reserve's
+ * heap_cap > 0) -- without it the geometry is restored with heap_cap = 0 (the default, which the
+ * engine may cut to its limit). */
 int pmp_astar2d_geometry(pmp_ctx* ctx, int32_t* out6);
 /* Forget the host's pmp_astar2d_reserve geometry: the next launch sizes the scratch for its own
  * batch and later larger batches grow it, as on a fresh context (allocated scratch is kept). */

@@ -32,6 +32,9 @@ SIGNATURES = {
     "pmp_astar2d_reserve_auto": (_i, [_vp]),
     "pmp_set_timing": (_i, [_vp, _vp]),
     "pmp_wall_clock_khz": (_i, [_vp, _vp]),
+    "pmp_set_stats": (_i, [_vp, _vp]),
+    "pmp_dwa_set_split": (_i, [_vp, _i]),
+    "pmp_astar2d_sq_cap": (_i, [_i, _i]),
     "pmp_astar2d_set_schedule": (_i, [_vp, _i]),
     "pmp_astar2d_set_priority": (_i, [_vp, _i]),
     "pmp_astar2d_set_residency": (_i, [_vp, _i]),

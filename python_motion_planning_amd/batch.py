@@ -74,23 +74,37 @@ def astar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: in
     if retry_overflow:
         redo = torch.nonzero(out["status"] == _lib.STATUS_CAP_OVERFLOW).flatten()
         if redo.numel():
-            full = 8 * W * H + 8
-            workers = max(1, min(int(redo.numel()), 256))
-            geo = np.zeros(6, np.int32)  # the geometry in force, restored after the re-run
-            _lib.check(ctx, L.pmp_astar2d_geometry(ctx, geo.ctypes.data), "pmp_astar2d_geometry")
-            _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, workers, full), "pmp_astar2d_reserve")
-            r = astar2d_batch((W, H), s[redo], g[redo], heuristic, path_cap, expand_cap, counters, occ_bits,
-                              retry_overflow=False, algo=algo)
+            r = astar2d_full_bound((W, H), s[redo], g[redo], heuristic, path_cap, expand_cap, counters, occ_bits,
+                                   algo=algo)
             for k in ("cost", "path_len", "path", "n_expanded", "status", "expand", "counters"):
                 if out[k] is not None:
                     out[k][redo] = r[k]
-            if geo[5] or not geo[0]:  # sized by the launches: keep it that way (grows with the batches)
-                _lib.check(ctx, L.pmp_astar2d_reserve_auto(ctx), "pmp_astar2d_reserve_auto")
-            else:  # the host's own reservation
-                _lib.check(ctx, L.pmp_astar2d_reserve(ctx, int(geo[0]), int(geo[1]), int(geo[2]), int(geo[3])),
-                           "pmp_astar2d_reserve")
     out["W"], out["H"] = W, H
     return out
+
+
+def astar2d_full_bound(shape, starts, goals, heuristic="euclidean", path_cap=None, expand_cap=0, counters=False,
+                       occ_bits=None, algo="astar"):
+    """The overflow re-plan: the queries (a few) planned with the full heap bound (8 W H + 8 entries,
+    which no search exceeds) on at most 256 workers, then the context's geometry restored as it was --
+    the host's own reservation (its explicit heap_cap, or the default when it asked for none, so the
+    engine choice of later batches is unchanged) or launch-sized scratch."""
+    W, H = shape
+    L, ctx = _lib.load_library(), _lib.context()
+    nq = int(starts.shape[0])
+    geo = np.zeros(6, np.int32)  # the geometry in force, restored after the re-run
+    _lib.check(ctx, L.pmp_astar2d_geometry(ctx, geo.ctypes.data), "pmp_astar2d_geometry")
+    _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, max(1, min(nq, 256)), 8 * W * H + 8), "pmp_astar2d_reserve")
+    try:
+        return astar2d_batch((W, H), starts, goals, heuristic, path_cap, expand_cap, counters, occ_bits,
+                             retry_overflow=False, algo=algo)
+    finally:
+        if geo[5] or not geo[0]:  # sized by the launches: keep it that way (grows with the batches)
+            _lib.check(ctx, L.pmp_astar2d_reserve_auto(ctx), "pmp_astar2d_reserve_auto")
+        else:  # the host's own reservation, with the capacity it asked for (0 = the default)
+            cap = int(geo[3]) if geo[4] & 2 else 0
+            _lib.check(ctx, L.pmp_astar2d_reserve(ctx, int(geo[0]), int(geo[1]), int(geo[2]), cap),
+                       "pmp_astar2d_reserve")
 
 
 _ONE = {}
@@ -205,12 +219,13 @@ def pack_paths(paths):
 
 
 def dwa_step_batch(grid, lp_params, dwa_params, state, goal, path_xy, path_off, iters: int = 1,
-                   want_eval: bool = False, want_traj: bool = False, want_hist: bool = False):
+                   want_eval: bool = False, want_traj: bool = False, want_hist: bool = False, parts: int = 0):
     """Batched DWA.plan iterations (dwa.py:72-93) on the gfx950 kernel dwa.hip.
 
     grid: (ox, oy, occ[W, H]) from obstacle_grid() (or with occ already a device bit tensor plus W, H).
     lp_params: _lib.LPParams; dwa_params: _lib.DWAParams.
     state [na, 5] f64 device tensor, updated in place; goal [na, 3]; path_xy / path_off from pack_paths().
+    parts: workgroups per agent (pmp_dwa_set_split: 0 auto, 1 one per agent, k); results are identical.
     Returns dict of device tensors (u, best, status, n_steps, optional hist_pose, eval, best_traj).
     """
     torch = _lib.device_check()
@@ -235,6 +250,7 @@ def dwa_step_batch(grid, lp_params, dwa_params, state, goal, path_xy, path_off, 
     out["eval"] = torch.zeros((na, 4096, 3), dtype=torch.float64, device="cuda") if want_eval else None
     out["best_traj"] = (torch.zeros((na, iters, max(H_steps, 1), 5), dtype=torch.float64, device="cuda")
                         if want_traj else None)
+    _lib.check(ctx, L.pmp_dwa_set_split(ctx, int(parts)), "pmp_dwa_set_split")
     rc = L.pmp_dwa_step_batch(ctx, _lib.stream_ptr(), occ_bits.data_ptr(),
                               ox, oy, W, H, ctypes.byref(lp_params), ctypes.byref(dwa_params), na, state.data_ptr(),
                               goal.data_ptr(), path_xy.data_ptr(), path_off.data_ptr(), int(iters),

@@ -1170,7 +1170,7 @@ extern "C" int pmp_astar2d_geometry(pmp_ctx* ctx, int32_t* out6)
     out6[1] = ctx->astar_H;
     out6[2] = ctx->astar_workers;
     out6[3] = ctx->astar_heap_cap;
-    out6[4] = ctx->astar_reserved_mq;
+    out6[4] = (ctx->astar_reserved_mq ? 1 : 0) | (ctx->astar_cap_explicit ? 2 : 0);
     out6[5] = ctx->astar_auto;
     return PMP_OK;
 }

@@ -160,6 +160,7 @@ struct GHeap {
     uint32_t gbase;  // kBlocks: this group's byte offset in the wave's spill region
     int L0;          // kBlocks: level of position cap (the first level with spilled positions)
     int cap;
+    __amdgpu_buffer_rsrc_t mirror;  // kMirror: the mirror of the wave's spill region
 };
 constexpr uint32_t kOOR = 0x80000000u;  // a buffer offset beyond any spill region: loads 0, stores dropped
 #ifndef PMP_MQ_SPILL_SHIFT
@@ -182,6 +183,16 @@ constexpr int kEntLds = kKeys ? 16 : 12;  // LDS bytes per heap position
 #define PMP_MQ_BLOCKS 1
 #endif
 constexpr bool kBlocks = PMP_MQ_BLOCKS != 0;
+// Write-traffic attribution (dev builds only, tools/build_variant.sh): every store of the selected
+// categories is issued twice, the copy into a mirror region with the same layout, so the extra
+// WRITE_SIZE over the default build is that category's write traffic.  Bits: 1 the trivial-push run's
+// spill stores, 2 a push rotation's spill stores, 4 a pop rotation's spill stores, 8 the cell-state
+// byte and G of a closed cell (even slots only: the mirror of every slot's 9 MB would not fit beside
+// the 15,360 slots' own, so that category's extra is doubled in the analysis).
+#ifndef PMP_MQ_MIRROR
+#define PMP_MQ_MIRROR 0
+#endif
+constexpr int kMirror = PMP_MQ_MIRROR;
 
 // byte offset of spilled heap position p (>= cap) in the wave's spill region
 __device__ __forceinline__ uint32_t spill_off(const GHeap& h, int p)
@@ -225,7 +236,7 @@ struct Ld {
         k = kKeys ? sel_lanes(m, kl, v.w) : hkey<HEUR>(c);
     }
 };
-__device__ __forceinline__ void hst(const GHeap& h, bool on, int p, double f, uint32_t c, uint32_t k)
+__device__ __forceinline__ void hst(const GHeap& h, bool on, int p, double f, uint32_t c, uint32_t k, int cat = 0)
 {
     if (on && p < h.cap) {
         h.F[p] = f;
@@ -237,6 +248,9 @@ __device__ __forceinline__ void hst(const GHeap& h, bool on, int p, double f, ui
     const uint32_t off = (on && p >= h.cap) ? spill_off(h, p) : kOOR;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
                                            h.spill, off, 0, 0);
+    if (kMirror & cat)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
+                                               h.mirror, off, 0, 0);
 }
 
 // ---- direction bits (astar2d.hip: bit(p) = !(heap[2p+1] < heap[2p+2]) for nodes with two children,
@@ -400,7 +414,7 @@ __device__ __forceinline__ int path_op(const GHeap& h, bool on, bool pop, uint32
     nf = atb ? Xf : (shift ? (pop ? upf : dnf) : Vf);
     nc = atb ? Xc : (shift ? (pop ? upc : dnc) : Vc);
     nk = atb ? Xk : (shift ? (pop ? upk : dnk) : Vk);
-    hst(h, on && (pop ? gl <= b : (gl >= b && lvl)), q, nf, nc, nk);
+    hst(h, on && (pop ? gl <= b : (gl >= b && lvl)), q, nf, nc, nk, pop ? 4 : 2);
     // the bits of the changed levels' parents: lane L (>= 1) sets its parent's from its new content
     // and its sibling's
     {
@@ -461,9 +475,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void as
         hp.gbase = (uint32_t)grp * (uint32_t)spill_n * 16u;
         hp.L0 = 31 - __clz(lds_cap + 1);
         hp.cap = lds_cap;
+        if (kMirror & 7)
+            hp.mirror = __builtin_amdgcn_make_buffer_rsrc(
+                spill_all + ((size_t)gridDim.x + blockIdx.x) * 4u * (size_t)spill_n, 0,
+                (int)(4u * (uint32_t)spill_n * 16u), 0x00020000);
     }
     uint8_t* cst = cst_all + slot * cst_bytes;
     double* G = G_all + slot * ((size_t)W * (size_t)H);
+    const size_t nslots = (size_t)gridDim.x * 4u;
+    const bool mir8 = (kMirror & 8) && (slot & 1u) == 0u;
+    uint8_t* cst_m = cst_all + (nslots + slot / 2) * cst_bytes;
+    double* G_m = G_all + (nslots + slot / 2) * ((size_t)W * (size_t)H);
 
     Walk wk;
     wk.init(gl);
@@ -587,7 +609,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void as
                 const uint32_t leftk = rank == 0 ? lastk : lkp;
                 bit_set<T2LDS>(hp, inrun && (pos & 1) == 0 && pos > 0, 30 - __clz(pos + 1), (uint32_t)(pos + 1) >> 1,
                                !key_lt(leftf, leftk, ifv, ikk));
-                hst(hp, inrun, pos, ifv, icm, ikk);
+                hst(hp, inrun, pos, ifv, icm, ikk, 1);
                 const int top = 31 - __clz(run);
                 lastf = bpf(ifv, gb + top);
                 lastc = bp(icm, gb + top);
@@ -719,6 +741,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void as
                 // CLOSED[node.current] = node (a_star.py:82)
                 if (gl == 0) cst[nlin] = (uint8_t)((ep << 4) | (uint32_t)(ndir + 1));
                 if (!GZERO && gl == 1) G[nlin] = gnode;
+                if (mir8 && gl == 0) cst_m[nlin] = (uint8_t)((ep << 4) | (uint32_t)(ndir + 1));
+                if (mir8 && !GZERO && gl == 1) G_m[nlin] = gnode;
                 if (gl == 2 && expand_out && nexp < expand_cap)
                     expand_out[(size_t)q * expand_cap + nexp] = nlin | ((uint32_t)ndir << 28);
                 nexp++;
@@ -798,8 +822,9 @@ int pmp_astar2d_slot_scratch(pmp_ctx* ctx, hipStream_t s, size_t slots, int W, i
 {
     const size_t cb = mq_cst_bytes(W, H);
     const size_t ncell = (size_t)W * H;
-    *cst = (uint8_t*)pmp_scratch(ctx, SCR_MQ_CST, slots * cb + 16);
-    *G = (double*)pmp_scratch(ctx, SCR_MQ_G, slots * ncell * 8 + 16);
+    const size_t ms = (kMirror & 8) ? slots + slots / 2 + 1 : slots;  // kMirror: the even slots' mirrors
+    *cst = (uint8_t*)pmp_scratch(ctx, SCR_MQ_CST, ms * cb + 16);
+    *G = (double*)pmp_scratch(ctx, SCR_MQ_G, ms * ncell * 8 + 16);
     const bool fresh_epochs = ctx->cap[SCR_MQ_EPOCH] < slots * 4 || ctx->astar_mq_epoch_slots < slots ||
                               ctx->astar_mq_cst_bytes != cb;
     *ep = (uint32_t*)pmp_scratch(ctx, SCR_MQ_EPOCH, slots * 4 + 16);
@@ -846,7 +871,7 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
         spill_n = (int)(blocks * 8);
     }
     const size_t slots = (size_t)waves * 4;
-    uint4* spill = (uint4*)pmp_scratch(ctx, SCR_MQ_SPILL, slots * (size_t)spill_n * 16 + 16);
+    uint4* spill = (uint4*)pmp_scratch(ctx, SCR_MQ_SPILL, (kMirror & 7 ? 2 : 1) * slots * (size_t)spill_n * 16 + 16);
     uint32_t* t2 = (uint32_t*)pmp_scratch(ctx, SCR_MQ_T2, slots * kT2Words * 4 + 16);
     if (!spill || !t2) return PMP_ENOMEM;
     uint8_t* cstp;

@@ -594,7 +594,7 @@ bool sq_ldsg(size_t ncell) { return sq_grid_bytes(ncell) + (size_t)12 * kSqMinCa
 }  // namespace
 
 // Heap positions the single-query engine holds in LDS for a W x H grid (0: none worth it).
-int pmp_astar2d_sq_cap(int W, int H)
+extern "C" int pmp_astar2d_sq_cap(int W, int H)
 {
     const size_t ncell = (size_t)W * H;
     const size_t grid = sq_ldsg(ncell) ? sq_grid_bytes(ncell) : 0;

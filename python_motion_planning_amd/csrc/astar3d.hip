@@ -36,16 +36,7 @@ struct Key3 {
     static constexpr bool kStoredF = true;
     int gx, gy, gz;
     int heur;  // 0 euclidean, 1 manhattan, 2 zero (Dijkstra3D: h = 0, dijkstra3d.py:34,83)
-    int Y, Z;  // grid dims for cell(): the decrease-key position map
-
-    // an entry pushed beside a pending entry of its cell with the same f (below) is not tracked
-    static constexpr uint32_t kUntracked = 1u << 29;
-    static __device__ __forceinline__ bool tracked(const Ent& e) { return !(e.b & kUntracked); }
-    __device__ __forceinline__ uint32_t cell(const Ent& e) const
-    {
-        const uint32_t x = (e.b >> 21) & 255u, y = (e.b >> 13) & 255u, z = (e.b >> 5) & 255u;
-        return (x * (uint32_t)Y + y) * (uint32_t)Z + z;
-    }
+    int Y, Z;
 
     __device__ __forceinline__ uint32_t hkey(uint32_t b) const
     {
@@ -134,9 +125,6 @@ __device__ __forceinline__ double dist3(int dx, int dy, int dz)  // Planner3D.di
 // LazyThetaStar3D (lazy_theta_star3d.py:41-128).  Theta modes keep any-voxel parents: a per-cell
 // CLOSED parent (cpar) and, per push, the entry's parent in a side table indexed by the push
 // counter (ppar), since an entry's parent may be its pusher's parent.
-#ifndef PMP_A3_DKEY
-#define PMP_A3_DKEY 0
-#endif
 #ifndef PMP_A3_WAVES
 #define PMP_A3_WAVES 5  // waves per SIMD the A* / Dijkstra / GBFS variants are compiled for (A/B switch)
 #endif
@@ -148,7 +136,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
     uint32_t* __restrict__ expand_out, int expand_cap, int64_t* __restrict__ counters, int32_t* __restrict__ status_out,
     int* __restrict__ queue, uint4* __restrict__ spill_all, int heap_cap, int lds_cap, uint8_t* __restrict__ cdir_all,
     double* __restrict__ cg_all, int gzero, uint32_t* __restrict__ cpar_all, uint32_t* __restrict__ ppar_all,
-    uint32_t ppar_cap, const int32_t* __restrict__ order, int prio_n, uint32_t* __restrict__ hpos_all)
+    uint32_t ppar_cap, const int32_t* __restrict__ order, int prio_n)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
@@ -158,14 +146,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
     const size_t spill_n = (size_t)(heap_cap > lds_cap ? heap_cap - lds_cap : 0);
     heap16::Heap hp =
         heap16::make_heap<true>(smem, lds_cap, spill_all + (size_t)worker * spill_n * 2, spill_n);  // 32 B records
-    // PMP_A3_DKEY (A/B switch, off): A* / Dijkstra / GBFS keep one entry per pending cell -- an
-    // improved g replaces the cell's entry in place (decrease-key through a cell -> position map)
-    // instead of leaving a dead duplicate that would pop later and be skipped.  The key is a total
-    // order, so the live entries pop in the same order either way (parity green); the heap is smaller
-    // and those stale pops are gone, but the map's stores and corrections cost more issue slots than
-    // the pops they save on this issue-bound loop (round 4, same box: 1.71 M vs 1.84 M plans/s).
-    constexpr bool POS = THETA == 0 && PMP_A3_DKEY != 0;
-    if (POS) hp.hpos = hpos_all + (size_t)worker * ncell;
     lds_w32* occl = (lds_w32*)(smem + (size_t)heap16::lds_entry_bytes<true>() * lds_cap);  // OCC_LDS: the query's bitmap
     uint8_t* cdir = cdir_all + (size_t)worker * ncell;
     double* cg = cg_all + (size_t)worker * 2 * ncell;  // closed g
@@ -197,7 +177,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
         for (size_t i = lane; i < ncell; i += 64) {
             cdir[i] = 0;
             og[i] = __builtin_inf();
-            if (POS) hp.hpos[i] = heap16::kNoPos;
         }
         heap16::wsync();
         const int sx = start_xyz[3 * q], sy = start_xyz[3 * q + 1], sz = start_xyz[3 * q + 2];
@@ -226,7 +205,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
         root.b = scm;
         qc.set_f(root);
         if (lane == 0) heap16::store<true, true>(hp, 0, root);
-        if (POS && lane == 0) hp.hpos[((uint32_t)sx * (uint32_t)Y + (uint32_t)sy) * (uint32_t)Z + (uint32_t)sz] = 0u;
         if (THETA && lane == 0) ppar[0] = ((uint32_t)sx * (uint32_t)Y + (uint32_t)sy) * (uint32_t)Z + (uint32_t)sz;
         heap16::wsync();
         int n = 1;
@@ -266,9 +244,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
             // loaded on every lane (no zero-filled destination, see above)
             uint32_t epar = 0;
             if (THETA) epar = ppar[node.a < ppar_cap ? node.a : 0u];
-            // POS: the neighbour's pending entry position (before this expansion's operations)
-            uint32_t npos = heap16::kNoPos;
-            if (POS) npos = hp.hpos[nlin];
             if (lane < 26) {
                 if (OCC_LDS) {
 #define OCC(a, b, c) occ3l(occl, X, Y, Z, a, b, c)
@@ -298,20 +273,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
 #ifdef PMP_STAMPS
             const uint64_t ts0 = __builtin_amdgcn_s_memtime();
 #endif
-            int hole = 0;
             if (n > 0) {
-                if (n < lds_cap) hole = heap16::pop<Key3, false, true, POS>(hp, qc, n, root, lane, pop_jl, pop_ol, pop_w);
-                else hole = heap16::pop<Key3, true, true, POS>(hp, qc, n, root, lane, pop_jl, pop_ol, pop_w);
-            }
-            if (POS) {
-                // the popped entry left the heap; the pop moved the path below the root up one level
-                // and the old last entry (position n) to the hole
-                if (lane == 0) hp.hpos[lin] = heap16::kNoPos;
-                if (n > 0 && npos != heap16::kNoPos) {
-                    const int d = heap16::level_of(hole) - heap16::level_of((int)npos);
-                    if (npos == (uint32_t)n) npos = (uint32_t)hole;
-                    else if (npos != 0u && d >= 0 && (((uint32_t)hole + 1u) >> d) == npos + 1u) npos = (npos - 1u) >> 1;
-                }
+                if (n < lds_cap) heap16::pop<Key3, false, true>(hp, qc, n, root, lane, pop_jl, pop_ol, pop_w);
+                else heap16::pop<Key3, true, true>(hp, qc, n, root, lane, pop_jl, pop_ol, pop_w);
             }
 #ifdef PMP_STAMPS
             const uint64_t ts1 = __builtin_amdgcn_s_memtime();
@@ -462,18 +426,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
             item.a = 0u;
             item.b = ((((uint32_t)nx & 255u) << 16) | (((uint32_t)ny & 255u) << 8) | ((uint32_t)nz & 255u)) << 5 | (uint32_t)(lane < 26 ? lane : 0);
             qc.set_f(item);
-            bool fbelow = false;  // POS: item.f < f of the cell's pending entry (g = nog)
-            if (POS) {
-                Ent pend = item;
-                pend.g = nog;
-                qc.set_f(pend);
-                fbelow = item.f < pend.f;
-            }
             bool overflow = false;
 #ifndef PMP_A3_BATCH
 #define PMP_A3_BATCH 1
 #endif
-            if (THETA == 0 && !POS && PMP_A3_BATCH && vm) {
+            if (THETA == 0 && PMP_A3_BATCH && vm) {
                 // The key is a total order, so the heap's shape is free: the live neighbours are stored
                 // together at n, n + 1, ... (lane order) in one round, and only the ones below their
                 // parent (an entry from before this batch; else assumed below) sift up afterwards, in
@@ -498,26 +455,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA == 0 ?
                     if (it.a >= ppar_cap) { overflow = true; break; }
                     if (lane == 0) ppar[it.a] = rl_u32(qpar, m);
                 }
-                // decrease-key only when the new f is strictly below the pending entry's (nog + h): with
-                // equal f the reference's older entry pops first (smaller counter) and expands the cell
-                // with its g, then the newer one expands it again -- so it is pushed beside it instead,
-                // untracked (its moves leave the position map alone)
-                const uint32_t pm = POS ? rl_u32(npos, m) : heap16::kNoPos;
-                const bool dk = POS && pm != heap16::kNoPos && rl_u32(fbelow ? 1u : 0u, m) != 0u;
-                int p0 = n;
-                if (dk) p0 = (int)pm;
-                else if (n >= heap_cap) { overflow = true; break; }
-                if (POS && !dk && pm != heap16::kNoPos) it.b |= Key3::kUntracked;
-                int ip;
-                if (p0 < lds_cap) ip = heap16::sift_up<Key3, false, POS>(hp, qc, p0, it, root, lane);
-                else ip = heap16::sift_up<Key3, true, POS>(hp, qc, p0, it, root, lane);
-                if (!dk) n += 1;
-                if (POS && npos != heap16::kNoPos) {
-                    // the ancestors of p0 from ip down moved one level toward p0
-                    const int d = heap16::level_of(p0) - heap16::level_of((int)npos);
-                    if (d >= 1 && (((uint32_t)p0 + 1u) >> d) == npos + 1u && heap16::level_of((int)npos) >= heap16::level_of(ip))
-                        npos = (((uint32_t)p0 + 1u) >> (d - 1)) - 1u;
-                }
+                if (n >= heap_cap) { overflow = true; break; }
+                if (n < lds_cap) heap16::sift_up<Key3, false>(hp, qc, n, it, root, lane);
+                else heap16::sift_up<Key3, true>(hp, qc, n, it, root, lane);
+                n += 1;
             }
             seq += (uint32_t)__popc(okm);
 #ifdef PMP_STAMPS
@@ -655,7 +596,7 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     {
         // per-context scratch budget: fewer workers (each pulls more queries) rather than ENOMEM
         const size_t per_worker = spill_n * kSpill + ncell + ncell * 16 +
-                                  (theta ? ((size_t)ncell + ppar_cap) * 4 : (PMP_A3_DKEY ? ncell * 4 : 0));
+                                  (theta ? ((size_t)ncell + ppar_cap) * 4 : 0);
         const size_t fit = kScratchBudget3 / per_worker;
         if (fit < 1) return pmp_set_err(ctx, PMP_ENOMEM, "pmp_graph3d_batch: one worker exceeds the scratch budget");
         if ((size_t)workers > fit) workers = (int)fit;
@@ -664,9 +605,9 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
     uint8_t* cdir = (uint8_t*)pmp_scratch(ctx, SCR_AUX2, (size_t)workers * ncell + 16);
     double* cg = (double*)pmp_scratch(ctx, SCR_AUX3, (size_t)workers * ncell * 16 + 16);  // closed g + pending g
     int* queue = (int*)pmp_scratch(ctx, SCR_AUX0, 256);
-    uint32_t* tpar = nullptr;  // theta: CLOSED parents + push parents; PMP_A3_DKEY: the heap position map
-    if (theta || PMP_A3_DKEY) {
-        tpar = (uint32_t*)pmp_scratch(ctx, SCR_AUX4, (size_t)workers * (theta ? ncell + ppar_cap : ncell) * 4 + 16);
+    uint32_t* tpar = nullptr;  // theta: CLOSED parents + push parents
+    if (theta) {
+        tpar = (uint32_t*)pmp_scratch(ctx, SCR_AUX4, (size_t)workers * (ncell + ppar_cap) * 4 + 16);
         if (!tpar) return PMP_ENOMEM;
     }
     if (!spill || !cdir || !cg || !queue) return PMP_ENOMEM;
@@ -683,7 +624,7 @@ extern "C" int pmp_graph3d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
                        algo == PMP_ALGO_DIJKSTRA ? 2 : heuristic, start_xyz, goal_xyz, nq, cost, path_len, path, path_cap,
                        n_expanded, expand, expand_cap, counters, status, queue, spill, heap_cap, lds_cap, cdir, cg,
                        algo == PMP_ALGO_GBFS ? 1 : 0, theta ? tpar : nullptr, theta ? tpar + (size_t)workers * ncell : nullptr,
-                       ppar_cap, (const int32_t*)order, order ? ctx->astar_prio_n : 0, theta ? nullptr : tpar);
+                       ppar_cap, (const int32_t*)order, order ? ctx->astar_prio_n : 0);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }

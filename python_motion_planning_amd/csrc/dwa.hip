@@ -148,6 +148,50 @@ __device__ inline double pw_combine(const double* leafsum, int n, int& leaf)
     return 0.0;
 }
 
+// One sample's H-step rollout (dwa.py:152-160 via Robot.lookforward) and the stencil's minimum
+// squared obstacle distance along it.  min over cells of sqrt(d2) == sqrt(min d2): sqrt is monotone
+// and correctly rounded, so one square root per sample (scipy cdist: d = sqrt(dx*dx + dy*dy), no fused
+// multiply-add).  cos/sin of th_k by rotation (sd, cd = sin / cos(dt * w)): th_k = th_0 + k*(dt*w) up
+// to the rounding of the running sum (which pass 3 recomputes exactly as the reference), so (cs, sn)
+// stay within ~2e-14 of libm's cos/sin(th_k) over the horizon -- one sincos pair per sample.
+template <bool OCC_LDS>
+__device__ inline void rollout(const uint32_t* __restrict__ occ, const lds_w32* occl, int ox, int oy, int W, int H,
+                               double R, double dt, int Hh, double x, double y, double sn, double cs, double sd,
+                               double cd, double v, double& xo, double& yo, double& mind2o)
+{
+    double mind2 = INFINITY;
+    for (int k = 0; k < Hh; k++) {
+        const double nx = x + (dt * cs) * v, ny = y + (dt * sn) * v;
+        const double ncs = cs * cd - sn * sd, nsn = sn * cd + cs * sd;
+        cs = ncs;
+        sn = nsn;
+        x = nx;
+        y = ny;
+        const int x0 = (int)ceil(x - R), x1 = (int)floor(x + R);
+        const int y0 = (int)ceil(y - R), y1 = (int)floor(y + R);
+        // the stencil row by row: one bit run per row, distances only for its set bits (cells outside
+        // the grid are not obstacles); rows of up to 32 cells per run, so any inflation radius is covered
+        const int j0 = max(y0 - oy, 0), j1 = min(y1 - oy, H - 1);
+        for (int jc = j0; jc <= j1; jc += 32)
+            for (int cx = x0; cx <= x1; cx++) {
+                const int i = cx - ox;
+                if ((unsigned)i >= (unsigned)W) continue;
+                const int nrun = min(32, j1 - jc + 1);
+                uint32_t run = OCC_LDS ? occ_run(occl, H, i, jc, nrun) : occ_run(occ, H, i, jc, nrun);
+                while (run) {
+                    const int b = __ffs(run) - 1;
+                    run &= run - 1;
+                    const double dx = (double)cx - x, dy = (double)(oy + jc + b) - y;
+                    const double d2 = dx * dx + dy * dy;
+                    if (d2 < mind2) mind2 = d2;
+                }
+            }
+    }
+    xo = x;
+    yo = y;
+    mind2o = mind2;
+}
+
 template <bool OCC_LDS>
 __global__ __launch_bounds__(kThreads) void dwa_kernel(
     const uint32_t* __restrict__ occ, int ox, int oy, int W, int H, pmp_lp_params P, pmp_dwa_params D, int na,
@@ -208,44 +252,9 @@ __global__ __launch_bounds__(kThreads) void dwa_kernel(
         __syncthreads();
         const double sn0 = S.sn0, cs0 = S.cs0;
         for (int c = tid; c < N; c += kThreads) {
-            const double v = linsp_at(LV, c / nw);
-            double x = st[0], y = st[1];
-            // min over cells of sqrt(d2) == sqrt(min d2): sqrt is monotone and correctly rounded, so
-            // one square root per sample (scipy cdist: d = sqrt(dx*dx + dy*dy), no fused multiply-add)
-            double mind2 = INFINITY;
-            // cos/sin of th_k by rotation: th_k = th_0 + k*(dt*w) up to the rounding of the running
-            // sum (which pass 3 recomputes exactly as the reference), so (cs, sn) stay within ~2e-14
-            // of libm's cos/sin(th_k) over the horizon -- one sincos pair per sample, not per step.
-            double sn = sn0, cs = cs0;
-            const double sd = S.col[1][c], cd = S.col[2][c];
-            for (int k = 0; k < Hh; k++) {
-                const double nx = x + (dt * cs) * v, ny = y + (dt * sn) * v;
-                const double ncs = cs * cd - sn * sd, nsn = sn * cd + cs * sd;
-                cs = ncs;
-                sn = nsn;
-                x = nx;
-                y = ny;
-                const int x0 = (int)ceil(x - R), x1 = (int)floor(x + R);
-                const int y0 = (int)ceil(y - R), y1 = (int)floor(y + R);
-                // the stencil row by row: one bit run per row, distances only for its set bits
-                // (cells outside the grid are not obstacles); rows of up to 32 cells per run, so any
-                // inflation radius is covered
-                const int j0 = max(y0 - oy, 0), j1 = min(y1 - oy, H - 1);
-                for (int jc = j0; jc <= j1; jc += 32)
-                    for (int cx = x0; cx <= x1; cx++) {
-                        const int i = cx - ox;
-                        if ((unsigned)i >= (unsigned)W) continue;
-                        const int nrun = min(32, j1 - jc + 1);
-                        uint32_t run = OCC_LDS ? occ_run(occl, H, i, jc, nrun) : occ_run(occ, H, i, jc, nrun);
-                        while (run) {
-                            const int b = __ffs(run) - 1;
-                            run &= run - 1;
-                            const double dx = (double)cx - x, dy = (double)(oy + jc + b) - y;
-                            const double d2 = dx * dx + dy * dy;
-                            if (d2 < mind2) mind2 = d2;
-                        }
-                    }
-            }
+            double x, y, mind2;
+            rollout<OCC_LDS>(occ, occl, ox, oy, W, H, R, dt, Hh, st[0], st[1], sn0, cs0, S.col[1][c], S.col[2][c],
+                             linsp_at(LV, c / nw), x, y, mind2);
             S.col[0][c] = x;
             S.col[1][c] = mind2;
             S.col[2][c] = y;
@@ -334,7 +343,239 @@ __global__ __launch_bounds__(kThreads) void dwa_kernel(
     }
 }
 
+// ---- k-split: one agent's samples over k workgroups ------------------------------------------------
+// With fewer agents than CUs (the 8-GPU strong split gives a rank 32 of C4's 256 agents) the kernel
+// above keeps one CU per agent and the step time at one agent's latency.  Here part p of k workgroups
+// takes the numpy pairwise tree's leaves [nl p / k, nl (p + 1) / k) of the agent's N samples (dwa.py:
+// 176-181: leaves of <= 128 samples, splits at multiples of 8), evaluates them and stores their three
+// columns and leaf sums; the part that arrives last (an agent-scope arrival counter) combines the leaf
+// sums in the tree's own order -- the same tree, so the same bits as one workgroup -- then scores all N
+// samples, takes the first-index argmax (dwa.py:89) and moves the robot.  One launch per plan
+// iteration (the next iteration needs the moved state); an agent that stopped (goal reached, a
+// reference raise) is skipped by later launches through its status.
+constexpr int kSplitThreads = 512;
+constexpr int kSplitChunk = 1024;  // samples of one part held in LDS
+
+struct DwaSplitShared {
+    uint32_t occ[kOccLdsWords];
+    double col[3][kSplitChunk];
+    int leaf_lo[kMaxLeaves], leaf_n[kMaxLeaves];
+    double redd[kSplitThreads / 64];
+    int redi[kSplitThreads / 64];
+    double sums[3];
+    double sn0, cs0;
+    double pt[2];
+    int nleaves;
+    int last;
+};
+
+struct DwaSplitScratch {
+    double* cols;     // [na][3][kMaxN]
+    double* leafsum;  // [na][3][kMaxLeaves]
+    int* cnt;         // [na] arrivals of this launch (reset to 0 by the last part)
+};
+
+template <bool OCC_LDS>
+__global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
+    const uint32_t* __restrict__ occ, int ox, int oy, int W, int H, pmp_lp_params P, pmp_dwa_params D, int na, int k,
+    int it, int iters, double* __restrict__ state, const double* __restrict__ goal, const double* __restrict__ path_xy,
+    const int32_t* __restrict__ path_off, double* __restrict__ u_out, int32_t* __restrict__ best_out,
+    int32_t* __restrict__ status_out, int32_t* __restrict__ nsteps_out, double* __restrict__ hist_pose,
+    double* __restrict__ eval_out, double* __restrict__ best_traj, DwaSplitScratch X)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    DwaSplitShared& S = *reinterpret_cast<DwaSplitShared*>(smem_raw);
+    const int a = blockIdx.x / k, part = blockIdx.x - a * k;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    if (a >= na) return;
+    if (it > 0 && status_out[a] != 0) return;  // stopped in an earlier iteration (block-uniform)
+    double st[5];
+    for (int q = 0; q < 5; q++) st[q] = state[5 * a + q];
+    // a stop in this iteration: part 0 records it (at it = 0 also the outputs of a plan that never moved)
+    auto stop = [&](int status) {
+        if (part == 0 && tid == 0) {
+            status_out[a] = status;
+            if (it == 0) {
+                u_out[2 * a] = st[3];
+                u_out[2 * a + 1] = st[4];
+                best_out[a] = 0;
+                nsteps_out[a] = 0;
+            }
+        }
+    };
+    if (lp::reach_goal(st, goal + 3 * a, P)) { stop(PMP_FOUND + 1); return; }
+    if (OCC_LDS) {
+        const int words = (int)(((size_t)W * H + 31) / 32);
+        for (int i = tid; i < words; i += nt) S.occ[i] = occ[i];
+    }
+    const lds_w32* occl = (const lds_w32*)S.occ;
+    const double* path = path_xy + 2 * (size_t)path_off[a];
+    const int Pn = path_off[a + 1] - path_off[a];
+    const double dt = P.dt;
+    const int Hh = (int)(D.predict_time / dt);
+    const double R = D.inflation;
+    double pt[2] = {0, 0}, theta = 0, kappa = 0;
+    const int ls = lp::lookahead_block(path, Pn, st[0], st[1], st[3], P, pt, &theta, &kappa, S.redd, S.redi);
+    if (tid == 0) { S.pt[0] = pt[0]; S.pt[1] = pt[1]; }
+    __syncthreads();
+    if (ls) { stop(PMP_REF_RAISES); return; }
+    const double gx = S.pt[0], gy = S.pt[1];
+    const double vr0 = fmax(P.min_v, st[3] + P.min_v_inc * dt), vr1 = fmin(P.max_v, st[3] + P.max_v_inc * dt);
+    const double vr2 = fmax(P.min_w, st[4] + P.min_w_inc * dt), vr3 = fmin(P.max_w, st[4] + P.max_w_inc * dt);
+    const int nv = D.nv, nw = D.nw;  // the host splits only windows of fixed size (nv, nw > 0)
+    const int N = nv * nw;
+    const Linsp LV = make_linsp(vr0, vr1, nv), LW = make_linsp(vr2, vr3, nw);
+    if (tid == 0) {
+        int nl = 0;
+        pw_leaves<kPwDepth>(0, N, S.leaf_lo, S.leaf_n, nl);
+        S.nleaves = nl;
+        sincos(st[2], &S.sn0, &S.cs0);
+    }
+    __syncthreads();
+    const int nl = S.nleaves;
+    const int l0 = (int)(((long)nl * part) / k), l1 = (int)(((long)nl * (part + 1)) / k);
+    const int c0 = l0 < nl ? S.leaf_lo[l0] : N, c1 = l1 < nl ? S.leaf_lo[l1] : N;
+    // the three passes of dwa_kernel over this part's samples (LDS index c - c0)
+    for (int c = c0 + tid; c < c1; c += nt)
+        sincos(dt * linsp_at(LW, c % nw), &S.col[1][c - c0], &S.col[2][c - c0]);
+    __syncthreads();
+    const double sn0 = S.sn0, cs0 = S.cs0;
+    for (int c = c0 + tid; c < c1; c += nt) {
+        double x, y, mind2;
+        rollout<OCC_LDS>(occ, occl, ox, oy, W, H, R, dt, Hh, st[0], st[1], sn0, cs0, S.col[1][c - c0],
+                         S.col[2][c - c0], linsp_at(LV, c / nw), x, y, mind2);
+        S.col[0][c - c0] = x;
+        S.col[1][c - c0] = mind2;
+        S.col[2][c - c0] = y;
+    }
+    double* cols = X.cols + (size_t)a * 3 * kMaxN;
+    double* lsum = X.leafsum + (size_t)a * 3 * kMaxLeaves;
+    for (int c = c0 + tid; c < c1; c += nt) {
+        const double v = linsp_at(LV, c / nw), w = linsp_at(LW, c % nw);
+        double th = st[2];
+        for (int q = 0; q < Hh; q++) th = th + dt * w;
+        const double ang = atan2(gy - S.col[2][c - c0], gx - S.col[0][c - c0]);
+        const double h = lp::kPi - fabs(ang - th);
+        const double mind = sqrt(S.col[1][c - c0]);
+        const double o = mind < R ? mind : R;
+        const double vel = fabs(v);
+        S.col[0][c - c0] = h;
+        S.col[1][c - c0] = o;
+        S.col[2][c - c0] = vel;
+        cols[c] = h;
+        cols[kMaxN + c] = o;
+        cols[2 * kMaxN + c] = vel;
+    }
+    __syncthreads();
+    {
+        const int ml = l1 - l0;
+        if (tid < 3 * ml) {
+            const int cidx = tid / ml, l = l0 + tid % ml;
+            lsum[cidx * kMaxLeaves + l] = pw_leaf(&S.col[cidx][S.leaf_lo[l] - c0], S.leaf_n[l]);
+        }
+    }
+    // arrival: release this part's columns and leaf sums at agent scope; the last part goes on
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(X.cnt + a, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        S.last = old == k - 1;
+    }
+    __syncthreads();
+    if (!S.last) return;
+    __threadfence();
+    if (tid == 0) X.cnt[a] = 0;
+    if (tid < 3) {
+        int leaf = 0;
+        S.sums[tid] = 0.0 + pw_combine<kPwDepth>(lsum + tid * kMaxLeaves, N, leaf);
+    }
+    __syncthreads();
+    const double s0 = S.sums[0], s1 = S.sums[1], s2 = S.sums[2];
+    double bs = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int c = tid; c < N; c += nt) {
+        const double e0 = linsp_at(LV, c / nw), e1 = linsp_at(LW, c % nw);
+        const double h = cols[c], o = cols[kMaxN + c], vel = cols[2 * kMaxN + c];
+        const double e2 = s0 != 0 ? h / s0 : h;
+        const double e3 = s1 != 0 ? o / s1 : o;
+        const double e4 = s2 != 0 ? vel / s2 : vel;
+        const double sc = fma(e4, D.velocity_weight, fma(e3, D.obstacle_weight, fma(e2, D.heading_weight, fma(e1, 0.0, e0 * 0.0))));
+        if (eval_out && it == iters - 1) {
+            double* e = eval_out + ((size_t)a * kMaxN + c) * 3;
+            e[0] = fma(e4, 0.0, fma(e3, 0.0, fma(e2, 0.0, fma(e1, 0.0, e0 * 1.0))));
+            e[1] = fma(e4, 0.0, fma(e3, 0.0, fma(e2, 0.0, fma(e1, 1.0, e0 * 0.0))));
+            e[2] = sc;
+        }
+        if (sc > bs || bi == 0x7fffffff) { bs = sc; bi = c; }
+    }
+    lp::block_best<false>(bs, bi, S.redd, S.redi);
+    const int best = bi;
+    const double u0 = linsp_at(LV, best / nw), u1 = linsp_at(LW, best % nw);
+    if (tid == 0) {
+        if (hist_pose) {
+            double* hp = hist_pose + ((size_t)a * iters + it) * 3;
+            hp[0] = st[0]; hp[1] = st[1]; hp[2] = st[2];
+        }
+        if (best_traj) {
+            double x = st[0], y = st[1], th = st[2];
+            for (int q = 0; q < Hh; q++) {
+                double sn, cs;
+                sincos(th, &sn, &cs);
+                const double nx = x + (dt * cs) * u0, ny = y + (dt * sn) * u0, nth = th + dt * u1;
+                x = nx; y = ny; th = nth;
+                double* bt = best_traj + (((size_t)a * iters + it) * Hh + q) * 5;
+                bt[0] = x; bt[1] = y; bt[2] = th; bt[3] = u0; bt[4] = u1;
+            }
+        }
+        // Robot.kinematic(u, dt) (agent.py:68-89)
+        double sn, cs;
+        sincos(st[2], &sn, &cs);
+        const double nx = st[0] + (dt * cs) * u0, ny = st[1] + (dt * sn) * u0, nth = st[2] + dt * u1;
+        state[5 * a + 0] = nx;
+        state[5 * a + 1] = ny;
+        state[5 * a + 2] = nth;
+        state[5 * a + 3] = u0;
+        state[5 * a + 4] = u1;
+        u_out[2 * a] = u0;
+        u_out[2 * a + 1] = u1;
+        best_out[a] = best;
+        status_out[a] = 0;
+        nsteps_out[a] = (it == 0 ? 0 : nsteps_out[a]) + 1;
+    }
+}
+
+// host restatement of pw_leaves: the largest part of n samples over k parts (leaf-aligned)
+int split_max_chunk(int n, int k)
+{
+    int lo[kMaxLeaves], len[kMaxLeaves], nl = 0;
+    struct R {
+        static void go(int d, int l, int m, int* lo, int* len, int& nl)
+        {
+            if (d == 0 || m <= 128) { lo[nl] = l; len[nl] = m; nl++; return; }
+            const int m2 = (m / 2) - (m / 2) % 8;
+            go(d - 1, l, m2, lo, len, nl);
+            go(d - 1, l + m2, m - m2, lo, len, nl);
+        }
+    };
+    R::go(kPwDepth, 0, n, lo, len, nl);
+    int mx = 0;
+    for (int p = 0; p < k; p++) {
+        const int l0 = (int)(((long)nl * p) / k), l1 = (int)(((long)nl * (p + 1)) / k);
+        const int c0 = l0 < nl ? lo[l0] : n, c1 = l1 < nl ? lo[l1] : n;
+        mx = c1 - c0 > mx ? c1 - c0 : mx;
+    }
+    return k > nl ? kMaxN + 1 : mx;  // more parts than leaves: refused
+}
+
 }  // namespace
+
+extern "C" int pmp_dwa_set_split(pmp_ctx* ctx, int parts)
+{
+    if (!ctx) return PMP_EINVAL;
+    if (parts < 0 || parts > 64) return pmp_set_err(ctx, PMP_EINVAL, "pmp_dwa_set_split: parts must be 0 (auto) .. 64");
+    ctx->dwa_split = parts;
+    return PMP_OK;
+}
 
 extern "C" int pmp_dwa_step_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int ox, int oy, int W, int H,
                                   const pmp_lp_params* lp, const pmp_dwa_params* dp, int na, double* state,
@@ -352,6 +593,45 @@ extern "C" int pmp_dwa_step_batch(pmp_ctx* ctx, void* stream, const uint32_t* oc
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_dwa_step_batch: nv*nw must be <= 4096 and dt > 0");
     PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     const bool occ_lds = ((size_t)W * H + 31) / 32 <= (size_t)kOccLdsWords;
+    // parts per agent: auto (dwa_split 0) = the CUs over the agents, at most 16; 1 = one workgroup per
+    // agent.  Only windows of fixed size (nv, nw > 0) split, into leaf-aligned parts of <= kSplitChunk.
+    int k = 1;
+    if (dp->nv > 0 && dp->nw > 0 && dp->nv * dp->nw > 1) {
+        if (ctx->dwa_split > 0) {
+            k = ctx->dwa_split;
+        } else {
+            if (!ctx->cus) PMP_HIP_CHECK(ctx, hipDeviceGetAttribute(&ctx->cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+            k = na < ctx->cus ? ctx->cus / na : 1;
+            k = k > 16 ? 16 : (k < 1 ? 1 : k);
+        }
+        const int n = dp->nv * dp->nw;
+        while (k > 1 && split_max_chunk(n, k) > kMaxN) k--;  // more parts than leaves
+        while (k > 1 && k < 64 && split_max_chunk(n, k) > kSplitChunk) k++;
+        if (k > 1 && split_max_chunk(n, k) > kSplitChunk) k = 1;
+    }
+    if (k > 1) {
+        const size_t per = (size_t)3 * kMaxN * 8 + (size_t)3 * kMaxLeaves * 8;
+        char* scr = (char*)pmp_scratch(ctx, SCR_DWA, (size_t)na * per + (size_t)na * 4 + 64);
+        if (!scr) return PMP_ENOMEM;
+        DwaSplitScratch X;
+        X.cols = (double*)scr;
+        X.leafsum = (double*)(scr + (size_t)na * 3 * kMaxN * 8);
+        X.cnt = (int*)(scr + (size_t)na * per);
+        // the counters are zero between launches (each agent's last part resets its own); a new buffer
+        // or a new layout (the counters follow the na agents' columns) starts zeroed once
+        if (ctx->dwa_zeroed != scr || ctx->dwa_zeroed_n != na) {
+            PMP_HIP_CHECK(ctx, hipMemsetAsync(X.cnt, 0, (size_t)na * 4, (hipStream_t)stream));
+            ctx->dwa_zeroed = scr;
+            ctx->dwa_zeroed_n = na;
+        }
+        auto sk = occ_lds ? dwa_split_kernel<true> : dwa_split_kernel<false>;
+        for (int it = 0; it < iters; it++)
+            hipLaunchKernelGGL(sk, dim3((unsigned)(na * k)), dim3(kSplitThreads), sizeof(DwaSplitShared), (hipStream_t)stream,
+                               occ_bits, ox, oy, W, H, *lp, *dp, na, k, it, iters, state, goal, path_xy, path_off, u, best,
+                               status, n_steps, hist_pose, eval, best_traj, X);
+        PMP_HIP_CHECK(ctx, hipGetLastError());
+        return PMP_OK;
+    }
     auto kern = occ_lds ? dwa_kernel<true> : dwa_kernel<false>;
     hipLaunchKernelGGL(kern, dim3(na), dim3(kThreads), sizeof(DwaShared), (hipStream_t)stream, occ_bits, ox, oy, W,
                        H, *lp, *dp, na, state, goal, path_xy, path_off, iters, u, best, status, n_steps, hist_pose, eval,

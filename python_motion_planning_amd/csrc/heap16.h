@@ -9,7 +9,6 @@
 //   push: the ancestors load in one round; the "less than the new item" set is a prefix of the
 //         root path, so a ballot popcount gives the sift-up distance;
 //   push_batch: an expansion's pushes stored together, only those below their parent sifted up;
-//   sift_up from any position (a decrease-key, with the POS position map).
 // The key is supplied by a policy type K: K::derive(e) fills e.f / e.hk from the stored fields and
 // K::lt(x, y) is the strict order.  K::kStoredF: f is stored beside the entry (24 B in LDS: g, f, a,
 // b; 32 B spill records) instead of derived on every load, so a key costs no square root.
@@ -35,18 +34,7 @@ struct Heap {
     lds_u32* lb;
     __amdgpu_buffer_rsrc_t spill;  // {g lo, g hi, a, b} (+ {f lo, f hi} with stored f) for positions >= lds_cap
     int lds_cap;
-    uint32_t* hpos;  // POS operations: hpos[K::cell(e)] = the position of e, kept current by every move
 };
-constexpr uint32_t kNoPos = 0xFFFFFFFFu;
-
-// POS: record a stored entry's position (decrease-key in place needs the cell -> position map)
-template <class K, bool POS>
-__device__ __forceinline__ void note(const Heap& hp, const K& key, const Ent& e, int p)
-{
-    if constexpr (POS)
-        if (K::tracked(e)) hp.hpos[key.cell(e)] = (uint32_t)p;
-}
-__device__ __forceinline__ int level_of(int p) { return 31 - __clz(p + 1); }
 
 // LDS and spill bytes per entry
 template <bool SF> constexpr int lds_entry_bytes() { return SF ? 24 : 16; }
@@ -61,7 +49,6 @@ __device__ __forceinline__ Heap make_heap(unsigned char* smem, int lds_cap, uint
     hp.la = (lds_u32*)(smem + (size_t)(SF ? 16 : 8) * lds_cap);
     hp.lb = (lds_u32*)(smem + (size_t)(SF ? 20 : 12) * lds_cap);
     hp.lds_cap = lds_cap;
-    hp.hpos = nullptr;
     hp.spill = __builtin_amdgcn_make_buffer_rsrc(spill_base, 0, (int)(spill_n * spill_entry_bytes<SF>()), 0x00020000);
     return hp;
 }
@@ -155,8 +142,8 @@ __device__ __forceinline__ Walk6 walk6_consts(int lane, int jl, int ol)
 // at position n.  `root` receives the new minimum (wave-uniform).  PAR: the walk over each 6-level
 // chunk is evaluated lane-parallel from `w` (same result as the scalar walk).  Returns the final hole
 // (where the old last element landed): the entries on the path from the root's child down to it moved
-// up one level.  POS: the moved entries' positions are recorded.
-template <class K, bool SPILL, bool PAR = false, bool POS = false>
+// up one level.
+template <class K, bool SPILL, bool PAR = false>
 __device__ __forceinline__ int pop(const Heap& hp, const K& key, int n, Ent& root, int lane, int jl, int ol,
                                     const Walk6& w = Walk6{0ull, 0ull})
 {
@@ -224,7 +211,6 @@ __device__ __forceinline__ int pop(const Heap& hp, const K& key, int n, Ent& roo
             const bool rr = (movr >> lane) & 1ull;
             const int dst = ((rr ? li + 1 : li) - 1) >> 1;
             store<SPILL, SF>(hp, dst, rr ? R : L);
-            note<K, POS>(hp, key, rr ? R : L, dst);
         }
         if (first && (mover & 1ull)) root = rl_ent((movr & 1ull) ? R : L, 0);
         first = false;
@@ -232,19 +218,16 @@ __device__ __forceinline__ int pop(const Heap& hp, const K& key, int n, Ent& roo
         if (!go) break;
         wsync();
     }
-    if (lane == 0) {
-        store<SPILL, SF>(hp, hole, last);
-        note<K, POS>(hp, key, last, hole);
-    }
+    if (lane == 0) store<SPILL, SF>(hp, hole, last);
     if (hole == 0) root = last;
     wsync();
     return hole;
 }
 
-// Sift `it` (wave-uniform, derived) up from position p0: a push at p0 = n, or a decrease-key of the
-// entry at p0 (it is smaller than that entry).  `root` is updated if it becomes the minimum.  Returns
-// the position it lands at; the ancestors of p0 from there down moved one level toward p0.
-template <class K, bool SPILL, bool POS = false>
+// Sift `it` (wave-uniform, derived) up from position p0 (a push at p0 = n).  `root` is updated if it
+// becomes the minimum.  Returns the position it lands at; the ancestors of p0 from there down moved
+// one level toward p0.
+template <class K, bool SPILL>
 __device__ __forceinline__ int sift_up(const Heap& hp, const K& key, int p0, const Ent& it, Ent& root, int lane)
 {
     constexpr bool SF = K::kStoredF;
@@ -263,24 +246,18 @@ __device__ __forceinline__ int sift_up(const Heap& hp, const K& key, int p0, con
     }
     key.derive(a);
     const int t = __popcll(ballot(valid & K::lt(it, a)));
-    if (lane < t) {
-        store<SPILL, SF>(hp, (np1 >> lane) - 1, a);
-        note<K, POS>(hp, key, a, (np1 >> lane) - 1);
-    }
+    if (lane < t) store<SPILL, SF>(hp, (np1 >> lane) - 1, a);
     const int ipos = (np1 >> t) - 1;
-    if (lane == 0) {
-        store<SPILL, SF>(hp, ipos, it);
-        note<K, POS>(hp, key, it, ipos);
-    }
+    if (lane == 0) store<SPILL, SF>(hp, ipos, it);
     if (ipos == 0) root = it;
     wsync();
     return ipos;
 }
 // Insert `it` into a heap of n entries.
-template <class K, bool SPILL, bool POS = false>
+template <class K, bool SPILL>
 __device__ __forceinline__ int push(const Heap& hp, const K& key, int n, const Ent& it, Ent& root, int lane)
 {
-    return sift_up<K, SPILL, POS>(hp, key, n, it, root, lane);
+    return sift_up<K, SPILL>(hp, key, n, it, root, lane);
 }
 
 // Push the items of the lanes in pm (wave-uniform mask; each lane's `it` derived) into a heap of n

@@ -567,8 +567,9 @@ static int lpa_batch(int lite, pmp_ctx* ctx, void* stream, const uint32_t* occ_b
     }
     hipStream_t s = (hipStream_t)stream;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
-    // U's LDS share: the CU's 160 KiB over its resident workers, 20 B per list entry
-    const int per_cu = (workers + 255) / 256;
+    // U's LDS share: the CU's 160 KiB over its resident workers (or the residency the context was
+    // told to leave room for, pmp_set_resident_per_cu), 20 B per list entry
+    const int per_cu = pmp_lds_share(ctx, (workers + 255) / 256);
     int ucap = ((160 * 1024) / (per_cu < 1 ? 1 : per_cu) / 20) & ~15;
     if (ucap > 4096) ucap = 4096;
     hipLaunchKernelGGL(lpa_kernel, dim3(workers), dim3(64), (size_t)ucap * 20, s, occ_bits, W, H, heuristic, start_xy,

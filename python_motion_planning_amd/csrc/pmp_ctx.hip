@@ -59,6 +59,13 @@ int pmp_set_timing(pmp_ctx* ctx, uint64_t* span)
     return PMP_OK;
 }
 
+int pmp_set_stats(pmp_ctx* ctx, int64_t* stats)
+{
+    if (!ctx) return PMP_EINVAL;
+    ctx->stats = reinterpret_cast<unsigned long long*>(stats);
+    return PMP_OK;
+}
+
 int pmp_wall_clock_khz(pmp_ctx* ctx, int* khz)
 {
     if (!ctx || !khz) return PMP_EINVAL;

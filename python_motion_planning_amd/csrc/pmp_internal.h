@@ -13,6 +13,8 @@ struct pmp_ctx {
     int astar_W = 0, astar_H = 0, astar_workers = 0, astar_heap_cap = 0, astar_lds_cap = 0;
     // optional launch-span recording (pmp_set_timing): device u64[2] = {min start, max end}
     unsigned long long* span = nullptr;
+    // optional work counters (pmp_set_stats): device i64, [0] += MPC QP solves of track launches
+    unsigned long long* stats = nullptr;
     // A* 2D query scheduling: 1 = longest (start-goal distance) first, 0 = input order
     int astar_lpt = 1;
     // longest-first only: how many of the first (longest) queries run at raised wave priority
@@ -37,13 +39,19 @@ struct pmp_ctx {
     int astar_auto = 0;         // ... and was made by a launch (not the host): it grows with the batches
     size_t astar_mq_epoch_slots = 0, astar_mq_cst_bytes = 0;
     // grow-only scratch arena, one buffer per use
-    void* buf[16] = {nullptr};
-    size_t cap[16] = {0};
+    void* buf[24] = {nullptr};
+    size_t cap[24] = {0};
+    // DWA k-split (dwa.hip): the per-agent arrival counters in SCR_DWA were zeroed for this buffer
+    void* dwa_zeroed = nullptr;
+    int dwa_zeroed_n = 0;
+    // DWA parts per agent (pmp_dwa_set_split): 0 auto, 1 off, k
+    int dwa_split = 0;
+    int cus = 0;  // compute units of the device (0 = not queried yet)
 };
 
 enum ScratchSlot { SCR_HEAP = 0, SCR_CLOSED = 1, SCR_PDIR = 2, SCR_G = 3, SCR_AUX0 = 4, SCR_AUX1 = 5, SCR_AUX2 = 6, SCR_AUX3 = 7,
                    SCR_BITS = 8, SCR_AUX4 = 9, SCR_PAR = 10, SCR_MQ_SPILL = 11, SCR_MQ_CST = 12, SCR_MQ_G = 13,
-                   SCR_MQ_T2 = 14, SCR_MQ_EPOCH = 15, SCR_NSLOTS = 16 };
+                   SCR_MQ_T2 = 14, SCR_MQ_EPOCH = 15, SCR_DWA = 16, SCR_NSLOTS = 17 };
 
 int pmp_set_err(pmp_ctx* ctx, int code, const std::string& msg);
 // Workers per CU whose LDS shares a launch of `per_cu` workers per CU must fit beside
@@ -78,7 +86,7 @@ int pmp_astar2d_slot_scratch(pmp_ctx* ctx, hipStream_t s, size_t slots, int W, i
                              double** G, uint32_t** ep);
 // The single-query A* 2D engine (astar2d_sq.hip): one query per workgroup, the CU's LDS its heap.
 // Returns the heap capacity it can hold for this grid (0: not this engine's grid) / launches.
-int pmp_astar2d_sq_cap(int W, int H);
+extern "C" int pmp_astar2d_sq_cap(int W, int H);
 int pmp_astar2d_sq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t* occ_bits, int W, int H, int heuristic,
                           const int32_t* start_xy, const int32_t* goal_xy, int nq, int heap_cap, double* cost,
                           int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded, uint32_t* expand,

@@ -4,10 +4,12 @@
 // Per iteration (all decisions wave-uniform, results identical to the reference's sequential loop):
 //  1. sample from the query's np.random stream (generateRandomNode, rrt.py:91-103);
 //  2. nearest node = first argmin of the exact CPython hypot (rrt.py:117-118).  A coarse pass over a
-//     16-bit fixed-point copy of the coordinates (4 B/node, so 32 trees stay in an XCD's L2) finds
-//     the minimum; only nodes within a rigorous error band of it are re-evaluated exactly in f64;
-//     ties resolve to the lowest index.  A zero distance means the sample is already in
-//     sample_list (rrt.py:67-68);
+//     16-bit fixed-point copy of the coordinates (4 B/node) finds the minimum; only nodes within a
+//     rigorous error band of it are re-evaluated exactly in f64; ties resolve to the lowest index.
+//     The coarse copy lives in the workgroup's LDS (round 5: ~31k nodes beside the rest of the
+//     workgroup's state; nodes beyond that in HBM/L2), so the two whole-tree scans of an iteration
+//     (nearest, in-radius) read LDS instead of streaming the tree from L2.  A zero distance means
+//     the sample is already in sample_list (rrt.py:67-68);
 //  3. steer (hypot, atan2, cos, sin) and isCollision(new, near), the obstacle tests spread over the
 //     workgroup;
 //  4. RRT*: the sequential choose-parent/rewire scan (rrt_star.py:57-73) in parallel form.  With
@@ -25,10 +27,13 @@ constexpr int kNT = 512;
 constexpr int kWaves = kNT / 64;
 constexpr int kMaxObs = 256;   // per obstacle kind
 constexpr int kMaxBnd = 8;
-constexpr int kMaxA = 2048;    // collision-free improving candidates per iteration
-constexpr int kMaxT = 4096;    // candidates awaiting a collision test per phase
-constexpr int kMaxK = 1024;    // in-radius candidates kept in LDS (more spill to the HBM list)
-constexpr int kRnd = 1024;     // random doubles staged in LDS
+// The candidate lists keep their first entries in LDS and the rest in per-query HBM lists (C3: an
+// r = 10 ball holds tens of nodes), so the LDS goes to the coarse tree copy.
+constexpr int kMaxA = 256;     // collision-free improving candidates per iteration
+constexpr int kMaxT = 256;     // candidates awaiting a collision test per phase
+constexpr int kMaxK = 256;     // in-radius candidates kept in LDS (more spill to the HBM list)
+constexpr int kRnd = 256;      // random doubles staged in LDS
+constexpr int kLdsBytes = 160 * 1024;  // the CU's LDS: one workgroup per CU
 
 constexpr int KF_A = 1;        // c_i < G0
 constexpr int KF_VALID = 2;    // ... and collision-free
@@ -36,6 +41,14 @@ constexpr int KF_VALID = 2;    // ... and collision-free
 struct KEntry {
     int j, flags;
     double d;
+};
+struct TEntry {  // a candidate awaiting a collision test: K index, G_{i-1}
+    int k, pad;
+    double G;
+};
+struct AEntry {  // a collision-free improving candidate: node, c = g + d
+    int j, pad;
+    double c;
 };
 
 struct RrtArgs {
@@ -57,8 +70,11 @@ struct RrtArgs {
     int64_t* draws;
     int32_t* status;
     int64_t* counters;  // nullable [nq][4]
-    uint32_t* xyq;    // scratch [nq][cap]: 16-bit fixed-point x | y << 16 (the coarse scan copy)
+    uint32_t* xyq;    // scratch [nq][cap]: 16-bit fixed-point x | y << 16 (the coarse copy beyond LDS)
     KEntry* klist;    // scratch [nq][cap]
+    TEntry* tlist;    // scratch [nq][cap]
+    AEntry* alist;    // scratch [nq][cap]
+    int lcap;         // nodes of the coarse copy held in LDS
 };
 
 struct RrtShared {
@@ -235,10 +251,30 @@ __device__ __forceinline__ void kset_flags(RrtShared& S, KEntry* kl, int k, int 
     else kl[k].flags = fl;
 }
 
+__device__ __forceinline__ void tset(RrtShared& S, TEntry* tl, int t, int k, double G)
+{
+    if (t < kMaxT) { S.tk[t] = k; S.tG[t] = G; }
+    else { TEntry e; e.k = k; e.pad = 0; e.G = G; tl[t] = e; }
+}
+__device__ __forceinline__ int tget_k(const RrtShared& S, const TEntry* tl, int t) { return t < kMaxT ? S.tk[t] : tl[t].k; }
+__device__ __forceinline__ double tget_G(const RrtShared& S, const TEntry* tl, int t) { return t < kMaxT ? S.tG[t] : tl[t].G; }
+__device__ __forceinline__ void aset(RrtShared& S, AEntry* al, int a, int j, double c)
+{
+    if (a < kMaxA) { S.aj[a] = j; S.ac[a] = c; }
+    else { AEntry e; e.j = j; e.pad = 0; e.c = c; al[a] = e; }
+}
+__device__ __forceinline__ int aget_j(const RrtShared& S, const AEntry* al, int a) { return a < kMaxA ? S.aj[a] : al[a].j; }
+__device__ __forceinline__ double aget_c(const RrtShared& S, const AEntry* al, int a) { return a < kMaxA ? S.ac[a] : al[a].c; }
+
+typedef __attribute__((address_space(3))) uint32_t lds_xyq;
+
 template <bool STAR>
 __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
 {
     __shared__ RrtShared S;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_dyn[];
+    lds_xyq* xl = (lds_xyq*)smem_dyn;  // nodes 0 .. lcap-1 of the coarse copy
+    const int lcap = A.lcap;
     const int q = blockIdx.x;
     const int tid = threadIdx.x;
     if (q >= A.nq) return;
@@ -254,6 +290,14 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
     int32_t* tpar = A.tpar + (size_t)q * cap;
     uint32_t* xyq = A.xyq + (size_t)q * cap;
     KEntry* kl = A.klist + (size_t)q * cap;
+    TEntry* tl = A.tlist + (size_t)q * cap;
+    AEntry* al = A.alist + (size_t)q * cap;
+    // node j's coarse copy: LDS below lcap, HBM above (every node is written once, by thread 0, and
+    // read after a barrier)
+    auto xq_store = [&](int j, uint32_t v) {
+        if (j < lcap) xl[j] = v;
+        else xyq[j] = v;
+    };
     const double* rnd = A.rnd + (size_t)q * A.stride;
     const double sx0 = A.start[2 * q], sy0 = A.start[2 * q + 1];
     const double gx = A.goal[2 * q], gy = A.goal[2 * q + 1];
@@ -274,7 +318,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
     };
     if (tid == 0) {
         tx[0] = sx0; tx[1] = sy0; tg[0] = 0.0; tpar[0] = 0;
-        xyq[0] = qenc(sx0, sy0);
+        xq_store(0, qenc(sx0, sy0));
     }
     __syncthreads();
     const double lox = delta, rgx = (P.x_range - delta) - delta;
@@ -305,9 +349,16 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         // ---- 2. nearest ----
         const float sxf = (float)sx, syf = (float)sy;
         float best = INFINITY;
-        {
-            // 8 loads in flight per thread: the scan is bound by L2/MALL latency, not bandwidth
-            int j = tid;
+        const int nl = n < lcap ? n : lcap;
+        for (int j = tid; j < nl; j += kNT) {  // the LDS part
+            const uint32_t p = xl[j];
+            const float dx = fmaf((float)(p & 0xFFFFu), qinv, qlof) - sxf;
+            const float dy = fmaf((float)(p >> 16), qinv, qlof) - syf;
+            best = fminf(best, dx * dx + dy * dy);
+        }
+        if (n > lcap) {
+            // the HBM part, 8 loads in flight per thread (bound by L2/MALL latency, not bandwidth)
+            int j = lcap + tid;
             for (; j + 7 * kNT < n; j += 8 * kNT) {
                 uint32_t p[8];
 #pragma unroll
@@ -332,12 +383,16 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         double h = INFINITY, hx = 0.0, hy = 0.0, hg = 0.0;
         int hi = 0x7fffffff;
         if (best <= T) {
-            // 8 loads in flight per thread, as the scan above (one at a time made this pass a chain
-            // of n / 512 dependent L2 round trips per iteration)
+            // increasing j within the thread (the LDS part first): equal distances keep the first.
+            // 8 loads in flight per thread (one at a time made the HBM part a chain of dependent
+            // L2 round trips)
             for (int j0 = tid; j0 < n; j0 += 8 * kNT) {
                 uint32_t p[8];
 #pragma unroll
-                for (int u = 0; u < 8; u++) p[u] = (j0 + u * kNT < n) ? xyq[j0 + u * kNT] : 0u;
+                for (int u = 0; u < 8; u++) {
+                    const int j = j0 + u * kNT;
+                    p[u] = j < nl ? xl[j] : (j < n ? xyq[j] : 0u);
+                }
                 uint32_t hits = 0;
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
@@ -382,7 +437,10 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             for (int j0 = tid; j0 < n; j0 += 8 * kNT) {
                 uint32_t p[8];
 #pragma unroll
-                for (int u = 0; u < 8; u++) p[u] = (j0 + u * kNT < n) ? xyq[j0 + u * kNT] : 0u;
+                for (int u = 0; u < 8; u++) {
+                    const int j = j0 + u * kNT;
+                    p[u] = j < nl ? xl[j] : (j < n ? xyq[j] : 0u);
+                }
                 uint32_t hits = 0;
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
@@ -409,7 +467,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                 }
                 if (fl & KF_A) {
                     const int t = atomicAdd(&S.nT, 1);
-                    if (t < kMaxT) S.tk[t] = k;
+                    tset(S, tl, t, k, 0.0);
                 }
               }
             }
@@ -417,28 +475,30 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             const int nK = S.nK;
             const int nT = S.nT;
             slot = S.slot;
-            if (nT > kMaxT) { status = PMP_CAP_OVERFLOW; break; }
             c_cand += nK;
             c_scan += n;
             c_tests += nT;
             // ---- 4b. one wave per test: the collision-free improving set ----
             for (int t = wave; t < nT; t += kWaves) {
-                const int k = S.tk[t];
+                const int k = tget_k(S, tl, t);
                 const KRec e = kget(S, kl, tx, tg, k);
                 if (collision_wave(S, nr, nc, nb, delta, e.x, e.y, nx, ny)) continue;
                 if (lane == 0) {
                     const int a = atomicAdd(&S.nA, 1);
-                    if (a < kMaxA) { S.aj[a] = e.j; S.ac[a] = e.g + e.d; }
+                    aset(S, al, a, e.j, e.g + e.d);
                     kset_flags(S, kl, k, KF_A | KF_VALID);
                 }
             }
+            __threadfence_block();  // HBM list entries before the barrier
             __syncthreads();
             const int nA = S.nA;
-            if (nA > kMaxA) { status = PMP_CAP_OVERFLOW; break; }
             double cb = INFINITY;
             int jb = 0x7fffffff;
-            for (int a = tid; a < nA; a += kNT)
-                if (S.ac[a] < cb || (S.ac[a] == cb && S.aj[a] < jb)) { cb = S.ac[a]; jb = S.aj[a]; }
+            for (int a = tid; a < nA; a += kNT) {
+                const double c = aget_c(S, al, a);
+                const int j = aget_j(S, al, a);
+                if (c < cb || (c == cb && j < jb)) { cb = c; jb = j; }
+            }
             if (tid == 0) S.nT = 0;
             block_min_di(cb, jb, S);  // (its barriers also publish nT = 0)
             if (cb < G0) { G = cb; parent = jb; }
@@ -447,7 +507,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                 const KRec e = kget(S, kl, tx, tg, k);
                 double Gp = G0;
                 for (int a = 0; a < nA; a++)
-                    if (S.aj[a] < e.j) Gp = fmin(Gp, S.ac[a]);
+                    if (aget_j(S, al, a) < e.j) Gp = fmin(Gp, aget_c(S, al, a));
                 const double gj = e.g;
                 if ((e.fl & KF_VALID) && Gp > gj + e.d) continue;  // node_new re-parents here
                 const double c2 = Gp + e.d;
@@ -457,23 +517,23 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                     continue;
                 }
                 const int t = atomicAdd(&S.nT, 1);
-                if (t < kMaxT) { S.tk[t] = k; S.tG[t] = Gp; }
+                tset(S, tl, t, k, Gp);
             }
+            __threadfence_block();
             __syncthreads();
             const int nT2 = S.nT;
-            if (nT2 > kMaxT) { status = PMP_CAP_OVERFLOW; break; }
             c_tests += nT2;
             for (int t = wave; t < nT2; t += kWaves) {
-                const KRec e = kget(S, kl, tx, tg, S.tk[t]);
+                const KRec e = kget(S, kl, tx, tg, tget_k(S, tl, t));
                 if (collision_wave(S, nr, nc, nb, delta, e.x, e.y, nx, ny)) continue;
-                if (lane == 0) { tg[e.j] = S.tG[t] + e.d; tpar[e.j] = slot; }
+                if (lane == 0) { tg[e.j] = tget_G(S, tl, t) + e.d; tpar[e.j] = slot; }
             }
             __syncthreads();  // rewires land before the insert below may overwrite a duplicate slot
         }
         // ---- 5. insert + goal test (rrt.py:70-81) ----
         if (tid == 0) {
             tx[2 * slot] = nx; tx[2 * slot + 1] = ny; tg[slot] = G; tpar[slot] = parent;
-            xyq[slot] = qenc(nx, ny);
+            xq_store(slot, qenc(nx, ny));
         }
         if (slot == n) {
             if (n >= cap) { status = PMP_CAP_OVERFLOW; break; }
@@ -486,7 +546,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             if (n >= cap) { status = PMP_CAP_OVERFLOW; break; }
             if (tid == 0) {
                 tx[2 * n] = gx; tx[2 * n + 1] = gy; tg[n] = G + lp::py_hypot(nx - gx, ny - gy); tpar[n] = slot;
-                xyq[n] = qenc(gx, gy);
+                xq_store(n, qenc(gx, gy));
             }
             n++;
             status = PMP_FOUND;
@@ -547,7 +607,12 @@ extern "C" int pmp_rrt_batch(pmp_ctx* ctx, void* stream, const pmp_rrt_params* p
     PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     uint32_t* xyq = (uint32_t*)pmp_scratch(ctx, SCR_AUX0, sizeof(uint32_t) * (size_t)nq * tree_cap);
     KEntry* kl = (KEntry*)pmp_scratch(ctx, SCR_AUX1, sizeof(KEntry) * (size_t)nq * tree_cap);
-    if (!xyq || !kl) return PMP_ENOMEM;
+    TEntry* tl = (TEntry*)pmp_scratch(ctx, SCR_AUX2, sizeof(TEntry) * (size_t)nq * tree_cap);
+    AEntry* al = (AEntry*)pmp_scratch(ctx, SCR_AUX3, sizeof(AEntry) * (size_t)nq * tree_cap);
+    if (!xyq || !kl || !tl || !al) return PMP_ENOMEM;
+    // the coarse copy's LDS part: the CU's LDS beside the workgroup's static state
+    int lcap = (int)((kLdsBytes - sizeof(RrtShared) - 512) / 4) & ~63;
+    if (lcap > tree_cap) lcap = (tree_cap + 63) & ~63;
     RrtArgs A;
     A.P = *p;
     A.rect = rect; A.circ = circ; A.bnd = bnd;
@@ -557,10 +622,12 @@ extern "C" int pmp_rrt_batch(pmp_ctx* ctx, void* stream, const pmp_rrt_params* p
     A.txy = tree_xy; A.tg = tree_g; A.tpar = tree_parent; A.n_nodes = n_nodes;
     A.cost = cost; A.path_len = path_len; A.path = path_xy; A.path_cap = path_cap;
     A.draws = draws; A.status = status; A.counters = counters; A.xyq = xyq; A.klist = kl;
+    A.tlist = tl; A.alist = al; A.lcap = lcap;
+    const size_t dyn = (size_t)lcap * 4;
     if (p->star)
-        hipLaunchKernelGGL(rrt_kernel<true>, dim3(nq), dim3(kNT), 0, (hipStream_t)stream, A);
+        hipLaunchKernelGGL(rrt_kernel<true>, dim3(nq), dim3(kNT), dyn, (hipStream_t)stream, A);
     else
-        hipLaunchKernelGGL(rrt_kernel<false>, dim3(nq), dim3(kNT), 0, (hipStream_t)stream, A);
+        hipLaunchKernelGGL(rrt_kernel<false>, dim3(nq), dim3(kNT), dyn, (hipStream_t)stream, A);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }

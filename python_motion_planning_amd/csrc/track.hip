@@ -724,6 +724,7 @@ struct TrackCarry {
     double* in;    // [na][10]: s[3], sd[3], ur[2], rv, rw
     int32_t* flag;  // [na]
     int32_t* admm;  // [na]
+    unsigned long long* stats;  // nullable (pmp_set_stats): [0] += QP solves
 };
 
 __global__ __launch_bounds__(kWave) void track_mpc_step(pmp_lp_params P, int na, int it, int iters,
@@ -829,7 +830,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     const bool valid = ai < na;
     const int a = valid ? ai : na - 1;
     const bool solve = valid && (C.flag[a] & kSolve) != 0;
-    if (!ballot(solve)) return;  // wave-uniform
+    const uint64_t sm = ballot(solve && v == 0);
+    if (!sm) return;  // wave-uniform
+    if (C.stats && threadIdx.x == 0) atomicAdd(C.stats, (unsigned long long)__popcll(sm));
     MpcIn I;
     const double* in = C.in + 10 * (size_t)a;
     if (solve) {
@@ -927,6 +930,7 @@ extern "C" int pmp_track_step_batch(pmp_ctx* ctx, void* stream, int kind, const 
         C.in = (double*)scr;
         C.flag = (int32_t*)(scr + nb * 80);
         C.admm = C.flag + nb;
+        C.stats = ctx->stats;
         const dim3 grid((na + kRows - 1) / kRows);
         hipStream_t s = (hipStream_t)stream;
         for (int it = 0; it <= iters; it++) {

@@ -114,9 +114,12 @@ class AStar(GraphSearcher):
         if st == _lib.STATUS_CAP_OVERFLOW:  # heap outgrew the reservation: the batch path's full-bound re-plan
             # sized for any outcome (a path visits a cell at most once, a cell closes at most once): the
             # full search may close more cells than the overflowed run had reached
+            # (straight to the full bound: a plain batch call would first re-run the same engine at the
+            # same limit and overflow again)
             path_cap, expand_cap = W * H + 1, W * H
-            r = batch.astar2d_batch((W, H), np.array([s]), np.array([g]), self.heuristic_type, path_cap=path_cap,
-                                    expand_cap=expand_cap, algo=self._algo, occ_bits=cached[2])
+            sg = torch.as_tensor(np.array([[s[0], s[1]], [g[0], g[1]]], np.int32), device="cuda")
+            r = batch.astar2d_full_bound((W, H), sg[:1], sg[1:], self.heuristic_type, path_cap=path_cap,
+                                         expand_cap=expand_cap, algo=self._algo, occ_bits=cached[2])
             st, nexp, plen = (int(v) for v in torch.stack([r["status"][0], r["n_expanded"][0],
                                                             r["path_len"][0]]).cpu().tolist())
             cells = r["path"][0, :plen].cpu().numpy()

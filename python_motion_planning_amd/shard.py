@@ -130,6 +130,17 @@ def max_over_ranks(dist, values, device="cpu"):
     return [float(v) for v in t.tolist()]
 
 
+def sum_over_ranks(dist, values, device="cpu"):
+    """Element-wise sum of a list of floats over all ranks (identity without a process group)."""
+    if dist is None:
+        return [float(v) for v in values]
+    import torch
+
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(v) for v in t.tolist()]
+
+
 def barrier(dist):
     if dist is not None:
         dist.barrier()

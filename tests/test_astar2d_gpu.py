@@ -228,6 +228,8 @@ def test_explicit_heap_cap_and_overflow_retry_keep_geometry():
     """An explicit heap_cap above the multi-query engine's limit is kept (the one-query engine is
     reserved for it, not the limit); a batch's overflow re-run restores the geometry in force: the
     host's reservation, or launch-sized (auto) scratch on a context the host never reserved."""
+    import torch
+
     from oracle import oracle as O
     from python_motion_planning_amd import _lib, batch
 
@@ -249,9 +251,16 @@ def test_explicit_heap_cap_and_overflow_retry_keep_geometry():
         _lib.check(ctx, L.pmp_astar2d_set_engine(ctx, 1, 1), "engine")  # multi-query limit 16383
         limit = 16383
         _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, W, 4, limit + 1000), "reserve")
-        assert geometry()[3] == limit + 1000 and geometry()[4] == 0  # kept; one-query engine
+        assert geometry()[3] == limit + 1000 and geometry()[4] == 2  # kept (explicit); one-query engine
         _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, W, 4096, 0), "reserve")
-        assert geometry()[3] == limit and geometry()[4] == 1  # the default is the limit
+        assert geometry()[3] == limit and geometry()[4] == 1  # the default is the limit (multi-query)
+        # an overflow re-run on a default reservation restores the default (not the cut limit as an
+        # explicit cap, which would move later small batches off the single-query engine)
+        before = geometry()
+        r = batch.astar2d_full_bound((W, W), torch.as_tensor(starts, device="cuda"),
+                                     torch.as_tensor(goals, device="cuda"), path_cap=W * W + 1)
+        assert np.array_equal(r["cost"].cpu().numpy(), ref["cost"])
+        assert geometry() == before
         # a tiny explicit cap overflows every query; the re-run (full bound 8 W H + 8 = 39,208 > the
         # limit) must not be cut back to the limit, and the host's geometry comes back afterwards
         r = batch.astar2d_batch(occ, starts, goals, path_cap=W * W + 1, reserve_slots=4, heap_cap=8)
@@ -259,7 +268,7 @@ def test_explicit_heap_cap_and_overflow_retry_keep_geometry():
         assert np.array_equal(r["cost"].cpu().numpy(), ref["cost"])
         assert np.array_equal(r["n_expanded"].cpu().numpy(), ref["n_expanded"])
         geo = geometry()
-        assert geo[:4] == [W, W, 4, 8] and geo[5] == 0
+        assert geo[:4] == [W, W, 4, 8] and geo[4] & 2 and geo[5] == 0
         # a launch-sized context stays launch-sized after a re-run
         _lib.check(ctx, L.pmp_astar2d_reserve_auto(ctx), "reserve_auto")
         assert geometry()[0] == 0
@@ -392,6 +401,7 @@ def test_dropin_heap_beyond_single_query_capacity():
     engine's LDS heap: the kernel reports PMP_CAP_OVERFLOW and plan() re-runs it with the full bound
     (graph_search.AStar.plan) -- the answer, path and CLOSED order still equal the oracle's."""
     from oracle import oracle as O
+    from python_motion_planning_amd import _lib
 
     pmp = _pmp()
     W = 1400
@@ -400,7 +410,9 @@ def test_dropin_heap_beyond_single_query_capacity():
     occ[W // 2, 1:W - 40] = 1  # a wall across most of the grid: A* floods the near half first
     s, g = (W // 4, W // 2), (3 * W // 4, W // 2)
     ref = O.astar2d(occ, s, g)
-    assert ref["status"] == 0 and ref["max_heap"] > 13440  # beyond the single-query engine's LDS heap
+    sq_cap = _lib.load_library().pmp_astar2d_sq_cap(W, W)
+    assert sq_cap == 13632  # (160 KiB - 256 B) / 12 B, a multiple of 16 (no grid block at 1400^2)
+    assert ref["status"] == 0 and ref["max_heap"] > sq_cap  # beyond the single-query engine's LDS heap
     env = pmp.Grid(W, W)
     env.update({(int(a), int(b)) for a, b in np.argwhere(occ)})
     cost, path, expand = pmp.AStar(s, g, env).plan()

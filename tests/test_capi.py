@@ -71,3 +71,13 @@ def test_bindings_match_prototypes():
                 assert a is ctypes.c_int64, f"{name}: {p!r} bound as {a}"
             elif p.startswith("int") or p.startswith("int32_t"):
                 assert a is ctypes.c_int, f"{name}: {p!r} bound as {a}"
+
+
+def test_single_query_capacity_without_gpu():
+    """pmp_astar2d_sq_cap is host arithmetic (no device call): (160 KiB - 256 B) / 12 B per entry,
+    a multiple of 16, on grids too large for the engine's LDS grid block; less beside a small grid."""
+    from python_motion_planning_amd import _lib
+
+    L = _lib.load_library()
+    assert L.pmp_astar2d_sq_cap(1400, 1400) == 13632 == ((160 * 1024 - 256) // 12) & ~15
+    assert 0 < L.pmp_astar2d_sq_cap(51, 31) < 13632

@@ -142,3 +142,84 @@ def test_large_inflation_against_oracle(inflation):
         if rc == 0:
             np.testing.assert_allclose(new_st[i], ost, rtol=1e-12, atol=1e-14)
             np.testing.assert_allclose(u[i], ou, rtol=1e-12, atol=1e-14)
+
+
+def _c4_inputs(na, seed=None):
+    from python_motion_planning_amd import batch, workloads as wl
+
+    occ, states, goals = wl.c4_workload(256) if seed is None else wl.c4_workload(na, seed=seed)
+    occ, states, goals = occ, states[:na], goals[:na]
+    r = batch.astar2d_batch(occ, states[:, :2].astype(np.int32), np.tile([45, 25], (na, 1)).astype(np.int32),
+                            path_cap=2048)
+    pl, P = r["path_len"].cpu().numpy(), r["path"].cpu().numpy()
+    H = occ.shape[1]
+    paths = [np.column_stack([P[i, : pl[i]][::-1] // H, P[i, : pl[i]][::-1] % H]).astype(np.float64)
+             for i in range(na)]
+    return occ, states, goals, paths
+
+
+def test_c4_split_32_agents_against_oracle():
+    """The 8-GPU strong split's per-rank share (32 of C4's 256 agents): with fewer agents than CUs the
+    default splits each agent's 4096 samples over several workgroups (leaf-aligned parts of numpy's
+    pairwise tree, dwa.py:176-181; first-index argmax across parts, dwa.py:89).  Every agent against
+    the oracle, and the evaluation rows bit-equal to one workgroup per agent."""
+    import torch
+
+    from oracle import oracle as O
+    from python_motion_planning_amd import _lib, batch
+
+    occ, states, goals, paths = _c4_inputs(32)
+    xy, off = batch.pack_paths(paths)
+    lp = _lib.LPParams.from_params(_pmp().LocalPlanner.DEFAULTS)
+    dp = _lib.DWAParams(0.2, 0.1, 0.05, 3.0, 1.0, 0.05, 0.05, 64, 64)
+    grid = batch.obstacle_grid({(int(a), int(b)) for a, b in np.argwhere(occ)})
+    outs = {}
+    for parts in (0, 1):
+        st_d = torch.tensor(states, dtype=torch.float64, device="cuda")
+        o = batch.dwa_step_batch(grid, lp, dp, st_d, goals, xy, off, iters=1, want_eval=True, want_traj=True,
+                                 parts=parts)
+        torch.cuda.synchronize()
+        outs[parts] = {k: v.cpu().numpy() for k, v in o.items() if v is not None}
+        outs[parts]["state"] = st_d.cpu().numpy()
+    for k in outs[1]:
+        assert np.array_equal(outs[0][k], outs[1][k]), k
+    obs = np.argwhere(occ).astype(np.float64)
+    for i in range(32):
+        rc, ost, ou = O.dwa_step(obs, paths[i], goals[i], states[i], nv=64, nw=64, predict_time=3.0)
+        assert rc == outs[0]["status"][i], i
+        if rc == 0:
+            np.testing.assert_allclose(outs[0]["state"][i], ost, rtol=1e-12, atol=1e-14)
+            np.testing.assert_allclose(outs[0]["u"][i], ou, rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.parametrize("nv", [64, 40])
+def test_split_parts_bit_equal(nv):
+    """Any number of parts (incl. uneven leaf counts, more requested parts than leaves, a 40 x 40 window
+    whose pairwise tree has uneven leaves) gives the bits of one workgroup per agent over several plan
+    iterations, including an agent that starts at its goal (status 1 at iteration 0)."""
+    import torch
+
+    from python_motion_planning_amd import _lib, batch
+
+    occ, states, goals, paths = _c4_inputs(24, seed=3)
+    states = states.copy()
+    states[5, :3] = goals[5]  # at the goal: reachGoal stops it before any step
+    xy, off = batch.pack_paths(paths)
+    lp = _lib.LPParams.from_params(_pmp().LocalPlanner.DEFAULTS)
+    dp = _lib.DWAParams(0.2, 0.1, 0.05, 3.0, 1.0, 0.05, 0.05, nv, nv)
+    grid = batch.obstacle_grid({(int(a), int(b)) for a, b in np.argwhere(occ)})
+    ref = None
+    for parts in (1, 2, 3, 5, 8, 16, 64):
+        st_d = torch.tensor(states, dtype=torch.float64, device="cuda")
+        o = batch.dwa_step_batch(grid, lp, dp, st_d, goals, xy, off, iters=4, want_eval=True, want_traj=True,
+                                 want_hist=True, parts=parts)
+        torch.cuda.synchronize()
+        got = {k: v.cpu().numpy() for k, v in o.items() if v is not None}
+        got["state"] = st_d.cpu().numpy()
+        assert got["status"][5] == 1 and got["n_steps"][5] == 0
+        if ref is None:
+            ref = got
+            assert (got["n_steps"] > 0).sum() >= 20
+            continue
+        for k in ref:
+            assert np.array_equal(got[k], ref[k]), (parts, k)

@@ -343,6 +343,46 @@ def test_lpastar_long_lists(lite):
 
 
 @pytest.mark.parametrize("lite", [False, True])
+def test_lpastar_lists_beyond_lds_share(lite):
+    """U moving from the wave's LDS share to HBM mid-query (lpa.hip u_push: copy-out, then every
+    u_find / u_remove / min scan on the HBM arrays).  The context leaves LDS room for 32 workers per CU
+    (pmp_set_resident_per_cu), so a query's share is (160 KiB / 32 / 20 B) & ~15 = 256 entries, and the
+    256^2 queries' lists outgrow it; every query against the oracle (status, cost, path, len(EXPAND),
+    pushes, max |U|)."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import _lib, batch
+
+    ucap = ((160 * 1024) // 32 // 20) & ~15
+    rng = np.random.default_rng(12)
+    occ = (rng.random((256, 256)) < 0.1).astype(np.uint8)
+    occ[:, 0] = occ[:, -1] = 1
+    occ[0, :] = occ[-1, :] = 1
+    free = np.argwhere(occ == 0)
+    S = free[rng.integers(len(free), size=24)].astype(np.int32)
+    G = free[rng.integers(len(free), size=24)].astype(np.int32)
+    L, ctx = _lib.load_library(), _lib.context()
+    _lib.check(ctx, L.pmp_set_resident_per_cu(ctx, 32), "resident")
+    try:
+        r = batch.lpastar2d_batch(occ, S, G, counters=True, lite=lite)
+        st, cost = r["status"].cpu().numpy(), r["cost"].cpu().numpy()
+        ne, ctr = r["n_expanded"].cpu().numpy(), r["counters"].cpu().numpy()
+        P, pl = r["path"].cpu().numpy(), r["path_len"].cpu().numpy()
+    finally:
+        _lib.check(ctx, L.pmp_set_resident_per_cu(ctx, 0), "resident")
+    spilled = 0
+    for q in range(len(S)):
+        ref = O.lpastar2d(occ, S[q], G[q], lite=lite)
+        spilled += ref["max_u"] > ucap
+        assert st[q] == ref["status"] and ne[q] == ref["n_expanded"], q
+        assert ctr[q, 0] == ref["n_push"] and ctr[q, 3] == ref["max_u"], q
+        if ref["status"] in (0, 1):
+            assert cost[q] == ref["cost"], q
+        if ref["status"] == 0:
+            assert np.array_equal(P[q, : pl[q]], ref["path_cells"]), q
+    assert spilled >= 4, spilled
+
+
+@pytest.mark.parametrize("lite", [False, True])
 def test_lpastar_replan_against_reference_and_oracle(lite):
     """LPA* incremental replanning (pmp_lpastar2d_replan_batch: plan() + OnPress edits, lpa_star.py:101-137)
     vs the reference's replays (tests/golden/lpa_replan.npz), all 60 cases in one launch, then a 256-query

@@ -194,8 +194,10 @@ def traffic_and_mfma(src, dst):
         print(json.dumps({k: v.get("hbm_bytes_per_dispatch") for k, v in workloads.items()}))
         if any(unattributed.values()):
             print("pmc: not attributed (seen, manifest):", unattributed)
-    # MFMA utilisation pass (rocprofv3's MfmaUtil expression: SQ_VALU_MFMA_BUSY_CYCLES summed over the
-    # chip / (GRBM_GUI_ACTIVE x SIMDs), per dispatch)
+    # MFMA utilisation pass: SQ_VALU_MFMA_BUSY_CYCLES summed over the chip / (GPU cycles x SIMDs), per
+    # dispatch.  rocprofv3 reports GRBM_GUI_ACTIVE summed over the 8 XCDs (MI355X_MICROARCH.md, "DVFS
+    # give-back": effective clock = GRBM_GUI_ACTIVE / 8 / wall time), so the dispatch's cycles are
+    # GRBM_GUI_ACTIVE / 8; round 4 divided by the sum and under-reported utilisation 8x.
     path = os.path.join(src, "prof_mfma", "run_results.db")
     if os.path.exists(path):
         d = sqlite3.connect(path)
@@ -204,15 +206,26 @@ def traffic_and_mfma(src, dst):
                                           "counters_collection group by kernel_name, counter_name"):
             mf.setdefault(short(name), {})[cn] = avg
             mf[short(name)]["dispatches"] = n
-        simds = 256 * 4
-        for k, e in mf.items():
-            if e.get("GRBM_GUI_ACTIVE"):
-                e["mfma_util_pct"] = 100.0 * e.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (e["GRBM_GUI_ACTIVE"] * simds)
+        mfma_util(mf)
         mf["_note"] = ("per-dispatch averages of the separate --pmc pass; mfma_util_pct = SQ_VALU_MFMA_BUSY_CYCLES / "
-                       "(GRBM_GUI_ACTIVE x 1024 SIMDs) x 100 (rocprofv3 MfmaUtil)")
+                       "(GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs) x 100 (GRBM_GUI_ACTIVE is the sum over the 8 XCDs)")
         with open(os.path.join(dst, "pmc_mfma.json"), "w") as f:
             json.dump(mf, f, indent=1, sort_keys=True)
         print("mfma", {k: v.get("mfma_util_pct") for k, v in mf.items() if not k.startswith("_")})
+
+
+XCDS, SIMDS = 8, 256 * 4
+
+
+def mfma_util(mf):
+    """mfma_util_pct per kernel entry of a pmc_mfma dict (in place): MFMA busy cycles over the
+    dispatch's GPU cycles (GRBM_GUI_ACTIVE / 8 XCDs) x 1024 SIMDs."""
+    for k, e in mf.items():
+        if isinstance(e, dict) and e.get("GRBM_GUI_ACTIVE"):
+            cycles = e["GRBM_GUI_ACTIVE"] / XCDS
+            e["gpu_cycles_per_dispatch"] = cycles
+            e["mfma_util_pct"] = 100.0 * e.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (cycles * SIMDS)
+    return mf
 
 
 if __name__ == "__main__":
