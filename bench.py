@@ -857,7 +857,8 @@ def graphs_leg(args, torch, dist, world, rank):
         lanes = []
         for _ in range(S):
             ctx = L.pmp_create(torch.cuda.current_device())
-            _lib.check(ctx, L.pmp_astar2d_set_engine(ctx, 0, 0), "engine")  # Theta*: one query per wave
+            _lib.check(ctx, L.pmp_astar2d_set_engine(ctx, args.theta_engine, 1 if args.theta_engine == 2 else 0),
+                       "engine")
             _lib.check(ctx, L.pmp_astar2d_reserve(ctx, 1024, 1024, tw, 0), "reserve")
             if args.theta_residency:
                 _lib.check(ctx, L.pmp_astar2d_set_residency(ctx, args.theta_residency), "residency")
@@ -935,6 +936,7 @@ def graphs_leg(args, torch, dist, world, rank):
             "metric": f"{algo} 2D plans/sec on the C2 1024^2 grid", "value": nq * args.graph_steps * world / elapsed,
             "unit": "plans/s", "queries_per_gpu": nq, "steps": args.graph_steps, "streams": S,
             "batches_per_launch": B, "workers": tw, "resident_per_cu": args.theta_residency,
+            "engine": "multi-query (4 per wave, astar2d_mq.hip)" if args.theta_engine == 2 else "one query per wave",
             "timed_launches_checked": checked,
             "ms_per_step": elapsed / args.graph_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
             "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -1660,6 +1662,8 @@ def main():
                     help="A* queries in flight per launch (persistent 16-lane groups on engine 1, waves on engine 0); "
                          "0 = the engine's default")
     ap.add_argument("--theta-workers", type=int, default=768, help="persistent Theta* 2D workers per launch")
+    ap.add_argument("--theta-engine", type=int, default=2,
+                    help="Theta* 2D engine: 2 = four queries per wave (astar2d_mq.hip, round 5), 0 = one per wave")
     ap.add_argument("--theta-residency", type=int, default=24,
                     help="Theta* 2D workers resident per CU (as --residency; with one multi-batch launch: 256 x this "
                          "many workers; 12 / 18 / 24 / 28 / 32: 8.5 / 11.3 / 11.9 / 11.85 / 11.75 k plans/s)")

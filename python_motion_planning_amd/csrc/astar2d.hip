@@ -28,6 +28,7 @@
 // Both operations are written for a low instruction count: the kernel is issue-bound (one wave per
 // query, a few waves per SIMD), so every instruction on the heap path costs wall time.
 #include "pmp_internal.h"
+#include "grid2d.h"
 
 // Diagnostic build only (make stamps -> libpmp_hip_stamps.so): per-query cycle sums of the
 // expansion segments go to counters[4q+0..3] = {pop, 3x3 wait, push, total} instead of the counts.
@@ -533,58 +534,6 @@ __device__ __forceinline__ void push_any(const Heap& h, int n, double itf, uint3
 
 
 
-// ThetaStar.lineOfSight (theta_star.py:110-171): Bresenham from (x1, y1) to (x2, y2) over the bit
-// grid; tau = (d_y - d_x) / 2 is compared as 2e against d_y - d_x.  Both endpoints are in the grid
-// (they are cells the search reached), so the line stays inside its bounding box.  The step bound
-// is never reached by the reference's loop; it only guarantees termination.
-__device__ __forceinline__ bool occ_bit(const uint32_t* occ, int H, int x, int y)
-{
-    const uint32_t ci = (uint32_t)x * (uint32_t)H + (uint32_t)y;
-    return ((occ[ci >> 5] >> (ci & 31u)) & 1u) != 0u;
-}
-__device__ bool los2d(const uint32_t* occ, int H, int x1, int y1, int x2, int y2)
-{
-    if (occ_bit(occ, H, x1, y1) || occ_bit(occ, H, x2, y2)) return false;
-    const int dx = abs(x2 - x1), dy = abs(y2 - y1);
-    const int sx = x2 > x1 ? 1 : (x2 < x1 ? -1 : 0), sy = y2 > y1 ? 1 : (y2 < y1 ? -1 : 0);
-    int x = x1, y = y1, e = 0;
-    const bool xmaj = dx > dy;
-    const int T = xmaj ? dy - dx : dx - dy;
-    const int du = xmaj ? dx : dy, dv = xmaj ? dy : dx;  // major / minor deltas
-    // The cells a line visits do not depend on the grid, so 8 steps are generated first and their
-    // 8 bit loads issued as one round (one memory latency per 8 cells instead of per cell); the
-    // first blocked cell in step order decides, as in the reference's loop.
-    constexpr int kB = 8;
-    for (int it = 0; it <= dx + dy + 1; it += kB) {
-        uint32_t ci[kB];
-        int nv = 0;
-#pragma unroll
-        for (int j = 0; j < kB; j++) {
-            const bool go = !(xmaj ? x == x2 : y == y2);
-            if (go) {
-                const bool maj = 2 * e >= T, mino = 2 * e <= T;  // e > tau: major; e < tau: minor; equal: both
-                if (maj) {
-                    if (xmaj) x += sx; else y += sy;
-                }
-                if (mino) {
-                    if (xmaj) y += sy; else x += sx;
-                }
-                e += (maj ? -dv : 0) + (mino ? du : 0);
-                nv++;
-            }
-            ci[j] = go ? (uint32_t)x * (uint32_t)H + (uint32_t)y : ~0u;
-        }
-        uint32_t wv[kB];
-#pragma unroll
-        for (int j = 0; j < kB; j++) wv[j] = ci[j] != ~0u ? occ[ci[j] >> 5] : 0u;
-#pragma unroll
-        for (int j = 0; j < kB; j++)
-            if (ci[j] != ~0u && ((wv[j] >> (ci[j] & 31u)) & 1u)) return false;
-        if (nv < kB || (xmaj ? x == x2 : y == y2)) return true;
-    }
-    return false;
-}
-
 // 4-bit cell state: word i >> 3, nibble i & 7
 template <typename P>
 __device__ __forceinline__ uint32_t cst_at(P cst, uint32_t i) { return (cst[i >> 3] >> ((i & 7) * 4)) & 15u; }
@@ -824,7 +773,7 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 py = (int)(par_lin - (uint32_t)px * (uint32_t)H);
                 gnode = gp_g + ((ndir >= 16) ? __dsqrt_rn((double)((x - px) * (x - px) + (y - py) * (y - py)))
                                              : ((ndir & 1) ? kSqrt2 : 1.0));
-                if (THETA == 2 && !los2d(occ, H, px, py, x, y)) {
+                if (THETA == 2 && !grid2d::los2d(occ, H, px, py, x, y)) {
                     // set vertex (lazy_theta_star.py:55-65): the first CLOSED, collision-free
                     // neighbour minimising its g + dist becomes the parent; g = inf if there is none
                     const bool cand = lane < 8 && (occ9 & need) == 0u && (cls9 & self_bit) != 0u;
@@ -917,7 +866,7 @@ __global__ __launch_bounds__(64) void astar2d_kernel(
                 const int nxl = x + mx, nyl = y + my;
                 const double g2 =
                     gp_g + __dsqrt_rn((double)((px - nxl) * (px - nxl) + (py - nyl) * (py - nyl)));
-                if (lane < 8 && (vm >> lane & 1ull) && g2 <= ig && (THETA == 2 || los2d(occ, H, nxl, nyl, px, py))) {
+                if (lane < 8 && (vm >> lane & 1ull) && g2 <= ig && (THETA == 2 || grid2d::los2d(occ, H, nxl, nyl, px, py))) {
                     ig = g2;
                     icode = 16 + mo;
                 }
@@ -1296,7 +1245,8 @@ extern "C" int pmp_graph2d_batch(pmp_ctx* ctx, void* stream, int algo, const uin
                                          want < sq_cap ? want : sq_cap, cost, path_len, path, path_cap, n_expanded,
                                          expand, expand_cap, counters, status);
     }
-    if (!theta && ctx->astar_reserved_mq && (ctx->astar_engine == 2 || (!ldsg && nq >= kMqMinBatch))) {
+    // the multi-query engine (A* / Dijkstra / GBFS, and Theta* / Lazy Theta* since round 5)
+    if (ctx->astar_reserved_mq && (ctx->astar_engine == 2 || (!ldsg && nq >= kMqMinBatch))) {
         const int groups = ctx->astar_workers < nq ? ctx->astar_workers : nq;
         int* queue = (int*)ctx->buf[SCR_AUX0];
         hipStream_t s = (hipStream_t)stream;

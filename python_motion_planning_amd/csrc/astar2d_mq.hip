@@ -38,6 +38,7 @@
 // where the epoch (1..15) numbers the group's queries, so a new query needs no reset of the 1 MiB
 // array except every 15th query.  g of a CLOSED cell in a per-group f64 array (as astar2d.hip).
 #include "pmp_internal.h"
+#include "grid2d.h"
 
 namespace {
 
@@ -54,27 +55,34 @@ constexpr uint32_t kMx1 = 0x1A90u, kMy1 = 0x01A9u;
 __device__ __forceinline__ int mot_x(int d) { return (int)((kMx1 >> (2 * d)) & 3u) - 1; }
 __device__ __forceinline__ int mot_y(int d) { return (int)((kMy1 >> (2 * d)) & 3u) - 1; }
 
-// HEUR: 0 euclidean, 1 manhattan (GraphSearcher.h, graph_search.py:41-44), 2 zero (Dijkstra)
+// HEUR bits 0-1: 0 euclidean, 1 manhattan (GraphSearcher.h, graph_search.py:41-44), 2 zero
+// (Dijkstra); bit 2 (kThetaLayout): the Theta* entry layout of astar2d.hip -- a 5-bit code (0..7 the
+// pusher's motion, 16 + motion "path 2": the parent is the pusher's own parent, theta_star.py:104-108;
+// 8 the start) and a 13-bit dy (H <= 4096)
+constexpr int kThetaLayout = 4;
+template <int HEUR> constexpr int hkind() { return HEUR & 3; }
+template <int HEUR> constexpr int dbits() { return (HEUR & kThetaLayout) ? 5 : 4; }
 template <int HEUR>
 __device__ __forceinline__ uint32_t pack_cm(int dx, int dy, int dir)
 {
-    return ((uint32_t)dx << 18) | (((uint32_t)dy & 0x3FFFu) << 4) | (uint32_t)dir;
+    constexpr int S = dbits<HEUR>();
+    return ((uint32_t)dx << 18) | (((uint32_t)dy & ((1u << (18 - S)) - 1u)) << S) | (uint32_t)dir;
 }
-__device__ __forceinline__ int cm_dx(uint32_t cm) { return (int)cm >> 18; }
-__device__ __forceinline__ int cm_dy(uint32_t cm) { return (int)(cm << 14) >> 18; }
-__device__ __forceinline__ int cm_dir(uint32_t cm) { return (int)(cm & 15u); }
+template <int HEUR> __device__ __forceinline__ int cm_dx(uint32_t cm) { return (int)cm >> 18; }
+template <int HEUR> __device__ __forceinline__ int cm_dy(uint32_t cm) { return (int)(cm << 14) >> (14 + dbits<HEUR>()); }
+template <int HEUR> __device__ __forceinline__ int cm_dir(uint32_t cm) { return (int)(cm & ((1u << dbits<HEUR>()) - 1u)); }
 template <int HEUR>
 __device__ __forceinline__ uint32_t hkey(uint32_t cm)
 {
-    if (HEUR == 2) return 0u;
-    const int dx = cm_dx(cm), dy = cm_dy(cm);
-    if (HEUR == 1) return (uint32_t)(abs(dx) + abs(dy));
+    if (hkind<HEUR>() == 2) return 0u;
+    const int dx = cm_dx<HEUR>(cm), dy = cm_dy<HEUR>(cm);
+    if (hkind<HEUR>() == 1) return (uint32_t)(abs(dx) + abs(dy));
     return (uint32_t)(__mul24(dx, dx) + __mul24(dy, dy));
 }
 template <int HEUR>
 __device__ __forceinline__ double h_of_key(uint32_t hk)
 {
-    return HEUR == 2 ? 0.0 : (HEUR == 1 ? (double)hk : __dsqrt_rn((double)hk));
+    return hkind<HEUR>() == 2 ? 0.0 : (hkind<HEUR>() == 1 ? (double)hk : __dsqrt_rn((double)hk));
 }
 // Node.__lt__ (node.py:51-54)
 __device__ __forceinline__ bool key_lt(double fa, uint32_t ka, double fb, uint32_t kb)
@@ -183,6 +191,7 @@ constexpr int kEntLds = kKeys ? 16 : 12;  // LDS bytes per heap position
 #define PMP_MQ_BLOCKS 1
 #endif
 constexpr bool kBlocks = PMP_MQ_BLOCKS != 0;
+constexpr bool kBlocks2 = PMP_MQ_BLOCKS == 2;
 // Write-traffic attribution (dev builds only, tools/build_variant.sh): every store of the selected
 // categories is issued twice, the copy into a mirror region with the same layout, so the extra
 // WRITE_SIZE over the default build is that category's write traffic.  Bits: 1 the trivial-push run's
@@ -206,7 +215,10 @@ __device__ __forceinline__ uint32_t spill_off(const GHeap& h, int p)
     // blk = Q - 2^(L0-1) (2 4^b + 1) / 3, and (2 4^b + 1) / 3 = 1, 3, 11, 43, 171 for b = 0..4
     const uint32_t kb = (uint32_t)(0xAB2B0B0301ull >> (8 * b)) & 0xFFu;
     const uint32_t blk = Q - (kb << (h.L0 - 1));
-    const uint32_t slot = (u & ((2u << o) - 1u)) + 2u * (uint32_t)o;
+    // kBlocks 1: [c0 c1 g00 g01 g10 g11]; kBlocks 2: [c0 g00 g01 -][c1 g10 g11 -] (a child and its
+    // two children in one 64-B half: a path writes one half of a block)
+    const uint32_t slot = kBlocks2 ? (o ? ((u >> 1) & 1u) * 4u + 1u + (u & 1u) : (u & 1u) * 4u)
+                                   : (u & ((2u << o) - 1u)) + 2u * (uint32_t)o;
     return h.gbase + blk * 128u + slot * 16u;
 }
 
@@ -442,9 +454,12 @@ __device__ __forceinline__ int path_op(const GHeap& h, bool on, bool pop, uint32
     return b;
 }
 
-template <int HEUR, bool GZERO, bool T2LDS>
-// <= 128 VGPRs: four waves per SIMD, up to 64 queries resident per CU
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void astar2d_mqu_kernel(
+// THETA: 1 = ThetaStar (theta_star.py:44-108), 2 = LazyThetaStar (lazy_theta_star.py:38-114), with
+// HEUR's Theta* layout bit; the CLOSED parent of a cell (any cell) per slot in Pc_all.
+template <int HEUR, bool GZERO, bool T2LDS, int THETA = 0>
+// <= 128 VGPRs: four waves per SIMD, up to 64 queries resident per CU (Theta*: three, the line-of-sight
+// state would spill at 128)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 4))) void astar2d_mqu_kernel(
     const uint32_t* __restrict__ occ, int W, int H, const int32_t* __restrict__ start_xy,
     const int32_t* __restrict__ goal_xy, const int32_t* __restrict__ order, int nq, double* __restrict__ cost_out,
     int32_t* __restrict__ path_len_out, uint32_t* __restrict__ path_out, int path_cap,
@@ -452,7 +467,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void as
     int64_t* __restrict__ counters, int32_t* __restrict__ status_out, int* __restrict__ queue,
     uint4* __restrict__ spill_all, int spill_n, int heap_cap, int lds_cap, int region, uint8_t* __restrict__ cst_all,
     size_t cst_bytes, double* __restrict__ G_all, uint32_t* __restrict__ t2_all, uint32_t* __restrict__ epoch_all,
-    int prio_n, int lone, unsigned long long* __restrict__ span)
+    int prio_n, int lone, unsigned long long* __restrict__ span, uint32_t* __restrict__ Pc_all)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
@@ -482,6 +497,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void as
     }
     uint8_t* cst = cst_all + slot * cst_bytes;
     double* G = G_all + slot * ((size_t)W * (size_t)H);
+    uint32_t* Pc = THETA ? Pc_all + slot * ((size_t)W * (size_t)H) : nullptr;  // CLOSED parent cell
     const size_t nslots = (size_t)gridDim.x * 4u;
     const bool mir8 = (kMirror & 8) && (slot & 1u) == 0u;
     uint8_t* cst_m = cst_all + (nslots + slot / 2) * cst_bytes;
@@ -497,7 +513,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void as
     if (mo & 1) need |= (1u << (3 + (my + 1))) | (1u << ((mx + 1) * 3 + 1));
     const uint32_t self_bit = 1u << ((mx + 1) * 3 + (my + 1));
     // the 3x3 round: lanes 0..8 occupancy of cell (x + i/3 - 1, y + i%3 - 1); lanes 9..11 the
-    // cell-state bytes of row i - 9; lane 12 G[parent]
+    // cell-state bytes of row i - 9; lane 12 G[pusher]; THETA: lane 13 the pusher's CLOSED parent
     const int blk_dx = gl < 9 ? gl / 3 - 1 : (gl < 12 ? gl - 10 : 0);
     const int blk_dy = gl < 9 ? gl % 3 - 1 : 0;
 
@@ -641,6 +657,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void as
         int blk_sh = 0;
         bool blk_in = false;
         double gpar = 0.0;
+        uint32_t ppar = 0u;  // THETA: Pc[pusher] (lane 13)
         Ld pld;
         if (push) {
             const int m = __ffs((int)pend) - 1;
@@ -656,9 +673,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void as
             n -= 1;
             n0 = n;
             popn = 1;
-            const int ndir = cm_dir(ncm);
-            x = ndir == 8 ? sx : gx - cm_dx(ncm);
-            y = ndir == 8 ? sy : gy - cm_dy(ncm);
+            const int ndir = cm_dir<HEUR>(ncm);
+            x = ndir == 8 ? sx : gx - cm_dx<HEUR>(ncm);
+            y = ndir == 8 ? sy : gy - cm_dy<HEUR>(ncm);
+            const bool has_pusher = THETA ? ndir != 8 : ndir < 8;
+            const int pm = ndir & 7;  // the pusher's motion
             nlin = (uint32_t)x * (uint32_t)H + (uint32_t)y;
             // every lane issues all three loads (lanes that need none read index 0): no branch per
             // lane class, so no load destination is zero-filled under another exec mask
@@ -671,12 +690,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void as
                 const uint32_t lo =
                     (is_cst && in_cst) ? (uint32_t)cx * (uint32_t)H + (uint32_t)(y > 0 ? y - 1 : 0) : 0u;
                 const uint32_t a0 = lo & ~3u;
-                const uint32_t gi =
-                    (!GZERO && gl == 12 && ndir < 8) ? nlin - (uint32_t)(mot_x(ndir) * H + mot_y(ndir)) : 0u;
+                const uint32_t pusher = has_pusher ? nlin - (uint32_t)(mot_x(pm) * H + mot_y(pm)) : 0u;
+                const uint32_t gi = (!GZERO && gl == 12) ? pusher : 0u;
                 const uint32_t ow = occ[ci >> 5];
                 const uint32_t* p32 = reinterpret_cast<const uint32_t*>(cst + a0);
                 const uint32_t c0 = p32[0], c1 = p32[1];
                 gpar = GZERO ? 0.0 : G[gi];
+                if (THETA) ppar = Pc[gl == 13 ? pusher : 0u];
                 blk_in = is_occ ? in_occ : (is_cst && in_cst);
                 blk_sh = is_occ ? (int)(ci & 31u) : (int)((uint32_t)cx * (uint32_t)H + (uint32_t)y - 1u - a0);
                 blk_w = is_occ ? ow : c0;
@@ -736,20 +756,87 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void as
             const uint32_t cls9 = bc<9>(row) | (bc<10>(row) << 3) | (bc<11>(row) << 6);
             const double gp = bcf<12>(gpar);
             if (!(cls9 & 16u)) {  // node.current not in CLOSED (a_star.py:57-58)
-                const int ndir = cm_dir(ncm);
-                const double gnode = (GZERO || ndir == 8) ? 0.0 : gp + ((ndir & 1) ? kSqrt2 : 1.0);
+                const int ndir = cm_dir<HEUR>(ncm);
+                double gnode = (GZERO || ndir == 8) ? 0.0 : gp + ((ndir & 1) ? kSqrt2 : 1.0);
+                // THETA: the node's parent (cell, coordinates, g) and its expand-record code
+                uint32_t par_lin = nlin;
+                int px = x, py = y, ecode = ndir;
+                double gp_g = 0.0;
+                if (THETA && ndir != 8) {
+                    const int pm = ndir & 7;
+                    par_lin = nlin - (uint32_t)(mot_x(pm) * H + mot_y(pm));  // the pusher
+                    gp_g = gp;
+                    if (ndir >= 16) {  // path 2: node.g = parent.g + dist (theta_star.py:106-108)
+                        par_lin = bc<13>(ppar);
+                        const double t = G[gl == 12 ? par_lin : 0u];
+                        gp_g = bcf<12>(t);
+                    }
+                    px = (int)(par_lin / (uint32_t)H);
+                    py = (int)(par_lin - (uint32_t)px * (uint32_t)H);
+                    gnode = gp_g + (ndir >= 16 ? __dsqrt_rn((double)((x - px) * (x - px) + (y - py) * (y - py)))
+                                               : ((ndir & 1) ? kSqrt2 : 1.0));
+                    if (THETA == 2 && !grid2d::los2d(occ, H, px, py, x, y)) {
+                        // set vertex (lazy_theta_star.py:55-65): the first CLOSED, collision-free
+                        // neighbour minimising its g + dist becomes the parent; g = inf if there is none
+                        const bool cand = gl < 8 && (occ9 & need) == 0u && (cls9 & self_bit) != 0u;
+                        const uint32_t cl = (uint32_t)((int)nlin + mx * H + my);
+                        const double gn = G[cand ? cl : 0u];
+                        const double gc = gn + mcost;
+                        const uint32_t cmask = rbits(cand, gb) & 0xFFu;
+                        double best = __longlong_as_double(0x7ff0000000000000ll);
+                        int bm = -1;
+                        for (int m = 0; m < 8; m++) {  // motion order, first minimum
+                            const double c = bpf(gc, gb + m);
+                            if (((cmask >> m) & 1u) && best > c) {
+                                best = c;
+                                bm = m;
+                            }
+                        }
+                        gnode = best;
+                        if (bm >= 0) {
+                            gp_g = bpf(gn, gb + bm);
+                            px = x + mot_x(bm);
+                            py = y + mot_y(bm);
+                            par_lin = (uint32_t)px * (uint32_t)H + (uint32_t)py;
+                            ecode = 24 + bm;
+                        } else {
+                            ecode |= 32;
+                        }
+                    }
+                }
                 // CLOSED[node.current] = node (a_star.py:82)
-                if (gl == 0) cst[nlin] = (uint8_t)((ep << 4) | (uint32_t)(ndir + 1));
+                if (gl == 0) cst[nlin] = (uint8_t)((ep << 4) | (uint32_t)(THETA ? 1 : ndir + 1));
                 if (!GZERO && gl == 1) G[nlin] = gnode;
+                if (THETA && gl == 0) Pc[nlin] = par_lin;  // read back by this lane's extractPath
                 if (mir8 && gl == 0) cst_m[nlin] = (uint8_t)((ep << 4) | (uint32_t)(ndir + 1));
                 if (mir8 && !GZERO && gl == 1) G_m[nlin] = gnode;
                 if (gl == 2 && expand_out && nexp < expand_cap)
-                    expand_out[(size_t)q * expand_cap + nexp] = nlin | ((uint32_t)ndir << 28);
+                    expand_out[(size_t)q * expand_cap + nexp] =
+                        THETA ? (nlin | ((uint32_t)ecode << 26)) : (nlin | ((uint32_t)ndir << 28));
                 nexp++;
                 if (x == gx && y == gy) {  // goal (a_star.py:61-64): extractPath, goal -> start
                     st = PMP_FOUND;
                     wave_sync_mem();
-                    if (gl == 0) {
+                    if (THETA && gl == 0) {  // via the CLOSED parents (any cell), hypot per hop
+                        uint32_t li = nlin;
+                        int cx = x, cy = y;
+                        double cost = 0.0;
+                        int len = 0;
+                        uint32_t* pth = path_out + (size_t)q * path_cap;
+                        for (;;) {
+                            if (len < path_cap) pth[len] = li;
+                            len++;
+                            if (cx == sx && cy == sy) break;
+                            const uint32_t pl = Pc[li];
+                            const int qx = (int)(pl / (uint32_t)H), qy = (int)(pl - (uint32_t)qx * (uint32_t)H);
+                            cost += __dsqrt_rn((double)((cx - qx) * (cx - qx) + (cy - qy) * (cy - qy)));
+                            cx = qx;
+                            cy = qy;
+                            li = pl;
+                        }
+                        goal_cost = cost;
+                        plen = len;
+                    } else if (gl == 0) {
                         int cx = x, cy = y;
                         double cost = 0.0;
                         int len = 0;
@@ -774,8 +861,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void as
                     uint32_t vm = rbits(nb_ok, gb) & 0xFFu;
                     const uint32_t gm = rbits(nb_ok && ndx == 0 && ndy == 0, gb) & 0xFFu;
                     if (gm) vm &= (gm << 1) - 1u;
-                    const double ig = gnode + mcost;
-                    icm = pack_cm<HEUR>(ndx, ndy, mo);
+                    double ig = gnode + mcost;
+                    int icode = mo;
+                    if (THETA && ndir != 8) {
+                        // updateVertex(CLOSED[node.parent], node_n) (theta_star.py:96-108; lazy_theta_star.py:
+                        // 103-114 without the line of sight): path 2 when parent.g + dist <= node_n.g
+                        const int nxl = x + mx, nyl = y + my;
+                        const double g2 = gp_g + __dsqrt_rn((double)((px - nxl) * (px - nxl) + (py - nyl) * (py - nyl)));
+                        if (gl < 8 && ((vm >> mo) & 1u) && g2 <= ig &&
+                            (THETA == 2 || grid2d::los2d(occ, H, nxl, nyl, px, py))) {
+                            ig = g2;
+                            icode = 16 + mo;
+                        }
+                    }
+                    icm = pack_cm<HEUR>(ndx, ndy, icode);
                     ikk = hkey<HEUR>(icm);
                     ifv = ig + h_of_key<HEUR>(ikk);
                     if (n + __popc(vm) > heap_cap) st = PMP_CAP_OVERFLOW;  // a push would find n >= heap_cap
@@ -874,6 +973,12 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
     uint4* spill = (uint4*)pmp_scratch(ctx, SCR_MQ_SPILL, (kMirror & 7 ? 2 : 1) * slots * (size_t)spill_n * 16 + 16);
     uint32_t* t2 = (uint32_t*)pmp_scratch(ctx, SCR_MQ_T2, slots * kT2Words * 4 + 16);
     if (!spill || !t2) return PMP_ENOMEM;
+    const int theta = algo == PMP_ALGO_THETA ? 1 : (algo == PMP_ALGO_LAZY_THETA ? 2 : 0);
+    uint32_t* Pc = nullptr;  // Theta*: the CLOSED parent cell of every cell, per slot
+    if (theta) {
+        Pc = (uint32_t*)pmp_scratch(ctx, SCR_MQ_PC, slots * (size_t)W * H * 4 + 16);
+        if (!Pc) return PMP_ENOMEM;
+    }
     uint8_t* cstp;
     size_t cst_bytes;
     double* G;
@@ -884,14 +989,24 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
     }
     const size_t lds = (size_t)region * (lone ? 1 : 4);
     const int prio = order ? ctx->astar_prio_n : 0;
-#define MQ_LAUNCH(HE, GZ, T2)                                                                                       \
-    hipLaunchKernelGGL((astar2d_mqu_kernel<HE, GZ, T2>), dim3(waves), dim3(64), lds, s, occ_bits, W, H, start_xy,    \
+#define MQ_LAUNCH_T(HE, GZ, T2, TH)                                                                                 \
+    hipLaunchKernelGGL((astar2d_mqu_kernel<HE, GZ, T2, TH>), dim3(waves), dim3(64), lds, s, occ_bits, W, H, start_xy, \
                        goal_xy, order, nq, cost, path_len, path, path_cap, n_expanded, expand, expand_cap, counters, \
                        status, queue, spill, spill_n, heap_cap, lds_cap, region, cstp, cst_bytes, G, t2, ep, prio,   \
-                       lone ? 1 : 0, ctx->span)
+                       lone ? 1 : 0, ctx->span, Pc)
+#define MQ_LAUNCH(HE, GZ, T2) MQ_LAUNCH_T(HE, GZ, T2, 0)
     const int he = algo == PMP_ALGO_DIJKSTRA ? 2 : heuristic;
     const bool gz = algo == PMP_ALGO_GBFS;
-    if (t2lds) {
+    constexpr int TL = kThetaLayout;
+    if (theta) {
+        if (t2lds) {
+            if (theta == 1) { if (he == 1) MQ_LAUNCH_T(TL | 1, false, true, 1); else MQ_LAUNCH_T(TL, false, true, 1); }
+            else { if (he == 1) MQ_LAUNCH_T(TL | 1, false, true, 2); else MQ_LAUNCH_T(TL, false, true, 2); }
+        } else {
+            if (theta == 1) { if (he == 1) MQ_LAUNCH_T(TL | 1, false, false, 1); else MQ_LAUNCH_T(TL, false, false, 1); }
+            else { if (he == 1) MQ_LAUNCH_T(TL | 1, false, false, 2); else MQ_LAUNCH_T(TL, false, false, 2); }
+        }
+    } else if (t2lds) {
         if (gz) { if (he == 1) MQ_LAUNCH(1, true, true); else MQ_LAUNCH(0, true, true); }
         else if (he == 2) MQ_LAUNCH(2, false, true);
         else if (he == 1) MQ_LAUNCH(1, false, true);
@@ -903,6 +1018,7 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
         else MQ_LAUNCH(0, false, false);
     }
 #undef MQ_LAUNCH
+#undef MQ_LAUNCH_T
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }

@@ -174,6 +174,14 @@ struct L3 {
     UList U;
     double* g;
     double* rhs;
+    // Written-this-query bits of g / rhs (LDS, one bit per voxel; `touch`): a voxel whose bit is clear
+    // holds the query's initial value (inf; rhs(start) = 0 is written), so a query starts with no
+    // reset of the two HBM arrays (8 B x 2 per voxel, more than its whole search reads) and loads
+    // only the g / rhs values it wrote -- an expansion's 5x5x5 block mostly holds never-expanded
+    // voxels (g = inf).  Without `touch` (grids too large for the bits) the arrays are reset per query.
+    lds_u32* gt;
+    lds_u32* rt;
+    bool touch;
     lds_f64* cube;  // 125 g values of the 5x5x5 block around the centre
     int lane;
     int start, goal;  // voxel ids
@@ -189,6 +197,14 @@ struct L3 {
 #else
 #define LSTAMP(v)
 #endif
+
+    __device__ __forceinline__ bool gw(int c) const { return !touch || ((gt[c >> 5] >> (c & 31)) & 1u); }
+    __device__ __forceinline__ bool rw(int c) const { return !touch || ((rt[c >> 5] >> (c & 31)) & 1u); }
+    __device__ __forceinline__ double g_at(int c) const { return gw(c) ? g[c] : kInf; }
+    __device__ __forceinline__ void mark(lds_u32* t, int c) const
+    {
+        if (touch) __hip_atomic_fetch_or(t + (c >> 5), 1u << (c & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
 
     __device__ __forceinline__ double hval(int x, int y, int z) const
     {
@@ -286,15 +302,18 @@ struct L3 {
             const int x1 = cx + b1 / 25 - 2, y1 = cy + (b1 / 5) % 5 - 2, z1 = cz + b1 % 5 - 2;
             gin0 = geo.in(x0, y0, z0);
             gin1 = b1 < 125 && geo.in(x1, y1, z1);
-            gb0 = g[gin0 ? geo.id(x0, y0, z0) : center];
-            gb1 = g[gin1 ? geo.id(x1, y1, z1) : center];
+            const int i0 = gin0 ? geo.id(x0, y0, z0) : center, i1 = gin1 ? geo.id(x1, y1, z1) : center;
+            gin0 = gin0 && gw(i0);  // a voxel this query never wrote: g = inf, no load
+            gin1 = gin1 && gw(i1);
+            gb0 = gin0 ? g[i0] : kInf;
+            gb1 = gin1 ? g[i1] : kInf;
         }
         const int m = lane < 26 ? lane : 0;
         const int dx = lane < 26 ? c_m[m][0] : 0, dy = lane < 26 ? c_m[m][1] : 0, dz = lane < 26 ? c_m[m][2] : 0;
         const int px = cx + dx, py = cy + dy, pz = cz + dz;
         const bool mine = lane <= 26 && geo.in(px, py, pz);
         const int P = mine ? geo.id(px, py, pz) : 0;
-        const double rvl = rhs[mine ? P : center];
+        const double rvl = (mine && rw(P)) ? rhs[P] : kInf;
         cube[lane] = gin0 ? gb0 : kInf;
         if (lane < 61) cube[lane + 64] = gin1 ? gb1 : kInf;
         // ---- block masks: in the map / obstacle, as wave-uniform bits
@@ -424,8 +443,14 @@ struct L3 {
         // deferred stores: the updated voxels' rhs (the start keeps its own), the centre's new g
         {
             const bool upd = mine && P != start && (is_nb || (lane == 26 && do_center));
-            if (upd) rhs[P] = rv;
-            if (expand && lane == 0) g[center] = gnew;
+            if (upd) {
+                rhs[P] = rv;
+                mark(rt, P);
+            }
+            if (expand && lane == 0) {
+                g[center] = gnew;
+                mark(gt, center);
+            }
         }
         wsync();
 #ifdef PMP_STAMPS
@@ -461,6 +486,10 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
     S.U.cap = ucap;
     S.occ.l = (lds_u32*)(smem + 1024 + (size_t)20 * ucap);
     S.occ.lds = occ_lds != 0;
+    // the written-this-query bits after the occupancy (with it: both fit when the occupancy does)
+    S.touch = occ_lds != 0;
+    S.gt = S.occ.l + ((words + 3) & ~3);
+    S.rt = S.gt + ((words + 3) & ~3);
     S.occ.g = occ_scr + (size_t)blockIdx.x * (size_t)words;
     S.occ.geo = S.geo;
     {
@@ -523,9 +552,21 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
                 if (S.occ.lds) S.occ.l[w] = src[w];
                 else S.occ.g[w] = src[w];
             }
-            for (int c = lane; c < ncell; c += 64) {
-                S.g[c] = kInf;
-                S.rhs[c] = c == S.start ? 0.0 : kInf;
+            if (S.touch) {
+                for (int w = lane; w < words; w += 64) {
+                    S.gt[w] = 0u;
+                    S.rt[w] = 0u;
+                }
+                wsync();
+                if (lane == 0) {
+                    S.rhs[S.start] = 0.0;
+                    S.mark(S.rt, S.start);
+                }
+            } else {
+                for (int c = lane; c < ncell; c += 64) {
+                    S.g[c] = kInf;
+                    S.rhs[c] = c == S.start ? 0.0 : kInf;
+                }
             }
         }
         wsync();
@@ -646,7 +687,7 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
                     bool ok = lane < 26 && S.geo.in(nx, ny, nz) && !S.occ.at(nx, ny, nz) &&
                               !S.occ.coll(x, y, z, nx, ny, nz);
                     double gn = kInf;
-                    if (ok) gn = S.g[S.geo.id(nx, ny, nz)];
+                    if (ok) gn = S.g_at(S.geo.id(nx, ny, nz));
                     uint64_t vm = ballot(ok);
                     if (!vm) { st = PMP_NO_PATH; break; }
                     int bm = -1;
@@ -724,7 +765,8 @@ extern "C" int pmp_lpastar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* o
     // up to 16 waves per CU (tools/dyn3d_sweep.py): the LDS share of each holds the g block, U (20 B per
     // entry, the rest spills) and the occupancy
     const int per_cu = std::max(1, std::min(ctx->workers_per_cu > 0 ? ctx->workers_per_cu : 16, (nq + 255) / 256));
-    const int occ_bytes = occ_lds ? ((words * 4 + 15) & ~15) : 0;
+    // occupancy bits + the two written-this-query bitmaps (lpa3d_kernel S.gt / S.rt)
+    const int occ_bytes = occ_lds ? 3 * ((words * 4 + 15) & ~15) : 0;
     int ucap = (((160 * 1024) / per_cu - 1024 - occ_bytes) / 20) & ~15;
     if (ucap < 64) ucap = 64;
     if ((size_t)ucap > ncell + 1) ucap = (int)((ncell + 1 + 15) & ~(size_t)15);

@@ -51,7 +51,7 @@ struct pmp_ctx {
 
 enum ScratchSlot { SCR_HEAP = 0, SCR_CLOSED = 1, SCR_PDIR = 2, SCR_G = 3, SCR_AUX0 = 4, SCR_AUX1 = 5, SCR_AUX2 = 6, SCR_AUX3 = 7,
                    SCR_BITS = 8, SCR_AUX4 = 9, SCR_PAR = 10, SCR_MQ_SPILL = 11, SCR_MQ_CST = 12, SCR_MQ_G = 13,
-                   SCR_MQ_T2 = 14, SCR_MQ_EPOCH = 15, SCR_DWA = 16, SCR_NSLOTS = 17 };
+                   SCR_MQ_T2 = 14, SCR_MQ_EPOCH = 15, SCR_DWA = 16, SCR_MQ_PC = 17, SCR_NSLOTS = 18 };
 
 int pmp_set_err(pmp_ctx* ctx, int code, const std::string& msg);
 // Workers per CU whose LDS shares a launch of `per_cu` workers per CU must fit beside

@@ -42,7 +42,7 @@ KERNELS = {  # short name -> regex on the demangled kernel name
 # the 2D graph kernels' template <HEUR, GZERO, THETA> (astar2d.hip): one short name per planner, so the
 # headline's traffic is never taken from the Theta* launches of the same kernel template
 _G2D = re.compile(r"astar2d_kernel<(\d+), (true|false), (\d)(?:, (?:true|false))?>")  # 4th: LDS grid state
-_MQ = re.compile(r"astar2d_(?:mqu?|sq)_kernel<(\d+), (true|false), (true|false)>")  # multi- / single-query
+_MQ = re.compile(r"astar2d_(?:mqu?|sq)_kernel<(\d+), (true|false), (true|false)(?:, (\d))?>")  # multi- / single-query
 
 
 def short(name):
@@ -57,7 +57,9 @@ def short(name):
     m = _MQ.search(name)
     if m:  # the multi-query <HEUR, GZERO, T2LDS> and single-query <HEUR, GZERO, LDSG> engines: the
         # short names of the one-query-per-wave kernel (pmp_graph2d_batch picks among the three)
-        heur, gzero = int(m.group(1)), m.group(2) == "true"
+        heur, gzero, theta = int(m.group(1)), m.group(2) == "true", int(m.group(4) or 0)
+        if theta:  # <HEUR | Theta* layout, false, T2LDS, THETA> (round 5)
+            return "theta2d_kernel" if theta == 1 else "lazy_theta2d_kernel"
         return "gbfs2d_kernel" if gzero else ("dijkstra2d_kernel" if heur == 2 else "astar2d_kernel")
     for k, rx in KERNELS.items():
         if re.search(rx, name):

@@ -2,15 +2,20 @@
 # round 5: A* 2D write-traffic attribution at the bench geometry (20 C2 batches in one launch, 60 per
 # CU).  One WRITE_SIZE pass per build: the default and the mirror builds of astar2d_mq.hip
 # (PMP_MQ_MIRROR bits 1 / 2 / 4 / 8: tools/build_variant.sh mir<bit>), each store of the mirrored
-# category issued twice.  Per-dispatch WRITE_SIZE of the 20-batch launch -> gpurun_out/attr/summary.txt
+# category issued twice; blk2 / blk2mir = the half-block spill layout (PMP_MQ_BLOCKS=2), plain / all
+# spill stores mirrored.  Per-dispatch WRITE_SIZE of the 20-batch launch -> gpurun_out/attr/summary.txt
 R=${GRAFT_REPO_ROOT:-/root/repo}
 OUT=$R/gpurun_out/attr
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-for v in ${VARIANTS:-default mir1 mir2 mir4 mir8}; do
+# spec = build[:counter,counter...] (default counter WRITE_SIZE); blk2 = the half-block spill layout
+for spec in ${SPECS:-default:WRITE_SIZE,FETCH_SIZE mir1 mir2 mir4 mir8 blk2:WRITE_SIZE,FETCH_SIZE blk2mir}; do
+  v=${spec%%:*}
+  cs=WRITE_SIZE
+  [ "$spec" = "$v" ] || cs=${spec#*:}
   lib=$R/python_motion_planning_amd/libpmp_hip.so
   [ "$v" = default ] || lib=$R/python_motion_planning_amd/libpmp_hip_$v.so
-  for c in ${COUNTERS:-WRITE_SIZE}; do
+  for c in ${cs//,/ }; do
     PMP_HIP_LIB=$lib timeout -s KILL 240 rocprofv3 --pmc $c -d $OUT/$v-$c -o run -- \
       python3 $R/bench.py --legs none --no-cpu-baseline --steps 20 --warmup 5 --detail-out $OUT/$v-$c.detail.json \
       > $OUT/$v-$c.json 2> $OUT/$v-$c.err || { echo "$v $c failed"; tail -5 $OUT/$v-$c.err; exit 1; }

@@ -1,19 +1,24 @@
 #!/bin/bash
-# round 5, call 1: the GPU suite (RRT* coarse tree in LDS, DWA k-split, LPA* U past the LDS share, geometry restore, the 3D
-# kernel without the decrease-key variant), the DWA 32-agent step time, the MPC tolerance probe, then
-# the A* 2D write attribution (tools/r5_attr.sh)
+# round 5, call 1: the GPU suite (Theta* on the multi-query engine, RRT* coarse tree in LDS, DWA
+# k-split, LPA* U past the LDS share, LPAStar3D written-this-query bits, geometry restore), then
+# short bench legs for the changed kernels and the MPC tolerance probe
 R=${GRAFT_REPO_ROOT:-/root/repo}
 cd $R; mkdir -p gpurun_out/c1
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/c1/gpu_tests.log 2>&1 || { tail -60 gpurun_out/c1/gpu_tests.log; exit 1; }
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/c1/gpu_tests.log 2>&1 || { tail -60 gpurun_out/c1/gpu_tests.log; exit 1; }
 tail -3 gpurun_out/c1/gpu_tests.log
-for na in 32 256; do
-  timeout -k 10 200 python3 bench.py --legs dwa --agents $na --steps 2 --warmup 1 --no-cpu-baseline --control-steps 50 \
-    --detail-out gpurun_out/c1/dwa_$na.json > gpurun_out/c1/dwa_$na.out 2> gpurun_out/c1/dwa_$na.err || { tail -20 gpurun_out/c1/dwa_$na.err; exit 1; }
-  python3 -c "import json; d=json.load(open('gpurun_out/c1/dwa_$na.json'))['secondary']['mpc_sampled_dwa']; print('dwa agents $na', d['value'], 'kernel ms', d['kernel_ms_per_launch'], d.get('timed_launches_checked'))"
-done
-timeout -k 10 300 python3 bench.py --legs rrt --steps 2 --warmup 1 --no-cpu-baseline --rrt-steps 3 \
-  --detail-out gpurun_out/c1/rrt.json > gpurun_out/c1/rrt.out 2> gpurun_out/c1/rrt.err || { tail -20 gpurun_out/c1/rrt.err; exit 1; }
-python3 -c "import json; d=json.load(open('gpurun_out/c1/rrt.json'))['secondary']['rrt_star']; print('rrt*', d['value'], 'kernel ms', d['kernel_ms_per_launch'], d.get('timed_launches_checked'), d['roofline']['frac'])"
+leg() {  # name, bench args...
+  local n=$1; shift
+  timeout -k 10 300 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --detail-out gpurun_out/c1/$n.json "$@" \
+    > gpurun_out/c1/$n.out 2> gpurun_out/c1/$n.err || { tail -20 gpurun_out/c1/$n.err; exit 1; }
+  python3 -c "
+import json; d=json.load(open('gpurun_out/c1/$n.json'))['secondary']
+for k, v in d.items(): print('$n', k, round(v['value']), v.get('unit'), 'kernel_ms', v.get('kernel_ms_per_launch'), 'frac', v.get('roofline', {}).get('frac'), 'checked', v.get('timed_launches_checked'))"
+}
+leg dwa32 --legs dwa --agents 32 --control-steps 50
+leg dwa256 --legs dwa --control-steps 50
+leg rrt --legs rrt --rrt-steps 3
+leg dyn3d --legs dyn3d
+for r in 24 32 40; do leg theta_r$r --legs graphs --theta-residency $r; done
+leg theta_e0 --legs graphs --theta-engine 0
 timeout -k 10 200 python3 tools/mpc_tol.py > gpurun_out/c1/mpc_tol.log 2>&1 || { tail -20 gpurun_out/c1/mpc_tol.log; exit 1; }
 grep -v amdgpu.ids gpurun_out/c1/mpc_tol.log
-bash tools/r5_attr.sh
