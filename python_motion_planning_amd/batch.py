@@ -83,21 +83,21 @@ def astar2d_batch(occ, starts, goals, heuristic: str = "euclidean", path_cap: in
     return out
 
 
-def astar2d_full_bound(shape, starts, goals, heuristic="euclidean", path_cap=None, expand_cap=0, counters=False,
+def astar2d_full_bound(occ, starts, goals, heuristic="euclidean", path_cap=None, expand_cap=0, counters=False,
                        occ_bits=None, algo="astar"):
     """The overflow re-plan: the queries (a few) planned with the full heap bound (8 W H + 8 entries,
     which no search exceeds) on at most 256 workers, then the context's geometry restored as it was --
     the host's own reservation (its explicit heap_cap, or the default when it asked for none, so the
     engine choice of later batches is unchanged) or launch-sized scratch."""
-    W, H = shape
+    W, H = (int(occ[0]), int(occ[1])) if isinstance(occ, tuple) else (int(occ.shape[0]), int(occ.shape[1]))
     L, ctx = _lib.load_library(), _lib.context()
     nq = int(starts.shape[0])
     geo = np.zeros(6, np.int32)  # the geometry in force, restored after the re-run
     _lib.check(ctx, L.pmp_astar2d_geometry(ctx, geo.ctypes.data), "pmp_astar2d_geometry")
     _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, max(1, min(nq, 256)), 8 * W * H + 8), "pmp_astar2d_reserve")
     try:
-        return astar2d_batch((W, H), starts, goals, heuristic, path_cap, expand_cap, counters, occ_bits,
-                             retry_overflow=False, algo=algo)
+        return astar2d_batch(occ if occ_bits is None else (W, H), starts, goals, heuristic, path_cap, expand_cap,
+                             counters, occ_bits, retry_overflow=False, algo=algo)
     finally:
         if geo[5] or not geo[0]:  # sized by the launches: keep it that way (grows with the batches)
             _lib.check(ctx, L.pmp_astar2d_reserve_auto(ctx), "pmp_astar2d_reserve_auto")

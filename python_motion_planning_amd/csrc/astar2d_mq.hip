@@ -222,17 +222,46 @@ __device__ __forceinline__ uint32_t spill_off(const GHeap& h, int p)
     return h.gbase + blk * 128u + slot * 16u;
 }
 
+// The block layout's offset needs only the position's level below L0 (band b, parity o) besides the
+// position itself; the level constants are fixed per launch, so lane L of a group holds those of heap
+// level L (lane_cw, computed once) and a position at level K takes lane K's word (a DPP / bpermute,
+// not ~20 VALU instructions of clz and 64-bit shifts): spill_off_cw.  A path operation's lanes hold
+// the path's levels in order, so each uses its own word; a node's sibling sits in the next 16-B slot
+// of the same block (offset ^ 16) -- with an odd LDS cap (GHeap.cap), sibling pairs never straddle
+// the LDS / spill boundary.
+#ifndef PMP_MQ_LANECONST
+#define PMP_MQ_LANECONST 1
+#endif
+constexpr bool kLaneConst = PMP_MQ_LANECONST != 0 && kBlocks && !kBlocks2;
+__device__ __forceinline__ uint32_t lane_cw(int L0, int level)
+{
+    const int lam = level - L0;
+    if (lam < 0) return 0u;  // an LDS level: never used for an offset
+    const int o = lam & 1, b = lam >> 1;
+    const uint32_t kb = (uint32_t)(0xAB2B0B0301ull >> (8 * b)) & 0xFFu;
+    return ((kb << (L0 - 1)) << 1) | (uint32_t)o;
+}
+__device__ __forceinline__ uint32_t spill_off_cw(const GHeap& h, uint32_t cw, int p)
+{
+    const uint32_t u = (uint32_t)p + 1u;
+    const uint32_t o = cw & 1u;
+    const uint32_t blk = (u >> (o + 1u)) - (cw >> 1);
+    const uint32_t slot = (u & ((2u << o) - 1u)) + 2u * o;
+    return h.gbase + (blk << 7) + (slot << 4);
+}
+
 struct Ld {
     double fl;
     uint32_t cl, kl;
     uint4 v;
     bool in;
-    __device__ __forceinline__ void issue(const GHeap& h, int p)
+    __device__ __forceinline__ void issue(const GHeap& h, int p) { issue_off(h, p, p < h.cap ? kOOR : spill_off(h, p)); }
+    // off: the spill offset of p when p >= cap (else ignored)
+    __device__ __forceinline__ void issue_off(const GHeap& h, int p, uint32_t off)
     {
         in = p < h.cap;
         const int pl = in ? p : 0;
-        const uint32_t off = in ? kOOR : spill_off(h, p);
-        v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(h.spill, off, 0, 0));
+        v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(h.spill, in ? kOOR : off, 0, 0));
         fl = h.F[pl];
         cl = h.C[pl];
         if (kKeys) kl = h.K[pl];
@@ -248,7 +277,8 @@ struct Ld {
         k = kKeys ? sel_lanes(m, kl, v.w) : hkey<HEUR>(c);
     }
 };
-__device__ __forceinline__ void hst(const GHeap& h, bool on, int p, double f, uint32_t c, uint32_t k, int cat = 0)
+__device__ __forceinline__ void hst_off(const GHeap& h, bool on, int p, uint32_t soff, double f, uint32_t c, uint32_t k,
+                                        int cat = 0)
 {
     if (on && p < h.cap) {
         h.F[p] = f;
@@ -257,12 +287,16 @@ __device__ __forceinline__ void hst(const GHeap& h, bool on, int p, double f, ui
     }
     const uint64_t b = (uint64_t)__double_as_longlong(f);
     const uint4 v = make_uint4((uint32_t)b, (uint32_t)(b >> 32), c, kKeys ? k : 0u);
-    const uint32_t off = (on && p >= h.cap) ? spill_off(h, p) : kOOR;
+    const uint32_t off = (on && p >= h.cap) ? soff : kOOR;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
                                            h.spill, off, 0, 0);
     if (kMirror & cat)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
                                                h.mirror, off, 0, 0);
+}
+__device__ __forceinline__ void hst(const GHeap& h, bool on, int p, double f, uint32_t c, uint32_t k, int cat = 0)
+{
+    hst_off(h, on, p, (on && p >= h.cap) ? spill_off(h, p) : kOOR, f, c, k, cat);
 }
 
 // ---- direction bits (astar2d.hip: bit(p) = !(heap[2p+1] < heap[2p+2]) for nodes with two children,
@@ -274,7 +308,7 @@ __device__ __forceinline__ void hst(const GHeap& h, bool on, int p, double f, ui
 // path they agree with, so each lane tests two candidate leaves of a 5-level block (one of a 3-level
 // block) against masks fixed per lane (Walk), and the row's ballot names the leaf.
 struct Walk {
-    uint32_t MA, VA, MB, VB, M3, V3;  // leaves gl and gl + 16 of a 5-level block; leaf gl & 7 of a 3-level one
+    uint32_t MA, VA, MB, VB, MV3;  // leaves gl and gl + 16 of a 5-level block; leaf gl & 7 of a 3-level one (M | V << 8)
     __device__ __forceinline__ static void leaf(int L, int lev, uint32_t& M, uint32_t& V)
     {
         uint32_t pr = 1;
@@ -290,7 +324,9 @@ struct Walk {
     {
         leaf(gl, 5, MA, VA);
         leaf(gl + 16, 5, MB, VB);
+        uint32_t M3, V3;
         leaf(gl & 7, 3, M3, V3);
+        MV3 = M3 | (V3 << 8);
     }
     // path number (block-relative) after five / three steps from the block root; w2 = block word << 1
     __device__ __forceinline__ uint32_t five(uint32_t w2, int gb) const
@@ -300,7 +336,7 @@ struct Walk {
     }
     __device__ __forceinline__ uint32_t three(uint32_t w2, int gb) const
     {
-        return 8u + (uint32_t)(__ffs((int)(rbits((w2 & M3) == V3, gb) & 0xFFu)) - 1);
+        return 8u + (uint32_t)(__ffs((int)(rbits((w2 & MV3 & 0xFFu) == (MV3 >> 8), gb) & 0xFFu)) - 1);
     }
 };
 template <bool T2LDS>
@@ -338,6 +374,28 @@ __device__ __forceinline__ void bit_set(const GHeap& h, bool on, int level, uint
         if (bit) __hip_atomic_fetch_or(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else __hip_atomic_fetch_and(w, ~m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+}
+// bit_set at a level fixed per lane (a path operation's lane L writes level L - 1), tiers all in LDS:
+// the level's constants packed once per lane (lane_bc) -- r = level - 5 t, and the word index
+// (R >> s1) + c1 / the byte shift (R & mk) * 8 of the tier -- instead of rederived every step.
+#ifndef PMP_MQ_BITCONST
+#define PMP_MQ_BITCONST 0
+#endif
+__device__ __forceinline__ uint32_t lane_bc(int level)
+{
+    if (level < 0) return 0u;
+    const int t = level / 5, r = level - 5 * t;
+    const uint32_t s1 = t == 2 ? 2u : 0u, mk = t == 2 ? 3u : 0u;
+    const int c1 = t == 0 ? -1 : (t == 1 ? -31 : -220);  // t 0: R = 1 -> word 0; 1: R - 31; 2: 36 + (R - 1024) / 4
+    return (uint32_t)r | (s1 << 3) | (mk << 5) | ((uint32_t)(c1 + 1024) << 8);
+}
+__device__ __forceinline__ void bit_set_bc(const GHeap& h, bool on, uint32_t bc, uint32_t Pl, bool bit)
+{
+    const uint32_t r = bc & 7u, mr = (1u << r) - 1u;
+    const uint32_t R = Pl >> r;
+    const uint32_t widx = (uint32_t)((int)(R >> ((bc >> 3) & 3u)) + (int)(bc >> 8) - 1024);
+    const uint32_t m = (1u << ((Pl & mr) + mr)) << ((R & ((bc >> 5) & 3u)) << 3);
+    if (on) ds_mskor(h.B + widx, m, bit ? m : 0u);
 }
 // CPython _siftup's choice bit of the parent of `child` (a position) whose new content is v and
 // whose sibling holds s: bit = !(left < right), odd positions are left children
@@ -397,20 +455,33 @@ __device__ __forceinline__ void pop_leaf(const GHeap& h, const Walk& wk, int n, 
 template <bool T2LDS, int HEUR>
 __device__ __forceinline__ int path_op(const GHeap& h, bool on, bool pop, uint32_t Q, int Kd, int n, double Xf, uint32_t Xc,
                                        uint32_t Xk, int gl, int gb, double& lastf, uint32_t& lastc, uint32_t& lastk,
-                                       double& rootf, uint32_t& rootc, double& nf, uint32_t& nc, uint32_t& nk)
+                                       double& rootf, uint32_t& rootc, double& nf, uint32_t& nc, uint32_t& nk, uint32_t cwL,
+                                       uint32_t bcL)
 {
     const bool lvl = gl <= Kd;
     const int q = lvl ? (int)(Q >> (Kd - gl)) - 1 : 0;
     const bool lda = on && (pop ? (gl >= 1 && lvl) : gl < Kd);
-    const int ai = lda ? q : ((on && pop && gl == 15) ? n - 1 : 0);
+    const bool l15 = on && pop && gl == 15;  // a pop's lane 15: heap[n - 1], the new last
     const int si = ((q - 1) ^ 1) + 1;
     const bool hass = on && gl >= 1 && lvl && si < n;
     double Vf, Sf;
     uint32_t Vc, Sc, Vk, Sk;
+    // kLaneConst: one offset per lane -- lane L's level-L word for the path node q (lane 15 of a pop:
+    // the word of heap[n - 1]'s level, from that level's lane); the sibling is the next slot (^ 16);
+    // the stores go to q, at the same offset (every storing lane loaded its q)
+    uint32_t offq = kOOR;
     {
         Ld la, ls;
-        la.issue(h, ai);
-        ls.issue(h, hass ? si : 0);
+        if (kLaneConst) {
+            const uint32_t cwK = bp(cwL, gb + (31 - __clz(n > 0 ? n : 1)));
+            const int ai = on ? (l15 ? n - 1 : q) : 0;
+            offq = spill_off_cw(h, l15 ? cwK : cwL, ai);
+            la.issue_off(h, ai, offq);
+            ls.issue_off(h, hass ? si : 0, offq ^ 16u);
+        } else {
+            la.issue(h, lda ? q : (l15 ? n - 1 : 0));
+            ls.issue(h, hass ? si : 0);
+        }
         la.get<HEUR>(Vf, Vc, Vk);
         ls.get<HEUR>(Sf, Sc, Sk);
     }
@@ -426,13 +497,15 @@ __device__ __forceinline__ int path_op(const GHeap& h, bool on, bool pop, uint32
     nf = atb ? Xf : (shift ? (pop ? upf : dnf) : Vf);
     nc = atb ? Xc : (shift ? (pop ? upc : dnc) : Vc);
     nk = atb ? Xk : (shift ? (pop ? upk : dnk) : Vk);
-    hst(h, on && (pop ? gl <= b : (gl >= b && lvl)), q, nf, nc, nk, pop ? 4 : 2);
+    if (kLaneConst) hst_off(h, on && (pop ? gl <= b : (gl >= b && lvl)), q, offq, nf, nc, nk, pop ? 4 : 2);
+    else hst(h, on && (pop ? gl <= b : (gl >= b && lvl)), q, nf, nc, nk, pop ? 4 : 2);
     // the bits of the changed levels' parents: lane L (>= 1) sets its parent's from its new content
     // and its sibling's
     {
         const bool upd = hass && (pop ? gl <= b : gl >= b);
         const bool bit = choice_bit_k(q, nf, nk, Sf, Sk);
-        bit_set<T2LDS>(h, upd, gl - 1, Q >> (Kd - gl + 1), bit);
+        if (T2LDS && PMP_MQ_BITCONST) bit_set_bc(h, upd, bcL, Q >> (Kd - gl + 1), bit);
+        else bit_set<T2LDS>(h, upd, gl - 1, Q >> (Kd - gl + 1), bit);
     }
     {
         // selects, not a branch (every lane computes them): root = level 0's new content; the last
@@ -489,7 +562,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
         hp.sbase = (uint32_t)grp * (uint32_t)spill_n * 16u + (uint32_t)(kSpillShift - lds_cap) * 16u;
         hp.gbase = (uint32_t)grp * (uint32_t)spill_n * 16u;
         hp.L0 = 31 - __clz(lds_cap + 1);
-        hp.cap = lds_cap;
+        // kLaneConst: an odd cap (one LDS slot unused), so no sibling pair straddles LDS and spill
+        hp.cap = kLaneConst ? lds_cap - 1 : lds_cap;
         if (kMirror & 7)
             hp.mirror = __builtin_amdgcn_make_buffer_rsrc(
                 spill_all + ((size_t)gridDim.x + blockIdx.x) * 4u * (size_t)spill_n, 0,
@@ -505,13 +579,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
 
     Walk wk;
     wk.init(gl);
+    const uint32_t cwL = kLaneConst ? lane_cw(hp.L0, gl) : 0u;  // spill-offset word of heap level gl
+    const uint32_t bcL = (T2LDS && PMP_MQ_BITCONST) ? lane_bc(gl - 1) : 0u;  // bit_set word of level gl - 1
+    // a spilled position p's offset from its level's word (lane gb + level of p)
+    auto soff = [&](int p, bool on) -> uint32_t {
+        if (!kLaneConst) return (on && p >= hp.cap) ? spill_off(hp, p) : kOOR;
+        const uint32_t cw = bp(cwL, gb + (31 - __clz(p + 1)));
+        return spill_off_cw(hp, cw, p);
+    };
     // per-lane constants: lane m < 8 of a row is motion m (offset, cost, isCollision's cells)
     const int mo = gl & 7;
     const int mx = mot_x(mo), my = mot_y(mo);
-    const double mcost = GZERO ? 0.0 : ((mo & 1) ? kSqrt2 : 1.0);
-    uint32_t need = 16u | (1u << ((mx + 1) * 3 + (my + 1)));
-    if (mo & 1) need |= (1u << (3 + (my + 1))) | (1u << ((mx + 1) * 3 + 1));
-    const uint32_t self_bit = 1u << ((mx + 1) * 3 + (my + 1));
+    // need (the 3x3 cells isCollision wants free) | the motion's own cell << 16, one register
+    uint32_t nsb = 16u | (1u << ((mx + 1) * 3 + (my + 1)));
+    if (mo & 1) nsb |= (1u << (3 + (my + 1))) | (1u << ((mx + 1) * 3 + 1));
+    nsb |= (1u << ((mx + 1) * 3 + (my + 1))) << 16;
     // the 3x3 round: lanes 0..8 occupancy of cell (x + i/3 - 1, y + i%3 - 1); lanes 9..11 the
     // cell-state bytes of row i - 9; lane 12 G[pusher]; THETA: lane 13 the pusher's CLOSED parent
     const int blk_dx = gl < 9 ? gl / 3 - 1 : (gl < 12 ? gl - 10 : 0);
@@ -522,7 +604,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
     bool need_q = true, done = lone && grp != 0;
     int q = 0, qi = 0, sx = 0, sy = 0, gx = 0, gy = 0;
     int n = 0, nexp = 0, maxn = 0;
-    int64_t npush = 0, npop = 0;
+    int npush = 0, npop = 0;  // < 2^31 per query (heaps are capped at 32,767 entries: pushes <= 8 W H)
     double rootf = 0.0, lastf = 0.0;
     uint32_t rootc = 0u, lastc = 0u, lastk = 0u;  // lastk = hkey(lastc)
     // the pushes of the last expansion still to do (motion mask, in motion order) and their items
@@ -625,7 +707,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
                 const uint32_t leftk = rank == 0 ? lastk : lkp;
                 bit_set<T2LDS>(hp, inrun && (pos & 1) == 0 && pos > 0, 30 - __clz(pos + 1), (uint32_t)(pos + 1) >> 1,
                                !key_lt(leftf, leftk, ifv, ikk));
-                hst(hp, inrun, pos, ifv, icm, ikk, 1);
+                hst_off(hp, inrun, pos, soff(pos, inrun), ifv, icm, ikk, 1);
                 const int top = 31 - __clz(run);
                 lastf = bpf(ifv, gb + top);
                 lastc = bp(icm, gb + top);
@@ -707,13 +789,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
             if (n > 0) pop_leaf<T2LDS>(hp, wk, n, gb, Q, Kd);
         }
         const int pp = (n0 + (gl & 7) - 1) >> 1;  // lanes 0..7: parent of position n0 + lane
-        pld.issue(hp, pop && pc_ok && gl < 8 ? pp : 0);
+        {
+            const int pi = pop && pc_ok && gl < 8 ? pp : 0;
+            pld.issue_off(hp, pi, soff(pi, pi >= hp.cap));
+        }
         const bool op = push || (pop && n > 0);
         double nf = 0.0;
         uint32_t nc = 0u, nk = 0u;
         int b = 0;
         b = path_op<T2LDS, HEUR>(hp, op, pop, Q, Kd, n, Xf, Xc, Xk, gl, gb, lastf, lastc, lastk, rootf, rootc, nf, nc,
-                                 nk);
+                                 nk, cwL, bcL);
         {
             double f8;
             uint32_t c8, k8;
@@ -778,10 +863,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
                     if (THETA == 2 && !grid2d::los2d(occ, H, px, py, x, y)) {
                         // set vertex (lazy_theta_star.py:55-65): the first CLOSED, collision-free
                         // neighbour minimising its g + dist becomes the parent; g = inf if there is none
-                        const bool cand = gl < 8 && (occ9 & need) == 0u && (cls9 & self_bit) != 0u;
+                        const bool cand = gl < 8 && (occ9 & nsb & 0xFFFFu) == 0u && (cls9 & (nsb >> 16)) != 0u;
                         const uint32_t cl = (uint32_t)((int)nlin + mx * H + my);
                         const double gn = G[cand ? cl : 0u];
-                        const double gc = gn + mcost;
+                        const double gc = gn + ((mo & 1) ? kSqrt2 : 1.0);
                         const uint32_t cmask = rbits(cand, gb) & 0xFFu;
                         double best = __longlong_as_double(0x7ff0000000000000ll);
                         int bm = -1;
@@ -857,11 +942,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
                 } else {
                     // getNeighbor in motion order; push the goal and stop (a_star.py:66-80)
                     const int ndx = gx - x - mx, ndy = gy - y - my;
-                    const bool nb_ok = gl < 8 && (occ9 & need) == 0u && (cls9 & self_bit) == 0u;
+                    const bool nb_ok = gl < 8 && (occ9 & nsb & 0xFFFFu) == 0u && (cls9 & (nsb >> 16)) == 0u;
                     uint32_t vm = rbits(nb_ok, gb) & 0xFFu;
                     const uint32_t gm = rbits(nb_ok && ndx == 0 && ndy == 0, gb) & 0xFFu;
                     if (gm) vm &= (gm << 1) - 1u;
-                    double ig = gnode + mcost;
+                    double ig = gnode + (GZERO ? 0.0 : ((mo & 1) ? kSqrt2 : 1.0));
                     int icode = mo;
                     if (THETA && ndir != 8) {
                         // updateVertex(CLOSED[node.parent], node_n) (theta_star.py:96-108; lazy_theta_star.py:
@@ -894,8 +979,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
                 path_len_out[q] = st == PMP_FOUND ? plen : 0;
                 nexp_out[q] = nexp;
                 if (counters) {
-                    counters[4 * q + 0] = npush;
-                    counters[4 * q + 1] = npop;
+                    counters[4 * q + 0] = (int64_t)npush;
+                    counters[4 * q + 1] = (int64_t)npop;
                     counters[4 * q + 2] = nexp;
                     counters[4 * q + 3] = maxn;
                 }

@@ -442,7 +442,10 @@ struct L3 {
         }
         // deferred stores: the updated voxels' rhs (the start keeps its own), the centre's new g
         {
-            const bool upd = mine && P != start && (is_nb || (lane == 26 && do_center));
+            // (a recomputed rhs equal to the one held -- the implicit inf of a never-written voxel
+            // included -- is not stored: most of a block's updateVertex calls leave rhs as it was, and
+            // each store is a partly written line)
+            const bool upd = mine && P != start && (is_nb || (lane == 26 && do_center)) && rv != rvl;
             if (upd) {
                 rhs[P] = rv;
                 mark(rt, P);

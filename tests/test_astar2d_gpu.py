@@ -257,7 +257,7 @@ def test_explicit_heap_cap_and_overflow_retry_keep_geometry():
         # an overflow re-run on a default reservation restores the default (not the cut limit as an
         # explicit cap, which would move later small batches off the single-query engine)
         before = geometry()
-        r = batch.astar2d_full_bound((W, W), torch.as_tensor(starts, device="cuda"),
+        r = batch.astar2d_full_bound(occ, torch.as_tensor(starts, device="cuda"),
                                      torch.as_tensor(goals, device="cuda"), path_cap=W * W + 1)
         assert np.array_equal(r["cost"].cpu().numpy(), ref["cost"])
         assert geometry() == before

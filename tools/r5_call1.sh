@@ -14,6 +14,17 @@ leg() {  # name, bench args...
 import json; d=json.load(open('gpurun_out/c1/$n.json'))['secondary']
 for k, v in d.items(): print('$n', k, round(v['value']), v.get('unit'), 'kernel_ms', v.get('kernel_ms_per_launch'), 'frac', v.get('roofline', {}).get('frac'), 'checked', v.get('timed_launches_checked'))"
 }
+# the A* headline: lane-constant spill offsets (default) vs the round-4 offsets (lc0) vs the half-block
+# layout (blk2), alternating, same box
+for i in 1 2; do
+  for v in default lc0 blk2; do
+    lib=$R/python_motion_planning_amd/libpmp_hip.so
+    [ "$v" = default ] || lib=$R/python_motion_planning_amd/libpmp_hip_$v.so
+    PMP_HIP_LIB=$lib timeout -k 10 200 python3 bench.py --legs none --no-cpu-baseline --detail-out gpurun_out/c1/head_$v.json \
+      > gpurun_out/c1/head_${v}_$i.out 2> gpurun_out/c1/head_${v}_$i.err || { tail -20 gpurun_out/c1/head_${v}_$i.err; exit 1; }
+    python3 -c "import json; d=json.loads(open('gpurun_out/c1/head_${v}_$i.out').read().strip().splitlines()[-1]); print('headline $v', round(d['value']), 'ms/step', round(d['ms_per_step'], 1))"
+  done
+done
 leg dwa32 --legs dwa --agents 32 --control-steps 50
 leg dwa256 --legs dwa --control-steps 50
 leg rrt --legs rrt --rrt-steps 3
