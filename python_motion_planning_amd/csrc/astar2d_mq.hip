@@ -474,9 +474,10 @@ __device__ __forceinline__ int path_op(const GHeap& h, bool on, bool pop, uint32
         Ld la, ls;
         if (kLaneConst) {
             const uint32_t cwK = bp(cwL, gb + (31 - __clz(n > 0 ? n : 1)));
-            const int ai = on ? (l15 ? n - 1 : q) : 0;
-            offq = spill_off_cw(h, l15 ? cwK : cwL, ai);
-            la.issue_off(h, ai, offq);
+            // the offset of q (of n - 1 on a pop's lane 15, which stores nothing); only the lanes whose
+            // value the operation uses load
+            offq = spill_off_cw(h, l15 ? cwK : cwL, l15 ? n - 1 : q);
+            la.issue_off(h, lda ? q : (l15 ? n - 1 : 0), offq);
             ls.issue_off(h, hass ? si : 0, offq ^ 16u);
         } else {
             la.issue(h, lda ? q : (l15 ? n - 1 : 0));

@@ -493,9 +493,25 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
     const double s0 = S.sums[0], s1 = S.sums[1], s2 = S.sums[2];
     double bs = -INFINITY;
     int bi = 0x7fffffff;
-    for (int c = tid; c < N; c += nt) {
+    // the other parts' columns come from L2 / HBM: a thread's loads issue together (8 samples x 3
+    // columns in flight), then the scores, in increasing c (the first index wins a tie)
+    constexpr int kU = 8;
+    for (int c0 = tid; c0 < N; c0 += kU * nt) {
+        double hv[kU], ov[kU], vv[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int c = c0 + u * nt;
+            const int cc = c < N ? c : 0;
+            hv[u] = cols[cc];
+            ov[u] = cols[kMaxN + cc];
+            vv[u] = cols[2 * kMaxN + cc];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+        const int c = c0 + u * nt;
+        if (c >= N) break;
         const double e0 = linsp_at(LV, c / nw), e1 = linsp_at(LW, c % nw);
-        const double h = cols[c], o = cols[kMaxN + c], vel = cols[2 * kMaxN + c];
+        const double h = hv[u], o = ov[u], vel = vv[u];
         const double e2 = s0 != 0 ? h / s0 : h;
         const double e3 = s1 != 0 ? o / s1 : o;
         const double e4 = s2 != 0 ? vel / s2 : vel;
@@ -507,6 +523,7 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
             e[2] = sc;
         }
         if (sc > bs || bi == 0x7fffffff) { bs = sc; bi = c; }
+        }
     }
     lp::block_best<false>(bs, bi, S.redd, S.redi);
     const int best = bi;

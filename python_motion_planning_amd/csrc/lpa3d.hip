@@ -303,17 +303,20 @@ struct L3 {
             gin0 = geo.in(x0, y0, z0);
             gin1 = b1 < 125 && geo.in(x1, y1, z1);
             const int i0 = gin0 ? geo.id(x0, y0, z0) : center, i1 = gin1 ? geo.id(x1, y1, z1) : center;
-            gin0 = gin0 && gw(i0);  // a voxel this query never wrote: g = inf, no load
+            // loads first, unconditionally (in-map addresses): one round trip, no LDS round before it;
+            // a voxel this query never wrote holds a stale value: inf by its bit
+            gb0 = g[i0];
+            gb1 = g[i1];
+            gin0 = gin0 && gw(i0);
             gin1 = gin1 && gw(i1);
-            gb0 = gin0 ? g[i0] : kInf;
-            gb1 = gin1 ? g[i1] : kInf;
         }
         const int m = lane < 26 ? lane : 0;
         const int dx = lane < 26 ? c_m[m][0] : 0, dy = lane < 26 ? c_m[m][1] : 0, dz = lane < 26 ? c_m[m][2] : 0;
         const int px = cx + dx, py = cy + dy, pz = cz + dz;
         const bool mine = lane <= 26 && geo.in(px, py, pz);
         const int P = mine ? geo.id(px, py, pz) : 0;
-        const double rvl = (mine && rw(P)) ? rhs[P] : kInf;
+        const double rvr = rhs[mine ? P : center];
+        const double rvl = (mine && rw(P)) ? rvr : kInf;
         cube[lane] = gin0 ? gb0 : kInf;
         if (lane < 61) cube[lane + 64] = gin1 ? gb1 : kInf;
         // ---- block masks: in the map / obstacle, as wave-uniform bits

@@ -383,16 +383,24 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         double h = INFINITY, hx = 0.0, hy = 0.0, hg = 0.0;
         int hi = 0x7fffffff;
         if (best <= T) {
-            // increasing j within the thread (the LDS part first): equal distances keep the first.
-            // 8 loads in flight per thread (one at a time made the HBM part a chain of dependent
-            // L2 round trips)
-            for (int j0 = tid; j0 < n; j0 += 8 * kNT) {
+            // increasing j within the thread (the LDS part, then the HBM part): equal distances keep
+            // the first.  Separate loops: a select between an LDS and a global load per element would
+            // issue both.  8 loads in flight per thread in the HBM part (one at a time made it a chain
+            // of dependent L2 round trips)
+            auto band = [&](int j, uint32_t p) {
+                const float dx = fmaf((float)(p & 0xFFFFu), qinv, qlof) - sxf;
+                const float dy = fmaf((float)(p >> 16), qinv, qlof) - syf;
+                if (dx * dx + dy * dy <= T) {
+                    const double xj = tx[2 * j], yj = tx[2 * j + 1], gj = tg[j];  // one round
+                    const double e = lp::py_hypot(xj - sx, yj - sy);
+                    if (e < h) { h = e; hi = j; hx = xj; hy = yj; hg = gj; }  // increasing j: keeps the first
+                }
+            };
+            for (int j = tid; j < nl; j += kNT) band(j, xl[j]);
+            for (int j0 = lcap + tid; j0 < n; j0 += 8 * kNT) {
                 uint32_t p[8];
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const int j = j0 + u * kNT;
-                    p[u] = j < nl ? xl[j] : (j < n ? xyq[j] : 0u);
-                }
+                for (int u = 0; u < 8; u++) p[u] = (j0 + u * kNT < n) ? xyq[j0 + u * kNT] : 0u;
                 uint32_t hits = 0;
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
@@ -404,7 +412,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                     const int j = j0 + (__ffs(hits) - 1) * kNT;
                     const double xj = tx[2 * j], yj = tx[2 * j + 1], gj = tg[j];  // one round
                     const double e = lp::py_hypot(xj - sx, yj - sy);
-                    if (e < h) { h = e; hi = j; hx = xj; hy = yj; hg = gj; }  // increasing j: keeps the first
+                    if (e < h) { h = e; hi = j; hx = xj; hy = yj; hg = gj; }
                 }
             }
         }
@@ -434,12 +442,21 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             const float nxf = (float)nx, nyf = (float)ny;
             const double rb = P.radius + 2.0 * eps;
             const float Tr = (float)(rb * rb) * 1.0001f;
+            // the in-radius candidates (any order: the K list is order-free), the LDS part as 8-wide
+            // chunks of the same loop body, the HBM part 8 loads in flight per thread
             for (int j0 = tid; j0 < n; j0 += 8 * kNT) {
                 uint32_t p[8];
+                if (j0 + 7 * kNT < nl) {
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const int j = j0 + u * kNT;
-                    p[u] = j < nl ? xl[j] : (j < n ? xyq[j] : 0u);
+                    for (int u = 0; u < 8; u++) p[u] = xl[j0 + u * kNT];
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        const int j = j0 + u * kNT;
+                        p[u] = 0u;
+                        if (j < nl) p[u] = xl[j];
+                        else if (j < n) p[u] = xyq[j];
+                    }
                 }
                 uint32_t hits = 0;
 #pragma unroll
