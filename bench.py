@@ -518,6 +518,9 @@ def rrt_leg(args, torch, dist, world, rank):
                           tpar=torch.empty((nq, cap), **i32), nn=torch.empty(nq, **i32), cost=torch.empty(nq, **f64),
                           plen=torch.empty(nq, **i32), path=torch.empty((nq, cap, 2), **f64),
                           draws=torch.empty(nq, dtype=torch.int64, device="cuda"), st=torch.empty(nq, **i32)))
+        if args.rrt_resident > 0:  # the LDS tree share: room for this many workgroups per CU
+            _lib.check(lanes[-1]["ctx"], L.pmp_set_resident_per_cu(lanes[-1]["ctx"], args.rrt_resident),
+                       "pmp_set_resident_per_cu")
 
     def launch(i):
         b = lanes[i % len(lanes)]
@@ -1705,6 +1708,8 @@ def main():
     ap.add_argument("--rrt-steps", type=int, default=4)
     ap.add_argument("--rrt-streams", type=int, default=3, help="RRT* batches in flight (own stream + context each)")
     ap.add_argument("--rrt-cpu-sample", type=int, default=16)
+    ap.add_argument("--rrt-resident", type=int, default=0,
+                    help="RRT* workgroups per CU the LDS tree copy leaves room for (0: one, the whole LDS)")
     ap.add_argument("--a3-queries", type=int, default=8192)
     ap.add_argument("--a3-steps", type=int, default=32)
     ap.add_argument("--a3-streams", type=int, default=6, help="3D A* batches in flight (own stream + context each)")

@@ -232,7 +232,7 @@ __device__ __forceinline__ uint32_t spill_off(const GHeap& h, int p)
 #ifndef PMP_MQ_LANECONST
 #define PMP_MQ_LANECONST 1
 #endif
-constexpr bool kLaneConst = PMP_MQ_LANECONST != 0 && kBlocks && !kBlocks2;
+constexpr bool kLaneConst = PMP_MQ_LANECONST != 0 && kBlocks;
 __device__ __forceinline__ uint32_t lane_cw(int L0, int level)
 {
     const int lam = level - L0;
@@ -246,9 +246,13 @@ __device__ __forceinline__ uint32_t spill_off_cw(const GHeap& h, uint32_t cw, in
     const uint32_t u = (uint32_t)p + 1u;
     const uint32_t o = cw & 1u;
     const uint32_t blk = (u >> (o + 1u)) - (cw >> 1);
-    const uint32_t slot = (u & ((2u << o) - 1u)) + 2u * o;
+    const uint32_t slot = kBlocks2 ? (o ? ((u >> 1) & 1u) * 4u + 1u + (u & 1u) : (u & 1u) * 4u)
+                                   : (u & ((2u << o) - 1u)) + 2u * o;
     return h.gbase + (blk << 7) + (slot << 4);
 }
+// the sibling's offset: the next slot of the pair (kBlocks 1: slots 2i, 2i + 1), or the other half's
+// child / the pair 4i + 1, 4i + 2 (kBlocks 2)
+__device__ __forceinline__ uint32_t sib_xor(uint32_t cw) { return kBlocks2 ? ((cw & 1u) ? 48u : 64u) : 16u; }
 
 struct Ld {
     double fl;
@@ -478,7 +482,7 @@ __device__ __forceinline__ int path_op(const GHeap& h, bool on, bool pop, uint32
             // value the operation uses load
             offq = spill_off_cw(h, l15 ? cwK : cwL, l15 ? n - 1 : q);
             la.issue_off(h, lda ? q : (l15 ? n - 1 : 0), offq);
-            ls.issue_off(h, hass ? si : 0, offq ^ 16u);
+            ls.issue_off(h, hass ? si : 0, offq ^ sib_xor(cwL));
         } else {
             la.issue(h, lda ? q : (l15 ? n - 1 : 0));
             ls.issue(h, hass ? si : 0);

@@ -359,6 +359,7 @@ constexpr int kSplitChunk = 1024;  // samples of one part held in LDS
 struct DwaSplitShared {
     uint32_t occ[kOccLdsWords];
     double col[3][kSplitChunk];
+    double lsum[3][kMaxLeaves];  // the last part: every part's leaf sums, staged for the combine
     int leaf_lo[kMaxLeaves], leaf_n[kMaxLeaves];
     double redd[kSplitThreads / 64];
     int redi[kSplitThreads / 64];
@@ -369,12 +370,46 @@ struct DwaSplitShared {
     int last;
 };
 
+// The parts' hand-off (cdna_hip_programming.md Guideline 16, publish / consume): every column and leaf
+// sum another part reads is stored write-through (an agent-scope relaxed atomic store: `sc1`), each
+// storing wave drains (s_waitcnt vmcnt(0)) before the workgroup barrier and the arrival counter's
+// relaxed atomic add, and the last part reads them with agent-scope loads (ld_coh below) -- no
+// __threadfence(), whose L2 writeback (buffer_wbl2) flushed every dirty line of the XCD and cost
+// ~40 us per arrival (PMP_DWA_STAMPS, round 5).
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+__device__ __forceinline__ void st_wt(double* p, double v)
+{
+    __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The consumer side: agent-scope relaxed loads (sc1: served coherently, not from a stale line of
+// this XCD's L2 or the CU's L1), issued after the arrival counter showed every part in -- in place of
+// an acquire fence (buffer_inv sc1 over the whole cache; PMP_DWA_ACQ=1 restores it for A/B runs).
+#ifndef PMP_DWA_ACQ
+#define PMP_DWA_ACQ 0
+#endif
+__device__ __forceinline__ double ld_coh(const double* p)
+{
+#if PMP_DWA_ACQ
+    return *p;
+#else
+    return __longlong_as_double((long long)__hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#endif
+}
+
 struct DwaSplitScratch {
     double* cols;     // [na][3][kMaxN]
     double* leafsum;  // [na][3][kMaxLeaves]
     int* cnt;         // [na] arrivals of this launch (reset to 0 by the last part)
 };
 
+// PMP_DWA_STAMPS (dev builds, tools/dwa_split_probe.py): every part's tid 0 writes s_memtime at its
+// phase boundaries into best_traj (as raw u64), 10 slots per workgroup
+#ifdef PMP_DWA_STAMPS
+#define DSTAMP(i) do { if (tid == 0 && best_traj) reinterpret_cast<unsigned long long*>(best_traj)[(size_t)blockIdx.x * 10 + (i)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define DSTAMP(i) do {} while (0)
+#endif
 template <bool OCC_LDS>
 __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
     const uint32_t* __restrict__ occ, int ox, int oy, int W, int H, pmp_lp_params P, pmp_dwa_params D, int na, int k,
@@ -388,6 +423,7 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
     const int a = blockIdx.x / k, part = blockIdx.x - a * k;
     const int tid = threadIdx.x, nt = blockDim.x;
     if (a >= na) return;
+    DSTAMP(0);
     if (it > 0 && status_out[a] != 0) return;  // stopped in an earlier iteration (block-uniform)
     double st[5];
     for (int q = 0; q < 5; q++) st[q] = state[5 * a + q];
@@ -414,24 +450,53 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
     const double dt = P.dt;
     const int Hh = (int)(D.predict_time / dt);
     const double R = D.inflation;
-    double pt[2] = {0, 0}, theta = 0, kappa = 0;
-    const int ls = lp::lookahead_block(path, Pn, st[0], st[1], st[3], P, pt, &theta, &kappa, S.redd, S.redi);
-    if (tid == 0) { S.pt[0] = pt[0]; S.pt[1] = pt[1]; }
-    __syncthreads();
-    if (ls) { stop(PMP_REF_RAISES); return; }
+    const int nv = D.nv, nw = D.nw;  // the host splits only windows of fixed size (nv, nw > 0)
+    const int N = nv * nw;
+    {
+        // getLookaheadPoint (local_planner.py:103-170, lp::lookahead_block's steps) with one load
+        // round: each thread keeps the distances of its first two path points for the
+        // first-beyond-lookahead search; the serial tail runs on thread 0 while thread 64 builds the
+        // pairwise tree's leaf table and the heading's sin / cos
+        const double rx = st[0], ry = st[1];
+        const double L = lp::lookahead_dist(st[3], P);
+        double d0 = INFINITY, d1 = INFINITY, bd = INFINITY;
+        int bi = 0x7fffffff;
+        for (int i = tid; i < Pn; i += nt) {
+            const double d = lp::py_hypot(rx - path[2 * i], ry - path[2 * i + 1]);
+            if (i == tid) d0 = d;
+            else if (i == tid + nt) d1 = d;
+            if (d < bd) { bd = d; bi = i; }  // strided in increasing i: keeps the first minimum
+        }
+        lp::block_best<true>(bd, bi, S.redd, S.redi);
+        const int idx_closest = bi;
+        int fi = 0x7fffffff;  // first i >= idx_closest with dist >= L (this thread's, increasing i)
+        for (int i = tid; i < Pn; i += nt) {
+            if (i < idx_closest) continue;
+            const double d = i == tid ? d0 : (i == tid + nt ? d1 : lp::py_hypot(rx - path[2 * i], ry - path[2 * i + 1]));
+            if (d >= L) { fi = i; break; }
+        }
+        double fd = 0.0;
+        lp::block_best<true>(fd, fi, S.redd, S.redi);
+        __syncthreads();  // redd / redi read everywhere before thread 0 reuses them
+        if (tid == 0) {
+            double pt[2] = {0, 0}, theta = 0, kappa = 0;
+            S.redi[0] = lp::lookahead_tail(path, Pn, rx, ry, L, fi == 0x7fffffff ? Pn - 1 : fi, pt, &theta, &kappa);
+            S.pt[0] = pt[0];
+            S.pt[1] = pt[1];
+        } else if (tid == 64) {
+            int nl = 0;
+            pw_leaves<kPwDepth>(0, N, S.leaf_lo, S.leaf_n, nl);
+            S.nleaves = nl;
+            sincos(st[2], &S.sn0, &S.cs0);
+        }
+        __syncthreads();
+    }
+    if (S.redi[0]) { stop(PMP_REF_RAISES); return; }
+    DSTAMP(1);
     const double gx = S.pt[0], gy = S.pt[1];
     const double vr0 = fmax(P.min_v, st[3] + P.min_v_inc * dt), vr1 = fmin(P.max_v, st[3] + P.max_v_inc * dt);
     const double vr2 = fmax(P.min_w, st[4] + P.min_w_inc * dt), vr3 = fmin(P.max_w, st[4] + P.max_w_inc * dt);
-    const int nv = D.nv, nw = D.nw;  // the host splits only windows of fixed size (nv, nw > 0)
-    const int N = nv * nw;
     const Linsp LV = make_linsp(vr0, vr1, nv), LW = make_linsp(vr2, vr3, nw);
-    if (tid == 0) {
-        int nl = 0;
-        pw_leaves<kPwDepth>(0, N, S.leaf_lo, S.leaf_n, nl);
-        S.nleaves = nl;
-        sincos(st[2], &S.sn0, &S.cs0);
-    }
-    __syncthreads();
     const int nl = S.nleaves;
     const int l0 = (int)(((long)nl * part) / k), l1 = (int)(((long)nl * (part + 1)) / k);
     const int c0 = l0 < nl ? S.leaf_lo[l0] : N, c1 = l1 < nl ? S.leaf_lo[l1] : N;
@@ -439,6 +504,7 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
     for (int c = c0 + tid; c < c1; c += nt)
         sincos(dt * linsp_at(LW, c % nw), &S.col[1][c - c0], &S.col[2][c - c0]);
     __syncthreads();
+    DSTAMP(2);
     const double sn0 = S.sn0, cs0 = S.cs0;
     for (int c = c0 + tid; c < c1; c += nt) {
         double x, y, mind2;
@@ -448,6 +514,7 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
         S.col[1][c - c0] = mind2;
         S.col[2][c - c0] = y;
     }
+    DSTAMP(3);
     double* cols = X.cols + (size_t)a * 3 * kMaxN;
     double* lsum = X.leafsum + (size_t)a * 3 * kMaxLeaves;
     for (int c = c0 + tid; c < c1; c += nt) {
@@ -462,35 +529,44 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
         S.col[0][c - c0] = h;
         S.col[1][c - c0] = o;
         S.col[2][c - c0] = vel;
-        cols[c] = h;
-        cols[kMaxN + c] = o;
-        cols[2 * kMaxN + c] = vel;
+        st_wt(cols + c, h);
+        st_wt(cols + kMaxN + c, o);
+        st_wt(cols + 2 * kMaxN + c, vel);
     }
     __syncthreads();
     {
         const int ml = l1 - l0;
         if (tid < 3 * ml) {
             const int cidx = tid / ml, l = l0 + tid % ml;
-            lsum[cidx * kMaxLeaves + l] = pw_leaf(&S.col[cidx][S.leaf_lo[l] - c0], S.leaf_n[l]);
+            st_wt(lsum + cidx * kMaxLeaves + l, pw_leaf(&S.col[cidx][S.leaf_lo[l] - c0], S.leaf_n[l]));
         }
     }
-    // arrival: release this part's columns and leaf sums at agent scope; the last part goes on
-    __threadfence();
+    DSTAMP(4);
+    // arrival: every wave drains its write-through stores, then one lane counts the part in; the
+    // last part acquires (drops its CU's stale lines) before reading the others' columns
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-        const int old = __hip_atomic_fetch_add(X.cnt + a, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        const int old = __hip_atomic_fetch_add(X.cnt + a, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         S.last = old == k - 1;
     }
     __syncthreads();
+    DSTAMP(5);
     if (!S.last) return;
-    __threadfence();
-    if (tid == 0) X.cnt[a] = 0;
+#if PMP_DWA_ACQ
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+    if (tid == 0) __hip_atomic_store(X.cnt + a, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the leaf sums into LDS in one round (all threads), then the tree's combine from LDS
+    for (int i = tid; i < 3 * nl; i += nt) S.lsum[i / nl][i % nl] = ld_coh(lsum + (i / nl) * kMaxLeaves + i % nl);
+    __syncthreads();
     if (tid < 3) {
         int leaf = 0;
-        S.sums[tid] = 0.0 + pw_combine<kPwDepth>(lsum + tid * kMaxLeaves, N, leaf);
+        S.sums[tid] = 0.0 + pw_combine<kPwDepth>(S.lsum[tid], N, leaf);
     }
     __syncthreads();
     const double s0 = S.sums[0], s1 = S.sums[1], s2 = S.sums[2];
+    DSTAMP(6);
     double bs = -INFINITY;
     int bi = 0x7fffffff;
     // the other parts' columns come from L2 / HBM: a thread's loads issue together (8 samples x 3
@@ -502,9 +578,9 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
         for (int u = 0; u < kU; u++) {
             const int c = c0 + u * nt;
             const int cc = c < N ? c : 0;
-            hv[u] = cols[cc];
-            ov[u] = cols[kMaxN + cc];
-            vv[u] = cols[2 * kMaxN + cc];
+            hv[u] = ld_coh(cols + cc);
+            ov[u] = ld_coh(cols + kMaxN + cc);
+            vv[u] = ld_coh(cols + 2 * kMaxN + cc);
         }
 #pragma unroll
         for (int u = 0; u < kU; u++) {
@@ -526,6 +602,7 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
         }
     }
     lp::block_best<false>(bs, bi, S.redd, S.redi);
+    DSTAMP(7);
     const int best = bi;
     const double u0 = linsp_at(LV, best / nw), u1 = linsp_at(LW, best % nw);
     if (tid == 0) {
@@ -533,7 +610,11 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
             double* hp = hist_pose + ((size_t)a * iters + it) * 3;
             hp[0] = st[0]; hp[1] = st[1]; hp[2] = st[2];
         }
+#ifndef PMP_DWA_STAMPS
         if (best_traj) {
+#else
+        if (false) {
+#endif
             double x = st[0], y = st[1], th = st[2];
             for (int q = 0; q < Hh; q++) {
                 double sn, cs;
@@ -559,6 +640,7 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
         status_out[a] = 0;
         nsteps_out[a] = (it == 0 ? 0 : nsteps_out[a]) + 1;
     }
+    DSTAMP(8);
 }
 
 // host restatement of pw_leaves: the largest part of n samples over k parts (leaf-aligned)

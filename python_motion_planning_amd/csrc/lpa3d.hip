@@ -174,13 +174,15 @@ struct L3 {
     UList U;
     double* g;
     double* rhs;
-    // Written-this-query bits of g / rhs (LDS, one bit per voxel; `touch`): a voxel whose bit is clear
-    // holds the query's initial value (inf; rhs(start) = 0 is written), so a query starts with no
-    // reset of the two HBM arrays (8 B x 2 per voxel, more than its whole search reads) and loads
-    // only the g / rhs values it wrote -- an expansion's 5x5x5 block mostly holds never-expanded
-    // voxels (g = inf).  Without `touch` (grids too large for the bits) the arrays are reset per query.
-    lds_u32* gt;
-    lds_u32* rt;
+    // Written-this-query bits of g / rhs (one bit per voxel, the worker's own 2 x ceil(V / 32) words in
+    // HBM, L2-resident; `touch`): a voxel whose bit is clear holds the query's initial value (inf;
+    // rhs(start) = 0 is written), so a query starts with no reset of the two arrays (8 B x 2 per
+    // voxel, more than its whole search writes otherwise).  The bits are read beside the g / rhs
+    // loads (same round) with L1-bypassing agent-scope atomic loads and set by atomic ORs, so a read
+    // always sees this wave's earlier sets.  (Round 5 kept them in LDS first: the 2 KB they took from
+    // U's share spilled more lists to HBM -- +50 % writes, -9 % plans/s.)
+    uint32_t* gt;
+    uint32_t* rt;
     bool touch;
     lds_f64* cube;  // 125 g values of the 5x5x5 block around the centre
     int lane;
@@ -198,12 +200,16 @@ struct L3 {
 #define LSTAMP(v)
 #endif
 
-    __device__ __forceinline__ bool gw(int c) const { return !touch || ((gt[c >> 5] >> (c & 31)) & 1u); }
-    __device__ __forceinline__ bool rw(int c) const { return !touch || ((rt[c >> 5] >> (c & 31)) & 1u); }
-    __device__ __forceinline__ double g_at(int c) const { return gw(c) ? g[c] : kInf; }
-    __device__ __forceinline__ void mark(lds_u32* t, int c) const
+    __device__ __forceinline__ static uint32_t bw(const uint32_t* t, int c)
     {
-        if (touch) __hip_atomic_fetch_or(t + (c >> 5), 1u << (c & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return __hip_atomic_load(t + (c >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ __forceinline__ bool gw(int c) const { return !touch || ((bw(gt, c) >> (c & 31)) & 1u); }
+    __device__ __forceinline__ bool rw(int c) const { return !touch || ((bw(rt, c) >> (c & 31)) & 1u); }
+    __device__ __forceinline__ double g_at(int c) const { return gw(c) ? g[c] : kInf; }
+    __device__ __forceinline__ void mark(uint32_t* t, int c) const
+    {
+        if (touch) __hip_atomic_fetch_or(t + (c >> 5), 1u << (c & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
     __device__ __forceinline__ double hval(int x, int y, int z) const
@@ -475,7 +481,7 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
     int32_t* __restrict__ path_out, int path_cap, int64_t* __restrict__ nexp_out, int32_t* __restrict__ status_out,
     int64_t* __restrict__ counters, int64_t max_exp, int* __restrict__ queue, double* __restrict__ scr_f64,
     int32_t* __restrict__ scr_i32, uint32_t* __restrict__ occ_scr, int words, int occ_lds, int ucap,
-    const int32_t* __restrict__ order, int prio_n)
+    const int32_t* __restrict__ order, int prio_n, uint32_t* __restrict__ bits_all)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
@@ -492,10 +498,9 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
     S.U.cap = ucap;
     S.occ.l = (lds_u32*)(smem + 1024 + (size_t)20 * ucap);
     S.occ.lds = occ_lds != 0;
-    // the written-this-query bits after the occupancy (with it: both fit when the occupancy does)
-    S.touch = occ_lds != 0;
-    S.gt = S.occ.l + ((words + 3) & ~3);
-    S.rt = S.gt + ((words + 3) & ~3);
+    S.touch = true;
+    S.gt = bits_all + (size_t)blockIdx.x * 2 * (size_t)words;
+    S.rt = S.gt + words;
     S.occ.g = occ_scr + (size_t)blockIdx.x * (size_t)words;
     S.occ.geo = S.geo;
     {
@@ -560,8 +565,8 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
             }
             if (S.touch) {
                 for (int w = lane; w < words; w += 64) {
-                    S.gt[w] = 0u;
-                    S.rt[w] = 0u;
+                    __hip_atomic_store(S.gt + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(S.rt + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 wsync();
                 if (lane == 0) {
@@ -771,21 +776,21 @@ extern "C" int pmp_lpastar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* o
     // up to 16 waves per CU (tools/dyn3d_sweep.py): the LDS share of each holds the g block, U (20 B per
     // entry, the rest spills) and the occupancy
     const int per_cu = std::max(1, std::min(ctx->workers_per_cu > 0 ? ctx->workers_per_cu : 16, (nq + 255) / 256));
-    // occupancy bits + the two written-this-query bitmaps (lpa3d_kernel S.gt / S.rt)
-    const int occ_bytes = occ_lds ? 3 * ((words * 4 + 15) & ~15) : 0;
+    const int occ_bytes = occ_lds ? ((words * 4 + 15) & ~15) : 0;
     int ucap = (((160 * 1024) / per_cu - 1024 - occ_bytes) / 20) & ~15;
     if (ucap < 64) ucap = 64;
     if ((size_t)ucap > ncell + 1) ucap = (int)((ncell + 1 + 15) & ~(size_t)15);
     const size_t lds = 1024 + (size_t)20 * ucap + occ_bytes;
     const size_t spill = ncell + 1;
-    const size_t per_worker = (2 * ncell + 2 * spill) * 8 + spill * 4 + (occ_lds ? 0 : (size_t)words * 4) + 256;
+    const size_t per_worker = (2 * ncell + 2 * spill) * 8 + spill * 4 + (size_t)words * 8 + (occ_lds ? 0 : (size_t)words * 4) + 256;
     int workers = 256 * per_cu;
     const size_t fit = kScratchBudget / per_worker;
     if (fit < 1) return pmp_set_err(ctx, PMP_ENOMEM, "pmp_lpastar3d_batch: one worker exceeds the scratch budget");
     if ((size_t)workers > fit) workers = (int)fit;
     if (workers > nq) workers = nq;
     double* f = (double*)pmp_scratch(ctx, SCR_AUX2, (size_t)workers * (2 * ncell + 2 * spill) * 8 + 16);
-    int32_t* i32 = (int32_t*)pmp_scratch(ctx, SCR_AUX3, (size_t)workers * spill * 4 + 16);
+    // U cells of the HBM part, then the written-this-query bits (2 x words per worker)
+    int32_t* i32 = (int32_t*)pmp_scratch(ctx, SCR_AUX3, (size_t)workers * spill * 4 + (size_t)workers * 2 * words * 4 + 16);
     uint32_t* occw = (uint32_t*)pmp_scratch(ctx, SCR_AUX4, occ_lds ? 16 : (size_t)workers * words * 4 + 16);
     int* queue = (int*)pmp_scratch(ctx, SCR_AUX0, 256);
     if (!f || !i32 || !occw || !queue) return PMP_ENOMEM;
@@ -799,7 +804,7 @@ extern "C" int pmp_lpastar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* o
     hipLaunchKernelGGL(lpa3d_kernel, dim3(workers), dim3(64), lds, s, occ_bits, per_query, X, Y, Z, heuristic, start_xyz,
                        goal_xyz, nq, changes, nr, cost, path_len, path, path_cap, n_expanded, status, counters,
                        max_expansions, queue, f, i32, occw, words, occ_lds ? 1 : 0, ucap, (const int32_t*)order,
-                       order ? ctx->astar_prio_n : 0);
+                       order ? ctx->astar_prio_n : 0, (uint32_t*)(i32 + (size_t)workers * spill));
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }

@@ -23,7 +23,13 @@
 
 namespace {
 
-constexpr int kNT = 512;
+#ifndef PMP_RRT_NT
+#define PMP_RRT_NT 512  // threads per query (dev builds: 256)
+#endif
+#ifndef PMP_RRT_WPE
+#define PMP_RRT_WPE 0  // amdgpu_waves_per_eu cap (0: none; dev builds)
+#endif
+constexpr int kNT = PMP_RRT_NT;
 constexpr int kWaves = kNT / 64;
 constexpr int kMaxObs = 256;   // per obstacle kind
 constexpr int kMaxBnd = 8;
@@ -33,7 +39,7 @@ constexpr int kMaxA = 256;     // collision-free improving candidates per iterat
 constexpr int kMaxT = 256;     // candidates awaiting a collision test per phase
 constexpr int kMaxK = 256;     // in-radius candidates kept in LDS (more spill to the HBM list)
 constexpr int kRnd = 256;      // random doubles staged in LDS
-constexpr int kLdsBytes = 160 * 1024;  // the CU's LDS: one workgroup per CU
+constexpr int kLdsBytes = 160 * 1024;  // the CU's LDS
 
 constexpr int KF_A = 1;        // c_i < G0
 constexpr int KF_VALID = 2;    // ... and collision-free
@@ -269,7 +275,11 @@ __device__ __forceinline__ double aget_c(const RrtShared& S, const AEntry* al, i
 typedef __attribute__((address_space(3))) uint32_t lds_xyq;
 
 template <bool STAR>
-__global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
+__global__ __launch_bounds__(kNT)
+#if PMP_RRT_WPE
+__attribute__((amdgpu_waves_per_eu(PMP_RRT_WPE)))
+#endif
+void rrt_kernel(RrtArgs A)
 {
     __shared__ RrtShared S;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_dyn[];
@@ -328,6 +338,17 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
     int n = 1, status = 1;
     int64_t cur = 0;
     int64_t c_iter = 0, c_scan = 0, c_cand = 0, c_tests = 0;  // iterations, nodes scanned, in-radius, collision tests
+#ifdef PMP_RRT_STAMPS
+    // dev build (tools/rrt_time.py): the counters become s_memtime ticks (>> 6) summed per phase, two
+    // phases per counter (low / high 32 bits) -- nearest scan + min, band + argmin, steer + collision,
+    // in-radius scan, first tests, choose-parent, rewire decisions + tests, insert + goal test
+    uint64_t cy[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tq = 0;
+#define RSTAMP(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); cy[k] += t_ - tq; tq = t_; } while (0)
+#define RSTAMP_START() do { tq = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define RSTAMP(k) do {} while (0)
+#define RSTAMP_START() do {} while (0)
+#endif
 
     int64_t rb0 = 0, rb1 = 0;  // staged window [rb0, rb1) of the random stream
     for (int it = 0; it < P.sample_num; it++) {
@@ -346,38 +367,41 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         }
         c_iter++;
         c_scan += n;
+        RSTAMP_START();
         // ---- 2. nearest ----
         const float sxf = (float)sx, syf = (float)sy;
+        // one formula for every pass (the band test must see the same f32 distance as the minimum)
+        auto cd2 = [&](uint32_t p, float ax, float ay) -> float {
+            const float dx = fmaf((float)(p & 0xFFFFu), qinv, qlof) - ax;
+            const float dy = fmaf((float)(p >> 16), qinv, qlof) - ay;
+            return dx * dx + dy * dy;
+        };
         float best = INFINITY;
         const int nl = n < lcap ? n : lcap;
-        for (int j = tid; j < nl; j += kNT) {  // the LDS part
-            const uint32_t p = xl[j];
-            const float dx = fmaf((float)(p & 0xFFFFu), qinv, qlof) - sxf;
-            const float dy = fmaf((float)(p >> 16), qinv, qlof) - syf;
-            best = fminf(best, dx * dx + dy * dy);
-        }
-        if (n > lcap) {
-            // the HBM part, 8 loads in flight per thread (bound by L2/MALL latency, not bandwidth)
-            int j = lcap + tid;
+        {
+            // 8 loads in flight per thread, the LDS part then the HBM part (L2/MALL latency); a
+            // compare-select minimum (the distances are finite: no fminf NaN handling)
+            int j = tid;
+            for (; j + 7 * kNT < nl; j += 8 * kNT) {
+                uint32_t p[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) p[u] = xl[j + u * kNT];
+#pragma unroll
+                for (int u = 0; u < 8; u++) { const float d = cd2(p[u], sxf, syf); best = d < best ? d : best; }
+            }
+            for (; j < nl; j += kNT) { const float d = cd2(xl[j], sxf, syf); best = d < best ? d : best; }
+            j = lcap + tid;
             for (; j + 7 * kNT < n; j += 8 * kNT) {
                 uint32_t p[8];
 #pragma unroll
                 for (int u = 0; u < 8; u++) p[u] = xyq[j + u * kNT];
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const float dx = fmaf((float)(p[u] & 0xFFFFu), qinv, qlof) - sxf;
-                    const float dy = fmaf((float)(p[u] >> 16), qinv, qlof) - syf;
-                    best = fminf(best, dx * dx + dy * dy);
-                }
+                for (int u = 0; u < 8; u++) { const float d = cd2(p[u], sxf, syf); best = d < best ? d : best; }
             }
-            for (; j < n; j += kNT) {
-                const uint32_t p = xyq[j];
-                const float dx = fmaf((float)(p & 0xFFFFu), qinv, qlof) - sxf;
-                const float dy = fmaf((float)(p >> 16), qinv, qlof) - syf;
-                best = fminf(best, dx * dx + dy * dy);
-            }
+            for (; j < n; j += kNT) { const float d = cd2(xyq[j], sxf, syf); best = d < best ? d : best; }
         }
         const float m = block_min_f(best, S);
+        RSTAMP(0);
         const double band = sqrt((double)m) + 2.0 * eps;
         const float T = (float)(band * band) * 1.0001f;
         double h = INFINITY, hx = 0.0, hy = 0.0, hg = 0.0;
@@ -385,35 +409,29 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         if (best <= T) {
             // increasing j within the thread (the LDS part, then the HBM part): equal distances keep
             // the first.  Separate loops: a select between an LDS and a global load per element would
-            // issue both.  8 loads in flight per thread in the HBM part (one at a time made it a chain
-            // of dependent L2 round trips)
-            auto band = [&](int j, uint32_t p) {
-                const float dx = fmaf((float)(p & 0xFFFFu), qinv, qlof) - sxf;
-                const float dy = fmaf((float)(p >> 16), qinv, qlof) - syf;
-                if (dx * dx + dy * dy <= T) {
-                    const double xj = tx[2 * j], yj = tx[2 * j + 1], gj = tg[j];  // one round
-                    const double e = lp::py_hypot(xj - sx, yj - sy);
-                    if (e < h) { h = e; hi = j; hx = xj; hy = yj; hg = gj; }  // increasing j: keeps the first
-                }
+            // issue both.  8 loads in flight per thread, the hits of a chunk in increasing j
+            auto hit = [&](int j) {
+                const double xj = tx[2 * j], yj = tx[2 * j + 1], gj = tg[j];  // one round
+                const double e = lp::py_hypot(xj - sx, yj - sy);
+                if (e < h) { h = e; hi = j; hx = xj; hy = yj; hg = gj; }  // increasing j: keeps the first
             };
-            for (int j = tid; j < nl; j += kNT) band(j, xl[j]);
+            for (int j0 = tid; j0 < nl; j0 += 8 * kNT) {
+                uint32_t p[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) p[u] = (j0 + u * kNT < nl) ? xl[j0 + u * kNT] : 0u;
+                uint32_t hits = 0;
+#pragma unroll
+                for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < nl) & (cd2(p[u], sxf, syf) <= T)) << u;
+                for (; hits; hits &= hits - 1) hit(j0 + (__ffs(hits) - 1) * kNT);
+            }
             for (int j0 = lcap + tid; j0 < n; j0 += 8 * kNT) {
                 uint32_t p[8];
 #pragma unroll
                 for (int u = 0; u < 8; u++) p[u] = (j0 + u * kNT < n) ? xyq[j0 + u * kNT] : 0u;
                 uint32_t hits = 0;
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const float dx = fmaf((float)(p[u] & 0xFFFFu), qinv, qlof) - sxf;
-                    const float dy = fmaf((float)(p[u] >> 16), qinv, qlof) - syf;
-                    hits |= (uint32_t)((j0 + u * kNT < n) & (dx * dx + dy * dy <= T)) << u;
-                }
-                for (; hits; hits &= hits - 1) {  // increasing j within the thread
-                    const int j = j0 + (__ffs(hits) - 1) * kNT;
-                    const double xj = tx[2 * j], yj = tx[2 * j + 1], gj = tg[j];  // one round
-                    const double e = lp::py_hypot(xj - sx, yj - sy);
-                    if (e < h) { h = e; hi = j; hx = xj; hy = yj; hg = gj; }
-                }
+                for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < n) & (cd2(p[u], sxf, syf) <= T)) << u;
+                for (; hits; hits &= hits - 1) hit(j0 + (__ffs(hits) - 1) * kNT);
             }
         }
         const int my_hi = hi;
@@ -423,6 +441,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         __syncthreads();
         const int near = hi;
         const double nx0 = S.nearx, ny0 = S.neary, gnear = S.nearg;
+        RSTAMP(1);
         // ---- 3. steer + collision (rrt.py:121-129) ----
         double dist = lp::py_hypot(sx - nx0, sy - ny0);
         const double theta = atan2(sy - ny0, sx - nx0);
@@ -430,7 +449,8 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         const double nx = nx0 + dist * cos(theta), ny = ny0 + dist * sin(theta);
         const double G0 = gnear + dist;
         c_tests++;
-        if (collision_block(S, nr, nc, nb, delta, nx, ny, nx0, ny0)) continue;
+        if (collision_block(S, nr, nc, nb, delta, nx, ny, nx0, ny0)) { RSTAMP(2); continue; }
+        RSTAMP(2);
         double G = G0;
         int parent = near;
         int slot = n;
@@ -460,11 +480,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                 }
                 uint32_t hits = 0;
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const float dx = fmaf((float)(p[u] & 0xFFFFu), qinv, qlof) - nxf;
-                    const float dy = fmaf((float)(p[u] >> 16), qinv, qlof) - nyf;
-                    hits |= (uint32_t)((j0 + u * kNT < n) & (dx * dx + dy * dy <= Tr)) << u;
-                }
+                for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < n) & (cd2(p[u], nxf, nyf) <= Tr)) << u;
               for (; hits; hits &= hits - 1) {
                 const int j = j0 + (__ffs(hits) - 1) * kNT;
                 const double xj = tx[2 * j], yj = tx[2 * j + 1], gj = tg[j];  // one round
@@ -489,6 +505,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
               }
             }
             __syncthreads();
+            RSTAMP(3);
             const int nK = S.nK;
             const int nT = S.nT;
             slot = S.slot;
@@ -508,6 +525,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             }
             __threadfence_block();  // HBM list entries before the barrier
             __syncthreads();
+            RSTAMP(4);
             const int nA = S.nA;
             double cb = INFINITY;
             int jb = 0x7fffffff;
@@ -519,6 +537,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             if (tid == 0) S.nT = 0;
             block_min_di(cb, jb, S);  // (its barriers also publish nT = 0)
             if (cb < G0) { G = cb; parent = jb; }
+            RSTAMP(5);
             // ---- 4c. rewire decisions; untested candidates queue for a collision test ----
             for (int k = tid; k < nK; k += kNT) {
                 const KRec e = kget(S, kl, tx, tg, k);
@@ -547,6 +566,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             }
             __syncthreads();  // rewires land before the insert below may overwrite a duplicate slot
         }
+        RSTAMP(6);
         // ---- 5. insert + goal test (rrt.py:70-81) ----
         if (tid == 0) {
             tx[2 * slot] = nx; tx[2 * slot + 1] = ny; tg[slot] = G; tpar[slot] = parent;
@@ -569,16 +589,22 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             status = PMP_FOUND;
             break;
         }
+        RSTAMP(7);
     }
     __syncthreads();
     if (tid == 0) {
         A.n_nodes[q] = n;
         A.draws[q] = cur;
         if (A.counters) {
+#ifdef PMP_RRT_STAMPS
+            for (int k = 0; k < 4; k++)
+                A.counters[4 * q + k] = (int64_t)(((cy[2 * k] >> 6) & 0xFFFFFFFFull) | ((cy[2 * k + 1] >> 6) << 32));
+#else
             A.counters[4 * q] = c_iter;
             A.counters[4 * q + 1] = c_scan;
             A.counters[4 * q + 2] = c_cand;
             A.counters[4 * q + 3] = c_tests;
+#endif
         }
         int plen = 0;
         double c = 0.0;
@@ -627,8 +653,10 @@ extern "C" int pmp_rrt_batch(pmp_ctx* ctx, void* stream, const pmp_rrt_params* p
     TEntry* tl = (TEntry*)pmp_scratch(ctx, SCR_AUX2, sizeof(TEntry) * (size_t)nq * tree_cap);
     AEntry* al = (AEntry*)pmp_scratch(ctx, SCR_AUX3, sizeof(AEntry) * (size_t)nq * tree_cap);
     if (!xyq || !kl || !tl || !al) return PMP_ENOMEM;
-    // the coarse copy's LDS part: the CU's LDS beside the workgroup's static state
-    int lcap = (int)((kLdsBytes - sizeof(RrtShared) - 512) / 4) & ~63;
+    // the coarse copy's LDS part: the workgroup's share of the CU's LDS (one workgroup per CU unless
+    // pmp_set_resident_per_cu leaves room for more: several in flight) beside its static state
+    const long share = kLdsBytes / pmp_lds_share(ctx, 1);
+    int lcap = (int)(std::max(0L, share - (long)sizeof(RrtShared) - 512) / 4) & ~63;
     if (lcap > tree_cap) lcap = (tree_cap + 63) & ~63;
     RrtArgs A;
     A.P = *p;

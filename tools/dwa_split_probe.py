@@ -44,3 +44,25 @@ for na, parts_list in ((32, (1, 2, 4, 8, 16)), (256, (1, 2))):
         ms = float(np.mean([a.elapsed_time(b) for a, b in evs[5:]]))
         print(f"agents {na} parts {parts}: {ms * 1e3:.1f} us per step (event span incl. the wrapper's launches)",
               flush=True)
+
+if os.environ.get("PMP_HIP_LIB", "").endswith("dwastamps.so"):
+    # phase stamps of one 32-agent step at 8 parts (s_memtime ticks, tid 0 of every workgroup)
+    na, parts = 32, 8
+    xy, off = batch.pack_paths(paths[:na])
+    st = torch.tensor(states[:na], dtype=torch.float64, device="cuda")
+    for rep in range(3):
+        st.copy_(torch.tensor(states[:na], dtype=torch.float64, device="cuda"))
+        o = batch.dwa_step_batch(grid, lp, dp, st, goals[:na], xy, off, iters=1, want_traj=True, parts=parts)
+        torch.cuda.synchronize()
+    raw = o["best_traj"].reshape(-1).cpu().numpy().view(np.uint64)[: na * parts * 10].reshape(na * parts, 10)
+    raw = raw.astype(np.int64)
+    raw = raw[raw[:, 0] > 0]  # parts that ran (a stopped agent's parts return before stamping)
+    t0 = raw[:, 0].min()
+    names = ["start", "lookahead", "sincos", "rollout", "columns", "arrive", "sums", "scores", "end"]
+    part = raw[:, :6] - t0
+    print("all parts, mean ticks since the first start:", {n: int(part[:, i].mean()) for i, n in enumerate(names[:6])})
+    last = raw[raw[:, 6] > 0] - t0
+    print("per-phase mean ticks, all parts:", np.diff(raw[:, :6], axis=1).mean(axis=0).round().tolist())
+    print("per-phase mean ticks, last parts:", np.diff(raw[raw[:, 6] > 0][:, :9], axis=1).mean(axis=0).round().tolist())
+    print("last parts, mean ticks since the first start:", {n: int(last[:, i].mean()) for i, n in enumerate(names)})
+    print("last part end, max ticks:", int(last[:, 8].max()))

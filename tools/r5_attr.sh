@@ -5,7 +5,7 @@
 # category issued twice; blk2 / blk2mir = the half-block spill layout (PMP_MQ_BLOCKS=2), plain / all
 # spill stores mirrored.  Per-dispatch WRITE_SIZE of the 20-batch launch -> gpurun_out/attr/summary.txt
 R=${GRAFT_REPO_ROOT:-/root/repo}
-OUT=$R/gpurun_out/attr
+OUT=$R/gpurun_out/${ATTR_DIR:-attr}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 # spec = build[:counter,counter...] (default counter WRITE_SIZE); blk2 = the half-block spill layout

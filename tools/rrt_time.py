@@ -1,4 +1,5 @@
 """Dev probe: RRT* kernel time on the C3 map for a few batch sizes (HIP events around the launch)."""
+import os
 import sys
 import time
 
@@ -22,10 +23,25 @@ for nq, sn in [(int(a), int(b)) for a, b in (x.split("x") for x in sys.argv[1:])
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.time()
     e0.record()
-    out = batch.rrt_batch(env, s, g, rnd_d, sn, star=True)
+    out = batch.rrt_batch(env, s, g, rnd_d, sn, star=True, counters=True)
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1)
     nn = out["n_nodes"].cpu().numpy()
     print(f"nq={nq} samples={sn}: {ms:.1f} ms ({ms * 1e3 / sn:.2f} us/iteration), nodes mean {nn.mean():.0f} "
           f"max {nn.max()}, found {(out['status'].cpu().numpy() == 0).sum()}", flush=True)
+    c = out["counters"].cpu().numpy()
+    if "stamps" in os.environ.get("PMP_HIP_LIB", ""):  # per-phase s_memtime ticks >> 6, two per counter
+        ph = np.concatenate([(c & 0xFFFFFFFF)[:, :, None], (c >> 32)[:, :, None]], axis=2).reshape(nq, 8) * 64.0
+        names = ("nearest-scan", "band+argmin", "steer+collision", "radius-scan", "tests1", "choose", "rewire+tests2",
+                 "insert+goal")
+        tot = ph.sum(axis=1)
+        print("  phase ticks per iteration: " + ", ".join(f"{n} {v / sn:.0f}" for n, v in zip(names, ph.mean(axis=0)))
+              + f"; total {tot.mean() / sn:.0f}", flush=True)
+        continue
+    c = c.astype(np.float64)
+    if False:
+        pass
+    else:
+        print(f"  per iteration: nodes scanned {c[:, 1].sum() / c[:, 0].sum():.0f}, in-radius "
+              f"{c[:, 2].sum() / c[:, 0].sum():.1f}, collision tests {c[:, 3].sum() / c[:, 0].sum():.2f}", flush=True)
