@@ -353,8 +353,14 @@ __global__ __launch_bounds__(kThreads) void dwa_kernel(
 // samples, takes the first-index argmax (dwa.py:89) and moves the robot.  One launch per plan
 // iteration (the next iteration needs the moved state); an agent that stopped (goal reached, a
 // reference raise) is skipped by later launches through its status.
-constexpr int kSplitThreads = 512;
+constexpr int kSplitRoll = 512;                 // rollout threads (waves 0..7), one sample each
+constexpr int kSplitThreads = kSplitRoll + 64;  // + the control wave: lookahead and leaf table beside them
 constexpr int kSplitChunk = 1024;  // samples of one part held in LDS
+
+// part p's samples [c[p], c[p + 1]): the host's restatement of the tree's leaves (split_bounds)
+struct DwaSplitBounds {
+    int c[65];
+};
 
 struct DwaSplitShared {
     uint32_t occ[kOccLdsWords];
@@ -364,8 +370,8 @@ struct DwaSplitShared {
     double redd[kSplitThreads / 64];
     int redi[kSplitThreads / 64];
     double sums[3];
-    double sn0, cs0;
     double pt[2];
+    int raises;
     int nleaves;
     int last;
 };
@@ -416,7 +422,7 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
     int it, int iters, double* __restrict__ state, const double* __restrict__ goal, const double* __restrict__ path_xy,
     const int32_t* __restrict__ path_off, double* __restrict__ u_out, int32_t* __restrict__ best_out,
     int32_t* __restrict__ status_out, int32_t* __restrict__ nsteps_out, double* __restrict__ hist_pose,
-    double* __restrict__ eval_out, double* __restrict__ best_traj, DwaSplitScratch X)
+    double* __restrict__ eval_out, double* __restrict__ best_traj, DwaSplitScratch X, DwaSplitBounds B)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     DwaSplitShared& S = *reinterpret_cast<DwaSplitShared*>(smem_raw);
@@ -424,9 +430,12 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
     const int tid = threadIdx.x, nt = blockDim.x;
     if (a >= na) return;
     DSTAMP(0);
-    if (it > 0 && status_out[a] != 0) return;  // stopped in an earlier iteration (block-uniform)
+    // every independent load of the step in one round: the stop status, the state, the path's offsets
+    const int stp = it > 0 ? status_out[a] : 0;
     double st[5];
     for (int q = 0; q < 5; q++) st[q] = state[5 * a + q];
+    const int po = path_off[a], Pn = path_off[a + 1] - po;
+    if (stp != 0) return;  // stopped in an earlier iteration (block-uniform)
     // a stop in this iteration: part 0 records it (at it = 0 also the outputs of a plan that never moved)
     auto stop = [&](int status) {
         if (part == 0 && tid == 0) {
@@ -445,76 +454,75 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
         for (int i = tid; i < words; i += nt) S.occ[i] = occ[i];
     }
     const lds_w32* occl = (const lds_w32*)S.occ;
-    const double* path = path_xy + 2 * (size_t)path_off[a];
-    const int Pn = path_off[a + 1] - path_off[a];
     const double dt = P.dt;
     const int Hh = (int)(D.predict_time / dt);
     const double R = D.inflation;
     const int nv = D.nv, nw = D.nw;  // the host splits only windows of fixed size (nv, nw > 0)
     const int N = nv * nw;
-    {
-        // getLookaheadPoint (local_planner.py:103-170, lp::lookahead_block's steps) with one load
-        // round: each thread keeps the distances of its first two path points for the
-        // first-beyond-lookahead search; the serial tail runs on thread 0 while thread 64 builds the
-        // pairwise tree's leaf table and the heading's sin / cos
-        const double rx = st[0], ry = st[1];
-        const double L = lp::lookahead_dist(st[3], P);
-        double d0 = INFINITY, d1 = INFINITY, bd = INFINITY;
-        int bi = 0x7fffffff;
-        for (int i = tid; i < Pn; i += nt) {
-            const double d = lp::py_hypot(rx - path[2 * i], ry - path[2 * i + 1]);
-            if (i == tid) d0 = d;
-            else if (i == tid + nt) d1 = d;
-            if (d < bd) { bd = d; bi = i; }  // strided in increasing i: keeps the first minimum
-        }
-        lp::block_best<true>(bd, bi, S.redd, S.redi);
-        const int idx_closest = bi;
-        int fi = 0x7fffffff;  // first i >= idx_closest with dist >= L (this thread's, increasing i)
-        for (int i = tid; i < Pn; i += nt) {
-            if (i < idx_closest) continue;
-            const double d = i == tid ? d0 : (i == tid + nt ? d1 : lp::py_hypot(rx - path[2 * i], ry - path[2 * i + 1]));
-            if (d >= L) { fi = i; break; }
-        }
-        double fd = 0.0;
-        lp::block_best<true>(fd, fi, S.redd, S.redi);
-        __syncthreads();  // redd / redi read everywhere before thread 0 reuses them
-        if (tid == 0) {
-            double pt[2] = {0, 0}, theta = 0, kappa = 0;
-            S.redi[0] = lp::lookahead_tail(path, Pn, rx, ry, L, fi == 0x7fffffff ? Pn - 1 : fi, pt, &theta, &kappa);
-            S.pt[0] = pt[0];
-            S.pt[1] = pt[1];
-        } else if (tid == 64) {
-            int nl = 0;
-            pw_leaves<kPwDepth>(0, N, S.leaf_lo, S.leaf_n, nl);
-            S.nleaves = nl;
-            sincos(st[2], &S.sn0, &S.cs0);
-        }
-        __syncthreads();
-    }
-    if (S.redi[0]) { stop(PMP_REF_RAISES); return; }
-    DSTAMP(1);
-    const double gx = S.pt[0], gy = S.pt[1];
     const double vr0 = fmax(P.min_v, st[3] + P.min_v_inc * dt), vr1 = fmin(P.max_v, st[3] + P.max_v_inc * dt);
     const double vr2 = fmax(P.min_w, st[4] + P.min_w_inc * dt), vr3 = fmin(P.max_w, st[4] + P.max_w_inc * dt);
     const Linsp LV = make_linsp(vr0, vr1, nv), LW = make_linsp(vr2, vr3, nw);
-    const int nl = S.nleaves;
-    const int l0 = (int)(((long)nl * part) / k), l1 = (int)(((long)nl * (part + 1)) / k);
-    const int c0 = l0 < nl ? S.leaf_lo[l0] : N, c1 = l1 < nl ? S.leaf_lo[l1] : N;
-    // the three passes of dwa_kernel over this part's samples (LDS index c - c0)
-    for (int c = c0 + tid; c < c1; c += nt)
-        sincos(dt * linsp_at(LW, c % nw), &S.col[1][c - c0], &S.col[2][c - c0]);
+    const int c0 = B.c[part], c1 = B.c[part + 1];
+    __syncthreads();  // the occupancy in LDS
+    DSTAMP(1);
+    if (tid < kSplitRoll) {
+        // the rollouts (dwa.py:152-160) and their stencil minima, one sample per thread; they need only
+        // the state, so the control wave's lookahead runs beside them
+        double sn0, cs0;
+        sincos(st[2], &sn0, &cs0);
+        for (int c = c0 + tid; c < c1; c += kSplitRoll) {
+            double sd, cd, x, y, mind2;
+            sincos(dt * linsp_at(LW, c % nw), &sd, &cd);
+            rollout<OCC_LDS>(occ, occl, ox, oy, W, H, R, dt, Hh, st[0], st[1], sn0, cs0, sd, cd, linsp_at(LV, c / nw), x,
+                             y, mind2);
+            S.col[0][c - c0] = x;
+            S.col[1][c - c0] = mind2;
+            S.col[2][c - c0] = y;
+        }
+    } else {
+        // the control wave: getLookaheadPoint (local_planner.py:103-170, lp::lookahead_block's steps)
+        // with wave-level first-index reductions, its serial tail on lane 0 and the pairwise tree's
+        // leaf table on lane 1
+        const int ln = tid - kSplitRoll;
+        const double rx = st[0], ry = st[1];
+        const double L = lp::lookahead_dist(st[3], P);
+        const double* path = path_xy + 2 * (size_t)po;
+        double bd = INFINITY;
+        int bi = 0x7fffffff;
+        for (int i = ln; i < Pn; i += 64) {
+            const double d = lp::py_hypot(rx - path[2 * i], ry - path[2 * i + 1]);
+            if (d < bd) { bd = d; bi = i; }  // strided in increasing i: keeps the first minimum
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const double ov = __shfl_xor(bd, o, 64);
+            const int oi = __shfl_xor(bi, o, 64);
+            if (ov < bd || (ov == bd && oi < bi)) { bd = ov; bi = oi; }
+        }
+        const int idx_closest = bi;
+        int fi = 0x7fffffff;  // first i >= idx_closest with dist >= L
+        for (int i = idx_closest + ln; i < Pn; i += 64)
+            if (lp::py_hypot(rx - path[2 * i], ry - path[2 * i + 1]) >= L) { fi = i; break; }
+        for (int o = 32; o > 0; o >>= 1) {
+            const int oi = __shfl_xor(fi, o, 64);
+            fi = oi < fi ? oi : fi;
+        }
+        if (ln == 0) {
+            double pt[2] = {0, 0}, theta = 0, kappa = 0;
+            S.raises = lp::lookahead_tail(path, Pn, rx, ry, L, fi == 0x7fffffff ? Pn - 1 : fi, pt, &theta, &kappa);
+            S.pt[0] = pt[0];
+            S.pt[1] = pt[1];
+        } else if (ln == 1) {
+            int nl = 0;
+            pw_leaves<kPwDepth>(0, N, S.leaf_lo, S.leaf_n, nl);
+            S.nleaves = nl;
+        }
+    }
     __syncthreads();
     DSTAMP(2);
-    const double sn0 = S.sn0, cs0 = S.cs0;
-    for (int c = c0 + tid; c < c1; c += nt) {
-        double x, y, mind2;
-        rollout<OCC_LDS>(occ, occl, ox, oy, W, H, R, dt, Hh, st[0], st[1], sn0, cs0, S.col[1][c - c0],
-                         S.col[2][c - c0], linsp_at(LV, c / nw), x, y, mind2);
-        S.col[0][c - c0] = x;
-        S.col[1][c - c0] = mind2;
-        S.col[2][c - c0] = y;
-    }
-    DSTAMP(3);
+    if (S.raises) { stop(PMP_REF_RAISES); return; }
+    const double gx = S.pt[0], gy = S.pt[1];
+    const int nl = S.nleaves;
+    const int l0 = (int)(((long)nl * part) / k), l1 = (int)(((long)nl * (part + 1)) / k);
     double* cols = X.cols + (size_t)a * 3 * kMaxN;
     double* lsum = X.leafsum + (size_t)a * 3 * kMaxLeaves;
     for (int c = c0 + tid; c < c1; c += nt) {
@@ -533,6 +541,7 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
         st_wt(cols + kMaxN + c, o);
         st_wt(cols + 2 * kMaxN + c, vel);
     }
+    DSTAMP(3);
     __syncthreads();
     {
         const int ml = l1 - l0;
@@ -643,7 +652,28 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
     DSTAMP(8);
 }
 
-// host restatement of pw_leaves: the largest part of n samples over k parts (leaf-aligned)
+// host restatement of pw_leaves: part p of k takes leaves [nl p / k, nl (p + 1) / k), samples
+// [c[p], c[p + 1]) (c has k + 1 entries)
+void split_bounds(int n, int k, int* c)
+{
+    int lo[kMaxLeaves], len[kMaxLeaves], nl = 0;
+    struct R {
+        static void go(int d, int l, int m, int* lo, int* len, int& nl)
+        {
+            if (d == 0 || m <= 128) { lo[nl] = l; len[nl] = m; nl++; return; }
+            const int m2 = (m / 2) - (m / 2) % 8;
+            go(d - 1, l, m2, lo, len, nl);
+            go(d - 1, l + m2, m - m2, lo, len, nl);
+        }
+    };
+    R::go(kPwDepth, 0, n, lo, len, nl);
+    for (int p = 0; p <= k; p++) {
+        const int l = (int)(((long)nl * p) / k);
+        c[p] = l < nl ? lo[l] : n;
+    }
+}
+
+// the largest part of n samples over k parts (leaf-aligned)
 int split_max_chunk(int n, int k)
 {
     int lo[kMaxLeaves], len[kMaxLeaves], nl = 0;
@@ -723,11 +753,13 @@ extern "C" int pmp_dwa_step_batch(pmp_ctx* ctx, void* stream, const uint32_t* oc
             ctx->dwa_zeroed = scr;
             ctx->dwa_zeroed_n = na;
         }
+        DwaSplitBounds Bd;
+        split_bounds(dp->nv * dp->nw, k, Bd.c);
         auto sk = occ_lds ? dwa_split_kernel<true> : dwa_split_kernel<false>;
         for (int it = 0; it < iters; it++)
             hipLaunchKernelGGL(sk, dim3((unsigned)(na * k)), dim3(kSplitThreads), sizeof(DwaSplitShared), (hipStream_t)stream,
                                occ_bits, ox, oy, W, H, *lp, *dp, na, k, it, iters, state, goal, path_xy, path_off, u, best,
-                               status, n_steps, hist_pose, eval, best_traj, X);
+                               status, n_steps, hist_pose, eval, best_traj, X, Bd);
         PMP_HIP_CHECK(ctx, hipGetLastError());
         return PMP_OK;
     }

@@ -39,6 +39,7 @@ constexpr int kMaxA = 256;     // collision-free improving candidates per iterat
 constexpr int kMaxT = 256;     // candidates awaiting a collision test per phase
 constexpr int kMaxK = 256;     // in-radius candidates kept in LDS (more spill to the HBM list)
 constexpr int kRnd = 256;      // random doubles staged in LDS
+constexpr int kBins = 16;      // obstacle bins per axis over the map
 constexpr int kLdsBytes = 160 * 1024;  // the CU's LDS
 
 constexpr int KF_A = 1;        // c_i < G0
@@ -98,8 +99,15 @@ struct RrtShared {
     int kj[kMaxK], kf[kMaxK];
     double kd[kMaxK], kx[kMaxK], ky[kMaxK], kg[kMaxK];
     double rbuf[kRnd];  // window of the query's random stream
-    double nearx, neary, nearg;
-    int nK, nA, nT, slot;
+    // obstacle bins: bit o of bin (bx, by) = obstacle o's inflated box (plus a margin) meets the bin
+    // (o: circles, then rects, then the boundary -- coll_item's order); <= 128 obstacles
+    uint64_t binm[kBins * kBins][2];
+    double bininv_x, bininv_y;
+    int use_bins;
+    float t2a[kWaves], t2b[kWaves];  // the nearest scan's per-wave top-2 ...
+    int t2i[kWaves];                 // ... and the minimum's index
+    double nearx, neary, nearg, nearh;
+    int nK, nA, nT, nT2, slot;
 };
 
 // ---- obstacle tests (sample_search.py), same operation order as the oracle ----
@@ -184,13 +192,73 @@ __device__ inline bool coll_item(const RrtShared& S, int nr, int nc, int nb, dou
 
 __device__ inline int coll_items(int nr, int nc, int nb) { return 2 * (nc + nr + nb) + nr + nc; }
 
+// ---- binned collision tests: only the obstacles whose bins meet the segment's bounding box --------
+// Every item coll_item can find true (p1 or p2 inside an inflated obstacle, the segment crossing
+// one) lies in the segment's bounding box and in the obstacle's inflated box, so the two boxes share
+// a bin (the same monotone bin map for both): the items of the other obstacles are false, and the
+// OR over the rest is isCollision's answer bit for bit.
+__device__ __forceinline__ int bin_of(double v, double inv)
+{
+    return (int)floor(fmin(fmax(v * inv, 0.0), (double)(kBins - 1)));
+}
+
+// j-th set bit of x (j < popcount(x))
+__device__ __forceinline__ int select64(uint64_t x, int j)
+{
+    int pos = 0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+        const int c = __popcll(x & ((1ull << w) - 1ull));
+        if (j >= c) { j -= c; x >>= w; pos += w; }
+    }
+    return pos;
+}
+
+// the obstacles of the bins the box of (x1, y1)-(x2, y2) meets; false: too many bins (test all)
+__device__ __forceinline__ bool bins_mask(const RrtShared& S, double x1, double y1, double x2, double y2, uint64_t& lo,
+                                          uint64_t& hi)
+{
+    const int bx0 = bin_of(fmin(x1, x2), S.bininv_x), bx1 = bin_of(fmax(x1, x2), S.bininv_x);
+    const int by0 = bin_of(fmin(y1, y2), S.bininv_y), by1 = bin_of(fmax(y1, y2), S.bininv_y);
+    if (!S.use_bins || (bx1 - bx0 + 1) * (by1 - by0 + 1) > 9) return false;
+    lo = 0;
+    hi = 0;
+    for (int by = by0; by <= by1; by++)
+        for (int bx = bx0; bx <= bx1; bx++) {
+            lo |= S.binm[by * kBins + bx][0];
+            hi |= S.binm[by * kBins + bx][1];
+        }
+    return true;
+}
+
+// item t of the binned list (3 per obstacle: inside p1, inside p2, crossing) as a coll_item index, or -1
+__device__ __forceinline__ int bin_item(uint64_t lo, int nlo, uint64_t hi, int t, int nr, int nc, int nb)
+{
+    const int j = t / 3, kind = t - 3 * j;
+    const int o = j < nlo ? select64(lo, j) : 64 + select64(hi, j - nlo);
+    const int per = nc + nr + nb;
+    if (kind < 2) return kind * per + o;
+    if (o < nc) return 2 * per + nr + o;       // circle crossing
+    if (o < nc + nr) return 2 * per + (o - nc);  // rect crossing
+    return -1;                                  // the boundary has no crossing test
+}
+
 // one wave cooperates on one isCollision(p1, p2); wave-uniform result
 __device__ bool collision_wave(const RrtShared& S, int nr, int nc, int nb, double d, double x1, double y1, double x2,
                                double y2)
 {
-    const int items = coll_items(nr, nc, nb);
     bool hit = false;
-    for (int it = lane_id(); it < items; it += 64) hit |= coll_item(S, nr, nc, nb, d, it, x1, y1, x2, y2);
+    uint64_t lo, hi;
+    if (bins_mask(S, x1, y1, x2, y2, lo, hi)) {
+        const int nlo = __popcll(lo), items = 3 * (nlo + __popcll(hi));
+        for (int t = lane_id(); t < items; t += 64) {
+            const int it = bin_item(lo, nlo, hi, t, nr, nc, nb);
+            if (it >= 0) hit |= coll_item(S, nr, nc, nb, d, it, x1, y1, x2, y2);
+        }
+    } else {
+        const int items = coll_items(nr, nc, nb);
+        for (int it = lane_id(); it < items; it += 64) hit |= coll_item(S, nr, nc, nb, d, it, x1, y1, x2, y2);
+    }
     return ballot(hit) != 0;
 }
 
@@ -198,9 +266,19 @@ __device__ bool collision_wave(const RrtShared& S, int nr, int nc, int nb, doubl
 __device__ bool collision_block(const RrtShared& S, int nr, int nc, int nb, double d, double x1, double y1, double x2,
                                 double y2)
 {
-    const int items = coll_items(nr, nc, nb);
     int hit = 0;
-    for (int it = threadIdx.x; it < items; it += kNT) hit |= coll_item(S, nr, nc, nb, d, it, x1, y1, x2, y2);
+    uint64_t lo, hi;
+    // (the bins only when the full list would take more than one pass of the workgroup)
+    if (coll_items(nr, nc, nb) > kNT && bins_mask(S, x1, y1, x2, y2, lo, hi)) {
+        const int nlo = __popcll(lo), items = 3 * (nlo + __popcll(hi));
+        for (int t = threadIdx.x; t < items; t += kNT) {
+            const int it = bin_item(lo, nlo, hi, t, nr, nc, nb);
+            if (it >= 0) hit |= coll_item(S, nr, nc, nb, d, it, x1, y1, x2, y2);
+        }
+    } else {
+        const int items = coll_items(nr, nc, nb);
+        for (int it = threadIdx.x; it < items; it += kNT) hit |= coll_item(S, nr, nc, nb, d, it, x1, y1, x2, y2);
+    }
     return __syncthreads_or(hit) != 0;
 }
 
@@ -293,6 +371,38 @@ void rrt_kernel(RrtArgs A)
     for (int i = tid; i < 3 * nc; i += kNT) S.circ[i] = A.circ[i];
     for (int i = tid; i < 4 * nb; i += kNT) S.bnd[i] = A.bnd[i];
     const pmp_rrt_params P = A.P;
+    if (tid == 0) {
+        S.use_bins = nc + nr + nb <= 128 && P.x_range > 0 && P.y_range > 0;
+        S.bininv_x = kBins / P.x_range;
+        S.bininv_y = kBins / P.y_range;
+    }
+    __syncthreads();
+    for (int b = tid; b < kBins * kBins; b += kNT) {
+        // obstacle boxes inflated by delta plus 1e-3 (far above every rounding slack of coll_item's
+        // tests at map coordinates), mapped with the query's bin_of
+        const int bx = b % kBins, by = b / kBins;
+        uint64_t m0 = 0, m1 = 0;
+        const double mg = P.delta + 1e-3;
+        for (int o = 0; S.use_bins && o < nc + nr + nb; o++) {
+            double x0, x1, y0, y1;
+            if (o < nc) {
+                const double* c = &S.circ[3 * o];
+                x0 = c[0] - c[2] - mg; x1 = c[0] + c[2] + mg; y0 = c[1] - c[2] - mg; y1 = c[1] + c[2] + mg;
+            } else {
+                const double* r = o < nc + nr ? &S.rect[4 * (o - nc)] : &S.bnd[4 * (o - nc - nr)];
+                x0 = r[0] - mg; x1 = r[0] + r[2] + mg; y0 = r[1] - mg; y1 = r[1] + r[3] + mg;
+            }
+            if (bin_of(x0, S.bininv_x) <= bx && bx <= bin_of(x1, S.bininv_x) && bin_of(y0, S.bininv_y) <= by &&
+                by <= bin_of(y1, S.bininv_y))
+            {
+                if (o < 64) m0 |= 1ull << o;
+                else m1 |= 1ull << (o - 64);
+            }
+        }
+        S.binm[b][0] = m0;
+        S.binm[b][1] = m1;
+    }
+    __syncthreads();
     const double delta = P.delta;
     const int cap = A.cap;
     double* tx = A.txy + (size_t)q * cap * 2;
@@ -376,69 +486,123 @@ void rrt_kernel(RrtArgs A)
             const float dy = fmaf((float)(p >> 16), qinv, qlof) - ay;
             return dx * dx + dy * dy;
         };
-        float best = INFINITY;
+        // each thread's minimum, its first index and its second-smallest distance: the band below
+        // holds only the thread's first minimum unless the second one is in it too (then the thread
+        // re-scans its nodes), so the common case needs no second pass over the tree
+        float best = INFINITY, second = INFINITY;
+        int bj = 0;
+        auto take = [&](float d, int j) {
+            const bool lt = d < best;  // strict: increasing j keeps the first
+            second = lt ? best : (d < second ? d : second);
+            bj = lt ? j : bj;
+            best = lt ? d : best;
+        };
         const int nl = n < lcap ? n : lcap;
         {
-            // 8 loads in flight per thread, the LDS part then the HBM part (L2/MALL latency); a
-            // compare-select minimum (the distances are finite: no fminf NaN handling)
+            // 8 loads in flight per thread, the LDS part then the HBM part (L2/MALL latency), in
+            // increasing j
             int j = tid;
             for (; j + 7 * kNT < nl; j += 8 * kNT) {
                 uint32_t p[8];
 #pragma unroll
                 for (int u = 0; u < 8; u++) p[u] = xl[j + u * kNT];
 #pragma unroll
-                for (int u = 0; u < 8; u++) { const float d = cd2(p[u], sxf, syf); best = d < best ? d : best; }
+                for (int u = 0; u < 8; u++) take(cd2(p[u], sxf, syf), j + u * kNT);
             }
-            for (; j < nl; j += kNT) { const float d = cd2(xl[j], sxf, syf); best = d < best ? d : best; }
+            for (; j < nl; j += kNT) take(cd2(xl[j], sxf, syf), j);
             j = lcap + tid;
             for (; j + 7 * kNT < n; j += 8 * kNT) {
                 uint32_t p[8];
 #pragma unroll
                 for (int u = 0; u < 8; u++) p[u] = xyq[j + u * kNT];
 #pragma unroll
-                for (int u = 0; u < 8; u++) { const float d = cd2(p[u], sxf, syf); best = d < best ? d : best; }
+                for (int u = 0; u < 8; u++) take(cd2(p[u], sxf, syf), j + u * kNT);
             }
-            for (; j < n; j += kNT) { const float d = cd2(xyq[j], sxf, syf); best = d < best ? d : best; }
+            for (; j < n; j += kNT) take(cd2(xyq[j], sxf, syf), j);
         }
-        const float m = block_min_f(best, S);
+        // the exact coordinates of this thread's minimum, loaded ahead of the block minimum
+        const double bxj = tx[2 * bj], byj = tx[2 * bj + 1], bgj = tg[bj];
+        // block top-2 of the threads' f32 distances (each thread's minimum and second) and the
+        // minimum's index: when nothing but the minimum lies in the band the minimum is the nearest
+        // node (the band's exact re-evaluation has one candidate) and its owner publishes it
+        float m, b2;
+        int im;
+        {
+            float ta = best, tb = second;
+            int ti = bj;
+            for (int o = 32; o > 0; o >>= 1) {
+                const float oa = __shfl_xor(ta, o), ob = __shfl_xor(tb, o);
+                const int oi = __shfl_xor(ti, o);
+                const float hi2 = oa < ta ? ta : oa;
+                tb = hi2 < tb ? hi2 : tb;
+                tb = ob < tb ? ob : tb;
+                if (oa < ta || (oa == ta && oi < ti)) { ta = oa; ti = oi; }
+            }
+            if ((tid & 63) == 0) { S.t2a[tid >> 6] = ta; S.t2b[tid >> 6] = tb; S.t2i[tid >> 6] = ti; }
+            __syncthreads();
+            m = S.t2a[0]; b2 = S.t2b[0]; im = S.t2i[0];
+            for (int w = 1; w < kWaves; w++) {
+                const float oa = S.t2a[w], ob = S.t2b[w];
+                const int oi = S.t2i[w];
+                const float hi2 = oa < m ? m : oa;
+                b2 = hi2 < b2 ? hi2 : b2;
+                b2 = ob < b2 ? ob : b2;
+                if (oa < m || (oa == m && oi < im)) { m = oa; im = oi; }
+            }
+        }
         RSTAMP(0);
         const double band = sqrt((double)m) + 2.0 * eps;
         const float T = (float)(band * band) * 1.0001f;
-        double h = INFINITY, hx = 0.0, hy = 0.0, hg = 0.0;
         int hi = 0x7fffffff;
-        if (best <= T) {
-            // increasing j within the thread (the LDS part, then the HBM part): equal distances keep
-            // the first.  Separate loops: a select between an LDS and a global load per element would
-            // issue both.  8 loads in flight per thread, the hits of a chunk in increasing j
-            auto hit = [&](int j) {
-                const double xj = tx[2 * j], yj = tx[2 * j + 1], gj = tg[j];  // one round
-                const double e = lp::py_hypot(xj - sx, yj - sy);
-                if (e < h) { h = e; hi = j; hx = xj; hy = yj; hg = gj; }  // increasing j: keeps the first
-            };
-            for (int j0 = tid; j0 < nl; j0 += 8 * kNT) {
-                uint32_t p[8];
-#pragma unroll
-                for (int u = 0; u < 8; u++) p[u] = (j0 + u * kNT < nl) ? xl[j0 + u * kNT] : 0u;
-                uint32_t hits = 0;
-#pragma unroll
-                for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < nl) & (cd2(p[u], sxf, syf) <= T)) << u;
-                for (; hits; hits &= hits - 1) hit(j0 + (__ffs(hits) - 1) * kNT);
+        if (!(b2 <= T)) {
+            // one candidate: the minimum's owner publishes it (the exact distance only for the
+            // sample-already-in-the-tree test; steering recomputes it)
+            if (best == m && bj == im) {
+                S.nearx = bxj; S.neary = byj; S.nearg = bgj;
+                S.nearh = lp::py_hypot(bxj - sx, byj - sy);
             }
-            for (int j0 = lcap + tid; j0 < n; j0 += 8 * kNT) {
-                uint32_t p[8];
+            __syncthreads();
+            hi = im;
+            if (S.nearh == 0.0) continue;  // node_rand.current already in sample_list
+        } else {
+            double h = INFINITY, hx = 0.0, hy = 0.0, hg = 0.0;
+            if (best <= T && !(second <= T)) {
+                h = lp::py_hypot(bxj - sx, byj - sy);
+                hi = bj; hx = bxj; hy = byj; hg = bgj;
+            } else if (best <= T) {
+                // increasing j within the thread (the LDS part, then the HBM part): equal distances keep
+                // the first.  Separate loops: a select between an LDS and a global load per element
+                // would issue both.  8 loads in flight per thread, the hits of a chunk in increasing j
+                auto hit = [&](int j) {
+                    const double xj = tx[2 * j], yj = tx[2 * j + 1], gj = tg[j];  // one round
+                    const double e = lp::py_hypot(xj - sx, yj - sy);
+                    if (e < h) { h = e; hi = j; hx = xj; hy = yj; hg = gj; }  // increasing j: keeps the first
+                };
+                for (int j0 = tid; j0 < nl; j0 += 8 * kNT) {
+                    uint32_t p[8];
 #pragma unroll
-                for (int u = 0; u < 8; u++) p[u] = (j0 + u * kNT < n) ? xyq[j0 + u * kNT] : 0u;
-                uint32_t hits = 0;
+                    for (int u = 0; u < 8; u++) p[u] = (j0 + u * kNT < nl) ? xl[j0 + u * kNT] : 0u;
+                    uint32_t hits = 0;
 #pragma unroll
-                for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < n) & (cd2(p[u], sxf, syf) <= T)) << u;
-                for (; hits; hits &= hits - 1) hit(j0 + (__ffs(hits) - 1) * kNT);
+                    for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < nl) & (cd2(p[u], sxf, syf) <= T)) << u;
+                    for (; hits; hits &= hits - 1) hit(j0 + (__ffs(hits) - 1) * kNT);
+                }
+                for (int j0 = lcap + tid; j0 < n; j0 += 8 * kNT) {
+                    uint32_t p[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) p[u] = (j0 + u * kNT < n) ? xyq[j0 + u * kNT] : 0u;
+                    uint32_t hits = 0;
+#pragma unroll
+                    for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < n) & (cd2(p[u], sxf, syf) <= T)) << u;
+                    for (; hits; hits &= hits - 1) hit(j0 + (__ffs(hits) - 1) * kNT);
+                }
             }
+            const int my_hi = hi;
+            block_min_di(h, hi, S);
+            if (h == 0.0) continue;  // node_rand.current already in sample_list
+            if (my_hi == hi) { S.nearx = hx; S.neary = hy; S.nearg = hg; }  // the owner publishes the node
+            __syncthreads();
         }
-        const int my_hi = hi;
-        block_min_di(h, hi, S);
-        if (h == 0.0) continue;  // node_rand.current already in sample_list
-        if (my_hi == hi) { S.nearx = hx; S.neary = hy; S.nearg = hg; }  // the owner publishes the node
-        __syncthreads();
         const int near = hi;
         const double nx0 = S.nearx, ny0 = S.neary, gnear = S.nearg;
         RSTAMP(1);
@@ -454,7 +618,7 @@ void rrt_kernel(RrtArgs A)
         double G = G0;
         int parent = near;
         int slot = n;
-        if (tid == 0) { S.nK = 0; S.nA = 0; S.nT = 0; S.slot = n; }
+        if (tid == 0) { S.nK = 0; S.nA = 0; S.nT = 0; S.nT2 = 0; S.slot = n; }
         __syncthreads();
         if (STAR) {
             const int wave = tid >> 6, lane = tid & 63;
@@ -527,15 +691,20 @@ void rrt_kernel(RrtArgs A)
             __syncthreads();
             RSTAMP(4);
             const int nA = S.nA;
+            // choose-parent: min (c, j) over the A list, reduced by every wave on its own (the list is
+            // short), so no workgroup round
             double cb = INFINITY;
             int jb = 0x7fffffff;
-            for (int a = tid; a < nA; a += kNT) {
+            for (int a = lane; a < nA; a += 64) {
                 const double c = aget_c(S, al, a);
                 const int j = aget_j(S, al, a);
                 if (c < cb || (c == cb && j < jb)) { cb = c; jb = j; }
             }
-            if (tid == 0) S.nT = 0;
-            block_min_di(cb, jb, S);  // (its barriers also publish nT = 0)
+            for (int o = 32; o > 0; o >>= 1) {
+                const double ov = __shfl_xor(cb, o);
+                const int oi = __shfl_xor(jb, o);
+                if (ov < cb || (ov == cb && oi < jb)) { cb = ov; jb = oi; }
+            }
             if (cb < G0) { G = cb; parent = jb; }
             RSTAMP(5);
             // ---- 4c. rewire decisions; untested candidates queue for a collision test ----
@@ -552,12 +721,12 @@ void rrt_kernel(RrtArgs A)
                     if (e.fl & KF_VALID) { tg[e.j] = c2; tpar[e.j] = slot; }
                     continue;
                 }
-                const int t = atomicAdd(&S.nT, 1);
+                const int t = atomicAdd(&S.nT2, 1);
                 tset(S, tl, t, k, Gp);
             }
             __threadfence_block();
             __syncthreads();
-            const int nT2 = S.nT;
+            const int nT2 = S.nT2;
             c_tests += nT2;
             for (int t = wave; t < nT2; t += kWaves) {
                 const KRec e = kget(S, kl, tx, tg, tget_k(S, tl, t));

@@ -58,7 +58,7 @@ if os.environ.get("PMP_HIP_LIB", "").endswith("dwastamps.so"):
     raw = raw.astype(np.int64)
     raw = raw[raw[:, 0] > 0]  # parts that ran (a stopped agent's parts return before stamping)
     t0 = raw[:, 0].min()
-    names = ["start", "lookahead", "sincos", "rollout", "columns", "arrive", "sums", "scores", "end"]
+    names = ["start", "occ", "rollout+lookahead", "columns", "leafsums", "arrive", "sums", "scores", "end"]
     part = raw[:, :6] - t0
     print("all parts, mean ticks since the first start:", {n: int(part[:, i].mean()) for i, n in enumerate(names[:6])})
     last = raw[raw[:, 6] > 0] - t0
