@@ -1667,9 +1667,10 @@ def main():
     ap.add_argument("--theta-workers", type=int, default=768, help="persistent Theta* 2D workers per launch")
     ap.add_argument("--theta-engine", type=int, default=2,
                     help="Theta* 2D engine: 2 = four queries per wave (astar2d_mq.hip, round 5), 0 = one per wave")
-    ap.add_argument("--theta-residency", type=int, default=24,
-                    help="Theta* 2D workers resident per CU (as --residency; with one multi-batch launch: 256 x this "
-                         "many workers; 12 / 18 / 24 / 28 / 32: 8.5 / 11.3 / 11.9 / 11.85 / 11.75 k plans/s)")
+    ap.add_argument("--theta-residency", type=int, default=32,
+                    help="Theta* 2D queries resident per CU (as --residency; with one multi-batch launch: 256 x this "
+                         "many groups; multi-query engine, round 5: 24 / 32 / 40 -> Theta* 10.8 / 13.6 / 9.7 k, Lazy "
+                         "9.9 / 12.3 / 12.6 k plans/s)")
     ap.add_argument("--residency", type=int, default=0,
                     help="A* queries resident per CU over all batches in flight (sets each one's LDS heap share; "
                          "0 = the engine's default)")

@@ -186,9 +186,12 @@ constexpr int kEntLds = kKeys ? 16 : 12;  // LDS bytes per heap position
 // levels; the block of a node Q at the level above a band holds Q's two children and four
 // grandchildren (6 x 16 B in one 128-B line), so a path and its siblings touch one line per two
 // spilled levels instead of one per level (round 4, same-box A/B: 15.5 k -> 16.6-17.1 k plans/s,
-// FETCH -18 %, WRITE -14 %).  PMP_MQ_BLOCKS=0: position order, sibling pairs 32-B aligned.
+// FETCH -18 %, WRITE -14 %).  Round 5 default (PMP_MQ_BLOCKS=2): each child with its own two
+// children in one 64-B half of the block, so a rotation's two stores per band dirty one half
+// (write-back sectors) instead of both -- WRITE -7 % at the same plans/s (profiles/r5/attribution.txt);
+// 1: the round-4 order [c0 c1 g00 g01 g10 g11]; 0: position order, sibling pairs 32-B aligned.
 #ifndef PMP_MQ_BLOCKS
-#define PMP_MQ_BLOCKS 1
+#define PMP_MQ_BLOCKS 2
 #endif
 constexpr bool kBlocks = PMP_MQ_BLOCKS != 0;
 constexpr bool kBlocks2 = PMP_MQ_BLOCKS == 2;

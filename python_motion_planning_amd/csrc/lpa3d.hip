@@ -223,19 +223,22 @@ struct L3 {
     template <bool SP>
     __device__ __forceinline__ void remove_at_t(int i)
     {
-        for (int base = i; base < U.n - 1; base += 256) {
+        // the loads of a round are unconditional (clamped to the last element) so they issue back to
+        // back with one wait; only the stores are masked
+        const int last = U.n - 1;
+        for (int base = i; base < last; base += 256) {
             int32_t c[4];
             double a[4], b[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int k = base + lane + 64 * j;
-                if (k < U.n - 1) U.template ld<SP>(k + 1, c[j], a[j], b[j]);
+                U.template ld<SP>(k < last ? k + 1 : last, c[j], a[j], b[j]);
             }
             wsync();
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int k = base + lane + 64 * j;
-                if (k < U.n - 1) U.template st<SP>(k, c[j], a[j], b[j]);
+                if (k < last) U.template st<SP>(k, c[j], a[j], b[j]);
             }
             wsync();
         }
@@ -404,9 +407,11 @@ struct L3 {
             const int k = base + lane;
             int32_t c = -1;
             double a, b;
-            if (k < U.n) {
-                if (usp) U.template ld<true>(k, c, a, b);
-                else U.template ld<false>(k, c, a, b);
+            {
+                const int kk = k < U.n ? k : U.n - 1;  // an unconditional load, the result masked
+                if (usp) U.template ld<true>(kk, c, a, b);
+                else U.template ld<false>(kk, c, a, b);
+                if (k >= U.n) c = -1;
             }
             // block index of c relative to the centre, or -1
             int bi = -1;
@@ -642,12 +647,15 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
                 double b1 = kInf, b2 = kInf;
                 int bi = 0x7fffffff;
                 const bool usp = S.U.n > S.U.cap;
-                for (int k = lane; k < S.U.n; k += 64) {
-                    int32_t c;
-                    double a1, a2;
-                    if (usp) S.U.template ld<true>(k, c, a1, a2);
-                    else S.U.template ld<false>(k, c, a1, a2);
-                    if (bi == 0x7fffffff || key_lt(a1, a2, b1, b2)) { b1 = a1; b2 = a2; bi = k; }
+                // two entries per lane per round, loads unconditional (clamped) and issued together
+                for (int k0 = lane; k0 < S.U.n; k0 += 128) {
+                    int32_t c, c2;
+                    double a1, a2, e1, e2;
+                    const int kb = k0 + 64 < S.U.n ? k0 + 64 : S.U.n - 1;
+                    if (usp) { S.U.template ld<true>(k0, c, a1, a2); S.U.template ld<true>(kb, c2, e1, e2); }
+                    else { S.U.template ld<false>(k0, c, a1, a2); S.U.template ld<false>(kb, c2, e1, e2); }
+                    if (bi == 0x7fffffff || key_lt(a1, a2, b1, b2)) { b1 = a1; b2 = a2; bi = k0; }
+                    if (k0 + 64 < S.U.n && key_lt(e1, e2, b1, b2)) { b1 = e1; b2 = e2; bi = k0 + 64; }
                 }
                 for (int o = 1; o < 64; o <<= 1) {
                     const double o1 = __shfl_xor(b1, o, 64), o2 = __shfl_xor(b2, o, 64);
