@@ -318,6 +318,9 @@ def with_mfma(roof: dict, kernel: str) -> dict:
 _STREAM_POOL = []
 
 
+_SHARED_CTX = []  # the headline's context kept for the Theta* legs (--theta-share-ctx)
+
+
 def pool_stream(torch, i):
     """Stream i of one pool shared by every leg.  HIP maps each new stream to the next of its
     GPU_MAX_HW_QUEUES hardware queues round-robin, so streams created leg after leg eventually share
@@ -859,13 +862,14 @@ def graphs_leg(args, torch, dist, world, rank):
         _LABEL[0] = algo + "_2d_warmup"
         lanes = []
         for _ in range(S):
-            ctx = L.pmp_create(torch.cuda.current_device())
+            shared = not lanes and bool(_SHARED_CTX)
+            ctx = _SHARED_CTX[0] if shared else L.pmp_create(torch.cuda.current_device())
             _lib.check(ctx, L.pmp_astar2d_set_engine(ctx, args.theta_engine, 1 if args.theta_engine == 2 else 0),
                        "engine")
             _lib.check(ctx, L.pmp_astar2d_reserve(ctx, 1024, 1024, tw, 0), "reserve")
             if args.theta_residency:
                 _lib.check(ctx, L.pmp_astar2d_set_residency(ctx, args.theta_residency), "residency")
-            lanes.append(dict(ctx=ctx, stream=pool_stream(torch, len(lanes)),
+            lanes.append(dict(ctx=ctx, shared=shared, stream=pool_stream(torch, len(lanes)),
                               cost=torch.empty(B * nq, dtype=torch.float64, device="cuda"),
                               plen=torch.empty(B * nq, dtype=torch.int32, device="cuda"),
                               path=torch.empty((B * nq, 8192), dtype=torch.int32, device="cuda"),
@@ -919,7 +923,8 @@ def graphs_leg(args, torch, dist, world, rank):
             outs += [{k: b[k][j * nq:(j + 1) * nq] for k in gkeys} for j in range(last_nb)]
         checked = check_timed(algo, ref_out, outs)
         for b in lanes:  # their scratch (about 40 GB each with the Theta* parents) is not needed later
-            L.pmp_destroy(b["ctx"])
+            if not b["shared"]:
+                L.pmp_destroy(b["ctx"])
         lanes.clear()
         alg = astar_algorithmic_bytes(c) * float(np.mean(nbs))
         achieved = alg / (kern_ms * 1e-3) / 1e9
@@ -948,6 +953,8 @@ def graphs_leg(args, torch, dist, world, rank):
                                      "theta2d_kernel" if algo == "theta_star" else "lazy_theta2d_kernel", f"{algo}_2d_x{B}"),
             "detail": {"expansions_per_batch": int(c[:, 2].sum()), "pushes_per_batch": int(c[:, 0].sum())},
             "cpu_baseline": cpu}
+    while _SHARED_CTX:
+        L.pmp_destroy(_SHARED_CTX.pop())
 
     occ = wl.readme_grid()
     free = np.argwhere(occ == 0)
@@ -1083,7 +1090,7 @@ def dstar_leg(args, torch, dist, world, rank):
             ctx = L.pmp_create(torch.cuda.current_device())
             _lib.check(ctx, L.pmp_set_workers_per_cu(ctx, args.dstar_workers_per_cu), "workers")
             _lib.check(ctx, L.pmp_set_resident_per_cu(ctx, args.dstar_residency), "residency")
-            lanes.append(dict(ctx=ctx, stream=pool_stream(torch, len(lanes)),
+            lanes.append(dict(ctx=ctx, shared=shared, stream=pool_stream(torch, len(lanes)),
                               cost=torch.empty(B * nq, dtype=torch.float64, device="cuda"),
                               plen=torch.empty(B * nq, dtype=torch.int32, device="cuda"),
                               path=torch.empty((B * nq, 4 * W), dtype=torch.int32, device="cuda"),
@@ -1667,6 +1674,11 @@ def main():
     ap.add_argument("--theta-workers", type=int, default=768, help="persistent Theta* 2D workers per launch")
     ap.add_argument("--theta-engine", type=int, default=2,
                     help="Theta* 2D engine: 2 = four queries per wave (astar2d_mq.hip, round 5), 0 = one per wave")
+    ap.add_argument("--theta-share-ctx", type=int, default=1,
+                    help="1: the Theta* 2D legs plan on the headline's context (its scratch, as one long-lived "
+                         "planner would) instead of fresh ones; 0: fresh contexts -- their new ~100 GB of scratch, "
+                         "allocated right after the headline's is freed, ran Theta* 1.85x slower on every box tried "
+                         "(7.2 s vs 3.9 s per 12-batch launch, tools/r5_call15.sh)")
     ap.add_argument("--theta-residency", type=int, default=32,
                     help="Theta* 2D queries resident per CU (as --residency; with one multi-batch launch: 256 x this "
                          "many groups; multi-query engine, round 5: 24 / 32 / 40 -> Theta* 10.8 / 13.6 / 9.7 k, Lazy "
@@ -1918,11 +1930,16 @@ def main():
         args.scaling == "strong" and dist is not None) else counters
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
 
-    # the headline's scratch (about 30 GB per batch in flight) is not needed by the other legs
+    # the headline's scratch (about 30 GB per batch in flight) is not needed by the other legs, except
+    # with --theta-share-ctx: the Theta* legs then plan on the headline's context (its grow-only
+    # scratch already holds their per-slot state, so they allocate only the CLOSED-parent array)
     torch.cuda.synchronize()
     cost = ref_out["cost"].cpu()
-    for b in lanes:
-        L.pmp_destroy(b["ctx"])
+    for i, b in enumerate(lanes):
+        if i == 0 and args.theta_share_ctx and "graphs" in args.legs.split(","):
+            _SHARED_CTX.append(b["ctx"])
+        else:
+            L.pmp_destroy(b["ctx"])
     lanes.clear()
 
     cpu = None
