@@ -1090,7 +1090,7 @@ def dstar_leg(args, torch, dist, world, rank):
             ctx = L.pmp_create(torch.cuda.current_device())
             _lib.check(ctx, L.pmp_set_workers_per_cu(ctx, args.dstar_workers_per_cu), "workers")
             _lib.check(ctx, L.pmp_set_resident_per_cu(ctx, args.dstar_residency), "residency")
-            lanes.append(dict(ctx=ctx, shared=shared, stream=pool_stream(torch, len(lanes)),
+            lanes.append(dict(ctx=ctx, stream=pool_stream(torch, len(lanes)),
                               cost=torch.empty(B * nq, dtype=torch.float64, device="cuda"),
                               plen=torch.empty(B * nq, dtype=torch.int32, device="cuda"),
                               path=torch.empty((B * nq, 4 * W), dtype=torch.int32, device="cuda"),
@@ -1674,6 +1674,8 @@ def main():
     ap.add_argument("--theta-workers", type=int, default=768, help="persistent Theta* 2D workers per launch")
     ap.add_argument("--theta-engine", type=int, default=2,
                     help="Theta* 2D engine: 2 = four queries per wave (astar2d_mq.hip, round 5), 0 = one per wave")
+    ap.add_argument("--keep-headline-ctx", type=int, default=0,
+                    help="dev A/B: keep the headline's context (and its scratch) until exit")
     ap.add_argument("--theta-share-ctx", type=int, default=1,
                     help="1: the Theta* 2D legs plan on the headline's context (its scratch, as one long-lived "
                          "planner would) instead of fresh ones; 0: fresh contexts -- their new ~100 GB of scratch, "
@@ -1936,7 +1938,7 @@ def main():
     torch.cuda.synchronize()
     cost = ref_out["cost"].cpu()
     for i, b in enumerate(lanes):
-        if i == 0 and args.theta_share_ctx and "graphs" in args.legs.split(","):
+        if i == 0 and ((args.theta_share_ctx and "graphs" in args.legs.split(",")) or args.keep_headline_ctx):
             _SHARED_CTX.append(b["ctx"])
         else:
             L.pmp_destroy(b["ctx"])
