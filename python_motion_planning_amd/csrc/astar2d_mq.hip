@@ -204,6 +204,11 @@ constexpr bool kBlocks2 = PMP_MQ_BLOCKS == 2;
 #ifndef PMP_MQ_MIRROR
 #define PMP_MQ_MIRROR 0
 #endif
+// path_op's level shift: ds_bpermute from the group's direction (1, default: +0.8 % plans/s on the
+// VALU-bound step, three alternating rounds in tools/r5_call18.sh) or both DPP row shifts (0)
+#ifndef PMP_MQ_BPERM
+#define PMP_MQ_BPERM 1
+#endif
 constexpr int kMirror = PMP_MQ_MIRROR;
 
 // byte offset of spilled heap position p (>= cap) in the wave's spill region
@@ -499,12 +504,30 @@ __device__ __forceinline__ int path_op(const GHeap& h, bool on, bool pop, uint32
     const int b = pop ? cnt : Kd - cnt;
     // new contents: a pop shifts levels 1..b up one (lane L takes lane L+1's), a push shifts levels
     // b..Kd-1 down one (lane L takes lane L-1's); X at level b
+    const bool atb = gl == b, shift = pop ? gl < b : (gl > b && lvl);
+#if PMP_MQ_BPERM
+    // one ds_bpermute per word from lane L +- 1 (the group's own direction) instead of both DPP
+    // shifts and a select: the kernel is VALU-issue-bound, the permutes run on the LDS pipe.  A
+    // shifting lane's source stays in its row (a pop shifts levels < b <= 14, a push levels > b >= 0)
+    {
+        const int sa = ((int)__lane_id() + (pop ? 1 : -1)) << 2;
+        const uint64_t vb = (uint64_t)__double_as_longlong(Vf);
+        const uint32_t flo = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)(uint32_t)vb);
+        const uint32_t fhi = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)(uint32_t)(vb >> 32));
+        const uint32_t shc = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)Vc);
+        const uint32_t shk = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)Vk);
+        const double shf = __longlong_as_double(((uint64_t)fhi << 32) | flo);
+        nf = atb ? Xf : (shift ? shf : Vf);
+        nc = atb ? Xc : (shift ? shc : Vc);
+        nk = atb ? Xk : (shift ? shk : Vk);
+    }
+#else
     const double upf = shl1f(Vf), dnf = shr1f(Vf);
     const uint32_t upc = shl1(Vc), upk = shl1(Vk), dnc = shr1(Vc), dnk = shr1(Vk);
-    const bool atb = gl == b, shift = pop ? gl < b : (gl > b && lvl);
     nf = atb ? Xf : (shift ? (pop ? upf : dnf) : Vf);
     nc = atb ? Xc : (shift ? (pop ? upc : dnc) : Vc);
     nk = atb ? Xk : (shift ? (pop ? upk : dnk) : Vk);
+#endif
     if (kLaneConst) hst_off(h, on && (pop ? gl <= b : (gl >= b && lvl)), q, offq, nf, nc, nk, pop ? 4 : 2);
     else hst(h, on && (pop ? gl <= b : (gl >= b && lvl)), q, nf, nc, nk, pop ? 4 : 2);
     // the bits of the changed levels' parents: lane L (>= 1) sets its parent's from its new content
