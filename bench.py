@@ -1681,10 +1681,11 @@ def main():
                          "planner would) instead of fresh ones; 0: fresh contexts -- their new ~100 GB of scratch, "
                          "allocated right after the headline's is freed, ran Theta* 1.85x slower on every box tried "
                          "(7.2 s vs 3.9 s per 12-batch launch, tools/r5_call15.sh)")
-    ap.add_argument("--theta-residency", type=int, default=32,
+    ap.add_argument("--theta-residency", type=int, default=48,
                     help="Theta* 2D queries resident per CU (as --residency; with one multi-batch launch: 256 x this "
-                         "many groups; multi-query engine, round 5: 24 / 32 / 40 -> Theta* 10.8 / 13.6 / 9.7 k, Lazy "
-                         "9.9 / 12.3 / 12.6 k plans/s)")
+                         "many groups; multi-query engine on the headline's context, round 5: 24 / 32 / 40 / 48 -> "
+                         "Theta* 10.7 / 13.4 / 14.5 / 18.0 k, Lazy 9.8 / 12.2 / 13.1 / 16.2 k plans/s; 48 = 12 waves "
+                         "per CU, the Theta* build's 3 per SIMD)")
     ap.add_argument("--residency", type=int, default=0,
                     help="A* queries resident per CU over all batches in flight (sets each one's LDS heap share; "
                          "0 = the engine's default)")

@@ -563,7 +563,10 @@ __device__ __forceinline__ int path_op(const GHeap& h, bool on, bool pop, uint32
 template <int HEUR, bool GZERO, bool T2LDS, int THETA = 0>
 // <= 128 VGPRs: four waves per SIMD, up to 64 queries resident per CU (Theta*: three, the line-of-sight
 // state would spill at 128)
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 4))) void astar2d_mqu_kernel(
+#ifndef PMP_MQ_THETA_WPE
+#define PMP_MQ_THETA_WPE 3  // Theta* variants: 3 waves per SIMD (no scratch); 4 spills 20-60 B
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? PMP_MQ_THETA_WPE : 4))) void astar2d_mqu_kernel(
     const uint32_t* __restrict__ occ, int W, int H, const int32_t* __restrict__ start_xy,
     const int32_t* __restrict__ goal_xy, const int32_t* __restrict__ order, int nq, double* __restrict__ cost_out,
     int32_t* __restrict__ path_len_out, uint32_t* __restrict__ path_out, int path_cap,

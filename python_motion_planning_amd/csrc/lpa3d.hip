@@ -28,6 +28,14 @@
 namespace {
 
 constexpr int kMaxDim = 256;
+// Write-traffic attribution (dev builds, tools/build_variant.sh): every store of the selected
+// categories is issued twice, the copy into a mirror of the worker's arrays, so the extra WRITE_SIZE
+// over the plain build is that category's traffic.  Bits: 1 U's spilled positions (shifts, pushes),
+// 2 the g / rhs values, 4 the written-this-query bits (ORs and the per-query clear).
+#ifndef PMP_L3_MIRROR
+#define PMP_L3_MIRROR 0
+#endif
+constexpr int kL3Mirror = PMP_L3_MIRROR;
 constexpr double kInf = __builtin_huge_val();
 
 __device__ __constant__ int8_t c_m[26][3] = {
@@ -131,6 +139,9 @@ struct UList {
     int32_t* gc;
     double* g1;
     double* g2;
+    int32_t* mgc;  // kL3Mirror & 1: the mirror of the spilled part
+    double* mg1;
+    double* mg2;
     int cap;
     int n;
     // SP = false: every position touched is < cap (pure LDS code, no vector-memory waits)
@@ -158,6 +169,11 @@ struct UList {
             gc[k - cap] = c;
             g1[k - cap] = a;
             g2[k - cap] = b;
+            if (kL3Mirror & 1) {
+                mgc[k - cap] = c;
+                mg1[k - cap] = a;
+                mg2[k - cap] = b;
+            }
         }
     }
 };
@@ -183,6 +199,10 @@ struct L3 {
     // U's share spilled more lists to HBM -- +50 % writes, -9 % plans/s.)
     uint32_t* gt;
     uint32_t* rt;
+    double* mg;     // kL3Mirror & 2: mirrors of g / rhs
+    double* mrhs;
+    uint32_t* mgt;  // kL3Mirror & 4: mirrors of the bits
+    uint32_t* mrt;
     bool touch;
     lds_f64* cube;  // 125 g values of the 5x5x5 block around the centre
     int lane;
@@ -210,6 +230,8 @@ struct L3 {
     __device__ __forceinline__ void mark(uint32_t* t, int c) const
     {
         if (touch) __hip_atomic_fetch_or(t + (c >> 5), 1u << (c & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((kL3Mirror & 4) && touch)
+            __hip_atomic_fetch_or((t == gt ? mgt : mrt) + (c >> 5), 1u << (c & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
     __device__ __forceinline__ double hval(int x, int y, int z) const
@@ -462,10 +484,12 @@ struct L3 {
             const bool upd = mine && P != start && (is_nb || (lane == 26 && do_center)) && rv != rvl;
             if (upd) {
                 rhs[P] = rv;
+                if (kL3Mirror & 2) mrhs[P] = rv;
                 mark(rt, P);
             }
             if (expand && lane == 0) {
                 g[center] = gnew;
+                if (kL3Mirror & 2) mg[center] = gnew;
                 mark(gt, center);
             }
         }
@@ -479,6 +503,11 @@ struct L3 {
     }
 };
 
+__host__ __device__ inline size_t l3_mirror_bytes(size_t ncell, int words)
+{
+    return ((2 * ncell + 2 * (ncell + 1)) * 8 + (ncell + 1) * 4 + (size_t)words * 8 + 255) & ~(size_t)255;
+}
+
 __global__ __launch_bounds__(64) void lpa3d_kernel(
     const uint32_t* __restrict__ occ_all, int per_query, int X, int Y, int Z, int heur,
     const int32_t* __restrict__ start_xyz, const int32_t* __restrict__ goal_xyz, int nq,
@@ -486,7 +515,7 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
     int32_t* __restrict__ path_out, int path_cap, int64_t* __restrict__ nexp_out, int32_t* __restrict__ status_out,
     int64_t* __restrict__ counters, int64_t max_exp, int* __restrict__ queue, double* __restrict__ scr_f64,
     int32_t* __restrict__ scr_i32, uint32_t* __restrict__ occ_scr, int words, int occ_lds, int ucap,
-    const int32_t* __restrict__ order, int prio_n, uint32_t* __restrict__ bits_all)
+    const int32_t* __restrict__ order, int prio_n, uint32_t* __restrict__ bits_all, unsigned char* __restrict__ mirror)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
@@ -516,6 +545,16 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
         S.U.g1 = f + 2 * (size_t)ncell;
         S.U.g2 = S.U.g1 + spill;
         S.U.gc = scr_i32 + (size_t)blockIdx.x * spill;
+        if (kL3Mirror) {  // the mirror: g, rhs, U keys, U cells, the two bit arrays
+            double* mf = (double*)(mirror + (size_t)blockIdx.x * l3_mirror_bytes(ncell, words));
+            S.mg = mf;
+            S.mrhs = mf + ncell;
+            S.U.mg1 = mf + 2 * (size_t)ncell;
+            S.U.mg2 = S.U.mg1 + spill;
+            S.U.mgc = (int32_t*)(S.U.mg2 + spill);
+            S.mgt = (uint32_t*)(S.U.mgc + spill);
+            S.mrt = S.mgt + words;
+        }
     }
     const int R1 = nr + 1;
 
@@ -572,10 +611,15 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
                 for (int w = lane; w < words; w += 64) {
                     __hip_atomic_store(S.gt + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(S.rt + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (kL3Mirror & 4) {
+                        __hip_atomic_store(S.mgt + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(S.mrt + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
                 }
                 wsync();
                 if (lane == 0) {
                     S.rhs[S.start] = 0.0;
+                    if (kL3Mirror & 2) S.mrhs[S.start] = 0.0;
                     S.mark(S.rt, S.start);
                 }
             } else {
@@ -809,10 +853,15 @@ extern "C" int pmp_lpastar3d_batch(pmp_ctx* ctx, void* stream, const uint32_t* o
         const int rc = pmp_lpt_order3d(ctx, s, start_xyz, goal_xyz, nq, X, Y, Z, workers, &order);
         if (rc) return rc;
     }
+    unsigned char* mirror = nullptr;
+    if (kL3Mirror) {
+        mirror = (unsigned char*)pmp_scratch(ctx, SCR_MQ_PC, (size_t)workers * l3_mirror_bytes(ncell, words));
+        if (!mirror) return PMP_ENOMEM;
+    }
     hipLaunchKernelGGL(lpa3d_kernel, dim3(workers), dim3(64), lds, s, occ_bits, per_query, X, Y, Z, heuristic, start_xyz,
                        goal_xyz, nq, changes, nr, cost, path_len, path, path_cap, n_expanded, status, counters,
                        max_expansions, queue, f, i32, occw, words, occ_lds ? 1 : 0, ucap, (const int32_t*)order,
-                       order ? ctx->astar_prio_n : 0, (uint32_t*)(i32 + (size_t)workers * spill));
+                       order ? ctx->astar_prio_n : 0, (uint32_t*)(i32 + (size_t)workers * spill), mirror);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }

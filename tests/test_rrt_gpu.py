@@ -135,3 +135,33 @@ def test_c3_full_size_properties():
         assert np.all(g[1:] >= g[par[1:]] + edge[1:] - 1e-9)
         for j in rng.choice(np.arange(1, n), 200, replace=False):
             assert not O.map_collision(rects, circs, 512, 512, xy[j], xy[par[j]])
+
+
+@pytest.mark.parametrize("case", ["long_segments", "many_obstacles"])
+def test_collision_bins_edge_cases_against_oracle(case):
+    """The obstacle bins (rrt.hip, round 5) on the paths the C3 runs do not take: segments whose
+    bounding box meets more than 9 bins (max_dist 60, radius 80: the full item list instead), and a
+    map of more than 128 obstacles (no bins at all).  RRT* and RRT trees vs the oracle."""
+    import python_motion_planning_amd as pmp
+    from oracle import oracle as O
+    from python_motion_planning_amd import batch, workloads as wl
+
+    if case == "long_segments":
+        rects, circs = wl.c3_map()
+        kw = dict(max_dist=60.0, radius=80.0)
+        sn = 600
+    else:
+        rects, circs = wl.c3_map(n_rect=80, n_circ=60, seed=11)
+        kw = {}
+        sn = 1500
+    env = pmp.Map(512, 512)
+    env.update(obs_rect=rects, obs_circ=circs)
+    nq = 16
+    rnd = np.stack([np.random.RandomState(500 + q).random_sample(3 * sn + 1) for q in range(nq)])
+    starts, goals = np.tile([5.0, 5.0], (nq, 1)), np.tile([505.0, 505.0], (nq, 1))
+    for star in (True, False):
+        out = batch.rrt_batch(env, starts, goals, rnd, sn, star=star, **kw)
+        ref = O.rrt_batch(star, rects, circs, 512, 512, starts, goals, rnd, sn, **kw)
+        for q in range(nq):
+            _check_tree(out, q, ref["tree"][q, : ref["n_nodes"][q]], (case, star, q))
+            assert int(out["status"][q]) == ref["status"][q]
