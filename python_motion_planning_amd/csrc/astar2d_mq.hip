@@ -387,28 +387,6 @@ __device__ __forceinline__ void bit_set(const GHeap& h, bool on, int level, uint
         else __hip_atomic_fetch_and(w, ~m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
-// bit_set at a level fixed per lane (a path operation's lane L writes level L - 1), tiers all in LDS:
-// the level's constants packed once per lane (lane_bc) -- r = level - 5 t, and the word index
-// (R >> s1) + c1 / the byte shift (R & mk) * 8 of the tier -- instead of rederived every step.
-#ifndef PMP_MQ_BITCONST
-#define PMP_MQ_BITCONST 0
-#endif
-__device__ __forceinline__ uint32_t lane_bc(int level)
-{
-    if (level < 0) return 0u;
-    const int t = level / 5, r = level - 5 * t;
-    const uint32_t s1 = t == 2 ? 2u : 0u, mk = t == 2 ? 3u : 0u;
-    const int c1 = t == 0 ? -1 : (t == 1 ? -31 : -220);  // t 0: R = 1 -> word 0; 1: R - 31; 2: 36 + (R - 1024) / 4
-    return (uint32_t)r | (s1 << 3) | (mk << 5) | ((uint32_t)(c1 + 1024) << 8);
-}
-__device__ __forceinline__ void bit_set_bc(const GHeap& h, bool on, uint32_t bc, uint32_t Pl, bool bit)
-{
-    const uint32_t r = bc & 7u, mr = (1u << r) - 1u;
-    const uint32_t R = Pl >> r;
-    const uint32_t widx = (uint32_t)((int)(R >> ((bc >> 3) & 3u)) + (int)(bc >> 8) - 1024);
-    const uint32_t m = (1u << ((Pl & mr) + mr)) << ((R & ((bc >> 5) & 3u)) << 3);
-    if (on) ds_mskor(h.B + widx, m, bit ? m : 0u);
-}
 // CPython _siftup's choice bit of the parent of `child` (a position) whose new content is v and
 // whose sibling holds s: bit = !(left < right), odd positions are left children
 __device__ __forceinline__ bool choice_bit_k(int child, double vf, uint32_t vk, double sf, uint32_t sk)
@@ -467,8 +445,7 @@ __device__ __forceinline__ void pop_leaf(const GHeap& h, const Walk& wk, int n, 
 template <bool T2LDS, int HEUR>
 __device__ __forceinline__ int path_op(const GHeap& h, bool on, bool pop, uint32_t Q, int Kd, int n, double Xf, uint32_t Xc,
                                        uint32_t Xk, int gl, int gb, double& lastf, uint32_t& lastc, uint32_t& lastk,
-                                       double& rootf, uint32_t& rootc, double& nf, uint32_t& nc, uint32_t& nk, uint32_t cwL,
-                                       uint32_t bcL)
+                                       double& rootf, uint32_t& rootc, double& nf, uint32_t& nc, uint32_t& nk, uint32_t cwL)
 {
     const bool lvl = gl <= Kd;
     const int q = lvl ? (int)(Q >> (Kd - gl)) - 1 : 0;
@@ -535,8 +512,7 @@ __device__ __forceinline__ int path_op(const GHeap& h, bool on, bool pop, uint32
     {
         const bool upd = hass && (pop ? gl <= b : gl >= b);
         const bool bit = choice_bit_k(q, nf, nk, Sf, Sk);
-        if (T2LDS && PMP_MQ_BITCONST) bit_set_bc(h, upd, bcL, Q >> (Kd - gl + 1), bit);
-        else bit_set<T2LDS>(h, upd, gl - 1, Q >> (Kd - gl + 1), bit);
+        bit_set<T2LDS>(h, upd, gl - 1, Q >> (Kd - gl + 1), bit);
     }
     {
         // selects, not a branch (every lane computes them): root = level 0's new content; the last
@@ -563,10 +539,9 @@ __device__ __forceinline__ int path_op(const GHeap& h, bool on, bool pop, uint32
 template <int HEUR, bool GZERO, bool T2LDS, int THETA = 0>
 // <= 128 VGPRs: four waves per SIMD, up to 64 queries resident per CU (Theta*: three, the line-of-sight
 // state would spill at 128)
-#ifndef PMP_MQ_THETA_WPE
-#define PMP_MQ_THETA_WPE 3  // Theta* variants: 3 waves per SIMD (no scratch); 4 spills 20-60 B
-#endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? PMP_MQ_THETA_WPE : 4))) void astar2d_mqu_kernel(
+// Theta* variants: 3 waves per SIMD (no scratch; a 128-VGPR build spills 20-60 B and was no faster,
+// profiles/r5/theta_residency.txt)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 4))) void astar2d_mqu_kernel(
     const uint32_t* __restrict__ occ, int W, int H, const int32_t* __restrict__ start_xy,
     const int32_t* __restrict__ goal_xy, const int32_t* __restrict__ order, int nq, double* __restrict__ cost_out,
     int32_t* __restrict__ path_len_out, uint32_t* __restrict__ path_out, int path_cap,
@@ -614,7 +589,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? PMP_
     Walk wk;
     wk.init(gl);
     const uint32_t cwL = kLaneConst ? lane_cw(hp.L0, gl) : 0u;  // spill-offset word of heap level gl
-    const uint32_t bcL = (T2LDS && PMP_MQ_BITCONST) ? lane_bc(gl - 1) : 0u;  // bit_set word of level gl - 1
     // a spilled position p's offset from its level's word (lane gb + level of p)
     auto soff = [&](int p, bool on) -> uint32_t {
         if (!kLaneConst) return (on && p >= hp.cap) ? spill_off(hp, p) : kOOR;
@@ -832,7 +806,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? PMP_
         uint32_t nc = 0u, nk = 0u;
         int b = 0;
         b = path_op<T2LDS, HEUR>(hp, op, pop, Q, Kd, n, Xf, Xc, Xk, gl, gb, lastf, lastc, lastk, rootf, rootc, nf, nc,
-                                 nk, cwL, bcL);
+                                 nk, cwL);
         {
             double f8;
             uint32_t c8, k8;

@@ -23,13 +23,9 @@
 
 namespace {
 
-#ifndef PMP_RRT_NT
-#define PMP_RRT_NT 512  // threads per query (dev builds: 256)
-#endif
-#ifndef PMP_RRT_WPE
-#define PMP_RRT_WPE 0  // amdgpu_waves_per_eu cap (0: none; dev builds)
-#endif
-constexpr int kNT = PMP_RRT_NT;
+// threads per query (round 5: 256 threads at 2 / 3 workgroups per CU and a 128-VGPR build at 2 per CU
+// were slower, profiles/r5/rrt_phases.txt)
+constexpr int kNT = 512;
 constexpr int kWaves = kNT / 64;
 constexpr int kMaxObs = 256;   // per obstacle kind
 constexpr int kMaxBnd = 8;
@@ -353,11 +349,7 @@ __device__ __forceinline__ double aget_c(const RrtShared& S, const AEntry* al, i
 typedef __attribute__((address_space(3))) uint32_t lds_xyq;
 
 template <bool STAR>
-__global__ __launch_bounds__(kNT)
-#if PMP_RRT_WPE
-__attribute__((amdgpu_waves_per_eu(PMP_RRT_WPE)))
-#endif
-void rrt_kernel(RrtArgs A)
+__global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
 {
     __shared__ RrtShared S;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_dyn[];
