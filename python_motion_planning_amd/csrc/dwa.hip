@@ -1,7 +1,10 @@
-// Batched DWA control step for gfx950 (local_planner/dwa.py:72-212): one 768-thread workgroup
-// (12 waves) per agent, one lane per (v, w) sample (the 4096 samples in passes over the threads),
-// H-step rollout, obstacle cost from an occupancy stencil,
-// numpy-exact normalisation and scoring, first-index argmax, Robot.kinematic.
+// Batched DWA control step for gfx950 (local_planner/dwa.py:72-212): one lane per (v, w) sample,
+// H-step rollout, obstacle cost from an occupancy stencil, numpy-exact normalisation and scoring,
+// first-index argmax, Robot.kinematic.  Three launch shapes (pmp_dwa_step_batch):
+//  - fixed windows (nv, nw > 0), fewer agents than CUs: dwa_split_kernel, k workgroups per agent;
+//  - fixed windows otherwise: the same kernel at k = 1 (LOCAL), one 1024-thread workgroup per agent;
+//  - resolution-sized windows (the drop-in DWA.plan): dwa_kernel, 768 threads, every plan iteration
+//    in one launch.
 //
 // Numerics follow the reference operation by operation (-ffp-contract=off):
 //  - Robot.lookforward (agent.py:91-116): x' = x + (dt*cos th)*v, y' = y + (dt*sin th)*v,
@@ -53,6 +56,7 @@ __device__ inline double linsp_at(const Linsp& L, int i)
 
 typedef __attribute__((address_space(3))) uint32_t lds_w32;
 constexpr int kOccLdsWords = 4096;  // grids up to 131072 cells keep their occupancy in LDS (16 KiB)
+constexpr int kNibWords = 4096;     // SCHEME 3's nibble map: (W + 1) (H + 1) cells of 4 bits, <= 32768 cells
 
 // The occupancy bits of cells (i, j0 .. j0 + n - 1) of one grid row (x-major: consecutive j are
 // consecutive bits), n <= 32, all inside the grid: bit b of the result = cell (i, j0 + b).
@@ -101,6 +105,7 @@ __device__ inline int pw_half(int n)
 
 struct DwaShared {
     uint32_t occ[kOccLdsWords];      // the occupancy bitmap (when it fits)
+    uint32_t nib[kNibWords];         // SCHEME 3's nibble map
     double col[3][kMaxN];            // heading, obstacle, velocity per sample
     double leafsum[3][kMaxLeaves];
     int leaf_lo[kMaxLeaves], leaf_n[kMaxLeaves];
@@ -192,7 +197,150 @@ __device__ inline void rollout(const uint32_t* __restrict__ occ, const lds_w32* 
     mind2o = mind2;
 }
 
-template <bool OCC_LDS>
+// ---- small inflation radii (R < 2, the reference's default R = 1), occupancy in LDS -----------------
+// The stencil [ceil(x - R), floor(x + R)] x [ceil(y - R), floor(y + R)] is then at most 3 x 3 cells:
+// up to three columns (two unless x is within rounding of an integer), one run of <= 3 bits each (two
+// words only when the run crosses one).  Two schemes:
+//  - SCHEME 1 (R < 2): all six words in one LDS round (clamped addresses, masked results) instead of
+//    one dependent round trip per column; the cells, and so the minimum, are rollout()'s.
+//  - SCHEME 3 (R <= 1): any cell closer than R <= 1 to (x, y) is one of the four cells (fx + {0, 1},
+//    fy + {0, 1}), fx, fy = floor(x, y), since |cx - x| < 1.  Cells of the box at distance >= R leave
+//    min(sqrt(min d2), R) = R unchanged (dwa.py:164 caps at R), so this superset of the stencil's cells
+//    gives the same obstacle term bit for bit.  A nibble map (four occupancy bits per (fx, fy), built in
+//    LDS per launch) gives the four cells in one LDS read.
+#ifndef PMP_DWA_ROLL_SPLIT
+#define PMP_DWA_ROLL_SPLIT 3  // k-split parts
+#endif
+#ifndef PMP_DWA_ROLL_LOCAL
+#define PMP_DWA_ROLL_LOCAL 3  // one 1024-thread workgroup per agent
+#endif
+#ifndef PMP_DWA_ROLL_PLAN
+#define PMP_DWA_ROLL_PLAN 3  // dwa_kernel (resolution-sized windows, DWA.plan)
+#endif
+
+struct SmallStencil {
+    const lds_w32* occ;
+    const lds_w32* nib;  // SCHEME 3: nibble of (fx, fy) at index (fx + 1) (H + 1) + fy + 1, fx >= -1, fy >= -1
+    int words;           // occupancy words (the last readable one: words - 1)
+    int ox, oy, W, H;
+    double R;
+};
+
+template <int SCHEME>
+__device__ inline void stencil3(const SmallStencil& T, double x, double y, double& mind2)
+{
+    if constexpr (SCHEME == 3) {
+        // outside fx in [-1, W - 1], fy in [-1, H - 1] none of the four cells is in the grid (compared
+        // in doubles: no int overflow far away)
+        const double fxd = floor(x) - (double)T.ox, fyd = floor(y) - (double)T.oy;
+        if (!(fxd >= -1.0 && fxd < (double)T.W && fyd >= -1.0 && fyd < (double)T.H)) return;
+        const int fx = (int)fxd, fy = (int)fyd;
+        const uint32_t q = (uint32_t)((fx + 1) * (T.H + 1) + fy + 1);
+        uint32_t nb = (T.nib[q >> 3] >> ((q & 7u) * 4u)) & 15u;
+        while (nb) {
+            const int b = __ffs(nb) - 1;
+            nb &= nb - 1;
+            const double dx = (double)(T.ox + fx + (b & 1)) - x, dy = (double)(T.oy + fy + (b >> 1)) - y;
+            const double d2 = dx * dx + dy * dy;
+            if (d2 < mind2) mind2 = d2;
+        }
+        return;
+    }
+    const int x0 = (int)ceil(x - T.R), x1 = (int)floor(x + T.R);
+    const int y0 = (int)ceil(y - T.R), y1 = (int)floor(y + T.R);
+    const int j0 = max(y0 - T.oy, 0), j1 = min(y1 - T.oy, T.H - 1);
+    if (j0 > j1) return;
+    const int nrun = j1 - j0 + 1;
+    const uint32_t mask = (1u << nrun) - 1u;
+    uint32_t run[3];
+    if constexpr (SCHEME == 1) {
+#pragma unroll
+        for (int u = 0; u < 3; u++) {
+            const int i = x0 + u - T.ox;
+            const uint32_t ok = (uint32_t)(x0 + u <= x1) & (uint32_t)((unsigned)i < (unsigned)T.W);
+            const uint32_t k = (uint32_t)min(max(i, 0), T.W - 1) * (uint32_t)T.H + (uint32_t)j0;
+            const uint32_t w = k >> 5, w1 = min(w + 1u, (uint32_t)T.words - 1u);
+            const uint64_t pair = ((uint64_t)T.occ[w1] << 32) | (uint64_t)T.occ[w];
+            run[u] = (uint32_t)(pair >> (k & 31u)) & (mask & (0u - ok));
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 3; u++) {
+        uint32_t r = run[u];
+        while (r) {
+            const int b = __ffs(r) - 1;
+            r &= r - 1;
+            const double dx = (double)(x0 + u) - x, dy = (double)(T.oy + j0 + b) - y;
+            const double d2 = dx * dx + dy * dy;
+            if (d2 < mind2) mind2 = d2;
+        }
+    }
+}
+
+// rollout() for R < 2: the same trajectory recurrence and cells
+template <int SCHEME>
+__device__ inline void rollout_small(const SmallStencil& T, double dt, int Hh, double x, double y, double sn,
+                                     double cs, double sd, double cd, double v, double& xo, double& yo,
+                                     double& mind2o)
+{
+    double mind2 = INFINITY;
+    for (int k = 0; k < Hh; k++) {
+        const double nx = x + (dt * cs) * v, ny = y + (dt * sn) * v;
+        const double ncs = cs * cd - sn * sd, nsn = sn * cd + cs * sd;
+        cs = ncs;
+        sn = nsn;
+        x = nx;
+        y = ny;
+        stencil3<SCHEME>(T, x, y, mind2);
+    }
+    xo = x;
+    yo = y;
+    mind2o = mind2;
+}
+
+__device__ inline SmallStencil small_stencil(const lds_w32* occl, const lds_w32* nib, int ox, int oy, int W, int H,
+                                             double R)
+{
+    SmallStencil T;
+    T.occ = occl;
+    T.nib = nib;
+    T.words = (int)(((size_t)W * H + 31) / 32);
+    T.ox = ox;
+    T.oy = oy;
+    T.W = W;
+    T.H = H;
+    T.R = R;
+    return T;
+}
+
+// SCHEME 3's nibble map from the occupancy in LDS (all threads; the caller barriers before and after)
+__device__ inline void build_nib(const SmallStencil& T, lds_w32* nib, int tid, int nt)
+{
+    const int Hn = T.H + 1, ncell = (T.W + 1) * Hn;
+    auto bit = [&](int i, int j) -> uint32_t {
+        return ((unsigned)i < (unsigned)T.W && (unsigned)j < (unsigned)T.H) ? occ_at(T.occ, 0, 0, T.W, T.H, i, j) : 0u;
+    };
+    for (int w = tid; w < (ncell + 7) / 8; w += nt) {
+        uint32_t v = 0;
+        for (int e = 0; e < 8; e++) {
+            const int q = 8 * w + e;
+            if (q >= ncell) break;
+            const int fx = q / Hn - 1, fy = q % Hn - 1;
+            v |= (bit(fx, fy) | bit(fx + 1, fy) << 1 | bit(fx, fy + 1) << 2 | bit(fx + 1, fy + 1) << 3) << (4 * e);
+        }
+        nib[w] = v;
+    }
+}
+
+// the host's choice of stencil scheme for a kernel built with `want` (0: rollout())
+int small_scheme(int want, int W, int H, double R, bool occ_lds)
+{
+    if (want == 0 || !occ_lds || !(R >= 0.0) || (long)W * H <= 0) return 0;
+    if (want == 3 && R <= 1.0 && ((long)(W + 1) * (H + 1) + 7) / 8 <= (long)kNibWords) return 3;
+    return R < 2.0 ? 1 : 0;
+}
+
+template <bool OCC_LDS, int SCHEME>
 __global__ __launch_bounds__(kThreads) void dwa_kernel(
     const uint32_t* __restrict__ occ, int ox, int oy, int W, int H, pmp_lp_params P, pmp_dwa_params D, int na,
     double* __restrict__ state, const double* __restrict__ goal, const double* __restrict__ path_xy,
@@ -211,6 +359,11 @@ __global__ __launch_bounds__(kThreads) void dwa_kernel(
         __syncthreads();
     }
     const lds_w32* occl = (const lds_w32*)S.occ;
+    const SmallStencil T = small_stencil(occl, (const lds_w32*)S.nib, ox, oy, W, H, D.inflation);
+    if constexpr (OCC_LDS && SCHEME == 3) {
+        build_nib(T, (lds_w32*)S.nib, tid, kThreads);
+        __syncthreads();
+    }
     const double* path = path_xy + 2 * (size_t)path_off[a];
     const int Pn = path_off[a + 1] - path_off[a];
     const double gl[3] = {goal[3 * a], goal[3 * a + 1], goal[3 * a + 2]};
@@ -253,8 +406,12 @@ __global__ __launch_bounds__(kThreads) void dwa_kernel(
         const double sn0 = S.sn0, cs0 = S.cs0;
         for (int c = tid; c < N; c += kThreads) {
             double x, y, mind2;
-            rollout<OCC_LDS>(occ, occl, ox, oy, W, H, R, dt, Hh, st[0], st[1], sn0, cs0, S.col[1][c], S.col[2][c],
-                             linsp_at(LV, c / nw), x, y, mind2);
+            if constexpr (OCC_LDS && SCHEME == 3)
+                rollout_small<3>(T, dt, Hh, st[0], st[1], sn0, cs0, S.col[1][c], S.col[2][c], linsp_at(LV, c / nw), x, y,
+                                 mind2);
+            else
+                rollout<OCC_LDS>(occ, occl, ox, oy, W, H, R, dt, Hh, st[0], st[1], sn0, cs0, S.col[1][c], S.col[2][c],
+                                 linsp_at(LV, c / nw), x, y, mind2);
             S.col[0][c] = x;
             S.col[1][c] = mind2;
             S.col[2][c] = y;
@@ -356,19 +513,27 @@ __global__ __launch_bounds__(kThreads) void dwa_kernel(
 constexpr int kSplitRoll = 512;                 // rollout threads (waves 0..7), one sample each
 constexpr int kSplitThreads = kSplitRoll + 64;  // + the control wave: lookahead and leaf table beside them
 constexpr int kSplitChunk = 1024;  // samples of one part held in LDS
+// k = 1 (LOCAL): one 1024-thread workgroup per agent (16 waves, 4 per SIMD at <= 128 VGPRs), all N
+// samples' columns in LDS, no hand-off; the last wave computes the lookahead before its rollouts
+constexpr int kLocalThreads = 1024;
+#ifndef PMP_DWA_LOCAL
+#define PMP_DWA_LOCAL 1  // 0: fixed windows at k = 1 on dwa_kernel (A/B builds)
+#endif
 
 // part p's samples [c[p], c[p + 1]): the host's restatement of the tree's leaves (split_bounds)
 struct DwaSplitBounds {
     int c[65];
 };
 
+template <int CHUNK, int NT>
 struct DwaSplitShared {
     uint32_t occ[kOccLdsWords];
-    double col[3][kSplitChunk];
+    uint32_t nib[kNibWords];
+    double col[3][CHUNK];
     double lsum[3][kMaxLeaves];  // the last part: every part's leaf sums, staged for the combine
     int leaf_lo[kMaxLeaves], leaf_n[kMaxLeaves];
-    double redd[kSplitThreads / 64];
-    int redi[kSplitThreads / 64];
+    double redd[NT / 64];
+    int redi[NT / 64];
     double sums[3];
     double pt[2];
     int raises;
@@ -409,8 +574,11 @@ struct DwaSplitScratch {
 #else
 #define DSTAMP(i) do {} while (0)
 #endif
-template <bool OCC_LDS>
-__global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
+template <bool LOCAL>
+using PartShared = DwaSplitShared<LOCAL ? kMaxN : kSplitChunk, LOCAL ? kLocalThreads : kSplitThreads>;
+
+template <bool OCC_LDS, int SCHEME, bool LOCAL>
+__global__ __launch_bounds__(LOCAL ? kLocalThreads : kSplitThreads) void dwa_split_kernel(
     const uint32_t* __restrict__ occ, int ox, int oy, int W, int H, pmp_lp_params P, pmp_dwa_params D, int na, int k,
     int it, int iters, double* __restrict__ state, const double* __restrict__ goal, const double* __restrict__ path_xy,
     const int32_t* __restrict__ path_off, double* __restrict__ u_out, int32_t* __restrict__ best_out,
@@ -418,7 +586,7 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
     double* __restrict__ eval_out, double* __restrict__ best_traj, DwaSplitScratch X, DwaSplitBounds B)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    DwaSplitShared& S = *reinterpret_cast<DwaSplitShared*>(smem_raw);
+    PartShared<LOCAL>& S = *reinterpret_cast<PartShared<LOCAL>*>(smem_raw);
     const int a = blockIdx.x / k, part = blockIdx.x - a * k;
     const int tid = threadIdx.x, nt = blockDim.x;
     if (a >= na) return;
@@ -447,6 +615,8 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
         for (int i = tid; i < words; i += nt) S.occ[i] = occ[i];
     }
     const lds_w32* occl = (const lds_w32*)S.occ;
+    const SmallStencil T = small_stencil(occl, (const lds_w32*)S.nib, ox, oy, W, H, D.inflation);
+    constexpr bool small = OCC_LDS && SCHEME > 0;
     const double dt = P.dt;
     const int Hh = (int)(D.predict_time / dt);
     const double R = D.inflation;
@@ -457,26 +627,33 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
     const Linsp LV = make_linsp(vr0, vr1, nv), LW = make_linsp(vr2, vr3, nw);
     const int c0 = B.c[part], c1 = B.c[part + 1];
     __syncthreads();  // the occupancy in LDS
+    if constexpr (small && SCHEME == 3) {
+        build_nib(T, (lds_w32*)S.nib, tid, nt);
+        __syncthreads();
+    }
     DSTAMP(1);
-    if (tid < kSplitRoll) {
-        // the rollouts (dwa.py:152-160) and their stencil minima, one sample per thread; they need only
-        // the state, so the control wave's lookahead runs beside them
+    // the rollouts (dwa.py:152-160) and their stencil minima, one sample per thread per round; they
+    // need only the state, so the control wave's lookahead runs beside them
+    auto rollouts = [&](int stride) {
         double sn0, cs0;
         sincos(st[2], &sn0, &cs0);
-        for (int c = c0 + tid; c < c1; c += kSplitRoll) {
+        for (int c = c0 + tid; c < c1; c += stride) {
             double sd, cd, x, y, mind2;
             sincos(dt * linsp_at(LW, c % nw), &sd, &cd);
-            rollout<OCC_LDS>(occ, occl, ox, oy, W, H, R, dt, Hh, st[0], st[1], sn0, cs0, sd, cd, linsp_at(LV, c / nw), x,
-                             y, mind2);
+            if constexpr (small)
+                rollout_small<SCHEME>(T, dt, Hh, st[0], st[1], sn0, cs0, sd, cd, linsp_at(LV, c / nw), x, y, mind2);
+            else
+                rollout<OCC_LDS>(occ, occl, ox, oy, W, H, R, dt, Hh, st[0], st[1], sn0, cs0, sd, cd,
+                                 linsp_at(LV, c / nw), x, y, mind2);
             S.col[0][c - c0] = x;
             S.col[1][c - c0] = mind2;
             S.col[2][c - c0] = y;
         }
-    } else {
-        // the control wave: getLookaheadPoint (local_planner.py:103-170, lp::lookahead_block's steps)
-        // with wave-level first-index reductions, its serial tail on lane 0 and the pairwise tree's
-        // leaf table on lane 1
-        const int ln = tid - kSplitRoll;
+    };
+    // the control wave: getLookaheadPoint (local_planner.py:103-170, lp::lookahead_block's steps) with
+    // wave-level first-index reductions, its serial tail on lane 0 and the pairwise tree's leaf table on
+    // lane 1
+    auto control = [&](int ln) {
         const double rx = st[0], ry = st[1];
         const double L = lp::lookahead_dist(st[3], P);
         const double* path = path_xy + 2 * (size_t)po;
@@ -509,6 +686,14 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
             pw_leaves<kPwDepth>(0, N, S.leaf_lo, S.leaf_n, nl);
             S.nleaves = nl;
         }
+    };
+    if constexpr (LOCAL) {
+        // all 16 waves roll out (N / 1024 rounds each); the last one computes the lookahead first
+        if (tid >= nt - 64) control(tid - (nt - 64));
+        rollouts(nt);
+    } else {
+        if (tid < kSplitRoll) rollouts(kSplitRoll);
+        else control(tid - kSplitRoll);
     }
     __syncthreads();
     DSTAMP(2);
@@ -530,9 +715,11 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
         S.col[0][c - c0] = h;
         S.col[1][c - c0] = o;
         S.col[2][c - c0] = vel;
-        st_wt(cols + c, h);
-        st_wt(cols + kMaxN + c, o);
-        st_wt(cols + 2 * kMaxN + c, vel);
+        if constexpr (!LOCAL) {
+            st_wt(cols + c, h);
+            st_wt(cols + kMaxN + c, o);
+            st_wt(cols + 2 * kMaxN + c, vel);
+        }
     }
     DSTAMP(3);
     __syncthreads();
@@ -540,24 +727,28 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
         const int ml = l1 - l0;
         if (tid < 3 * ml) {
             const int cidx = tid / ml, l = l0 + tid % ml;
-            st_wt(lsum + cidx * kMaxLeaves + l, pw_leaf(&S.col[cidx][S.leaf_lo[l] - c0], S.leaf_n[l]));
+            const double ls = pw_leaf(&S.col[cidx][S.leaf_lo[l] - c0], S.leaf_n[l]);
+            if constexpr (LOCAL) S.lsum[cidx][l] = ls;
+            else st_wt(lsum + cidx * kMaxLeaves + l, ls);
         }
     }
     DSTAMP(4);
-    // arrival: every wave drains its write-through stores, then one lane counts the part in; the
-    // last part acquires (drops its CU's stale lines) before reading the others' columns
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        const int old = __hip_atomic_fetch_add(X.cnt + a, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        S.last = old == k - 1;
+    if constexpr (!LOCAL) {
+        // arrival: every wave drains its write-through stores, then one lane counts the part in; the
+        // last part reads the others' columns and leaf sums with agent-scope loads
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            const int old = __hip_atomic_fetch_add(X.cnt + a, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            S.last = old == k - 1;
+        }
+        __syncthreads();
+        DSTAMP(5);
+        if (!S.last) return;
+        if (tid == 0) __hip_atomic_store(X.cnt + a, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the leaf sums into LDS in one round (all threads), then the tree's combine from LDS
+        for (int i = tid; i < 3 * nl; i += nt) S.lsum[i / nl][i % nl] = ld_coh(lsum + (i / nl) * kMaxLeaves + i % nl);
     }
-    __syncthreads();
-    DSTAMP(5);
-    if (!S.last) return;
-    if (tid == 0) __hip_atomic_store(X.cnt + a, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // the leaf sums into LDS in one round (all threads), then the tree's combine from LDS
-    for (int i = tid; i < 3 * nl; i += nt) S.lsum[i / nl][i % nl] = ld_coh(lsum + (i / nl) * kMaxLeaves + i % nl);
     __syncthreads();
     if (tid < 3) {
         int leaf = 0;
@@ -569,17 +760,24 @@ __global__ __launch_bounds__(kSplitThreads) void dwa_split_kernel(
     double bs = -INFINITY;
     int bi = 0x7fffffff;
     // the other parts' columns come from L2 / HBM: a thread's loads issue together (8 samples x 3
-    // columns in flight), then the scores, in increasing c (the first index wins a tie)
-    constexpr int kU = 8;
+    // columns in flight), then the scores, in increasing c (the first index wins a tie); LOCAL reads
+    // its own columns from LDS
+    constexpr int kU = LOCAL ? 1 : 8;
     for (int c0 = tid; c0 < N; c0 += kU * nt) {
         double hv[kU], ov[kU], vv[kU];
 #pragma unroll
         for (int u = 0; u < kU; u++) {
             const int c = c0 + u * nt;
             const int cc = c < N ? c : 0;
-            hv[u] = ld_coh(cols + cc);
-            ov[u] = ld_coh(cols + kMaxN + cc);
-            vv[u] = ld_coh(cols + 2 * kMaxN + cc);
+            if constexpr (LOCAL) {
+                hv[u] = S.col[0][cc];
+                ov[u] = S.col[1][cc];
+                vv[u] = S.col[2][cc];
+            } else {
+                hv[u] = ld_coh(cols + cc);
+                ov[u] = ld_coh(cols + kMaxN + cc);
+                vv[u] = ld_coh(cols + 2 * kMaxN + cc);
+            }
         }
 #pragma unroll
         for (int u = 0; u < kU; u++) {
@@ -712,10 +910,13 @@ extern "C" int pmp_dwa_step_batch(pmp_ctx* ctx, void* stream, const uint32_t* oc
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_dwa_step_batch: nv*nw must be <= 4096 and dt > 0");
     PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     const bool occ_lds = ((size_t)W * H + 31) / 32 <= (size_t)kOccLdsWords;
+    const int scheme_split = small_scheme(PMP_DWA_ROLL_SPLIT, W, H, dp->inflation, occ_lds);
+    const int scheme_local = small_scheme(PMP_DWA_ROLL_LOCAL, W, H, dp->inflation, occ_lds);
     // parts per agent: auto (dwa_split 0) = the CUs over the agents, at most 16; 1 = one workgroup per
     // agent.  Only windows of fixed size (nv, nw > 0) split, into leaf-aligned parts of <= kSplitChunk.
     int k = 1;
-    if (dp->nv > 0 && dp->nw > 0 && dp->nv * dp->nw > 1) {
+    const bool fixed = dp->nv > 0 && dp->nw > 0;
+    if (fixed && dp->nv * dp->nw > 1) {
         if (ctx->dwa_split > 0) {
             k = ctx->dwa_split;
         } else {
@@ -745,15 +946,37 @@ extern "C" int pmp_dwa_step_batch(pmp_ctx* ctx, void* stream, const uint32_t* oc
         }
         DwaSplitBounds Bd;
         split_bounds(dp->nv * dp->nw, k, Bd.c);
-        auto sk = occ_lds ? dwa_split_kernel<true> : dwa_split_kernel<false>;
+        auto sk = scheme_split == 3 ? dwa_split_kernel<true, 3, false>
+                  : scheme_split == 1 ? dwa_split_kernel<true, 1, false>
+                  : occ_lds           ? dwa_split_kernel<true, 0, false>
+                                      : dwa_split_kernel<false, 0, false>;
         for (int it = 0; it < iters; it++)
-            hipLaunchKernelGGL(sk, dim3((unsigned)(na * k)), dim3(kSplitThreads), sizeof(DwaSplitShared), (hipStream_t)stream,
-                               occ_bits, ox, oy, W, H, *lp, *dp, na, k, it, iters, state, goal, path_xy, path_off, u, best,
+            hipLaunchKernelGGL(sk, dim3((unsigned)(na * k)), dim3(kSplitThreads), sizeof(PartShared<false>),
+                               (hipStream_t)stream, occ_bits, ox, oy, W, H, *lp, *dp, na, k, it, iters, state, goal,
+                               path_xy, path_off, u, best, status, n_steps, hist_pose, eval, best_traj, X, Bd);
+        PMP_HIP_CHECK(ctx, hipGetLastError());
+        return PMP_OK;
+    }
+    if (PMP_DWA_LOCAL && fixed) {
+        // one workgroup per agent, one launch per plan iteration (the k-split kernel at k = 1: no scratch,
+        // no hand-off)
+        DwaSplitScratch X = {nullptr, nullptr, nullptr};
+        DwaSplitBounds Bd;
+        Bd.c[0] = 0;
+        Bd.c[1] = dp->nv * dp->nw;
+        auto lk = scheme_local == 3 ? dwa_split_kernel<true, 3, true>
+                  : scheme_local == 1 ? dwa_split_kernel<true, 1, true>
+                  : occ_lds           ? dwa_split_kernel<true, 0, true>
+                                      : dwa_split_kernel<false, 0, true>;
+        for (int it = 0; it < iters; it++)
+            hipLaunchKernelGGL(lk, dim3((unsigned)na), dim3(kLocalThreads), sizeof(PartShared<true>), (hipStream_t)stream,
+                               occ_bits, ox, oy, W, H, *lp, *dp, na, 1, it, iters, state, goal, path_xy, path_off, u, best,
                                status, n_steps, hist_pose, eval, best_traj, X, Bd);
         PMP_HIP_CHECK(ctx, hipGetLastError());
         return PMP_OK;
     }
-    auto kern = occ_lds ? dwa_kernel<true> : dwa_kernel<false>;
+    const int scheme_plan = small_scheme(PMP_DWA_ROLL_PLAN, W, H, dp->inflation, occ_lds) == 3 ? 3 : 0;
+    auto kern = scheme_plan == 3 ? dwa_kernel<true, 3> : occ_lds ? dwa_kernel<true, 0> : dwa_kernel<false, 0>;
     hipLaunchKernelGGL(kern, dim3(na), dim3(kThreads), sizeof(DwaShared), (hipStream_t)stream, occ_bits, ox, oy, W,
                        H, *lp, *dp, na, state, goal, path_xy, path_off, iters, u, best, status, n_steps, hist_pose, eval,
                        best_traj);

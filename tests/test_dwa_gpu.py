@@ -223,3 +223,48 @@ def test_split_parts_bit_equal(nv):
             continue
         for k in ref:
             assert np.array_equal(got[k], ref[k]), (parts, k)
+
+
+@pytest.mark.parametrize("inflation", [0.0, 0.5, 1.0, 1.5, 1.999])
+def test_small_radius_dense_obstacles_against_oracle(inflation):
+    """Radii below 2 take the 3 x 3 stencil behind the dilated-occupancy skip (dwa.hip rollout_small):
+    a grid with extra random obstacles (most trajectory points near one, several cells per stencil),
+    every agent against the oracle (dwa.py:162-164 over the obstacle list), one workgroup and the
+    k-split kernel both."""
+    import torch
+
+    from oracle import oracle as O
+    from python_motion_planning_amd import _lib, batch, workloads as wl
+
+    occ, states, goals = wl.c4_workload(48, seed=7)
+    rng = np.random.default_rng(11)
+    occ = occ.copy()
+    occ |= rng.random(occ.shape) < 0.12
+    keep = [i for i in range(48)]
+    for i in keep:
+        occ[int(states[i, 0]), int(states[i, 1])] = False
+    occ[45, 25] = False
+    r = batch.astar2d_batch(occ, states[:, :2].astype(np.int32), np.tile([45, 25], (48, 1)).astype(np.int32),
+                            path_cap=2048)
+    pl, P = r["path_len"].cpu().numpy(), r["path"].cpu().numpy()
+    keep = [i for i in range(48) if pl[i] > 1][:24]
+    assert len(keep) >= 12
+    H = occ.shape[1]
+    paths = [np.column_stack([P[i, : pl[i]][::-1] // H, P[i, : pl[i]][::-1] % H]).astype(np.float64) for i in keep]
+    states, goals = states[keep], goals[keep]
+    xy, off = batch.pack_paths(paths)
+    lp = _lib.LPParams.from_params(_pmp().LocalPlanner.DEFAULTS)
+    dp = _lib.DWAParams(0.2, 0.1, 0.05, 3.0, inflation, 0.05, 0.05, 32, 32)
+    grid = batch.obstacle_grid({(int(a), int(b)) for a, b in np.argwhere(occ)})
+    obs = np.argwhere(occ).astype(np.float64)
+    for parts in (1, 4):
+        st_d = torch.tensor(states, dtype=torch.float64, device="cuda")
+        out = batch.dwa_step_batch(grid, lp, dp, st_d, goals, xy, off, iters=1, parts=parts)
+        status, new_st, u = out["status"].cpu().numpy(), st_d.cpu().numpy(), out["u"].cpu().numpy()
+        for i in range(len(keep)):
+            rc, ost, ou = O.dwa_step(obs, paths[i], goals[i], states[i], nv=32, nw=32, predict_time=3.0,
+                                     inflation=inflation)
+            assert rc == status[i], (parts, i)
+            if rc == 0:
+                np.testing.assert_allclose(new_st[i], ost, rtol=1e-12, atol=1e-14)
+                np.testing.assert_allclose(u[i], ou, rtol=1e-12, atol=1e-14)
