@@ -79,22 +79,29 @@ __device__ inline bool occ_at(PTR occ, int ox, int oy, int W, int H, int cx, int
     return (occ[k >> 5] >> (k & 31)) & 1u;
 }
 
-// numpy pairwise-sum leaf (n <= 128)
-__device__ inline double pw_leaf(const double* a, int n)
+// numpy's pairwise-sum leaf (n <= 128: eight accumulators r[j] over a[j], a[j + 8], ..., combined as
+// ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), then the tail; n < 8: a plain running sum) on
+// eight lanes (an aligned 8-lane group, all lanes with the same a and n): lane j keeps
+// accumulator r[j] (a[j], a[j + 8], ... in order: consecutive lanes read consecutive words, no LDS bank
+// conflicts), the groups' shuffles combine ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) in that
+// order, lane 0 adds the tail; the result is valid in lane j = 0
+__device__ inline double pw_leaf8(const double* a, int n, int j)
 {
     if (n < 8) {
         double res = 0.0;
-        for (int i = 0; i < n; i++) res += a[i];
+        if (j == 0)
+            for (int i = 0; i < n; i++) res += a[i];
         return res;
     }
-    double r[8];
-    for (int j = 0; j < 8; j++) r[j] = a[j];
-    int i;
-    for (i = 8; i < n - (n % 8); i += 8)
-        for (int j = 0; j < 8; j++) r[j] += a[i + j];
-    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (; i < n; i++) res += a[i];
-    return res;
+    const int n8 = n - n % 8;
+    double r = a[j];
+    for (int i = 8; i < n8; i += 8) r += a[i + j];
+    r = r + __shfl_down(r, 1, 8);  // even j: r[j] + r[j + 1]
+    r = r + __shfl_down(r, 2, 8);  // j = 0, 4: (r[j] + r[j + 1]) + (r[j + 2] + r[j + 3])
+    r = r + __shfl_down(r, 4, 8);  // j = 0: the two halves
+    if (j == 0)
+        for (int i = n8; i < n; i++) r += a[i];
+    return r;
 }
 
 __device__ inline int pw_half(int n)
@@ -226,24 +233,44 @@ struct SmallStencil {
     double R;
 };
 
+// SCHEME 3: the four cells' occupancy bits at (x, y) -- (fx, fy) clamped into the map and the bits
+// masked when outside fx in [-1, W - 1], fy in [-1, H - 1] (none of the four cells is in the grid;
+// compared in doubles, no int overflow far away), so the read issues without a branch
+struct Nib {
+    uint32_t bits;
+    int fx, fy;
+};
+
+__device__ inline Nib nib_lookup(const SmallStencil& T, double x, double y)
+{
+    const double fxd = floor(x) - (double)T.ox, fyd = floor(y) - (double)T.oy;
+    const uint32_t in = (uint32_t)(fxd >= -1.0) & (uint32_t)(fxd < (double)T.W) & (uint32_t)(fyd >= -1.0) &
+                        (uint32_t)(fyd < (double)T.H);
+    Nib n;
+    n.fx = (int)fmin(fmax(fxd, -1.0), (double)(T.W - 1));
+    n.fy = (int)fmin(fmax(fyd, -1.0), (double)(T.H - 1));
+    const uint32_t q = (uint32_t)((n.fx + 1) * (T.H + 1) + n.fy + 1);
+    n.bits = (T.nib[q >> 3] >> ((q & 7u) * 4u)) & (15u & (0u - in));
+    return n;
+}
+
+__device__ inline void nib_min(const SmallStencil& T, Nib n, double x, double y, double& mind2)
+{
+    uint32_t nb = n.bits;
+    while (nb) {
+        const int b = __ffs(nb) - 1;
+        nb &= nb - 1;
+        const double dx = (double)(T.ox + n.fx + (b & 1)) - x, dy = (double)(T.oy + n.fy + (b >> 1)) - y;
+        const double d2 = dx * dx + dy * dy;
+        if (d2 < mind2) mind2 = d2;
+    }
+}
+
 template <int SCHEME>
 __device__ inline void stencil3(const SmallStencil& T, double x, double y, double& mind2)
 {
     if constexpr (SCHEME == 3) {
-        // outside fx in [-1, W - 1], fy in [-1, H - 1] none of the four cells is in the grid (compared
-        // in doubles: no int overflow far away)
-        const double fxd = floor(x) - (double)T.ox, fyd = floor(y) - (double)T.oy;
-        if (!(fxd >= -1.0 && fxd < (double)T.W && fyd >= -1.0 && fyd < (double)T.H)) return;
-        const int fx = (int)fxd, fy = (int)fyd;
-        const uint32_t q = (uint32_t)((fx + 1) * (T.H + 1) + fy + 1);
-        uint32_t nb = (T.nib[q >> 3] >> ((q & 7u) * 4u)) & 15u;
-        while (nb) {
-            const int b = __ffs(nb) - 1;
-            nb &= nb - 1;
-            const double dx = (double)(T.ox + fx + (b & 1)) - x, dy = (double)(T.oy + fy + (b >> 1)) - y;
-            const double d2 = dx * dx + dy * dy;
-            if (d2 < mind2) mind2 = d2;
-        }
+        nib_min(T, nib_lookup(T, x, y), x, y, mind2);
         return;
     }
     const int x0 = (int)ceil(x - T.R), x1 = (int)floor(x + T.R);
@@ -278,19 +305,42 @@ __device__ inline void stencil3(const SmallStencil& T, double x, double y, doubl
 }
 
 // rollout() for R < 2: the same trajectory recurrence and cells
-template <int SCHEME>
+#ifndef PMP_DWA_PAIR
+#define PMP_DWA_PAIR 1
+#endif
+#ifndef PMP_DWA_COLPAIR
+#define PMP_DWA_COLPAIR 1
+#endif
+template <int SCHEME, bool PAIR = PMP_DWA_PAIR>
 __device__ inline void rollout_small(const SmallStencil& T, double dt, int Hh, double x, double y, double sn,
                                      double cs, double sd, double cd, double v, double& xo, double& yo,
                                      double& mind2o)
 {
     double mind2 = INFINITY;
-    for (int k = 0; k < Hh; k++) {
+    auto advance = [&]() {
         const double nx = x + (dt * cs) * v, ny = y + (dt * sn) * v;
         const double ncs = cs * cd - sn * sd, nsn = sn * cd + cs * sd;
         cs = ncs;
         sn = nsn;
         x = nx;
         y = ny;
+    };
+    int k = 0;
+    if constexpr (SCHEME == 3 && PAIR) {
+        // two steps per round: both lookups' LDS reads in flight together, one branch for the (rare) hits
+        for (; k + 1 < Hh; k += 2) {
+            advance();
+            const double xa = x, ya = y;
+            advance();
+            const Nib na = nib_lookup(T, xa, ya), nb = nib_lookup(T, x, y);
+            if (na.bits | nb.bits) {
+                nib_min(T, na, xa, ya, mind2);
+                nib_min(T, nb, x, y, mind2);
+            }
+        }
+    }
+    for (; k < Hh; k++) {
+        advance();
         stencil3<SCHEME>(T, x, y, mind2);
     }
     xo = x;
@@ -320,8 +370,24 @@ __device__ inline void build_nib(const SmallStencil& T, lds_w32* nib, int tid, i
     auto bit = [&](int i, int j) -> uint32_t {
         return ((unsigned)i < (unsigned)T.W && (unsigned)j < (unsigned)T.H) ? occ_at(T.occ, 0, 0, T.W, T.H, i, j) : 0u;
     };
+    // rows j0 .. j0 + 8 of column i as bits 0 .. 8 (cells outside the grid: 0)
+    auto col9 = [&](int i, int j0) -> uint32_t {
+        if ((unsigned)i >= (unsigned)T.W) return 0u;
+        const int lo = max(j0, 0), hi = min(j0 + 9, T.H);
+        return hi > lo ? occ_run(T.occ, T.H, i, lo, hi - lo) << (lo - j0) : 0u;
+    };
     for (int w = tid; w < (ncell + 7) / 8; w += nt) {
         uint32_t v = 0;
+        const int q0 = 8 * w, fx = q0 / Hn - 1, fy = q0 % Hn - 1;
+        if (q0 % Hn + 8 <= Hn && q0 + 8 <= ncell) {
+            // the word's eight cells share fx: two column runs give all their bits
+            const uint32_t A = col9(fx, fy), Bc = col9(fx + 1, fy);
+            for (int e = 0; e < 8; e++)
+                v |= (((A >> e) & 1u) | ((Bc >> e) & 1u) << 1 | ((A >> (e + 1)) & 1u) << 2 | ((Bc >> (e + 1)) & 1u) << 3)
+                     << (4 * e);
+            nib[w] = v;
+            continue;
+        }
         for (int e = 0; e < 8; e++) {
             const int q = 8 * w + e;
             if (q >= ncell) break;
@@ -407,8 +473,8 @@ __global__ __launch_bounds__(kThreads) void dwa_kernel(
         for (int c = tid; c < N; c += kThreads) {
             double x, y, mind2;
             if constexpr (OCC_LDS && SCHEME == 3)
-                rollout_small<3>(T, dt, Hh, st[0], st[1], sn0, cs0, S.col[1][c], S.col[2][c], linsp_at(LV, c / nw), x, y,
-                                 mind2);
+                rollout_small<3, false>(T, dt, Hh, st[0], st[1], sn0, cs0, S.col[1][c], S.col[2][c], linsp_at(LV, c / nw),
+                                        x, y, mind2);  // (the paired form spills at this kernel's 168 VGPRs)
             else
                 rollout<OCC_LDS>(occ, occl, ox, oy, W, H, R, dt, Hh, st[0], st[1], sn0, cs0, S.col[1][c], S.col[2][c],
                                  linsp_at(LV, c / nw), x, y, mind2);
@@ -434,9 +500,10 @@ __global__ __launch_bounds__(kThreads) void dwa_kernel(
         }
         __syncthreads();
         const int nl = S.nleaves;
-        if (tid < 3 * nl) {
-            const int cidx = tid / nl, l = tid % nl;
-            S.leafsum[cidx][l] = pw_leaf(&S.col[cidx][S.leaf_lo[l]], S.leaf_n[l]);
+        for (int g = tid >> 3; g < 3 * nl; g += kThreads >> 3) {  // one 8-lane group per (column, leaf)
+            const int cidx = g / nl, l = g % nl;
+            const double ls = pw_leaf8(&S.col[cidx][S.leaf_lo[l]], S.leaf_n[l], tid & 7);
+            if ((tid & 7) == 0) S.leafsum[cidx][l] = ls;
         }
         __syncthreads();
         if (tid < 3) {
@@ -703,15 +770,15 @@ __global__ __launch_bounds__(LOCAL ? kLocalThreads : kSplitThreads) void dwa_spl
     const int l0 = (int)(((long)nl * part) / k), l1 = (int)(((long)nl * (part + 1)) / k);
     double* cols = X.cols + (size_t)a * 3 * kMaxN;
     double* lsum = X.leafsum + (size_t)a * 3 * kMaxLeaves;
-    for (int c = c0 + tid; c < c1; c += nt) {
-        const double v = linsp_at(LV, c / nw), w = linsp_at(LW, c % nw);
-        double th = st[2];
-        for (int q = 0; q < Hh; q++) th = th + dt * w;
+    // the heading / obstacle / velocity columns (dwa.py:166-174), two samples per thread per round: th
+    // after Hh steps is a chain of Hh dependent additions (th + dt*w, the rollout's order), two chains
+    // interleave
+    auto column = [&](int c, double th) {
         const double ang = atan2(gy - S.col[2][c - c0], gx - S.col[0][c - c0]);
         const double h = lp::kPi - fabs(ang - th);
         const double mind = sqrt(S.col[1][c - c0]);
         const double o = mind < R ? mind : R;
-        const double vel = fabs(v);
+        const double vel = fabs(linsp_at(LV, c / nw));
         S.col[0][c - c0] = h;
         S.col[1][c - c0] = o;
         S.col[2][c - c0] = vel;
@@ -720,16 +787,30 @@ __global__ __launch_bounds__(LOCAL ? kLocalThreads : kSplitThreads) void dwa_spl
             st_wt(cols + kMaxN + c, o);
             st_wt(cols + 2 * kMaxN + c, vel);
         }
+    };
+    for (int c = c0 + tid; c < c1; c += (1 + PMP_DWA_COLPAIR) * nt) {
+        const int c2 = PMP_DWA_COLPAIR && c + nt < c1 ? c + nt : c;
+        const double w = linsp_at(LW, c % nw), w2 = linsp_at(LW, c2 % nw);
+        double th = st[2], th2 = st[2];
+        for (int q = 0; q < Hh; q++) {
+            th = th + dt * w;
+            th2 = th2 + dt * w2;
+        }
+        column(c, th);
+        if (PMP_DWA_COLPAIR && c + nt < c1) column(c2, th2);
     }
     DSTAMP(3);
     __syncthreads();
     {
+        // one 8-lane group per (column, leaf); groups are wave-aligned and their loop bounds uniform
         const int ml = l1 - l0;
-        if (tid < 3 * ml) {
-            const int cidx = tid / ml, l = l0 + tid % ml;
-            const double ls = pw_leaf(&S.col[cidx][S.leaf_lo[l] - c0], S.leaf_n[l]);
-            if constexpr (LOCAL) S.lsum[cidx][l] = ls;
-            else st_wt(lsum + cidx * kMaxLeaves + l, ls);
+        for (int g = tid >> 3; g < 3 * ml; g += nt >> 3) {
+            const int cidx = g / ml, l = l0 + g % ml;
+            const double ls = pw_leaf8(&S.col[cidx][S.leaf_lo[l] - c0], S.leaf_n[l], tid & 7);
+            if ((tid & 7) == 0) {
+                if constexpr (LOCAL) S.lsum[cidx][l] = ls;
+                else st_wt(lsum + cidx * kMaxLeaves + l, ls);
+            }
         }
     }
     DSTAMP(4);

@@ -66,3 +66,20 @@ if os.environ.get("PMP_HIP_LIB", "").endswith("dwastamps.so"):
     print("per-phase mean ticks, last parts:", np.diff(raw[raw[:, 6] > 0][:, :9], axis=1).mean(axis=0).round().tolist())
     print("last parts, mean ticks since the first start:", {n: int(last[:, i].mean()) for i, n in enumerate(names)})
     print("last part end, max ticks:", int(last[:, 8].max()))
+
+if os.environ.get("PMP_HIP_LIB", "").endswith("dwastamps.so"):
+    # phase stamps of one 256-agent step on the one-workgroup (LOCAL, k = 1) kernel
+    na = 256
+    xy, off = batch.pack_paths(paths[:na])
+    st = torch.tensor(states[:na], dtype=torch.float64, device="cuda")
+    for rep in range(3):
+        st.copy_(torch.tensor(states[:na], dtype=torch.float64, device="cuda"))
+        o = batch.dwa_step_batch(grid, lp, dp, st, goals[:na], xy, off, iters=1, want_traj=True, parts=1)
+        torch.cuda.synchronize()
+    raw = o["best_traj"].reshape(-1).cpu().numpy().view(np.uint64)[: na * 10].reshape(na, 10).astype(np.int64)
+    raw = raw[raw[:, 8] > 0]
+    names = ["occ+nib", "rollout+lookahead", "columns", "leafsums", "sums", "scores", "end"]
+    cols = [0, 1, 2, 3, 4, 6, 7, 8]
+    d = np.diff(raw[:, cols], axis=1).mean(axis=0).round().astype(int).tolist()
+    print("LOCAL 256 agents, per-phase mean ticks:", dict(zip(names, d)), "total", int((raw[:, 8] - raw[:, 0]).mean()),
+          "span", int(raw[:, 8].max() - raw[:, 0].min()))
