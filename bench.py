@@ -190,7 +190,7 @@ def control_leg(args, torch, dist, world, rank):
                                       "frac": achieved_tf / 78.6, "traffic": None,
                                       "flops_per_agent_step": flops_per_step,
                                       "flops_note": "SURVEY.md 8(d) stencil formulation, sin/cos/atan2 not counted"},
-                                     "dwa_kernel", "mpc_sampled_dwa"),
+                                     "dwa_split_kernel", "mpc_sampled_dwa"),
             "cpu_baseline": cpu}
 
 
@@ -214,7 +214,7 @@ ENTRY_KERNEL = {  # C-ABI entry -> (short name of the kernel it launches, as too
     "pmp_dstarlite2d_batch": lambda a: "lpa_kernel",
     "pmp_lpastar2d_replan_batch": lambda a: "lpa_kernel",
     "pmp_dstarlite2d_replan_batch": lambda a: "lpa_kernel",
-    "pmp_dwa_step_batch": lambda a: "dwa_kernel",
+    "pmp_dwa_step_batch": lambda a: _dwa_kernels(a),
     "pmp_rrt_batch": lambda a: "rrt_kernel",
     "pmp_totp3d_batch": lambda a: "totp3d_kernel",
     # MPC: per plan iteration a step and a solve dispatch, then a last step (track.hip)
@@ -223,6 +223,15 @@ ENTRY_KERNEL = {  # C-ABI entry -> (short name of the kernel it launches, as too
     "pmp_lqr_control_batch": lambda a: "lqr_control_kernel",
     "pmp_mpc_control_batch": lambda a: "mpc_control_kernel",
 }
+
+
+def _dwa_kernels(a):
+    """pmp_dwa_step_batch's dispatches (dwa.hip): fixed windows (nv, nw > 0) launch dwa_split_kernel once
+    per plan iteration (k parts, or k = 1); resolution-sized windows one dwa_kernel for all iterations."""
+    dp = getattr(a[8], "_obj", a[8])
+    if dp.nv > 0 and dp.nw > 0:
+        return [("dwa_split_kernel", int(a[14]))]
+    return "dwa_kernel"
 
 
 def count_launches(L):

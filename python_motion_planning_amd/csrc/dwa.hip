@@ -234,22 +234,32 @@ struct SmallStencil {
 };
 
 // SCHEME 3: the four cells' occupancy bits at (x, y) -- (fx, fy) clamped into the map and the bits
-// masked when outside fx in [-1, W - 1], fy in [-1, H - 1] (none of the four cells is in the grid;
-// compared in doubles, no int overflow far away), so the read issues without a branch
+// masked when outside fx in [-1, W - 1], fy in [-1, H - 1] (none of the four cells is in the grid), so
+// the read issues without a branch
 struct Nib {
     uint32_t bits;
     int fx, fy;
 };
 
+// v_cvt_i32_f64 saturates out-of-range values (and gives 0 for NaN): the range test runs on integers
+__device__ inline int cvt_sat_i32(double d)
+{
+    int r;
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(r) : "v"(d));
+    return r;
+}
+
 __device__ inline Nib nib_lookup(const SmallStencil& T, double x, double y)
 {
-    const double fxd = floor(x) - (double)T.ox, fyd = floor(y) - (double)T.oy;
-    const uint32_t in = (uint32_t)(fxd >= -1.0) & (uint32_t)(fxd < (double)T.W) & (uint32_t)(fyd >= -1.0) &
-                        (uint32_t)(fyd < (double)T.H);
+    // fx + 1 in [0, W], fy + 1 in [0, H] (unsigned compares; a saturated far-away coordinate fails them)
+    const uint32_t ux = (uint32_t)cvt_sat_i32(floor(x)) - (uint32_t)(T.ox - 1);
+    const uint32_t uy = (uint32_t)cvt_sat_i32(floor(y)) - (uint32_t)(T.oy - 1);
+    const uint32_t in = (uint32_t)(ux <= (uint32_t)T.W) & (uint32_t)(uy <= (uint32_t)T.H);
+    const uint32_t cx = in ? ux : 0u, cy = in ? uy : 0u;
     Nib n;
-    n.fx = (int)fmin(fmax(fxd, -1.0), (double)(T.W - 1));
-    n.fy = (int)fmin(fmax(fyd, -1.0), (double)(T.H - 1));
-    const uint32_t q = (uint32_t)((n.fx + 1) * (T.H + 1) + n.fy + 1);
+    n.fx = (int)cx - 1;
+    n.fy = (int)cy - 1;
+    const uint32_t q = cx * (uint32_t)(T.H + 1) + cy;
     n.bits = (T.nib[q >> 3] >> ((q & 7u) * 4u)) & (15u & (0u - in));
     return n;
 }
@@ -704,7 +714,8 @@ __global__ __launch_bounds__(LOCAL ? kLocalThreads : kSplitThreads) void dwa_spl
     auto rollouts = [&](int stride) {
         double sn0, cs0;
         sincos(st[2], &sn0, &cs0);
-        for (int c = c0 + tid; c < c1; c += stride) {
+        int c = c0 + tid;
+        for (; c < c1; c += stride) {
             double sd, cd, x, y, mind2;
             sincos(dt * linsp_at(LW, c % nw), &sd, &cd);
             if constexpr (small)

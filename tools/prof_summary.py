@@ -23,6 +23,7 @@ KERNELS = {  # short name -> regex on the demangled kernel name
     "lpt_hist": r"lpt_hist\(", "lpt_scan": r"lpt_scan\(", "lpt_scatter": r"lpt_scatter\(",
     "lpt3_hist": r"lpt3_hist\(", "lpt3_scan": r"lpt3_scan\(", "lpt3_scatter": r"lpt3_scatter\(",
     "dwa_kernel": r"\bdwa_kernel[<(]",
+    "dwa_split_kernel": r"\bdwa_split_kernel[<(]",
     "rrt_kernel": r"\brrt_kernel[<(]",
     "astar3d_kernel": r"\bastar3d_kernel[<(]",
     "dstar_kernel": r"\bdstar_kernel[<(]",
