@@ -85,22 +85,24 @@ __device__ inline bool occ_at(PTR occ, int ox, int oy, int W, int H, int cx, int
 // accumulator r[j] (a[j], a[j + 8], ... in order: consecutive lanes read consecutive words, no LDS bank
 // conflicts), the groups' shuffles combine ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) in that
 // order, lane 0 adds the tail; the result is valid in lane j = 0
-__device__ inline double pw_leaf8(const double* a, int n, int j)
+__device__ inline double pw_leaf8(const double* col, int lo, int n, int j)
 {
+    auto a = [&](int i) -> double { return col[lo + i]; };
     if (n < 8) {
         double res = 0.0;
         if (j == 0)
-            for (int i = 0; i < n; i++) res += a[i];
+            for (int i = 0; i < n; i++) res += a(i);
         return res;
     }
     const int n8 = n - n % 8;
-    double r = a[j];
-    for (int i = 8; i < n8; i += 8) r += a[i + j];
+    double r = a(j);
+#pragma unroll 8
+    for (int i = 8; i < n8; i += 8) r += a(i + j);
     r = r + __shfl_down(r, 1, 8);  // even j: r[j] + r[j + 1]
     r = r + __shfl_down(r, 2, 8);  // j = 0, 4: (r[j] + r[j + 1]) + (r[j + 2] + r[j + 3])
     r = r + __shfl_down(r, 4, 8);  // j = 0: the two halves
     if (j == 0)
-        for (int i = n8; i < n; i++) r += a[i];
+        for (int i = n8; i < n; i++) r += a(i);
     return r;
 }
 
@@ -512,7 +514,7 @@ __global__ __launch_bounds__(kThreads) void dwa_kernel(
         const int nl = S.nleaves;
         for (int g = tid >> 3; g < 3 * nl; g += kThreads >> 3) {  // one 8-lane group per (column, leaf)
             const int cidx = g / nl, l = g % nl;
-            const double ls = pw_leaf8(&S.col[cidx][S.leaf_lo[l]], S.leaf_n[l], tid & 7);
+            const double ls = pw_leaf8(S.col[cidx], S.leaf_lo[l], S.leaf_n[l], tid & 7);
             if ((tid & 7) == 0) S.leafsum[cidx][l] = ls;
         }
         __syncthreads();
@@ -817,7 +819,7 @@ __global__ __launch_bounds__(LOCAL ? kLocalThreads : kSplitThreads) void dwa_spl
         const int ml = l1 - l0;
         for (int g = tid >> 3; g < 3 * ml; g += nt >> 3) {
             const int cidx = g / ml, l = l0 + g % ml;
-            const double ls = pw_leaf8(&S.col[cidx][S.leaf_lo[l] - c0], S.leaf_n[l], tid & 7);
+            const double ls = pw_leaf8(S.col[cidx], S.leaf_lo[l] - c0, S.leaf_n[l], tid & 7);
             if ((tid & 7) == 0) {
                 if constexpr (LOCAL) S.lsum[cidx][l] = ls;
                 else st_wt(lsum + cidx * kMaxLeaves + l, ls);
@@ -855,6 +857,7 @@ __global__ __launch_bounds__(LOCAL ? kLocalThreads : kSplitThreads) void dwa_spl
     // columns in flight), then the scores, in increasing c (the first index wins a tie); LOCAL reads
     // its own columns from LDS
     constexpr int kU = LOCAL ? 1 : 8;
+    const bool want_eval = eval_out && it == iters - 1;
     for (int c0 = tid; c0 < N; c0 += kU * nt) {
         double hv[kU], ov[kU], vv[kU];
 #pragma unroll
@@ -875,13 +878,20 @@ __global__ __launch_bounds__(LOCAL ? kLocalThreads : kSplitThreads) void dwa_spl
         for (int u = 0; u < kU; u++) {
         const int c = c0 + u * nt;
         if (c >= N) break;
-        const double e0 = linsp_at(LV, c / nw), e1 = linsp_at(LW, c % nw);
         const double h = hv[u], o = ov[u], vel = vv[u];
         const double e2 = s0 != 0 ? h / s0 : h;
         const double e3 = s1 != 0 ? o / s1 : o;
         const double e4 = s2 != 0 ? vel / s2 : vel;
-        const double sc = fma(e4, D.velocity_weight, fma(e3, D.obstacle_weight, fma(e2, D.heading_weight, fma(e1, 0.0, e0 * 0.0))));
-        if (eval_out && it == iters - 1) {
+        // the (v, w) terms enter the score times 0: +-0 for a finite window, which changes neither the
+        // score's value nor any comparison, so they are evaluated only for the eval rows
+        double e0 = 0.0, e1 = 0.0, z = 0.0;
+        if (want_eval) {
+            e0 = linsp_at(LV, c / nw);
+            e1 = linsp_at(LW, c % nw);
+            z = fma(e1, 0.0, e0 * 0.0);
+        }
+        const double sc = fma(e4, D.velocity_weight, fma(e3, D.obstacle_weight, fma(e2, D.heading_weight, z)));
+        if (want_eval) {
             double* e = eval_out + ((size_t)a * kMaxN + c) * 3;
             e[0] = fma(e4, 0.0, fma(e3, 0.0, fma(e2, 0.0, fma(e1, 0.0, e0 * 1.0))));
             e[1] = fma(e4, 0.0, fma(e3, 0.0, fma(e2, 0.0, fma(e1, 1.0, e0 * 0.0))));
