@@ -218,10 +218,10 @@ __device__ inline void rollout(const uint32_t* __restrict__ occ, const lds_w32* 
 //    gives the same obstacle term bit for bit.  A nibble map (four occupancy bits per (fx, fy), built in
 //    LDS per launch) gives the four cells in one LDS read.
 #ifndef PMP_DWA_ROLL_SPLIT
-#define PMP_DWA_ROLL_SPLIT 3  // k-split parts
+#define PMP_DWA_ROLL_SPLIT 3  // k-split parts (the rotation table costs a part more than it saves on 512 samples)
 #endif
 #ifndef PMP_DWA_ROLL_LOCAL
-#define PMP_DWA_ROLL_LOCAL 3  // one 1024-thread workgroup per agent
+#define PMP_DWA_ROLL_LOCAL 4  // one 1024-thread workgroup per agent
 #endif
 #ifndef PMP_DWA_ROLL_PLAN
 #define PMP_DWA_ROLL_PLAN 3  // dwa_kernel (resolution-sized windows, DWA.plan)
@@ -281,7 +281,7 @@ __device__ inline void nib_min(const SmallStencil& T, Nib n, double x, double y,
 template <int SCHEME>
 __device__ inline void stencil3(const SmallStencil& T, double x, double y, double& mind2)
 {
-    if constexpr (SCHEME == 3) {
+    if constexpr (SCHEME >= 3) {
         nib_min(T, nib_lookup(T, x, y), x, y, mind2);
         return;
     }
@@ -360,6 +360,60 @@ __device__ inline void rollout_small(const SmallStencil& T, double dt, int Hh, d
     mind2o = mind2;
 }
 
+// SCHEME 4 = SCHEME 3 with the rotation precomputed: a sample's heading sequence th_k depends only on
+// its w, so (dt cos th_k, dt sin th_k) -- the rotation recurrence of rollout(), started from sincos(th0)
+// with sincos(dt w), the same operations in the same order -- is tabulated once per w index in LDS
+// (rot[k][iw], built by one thread per w), and each step of a rollout reads its pair: x + (dt cs) v
+// with the same (dt cs) bits, one sincos per w instead of one per sample, 4 instead of 12 f64
+// operations per step
+constexpr int kRotMax = 2048;  // nw x Hh pairs (C4: 64 x 30)
+
+__device__ inline void build_rot(double* rot, const Linsp& LW, int nw, int Hh, double dt, double th0, int tid, int nt)
+{
+    double sn0, cs0;
+    sincos(th0, &sn0, &cs0);
+    for (int iw = tid; iw < nw; iw += nt) {
+        double sd, cd;
+        sincos(dt * linsp_at(LW, iw), &sd, &cd);
+        double cs = cs0, sn = sn0;
+        double2* r = reinterpret_cast<double2*>(rot) + iw;
+        for (int k = 0; k < Hh; k++) {
+            r[k * nw] = make_double2(dt * cs, dt * sn);
+            const double ncs = cs * cd - sn * sd, nsn = sn * cd + cs * sd;
+            cs = ncs;
+            sn = nsn;
+        }
+    }
+}
+
+__device__ inline void rollout_rot(const SmallStencil& T, const double* rot, int nw, int iw, int Hh, double x, double y,
+                                   double v, double& xo, double& yo, double& mind2o)
+{
+    double mind2 = INFINITY;
+    const double2* r = reinterpret_cast<const double2*>(rot) + iw;
+    int k = 0;
+    for (; k + 1 < Hh; k += 2) {  // two steps per round, as rollout_small
+        const double2 a = r[k * nw], b = r[(k + 1) * nw];
+        const double xa = x + a.x * v, ya = y + a.y * v;
+        x = xa + b.x * v;
+        y = ya + b.y * v;
+        const Nib na = nib_lookup(T, xa, ya), nb = nib_lookup(T, x, y);
+        if (na.bits | nb.bits) {
+            nib_min(T, na, xa, ya, mind2);
+            nib_min(T, nb, x, y, mind2);
+        }
+    }
+    for (; k < Hh; k++) {
+        const double2 a = r[k * nw];
+        x = x + a.x * v;
+        y = y + a.y * v;
+        nib_min(T, nib_lookup(T, x, y), x, y, mind2);
+    }
+    xo = x;
+    yo = y;
+    mind2o = mind2;
+}
+
 __device__ inline SmallStencil small_stencil(const lds_w32* occl, const lds_w32* nib, int ox, int oy, int W, int H,
                                              double R)
 {
@@ -410,9 +464,14 @@ __device__ inline void build_nib(const SmallStencil& T, lds_w32* nib, int tid, i
     }
 }
 
-// the host's choice of stencil scheme for a kernel built with `want` (0: rollout())
-int small_scheme(int want, int W, int H, double R, bool occ_lds)
+// the host's choice of stencil scheme for a kernel built with `want` (0: rollout()); 3 becomes 4 (the
+// rotation table) where the caller's fixed window fits kRotMax
+int small_scheme(int want, int W, int H, double R, bool occ_lds, long rot_pairs = -1)
 {
+    if (want == 4) {
+        const int s3 = small_scheme(3, W, H, R, occ_lds);
+        return s3 == 3 && rot_pairs >= 0 && rot_pairs <= kRotMax ? 4 : s3;
+    }
     if (want == 0 || !occ_lds || !(R >= 0.0) || (long)W * H <= 0) return 0;
     if (want == 3 && R <= 1.0 && ((long)(W + 1) * (H + 1) + 7) / 8 <= (long)kNibWords) return 3;
     return R < 2.0 ? 1 : 0;
@@ -606,7 +665,10 @@ struct DwaSplitBounds {
 
 template <int CHUNK, int NT>
 struct DwaSplitShared {
-    uint32_t occ[kOccLdsWords];
+    union {
+        uint32_t occ[kOccLdsWords];
+        double rot[2 * kRotMax];  // SCHEME 4, over the occupancy once the nibble map is built
+    };
     uint32_t nib[kNibWords];
     double col[3][CHUNK];
     double lsum[3][kMaxLeaves];  // the last part: every part's leaf sums, staged for the combine
@@ -706,8 +768,12 @@ __global__ __launch_bounds__(LOCAL ? kLocalThreads : kSplitThreads) void dwa_spl
     const Linsp LV = make_linsp(vr0, vr1, nv), LW = make_linsp(vr2, vr3, nw);
     const int c0 = B.c[part], c1 = B.c[part + 1];
     __syncthreads();  // the occupancy in LDS
-    if constexpr (small && SCHEME == 3) {
+    if constexpr (small && SCHEME >= 3) {
         build_nib(T, (lds_w32*)S.nib, tid, nt);
+        __syncthreads();
+    }
+    if constexpr (small && SCHEME == 4) {
+        build_rot(S.rot, LW, nw, Hh, dt, st[2], tid, nt);
         __syncthreads();
     }
     DSTAMP(1);
@@ -717,6 +783,16 @@ __global__ __launch_bounds__(LOCAL ? kLocalThreads : kSplitThreads) void dwa_spl
         double sn0, cs0;
         sincos(st[2], &sn0, &cs0);
         int c = c0 + tid;
+        if constexpr (small && SCHEME == 4) {
+            for (; c < c1; c += stride) {
+                double x, y, mind2;
+                rollout_rot(T, S.rot, nw, c % nw, Hh, st[0], st[1], linsp_at(LV, c / nw), x, y, mind2);
+                S.col[0][c - c0] = x;
+                S.col[1][c - c0] = mind2;
+                S.col[2][c - c0] = y;
+            }
+            return;
+        }
         for (; c < c1; c += stride) {
             double sd, cd, x, y, mind2;
             sincos(dt * linsp_at(LW, c % nw), &sd, &cd);
@@ -1012,8 +1088,9 @@ extern "C" int pmp_dwa_step_batch(pmp_ctx* ctx, void* stream, const uint32_t* oc
         return pmp_set_err(ctx, PMP_EINVAL, "pmp_dwa_step_batch: nv*nw must be <= 4096 and dt > 0");
     PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     const bool occ_lds = ((size_t)W * H + 31) / 32 <= (size_t)kOccLdsWords;
-    const int scheme_split = small_scheme(PMP_DWA_ROLL_SPLIT, W, H, dp->inflation, occ_lds);
-    const int scheme_local = small_scheme(PMP_DWA_ROLL_LOCAL, W, H, dp->inflation, occ_lds);
+    const long rot_pairs = dp->nw > 0 ? (long)dp->nw * (long)(int)(dp->predict_time / lp->dt) : -1;
+    const int scheme_split = small_scheme(PMP_DWA_ROLL_SPLIT, W, H, dp->inflation, occ_lds, rot_pairs);
+    const int scheme_local = small_scheme(PMP_DWA_ROLL_LOCAL, W, H, dp->inflation, occ_lds, rot_pairs);
     // parts per agent: auto (dwa_split 0) = the CUs over the agents, at most 16; 1 = one workgroup per
     // agent.  Only windows of fixed size (nv, nw > 0) split, into leaf-aligned parts of <= kSplitChunk.
     int k = 1;
@@ -1048,7 +1125,8 @@ extern "C" int pmp_dwa_step_batch(pmp_ctx* ctx, void* stream, const uint32_t* oc
         }
         DwaSplitBounds Bd;
         split_bounds(dp->nv * dp->nw, k, Bd.c);
-        auto sk = scheme_split == 3 ? dwa_split_kernel<true, 3, false>
+        auto sk = scheme_split == 4 ? dwa_split_kernel<true, 4, false>
+                  : scheme_split == 3 ? dwa_split_kernel<true, 3, false>
                   : scheme_split == 1 ? dwa_split_kernel<true, 1, false>
                   : occ_lds           ? dwa_split_kernel<true, 0, false>
                                       : dwa_split_kernel<false, 0, false>;
@@ -1066,7 +1144,8 @@ extern "C" int pmp_dwa_step_batch(pmp_ctx* ctx, void* stream, const uint32_t* oc
         DwaSplitBounds Bd;
         Bd.c[0] = 0;
         Bd.c[1] = dp->nv * dp->nw;
-        auto lk = scheme_local == 3 ? dwa_split_kernel<true, 3, true>
+        auto lk = scheme_local == 4 ? dwa_split_kernel<true, 4, true>
+                  : scheme_local == 3 ? dwa_split_kernel<true, 3, true>
                   : scheme_local == 1 ? dwa_split_kernel<true, 1, true>
                   : occ_lds           ? dwa_split_kernel<true, 0, true>
                                       : dwa_split_kernel<false, 0, true>;

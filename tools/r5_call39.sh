@@ -1,0 +1,21 @@
+#!/bin/bash
+# round 5, call 39: DWA per-w rotation table (scheme 4) vs scheme 3, stamps -- parity, DWA.plan, control leg
+R=${GRAFT_REPO_ROOT:-/root/repo}
+cd $R; mkdir -p gpurun_out/c39
+timeout -k 10 400 python3 -u -m pytest tests/test_dwa_gpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/c39/test.log 2>&1 || { tail -30 gpurun_out/c39/test.log; exit 1; }
+tail -1 gpurun_out/c39/test.log
+timeout -k 10 200 python3 tools/dwa_plan_time.py 3 || exit 1
+for rnd in 1 2; do
+  for L in libpmp_hip.so libpmp_hip_s3.so; do
+    for A in 256 32; do
+      n=${L%.so}_${A}_$rnd
+      PMP_HIP_LIB=$R/python_motion_planning_amd/$L timeout -k 10 200 python3 bench.py --legs dwa --agents $A --steps 1 --warmup 1 \
+        --no-cpu-baseline --control-steps 40 --detail-out gpurun_out/c39/$n.json > gpurun_out/c39/$n.out 2> gpurun_out/c39/$n.err || { tail -20 gpurun_out/c39/$n.err; exit 1; }
+      python3 -c "
+import json; d=json.load(open('gpurun_out/c39/$n.json'))['secondary']
+print('$n', {k: (round(v['value']), round(v['kernel_ms_per_launch']*1e3, 1), v.get('timed_launches_checked')) for k, v in d.items()})"
+    done
+  done
+done
+PMP_HIP_LIB=$R/python_motion_planning_amd/libpmp_hip_dwastamps.so timeout -k 10 200 python3 tools/dwa_split_probe.py > gpurun_out/c39/dwa_stamps.log 2>&1 || { tail -20 gpurun_out/c39/dwa_stamps.log; exit 1; }
+grep -E "per-phase|LOCAL" gpurun_out/c39/dwa_stamps.log
