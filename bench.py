@@ -1689,7 +1689,7 @@ def main():
                     help="1: the Theta* 2D legs plan on the headline's context (its scratch, as one long-lived "
                          "planner would) instead of fresh ones; 0: fresh contexts -- their new ~100 GB of scratch, "
                          "allocated right after the headline's is freed, ran Theta* 1.85x slower on every box tried "
-                         "(7.2 s vs 3.9 s per 12-batch launch, tools/r5_call15.sh)")
+                         "(7.2 s vs 3.9 s per 12-batch launch, tools/calls/r5_call15.sh)")
     ap.add_argument("--theta-residency", type=int, default=48,
                     help="Theta* 2D queries resident per CU (as --residency; with one multi-batch launch: 256 x this "
                          "many groups; multi-query engine on the headline's context, round 5: 24 / 32 / 40 / 48 -> "

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 5, call 3: DWA split phase stamps + timings after the LDS leaf-sum staging; the A* headline
-# write attribution (mirror builds, tools/r5_attr.sh); LPAStar3D FETCH / WRITE passes
+# write attribution (mirror builds, tools/calls/r5_attr.sh); LPAStar3D FETCH / WRITE passes
 R=${GRAFT_REPO_ROOT:-/root/repo}
 cd $R; mkdir -p gpurun_out/c3
 timeout -k 10 300 python -u -m pytest tests/test_dwa_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/c3/dwa_tests.log 2>&1 || { tail -40 gpurun_out/c3/dwa_tests.log; exit 1; }
@@ -27,4 +27,4 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
         print(c, k, "per-dispatch KiB", [round(x) for x in v])
 PY
 rm -rf $R/gpurun_out/c3/dyn3d_FETCH_SIZE $R/gpurun_out/c3/dyn3d_WRITE_SIZE
-cd $R && SPECS="default:WRITE_SIZE,FETCH_SIZE mir1 mir2 mir4 mir8" bash tools/r5_attr.sh
+cd $R && SPECS="default:WRITE_SIZE,FETCH_SIZE mir1 mir2 mir4 mir8" bash tools/calls/r5_attr.sh

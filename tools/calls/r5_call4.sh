@@ -46,4 +46,4 @@ for i in 1 2 3; do
     python3 -c "import json; d=json.loads(open('gpurun_out/c4/head_${v}_$i.out').read().strip().splitlines()[-1]); print('headline $v', round(d['value']), 'ms/step', round(d['ms_per_step'], 1))"
   done
 done
-ATTR_DIR=attr4 SPECS="blk2:WRITE_SIZE,FETCH_SIZE blk2mir" bash tools/r5_attr.sh
+ATTR_DIR=attr4 SPECS="blk2:WRITE_SIZE,FETCH_SIZE blk2mir" bash tools/calls/r5_attr.sh
