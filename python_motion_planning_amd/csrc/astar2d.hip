@@ -1017,9 +1017,6 @@ int default_heap_cap(int W, int H)
 }
 // per-context scratch budget: workers are reduced to fit (heap spill + cell state + G per worker)
 constexpr size_t kScratchBudget = (size_t)64 << 30;
-// the multi-query engine keeps 3-4x more queries in flight (9.5 MB of cell state, g and heap spill
-// each at 1024^2): its per-context budget
-constexpr size_t kScratchBudgetMq = (size_t)160 << 30;
 
 // longest-first order of a batch in the context's SCR_PDIR scratch (counting sort, descending
 // start-goal distance)

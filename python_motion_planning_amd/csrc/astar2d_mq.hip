@@ -82,13 +82,25 @@ __device__ __forceinline__ uint32_t hkey(uint32_t cm)
 template <int HEUR>
 __device__ __forceinline__ double h_of_key(uint32_t hk)
 {
-    return hkind<HEUR>() == 2 ? 0.0 : (hkind<HEUR>() == 1 ? (double)hk : __dsqrt_rn((double)hk));
+    return hkind<HEUR>() == 2 ? 0.0 : (hkind<HEUR>() == 1 ? (double)hk : sqrt_int_rn(hk));
 }
 // Node.__lt__ (node.py:51-54)
 __device__ __forceinline__ bool key_lt(double fa, uint32_t ka, double fb, uint32_t kb)
 {
     return (fa < fb) | ((fa == fb) & (ka < kb));
 }
+// the same as a lane mask: three compares into SGPR pairs and two scalar ops (a ballot of the bool
+// above would first turn it into a 0 / 1 VGPR and compare that again)
+__device__ __forceinline__ lmask key_lt_m(double fa, uint32_t ka, double fb, uint32_t kb)
+{
+    return lm(fa < fb) | (lm(fa == fb) & lm(ka < kb));
+}
+
+// lane masks of the row positions (lane & 15) a predicate depends on
+constexpr lmask kLanesGe1 = ~0x0001000100010001ull;  // gl >= 1
+constexpr lmask kLane15 = 0x8000800080008000ull;     // gl == 15
+constexpr lmask kLanesLt8 = 0x00FF00FF00FF00FFull;   // gl < 8
+constexpr lmask kLanesLt9 = 0x01FF01FF01FF01FFull;   // gl < 9
 
 typedef __attribute__((address_space(3))) double lds_f64;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
@@ -97,7 +109,9 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 template <int K>
 __device__ __forceinline__ uint32_t bc(uint32_t v)  // lane K of my row
 {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + K, 0xF, 0xF, false);
+    // mov_dpp (no `old` operand): every lane of a row_newbcast reads a valid lane, so no v_mov of a
+    // fallback value is needed
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + K, 0xF, 0xF, false);
 }
 template <int K>
 __device__ __forceinline__ int bci(int v) { return (int)bc<K>((uint32_t)v); }
@@ -127,10 +141,10 @@ __device__ __forceinline__ double shl1f(double v)
 }
 __device__ __forceinline__ uint32_t ror_or(uint32_t v)  // OR over my row
 {
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xF, 0xF, false);
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xF, 0xF, false);
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);
+    v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x121, 0xF, 0xF, false);
+    v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x122, 0xF, 0xF, false);
+    v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false);
+    v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);
     return v;
 }
 // value of absolute lane `src` (same row), any src per lane
@@ -141,7 +155,7 @@ __device__ __forceinline__ double bpf(double v, int src)
     return __longlong_as_double(((uint64_t)bp((uint32_t)(b >> 32), src) << 32) | bp((uint32_t)b, src));
 }
 // my row's 16 bits of a ballot
-__device__ __forceinline__ uint32_t rbits(bool p, int gb) { return (uint32_t)(__ballot(p) >> gb) & 0xFFFFu; }
+__device__ __forceinline__ uint32_t rbits(bool p, int gb) { return (uint32_t)(lm(p) >> gb) & 0xFFFFu; }
 
 // per lane: bit `lane` of mask ? a : b, as one v_cndmask (see astar2d.hip Ld::get)
 __device__ __forceinline__ uint32_t sel_lanes(uint64_t mask, uint32_t a, uint32_t b)
@@ -344,11 +358,11 @@ struct Walk {
     __device__ __forceinline__ uint32_t five(uint32_t w2, int gb) const
     {
         const uint32_t a = rbits((w2 & MA) == VA, gb), b = rbits((w2 & MB) == VB, gb);
-        return 32u + (uint32_t)(__ffs((int)(a | (b << 16))) - 1);
+        return 32u + (uint32_t)__builtin_ctz(a | (b << 16));  // exactly one leaf matches: never 0
     }
     __device__ __forceinline__ uint32_t three(uint32_t w2, int gb) const
     {
-        return 8u + (uint32_t)(__ffs((int)(rbits((w2 & MV3 & 0xFFu) == (MV3 >> 8), gb) & 0xFFu)) - 1);
+        return 8u + (uint32_t)__builtin_ctz(rbits((w2 & MV3 & 0xFFu) == (MV3 >> 8), gb) & 0xFFu);
     }
 };
 template <bool T2LDS>
@@ -386,6 +400,23 @@ __device__ __forceinline__ void bit_set(const GHeap& h, bool on, int level, uint
         if (bit) __hip_atomic_fetch_or(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else __hip_atomic_fetch_and(w, ~m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+}
+// path_op's form: lane L (1..15) sets the bit of its parent, node Pl at level L - 1, so each lane's
+// tier is a compile-time lane mask (levels 0-4 / 5-9 / 10-14 at lanes 1-5 / 6-10 / 11-15) and, with
+// the tier-2 bytes in LDS, the word is one shift and add: tier 0's block root is 1 (word 0), tier 1's
+// 32..63 (words 1..32), tier 2's 1024..2047 (bytes from word 36).  Only heaps of <= 16,383 entries
+// (T2LDS) use it; the HBM tier-2 form keeps bit_set.
+constexpr lmask kTier1 = 0x07C007C007C007C0ull;  // gl 6..10
+constexpr lmask kTier2 = 0xF800F800F800F800ull;  // gl 11..15
+__device__ __forceinline__ void bit_set_lane(const GHeap& h, bool on, int gl, uint32_t Pl, bool bit)
+{
+    const bool t1 = lb(kTier1), t2 = lb(kTier2);
+    const int r = gl - 1 - (t2 ? 10 : (t1 ? 5 : 0));  // level - 5 t
+    const uint32_t R = Pl >> r;
+    const uint32_t mr = (1u << r) - 1u;
+    const uint32_t widx = t2 ? (R >> 2) - 220u : (t1 ? R - 31u : R - 1u);
+    const uint32_t m = 1u << ((Pl & mr) + mr + (t2 ? (R & 3u) << 3 : 0u));
+    if (on) ds_mskor(h.B + widx, m, bit ? m : 0u);
 }
 // CPython _siftup's choice bit of the parent of `child` (a position) whose new content is v and
 // whose sibling holds s: bit = !(left < right), odd positions are left children
@@ -443,16 +474,21 @@ __device__ __forceinline__ void pop_leaf(const GHeap& h, const Walk& wk, int n, 
 // a ballot for b, the stores, the bits of the changed levels' parents.  Returns b; lane L's new
 // heap[q_L] in (nf, nc, nk) (for the caller's cached parents).
 template <bool T2LDS, int HEUR>
-__device__ __forceinline__ int path_op(const GHeap& h, bool on, bool pop, uint32_t Q, int Kd, int n, double Xf, uint32_t Xc,
+__device__ __forceinline__ int path_op(const GHeap& h, lmask mon, lmask mpop, uint32_t Q, int Kd, int n, double Xf, uint32_t Xc,
                                        uint32_t Xk, int gl, int gb, double& lastf, uint32_t& lastc, uint32_t& lastk,
                                        double& rootf, uint32_t& rootc, double& nf, uint32_t& nc, uint32_t& nk, uint32_t cwL)
 {
+    // the lane predicates as lane masks (scalar logic, lm / lb): the step is VALU-issue-bound
     const bool lvl = gl <= Kd;
     const int q = lvl ? (int)(Q >> (Kd - gl)) - 1 : 0;
-    const bool lda = on && (pop ? (gl >= 1 && lvl) : gl < Kd);
-    const bool l15 = on && pop && gl == 15;  // a pop's lane 15: heap[n - 1], the new last
+    const bool on = lb(mon), pop = lb(mpop);
+    const lmask mlvl = lm(lvl);
+    const lmask mlda = mon & ((mpop & mlvl & kLanesGe1) | (~mpop & lm(gl < Kd)));
+    const bool lda = lb(mlda);
+    const bool l15 = lb(mon & mpop & kLane15);  // a pop's lane 15: heap[n - 1], the new last
     const int si = ((q - 1) ^ 1) + 1;
-    const bool hass = on && gl >= 1 && lvl && si < n;
+    const lmask mhass = mon & kLanesGe1 & mlvl & lm(si < n);
+    const bool hass = lb(mhass);
     double Vf, Sf;
     uint32_t Vc, Sc, Vk, Sk;
     // kLaneConst: one offset per lane -- lane L's level-L word for the path node q (lane 15 of a pop:
@@ -476,12 +512,14 @@ __device__ __forceinline__ int path_op(const GHeap& h, bool on, bool pop, uint32
         ls.get<HEUR>(Sf, Sc, Sk);
     }
     // the boundary level b
-    const bool lt = key_lt(Xf, Xk, Vf, Vk);
-    const int cnt = __popc(rbits(lda && (pop ? !lt : lt), gb));
+    const int cnt = __popc((uint32_t)((mlda & (mpop ^ key_lt_m(Xf, Xk, Vf, Vk))) >> gb) & 0xFFFFu);  // pop: !lt, push: lt
     const int b = pop ? cnt : Kd - cnt;
     // new contents: a pop shifts levels 1..b up one (lane L takes lane L+1's), a push shifts levels
     // b..Kd-1 down one (lane L takes lane L-1's); X at level b
-    const bool atb = gl == b, shift = pop ? gl < b : (gl > b && lvl);
+    const lmask mblt = lm(gl < b), mbeq = lm(gl == b), mbgt = lm(gl > b);
+    const bool atb = lb(mbeq), shift = lb((mpop & mblt) | (~mpop & mbgt & mlvl));
+    // the levels a pop (<= b) / a push (>= b) rewrites
+    const lmask mchg = (mpop & (mblt | mbeq)) | (~mpop & (mbgt | mbeq));
 #if PMP_MQ_BPERM
     // one ds_bpermute per word from lane L +- 1 (the group's own direction) instead of both DPP
     // shifts and a select: the kernel is VALU-issue-bound, the permutes run on the LDS pipe.  A
@@ -505,14 +543,19 @@ __device__ __forceinline__ int path_op(const GHeap& h, bool on, bool pop, uint32
     nc = atb ? Xc : (shift ? (pop ? upc : dnc) : Vc);
     nk = atb ? Xk : (shift ? (pop ? upk : dnk) : Vk);
 #endif
-    if (kLaneConst) hst_off(h, on && (pop ? gl <= b : (gl >= b && lvl)), q, offq, nf, nc, nk, pop ? 4 : 2);
-    else hst(h, on && (pop ? gl <= b : (gl >= b && lvl)), q, nf, nc, nk, pop ? 4 : 2);
+    const bool stq = lb(mon & mchg & mlvl);
+    if (kLaneConst) hst_off(h, stq, q, offq, nf, nc, nk, pop ? 4 : 2);
+    else hst(h, stq, q, nf, nc, nk, pop ? 4 : 2);
     // the bits of the changed levels' parents: lane L (>= 1) sets its parent's from its new content
-    // and its sibling's
+    // and its sibling's: bit = !(left < right), an odd position is the left child (choice_bit_k)
     {
-        const bool upd = hass && (pop ? gl <= b : gl >= b);
-        const bool bit = choice_bit_k(q, nf, nk, Sf, Sk);
-        bit_set<T2LDS>(h, upd, gl - 1, Q >> (Kd - gl + 1), bit);
+        const bool fe = nf == Sf;
+        const lmask lt_ns = lm(nf < Sf) | (lm(fe) & lm(nk < Sk));
+        const lmask lt_sn = lm(nf > Sf) | (lm(fe) & lm(nk > Sk));
+        const lmask modd = lm((q & 1) != 0);
+        const bool bit = lb((modd & ~lt_ns) | (~modd & ~lt_sn));
+        if (T2LDS) bit_set_lane(h, lb(mhass & mchg), gl, Q >> (Kd - gl + 1), bit);
+        else bit_set<T2LDS>(h, lb(mhass & mchg), gl - 1, Q >> (Kd - gl + 1), bit);
     }
     {
         // selects, not a branch (every lane computes them): root = level 0's new content; the last
@@ -523,7 +566,7 @@ __device__ __forceinline__ int path_op(const GHeap& h, bool on, bool pop, uint32
         const int src = gb + (pop ? 15 : Kd);
         const double lf = bpf(pop ? Vf : nf, src);
         const uint32_t lc = bp(pop ? Vc : nc, src), lk = bp(pop ? Vk : nk, src);
-        const bool setl = on && !(pop && b == Kd && Q == (uint32_t)n);
+        const bool setl = lb(mon & ~(mpop & lm(b == Kd && Q == (uint32_t)n)));
         rootf = on ? r0f : rootf;
         rootc = on ? r0c : rootc;
         lastf = setl ? lf : lastf;
@@ -602,14 +645,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
     uint32_t nsb = 16u | (1u << ((mx + 1) * 3 + (my + 1)));
     if (mo & 1) nsb |= (1u << (3 + (my + 1))) | (1u << ((mx + 1) * 3 + 1));
     nsb |= (1u << ((mx + 1) * 3 + (my + 1))) << 16;
-    // the 3x3 round: lanes 0..8 occupancy of cell (x + i/3 - 1, y + i%3 - 1); lanes 9..11 the
-    // cell-state bytes of row i - 9; lane 12 G[pusher]; THETA: lane 13 the pusher's CLOSED parent
-    const int blk_dx = gl < 9 ? gl / 3 - 1 : (gl < 12 ? gl - 10 : 0);
+    // the 3x3 round: lanes 0..8 the occupancy and the cell-state byte of cell (x + i/3 - 1,
+    // y + i%3 - 1) (tiled cell states, cst_idx); lane 12 G[pusher]; THETA: lane 13 the pusher's CLOSED parent
+    const int blk_dx = gl < 9 ? gl / 3 - 1 : 0;
     const int blk_dy = gl < 9 ? gl % 3 - 1 : 0;
+    const uint32_t tH = (uint32_t)(H + 15) >> 4;
 
     // group state (equal across the row)
     uint32_t ep = epoch_all[slot];
-    bool need_q = true, done = lone && grp != 0;
+    // per-group flags as lane masks (SGPR pairs, scalar logic): a group needs a query / is done
+    lmask Mneed = ~0ull, Mdone = lone ? lm(grp != 0) : 0ull;
     int q = 0, qi = 0, sx = 0, sy = 0, gx = 0, gy = 0;
     int n = 0, nexp = 0, maxn = 0;
     int npush = 0, npop = 0;  // < 2^31 per query (heaps are capped at 32,767 entries: pushes <= 8 W H)
@@ -620,21 +665,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
     uint32_t pend = 0u;
     double ifv = 0.0;
     uint32_t icm = 0u, ikk = 0u;
-    bool pc_ok = false;
+    lmask Mpc = 0ull;  // the group's cached parents (pf8, pk8) are valid ("pc_ok")
     double pf8 = 0.0;
     uint32_t pk8 = 0u;
     int n0 = 0;
 
     for (;;) {
         // ---- groups without a query take the next one (or retire)
-        const bool fetch_any = __ballot(need_q && !done) != 0ull;
-        if (need_q && !done) {
+        const lmask mfetch = Mneed & ~Mdone;
+        if (lb(mfetch)) {
             int v = 0;
             if (gl == 0) v = atomicAdd(queue, 1);
             qi = bci<0>(v);
-            if (qi >= nq) {
-                done = true;
-            } else {
+            if (qi < nq) {
                 q = order ? order[qi] : qi;
                 sx = start_xy[2 * q];
                 sy = start_xy[2 * q + 1];
@@ -676,23 +719,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
                     nexp = 0;
                     maxn = 1;
                     pend = 0u;
-                    pc_ok = false;
-                    need_q = false;
                 }
             }
             wave_sync_mem();
         }
-        if (fetch_any) {
+        if (mfetch) {
+            // the fetch's outcome (compares on every lane, kept to the fetching groups): the queue ran
+            // out, or a query inside the grid started
+            const lmask mend = mfetch & lm(qi >= nq);
+            const lmask mstart = mfetch & ~mend & lm((unsigned)sx < (unsigned)W) & lm((unsigned)sy < (unsigned)H) &
+                                 lm((unsigned)gx < (unsigned)W) & lm((unsigned)gy < (unsigned)H);
+            Mdone |= mend;
+            Mneed &= ~mstart;
+            Mpc &= ~mstart;
             // the longest queries (first in the longest-first order) get issue priority
-            if (__ballot(!done && !need_q && qi < prio_n)) __builtin_amdgcn_s_setprio(3);
+            if (~Mdone & ~Mneed & lm(qi < prio_n)) __builtin_amdgcn_s_setprio(3);
             else __builtin_amdgcn_s_setprio(0);
         }
-        if (__ballot(!done) == 0ull) break;
-        const bool act = !done && !need_q;
+        if (Mdone == ~0ull) break;
+        const lmask Mact = ~Mdone & ~Mneed;
 
         // ---- 1. the leading run of trivial pushes (the item is not less than its parent, so
         //      CPython's _siftdown stops at once): stored in one step
-        if (act && pend != 0u && pc_ok) {
+        if (lb(Mact & Mpc & lm(pend != 0u))) {
             const uint32_t mine = (pend >> mo) & 1u;  // lane m < 8: my item is pending
             const uint32_t below = pend & ((1u << mo) - 1u);
             const int rank = __popc(below);
@@ -700,8 +749,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
             const int pl = gb + (pos - n0 < 8 ? pos - n0 : 7);
             const double pf = bpf(pf8, pl);
             const uint32_t pk = bp(pk8, pl);
-            const bool triv = gl < 8 && mine && !key_lt(ifv, ikk, pf, pk);
-            const uint32_t tm = rbits(triv, gb) & 0xFFu;
+            const lmask mtriv = kLanesLt8 & lm(mine != 0u) & ~key_lt_m(ifv, ikk, pf, pk);
+            const uint32_t tm = (uint32_t)(mtriv >> gb) & 0xFFu;
             const uint32_t nt = pend & ~tm;
             const uint32_t run = nt ? pend & ((nt & (0u - nt)) - 1u) : pend;
             if (run != 0u) {
@@ -713,8 +762,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
                 const uint32_t lkp = bp(ikk, gb + prev);
                 const double leftf = rank == 0 ? lastf : lfp;
                 const uint32_t leftk = rank == 0 ? lastk : lkp;
-                bit_set<T2LDS>(hp, inrun && (pos & 1) == 0 && pos > 0, 30 - __clz(pos + 1), (uint32_t)(pos + 1) >> 1,
-                               !key_lt(leftf, leftk, ifv, ikk));
+                bit_set<T2LDS>(hp, lb(lm(inrun) & lm((pos & 1) == 0) & lm(pos > 0)), 30 - __clz(pos + 1),
+                               (uint32_t)(pos + 1) >> 1, lb(~key_lt_m(leftf, leftk, ifv, ikk)));
                 hst_off(hp, inrun, pos, soff(pos, inrun), ifv, icm, ikk, 1);
                 const int top = 31 - __clz(run);
                 lastf = bpf(ifv, gb + top);
@@ -729,23 +778,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
         }
 
         // ---- 2. this step's heap operation: the next pending push, else a pop
-        const bool push = act && pend != 0u;
+        const lmask Mpush = Mact & lm(pend != 0u);
+        const bool push = lb(Mpush);
         int st = -1;  // >= 0: the query ends this step with this status
         double goal_cost = 0.0;
         int plen = 0;
-        if (act && !push && n == 0) st = PMP_NO_PATH;  // OPEN exhausted (a_star.py:83)
-        const bool pop = act && !push && n > 0;
+        if (lb(Mact & ~Mpush & lm(n == 0))) st = PMP_NO_PATH;  // OPEN exhausted (a_star.py:83)
+        const lmask Mpop = Mact & ~Mpush & lm(n > 0);
+        const bool pop = lb(Mpop);
         double Xf = lastf;
         uint32_t Xc = lastc, Xk = lastk;
         uint32_t Q = 0u;
         int Kd = 0;
-        int popn = 0;  // the popped node (pop): its code, and the 3x3 round's loads
-        uint32_t ncm = rootc;
+        uint32_t ncm = rootc;  // the popped node (pop): its code, and the 3x3 round's loads
         int x = 0, y = 0;
         uint32_t nlin = 0u;
-        uint32_t blk_w = 0u, blk_w2 = 0u;
+        uint32_t blk_w = 0u, blk_c = 0u;
         int blk_sh = 0;
-        bool blk_in = false;
         double gpar = 0.0;
         uint32_t ppar = 0u;  // THETA: Pc[pusher] (lane 13)
         Ld pld;
@@ -762,7 +811,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
             npop++;
             n -= 1;
             n0 = n;
-            popn = 1;
             const int ndir = cm_dir<HEUR>(ncm);
             x = ndir == 8 ? sx : gx - cm_dx<HEUR>(ncm);
             y = ndir == 8 ? sy : gy - cm_dy<HEUR>(ncm);
@@ -773,39 +821,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
             // lane class, so no load destination is zero-filled under another exec mask
             {
                 const int cx = x + blk_dx, cy = y + blk_dy;
-                const bool is_occ = gl < 9, is_cst = gl >= 9 && gl < 12;
-                const bool in_occ = (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
-                const bool in_cst = (unsigned)cx < (unsigned)W;
-                const uint32_t ci = (is_occ && in_occ) ? (uint32_t)cx * (uint32_t)H + (uint32_t)cy : 0u;
-                const uint32_t lo =
-                    (is_cst && in_cst) ? (uint32_t)cx * (uint32_t)H + (uint32_t)(y > 0 ? y - 1 : 0) : 0u;
-                const uint32_t a0 = lo & ~3u;
+                const bool in_occ = gl < 9 && (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
+                const uint32_t ci = in_occ ? (uint32_t)cx * (uint32_t)H + (uint32_t)cy : 0u;
+                const uint32_t cti = in_occ ? cst_idx(cx, cy, tH) : 0u;
                 const uint32_t pusher = has_pusher ? nlin - (uint32_t)(mot_x(pm) * H + mot_y(pm)) : 0u;
                 const uint32_t gi = (!GZERO && gl == 12) ? pusher : 0u;
                 const uint32_t ow = occ[ci >> 5];
-                const uint32_t* p32 = reinterpret_cast<const uint32_t*>(cst + a0);
-                const uint32_t c0 = p32[0], c1 = p32[1];
+                blk_c = cst[cti];
                 gpar = GZERO ? 0.0 : G[gi];
                 if (THETA) ppar = Pc[gl == 13 ? pusher : 0u];
-                blk_in = is_occ ? in_occ : (is_cst && in_cst);
-                blk_sh = is_occ ? (int)(ci & 31u) : (int)((uint32_t)cx * (uint32_t)H + (uint32_t)y - 1u - a0);
-                blk_w = is_occ ? ow : c0;
-                blk_w2 = c1;
+                blk_sh = (int)(ci & 31u);
+                blk_w = ow;
             }
-            // the pushes will take positions n0, n0 + 1, ...: their parents, while all 8 share a depth
-            pc_ok = n0 > 0 && (31 - __clz(n0 + 1)) == (31 - __clz(n0 + 8));
             if (n > 0) pop_leaf<T2LDS>(hp, wk, n, gb, Q, Kd);
         }
+        // the pushes will take positions n0, n0 + 1, ...: their parents, while all 8 share a depth
+        Mpc = (Mpc & ~Mpop) | (Mpop & lm(n0 > 0) & lm(__clz(n0 + 1) == __clz(n0 + 8)));
         const int pp = (n0 + (gl & 7) - 1) >> 1;  // lanes 0..7: parent of position n0 + lane
         {
-            const int pi = pop && pc_ok && gl < 8 ? pp : 0;
+            const int pi = lb(Mpop & Mpc & kLanesLt8) ? pp : 0;
             pld.issue_off(hp, pi, soff(pi, pi >= hp.cap));
         }
-        const bool op = push || (pop && n > 0);
+        const lmask Mop = Mpush | (Mpop & lm(n > 0));
         double nf = 0.0;
         uint32_t nc = 0u, nk = 0u;
         int b = 0;
-        b = path_op<T2LDS, HEUR>(hp, op, pop, Q, Kd, n, Xf, Xc, Xk, gl, gb, lastf, lastc, lastk, rootf, rootc, nf, nc,
+        b = path_op<T2LDS, HEUR>(hp, Mop, Mpop, Q, Kd, n, Xf, Xc, Xk, gl, gb, lastf, lastc, lastk, rootf, rootc, nf, nc,
                                  nk, cwL);
         {
             double f8;
@@ -816,10 +857,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
         }
         // the cached parents (lanes 0..7: heap[parent(n0 + lane)]) after the operation: a position on
         // the path at a level the operation rewrote now holds that level's new content
-        if (op && pc_ok) {
+        if (lb(Mop & Mpc)) {
             const int Lp = 31 - __clz(pp + 1);
-            const bool onpath = gl < 8 && Lp <= Kd && (int)(Q >> (Kd - Lp)) - 1 == pp &&
-                                (pop ? Lp <= b : Lp >= b);
+            const bool onpath = lb(kLanesLt8 & lm(Lp <= Kd) & lm((int)(Q >> (Kd - Lp)) - 1 == pp) &
+                                   ((Mpop & lm(Lp <= b)) | (~Mpop & lm(Lp >= b))));
             const int src = gb + (Lp < 16 ? Lp : 15);
             const double af = bpf(nf, src);
             const uint32_t ak = bp(nk, src);
@@ -832,21 +873,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
 
         // ---- 3. the popped node: 3x3 masks (bit k = cell (x + k/3 - 1, y + k%3 - 1)), CLOSED test,
         //      goal test, getNeighbor (a_star.py:57-82)
-        if (popn) {
-            const uint32_t occ9 = rbits(gl < 9 && (!blk_in || ((blk_w >> blk_sh) & 1u)), gb) & 0x1FFu;
-            uint32_t row = 0u;
-            if (gl >= 9 && gl < 12 && blk_in) {
-                // the bytes of cells y-1, y, y+1 as bytes 0..2 of v (blk_sh = -1 when y = 0: byte 0 is
-                // then off the grid and masked below), tested together: a byte is CLOSED in this
-                // query when its high nibble is the epoch and its low nibble (motion + 1) is nonzero
-                const uint64_t win = ((uint64_t)blk_w2 << 32) | blk_w;
-                const uint32_t v = blk_sh < 0 ? (blk_w << 8) : (uint32_t)(win >> (8 * blk_sh));
-                const uint32_t lo = v & 0x0F0F0Fu, eq = ((v >> 4) & 0x0F0F0Fu) ^ (ep * 0x010101u);
-                const uint32_t m = (lo + 0x7F7F7Fu) & ~(eq + 0x7F7F7Fu) & 0x808080u;
-                row = ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u);
-                row &= (y > 0 ? 1u : 0u) | 2u | (y + 1 < H ? 4u : 0u);
-            }
-            const uint32_t cls9 = bc<9>(row) | (bc<10>(row) << 3) | (bc<11>(row) << 6);
+        // lanes 0..8: the cell is in the grid
+        const lmask Mblk = kLanesLt9 & lm((unsigned)(x + blk_dx) < (unsigned)W) & lm((unsigned)(y + blk_dy) < (unsigned)H);
+        if (pop) {
+            const uint32_t occ9 =
+                (uint32_t)((kLanesLt9 & (~Mblk | lm(((blk_w >> blk_sh) & 1u) != 0u))) >> gb) & 0x1FFu;
+            // a cell is CLOSED in this query when its byte's high nibble is the epoch and its low nibble
+            // (motion + 1) is nonzero
+            const uint32_t cls9 = (uint32_t)((Mblk & lm((blk_c >> 4) == ep) & lm((blk_c & 15u) != 0u)) >> gb) & 0x1FFu;
             const double gp = bcf<12>(gpar);
             if (!(cls9 & 16u)) {  // node.current not in CLOSED (a_star.py:57-58)
                 const int ndir = cm_dir<HEUR>(ncm);
@@ -898,10 +932,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
                     }
                 }
                 // CLOSED[node.current] = node (a_star.py:82)
-                if (gl == 0) cst[nlin] = (uint8_t)((ep << 4) | (uint32_t)(THETA ? 1 : ndir + 1));
+                if (gl == 0) cst[cst_idx(x, y, tH)] = (uint8_t)((ep << 4) | (uint32_t)(THETA ? 1 : ndir + 1));
                 if (!GZERO && gl == 1) G[nlin] = gnode;
                 if (THETA && gl == 0) Pc[nlin] = par_lin;  // read back by this lane's extractPath
-                if (mir8 && gl == 0) cst_m[nlin] = (uint8_t)((ep << 4) | (uint32_t)(ndir + 1));
+                if (mir8 && gl == 0) cst_m[cst_idx(x, y, tH)] = (uint8_t)((ep << 4) | (uint32_t)(ndir + 1));
                 if (mir8 && !GZERO && gl == 1) G_m[nlin] = gnode;
                 if (gl == 2 && expand_out && nexp < expand_cap)
                     expand_out[(size_t)q * expand_cap + nexp] =
@@ -939,7 +973,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
                             if (len < path_cap) pth[len] = li;
                             len++;
                             if (cx == sx && cy == sy) break;
-                            const int d = (int)(cst[li] & 15u) - 1;
+                            const int d = (int)(cst[cst_idx(cx, cy, tH)] & 15u) - 1;
                             cost += (d & 1) ? kSqrt2 : 1.0;
                             cx -= mot_x(d);
                             cy -= mot_y(d);
@@ -950,9 +984,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
                 } else {
                     // getNeighbor in motion order; push the goal and stop (a_star.py:66-80)
                     const int ndx = gx - x - mx, ndy = gy - y - my;
-                    const bool nb_ok = gl < 8 && (occ9 & nsb & 0xFFFFu) == 0u && (cls9 & (nsb >> 16)) == 0u;
-                    uint32_t vm = rbits(nb_ok, gb) & 0xFFu;
-                    const uint32_t gm = rbits(nb_ok && ndx == 0 && ndy == 0, gb) & 0xFFu;
+                    const lmask Mnb = kLanesLt8 & lm((occ9 & nsb & 0xFFFFu) == 0u) & lm((cls9 & (nsb >> 16)) == 0u);
+                    uint32_t vm = (uint32_t)(Mnb >> gb) & 0xFFu;
+                    const uint32_t gm = (uint32_t)((Mnb & lm(ndx == 0) & lm(ndy == 0)) >> gb) & 0xFFu;
                     if (gm) vm &= (gm << 1) - 1u;
                     double ig = gnode + (GZERO ? 0.0 : ((mo & 1) ? kSqrt2 : 1.0));
                     int icode = mo;
@@ -978,7 +1012,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
         if (n > maxn) maxn = n;
 
         // ---- the groups whose query ended: results, then a new query next step
-        if (st >= 0) {
+        const lmask Mend = lm(st >= 0);
+        Mneed |= Mend;
+        if (lb(Mend)) {
             if (gl == 0) {
                 int s = st;
                 if (s == PMP_FOUND && plen > path_cap) s = PMP_PATH_OVERFLOW;
@@ -994,14 +1030,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
                 }
             }
             pend = 0u;
-            need_q = true;
         }
     }
     if (gl == 0) epoch_all[slot] = ep;
     span_end(span);
 }
 
-size_t mq_cst_bytes(int W, int H) { return (((size_t)W * H + 8 + 255) & ~(size_t)255); }
+size_t mq_cst_bytes(int W, int H) { return (cst_tiled_bytes(W, H) + 255) & ~(size_t)255; }
 
 }  // namespace
 
@@ -1039,11 +1074,21 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
                           int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded, uint32_t* expand,
                           int expand_cap, int64_t* counters, int32_t* status, int* queue)
 {
-    const int groups = ctx->astar_workers < nq ? ctx->astar_workers : nq;
+    int groups = ctx->astar_workers < nq ? ctx->astar_workers : nq;
     const bool t2lds = ctx->astar_mq_t2lds != 0;
     const int bits_b = t2lds ? kBits01 + kT2LBytes : kBits01;
     const int cap_max = t2lds ? kMqCapT2L : kMqCap;
     const int heap_cap = ctx->astar_heap_cap < cap_max ? ctx->astar_heap_cap : cap_max;
+    const int theta = algo == PMP_ALGO_THETA ? 1 : (algo == PMP_ALGO_LAZY_THETA ? 2 : 0);
+    if (theta) {
+        // the reservation's fit (astar2d_reserve_impl) counts cell state, G, spill and bits per slot;
+        // Theta* adds a W*H*4-byte CLOSED-parent array per slot: fewer groups (the persistent queue
+        // serves every query) instead of growing past the budget
+        const size_t per_slot = (size_t)W * H * 13 + (size_t)cap_max * 16 + 4096 + 256;
+        const size_t fit = (kScratchBudgetMq / per_slot) & ~(size_t)3;
+        if (fit < 4) return pmp_set_err(ctx, PMP_ENOMEM, "ThetaStar: one wave's slots exceed the scratch budget");
+        if ((size_t)groups > fit) groups = (int)fit;
+    }
     // lone: fewer queries than CUs -- one query per wave, in group 0, with the CU's whole LDS as its
     // heap share (the drop-in single query: latency, not throughput)
     const bool lone = nq <= kMqLoneMax;
@@ -1066,7 +1111,6 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
     uint4* spill = (uint4*)pmp_scratch(ctx, SCR_MQ_SPILL, (kMirror & 7 ? 2 : 1) * slots * (size_t)spill_n * 16 + 16);
     uint32_t* t2 = (uint32_t*)pmp_scratch(ctx, SCR_MQ_T2, slots * kT2Words * 4 + 16);
     if (!spill || !t2) return PMP_ENOMEM;
-    const int theta = algo == PMP_ALGO_THETA ? 1 : (algo == PMP_ALGO_LAZY_THETA ? 2 : 0);
     uint32_t* Pc = nullptr;  // Theta*: the CLOSED parent cell of every cell, per slot
     if (theta) {
         Pc = (uint32_t*)pmp_scratch(ctx, SCR_MQ_PC, slots * (size_t)W * H * 4 + 16);

@@ -313,6 +313,12 @@ __global__ __launch_bounds__(64) void astar2d_sq_kernel(
     typename SqGrid<LDSG>::Cst cst;
     typename SqGrid<LDSG>::Gv G;
     uint32_t ep = 1u;
+    // cell-state byte of (x, y): row-major in the LDS grid block, tiled in the per-slot HBM states
+    // shared with the multi-query engine (cst_idx)
+    const uint32_t tH = (uint32_t)(H + 15) >> 4;
+    auto cidx = [&](int x, int y) -> uint32_t {
+        return LDSG ? (uint32_t)x * (uint32_t)H + (uint32_t)y : cst_idx(x, y, tH);
+    };
     if constexpr (LDSG) {
         unsigned char* gb = smem + (size_t)12 * lds_cap;
         lds_u32* ow = (lds_u32*)gb;
@@ -412,7 +418,7 @@ __global__ __launch_bounds__(64) void astar2d_sq_kernel(
             blk_in = lane < 18 && (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
             const uint32_t ci = blk_in ? (uint32_t)cx * (uint32_t)H + (uint32_t)cy : 0u;
             ow = occg[ci >> 5] >> (ci & 31u);
-            cb = cst[ci];
+            cb = cst[blk_in ? cidx(cx, cy) : 0u];
             const uint32_t gi = (!GZERO && lane == 18 && ndir < 8) ? nlin - (uint32_t)(mot_x(ndir) * H + mot_y(ndir)) : 0u;
             if (!GZERO) gpar = G[gi];
         }
@@ -441,7 +447,7 @@ __global__ __launch_bounds__(64) void astar2d_sq_kernel(
 
         // CLOSED[node.current] = node (a_star.py:82)
         const double gnode = (GZERO || ndir == 8) ? 0.0 : rl_f64(gpar, 18) + ((ndir & 1) ? kSqrt2 : 1.0);
-        if (lane == 0) cst[nlin] = (uint8_t)(LDSG ? (uint32_t)(ndir + 1) : ((ep << 4) | (uint32_t)(ndir + 1)));
+        if (lane == 0) cst[cidx(x, y)] = (uint8_t)(LDSG ? (uint32_t)(ndir + 1) : ((ep << 4) | (uint32_t)(ndir + 1)));
         if (!GZERO && lane == 1) G[nlin] = gnode;
         if (lane == 2 && expand_out && nexp < expand_cap) expand_out[(size_t)q * expand_cap + nexp] = nlin | ((uint32_t)ndir << 28);
         nexp++;
@@ -459,7 +465,7 @@ __global__ __launch_bounds__(64) void astar2d_sq_kernel(
                     if (len < path_cap) pth[len] = li;
                     len++;
                     if (px == sx && py == sy) break;
-                    const int d = (int)(cst[li] & 15u) - 1;
+                    const int d = (int)(cst[cidx(px, py)] & 15u) - 1;
                     cost += (d & 1) ? kSqrt2 : 1.0;
                     px -= mot_x(d);
                     py -= mot_y(d);

@@ -688,6 +688,16 @@ struct DwaSplitShared {
 // relaxed atomic add, and the last part reads them with agent-scope loads (ld_coh below) -- no
 // __threadfence(), whose L2 writeback (buffer_wbl2) flushed every dirty line of the XCD and cost
 // ~40 us per arrival (PMP_DWA_STAMPS, round 5).
+// ISA assumption (not the HIP memory model, which gives relaxed operations no happens-before): on
+// gfx950 an agent-scope relaxed store is issued with sc1 (written through to the coherent point, the
+// die's memory-side cache, past every XCD's L2) and an agent-scope relaxed load with sc1 (served from
+// there, never from a stale line of the reader's L2 / L1); `s_waitcnt vmcnt(0)` before the arrival
+// add orders the stores' completion ahead of the count.  Other targets would need a release on the
+// counter add and an acquire on the last part's read; tests/test_dwa_gpu.py's bit-equality of every
+// part count against one workgroup (test_split_parts_bit_equal) guards this on the hardware.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "dwa.hip's k-split hand-off relies on gfx950's sc1 write-through stores and coherent loads"
+#endif
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 __device__ __forceinline__ void st_wt(double* p, double v)
 {

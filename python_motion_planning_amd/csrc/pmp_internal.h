@@ -82,6 +82,9 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
                           int32_t* path_len, uint32_t* path, int path_cap, int32_t* n_expanded, uint32_t* expand,
                           int expand_cap, int64_t* counters, int32_t* status, int* queue);
 int pmp_astar2d_mq_lds_cap(int per_cu, bool t2lds);
+// the multi-query engine keeps 3-4x more queries in flight (9.5 MB of cell state, g and heap spill
+// each at 1024^2; Theta* another 4 MB of CLOSED parents): its per-context scratch budget
+constexpr size_t kScratchBudgetMq = (size_t)160 << 30;
 int pmp_astar2d_slot_scratch(pmp_ctx* ctx, hipStream_t s, size_t slots, int W, int H, uint8_t** cst, size_t* cst_bytes,
                              double** G, uint32_t** ep);
 // The single-query A* 2D engine (astar2d_sq.hip): one query per workgroup, the CU's LDS its heap.
@@ -126,6 +129,45 @@ __device__ __forceinline__ int next_query(int* queue, int lane)
     return __builtin_amdgcn_readfirstlane(qi);
 }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+// Per-lane bools kept as the wave's 64-bit lane mask (SGPR pair): a select between two divergent
+// bools written as `c ? a : b` is lowered through 0/1 VGPRs and v_cndmask (five VALU instructions);
+// as masks it is three scalar ops.  lm() of a compare is the compare itself (its SGPR result).
+typedef unsigned long long lmask;
+__device__ __forceinline__ lmask lm(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+__device__ __forceinline__ bool lb(lmask m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+
+// Per-slot A* 2D cell-state bytes (astar2d_mq.hip / astar2d_sq.hip) in tiles of 8 (x) x 16 (y)
+// cells: a tile is one 128-B line, so the 3x3 round of an expansion touches ~1.4 lines on average
+// instead of one per grid row x-1, x, x+1 (the row-major layout, x * H + y), and an A* front's
+// cells share lines in both directions.  tH = tiles along y.
+__host__ __device__ inline size_t cst_tiled_bytes(int W, int H)
+{
+    return (size_t)((W + 7) >> 3) * (size_t)((H + 15) >> 4) * 128u;
+}
+__device__ __forceinline__ uint32_t cst_idx(int x, int y, uint32_t tH)
+{
+    return (((uint32_t)x >> 3) * tH + ((uint32_t)y >> 4)) * 128u + (((uint32_t)x & 7u) << 4) + ((uint32_t)y & 15u);
+}
+
+// Correctly rounded sqrt of an integer 0 <= k < 2^31: the operation sequence of LLVM's f64 sqrt
+// lowering for gfx9 (rsq, two Newton-Raphson corrections of (s, h = y/2), two residual corrections),
+// without its input scaling (only for x < 2^-767) and its 0 / inf class test (0 handled here), so the
+// bits equal __dsqrt_rn((double)k) in 12 instead of 20 VALU instructions.
+__device__ __forceinline__ double sqrt_int_rn(uint32_t k)
+{
+    const double x = (double)k;
+    const double y = __builtin_amdgcn_rsq(x);
+    const double s0 = x * y, h0 = y * 0.5;
+    const double r0 = __builtin_fma(-h0, s0, 0.5);
+    const double h1 = __builtin_fma(h0, r0, h0);
+    const double s1 = __builtin_fma(s0, r0, s0);
+    const double d0 = __builtin_fma(-s1, s1, x);
+    const double s2 = __builtin_fma(d0, h1, s1);
+    const double d1 = __builtin_fma(-s2, s2, x);
+    const double s3 = __builtin_fma(d1, h1, s2);
+    return k == 0u ? 0.0 : s3;
+}
 
 // launch-span stamps (pmp_set_timing): each worker's lane 0 folds its start / end wall-clock tick
 __device__ __forceinline__ void span_begin(unsigned long long* span)

@@ -37,6 +37,7 @@ constexpr int kMaxK = 256;     // in-radius candidates kept in LDS (more spill t
 constexpr int kRnd = 256;      // random doubles staged in LDS
 constexpr int kBins = 16;      // obstacle bins per axis over the map
 constexpr int kLdsBytes = 160 * 1024;  // the CU's LDS
+constexpr int kRrtMaxResident = 4;     // LDS tree shares per CU RRT honours from pmp_set_resident_per_cu
 
 constexpr int KF_A = 1;        // c_i < G0
 constexpr int KF_VALID = 2;    // ... and collision-free
@@ -816,7 +817,11 @@ extern "C" int pmp_rrt_batch(pmp_ctx* ctx, void* stream, const pmp_rrt_params* p
     if (!xyq || !kl || !tl || !al) return PMP_ENOMEM;
     // the coarse copy's LDS part: the workgroup's share of the CU's LDS (one workgroup per CU unless
     // pmp_set_resident_per_cu leaves room for more: several in flight) beside its static state
-    const long share = kLdsBytes / pmp_lds_share(ctx, 1);
+    // (ctx->resident_per_cu is shared with the one-wave planners, whose 16-32 per CU would leave an
+    // RRT workgroup almost no tree in LDS: RRT honours at most kRrtMaxResident of it)
+    int per = pmp_lds_share(ctx, 1);
+    if (per > kRrtMaxResident) per = kRrtMaxResident;
+    const long share = kLdsBytes / per;
     int lcap = (int)(std::max(0L, share - (long)sizeof(RrtShared) - 512) / 4) & ~63;
     if (lcap > tree_cap) lcap = (tree_cap + 63) & ~63;
     RrtArgs A;

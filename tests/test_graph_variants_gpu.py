@@ -69,8 +69,9 @@ def test_c2_subset_against_oracle():
         assert np.array_equal(r["status"].cpu().numpy(), ref["status"]), algo
         assert np.array_equal(r["cost"].cpu().numpy(), ref["cost"]), algo
         assert np.array_equal(r["n_expanded"].cpu().numpy(), ref["n_expanded"]), algo
-        # pushes, pops, expansions (column 3, the largest heap, is sampled once per step on engine 2)
-        assert np.array_equal(r["counters"].cpu().numpy()[:, :3], ref["counters"][:, :3]), algo
+        # pushes, pops, expansions and the largest heap (24 queries: the single-query engine, which
+        # samples the heap size after each expansion's pushes, as the oracle's maximum lands there)
+        assert np.array_equal(r["counters"].cpu().numpy(), ref["counters"]), algo
         P = r["path"].cpu().numpy()
         for k in range(len(idx)):
             n = ref["path_len"][k]
@@ -254,8 +255,10 @@ def test_theta2d_c2_subset_against_oracle(theta_engine):
         assert np.array_equal(r["status"].cpu().numpy(), ref["status"]), algo
         assert np.array_equal(r["cost"].cpu().numpy(), ref["cost"]), algo
         assert np.array_equal(r["n_expanded"].cpu().numpy(), ref["n_expanded"]), algo
-        # pushes, pops, expansions (column 3, the largest heap, is sampled once per step on engine 2)
-        assert np.array_equal(r["counters"].cpu().numpy()[:, :3], ref["counters"][:, :3]), algo
+        # pushes, pops, expansions, and the largest heap except on engine 2 (which samples it once
+        # per step, after a step's pop may already have shrunk the heap)
+        cols = 3 if theta_engine[0] == 2 else 4
+        assert np.array_equal(r["counters"].cpu().numpy()[:, :cols], ref["counters"][:, :cols]), algo
         P = r["path"].cpu().numpy()
         for k in range(len(idx)):
             n = ref["path_len"][k]
