@@ -98,8 +98,34 @@ def test_c3_batch_against_oracle():
         assert int(out["status"][q]) == ref["status"][q]
 
 
+def test_c3_midsize_against_oracle():
+    """C3 map, 8 queries x 12,000 samples (trees of ~9.4k nodes, past the 3,000-sample batch test and
+    into the sizes where rewiring lists are long): whole RRT* trees (parents, draw counts; coordinates
+    to 1e-12) equal to the oracle's, and four plain-RRT trees."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import batch, workloads as wl
+
+    env = _map("c3")
+    rects, circs = wl.c3_map()
+    nq, sn = 8, 12000
+    rnd = np.stack([np.random.RandomState(500 + q).random_sample(3 * sn + 1) for q in range(nq)])
+    starts, goals = np.tile([5.0, 5.0], (nq, 1)), np.tile([505.0, 505.0], (nq, 1))
+    out = batch.rrt_batch(env, starts, goals, rnd, sn, star=True)
+    ref = O.rrt_batch(True, rects, circs, 512, 512, starts, goals, rnd, sn)
+    assert (ref["n_nodes"] > 3000).all()
+    for q in range(nq):
+        _check_tree(out, q, ref["tree"][q, : ref["n_nodes"][q]], q)
+        assert int(out["status"][q]) == ref["status"][q]
+    # plain RRT through the same index (nearest only)
+    out = batch.rrt_batch(env, starts[:4], goals[:4], rnd[:4], sn, star=False)
+    ref = O.rrt_batch(False, rects, circs, 512, 512, starts[:4], goals[:4], rnd[:4], sn)
+    for q in range(4):
+        _check_tree(out, q, ref["tree"][q, : ref["n_nodes"][q]], q)
+        assert int(out["status"][q]) == ref["status"][q]
+
+
 def test_c3_full_size_properties():
-    """C3 at BASELINE size (65,536 samples), 4 queries: two whole trees against the oracle, and tree
+    """C3 at BASELINE size (65,536 samples), 4 queries: the four whole trees against the oracle, and tree
     invariants on every node of all four -- parents reach the start without cycles, g >= g(parent) +
     edge length (rewires never raise a cost), sampled edges collision-free under the oracle's
     isCollision, draw counts consistent."""
@@ -111,10 +137,10 @@ def test_c3_full_size_properties():
     nq, sn = 4, 65536
     rnd = np.stack([np.random.RandomState(100 + q).random_sample(3 * sn + 1) for q in range(nq)])
     out = batch.rrt_batch(env, np.tile([5.0, 5.0], (nq, 1)), np.tile([505.0, 505.0], (nq, 1)), rnd, sn, star=True)
-    # two of the four trees against the oracle at full size (about 30 s of host time, in parallel)
-    ref = O.rrt_batch(True, rects, circs, 512, 512, np.tile([5.0, 5.0], (2, 1)), np.tile([505.0, 505.0], (2, 1)),
-                      rnd[:2], sn)
-    for q in range(2):
+    # all four trees against the oracle at full size (the oracle's OpenMP runs them in parallel)
+    ref = O.rrt_batch(True, rects, circs, 512, 512, np.tile([5.0, 5.0], (nq, 1)), np.tile([505.0, 505.0], (nq, 1)),
+                      rnd, sn)
+    for q in range(nq):
         _check_tree(out, q, ref["tree"][q, : ref["n_nodes"][q]], q)
         assert int(out["status"][q]) == ref["status"][q]
     rng = np.random.default_rng(0)

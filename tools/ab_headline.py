@@ -1,6 +1,7 @@
 """Same-process A/B of libpmp_hip builds on the A* headline launch (C2, engine 1, the bench's
 geometry): each build is loaded with its own ctypes handle (RTLD_LOCAL: the same C-ABI symbols
-resolve per handle), and the builds take turns -- create a context, one warmup launch, R timed
+resolve per handle), and the builds take turns -- create a context, one warmup launch (5 batches:
+every slot first-touched, as the driver's --warmup 5), R timed
 launches of B batches (HIP events on the launch stream), destroy the context (its ~150 GB of
 per-slot scratch) -- so box-level drift hits every build alike.  Outputs are checked equal across
 builds.
@@ -34,7 +35,10 @@ def main():
     ap.add_argument("libs", nargs="+")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=2)
-    ap.add_argument("--batches", type=int, default=5)
+    ap.add_argument("--batches", type=int, default=20)
+    ap.add_argument("--warmup-batches", type=int, default=5,
+                    help="the first launch on a fresh context: >= workers / 4096 batches touches every slot's "
+                         "scratch (a launch that first-touches ~150 GB runs ~1.3 s slower)")
     ap.add_argument("--workers", type=int, default=15360)
     ap.add_argument("--residency", type=int, default=60)
     ap.add_argument("--out", default=None)
@@ -48,12 +52,13 @@ def main():
     W, H = occ.shape
     nq, B = len(starts), args.batches
     occ_bits = batch.occ_bits_device(occ, torch)
-    s_rep = torch.as_tensor(starts, device="cuda").repeat(B, 1)
-    g_rep = torch.as_tensor(goals, device="cuda").repeat(B, 1)
+    s_rep = torch.as_tensor(starts, device="cuda").repeat(max(B, args.warmup_batches), 1)
+    g_rep = torch.as_tensor(goals, device="cuda").repeat(max(B, args.warmup_batches), 1)
     path_cap = 4096
-    out = {k: torch.empty(B * nq, dtype=dt, device="cuda") for k, dt in
+    NB = max(B, args.warmup_batches)
+    out = {k: torch.empty(NB * nq, dtype=dt, device="cuda") for k, dt in
            (("cost", torch.float64), ("plen", torch.int32), ("nexp", torch.int32), ("status", torch.int32))}
-    path = torch.empty((B * nq, path_cap), dtype=torch.int32, device="cuda")
+    path = torch.empty((NB * nq, path_cap), dtype=torch.int32, device="cuda")
     stream = torch.cuda.Stream()
     libs = [(os.path.basename(p), bind(p)) for p in args.libs]
     times = {n: [] for n, _ in libs}
@@ -79,7 +84,7 @@ def main():
                                            path.data_ptr(), path_cap, out["nexp"].data_ptr(), None, 0, None,
                                            out["status"].data_ptr())
 
-            chk(launch(1), "warmup")
+            chk(launch(min(B, args.warmup_batches)), "warmup")
             torch.cuda.synchronize()
             for _ in range(args.reps):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -88,7 +93,7 @@ def main():
                 e1.record(stream)
                 torch.cuda.synchronize()
                 times[name].append(e0.elapsed_time(e1))
-                got = {k: v.cpu().numpy().copy() for k, v in out.items()}
+                got = {k: v[:B * nq].cpu().numpy().copy() for k, v in out.items()}
                 if ref is None:
                     ref = got
                     assert (ref["status"] == 0).all()

@@ -4,7 +4,7 @@
 R=${GRAFT_REPO_ROOT:-/root/repo}
 L=$R/python_motion_planning_amd
 cd $R; mkdir -p gpurun_out/c3
-timeout -k 10 300 python3 tools/ab_headline.py $L/libpmp_hip_base.so $L/libpmp_hip.so --rounds 4 --reps 2 --batches 5 \
+timeout -k 10 300 python3 tools/ab_headline.py $L/libpmp_hip_base.so $L/libpmp_hip.so $L/libpmp_hip_gtile.so --rounds 4 --reps 2 --batches 5 \
   --out gpurun_out/c3/ab.json > gpurun_out/c3/ab.log 2>&1 || { tail -20 gpurun_out/c3/ab.log; exit 1; }
 tail -2 gpurun_out/c3/ab.log
 for r in 52 64; do
