@@ -105,35 +105,44 @@ def control_leg(args, torch, dist, world, rank):
     offd = torch.tensor(off, dtype=torch.int32, device="cuda")
     L = _lib.load_library()
     ctx = _lib.context()
-    u = torch.empty((na, 2), dtype=torch.float64, device="cuda")
-    best = torch.empty(na, dtype=torch.int32, device="cuda")
-    status = torch.empty(na, dtype=torch.int32, device="cuda")
+    K = args.control_steps
+    # every step writes its own output rows (the state advances in place), so each timed step is
+    # checked below against the same step of an untimed replay
+    u_all = torch.empty((K, na, 2), dtype=torch.float64, device="cuda")
+    best_all = torch.empty((K, na), dtype=torch.int32, device="cuda")
+    status_all = torch.empty((K, na), dtype=torch.int32, device="cuda")
     nst = torch.empty(na, dtype=torch.int32, device="cuda")
     _LABEL[0] = "mpc_sampled_dwa"
 
-    def step():
+    def step(k):
         rc = L.pmp_dwa_step_batch(ctx, _lib.stream_ptr(), occ_bits.data_ptr(), ox, oy, gocc.shape[0], gocc.shape[1],
                                   ctypes.byref(lp), ctypes.byref(dp), na, st.data_ptr(), gd.data_ptr(), xyd.data_ptr(),
-                                  offd.data_ptr(), 1, u.data_ptr(), best.data_ptr(), status.data_ptr(),
-                                  nst.data_ptr(), None, None, None)
+                                  offd.data_ptr(), 1, u_all[k].data_ptr(), best_all[k].data_ptr(),
+                                  status_all[k].data_ptr(), nst.data_ptr(), None, None, None)
         if rc:
             _lib.check(ctx, rc, "pmp_dwa_step_batch")
 
     for _ in range(max(1, args.warmup)):
-        step()
+        step(0)
     torch.cuda.synchronize()
     st.copy_(st0)
-    K = args.control_steps
-    elapsed, kern_ms = timed(torch, dist, lambda i: step(), K)
-    # the timed work checked: an untimed replay of the same K steps from the same states must end in
-    # the same agent states and controls (the first step's evaluation is pinned to the oracle by
-    # tests/test_dwa_gpu.py)
-    ref_out = {"state": st.clone(), "u": u.clone(), "best": best.clone(), "status": status.clone()}
+    poison([u_all, best_all, status_all])
+    elapsed, kern_ms = timed(torch, dist, step, K)
+    # the timed work checked: an untimed replay of the same K steps from the same states gives the same
+    # controls, argmax and status at every step and the same final agent states (the first step's
+    # evaluation is pinned to the oracle by tests/test_dwa_gpu.py)
+    timed_rows = [{"u": u_all[k].clone(), "best": best_all[k].clone(), "status": status_all[k].clone()}
+                  for k in range(K)]
+    st_timed = st.clone()
     st.copy_(st0)
-    for _ in range(K):
-        step()
+    for k in range(K):
+        step(k)
     torch.cuda.synchronize()
-    checked = check_timed("dwa", ref_out, [{"state": st, "u": u, "best": best, "status": status}])
+    checked = 0
+    for k in range(K):
+        checked += check_timed("dwa", {"u": u_all[k], "best": best_all[k], "status": status_all[k]}, [timed_rows[k]])
+    check_timed("dwa", {"state": st}, [{"state": st_timed}])
+    ref_out = {"state": st_timed, "u": u_all[K - 1], "best": best_all[K - 1]}
     steps_done = (args.agents if args.scaling == "strong" else na * world) * K
     gathered = None
     if args.scaling == "strong":
@@ -186,11 +195,16 @@ def control_leg(args, torch, dist, world, rank):
             "ms_per_step": elapsed / K * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
             "timed_launches_checked": checked,
             "config": {"workload": "C4: README 51x31 grid, 64x64 (v,w) samples, H=30, weights 0.2/0.1/0.05"},
-            "roofline": with_traffic({"bound": "fp64-valu", "achieved": achieved_tf, "peak": 78.6, "unit": "TFLOP/s",
-                                      "frac": achieved_tf / 78.6, "traffic": None,
-                                      "flops_per_agent_step": flops_per_step,
-                                      "flops_note": "SURVEY.md 8(d) stencil formulation, sin/cos/atan2 not counted"},
-                                     "dwa_split_kernel", "mpc_sampled_dwa"),
+            "roofline": with_issue(with_traffic({"bound": "fp64-valu", "achieved": achieved_tf, "peak": 78.6,
+                                                 "unit": "TFLOP/s", "frac": achieved_tf / 78.6, "traffic": None,
+                                                 "frac_basis": "model flops (SURVEY.md 8(d) stencil form), not the "
+                                                               "instructions executed: see issue",
+                                                 "flops_per_agent_step": flops_per_step,
+                                                 "flops_note": "SURVEY.md 8(d) stencil formulation, sin/cos/atan2 "
+                                                               "not counted; the kernel's 2x2 nibble stencil and "
+                                                               "per-w rotation table execute fewer"},
+                                                "dwa_split_kernel", "mpc_sampled_dwa"),
+                                   "dwa_split_kernel", "mpc_sampled_dwa", na, "agent-step"),
             "cpu_baseline": cpu}
 
 
@@ -306,6 +320,35 @@ def with_traffic(roof: dict, kernel: str, workload: str) -> dict:
     alg = roof.get("algorithmic_bytes_per_launch")
     if t and alg:
         roof["traffic_over_algorithmic"] = t / alg
+    return roof
+
+
+def with_issue(roof: dict, kernel: str, workload: str, units_per_dispatch: float, unit: str) -> dict:
+    """The binding resource of an issue-bound leg beside its memory roof: instructions per unit of
+    work and the VALU issue fraction of `kernel`'s dispatches in the leg `workload`, from the newest
+    committed profiles/r*/pmc_issue.json (the SQ issue pass of tools/profile_round.sh, keyed per
+    workload by tools/prof_summary.py).  valu_issue_frac = SQ_INSTS_VALU / (1024 SIMDs x
+    GRBM_GUI_ACTIVE / 8 XCDs / 2 cycles per wave64 VALU instruction)."""
+    path = _newest_profile("pmc_issue.json")
+    if not path:
+        roof["issue"] = {"source": "no committed pmc_issue.json"}
+        return roof
+    src = os.path.relpath(path, REPO)
+    with open(path) as f:
+        d = json.load(f).get("workloads", {}).get(workload)
+    if not d or d.get("kernel") != kernel:
+        roof["issue"] = {"source": f"{src} has no {kernel} entry for workload {workload}: refused"}
+        return roof
+    per = 1.0 / float(units_per_dispatch) if units_per_dispatch else None
+    roof["issue"] = {
+        "unit": unit,
+        "valu_insts_per_unit": d["SQ_INSTS_VALU_per_dispatch"] * per if per else None,
+        "salu_insts_per_unit": d.get("SQ_INSTS_SALU_per_dispatch", 0.0) * per if per else None,
+        "lds_insts_per_unit": d.get("SQ_INSTS_LDS_per_dispatch", 0.0) * per if per else None,
+        "valu_issue_frac": d.get("valu_issue_frac"),
+        "wave_issue_frac": d.get("wave_issue_frac"), "wave_wait_frac": d.get("wave_wait_frac"),
+        "units_per_dispatch": units_per_dispatch,
+        "source": f"{src} [{workload}: {kernel}, SQ pass of the short bench; units from this run]"}
     return roof
 
 
@@ -606,7 +649,7 @@ def rrt_leg(args, torch, dist, world, rank):
                                    "65536 samples, max_dist 0.5, r 10, goal rate 0.05"},
             # frac on SURVEY.md 8(d)'s algorithmic bytes (the line's model, "bytes_model"), against the L2
             # roof (the trees are L2 / Infinity-Cache resident); the kernel's own loads beside it
-            "roofline": with_traffic({"bound": "l2", "achieved": sv_gbs, "peak": L2_PEAK_GBS, "unit": "GB/s",
+            "roofline": with_issue(with_traffic({"bound": "l2", "achieved": sv_gbs, "peak": L2_PEAK_GBS, "unit": "GB/s",
                                       "frac": sv_gbs / L2_PEAK_GBS, "traffic": None,
                                       "algorithmic_bytes_per_launch": sv_bytes,
                                       "bytes_model": "8d: 16 B xy/node scanned + 8 B g/in-radius node",
@@ -618,7 +661,8 @@ def rrt_leg(args, torch, dist, world, rank):
                                                     "frac_l2": achieved / L2_PEAK_GBS,
                                                     "note": "the kernel's own loads: 4 B per node scanned (16-bit "
                                                             "fixed-point coarse copy) + 24 B per in-radius candidate"}},
-                                     "rrt_kernel", "rrt_star"),
+                                                "rrt_kernel", "rrt_star"),
+                                   "rrt_kernel", "rrt_star", float(ctr[:, 0].sum()), "iteration"),
             "detail": {"found": int((status == 0).sum()), "mean_nodes": float(out["n_nodes"].float().mean().item()),
                        "iterations_per_launch": int(ctr[:, 0].sum()), "nodes_scanned_per_launch": int(ctr[:, 1].sum()),
                        "collision_tests_per_launch": int(ctr[:, 3].sum())},
@@ -761,9 +805,11 @@ def astar3d_leg(args, torch, dist, world, rank):
             "streams": len(lanes), "batches_per_launch": B, "timed_launches_checked": checked,
             "workers_per_cu": wpc, "resident_per_cu": args.a3_residency,
             "config": {"workload": "C5: Grid3D(26,20,16) door, random.seed(i) pairs, safety bubbles r=1, euclidean"},
-            "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                                      "algorithmic_bytes_per_launch": alg_bytes}, "astar3d_kernel", f"astar3d_x{B}"),
+            "roofline": with_issue(with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                                 "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                                                 "algorithmic_bytes_per_launch": alg_bytes},
+                                                "astar3d_kernel", f"astar3d_x{B}"),
+                                   "astar3d_kernel", f"astar3d_x{B}", float(c[:, 2].sum()) * B, "expansion"),
             "detail": {"expansions_per_batch": int(c[:, 2].sum()), "reference_pushes_per_batch": int(c[:, 0].sum()),
                        "heap_pops_per_batch": int(c[:, 1].sum()), "max_heap_entries": int(c[:, 3].max())},
             "cpu_baseline": cpu, "trajectory": traj}
@@ -1300,9 +1346,13 @@ def dyn3d_leg(args, torch, dist, world, rank):
             "timed_launches_checked": checked,
             "steps": args.dyn3d_steps, "ms_per_step": elapsed / args.dyn3d_steps * 1e3, "kernel_ms_per_launch": kern_ms,
             "dtype": "f64",
-            "roofline": with_traffic(dyn3d_roof(kind, int(np.maximum(nexp, 0).sum() * np.mean(nbs)),
-                                                None if pushes is None else int(pushes * np.mean(nbs)), kern_ms),
-                                     "dstar3d_kernel" if kind == "dstar3d" else "lpa3d_kernel", f"{name}_x{B}"),
+            "roofline": with_issue(with_traffic(dyn3d_roof(kind, int(np.maximum(nexp, 0).sum() * np.mean(nbs)),
+                                                           None if pushes is None else int(pushes * np.mean(nbs)),
+                                                           kern_ms),
+                                                "dstar3d_kernel" if kind == "dstar3d" else "lpa3d_kernel", f"{name}_x{B}"),
+                                   "dstar3d_kernel" if kind == "dstar3d" else "lpa3d_kernel", f"{name}_x{B}",
+                                   float(np.maximum(nexp, 0).sum() * np.mean(nbs)),
+                                   "processState" if kind == "dstar3d" else "expansion"),
             "roofline_note": "latency-bound list machines (OPEN / U with Python-list semantics): a small frac is "
                              "the expected reading",
             "streams": len(streams), "batches_per_launch": B,
@@ -1420,15 +1470,20 @@ def track_leg(args, torch, dist, world, rank, kind):
     ref_out = {"u": o["u"].clone(), "n_steps": o["n_steps"].clone(), "admm_iters": o["admm_iters"].clone(),
                "state": st.clone(), "u_p": up.clone()}
 
-    def run(i):
-        st.copy_(st0)
-        up.zero_()
-        r = batch.track_step_batch(kind, lp, st, gd, xyd, offd, iters=iters, u_p=up, **kw)
-        return {"u": r["u"], "n_steps": r["n_steps"], "admm_iters": r["admm_iters"], "state": st, "u_p": up}
+    # every timed launch starts from its own copy of the initial states (made before the timed
+    # region) and keeps its outputs, so each one is checked against the first launch's
+    st_k = [st0.clone() for _ in range(args.track_steps)]
+    up_k = [torch.zeros_like(up) for _ in range(args.track_steps)]
+    outs = []
 
-    last = []
-    elapsed, kern_ms = timed(torch, dist, run, args.track_steps, last=last)
-    checked = check_timed(kind, ref_out, last)
+    def run(i):
+        r = batch.track_step_batch(kind, lp, st_k[i], gd, xyd, offd, iters=iters, u_p=up_k[i], **kw)
+        outs.append({"u": r["u"], "n_steps": r["n_steps"], "admm_iters": r["admm_iters"], "state": st_k[i],
+                     "u_p": up_k[i]})
+        return outs[-1]
+
+    elapsed, kern_ms = timed(torch, dist, run, args.track_steps)
+    checked = check_timed(kind, ref_out, outs)
     gathered = None
     steps_all = stepped * world
     if args.scaling == "strong":
@@ -1535,6 +1590,11 @@ def compact_leg(rec: dict) -> dict:
         out["mfma_util_pct_analytic"] = _sig(rec["mfma"]["mfma_util_pct_analytic"], 3)
     if roof.get("bytes_model"):
         out["bytes_model"] = roof["bytes_model"]
+    iss = roof.get("issue") or {}
+    if iss.get("valu_issue_frac") is not None:  # the SQ issue pass (profiles/): the binding resource
+        out["valu_issue_frac"] = _sig(iss["valu_issue_frac"], 3)
+        out["valu_per_unit"] = _sig(iss.get("valu_insts_per_unit"), 4)
+        out["unit_of_issue"] = iss.get("unit")
     return out
 
 
@@ -1556,6 +1616,8 @@ def headline_line(out: dict, detail_path) -> dict:
     and a compact map of the secondary legs."""
     roof = dict(out["roofline"])
     roof = {k: (_sig(v) if isinstance(v, float) else v) for k, v in roof.items()}
+    if isinstance(roof.get("issue"), dict):
+        roof["issue"] = {k: (_sig(v, 4) if isinstance(v, float) else v) for k, v in roof["issue"].items()}
     cpu = out["cpu_baseline"]
     if cpu:
         host = cpu.get("host") or {}
@@ -1575,7 +1637,8 @@ def headline_line(out: dict, detail_path) -> dict:
     line["secondary"] = {k: compact_leg(v) for k, v in out["secondary"].items()}
     s = json.dumps(line)
     # keep the line inside the driver's window whatever the leg set: drop optional fields first
-    for drop in (("secondary", "traffic_x"), ("secondary", "checked"), ("cpu_baseline", "sample")):
+    for drop in (("secondary", "unit_of_issue"), ("secondary", "traffic_x"), ("secondary", "checked"),
+                 ("cpu_baseline", "sample")):
         if len(s) <= 4000:
             break
         if drop[0] == "secondary":
@@ -1661,11 +1724,97 @@ def dry_run(args, rank, world):
         dist.destroy_process_group()
 
 
+def c2_share_mode(args):
+    """--strong-share R/N (diagnostic, one GPU, one process): rank R's share of C2 under the N-rank
+    strong split (shard.lpt_deal of the default_rng(1) pairs by octile distance, as --scaling strong
+    deals it) repeated --steps times in one launch, the share's per-rank launch time measured; with
+    --tail-sq K the K longest of the launch's queries (octile) run on the single-query engine
+    (astar2d_sq.hip: a workgroup and a CU's LDS per query) on a second stream beside the multi-query
+    launch of the rest.  Every query's outputs are checked against an all-multi-query run."""
+    import torch
+
+    from python_motion_planning_amd import _lib, batch, shard, workloads as wl
+
+    R, N = (int(v) for v in args.strong_share.split("/"))
+    torch.cuda.set_device(0)
+    occ, s_all, g_all = wl.c2_workload(nq=args.nq, pair_seed=1)
+    mine = shard.lpt_deal(shard.octile(s_all, g_all), N, R)
+    starts, goals = np.tile(s_all[mine], (args.steps, 1)), np.tile(g_all[mine], (args.steps, 1))
+    nq, W, H = len(starts), occ.shape[0], occ.shape[1]
+    L = _lib.load_library()
+    occ_bits = batch.occ_bits_device(occ, torch)
+    path_cap = 4096
+    ctxs = []
+
+    def mk(engine, workers):
+        ctx = L.pmp_create(0)
+        _lib.check(ctx, L.pmp_astar2d_set_engine(ctx, engine, 1), "engine")
+        _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, workers, 0), "reserve")
+        _lib.check(ctx, L.pmp_astar2d_set_residency(ctx, 60), "residency")
+        ctxs.append(ctx)
+        return ctx
+
+    def outs(n):
+        return {k: torch.empty(n, dtype=dt, device="cuda") for k, dt in
+                (("cost", torch.float64), ("plen", torch.int32), ("nexp", torch.int32), ("status", torch.int32))}
+
+    def launch(ctx, stream, idx, o):
+        s_d = torch.as_tensor(starts[idx], device="cuda")
+        g_d = torch.as_tensor(goals[idx], device="cuda")
+        path = torch.empty((len(idx), path_cap), dtype=torch.int32, device="cuda")
+        keep.append((s_d, g_d, path))
+        rc = L.pmp_astar2d_batch(ctx, stream.cuda_stream, occ_bits.data_ptr(), W, H, 0, s_d.data_ptr(), g_d.data_ptr(),
+                                 len(idx), o["cost"].data_ptr(), o["plen"].data_ptr(), path.data_ptr(), path_cap,
+                                 o["nexp"].data_ptr(), None, 0, None, o["status"].data_ptr())
+        _lib.check(ctx, rc, "pmp_astar2d_batch")
+
+    keep = []
+    sA, sB = torch.cuda.Stream(), torch.cuda.Stream()
+    mq = mk(1, 15360)
+    allidx = np.arange(nq)
+    # reference: every query on the multi-query engine (also the warmup that touches its slots)
+    ref = outs(nq)
+    launch(mq, sA, allidx, ref)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    launch(mq, sA, allidx, ref)
+    torch.cuda.synchronize()
+    t_mq = time.perf_counter() - t0
+    rec = {"metric": f"C2 strong-split share: rank {R} of {N}, {len(mine)} pairs x {args.steps} in one launch",
+           "queries": nq, "launch_s_multi_query_only": t_mq}
+    K = args.tail_sq
+    if K > 0:
+        order = np.argsort(-shard.octile(starts, goals), kind="stable")
+        heavy, light = np.sort(order[:K]), np.sort(order[K:])
+        sq = mk(3, K)
+        oh, ol = outs(K), outs(nq - K)
+        for rep_i in range(2):  # the first pass touches the single-query slots
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            launch(sq, sB, heavy, oh)   # the long queries first: a CU each
+            launch(mq, sA, light, ol)
+            torch.cuda.synchronize()
+            t_split = time.perf_counter() - t0
+        for k in ref:
+            assert torch.equal(oh[k], ref[k][torch.as_tensor(heavy, device="cuda")]), k
+            assert torch.equal(ol[k], ref[k][torch.as_tensor(light, device="cuda")]), k
+        rec.update({"tail_sq": K, "launch_s_with_tail_on_single_query_engine": t_split,
+                    "heavy_expansions": int(oh["nexp"].sum().item()), "all_expansions": int(ref["nexp"].sum().item())})
+    assert (ref["status"] == 0).all()
+    for c in ctxs:
+        L.pmp_destroy(c)
+    print(json.dumps(rec))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--strong-share", default="",
+                    help="diagnostic R/N: rank R's share of C2 under the N-rank strong split on this GPU (c2_share_mode)")
+    ap.add_argument("--tail-sq", type=int, default=0,
+                    help="with --strong-share: the K longest queries on the single-query engine on a second stream")
     ap.add_argument("--nq", type=int, default=4096)
     ap.add_argument("--cpu-sample", type=int, default=4096, help="queries in the CPU-baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="minimum CPU-baseline wall time of the short legs")
@@ -1785,6 +1934,8 @@ def main():
         args.residency = 60 if args.engine else 18
     if not args.batches_per_launch and args.engine == 0:
         args.batches_per_launch = 1
+    if args.strong_share:
+        return c2_share_mode(args)
 
     from python_motion_planning_amd import shard
 
@@ -1868,7 +2019,9 @@ def main():
 
     # warmup: every lane once (the first launch also records the deterministic push/pop/expansion counts);
     # its launches are smaller than the timed ones, so the profile keys them apart
-    wb = max(1, min(B, args.warmup))
+    # (at least as many batches as the launch has query slots: a launch that first-touches the ~150 GB
+    # of per-slot scratch runs ~1.3 s slower, tools/ab_headline.py)
+    wb = max(1, min(B, max(args.warmup, -(-args.workers // nq) if args.engine else 1)))
     _LABEL[0] = "astar2d_c2_warmup"
     step(0, wb, ctr.data_ptr())
     for i in range(1, S):
@@ -2019,13 +2172,15 @@ def main():
                                    if args.scaling == "weak" else
                                    f"C2 batched A* 1024x1024 Grid, one {args.nq}-pair batch split over the GPUs",
                        "grid": [W, H], "queries_per_gpu": nq, "parallelism": f"query-sharded x{world}"},
-            "roofline": with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                                      "algorithmic_bytes_per_launch": bytes_per_launch,
-                                      # launches in flight overlap: bytes of one batch per step interval
-                                      "achieved_aggregate": bytes_per_batch / (elapsed / args.steps) / 1e9,
-                                      "frac_aggregate": bytes_per_batch / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS},
-                                     "astar2d_kernel", f"astar2d_c2_x{B}"),
+            "roofline": with_issue(with_traffic({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                                                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                                                 "algorithmic_bytes_per_launch": bytes_per_launch,
+                                                 # launches in flight overlap: bytes of one batch per step interval
+                                                 "achieved_aggregate": bytes_per_batch / (elapsed / args.steps) / 1e9,
+                                                 "frac_aggregate": bytes_per_batch / (elapsed / args.steps) / 1e9
+                                                                   / HBM_PEAK_GBS},
+                                                "astar2d_kernel", f"astar2d_c2_x{B}"),
+                                   "astar2d_kernel", f"astar2d_c2_x{B}", float(counters[:, 2].sum()) * B, "expansion"),
             "cpu_baseline": cpu,
             "secondary": secondary,
             "detail": {"kernel_ms_per_launch": kern_ms,

@@ -8,6 +8,10 @@
                                  MI355X_MICROARCH.md (FETCH_SIZE counts half the bytes of wide streaming
                                  reads: doubled; WRITE_SIZE as is; both in KiB)
   pmc_mfma.json               -- MFMA busy cycles of the MPC pass
+  pmc_issue.json              -- the SQ issue pass (SQ_INSTS_VALU / SALU / LDS, wave cycles, GRBM_GUI_ACTIVE)
+                                 per dispatch, keyed per workload: valu_issue_frac = VALU instructions over
+                                 1024 SIMDs x (GRBM_GUI_ACTIVE / 8 XCDs) / 2 (one wave64 VALU instruction per
+                                 2 cycles per SIMD, MI355X_MICROARCH.md)
 A kernel whose dispatch count in a database differs from its manifest total is not attributed (its
 workload entries are left out, so bench.py reports traffic null rather than a mis-keyed number).
 usage: python tools/prof_summary.py gpurun_out profiles/r3
@@ -103,6 +107,7 @@ def main(src, dst):
     if os.path.exists(kt):
         kernel_stats(kt, dst, load_manifest(os.path.join(src, "prof_kt", "detail.json")))
     traffic_and_mfma(src, dst)
+    issue(src, dst)
 
 
 def kernel_stats(kt, dst, manifest):
@@ -218,6 +223,56 @@ def traffic_and_mfma(src, dst):
 
 
 XCDS, SIMDS = 8, 256 * 4
+ISSUE_COUNTERS = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_ANY",
+                  "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAVES", "GRBM_GUI_ACTIVE")
+
+
+def issue(src, dst):
+    """The SQ issue pass (tools/profile_round.sh, prof_issue): per dispatch sums of each counter, keyed
+    per workload through the launch manifest like the traffic passes."""
+    path = os.path.join(src, "prof_issue", "run_results.db")
+    if not os.path.exists(path):
+        return
+    manifest = load_manifest(os.path.join(src, "prof_issue", "detail.json"))
+    workloads, unattributed = {}, {}
+    for counter in ISSUE_COUNTERS:
+        seq, _ = pmc_dispatches(path, counter)
+        if not seq or not manifest:
+            continue
+        per, bad = attribute(seq, manifest)
+        if bad:
+            unattributed[counter] = bad
+        for label, recs in per.items():
+            ks = {k for k, _ in recs}
+            for k in ks:
+                v = [x for kk, x in recs if kk == k]
+                key = label if len(ks) == 1 else f"{label}:{k}"
+                e = workloads.setdefault(key, {"kernel": k})
+                e[f"{counter}_per_dispatch"] = sum(v) / len(v)
+                e["dispatches"] = len(v)
+    for e in workloads.values():
+        valu, grbm = e.get("SQ_INSTS_VALU_per_dispatch"), e.get("GRBM_GUI_ACTIVE_per_dispatch")
+        if valu is not None and grbm:
+            cycles = grbm / XCDS
+            e["gpu_cycles_per_dispatch"] = cycles
+            e["valu_issue_frac"] = valu / (SIMDS * cycles / 2.0)
+        wc = e.get("SQ_WAVE_CYCLES_per_dispatch")
+        if wc:
+            for c, name in (("SQ_ACTIVE_INST_ANY", "wave_issue_frac"), ("SQ_WAIT_ANY", "wave_wait_frac"),
+                            ("SQ_WAIT_INST_ANY", "wave_issue_stall_frac")):
+                if e.get(f"{c}_per_dispatch") is not None:
+                    e[name] = e[f"{c}_per_dispatch"] / wc
+    out = {"workloads": workloads, "unattributed": unattributed,
+           "_note": ("per dispatch sums of the SQ issue pass (one rocprofv3 --pmc run of the short bench, the default "
+                     "per-launch batch counts); valu_issue_frac = SQ_INSTS_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 "
+                     "XCDs / 2): one wave64 VALU instruction per 2 cycles per SIMD (f64 and 64-bit-shift instructions "
+                     "take longer, so this is a lower bound on the VALU pipe's busy time); wave_*_frac over "
+                     "SQ_WAVE_CYCLES (all in quad-cycles, ratios unaffected)")}
+    with open(os.path.join(dst, "pmc_issue.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    print("issue", {k: round(v.get("valu_issue_frac", 0.0), 4) for k, v in workloads.items()})
+    if unattributed:
+        print("issue: not attributed (seen, manifest):", unattributed)
 
 
 def mfma_util(mf):
