@@ -1928,10 +1928,13 @@ def main():
     # blocks) -- 15,360 groups in flight, 60 per CU = 3.75 waves per SIMD (round 4, same box,
     # alternating, three rounds: 56 / 60 / 64 per CU 17.38-17.41 k / 17.70-17.82 k / 16.69-18.06 k
     # plans/s; before the block layout 56 was best); engine 0 -- 768 waves, 18 per CU (round 2)
+    # round 6 (tiled cell states): 56 per CU, 14,336 groups -- the LDS share then holds 127 heap positions,
+    # exactly levels 0-6, so the spill starts at a level boundary (56 / 60 / 64 per CU: 19.04-19.16 k /
+    # 18.56-18.72 k / 18.65 k plans/s on one box, tools/calls/r6_call8.sh, r6_call9.sh)
     if not args.workers:
-        args.workers = 15360 if args.engine else 768
+        args.workers = 14336 if args.engine else 768
     if not args.residency:
-        args.residency = 60 if args.engine else 18
+        args.residency = 56 if args.engine else 18
     if not args.batches_per_launch and args.engine == 0:
         args.batches_per_launch = 1
     if args.strong_share:

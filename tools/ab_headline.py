@@ -39,8 +39,9 @@ def main():
     ap.add_argument("--warmup-batches", type=int, default=5,
                     help="the first launch on a fresh context: >= workers / 4096 batches touches every slot's "
                          "scratch (a launch that first-touches ~150 GB runs ~1.3 s slower)")
-    ap.add_argument("--workers", type=int, default=15360)
-    ap.add_argument("--residency", type=int, default=60)
+    ap.add_argument("--workers", type=int, default=14336)
+    ap.add_argument("--residency", type=int, default=56)
+    ap.add_argument("--prio", type=int, default=64)
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     import torch
@@ -75,7 +76,7 @@ def main():
             chk(L.pmp_astar2d_set_engine(ctx, 1, 1), "engine")
             chk(L.pmp_astar2d_reserve(ctx, W, H, args.workers, 0), "reserve")
             chk(L.pmp_astar2d_set_schedule(ctx, 1), "schedule")
-            chk(L.pmp_astar2d_set_priority(ctx, 64), "priority")
+            chk(L.pmp_astar2d_set_priority(ctx, args.prio), "priority")
             chk(L.pmp_astar2d_set_residency(ctx, args.residency), "residency")
 
             def launch(nb):
