@@ -371,10 +371,11 @@ def test_residency_batches_in_flight(eng, per_cu):
         L.pmp_destroy(b["ctx"])
 
 
-def test_c2_headline_schedule_against_oracle():
-    """The bench's headline schedule (engine 2, 15,360 groups = 60 per CU, several batches streamed
-    through one launch longest first): two copies of the 4096 C2 queries in one launch, every query
-    bit-exact vs the oracle."""
+@pytest.mark.parametrize("per_cu", [56, 60], ids=["56_per_cu", "60_per_cu"])
+def test_c2_headline_schedule_against_oracle(per_cu):
+    """The bench's headline schedule (engine 2, 14,336 groups = 56 per CU since round 6, and round 5's
+    60 per CU; several batches streamed through one launch longest first): two copies of the 4096 C2
+    queries in one launch, every query bit-exact vs the oracle."""
     import torch
 
     from python_motion_planning_amd import _lib, batch
@@ -385,8 +386,8 @@ def test_c2_headline_schedule_against_oracle():
     L, ctx = _lib.load_library(), _lib.context()
     try:
         _lib.check(ctx, L.pmp_astar2d_set_engine(ctx, 1, 1), "engine")
-        _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, 15360, 0), "reserve")
-        _lib.check(ctx, L.pmp_astar2d_set_residency(ctx, 60), "residency")
+        _lib.check(ctx, L.pmp_astar2d_reserve(ctx, W, H, 256 * per_cu, 0), "reserve")
+        _lib.check(ctx, L.pmp_astar2d_set_residency(ctx, per_cu), "residency")
         r = batch.astar2d_batch(occ, np.tile(starts, (2, 1)), np.tile(goals, (2, 1)), path_cap=4096, counters=True)
         torch.cuda.synchronize()
         _assert_c2_equal(ref, r, copies=2)
