@@ -313,12 +313,12 @@ __global__ __launch_bounds__(64) void astar2d_sq_kernel(
     typename SqGrid<LDSG>::Cst cst;
     typename SqGrid<LDSG>::Gv G;
     uint32_t ep = 1u;
-    // cell-state byte of (x, y): row-major in the LDS grid block, tiled in the per-slot HBM states
-    // shared with the multi-query engine (cst_idx)
-    const uint32_t tH = (uint32_t)(H + 15) >> 4;
-    auto cidx = [&](int x, int y) -> uint32_t {
-        return LDSG ? (uint32_t)x * (uint32_t)H + (uint32_t)y : cst_idx(x, y, tH);
-    };
+    // cell-state byte of (x, y): row-major, in the LDS grid block and in the per-slot HBM states it
+    // shares with the multi-query engine (which tiles them, cst_idx: a query only reads bytes of its
+    // own epoch, written by itself, so engines with different layouts can share a slot; the tiled
+    // index costs this latency-bound single wave 4 % on a C2 query and gains it nothing -- one query's
+    // states stay in L2)
+    auto cidx = [&](int x, int y) -> uint32_t { return (uint32_t)x * (uint32_t)H + (uint32_t)y; };
     if constexpr (LDSG) {
         unsigned char* gb = smem + (size_t)12 * lds_cap;
         lds_u32* ow = (lds_u32*)gb;

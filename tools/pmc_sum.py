@@ -7,7 +7,9 @@ import sys
 out, sub = sys.argv[1], sys.argv[2]
 units = float(sys.argv[3]) if len(sys.argv) > 3 else 0.0
 tot = {}
-for db in glob.glob(f"{out}/**/*.db", recursive=True) + glob.glob(f"{out}/*.db"):
+# (round 6: "**/*.db" with recursive=True already matches the top directory's databases; the round-5
+# version also globbed "*.db" and counted those twice -- the 2x of profiles/r5/pmc_mq_issue_r5.txt)
+for db in sorted(set(glob.glob(f"{out}/**/*.db", recursive=True))):
     d = sqlite3.connect(db)
     for name, cn, v in d.execute("select kernel_name, counter_name, value from counters_collection"):
         if sub in name:
