@@ -17,7 +17,7 @@ cd /tmp && export TMPDIR=/tmp
 SHORT="--no-cpu-baseline --warmup 1 --rrt-steps 1 --track-steps 1 --control-steps 2 --graph-steps 12 --dstar-steps 2 --dyn3d-steps 6"
 # PASSES=kt / pmc / issue / all (separate gpurun calls fit the per-call limit better than one)
 P=${PASSES:-all}
-[ "$P" = pmc ] || [ "$P" = issue ] || timeout -k 10 700 rocprofv3 --kernel-trace --stats -d $OUT/prof_kt -o run -- python3 $R/bench.py \
+[ "$P" = pmc ] || [ "$P" = issue ] || timeout -k 10 700 rocprofv3 --kernel-trace --stats -d $OUT/prof_kt -o run -- python3 $R/bench.py --steps 20 --warmup 5 \
     --detail-out $OUT/prof_kt/detail.json > $OUT/bench_prof.json 2> $OUT/bench_prof.err
 if [ "$P" = pmc ] || [ "$P" = all ]; then
 timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE -d $OUT/prof_fetch -o run -- python3 $R/bench.py $SHORT \
