@@ -224,6 +224,15 @@ constexpr bool kBlocks2 = PMP_MQ_BLOCKS == 2;
 #define PMP_MQ_BPERM 1
 #endif
 constexpr int kMirror = PMP_MQ_MIRROR;
+// Push pairs (round 6): a group whose next two pending pushes land at sibling positions (n, n + 1
+// with n odd) runs both in one path operation -- the second _siftdown walks the same ancestors.
+// Parity-green (tests/test_heap_path_form.py models it against heapq; the GPU suite passed with it
+// on) but neutral on the headline: 19,129 vs 19,167 plans/s without (tools/calls/r6_call13.sh,
+// interleaved): 7 % fewer path operations, each heavier, on a step that waits on memory.  Off.
+#ifndef PMP_MQ_PAIR
+#define PMP_MQ_PAIR 0
+#endif
+constexpr bool kPair = PMP_MQ_PAIR != 0;
 
 // byte offset of spilled heap position p (>= cap) in the wave's spill region
 __device__ __forceinline__ uint32_t spill_off(const GHeap& h, int p)
@@ -476,7 +485,8 @@ __device__ __forceinline__ void pop_leaf(const GHeap& h, const Walk& wk, int n, 
 template <bool T2LDS, int HEUR>
 __device__ __forceinline__ int path_op(const GHeap& h, lmask mon, lmask mpop, uint32_t Q, int Kd, int n, double Xf, uint32_t Xc,
                                        uint32_t Xk, int gl, int gb, double& lastf, uint32_t& lastc, uint32_t& lastk,
-                                       double& rootf, uint32_t& rootc, double& nf, uint32_t& nc, uint32_t& nk, uint32_t cwL)
+                                       double& rootf, uint32_t& rootc, double& nf, uint32_t& nc, uint32_t& nk, uint32_t cwL,
+                                       lmask mpair = 0ull, double X2f = 0.0, uint32_t X2c = 0u, uint32_t X2k = 0u)
 {
     // the lane predicates as lane masks (scalar logic, lm / lb): the step is VALU-issue-bound
     const bool lvl = gl <= Kd;
@@ -486,6 +496,7 @@ __device__ __forceinline__ int path_op(const GHeap& h, lmask mon, lmask mpop, ui
     const lmask mlda = mon & ((mpop & mlvl & kLanesGe1) | (~mpop & lm(gl < Kd)));
     const bool lda = lb(mlda);
     const bool l15 = lb(mon & mpop & kLane15);  // a pop's lane 15: heap[n - 1], the new last
+    const bool p15 = kPair && lb(mpair & kLane15);  // a push pair's lane 15: the second leaf, position n + 1
     const int si = ((q - 1) ^ 1) + 1;
     const lmask mhass = mon & kLanesGe1 & mlvl & lm(si < n);
     const bool hass = lb(mhass);
@@ -498,10 +509,10 @@ __device__ __forceinline__ int path_op(const GHeap& h, lmask mon, lmask mpop, ui
     {
         Ld la, ls;
         if (kLaneConst) {
-            const uint32_t cwK = bp(cwL, gb + (31 - __clz(n > 0 ? n : 1)));
-            // the offset of q (of n - 1 on a pop's lane 15, which stores nothing); only the lanes whose
-            // value the operation uses load
-            offq = spill_off_cw(h, l15 ? cwK : cwL, l15 ? n - 1 : q);
+            const uint32_t cwK = bp(cwL, gb + (p15 ? Kd : 31 - __clz(n > 0 ? n : 1)));
+            // the offset of q (of n - 1 on a pop's lane 15, which stores nothing; of n + 1, the pair's
+            // second leaf, on a pair's lane 15); only the lanes whose value the operation uses load
+            offq = spill_off_cw(h, (l15 || p15) ? cwK : cwL, l15 ? n - 1 : (p15 ? n + 1 : q));
             la.issue_off(h, lda ? q : (l15 ? n - 1 : 0), offq);
             ls.issue_off(h, hass ? si : 0, offq ^ sib_xor(cwL));
         } else {
@@ -543,19 +554,53 @@ __device__ __forceinline__ int path_op(const GHeap& h, lmask mon, lmask mpop, ui
     nc = atb ? Xc : (shift ? (pop ? upc : dnc) : Vc);
     nk = atb ? Xk : (shift ? (pop ? upk : dnk) : Vk);
 #endif
-    const bool stq = lb(mon & mchg & mlvl);
-    if (kLaneConst) hst_off(h, stq, q, offq, nf, nc, nk, pop ? 4 : 2);
-    else hst(h, stq, q, nf, nc, nk, pop ? 4 : 2);
+    // ---- a push pair: the second item X2 goes in at position n + 1, the sibling of the first's, so
+    // CPython's _siftdown walks the same ancestors, which now hold the first push's result: X2 lands
+    // at the top of the chain's run of levels greater than it (b2 <= Kd - 1; the chain is ordered),
+    // those levels move down one, and the chain's old bottom (or X2 itself, cnt2 = 0) becomes the
+    // new leaf, which lane 15 holds and stores.  The first leaf stays on lane Kd.
+    int bst = b;  // the first level the operation rewrote
+    lmask mchg2 = mchg;
+    if (kPair && mpair) {
+        const int cnt2 = __popc((uint32_t)((mpair & lm(gl < Kd) & key_lt_m(X2f, X2k, nf, nk)) >> gb) & 0xFFFFu);
+        const int b2 = Kd - cnt2;
+        // lane L takes lane L - 1's chain value (L > b2), lane 15 the chain's bottom (lane Kd - 1);
+        // gl = 0 never shifts (b2 >= 0), so its wrapped source is never used
+        const int src2 = gb + (gl == 15 ? Kd - 1 : gl - 1);
+        const double shf2 = bpf(nf, src2);
+        const uint32_t shc2 = bp(nc, src2), shk2 = bp(nk, src2);
+        const bool at2 = lb(mpair & lm(gl == b2) & lm(gl < Kd)) || (p15 && cnt2 == 0);
+        const bool sh2 = lb(mpair & lm(gl > b2) & lm(gl < Kd)) || (p15 && cnt2 > 0);
+        nf = at2 ? X2f : (sh2 ? shf2 : nf);
+        nc = at2 ? X2c : (sh2 ? shc2 : nc);
+        nk = at2 ? X2k : (sh2 ? shk2 : nk);
+        if (lb(mpair)) bst = b2 < b ? b2 : b;
+        mchg2 = (mchg & ~mpair) | (mpair & lm(gl >= bst));
+    }
+    const bool stq = lb((mon & mchg2 & mlvl) | (kPair ? mpair & kLane15 : 0ull));
+    const int qs = p15 ? n + 1 : q;
+    if (kLaneConst) hst_off(h, stq, qs, offq, nf, nc, nk, pop ? 4 : 2);
+    else hst(h, stq, qs, nf, nc, nk, pop ? 4 : 2);
     // the bits of the changed levels' parents: lane L (>= 1) sets its parent's from its new content
     // and its sibling's: bit = !(left < right), an odd position is the left child (choice_bit_k)
     {
+        lmask mbit = mhass & mchg2;
+        if (kPair && mpair) {
+            // a pair's first leaf (lane Kd, a left child) has the second leaf (lane 15) as its sibling
+            const double lf2 = bpf(nf, gb + 15);
+            const uint32_t lk2 = bp(nk, gb + 15);
+            const lmask mkd = mpair & lm(gl == Kd);
+            Sf = lb(mkd) ? lf2 : Sf;
+            Sk = lb(mkd) ? lk2 : Sk;
+            mbit |= mkd;
+        }
         const bool fe = nf == Sf;
         const lmask lt_ns = lm(nf < Sf) | (lm(fe) & lm(nk < Sk));
         const lmask lt_sn = lm(nf > Sf) | (lm(fe) & lm(nk > Sk));
         const lmask modd = lm((q & 1) != 0);
         const bool bit = lb((modd & ~lt_ns) | (~modd & ~lt_sn));
-        if (T2LDS) bit_set_lane(h, lb(mhass & mchg), gl, Q >> (Kd - gl + 1), bit);
-        else bit_set<T2LDS>(h, lb(mhass & mchg), gl - 1, Q >> (Kd - gl + 1), bit);
+        if (T2LDS) bit_set_lane(h, lb(mbit), gl, Q >> (Kd - gl + 1), bit);
+        else bit_set<T2LDS>(h, lb(mbit), gl - 1, Q >> (Kd - gl + 1), bit);
     }
     {
         // selects, not a branch (every lane computes them): root = level 0's new content; the last
@@ -563,7 +608,7 @@ __device__ __forceinline__ int path_op(const GHeap& h, lmask mon, lmask mpop, ui
         // heap[n] (level Kd)
         const double r0f = bcf<0>(nf);
         const uint32_t r0c = bc<0>(nc);
-        const int src = gb + (pop ? 15 : Kd);
+        const int src = gb + ((pop || p15 || (kPair && lb(mpair))) ? 15 : Kd);
         const double lf = bpf(pop ? Vf : nf, src);
         const uint32_t lc = bp(pop ? Vc : nc, src), lk = bp(pop ? Vk : nk, src);
         const bool setl = lb(mon & ~(mpop & lm(b == Kd && Q == (uint32_t)n)));
@@ -574,7 +619,7 @@ __device__ __forceinline__ int path_op(const GHeap& h, lmask mon, lmask mpop, ui
         lastk = setl ? lk : lastk;
     }
     wave_sync_mem();
-    return b;
+    return bst;
 }
 
 // THETA: 1 = ThetaStar (theta_star.py:44-108), 2 = LazyThetaStar (lazy_theta_star.py:38-114), with
@@ -649,7 +694,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
     // y + i%3 - 1) (tiled cell states, cst_idx); lane 12 G[pusher]; THETA: lane 13 the pusher's CLOSED parent
     const int blk_dx = gl < 9 ? gl / 3 - 1 : 0;
     const int blk_dy = gl < 9 ? gl % 3 - 1 : 0;
-    const uint32_t tH = (uint32_t)(H + 15) >> 4;
+    const uint32_t tH = cst_tiles_y(H);
 
     // group state (equal across the row)
     uint32_t ep = epoch_all[slot];
@@ -798,6 +843,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
         double gpar = 0.0;
         uint32_t ppar = 0u;  // THETA: Pc[pusher] (lane 13)
         Ld pld;
+        // a push pair: the next two pending pushes, the first at an odd position (its sibling next);
+        // heaps of >= 16 entries, so no cached parent (of positions <= n0 + 7) is a new leaf
+        const uint32_t pend2 = pend & (pend - 1u);
+        const lmask Mpair = kPair ? (Mpush & lm(pend2 != 0u) & lm((n & 1) != 0) & lm(n >= 16)) : 0ull;
+        double X2f = 0.0;
+        uint32_t X2c = 0u, X2k = 0u;
         if (push) {
             const int m = __ffs((int)pend) - 1;
             Xf = bpf(ifv, gb + m);
@@ -805,6 +856,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
             Xk = bp(ikk, gb + m);
             Q = (uint32_t)n + 1u;
             Kd = 31 - __clz((int)Q);
+            if (kPair) {
+                const int m2 = __ffs((int)pend2) - 1;  // (garbage lanes without a pair never use it)
+                X2f = bpf(ifv, gb + (m2 & 7));
+                X2c = bp(icm, gb + (m2 & 7));
+                X2k = bp(ikk, gb + (m2 & 7));
+            }
         }
         if (pop) {
             // ---- heappop (a_star.py:54), with the 3x3 round and the parent prefetch issued first
@@ -847,7 +904,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
         uint32_t nc = 0u, nk = 0u;
         int b = 0;
         b = path_op<T2LDS, HEUR>(hp, Mop, Mpop, Q, Kd, n, Xf, Xc, Xk, gl, gb, lastf, lastc, lastk, rootf, rootc, nf, nc,
-                                 nk, cwL);
+                                 nk, cwL, Mpair, X2f, X2c, X2k);
         {
             double f8;
             uint32_t c8, k8;
@@ -867,9 +924,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
             pf8 = onpath ? af : pf8;
             pk8 = onpath ? ak : pk8;
         }
-        pend = push ? pend & (pend - 1u) : pend;
-        n += push ? 1 : 0;
-        npush += push ? 1 : 0;
+        {
+            const bool pr = lb(Mpair);
+            pend = push ? (pr ? pend2 & (pend2 - 1u) : pend2) : pend;
+            n += push ? (pr ? 2 : 1) : 0;
+            npush += push ? (pr ? 2 : 1) : 0;
+        }
 
         // ---- 3. the popped node: 3x3 masks (bit k = cell (x + k/3 - 1, y + k%3 - 1)), CLOSED test,
         //      goal test, getNeighbor (a_star.py:57-82)

@@ -141,13 +141,23 @@ __device__ __forceinline__ bool lb(lmask m) { return __builtin_amdgcn_inverse_ba
 // cells: a tile is one 128-B line, so the 3x3 round of an expansion touches ~1.4 lines on average
 // instead of one per grid row x-1, x, x+1 (the row-major layout, x * H + y), and an A* front's
 // cells share lines in both directions.  tH = tiles along y.
+#ifndef PMP_CST_TX
+#define PMP_CST_TX 3  // log2 tile width along x
+#endif
+#ifndef PMP_CST_TY
+#define PMP_CST_TY 4  // log2 tile height along y
+#endif
+constexpr int kCstTx = PMP_CST_TX, kCstTy = PMP_CST_TY;
 __host__ __device__ inline size_t cst_tiled_bytes(int W, int H)
 {
-    return (size_t)((W + 7) >> 3) * (size_t)((H + 15) >> 4) * 128u;
+    return (size_t)((W + (1 << kCstTx) - 1) >> kCstTx) * (size_t)((H + (1 << kCstTy) - 1) >> kCstTy) *
+           ((size_t)1 << (kCstTx + kCstTy));
 }
+__device__ __forceinline__ uint32_t cst_tiles_y(int H) { return (uint32_t)(H + (1 << kCstTy) - 1) >> kCstTy; }
 __device__ __forceinline__ uint32_t cst_idx(int x, int y, uint32_t tH)
 {
-    return (((uint32_t)x >> 3) * tH + ((uint32_t)y >> 4)) * 128u + (((uint32_t)x & 7u) << 4) + ((uint32_t)y & 15u);
+    return ((((uint32_t)x >> kCstTx) * tH + ((uint32_t)y >> kCstTy)) << (kCstTx + kCstTy)) +
+           (((uint32_t)x & ((1u << kCstTx) - 1u)) << kCstTy) + ((uint32_t)y & ((1u << kCstTy) - 1u));
 }
 
 // Correctly rounded sqrt of an integer 0 <= k < 2^31: the operation sequence of LLVM's f64 sqrt

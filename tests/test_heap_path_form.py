@@ -83,6 +83,38 @@ class PathHeap:
         Q = n + 1
         self._path_op(False, Q, Q.bit_length() - 1, n, x)
 
+    def push_pair(self, x1, x2):
+        """astar2d_mq.hip's push pair (round 6): the first push at position n (odd: a left child) and
+        the second at n + 1, its sibling, in one operation -- the second insertion runs on the chain
+        (levels 0..Kd-1) the first produced, X2 at the top of the chain's run of levels greater than
+        it, the chain's old bottom (or X2) in the new leaf; the first leaf's parent bit compares the
+        two leaves."""
+        n = len(self.a)
+        assert n % 2 == 1
+        Q = n + 1
+        Kd = Q.bit_length() - 1
+        q = [(Q >> (Kd - L)) - 1 for L in range(Kd + 1)]
+        V = [self.a[p] if p < n else None for p in q]
+        b = Kd - sum(1 for L in range(Kd) if lt(x1, V[L]))
+        new = [x1 if L == b else (V[L - 1] if L > b else V[L]) for L in range(Kd + 1)]
+        cnt2 = sum(1 for L in range(Kd) if lt(x2, new[L]))
+        b2 = Kd - cnt2
+        chain = [x2 if L == b2 else (new[L - 1] if L > b2 else new[L]) for L in range(Kd)] + [new[Kd]]
+        leaf2 = new[Kd - 1] if cnt2 > 0 else x2
+        bst = min(b, b2)
+        self.a.extend([None, None])
+        for L in range(bst, Kd + 1):
+            self.a[q[L]] = chain[L]
+        self.a[n + 1] = leaf2
+        for L in range(max(1, bst), Kd):
+            s = ((q[L] - 1) ^ 1) + 1
+            if s < n:
+                self._set_bit(q[L - 1], (q[L], chain[L]), self.a[s])
+        self._set_bit(q[Kd - 1], (q[Kd], chain[Kd]), leaf2)
+        self.root = chain[0]
+        self.last = leaf2
+        return bst
+
     def pop_leaf(self, n):
         """_siftup's leaf from the bits: levels 0..D-2 unconditionally, then one conditional step."""
         D = n.bit_length() - 1
@@ -135,3 +167,37 @@ def test_path_form_equals_cpython_heapq():
             if ref:
                 assert ph.root is ref[0] and ph.last is ref[-1], (trial, step)
             check_bits(ph)
+
+
+def test_push_pairs_equal_two_cpython_heappushes():
+    """The multi-query kernel's push pairs (two pending pushes at sibling positions n, n + 1 in one
+    path operation, heaps of >= 16 entries) against two heapq.heappush calls, interleaved with pops
+    and single pushes: array, bits, root and last after every operation."""
+    rng = random.Random(11)
+    pairs = 0
+    for trial in range(60):
+        ref, ph = [], PathHeap()
+        tag = 0
+        for step in range(rng.randint(100, 1500)):
+            n = len(ref)
+            r = rng.random()
+            if ref and r < 0.4:
+                assert heapq.heappop(ref) is ph.pop(), (trial, step)
+            elif n >= 16 and n % 2 == 1 and r < 0.8:
+                x1 = Item(float(rng.randint(0, 12)), rng.randint(0, 3), tag)
+                x2 = Item(float(rng.randint(0, 12)), rng.randint(0, 3), tag + 1)
+                tag += 2
+                heapq.heappush(ref, x1)
+                heapq.heappush(ref, x2)
+                ph.push_pair(x1, x2)
+                pairs += 1
+            else:
+                it = Item(float(rng.randint(0, 12)), rng.randint(0, 3), tag)
+                tag += 1
+                heapq.heappush(ref, it)
+                ph.push(it)
+            assert len(ref) == len(ph.a) and all(x is y for x, y in zip(ref, ph.a)), (trial, step)
+            if ref:
+                assert ph.root is ref[0] and ph.last is ref[-1], (trial, step)
+            check_bits(ph)
+    assert pairs > 5000
