@@ -36,6 +36,14 @@ constexpr int kMaxDim = 256;
 #define PMP_L3_MIRROR 0
 #endif
 constexpr int kL3Mirror = PMP_L3_MIRROR;
+// Deferred removes (round 6): U.remove inside one expansion's block leaves a hole instead of shifting
+// the tail; positions stay logical (the reference's list indices) and map to the physical array
+// through the pending holes; the block's end closes every hole in one compaction pass.  0: the
+// round-5 form (every remove shifts the tail at once).
+#ifndef PMP_L3_DEFER
+#define PMP_L3_DEFER 1
+#endif
+constexpr bool kDefer = PMP_L3_DEFER != 0;
 constexpr double kInf = __builtin_huge_val();
 
 __device__ __constant__ int8_t c_m[26][3] = {
@@ -57,9 +65,10 @@ typedef __attribute__((address_space(3))) double lds_f64;
 
 __device__ __forceinline__ void wsync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
+// list `<` on [k1, k2]; branch-free (the short-circuit form compiled to exec-mask branches)
 __device__ __forceinline__ bool key_lt(double a1, double a2, double b1, double b2)
 {
-    return a1 < b1 || (a1 == b1 && a2 < b2);
+    return (a1 < b1) | ((a1 == b1) & (a2 < b2));
 }
 
 // c / d for 0 <= c < 2^24 through an f32 reciprocal (error <= 1 before the correction): a handful
@@ -206,6 +215,11 @@ struct L3 {
     bool touch;
     lds_f64* cube;  // 125 g values of the 5x5x5 block around the centre
     int lane;
+    // kDefer: the holes pending in U's physical array (wave-uniform count hm <= 28 -- the popped node
+    // and the 27 block voxels; lane j < hm holds hole j's boundary b_j = the live entries before it).
+    // Logical position L sits at physical L + #{j : b_j <= L}.
+    int hb;
+    int hm;
     int start, goal;  // voxel ids
     int gx, gy, gz;
     int heur;
@@ -215,7 +229,7 @@ struct L3 {
     double goal_g, goal_rhs;  // the goal's g / rhs, kept in registers for the termination test
 #ifdef PMP_STAMPS
     uint64_t cyc[4];  // diagnostic build: min scan, g block + rhs minima, membership scan, updates
-#define LSTAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define LSTAMP(v) [[maybe_unused]] const uint64_t v = __builtin_amdgcn_s_memtime()
 #else
 #define LSTAMP(v)
 #endif
@@ -267,39 +281,112 @@ struct L3 {
     }
     __device__ __forceinline__ void remove_at(int i, Track& t)
     {
-        if (U.n <= U.cap) remove_at_t<false>(i);
-        else remove_at_t<true>(i);
+        if (kDefer) {  // a hole at logical i: later holes' boundaries past i drop by one
+            if (lane < hm && hb > i) hb -= 1;
+            if (lane == hm) hb = i;
+            hm += 1;
+        } else if (U.n <= U.cap) {
+            remove_at_t<false>(i);
+        } else {
+            remove_at_t<true>(i);
+        }
         U.n -= 1;
         if (t.pos == i) t.pos = -1;
         else if (t.pos > i) t.pos -= 1;
     }
+    // physical index of logical position L (kDefer)
+    __device__ __forceinline__ int phys(int L) const
+    {
+        int P = L;
+        for (int j = 0; j < hm; j++) P += L >= __builtin_amdgcn_readlane(hb, j) ? 1 : 0;
+        return P;
+    }
+    // close every pending hole: logical L takes physical phys(L), ascending from the first hole, 4
+    // entries per lane per round, all loads of a round before its stores (a store goes to L <= its
+    // source, below every later round's sources)
+    template <bool SP>
+    __device__ __forceinline__ void compact_t(int from)
+    {
+        const int n = U.n;
+        for (int base = from; base < n; base += 256) {
+            int L[4], P[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int k = base + lane + 64 * j;
+                L[j] = k < n ? k : n - 1;
+                P[j] = L[j];
+            }
+            for (int h = 0; h < hm; h++) {
+                const int bh = __builtin_amdgcn_readlane(hb, h);
+#pragma unroll
+                for (int j = 0; j < 4; j++) P[j] += L[j] >= bh ? 1 : 0;
+            }
+            int32_t c[4];
+            double a[4], b[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) U.template ld<SP>(P[j], c[j], a[j], b[j]);
+            wsync();
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (base + lane + 64 * j < n && P[j] != L[j]) U.template st<SP>(L[j], c[j], a[j], b[j]);
+            wsync();
+        }
+    }
+    __device__ __forceinline__ void compact()
+    {
+        if (!kDefer || hm == 0) return;
+        int from = U.n;
+        for (int j = 0; j < hm; j++) from = min(from, __builtin_amdgcn_readlane(hb, j));
+        if (U.n + hm <= U.cap) compact_t<false>(from);
+        else compact_t<true>(from);
+        hm = 0;
+    }
 
     // heapq.heappush(U, node): lane j (1..D) loads ancestor j of position n; the ancestors that move
     // down are the run of "new < ancestor" from the parent up (_siftdown stops at the first one that
-    // is not greater).  `me` = this lane tracks the pushed voxel.
+    // is not greater).  `me` = this lane tracks the pushed voxel.  kDefer: lane j (0..D) maps path
+    // position (np1 >> j) - 1 to its physical index first.
     template <bool SP>
     __device__ __forceinline__ int push_t(int32_t c, double k1, double k2, uint32_t np1, int& s)
     {
         const int D = 31 - __clz((int)np1);
         const bool on = lane >= 1 && lane <= D;
         const int aj = on ? (int)(np1 >> lane) - 1 : 0;
+        // kDefer: lane j's path position and the one below it (its store target), both mapped
+        int pj = aj, pdown = 0;
+        if (kDefer) {
+            const int L0 = lane <= D ? (int)(np1 >> lane) - 1 : 0;
+            const int L1 = on ? (int)(np1 >> (lane - 1)) - 1 : 0;
+            pj = L0;
+            pdown = L1;
+            for (int h = 0; h < hm; h++) {
+                const int bh = __builtin_amdgcn_readlane(hb, h);
+                pj += L0 >= bh ? 1 : 0;
+                pdown += L1 >= bh ? 1 : 0;
+            }
+        }
         int32_t ac = 0;
         double a1 = 0.0, a2 = 0.0;
-        if (on) U.template ld<SP>(aj, ac, a1, a2);
+        if (on) U.template ld<SP>(pj, ac, a1, a2);
         const uint64_t lt = ballot(on && key_lt(k1, k2, a1, a2));
         s = __builtin_ctzll(~(lt >> 1));  // trailing ones from lane 1
         wsync();
-        if (on && lane <= s) U.template st<SP>((int)(np1 >> (lane - 1)) - 1, ac, a1, a2);
-        const int dst = (int)(np1 >> s) - 1;
-        if (lane == 0) U.template st<SP>(dst, c, k1, k2);
+        if (kDefer) {
+            if (on && lane <= s) U.template st<SP>(pdown, ac, a1, a2);
+            const int pdst = __builtin_amdgcn_readlane(pj, s);
+            if (lane == 0) U.template st<SP>(pdst, c, k1, k2);
+        } else {
+            if (on && lane <= s) U.template st<SP>((int)(np1 >> (lane - 1)) - 1, ac, a1, a2);
+            if (lane == 0) U.template st<SP>((int)(np1 >> s) - 1, c, k1, k2);
+        }
         wsync();
-        return dst;
+        return (int)(np1 >> s) - 1;
     }
     __device__ __forceinline__ void push(int32_t c, double k1, double k2, Track& t, bool me)
     {
         const uint32_t np1 = (uint32_t)U.n + 1u;
         int s;
-        const int dst = U.n < U.cap ? push_t<false>(c, k1, k2, np1, s) : push_t<true>(c, k1, k2, np1, s);
+        const int dst = U.n + (kDefer ? hm : 0) < U.cap ? push_t<false>(c, k1, k2, np1, s) : push_t<true>(c, k1, k2, np1, s);
         // tracked positions: ancestor j (1..s) -> ancestor j-1
         if (t.pos >= 0) {
             const int p1 = t.pos + 1;
@@ -424,16 +511,20 @@ struct L3 {
         // ---- U positions of the 27 voxels: one scan
         Track t;
         t.pos = -1;
-        const bool usp = U.n > U.cap;
-        for (int base = 0; base < U.n; base += 64) {
+        // kDefer: at most one hole here (the popped node's, expand); the scan walks the physical
+        // array, skips the hole and reports logical positions
+        const int hole = (kDefer && hm) ? __builtin_amdgcn_readlane(hb, 0) : 0x7fffffff;
+        const int nph = U.n + (kDefer ? hm : 0);
+        const bool usp = nph > U.cap;
+        for (int base = 0; base < nph; base += 64) {
             const int k = base + lane;
             int32_t c = -1;
             double a, b;
             {
-                const int kk = k < U.n ? k : U.n - 1;  // an unconditional load, the result masked
+                const int kk = k < nph ? k : nph - 1;  // an unconditional load, the result masked
                 if (usp) U.template ld<true>(kk, c, a, b);
                 else U.template ld<false>(kk, c, a, b);
-                if (k >= U.n) c = -1;
+                if (k >= nph || k == hole) c = -1;
             }
             // block index of c relative to the centre, or -1
             int bi = -1;
@@ -447,9 +538,9 @@ struct L3 {
             while (hits) {
                 const int l = __ffsll((long long)hits) - 1;
                 hits &= hits - 1;
-                const int hb = __builtin_amdgcn_readlane(bi, l);
+                const int hbi = __builtin_amdgcn_readlane(bi, l);
                 const int myb = (dx + 1) * 9 + (dy + 1) * 3 + (dz + 1);
-                if (lane <= 26 && myb == hb) t.pos = base + l;
+                if (lane <= 26 && myb == hbi) t.pos = base + l - (base + l > hole ? 1 : 0);
             }
         }
         LSTAMP(t2);
@@ -470,11 +561,18 @@ struct L3 {
             const double gw = rl_f64(gv, who);
             if (Pw == goal) goal_rhs = rw;
             const int pw = __builtin_amdgcn_readlane(t.pos, who);
+            LSTAMP(u0);
             if (pw >= 0) remove_at(pw, t);
+            LSTAMP(u1);
             if (gw != rw) {
                 const double mn = gw < rw ? gw : rw;
                 push(Pw, mn + rl_f64(hv, who), mn, t, lane == who);
             }
+#if defined(PMP_STAMPS) && PMP_STAMPS == 2
+            LSTAMP(u2);
+            cyc[0] += u1 - u0;
+            cyc[1] += u2 - u1;
+#endif
         }
         // deferred stores: the updated voxels' rhs (the start keeps its own), the centre's new g
         {
@@ -493,8 +591,14 @@ struct L3 {
                 mark(gt, center);
             }
         }
+        LSTAMP(tc);
+        compact();
         wsync();
-#ifdef PMP_STAMPS
+#if defined(PMP_STAMPS) && PMP_STAMPS == 2  // remove, push, compaction, the whole block
+        LSTAMP(t3);
+        cyc[2] += t3 - tc;
+        cyc[3] += t3 - t0;
+#elif defined(PMP_STAMPS)
         LSTAMP(t3);
         cyc[1] += t1 - t0;
         cyc[2] += t2 - t1;
@@ -533,6 +637,8 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
     S.occ.l = (lds_u32*)(smem + 1024 + (size_t)20 * ucap);
     S.occ.lds = occ_lds != 0;
     S.touch = true;
+    S.hb = 0;
+    S.hm = 0;
     S.gt = bits_all + (size_t)blockIdx.x * 2 * (size_t)words;
     S.rt = S.gt + words;
     S.occ.g = occ_scr + (size_t)blockIdx.x * (size_t)words;
@@ -683,7 +789,7 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
             for (;;) {
                 if (S.U.n == 0) break;
 #ifdef PMP_STAMPS
-                const uint64_t ts = __builtin_amdgcn_s_memtime();
+                [[maybe_unused]] const uint64_t ts = __builtin_amdgcn_s_memtime();
 #endif
                 if (max_exp > 0 && S.nexp >= max_exp) { st = PMP_CAP_OVERFLOW; break; }
                 const double gg = S.goal_g, gr = S.goal_rhs;
@@ -713,7 +819,7 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
                 b2 = rl_f64(b2, 0);
                 const double gm = gg < gr ? gg : gr;
                 // node.key >= calculateKey(goal) and goal.rhs == goal.g (:131-133); h(goal, goal) = 0
-#ifdef PMP_STAMPS
+#if defined(PMP_STAMPS) && PMP_STAMPS != 2
                 S.cyc[0] += __builtin_amdgcn_s_memtime() - ts;
 #endif
                 if (!key_lt(b1, b2, gm + 0.0, gm) && gr == gg) break;

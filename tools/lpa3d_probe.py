@@ -37,8 +37,15 @@ for w in [int(x) for x in (sys.argv[1:] or ["16"])]:
           f"one launch alone)", flush=True)
     if stamps:
         tot = c.sum(axis=0).astype(np.float64)
-        print("  cycle share: min-scan %.3f block+rhs %.3f membership %.3f updates %.3f" % tuple(tot / tot.sum()),
-              flush=True)
+        ne = float(r["n_expanded"].sum().item())
+        if "stamps2" in os.environ.get("PMP_HIP_LIB", ""):
+            print("  ticks per expansion: removes %.0f pushes %.0f compaction %.0f whole block %.0f" % tuple(tot / ne),
+                  flush=True)
+        else:
+            print("  cycle share: min-scan %.3f block+rhs %.3f membership %.3f updates %.3f" % tuple(tot / tot.sum()),
+                  flush=True)
+            print("  ticks per expansion: min-scan %.0f block+rhs %.0f membership %.0f updates %.0f" % tuple(tot / ne),
+                  flush=True)
     else:
         nexp = c[:, 1]
         mx = c[:, 3]
