@@ -594,10 +594,9 @@ struct L3 {
         LSTAMP(tc);
         compact();
         wsync();
-#if defined(PMP_STAMPS) && PMP_STAMPS == 2  // remove, push, compaction, the whole block
+#if defined(PMP_STAMPS) && PMP_STAMPS == 2  // remove, push, the whole block, the whole query
         LSTAMP(t3);
-        cyc[2] += t3 - tc;
-        cyc[3] += t3 - t0;
+        cyc[2] += t3 - t0;
 #elif defined(PMP_STAMPS)
         LSTAMP(t3);
         cyc[1] += t1 - t0;
@@ -692,6 +691,7 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
         S.maxn = 0;
 #ifdef PMP_STAMPS
         S.cyc[0] = S.cyc[1] = S.cyc[2] = S.cyc[3] = 0;
+        const uint64_t tq0 = __builtin_amdgcn_s_memtime();
 #endif
         if (S.start == S.goal) {
             for (int r = 0; r < R1; r++) {
@@ -848,6 +848,14 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
                 if (lane == 0 && len < path_cap) pth[len] = node;
                 len++;
                 int safety = 0;
+                // Brent's cycle detection: the walk's next node is a function of the node alone (g
+                // and the map are fixed here), so a repeated node is a cycle the walk never leaves
+                // and the reference walks on to its 100000-step guard, returning (cost, []).  Once a
+                // cycle of <= 64 steps is found, the steps left repeat its step costs: they are
+                // added in order (the same f64 sums) without the per-step memory rounds (a stuck
+                // C5 query took ~270 ms of one wave walking them).
+                int tort = node, power = 1, lam = 0, ring = 0;
+                bool chk = true, cyc = false;
                 while (node != S.start) {
                     int x, y, z;
                     S.geo.xyz(node, x, y, z);
@@ -872,6 +880,31 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
                     if (lane == 0 && len < path_cap) pth[len] = node;
                     len++;
                     if (++safety >= 100000) { st = PMP_NO_PATH; break; }
+                    if (chk) {
+                        if (lane == (safety & 63)) ring = bm;  // step t's motion at lane t & 63
+                        lam++;
+                        if (node == tort) {
+                            if (lam <= 64) { cyc = true; break; }
+                            chk = false;  // a longer cycle: walk it
+                        } else if (lam == power) {
+                            tort = node;
+                            power <<= 1;
+                            lam = 0;
+                        }
+                    }
+                }
+                if (cyc) {
+                    // cycle step i (0..lam-1) = step safety - lam + 1 + i; the steps left,
+                    // safety + 1 .. 99999 + 1, take them in turn
+                    const int mi = __builtin_amdgcn_ds_bpermute(((safety - lam + 1 + lane) & 63) << 2, ring);
+                    const int mm = lane < lam ? mi : 0;
+                    const double dc = dist_unit(c_m[mm][0], c_m[mm][1], c_m[mm][2]);
+                    int i = 0;
+                    for (int j = safety; j < 100000; j++) {
+                        cost += rl_f64(dc, i);
+                        i = i + 1 == lam ? 0 : i + 1;
+                    }
+                    st = PMP_NO_PATH;
                 }
                 wsync();
                 if (st == 0) {
@@ -895,6 +928,9 @@ __global__ __launch_bounds__(64) void lpa3d_kernel(
         }
         if (counters && lane == 0) {
 #ifdef PMP_STAMPS
+#if PMP_STAMPS == 2
+            S.cyc[3] = __builtin_amdgcn_s_memtime() - tq0;
+#endif
             for (int k = 0; k < 4; k++) counters[4 * q + k] = (int64_t)S.cyc[k];
 #else
             counters[4 * q] = S.npush;

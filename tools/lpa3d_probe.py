@@ -33,13 +33,15 @@ for w in [int(x) for x in (sys.argv[1:] or ["16"])]:
         torch.cuda.synchronize()
         ms.append(e0.elapsed_time(e1))
     c = r["counters"].cpu().numpy()
+    if os.environ.get("PMP_PROBE_OUT"):  # per-query counters and expansions, for offline joins
+        np.savez(os.environ["PMP_PROBE_OUT"], counters=c, n_expanded=r["n_expanded"].cpu().numpy())
     print(f"workers/CU {w}: {np.median(ms):.1f} ms per {rep * nq}-query launch ({rep * nq / np.median(ms) * 1e3:.0f} plans/s "
           f"one launch alone)", flush=True)
     if stamps:
         tot = c.sum(axis=0).astype(np.float64)
         ne = float(r["n_expanded"].sum().item())
         if "stamps2" in os.environ.get("PMP_HIP_LIB", ""):
-            print("  ticks per expansion: removes %.0f pushes %.0f compaction %.0f whole block %.0f" % tuple(tot / ne),
+            print("  ticks per expansion: removes %.0f pushes %.0f whole block %.0f whole query %.0f" % tuple(tot / ne),
                   flush=True)
         else:
             print("  cycle share: min-scan %.3f block+rhs %.3f membership %.3f updates %.3f" % tuple(tot / tot.sum()),
