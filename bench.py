@@ -556,12 +556,19 @@ def rrt_leg(args, torch, dist, world, rank):
     ctr = out["counters"].cpu().numpy()
     status = out["status"].cpu().numpy()
     assert np.isin(status, (0, 1)).all(), f"unexpected RRT* statuses {np.unique(status)}"
-    # batches in flight: one workgroup grows one tree, so a launch lasts as long as its slowest query;
-    # consecutive launches on different streams (own pmp_ctx each) fill the CUs the early finishers free
+    # One workgroup grows one tree and a query's time grows with the square of its iterations
+    # (12 k - 42 k per C3 query: the whole-tree scans), so a 256-query launch lasts as long as its
+    # slowest query.  Continuous batching: --rrt-batches batches of the 256 queries go to the planner
+    # as ONE launch (grid = every query of them, one workgroup per CU at a time), and the hardware
+    # dispatcher hands each CU its next query as its last one finishes; --rrt-streams launches in
+    # flight on their own streams (own pmp_ctx each) overlap the launches' tails.
+    nb = max(1, args.rrt_batches)
+    nql = nq * nb
     L = _lib.load_library()
     rect, circ, bnd = batch.map_arrays(env, torch)
-    s_d = torch.as_tensor(starts, device="cuda")
-    g_d = torch.as_tensor(goals, device="cuda")
+    s_d = torch.as_tensor(np.tile(starts, (nb, 1)), device="cuda")
+    g_d = torch.as_tensor(np.tile(goals, (nb, 1)), device="cuda")
+    rnd_l = rnd_d.repeat(nb, 1) if nb > 1 else rnd_d
     cap = sn + 2
     P = _lib.RRTParams(512.0, 512.0, 0.5, 0.5, 10.0, 0.05, sn, 1)
     lanes = []
@@ -569,10 +576,10 @@ def rrt_leg(args, torch, dist, world, rank):
         f64 = dict(dtype=torch.float64, device="cuda")
         i32 = dict(dtype=torch.int32, device="cuda")
         lanes.append(dict(ctx=L.pmp_create(torch.cuda.current_device()), stream=pool_stream(torch, len(lanes)),
-                          txy=torch.empty((nq, cap, 2), **f64), tg=torch.empty((nq, cap), **f64),
-                          tpar=torch.empty((nq, cap), **i32), nn=torch.empty(nq, **i32), cost=torch.empty(nq, **f64),
-                          plen=torch.empty(nq, **i32), path=torch.empty((nq, cap, 2), **f64),
-                          draws=torch.empty(nq, dtype=torch.int64, device="cuda"), st=torch.empty(nq, **i32)))
+                          txy=torch.empty((nql, cap, 2), **f64), tg=torch.empty((nql, cap), **f64),
+                          tpar=torch.empty((nql, cap), **i32), nn=torch.empty(nql, **i32), cost=torch.empty(nql, **f64),
+                          plen=torch.empty(nql, **i32), path=torch.empty((nql, cap, 2), **f64),
+                          draws=torch.empty(nql, dtype=torch.int64, device="cuda"), st=torch.empty(nql, **i32)))
         if args.rrt_resident > 0:  # the LDS tree share: room for this many workgroups per CU
             _lib.check(lanes[-1]["ctx"], L.pmp_set_resident_per_cu(lanes[-1]["ctx"], args.rrt_resident),
                        "pmp_set_resident_per_cu")
@@ -581,7 +588,7 @@ def rrt_leg(args, torch, dist, world, rank):
         b = lanes[i % len(lanes)]
         rc = L.pmp_rrt_batch(b["ctx"], b["stream"].cuda_stream, ctypes.byref(P), rect.data_ptr(), int(rect.shape[0]),
                              circ.data_ptr(), int(circ.shape[0]), bnd.data_ptr(), int(bnd.shape[0]), s_d.data_ptr(),
-                             g_d.data_ptr(), nq, rnd_d.data_ptr(), int(rnd_d.shape[1]), cap, b["txy"].data_ptr(),
+                             g_d.data_ptr(), nql, rnd_l.data_ptr(), int(rnd_l.shape[1]), cap, b["txy"].data_ptr(),
                              b["tg"].data_ptr(), b["tpar"].data_ptr(), b["nn"].data_ptr(), b["cost"].data_ptr(),
                              b["plen"].data_ptr(), b["path"].data_ptr(), cap, b["draws"].data_ptr(), b["st"].data_ptr(),
                              None)
@@ -591,8 +598,9 @@ def rrt_leg(args, torch, dist, world, rank):
     for i in range(len(lanes)):  # warm every lane's scratch
         launch(i)
     torch.cuda.synchronize()
-    for b in lanes:
-        assert torch.equal(b["nn"], out["n_nodes"]) and torch.equal(b["st"], out["status"])
+    for b in lanes:  # every repeat of the batch equals the warmup's 256 queries
+        assert torch.equal(b["nn"], out["n_nodes"].repeat(nb)) and torch.equal(b["st"], out["status"].repeat(nb))
+        assert torch.equal(b["cost"], out["cost"].repeat(nb)) and torch.equal(b["draws"], out["draws"].repeat(nb))
     rkeys = ("nn", "st", "cost", "plen", "draws")
     ref_out = {k: lanes[0][k].clone() for k in rkeys}
     for b in lanes:
@@ -622,10 +630,10 @@ def rrt_leg(args, torch, dist, world, rank):
     # coordinate copy of the coarse nearest / radius scans) + 24 B per in-radius candidate (exact
     # f64 x, y and g).  The trees (4 B x 65,537 nodes per query) stay in L2 / Infinity Cache, so the
     # roof is the L2 bandwidth (MI355X_MICROARCH.md: ~34.5 TB/s aggregate)
-    alg_bytes = float(4.0 * ctr[:, 1].sum() + 24.0 * ctr[:, 2].sum())
+    alg_bytes = float(4.0 * ctr[:, 1].sum() + 24.0 * ctr[:, 2].sum()) * nb
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     # SURVEY.md §8(d)'s own accounting: 16 B of xy per node scanned + 8 B of g per in-radius node
-    sv_bytes = float(16.0 * ctr[:, 1].sum() + 8.0 * ctr[:, 2].sum())
+    sv_bytes = float(16.0 * ctr[:, 1].sum() + 8.0 * ctr[:, 2].sum()) * nb
     sv_gbs = sv_bytes / (kern_ms * 1e-3) / 1e9
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -641,8 +649,9 @@ def rrt_leg(args, torch, dist, world, rank):
                "sample": f"first {ns} C3 queries at the full 65,536 samples, C restatement of RRT* "
                          f"(oracle/pmp_oracle.c, same O(N^2) loops as the reference) with OpenMP over queries, "
                          f"{dt:.1f} s wall"}
-    return {"metric": "RRT* plans/sec on 512x512 Map, 65536 samples", "value": nq * args.rrt_steps * world / elapsed,
-            "unit": "plans/s", "queries_per_gpu": nq, "steps": args.rrt_steps,
+    return {"metric": "RRT* plans/sec on 512x512 Map, 65536 samples", "value": nql * args.rrt_steps * world / elapsed,
+            "unit": "plans/s", "queries_per_gpu": nq, "steps": args.rrt_steps, "batches_per_launch": nb,
+            "queries_per_launch": nql,
             "ms_per_step": elapsed / args.rrt_steps * 1e3, "kernel_ms_per_launch": kern_ms, "dtype": "f64",
             "streams": len(lanes), "timed_launches_checked": checked,
             "config": {"workload": "C3: Map(512,512), 40 rects + 40 circles (default_rng(7)), (5,5)->(505,505), "
@@ -662,10 +671,12 @@ def rrt_leg(args, torch, dist, world, rank):
                                                     "note": "the kernel's own loads: 4 B per node scanned (16-bit "
                                                             "fixed-point coarse copy) + 24 B per in-radius candidate"}},
                                                 "rrt_kernel", "rrt_star"),
-                                   "rrt_kernel", "rrt_star", float(ctr[:, 0].sum()), "iteration"),
+                                   "rrt_kernel", "rrt_star", float(ctr[:, 0].sum()) * nb, "iteration"),
             "detail": {"found": int((status == 0).sum()), "mean_nodes": float(out["n_nodes"].float().mean().item()),
-                       "iterations_per_launch": int(ctr[:, 0].sum()), "nodes_scanned_per_launch": int(ctr[:, 1].sum()),
-                       "collision_tests_per_launch": int(ctr[:, 3].sum())},
+                       "iterations_per_launch": int(ctr[:, 0].sum()) * nb,
+                       "nodes_scanned_per_launch": int(ctr[:, 1].sum()) * nb,
+                       "collision_tests_per_launch": int(ctr[:, 3].sum()) * nb,
+                       "iterations_per_query_q50_max": [float(np.percentile(ctr[:, 0], 50)), int(ctr[:, 0].max())]},
             "cpu_baseline": cpu}
 
 
@@ -1880,7 +1891,9 @@ def main():
     ap.add_argument("--rrt-queries", type=int, default=256)
     ap.add_argument("--rrt-samples", type=int, default=65536)
     ap.add_argument("--rrt-steps", type=int, default=4)
-    ap.add_argument("--rrt-streams", type=int, default=3, help="RRT* batches in flight (own stream + context each)")
+    ap.add_argument("--rrt-streams", type=int, default=2, help="RRT* launches in flight (own stream + context each)")
+    ap.add_argument("--rrt-batches", type=int, default=8,
+                    help="RRT* batches (of --rrt-queries) per launch: continuous batching, one launch over all of them")
     ap.add_argument("--rrt-cpu-sample", type=int, default=16)
     ap.add_argument("--rrt-resident", type=int, default=0,
                     help="RRT* workgroups per CU the LDS tree copy leaves room for (0: one, the whole LDS)")

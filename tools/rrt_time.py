@@ -31,6 +31,13 @@ for nq, sn in [(int(a), int(b)) for a, b in (x.split("x") for x in sys.argv[1:])
     print(f"nq={nq} samples={sn}: {ms:.1f} ms ({ms * 1e3 / sn:.2f} us/iteration), nodes mean {nn.mean():.0f} "
           f"max {nn.max()}, found {(out['status'].cpu().numpy() == 0).sum()}", flush=True)
     c = out["counters"].cpu().numpy()
+    it = c[:, 0].astype(np.float64)
+    st = out["status"].cpu().numpy()
+    print("  iterations per query: quantiles 0/10/50/90/99/100 " +
+          "/".join(f"{np.percentile(it, p):.0f}" for p in (0, 10, 50, 90, 99, 100)) +
+          f"; share of the launch's iterations held by the top 5% queries "
+          f"{np.sort(it)[::-1][: max(1, nq // 20)].sum() / it.sum():.3f}; statuses {np.unique(st, return_counts=True)}",
+          flush=True)
     if "stamps" in os.environ.get("PMP_HIP_LIB", ""):  # per-phase s_memtime ticks >> 6, two per counter
         ph = np.concatenate([(c & 0xFFFFFFFF)[:, :, None], (c >> 32)[:, :, None]], axis=2).reshape(nq, 8) * 64.0
         names = ("nearest-scan", "band+argmin", "steer+collision", "radius-scan", "tests1", "choose", "rewire+tests2",
