@@ -35,6 +35,7 @@ constexpr int kMaxA = 256;     // collision-free improving candidates per iterat
 constexpr int kMaxT = 256;     // candidates awaiting a collision test per phase
 constexpr int kMaxK = 256;     // in-radius candidates kept in LDS (more spill to the HBM list)
 constexpr int kRnd = 256;      // random doubles staged in LDS
+constexpr int kMaxH = 512;     // coarse in-radius hits staged in LDS (more are resolved inline)
 constexpr int kBins = 16;      // obstacle bins per axis over the map
 constexpr int kLdsBytes = 160 * 1024;  // the CU's LDS
 constexpr int kRrtMaxResident = 4;     // LDS tree shares per CU RRT honours from pmp_set_resident_per_cu
@@ -105,6 +106,8 @@ struct RrtShared {
     int t2i[kWaves];                 // ... and the minimum's index
     double nearx, neary, nearg, nearh;
     int nK, nA, nT, nT2, slot;
+    int hj[kMaxH];  // coarse in-radius hits of the scan, resolved exactly after it (one load round)
+    int nH;
 };
 
 // ---- obstacle tests (sample_search.py), same operation order as the oracle ----
@@ -255,6 +258,21 @@ __device__ bool collision_wave(const RrtShared& S, int nr, int nc, int nb, doubl
     } else {
         const int items = coll_items(nr, nc, nb);
         for (int it = lane_id(); it < items; it += 64) hit |= coll_item(S, nr, nc, nb, d, it, x1, y1, x2, y2);
+    }
+    return ballot(hit) != 0;
+}
+
+// the same with the obstacle set given (a superset of every obstacle the segment's items can find
+// true for: the extra items are exact tests that come out false); om = false: the segment's own bins
+__device__ bool collision_wave_o(const RrtShared& S, int nr, int nc, int nb, double d, double x1, double y1, double x2,
+                                 double y2, bool om, uint64_t lo, uint64_t hi)
+{
+    if (!om) return collision_wave(S, nr, nc, nb, d, x1, y1, x2, y2);
+    bool hit = false;
+    const int nlo = __popcll(lo), items = 3 * (nlo + __popcll(hi));
+    for (int t = lane_id(); t < items; t += 64) {
+        const int it = bin_item(lo, nlo, hi, t, nr, nc, nb);
+        if (it >= 0) hit |= coll_item(S, nr, nc, nb, d, it, x1, y1, x2, y2);
     }
     return ballot(hit) != 0;
 }
@@ -611,7 +629,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         double G = G0;
         int parent = near;
         int slot = n;
-        if (tid == 0) { S.nK = 0; S.nA = 0; S.nT = 0; S.nT2 = 0; S.slot = n; }
+        if (tid == 0) { S.nK = 0; S.nA = 0; S.nT = 0; S.nT2 = 0; S.slot = n; S.nH = 0; }
         __syncthreads();
         if (STAR) {
             const int wave = tid >> 6, lane = tid & 63;
@@ -619,6 +637,32 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             const float nxf = (float)nx, nyf = (float)ny;
             const double rb = P.radius + 2.0 * eps;
             const float Tr = (float)(rb * rb) * 1.0001f;
+            // node j's exact test: in the radius -> a K entry (and a T entry when c_j < G0)
+            auto in_radius = [&](int j) {
+                const double xj = tx[2 * j], yj = tx[2 * j + 1], gj = tg[j];  // one round
+                if (xj == nx && yj == ny) atomicMin(&S.slot, j);
+                const double d = lp::py_hypot(nx - xj, ny - yj);
+                if (!(d < P.radius)) return;
+                const int k = atomicAdd(&S.nK, 1);
+                const int fl = (gj + d < G0) ? KF_A : 0;
+                if (k < kMaxK) {
+                    S.kj[k] = j; S.kf[k] = fl; S.kd[k] = d; S.kx[k] = xj; S.ky[k] = yj; S.kg[k] = gj;
+                } else {
+                    KEntry e;
+                    e.j = j;
+                    e.d = d;
+                    e.flags = fl;
+                    kl[k] = e;
+                }
+                if (fl & KF_A) {
+                    const int t = atomicAdd(&S.nT, 1);
+                    tset(S, tl, t, k, 0.0);
+                }
+            };
+            // the obstacles any candidate -- node_new segment can meet (each lies in the box of the
+            // radius disk around node_new): one mask for every test of 4b / 4c
+            uint64_t olo = 0, ohi = 0;
+            const bool om = bins_mask(S, nx - P.radius, ny - P.radius, nx + P.radius, ny + P.radius, olo, ohi);
             // the in-radius candidates (any order: the K list is order-free), the LDS part as 8-wide
             // chunks of the same loop body, the HBM part 8 loads in flight per thread
             for (int j0 = tid; j0 < n; j0 += 8 * kNT) {
@@ -638,28 +682,33 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                 uint32_t hits = 0;
 #pragma unroll
                 for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < n) & (cd2(p[u], nxf, nyf) <= Tr)) << u;
+              // a coarse hit is staged: its exact test waits for the scan's end, so the hits' node
+              // loads go out in one round instead of one dependent round per chunk
               for (; hits; hits &= hits - 1) {
-                const int j = j0 + (__ffs(hits) - 1) * kNT;
-                const double xj = tx[2 * j], yj = tx[2 * j + 1], gj = tg[j];  // one round
-                if (xj == nx && yj == ny) atomicMin(&S.slot, j);
-                const double d = lp::py_hypot(nx - xj, ny - yj);
-                if (!(d < P.radius)) continue;
-                const int k = atomicAdd(&S.nK, 1);
-                const int fl = (gj + d < G0) ? KF_A : 0;
-                if (k < kMaxK) {
-                    S.kj[k] = j; S.kf[k] = fl; S.kd[k] = d; S.kx[k] = xj; S.ky[k] = yj; S.kg[k] = gj;
-                } else {
-                    KEntry e;
-                    e.j = j;
-                    e.d = d;
-                    e.flags = fl;
-                    kl[k] = e;
-                }
-                if (fl & KF_A) {
-                    const int t = atomicAdd(&S.nT, 1);
-                    tset(S, tl, t, k, 0.0);
-                }
+                const int h = atomicAdd(&S.nH, 1);
+                if (h < kMaxH) S.hj[h] = j0 + (__ffs(hits) - 1) * kNT;
               }
+            }
+            __syncthreads();
+            if (S.nH <= kMaxH) {
+                for (int h = tid; h < S.nH; h += kNT) in_radius(S.hj[h]);
+            } else {
+                // more coarse hits than the stage holds (a dense ball): the whole scan again, each
+                // hit tested where it is found
+                for (int j0 = tid; j0 < n; j0 += 8 * kNT) {
+                    uint32_t p[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        const int j = j0 + u * kNT;
+                        p[u] = 0u;
+                        if (j < nl) p[u] = xl[j];
+                        else if (j < n) p[u] = xyq[j];
+                    }
+                    uint32_t hits = 0;
+#pragma unroll
+                    for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < n) & (cd2(p[u], nxf, nyf) <= Tr)) << u;
+                    for (; hits; hits &= hits - 1) in_radius(j0 + (__ffs(hits) - 1) * kNT);
+                }
             }
             __syncthreads();
             RSTAMP(3);
@@ -673,7 +722,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             for (int t = wave; t < nT; t += kWaves) {
                 const int k = tget_k(S, tl, t);
                 const KRec e = kget(S, kl, tx, tg, k);
-                if (collision_wave(S, nr, nc, nb, delta, e.x, e.y, nx, ny)) continue;
+                if (collision_wave_o(S, nr, nc, nb, delta, e.x, e.y, nx, ny, om, olo, ohi)) continue;
                 if (lane == 0) {
                     const int a = atomicAdd(&S.nA, 1);
                     aset(S, al, a, e.j, e.g + e.d);
@@ -723,7 +772,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             c_tests += nT2;
             for (int t = wave; t < nT2; t += kWaves) {
                 const KRec e = kget(S, kl, tx, tg, tget_k(S, tl, t));
-                if (collision_wave(S, nr, nc, nb, delta, e.x, e.y, nx, ny)) continue;
+                if (collision_wave_o(S, nr, nc, nb, delta, e.x, e.y, nx, ny, om, olo, ohi)) continue;
                 if (lane == 0) { tg[e.j] = tget_G(S, tl, t) + e.d; tpar[e.j] = slot; }
             }
             __syncthreads();  // rewires land before the insert below may overwrite a duplicate slot
