@@ -124,6 +124,28 @@ def test_c3_midsize_against_oracle():
         assert int(out["status"][q]) == ref["status"][q]
 
 
+def test_rrt_star_dense_ball_against_oracle():
+    """README map with the goal inside an obstacle (never connected, so the tree takes every sample):
+    6,000 samples on 51x31 put hundreds of nodes in one r = 10 ball, past the kernel's 512 staged
+    coarse hits -- the rescan path (rrt.hip 4a) -- and the trees equal the oracle's."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import batch, workloads as wl
+
+    env = _map("readme")
+    nq, sn = 4, 6000
+    rnd = np.stack([np.random.RandomState(900 + q).random_sample(3 * sn + 1) for q in range(nq)])
+    starts, goals = np.tile([5.0, 5.0], (nq, 1)), np.tile([27.0, 13.0], (nq, 1))  # inside rect (26, 7, 2, 12)
+    out = batch.rrt_batch(env, starts, goals, rnd, sn, star=True, counters=True)
+    ref = O.rrt_batch(True, wl.README_MAP_RECT, wl.README_MAP_CIRC, 51, 31, starts, goals, rnd, sn)
+    assert (ref["n_nodes"] > 3500).all()
+    # in-radius candidates per iteration: a ball of this tree holds hundreds of nodes
+    c = out["counters"].cpu().numpy()
+    assert (c[:, 2] / np.maximum(c[:, 0], 1)).max() > 200
+    for q in range(nq):
+        _check_tree(out, q, ref["tree"][q, : ref["n_nodes"][q]], q)
+        assert int(out["status"][q]) == ref["status"][q]
+
+
 def test_c3_full_size_properties():
     """C3 at BASELINE size (65,536 samples), 4 queries: the four whole trees against the oracle, and tree
     invariants on every node of all four -- parents reach the start without cycles, g >= g(parent) +
