@@ -744,7 +744,7 @@ def dstar2d_onpress(occ: np.ndarray, start, goal, presses, path_cap: int = 0, ma
     L.oracle_dstar2d_onpress(_p(occ, _u8p), W, H, int(start[0]), int(start[1]), int(goal[0]), int(goal[1]),
                              _p(pr, _i32p), n, _p(cost, _dp), _p(path, _i32p), path_cap, _p(plen, _i32p), _p(npr, _i64p),
                              _p(st, _i32p), int(max_process))
-    return dict(cost=cost, status=st, n_process=npr, path_len=plen,
+    return dict(cost=cost, status=st, n_process=npr, path_len=plen, first=path[:, 0].copy(),
                 paths=[path[r, : max(0, min(plen[r], path_cap))].copy() for r in range(n + 1)])
 
 

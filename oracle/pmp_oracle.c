@@ -2383,8 +2383,8 @@ int oracle_dstar3d(const uint8_t* occ_in, int X, int Y, int Z, const int32_t* s,
  * empty OPEN) or max_process, 4 the reference raises, -1 not run.
  * ============================================================================================ */
 /* returns 0 = OPEN empty on entry (-1), 1 = processed, OPEN non-empty, 2 = processed, OPEN empty
- * (min_k raises), 3 = allocation failure */
-static int d2_process(dstate_t* S, const uint8_t* occ, int W, int H, int64_t* np)
+ * (min_k raises), 3 = allocation failure, 4 = getNeighbor raised KeyError (*raise_cell = the node) */
+static int d2_process(dstate_t* S, const uint8_t* occ, int W, int H, int64_t* np, int32_t* raise_cell)
 {
     int64_t pos = d_minpos(S);
     (*np)++;
@@ -2395,6 +2395,9 @@ static int d2_process(dstate_t* S, const uint8_t* occ, int W, int H, int64_t* np
     memmove(&S->open[pos], &S->open[pos + 1], sizeof(int32_t) * (size_t)(S->nopen - pos - 1));
     S->nopen--;
     const int32_t xc = x == S->goal_slot ? S->goal_cell : x; /* node.current */
+    /* getNeighbor (:276-291): self.map[node + motion] for all 8 motions before the collision test;
+     * self.map holds the in-grid cells only (env.py:34-35): a border node raises KeyError */
+    if (xc / H == 0 || xc % H == 0 || xc / H == W - 1 || xc % H == H - 1) { *raise_cell = xc; return 4; }
     int32_t nb[8];
     double nc[8];
     int nn = d_neighbors(occ, W, H, xc, nb, nc);
@@ -2452,9 +2455,12 @@ int oracle_dstar2d_onpress(const uint8_t* occ_in, int W, int H, int sx, int sy, 
     d_insert(&S, S.goal_slot, 0.0);
     int64_t np = 0;
     int st = 0;
+    int32_t raise_cell = -1;
+    int plen0 = 0; /* round 0's path length when it raises: -2 = getNeighbor's KeyError (path[0] = the node) */
     for (;;) {
-        const int ps = d2_process(&S, occ, W, H, &np);
+        const int ps = d2_process(&S, occ, W, H, &np, &raise_cell);
         if (ps == 3) { st = 3; break; }
+        if (ps == 4) { st = 4; plen0 = -2; break; }
         if (ps != 1) { st = 4; break; }
         if (S.t[start] == T_CLOSED) break;
         if (max_process > 0 && np >= max_process) { st = 3; break; }
@@ -2464,6 +2470,7 @@ int oracle_dstar2d_onpress(const uint8_t* occ_in, int W, int H, int sx, int sy, 
         int n = 0, rst = st;
         double c = 0.0;
         if (r == 0) {
+            if (plen0 == -2) { n = -2; pth[0] = raise_cell; }
             if (st == 0) {
                 int32_t x = start;
                 pth[n++] = x;
@@ -2497,8 +2504,9 @@ int oracle_dstar2d_onpress(const uint8_t* occ_in, int W, int H, int sx, int sy, 
                     if (collide2(occ, W, H, cx, cy, qx, qy)) {
                         if (S.t[node] == T_CLOSED && d_insert(&S, node, S.h[p] + INFINITY)) { rst = 3; break; }
                         for (;;) {
-                            const int ps = d2_process(&S, occ, W, H, &np);
+                            const int ps = d2_process(&S, occ, W, H, &np, &raise_cell);
                             if (ps == 3) { rst = 3; break; }
+                            if (ps == 4) { rst = 4; n = -2; pth[0] = raise_cell; break; }
                             if (ps == 2) { rst = 4; break; }
                             if (ps == 0) { rst = 3; break; } /* -1 >= node.h never holds: endless loop */
                             if (max_process > 0 && np >= max_process) { rst = 3; break; }

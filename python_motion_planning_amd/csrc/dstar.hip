@@ -103,12 +103,14 @@ struct Search2 {
     int goal_slot, goal_cell;  // start == goal: the goal object lives in slot W*H (d_star.py:66-68)
     bool start_closed;  // self.start.t == 'CLOSED'
     bool overflow;
+    int raise_cell;     // PS_RAISE: the border node whose getNeighbor raised KeyError
 };
 
 // processState outcome: EMPTY = OPEN was empty (the reference appends None to EXPAND, returns -1),
 // DONE = processed and OPEN is non-empty (min_k is S.root after clean_top), EMPTIED = processed and
-// OPEN is empty (the reference's `return self.min_k` raises AttributeError), OVER = a cap was hit
-enum { PS_EMPTY = 0, PS_DONE = 1, PS_EMPTIED = 2, PS_OVER = 3 };
+// OPEN is empty (the reference's `return self.min_k` raises AttributeError), OVER = a cap was hit,
+// RAISE = getNeighbor of a node on the grid's border looked up an out-of-grid cell (KeyError)
+enum { PS_EMPTY = 0, PS_DONE = 1, PS_EMPTIED = 2, PS_OVER = 3, PS_RAISE = 4 };
 
 struct D2 {
     const uint32_t* occ;  // the shared grid, or the worker's working copy (OnPress adds obstacles)
@@ -207,6 +209,13 @@ struct D2 {
         // getNeighbor's collision test only decides below whether a lane uses its cell)
         const int Xc0 = X == S.goal_slot ? S.goal_cell : X;
         const int x = Xc0 / H, y = Xc0 % H;
+        // getNeighbor (:276-291) looks up self.map[node + motion] for all 8 motions before any
+        // collision test, and self.map holds the in-grid cells only (env.py:34-35): processing a node
+        // on the grid's border raises KeyError (only on a grid whose border cells are not walls)
+        if (x == 0 || y == 0 || x == W - 1 || y == H - 1) {
+            S.raise_cell = Xc0;
+            return PS_RAISE;
+        }
         const int nx = x + mdx, ny = y + mdy;
         const bool nin = lane < 8 && (unsigned)nx < (unsigned)W && (unsigned)ny < (unsigned)H;
         const int Y = nin ? nx * H + ny : 0;
@@ -439,9 +448,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void ds
         d.insert_uniform(S.goal_slot, 0.0);
         // ---- plan(): processState until the start is CLOSED (:84-87)
         int st = PMP_FOUND;
+        int plen0 = 0;  // round 0's path_len when it raises: -2 = getNeighbor's KeyError (path[0] = the node)
         for (;;) {
             const int ps = d.process_state();
             if (ps == PS_OVER) { st = PMP_CAP_OVERFLOW; break; }
+            if (ps == PS_RAISE) { st = PMP_REF_RAISES; plen0 = -2; break; }
             if (ps != PS_DONE) { st = PMP_REF_RAISES; break; }  // min_k of an empty OPEN (:234)
             if (S.start_closed) break;
             if (max_process > 0 && S.np >= max_process) { st = PMP_CAP_OVERFLOW; break; }
@@ -452,6 +463,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void ds
             int plen = 0;
             int32_t* pth = path_out + ((size_t)q * R1 + r) * (size_t)path_cap;
             if (r == 0) {
+                if (plen0 == -2) {
+                    plen = -2;
+                    if (lane == 0) pth[0] = S.raise_cell;
+                }
                 if (st == PMP_FOUND && lane == 0) {
                     // extractPath (:136-156): start -> goal through parents, cost via GraphSearcher.cost
                     int c = start;
@@ -498,6 +513,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void ds
                             for (;;) {
                                 const int ps = S.overflow ? PS_OVER : d.process_state();
                                 if (ps == PS_OVER) { rst = PMP_CAP_OVERFLOW; break; }
+                                if (ps == PS_RAISE) {  // getNeighbor's KeyError: path_len -2, path[0] = the node
+                                    rst = PMP_REF_RAISES;
+                                    plen = -2;
+                                    if (lane == 0) pth[0] = S.raise_cell;
+                                    break;
+                                }
                                 if (ps == PS_EMPTIED) { rst = PMP_REF_RAISES; break; }
                                 // an OPEN empty on entry makes processState return -1 forever: the
                                 // reference's loop never ends

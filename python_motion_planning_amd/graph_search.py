@@ -270,6 +270,17 @@ class DStarLite(LPAStar):
         return "D* Lite"
 
 
+def dstar_border_key(cell: int, W: int, H: int) -> tuple:
+    """The key DStar.getNeighbor (d_star.py:276-291) fails on for a node on the grid's border: the
+    first motion (env.py:52-55 order) whose target is outside the grid (self.map holds the in-grid
+    cells only).  The kernel reports that node as status 4 with path_len -2 and path[0] = its cell."""
+    x, y = divmod(int(cell), H)
+    for dx, dy in ((-1, 0), (-1, 1), (0, 1), (1, 1), (1, 0), (1, -1), (0, -1), (-1, -1)):
+        if not (0 <= x + dx < W and 0 <= y + dy < H):
+            return (x + dx, y + dy)
+    raise ValueError(f"cell {cell} is not on the border of a {W}x{H} grid")
+
+
 class DStar(GraphSearcher):
     """Dynamic A* (d_star.py:37-291) -- the static plan (processState until the start is CLOSED)
     runs in the gfx950 kernel dstar.hip with the reference's list-semantics OPEN."""
@@ -291,6 +302,8 @@ class DStar(GraphSearcher):
         st = int(r["status"][0])
         self.n_process = int(r["n_process"][0])
         if st == 4:
+            if int(r["path_len"][0]) == -2:  # getNeighbor of a border node (a grid without walls)
+                raise KeyError(dstar_border_key(int(r["path"][0, 0]), W, H))
             raise AttributeError("'NoneType' object has no attribute 'k'")
         if st != 0:
             raise RuntimeError(f"D* kernel status {st}")
@@ -324,6 +337,8 @@ class DStar(GraphSearcher):
         k = len(self._presses)
         st = int(r["status"][0, k])
         if st == 4:
+            if int(r["path_len"][0, k]) == -2:  # getNeighbor of a border node (a grid without walls)
+                raise KeyError(dstar_border_key(int(r["path"][0, k, 0]), W, H))
             if int(r["path_len"][0, k]) < 0:
                 raise KeyError(None)  # self.map[node.parent] of a parentless node
             raise AttributeError("'NoneType' object has no attribute 'k'")  # min_k of an emptied OPEN

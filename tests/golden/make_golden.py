@@ -1260,7 +1260,114 @@ def sec_totp():
     print("totp cases", len(cases), "samples", prof_off[-1], "points", pts_off[-1])
 
 
-SECTIONS = dict(rrt=sec_rrt, mpc=sec_mpc, dwa=sec_dwa, local_plans=sec_local_plans, lqr=sec_lqr, astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
+def run_dstar_nowall(args):
+    """run_dstar_onpress on a grid whose border cells are free: getNeighbor (d_star.py:276-291) of a
+    border node looks up an out-of-grid key and raises KeyError -- recorded with its key."""
+    occ, start, goal, presses = args
+    pmp = import_reference()
+    import contextlib
+    import io
+
+    W, H = occ.shape
+    env = pmp.Grid(W, H)
+    env.update(obstacles_of(occ))  # no border walls
+    p = pmp.DStar(tuple(start), tuple(goal), env)
+    out = dict(cost=[], path=[], nexp=[], kind=[], key=[])
+
+    def fail(e):
+        out["cost"].append(float("nan")); out["path"].append([]); out["nexp"].append(len(p.EXPAND))
+        out["kind"].append(type(e).__name__)
+        k = e.args[0] if isinstance(e, KeyError) and e.args else None
+        out["key"].append(tuple(int(v) for v in k) if isinstance(k, tuple) else (-1, -1))
+
+    try:
+        cost, path, _ = p.plan()
+    except Exception as e:  # noqa: BLE001
+        fail(e)
+        close_figs()
+        return out
+    out["cost"].append(float(cost)); out["path"].append([x * H + y for (x, y) in path])
+    out["nexp"].append(len(p.EXPAND)); out["kind"].append(""); out["key"].append((-1, -1))
+    p.plot = unittest.mock.MagicMock()
+    for (x, y) in presses:
+        ev = types.SimpleNamespace(xdata=float(x) + 0.25, ydata=float(y) + 0.25)
+        p.plot.animation.reset_mock()
+        try:
+            with contextlib.redirect_stdout(io.StringIO()):
+                p.OnPress(ev)
+        except Exception as e:  # noqa: BLE001
+            fail(e)
+            break
+        if p.plot.animation.called:
+            wpath, _, wcost, _ = p.plot.animation.call_args[0]
+            out["cost"].append(float(wcost)); out["path"].append([x * H + y for (x, y) in wpath])
+            out["nexp"].append(len(p.EXPAND)); out["kind"].append(""); out["key"].append((-1, -1))
+        else:
+            out["cost"].append(0.0); out["path"].append([]); out["nexp"].append(len(p.EXPAND)); out["kind"].append("noop")
+            out["key"].append((-1, -1))
+    close_figs()
+    return out
+
+
+def sec_dstar_nowall(n=48, npress=3):
+    """D* plan + OnPress on grids without border walls (round 6): the border KeyError."""
+    rng = np.random.default_rng(4242)
+    cases = []
+    for i in range(n):
+        W, H = int(rng.integers(8, 31)), int(rng.integers(8, 31))
+        occ = (rng.random((W, H)) < float(rng.uniform(0.0, 0.25))).astype(np.uint8)
+        free = np.argwhere(occ == 0)
+        if i % 2:  # start and goal near the middle: the plan can finish before any border node
+            mid = free[(np.abs(free[:, 0] - W // 2) <= 2) & (np.abs(free[:, 1] - H // 2) <= 2)]
+            pick = mid if len(mid) >= 2 else free
+        else:
+            pick = free
+        s = tuple(int(v) for v in pick[rng.integers(len(pick))])
+        g = tuple(int(v) for v in pick[rng.integers(len(pick))])
+        cases.append([occ, s, g, None])
+    with Pool(8) as pool:
+        first = pool.map(run_dstar_nowall, [(c[0], c[1], c[2], []) for c in cases])
+        for c, f in zip(cases, first):
+            W, H = c[0].shape
+            path = f["path"][0]
+            pr = []
+            for k in range(npress):
+                if path and len(path) > 3:
+                    v = path[int(rng.integers(1, len(path) - 1))]
+                    pr.append((v // H, v % H))
+                else:
+                    pr.append((int(rng.integers(0, W)), int(rng.integers(0, H))))
+            c[3] = pr
+        res = pool.map(run_dstar_nowall, [tuple(c) for c in cases])
+    dims = np.array([c[0].shape for c in cases], np.int32)
+    occ_flat, occ_off = ragged([np.packbits(c[0].ravel()) for c in cases], np.uint8)
+    R = npress + 1
+    kinds = np.full((n, R), "", dtype="<U16")
+    keys = np.full((n, R, 2), -1, np.int32)
+    cost = np.full((n, R), np.nan)
+    nexp = np.full((n, R), -1, np.int64)
+    paths = []
+    for i, r in enumerate(res):
+        for k in range(R):
+            if k < len(r["kind"]):
+                kinds[i, k] = r["kind"][k]
+                keys[i, k] = r["key"][k]
+                cost[i, k] = r["cost"][k]
+                nexp[i, k] = r["nexp"][k]
+                paths.append(r["path"][k])
+            else:
+                kinds[i, k] = "notrun"
+                paths.append([])
+    path_flat, path_off = ragged(paths)
+    np.savez_compressed(
+        os.path.join(HERE, "dstar_nowall.npz"), dims=dims, occ_bits=occ_flat, occ_off=occ_off,
+        start=np.array([c[1] for c in cases], np.int32), goal=np.array([c[2] for c in cases], np.int32),
+        presses=np.array([c[3] for c in cases], np.int32), kind=kinds, key=keys, cost=cost, nexp=nexp,
+        path=path_flat, path_off=path_off)
+    print("dstar_nowall", [list(r["kind"]) for r in res])
+
+
+SECTIONS = dict(dstar_nowall=sec_dstar_nowall, rrt=sec_rrt, mpc=sec_mpc, dwa=sec_dwa, local_plans=sec_local_plans, lqr=sec_lqr, astar_readme=sec_astar_readme, astar_small=sec_astar_small, astar_1024=sec_astar_1024,
                 dstar=sec_dstar, astar3d=sec_astar3d,
                 graph2d=sec_graph2d, graph3d=sec_graph3d, theta3d=sec_theta3d, theta2d=sec_theta2d, lpa=sec_lpa,
                 dstarlite=lambda: sec_lpa(lite=True), lpa_replan=sec_lpa_replan,

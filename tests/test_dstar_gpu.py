@@ -107,6 +107,46 @@ def test_dstar_onpress_against_reference():
     assert n_walk >= 100
 
 
+def test_dstar_nowall_against_reference():
+    """Grids without border walls (48 reference sessions, plan + 3 OnPress): the reference raises
+    KeyError when it processes a border node (d_star.py:276-291) -- in plan() or in a repair; the
+    kernel reports status 4, path_len -2, path[0] = the node, with len(EXPAND) at the raise; the
+    drop-in DStar raises KeyError with the reference's key."""
+    import python_motion_planning_amd as pmp
+    from golden_io import load_npz
+    from python_motion_planning_amd import batch
+    from python_motion_planning_amd.graph_search import dstar_border_key
+
+    z = load_npz("dstar_nowall.npz")
+    R = z["presses"].shape[1] + 1
+    n_raise = 0
+    for i, occ, _ in grid_cases("dstar_nowall.npz"):
+        W, H = occ.shape
+        out = batch.dstar2d_onpress_batch(occ, z["start"][i][None], z["goal"][i][None], z["presses"][i][None])
+        st, npr = out["status"][0].cpu().numpy(), out["n_process"][0].cpu().numpy()
+        cost, pl, path = out["cost"][0].cpu().numpy(), out["path_len"][0].cpu().numpy(), out["path"][0].cpu().numpy()
+        for r in range(R):
+            k = str(z["kind"][i][r])
+            if k == "notrun":
+                assert st[r] == -1, (i, r)
+                continue
+            assert st[r] == {"": 0, "noop": 1, "KeyError": 4}[k], (i, r, k, st)
+            assert npr[r] == z["nexp"][i][r], (i, r)
+            if k == "KeyError":
+                assert pl[r] == -2 and dstar_border_key(path[r, 0], W, H) == tuple(z["key"][i][r]), (i, r)
+                n_raise += 1
+            if k == "":
+                assert cost[r] == z["cost"][i][r], (i, r)
+                assert np.array_equal(path[r, : pl[r]], seg(z["path"], z["path_off"], i * R + r)), (i, r)
+        if str(z["kind"][i][0]) == "KeyError":  # the drop-in plan() raises the reference's KeyError
+            env = pmp.Grid(W, H)
+            env.update({(int(a), int(b)) for a, b in np.argwhere(occ)})
+            with pytest.raises(KeyError) as ei:
+                pmp.DStar(tuple(int(v) for v in z["start"][i]), tuple(int(v) for v in z["goal"][i]), env).plan()
+            assert ei.value.args[0] == tuple(z["key"][i][0]), i
+    assert n_raise >= 20
+
+
 def test_dstar_onpress_batch_against_oracle():
     """128 sessions on a 128^2 grid, 3 presses each on cells of the planned path: the repairs run
     processState on the kept state; every output against the oracle."""

@@ -469,6 +469,36 @@ def test_dstar_onpress_against_reference():
     assert {"", "noop"} <= kinds
 
 
+def test_dstar_nowall_against_reference():
+    """D* plan + 3 OnPress calls on 48 grids WITHOUT border walls, replayed from the reference: its
+    getNeighbor (d_star.py:276-291) looks up self.map[node + motion] before any collision test, so
+    processing a border node raises KeyError -- in plan() or in an OnPress repair.  Status 4 with
+    path_len -2 and path[0] = the node; its first out-of-grid neighbour is the reference's key."""
+    from python_motion_planning_amd.graph_search import dstar_border_key
+
+    z = load_npz("dstar_nowall.npz")
+    R = z["presses"].shape[1] + 1
+    kinds = set()
+    for i, occ, _ in grid_cases("dstar_nowall.npz"):
+        W, H = occ.shape
+        res = O.dstar2d_onpress(occ, z["start"][i], z["goal"][i], z["presses"][i])
+        for r in range(R):
+            k = str(z["kind"][i][r])
+            kinds.add(k)
+            if k == "notrun":
+                assert res["status"][r] == -1, (i, r)
+                continue
+            assert res["status"][r] == {"": 0, "noop": 1, "KeyError": 4}[k], (i, r, k, res["status"])
+            assert res["n_process"][r] == z["nexp"][i][r], (i, r)
+            if k == "KeyError":
+                assert res["path_len"][r] == -2, (i, r)
+                assert dstar_border_key(res["first"][r], W, H) == tuple(z["key"][i][r]), (i, r)
+            if k == "":
+                assert res["cost"][r] == z["cost"][i][r], (i, r)
+                assert np.array_equal(res["paths"][r], seg(z["path"], z["path_off"], i * R + r)), (i, r)
+    assert {"", "noop", "KeyError"} <= kinds
+
+
 def test_lpastar3d_published_csv():
     """All 500 distinct LPAStar3D rows of 3d_pathfinding_results.csv: cost repr and len(EXPAND)."""
     rows = load_json("lpastar3d_csv.json")
