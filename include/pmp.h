@@ -185,10 +185,12 @@ int pmp_dwa_step_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int
  *   path [nq][path_cap]  cells x*H + y, start -> goal; path_len [nq]
  *   n_process [nq] i64   processState calls (len(DStar.EXPAND))
  *   status [nq]          0 found, 2 path_cap overflow, 3 capacity / max_process exceeded,
- *                        4 the reference raises (OPEN empties: AttributeError at d_star.py:234)
+ *                        4 the reference raises (OPEN empties: AttributeError at d_star.py:234;
+ *                        path_len -2: processState reached a node on the grid's border, whose
+ *                        getNeighbor looks up an out-of-grid key -- KeyError, d_star.py:276-291 --
+ *                        and path[0] is that node's cell)
  *   max_process          0 = unbounded, else stop with status 3 after that many processState calls
- * Neighbours outside the grid count as blocked (the reference raises KeyError there; grids built
- * by Grid.init have obstacle borders, so it never happens for them).
+ * Grids built by Grid.init have obstacle borders, so the border KeyError never happens for them.
  */
 int pmp_dstar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H, const int32_t* start_xy,
                       const int32_t* goal_xy, int nq, double* cost, int32_t* path_len, int32_t* path, int path_cap,
@@ -205,8 +207,9 @@ int pmp_dstar2d_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int 
  *       status 0 walked to the goal, 1 the press changed nothing (off the grid or already an
  *       obstacle: len(EXPAND) is kept), 2 path_cap overflow, 3 a cap or a loop the reference never
  *       leaves (4*W*H+4 steps, or modify() on an empty OPEN), 4 the reference raises (a parentless
- *       node: KeyError, reported with path_len -1; OPEN emptied: AttributeError), -1 not run (an
- *       earlier call raised or capped)
+ *       node: KeyError, reported with path_len -1; a border node processed: KeyError, path_len -2
+ *       and path[r][0] = its cell; OPEN emptied: AttributeError), -1 not run (an earlier call
+ *       raised or capped)
  * pmp_dstar2d_batch is this call with npress = 0.
  */
 int pmp_dstar2d_onpress_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H,
