@@ -108,6 +108,8 @@ struct RrtShared {
     int nK, nA, nT, nT2, slot;
     int hj[kMaxH];  // coarse in-radius hits of the scan, resolved exactly after it (one load round)
     int nH;
+    double newx, newy, newG;  // the fused step's node_new (wave 0's steering)
+    int fflag;                // ... 1 the sample is already in the tree, 2 the segment collides
 };
 
 // ---- obstacle tests (sample_search.py), same operation order as the oracle ----
@@ -463,11 +465,21 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
     // dev build (tools/rrt_time.py): the counters become s_memtime ticks (>> 6) summed per phase, two
     // phases per counter (low / high 32 bits) -- nearest scan + min, band + argmin, steer + collision,
     // in-radius scan, first tests, choose-parent, rewire decisions + tests, insert + goal test
+    // PMP_RRT_STAMPS=2: finer phases -- nearest scan loop, its top-2 reduction, band + publish, steer +
+    // collision, in-radius scan (staging), hit resolution, tests + choose + rewire, insert + goal
     uint64_t cy[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tq = 0;
+#if PMP_RRT_STAMPS == 2
+    constexpr int kRemap[8] = {1, 2, 3, 5, 6, 6, 6, 7};
+#define RSTAMP(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); cy[kRemap[k]] += t_ - tq; tq = t_; } while (0)
+#define RSTAMPF(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); cy[k] += t_ - tq; tq = t_; } while (0)
+#else
 #define RSTAMP(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); cy[k] += t_ - tq; tq = t_; } while (0)
+#define RSTAMPF(k) do {} while (0)
+#endif
 #define RSTAMP_START() do { tq = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define RSTAMP(k) do {} while (0)
+#define RSTAMPF(k) do {} while (0)
 #define RSTAMP_START() do {} while (0)
 #endif
 
@@ -488,6 +500,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         }
         c_iter++;
         c_scan += n;
+        if (tid == 0) S.nH = 0;  // (the staging of this iteration comes after a barrier)
         RSTAMP_START();
         // ---- 2. nearest ----
         const float sxf = (float)sx, syf = (float)sy;
@@ -531,8 +544,12 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             }
             for (; j < n; j += kNT) take(cd2(xyq[j], sxf, syf), j);
         }
-        // the exact coordinates of this thread's minimum, loaded ahead of the block minimum
-        const double bxj = tx[2 * bj], byj = tx[2 * bj + 1], bgj = tg[bj];
+        RSTAMPF(0);
+        // the exact coordinates of this thread's minimum, loaded ahead of the block minimum (RRT: its
+        // owner publishes them; RRT*'s fused step has wave 0 load the minimum's, so these would only
+        // hold the barrier below on an L2 round -- loaded in the rare band case instead)
+        double bxj = 0.0, byj = 0.0, bgj = 0.0;
+        if (!STAR) { bxj = tx[2 * bj]; byj = tx[2 * bj + 1]; bgj = tg[bj]; }
         // block top-2 of the threads' f32 distances (each thread's minimum and second) and the
         // minimum's index: when nothing but the minimum lies in the band the minimum is the nearest
         // node (the band's exact re-evaluation has one candidate) and its owner publishes it
@@ -565,71 +582,140 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         const double band = sqrt((double)m) + 2.0 * eps;
         const float T = (float)(band * band) * 1.0001f;
         int hi = 0x7fffffff;
-        if (!(b2 <= T)) {
-            // one candidate: the minimum's owner publishes it (the exact distance only for the
-            // sample-already-in-the-tree test; steering recomputes it)
-            if (best == m && bj == im) {
-                S.nearx = bxj; S.neary = byj; S.nearg = bgj;
-                S.nearh = lp::py_hypot(bxj - sx, byj - sy);
+        double nx0, ny0, gnear, nx, ny, G0;
+        bool staged = false;  // the in-radius coarse hits are staged already (the fused step)
+        if (STAR && !(b2 <= T)) {
+            // RRT*, one candidate: wave 0 loads the nearest node's exact coordinates (one L2 round),
+            // steers and tests the segment (isCollision(node_new, node_near) on one wave, its bins),
+            // while the other waves stage the in-radius coarse hits of every node_new within max_dist
+            // of that node -- around its coarse position with the margin max_dist + 4 eps, a superset
+            // of the exact radius test that resolves them below (round 6)
+            if ((tid >> 6) == 0) {
+                const double ex = tx[2 * im], ey = tx[2 * im + 1], eg = tg[im];
+                int fl = 0;
+                double fnx = 0.0, fny = 0.0, fG0 = 0.0;
+                if (lp::py_hypot(ex - sx, ey - sy) == 0.0) {
+                    fl = 1;  // node_rand.current already in sample_list
+                } else {
+                    double dist = lp::py_hypot(sx - ex, sy - ey);
+                    const double theta = atan2(sy - ey, sx - ex);
+                    if (P.max_dist < dist) dist = P.max_dist;
+                    fnx = ex + dist * cos(theta);
+                    fny = ey + dist * sin(theta);
+                    fG0 = eg + dist;
+                    if (collision_wave(S, nr, nc, nb, delta, fnx, fny, ex, ey)) fl = 2;
+                }
+                if ((tid & 63) == 0) {
+                    S.nearx = ex; S.neary = ey; S.nearg = eg;
+                    S.newx = fnx; S.newy = fny; S.newG = fG0; S.fflag = fl;
+                }
+            } else {
+                const uint32_t pn = im < lcap ? xl[im] : xyq[im];
+                const float fxn = fmaf((float)(pn & 0xFFFFu), qinv, qlof), fyn = fmaf((float)(pn >> 16), qinv, qlof);
+                const double rbn = P.radius + P.max_dist + 4.0 * eps;
+                const float Trn = (float)(rbn * rbn) * 1.0001f;
+                constexpr int kST = kNT - 64;  // the staging threads
+                for (int j0 = tid - 64; j0 < n; j0 += 8 * kST) {
+                    uint32_t p[8];
+                    if (j0 + 7 * kST < nl) {
+#pragma unroll
+                        for (int u = 0; u < 8; u++) p[u] = xl[j0 + u * kST];
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < 8; u++) {
+                            const int j = j0 + u * kST;
+                            p[u] = 0u;
+                            if (j < nl) p[u] = xl[j];
+                            else if (j < n) p[u] = xyq[j];
+                        }
+                    }
+                    uint32_t hits = 0;
+#pragma unroll
+                    for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kST < n) & (cd2(p[u], fxn, fyn) <= Trn)) << u;
+                    for (; hits; hits &= hits - 1) {
+                        const int h = atomicAdd(&S.nH, 1);
+                        if (h < kMaxH) S.hj[h] = j0 + (__ffs(hits) - 1) * kST;
+                    }
+                }
             }
             __syncthreads();
+            const int fl = S.fflag;
+            if (fl == 1) continue;
+            c_tests++;
+            if (fl == 2) { RSTAMP(2); continue; }
             hi = im;
-            if (S.nearh == 0.0) continue;  // node_rand.current already in sample_list
+            nx0 = S.nearx; ny0 = S.neary; gnear = S.nearg;
+            nx = S.newx; ny = S.newy; G0 = S.newG;
+            staged = true;
         } else {
-            double h = INFINITY, hx = 0.0, hy = 0.0, hg = 0.0;
-            if (best <= T && !(second <= T)) {
-                h = lp::py_hypot(bxj - sx, byj - sy);
-                hi = bj; hx = bxj; hy = byj; hg = bgj;
-            } else if (best <= T) {
-                // increasing j within the thread (the LDS part, then the HBM part): equal distances keep
-                // the first.  Separate loops: a select between an LDS and a global load per element
-                // would issue both.  8 loads in flight per thread, the hits of a chunk in increasing j
-                auto hit = [&](int j) {
-                    const double xj = tx[2 * j], yj = tx[2 * j + 1], gj = tg[j];  // one round
-                    const double e = lp::py_hypot(xj - sx, yj - sy);
-                    if (e < h) { h = e; hi = j; hx = xj; hy = yj; hg = gj; }  // increasing j: keeps the first
-                };
-                for (int j0 = tid; j0 < nl; j0 += 8 * kNT) {
-                    uint32_t p[8];
-#pragma unroll
-                    for (int u = 0; u < 8; u++) p[u] = (j0 + u * kNT < nl) ? xl[j0 + u * kNT] : 0u;
-                    uint32_t hits = 0;
-#pragma unroll
-                    for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < nl) & (cd2(p[u], sxf, syf) <= T)) << u;
-                    for (; hits; hits &= hits - 1) hit(j0 + (__ffs(hits) - 1) * kNT);
+            if (!(b2 <= T)) {
+                // one candidate: the minimum's owner publishes it (the exact distance only for the
+                // sample-already-in-the-tree test; steering recomputes it)
+                if (best == m && bj == im) {
+                    S.nearx = bxj; S.neary = byj; S.nearg = bgj;
+                    S.nearh = lp::py_hypot(bxj - sx, byj - sy);
                 }
-                for (int j0 = lcap + tid; j0 < n; j0 += 8 * kNT) {
-                    uint32_t p[8];
-#pragma unroll
-                    for (int u = 0; u < 8; u++) p[u] = (j0 + u * kNT < n) ? xyq[j0 + u * kNT] : 0u;
-                    uint32_t hits = 0;
-#pragma unroll
-                    for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < n) & (cd2(p[u], sxf, syf) <= T)) << u;
-                    for (; hits; hits &= hits - 1) hit(j0 + (__ffs(hits) - 1) * kNT);
+                __syncthreads();
+                hi = im;
+                if (S.nearh == 0.0) continue;  // node_rand.current already in sample_list
+            } else {
+                if (STAR) { bxj = tx[2 * bj]; byj = tx[2 * bj + 1]; bgj = tg[bj]; }
+                double h = INFINITY, hx = 0.0, hy = 0.0, hg = 0.0;
+                if (best <= T && !(second <= T)) {
+                    h = lp::py_hypot(bxj - sx, byj - sy);
+                    hi = bj; hx = bxj; hy = byj; hg = bgj;
+                } else if (best <= T) {
+                    // increasing j within the thread (the LDS part, then the HBM part): equal distances keep
+                    // the first.  Separate loops: a select between an LDS and a global load per element
+                    // would issue both.  8 loads in flight per thread, the hits of a chunk in increasing j
+                    auto hit = [&](int j) {
+                        const double xj = tx[2 * j], yj = tx[2 * j + 1], gj = tg[j];  // one round
+                        const double e = lp::py_hypot(xj - sx, yj - sy);
+                        if (e < h) { h = e; hi = j; hx = xj; hy = yj; hg = gj; }  // increasing j: keeps the first
+                    };
+                    for (int j0 = tid; j0 < nl; j0 += 8 * kNT) {
+                        uint32_t p[8];
+    #pragma unroll
+                        for (int u = 0; u < 8; u++) p[u] = (j0 + u * kNT < nl) ? xl[j0 + u * kNT] : 0u;
+                        uint32_t hits = 0;
+    #pragma unroll
+                        for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < nl) & (cd2(p[u], sxf, syf) <= T)) << u;
+                        for (; hits; hits &= hits - 1) hit(j0 + (__ffs(hits) - 1) * kNT);
+                    }
+                    for (int j0 = lcap + tid; j0 < n; j0 += 8 * kNT) {
+                        uint32_t p[8];
+    #pragma unroll
+                        for (int u = 0; u < 8; u++) p[u] = (j0 + u * kNT < n) ? xyq[j0 + u * kNT] : 0u;
+                        uint32_t hits = 0;
+    #pragma unroll
+                        for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < n) & (cd2(p[u], sxf, syf) <= T)) << u;
+                        for (; hits; hits &= hits - 1) hit(j0 + (__ffs(hits) - 1) * kNT);
+                    }
                 }
+                const int my_hi = hi;
+                block_min_di(h, hi, S);
+                if (h == 0.0) continue;  // node_rand.current already in sample_list
+                if (my_hi == hi) { S.nearx = hx; S.neary = hy; S.nearg = hg; }  // the owner publishes the node
+                __syncthreads();
             }
-            const int my_hi = hi;
-            block_min_di(h, hi, S);
-            if (h == 0.0) continue;  // node_rand.current already in sample_list
-            if (my_hi == hi) { S.nearx = hx; S.neary = hy; S.nearg = hg; }  // the owner publishes the node
-            __syncthreads();
+            nx0 = S.nearx; ny0 = S.neary; gnear = S.nearg;
+            RSTAMP(1);
+            // ---- 3. steer + collision (rrt.py:121-129) ----
+            double dist = lp::py_hypot(sx - nx0, sy - ny0);
+            const double theta = atan2(sy - ny0, sx - nx0);
+            if (P.max_dist < dist) dist = P.max_dist;
+            nx = nx0 + dist * cos(theta);
+            ny = ny0 + dist * sin(theta);
+            G0 = gnear + dist;
+            c_tests++;
+            if (collision_block(S, nr, nc, nb, delta, nx, ny, nx0, ny0)) { RSTAMP(2); continue; }
         }
         const int near = hi;
-        const double nx0 = S.nearx, ny0 = S.neary, gnear = S.nearg;
-        RSTAMP(1);
-        // ---- 3. steer + collision (rrt.py:121-129) ----
-        double dist = lp::py_hypot(sx - nx0, sy - ny0);
-        const double theta = atan2(sy - ny0, sx - nx0);
-        if (P.max_dist < dist) dist = P.max_dist;
-        const double nx = nx0 + dist * cos(theta), ny = ny0 + dist * sin(theta);
-        const double G0 = gnear + dist;
-        c_tests++;
-        if (collision_block(S, nr, nc, nb, delta, nx, ny, nx0, ny0)) { RSTAMP(2); continue; }
         RSTAMP(2);
         double G = G0;
         int parent = near;
         int slot = n;
-        if (tid == 0) { S.nK = 0; S.nA = 0; S.nT = 0; S.nT2 = 0; S.slot = n; S.nH = 0; }
+        if (tid == 0) { S.nK = 0; S.nA = 0; S.nT = 0; S.nT2 = 0; S.slot = n; }
         __syncthreads();
         if (STAR) {
             const int wave = tid >> 6, lane = tid & 63;
@@ -665,7 +751,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             const bool om = bins_mask(S, nx - P.radius, ny - P.radius, nx + P.radius, ny + P.radius, olo, ohi);
             // the in-radius candidates (any order: the K list is order-free), the LDS part as 8-wide
             // chunks of the same loop body, the HBM part 8 loads in flight per thread
-            for (int j0 = tid; j0 < n; j0 += 8 * kNT) {
+            for (int j0 = tid; !staged && j0 < n; j0 += 8 * kNT) {
                 uint32_t p[8];
                 if (j0 + 7 * kNT < nl) {
 #pragma unroll
@@ -689,7 +775,8 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                 if (h < kMaxH) S.hj[h] = j0 + (__ffs(hits) - 1) * kNT;
               }
             }
-            __syncthreads();
+            if (!staged) __syncthreads();
+            RSTAMPF(4);
             if (S.nH <= kMaxH) {
                 for (int h = tid; h < S.nH; h += kNT) in_radius(S.hj[h]);
             } else {

@@ -42,9 +42,15 @@ for nq, sn in [(int(a), int(b)) for a, b in (x.split("x") for x in sys.argv[1:])
         ph = np.concatenate([(c & 0xFFFFFFFF)[:, :, None], (c >> 32)[:, :, None]], axis=2).reshape(nq, 8) * 64.0
         names = ("nearest-scan", "band+argmin", "steer+collision", "radius-scan", "tests1", "choose", "rewire+tests2",
                  "insert+goal")
+        if "stamps2" in os.environ.get("PMP_HIP_LIB", ""):
+            names = ("nearest-loop", "nearest-reduce", "band+publish", "steer+collision", "radius-stage", "radius-resolve",
+                     "tests+choose+rewire", "insert+goal")
         tot = ph.sum(axis=1)
         print("  phase ticks per iteration: " + ", ".join(f"{n} {v / sn:.0f}" for n, v in zip(names, ph.mean(axis=0)))
               + f"; total {tot.mean() / sn:.0f}", flush=True)
+        sh = ph.sum(axis=0) / ph.sum()
+        print("  phase shares: " + ", ".join(f"{n} {v:.3f}" for n, v in zip(names, sh))
+              + f"; mean query {tot.mean() / 2.382e6:.1f} ms in-kernel (2,382 MHz ticks)", flush=True)
         continue
     c = c.astype(np.float64)
     if False:
