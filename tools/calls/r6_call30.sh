@@ -14,7 +14,7 @@ for r in 1 2; do
   done
 done
 unset PMP_HIP_LIB
-PMP_HIP_LIB=$L/libpmp_hip_rrtstamps2.so timeout -k 10 300 python3 -u tools/rrt_time.py 256x65536 2>&1 | grep "phase shares" || exit 1
+
 timeout -k 10 300 python3 bench.py --legs rrt --steps 2 --warmup 1 --no-cpu-baseline --detail-out gpurun_out/r6c30/d.json \
   > gpurun_out/r6c30/b.out 2> gpurun_out/r6c30/b.err || { tail -20 gpurun_out/r6c30/b.err; exit 1; }
 python3 -c "
