@@ -102,7 +102,7 @@ struct RrtShared {
     uint64_t binm[kBins * kBins][2];
     double bininv_x, bininv_y;
     int use_bins;
-    float t2a[kWaves], t2b[kWaves];  // the nearest scan's per-wave top-2 ...
+    uint32_t t2a[kWaves], t2b[kWaves];  // the nearest scan's per-wave top-2 ...
     int t2i[kWaves];                 // ... and the minimum's index
     double nearx, neary, nearg, nearh;
     int nK, nA, nT, nT2, slot;
@@ -299,6 +299,14 @@ __device__ bool collision_block(const RrtShared& S, int nr, int nc, int nb, doub
     return __syncthreads_or(hit) != 0;
 }
 
+typedef short rrt_v2i16 __attribute__((ext_vector_type(2)));
+// squared distance of two quantised points (x | y << 16, 15-bit coordinates): exact
+__device__ __forceinline__ uint32_t cd2(uint32_t p, uint32_t q)
+{
+    const rrt_v2i16 d = __builtin_bit_cast(rrt_v2i16, p) - __builtin_bit_cast(rrt_v2i16, q);
+    return (uint32_t)__builtin_amdgcn_sdot2(d, d, 0, false);
+}
+
 // ---- workgroup reductions ----
 __device__ float block_min_f(float v, RrtShared& S)
 {
@@ -435,18 +443,20 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
     const double sx0 = A.start[2 * q], sy0 = A.start[2 * q + 1];
     const double gx = A.goal[2 * q], gy = A.goal[2 * q + 1];
     // Coarse coordinates: every node lies in the box spanned by the map, the start and the goal
-    // (steering moves toward samples inside the map), quantised to 16 bits per axis.  A decoded
-    // value is within half a step (+ f32 rounding) of the node, so the f32 distance of the coarse
-    // copy is within eps of the exact one: candidates within 2*eps of the coarse minimum include
-    // every exact-minimum node, and the exact f64 CPython hypot decides among them.
+    // (steering moves toward samples inside the map), quantised to 15 bits per axis (round 6; 16
+    // before) and packed x | y << 16.  Query points (the sample, node_new, the nearest node) are
+    // quantised the same way, so a coarse squared distance is exact integer arithmetic on the
+    // quantised points -- one packed i16 subtraction and one dot2 (|dx|, |dy| <= 32767, the sum
+    // < 2^31) -- and it is within eps_q quanta of the exact distance times qscale (each axis' two
+    // roundings <= 1 quantum together: sqrt(2) < eps_q).  Candidates within 2 eps_q of the coarse
+    // minimum include every exact-minimum node, and the exact f64 CPython hypot decides among them.
     const double qlo = fmin(fmin(0.0, fmin(sx0, sy0)), fmin(gx, gy));
     const double qhi = fmax(fmax(fmax(P.x_range, P.y_range), fmax(sx0, sy0)), fmax(gx, gy));
-    const double qscale = 65535.0 / (qhi - qlo);
-    const float qinv = (float)((qhi - qlo) / 65535.0);
-    const float qlof = (float)qlo;
+    constexpr double kQ = 32767.0;
+    const double qscale = kQ / (qhi - qlo);
     auto qenc = [&](double x, double y) -> uint32_t {
-        const double ux = fmin(fmax(rint((x - qlo) * qscale), 0.0), 65535.0);
-        const double uy = fmin(fmax(rint((y - qlo) * qscale), 0.0), 65535.0);
+        const double ux = fmin(fmax(rint((x - qlo) * qscale), 0.0), kQ);
+        const double uy = fmin(fmax(rint((y - qlo) * qscale), 0.0), kQ);
         return (uint32_t)ux | ((uint32_t)uy << 16);
     };
     if (tid == 0) {
@@ -456,8 +466,15 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
     __syncthreads();
     const double lox = delta, rgx = (P.x_range - delta) - delta;
     const double loy = delta, rgy = (P.y_range - delta) - delta;
-    // |coarse - exact| per node distance <= sqrt(2) * (half step + f32 decode rounding) + f32 arithmetic
-    const double eps = (qhi - qlo) / 65535.0 + 1e-6 * (qhi - qlo) + 2e-4;
+    // |coarse distance - exact distance * qscale| <= sqrt(2) (+ the f64 rounding of the quantiser)
+    constexpr double eps_q = 1.5;
+    // a coarse threshold: squared quanta of (a distance r in map units plus e quanta), its integer
+    // part (d2 <= floor(t) for an integer d2)
+    auto qthr = [&](double r, double e) -> uint32_t {
+        const double t = r * qscale + e;
+        const double t2 = t * t;
+        return t2 >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t2;
+    };
     int n = 1, status = 1;
     int64_t cur = 0;
     int64_t c_iter = 0, c_scan = 0, c_cand = 0, c_tests = 0;  // iterations, nodes scanned, in-radius, collision tests
@@ -503,23 +520,17 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         if (tid == 0) S.nH = 0;  // (the staging of this iteration comes after a barrier)
         RSTAMP_START();
         // ---- 2. nearest ----
-        const float sxf = (float)sx, syf = (float)sy;
-        // one formula for every pass (the band test must see the same f32 distance as the minimum)
-        auto cd2 = [&](uint32_t p, float ax, float ay) -> float {
-            const float dx = fmaf((float)(p & 0xFFFFu), qinv, qlof) - ax;
-            const float dy = fmaf((float)(p >> 16), qinv, qlof) - ay;
-            return dx * dx + dy * dy;
-        };
+        const uint32_t qs = qenc(sx, sy);  // the sample, quantised (one distance formula, cd2, for every pass)
         // each thread's minimum, its first index and its second-smallest distance: the band below
         // holds only the thread's first minimum unless the second one is in it too (then the thread
         // re-scans its nodes), so the common case needs no second pass over the tree
-        float best = INFINITY, second = INFINITY;
+        uint32_t best = 0xFFFFFFFFu, second = 0xFFFFFFFFu;
         int bj = 0;
-        auto take = [&](float d, int j) {
+        auto take = [&](uint32_t d, int j) {
             const bool lt = d < best;  // strict: increasing j keeps the first
-            second = lt ? best : (d < second ? d : second);
+            second = min(second, max(best, d));  // lt: the old best; else min(second, d)
             bj = lt ? j : bj;
-            best = lt ? d : best;
+            best = min(best, d);
         };
         const int nl = n < lcap ? n : lcap;
         {
@@ -531,18 +542,18 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
 #pragma unroll
                 for (int u = 0; u < 8; u++) p[u] = xl[j + u * kNT];
 #pragma unroll
-                for (int u = 0; u < 8; u++) take(cd2(p[u], sxf, syf), j + u * kNT);
+                for (int u = 0; u < 8; u++) take(cd2(p[u], qs), j + u * kNT);
             }
-            for (; j < nl; j += kNT) take(cd2(xl[j], sxf, syf), j);
+            for (; j < nl; j += kNT) take(cd2(xl[j], qs), j);
             j = lcap + tid;
             for (; j + 7 * kNT < n; j += 8 * kNT) {
                 uint32_t p[8];
 #pragma unroll
                 for (int u = 0; u < 8; u++) p[u] = xyq[j + u * kNT];
 #pragma unroll
-                for (int u = 0; u < 8; u++) take(cd2(p[u], sxf, syf), j + u * kNT);
+                for (int u = 0; u < 8; u++) take(cd2(p[u], qs), j + u * kNT);
             }
-            for (; j < n; j += kNT) take(cd2(xyq[j], sxf, syf), j);
+            for (; j < n; j += kNT) take(cd2(xyq[j], qs), j);
         }
         RSTAMPF(0);
         // the exact coordinates of this thread's minimum, loaded ahead of the block minimum (RRT: its
@@ -553,15 +564,15 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         // block top-2 of the threads' f32 distances (each thread's minimum and second) and the
         // minimum's index: when nothing but the minimum lies in the band the minimum is the nearest
         // node (the band's exact re-evaluation has one candidate) and its owner publishes it
-        float m, b2;
+        uint32_t m, b2;
         int im;
         {
-            float ta = best, tb = second;
+            uint32_t ta = best, tb = second;
             int ti = bj;
             for (int o = 32; o > 0; o >>= 1) {
-                const float oa = __shfl_xor(ta, o), ob = __shfl_xor(tb, o);
+                const uint32_t oa = (uint32_t)__shfl_xor((int)ta, o), ob = (uint32_t)__shfl_xor((int)tb, o);
                 const int oi = __shfl_xor(ti, o);
-                const float hi2 = oa < ta ? ta : oa;
+                const uint32_t hi2 = oa < ta ? ta : oa;
                 tb = hi2 < tb ? hi2 : tb;
                 tb = ob < tb ? ob : tb;
                 if (oa < ta || (oa == ta && oi < ti)) { ta = oa; ti = oi; }
@@ -570,17 +581,16 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             __syncthreads();
             m = S.t2a[0]; b2 = S.t2b[0]; im = S.t2i[0];
             for (int w = 1; w < kWaves; w++) {
-                const float oa = S.t2a[w], ob = S.t2b[w];
+                const uint32_t oa = S.t2a[w], ob = S.t2b[w];
                 const int oi = S.t2i[w];
-                const float hi2 = oa < m ? m : oa;
+                const uint32_t hi2 = oa < m ? m : oa;
                 b2 = hi2 < b2 ? hi2 : b2;
                 b2 = ob < b2 ? ob : b2;
                 if (oa < m || (oa == m && oi < im)) { m = oa; im = oi; }
             }
         }
         RSTAMP(0);
-        const double band = sqrt((double)m) + 2.0 * eps;
-        const float T = (float)(band * band) * 1.0001f;
+        const uint32_t T = qthr(sqrt((double)m) / qscale, 2.0 * eps_q);
         int hi = 0x7fffffff;
         double nx0, ny0, gnear, nx, ny, G0;
         bool staged = false;  // the in-radius coarse hits are staged already (the fused step)
@@ -611,9 +621,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                 }
             } else {
                 const uint32_t pn = im < lcap ? xl[im] : xyq[im];
-                const float fxn = fmaf((float)(pn & 0xFFFFu), qinv, qlof), fyn = fmaf((float)(pn >> 16), qinv, qlof);
-                const double rbn = P.radius + P.max_dist + 4.0 * eps;
-                const float Trn = (float)(rbn * rbn) * 1.0001f;
+                const uint32_t Trn = qthr(P.radius + P.max_dist, eps_q + 0.01);
                 constexpr int kST = kNT - 64;  // the staging threads
                 for (int j0 = tid - 64; j0 < n; j0 += 8 * kST) {
                     uint32_t p[8];
@@ -631,7 +639,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                     }
                     uint32_t hits = 0;
 #pragma unroll
-                    for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kST < n) & (cd2(p[u], fxn, fyn) <= Trn)) << u;
+                    for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kST < n) & (cd2(p[u], pn) <= Trn)) << u;
                     for (; hits; hits &= hits - 1) {
                         const int h = atomicAdd(&S.nH, 1);
                         if (h < kMaxH) S.hj[h] = j0 + (__ffs(hits) - 1) * kST;
@@ -679,7 +687,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                         for (int u = 0; u < 8; u++) p[u] = (j0 + u * kNT < nl) ? xl[j0 + u * kNT] : 0u;
                         uint32_t hits = 0;
     #pragma unroll
-                        for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < nl) & (cd2(p[u], sxf, syf) <= T)) << u;
+                        for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < nl) & (cd2(p[u], qs) <= T)) << u;
                         for (; hits; hits &= hits - 1) hit(j0 + (__ffs(hits) - 1) * kNT);
                     }
                     for (int j0 = lcap + tid; j0 < n; j0 += 8 * kNT) {
@@ -688,7 +696,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                         for (int u = 0; u < 8; u++) p[u] = (j0 + u * kNT < n) ? xyq[j0 + u * kNT] : 0u;
                         uint32_t hits = 0;
     #pragma unroll
-                        for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < n) & (cd2(p[u], sxf, syf) <= T)) << u;
+                        for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < n) & (cd2(p[u], qs) <= T)) << u;
                         for (; hits; hits &= hits - 1) hit(j0 + (__ffs(hits) - 1) * kNT);
                     }
                 }
@@ -720,9 +728,8 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         if (STAR) {
             const int wave = tid >> 6, lane = tid & 63;
             // ---- 4a. in-radius candidates; those with c_i < G0 queue for a collision test ----
-            const float nxf = (float)nx, nyf = (float)ny;
-            const double rb = P.radius + 2.0 * eps;
-            const float Tr = (float)(rb * rb) * 1.0001f;
+            const uint32_t qn = qenc(nx, ny);
+            const uint32_t Tr = qthr(P.radius, eps_q + 0.01);
             // node j's exact test: in the radius -> a K entry (and a T entry when c_j < G0)
             auto in_radius = [&](int j) {
                 const double xj = tx[2 * j], yj = tx[2 * j + 1], gj = tg[j];  // one round
@@ -767,7 +774,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                 }
                 uint32_t hits = 0;
 #pragma unroll
-                for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < n) & (cd2(p[u], nxf, nyf) <= Tr)) << u;
+                for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < n) & (cd2(p[u], qn) <= Tr)) << u;
               // a coarse hit is staged: its exact test waits for the scan's end, so the hits' node
               // loads go out in one round instead of one dependent round per chunk
               for (; hits; hits &= hits - 1) {
@@ -793,7 +800,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                     }
                     uint32_t hits = 0;
 #pragma unroll
-                    for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < n) & (cd2(p[u], nxf, nyf) <= Tr)) << u;
+                    for (int u = 0; u < 8; u++) hits |= (uint32_t)((j0 + u * kNT < n) & (cd2(p[u], qn) <= Tr)) << u;
                     for (; hits; hits &= hits - 1) in_radius(j0 + (__ffs(hits) - 1) * kNT);
                 }
             }
