@@ -307,6 +307,59 @@ __device__ __forceinline__ uint32_t cd2(uint32_t p, uint32_t q)
     return (uint32_t)__builtin_amdgcn_sdot2(d, d, 0, false);
 }
 
+// One step of a wave's top-2 reduction (the minimum with its lowest index, the second-smallest value)
+// over DPP: lanes take the value of another lane (CTRL) in the rows RM enables, the others combine
+// with the neutral element.  row_ror 1, 2, 4, 8 then row_bcast 15 / 31 cover disjoint lane sets at
+// every step, so lane 63 ends with the wave's top-2 (a VALU chain instead of six LDS-pipe permutes).
+template <int CTRL, int RM>
+__device__ __forceinline__ void top2_dpp(uint32_t& a, uint32_t& b, int& i)
+{
+    const uint32_t oa = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)a, CTRL, RM, 0xF, false);
+    const uint32_t ob = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)b, CTRL, RM, 0xF, false);
+    const int oi = __builtin_amdgcn_update_dpp(0x7fffffff, i, CTRL, RM, 0xF, false);
+    b = min(min(max(oa, a), b), ob);
+    const bool take = oa < a || (oa == a && oi < i);
+    a = take ? oa : a;
+    i = take ? oi : i;
+}
+__device__ __forceinline__ void wave_top2(uint32_t& a, uint32_t& b, int& i)
+{
+    top2_dpp<0x121, 0xF>(a, b, i);  // row_ror:1
+    top2_dpp<0x122, 0xF>(a, b, i);  // row_ror:2
+    top2_dpp<0x124, 0xF>(a, b, i);  // row_ror:4
+    top2_dpp<0x128, 0xF>(a, b, i);  // row_ror:8
+    top2_dpp<0x142, 0xA>(a, b, i);  // row_bcast:15 into rows 1, 3
+    top2_dpp<0x143, 0x8>(a, b, i);  // row_bcast:31 into row 3
+    a = (uint32_t)__builtin_amdgcn_readlane((int)a, 63);
+    b = (uint32_t)__builtin_amdgcn_readlane((int)b, 63);
+    i = __builtin_amdgcn_readlane(i, 63);
+}
+
+// The same for the lexicographic minimum of (f64 v, index i): every lane gets it
+template <int CTRL, int RM>
+__device__ __forceinline__ void min_di_dpp(double& v, int& i)
+{
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, RM, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0x7FF00000, (int)(uint32_t)(b >> 32), CTRL, RM, 0xF, false);
+    const double ov = __longlong_as_double(((uint64_t)hi << 32) | lo);  // neutral: +inf
+    const int oi = __builtin_amdgcn_update_dpp(0x7fffffff, i, CTRL, RM, 0xF, false);
+    const bool take = ov < v || (ov == v && oi < i);
+    v = take ? ov : v;
+    i = take ? oi : i;
+}
+__device__ __forceinline__ void wave_min_di(double& v, int& i)
+{
+    min_di_dpp<0x121, 0xF>(v, i);
+    min_di_dpp<0x122, 0xF>(v, i);
+    min_di_dpp<0x124, 0xF>(v, i);
+    min_di_dpp<0x128, 0xF>(v, i);
+    min_di_dpp<0x142, 0xA>(v, i);
+    min_di_dpp<0x143, 0x8>(v, i);
+    v = rl_f64(v, 63);
+    i = __builtin_amdgcn_readlane(i, 63);
+}
+
 // ---- workgroup reductions ----
 __device__ float block_min_f(float v, RrtShared& S)
 {
@@ -569,14 +622,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         {
             uint32_t ta = best, tb = second;
             int ti = bj;
-            for (int o = 32; o > 0; o >>= 1) {
-                const uint32_t oa = (uint32_t)__shfl_xor((int)ta, o), ob = (uint32_t)__shfl_xor((int)tb, o);
-                const int oi = __shfl_xor(ti, o);
-                const uint32_t hi2 = oa < ta ? ta : oa;
-                tb = hi2 < tb ? hi2 : tb;
-                tb = ob < tb ? ob : tb;
-                if (oa < ta || (oa == ta && oi < ti)) { ta = oa; ti = oi; }
-            }
+            wave_top2(ta, tb, ti);
             if ((tid & 63) == 0) { S.t2a[tid >> 6] = ta; S.t2b[tid >> 6] = tb; S.t2i[tid >> 6] = ti; }
             __syncthreads();
             m = S.t2a[0]; b2 = S.t2b[0]; im = S.t2i[0];
@@ -836,11 +882,7 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                 const int j = aget_j(S, al, a);
                 if (c < cb || (c == cb && j < jb)) { cb = c; jb = j; }
             }
-            for (int o = 32; o > 0; o >>= 1) {
-                const double ov = __shfl_xor(cb, o);
-                const int oi = __shfl_xor(jb, o);
-                if (ov < cb || (ov == cb && oi < jb)) { cb = ov; jb = oi; }
-            }
+            wave_min_di(cb, jb);
             if (cb < G0) { G = cb; parent = jb; }
             RSTAMP(5);
             // ---- 4c. rewire decisions; untested candidates queue for a collision test ----
