@@ -656,8 +656,10 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
                     double dist = lp::py_hypot(sx - ex, sy - ey);
                     const double theta = atan2(sy - ey, sx - ex);
                     if (P.max_dist < dist) dist = P.max_dist;
-                    fnx = ex + dist * cos(theta);
-                    fny = ey + dist * sin(theta);
+                    double st, ct;
+                    sincos(theta, &st, &ct);  // one range reduction; the same bits as cos / sin (tools/sincos_check.hip)
+                    fnx = ex + dist * ct;
+                    fny = ey + dist * st;
                     fG0 = eg + dist;
                     if (collision_wave(S, nr, nc, nb, delta, fnx, fny, ex, ey)) fl = 2;
                 }
@@ -758,8 +760,10 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
             double dist = lp::py_hypot(sx - nx0, sy - ny0);
             const double theta = atan2(sy - ny0, sx - nx0);
             if (P.max_dist < dist) dist = P.max_dist;
-            nx = nx0 + dist * cos(theta);
-            ny = ny0 + dist * sin(theta);
+            double st, ct;
+            sincos(theta, &st, &ct);
+            nx = nx0 + dist * ct;
+            ny = ny0 + dist * st;
             G0 = gnear + dist;
             c_tests++;
             if (collision_block(S, nr, nc, nb, delta, nx, ny, nx0, ny0)) { RSTAMP(2); continue; }
