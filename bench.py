@@ -1900,7 +1900,7 @@ def main():
     ap.add_argument("--rrt-samples", type=int, default=65536)
     ap.add_argument("--rrt-steps", type=int, default=4)
     ap.add_argument("--rrt-streams", type=int, default=2, help="RRT* launches in flight (own stream + context each)")
-    ap.add_argument("--rrt-batches", type=int, default=8,
+    ap.add_argument("--rrt-batches", type=int, default=16,
                     help="RRT* batches (of --rrt-queries) per launch: continuous batching, one launch over all of them")
     ap.add_argument("--rrt-cpu-sample", type=int, default=16)
     ap.add_argument("--rrt-resident", type=int, default=0,

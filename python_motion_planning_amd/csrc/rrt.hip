@@ -23,17 +23,31 @@
 
 namespace {
 
-// threads per query (round 5: 256 threads at 2 / 3 workgroups per CU and a 128-VGPR build at 2 per CU
-// were slower, profiles/r5/rrt_phases.txt)
-constexpr int kNT = 512;
+// threads per query: 256, two workgroups per CU (round 6, tools/calls/r6_call37-39.sh: the iteration is a
+// chain of barriers and dependent L2 rounds, so a second query per CU hides it -- 955 -> 1,475 plans/s
+// over 512 x 1; 128 x 4 and a 168-VGPR 256 x 3 build are slower.  Round 5, when the whole-tree f32 scans
+// dominated, 512 x 1 was the faster shape)
+#ifndef PMP_RRT_NT
+#define PMP_RRT_NT 256
+#endif
+constexpr int kNT = PMP_RRT_NT;
+#ifndef PMP_RRT_PERCU
+#define PMP_RRT_PERCU (512 / PMP_RRT_NT)
+#endif
+#ifndef PMP_RRT_MINW
+#define PMP_RRT_MINW 1
+#endif
 constexpr int kWaves = kNT / 64;
 constexpr int kMaxObs = 256;   // per obstacle kind
 constexpr int kMaxBnd = 8;
 // The candidate lists keep their first entries in LDS and the rest in per-query HBM lists (C3: an
 // r = 10 ball holds tens of nodes), so the LDS goes to the coarse tree copy.
-constexpr int kMaxA = 256;     // collision-free improving candidates per iteration
-constexpr int kMaxT = 256;     // candidates awaiting a collision test per phase
-constexpr int kMaxK = 256;     // in-radius candidates kept in LDS (more spill to the HBM list)
+#ifndef PMP_RRT_KMAX
+#define PMP_RRT_KMAX 128
+#endif
+constexpr int kMaxA = PMP_RRT_KMAX;  // collision-free improving candidates per iteration
+constexpr int kMaxT = PMP_RRT_KMAX;  // candidates awaiting a collision test per phase
+constexpr int kMaxK = PMP_RRT_KMAX;  // in-radius candidates kept in LDS (more spill to the HBM list)
 constexpr int kRnd = 256;      // random doubles staged in LDS
 constexpr int kMaxH = 512;     // coarse in-radius hits staged in LDS (more are resolved inline)
 constexpr int kBins = 16;      // obstacle bins per axis over the map
@@ -83,9 +97,6 @@ struct RrtArgs {
 };
 
 struct RrtShared {
-    double rect[kMaxObs * 4];
-    double circ[kMaxObs * 3];
-    double bnd[kMaxBnd * 4];
     float redf[kWaves];
     double redd[kWaves];
     int redi[kWaves];
@@ -111,6 +122,16 @@ struct RrtShared {
     double newx, newy, newG;  // the fused step's node_new (wave 0's steering)
     int fflag;                // ... 1 the sample is already in the tree, 2 the segment collides
 };
+
+// The obstacles sit at the head of the dynamic LDS (rects, 4 doubles each, then circles, 3, then the
+// boundary, 4), sized to the map's counts; the coarse tree copy follows them
+}  // namespace
+extern __shared__ __attribute__((aligned(16))) unsigned char rrt_lds_dyn[];
+namespace {
+__device__ __forceinline__ const double* obs_rect() { return (const double*)rrt_lds_dyn; }
+__device__ __forceinline__ const double* obs_circ(int nr) { return obs_rect() + 4 * nr; }
+__device__ __forceinline__ const double* obs_bnd(int nr, int nc) { return obs_rect() + 4 * nr + 3 * nc; }
+__host__ __device__ inline int obs_bytes(int nr, int nc, int nb) { return ((4 * nr + 3 * nc + 4 * nb) * 8 + 15) & ~15; }
 
 // ---- obstacle tests (sample_search.py), same operation order as the oracle ----
 __device__ inline bool in_box(const double* r, double d, double x, double y)
@@ -167,24 +188,24 @@ __device__ inline bool coll_item(const RrtShared& S, int nr, int nc, int nb, dou
     if (it >= per && it < 2 * per) { it -= per; x = x2; y = y2; }
     if (it < per) {
         if (it < nc) {
-            const double* c = &S.circ[3 * it];
+            const double* c = &obs_circ(nr)[3 * it];
             const double rr = c[2] + d;
             if (fabs(x - c[0]) > rr || fabs(y - c[1]) > rr) return false;
             return lp::py_hypot(x - c[0], y - c[1]) <= rr;
         }
         it -= nc;
-        if (it < nr) return in_box(&S.rect[4 * it], d, x, y);
-        return in_box(&S.bnd[4 * (it - nr)], d, x, y);
+        if (it < nr) return in_box(&obs_rect()[4 * it], d, x, y);
+        return in_box(&obs_bnd(nr, nc)[4 * (it - nr)], d, x, y);
     }
     it -= 2 * per;
     const double bx0 = fmin(x1, x2), bx1 = fmax(x1, x2), by0 = fmin(y1, y2), by1 = fmax(y1, y2);
     if (it < nr) {
-        const double* r = &S.rect[4 * it];
+        const double* r = &obs_rect()[4 * it];
         if (bx1 < r[0] - d || bx0 > r[0] + r[2] + d || by1 < r[1] - d || by0 > r[1] + r[3] + d) return false;
         return inter_rect(r, d, x1, y1, x2, y2);
     }
     it -= nr;
-    const double* c = &S.circ[3 * it];
+    const double* c = &obs_circ(nr)[3 * it];
     // the projected point lies within the segment's bbox (up to rounding): a gap of more than
     // r + d (with slack for the rounding) rules the circle out
     const double rr = (c[2] + d) * (1.0 + 1e-12) + 1e-12;
@@ -431,19 +452,21 @@ __device__ __forceinline__ double aget_c(const RrtShared& S, const AEntry* al, i
 typedef __attribute__((address_space(3))) uint32_t lds_xyq;
 
 template <bool STAR>
-__global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
+__global__ __launch_bounds__(kNT, PMP_RRT_MINW) void rrt_kernel(RrtArgs A)
 {
     __shared__ RrtShared S;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_dyn[];
-    lds_xyq* xl = (lds_xyq*)smem_dyn;  // nodes 0 .. lcap-1 of the coarse copy
     const int lcap = A.lcap;
     const int q = blockIdx.x;
     const int tid = threadIdx.x;
     if (q >= A.nq) return;
     const int nr = A.nr, nc = A.nc, nb = A.nb;
-    for (int i = tid; i < 4 * nr; i += kNT) S.rect[i] = A.rect[i];
-    for (int i = tid; i < 3 * nc; i += kNT) S.circ[i] = A.circ[i];
-    for (int i = tid; i < 4 * nb; i += kNT) S.bnd[i] = A.bnd[i];
+    lds_xyq* xl = (lds_xyq*)(rrt_lds_dyn + obs_bytes(nr, nc, nb));  // nodes 0 .. lcap-1 of the coarse copy
+    {
+        double* ob = (double*)rrt_lds_dyn;
+        for (int i = tid; i < 4 * nr; i += kNT) ob[i] = A.rect[i];
+        for (int i = tid; i < 3 * nc; i += kNT) ob[4 * nr + i] = A.circ[i];
+        for (int i = tid; i < 4 * nb; i += kNT) ob[4 * nr + 3 * nc + i] = A.bnd[i];
+    }
     const pmp_rrt_params P = A.P;
     if (tid == 0) {
         S.use_bins = nc + nr + nb <= 128 && P.x_range > 0 && P.y_range > 0;
@@ -460,10 +483,10 @@ __global__ __launch_bounds__(kNT) void rrt_kernel(RrtArgs A)
         for (int o = 0; S.use_bins && o < nc + nr + nb; o++) {
             double x0, x1, y0, y1;
             if (o < nc) {
-                const double* c = &S.circ[3 * o];
+                const double* c = &obs_circ(nr)[3 * o];
                 x0 = c[0] - c[2] - mg; x1 = c[0] + c[2] + mg; y0 = c[1] - c[2] - mg; y1 = c[1] + c[2] + mg;
             } else {
-                const double* r = o < nc + nr ? &S.rect[4 * (o - nc)] : &S.bnd[4 * (o - nc - nr)];
+                const double* r = o < nc + nr ? &obs_rect()[4 * (o - nc)] : &obs_bnd(nr, nc)[4 * (o - nc - nr)];
                 x0 = r[0] - mg; x1 = r[0] + r[2] + mg; y0 = r[1] - mg; y1 = r[1] + r[3] + mg;
             }
             if (bin_of(x0, S.bininv_x) <= bx && bx <= bin_of(x1, S.bininv_x) && bin_of(y0, S.bininv_y) <= by &&
@@ -1010,8 +1033,10 @@ extern "C" int pmp_rrt_batch(pmp_ctx* ctx, void* stream, const pmp_rrt_params* p
     // RRT workgroup almost no tree in LDS: RRT honours at most kRrtMaxResident of it)
     int per = pmp_lds_share(ctx, 1);
     if (per > kRrtMaxResident) per = kRrtMaxResident;
+    if (per < PMP_RRT_PERCU) per = PMP_RRT_PERCU;  // narrower workgroups: two per CU
     const long share = kLdsBytes / per;
-    int lcap = (int)(std::max(0L, share - (long)sizeof(RrtShared) - 512) / 4) & ~63;
+    const int ob = obs_bytes(nr, nc, nb);
+    int lcap = (int)(std::max(0L, share - (long)sizeof(RrtShared) - ob - 512) / 4) & ~63;
     if (lcap > tree_cap) lcap = (tree_cap + 63) & ~63;
     RrtArgs A;
     A.P = *p;
@@ -1023,7 +1048,7 @@ extern "C" int pmp_rrt_batch(pmp_ctx* ctx, void* stream, const pmp_rrt_params* p
     A.cost = cost; A.path_len = path_len; A.path = path_xy; A.path_cap = path_cap;
     A.draws = draws; A.status = status; A.counters = counters; A.xyq = xyq; A.klist = kl;
     A.tlist = tl; A.alist = al; A.lcap = lcap;
-    const size_t dyn = (size_t)lcap * 4;
+    const size_t dyn = (size_t)ob + (size_t)lcap * 4;
     if (p->star)
         hipLaunchKernelGGL(rrt_kernel<true>, dim3(nq), dim3(kNT), dyn, (hipStream_t)stream, A);
     else
