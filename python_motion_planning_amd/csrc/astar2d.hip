@@ -1055,7 +1055,7 @@ static int astar2d_reserve_impl(pmp_ctx* ctx, int W, int H, int workers, int hea
     if (ctx->astar_engine >= 1 && dflt && heap_cap > mq_cap) heap_cap = mq_cap;
     if (ctx->astar_engine >= 1 && heap_cap <= mq_cap) {
         // workers = queries in flight (16-lane groups, 4 per wave); scratch is taken at launch
-        const size_t per_slot = (size_t)W * H * 9 + (size_t)mq_cap * 16 + 4096 + 256;
+        const size_t per_slot = (size_t)W * H + g_slot_cells(W, H) * 8 + (size_t)mq_cap * 16 + 4096 + 256;
         const size_t fit = kScratchBudgetMq / per_slot;
         if (fit < 4) return pmp_set_err(ctx, PMP_ENOMEM, "pmp_astar2d_reserve: one wave exceeds the scratch budget");
         if ((size_t)workers > fit) workers = (int)(fit & ~(size_t)3);

@@ -667,12 +667,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
                 (int)(4u * (uint32_t)spill_n * 16u), 0x00020000);
     }
     uint8_t* cst = cst_all + slot * cst_bytes;
-    double* G = G_all + slot * ((size_t)W * (size_t)H);
-    uint32_t* Pc = THETA ? Pc_all + slot * ((size_t)W * (size_t)H) : nullptr;  // CLOSED parent cell
+    const size_t gsc = g_slot_cells(W, H);  // G: tiled (g_idx), slot stride gsc cells
+    const uint32_t tHg = g_tiles_y(H);
+    double* G = G_all + slot * gsc;
+    // Theta*: G and Pc in 4 x 4 tiles (g_idx); A* keeps row-major G (the tile index cost the headline's
+    // dependent chain 1.3 %, tools/calls/r6_call42.sh)
+    auto gix = [&](int gx_, int gy_) -> uint32_t {
+        return THETA ? g_idx(gx_, gy_, tHg) : (uint32_t)gx_ * (uint32_t)H + (uint32_t)gy_;
+    };
+    uint32_t* Pc = THETA ? Pc_all + slot * gsc : nullptr;  // CLOSED parent cell (linear), tiled like G
     const size_t nslots = (size_t)gridDim.x * 4u;
     const bool mir8 = (kMirror & 8) && (slot & 1u) == 0u;
     uint8_t* cst_m = cst_all + (nslots + slot / 2) * cst_bytes;
-    double* G_m = G_all + (nslots + slot / 2) * ((size_t)W * (size_t)H);
+    double* G_m = G_all + (nslots + slot / 2) * gsc;
 
     Walk wk;
     wk.init(gl);
@@ -881,7 +888,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
                 const bool in_occ = gl < 9 && (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
                 const uint32_t ci = in_occ ? (uint32_t)cx * (uint32_t)H + (uint32_t)cy : 0u;
                 const uint32_t cti = in_occ ? cst_idx(cx, cy, tH) : 0u;
-                const uint32_t pusher = has_pusher ? nlin - (uint32_t)(mot_x(pm) * H + mot_y(pm)) : 0u;
+                const uint32_t pusher = !has_pusher ? 0u
+                                        : THETA     ? gix(x - mot_x(pm), y - mot_y(pm))
+                                                    : nlin - (uint32_t)(mot_x(pm) * H + mot_y(pm));
                 const uint32_t gi = (!GZERO && gl == 12) ? pusher : 0u;
                 const uint32_t ow = occ[ci >> 5];
                 blk_c = cst[cti];
@@ -955,7 +964,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
                     gp_g = gp;
                     if (ndir >= 16) {  // path 2: node.g = parent.g + dist (theta_star.py:106-108)
                         par_lin = bc<13>(ppar);
-                        const double t = G[gl == 12 ? par_lin : 0u];
+                        const int qx = (int)(par_lin / (uint32_t)H), qy = (int)(par_lin - (uint32_t)qx * (uint32_t)H);
+                        const double t = G[gl == 12 ? gix(qx, qy) : 0u];
                         gp_g = bcf<12>(t);
                     }
                     px = (int)(par_lin / (uint32_t)H);
@@ -966,8 +976,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
                         // set vertex (lazy_theta_star.py:55-65): the first CLOSED, collision-free
                         // neighbour minimising its g + dist becomes the parent; g = inf if there is none
                         const bool cand = gl < 8 && (occ9 & nsb & 0xFFFFu) == 0u && (cls9 & (nsb >> 16)) != 0u;
-                        const uint32_t cl = (uint32_t)((int)nlin + mx * H + my);
-                        const double gn = G[cand ? cl : 0u];
+                        const double gn = G[cand ? gix(x + mx, y + my) : 0u];
                         const double gc = gn + ((mo & 1) ? kSqrt2 : 1.0);
                         const uint32_t cmask = rbits(cand, gb) & 0xFFu;
                         double best = __longlong_as_double(0x7ff0000000000000ll);
@@ -993,10 +1002,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
                 }
                 // CLOSED[node.current] = node (a_star.py:82)
                 if (gl == 0) cst[cst_idx(x, y, tH)] = (uint8_t)((ep << 4) | (uint32_t)(THETA ? 1 : ndir + 1));
-                if (!GZERO && gl == 1) G[nlin] = gnode;
-                if (THETA && gl == 0) Pc[nlin] = par_lin;  // read back by this lane's extractPath
+                if (!GZERO && gl == 1) G[gix(x, y)] = gnode;
+                if (THETA && gl == 0) Pc[gix(x, y)] = par_lin;  // read back by this lane's extractPath
                 if (mir8 && gl == 0) cst_m[cst_idx(x, y, tH)] = (uint8_t)((ep << 4) | (uint32_t)(ndir + 1));
-                if (mir8 && !GZERO && gl == 1) G_m[nlin] = gnode;
+                if (mir8 && !GZERO && gl == 1) G_m[gix(x, y)] = gnode;
                 if (gl == 2 && expand_out && nexp < expand_cap)
                     expand_out[(size_t)q * expand_cap + nexp] =
                         THETA ? (nlin | ((uint32_t)ecode << 26)) : (nlin | ((uint32_t)ndir << 28));
@@ -1014,7 +1023,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(THETA ? 3 : 
                             if (len < path_cap) pth[len] = li;
                             len++;
                             if (cx == sx && cy == sy) break;
-                            const uint32_t pl = Pc[li];
+                            const uint32_t pl = Pc[gix(cx, cy)];
                             const int qx = (int)(pl / (uint32_t)H), qy = (int)(pl - (uint32_t)qx * (uint32_t)H);
                             cost += __dsqrt_rn((double)((cx - qx) * (cx - qx) + (cy - qy) * (cy - qy)));
                             cx = qx;
@@ -1108,10 +1117,10 @@ int pmp_astar2d_slot_scratch(pmp_ctx* ctx, hipStream_t s, size_t slots, int W, i
                              double** G, uint32_t** ep)
 {
     const size_t cb = mq_cst_bytes(W, H);
-    const size_t ncell = (size_t)W * H;
+    const size_t gsc = g_slot_cells(W, H);
     const size_t ms = (kMirror & 8) ? slots + slots / 2 + 1 : slots;  // kMirror: the even slots' mirrors
     *cst = (uint8_t*)pmp_scratch(ctx, SCR_MQ_CST, ms * cb + 16);
-    *G = (double*)pmp_scratch(ctx, SCR_MQ_G, ms * ncell * 8 + 16);
+    *G = (double*)pmp_scratch(ctx, SCR_MQ_G, ms * gsc * 8 + 16);
     const bool fresh_epochs = ctx->cap[SCR_MQ_EPOCH] < slots * 4 || ctx->astar_mq_epoch_slots < slots ||
                               ctx->astar_mq_cst_bytes != cb;
     *ep = (uint32_t*)pmp_scratch(ctx, SCR_MQ_EPOCH, slots * 4 + 16);
@@ -1144,7 +1153,7 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
         // the reservation's fit (astar2d_reserve_impl) counts cell state, G, spill and bits per slot;
         // Theta* adds a W*H*4-byte CLOSED-parent array per slot: fewer groups (the persistent queue
         // serves every query) instead of growing past the budget
-        const size_t per_slot = (size_t)W * H * 13 + (size_t)cap_max * 16 + 4096 + 256;
+        const size_t per_slot = (size_t)W * H + g_slot_cells(W, H) * 12 + (size_t)cap_max * 16 + 4096 + 256;
         const size_t fit = (kScratchBudgetMq / per_slot) & ~(size_t)3;
         if (fit < 4) return pmp_set_err(ctx, PMP_ENOMEM, "ThetaStar: one wave's slots exceed the scratch budget");
         if ((size_t)groups > fit) groups = (int)fit;
@@ -1173,7 +1182,7 @@ int pmp_astar2d_mq_launch(pmp_ctx* ctx, hipStream_t s, int algo, const uint32_t*
     if (!spill || !t2) return PMP_ENOMEM;
     uint32_t* Pc = nullptr;  // Theta*: the CLOSED parent cell of every cell, per slot
     if (theta) {
-        Pc = (uint32_t*)pmp_scratch(ctx, SCR_MQ_PC, slots * (size_t)W * H * 4 + 16);
+        Pc = (uint32_t*)pmp_scratch(ctx, SCR_MQ_PC, slots * g_slot_cells(W, H) * 4 + 16);
         if (!Pc) return PMP_ENOMEM;
     }
     uint8_t* cstp;

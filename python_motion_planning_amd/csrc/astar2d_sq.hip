@@ -332,7 +332,7 @@ __global__ __launch_bounds__(64) void astar2d_sq_kernel(
     } else {
         occg = occ;
         cst = cst_all + (size_t)q * cst_slot_bytes;
-        G = G_all + (size_t)q * ncell;
+        G = G_all + (size_t)q * g_slot_cells(W, H);  // (the shared slot stride; row-major inside)
         // next epoch; every 15th query (and a fresh slot, epoch 0) clears the cell states
         ep = epoch_all[q];
         if (ep == 0u || ep >= 15u) {

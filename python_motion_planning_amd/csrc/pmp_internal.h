@@ -160,6 +160,28 @@ __device__ __forceinline__ uint32_t cst_idx(int x, int y, uint32_t tH)
            (((uint32_t)x & ((1u << kCstTx) - 1u)) << kCstTy) + ((uint32_t)y & ((1u << kCstTy) - 1u));
 }
 
+// Per-slot G (f64) of the multi-query engine in tiles of 4 (x) x 4 (y) cells, one 128-B line: the
+// pusher's G (read at every pop) and the node's (written at its expansion) are neighbours, in one line
+// for most motions (the row-major layout puts every x +- 1 neighbour in another line).  The slot stride
+// (cells) covers the padded tiles; the single-query engine keeps row-major G inside the same stride.
+#ifndef PMP_G_TX
+#define PMP_G_TX 2  // log2 tile width along x
+#endif
+#ifndef PMP_G_TY
+#define PMP_G_TY 2  // log2 tile height along y
+#endif
+constexpr int kGTx = PMP_G_TX, kGTy = PMP_G_TY;
+__host__ __device__ inline size_t g_slot_cells(int W, int H)
+{
+    return (size_t)((W + (1 << kGTx) - 1) >> kGTx) * (size_t)((H + (1 << kGTy) - 1) >> kGTy) * ((size_t)1 << (kGTx + kGTy));
+}
+__device__ __forceinline__ uint32_t g_tiles_y(int H) { return (uint32_t)(H + (1 << kGTy) - 1) >> kGTy; }
+__device__ __forceinline__ uint32_t g_idx(int x, int y, uint32_t tHg)
+{
+    return ((((uint32_t)x >> kGTx) * tHg + ((uint32_t)y >> kGTy)) << (kGTx + kGTy)) +
+           (((uint32_t)x & ((1u << kGTx) - 1u)) << kGTy) + ((uint32_t)y & ((1u << kGTy) - 1u));
+}
+
 // Correctly rounded sqrt of an integer 0 <= k < 2^31: the operation sequence of LLVM's f64 sqrt
 // lowering for gfx9 (rsq, two Newton-Raphson corrections of (s, h = y/2), two residual corrections),
 // without its input scaling (only for x < 2^-767) and its 0 / inf class test (0 handled here), so the
