@@ -554,6 +554,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void ds
 
 }  // namespace
 
+#ifndef PMP_DSTAR_BUDGET_GIB
+#define PMP_DSTAR_BUDGET_GIB 48
+#endif
 extern "C" int pmp_dstar2d_onpress_batch(pmp_ctx* ctx, void* stream, const uint32_t* occ_bits, int W, int H,
                                          const int32_t* start_xy, const int32_t* goal_xy, int nq, const int32_t* presses,
                                          int npress, double* cost, int32_t* path_len, int32_t* path, int path_cap,
@@ -581,7 +584,7 @@ extern "C" int pmp_dstar2d_onpress_batch(pmp_ctx* ctx, void* stream, const uint3
     const size_t per_worker = (ncell + 1) * sizeof(DCell) + (size_t)entry_cap * 4 + spill_n * 16 + 4096 +
                               (npress > 0 ? words * 4 : 0);
     int workers = 256 * per_cu;
-    const size_t max_workers = ((size_t)48 << 30) / per_worker;  // keep the scratch under 48 GiB
+    const size_t max_workers = ((size_t)PMP_DSTAR_BUDGET_GIB << 30) / per_worker;  // the scratch budget
     if ((size_t)workers > max_workers) workers = (int)(max_workers > 0 ? max_workers : 1);
     if (workers > nq) workers = nq;
     uint4* spill = (uint4*)pmp_scratch(ctx, SCR_AUX1, (size_t)workers * spill_n * 16 + 16);
