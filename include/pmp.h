@@ -512,6 +512,12 @@ int pmp_astar2d_sq_cap(int W, int H);
  * (pmp_astar2d_set_schedule, pmp_astar2d_set_priority) apply to these planners as well.  Results are
  * identical for any value. */
 int pmp_set_workers_per_cu(pmp_ctx* ctx, int per_cu);
+/* pmp_dstar2d_batch / pmp_dstar2d_onpress_batch run in two passes: the first with a heap and entry
+ * capacity of `entries` per query (0 = the default, W*H + 64: a smaller per-worker scratch, so more
+ * workers fit the scratch budget), the second, on the same stream, re-runs every query whose heap or
+ * entry list outgrew it with the bound (4 W*H + 64) on a few workers.  Results are identical for any
+ * value. */
+int pmp_dstar_set_first_cap(pmp_ctx* ctx, int entries);
 /* Workers resident per CU over all the launches that run at once, for pmp_graph3d_batch,
  * pmp_dstar2d_batch / pmp_dstar2d_onpress_batch and pmp_dstar3d_batch: each worker's LDS heap share
  * is sized for max(this, the launch's own workers per CU), so several batches in flight with few

@@ -41,6 +41,7 @@ SIGNATURES = {
     "pmp_astar2d_set_engine": (_i, [_vp, _i, _i]),
     "pmp_set_resident_per_cu": (_i, [_vp, _i]),
     "pmp_set_workers_per_cu": (_i, [_vp, _i]),
+    "pmp_dstar_set_first_cap": (_i, [_vp, _i]),
     "pmp_astar3d_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _i,
                                _vp, _vp]),
     "pmp_dwa_step_batch": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp,

@@ -379,8 +379,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void ds
                                                    int64_t* __restrict__ nproc_out, int32_t* __restrict__ status_out,
                                                    int64_t max_process, int* __restrict__ queue, uint4* __restrict__ spill_all,
                                                    int heap_cap, int lds_cap, DCell* __restrict__ cells_all,
-                                                   int32_t* __restrict__ next_all, int entry_cap, uint32_t* __restrict__ occw_all)
+                                                   int32_t* __restrict__ next_all, int entry_cap, uint32_t* __restrict__ occw_all,
+                                                   int* __restrict__ ovf, int retry)
 {
+    // ovf (nullable): [0] queries whose heap / entry list outgrew this launch's capacity, [1] the
+    // re-run's queue, [2..] their indices.  retry = 0: the first pass (appends to it); 1: the re-run
+    // at the bound over that list
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
     const int worker = blockIdx.x;
@@ -402,8 +406,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void ds
     const int R1 = npress + 1;
 
     for (;;) {
-        const int q = next_query(queue, lane);
-        if (q >= nq) break;
+        int q;
+        if (retry) {
+            const int qi = next_query(ovf + 1, lane);
+            if (qi >= uni(ovf[0])) break;
+            q = uni(ovf[2 + qi]);
+        } else {
+            q = next_query(queue, lane);
+            if (q >= nq) break;
+        }
+        bool hover = false;  // the heap / entry list outgrew the capacity (the re-run's case)
         const int sx = uni(start_xy[2 * q]), sy = uni(start_xy[2 * q + 1]);
         const int gx = uni(goal_xy[2 * q]), gy = uni(goal_xy[2 * q + 1]);
         if ((unsigned)sx >= (unsigned)W || (unsigned)sy >= (unsigned)H || (unsigned)gx >= (unsigned)W ||
@@ -451,7 +463,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void ds
         int plen0 = 0;  // round 0's path_len when it raises: -2 = getNeighbor's KeyError (path[0] = the node)
         for (;;) {
             const int ps = d.process_state();
-            if (ps == PS_OVER) { st = PMP_CAP_OVERFLOW; break; }
+            if (ps == PS_OVER) { st = PMP_CAP_OVERFLOW; hover = true; break; }
             if (ps == PS_RAISE) { st = PMP_REF_RAISES; plen0 = -2; break; }
             if (ps != PS_DONE) { st = PMP_REF_RAISES; break; }  // min_k of an empty OPEN (:234)
             if (S.start_closed) break;
@@ -512,7 +524,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void ds
                                 d.insert_uniform(node, load_cell(S.cells, p).h + __builtin_inf());
                             for (;;) {
                                 const int ps = S.overflow ? PS_OVER : d.process_state();
-                                if (ps == PS_OVER) { rst = PMP_CAP_OVERFLOW; break; }
+                                if (ps == PS_OVER) { rst = PMP_CAP_OVERFLOW; hover = true; break; }
                                 if (ps == PS_RAISE) {  // getNeighbor's KeyError: path_len -2, path[0] = the node
                                     rst = PMP_REF_RAISES;
                                     plen = -2;
@@ -548,6 +560,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void ds
                 nproc_out[(size_t)q * R1 + r] = rst == -1 ? 0 : S.np;  // a no-op press keeps EXPAND
             }
         }
+        if (!retry && ovf && hover && lane == 0) {  // the re-run overwrites every output of q
+            const int i = atomicAdd(ovf, 1);
+            ovf[2 + i] = q;
+        }
         heap16::wsync();
     }
 }
@@ -573,31 +589,54 @@ extern "C" int pmp_dstar2d_onpress_batch(pmp_ctx* ctx, void* stream, const uint3
     PMP_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     const size_t ncell = (size_t)W * H;
     const size_t words = (ncell + 31) / 32;
-    // per worker: 32 B cell state + 4 entries (16 B) + 4 heap elements (64 B) per cell, over the LDS part
-    const size_t hc = 4 * ncell + 64;
-    const int heap_cap = (int)(hc > (size_t)(1 << 26) ? (size_t)(1 << 26) : hc);
-    const int entry_cap = heap_cap;
+    // per worker: 32 B cell state, 4 B per entry and 16 B per heap element beyond the LDS part.  The
+    // bound is 4 entries / heap elements per cell; the first pass takes ctx->dstar_first_cap (default
+    // one per cell: a third of the scratch, twice the workers at 512^2 within the budget), and a second
+    // launch re-runs at the bound the queries whose heap or entry list outgrew it
+    const size_t hb = 4 * ncell + 64;
+    const int cap_full = (int)(hb > (size_t)(1 << 26) ? (size_t)(1 << 26) : hb);
+    const size_t h1 = ctx->dstar_first_cap > 0 ? (size_t)ctx->dstar_first_cap : ncell + 64;
+    const int cap1 = (int)std::min(h1, (size_t)cap_full);
+    const bool two = cap1 < cap_full;
     const int per_cu = std::max(1, std::min(ctx->workers_per_cu > 0 ? ctx->workers_per_cu : 16, (nq + 255) / 256));
     int lds_cap = (((160 * 1024) / pmp_lds_share(ctx, per_cu) - 256) / 16) & ~15;
-    if (lds_cap > heap_cap) lds_cap = (heap_cap + 15) & ~15;
-    const size_t spill_n = heap_cap > lds_cap ? (size_t)(heap_cap - lds_cap) : 0;
-    const size_t per_worker = (ncell + 1) * sizeof(DCell) + (size_t)entry_cap * 4 + spill_n * 16 + 4096 +
-                              (npress > 0 ? words * 4 : 0);
+    if (lds_cap > cap1) lds_cap = (cap1 + 15) & ~15;
+    auto spill_of = [&](int cap) { return cap > lds_cap ? (size_t)(cap - lds_cap) : (size_t)0; };
+    auto per_worker = [&](int cap) {
+        return (ncell + 1) * sizeof(DCell) + (size_t)cap * 4 + spill_of(cap) * 16 + 4096 + (npress > 0 ? words * 4 : 0);
+    };
     int workers = 256 * per_cu;
-    const size_t max_workers = ((size_t)PMP_DSTAR_BUDGET_GIB << 30) / per_worker;  // the scratch budget
+    const size_t budget = (size_t)PMP_DSTAR_BUDGET_GIB << 30;
+    const size_t max_workers = budget / per_worker(cap1);
     if ((size_t)workers > max_workers) workers = (int)(max_workers > 0 ? max_workers : 1);
     if (workers > nq) workers = nq;
-    uint4* spill = (uint4*)pmp_scratch(ctx, SCR_AUX1, (size_t)workers * spill_n * 16 + 16);
-    DCell* cells = (DCell*)pmp_scratch(ctx, SCR_AUX2, (size_t)workers * (ncell + 1) * sizeof(DCell) + 16);
-    int32_t* nxt = (int32_t*)pmp_scratch(ctx, SCR_AUX3, (size_t)workers * entry_cap * 4 + 16);
+    // the re-run: one worker per CU at most, within the first pass's allocations where they suffice
+    int rw = 0;
+    if (two) {
+        rw = std::min(nq, 256);
+        const size_t mw = budget / per_worker(cap_full);
+        if ((size_t)rw > mw) rw = (int)(mw > 0 ? mw : 1);
+    }
+    const size_t spill_b = std::max((size_t)workers * spill_of(cap1), (size_t)rw * spill_of(cap_full)) * 16 + 16;
+    const size_t cells_b = (size_t)std::max(workers, rw) * (ncell + 1) * sizeof(DCell) + 16;
+    const size_t nxt_b = std::max((size_t)workers * cap1, (size_t)rw * cap_full) * 4 + 16;
+    uint4* spill = (uint4*)pmp_scratch(ctx, SCR_AUX1, spill_b);
+    DCell* cells = (DCell*)pmp_scratch(ctx, SCR_AUX2, cells_b);
+    int32_t* nxt = (int32_t*)pmp_scratch(ctx, SCR_AUX3, nxt_b);
     int* queue = (int*)pmp_scratch(ctx, SCR_AUX0, 256);
-    uint32_t* occw = npress > 0 ? (uint32_t*)pmp_scratch(ctx, SCR_AUX4, (size_t)workers * words * 4 + 16) : nullptr;
-    if (!spill || !cells || !nxt || !queue || (npress > 0 && !occw)) return PMP_ENOMEM;
+    uint32_t* occw = npress > 0 ? (uint32_t*)pmp_scratch(ctx, SCR_AUX4, (size_t)std::max(workers, rw) * words * 4 + 16) : nullptr;
+    int* ovf = two ? (int*)pmp_scratch(ctx, SCR_DSTAR_OVF, ((size_t)nq + 2) * 4 + 16) : nullptr;
+    if (!spill || !cells || !nxt || !queue || (npress > 0 && !occw) || (two && !ovf)) return PMP_ENOMEM;
     hipStream_t s = (hipStream_t)stream;
     PMP_HIP_CHECK(ctx, hipMemsetAsync(queue, 0, 16, s));
+    if (two) PMP_HIP_CHECK(ctx, hipMemsetAsync(ovf, 0, 8, s));
     hipLaunchKernelGGL(dstar_kernel, dim3(workers), dim3(64), (size_t)lds_cap * 16, s, occ_bits, W, H, start_xy, goal_xy,
                        nq, presses, npress, cost, path_len, path, path_cap, n_process, status, max_process, queue, spill,
-                       heap_cap, lds_cap, cells, nxt, entry_cap, occw);
+                       cap1, lds_cap, cells, nxt, cap1, occw, ovf, 0);
+    if (two)
+        hipLaunchKernelGGL(dstar_kernel, dim3(rw), dim3(64), (size_t)lds_cap * 16, s, occ_bits, W, H, start_xy, goal_xy,
+                           nq, presses, npress, cost, path_len, path, path_cap, n_process, status, max_process, queue,
+                           spill, cap_full, lds_cap, cells, nxt, cap_full, occw, ovf, 1);
     PMP_HIP_CHECK(ctx, hipGetLastError());
     return PMP_OK;
 }

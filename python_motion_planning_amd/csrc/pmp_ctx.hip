@@ -95,6 +95,14 @@ int pmp_set_resident_per_cu(pmp_ctx* ctx, int per_cu)
     return PMP_OK;
 }
 
+int pmp_dstar_set_first_cap(pmp_ctx* ctx, int entries)
+{
+    if (!ctx) return PMP_EINVAL;
+    if (entries < 0) return pmp_set_err(ctx, PMP_EINVAL, "pmp_dstar_set_first_cap: entries must be >= 0");
+    ctx->dstar_first_cap = entries;
+    return PMP_OK;
+}
+
 int pmp_set_workers_per_cu(pmp_ctx* ctx, int per_cu)
 {
     if (!ctx) return PMP_EINVAL;

@@ -23,6 +23,8 @@ struct pmp_ctx {
     int astar_resident_per_cu = 0;
     // one-wave-per-query planners (3D A* family, D*): persistent workers per CU (0 = each one's default)
     int workers_per_cu = 0;
+    // D* 2D: the first pass's heap / entry capacity (0 = one per cell + 64; pmp_dstar_set_first_cap)
+    int dstar_first_cap = 0;
     // ... and the workers resident per CU over all concurrent launches, which sets their LDS share
     // (0 = this launch's own workers per CU; pmp_set_resident_per_cu)
     int resident_per_cu = 0;
@@ -51,7 +53,7 @@ struct pmp_ctx {
 
 enum ScratchSlot { SCR_HEAP = 0, SCR_CLOSED = 1, SCR_PDIR = 2, SCR_G = 3, SCR_AUX0 = 4, SCR_AUX1 = 5, SCR_AUX2 = 6, SCR_AUX3 = 7,
                    SCR_BITS = 8, SCR_AUX4 = 9, SCR_PAR = 10, SCR_MQ_SPILL = 11, SCR_MQ_CST = 12, SCR_MQ_G = 13,
-                   SCR_MQ_T2 = 14, SCR_MQ_EPOCH = 15, SCR_DWA = 16, SCR_MQ_PC = 17, SCR_NSLOTS = 18 };
+                   SCR_MQ_T2 = 14, SCR_MQ_EPOCH = 15, SCR_DWA = 16, SCR_MQ_PC = 17, SCR_DSTAR_OVF = 18, SCR_NSLOTS = 19 };
 
 int pmp_set_err(pmp_ctx* ctx, int code, const std::string& msg);
 // Workers per CU whose LDS shares a launch of `per_cu` workers per CU must fit beside

@@ -202,3 +202,45 @@ def test_dstar_onpress_dropin():
             if k == "":
                 assert p.cost == z["cost"][i][r]
                 assert [c[0] * H + c[1] for c in p.path] == seg(z["path"], z["path_off"], i * R + r).tolist()
+
+
+@pytest.mark.parametrize("first_cap", [96, 700])
+def test_dstar_first_cap_rerun(first_cap):
+    """The two-pass launch (pmp_dstar_set_first_cap): with a first-pass capacity far below what the
+    searches need, most queries outgrow it and the second launch re-runs them at the bound; every
+    output of plan() and of three OnPress repairs still equals the oracle's, and the queries that did
+    fit are left as the first pass wrote them."""
+    from oracle import oracle as O
+    from python_motion_planning_amd import _lib, batch, workloads as wl
+
+    L = _lib.load_library()
+    ctx = _lib.context()
+    occ, s, g = wl.c2_workload(nq=96, W=96, H=96, density=0.15, grid_seed=31, pair_seed=32)
+    rng = np.random.default_rng(33)
+    presses = np.zeros((96, 3, 2), np.int32)
+    r0 = batch.dstar2d_batch(occ, s, g)  # default capacity: the presses on its paths
+    pl0, p0 = r0["path_len"].cpu().numpy(), r0["path"].cpu().numpy()
+    for q in range(96):
+        cells = p0[q, 1 : max(2, pl0[q] - 1)]
+        for k in range(3):
+            c = int(cells[rng.integers(len(cells))]) if len(cells) else 0
+            presses[q, k] = (c // 96, c % 96)
+    _lib.check(ctx, L.pmp_dstar_set_first_cap(ctx, first_cap), "pmp_dstar_set_first_cap")
+    try:
+        r = batch.dstar2d_batch(occ, s, g)
+        out = batch.dstar2d_onpress_batch(occ, s, g, presses)
+    finally:
+        _lib.check(ctx, L.pmp_dstar_set_first_cap(ctx, 0), "pmp_dstar_set_first_cap")
+    for k in ("cost", "path_len", "n_process", "status"):
+        assert np.array_equal(r[k].cpu().numpy(), r0[k].cpu().numpy()), k
+    st, npr = out["status"].cpu().numpy(), out["n_process"].cpu().numpy()
+    cost, pl, path = out["cost"].cpu().numpy(), out["path_len"].cpu().numpy(), out["path"].cpu().numpy()
+    big = 0
+    for q in range(96):
+        ref = O.dstar2d_onpress(occ, s[q], g[q], presses[q])
+        big += int(ref["n_process"][0]) > first_cap // 4
+        for rr in range(4):
+            assert st[q, rr] == ref["status"][rr] and npr[q, rr] == ref["n_process"][rr], (q, rr)
+            assert cost[q, rr] == ref["cost"][rr] and pl[q, rr] == ref["path_len"][rr], (q, rr)
+            assert np.array_equal(path[q, rr, : max(pl[q, rr], 0)], ref["paths"][rr]), (q, rr)
+    assert big > 10  # searches well past the first capacity: the re-run was exercised
