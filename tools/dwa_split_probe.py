@@ -20,7 +20,7 @@ pl, P = r["path_len"].cpu().numpy(), r["path"].cpu().numpy()
 H = occ.shape[1]
 paths = [np.column_stack([P[i, : pl[i]][::-1] // H, P[i, : pl[i]][::-1] % H]).astype(np.float64) for i in range(256)]
 grid = batch.obstacle_grid({(int(a), int(b)) for a, b in np.argwhere(occ)})
-for na, parts_list in ((32, (1, 2, 4, 8, 16)), (256, (1, 2))):
+for na, parts_list in ((32, (1, 2, 4, 8, 16)), (256, (1, 2, 4))):
     xy, off = batch.pack_paths(paths[:na])
     ref = None
     for parts in parts_list:
