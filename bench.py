@@ -220,8 +220,9 @@ ENTRY_KERNEL = {  # C-ABI entry -> (short name of the kernel it launches, as too
     "pmp_graph2d_batch": lambda a: _G2D[int(a[2])],
     "pmp_astar3d_batch": lambda a: "astar3d_kernel",
     "pmp_graph3d_batch": lambda a: "astar3d_kernel",
-    "pmp_dstar2d_batch": lambda a: "dstar_kernel",
-    "pmp_dstar2d_onpress_batch": lambda a: "dstar_kernel",
+    # D* 2D: the first pass and the re-run at the bound (default first capacity: two dispatches per call)
+    "pmp_dstar2d_batch": lambda a: [("dstar_kernel", 1), ("dstar_rerun_kernel", 1)],
+    "pmp_dstar2d_onpress_batch": lambda a: [("dstar_kernel", 1), ("dstar_rerun_kernel", 1)],
     "pmp_dstar3d_batch": lambda a: "dstar3d_kernel",
     "pmp_lpastar3d_batch": lambda a: "lpa3d_kernel",
     "pmp_lpastar2d_batch": lambda a: "lpa_kernel",

@@ -31,6 +31,7 @@ KERNELS = {  # short name -> regex on the demangled kernel name
     "rrt_kernel": r"\brrt_kernel[<(]",
     "astar3d_kernel": r"\bastar3d_kernel[<(]",
     "dstar_kernel": r"\bdstar_kernel[<(]",
+    "dstar_rerun_kernel": r"\bdstar_rerun_kernel[<(]",
     "dstar3d_kernel": r"\bdstar3d_kernel[<(]",
     "lpa_kernel": r"\blpa_kernel[<(]",
     "lpa3d_kernel": r"\blpa3d_kernel[<(]",
