@@ -629,6 +629,8 @@ def rrt_leg(args, torch, dist, world, rank):
 
     elapsed, kern_ms = shard.max_over_ranks(dist, [elapsed, kern_ms], "cuda")
     checked = check_timed("rrt_star", ref_out, lanes[: min(len(lanes), args.rrt_steps)])
+    for b in lanes:  # the lanes' per-query lists and coarse copies (about 14 GB each): not needed later
+        L.pmp_destroy(b["ctx"])
     # the bytes the kernel loads: 4 B per node scanned (the 16-bit fixed-point
     # coordinate copy of the coarse nearest / radius scans) + 24 B per in-radius candidate (exact
     # f64 x, y and g).  The trees (4 B x 65,537 nodes per query) stay in L2 / Infinity Cache, so the

@@ -524,7 +524,10 @@ __global__ void lpt3_scatter(const int32_t* s, const int32_t* g, int nq, int nb,
 }
 
 // per-context scratch budget of the 3D planners (heap spill + closed state + Theta* parents per worker)
-constexpr size_t kScratchBudget3 = (size_t)32 << 30;
+#ifndef PMP_ASTAR3D_BUDGET_GIB
+#define PMP_ASTAR3D_BUDGET_GIB 48  // 32: ~4,870 workers at C5 (2.05 M plans/s), 48: the 20-per-CU 5,120 (2.09-2.11 M, tools/calls/r6_call53.sh)
+#endif
+constexpr size_t kScratchBudget3 = (size_t)PMP_ASTAR3D_BUDGET_GIB << 30;
 
 }  // namespace
 
