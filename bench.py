@@ -1251,7 +1251,7 @@ def dstar_leg(args, torch, dist, world, rank):
                                       "algorithmic_bytes_per_launch": alg,
                                       "bytes_note": "248 B per processState (3x3 cell states 9 x 24 B + 2 OPEN "
                                                     "entries x 16 B); latency-bound, one wave per query"},
-                                     "dstar_kernel", f"dstar_{W}"),
+                                     "dstar_kernel", f"dstar_{W}:dstar_kernel"),
             "detail": {"process_state_per_launch": int(npr.sum()), "max_process_state_query": int(npr.max()),
                        "statuses": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))}},
             "cpu_baseline": cpu}
