@@ -522,8 +522,9 @@ int pmp_dstar_set_first_cap(pmp_ctx* ctx, int entries);
  * pmp_dstar2d_batch / pmp_dstar2d_onpress_batch and pmp_dstar3d_batch: each worker's LDS heap share
  * is sized for max(this, the launch's own workers per CU), so several batches in flight with few
  * workers each stay resident together (as pmp_astar2d_set_residency for A* 2D); 0 = the launch's own
- * count.  pmp_rrt_batch sizes each query's LDS copy of its tree for this many workgroups per CU (0 or
- * 1: the whole LDS beside the workgroup's state).  Results are identical for any value. */
+ * count.  pmp_rrt_batch sizes each query's LDS copy of its tree for this many workgroups per CU, at
+ * least 2 (its 256-thread workgroups run two per CU) and at most 4.  Results are identical for any
+ * value. */
 int pmp_set_resident_per_cu(pmp_ctx* ctx, int per_cu);
 
 /* Pre-size the A* scratch (heap of heap_cap entries per concurrent query, up to max_slots
