@@ -48,8 +48,14 @@ constexpr int kMaxBnd = 8;
 constexpr int kMaxA = PMP_RRT_KMAX;  // collision-free improving candidates per iteration
 constexpr int kMaxT = PMP_RRT_KMAX;  // candidates awaiting a collision test per phase
 constexpr int kMaxK = PMP_RRT_KMAX;  // in-radius candidates kept in LDS (more spill to the HBM list)
-constexpr int kRnd = 256;      // random doubles staged in LDS
-constexpr int kMaxH = 512;     // coarse in-radius hits staged in LDS (more are resolved inline)
+#ifndef PMP_RRT_RND
+#define PMP_RRT_RND 256
+#endif
+#ifndef PMP_RRT_MAXH
+#define PMP_RRT_MAXH 512
+#endif
+constexpr int kRnd = PMP_RRT_RND;    // random doubles staged in LDS
+constexpr int kMaxH = PMP_RRT_MAXH;  // coarse in-radius hits staged in LDS (more are resolved inline)
 constexpr int kBins = 16;      // obstacle bins per axis over the map
 constexpr int kLdsBytes = 160 * 1024;  // the CU's LDS
 constexpr int kRrtMaxResident = 4;     // LDS tree shares per CU RRT honours from pmp_set_resident_per_cu
